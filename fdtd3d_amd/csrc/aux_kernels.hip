@@ -1,0 +1,186 @@
+// Auxiliary kernels: sources, halo pack/unpack, reductions, amplitude
+// tracking.  All launch on the caller's stream and never synchronise, so they
+// can be captured into HIP graphs together with the stencil kernels.
+
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- sources
+// Hard source: field[off] = value (Scheme3D.cpp:2011-2022).  The value is a
+// host-computed double so the waveform (sin(2 pi f dt t), Gaussian, ...) is
+// bit-identical between backends.
+template <typename T>
+__global__ void k_set_value(T* __restrict__ f, long long off, double v) {
+  if (threadIdx.x == 0) f[off] = (T)v;
+}
+
+// Line/point list source: f[offs[n]] = v (amplitude-mode z-line source,
+// Scheme3D.cpp:2995-3013).
+template <typename T>
+__global__ void k_set_values(T* __restrict__ f, const long long* __restrict__ offs, int n, double v) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) f[offs[t]] = (T)v;
+}
+
+// ---------------------------------------------------------------- halo boxes
+// Copy a strided box of `ncomp` fields into a packed buffer (pack) or back
+// (unpack).  One thread per element; the z run of each box row is contiguous
+// in both the field and the buffer, so rows are coalesced.
+template <typename T>
+struct FieldPtrs {
+  T* p[8];
+};
+
+template <typename T, bool PACK>
+__global__ void k_box_copy(FieldPtrs<T> fields, T* __restrict__ buf, int ncomp, int ny, int nz, Box3 b) {
+  const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1], bz = b.hi[2] - b.lo[2];
+  const long long n = (long long)bx * by * bz;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n * ncomp;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t / n);
+    long long r = t - (long long)c * n;
+    const int k = (int)(r % bz);
+    r /= bz;
+    const int j = (int)(r % by);
+    const int i = (int)(r / by);
+    const size_t off = ((size_t)(b.lo[0] + i) * ny + (b.lo[1] + j)) * nz + (b.lo[2] + k);
+    if (PACK)
+      buf[t] = fields.p[c][off];
+    else
+      fields.p[c][off] = buf[t];
+  }
+}
+
+// ---------------------------------------------------------------- reductions
+// max |f| over a box -> atomicMax on the float bit pattern (non-negative
+// floats order like their integer bits).  Used by the amplitude mode and the
+// non-finite watchdog (NaN is mapped to +inf so it is never lost).
+template <typename T>
+__device__ __forceinline__ float absf_sat(T v) {
+  float a = fabsf((float)v);
+  return (a != a) ? __builtin_huge_valf() : a;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_box_maxabs(const T* __restrict__ f, int ny, int nz, Box3 b,
+                                                    unsigned int* __restrict__ out) {
+  const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1], bz = b.hi[2] - b.lo[2];
+  const long long n = (long long)bx * by * bz;
+  float m = 0.f;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(t % bz);
+    const long long r = t / bz;
+    const int j = (int)(r % by);
+    const int i = (int)(r / by);
+    const size_t off = ((size_t)(b.lo[0] + i) * ny + (b.lo[1] + j)) * nz + (b.lo[2] + k);
+    m = fmaxf(m, absf_sat(f[off]));
+  }
+  // wave64 reduction
+  for (int d = 32; d > 0; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = red[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = fmaxf(r, red[w]);
+    atomicMax(out, __float_as_uint(r));
+  }
+}
+
+// Amplitude mode (Scheme3D.cpp:3294-3333): amp = max(amp, |f|) over a box and
+// count the cells whose amplitude changed by more than `accuracy` relative.
+template <typename T>
+__global__ __launch_bounds__(256) void k_amplitude_update(const T* __restrict__ f, T* __restrict__ amp, int ny,
+                                                          int nz, Box3 b, double accuracy,
+                                                          unsigned int* __restrict__ changed) {
+  const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1], bz = b.hi[2] - b.lo[2];
+  const long long n = (long long)bx * by * bz;
+  unsigned int cnt = 0;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(t % bz);
+    const long long r = t / bz;
+    const int j = (int)(r % by);
+    const int i = (int)(r / by);
+    const size_t off = ((size_t)(b.lo[0] + i) * ny + (b.lo[1] + j)) * nz + (b.lo[2] + k);
+    const T v = f[off] < T(0) ? -f[off] : f[off];
+    const T a = amp[off];
+    if (v >= a) {
+      // relative growth, exactly Scheme3D::updateAmplitude (Scheme3D.cpp:3294-3333)
+      T acc = v - a;
+      if (a != T(0))
+        acc /= a;
+      else if (v != T(0))
+        acc /= v;
+      if (acc > (T)accuracy) {
+        cnt++;
+        amp[off] = v;
+      }
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(changed, cnt);
+}
+
+inline unsigned reduce_grid(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+#define FDTD_AUX_API(SUF, T)                                                                                  \
+  FDTD_API int fdtd_set_value_##SUF(T* f, long long off, double v, void* s) {                                 \
+    k_set_value<T><<<1, 64, 0, (hipStream_t)s>>>(f, off, v);                                                   \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_set_values_##SUF(T* f, const long long* offs, int n, double v, void* s) {                 \
+    if (n <= 0) return 0;                                                                                     \
+    k_set_values<T><<<cdiv(n, 256), 256, 0, (hipStream_t)s>>>(f, offs, n, v);                                  \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_box_pack_##SUF(T* const* fields, T* buf, int ncomp, int ny, int nz, const int* box,        \
+                                   void* s) {                                                                 \
+    Box3 b = make_box(box);                                                                                   \
+    if (box_empty(b) || ncomp <= 0 || ncomp > 8) return ncomp > 8 ? (int)hipErrorInvalidValue : 0;             \
+    FieldPtrs<T> fp;                                                                                          \
+    for (int c = 0; c < ncomp; ++c) fp.p[c] = fields[c];                                                      \
+    long long n = (long long)(b.hi[0] - b.lo[0]) * (b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]) * ncomp;         \
+    k_box_copy<T, true><<<reduce_grid(n), 256, 0, (hipStream_t)s>>>(fp, buf, ncomp, ny, nz, b);            \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_box_unpack_##SUF(T* const* fields, const T* buf, int ncomp, int ny, int nz,                \
+                                     const int* box, void* s) {                                               \
+    Box3 b = make_box(box);                                                                                   \
+    if (box_empty(b) || ncomp <= 0 || ncomp > 8) return ncomp > 8 ? (int)hipErrorInvalidValue : 0;             \
+    FieldPtrs<T> fp;                                                                                          \
+    for (int c = 0; c < ncomp; ++c) fp.p[c] = fields[c];                                                      \
+    long long n = (long long)(b.hi[0] - b.lo[0]) * (b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]) * ncomp;         \
+    k_box_copy<T, false><<<reduce_grid(n), 256, 0, (hipStream_t)s>>>(fp, (T*)buf, ncomp, ny, nz, b);       \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_box_maxabs_##SUF(const T* f, int ny, int nz, const int* box, unsigned int* out, void* s) { \
+    Box3 b = make_box(box);                                                                                   \
+    if (box_empty(b)) return 0;                                                                               \
+    long long n = (long long)(b.hi[0] - b.lo[0]) * (b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]);                \
+    k_box_maxabs<T><<<reduce_grid(n), 256, 0, (hipStream_t)s>>>(f, ny, nz, b, out);                            \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_amplitude_update_##SUF(const T* f, T* amp, int ny, int nz, const int* box,                \
+                                           double accuracy, unsigned int* changed, void* s) {                 \
+    Box3 b = make_box(box);                                                                                   \
+    if (box_empty(b)) return 0;                                                                               \
+    long long n = (long long)(b.hi[0] - b.lo[0]) * (b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]);                \
+    k_amplitude_update<T><<<reduce_grid(n), 256, 0, (hipStream_t)s>>>(f, amp, ny, nz, b, accuracy, changed);   \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }
+
+FDTD_AUX_API(f32, float)
+FDTD_AUX_API(f64, double)
+
+FDTD_API int fdtd_abi_version() { return 1; }

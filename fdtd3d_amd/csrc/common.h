@@ -1,0 +1,49 @@
+// Shared definitions for the fdtd3d-amd HIP kernels (gfx950 / MI355X).
+//
+// Layout convention (same as the reference Grid, Source/Grid/Grid.cpp:127-139):
+// a field of local shape (nx, ny, nz) is one contiguous array, z fastest,
+// linear index  i*ny*nz + j*nz + k.  All kernels take boxes in LOCAL indices;
+// the Python/C++ host code maps global computation ranges to local boxes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FDTD_API extern "C" __attribute__((visibility("default")))
+
+struct Box3 {
+  int lo[3];
+  int hi[3];
+};
+
+__device__ __forceinline__ bool in_box(const Box3& b, int i, int j, int k) {
+  return i >= b.lo[0] && i < b.hi[0] && j >= b.lo[1] && j < b.hi[1] && k >= b.lo[2] && k < b.hi[2];
+}
+
+static inline bool box_empty(const Box3& b) {
+  return b.hi[0] <= b.lo[0] || b.hi[1] <= b.lo[1] || b.hi[2] <= b.lo[2];
+}
+
+static inline Box3 box_union(const Box3& a, const Box3& b) {
+  if (box_empty(a)) return b;
+  if (box_empty(b)) return a;
+  Box3 r;
+  for (int d = 0; d < 3; ++d) {
+    r.lo[d] = a.lo[d] < b.lo[d] ? a.lo[d] : b.lo[d];
+    r.hi[d] = a.hi[d] > b.hi[d] ? a.hi[d] : b.hi[d];
+  }
+  return r;
+}
+
+static inline Box3 make_box(const int* lohi) {
+  Box3 b;
+  for (int d = 0; d < 3; ++d) {
+    b.lo[d] = lohi[d];
+    b.hi[d] = lohi[3 + d];
+  }
+  return b;
+}
+
+static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+#define FDTD_RETURN_LAUNCH_STATUS() return (int)hipGetLastError()

@@ -1,0 +1,192 @@
+// Generic building blocks for the reference-compatible UPML/Drude chain,
+// TF/SF injection and the incident 1D line.
+//
+// The reference runs its UPML as three sweeps per component with per-cell
+// virtual material lookups (Scheme3D.cpp:266-416, 1158-1306).  Here every
+// coefficient is a factorised product  s * px[i] * py[j] * pz[k] * cell[ijk]
+// (fdtd3d_amd/ops/coef.py) precomputed once, and the chain is two kinds of
+// one-thread-per-cell launches:
+//   curl_general: out = Ca*in + Cb*curl(src)        (D/B update)
+//   lincomb:      out = sum_n coef_n * x_n  (n<=5)  (Drude ADE, E-from-D)
+// Lanes walk z (contiguous), 4 waves per workgroup walk y.
+
+#include "common.h"
+
+namespace {
+
+template <typename T>
+struct Coef3 {
+  double s;
+  const T* px;
+  const T* py;
+  const T* pz;
+  const T* cell;
+};
+
+template <typename T>
+__device__ __forceinline__ T coef_at(const Coef3<T>& c, int i, int j, int k, size_t off) {
+  T v = (T)c.s;
+  if (c.px) v *= c.px[i];
+  if (c.py) v *= c.py[j];
+  if (c.pz) v *= c.pz[k];
+  if (c.cell) v *= c.cell[off];
+  return v;
+}
+
+template <typename T>
+struct Term {
+  const T* src;
+  int axis;
+  int sign;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_curl_general(T* __restrict__ out, const T* __restrict__ inp, Term<T> t0,
+                                                      Term<T> t1, int nterms, int kind_e, Coef3<T> ca,
+                                                      Coef3<T> cb, int ny, int nz, Box3 b) {
+  const int k = b.lo[2] + blockIdx.x * 64 + threadIdx.x;
+  const int j = b.lo[1] + blockIdx.y * 4 + threadIdx.y;
+  const int i = b.lo[0] + blockIdx.z;
+  if (k >= b.hi[2] || j >= b.hi[1]) return;
+  const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
+  const size_t off = ((size_t)i * ny + j) * nz + k;
+  T acc = 0;
+  if (nterms > 0) {
+    const long long s = stride[t0.axis];
+    const T d = kind_e ? (t0.src[off] - t0.src[off - s]) : (t0.src[off + s] - t0.src[off]);
+    acc = t0.sign > 0 ? d : -d;
+  }
+  if (nterms > 1) {
+    const long long s = stride[t1.axis];
+    const T d = kind_e ? (t1.src[off] - t1.src[off - s]) : (t1.src[off + s] - t1.src[off]);
+    acc = t1.sign > 0 ? acc + d : acc - d;
+  }
+  out[off] = coef_at(ca, i, j, k, off) * inp[off] + coef_at(cb, i, j, k, off) * acc;
+}
+
+template <typename T>
+struct LinTerms {
+  Coef3<T> c[5];
+  const T* x[5];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_lincomb(T* __restrict__ out, LinTerms<T> terms, int nterms, int ny,
+                                                 int nz, Box3 b) {
+  const int k = b.lo[2] + blockIdx.x * 64 + threadIdx.x;
+  const int j = b.lo[1] + blockIdx.y * 4 + threadIdx.y;
+  const int i = b.lo[0] + blockIdx.z;
+  if (k >= b.hi[2] || j >= b.hi[1]) return;
+  const size_t off = ((size_t)i * ny + j) * nz + k;
+  T v = 0;
+#pragma unroll
+  for (int n = 0; n < 5; ++n) {
+    if (n < nterms) {
+      const T t = coef_at(terms.c[n], i, j, k, off) * terms.x[n][off];
+      v = (n == 0) ? t : v + t;
+    }
+  }
+  out[off] = v;
+}
+
+// TF/SF correction table (fdtd3d_amd/models/tfsf.py): one entry per target
+// cell (tables are layered so targets are unique -> no atomics).
+template <typename T>
+__global__ void k_tfsf_apply(T* __restrict__ target, const long long* __restrict__ off,
+                             const long long* __restrict__ i0, const T* __restrict__ w0, const T* __restrict__ w1,
+                             const T* __restrict__ coef, const int* __restrict__ ijk, int n,
+                             const T* __restrict__ inc, Box3 b) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int i = ijk[3 * e], j = ijk[3 * e + 1], k = ijk[3 * e + 2];
+  if (!in_box(b, i, j, k)) return;
+  const long long p = i0[e];
+  target[off[e]] += coef[e] * (w0[e] * inc[p] + w1[e] * inc[p + 1]);
+}
+
+// 1D incident line (Scheme3D.cpp:25-82)
+template <typename T>
+__global__ void k_inc_e(T* __restrict__ einc, const T* __restrict__ hinc, int n, T c, double src) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (i == 0)
+    einc[0] = (T)src;
+  else
+    einc[i] += c * (hinc[i - 1] - hinc[i]);
+}
+
+template <typename T>
+__global__ void k_inc_h(const T* __restrict__ einc, T* __restrict__ hinc, int n, T c) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n - 1) return;
+  hinc[i] += c * (einc[i] - einc[i + 1]);
+}
+
+template <typename T>
+Coef3<T> coef_from(const double* s, const void* const* p) {
+  Coef3<T> c;
+  c.s = s[0];
+  c.px = (const T*)p[0];
+  c.py = (const T*)p[1];
+  c.pz = (const T*)p[2];
+  c.cell = (const T*)p[3];
+  return c;
+}
+
+inline dim3 cell_grid(const Box3& b) {
+  return dim3(cdiv(b.hi[2] - b.lo[2], 64), cdiv(b.hi[1] - b.lo[1], 4), (unsigned)(b.hi[0] - b.lo[0]));
+}
+
+}  // namespace
+
+// terms: srcs[2], axes[2], signs[2]; coefs: scalar + 4 pointers (px, py, pz, cell)
+#define FDTD_GENERIC_API(SUF, T)                                                                              \
+  FDTD_API int fdtd_curl_general_##SUF(T* out, const T* inp, const T* const* srcs, const int* axes,          \
+                                       const int* signs, int nterms, int kind_e, double ca_s,                \
+                                       const void* const* ca_p, double cb_s, const void* const* cb_p, int ny, \
+                                       int nz, const int* box, void* s) {                                    \
+    Box3 b = make_box(box);                                                                                   \
+    if (box_empty(b)) return 0;                                                                               \
+    Term<T> t0 = {nterms > 0 ? srcs[0] : nullptr, nterms > 0 ? axes[0] : 0, nterms > 0 ? signs[0] : 1};       \
+    Term<T> t1 = {nterms > 1 ? srcs[1] : nullptr, nterms > 1 ? axes[1] : 0, nterms > 1 ? signs[1] : 1};       \
+    k_curl_general<T><<<cell_grid(b), dim3(64, 4), 0, (hipStream_t)s>>>(                                      \
+        out, inp, t0, t1, nterms, kind_e, coef_from<T>(&ca_s, ca_p), coef_from<T>(&cb_s, cb_p), ny, nz, b);    \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_lincomb_##SUF(T* out, int nterms, const double* scalars, const void* const* ptrs,         \
+                                  const T* const* xs, int ny, int nz, const int* box, void* s) {              \
+    Box3 b = make_box(box);                                                                                   \
+    if (box_empty(b)) return 0;                                                                               \
+    if (nterms < 1 || nterms > 5) return (int)hipErrorInvalidValue;                                           \
+    LinTerms<T> lt;                                                                                           \
+    for (int n = 0; n < 5; ++n) {                                                                             \
+      if (n < nterms) {                                                                                       \
+        lt.c[n] = coef_from<T>(scalars + n, ptrs + 4 * n);                                                    \
+        lt.x[n] = xs[n];                                                                                      \
+      } else {                                                                                                \
+        lt.c[n] = Coef3<T>{0.0, nullptr, nullptr, nullptr, nullptr};                                          \
+        lt.x[n] = nullptr;                                                                                    \
+      }                                                                                                       \
+    }                                                                                                         \
+    k_lincomb<T><<<cell_grid(b), dim3(64, 4), 0, (hipStream_t)s>>>(out, lt, nterms, ny, nz, b);               \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_tfsf_apply_##SUF(T* target, const long long* off, const long long* i0, const T* w0,      \
+                                     const T* w1, const T* coef, const int* ijk, int n, const T* inc,         \
+                                     const int* box, void* s) {                                               \
+    Box3 b = make_box(box);                                                                                   \
+    if (n <= 0 || box_empty(b)) return 0;                                                                     \
+    k_tfsf_apply<T><<<cdiv(n, 256), 256, 0, (hipStream_t)s>>>(target, off, i0, w0, w1, coef, ijk, n, inc, b);  \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_inc_e_##SUF(T* einc, const T* hinc, int n, double c, double src, void* s) {               \
+    k_inc_e<T><<<cdiv(n, 256), 256, 0, (hipStream_t)s>>>(einc, hinc, n, (T)c, src);                           \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_inc_h_##SUF(const T* einc, T* hinc, int n, double c, void* s) {                           \
+    k_inc_h<T><<<cdiv(n, 256), 256, 0, (hipStream_t)s>>>(einc, hinc, n, (T)c);                                 \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }
+
+FDTD_GENERIC_API(f32, float)
+FDTD_GENERIC_API(f64, double)

@@ -1,0 +1,239 @@
+// 2D (TMz, TEz) and 1D Yee kernels.
+//
+// The reference's 2D schemes (Source/Scheme/SchemeTMz.cpp:162-1309,
+// SchemeTEz.cpp:109-1025) and its CUDA TMz kernels
+// (Source/Cuda/CudaGlobalKernels.cu:5-153) update one component per launch
+// with one thread per cell.  Here each half step is one launch; lanes walk the
+// contiguous y axis (arrays are (nx, ny, 1), y fastest) and each thread
+// marches along x carrying the x-neighbour in a register, as in yee3d.hip.
+// The 1D scheme (Ez/Hy along x) is new: the reference lists 1D as NYI
+// (Source/Settings/Settings.cpp:29).
+
+#include "common.h"
+
+namespace {
+
+constexpr int TX = 64;
+constexpr int TY = 4;
+
+// TMz: Ez += cb*((Hy[i]-Hy[i-1]) - (Hx[j]-Hx[j-1]))   (Kernels.h:64-74)
+template <typename T, bool PERCELL>
+__global__ __launch_bounds__(TX * TY) void k_tmz_e(T* __restrict__ ez, const T* __restrict__ hx,
+                                                   const T* __restrict__ hy, const T* __restrict__ cbz, T cb,
+                                                   int nx, int ny, Box3 bz, int xchunk) {
+  const int j = bz.lo[1] + blockIdx.x * TX + threadIdx.x;
+  if (j >= bz.hi[1]) return;
+  const int i0 = bz.lo[0] + (blockIdx.y * TY + threadIdx.y) * xchunk;
+  const int i1 = min(i0 + xchunk, bz.hi[0]);
+  if (i0 >= i1) return;
+  T hy_m = hy[(size_t)(i0 - 1) * ny + j];
+  for (int i = i0; i < i1; ++i) {
+    const size_t off = (size_t)i * ny + j;
+    const T hyc = hy[off];
+    const T c = PERCELL ? cbz[off] : cb;
+    ez[off] += c * ((hyc - hy_m) - (hx[off] - hx[off - 1]));
+    hy_m = hyc;
+  }
+}
+
+// TMz: Hx += db*(-(Ez[j+1]-Ez[j])), Hy += db*(Ez[i+1]-Ez[i])
+template <typename T, bool PERCELL>
+__global__ __launch_bounds__(TX * TY) void k_tmz_h(T* __restrict__ hx, T* __restrict__ hy,
+                                                   const T* __restrict__ ez, const T* __restrict__ dbx,
+                                                   const T* __restrict__ dby, T db, int nx, int ny, Box3 bx,
+                                                   Box3 by, Box3 bu, int xchunk) {
+  const int j = bu.lo[1] + blockIdx.x * TX + threadIdx.x;
+  if (j >= bu.hi[1]) return;
+  const int i0 = bu.lo[0] + (blockIdx.y * TY + threadIdx.y) * xchunk;
+  const int i1 = min(i0 + xchunk, bu.hi[0]);
+  if (i0 >= i1) return;
+  T ez_c = ez[(size_t)i0 * ny + j];
+  for (int i = i0; i < i1; ++i) {
+    const size_t off = (size_t)i * ny + j;
+    const T ez_n = (i + 1 < nx) ? ez[off + ny] : T(0);
+    if (in_box(bx, i, j, 0)) {
+      const T c = PERCELL ? dbx[off] : db;
+      hx[off] += c * (-(ez[off + 1] - ez_c));
+    }
+    if (in_box(by, i, j, 0)) {
+      const T c = PERCELL ? dby[off] : db;
+      hy[off] += c * (ez_n - ez_c);
+    }
+    ez_c = ez_n;
+  }
+}
+
+// TEz: Ex += cb*(Hz[j]-Hz[j-1]), Ey += cb*(-(Hz[i]-Hz[i-1]))
+template <typename T, bool PERCELL>
+__global__ __launch_bounds__(TX * TY) void k_tez_e(T* __restrict__ ex, T* __restrict__ ey,
+                                                   const T* __restrict__ hz, const T* __restrict__ cbx,
+                                                   const T* __restrict__ cby, T cb, int nx, int ny, Box3 bx,
+                                                   Box3 by, Box3 bu, int xchunk) {
+  const int j = bu.lo[1] + blockIdx.x * TX + threadIdx.x;
+  if (j >= bu.hi[1]) return;
+  const int i0 = bu.lo[0] + (blockIdx.y * TY + threadIdx.y) * xchunk;
+  const int i1 = min(i0 + xchunk, bu.hi[0]);
+  if (i0 >= i1) return;
+  T hz_m = i0 > 0 ? hz[(size_t)(i0 - 1) * ny + j] : T(0);
+  for (int i = i0; i < i1; ++i) {
+    const size_t off = (size_t)i * ny + j;
+    const T hzc = hz[off];
+    if (in_box(bx, i, j, 0)) {
+      const T c = PERCELL ? cbx[off] : cb;
+      ex[off] += c * (hzc - hz[off - 1]);
+    }
+    if (in_box(by, i, j, 0)) {
+      const T c = PERCELL ? cby[off] : cb;
+      ey[off] += c * (-(hzc - hz_m));
+    }
+    hz_m = hzc;
+  }
+}
+
+// TEz: Hz += db*((Ex[j+1]-Ex[j]) - (Ey[i+1]-Ey[i]))
+template <typename T, bool PERCELL>
+__global__ __launch_bounds__(TX * TY) void k_tez_h(T* __restrict__ hz, const T* __restrict__ ex,
+                                                   const T* __restrict__ ey, const T* __restrict__ dbz, T db,
+                                                   int nx, int ny, Box3 bz, int xchunk) {
+  const int j = bz.lo[1] + blockIdx.x * TX + threadIdx.x;
+  if (j >= bz.hi[1]) return;
+  const int i0 = bz.lo[0] + (blockIdx.y * TY + threadIdx.y) * xchunk;
+  const int i1 = min(i0 + xchunk, bz.hi[0]);
+  if (i0 >= i1) return;
+  T ey_c = ey[(size_t)i0 * ny + j];
+  for (int i = i0; i < i1; ++i) {
+    const size_t off = (size_t)i * ny + j;
+    const T ey_n = ey[off + ny];
+    const T c = PERCELL ? dbz[off] : db;
+    hz[off] += c * ((ex[off + 1] - ex[off]) - (ey_n - ey_c));
+    ey_c = ey_n;
+  }
+}
+
+// 1D: Ez += cb*(Hy[i]-Hy[i-1]) on [lo, hi); Hy += db*(Ez[i+1]-Ez[i])
+template <typename T, bool PERCELL>
+__global__ void k_1d_e(T* __restrict__ ez, const T* __restrict__ hy, const T* __restrict__ cbz, T cb, int lo,
+                       int hi) {
+  const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= hi) return;
+  const T c = PERCELL ? cbz[i] : cb;
+  ez[i] += c * (hy[i] - hy[i - 1]);
+}
+
+template <typename T, bool PERCELL>
+__global__ void k_1d_h(T* __restrict__ hy, const T* __restrict__ ez, const T* __restrict__ dby, T db, int lo,
+                       int hi) {
+  const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= hi) return;
+  const T c = PERCELL ? dby[i] : db;
+  hy[i] += c * (ez[i + 1] - ez[i]);
+}
+
+inline dim3 grid2d(const Box3& b, int xchunk) {
+  return dim3(cdiv(b.hi[1] - b.lo[1], TX), cdiv(cdiv(b.hi[0] - b.lo[0], xchunk), TY), 1);
+}
+
+template <typename T>
+int tmz_e(T* ez, const T* hx, const T* hy, const T* cbz, double cb, int nx, int ny, const int* box, int xchunk,
+          hipStream_t s) {
+  Box3 bz = make_box(box);
+  if (box_empty(bz)) return 0;
+  if (xchunk <= 0) xchunk = 16;
+  if (cbz)
+    k_tmz_e<T, true><<<grid2d(bz, xchunk), dim3(TX, TY), 0, s>>>(ez, hx, hy, cbz, (T)cb, nx, ny, bz, xchunk);
+  else
+    k_tmz_e<T, false><<<grid2d(bz, xchunk), dim3(TX, TY), 0, s>>>(ez, hx, hy, cbz, (T)cb, nx, ny, bz, xchunk);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <typename T>
+int tmz_h(T* hx, T* hy, const T* ez, const T* dbx, const T* dby, double db, int nx, int ny, const int* boxes,
+          int xchunk, hipStream_t s) {
+  Box3 bx = make_box(boxes), by = make_box(boxes + 6), bu = box_union(bx, by);
+  if (box_empty(bu)) return 0;
+  if (xchunk <= 0) xchunk = 16;
+  if (dbx)
+    k_tmz_h<T, true><<<grid2d(bu, xchunk), dim3(TX, TY), 0, s>>>(hx, hy, ez, dbx, dby, (T)db, nx, ny, bx, by, bu,
+                                                                 xchunk);
+  else
+    k_tmz_h<T, false><<<grid2d(bu, xchunk), dim3(TX, TY), 0, s>>>(hx, hy, ez, dbx, dby, (T)db, nx, ny, bx, by, bu,
+                                                                  xchunk);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <typename T>
+int tez_e(T* ex, T* ey, const T* hz, const T* cbx, const T* cby, double cb, int nx, int ny, const int* boxes,
+          int xchunk, hipStream_t s) {
+  Box3 bx = make_box(boxes), by = make_box(boxes + 6), bu = box_union(bx, by);
+  if (box_empty(bu)) return 0;
+  if (xchunk <= 0) xchunk = 16;
+  if (cbx)
+    k_tez_e<T, true><<<grid2d(bu, xchunk), dim3(TX, TY), 0, s>>>(ex, ey, hz, cbx, cby, (T)cb, nx, ny, bx, by, bu,
+                                                                 xchunk);
+  else
+    k_tez_e<T, false><<<grid2d(bu, xchunk), dim3(TX, TY), 0, s>>>(ex, ey, hz, cbx, cby, (T)cb, nx, ny, bx, by, bu,
+                                                                  xchunk);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <typename T>
+int tez_h(T* hz, const T* ex, const T* ey, const T* dbz, double db, int nx, int ny, const int* box, int xchunk,
+          hipStream_t s) {
+  Box3 bz = make_box(box);
+  if (box_empty(bz)) return 0;
+  if (xchunk <= 0) xchunk = 16;
+  if (dbz)
+    k_tez_h<T, true><<<grid2d(bz, xchunk), dim3(TX, TY), 0, s>>>(hz, ex, ey, dbz, (T)db, nx, ny, bz, xchunk);
+  else
+    k_tez_h<T, false><<<grid2d(bz, xchunk), dim3(TX, TY), 0, s>>>(hz, ex, ey, dbz, (T)db, nx, ny, bz, xchunk);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <typename T>
+int oned_e(T* ez, const T* hy, const T* cbz, double cb, int lo, int hi, hipStream_t s) {
+  if (hi <= lo) return 0;
+  if (cbz)
+    k_1d_e<T, true><<<cdiv(hi - lo, 256), 256, 0, s>>>(ez, hy, cbz, (T)cb, lo, hi);
+  else
+    k_1d_e<T, false><<<cdiv(hi - lo, 256), 256, 0, s>>>(ez, hy, cbz, (T)cb, lo, hi);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <typename T>
+int oned_h(T* hy, const T* ez, const T* dby, double db, int lo, int hi, hipStream_t s) {
+  if (hi <= lo) return 0;
+  if (dby)
+    k_1d_h<T, true><<<cdiv(hi - lo, 256), 256, 0, s>>>(hy, ez, dby, (T)db, lo, hi);
+  else
+    k_1d_h<T, false><<<cdiv(hi - lo, 256), 256, 0, s>>>(hy, ez, dby, (T)db, lo, hi);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+}  // namespace
+
+#define FDTD_LOWDIM_API(SUF, T)                                                                                \
+  FDTD_API int fdtd_tmz_e_##SUF(T* ez, const T* hx, const T* hy, const T* cbz, double cb, int nx, int ny,      \
+                                const int* box, int xchunk, void* s) {                                         \
+    return tmz_e<T>(ez, hx, hy, cbz, cb, nx, ny, box, xchunk, (hipStream_t)s);                                 \
+  }                                                                                                            \
+  FDTD_API int fdtd_tmz_h_##SUF(T* hx, T* hy, const T* ez, const T* dbx, const T* dby, double db, int nx,      \
+                                int ny, const int* boxes, int xchunk, void* s) {                               \
+    return tmz_h<T>(hx, hy, ez, dbx, dby, db, nx, ny, boxes, xchunk, (hipStream_t)s);                          \
+  }                                                                                                            \
+  FDTD_API int fdtd_tez_e_##SUF(T* ex, T* ey, const T* hz, const T* cbx, const T* cby, double cb, int nx,      \
+                                int ny, const int* boxes, int xchunk, void* s) {                               \
+    return tez_e<T>(ex, ey, hz, cbx, cby, cb, nx, ny, boxes, xchunk, (hipStream_t)s);                          \
+  }                                                                                                            \
+  FDTD_API int fdtd_tez_h_##SUF(T* hz, const T* ex, const T* ey, const T* dbz, double db, int nx, int ny,      \
+                                const int* box, int xchunk, void* s) {                                         \
+    return tez_h<T>(hz, ex, ey, dbz, db, nx, ny, box, xchunk, (hipStream_t)s);                                 \
+  }                                                                                                            \
+  FDTD_API int fdtd_1d_e_##SUF(T* ez, const T* hy, const T* cbz, double cb, int lo, int hi, void* s) {         \
+    return oned_e<T>(ez, hy, cbz, cb, lo, hi, (hipStream_t)s);                                                 \
+  }                                                                                                            \
+  FDTD_API int fdtd_1d_h_##SUF(T* hy, const T* ez, const T* dby, double db, int lo, int hi, void* s) {         \
+    return oned_h<T>(hy, ez, dby, db, lo, hi, (hipStream_t)s);                                                 \
+  }
+
+FDTD_LOWDIM_API(f32, float)
+FDTD_LOWDIM_API(f64, double)

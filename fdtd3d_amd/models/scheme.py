@@ -1,0 +1,603 @@
+"""The Yee leapfrog scheme: one class for the 1D, 2D (TMz/TEz) and 3D solvers.
+
+Re-designs the reference's ``Scheme3D`` / ``SchemeTMz`` / ``SchemeTEz``
+(``Source/Scheme/*.cpp``): fields are flat device tensors (z fastest, same
+linear layout as ``Grid.cpp:127-139``), all geometry and material work happens
+once in :meth:`YeeScheme.init_grids`, and the time loop is a fixed sequence of
+backend operations (:mod:`fdtd3d_amd.ops`).  On the HIP backend each of those
+is one HIP launch on the current stream, so a step can be captured in a HIP
+graph.
+
+Per time step ``t`` (reference ``Scheme3D::performNSteps``,
+``Scheme3D.cpp:1900-2942``):
+
+1. [TF/SF] 1D incident line, E half step.
+2. E update -- plain ``E += Cb curl H`` or the UPML chain
+   ``D' = CaD D + CbD curl H`` -> [Drude ``D1' = b0 D' + b1 D + b2 D_ - a1 D1 - a2 D1_``]
+   -> ``E' = CaE E + CbE src' - CcE src``; TF/SF corrections folded in.
+3. Hard source (point ``sin(2 pi f dt t)`` unless TF/SF is on).
+4. [decomposed] E halo exchange.
+5. [TF/SF] 1D incident line, H half step; H update (mirror of 2.).
+6. [decomposed] H halo exchange.
+7. Periodic hooks: NTFF, intermediate dumps, checkpoints, finite check.
+
+Complex fields (reference ``COMPLEX_FIELD_VALUES``) are two real planes
+stepped independently -- the update coefficients are real, so this is exact --
+with the complex source ``sin + i cos`` split between them.
+"""
+
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..layout.approximation import (phase_velocity_incident_wave_2d, phase_velocity_incident_wave_3d)
+from ..layout.materials import MaterialSampler, Scene, sigma_profile_1d
+from ..layout.yee import (E_COMPONENTS, H_COMPONENTS, MATERIAL_STENCIL, MATERIAL_STENCIL_DOUBLE, UPML_AXES,
+                          YeeLayout)
+from ..layout.approximation import approximate_material
+from ..ops.coef import Coef
+from ..parallel.domain import Domain, box_empty, box_intersect
+from ..utils.assertions import FdtdError, fdtd_assert
+from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
+from ..utils import logging as log
+from .tfsf import build_tfsf_tables, incident_line_length
+
+Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
+
+
+@dataclass
+class SchemeConfig:
+    """Everything that defines a run (mirrors the relevant reference flags)."""
+
+    scheme: str = "3d"                       # 3d | tmz | tez | 1d
+    size: Tuple[int, int, int] = (100, 100, 100)
+    time_steps: int = 100
+    amplitude_steps: int = 10
+    pml_size: Tuple[int, int, int] = (10, 10, 10)
+    tfsf_size: Tuple[int, int, int] = (20, 20, 20)
+    ntff_size: Tuple[int, int, int] = (15, 15, 15)
+    theta: float = 90.0                      # degrees
+    phi: float = 0.0
+    psi: float = 90.0
+    use_pml: bool = False
+    pml_type: str = "upml"
+    use_tfsf: bool = False
+    use_ntff: bool = False
+    use_metamaterials: bool = False
+    use_amp_mode: bool = False
+    use_point_source: bool = False
+    double_material_precision: bool = False
+    dx: float = 0.0005
+    wavelength: float = 0.02
+    courant: float = 0.5
+    dtype: str = "f64"
+    complex_values: bool = False
+    scene: str = "reference"
+    sphere_eps: float = 2.0
+    sphere_radius: float = 20.0
+    sphere_center: Tuple[float, float, float] = (40.5, 40.5, 40.5)
+    source: str = "sine"                     # sine | gaussian
+    gaussian_width: float = 30.0
+    gaussian_delay: float = 120.0
+    ntff_step: int = 100
+    check_finite: bool = False
+    finite_check_step: int = 100
+
+    @classmethod
+    def from_settings(cls, s) -> "SchemeConfig":
+        dim = s.dimension
+        if dim == 3:
+            scheme = "3d"
+            size = (s.sizeX, s.sizeY, s.sizeZ)
+        elif dim == 2:
+            scheme = s.mode2D
+            size = (s.sizeX, s.sizeY, 1)
+        else:
+            scheme = "1d"
+            size = (s.sizeX, 1, 1)
+        return cls(
+            scheme=scheme, size=size, time_steps=s.numTimeSteps, amplitude_steps=s.numAmplitudeTimeSteps,
+            pml_size=(s.pmlSizeX, s.pmlSizeY, s.pmlSizeZ), tfsf_size=(s.tfsfSizeX, s.tfsfSizeY, s.tfsfSizeZ),
+            ntff_size=(s.ntffSizeX, s.ntffSizeY, s.ntffSizeZ), theta=s.incidentWaveAngle1,
+            phi=s.incidentWaveAngle2, psi=s.incidentWaveAngle3, use_pml=s.doUsePML, pml_type=s.pmlType,
+            use_tfsf=s.doUseTFSF, use_ntff=s.doUseNTFF, use_metamaterials=s.doUseMetamaterials,
+            use_amp_mode=s.doUseAmplitudeMode, use_point_source=s.doUsePointSource,
+            double_material_precision=s.doUseDoubleMaterialPrecision, dx=s.gridStep,
+            wavelength=s.sourceWaveLength, courant=s.courantNum, dtype=s.valueType,
+            complex_values=s.doUseComplexFieldValues, scene=s.scene, sphere_eps=s.sphereEps,
+            sphere_radius=s.sphereRadius, sphere_center=(s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ),
+            source=s.sourceType, gaussian_width=s.gaussianWidth, gaussian_delay=s.gaussianDelay,
+            ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep)
+
+
+def _torch_dtype(name: str):
+    return {"f32": torch.float32, "f64": torch.float64}[name]
+
+
+class YeeScheme:
+    """A Yee FDTD solver on one (possibly decomposed) domain."""
+
+    def __init__(self, cfg: SchemeConfig, ops, domain: Optional[Domain] = None, halo=None):
+        self.cfg = cfg
+        self.ops = ops
+        self.device = ops.device
+        self.dtype = _torch_dtype(cfg.dtype)
+        fdtd_assert(ops.dtype == self.dtype, "backend dtype mismatch")
+        self.domain = domain if domain is not None else Domain.serial(cfg.size)
+        fdtd_assert(tuple(self.domain.global_size) == tuple(cfg.size), "domain does not match grid size")
+        self.halo = halo
+        scheme = cfg.scheme
+        psi = cfg.psi
+        if scheme == "tmz":
+            psi = 90.0
+        elif scheme == "tez":
+            psi = 0.0
+        self.layout = YeeLayout(cfg.size, scheme, tuple(cfg.pml_size) if cfg.use_pml else (0, 0, 0),
+                                tuple(cfg.tfsf_size), math.radians(cfg.theta) if scheme == "3d" else PI / 2,
+                                math.radians(cfg.phi), math.radians(psi), cfg.double_material_precision)
+        if ops.layout is None:
+            ops.layout = self.layout
+        self.comps = self.layout.components
+        self.e_comps = tuple(c for c in self.comps if c[0] == "E")
+        self.h_comps = tuple(c for c in self.comps if c[0] == "H")
+        self.planes = 2 if cfg.complex_values else 1
+        self.use_upml_chain = (cfg.use_pml and cfg.pml_type == "upml") or cfg.use_metamaterials
+        self.use_cpml = cfg.use_pml and cfg.pml_type == "cpml" and not cfg.use_metamaterials
+        self.t = 0
+        self.sub_step = 0
+        self.timers: Dict[str, float] = {}
+        self.hooks: List[Callable[["YeeScheme", int], None]] = []
+        self.initialized = False
+
+    # ================================================================ init
+    def init_scheme(self, dx: Optional[float] = None, source_frequency: Optional[float] = None) -> None:
+        """``Scheme3D::initScheme`` (Scheme3D.cpp:3388-3402): dt from the
+        Courant number and the incident line's relative phase velocity."""
+        cfg = self.cfg
+        self.dx = cfg.dx if dx is None else dx
+        self.source_frequency = SPEED_OF_LIGHT / cfg.wavelength if source_frequency is None else source_frequency
+        self.wavelength = SPEED_OF_LIGHT / self.source_frequency
+        self.courant = cfg.courant
+        self.dt = self.dx * self.courant / SPEED_OF_LIGHT
+        n_lambda = self.wavelength / self.dx
+        if cfg.scheme == "3d":
+            v0 = phase_velocity_incident_wave_3d(self.dx, self.wavelength, self.courant, n_lambda, PI / 2, 0.0)
+            v = phase_velocity_incident_wave_3d(self.dx, self.wavelength, self.courant, n_lambda,
+                                                self.layout.theta, self.layout.phi)
+        else:
+            v0 = phase_velocity_incident_wave_2d(self.dx, self.wavelength, self.courant, n_lambda, 0.0)
+            v = phase_velocity_incident_wave_2d(self.dx, self.wavelength, self.courant, n_lambda, self.layout.phi)
+        self.rel_phase_velocity = v0 / v
+
+    # ------------------------------------------------------------------
+    def _global_box(self, comp: str) -> Box:
+        return self.layout.global_range(comp)
+
+    def local_box(self, comp: str, window: Optional[Box] = None) -> Box:
+        """Local box on which ``comp`` is updated (global range ∩ window ∩
+        allocated region), in local indices."""
+        g = self._global_box(comp)
+        if window is None:
+            window = self.domain.owned_global()
+        b = box_intersect(box_intersect(g, window), self.domain.allocated_global())
+        return self.domain.to_local(b)
+
+    def _zeros(self):
+        return torch.zeros(self.domain.shape, dtype=self.dtype, device=self.device)
+
+    def init_grids(self) -> None:
+        """Allocate fields, evaluate materials and build every static table
+        (``Scheme3D::initGrids``, Scheme3D.cpp:3405-4067)."""
+        if not hasattr(self, "dt"):
+            self.init_scheme()
+        cfg = self.cfg
+        t0 = time.perf_counter()
+        dom = self.domain
+        shape = dom.shape
+        self.F: List[Dict[str, torch.Tensor]] = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+
+        self.scene = Scene(cfg.scene, cfg.scheme, self.source_frequency, cfg.sphere_eps, cfg.sphere_radius,
+                           tuple(cfg.sphere_center))
+        vacuum = self.scene.is_vacuum(cfg.use_metamaterials)
+        self.vacuum = vacuum
+        sampler = MaterialSampler(self.layout, self.scene, dom.origin, shape, self.device)
+        self.sampler = sampler
+        dt, dx = self.dt, self.dx
+
+        # ---- per-component material (relative eps / mu at the component)
+        self.mat: Dict[str, Optional[torch.Tensor]] = {}
+        for c in self.comps:
+            if vacuum:
+                self.mat[c] = None
+            else:
+                self.mat[c] = sampler.averaged(c, "eps" if c[0] == "E" else "mu")
+
+        # ---- plain-update coefficients Cb = dt / (eps eps0 dx), Db = dt / (mu mu0 dx)
+        self.cb: Dict[str, Coef] = {}
+        for c in self.comps:
+            base = EPS0 if c[0] == "E" else MU0
+            if self.mat[c] is None:
+                self.cb[c] = Coef(dt / (base * dx))
+            else:
+                self.cb[c] = Coef(dt / (base * dx), cell=(1.0 / self.mat[c]).to(self.dtype))
+
+        if self.use_upml_chain:
+            self._init_upml()
+        if self.use_cpml:
+            from .cpml import CPML
+            self.cpml = CPML(self)
+        if cfg.use_tfsf:
+            self._init_tfsf()
+        self._init_source()
+        if cfg.use_amp_mode:
+            self.amp = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+        self.initialized = True
+        self.timers["init"] = time.perf_counter() - t0
+
+    # ------------------------------------------------------------------ UPML
+    def _sigma_profiles(self) -> Dict[int, torch.Tensor]:
+        """Global-eps-layout sigma profile along each axis, restricted to the
+        local eps region (float64)."""
+        dom = self.domain
+        dbl = self.layout.double_material_precision
+        prof = {}
+        for a in range(3):
+            n_glob = (self.cfg.size[a] + 1) * (2 if dbl else 1)
+            pml = self.layout.pml_size[a] if (self.cfg.use_pml and self.layout.active(a)) else 0
+            p = sigma_profile_1d(n_glob, pml, self.dx, dbl)
+            lo = dom.origin[a] * (2 if dbl else 1)
+            n_loc = (dom.shape[a] + 1) * (2 if dbl else 1)
+            seg = np.zeros(n_loc)
+            take = p[max(lo, 0):max(lo, 0) + n_loc]
+            seg[:take.size] = take
+            if not self.layout.active(a):
+                seg[:] = 0.0
+            prof[a] = torch.as_tensor(seg, dtype=torch.float64, device=self.device)
+        return prof
+
+    def _avg_profile(self, comp: str, axis: int, p: torch.Tensor) -> torch.Tensor:
+        """sigma along ``axis`` averaged at ``comp`` positions (1D, local)."""
+        n = self.domain.shape[axis]
+        if not self.layout.active(axis):
+            return torch.zeros(n, dtype=torch.float64, device=self.device)
+        pts = []
+        if not self.layout.double_material_precision:
+            for off in MATERIAL_STENCIL[comp]:
+                o = off[axis]
+                pts.append(p[o:o + n])
+        else:
+            for base, sub in MATERIAL_STENCIL_DOUBLE[comp]:
+                o = 2 * base[axis] + sub[axis]
+                pts.append(p[o:o + 2 * n:2])
+        return approximate_material(pts)
+
+    def _init_upml(self) -> None:
+        cfg = self.cfg
+        dt, dx = self.dt, self.dx
+        prof = self._sigma_profiles()
+        dtp = self.dtype
+        self.upml: Dict[str, dict] = {}
+        for c in self.comps:
+            aD, aCa, aCb = UPML_AXES[c]
+            sD = self._avg_profile(c, aD, prof[aD])
+            sCa = self._avg_profile(c, aCa, prof[aCa])
+            sCb = self._avg_profile(c, aCb, prof[aCb])
+            two = 2 * EPS0  # the reference normalises H-side sigma by eps0 too (Scheme3D.cpp:1198-1201)
+            caD = (two - sD * dt) / (two + sD * dt)
+            cbD = (two * dt / dx) / (two + sD * dt)
+            caE = (two - sCa * dt) / (two + sCa * dt)
+            cbE_a = (two + sCb * dt)
+            ccE_a = -(two - sCb * dt)
+            inv_ca = 1.0 / (two + sCa * dt)
+            drude = cfg.use_metamaterials
+            base = EPS0 if c[0] == "E" else MU0
+            if drude:
+                inv_mod = None
+                inv_mod_s = 1.0
+            elif self.mat[c] is None:
+                inv_mod = None
+                inv_mod_s = 1.0 / base
+            else:
+                inv_mod = (1.0 / (self.mat[c] * base))
+                inv_mod_s = 1.0
+
+            def prof_coef(scalar, axis_vals: Dict[int, torch.Tensor], cell=None) -> Coef:
+                k = Coef(scalar)
+                for a, v in axis_vals.items():
+                    v = v.to(dtp)
+                    if a == 0:
+                        k.px = v if k.px is None else k.px * v
+                    elif a == 1:
+                        k.py = v if k.py is None else k.py * v
+                    else:
+                        k.pz = v if k.pz is None else k.pz * v
+                if cell is not None:
+                    k.cell = cell.to(dtp)
+                return k
+
+            st = {
+                "caD": prof_coef(1.0, {aD: caD}),
+                "cbD": prof_coef(1.0, {aD: cbD}),
+                "caE": prof_coef(1.0, {aCa: caE}),
+                "cbE": prof_coef(inv_mod_s, {aCb: cbE_a, aCa: inv_ca}, inv_mod),
+                "ccE": prof_coef(inv_mod_s, {aCb: ccE_a, aCa: inv_ca}, inv_mod),
+            }
+            nlev = 3 if drude else 2
+            st["D"] = [[self._zeros() for _ in range(nlev)] for _ in range(self.planes)]
+            if drude:
+                st["D1"] = [[self._zeros() for _ in range(3)] for _ in range(self.planes)]
+                eps_c = self.sampler.averaged(c, "eps" if c[0] == "E" else "mu")
+                w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
+                e0 = base
+                A = 4 * e0 * eps_c + 2 * dt * e0 * eps_c * g + e0 * dt * dt * w * w
+                st["b0"] = Coef(1.0, cell=((4 + 2 * dt * g) / A).to(dtp))
+                st["b1"] = Coef(1.0, cell=(-8.0 / A).to(dtp))
+                st["b2"] = Coef(1.0, cell=((4 - 2 * dt * g) / A).to(dtp))
+                st["ma1"] = Coef(1.0, cell=(-(2 * e0 * dt * dt * w * w - 8 * e0 * eps_c) / A).to(dtp))
+                st["ma2"] = Coef(1.0, cell=(-(4 * e0 * eps_c - 2 * dt * e0 * eps_c * g + e0 * dt * dt * w * w) / A).to(dtp))
+            self.upml[c] = st
+
+    # ----------------------------------------------------------------- TF/SF
+    def _init_tfsf(self) -> None:
+        n = incident_line_length(self.cfg.size, self.cfg.scheme)
+        self.inc_len = n
+        self.einc = [torch.zeros(n, dtype=self.dtype, device=self.device) for _ in range(self.planes)]
+        self.hinc = [torch.zeros(n, dtype=self.dtype, device=self.device) for _ in range(self.planes)]
+        self.inc_ce = self.dt / (self.rel_phase_velocity * EPS0 * self.dx)
+        self.inc_ch = self.dt / (self.rel_phase_velocity * MU0 * self.dx)
+        # tables on the full allocated region; each step filters by window
+        coefs = {}
+        for c in self.comps:
+            coefs[c] = self.upml[c]["cbD"] if self.use_upml_chain else self.cb[c]
+        alloc = self.domain.allocated_global()
+        boxes = {c: self.local_box(c, alloc) for c in self.comps}
+        self.tfsf = build_tfsf_tables(self.layout, self.comps, self.domain.origin, self.domain.shape, boxes,
+                                      coefs, self.device, self.dtype, n)
+
+    # ---------------------------------------------------------------- source
+    def _init_source(self) -> None:
+        cfg = self.cfg
+        size = cfg.size
+        self.point_source = None
+        self.line_source = None
+        if cfg.use_tfsf and not cfg.use_point_source:
+            return
+        if cfg.scheme == "3d":
+            comp, g = "Ez", (size[0] // 2, size[1] // 2, size[2] // 2)
+        elif cfg.scheme == "tmz":
+            # reference SchemeTMz.cpp:1345: Ez at (70, Ny/2)
+            comp, g = "Ez", (70 if size[0] > 140 else size[0] // 2, size[1] // 2, 0)
+        elif cfg.scheme == "tez":
+            comp, g = "Hz", (size[0] // 2, size[1] // 2, 0)
+        else:
+            comp, g = "Ez", (size[0] // 2, 0, 0)
+        li = self.domain.local_index(g)
+        self.point_source = (comp, li, g)
+        if cfg.use_amp_mode and cfg.scheme == "3d":
+            # amplitude mode drives an Ez z-line at (Nx/8, Ny/2, k in the non-PML range)
+            # (Scheme3D.cpp:2995-3013)
+            lo = self.layout.pml_size[2] if cfg.use_pml else 0
+            hi = size[2] - lo
+            offs = []
+            for k in range(lo, hi):
+                li2 = self.domain.local_index((size[0] // 8, size[1] // 2, k))
+                if li2 is not None:
+                    s = self.domain.shape
+                    offs.append((li2[0] * s[1] + li2[1]) * s[2] + li2[2])
+            self.line_source = ("Ez", torch.as_tensor(offs, dtype=torch.int64, device=self.device))
+
+    def source_value(self, t: int, plane: int) -> float:
+        cfg = self.cfg
+        if cfg.source == "gaussian":
+            v = math.exp(-((t - cfg.gaussian_delay) / cfg.gaussian_width) ** 2)
+            return v if plane == 0 else 0.0
+        arg = self.dt * t * 2 * PI * self.source_frequency
+        return math.sin(arg) if plane == 0 else math.cos(arg)
+
+    # ================================================================ stepping
+    def _window(self, kind: str) -> Box:
+        return self.domain.window(kind, self.sub_step)
+
+    def _boxes(self, comps, kind) -> Dict[str, Box]:
+        w = self._window(kind)
+        return {c: self.local_box(c, w) for c in comps}
+
+    def _update(self, kind: str, p: int, windows: Optional[Sequence[Box]] = None) -> None:
+        """Update all E (or H) components of plane ``p`` on the given global
+        windows (default: this sub-step's window)."""
+        comps = self.e_comps if kind == "E" else self.h_comps
+        F = self.F[p]
+        if windows is None:
+            windows = [self._window(kind)]
+        for w in windows:
+            boxes = {c: self.local_box(c, w) for c in comps}
+            if self.use_upml_chain:
+                for c in comps:
+                    self._upml_region(kind, c, p, boxes[c])
+                continue
+            self.ops.curl_update(kind, boxes, F, F, self.cb)
+            if self.use_cpml:
+                self.cpml.apply(kind, p, boxes)
+            if self.cfg.use_tfsf:
+                inc = self.hinc[p] if kind == "E" else self.einc[p]
+                for c in comps:
+                    for tab in self.tfsf[c]:
+                        self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
+        if self.use_upml_chain:
+            for c in comps:
+                self._upml_rotate(c, p)
+
+    def _upml_region(self, kind: str, c: str, p: int, box: Box) -> None:
+        F = self.F[p]
+        st = self.upml[c]
+        D = st["D"][p]
+        Dn = D[-1]
+        Dc = D[0]
+        self.ops.curl_general(kind, c, box, Dn, Dc, F, st["caD"], st["cbD"])
+        if self.cfg.use_tfsf:
+            inc = self.hinc[p] if kind == "E" else self.einc[p]
+            for tab in self.tfsf[c]:
+                self.ops.tfsf_apply(Dn, tab, inc, box)
+        if self.cfg.use_metamaterials:
+            D1 = st["D1"][p]
+            D1n, D1c, D1p = D1[2], D1[0], D1[1]
+            Dp = D[1]
+            self.ops.lincomb(D1n, box, [(st["b0"], Dn), (st["b1"], Dc), (st["b2"], Dp),
+                                        (st["ma1"], D1c), (st["ma2"], D1p)])
+            src_new, src_old = D1n, D1c
+        else:
+            src_new, src_old = Dn, Dc
+        self.ops.lincomb(F[c], box, [(st["caE"], F[c]), (st["cbE"], src_new), (st["ccE"], src_old)])
+
+    def _upml_rotate(self, c: str, p: int) -> None:
+        """new -> cur -> prev (the reference's ``nextTimeStep`` shift)."""
+        st = self.upml[c]
+        D = st["D"][p]
+        if self.cfg.use_metamaterials:
+            D[0], D[1], D[2] = D[2], D[0], D[1]
+            D1 = st["D1"][p]
+            D1[0], D1[1], D1[2] = D1[2], D1[0], D1[1]
+        else:
+            D[0], D[1] = D[1], D[0]
+
+    def state_tensors(self) -> List[torch.Tensor]:
+        """Every array that carries state between steps (for deep-halo
+        exchanges and checkpoints)."""
+        out = []
+        for p in range(self.planes):
+            out += [self.F[p][c] for c in self.comps]
+            if self.use_upml_chain:
+                for c in self.comps:
+                    out += list(self.upml[c]["D"][p])
+                    if self.cfg.use_metamaterials:
+                        out += list(self.upml[c]["D1"][p])
+            if self.use_cpml:
+                out += self.cpml.state_tensors(p)
+        return out
+
+    def _apply_sources(self, t: int, p: int) -> None:
+        if self.line_source is not None and self.cfg.use_amp_mode and self.in_amplitude:
+            comp, offs = self.line_source
+            if offs.numel():
+                self.ops.set_values(self.F[p][comp], offs, self.source_value(t, p))
+            return
+        if self.point_source is not None:
+            comp, li, _ = self.point_source
+            if li is not None:
+                self.ops.set_value(self.F[p][comp], li, self.source_value(t, p))
+
+    in_amplitude = False
+
+    def step(self) -> None:
+        """Advance one full leapfrog step."""
+        t = self.t
+        cfg = self.cfg
+        B = self.domain.buffer_size
+        halo = self.halo
+        deep = halo is not None and B > 1
+        if deep and self.sub_step == 0:
+            halo.exchange_all(self)
+        for p in range(self.planes):
+            if cfg.use_tfsf:
+                self.ops.inc_step_e(self.einc[p], self.hinc[p], self.inc_ce, self.source_value(t, p))
+            if halo is not None and not deep:
+                halo.finish_and_update(self, "E", p)
+            else:
+                self._update("E", p)
+            self._apply_sources(t, p)
+            if halo is not None and not deep:
+                halo.start(self, "E", p)
+            if cfg.use_tfsf:
+                self.ops.inc_step_h(self.einc[p], self.hinc[p], self.inc_ch)
+            if halo is not None and not deep:
+                halo.finish_and_update(self, "H", p)
+                halo.start(self, "H", p)
+            else:
+                self._update("H", p)
+        self.t += 1
+        if deep:
+            self.sub_step = (self.sub_step + 1) % B
+        for h in self.hooks:
+            h(self, self.t)
+        if cfg.check_finite and self.t % max(1, cfg.finite_check_step) == 0:
+            self.check_finite()
+
+    def perform_steps(self, n: Optional[int] = None) -> None:
+        """``Scheme3D::performSteps`` (Scheme3D.cpp:3336-3385)."""
+        n = self.cfg.time_steps if n is None else n
+        for _ in range(n):
+            self.step()
+        if self.cfg.use_amp_mode:
+            self.perform_amplitude_steps()
+
+    # ------------------------------------------------------------ amplitude
+    def amplitude_box(self, c: str) -> Box:
+        """Computation box of ``c`` minus PML cells (Scheme3D.cpp:3016-3030)."""
+        lo_g, hi_g = self._global_box(c)
+        m = self.layout.min_coord_fp(c)
+        left, right = self.layout.pml_borders()
+        lo, hi = list(lo_g), list(hi_g)
+        for a in self.layout.axes:
+            if left[a] != right[a]:
+                lo[a] = max(lo[a], int(math.ceil(left[a] - m[a])))
+                hi[a] = min(hi[a], int(math.ceil(right[a] - m[a])))
+        b = box_intersect((tuple(lo), tuple(hi)), self.domain.owned_global())
+        return self.domain.to_local(b)
+
+    def perform_amplitude_steps(self) -> int:
+        """Steady-state mode: keep stepping until no cell's running max |f|
+        grows by more than ``ACCURACY`` (relative), or until
+        ``amplitude_steps`` extra steps.  The reference loop never sets its
+        stable flag (``Scheme3D.cpp:2945-3291``); this implements the
+        documented intent.  Returns the number of steps taken."""
+        fdtd_assert(self.planes == 1, "amplitude mode needs real field values (reference asserts the same)")
+        self.in_amplitude = True
+        taken = 0
+        try:
+            for _ in range(self.cfg.amplitude_steps):
+                self.step()
+                taken += 1
+                changed = 0
+                for c in self.comps:
+                    changed += self.ops.amplitude_update(self.F[0][c], self.amp[0][c], self.amplitude_box(c),
+                                                         ACCURACY)
+                if self.halo is not None:
+                    changed = self.halo.allreduce_sum(changed)
+                if changed == 0 and taken > 1:
+                    self.amplitude_converged = True
+                    return taken
+            self.amplitude_converged = False
+            log.log(0, "amplitude mode: stable state not reached after %d steps" % taken)
+            return taken
+        finally:
+            self.in_amplitude = False
+
+    # -------------------------------------------------------------- checks
+    def check_finite(self) -> None:
+        for p in range(self.planes):
+            for c in self.comps:
+                m = self.ops.maxabs(self.F[p][c], ((0, 0, 0), tuple(self.domain.shape)))
+                if not math.isfinite(m):
+                    raise FdtdError("non-finite values in %s at step %d" % (c, self.t))
+
+    # -------------------------------------------------------------- access
+    def field(self, comp: str, plane: int = 0) -> torch.Tensor:
+        return self.F[plane][comp]
+
+    def owned_field(self, comp: str, plane: int = 0) -> torch.Tensor:
+        """View of the owned (non-ghost) part of a field."""
+        gl = self.domain.ghost_lo
+        s = self.domain.owned_shape
+        return self.F[plane][comp][gl[0]:gl[0] + s[0], gl[1]:gl[1] + s[1], gl[2]:gl[2] + s[2]]
+
+    def cells(self) -> int:
+        n = 1
+        for v in self.cfg.size:
+            n *= v
+        return n

@@ -1,0 +1,381 @@
+"""HIP backend: the solver operations as launches of the hand-written gfx950
+kernels in ``libfdtd3d_hip.so`` (``fdtd3d_amd/csrc/*.hip``).
+
+The library is a plain C ABI loaded with ctypes *after* ``import torch``, so
+it binds to the HIP runtime PyTorch already loaded; every launch goes to
+``torch.cuda.current_stream()``, which makes the whole time step capturable
+in a HIP graph (``torch.cuda.CUDAGraph``) and orders it with RCCL work issued
+by ``torch.distributed``.
+
+Every entry point validates on the host that the boxes it passes keep all
+stencil reads inside the arrays (the kernels do no bounds checks beyond their
+boxes), and raises if the library is missing -- a GPU run never silently falls
+back to the torch reference ops.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..layout.yee import YeeLayout
+from .coef import Coef
+
+Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
+
+_LIB = None
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libfdtd3d_hip.so")
+
+c_int = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_double = ctypes.c_double
+c_vp = ctypes.c_void_p
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load_library(build_if_missing: bool = True):
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(_LIB_PATH) and build_if_missing:
+        from .build import build
+        build(exe=False)
+    if not os.path.exists(_LIB_PATH):
+        raise HipError("libfdtd3d_hip.so not found at %s: run `python -m fdtd3d_amd.ops.build`" % _LIB_PATH)
+    _LIB = ctypes.CDLL(_LIB_PATH)
+    _LIB.fdtd_abi_version.restype = c_int
+    return _LIB
+
+
+def available() -> bool:
+    try:
+        load_library(build_if_missing=False)
+    except (HipError, OSError):
+        return False
+    return torch.cuda.is_available()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise HipError("%s failed: hipError %d" % (what, rc))
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _box_arr(boxes: Sequence[Box]):
+    vals = []
+    for b in boxes:
+        vals += list(b[0]) + list(b[1])
+    return (c_int * len(vals))(*vals)
+
+
+def _empty(b: Box) -> bool:
+    return any(b[1][d] <= b[0][d] for d in range(3))
+
+
+class HipOps:
+    name = "hip"
+
+    def __init__(self, layout: Optional[YeeLayout], device, dtype, xchunk: int = 0):
+        self.layout = layout
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise HipError("the HIP backend needs a GPU device, got %s" % self.device)
+        self.dtype = dtype
+        self.suf = {torch.float32: "f32", torch.float64: "f64"}[dtype]
+        self.lib = load_library()
+        self.xchunk = xchunk
+        self._fn: Dict[str, object] = {}
+        self.launches = 0
+
+    def fn(self, name: str):
+        f = self._fn.get(name)
+        if f is None:
+            f = getattr(self.lib, "fdtd_%s_%s" % (name, self.suf))
+            f.restype = c_int
+            self._fn[name] = f
+        return f
+
+    # ------------------------------------------------------------ validation
+    def _check_tensor(self, t: torch.Tensor, shape=None) -> None:
+        if t.device.type != "cuda" or t.dtype != self.dtype or not t.is_contiguous():
+            raise HipError("HIP op got a tensor on %s/%s (contiguous=%s)" % (t.device, t.dtype, t.is_contiguous()))
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise HipError("HIP op shape mismatch %s vs %s" % (tuple(t.shape), tuple(shape)))
+
+    def _check_stencil_box(self, kind: str, comp: str, box: Box, shape) -> None:
+        for d in range(3):
+            if box[0][d] < 0 or box[1][d] > shape[d]:
+                raise HipError("box %s of %s outside array %s" % (box, comp, shape))
+        for (s, axis, _) in self.layout.curl_terms(comp):
+            if kind == "E" and box[0][axis] < 1:
+                raise HipError("E box %s of %s would read index -1 along axis %d" % (box, comp, axis))
+            if kind == "H" and box[1][axis] > shape[axis] - 1:
+                raise HipError("H box %s of %s would read past the array along axis %d" % (box, comp, axis))
+
+    def _coef_args(self, c: Coef):
+        ps = (c_vp * 4)(*[None if t is None else t.data_ptr() for t in (c.px, c.py, c.pz, c.cell)])
+        for t in (c.px, c.py, c.pz, c.cell):
+            if t is not None:
+                self._check_tensor(t)
+        return c_double(c.scalar), ps
+
+    @staticmethod
+    def _cell_or_none(c: Coef):
+        if c.px is not None or c.py is not None or c.pz is not None:
+            raise HipError("fast-path coefficient must be scalar or per-cell")
+        return c.cell
+
+    # ------------------------------------------------------------------ curl
+    def curl_update(self, kind: str, boxes: Dict[str, Box], dst: Dict[str, torch.Tensor],
+                    src: Dict[str, torch.Tensor], cb: Dict[str, Coef]) -> None:
+        lay = self.layout
+        comps = list(boxes.keys())
+        any_t = dst[comps[0]]
+        shape = tuple(any_t.shape)
+        for c in comps:
+            self._check_tensor(dst[c], shape)
+            if not _empty(boxes[c]):
+                self._check_stencil_box(kind, c, boxes[c], shape)
+        scheme = lay.scheme
+        st = _stream()
+        if scheme == "3d":
+            names = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
+            other = ("Hx", "Hy", "Hz") if kind == "E" else ("Ex", "Ey", "Ez")
+            for c in other:
+                self._check_tensor(src[c], shape)
+            per = [self._cell_or_none(cb[c]) for c in names]
+            if any(p is None for p in per) and not all(p is None for p in per):
+                raise HipError("mixed scalar/per-cell coefficients")
+            scal = cb[names[0]].scalar
+            if per[0] is None and any(cb[c].scalar != scal for c in names):
+                raise HipError("scalar coefficients must agree across components")
+            bx = _box_arr([boxes[c] for c in names])
+            fn = self.fn("update_e3d" if kind == "E" else "update_h3d")
+            per_p = [_ptr(p) if p is not None else None for p in per]
+            if per[0] is not None:
+                scal_use = 1.0
+                # per-cell arrays already include the scalar? No: multiply on the host once
+                per_p = [_ptr(self._scaled_cell(cb[c])) for c in names]
+            else:
+                scal_use = scal
+            rc = fn(*[_ptr(dst[c]) for c in names], *[_ptr(src[c]) for c in other], *per_p, c_double(scal_use),
+                    c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), bx, c_int(self.xchunk), st)
+            _check(rc, "update_%s3d" % kind.lower())
+            self.launches += 1
+            return
+        if scheme == "tmz":
+            if kind == "E":
+                b = boxes["Ez"]
+                rc = self.fn("tmz_e")(_ptr(dst["Ez"]), _ptr(src["Hx"]), _ptr(src["Hy"]),
+                                      self._cellp(cb["Ez"]), c_double(self._scal(cb["Ez"])),
+                                      c_int(shape[0]), c_int(shape[1]), _box_arr([b]), c_int(0), st)
+            else:
+                rc = self.fn("tmz_h")(_ptr(dst["Hx"]), _ptr(dst["Hy"]), _ptr(src["Ez"]),
+                                      self._cellp(cb["Hx"]), self._cellp(cb["Hy"]), c_double(self._scal(cb["Hx"])),
+                                      c_int(shape[0]), c_int(shape[1]), _box_arr([boxes["Hx"], boxes["Hy"]]),
+                                      c_int(0), st)
+        elif scheme == "tez":
+            if kind == "E":
+                rc = self.fn("tez_e")(_ptr(dst["Ex"]), _ptr(dst["Ey"]), _ptr(src["Hz"]),
+                                      self._cellp(cb["Ex"]), self._cellp(cb["Ey"]), c_double(self._scal(cb["Ex"])),
+                                      c_int(shape[0]), c_int(shape[1]), _box_arr([boxes["Ex"], boxes["Ey"]]),
+                                      c_int(0), st)
+            else:
+                rc = self.fn("tez_h")(_ptr(dst["Hz"]), _ptr(src["Ex"]), _ptr(src["Ey"]),
+                                      self._cellp(cb["Hz"]), c_double(self._scal(cb["Hz"])),
+                                      c_int(shape[0]), c_int(shape[1]), _box_arr([boxes["Hz"]]), c_int(0), st)
+        else:  # 1d
+            if kind == "E":
+                b = boxes["Ez"]
+                rc = self.fn("1d_e")(_ptr(dst["Ez"]), _ptr(src["Hy"]), self._cellp(cb["Ez"]),
+                                     c_double(self._scal(cb["Ez"])), c_int(b[0][0]), c_int(b[1][0] if not _empty(b) else b[0][0]), st)
+            else:
+                b = boxes["Hy"]
+                rc = self.fn("1d_h")(_ptr(dst["Hy"]), _ptr(src["Ez"]), self._cellp(cb["Hy"]),
+                                     c_double(self._scal(cb["Hy"])), c_int(b[0][0]), c_int(b[1][0] if not _empty(b) else b[0][0]), st)
+        _check(rc, "%s %s update" % (scheme, kind))
+        self.launches += 1
+
+    # per-cell coefficient arrays for the fast kernels are scalar*cell, cached
+    def _scaled_cell(self, c: Coef) -> torch.Tensor:
+        key = "_scaled"
+        cached = getattr(c, key, None)
+        if cached is None:
+            cached = (c.cell * c.scalar).to(self.dtype).contiguous()
+            setattr(c, key, cached)
+        return cached
+
+    def _cellp(self, c: Coef):
+        self._cell_or_none(c)
+        return None if c.cell is None else _ptr(self._scaled_cell(c))
+
+    @staticmethod
+    def _scal(c: Coef) -> float:
+        return 1.0 if c.cell is not None else c.scalar
+
+    def curl_general(self, kind: str, comp: str, box: Box, out: torch.Tensor, inp: torch.Tensor,
+                     src: Dict[str, torch.Tensor], ca: Coef, cb: Coef) -> None:
+        if _empty(box):
+            return
+        shape = tuple(out.shape)
+        self._check_tensor(out, shape)
+        self._check_tensor(inp, shape)
+        self._check_stencil_box(kind, comp, box, shape)
+        terms = self.layout.curl_terms(comp)
+        srcs = (c_vp * 2)(*[src[s].data_ptr() for (s, _, _) in terms] + [0] * (2 - len(terms)))
+        axes = (c_int * 2)(*[a for (_, a, _) in terms] + [0] * (2 - len(terms)))
+        signs = (c_int * 2)(*[g for (_, _, g) in terms] + [1] * (2 - len(terms)))
+        for (s, _, _) in terms:
+            self._check_tensor(src[s], shape)
+        cas, cap = self._coef_args(ca)
+        cbs, cbp = self._coef_args(cb)
+        rc = self.fn("curl_general")(_ptr(out), _ptr(inp), srcs, axes, signs, c_int(len(terms)),
+                                     c_int(1 if kind == "E" else 0), cas, cap, cbs, cbp, c_int(shape[1]),
+                                     c_int(shape[2]), _box_arr([box]), _stream())
+        _check(rc, "curl_general")
+        self.launches += 1
+
+    def lincomb(self, out: torch.Tensor, box: Box, terms: Sequence[Tuple[Coef, torch.Tensor]]) -> None:
+        if _empty(box):
+            return
+        shape = tuple(out.shape)
+        self._check_tensor(out, shape)
+        n = len(terms)
+        scal = (c_double * n)(*[c.scalar for c, _ in terms])
+        ptrs = []
+        for c, x in terms:
+            self._check_tensor(x, shape)
+            for t in (c.px, c.py, c.pz, c.cell):
+                if t is not None:
+                    self._check_tensor(t)
+                ptrs.append(None if t is None else t.data_ptr())
+        pa = (c_vp * len(ptrs))(*ptrs)
+        xs = (c_vp * n)(*[x.data_ptr() for _, x in terms])
+        rc = self.fn("lincomb")(_ptr(out), c_int(n), scal, pa, xs, c_int(shape[1]), c_int(shape[2]),
+                                _box_arr([box]), _stream())
+        _check(rc, "lincomb")
+        self.launches += 1
+
+    # --------------------------------------------------------------- sources
+    def set_value(self, t: torch.Tensor, idx: Sequence[int], value: float) -> None:
+        s = t.shape
+        for d in range(3):
+            if not (0 <= idx[d] < s[d]):
+                raise HipError("source index %s outside %s" % (idx, tuple(s)))
+        off = (idx[0] * s[1] + idx[1]) * s[2] + idx[2]
+        _check(self.fn("set_value")(_ptr(t), c_ll(off), c_double(value), _stream()), "set_value")
+        self.launches += 1
+
+    def set_values(self, t: torch.Tensor, flat_idx: torch.Tensor, value: float) -> None:
+        if flat_idx.numel() == 0:
+            return
+        if flat_idx.device != t.device or flat_idx.dtype != torch.int64:
+            raise HipError("set_values needs int64 indices on the field device")
+        _check(self.fn("set_values")(_ptr(t), _ptr(flat_idx), c_int(flat_idx.numel()), c_double(value), _stream()),
+               "set_values")
+        self.launches += 1
+
+    # ------------------------------------------------------------------ halo
+    def pack(self, tensors: Sequence[torch.Tensor], box: Box, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        shape = tuple(tensors[0].shape)
+        n = 1
+        for d in range(3):
+            n *= max(0, box[1][d] - box[0][d])
+            if box[0][d] < 0 or box[1][d] > shape[d]:
+                raise HipError("pack box %s outside %s" % (box, shape))
+        if out is None:
+            out = torch.empty(n * len(tensors), dtype=self.dtype, device=self.device)
+        if out.numel() < n * len(tensors):
+            raise HipError("pack buffer too small")
+        for t in tensors:
+            self._check_tensor(t, shape)
+        ptrs = (c_vp * len(tensors))(*[t.data_ptr() for t in tensors])
+        rc = self.fn("box_pack")(ptrs, _ptr(out), c_int(len(tensors)), c_int(shape[1]), c_int(shape[2]),
+                                 _box_arr([box]), _stream())
+        _check(rc, "box_pack")
+        self.launches += 1
+        return out
+
+    def unpack(self, tensors: Sequence[torch.Tensor], box: Box, buf: torch.Tensor) -> None:
+        shape = tuple(tensors[0].shape)
+        n = 1
+        for d in range(3):
+            n *= max(0, box[1][d] - box[0][d])
+            if box[0][d] < 0 or box[1][d] > shape[d]:
+                raise HipError("unpack box %s outside %s" % (box, shape))
+        if buf.numel() < n * len(tensors):
+            raise HipError("unpack buffer too small")
+        for t in tensors:
+            self._check_tensor(t, shape)
+        ptrs = (c_vp * len(tensors))(*[t.data_ptr() for t in tensors])
+        rc = self.fn("box_unpack")(ptrs, _ptr(buf), c_int(len(tensors)), c_int(shape[1]), c_int(shape[2]),
+                                   _box_arr([box]), _stream())
+        _check(rc, "box_unpack")
+        self.launches += 1
+
+    # ------------------------------------------------------------ reductions
+    def _scratch_u32(self):
+        s = getattr(self, "_u32", None)
+        if s is None:
+            s = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._u32 = s
+        return s
+
+    def maxabs(self, t: torch.Tensor, box: Box) -> float:
+        if _empty(box):
+            return 0.0
+        self._check_tensor(t)
+        s = self._scratch_u32()
+        s.zero_()
+        rc = self.fn("box_maxabs")(_ptr(t), c_int(t.shape[1]), c_int(t.shape[2]), _box_arr([box]), _ptr(s), _stream())
+        _check(rc, "box_maxabs")
+        return float(s.view(torch.float32).item())
+
+    def amplitude_update(self, f: torch.Tensor, amp: torch.Tensor, box: Box, accuracy: float) -> int:
+        if _empty(box):
+            return 0
+        self._check_tensor(f)
+        self._check_tensor(amp, tuple(f.shape))
+        s = self._scratch_u32()
+        s.zero_()
+        rc = self.fn("amplitude_update")(_ptr(f), _ptr(amp), c_int(f.shape[1]), c_int(f.shape[2]), _box_arr([box]),
+                                         c_double(accuracy), _ptr(s), _stream())
+        _check(rc, "amplitude_update")
+        return int(s.item())
+
+    # ----------------------------------------------------------------- TF/SF
+    def inc_step_e(self, einc: torch.Tensor, hinc: torch.Tensor, coef: float, source: float) -> None:
+        _check(self.fn("inc_e")(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(coef), c_double(source),
+                                _stream()), "inc_e")
+
+    def inc_step_h(self, einc: torch.Tensor, hinc: torch.Tensor, coef: float) -> None:
+        _check(self.fn("inc_h")(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(coef), _stream()), "inc_h")
+
+    def tfsf_apply(self, target: torch.Tensor, table, inc: torch.Tensor, box: Box) -> None:
+        if table.n == 0 or _empty(box):
+            return
+        if int(table.off.max()) >= target.numel() if not hasattr(table, "_checked") else False:
+            raise HipError("TF/SF table targets outside the array")
+        table._checked = True
+        rc = self.fn("tfsf_apply")(_ptr(target), _ptr(table.off), _ptr(table.i0), _ptr(table.w0), _ptr(table.w1),
+                                   _ptr(table.coef), _ptr(table.ijk), c_int(table.n), _ptr(inc), _box_arr([box]),
+                                   _stream())
+        _check(rc, "tfsf_apply")
+        self.launches += 1

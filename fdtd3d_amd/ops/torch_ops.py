@@ -1,0 +1,192 @@
+"""Reference backend: every solver operation as vectorised torch ops.
+
+This is the CPU oracle of the framework: it runs on
+any torch device, is used by the CPU test-suite and is the numerics reference
+the HIP kernels are compared against.  It implements exactly the same operation
+interface as :class:`fdtd3d_amd.ops.hip_ops.HipOps`.
+
+Operation semantics (shared by both backends):
+
+* ``curl_update(kind, boxes, dst, src, cb)`` -- fast path
+  ``dst[c] += cb[c] * curl(src)[c]`` on each component's local box.  ``curl``
+  follows :data:`fdtd3d_amd.layout.yee.CURL_TERMS` (reference ``Kernels.h``).
+* ``curl_general(kind, comp, box, out, inp, src, ca, cb)`` --
+  ``out = ca*inp + cb*curl(src)`` (UPML D/B update, ``Scheme3D.cpp:266-324``).
+* ``lincomb(out, box, terms)`` -- ``out = sum coef_i * x_i`` (Drude ADE and
+  E-from-D, ``Kernels.h:80-107``).
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..layout.yee import YeeLayout
+from .coef import Coef
+
+Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
+
+
+def box_slices(box: Box) -> Tuple[slice, slice, slice]:
+    return tuple(slice(box[0][d], box[1][d]) for d in range(3))
+
+
+def _shift(sl, axis, off):
+    s = list(sl)
+    s[axis] = slice(sl[axis].start + off, sl[axis].stop + off)
+    return tuple(s)
+
+
+def _empty(box: Box) -> bool:
+    return any(box[1][d] <= box[0][d] for d in range(3))
+
+
+class TorchOps:
+    name = "torch"
+
+    def __init__(self, layout: YeeLayout, device, dtype):
+        self.layout = layout
+        self.device = torch.device(device)
+        self.dtype = dtype
+
+    # ------------------------------------------------------------------ curl
+    def curl(self, kind: str, comp: str, sl, src: Dict[str, torch.Tensor]):
+        acc = None
+        for (s, axis, sign) in self.layout.curl_terms(comp):
+            S = src[s]
+            if kind == "E":
+                d = S[sl] - S[_shift(sl, axis, -1)]
+            else:
+                d = S[_shift(sl, axis, +1)] - S[sl]
+            if acc is None:
+                acc = d if sign > 0 else -d
+            else:
+                acc = acc + d if sign > 0 else acc - d
+        return acc
+
+    def curl_update(self, kind: str, boxes: Dict[str, Box], dst: Dict[str, torch.Tensor],
+                    src: Dict[str, torch.Tensor], cb: Dict[str, Coef]) -> None:
+        for comp, box in boxes.items():
+            if _empty(box):
+                continue
+            sl = box_slices(box)
+            c = self.curl(kind, comp, sl, src)
+            if c is None:
+                continue
+            dst[comp][sl] += cb[comp].materialize(sl) * c
+
+    def curl_general(self, kind: str, comp: str, box: Box, out: torch.Tensor, inp: torch.Tensor,
+                     src: Dict[str, torch.Tensor], ca: Coef, cb: Coef) -> None:
+        if _empty(box):
+            return
+        sl = box_slices(box)
+        c = self.curl(kind, comp, sl, src)
+        v = ca.materialize(sl) * inp[sl]
+        if c is not None:
+            v = v + cb.materialize(sl) * c
+        out[sl] = v
+
+    def lincomb(self, out: torch.Tensor, box: Box, terms: Sequence[Tuple[Coef, torch.Tensor]]) -> None:
+        if _empty(box):
+            return
+        sl = box_slices(box)
+        v = None
+        for coef, x in terms:
+            t = coef.materialize(sl) * x[sl]
+            v = t if v is None else v + t
+        out[sl] = v
+
+    # --------------------------------------------------------------- sources
+    def set_value(self, t: torch.Tensor, idx: Sequence[int], value: float) -> None:
+        t[tuple(idx)] = value
+
+    def set_values(self, t: torch.Tensor, flat_idx: torch.Tensor, value: float) -> None:
+        t.view(-1)[flat_idx] = value
+
+    # ------------------------------------------------------------------ halo
+    def pack(self, tensors: Sequence[torch.Tensor], box: Box, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        sl = box_slices(box)
+        parts = [t[sl].reshape(-1) for t in tensors]
+        buf = torch.cat(parts)
+        if out is not None:
+            out.copy_(buf)
+            return out
+        return buf
+
+    def unpack(self, tensors: Sequence[torch.Tensor], box: Box, buf: torch.Tensor) -> None:
+        sl = box_slices(box)
+        n = 1
+        for d in range(3):
+            n *= box[1][d] - box[0][d]
+        for c, t in enumerate(tensors):
+            t[sl] = buf[c * n:(c + 1) * n].view(t[sl].shape)
+
+    # ------------------------------------------------------------ reductions
+    def maxabs(self, t: torch.Tensor, box: Box) -> float:
+        if _empty(box):
+            return 0.0
+        v = t[box_slices(box)].abs()
+        if torch.isnan(v).any():
+            return float("inf")
+        return float(v.max())
+
+    def amplitude_update(self, f: torch.Tensor, amp: torch.Tensor, box: Box, accuracy: float) -> int:
+        """Running max-|f| with the reference's convergence test
+        (``Scheme3D::updateAmplitude``, Scheme3D.cpp:3294-3333): the stored
+        amplitude is raised only when it grows by more than ``accuracy``
+        (relative); returns the number of such cells."""
+        if _empty(box):
+            return 0
+        sl = box_slices(box)
+        v = f[sl].abs()
+        a = amp[sl]
+        ge = v >= a
+        diff = v - a
+        denom = torch.where(a != 0, a, torch.where(v != 0, v, torch.ones_like(v)))
+        acc = diff / denom
+        upd = ge & (acc > accuracy)
+        amp[sl] = torch.where(upd, v, a)
+        return int(upd.sum())
+
+    # ----------------------------------------------------------------- TF/SF
+    def inc_step_e(self, einc: torch.Tensor, hinc: torch.Tensor, coef: float, source: float) -> None:
+        """1D incident line, E half step (Scheme3D.cpp:25-59)."""
+        einc[1:] = einc[1:] + coef * (hinc[:-1] - hinc[1:])
+        einc[0] = source
+
+    def inc_step_h(self, einc: torch.Tensor, hinc: torch.Tensor, coef: float) -> None:
+        """1D incident line, H half step (Scheme3D.cpp:62-82)."""
+        hinc[:-1] = hinc[:-1] + coef * (einc[:-1] - einc[1:])
+
+    def tfsf_apply(self, target: torch.Tensor, table: "TfsfTable", inc: torch.Tensor, box: Box) -> None:
+        """``target[cell] += coef * (w0 inc[i0] + w1 inc[i0+1])`` for the
+        table's cells inside ``box`` (local)."""
+        if table.n == 0 or _empty(box):
+            return
+        ijk = table.ijk
+        m = torch.ones(table.n, dtype=torch.bool, device=ijk.device)
+        for d in range(3):
+            m &= (ijk[:, d] >= box[0][d]) & (ijk[:, d] < box[1][d])
+        v = (inc[table.i0] * table.w0 + inc[table.i0 + 1] * table.w1) * table.coef
+        v = torch.where(m, v, torch.zeros_like(v))
+        flat = target.view(-1)
+        flat.index_add_(0, table.off, v.to(target.dtype))
+
+
+class TfsfTable:
+    """Per-component TF/SF correction list: ``target[off] += coef *
+    (w0*inc[i0] + w1*inc[i0+1])`` (built by :mod:`fdtd3d_amd.models.tfsf`).
+    Target cells within one table are unique."""
+
+    def __init__(self, off, i0, w0, w1, coef, ijk):
+        self.off = off
+        self.i0 = i0
+        self.w0 = w0
+        self.w1 = w1
+        self.coef = coef
+        self.ijk = ijk
+
+    @property
+    def n(self) -> int:
+        return int(self.off.numel())
