@@ -190,3 +190,45 @@ inline dim3 cell_grid(const Box3& b) {
 
 FDTD_GENERIC_API(f32, float)
 FDTD_GENERIC_API(f64, double)
+
+// ---------------------------------------------------------------------------
+// CPML slab correction (fdtd3d_amd/models/cpml.py): psi = b psi + c dS;
+// F += Cb * sign * ((1/kappa - 1) dS + psi).  One thread per slab cell.
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void k_cpml(T* __restrict__ target, const T* __restrict__ src,
+                                              T* __restrict__ psi, int axis, int sign, int kind_e,
+                                              const T* __restrict__ bc, const T* __restrict__ cc,
+                                              const T* __restrict__ kc, Coef3<T> cb, int ny, int nz, Box3 b,
+                                              Box3 pb) {
+  const int k = b.lo[2] + blockIdx.x * 64 + threadIdx.x;
+  const int j = b.lo[1] + blockIdx.y * 4 + threadIdx.y;
+  const int i = b.lo[0] + blockIdx.z;
+  if (k >= b.hi[2] || j >= b.hi[1]) return;
+  const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
+  const size_t off = ((size_t)i * ny + j) * nz + k;
+  const long long s = stride[axis];
+  const T d = kind_e ? (src[off] - src[off - s]) : (src[off + s] - src[off]);
+  const int pny = pb.hi[1] - pb.lo[1], pnz = pb.hi[2] - pb.lo[2];
+  const size_t poff = ((size_t)(i - pb.lo[0]) * pny + (j - pb.lo[1])) * pnz + (k - pb.lo[2]);
+  const int n = axis == 0 ? i : (axis == 1 ? j : k);
+  const T ps = bc[n] * psi[poff] + cc[n] * d;
+  psi[poff] = ps;
+  const T corr = kc[n] * d + ps;
+  target[off] += coef_at(cb, i, j, k, off) * (sign > 0 ? corr : -corr);
+}
+}  // namespace
+
+#define FDTD_CPML_API(SUF, T)                                                                                 \
+  FDTD_API int fdtd_cpml_apply_##SUF(T* target, const T* src, T* psi, int axis, int sign, int kind_e,         \
+                                     const T* bc, const T* cc, const T* kc, double cb_s,                      \
+                                     const void* const* cb_p, int ny, int nz, const int* box,                \
+                                     const int* psi_box, void* s) {                                           \
+    Box3 b = make_box(box), pb = make_box(psi_box);                                                           \
+    if (box_empty(b)) return 0;                                                                               \
+    k_cpml<T><<<cell_grid(b), dim3(64, 4), 0, (hipStream_t)s>>>(target, src, psi, axis, sign, kind_e, bc, cc, \
+                                                                kc, coef_from<T>(&cb_s, cb_p), ny, nz, b, pb);  \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }
+FDTD_CPML_API(f32, float)
+FDTD_CPML_API(f64, double)

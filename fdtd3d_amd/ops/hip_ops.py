@@ -273,6 +273,30 @@ class HipOps:
         _check(rc, "lincomb")
         self.launches += 1
 
+    def cpml_apply(self, kind: str, target: torch.Tensor, src: torch.Tensor, axis: int, sign: int,
+                   psi: torch.Tensor, psi_box: Box, box: Box, b: torch.Tensor, c: torch.Tensor,
+                   kinv_m1: torch.Tensor, cb: Coef) -> None:
+        if _empty(box):
+            return
+        shape = tuple(target.shape)
+        self._check_tensor(target, shape)
+        self._check_tensor(src, shape)
+        for d in range(3):
+            if not (psi_box[0][d] <= box[0][d] and box[1][d] <= psi_box[1][d]):
+                raise HipError("CPML box %s outside psi box %s" % (box, psi_box))
+            if box[0][d] < 0 or box[1][d] > shape[d]:
+                raise HipError("CPML box %s outside array %s" % (box, shape))
+        if kind == "E" and box[0][axis] < 1 or kind == "H" and box[1][axis] > shape[axis] - 1:
+            raise HipError("CPML box %s would read outside the array" % (box,))
+        if tuple(psi.shape) != tuple(psi_box[1][d] - psi_box[0][d] for d in range(3)):
+            raise HipError("psi shape mismatch")
+        cbs, cbp = self._coef_args(cb)
+        rc = self.fn("cpml_apply")(_ptr(target), _ptr(src), _ptr(psi), c_int(axis), c_int(sign),
+                                   c_int(1 if kind == "E" else 0), _ptr(b), _ptr(c), _ptr(kinv_m1), cbs, cbp,
+                                   c_int(shape[1]), c_int(shape[2]), _box_arr([box]), _box_arr([psi_box]), _stream())
+        _check(rc, "cpml_apply")
+        self.launches += 1
+
     # --------------------------------------------------------------- sources
     def set_value(self, t: torch.Tensor, idx: Sequence[int], value: float) -> None:
         s = t.shape

