@@ -186,3 +186,190 @@ FDTD_API int fdtd_update_h3d_f64(double* hx, double* hy, double* hz, const doubl
   return launch_h3d<double>(hx, hy, hz, ex, ey, ez, dbx, dby, dbz, db, nx, ny, nz, boxes, xchunk,
                             (hipStream_t)stream);
 }
+
+// ===========================================================================
+// Fused leapfrog step (E then H in ONE pass, ping-pong buffers).
+//
+// The split kernels above move 72 B/cell/step in fp32 (E pass: read E,H
+// write E; H pass: read H,E write H).  Reading old E/H from one buffer pair
+// and writing new E/H to the other lets one workgroup do both half steps on a
+// tile before moving on: 48 B/cell/step.  Per workgroup: a (TY x 64) tile in
+// (y, z) marching along x.  At plane x it computes E_new(x) on the tile plus
+// one halo row (wave TY) and one halo column (extra Ex/Ey at k+64 by lane 63)
+// -- exactly the E values H_new(x-1) needs -- keeps three E planes in LDS
+// (3 buffers, one barrier per plane) and then writes H_new(x-1).  Halo E
+// values are recomputed, never exchanged, so there are no inter-workgroup
+// dependencies.  The hard point source is applied inside the kernel so H
+// sees the sourced E, as in the reference loop (Scheme3D.cpp:2003-2024).
+// ===========================================================================
+namespace {
+
+template <typename T, bool PERCELL, int TY>
+__global__ __launch_bounds__(64 * (TY + 1)) void k_fused3d(
+    const T* __restrict__ exi, const T* __restrict__ eyi, const T* __restrict__ ezi,
+    const T* __restrict__ hxi, const T* __restrict__ hyi, const T* __restrict__ hzi,
+    T* __restrict__ exo, T* __restrict__ eyo, T* __restrict__ ezo,
+    T* __restrict__ hxo, T* __restrict__ hyo, T* __restrict__ hzo,
+    const T* __restrict__ cbx, const T* __restrict__ cby, const T* __restrict__ cbz,
+    const T* __restrict__ dbx, const T* __restrict__ dby, const T* __restrict__ dbz, T cb, T db,
+    int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 R, int xchunk,
+    long long src_off, int src_comp, T src_val) {
+  __shared__ T sE[3][3][TY + 1][65];  // [buffer][component][row][lane (+1 halo column)]
+  const int lane = threadIdx.x;
+  const int w = threadIdx.y;
+  const int k = R.lo[2] + blockIdx.x * 64 + lane;
+  const int j = R.lo[1] + blockIdx.y * TY + w;
+  const int i0 = R.lo[0] + blockIdx.z * xchunk;
+  const int i1 = min(i0 + xchunk, R.hi[0]);
+  const bool owned = (w < TY) && (j < R.hi[1]) && (k < R.hi[2]);
+  const bool valid = (j < ny) && (k < nz);           // may compute E here (halo included)
+  const bool extra = (lane == 63) && (w < TY) && (j < ny) && (k + 1 < nz);  // E at k+1
+  const size_t plane = (size_t)ny * nz;
+  const size_t row = (size_t)j * nz + k;
+
+  // plane x-1 values carried in registers
+  T hxp = 0, hyp = 0, hzp = 0, hz_p1 = 0;  // hz_p1: Hz(x-1, j, k+1) for the extra column
+  if (valid && i0 > 0) {
+    const size_t o = (size_t)(i0 - 1) * plane + row;
+    hxp = hxi[o];
+    hyp = hyi[o];
+    hzp = hzi[o];
+    if (extra) hz_p1 = hzi[o + 1];
+  }
+  for (int x = i0; x <= i1; ++x) {
+    const int buf = (x - i0) % 3;
+    T hxc = 0, hyc = 0, hzc = 0;
+    T exn = 0, eyn = 0, ezn = 0;
+    if (valid && x < nx) {
+      const size_t off = (size_t)x * plane + row;
+      hxc = hxi[off];
+      hyc = hyi[off];
+      hzc = hzi[off];
+      exn = exi[off];
+      eyn = eyi[off];
+      ezn = ezi[off];
+      if (in_box(bex, x, j, k)) {
+        const T c = PERCELL ? cbx[off] : cb;
+        exn += c * ((hzc - hzi[off - nz]) - (hyc - hyi[off - 1]));
+      }
+      if (in_box(bey, x, j, k)) {
+        const T c = PERCELL ? cby[off] : cb;
+        eyn += c * ((hxc - hxi[off - 1]) - (hzc - hzp));
+      }
+      if (in_box(bez, x, j, k)) {
+        const T c = PERCELL ? cbz[off] : cb;
+        ezn += c * ((hyc - hyp) - (hxc - hxi[off - nz]));
+      }
+      if (src_comp >= 0 && (long long)off == src_off) {
+        if (src_comp == 0) exn = src_val;
+        if (src_comp == 1) eyn = src_val;
+        if (src_comp == 2) ezn = src_val;
+      }
+      if (owned && x < i1) {
+        exo[off] = exn;
+        eyo[off] = eyn;
+        ezo[off] = ezn;
+      }
+    }
+    sE[buf][0][w][lane] = exn;
+    sE[buf][1][w][lane] = eyn;
+    sE[buf][2][w][lane] = ezn;
+    T hz_c1 = 0;
+    if (extra && x < nx) {
+      // Ex, Ey at (x, j, k+1): the halo column the H update of lane 63 needs
+      const size_t off = (size_t)x * plane + row + 1;
+      const int k1 = k + 1;
+      T ex1 = exi[off], ey1 = eyi[off];
+      hz_c1 = hzi[off];
+      if (in_box(bex, x, j, k1)) {
+        const T c = PERCELL ? cbx[off] : cb;
+        ex1 += c * ((hz_c1 - hzi[off - nz]) - (hyi[off] - hyi[off - 1]));
+      }
+      if (in_box(bey, x, j, k1)) {
+        const T c = PERCELL ? cby[off] : cb;
+        ey1 += c * ((hxi[off] - hxi[off - 1]) - (hz_c1 - hz_p1));
+      }
+      if (src_comp >= 0 && (long long)off == src_off) {
+        if (src_comp == 0) ex1 = src_val;
+        if (src_comp == 1) ey1 = src_val;
+      }
+      sE[buf][0][w][64] = ex1;
+      sE[buf][1][w][64] = ey1;
+    }
+    __syncthreads();
+    if (x > i0 && owned) {
+      // H_new at plane xm = x-1 from E_new planes xm (buffer pb) and x (buffer buf)
+      const int xm = x - 1;
+      const int pb = (x - 1 - i0) % 3;
+      const size_t off = (size_t)xm * plane + row;
+      const T ex_c = sE[pb][0][w][lane], ey_c = sE[pb][1][w][lane], ez_c = sE[pb][2][w][lane];
+      const T ey_kp = sE[pb][1][w][lane + 1], ex_kp = sE[pb][0][w][lane + 1];
+      const T ez_jp = sE[pb][2][w + 1][lane], ex_jp = sE[pb][0][w + 1][lane];
+      const T ez_ip = sE[buf][2][w][lane], ey_ip = sE[buf][1][w][lane];
+      T hxn = hxp, hyn = hyp, hzn = hzp;
+      if (in_box(bhx, xm, j, k)) {
+        const T c = PERCELL ? dbx[off] : db;
+        hxn += c * ((ey_kp - ey_c) - (ez_jp - ez_c));
+      }
+      if (in_box(bhy, xm, j, k)) {
+        const T c = PERCELL ? dby[off] : db;
+        hyn += c * ((ez_ip - ez_c) - (ex_kp - ex_c));
+      }
+      if (in_box(bhz, xm, j, k)) {
+        const T c = PERCELL ? dbz[off] : db;
+        hzn += c * ((ex_jp - ex_c) - (ey_ip - ey_c));
+      }
+      hxo[off] = hxn;
+      hyo[off] = hyn;
+      hzo[off] = hzn;
+    }
+    hxp = hxc;
+    hyp = hyc;
+    hzp = hzc;
+    hz_p1 = hz_c1;
+  }
+}
+
+template <typename T, int TY>
+int launch_fused(const T* const* ein, const T* const* hin, T* const* eout, T* const* hout, const T* const* cbs,
+                 const T* const* dbs, double cb, double db, int nx, int ny, int nz, const int* boxes, int xchunk,
+                 long long src_off, int src_comp, double src_val, hipStream_t s) {
+  Box3 b[6];
+  for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
+  Box3 R = b[0];
+  for (int n = 1; n < 6; ++n) R = box_union(R, b[n]);
+  if (box_empty(R)) return 0;
+  if (xchunk <= 0) xchunk = 32;
+  dim3 block(64, TY + 1, 1);
+  dim3 grid(cdiv(R.hi[2] - R.lo[2], 64), cdiv(R.hi[1] - R.lo[1], TY), cdiv(R.hi[0] - R.lo[0], xchunk));
+  if (cbs[0] != nullptr)
+    k_fused3d<T, true, TY><<<grid, block, 0, s>>>(ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1],
+                                                  eout[2], hout[0], hout[1], hout[2], cbs[0], cbs[1], cbs[2], dbs[0],
+                                                  dbs[1], dbs[2], (T)cb, (T)db, nx, ny, nz, b[0], b[1], b[2], b[3],
+                                                  b[4], b[5], R, xchunk, src_off, src_comp, (T)src_val);
+  else
+    k_fused3d<T, false, TY><<<grid, block, 0, s>>>(ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1],
+                                                   eout[2], hout[0], hout[1], hout[2], cbs[0], cbs[1], cbs[2], dbs[0],
+                                                   dbs[1], dbs[2], (T)cb, (T)db, nx, ny, nz, b[0], b[1], b[2], b[3],
+                                                   b[4], b[5], R, xchunk, src_off, src_comp, (T)src_val);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+}  // namespace
+
+// ein/hin/eout/hout/cbs/dbs: arrays of 3 pointers; boxes: 6 boxes (Ex,Ey,Ez,Hx,Hy,Hz)
+FDTD_API int fdtd_fused3d_f32(const float* const* ein, const float* const* hin, float* const* eout,
+                              float* const* hout, const float* const* cbs, const float* const* dbs, double cb,
+                              double db, int nx, int ny, int nz, const int* boxes, int xchunk, long long src_off,
+                              int src_comp, double src_val, void* s) {
+  return launch_fused<float, 7>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, boxes, xchunk, src_off,
+                                src_comp, src_val, (hipStream_t)s);
+}
+
+FDTD_API int fdtd_fused3d_f64(const double* const* ein, const double* const* hin, double* const* eout,
+                              double* const* hout, const double* const* cbs, const double* const* dbs, double cb,
+                              double db, int nx, int ny, int nz, const int* boxes, int xchunk, long long src_off,
+                              int src_comp, double src_val, void* s) {
+  return launch_fused<double, 7>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, boxes, xchunk, src_off,
+                                 src_comp, src_val, (hipStream_t)s);
+}

@@ -88,6 +88,9 @@ class SchemeConfig:
     ntff_step: int = 100
     check_finite: bool = False
     finite_check_step: int = 100
+    use_fused: bool = False
+    cpml_kappa_max: float = 1.0
+    cpml_alpha_max: float = 0.0
 
     @classmethod
     def from_settings(cls, s) -> "SchemeConfig":
@@ -113,7 +116,8 @@ class SchemeConfig:
             complex_values=s.doUseComplexFieldValues, scene=s.scene, sphere_eps=s.sphereEps,
             sphere_radius=s.sphereRadius, sphere_center=(s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ),
             source=s.sourceType, gaussian_width=s.gaussianWidth, gaussian_delay=s.gaussianDelay,
-            ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep)
+            ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
+            use_fused=s.doUseFusedKernel, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax)
 
 
 def _torch_dtype(name: str):
@@ -237,6 +241,13 @@ class YeeScheme:
         self._init_source()
         if cfg.use_amp_mode:
             self.amp = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+        # fused E+H kernel (ping-pong buffers): plain 3D updates with at most a
+        # hard E point source
+        self.fused = (cfg.use_fused and hasattr(self.ops, "fused_step") and cfg.scheme == "3d"
+                      and not self.use_upml_chain and not self.use_cpml and not cfg.use_tfsf
+                      and not cfg.use_amp_mode)
+        if self.fused:
+            self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
         self.initialized = True
         self.timers["init"] = time.perf_counter() - t0
 
@@ -500,6 +511,9 @@ class YeeScheme:
         cfg = self.cfg
         B = self.domain.buffer_size
         halo = self.halo
+        if self.fused:
+            self._fused_step(t)
+            return
         deep = halo is not None and B > 1
         if deep and self.sub_step == 0:
             halo.exchange_all(self)
@@ -526,6 +540,32 @@ class YeeScheme:
         for h in self.hooks:
             h(self, self.t)
         if cfg.check_finite and self.t % max(1, cfg.finite_check_step) == 0:
+            self.check_finite()
+
+    def _fused_step(self, t: int) -> None:
+        """One step through the fused E+H kernel.  Decomposed runs use the
+        deep-halo protocol for any buffer size (a full ghost exchange every
+        ``B`` steps, redundant compute in between)."""
+        B = self.domain.buffer_size
+        if self.halo is not None and self.sub_step == 0:
+            self.halo.exchange_all(self)
+        wE = self.domain.window_fused("E", self.sub_step)
+        wH = self.domain.window_fused("H", self.sub_step)
+        boxes = {c: self.local_box(c, wE) for c in self.e_comps}
+        boxes.update({c: self.local_box(c, wH) for c in self.h_comps})
+        for p in range(self.planes):
+            src = None
+            if self.point_source is not None and self.point_source[1] is not None:
+                comp, li, _ = self.point_source
+                src = (comp, li, self.source_value(t, p))
+            self.ops.fused_step(self.F[p], self.F_alt[p], boxes, self.cb, src)
+            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
+        self.t += 1
+        if self.halo is not None:
+            self.sub_step = (self.sub_step + 1) % B
+        for h in self.hooks:
+            h(self, self.t)
+        if self.cfg.check_finite and self.t % max(1, self.cfg.finite_check_step) == 0:
             self.check_finite()
 
     def perform_steps(self, n: Optional[int] = None) -> None:

@@ -213,6 +213,55 @@ class HipOps:
         _check(rc, "%s %s update" % (scheme, kind))
         self.launches += 1
 
+    def fused_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                   cb: Dict[str, Coef], source=None) -> None:
+        """One fused E+H leapfrog step (yee3d.hip ``k_fused3d``): reads
+        ``fin``, writes ``fout`` on the union of the six boxes.  ``source`` =
+        (component, local index, value) of a hard point source or None."""
+        E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
+        shape = tuple(fin["Ex"].shape)
+        for c in E + H:
+            self._check_tensor(fin[c], shape)
+            self._check_tensor(fout[c], shape)
+            if fin[c].data_ptr() == fout[c].data_ptr():
+                raise HipError("fused step needs distinct in/out buffers")
+            b = boxes[c]
+            if not _empty(b):
+                self._check_stencil_box("E" if c[0] == "E" else "H", c, b, shape)
+        pe = [self._cell_or_none(cb[c]) for c in E]
+        ph = [self._cell_or_none(cb[c]) for c in H]
+        percell = pe[0] is not None
+        if any((p is not None) != percell for p in pe + ph):
+            raise HipError("fused step: mixed scalar/per-cell coefficients")
+        if percell:
+            cbs = (c_vp * 3)(*[self._scaled_cell(cb[c]).data_ptr() for c in E])
+            dbs = (c_vp * 3)(*[self._scaled_cell(cb[c]).data_ptr() for c in H])
+            cbv, dbv = 1.0, 1.0
+        else:
+            cbs = (c_vp * 3)(None, None, None)
+            dbs = (c_vp * 3)(None, None, None)
+            cbv, dbv = cb["Ex"].scalar, cb["Hx"].scalar
+            if any(cb[c].scalar != cbv for c in E) or any(cb[c].scalar != dbv for c in H):
+                raise HipError("fused step: scalar coefficients must agree per kind")
+        src_off, src_comp, src_val = -1, -1, 0.0
+        if source is not None:
+            comp, idx, val = source
+            if comp not in E:
+                raise HipError("fused step supports E point sources only")
+            for d in range(3):
+                if not (0 <= idx[d] < shape[d]):
+                    raise HipError("source index outside array")
+            src_off = (idx[0] * shape[1] + idx[1]) * shape[2] + idx[2]
+            src_comp = E.index(comp)
+            src_val = val
+        arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
+        rc = self.fn("fused3d")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
+                                c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
+                                _box_arr([boxes[c] for c in E + H]), c_int(self.xchunk), c_ll(src_off),
+                                c_int(src_comp), c_double(src_val), _stream())
+        _check(rc, "fused3d")
+        self.launches += 1
+
     # per-cell coefficient arrays for the fast kernels are scalar*cell, cached
     def _scaled_cell(self, c: Coef) -> torch.Tensor:
         key = "_scaled"

@@ -76,6 +76,21 @@ class TorchOps:
                 continue
             dst[comp][sl] += cb[comp].materialize(sl) * c
 
+    def fused_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                   cb: Dict[str, Coef], source=None) -> None:
+        """Reference semantics of the fused E+H kernel: E_new from (E_old,
+        H_old) on the E boxes, the point source, then H_new from (H_old, E_new)
+        on the H boxes, all written to ``fout``."""
+        for c in fin:
+            fout[c].copy_(fin[c])
+        e = {c: b for c, b in boxes.items() if c[0] == "E"}
+        h = {c: b for c, b in boxes.items() if c[0] == "H"}
+        self.curl_update("E", e, fout, fin, cb)
+        if source is not None:
+            comp, idx, val = source
+            fout[comp][tuple(idx)] = val
+        self.curl_update("H", h, fout, fout, cb)
+
     def curl_general(self, kind: str, comp: str, box: Box, out: torch.Tensor, inp: torch.Tensor,
                      src: Dict[str, torch.Tensor], ca: Coef, cb: Coef) -> None:
         if _empty(box):

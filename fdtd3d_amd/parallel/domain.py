@@ -134,3 +134,16 @@ class Domain:
                 if self.has_high(d):
                     hi[d] = self.hi[d] + B - sub_step - (1 if kind == "H" else 0)
         return tuple(lo), tuple(hi)
+
+    def window_fused(self, kind: str, sub_step: int) -> Box:
+        """Windows of the fused E+H kernel: the deep-halo windows for any
+        ``buffer_size >= 1`` (E extends one layer further than H on the high
+        side; ``B = 1`` needs a 1-deep full exchange every step)."""
+        B = self.buffer_size
+        lo, hi = list(self.lo), list(self.hi)
+        for d in range(3):
+            if self.has_low(d):
+                lo[d] = self.lo[d] - B + 1 + sub_step
+            if self.has_high(d):
+                hi[d] = self.hi[d] + B - sub_step - (1 if kind == "H" else 0)
+        return tuple(lo), tuple(hi)

@@ -99,3 +99,27 @@ def test_amplitude_mode_3d(gpu):
     b = run(cfg, "torch", "cpu", torch.float64)
     for c in a.comps:
         assert torch.allclose(a.amp[0][c].cpu(), b.amp[0][c], rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_fused_vacuum_3d(gpu, dtype):
+    compare(SchemeConfig(scheme="3d", size=(50, 37, 131), time_steps=21, scene="vacuum", dtype=dtype,
+                         use_fused=True), gpu, 2e-5 if dtype == "f32" else 1e-12)
+
+
+def test_fused_dielectric_complex_3d(gpu):
+    compare(SchemeConfig(scheme="3d", size=(45, 40, 70), time_steps=15, scene="sphere", sphere_radius=9,
+                         sphere_center=(20.5, 22.5, 30.5), complex_values=True, dtype="f64", use_fused=True), gpu,
+            1e-12)
+
+
+def test_fused_matches_split_bitwise(gpu):
+    """fp32 fused kernel vs fp32 split kernels: same arithmetic per cell."""
+    cfg = SchemeConfig(scheme="3d", size=(64, 64, 64), time_steps=10, scene="vacuum", dtype="f32")
+    import dataclasses
+    a = run(cfg, "hip", gpu, torch.float32)
+    b = run(dataclasses.replace(cfg, use_fused=True), "hip", gpu, torch.float32)
+    assert b.fused
+    for c in a.comps:
+        scale = float(a.F[0][c].abs().max()) + 1e-30
+        assert float((a.F[0][c] - b.F[0][c]).abs().max()) <= 1e-6 * scale

@@ -90,6 +90,10 @@ CASES = [
                                     complex_values=True), 2, "x", 1),
     ("1d-x4", SchemeConfig(scheme="1d", size=(200, 1, 1), time_steps=80, scene="vacuum", source="gaussian"), 4,
      "x", 1),
+    ("fused-xyz8-b1", SchemeConfig(scheme="3d", size=(18, 16, 20), time_steps=9, scene="sphere", sphere_radius=5,
+                                   sphere_center=(9.5, 8.5, 10.5), use_fused=True), 8, "xyz", 1),
+    ("fused-xy4-b2", SchemeConfig(scheme="3d", size=(20, 20, 12), time_steps=9, scene="vacuum", use_fused=True,
+                                  complex_values=True), 4, "xy", 2),
 ]
 
 
