@@ -92,7 +92,8 @@ def _empty(b: Box) -> bool:
 class HipOps:
     name = "hip"
 
-    def __init__(self, layout: Optional[YeeLayout], device, dtype, xchunk: int = 0):
+    def __init__(self, layout: Optional[YeeLayout], device, dtype, xchunk: int = 0, vec4: bool = True):
+        self.vec4 = vec4
         self.layout = layout
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -167,7 +168,10 @@ class HipOps:
             if per[0] is None and any(cb[c].scalar != scal for c in names):
                 raise HipError("scalar coefficients must agree across components")
             bx = _box_arr([boxes[c] for c in names])
-            fn = self.fn("update_e3d" if kind == "E" else "update_h3d")
+            base = "update_e3d" if kind == "E" else "update_h3d"
+            if self.vec4 and self.dtype == torch.float32 and shape[2] % 4 == 0:
+                base += "_v4"
+            fn = self.fn(base)
             per_p = [_ptr(p) if p is not None else None for p in per]
             if per[0] is not None:
                 scal_use = 1.0

@@ -113,6 +113,31 @@ def test_fused_dielectric_complex_3d(gpu):
             1e-12)
 
 
+def test_vec4_windows_match_scalar(gpu):
+    """float4 split kernels vs scalar split kernels on odd windows (box edges
+    not multiple of 4, lanes past the box feeding neighbours)."""
+    from fdtd3d_amd.ops.hip_ops import HipOps
+    shape = (20, 24, 40)
+    torch.manual_seed(0)
+    base = {c: torch.randn(shape, dtype=torch.float32, device=gpu) for c in
+            ("Ex", "Ey", "Ez", "Hx", "Hy", "Hz")}
+    from fdtd3d_amd.layout.yee import YeeLayout
+    from fdtd3d_amd.ops.coef import Coef
+    lay = YeeLayout(shape)
+    boxes_e = {"Ex": ((2, 3, 5), (17, 21, 31)), "Ey": ((3, 1, 6), (19, 20, 33)), "Ez": ((1, 2, 1), (18, 22, 37))}
+    boxes_h = {"Hx": ((2, 3, 5), (17, 21, 31)), "Hy": ((3, 1, 6), (19, 20, 33)), "Hz": ((1, 2, 1), (18, 22, 38))}
+    cb = {c: Coef(0.3) for c in base}
+    out = []
+    for v4 in (False, True):
+        ops = HipOps(lay, gpu, torch.float32, vec4=v4)
+        f = {c: t.clone() for c, t in base.items()}
+        ops.curl_update("E", boxes_e, f, f, cb)
+        ops.curl_update("H", boxes_h, f, f, cb)
+        out.append(f)
+    for c in base:
+        assert torch.allclose(out[0][c], out[1][c], rtol=1e-5, atol=1e-5), c
+
+
 def test_fused_matches_split_bitwise(gpu):
     """fp32 fused kernel vs fp32 split kernels: same arithmetic per cell."""
     cfg = SchemeConfig(scheme="3d", size=(64, 64, 64), time_steps=10, scene="vacuum", dtype="f32")
