@@ -259,7 +259,10 @@ class HipOps:
             src_comp = E.index(comp)
             src_val = val
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
-        rc = self.fn("fused3d")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
+        name = "fused3d"
+        if self.vec4 and self.dtype == torch.float32 and shape[2] % 4 == 0:
+            name = "fused3d_v4"
+        rc = self.fn(name)(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
                                 c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                                 _box_arr([boxes[c] for c in E + H]), c_int(self.xchunk), c_ll(src_off),
                                 c_int(src_comp), c_double(src_val), _stream())
