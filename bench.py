@@ -33,7 +33,7 @@ def main(argv=None) -> int:
     ap.add_argument("--size", type=int, nargs=3, default=[1024, 1024, 1024])
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--backend", default="auto")
-    ap.add_argument("--fused", action="store_true", help="use the fused E+H kernel")
+    ap.add_argument("--split", action="store_true", help="use the split E / H kernels instead of the fused one")
     ap.add_argument("--xchunk", type=int, default=0)
     ap.add_argument("--buffer-size", type=int, default=1, help="halo depth (deep halo when > 1)")
     a = ap.parse_args(argv)
@@ -61,7 +61,7 @@ def main(argv=None) -> int:
 
     size = tuple(a.size)
     cfg = SchemeConfig(scheme="3d", size=size, time_steps=a.steps, scene="vacuum", dtype=a.dtype,
-                       use_pml=False, use_tfsf=False, use_fused=a.fused)
+                       use_pml=False, use_tfsf=False, use_fused=not a.split)
     dtype = torch.float32 if a.dtype == "f32" else torch.float64
     if world > 1:
         core = ParallelGridCore.create(size, world, "xyz")

@@ -265,10 +265,12 @@ __global__ __launch_bounds__(64 * (TY + 1)) void k_fused3d(
         if (src_comp == 1) eyn = src_val;
         if (src_comp == 2) ezn = src_val;
       }
+      // only cells inside a component's box are written: launches on
+      // overlapping regions (interior / boundary shell) never clobber each other
       if (owned && x < i1) {
-        exo[off] = exn;
-        eyo[off] = eyn;
-        ezo[off] = ezn;
+        if (in_box(bex, x, j, k)) exo[off] = exn;
+        if (in_box(bey, x, j, k)) eyo[off] = eyn;
+        if (in_box(bez, x, j, k)) ezo[off] = ezn;
       }
     }
     sE[buf][0][w][lane] = exn;
@@ -319,9 +321,9 @@ __global__ __launch_bounds__(64 * (TY + 1)) void k_fused3d(
         const T c = PERCELL ? dbz[off] : db;
         hzn += c * ((ex_jp - ex_c) - (ey_ip - ey_c));
       }
-      hxo[off] = hxn;
-      hyo[off] = hyn;
-      hzo[off] = hzn;
+      if (in_box(bhx, xm, j, k)) hxo[off] = hxn;
+      if (in_box(bhy, xm, j, k)) hyo[off] = hyn;
+      if (in_box(bhz, xm, j, k)) hzo[off] = hzn;
     }
     hxp = hxc;
     hyp = hyc;

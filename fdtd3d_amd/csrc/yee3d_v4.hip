@@ -48,6 +48,19 @@ __device__ __forceinline__ void st4(float* p, size_t off, const float4& v) {
   *reinterpret_cast<float4*>(p + off) = v;
 }
 
+// store the elements selected by `mask` (bit e = element e); one 16-byte
+// store in the common all-inside case
+__device__ __forceinline__ void st4m(float* p, size_t off, const float4& v, unsigned mask) {
+  if (mask == 0xFu) {
+    st4(p, off, v);
+  } else if (mask) {
+    if (mask & 1u) p[off] = v.x;
+    if (mask & 2u) p[off + 1] = v.y;
+    if (mask & 4u) p[off + 2] = v.z;
+    if (mask & 8u) p[off + 3] = v.w;
+  }
+}
+
 template <bool PERCELL>
 __global__ __launch_bounds__(64 * TY) void k_update_e3d_v4(
     float* __restrict__ ex, float* __restrict__ ey, float* __restrict__ ez,
@@ -319,10 +332,12 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
         if (src_comp == 1) f4set(eyn, q, src_val);
         if (src_comp == 2) f4set(ezn, q, src_val);
       }
+      // only cells inside a component's box are written: launches on
+      // overlapping regions (interior / boundary shell) never clobber each other
       if (owned && x < i1) {
-        st4(exo, off, exn);
-        st4(eyo, off, eyn);
-        st4(ezo, off, ezn);
+        st4m(exo, off, exn, (x >= bex.lo[0] && x < bex.hi[0]) ? mex : 0u);
+        st4m(eyo, off, eyn, (x >= bey.lo[0] && x < bey.hi[0]) ? mey : 0u);
+        st4m(ezo, off, ezn, (x >= bez.lo[0] && x < bez.hi[0]) ? mez : 0u);
       }
     }
     sE[buf][0][w][lane] = exn;
@@ -387,15 +402,9 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
           if (mhz & (1u << q))
             f4set(hzn, q, f4(hzn, q) + f4(c4, q) * ((f4(ex_jp, q) - f4(exp_, q)) - (f4(eyn, q) - f4(eyp, q))));
       }
-      st4(hxo, o, hxn);
-      st4(hyo, o, hyn);
-      st4(hzo, o, hzn);
-    } else if (x > i0 && owned) {
-      // owned cells outside every H box keep their old value in the new buffer
-      const size_t o = (size_t)(x - 1) * plane + row;
-      st4(hxo, o, hxp);
-      st4(hyo, o, hyp);
-      st4(hzo, o, hzp);
+      st4m(hxo, o, hxn, (xm >= bhx.lo[0] && xm < bhx.hi[0]) ? mhx : 0u);
+      st4m(hyo, o, hyn, (xm >= bhy.lo[0] && xm < bhy.hi[0]) ? mhy : 0u);
+      st4m(hzo, o, hzn, (xm >= bhz.lo[0] && xm < bhz.hi[0]) ? mhz : 0u);
     }
     hxp = hxc;
     hyp = hyc;
@@ -416,18 +425,39 @@ inline dim3 grid_v4(const Box3& bu, int xchunk) {
 
 }  // namespace
 
+static int g_fused_rows = 7;  // owned rows per workgroup (3 or 7); tuning knob
+
+FDTD_API void fdtd_set_fused_rows(int rows) { g_fused_rows = (rows == 3) ? 3 : 7; }
+
+template <int FTY>
+static int launch_fused_v4(const float* const* ein, const float* const* hin, float* const* eout,
+                           float* const* hout, const float* const* cbs, const float* const* dbs, double cb,
+                           double db, int nx, int ny, int nz, const int* boxes, int xchunk, long long src_off,
+                           int src_comp, double src_val, void* s);
+
 FDTD_API int fdtd_fused3d_v4_f32(const float* const* ein, const float* const* hin, float* const* eout,
                                  float* const* hout, const float* const* cbs, const float* const* dbs, double cb,
                                  double db, int nx, int ny, int nz, const int* boxes, int xchunk, long long src_off,
                                  int src_comp, double src_val, void* s) {
-  constexpr int FTY = 7;
+  if (g_fused_rows == 3)
+    return launch_fused_v4<3>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, boxes, xchunk, src_off, src_comp,
+                              src_val, s);
+  return launch_fused_v4<7>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, boxes, xchunk, src_off, src_comp,
+                            src_val, s);
+}
+
+template <int FTY>
+static int launch_fused_v4(const float* const* ein, const float* const* hin, float* const* eout,
+                           float* const* hout, const float* const* cbs, const float* const* dbs, double cb,
+                           double db, int nx, int ny, int nz, const int* boxes, int xchunk, long long src_off,
+                           int src_comp, double src_val, void* s) {
   if (nz % 4 != 0) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   Box3 R = b[0];
   for (int n = 1; n < 6; ++n) R = box_union(R, b[n]);
   if (box_empty(R)) return 0;
-  if (xchunk <= 0) xchunk = 32;
+  if (xchunk <= 0) xchunk = 16;  // measured: 16 >= 64 >= 32 at 1024^3 (tools/kbench.py)
   const int kspan = R.hi[2] - (R.lo[2] & ~3);
   dim3 grid(cdiv(kspan, 256), cdiv(R.hi[1] - R.lo[1], FTY), cdiv(R.hi[0] - R.lo[0], xchunk));
   dim3 block(64, FTY + 1);

@@ -117,7 +117,7 @@ class SchemeConfig:
             sphere_radius=s.sphereRadius, sphere_center=(s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ),
             source=s.sourceType, gaussian_width=s.gaussianWidth, gaussian_delay=s.gaussianDelay,
             ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
-            use_fused=s.doUseFusedKernel, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax)
+            use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax)
 
 
 def _torch_dtype(name: str):
@@ -547,6 +547,9 @@ class YeeScheme:
         deep-halo protocol for any buffer size (a full ghost exchange every
         ``B`` steps, redundant compute in between)."""
         B = self.domain.buffer_size
+        if self.halo is not None and B == 1:
+            self._fused_step_overlap(t)
+            return
         if self.halo is not None and self.sub_step == 0:
             self.halo.exchange_all(self)
         wE = self.domain.window_fused("E", self.sub_step)
@@ -563,6 +566,85 @@ class YeeScheme:
         self.t += 1
         if self.halo is not None:
             self.sub_step = (self.sub_step + 1) % B
+        for h in self.hooks:
+            h(self, self.t)
+        if self.cfg.check_finite and self.t % max(1, self.cfg.finite_check_step) == 0:
+            self.check_finite()
+
+    def _fused_regions(self):
+        """(E box, H box) global pairs of the overlapped fused step: first the
+        interior (needs no ghost), then the one-cell H shell slabs next to
+        neighbours, each with the E cells its H update needs."""
+        key = "_fused_regions_cache"
+        cached = getattr(self, key, None)
+        if cached is not None:
+            return cached
+        dom = self.domain
+        wE = dom.window_fused("E", 0)
+        wH = dom.window_fused("H", 0)
+        hl = [dom.has_low(a) for a in range(3)]
+        hh = [dom.has_high(a) for a in range(3)]
+        hI = (tuple(dom.lo[a] + (1 if hl[a] else 0) for a in range(3)),
+              tuple(dom.hi[a] - (1 if hh[a] else 0) for a in range(3)))
+        eI = box_intersect(wE, (hI[0], tuple(hI[1][a] + 1 for a in range(3))))
+        regions = [(eI, hI)]
+        lo, hi = list(wH[0]), list(wH[1])
+        for a in range(3):
+            for side in (0, 1):
+                if (side == 0 and hl[a]) or (side == 1 and hh[a]):
+                    slo, shi = list(lo), list(hi)
+                    if side == 0:
+                        shi[a] = lo[a] + 1
+                        lo[a] += 1
+                    else:
+                        slo[a] = hi[a] - 1
+                        hi[a] -= 1
+                    S = (tuple(slo), tuple(shi))
+                    if box_empty(S):
+                        continue
+                    E = box_intersect(wE, (S[0], tuple(S[1][d] + 1 for d in range(3))))
+                    regions.append((E, S))
+        setattr(self, key, regions)
+        return regions
+
+    def _fused_step_overlap(self, t: int) -> None:
+        """Decomposed fused step (``--buffer-size 1``): the interior update runs
+        while the 1-deep ghost exchange (all axes, edges included) proceeds on
+        a side stream; the boundary shell follows once the ghosts are in."""
+        regions = self._fused_regions()
+
+        def boxes_of(eb, hb):
+            b = {c: self.local_box(c, eb) for c in self.e_comps}
+            b.update({c: self.local_box(c, hb) for c in self.h_comps})
+            return b
+
+        srcs = []
+        for p in range(self.planes):
+            src = None
+            if self.point_source is not None and self.point_source[1] is not None:
+                comp, li, _ = self.point_source
+                src = (comp, li, self.source_value(t, p))
+            srcs.append(src)
+        interior = boxes_of(*regions[0])
+        for p in range(self.planes):
+            self.ops.fused_step(self.F[p], self.F_alt[p], interior, self.cb, srcs[p])
+        side = None
+        if self.device.type == "cuda":
+            side = getattr(self, "_side_stream", None)
+            if side is None:
+                side = torch.cuda.Stream(device=self.device)
+                self._side_stream = side
+            side.wait_stream(torch.cuda.current_stream(self.device))
+        self.halo.exchange_all(self, stream=side)
+        if side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(side)
+        for eb, hb in regions[1:]:
+            bx = boxes_of(eb, hb)
+            for p in range(self.planes):
+                self.ops.fused_step(self.F[p], self.F_alt[p], bx, self.cb, srcs[p])
+        for p in range(self.planes):
+            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
+        self.t += 1
         for h in self.hooks:
             h(self, self.t)
         if self.cfg.check_finite and self.t % max(1, self.cfg.finite_check_step) == 0:

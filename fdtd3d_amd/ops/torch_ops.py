@@ -81,15 +81,19 @@ class TorchOps:
         """Reference semantics of the fused E+H kernel: E_new from (E_old,
         H_old) on the E boxes, the point source, then H_new from (H_old, E_new)
         on the H boxes, all written to ``fout``."""
-        for c in fin:
-            fout[c].copy_(fin[c])
+        # like the kernel, only cells inside a component's box are written
+        tmp = {c: fin[c].clone() for c in fin}
         e = {c: b for c, b in boxes.items() if c[0] == "E"}
         h = {c: b for c, b in boxes.items() if c[0] == "H"}
-        self.curl_update("E", e, fout, fin, cb)
+        self.curl_update("E", e, tmp, fin, cb)
         if source is not None:
             comp, idx, val = source
-            fout[comp][tuple(idx)] = val
-        self.curl_update("H", h, fout, fout, cb)
+            tmp[comp][tuple(idx)] = val
+        self.curl_update("H", h, tmp, tmp, cb)
+        for c, b in boxes.items():
+            if not _empty(b):
+                sl = box_slices(b)
+                fout[c][sl] = tmp[c][sl]
 
     def curl_general(self, kind: str, comp: str, box: Box, out: torch.Tensor, inp: torch.Tensor,
                      src: Dict[str, torch.Tensor], ca: Coef, cb: Coef) -> None:

@@ -31,6 +31,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from .comm import P2P, DistComm
 from .domain import Domain, box_empty, box_intersect
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
@@ -49,12 +50,11 @@ def _face_components(layout, kind_needed: str, axis: int) -> List[str]:
 
 
 class HaloExchanger:
-    def __init__(self, domain: Domain, group=None, use_batch: Optional[bool] = None):
+    def __init__(self, domain: Domain, group=None, comm=None):
         self.domain = domain
         self.group = group
-        backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
-        self.backend = backend
-        self.use_batch = (backend == "nccl") if use_batch is None else use_batch
+        self.comm = comm if comm is not None else DistComm(group)
+        self.backend = self.comm.backend
         self.pending: Dict[Tuple[str, int], list] = {}
         self.bufs: Dict[tuple, torch.Tensor] = {}
         self.bytes_sent = 0
@@ -69,17 +69,7 @@ class HaloExchanger:
         return b
 
     def _post(self, ops_list):
-        if not ops_list:
-            return []
-        if self.use_batch:
-            return dist.batch_isend_irecv(ops_list)
-        works = []
-        for op in ops_list:
-            if op.op is dist.isend:
-                works.append(dist.isend(op.tensor, op.peer, group=self.group, tag=op.tag))
-            else:
-                works.append(dist.irecv(op.tensor, op.peer, group=self.group, tag=op.tag))
-        return works
+        return self.comm.post(ops_list)
 
     def _face_box(self, axis: int, side: str, kind: str, send: bool) -> Box:
         """Global box of the one-cell face layer for face mode."""
@@ -119,14 +109,14 @@ class HaloExchanger:
                 n = _vol(box) * len(comps)
                 sb = self._buf(("s", kind, p, a), n, tensors[0])
                 ops.pack(tensors, box, sb)
-                ops_list.append(dist.P2POp(dist.isend, sb, to, self.group, tag=_tag(kind, a)))
+                ops_list.append(P2P(True,sb, to,_tag(kind, a)))
                 self.bytes_sent += sb.numel() * sb.element_size()
                 self.messages += 1
             if frm >= 0:
                 box = d.to_local(self._face_box(a, None, kind, False))
                 n = _vol(box) * len(comps)
                 rb = self._buf(("r", kind, p, a), n, tensors[0])
-                ops_list.append(dist.P2POp(dist.irecv, rb, frm, self.group, tag=_tag(kind, a)))
+                ops_list.append(P2P(False,rb, frm,_tag(kind, a)))
                 recvs.append((tensors, box, rb))
         works = self._post(ops_list)
         self.pending[(kind, p)] = (works, recvs)
@@ -185,9 +175,18 @@ class HaloExchanger:
             self._wait(key[0], key[1], scheme.ops)
 
     # ------------------------------------------------------------ deep halo
-    def exchange_all(self, scheme) -> None:
+    def exchange_all(self, scheme, stream=None) -> None:
         """B-deep exchange of every state array, axis by axis (fills edges and
-        corners through the sequential sweep)."""
+        corners through the sequential sweep).  With ``stream`` the packing,
+        RCCL transfers and unpacking are issued on that (side) stream so they
+        overlap compute on the current stream."""
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                self._exchange_all(scheme)
+        else:
+            self._exchange_all(scheme)
+
+    def _exchange_all(self, scheme) -> None:
         d = self.domain
         B = d.buffer_size
         ops = scheme.ops
@@ -210,8 +209,8 @@ class HaloExchanger:
                 sb = self._buf(("ds", a, 0), _vol(sbox) * len(tensors), tensors[0])
                 _pack_many(ops, tensors, sbox, sb)
                 rb = self._buf(("dr", a, 0), _vol(rbox) * len(tensors), tensors[0])
-                ops_list.append(dist.P2POp(dist.isend, sb, lo_n, self.group, tag=100 + 2 * a))
-                ops_list.append(dist.P2POp(dist.irecv, rb, lo_n, self.group, tag=101 + 2 * a))
+                ops_list.append(P2P(True,sb, lo_n,100 + 2 * a))
+                ops_list.append(P2P(False,rb, lo_n,101 + 2 * a))
                 recvs.append((rbox, rb))
                 self.bytes_sent += sb.numel() * sb.element_size()
                 self.messages += 1
@@ -221,8 +220,8 @@ class HaloExchanger:
                 sb = self._buf(("ds", a, 1), _vol(sbox) * len(tensors), tensors[0])
                 _pack_many(ops, tensors, sbox, sb)
                 rb = self._buf(("dr", a, 1), _vol(rbox) * len(tensors), tensors[0])
-                ops_list.append(dist.P2POp(dist.isend, sb, hi_n, self.group, tag=101 + 2 * a))
-                ops_list.append(dist.P2POp(dist.irecv, rb, hi_n, self.group, tag=100 + 2 * a))
+                ops_list.append(P2P(True,sb, hi_n,101 + 2 * a))
+                ops_list.append(P2P(False,rb, hi_n,100 + 2 * a))
                 recvs.append((rbox, rb))
                 self.bytes_sent += sb.numel() * sb.element_size()
                 self.messages += 1
@@ -233,16 +232,10 @@ class HaloExchanger:
 
     # ------------------------------------------------------------ collectives
     def allreduce_sum(self, v: int) -> int:
-        dev = "cuda" if self.backend == "nccl" else "cpu"
-        t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, group=self.group)
-        return int(t.item())
+        return int(self.comm.allreduce(v, "sum"))
 
     def allreduce_max(self, v: float) -> float:
-        dev = "cuda" if self.backend == "nccl" else "cpu"
-        t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return float(t.item())
+        return float(self.comm.allreduce(v, "max"))
 
 
 def _tag(kind: str, axis: int) -> int:

@@ -1,0 +1,90 @@
+"""Decomposed runs through the HIP kernels on ONE GPU (GPU only).
+
+The ranks are threads of the test process talking through the in-process
+:class:`~fdtd3d_amd.parallel.comm.LocalHub` transport (RCCL refuses several
+ranks on one device, and spawning processes from a GPU-initialised test
+process is not allowed on the GPU pool).  This exercises the GPU pack/unpack
+kernels, the split face-mode overlap, the interior/shell split of the
+overlapped fused step and its side stream, and compares the assembled global
+fields with a serial HIP run.
+"""
+
+import threading
+
+import pytest
+import torch
+
+from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+from fdtd3d_amd.ops import make_ops
+from fdtd3d_amd.parallel.comm import LocalHub
+from fdtd3d_amd.parallel.halo import HaloExchanger
+from fdtd3d_amd.parallel.topology import ParallelGridCore
+
+pytestmark = pytest.mark.gpu
+
+
+def run_threads(cfg, world, axes, buf, device):
+    core = ParallelGridCore.create(cfg.size, world, axes)
+    hub = LocalHub(world)
+    dt = torch.float32 if cfg.dtype == "f32" else torch.float64
+    schemes = [None] * world
+    errors = []
+
+    def body(rank):
+        try:
+            dom = core.domain(rank, buf)
+            halo = HaloExchanger(dom, comm=hub.comm(rank))
+            s = YeeScheme(cfg, make_ops("hip", None, device, dt), dom, halo)
+            s.init_scheme()
+            s.init_grids()
+            s.perform_steps()
+            halo.drain(s)
+            torch.cuda.synchronize()
+            schemes[rank] = s
+        except BaseException as e:  # surface thread failures in the test
+            errors.append(e)
+
+    ths = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=600)
+    if errors:
+        raise errors[0]
+    full = {}
+    for c in schemes[0].comps:
+        f = torch.zeros(cfg.size, dtype=torch.float64)
+        for s in schemes:
+            d = s.domain
+            f[d.lo[0]:d.hi[0], d.lo[1]:d.hi[1], d.lo[2]:d.hi[2]] = s.owned_field(c).double().cpu()
+        full[c] = f
+    return full
+
+
+CASES = [
+    ("split-face-x2", SchemeConfig(scheme="3d", size=(32, 24, 40), time_steps=12, scene="vacuum", dtype="f32"),
+     2, "x", 1),
+    ("split-pml-tfsf-xy4", SchemeConfig(scheme="3d", size=(32, 32, 32), time_steps=10, use_pml=True, use_tfsf=True,
+                                        pml_size=(4, 4, 4), tfsf_size=(8, 8, 8), dtype="f64"), 4, "xy", 1),
+    ("fused-overlap-xyz8", SchemeConfig(scheme="3d", size=(40, 36, 64), time_steps=11, scene="sphere",
+                                        sphere_radius=8, sphere_center=(20.5, 17.5, 30.5), dtype="f32",
+                                        use_fused=True), 8, "xyz", 1),
+    ("fused-deep-b2-yz2", SchemeConfig(scheme="3d", size=(24, 40, 48), time_steps=9, scene="vacuum", dtype="f32",
+                                       use_fused=True), 2, "yz", 2),
+]
+
+
+@pytest.mark.parametrize("name,cfg,world,axes,buf", CASES, ids=[c[0] for c in CASES])
+def test_gpu_decomposed_equals_serial(gpu, name, cfg, world, axes, buf):
+    par = run_threads(cfg, world, axes, buf, gpu)
+    dt = torch.float32 if cfg.dtype == "f32" else torch.float64
+    s = YeeScheme(cfg, make_ops("hip", None, gpu, dt))
+    s.init_scheme()
+    s.init_grids()
+    s.perform_steps()
+    for c in s.comps:
+        a = par[c]
+        b = s.F[0][c].double().cpu()
+        scale = max(float(s.F[0][o].abs().max()) for o in s.comps if o[0] == c[0]) + 1e-30
+        err = float((a - b).abs().max())
+        assert err <= 1e-6 * scale, (name, c, err, scale)

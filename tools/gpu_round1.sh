@@ -8,7 +8,7 @@ timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.lo
 rc=$?
 tail -15 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then echo "pytest rc=$rc"; exit $rc; fi
-for extra in "" "--fused" ${BENCH_EXTRA}; do
+for extra in "" "--split" ${BENCH_EXTRA}; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 $extra > gpurun_out/bench.log 2>&1 || { cat gpurun_out/bench.log; exit 1; }
   echo "[$extra] $(grep metric gpurun_out/bench.log | cut -c1-200)"
 done
