@@ -1,0 +1,170 @@
+"""Near-to-far-field transform: scattered power diagram.
+
+Same observable as the reference's ``Scheme3D::Pointing_scat / Pointing_inc``
+(``Scheme3D.cpp:2263-2307, 4093-4509``): on a closed box surface the
+tangential fields define equivalent currents ``J = n x H`` and
+``M = -n x E``; their radiation vectors
+
+    N = sum_faces sum_cells J exp(i k r_hat . r') dS,   L = (same with M)
+
+give the far-field power per unit solid angle, normalised by the incident
+plane-wave intensity ``1/eta0``:
+
+    P(theta, phi) = k^2 / (8 pi eta0) (|L_phi + eta0 N_theta|^2 + |L_theta - eta0 N_phi|^2) * eta0.
+
+Differences from the reference, all deliberate:
+
+* every angle of the diagram is evaluated at once: the face sums are complex
+  matrix-vector products ``exp(i k r_hat(phi) . r') @ J`` (torch on the
+  solver's device);
+* the box is set by ``--ntff-size{x,y,z}`` (the reference hard-codes 13 cells,
+  ``Scheme3D.h:231-232``, and ignores the option);
+* real-valued runs are handled as complex fields with zero imaginary part
+  (the reference only builds 3D with complex values).
+
+Tangential fields are brought to the face-cell centres by averaging the two
+(H) or four (E) nearest Yee samples.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..layout.yee import MIN_COORD_FP
+from ..utils.constants import EPS0, MU0, PI
+
+ETA0 = math.sqrt(MU0 / EPS0)
+
+
+def _sample(F: torch.Tensor, comp: str, axis: int, x0: float, lo: Sequence[float], hi: Sequence[float]):
+    """Values of ``comp`` at the face-cell centres of the face ``axis = x0``
+    spanning ``[lo, hi)`` along the two other axes (centres at lo+0.5 ...).
+    Returns a 2D tensor (other axes in increasing order)."""
+    m = MIN_COORD_FP[comp]
+    others = [a for a in range(3) if a != axis]
+    # for each axis: list of (index_start, count) slices whose average gives the target
+    idx_sets = []
+    for a in range(3):
+        if a == axis:
+            targets = [float(x0)]
+        else:
+            n = int(round(hi[a] - lo[a]))
+            targets = [lo[a] + 0.5 + t for t in range(n)]
+        first = targets[0] - m[a]
+        if abs(first - round(first)) < 1e-9:
+            offs = [0]
+            base = int(round(first))
+        else:
+            offs = [0, 1]
+            base = int(math.floor(first))
+        idx_sets.append((base, len(targets), offs))
+    acc = None
+    cnt = 0
+    for ox in idx_sets[0][2]:
+        for oy in idx_sets[1][2]:
+            for oz in idx_sets[2][2]:
+                o = (ox, oy, oz)
+                sl = tuple(slice(idx_sets[a][0] + o[a], idx_sets[a][0] + o[a] + idx_sets[a][1]) for a in range(3))
+                v = F[sl]
+                acc = v if acc is None else acc + v
+                cnt += 1
+    out = acc / cnt
+    return out.squeeze(axis)
+
+
+def ntff_power(fields_re: Dict[str, torch.Tensor], fields_im: Optional[Dict[str, torch.Tensor]], size, ntff,
+               dx: float, wavelength: float, theta: float, phis: torch.Tensor) -> torch.Tensor:
+    """Normalised scattered power for every angle in ``phis`` (radians) at
+    polar angle ``theta``.  ``fields_*`` are full (gathered) global grids."""
+    dev = fields_re["Ex"].device
+    cdt = torch.complex128
+    k = 2 * PI / wavelength
+    L = [float(ntff[a]) for a in range(3)]
+    R = [float(size[a] - ntff[a]) for a in range(3)]
+    center = size[0] / 2.0  # the reference measures r' from Nx/2 on every axis (Scheme3D.cpp:4098)
+    phis = phis.to(dev, torch.float64)
+    st, ct = math.sin(theta), math.cos(theta)
+    rhat = torch.stack([st * torch.cos(phis), st * torch.sin(phis), torch.full_like(phis, ct)], dim=1)  # (A, 3)
+
+    def cplx(comp):
+        re = fields_re[comp].to(torch.float64)
+        im = fields_im[comp].to(torch.float64) if fields_im is not None else torch.zeros_like(re)
+        return re, im
+
+    Nvec = torch.zeros(phis.numel(), 3, dtype=cdt, device=dev)
+    Lvec = torch.zeros(phis.numel(), 3, dtype=cdt, device=dev)
+    for axis in range(3):
+        for x0, s in ((L[axis], -1.0), (R[axis], 1.0)):
+            others = [a for a in range(3) if a != axis]
+            lo = [L[a] for a in range(3)]
+            hi = [R[a] for a in range(3)]
+            Ht, Et = {}, {}
+            for a in others:
+                hc = "H" + "xyz"[a]
+                ec = "E" + "xyz"[a]
+                hr, hi_ = cplx(hc)
+                er, ei = cplx(ec)
+                Ht[a] = torch.complex(_sample(hr, hc, axis, x0, lo, hi), _sample(hi_, hc, axis, x0, lo, hi))
+                Et[a] = torch.complex(_sample(er, ec, axis, x0, lo, hi), _sample(ei, ec, axis, x0, lo, hi))
+            # n = s e_axis;  J = n x H ; M = -n x E
+            a1, a2 = others  # cyclic order check: e_axis x e_a1 = +/- e_a2
+            cyc = 1.0 if (a1 - axis) % 3 == 1 else -1.0
+            J = {a2: s * cyc * Ht[a1], a1: -s * cyc * Ht[a2]}
+            M = {a2: -s * cyc * Et[a1], a1: s * cyc * Et[a2]}
+            # r' of face-cell centres (in metres, relative to the centre)
+            u = torch.arange(int(round(hi[a1] - lo[a1])), device=dev, dtype=torch.float64) + lo[a1] + 0.5
+            v = torch.arange(int(round(hi[a2] - lo[a2])), device=dev, dtype=torch.float64) + lo[a2] + 0.5
+            U, V = torch.meshgrid(u, v, indexing="ij")
+            coords = [None, None, None]
+            coords[axis] = torch.full_like(U, x0)
+            coords[a1] = U
+            coords[a2] = V
+            rp = torch.stack([(c - center).reshape(-1) for c in coords], dim=1) * dx  # (P, 3)
+            # fields carry exp(-i w t) (source sin + i cos = i exp(-i w t)), so the
+            # radiation kernel is exp(-i k r_hat . r')
+            phase = torch.exp(-1j * k * (rhat @ rp.T).to(cdt))  # (A, P)
+            for comp_axis, val in J.items():
+                Nvec[:, comp_axis] += phase @ val.reshape(-1) * (dx * dx)
+            for comp_axis, val in M.items():
+                Lvec[:, comp_axis] += phase @ val.reshape(-1) * (dx * dx)
+    cp, sp = torch.cos(phis).to(cdt), torch.sin(phis).to(cdt)
+    N_th = Nvec[:, 0] * ct * cp + Nvec[:, 1] * ct * sp - Nvec[:, 2] * st
+    N_ph = -Nvec[:, 0] * sp + Nvec[:, 1] * cp
+    L_th = Lvec[:, 0] * ct * cp + Lvec[:, 1] * ct * sp - Lvec[:, 2] * st
+    L_ph = -Lvec[:, 0] * sp + Lvec[:, 1] * cp
+    p = (k * k) / (8 * PI * ETA0) * ((L_ph + ETA0 * N_th).abs() ** 2 + (L_th - ETA0 * N_ph).abs() ** 2)
+    return (p / (1.0 / ETA0)).real if torch.is_complex(p) else p / (1.0 / ETA0)
+
+
+def reference_angles() -> torch.Tensor:
+    """phi in [0, 2 pi + pi/180] with step pi/90 (Scheme3D.cpp:2283)."""
+    out = []
+    a = 0.0
+    while a <= 2 * PI + PI / 180:
+        out.append(a)
+        a += PI / 90
+    return torch.tensor(out, dtype=torch.float64)
+
+
+def ntff_report(scheme, t: int, out=None) -> Optional[torch.Tensor]:
+    """Evaluate the diagram for the scheme's current fields (gathering a
+    decomposed run on rank 0) and print the reference's report lines."""
+    import sys
+    from ..parallel.halo import gather_field
+    out = out or sys.stdout
+    comps = ("Ex", "Ey", "Ez", "Hx", "Hy", "Hz")
+    re = {c: gather_field(scheme, c, 0) if scheme.halo is not None else scheme.owned_field(c, 0) for c in comps}
+    im = None
+    if scheme.planes == 2:
+        im = {c: gather_field(scheme, c, 1) if scheme.halo is not None else scheme.owned_field(c, 1) for c in comps}
+    if re["Ex"] is None:
+        return None
+    phis = reference_angles()
+    p = ntff_power(re, im, scheme.cfg.size, scheme.cfg.ntff_size, scheme.dx, scheme.wavelength,
+                   scheme.layout.theta, phis)
+    for a, v in zip(phis.tolist(), p.cpu().tolist()):
+        out.write("=== t=%u, inc angle=%f; angle %f === %.17g \n" % (t, scheme.layout.phi, a, v))
+    return p

@@ -477,6 +477,32 @@ class YeeScheme:
         else:
             D[0], D[1] = D[1], D[0]
 
+    def named_state(self) -> Dict[str, torch.Tensor]:
+        """Every array needed to resume the run, by stable name (checkpoints)."""
+        out: Dict[str, torch.Tensor] = {}
+        for p in range(self.planes):
+            sfx = "" if p == 0 else "-im"
+            for c in self.comps:
+                out[c + sfx] = self.F[p][c]
+            if self.use_upml_chain:
+                for c in self.comps:
+                    for lv, t in enumerate(self.upml[c]["D"][p]):
+                        out["%s%s-aux%d%s" % ("D" if c[0] == "E" else "B", c[1], lv, sfx)] = t
+                    if self.cfg.use_metamaterials:
+                        for lv, t in enumerate(self.upml[c]["D1"][p]):
+                            out["%s1%s-aux%d%s" % ("D" if c[0] == "E" else "B", c[1], lv, sfx)] = t
+            if self.use_cpml:
+                for c, slabs in self.cpml.slabs.items():
+                    for n, sl in enumerate(slabs):
+                        out["psi-%s-%s-a%d-s%d%s" % (c, sl.src, sl.axis, sl.side, sfx)] = sl.psi[p]
+            if self.cfg.use_tfsf:
+                out["EInc" + sfx] = self.einc[p]
+                out["HInc" + sfx] = self.hinc[p]
+            if self.cfg.use_amp_mode:
+                for c in self.comps:
+                    out["%sAmplitude%s" % (c, sfx)] = self.amp[p][c]
+        return out
+
     def state_tensors(self) -> List[torch.Tensor]:
         """Every array that carries state between steps (for deep-halo
         exchanges and checkpoints)."""

@@ -49,7 +49,8 @@ def chunk_bounds(n: int, p: int, coord: int) -> Tuple[int, int]:
 
 
 def halo_cost(size: Sequence[int], topo: Sequence[int]) -> float:
-    """Cells exchanged per rank per half step (both faces of every split axis)."""
+    """Halo cells of the busiest rank: along a split axis an interior rank has
+    two face neighbours (one when the axis has just 2 ranks)."""
     chunk = [size[a] / topo[a] for a in range(3)]
     cost = 0.0
     for a in range(3):
@@ -58,7 +59,7 @@ def halo_cost(size: Sequence[int], topo: Sequence[int]) -> float:
             for b in range(3):
                 if b != a:
                     other *= chunk[b]
-            cost += 2 * other
+            cost += (2 if topo[a] > 2 else 1) * other
     return cost
 
 

