@@ -1,0 +1,144 @@
+"""Analytic physics checks (CPU, torch reference backend).
+
+The reference has no physics validation.  These tests pin
+the solver to known results: propagation speed, cavity eigenfrequencies,
+energy conservation, absorbing-boundary reflection and TF/SF leakage.
+"""
+
+import math
+
+import numpy as np
+import torch
+
+from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+from fdtd3d_amd.ops import make_ops
+from fdtd3d_amd.utils.constants import EPS0, MU0, SPEED_OF_LIGHT
+
+
+def make(cfg):
+    s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+    s.init_scheme()
+    s.init_grids()
+    return s
+
+
+def test_1d_gaussian_pulse_speed():
+    """BASELINE config 1: 1D vacuum, Gaussian pulse -- the peak travels at c
+    (numerical dispersion of a well-resolved pulse is negligible)."""
+    cfg = SchemeConfig(scheme="1d", size=(2000, 1, 1), time_steps=0, scene="vacuum", source="gaussian",
+                       gaussian_width=20, gaussian_delay=80)
+    s = make(cfg)
+    src = 1000
+    s.perform_steps(300)
+    ez = s.F[0]["Ez"][:, 0, 0]
+    right = int(torch.argmax(ez[src + 5:]).item()) + src + 5
+    # after the pulse peak left the source (t = delay), it moved c*dt*(T - delay)
+    expected = src + s.courant * (300 - 80)
+    assert abs(right - expected) <= 2, (right, expected)
+
+
+def test_cavity_resonance_tmz():
+    """PEC-bounded 2D TMz cavity: the dominant mode after a broadband kick is
+    TM11 with f = c/2 * sqrt((1/a)^2 + (1/b)^2) (up to Yee dispersion)."""
+    n = 40
+    cfg = SchemeConfig(scheme="tmz", size=(n, n, 1), time_steps=0, scene="vacuum", source="gaussian",
+                       gaussian_width=4, gaussian_delay=12)
+    s = make(cfg)
+    # smooth off-centre blob: excites the low modes, TM11 the lowest and strongest
+    rec = []
+    s.point_source = None
+    x = torch.arange(n, dtype=torch.float64) + 0.5
+    X, Y = torch.meshgrid(x, x, indexing="ij")
+    blob = torch.exp(-((X - 16) ** 2 + (Y - 18) ** 2) / 30.0)
+    s.F[0]["Ez"][1:, 1:, 0] = blob[1:, 1:]
+    steps = 4096
+    for _ in range(steps):
+        s.step()
+        rec.append(float(s.F[0]["Ez"][13, 17, 0]))
+    sig = np.array(rec) - np.mean(rec)
+    spec = np.abs(np.fft.rfft(sig * np.hanning(steps)))
+    freqs = np.fft.rfftfreq(steps, d=s.dt)
+    peaks = [freqs[i] for i in range(2, len(spec) - 1)
+             if spec[i] > spec[i - 1] and spec[i] > spec[i + 1] and spec[i] > 0.1 * spec.max()]
+    # The reference's computation ranges (YeeGridLayout.h:131-182) make the low
+    # border an electric wall (Ez index 0 never updated, at x = 0.5) and the high
+    # border a magnetic wall (Hy index N-1 never updated, at x = N): a
+    # quarter-wave cavity of length L = (N - 0.5) dx with modes
+    # f = c / (2L) * sqrt((m + 1/2)^2 + (n + 1/2)^2).
+    L = (n - 0.5) * s.dx
+    expect = sorted(SPEED_OF_LIGHT / (2 * L) * math.sqrt((m + 0.5) ** 2 + (q + 0.5) ** 2)
+                    for m in range(3) for q in range(3))
+    for f in peaks[:3]:
+        rel = min(abs(f - e) / e for e in expect)
+        assert rel < 0.02, (f, expect[:4])
+    assert abs(peaks[0] - expect[0]) / expect[0] < 0.02
+
+
+def test_energy_conservation_pec_cavity():
+    """Closed PEC cavity, source off: discrete EM energy stays constant."""
+    cfg = SchemeConfig(scheme="3d", size=(20, 22, 24), time_steps=0, scene="vacuum")
+    s = make(cfg)
+    s.point_source = None
+    g = torch.Generator().manual_seed(1)
+    for c in ("Ex", "Ey", "Ez"):
+        lo, hi = s.layout.global_range(c)
+        sl = tuple(slice(lo[d], hi[d]) for d in range(3))
+        s.F[0][c][sl] = torch.randn(s.F[0][c][sl].shape, generator=g, dtype=torch.float64)
+
+    def staggered_energy_step():
+        """Leapfrog's exactly conserved discrete energy
+        eps0 |E^{n+1}|^2 + mu0 H^{n+1/2} . H^{n+3/2}, measured across one step."""
+        h_old = {c: s.F[0][c].clone() for c in ("Hx", "Hy", "Hz")}
+        s.step()
+        e = sum(float((s.F[0][c] ** 2).sum()) for c in ("Ex", "Ey", "Ez")) * EPS0
+        h = sum(float((h_old[c] * s.F[0][c]).sum()) for c in ("Hx", "Hy", "Hz")) * MU0
+        return 0.5 * (e + h)
+
+    e0 = staggered_energy_step()
+    vals = [staggered_energy_step() for _ in range(200)]
+    assert max(abs(v - e0) / e0 for v in vals) < 1e-10
+
+
+def _reflection(pml_type):
+    def run(size, use_pml):
+        cfg = SchemeConfig(scheme="tmz", size=size, time_steps=0, scene="vacuum", use_pml=use_pml,
+                           pml_type=pml_type, pml_size=(10, 10, 1), source="gaussian", gaussian_width=6,
+                           gaussian_delay=25)
+        return make(cfg)
+    small = run((80, 80, 1), True)
+    big = run((400, 400, 1), False)
+    small.point_source = ("Ez", (40, 40, 0), (40, 40, 0))
+    big.point_source = ("Ez", (200, 200, 0), (200, 200, 0))
+    err, peak = 0.0, 0.0
+    for t in range(260):
+        small.step()
+        big.step()
+        if t % 4 == 0:
+            a = small.F[0]["Ez"][10:70, 10:70, 0]
+            b = big.F[0]["Ez"][170:230, 170:230, 0]
+            peak = max(peak, float(b.abs().max()))
+            err = max(err, float((a - b).abs().max()))
+    return err / peak
+
+
+def test_upml_reflection():
+    assert _reflection("upml") < 2e-2
+
+
+def test_cpml_reflection():
+    assert _reflection("cpml") < 2e-2
+
+
+def test_tfsf_leakage_3d():
+    """Plane wave through an empty TF/SF box: the scattered-field region stays
+    (almost) empty while the total-field region carries the full wave."""
+    cfg = SchemeConfig(scheme="3d", size=(40, 40, 40), time_steps=120, scene="vacuum", use_pml=True,
+                       pml_type="cpml", pml_size=(6, 6, 6), use_tfsf=True, tfsf_size=(11, 11, 11),
+                       theta=70, phi=25, psi=40)
+    s = make(cfg)
+    s.perform_steps()
+    ez = s.F[0]["Ez"]
+    inside = float(ez[14:26, 14:26, 14:26].abs().max())
+    outside = max(float(ez[7:9, 7:33, 7:33].abs().max()), float(ez[31:33, 7:33, 7:33].abs().max()))
+    assert inside > 0.3
+    assert outside < 0.05 * inside, (outside, inside)
