@@ -1,0 +1,63 @@
+// C ABI of libfdtd3d_hip (the HIP kernels): prototypes for native callers.
+// The Python side binds the same symbols through ctypes (ops/hip_ops.py).
+#pragma once
+
+#include <stdint.h>
+
+extern "C" {
+int fdtd_abi_version();
+
+int fdtd_update_e3d_f32(float* ex, float* ey, float* ez, const float* hx, const float* hy, const float* hz,
+                        const float* cbx, const float* cby, const float* cbz, double cb, int nx, int ny, int nz,
+                        const int* boxes, int xchunk, void* stream);
+int fdtd_update_h3d_f32(float* hx, float* hy, float* hz, const float* ex, const float* ey, const float* ez,
+                        const float* dbx, const float* dby, const float* dbz, double db, int nx, int ny, int nz,
+                        const int* boxes, int xchunk, void* stream);
+int fdtd_update_e3d_f64(double* ex, double* ey, double* ez, const double* hx, const double* hy, const double* hz,
+                        const double* cbx, const double* cby, const double* cbz, double cb, int nx, int ny, int nz,
+                        const int* boxes, int xchunk, void* stream);
+int fdtd_update_h3d_f64(double* hx, double* hy, double* hz, const double* ex, const double* ey, const double* ez,
+                        const double* dbx, const double* dby, const double* dbz, double db, int nx, int ny, int nz,
+                        const int* boxes, int xchunk, void* stream);
+int fdtd_update_e3d_v4_f32(float* ex, float* ey, float* ez, const float* hx, const float* hy, const float* hz,
+                           const float* cbx, const float* cby, const float* cbz, double cb, int nx, int ny, int nz,
+                           const int* boxes, int xchunk, void* stream);
+int fdtd_update_h3d_v4_f32(float* hx, float* hy, float* hz, const float* ex, const float* ey, const float* ez,
+                           const float* dbx, const float* dby, const float* dbz, double db, int nx, int ny, int nz,
+                           const int* boxes, int xchunk, void* stream);
+int fdtd_fused3d_f32(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
+                     const float* const* cbs, const float* const* dbs, double cb, double db, int nx, int ny, int nz,
+                     const int* boxes, int xchunk, long long src_off, int src_comp, double src_val, void* s);
+int fdtd_fused3d_f64(const double* const* ein, const double* const* hin, double* const* eout,
+                     double* const* hout, const double* const* cbs, const double* const* dbs, double cb, double db,
+                     int nx, int ny, int nz, const int* boxes, int xchunk, long long src_off, int src_comp,
+                     double src_val, void* s);
+int fdtd_fused3d_v4_f32(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
+                        const float* const* cbs, const float* const* dbs, double cb, double db, int nx, int ny,
+                        int nz, const int* boxes, int xchunk, long long src_off, int src_comp, double src_val,
+                        void* s);
+
+int fdtd_tmz_e_f32(float* ez, const float* hx, const float* hy, const float* cbz, double cb, int nx, int ny,
+                   const int* box, int xchunk, void* s);
+int fdtd_tmz_h_f32(float* hx, float* hy, const float* ez, const float* dbx, const float* dby, double db, int nx,
+                   int ny, const int* boxes, int xchunk, void* s);
+int fdtd_tez_e_f32(float* ex, float* ey, const float* hz, const float* cbx, const float* cby, double cb, int nx,
+                   int ny, const int* boxes, int xchunk, void* s);
+int fdtd_tez_h_f32(float* hz, const float* ex, const float* ey, const float* dbz, double db, int nx, int ny,
+                   const int* box, int xchunk, void* s);
+int fdtd_1d_e_f32(float* ez, const float* hy, const float* cbz, double cb, int lo, int hi, void* s);
+int fdtd_1d_h_f32(float* hy, const float* ez, const float* dby, double db, int lo, int hi, void* s);
+int fdtd_tmz_e_f64(double* ez, const double* hx, const double* hy, const double* cbz, double cb, int nx, int ny,
+                   const int* box, int xchunk, void* s);
+int fdtd_tmz_h_f64(double* hx, double* hy, const double* ez, const double* dbx, const double* dby, double db, int nx,
+                   int ny, const int* boxes, int xchunk, void* s);
+int fdtd_tez_e_f64(double* ex, double* ey, const double* hz, const double* cbx, const double* cby, double cb, int nx,
+                   int ny, const int* boxes, int xchunk, void* s);
+int fdtd_tez_h_f64(double* hz, const double* ex, const double* ey, const double* dbz, double db, int nx, int ny,
+                   const int* box, int xchunk, void* s);
+int fdtd_1d_e_f64(double* ez, const double* hy, const double* cbz, double cb, int lo, int hi, void* s);
+int fdtd_1d_h_f64(double* hy, const double* ez, const double* dby, double db, int lo, int hi, void* s);
+
+int fdtd_set_value_f32(float* f, long long off, double v, void* s);
+int fdtd_set_value_f64(double* f, long long off, double v, void* s);
+}

@@ -1,0 +1,30 @@
+// Host-side native runtime pieces shared by the standalone driver:
+// topology optimiser, Yee computation ranges, DAT/BMP writers.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace fdtd {
+
+using Int3 = std::array<int, 3>;
+
+// ---- topology (same cost model as fdtd3d_amd/parallel/topology.py) ----
+double halo_cost(const Int3& size, const Int3& topo);
+Int3 optimal_topology(const Int3& size, int nprocs, const std::vector<int>& axes);
+void chunk_bounds(int n, int p, int coord, int& lo, int& hi);
+
+// ---- Yee layout (fdtd3d_amd/layout/yee.py) ----
+// component index: 0..2 = Ex,Ey,Ez; 3..5 = Hx,Hy,Hz
+void global_range(int comp, const Int3& size, const std::vector<int>& active_axes, Int3& lo, Int3& hi);
+
+// ---- files (reference naming, Source/File-Management/Commons.h:56-68) ----
+std::string grid_file_name(long step, int rank, const std::string& name, const std::string& dir);
+bool write_dat(const std::string& path, const void* data, size_t bytes);
+// rgb: "rgb" (blue-green-red) or "gray"; values row-major [w][h]; pixel (x, y), y = 0 top
+bool write_bmp(const std::string& path, const std::vector<double>& values, int w, int h,
+               const std::string& palette);
+
+}  // namespace fdtd

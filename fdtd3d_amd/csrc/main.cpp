@@ -1,0 +1,360 @@
+// fdtd3d -- standalone native driver (no Python): command line -> device
+// fields -> HIP kernels -> timing report, the counterpart of the reference's
+// Source/main.cpp built directly on libfdtd3d_hip's C ABI.
+//
+// Covers the plain Yee solvers (1D, 2D TMz/TEz, 3D) on one GPU with the
+// vacuum / dielectric-sphere scenes and the hard point source, fp32 or fp64,
+// fused or split 3D kernels, DAT/BMP output of the final fields.  Absorbing
+// layers, TF/SF, dispersive media, NTFF, amplitude mode and multi-GPU runs go
+// through the Python driver (python -m fdtd3d_amd), which shares the kernels;
+// asking this binary for them is an error, never a silent fallback.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "capi.h"
+#include "host_native.h"
+#include "settings_native.h"
+
+namespace {
+
+constexpr double kC = 2.99792458e8;
+constexpr double kEps0 = 8.8541878176203892e-12;
+constexpr double kMu0 = 1.2566370614359173e-6;
+constexpr double kPi = 3.14159265358979323846;
+
+#define HIP_OK(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) {                                                             \
+      std::fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      std::exit(1);                                                                     \
+    }                                                                                   \
+  } while (0)
+
+#define K_OK(x)                                                              \
+  do {                                                                       \
+    int r_ = (x);                                                            \
+    if (r_ != 0) {                                                           \
+      std::fprintf(stderr, "kernel launch failed (%d) at %s:%d\n", r_, __FILE__, __LINE__); \
+      std::exit(1);                                                          \
+    }                                                                        \
+  } while (0)
+
+double sphere_eps(double x, double y, double z, const double c[3], double r, double eps) {
+  // linear sub-cell smoothing (reference Approximation.cpp:286-314)
+  const double d = std::sqrt((x - c[0]) * (x - c[0]) + (y - c[1]) * (y - c[1]) + (z - c[2]) * (z - c[2]));
+  const double diff = d - r;
+  if (diff < -0.5) return eps;
+  if (diff > 0.5) return 1.0;
+  const double p = 0.5 - diff;
+  return p * eps + (1 - p) * 1.0;
+}
+
+template <typename T>
+struct Dev {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    n = count;
+    HIP_OK(hipMalloc(&p, n * sizeof(T)));
+    HIP_OK(hipMemset(p, 0, n * sizeof(T)));
+  }
+  ~Dev() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+template <typename T>
+struct Api;
+template <>
+struct Api<float> {
+  static constexpr const char* name = "float";
+};
+template <>
+struct Api<double> {
+  static constexpr const char* name = "double";
+};
+
+int e3d(float* a, float* b, float* c, const float* d, const float* e, const float* f, const float* g,
+        const float* h, const float* i, double cb, int nx, int ny, int nz, const int* bx, int xc, void* s, bool v4) {
+  return v4 ? fdtd_update_e3d_v4_f32(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s)
+            : fdtd_update_e3d_f32(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s);
+}
+int e3d(double* a, double* b, double* c, const double* d, const double* e, const double* f, const double* g,
+        const double* h, const double* i, double cb, int nx, int ny, int nz, const int* bx, int xc, void* s, bool) {
+  return fdtd_update_e3d_f64(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s);
+}
+int h3d(float* a, float* b, float* c, const float* d, const float* e, const float* f, const float* g,
+        const float* h, const float* i, double cb, int nx, int ny, int nz, const int* bx, int xc, void* s, bool v4) {
+  return v4 ? fdtd_update_h3d_v4_f32(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s)
+            : fdtd_update_h3d_f32(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s);
+}
+int h3d(double* a, double* b, double* c, const double* d, const double* e, const double* f, const double* g,
+        const double* h, const double* i, double cb, int nx, int ny, int nz, const int* bx, int xc, void* s, bool) {
+  return fdtd_update_h3d_f64(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s);
+}
+int fused(const float* const* ei, const float* const* hi, float* const* eo, float* const* ho,
+          const float* const* cbs, const float* const* dbs, double cb, double db, int nx, int ny, int nz,
+          const int* bx, long long so, int sc, double sv, void* s, bool v4) {
+  return v4 ? fdtd_fused3d_v4_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s)
+            : fdtd_fused3d_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s);
+}
+int fused(const double* const* ei, const double* const* hi, double* const* eo, double* const* ho,
+          const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
+          const int* bx, long long so, int sc, double sv, void* s, bool) {
+  return fdtd_fused3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s);
+}
+int setv(float* f, long long off, double v, void* s) { return fdtd_set_value_f32(f, off, v, s); }
+int setv(double* f, long long off, double v, void* s) { return fdtd_set_value_f64(f, off, v, s); }
+int tmz_e(float* a, const float* b, const float* c, const float* d, double cb, int nx, int ny, const int* bx, void* s) {
+  return fdtd_tmz_e_f32(a, b, c, d, cb, nx, ny, bx, 0, s);
+}
+int tmz_e(double* a, const double* b, const double* c, const double* d, double cb, int nx, int ny, const int* bx,
+          void* s) {
+  return fdtd_tmz_e_f64(a, b, c, d, cb, nx, ny, bx, 0, s);
+}
+int tmz_h(float* a, float* b, const float* c, const float* d, const float* e, double db, int nx, int ny,
+          const int* bx, void* s) {
+  return fdtd_tmz_h_f32(a, b, c, d, e, db, nx, ny, bx, 0, s);
+}
+int tmz_h(double* a, double* b, const double* c, const double* d, const double* e, double db, int nx, int ny,
+          const int* bx, void* s) {
+  return fdtd_tmz_h_f64(a, b, c, d, e, db, nx, ny, bx, 0, s);
+}
+int tez_e(float* a, float* b, const float* c, const float* d, const float* e, double cb, int nx, int ny,
+          const int* bx, void* s) {
+  return fdtd_tez_e_f32(a, b, c, d, e, cb, nx, ny, bx, 0, s);
+}
+int tez_e(double* a, double* b, const double* c, const double* d, const double* e, double cb, int nx, int ny,
+          const int* bx, void* s) {
+  return fdtd_tez_e_f64(a, b, c, d, e, cb, nx, ny, bx, 0, s);
+}
+int tez_h(float* a, const float* b, const float* c, const float* d, double db, int nx, int ny, const int* bx, void* s) {
+  return fdtd_tez_h_f32(a, b, c, d, db, nx, ny, bx, 0, s);
+}
+int tez_h(double* a, const double* b, const double* c, const double* d, double db, int nx, int ny, const int* bx,
+          void* s) {
+  return fdtd_tez_h_f64(a, b, c, d, db, nx, ny, bx, 0, s);
+}
+int e1d(float* a, const float* b, const float* c, double cb, int lo, int hi, void* s) {
+  return fdtd_1d_e_f32(a, b, c, cb, lo, hi, s);
+}
+int e1d(double* a, const double* b, const double* c, double cb, int lo, int hi, void* s) {
+  return fdtd_1d_e_f64(a, b, c, cb, lo, hi, s);
+}
+int h1d(float* a, const float* b, const float* c, double db, int lo, int hi, void* s) {
+  return fdtd_1d_h_f32(a, b, c, db, lo, hi, s);
+}
+int h1d(double* a, const double* b, const double* c, double db, int lo, int hi, void* s) {
+  return fdtd_1d_h_f64(a, b, c, db, lo, hi, s);
+}
+
+template <typename T>
+int run(const fdtd::Settings& s) {
+  const int dim = s.dimension;
+  std::string scheme = dim == 3 ? "3d" : (dim == 2 ? s.mode2D : "1d");
+  fdtd::Int3 N = {s.sizeX, dim >= 2 ? s.sizeY : 1, dim == 3 ? s.sizeZ : 1};
+  std::vector<int> active = dim == 3 ? std::vector<int>{0, 1, 2} : (dim == 2 ? std::vector<int>{0, 1} : std::vector<int>{0});
+  const size_t cells = (size_t)N[0] * N[1] * N[2];
+  const double dx = s.gridStep, courant = s.courantNum;
+  const double dt = dx * courant / kC;
+  const double freq = kC / s.sourceWaveLength;
+  const bool vacuum = s.scene == "vacuum" || (s.scene == "reference" && dim != 3);
+  const bool v4 = sizeof(T) == 4 && N[2] % 4 == 0 && dim == 3;
+  const bool use_fused = dim == 3 && !s.doUseSplitKernels;
+  hipStream_t st;
+  HIP_OK(hipStreamCreate(&st));
+
+  // components present: 0..2 E, 3..5 H
+  bool present[6];
+  for (int c = 0; c < 6; ++c) present[c] = dim == 3;
+  if (scheme == "tmz") present[2] = present[3] = present[4] = true;
+  if (scheme == "tez") present[0] = present[1] = present[5] = true;
+  if (scheme == "1d") present[2] = present[4] = true;
+  Dev<T> F[6], G[6], C[6];
+  for (int c = 0; c < 6; ++c)
+    if (present[c]) {
+      F[c].alloc(cells);
+      if (use_fused) G[c].alloc(cells);
+    }
+  double cb = dt / (kEps0 * dx), db = dt / (kMu0 * dx);
+  const bool percell = !vacuum;
+  if (percell) {
+    // per-component averaged eps on the eps layout (2-point E averaging,
+    // YeeGridLayout.h:1007-1263); mu = 1 -> constant H arrays
+    const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
+    auto eps_at = [&](int i, int j, int k) {
+      return sphere_eps(i + 0.5, j + 0.5, dim == 3 ? k + 0.5 : ctr[2], ctr, s.sphereRadius, s.sphereEps);
+    };
+    std::vector<T> host(cells);
+    for (int c = 0; c < 6; ++c) {
+      if (!present[c]) continue;
+      for (int i = 0; i < N[0]; ++i)
+        for (int j = 0; j < N[1]; ++j)
+          for (int k = 0; k < N[2]; ++k) {
+            double v;
+            if (c < 3) {
+              const int di = c == 0, dj = c == 1 && dim >= 2, dk = c == 2 && dim == 3;
+              v = cb * 2.0 / (eps_at(i, j, k) + eps_at(i + di, j + dj, k + dk));
+            } else {
+              v = db;
+            }
+            host[((size_t)i * N[1] + j) * N[2] + k] = (T)v;
+          }
+      C[c].alloc(cells);
+      HIP_OK(hipMemcpy(C[c].p, host.data(), cells * sizeof(T), hipMemcpyHostToDevice));
+    }
+  }
+  int boxes[36];
+  for (int c = 0; c < 6; ++c) {
+    fdtd::Int3 lo, hi;
+    fdtd::global_range(c, N, active, lo, hi);
+    for (int a = 0; a < 3; ++a) {
+      boxes[6 * c + a] = lo[a];
+      boxes[6 * c + 3 + a] = hi[a];
+    }
+  }
+  // point source (reference Scheme3D.cpp:2011-2022, SchemeTMz.cpp:1345)
+  int src_comp = 2;
+  fdtd::Int3 sp = {N[0] / 2, N[1] / 2, N[2] / 2};
+  if (scheme == "tmz") sp = {N[0] > 140 ? 70 : N[0] / 2, N[1] / 2, 0};
+  if (scheme == "tez") src_comp = 5;
+  if (scheme == "1d") sp = {N[0] / 2, 0, 0};
+  const long long src_off = ((long long)sp[0] * N[1] + sp[1]) * N[2] + sp[2];
+  auto src_val = [&](int t) {
+    if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
+    return std::sin(dt * t * 2 * kPi * freq);
+  };
+  auto cp = [&](Dev<T>* A, int c) -> const T* { return A[c].p; };
+  (void)cp;
+
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventRecord(e0, st));
+  const int steps = s.numTimeSteps;
+  for (int t = 0; t < steps; ++t) {
+    const double sv = src_val(t);
+    if (scheme == "3d") {
+      if (use_fused) {
+        const T* ei[3] = {F[0].p, F[1].p, F[2].p};
+        const T* hi[3] = {F[3].p, F[4].p, F[5].p};
+        T* eo[3] = {G[0].p, G[1].p, G[2].p};
+        T* ho[3] = {G[3].p, G[4].p, G[5].p};
+        const T* cbs[3] = {C[0].p, C[1].p, C[2].p};
+        const T* dbs[3] = {C[3].p, C[4].p, C[5].p};
+        K_OK(fused(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, percell ? 1.0 : db, N[0], N[1], N[2], boxes,
+                   src_off, src_comp, sv, st, v4));
+        for (int c = 0; c < 6; ++c) std::swap(F[c].p, G[c].p);
+      } else {
+        K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, percell ? 1.0 : cb, N[0],
+                 N[1], N[2], boxes, 0, st, v4));
+        K_OK(setv(F[src_comp].p, src_off, sv, st));
+        K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, percell ? 1.0 : db, N[0],
+                 N[1], N[2], boxes + 18, 0, st, v4));
+      }
+    } else if (scheme == "tmz") {
+      K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], boxes + 12, st));
+      K_OK(setv(F[2].p, src_off, sv, st));
+      int hb[12];
+      std::memcpy(hb, boxes + 18, 12 * sizeof(int));
+      K_OK(tmz_h(F[3].p, F[4].p, F[2].p, C[3].p, C[4].p, percell ? 1.0 : db, N[0], N[1], hb, st));
+    } else if (scheme == "tez") {
+      K_OK(tez_e(F[0].p, F[1].p, F[5].p, C[0].p, C[1].p, percell ? 1.0 : cb, N[0], N[1], boxes, st));
+      K_OK(setv(F[5].p, src_off, sv, st));  // hard source between the E and H updates
+      K_OK(tez_h(F[5].p, F[0].p, F[1].p, C[5].p, percell ? 1.0 : db, N[0], N[1], boxes + 30, st));
+    } else {
+      K_OK(e1d(F[2].p, F[4].p, C[2].p, percell ? 1.0 : cb, boxes[12], boxes[15], st));
+      K_OK(setv(F[2].p, src_off, sv, st));
+      K_OK(h1d(F[4].p, F[2].p, C[4].p, percell ? 1.0 : db, boxes[24], boxes[27], st));
+    }
+  }
+  HIP_OK(hipEventRecord(e1, st));
+  HIP_OK(hipEventSynchronize(e1));
+  HIP_OK(hipGetLastError());
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  const double sec = ms / 1e3;
+
+  std::printf("Total time = %f seconds\n", sec);
+  std::printf("Dimension: %d\n", dim);
+  if (dim == 3)
+    std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);
+  else if (dim == 2)
+    std::printf("Grid size: %dx%d\n", N[0], N[1]);
+  else
+    std::printf("Grid size: %d\n", N[0]);
+  std::printf("Number of time steps: %d\n\n", steps);
+  std::printf("Value type: %s\n", Api<T>::name);
+  std::printf("\n-------- Details --------\n");
+  std::printf("Parallel grid: 0\n");
+  std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
+  std::printf("Throughput: %.1f Mcells/s\n", cells * (double)steps / sec / 1e6);
+  if (s.doPrintJson)
+    std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f}\n", sec, steps,
+                cells * (double)steps / sec / 1e6);
+
+  if (s.doSaveRes) {
+    const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
+    std::vector<T> host(cells);
+    for (int c = 0; c < 6; ++c) {
+      if (!present[c]) continue;
+      HIP_OK(hipMemcpy(host.data(), F[c].p, cells * sizeof(T), hipMemcpyDeviceToHost));
+      const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
+      if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), cells * sizeof(T));
+      if (s.saveAsBMP || !s.saveAsDAT) {
+        // middle slice along z (3D) or the plane (2D) / line (1D)
+        const int w = N[0], h = N[1];
+        const int kz = dim == 3 ? N[2] / 2 : 0;
+        std::vector<double> v((size_t)w * h);
+        for (int i = 0; i < w; ++i)
+          for (int j = 0; j < h; ++j) v[(size_t)i * h + j] = host[((size_t)i * N[1] + j) * N[2] + kz];
+        const std::string name = dim == 3 ? base + std::to_string(kz) + "-Re.bmp" : base + "-Re.bmp";
+        fdtd::write_bmp(name, v, w, h, s.dumperPalette);
+      }
+    }
+  }
+  HIP_OK(hipStreamDestroy(st));
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  fdtd::Settings s;
+  int st = s.parse(argc, argv, true, 1);
+  if (st == fdtd::SETTINGS_BREAK) {
+    std::fputs(s.message.c_str(), stdout);
+    return 0;
+  }
+  if (st != fdtd::SETTINGS_OK) {
+    std::fputs(s.message.c_str(), stdout);
+    return st;
+  }
+  if (s.validate() != fdtd::SETTINGS_OK) {
+    std::fprintf(stdout, "ERROR: %s\n", s.message.c_str());
+    return 1;
+  }
+  if (s.doUsePML || s.doUseTFSF || s.doUseMetamaterials || s.doUseNTFF || s.doUseAmplitudeMode ||
+      s.doUseComplexFieldValues || s.doUseParallelGrid || s.doUseDoubleMaterialPrecision ||
+      !s.loadFromFile.empty()) {
+    std::fprintf(stderr,
+                 "fdtd3d (native): PML, TF/SF, metamaterials, NTFF, amplitude mode, complex fields, "
+                 "parallel grids and resume run through the Python driver: python -m fdtd3d_amd <same options>\n");
+    return 2;
+  }
+  int ndev = 0;
+  HIP_OK(hipGetDeviceCount(&ndev));
+  if (ndev < 1) {
+    std::fprintf(stderr, "no HIP device\n");
+    return 1;
+  }
+  HIP_OK(hipSetDevice(0 % (s.numCudaGPUs > 0 ? s.numCudaGPUs : 1)));
+  return s.valueType == "f32" ? run<float>(s) : run<double>(s);
+}

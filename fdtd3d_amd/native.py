@@ -1,0 +1,72 @@
+"""ctypes bindings of the native host runtime (``libfdtd3d_host.so``).
+
+The standalone ``fdtd3d`` executable (csrc/main.cpp) is built from the same
+objects; these bindings exist so the Python tests can pin the native settings
+parser and topology optimiser to their Python counterparts
+(utils/settings.py, parallel/topology.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from typing import Dict, Sequence, Tuple
+
+from .ops.build import EXE, LIB_HOST
+
+_lib = None
+
+
+def load_host_library(build_if_missing: bool = True) -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_HOST) and build_if_missing:
+        from .ops import build as _b
+        _b.build(exe=False)
+    lib = ctypes.CDLL(LIB_HOST)
+    lib.fdtd_settings_parse_json.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                             ctypes.c_char_p, ctypes.c_int]
+    lib.fdtd_settings_parse_json.restype = ctypes.c_int
+    lib.fdtd_optimal_topology.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_int)]
+    lib.fdtd_optimal_topology.restype = None
+    _lib = lib
+    return lib
+
+
+def parse_settings(argv: Sequence[str]) -> Tuple[int, object]:
+    """Parse ``argv`` with the native parser: (status, dict-or-message)."""
+    lib = load_host_library()
+    arr = (ctypes.c_char_p * len(argv))(*[a.encode() for a in argv])
+    buf = ctypes.create_string_buffer(1 << 16)
+    st = lib.fdtd_settings_parse_json(len(argv), arr, buf, len(buf))
+    text = buf.value.decode()
+    if st == 0:
+        return st, json.loads(text)
+    return st, text
+
+
+def optimal_topology(size: Sequence[int], nprocs: int, axes: Sequence[int] = (0, 1, 2)) -> Tuple[int, int, int]:
+    lib = load_host_library()
+    s = (ctypes.c_int * 3)(*size)
+    ax = (ctypes.c_int * len(axes))(*axes)
+    out = (ctypes.c_int * 3)()
+    lib.fdtd_optimal_topology(s, nprocs, ax, len(axes), out)
+    return tuple(out)
+
+
+def executable() -> str:
+    return EXE
+
+
+def settings_dict_equal(native: Dict[str, object], py: Dict[str, object]) -> bool:
+    for k, v in py.items():
+        n = native.get(k)
+        if isinstance(v, float):
+            if n is None or abs(float(n) - v) > 1e-12 * max(1.0, abs(v)):
+                return False
+        elif n != v:
+            return False
+    return True

@@ -1,0 +1,73 @@
+"""Standalone native driver (csrc/main.cpp) on the GPU vs the Python driver
+on the torch CPU backend: identical final fields for the plain Yee schemes."""
+import io
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from fdtd3d_amd import native
+from fdtd3d_amd.runner import run as py_run
+
+CASES = {
+    "3d_fused_vacuum": ["--3d", "--sizex", "28", "--sizey", "20", "--sizez", "24", "--time-steps", "12",
+                        "--scene", "vacuum"],
+    "3d_split_vacuum": ["--3d", "--sizex", "28", "--sizey", "20", "--sizez", "24", "--time-steps", "12",
+                        "--scene", "vacuum", "--split-kernels"],
+    "3d_fused_sphere": ["--3d", "--sizex", "32", "--same-size", "--time-steps", "15", "--scene", "sphere",
+                        "--sphere-center-x", "16", "--sphere-center-y", "16", "--sphere-center-z", "16",
+                        "--sphere-radius", "6", "--sphere-eps", "4"],
+    "2d_tmz": ["--2d", "--sizex", "60", "--sizey", "50", "--time-steps", "25", "--scene", "vacuum"],
+    "2d_tez": ["--2d", "--2d-mode", "tez", "--sizex", "60", "--sizey", "50", "--time-steps", "25",
+               "--scene", "vacuum"],
+    "1d": ["--1d", "--sizex", "300", "--time-steps", "40", "--scene", "vacuum", "--source", "gaussian",
+           "--gaussian-width", "8", "--gaussian-delay", "30"],
+}
+
+COMPS = {"3d": ["Ex", "Ey", "Ez", "Hx", "Hy", "Hz"], "tmz": ["Ez", "Hx", "Hy"], "tez": ["Ex", "Ey", "Hz"],
+         "1d": ["Ez", "Hy"]}
+
+
+def _shape(argv):
+    def get(flag, default):
+        return int(argv[argv.index(flag) + 1]) if flag in argv else default
+    nx = get("--sizex", 100)
+    same = "--same-size" in argv
+    if "--1d" in argv:
+        return (nx, 1, 1), "1d"
+    if "--2d" in argv:
+        return (nx, nx if same else get("--sizey", 100), 1), ("tez" if "tez" in argv else "tmz")
+    return (nx, nx if same else get("--sizey", 100), nx if same else get("--sizez", 100)), "3d"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("case", list(CASES))
+def test_native_driver_matches_python(case, dtype, tmp_path, gpu):
+    exe = native.executable()
+    assert os.path.exists(exe), "native fdtd3d executable missing (run python -m fdtd3d_amd.ops.build)"
+    argv = CASES[case] + ["--dtype", dtype, "--save-res", "--save-as-dat"]
+    nd, pd = tmp_path / "native", tmp_path / "py"
+    nd.mkdir()
+    pd.mkdir()
+    r = subprocess.run([exe] + argv + ["--output-dir", str(nd)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Mcells/s" in r.stdout
+    assert py_run(argv[:-4] + ["--dtype", "f64", "--save-res", "--save-as-dat", "--backend", "torch",
+                               "--device", "cpu", "--output-dir", str(pd)], out=io.StringIO()) == 0
+    shape, scheme = _shape(argv)
+    steps = int(argv[argv.index("--time-steps") + 1])
+    ndt = np.float32 if dtype == "f32" else np.float64
+    errs = {}
+    for c in COMPS[scheme]:
+        name = "current[%d]_rank-0_%s.dat" % (steps, c)
+        a = np.fromfile(nd / name, dtype=ndt).astype(np.float64).reshape(shape)
+        b = np.fromfile(pd / name, dtype=np.float64).reshape(shape)
+        errs[c] = (np.abs(a - b).max(), np.abs(b).max())
+    for kind in "EH":
+        peak = max(v[1] for c, v in errs.items() if c[0] == kind)
+        tol = 1e-11 if dtype == "f64" else 2e-5
+        for c, (err, _) in errs.items():
+            if c[0] == kind:
+                assert err <= tol * peak + 1e-300, (c, err, peak)
