@@ -19,6 +19,9 @@ Scenes:
   The Drude parts are used only with ``--use-metamaterials``.
 * ``vacuum`` -- eps = mu = 1 everywhere (headline benchmark).
 * ``sphere`` -- one dielectric sphere from ``--sphere-*`` options.
+* ``drude-sphere`` -- one electric Drude sphere (eps_inf = 1, omega_p =
+  sqrt(2)*2*pi*f as in the reference scene, gamma = 0) at ``--sphere-center-*``
+  with ``--sphere-radius``, in vacuum (BASELINE config 4).
 """
 
 from __future__ import annotations
@@ -54,14 +57,14 @@ class Scene:
         return x, y, z
 
     def is_vacuum(self, metamaterials: bool) -> bool:
-        if self.kind == "vacuum":
+        if self.kind == "vacuum" or (self.kind == "drude-sphere" and not metamaterials):
             return True
         if self.kind == "reference" and self.scheme != "3d" and not metamaterials:
             return True
         return False
 
     def eps(self, x, y, z, mod: float) -> torch.Tensor:
-        if self.kind == "vacuum" or (self.kind == "reference" and self.scheme != "3d"):
+        if self.kind in ("vacuum", "drude-sphere") or (self.kind == "reference" and self.scheme != "3d"):
             return torch.ones_like(x)
         if self.kind in ("reference", "sphere"):
             c = tuple(v * mod for v in self.sphere_center)
@@ -75,6 +78,11 @@ class Scene:
 
     def omega_pe(self, x, y, z, mod: float) -> torch.Tensor:
         w = SQRT2_F32 * 2 * math.pi * self.source_frequency
+        if self.kind == "drude-sphere":
+            c = tuple(v * mod for v in self.sphere_center)
+            zz = z if self.scheme == "3d" else torch.full_like(z, c[2])
+            inside = (x - c[0]) ** 2 + (y - c[1]) ** 2 + (zz - c[2]) ** 2 < (self.sphere_radius * mod) ** 2
+            return torch.where(inside, torch.full_like(x, w), torch.zeros_like(x))
         if self.kind != "reference":
             return torch.zeros_like(x)
         if self.scheme == "3d":

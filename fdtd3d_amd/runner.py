@@ -161,6 +161,10 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
         if dist is not None:
             dist.barrier()
 
+    warm = min(max(0, settings.warmupSteps), steps)
+    if warm:
+        scheme.perform_steps(warm)
+        steps -= warm
     sync()
     t0 = time.perf_counter()
     scheme.perform_steps(steps)
@@ -180,8 +184,6 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
             out.write(json.dumps({"seconds": seconds, "steps": steps, "mcells_per_s": mc,
                                   "size": list(scheme.cfg.size), "ranks": world,
                                   "backend": scheme.ops.name}) + "\n")
-    if settings.saveCmdToFile if hasattr(settings, "saveCmdToFile") else False:
-        pass
     if dist is not None:
         dist.destroy_process_group()
     return EXIT_OK

@@ -245,6 +245,12 @@ class Settings:
         if not (0.0 <= self.incidentWaveAngle1 <= 90.0 and 0.0 <= self.incidentWaveAngle2 <= 90.0):
             # reference YeeGridLayout.h:446-447 asserts theta, phi in [0, pi/2]
             raise SettingsError("--angle-teta and --angle-phi must be within [0, 90] degrees")
+        if self.scene not in ("reference", "vacuum", "sphere", "drude-sphere"):
+            raise SettingsError("--scene must be reference, vacuum, sphere or drude-sphere")
+        if self.dispersion not in ("drude", "lorentz"):
+            raise SettingsError("--dispersion must be drude or lorentz")
+        if self.sourceType not in ("sine", "gaussian"):
+            raise SettingsError("--source must be sine or gaussian")
         if self.bufferSize < 1:
             raise SettingsError("--buffer-size must be >= 1")
         for n in ("sizeX", "sizeY", "sizeZ"):
