@@ -21,9 +21,9 @@ def load_host_library(build_if_missing: bool = True) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_HOST) and build_if_missing:
+    if build_if_missing:
         from .ops import build as _b
-        _b.build(exe=False)
+        _b.build(exe=False, hip=False)  # incremental: rebuilds only when csrc changed
     lib = ctypes.CDLL(LIB_HOST)
     lib.fdtd_settings_parse_json.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                              ctypes.c_char_p, ctypes.c_int]

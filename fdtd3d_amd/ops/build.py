@@ -66,7 +66,9 @@ def host_sources() -> List[str]:
     return sorted(s for s in glob.glob(os.path.join(CSRC, "*.cpp")) if os.path.basename(s) != "main.cpp")
 
 
-def build(force: bool = False, jobs: int = 8, verbose: bool = False, exe: bool = True) -> None:
+def build(force: bool = False, jobs: int = 8, verbose: bool = False, exe: bool = True,
+          hip: bool = True) -> None:
+    """Incremental build; ``hip=False`` builds only the host library."""
     os.makedirs(BUILD_DIR, exist_ok=True)
     hdrs = _headers()
 
@@ -83,18 +85,18 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, exe: bool =
             _run(cmd)
         return o
 
-    hs = hip_sources()
+    hs = hip_sources() if hip else []
     cs = host_sources()
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         hip_objs = list(ex.map(lambda s: obj(s, True), hs))
         host_objs = list(ex.map(lambda s: obj(s, False), cs))
 
-    if force or _stale(LIB_HIP, hip_objs):
+    if hip and (force or _stale(LIB_HIP, hip_objs)):
         _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB_HIP] + hip_objs)
     if host_objs and (force or _stale(LIB_HOST, host_objs)):
         _run(["g++", "-shared", "-fPIC", "-o", LIB_HOST] + host_objs)
     main_cpp = os.path.join(CSRC, "main.cpp")
-    if exe and os.path.exists(main_cpp):
+    if hip and exe and os.path.exists(main_cpp):
         main_o = obj(main_cpp, True)
         if force or _stale(EXE, [main_o] + hip_objs + host_objs):
             _run([HIPCC, "--offload-arch=" + ARCH, "-o", EXE, main_o] + hip_objs + host_objs)
