@@ -36,6 +36,10 @@ def main(argv=None) -> int:
     ap.add_argument("--split", action="store_true", help="use the split E / H kernels instead of the fused one")
     ap.add_argument("--xchunk", type=int, default=0)
     ap.add_argument("--buffer-size", type=int, default=1, help="halo depth (deep halo when > 1)")
+    ap.add_argument("--time-block", type=int, default=1,
+                    help="leapfrog steps per HBM pass (temporally blocked kernel); decomposed runs use a "
+                         "halo of the same depth")
+    ap.add_argument("--tb-xchunk", type=int, default=0, help="x planes per workgroup of the blocked kernel")
     a = ap.parse_args(argv)
 
     import torch
@@ -61,7 +65,9 @@ def main(argv=None) -> int:
 
     size = tuple(a.size)
     cfg = SchemeConfig(scheme="3d", size=size, time_steps=a.steps, scene="vacuum", dtype=a.dtype,
-                       use_pml=False, use_tfsf=False, use_fused=not a.split)
+                       use_pml=False, use_tfsf=False, use_fused=not a.split, time_block=a.time_block)
+    if a.time_block > 1 and world > 1:
+        a.buffer_size = a.time_block
     dtype = torch.float32 if a.dtype == "f32" else torch.float64
     if world > 1:
         core = ParallelGridCore.create(size, world, "xyz")
@@ -72,6 +78,8 @@ def main(argv=None) -> int:
         domain, halo, topo = None, None, (1, 1, 1)
     kw = {"xchunk": a.xchunk} if backend == "hip" else {}
     ops = make_ops(backend, None, device, dtype, **kw)
+    if a.tb_xchunk:
+        ops.tb_xchunk = a.tb_xchunk
     scheme = YeeScheme(cfg, ops, domain, halo)
     scheme.init_scheme()
     scheme.init_grids()
@@ -82,14 +90,12 @@ def main(argv=None) -> int:
         if world > 1:
             dist.barrier()
 
-    for _ in range(a.warmup):
-        scheme.step()
+    scheme.advance(a.warmup)
     if halo is not None:
         halo.drain(scheme)
     sync()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        scheme.step()
+    scheme.advance(a.steps)
     if halo is not None:
         halo.drain(scheme)
     if device.startswith("cuda"):
@@ -125,6 +131,7 @@ def main(argv=None) -> int:
                 "seq_len": cells,
                 "parallelism": "domain-decomposition %s (dp%d-equivalent ranks)" % (par, world),
                 "backend": backend,
+                "time_block": scheme.tb,
                 "halo_bytes_per_step": (halo.bytes_sent // max(1, a.steps + a.warmup)) if halo else 0,
             },
         }

@@ -11,55 +11,11 @@
 // aligned because torch allocations are 256-byte aligned.
 
 #include "common.h"
+#include "vec4.h"
 
 namespace {
 
 constexpr int TY = 4;
-
-struct KMask {
-  // per-component bit e set when element e of the lane's 4-group is inside the box
-  unsigned m[3];
-};
-
-__device__ __forceinline__ unsigned kmask(const Box3& b, int j, int kb) {
-  if (j < b.lo[1] || j >= b.hi[1]) return 0u;
-  unsigned m = 0;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) m |= ((kb + e >= b.lo[2]) && (kb + e < b.hi[2])) ? (1u << e) : 0u;
-  return m;
-}
-
-__device__ __forceinline__ float f4(const float4& v, int e) {
-  return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
-}
-
-__device__ __forceinline__ void f4set(float4& v, int e, float s) {
-  if (e == 0) v.x = s;
-  else if (e == 1) v.y = s;
-  else if (e == 2) v.z = s;
-  else v.w = s;
-}
-
-__device__ __forceinline__ float4 ld4(const float* p, size_t off) {
-  return *reinterpret_cast<const float4*>(p + off);
-}
-
-__device__ __forceinline__ void st4(float* p, size_t off, const float4& v) {
-  *reinterpret_cast<float4*>(p + off) = v;
-}
-
-// store the elements selected by `mask` (bit e = element e); one 16-byte
-// store in the common all-inside case
-__device__ __forceinline__ void st4m(float* p, size_t off, const float4& v, unsigned mask) {
-  if (mask == 0xFu) {
-    st4(p, off, v);
-  } else if (mask) {
-    if (mask & 1u) p[off] = v.x;
-    if (mask & 2u) p[off + 1] = v.y;
-    if (mask & 4u) p[off + 2] = v.z;
-    if (mask & 8u) p[off + 3] = v.w;
-  }
-}
 
 template <bool PERCELL>
 __global__ __launch_bounds__(64 * TY) void k_update_e3d_v4(

@@ -91,6 +91,7 @@ class SchemeConfig:
     use_fused: bool = False
     cpml_kappa_max: float = 1.0
     cpml_alpha_max: float = 0.0
+    time_block: int = 1                      # fused steps per HBM pass (temporal blocking, 3D vacuum/dielectric)
 
     @classmethod
     def from_settings(cls, s) -> "SchemeConfig":
@@ -248,6 +249,14 @@ class YeeScheme:
                       and not cfg.use_amp_mode)
         if self.fused:
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+        # temporal blocking: T fused steps per pass (yee3d_tb.hip); decomposed
+        # runs exchange T-deep ghosts every T steps (buffer size == T)
+        T = max(1, int(cfg.time_block))
+        self.tb = 1
+        hip_ok = self.ops.name != "hip" or (self.dtype == torch.float32 and self.domain.shape[2] % 4 == 0)
+        if (T > 1 and self.fused and hasattr(self.ops, "tb_step") and hip_ok and T <= 4
+                and (self.halo is None or self.domain.buffer_size == T)):
+            self.tb = T
         self.initialized = True
         self.timers["init"] = time.perf_counter() - t0
 
@@ -676,11 +685,48 @@ class YeeScheme:
         if self.cfg.check_finite and self.t % max(1, self.cfg.finite_check_step) == 0:
             self.check_finite()
 
+    def advance(self, n: int) -> None:
+        """``n`` leapfrog steps, ``self.tb`` at a time through the temporally
+        blocked kernel where possible (no per-step hooks), single fused steps
+        for the remainder."""
+        T = self.tb
+        while n > 0:
+            if T > 1 and n >= T and not self.hooks and self.sub_step == 0:
+                self._tb_step(T)
+                n -= T
+            else:
+                self.step()
+                n -= 1
+
+    def _tb_step(self, T: int) -> None:
+        t = self.t
+        dom = self.domain
+        if self.halo is not None:
+            self.halo.exchange_all(self)
+        key = "_tb_boxes_cache"
+        cached = getattr(self, key, None)
+        if cached is None:
+            upd = {c: self.local_box(c, dom.allocated_global()) for c in self.comps}
+            obox = dom.to_local(dom.owned_global())
+            cached = (upd, obox)
+            setattr(self, key, cached)
+        upd, obox = cached
+        for p in range(self.planes):
+            srcs = None
+            if self.point_source is not None and self.point_source[1] is not None:
+                comp, li, _ = self.point_source
+                srcs = [(comp, li, self.source_value(t + l, p)) for l in range(T)]
+            self.ops.tb_step(self.F[p], self.F_alt[p], upd, obox, self.cb, T, srcs)
+            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
+        self.t += T
+        if self.cfg.check_finite and (self.t // max(1, self.cfg.finite_check_step)
+                                      != (self.t - T) // max(1, self.cfg.finite_check_step)):
+            self.check_finite()
+
     def perform_steps(self, n: Optional[int] = None) -> None:
         """``Scheme3D::performSteps`` (Scheme3D.cpp:3336-3385)."""
         n = self.cfg.time_steps if n is None else n
-        for _ in range(n):
-            self.step()
+        self.advance(n)
         if self.cfg.use_amp_mode:
             self.perform_amplitude_steps()
 

@@ -459,3 +459,72 @@ class HipOps:
                                    _stream())
         _check(rc, "tfsf_apply")
         self.launches += 1
+
+    # ------------------------------------------------------ temporal blocking
+    def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                obox: Box, cb: Dict[str, Coef], steps: int, sources=None) -> None:
+        """``steps`` fused leapfrog steps in one HBM pass (yee3d_tb.hip).
+
+        ``boxes`` are the update boxes (each component changes only there, at
+        every inner step), ``obox`` the cells stored to ``fout``.  The kernel
+        never reads outside the arrays whatever the boxes, but the caller must
+        give every stored cell ``steps`` valid layers of input around it.
+        ``sources`` = per-step list of (E component, local index, value) or
+        None."""
+        E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
+        if not (1 <= steps <= 4):
+            raise HipError("tb_step supports 1..4 steps per pass")
+        shape = tuple(fin["Ex"].shape)
+        if self.dtype != torch.float32 or shape[2] % 4 != 0:
+            raise HipError("tb_step needs fp32 fields with nz %% 4 == 0, got %s %s" % (self.dtype, shape))
+        for c in E + H:
+            self._check_tensor(fin[c], shape)
+            self._check_tensor(fout[c], shape)
+            if fin[c].data_ptr() == fout[c].data_ptr():
+                raise HipError("tb_step needs distinct in/out buffers")
+            b = boxes[c]
+            for d in range(3):
+                if not _empty(b) and (b[0][d] < 0 or b[1][d] > shape[d]):
+                    raise HipError("update box %s of %s outside array %s" % (b, c, shape))
+        for d in range(3):
+            if obox[0][d] < 0 or obox[1][d] > shape[d]:
+                raise HipError("output box %s outside array %s" % (obox, shape))
+        pe = [self._cell_or_none(cb[c]) for c in E]
+        ph = [self._cell_or_none(cb[c]) for c in H]
+        percell = pe[0] is not None
+        if any((p is not None) != percell for p in pe + ph):
+            raise HipError("tb_step: mixed scalar/per-cell coefficients")
+        if percell:
+            cbs = (c_vp * 3)(*[self._scaled_cell(cb[c]).data_ptr() for c in E])
+            dbs = (c_vp * 3)(*[self._scaled_cell(cb[c]).data_ptr() for c in H])
+            cbv, dbv = 1.0, 1.0
+        else:
+            cbs = (c_vp * 3)(None, None, None)
+            dbs = (c_vp * 3)(None, None, None)
+            cbv, dbv = cb["Ex"].scalar, cb["Hx"].scalar
+            if any(cb[c].scalar != cbv for c in E) or any(cb[c].scalar != dbv for c in H):
+                raise HipError("tb_step: scalar coefficients must agree per kind")
+        src = [-1, -1, -1, -1]
+        vals = [0.0] * 8
+        if sources is not None and any(s is not None for s in sources):
+            first = next(s for s in sources if s is not None)
+            comp, idx = first[0], tuple(first[1])
+            if comp not in E:
+                raise HipError("tb_step supports E point sources only")
+            for d in range(3):
+                if not (0 <= idx[d] < shape[d]):
+                    raise HipError("source index outside array")
+            for l, s in enumerate(sources):
+                if s is None or s[0] != comp or tuple(s[1]) != idx:
+                    raise HipError("tb_step: the source must be the same point at every step")
+                vals[l] = float(s[2])
+            src = [idx[0], idx[1], idx[2], E.index(comp)]
+        arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
+        rc = self.fn("tb3d_v4")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
+                                c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
+                                _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk),
+                                c_int(steps), (c_int * 4)(*src), (c_double * 8)(*vals), _stream())
+        _check(rc, "tb3d")
+        self.launches += 1
+
+    tb_xchunk = 0

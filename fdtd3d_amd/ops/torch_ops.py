@@ -42,6 +42,20 @@ def _empty(box: Box) -> bool:
     return any(box[1][d] <= box[0][d] for d in range(3))
 
 
+def box_intersect_(a: Box, b: Box) -> Box:
+    return (tuple(max(a[0][d], b[0][d]) for d in range(3)), tuple(min(a[1][d], b[1][d]) for d in range(3)))
+
+
+def cb_pad(cb: Dict[str, Coef]) -> Dict[str, Coef]:
+    """Coefficients re-indexed for fields padded by one zero layer per side."""
+    def p1(t):
+        return None if t is None else torch.nn.functional.pad(t, (1, 1))
+
+    def p3(t):
+        return None if t is None else torch.nn.functional.pad(t, (1, 1, 1, 1, 1, 1))
+    return {c: Coef(k.scalar, p1(k.px), p1(k.py), p1(k.pz), p3(k.cell)) for c, k in cb.items()}
+
+
 class TorchOps:
     name = "torch"
 
@@ -94,6 +108,31 @@ class TorchOps:
             if not _empty(b):
                 sl = box_slices(b)
                 fout[c][sl] = tmp[c][sl]
+
+    def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                obox: Box, cb: Dict[str, Coef], steps: int, sources=None) -> None:
+        """Reference semantics of the temporally blocked kernel: ``steps``
+        fused steps on the update boxes (reads outside the arrays count as
+        zero, like the kernel's unloaded rows), then only ``obox`` ∩ each
+        component's box is written to ``fout``."""
+        pad = {c: torch.nn.functional.pad(fin[c], (1, 1, 1, 1, 1, 1)) for c in fin}
+        shifted = {c: ((b[0][0] + 1, b[0][1] + 1, b[0][2] + 1), (b[1][0] + 1, b[1][1] + 1, b[1][2] + 1))
+                   for c, b in boxes.items()}
+        cur = pad
+        for l in range(steps):
+            nxt = {c: cur[c].clone() for c in cur}
+            src = None
+            if sources is not None and sources[l] is not None:
+                comp, idx, val = sources[l]
+                src = (comp, tuple(i + 1 for i in idx), val)
+            self.fused_step(cur, nxt, shifted, cb_pad(cb), src)
+            cur = nxt
+        for c, b in boxes.items():
+            ob = box_intersect_(b, obox)
+            if not _empty(ob):
+                sl = box_slices(ob)
+                sp = tuple(slice(s.start + 1, s.stop + 1) for s in sl)
+                fout[c][sl] = cur[c][sp]
 
     def curl_general(self, kind: str, comp: str, box: Box, out: torch.Tensor, inp: torch.Tensor,
                      src: Dict[str, torch.Tensor], ca: Coef, cb: Coef) -> None:
