@@ -41,15 +41,56 @@ struct TbSrc {
   float v[8];  // hard-source value applied after E update of level l
 };
 
-__device__ __forceinline__ F3 ld3(const float* a, const float* b, const float* c, size_t off) {
-  F3 r;
-  r.x = ld4(a, off);
-  r.y = ld4(b, off);
-  r.z = ld4(c, off);
-  return r;
+// Memory access through buffer descriptors: one descriptor per (array, x
+// plane) built in SGPRs from the wave-uniform plane index, plus ONE 32-bit
+// per-lane byte offset shared by every array (buffer_load ... offen).  Flat
+// 64-bit addressing would keep a per-lane pointer per array live across the
+// x loop (24 VGPRs for 12 arrays) and spill.  Offsets past the descriptor's
+// size read 0 / drop the store, which is how rows and planes outside the
+// array are handled -- no per-lane load guards.
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ __forceinline__ Rsrc plane_rsrc(const float* base, int x, int nx, size_t plane) {
+  const bool in = x >= 0 && x < nx;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)(in ? x : 0) * plane), (short)0,
+                                           in ? (int)(plane * 4) : 0, 0x00020000);
+}
+
+__device__ __forceinline__ float4 bld(Rsrc r, unsigned boff) {
+  const v4f v = __builtin_amdgcn_raw_buffer_load_b128(r, boff, 0, 0);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void bst(Rsrc r, unsigned boff, const float4& v, unsigned mask) {
+  if (mask == 0xFu) {
+    v4f t = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(t, r, boff, 0, 0);
+  } else if (mask) {
+    if (mask & 1u) __builtin_amdgcn_raw_buffer_store_b32(v.x, r, boff, 0, 0);
+    if (mask & 2u) __builtin_amdgcn_raw_buffer_store_b32(v.y, r, boff + 4, 0, 0);
+    if (mask & 4u) __builtin_amdgcn_raw_buffer_store_b32(v.z, r, boff + 8, 0, 0);
+    if (mask & 8u) __builtin_amdgcn_raw_buffer_store_b32(v.w, r, boff + 12, 0, 0);
+  }
 }
 
 __device__ __forceinline__ bool xin(const Box3& b, int x) { return x >= b.lo[0] && x < b.hi[0]; }
+
+// elements of c whose bit is set in m, zero elsewhere
+__device__ __forceinline__ float4 cmask(const float4& c, unsigned m) {
+  return make_float4((m & 1u) ? c.x : 0.f, (m & 2u) ? c.y : 0.f, (m & 4u) ? c.z : 0.f, (m & 8u) ? c.w : 0.f);
+}
+
+// v + c * ((a - b) - (d - e))
+__device__ __forceinline__ float4 upd(const float4& v, const float4& c, const float4& a, const float4& b,
+                                      const float4& d, const float4& e) {
+  return make_float4(v.x + c.x * ((a.x - b.x) - (d.x - e.x)), v.y + c.y * ((a.y - b.y) - (d.y - e.y)),
+                     v.z + c.z * ((a.z - b.z) - (d.z - e.z)), v.w + c.w * ((a.w - b.w) - (d.w - e.w)));
+}
+
+// z-1 / z+1 neighbours of a lane's 4 cells (s = the cell beyond the group)
+__device__ __forceinline__ float4 zm1(const float4& v, float s) { return make_float4(s, v.x, v.y, v.z); }
+__device__ __forceinline__ float4 zp1(const float4& v, float s) { return make_float4(v.y, v.z, v.w, s); }
 
 template <int T, bool PERCELL>
 __global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
@@ -71,7 +112,8 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
   const bool ld_ok = j >= 0 && j < ny && kb >= 0 && kb < nz;
   const bool own = ld_ok && lane >= 1 && lane <= 62 && w >= T && w < TBW - T && j >= O.lo[1] && j < O.hi[1];
   const size_t plane = (size_t)ny * nz;
-  const size_t row = ld_ok ? (size_t)j * nz + kb : 0;
+  // per-lane 32-bit offset inside a plane; plane bases are wave-uniform (SGPR)
+  const unsigned row = ld_ok ? (unsigned)(j * nz + kb) * 4u : 0xF0000000u;  // byte offset (past end: reads 0)
   // element masks of the update boxes (all rows) and of the stored cells
   const unsigned mex = ld_ok ? kmask(bex, j, kb) : 0u;
   const unsigned mey = ld_ok ? kmask(bey, j, kb) : 0u;
@@ -97,13 +139,12 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
 
   for (int X = i0 - T; X <= i1 + T - 1; ++X) {
     F3 Hc, Ec;
-    Hc.x = Hc.y = Hc.z = z4;
-    Ec = Hc;
-    if (ld_ok && X >= 0 && X < nx) {
-      const size_t off = (size_t)X * plane + row;
-      Hc = ld3(hxi, hyi, hzi, off);
-      Ec = ld3(exi, eyi, ezi, off);
-    }
+    Hc.x = bld(plane_rsrc(hxi, X, nx, plane), row);
+    Hc.y = bld(plane_rsrc(hyi, X, nx, plane), row);
+    Hc.z = bld(plane_rsrc(hzi, X, nx, plane), row);
+    Ec.x = bld(plane_rsrc(exi, X, nx, plane), row);
+    Ec.y = bld(plane_rsrc(eyi, X, nx, plane), row);
+    Ec.z = bld(plane_rsrc(ezi, X, nx, plane), row);
     F3 En;
 #pragma unroll
     for (int l = 0; l < T; ++l) {
@@ -123,34 +164,17 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
       buf ^= 1;
       const float hy_k0 = __shfl_up(Hc.y.w, 1, 64);
       const float hx_k0 = __shfl_up(Hc.x.w, 1, 64);
-      En = Ec;
-      const bool pin = pe >= 0 && pe < nx;
-      const size_t oe = (size_t)(pin ? pe : 0) * plane + row;
-      if (pin && mex && xin(bex, pe)) {
-        const float4 c4 = PERCELL ? ld4(cbx, oe) : make_float4(cb, cb, cb, cb);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (mex & (1u << q)) {
-            const float hym = q == 0 ? hy_k0 : f4(Hc.y, q - 1);
-            f4set(En.x, q, f4(En.x, q) + f4(c4, q) * ((f4(Hc.z, q) - f4(hz_j, q)) - (f4(Hc.y, q) - hym)));
-          }
-      }
-      if (pin && mey && xin(bey, pe)) {
-        const float4 c4 = PERCELL ? ld4(cby, oe) : make_float4(cb, cb, cb, cb);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (mey & (1u << q)) {
-            const float hxm = q == 0 ? hx_k0 : f4(Hc.x, q - 1);
-            f4set(En.y, q, f4(En.y, q) + f4(c4, q) * ((f4(Hc.x, q) - hxm) - (f4(Hc.z, q) - f4(Hp[l].z, q))));
-          }
-      }
-      if (pin && mez && xin(bez, pe)) {
-        const float4 c4 = PERCELL ? ld4(cbz, oe) : make_float4(cb, cb, cb, cb);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (mez & (1u << q))
-            f4set(En.z, q, f4(En.z, q) + f4(c4, q) * ((f4(Hc.y, q) - f4(Hp[l].y, q)) - (f4(Hc.x, q) - f4(hx_j, q))));
-      }
+      // coefficients are zeroed outside each component's update box, so the
+      // arithmetic is branch-free float4 work and untouched cells keep E_l
+      const float4 cex = cmask(PERCELL ? bld(plane_rsrc(cbx, xin(bex, pe) ? pe : -1, nx, plane), row) : make_float4(cb, cb, cb, cb),
+                               xin(bex, pe) ? mex : 0u);
+      En.x = upd(Ec.x, cex, Hc.z, hz_j, Hc.y, zm1(Hc.y, hy_k0));
+      const float4 cey = cmask(PERCELL ? bld(plane_rsrc(cby, xin(bey, pe) ? pe : -1, nx, plane), row) : make_float4(cb, cb, cb, cb),
+                               xin(bey, pe) ? mey : 0u);
+      En.y = upd(Ec.y, cey, Hc.x, zm1(Hc.x, hx_k0), Hc.z, Hp[l].z);
+      const float4 cez = cmask(PERCELL ? bld(plane_rsrc(cbz, xin(bez, pe) ? pe : -1, nx, plane), row) : make_float4(cb, cb, cb, cb),
+                               xin(bez, pe) ? mez : 0u);
+      En.z = upd(Ec.z, cez, Hc.y, Hp[l].y, Hc.x, hx_j);
       if (src_here && pe == src_i) {
         if (src_comp == 0) f4set(En.x, src_q, sv.v[l]);
         if (src_comp == 1) f4set(En.y, src_q, sv.v[l]);
@@ -161,55 +185,37 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
       const int ph = pe - 1;
       const float ey_k3 = __shfl_down(Ep[l].y.x, 1, 64);
       const float ex_k3 = __shfl_down(Ep[l].x.x, 1, 64);
-      F3 Hn = Hp[l];
-      const bool phin = ph >= 0 && ph < nx;
-      const size_t oh = (size_t)(phin ? ph : 0) * plane + row;
-      if (phin && mhx && xin(bhx, ph)) {
-        const float4 c4 = PERCELL ? ld4(dbx, oh) : make_float4(db, db, db, db);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (mhx & (1u << q)) {
-            const float eyk = q == 3 ? ey_k3 : f4(Ep[l].y, q + 1);
-            f4set(Hn.x, q, f4(Hn.x, q) + f4(c4, q) * ((eyk - f4(Ep[l].y, q)) - (f4(ez_jn, q) - f4(Ep[l].z, q))));
-          }
-      }
-      if (phin && mhy && xin(bhy, ph)) {
-        const float4 c4 = PERCELL ? ld4(dby, oh) : make_float4(db, db, db, db);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (mhy & (1u << q)) {
-            const float exk = q == 3 ? ex_k3 : f4(Ep[l].x, q + 1);
-            f4set(Hn.y, q, f4(Hn.y, q) + f4(c4, q) * ((f4(En.z, q) - f4(Ep[l].z, q)) - (exk - f4(Ep[l].x, q))));
-          }
-      }
-      if (phin && mhz && xin(bhz, ph)) {
-        const float4 c4 = PERCELL ? ld4(dbz, oh) : make_float4(db, db, db, db);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (mhz & (1u << q))
-            f4set(Hn.z, q, f4(Hn.z, q) + f4(c4, q) * ((f4(ex_jn, q) - f4(Ep[l].x, q)) - (f4(En.y, q) - f4(Ep[l].y, q))));
-      }
+      F3 Hn;
+      const float4 chx = cmask(PERCELL ? bld(plane_rsrc(dbx, xin(bhx, ph) ? ph : -1, nx, plane), row) : make_float4(db, db, db, db),
+                               xin(bhx, ph) ? mhx : 0u);
+      Hn.x = upd(Hp[l].x, chx, zp1(Ep[l].y, ey_k3), Ep[l].y, ez_jn, Ep[l].z);
+      const float4 chy = cmask(PERCELL ? bld(plane_rsrc(dby, xin(bhy, ph) ? ph : -1, nx, plane), row) : make_float4(db, db, db, db),
+                               xin(bhy, ph) ? mhy : 0u);
+      Hn.y = upd(Hp[l].y, chy, En.z, Ep[l].z, zp1(Ep[l].x, ex_k3), Ep[l].x);
+      const float4 chz = cmask(PERCELL ? bld(plane_rsrc(dbz, xin(bhz, ph) ? ph : -1, nx, plane), row) : make_float4(db, db, db, db),
+                               xin(bhz, ph) ? mhz : 0u);
+      Hn.z = upd(Hp[l].z, chz, ex_jn, Ep[l].x, En.y, Ep[l].y);
       // ---- rotate: next level reads E_{l+1}(X-l-1) and H_{l+1}(X-l-1)
       Ec = Ep[l];
       Ep[l] = En;
       Hp[l] = Hc;
       Hc = Hn;
     }
-    // outputs: E_T on plane X-T+1, H_T on plane X-T
+    // outputs: E_T on plane X-T+1, H_T on plane X-T.  Cells of the output box
+    // outside a component's update box are stored unchanged (PEC cells: equal
+    // in both ping-pong buffers), so only the output box masks the store.
     if (mo) {
       const int pe = X - T + 1;
       if (pe >= i0 && pe < i1) {
-        const size_t o = (size_t)pe * plane + row;
-        st4m(exo, o, En.x, xin(bex, pe) ? (mo & mex) : 0u);
-        st4m(eyo, o, En.y, xin(bey, pe) ? (mo & mey) : 0u);
-        st4m(ezo, o, En.z, xin(bez, pe) ? (mo & mez) : 0u);
+        bst(plane_rsrc(exo, pe, nx, plane), row, En.x, mo);
+        bst(plane_rsrc(eyo, pe, nx, plane), row, En.y, mo);
+        bst(plane_rsrc(ezo, pe, nx, plane), row, En.z, mo);
       }
       const int ph = X - T;
       if (ph >= i0 && ph < i1) {
-        const size_t o = (size_t)ph * plane + row;
-        st4m(hxo, o, Hc.x, xin(bhx, ph) ? (mo & mhx) : 0u);
-        st4m(hyo, o, Hc.y, xin(bhy, ph) ? (mo & mhy) : 0u);
-        st4m(hzo, o, Hc.z, xin(bhz, ph) ? (mo & mhz) : 0u);
+        bst(plane_rsrc(hxo, ph, nx, plane), row, Hc.x, mo);
+        bst(plane_rsrc(hyo, ph, nx, plane), row, Hc.y, mo);
+        bst(plane_rsrc(hzo, ph, nx, plane), row, Hc.z, mo);
       }
     }
   }
