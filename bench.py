@@ -74,8 +74,10 @@ def main(argv=None) -> int:
         a.buffer_size = a.time_block
     dtype = torch.float32 if a.dtype == "f32" else torch.float64
     if world > 1:
-        core = ParallelGridCore.create(size, world, "xyz")
-        domain = core.domain(rank, a.buffer_size)
+        # the blocked kernel tiles z in 248-cell rows, so a T-thick z shell would
+        # cost a whole tile row: decompose x and y only when blocking
+        core = ParallelGridCore.create(size, world, "xy" if a.time_block > 1 else "xyz")
+        domain = core.domain(rank, a.buffer_size, align_z=4 if a.time_block > 1 else 1)
         halo = HaloExchanger(domain)
         topo = core.topology
     else:

@@ -67,10 +67,11 @@ __device__ __forceinline__ void bst(Rsrc r, unsigned boff, const float4& v, unsi
     v4f t = {v.x, v.y, v.z, v.w};
     __builtin_amdgcn_raw_buffer_store_b128(t, r, boff, 0, 0);
   } else if (mask) {
-    if (mask & 1u) __builtin_amdgcn_raw_buffer_store_b32(v.x, r, boff, 0, 0);
-    if (mask & 2u) __builtin_amdgcn_raw_buffer_store_b32(v.y, r, boff + 4, 0, 0);
-    if (mask & 4u) __builtin_amdgcn_raw_buffer_store_b32(v.z, r, boff + 8, 0, 0);
-    if (mask & 8u) __builtin_amdgcn_raw_buffer_store_b32(v.w, r, boff + 12, 0, 0);
+    // the b32 builtin takes the raw bits (an implicit float->uint would convert)
+    if (mask & 1u) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.x), r, boff, 0, 0);
+    if (mask & 2u) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.y), r, boff + 4, 0, 0);
+    if (mask & 4u) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.z), r, boff + 8, 0, 0);
+    if (mask & 8u) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.w), r, boff + 12, 0, 0);
   }
 }
 

@@ -698,25 +698,68 @@ class YeeScheme:
                 self.step()
                 n -= 1
 
-    def _tb_step(self, T: int) -> None:
-        t = self.t
-        dom = self.domain
-        if self.halo is not None:
-            self.halo.exchange_all(self)
-        key = "_tb_boxes_cache"
+    def _tb_regions(self, T: int):
+        """(update boxes, [output boxes]) of a blocked pass, local indices.
+        Serial: one output box (the whole domain).  Decomposed: first the
+        interior (owned cells at least ``T`` from every neighbour -- needs no
+        fresh ghost), then the ``T``-thick shell slabs peeled off axis by axis
+        (disjoint), which run once the ghosts have arrived."""
+        key = "_tb_regions_cache"
         cached = getattr(self, key, None)
-        if cached is None:
-            upd = {c: self.local_box(c, dom.allocated_global()) for c in self.comps}
-            obox = dom.to_local(dom.owned_global())
-            cached = (upd, obox)
-            setattr(self, key, cached)
-        upd, obox = cached
+        if cached is not None:
+            return cached
+        dom = self.domain
+        upd = {c: self.local_box(c, dom.allocated_global()) for c in self.comps}
+        lo, hi = list(dom.lo), list(dom.hi)
+        shells = []
+        for a in range(3):
+            if dom.has_low(a):
+                slo, shi = list(lo), list(hi)
+                shi[a] = lo[a] + T
+                shells.append((tuple(slo), tuple(shi)))
+                lo[a] += T
+            if dom.has_high(a):
+                slo, shi = list(lo), list(hi)
+                slo[a] = hi[a] - T
+                shells.append((tuple(slo), tuple(shi)))
+                hi[a] -= T
+        outs = [dom.to_local((tuple(lo), tuple(hi)))] + [dom.to_local(b) for b in shells if not box_empty(b)]
+        cached = (upd, outs)
+        setattr(self, key, cached)
+        return cached
+
+    def _tb_step(self, T: int) -> None:
+        """``T`` steps in one blocked pass.  Decomposed runs overlap the
+        T-deep ghost exchange (side stream) with the interior pass and run the
+        shell slabs after it."""
+        t = self.t
+        upd, outs = self._tb_regions(T)
+        srcs = []
         for p in range(self.planes):
-            srcs = None
+            sp = None
             if self.point_source is not None and self.point_source[1] is not None:
                 comp, li, _ = self.point_source
-                srcs = [(comp, li, self.source_value(t + l, p)) for l in range(T)]
-            self.ops.tb_step(self.F[p], self.F_alt[p], upd, obox, self.cb, T, srcs)
+                sp = [(comp, li, self.source_value(t + l, p)) for l in range(T)]
+            srcs.append(sp)
+        for p in range(self.planes):
+            if not box_empty(outs[0]):
+                self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
+        if self.halo is not None:
+            side = None
+            if self.device.type == "cuda":
+                side = getattr(self, "_side_stream", None)
+                if side is None:
+                    side = torch.cuda.Stream(device=self.device)
+                    self._side_stream = side
+                # the side stream must see the previous pass's results
+                side.wait_stream(torch.cuda.current_stream(self.device))
+            self.halo.exchange_all(self, stream=side)
+            if side is not None:
+                torch.cuda.current_stream(self.device).wait_stream(side)
+            for ob in outs[1:]:
+                for p in range(self.planes):
+                    self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p])
+        for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
         self.t += T
         if self.cfg.check_finite and (self.t // max(1, self.cfg.finite_check_step)

@@ -64,6 +64,8 @@ class Domain:
     rank: int = 0
     coords: Tuple[int, int, int] = (0, 0, 0)
     topology: Tuple[int, int, int] = (1, 1, 1)
+    # extra allocated cells past the high ghosts (alignment padding, never owned)
+    pad_hi: Tuple[int, int, int] = (0, 0, 0)
 
     @classmethod
     def serial(cls, size: Sequence[int]) -> "Domain":
@@ -78,7 +80,8 @@ class Domain:
 
     @property
     def shape(self) -> Tuple[int, int, int]:
-        return tuple(self.hi[d] - self.lo[d] + self.ghost_lo[d] + self.ghost_hi[d] for d in range(3))
+        return tuple(self.hi[d] - self.lo[d] + self.ghost_lo[d] + self.ghost_hi[d] + self.pad_hi[d]
+                     for d in range(3))
 
     @property
     def owned_shape(self) -> Tuple[int, int, int]:

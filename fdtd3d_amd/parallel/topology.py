@@ -146,7 +146,11 @@ class ParallelGridCore:
     def used_procs(self) -> int:
         return self.topology[0] * self.topology[1] * self.topology[2]
 
-    def domain(self, rank: int, buffer_size: int = 1) -> Domain:
+    def domain(self, rank: int, buffer_size: int = 1, align_z: int = 1) -> Domain:
+        """Sub-domain of ``rank``.  ``align_z`` > 1 pads the local allocation at
+        the high z end so that its z extent is a multiple of ``align_z`` (the
+        float4 kernels need nz % 4 == 0); padding cells are never owned,
+        exchanged or stored."""
         topo = self.topology
         c = rank_coords(rank, topo)
         lo, hi, nbr = [], [], []
@@ -165,7 +169,11 @@ class ParallelGridCore:
                     raise ValueError("--buffer-size %d exceeds the chunk size %d along %s" % (B, core, AXIS_NAMES[a]))
         gl = tuple(B if nbr[a][0] >= 0 else 0 for a in range(3))
         gh = tuple(B if nbr[a][1] >= 0 else 0 for a in range(3))
-        return Domain(self.size, tuple(lo), tuple(hi), gl, gh, tuple(nbr), B, rank, c, topo)
+        d = Domain(self.size, tuple(lo), tuple(hi), gl, gh, tuple(nbr), B, rank, c, topo)
+        if align_z > 1:
+            nz = d.shape[2]
+            d.pad_hi = (0, 0, (-nz) % align_z)
+        return d
 
 
 # 26 halo directions (faces, edges, corners) in the reference's naming

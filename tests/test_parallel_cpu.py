@@ -40,11 +40,12 @@ def _worker(rank, world, port, cfg, topo_axes, buf, outdir):
     try:
         core = ParallelGridCore.create(cfg.size, world, topo_axes,
                                        active_axes=(0, 1, 2) if cfg.scheme == "3d" else ((0, 1) if cfg.scheme in ("tmz", "tez") else (0,)))
-        dom = core.domain(rank, buf)
+        dom = core.domain(rank, buf, align_z=4 if cfg.time_block > 1 else 1)
         halo = HaloExchanger(dom)
         s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64), dom, halo)
         s.init_scheme()
         s.init_grids()
+        assert s.tb == max(1, cfg.time_block)
         s.perform_steps()
         halo.drain(s)
         res = {}
@@ -94,6 +95,13 @@ CASES = [
                                    sphere_center=(9.5, 8.5, 10.5), use_fused=True), 8, "xyz", 1),
     ("fused-xy4-b2", SchemeConfig(scheme="3d", size=(20, 20, 12), time_steps=9, scene="vacuum", use_fused=True,
                                   complex_values=True), 4, "xy", 2),
+    # temporal blocking: T steps per pass, T-deep ghosts exchanged every T steps
+    ("tb2-xyz8", SchemeConfig(scheme="3d", size=(16, 18, 20), time_steps=9, scene="vacuum", use_fused=True,
+                              time_block=2), 8, "xyz", 2),
+    ("tb2-z2-pad", SchemeConfig(scheme="3d", size=(10, 12, 26), time_steps=6, scene="vacuum", use_fused=True,
+                                time_block=2), 2, "z", 2),
+    ("tb3-x2-sphere", SchemeConfig(scheme="3d", size=(22, 12, 16), time_steps=10, scene="sphere", sphere_radius=4,
+                                   sphere_center=(11.0, 6.0, 8.0), use_fused=True, time_block=3), 2, "x", 3),
 ]
 
 

@@ -32,11 +32,12 @@ def run_threads(cfg, world, axes, buf, device):
 
     def body(rank):
         try:
-            dom = core.domain(rank, buf)
+            dom = core.domain(rank, buf, align_z=4 if cfg.time_block > 1 else 1)
             halo = HaloExchanger(dom, comm=hub.comm(rank))
             s = YeeScheme(cfg, make_ops("hip", None, device, dt), dom, halo)
             s.init_scheme()
             s.init_grids()
+            assert s.tb == max(1, cfg.time_block)
             s.perform_steps()
             halo.drain(s)
             torch.cuda.synchronize()
@@ -71,6 +72,13 @@ CASES = [
                                         use_fused=True), 8, "xyz", 1),
     ("fused-deep-b2-yz2", SchemeConfig(scheme="3d", size=(24, 40, 48), time_steps=9, scene="vacuum", dtype="f32",
                                        use_fused=True), 2, "yz", 2),
+    # temporally blocked kernel, 2-deep ghosts every 2 steps; z split needs the
+    # alignment padding (local nz = 34 + 2)
+    ("tb2-xyz8", SchemeConfig(scheme="3d", size=(40, 36, 64), time_steps=11, scene="vacuum", dtype="f32",
+                              use_fused=True, time_block=2), 8, "xyz", 2),
+    ("tb2-z2-sphere", SchemeConfig(scheme="3d", size=(24, 30, 520), time_steps=8, scene="sphere", sphere_radius=9,
+                                   sphere_center=(12.0, 15.0, 260.0), dtype="f32", use_fused=True, time_block=2),
+     2, "z", 2),
 ]
 
 

@@ -34,6 +34,9 @@ CASES = [
     ((24, 26, 28), 3, "vacuum", ((3, 4, 4), (21, 22, 24)), True),
     ((24, 20, 264), 4, "sphere", ((4, 4, 8), (20, 16, 256)), False),
     ((30, 21, 20), 1, "vacuum", None, True),
+    # thin z shell of a decomposed rank with the source inside it
+    ((20, 20, 36), 2, "vacuum", ((0, 0, 2), (20, 20, 4)), "shell"),
+    ((20, 20, 36), 2, "vacuum", ((0, 0, 4), (20, 20, 34)), "shell"),
 ]
 
 
@@ -49,7 +52,9 @@ def test_tb_op_vs_torch(gpu, size, T, scene, obox, src):
     upd = {c: a.local_box(c) for c in a.comps}
     ob = obox if obox is not None else ((0, 0, 0), tuple(size))
     srcs = None
-    if src:
+    if src == "shell":
+        srcs = [("Ez", (10, 10, 2), 0.5 + 0.25 * l) for l in range(T)]
+    elif src:
         li = tuple(v // 2 for v in size)
         srcs = [("Ez", li, 0.5 + 0.25 * l) for l in range(T)]
     a.ops.tb_step(a.F[0], a.F_alt[0], upd, ob, a.cb, T, srcs)

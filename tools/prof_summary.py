@@ -12,6 +12,8 @@ import sys
 # algorithmic bytes per cell of each kernel family (fp32): reads + writes
 BYTES_PER_CELL = {
     "k_fused3d_v4": 48, "k_fused3d": 48,
+    # temporally blocked: one read + one write of the 6 fields per T-step pass
+    "k_tb3d_v4": 48,
     "k_update_e3d_v4": 36, "k_update_h3d_v4": 36,
     "k_update_e3d": 36, "k_update_h3d": 36,
 }
