@@ -42,7 +42,7 @@ from ..layout.yee import (E_COMPONENTS, H_COMPONENTS, MATERIAL_STENCIL, MATERIAL
                           YeeLayout)
 from ..layout.approximation import approximate_material
 from ..ops.coef import Coef
-from ..parallel.domain import Domain, box_empty, box_intersect
+from ..parallel.domain import Domain, box_empty, box_intersect, box_subtract
 from ..utils.assertions import FdtdError, fdtd_assert
 from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
 from ..utils import logging as log
@@ -361,7 +361,69 @@ class YeeScheme:
                 st["b2"] = Coef(1.0, cell=((4 - 2 * dt * g) / A).to(dtp))
                 st["ma1"] = Coef(1.0, cell=(-(2 * e0 * dt * dt * w * w - 8 * e0 * eps_c) / A).to(dtp))
                 st["ma2"] = Coef(1.0, cell=(-(4 * e0 * eps_c - 2 * dt * e0 * eps_c * g + e0 * dt * dt * w * w) / A).to(dtp))
+                st["drude_active"] = (w != 0) | (g != 0)
             self.upml[c] = st
+        self._init_chain_regions(prof)
+
+    def _bbox_global(self, mask: torch.Tensor) -> Box:
+        """Global bounding box of the True cells of a local mask (empty box
+        when none)."""
+        if mask is None or not bool(mask.any()):
+            o = self.domain.origin
+            return o, o
+        lo, hi = [], []
+        for a in range(3):
+            other = tuple(d for d in range(3) if d != a)
+            nzv = torch.nonzero(mask.any(dim=other[1]).any(dim=other[0])).flatten()
+            lo.append(int(nzv.min()))
+            hi.append(int(nzv.max()) + 1)
+        return self.domain.to_global((tuple(lo), tuple(hi)))
+
+    def _init_chain_regions(self, prof) -> None:
+        """Region-local UPML/Drude chain (3D).  Where all three sigma values
+        of a component vanish and its Drude parameters are zero the chain is
+        algebraically the plain Yee update (D' - D = (dt/dx) curl, E = D/(eps eps0)
+        and, for Drude, D1 = D/(eps eps0) exactly), so each component's box is
+        split into ``plain`` slabs (float4 Yee kernels) and ``chain`` boxes
+        (fused chain kernel): 6 PML slabs + the dispersive bounding box.  D / D1
+        are only ever read in the chain boxes, which are static."""
+        self.chain_regions = None
+        if self.cfg.scheme != "3d":
+            return
+        cfg = self.cfg
+        dom = self.domain
+        alloc = dom.allocated_global()
+        per = {}
+        for c in self.comps:
+            C = box_intersect(self._global_box(c), alloc)
+            lo, hi = list(C[0]), list(C[1])
+            for a in range(3):
+                if not (cfg.use_pml and self.layout.active(a)):
+                    continue
+                sv = self._avg_profile(c, a, prof[a]).cpu().numpy()
+                zero = np.nonzero(sv == 0.0)[0]
+                if zero.size == 0:
+                    lo[a], hi[a] = C[0][a], C[0][a]
+                    continue
+                zl, zh = int(zero.min()), int(zero.max()) + 1
+                fdtd_assert(bool((sv[zl:zh] == 0.0).all()), "sigma profile is not zero on one contiguous range")
+                lo[a] = max(lo[a], zl + dom.origin[a])
+                hi[a] = min(hi[a], zh + dom.origin[a])
+            I = box_intersect(C, (tuple(lo), tuple(hi)))
+            if box_empty(I):
+                I = (C[0], C[0])
+            Dbox = self._bbox_global(self.upml[c].get("drude_active"))
+            plain_core = I
+            plain = box_subtract(plain_core, Dbox) if not box_empty(plain_core) else [(C[0], C[0])] * 6
+            chain = box_subtract(C, plain_core) + [box_intersect(plain_core, Dbox)]
+            per[c] = (plain, chain)
+        regions = {}
+        for kind, comps in (("E", self.e_comps), ("H", self.h_comps)):
+            plain = [{c: per[c][0][n] for c in comps} for n in range(6)]
+            chain = [{c: per[c][1][n] for c in comps} for n in range(7)]
+            regions[kind] = {"plain": [r for r in plain if any(not box_empty(b) for b in r.values())],
+                             "chain": [r for r in chain if any(not box_empty(b) for b in r.values())]}
+        self.chain_regions = regions
 
     # ----------------------------------------------------------------- TF/SF
     def _init_tfsf(self) -> None:
@@ -372,13 +434,26 @@ class YeeScheme:
         self.inc_ce = self.dt / (self.rel_phase_velocity * EPS0 * self.dx)
         self.inc_ch = self.dt / (self.rel_phase_velocity * MU0 * self.dx)
         # tables on the full allocated region; each step filters by window
-        coefs = {}
-        for c in self.comps:
-            coefs[c] = self.upml[c]["cbD"] if self.use_upml_chain else self.cb[c]
         alloc = self.domain.allocated_global()
         boxes = {c: self.local_box(c, alloc) for c in self.comps}
+        # E-form tables (coefficient Cb, applied to E after a plain update) and,
+        # with the UPML chain, D-form tables (coefficient CbD, applied to D)
         self.tfsf = build_tfsf_tables(self.layout, self.comps, self.domain.origin, self.domain.shape, boxes,
-                                      coefs, self.device, self.dtype, n)
+                                      dict(self.cb), self.device, self.dtype, n)
+        self.tfsf_D = self.tfsf
+        if self.use_upml_chain:
+            self.tfsf_D = build_tfsf_tables(self.layout, self.comps, self.domain.origin, self.domain.shape, boxes,
+                                            {c: self.upml[c]["cbD"] for c in self.comps}, self.device, self.dtype, n)
+        # local bounding box of each component's TF/SF targets
+        self.tfsf_bbox = {}
+        for c in self.comps:
+            ijk = [t.ijk for t in self.tfsf[c] if t.n > 0]
+            if ijk:
+                allv = torch.cat(ijk).view(-1, 3)
+                self.tfsf_bbox[c] = (tuple(int(v) for v in allv.min(0).values),
+                                     tuple(int(v) + 1 for v in allv.max(0).values))
+            else:
+                self.tfsf_bbox[c] = None
 
     # ---------------------------------------------------------------- source
     def _init_source(self) -> None:
@@ -436,6 +511,9 @@ class YeeScheme:
         if windows is None:
             windows = [self._window(kind)]
         for w in windows:
+            if self.use_upml_chain and getattr(self, "chain_regions", None) is not None:
+                self._update_chain_regions(kind, p, w)
+                continue
             boxes = {c: self.local_box(c, w) for c in comps}
             if self.use_upml_chain:
                 for c in comps:
@@ -453,6 +531,43 @@ class YeeScheme:
             for c in comps:
                 self._upml_rotate(c, p)
 
+    def _update_chain_regions(self, kind: str, p: int, w: Box) -> None:
+        """UPML/Drude step on window ``w``: plain float4 Yee kernels on the
+        plain slabs, the fused chain kernel on the chain boxes (components whose
+        chain box holds TF/SF targets take the generic D-form path there)."""
+        comps = self.e_comps if kind == "E" else self.h_comps
+        F = self.F[p]
+        dom = self.domain
+        tfsf = self.cfg.use_tfsf
+        inc = (self.hinc[p] if kind == "E" else self.einc[p]) if tfsf else None
+        reg = self.chain_regions[kind]
+        for r in reg["plain"]:
+            boxes = {c: dom.to_local(box_intersect(r[c], w)) for c in comps}
+            if all(box_empty(b) for b in boxes.values()):
+                continue
+            self.ops.curl_update(kind, boxes, F, F, self.cb)
+            if tfsf:
+                for c in comps:
+                    for tab in self.tfsf[c]:
+                        self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
+        for r in reg["chain"]:
+            boxes = {c: dom.to_local(box_intersect(r[c], w)) for c in comps}
+            if all(box_empty(b) for b in boxes.values()):
+                continue
+            fast, slow = {}, []
+            for c in comps:
+                b = boxes[c]
+                tb = self.tfsf_bbox.get(c) if tfsf else None
+                if tb is not None and not box_empty(b) and not box_empty(box_intersect(b, tb)):
+                    slow.append(c)
+                    fast[c] = (b[0], b[0])
+                else:
+                    fast[c] = b
+            if any(not box_empty(b) for b in fast.values()):
+                self.ops.chain_update(kind, fast, F, self.upml, p, self.cfg.use_metamaterials)
+            for c in slow:
+                self._upml_region(kind, c, p, boxes[c])
+
     def _upml_region(self, kind: str, c: str, p: int, box: Box) -> None:
         F = self.F[p]
         st = self.upml[c]
@@ -462,7 +577,7 @@ class YeeScheme:
         self.ops.curl_general(kind, c, box, Dn, Dc, F, st["caD"], st["cbD"])
         if self.cfg.use_tfsf:
             inc = self.hinc[p] if kind == "E" else self.einc[p]
-            for tab in self.tfsf[c]:
+            for tab in self.tfsf_D[c]:
                 self.ops.tfsf_apply(Dn, tab, inc, box)
         if self.cfg.use_metamaterials:
             D1 = st["D1"][p]

@@ -134,6 +134,30 @@ class TorchOps:
                 sp = tuple(slice(s.start + 1, s.stop + 1) for s in sl)
                 fout[c][sl] = cur[c][sp]
 
+    def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
+                     p: int, drude: bool) -> None:
+        """Reference semantics of the fused UPML/Drude chain kernel
+        (chain_kernels.hip): D -> [D1] -> E per cell of each box."""
+        for c, box in boxes.items():
+            if _empty(box):
+                continue
+            st = upml[c]
+            sl = box_slices(box)
+            curl = self.curl(kind, c, sl, F)
+            D = st["D"][p]
+            Dn = st["caD"].materialize(sl) * D[0][sl] + st["cbD"].materialize(sl) * curl
+            D[-1][sl] = Dn
+            nw, old = Dn, D[0][sl]
+            if drude:
+                D1 = st["D1"][p]
+                D1n = (st["b0"].materialize(sl) * Dn + st["b1"].materialize(sl) * D[0][sl]
+                       + st["b2"].materialize(sl) * D[1][sl] + st["ma1"].materialize(sl) * D1[0][sl]
+                       + st["ma2"].materialize(sl) * D1[1][sl])
+                D1[2][sl] = D1n
+                nw, old = D1n, D1[0][sl]
+            F[c][sl] = (st["caE"].materialize(sl) * F[c][sl] + st["cbE"].materialize(sl) * nw
+                        + st["ccE"].materialize(sl) * old)
+
     def curl_general(self, kind: str, comp: str, box: Box, out: torch.Tensor, inp: torch.Tensor,
                      src: Dict[str, torch.Tensor], ca: Coef, cb: Coef) -> None:
         if _empty(box):

@@ -45,6 +45,28 @@ def box_volume(b: Box) -> int:
     return v
 
 
+def box_subtract(a: Box, b: Box) -> List[Box]:
+    """``a`` minus ``b`` as exactly 6 disjoint boxes (x-low, x-high, y-low,
+    y-high, z-low, z-high slabs; some may be empty).  The fixed order lets
+    callers launch the same slab of several staggered components together."""
+    out: List[Box] = []
+    lo, hi = list(a[0]), list(a[1])
+    inter = box_intersect(a, b)
+    if box_empty(inter):
+        out.append((tuple(lo), tuple(hi)))
+        empty = (tuple(lo), tuple(lo))
+        return out + [empty] * 5
+    for d in range(3):
+        slo, shi = list(lo), list(hi)
+        shi[d] = inter[0][d]
+        out.append((tuple(slo), tuple(shi)))
+        slo, shi = list(lo), list(hi)
+        slo[d] = inter[1][d]
+        out.append((tuple(slo), tuple(shi)))
+        lo[d], hi[d] = inter[0][d], inter[1][d]
+    return out
+
+
 def box_shift(b: Box, off: Sequence[int]) -> Box:
     return (tuple(b[0][d] + off[d] for d in range(3)), tuple(b[1][d] + off[d] for d in range(3)))
 
