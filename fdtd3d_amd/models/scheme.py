@@ -92,6 +92,8 @@ class SchemeConfig:
     cpml_kappa_max: float = 1.0
     cpml_alpha_max: float = 0.0
     time_block: int = 1                      # fused steps per HBM pass (temporal blocking, 3D vacuum/dielectric)
+    dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
+    lorentz_omega0_ratio: float = 0.5        # Lorentz resonance / source frequency
 
     @classmethod
     def from_settings(cls, s) -> "SchemeConfig":
@@ -118,7 +120,8 @@ class SchemeConfig:
             sphere_radius=s.sphereRadius, sphere_center=(s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ),
             source=s.sourceType, gaussian_width=s.gaussianWidth, gaussian_delay=s.gaussianDelay,
             ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
-            use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax)
+            use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
+            dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio)
 
 
 def _torch_dtype(name: str):
@@ -355,12 +358,24 @@ class YeeScheme:
                 eps_c = self.sampler.averaged(c, "eps" if c[0] == "E" else "mu")
                 w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
                 e0 = base
-                A = 4 * e0 * eps_c + 2 * dt * e0 * eps_c * g + e0 * dt * dt * w * w
-                st["b0"] = Coef(1.0, cell=((4 + 2 * dt * g) / A).to(dtp))
-                st["b1"] = Coef(1.0, cell=(-8.0 / A).to(dtp))
-                st["b2"] = Coef(1.0, cell=((4 - 2 * dt * g) / A).to(dtp))
-                st["ma1"] = Coef(1.0, cell=(-(2 * e0 * dt * dt * w * w - 8 * e0 * eps_c) / A).to(dtp))
-                st["ma2"] = Coef(1.0, cell=(-(4 * e0 * eps_c - 2 * dt * e0 * eps_c * g + e0 * dt * dt * w * w) / A).to(dtp))
+                # second-order ADE  D -> D1 (= E) of the dispersive permittivity,
+                # bilinear in the non-derivative terms (reference Drude form,
+                # Kernels.h:103-107):
+                #   drude:   eps(w) = eps - wp^2 / (w^2 + i g w)
+                #   lorentz: eps(w) = eps + wp^2 / (w0^2 - w^2 - i g w)
+                # Lorentz multiplies both sides by (w0^2 + d_t^2 + g d_t); with
+                # w0 = 0 it is exactly the Drude recurrence.
+                w0 = 0.0
+                if cfg.dispersion == "lorentz":
+                    w0 = cfg.lorentz_omega0_ratio * 2 * PI * self.source_frequency
+                q = dt * dt * w0 * w0
+                A = 4 * e0 * eps_c + 2 * dt * e0 * eps_c * g + e0 * (dt * dt * w * w + q * eps_c)
+                st["b0"] = Coef(1.0, cell=((4 + 2 * dt * g + q) / A).to(dtp))
+                st["b1"] = Coef(1.0, cell=((-8.0 + 2 * q) / A).to(dtp))
+                st["b2"] = Coef(1.0, cell=((4 - 2 * dt * g + q) / A).to(dtp))
+                st["ma1"] = Coef(1.0, cell=(-(2 * e0 * (dt * dt * w * w + q * eps_c) - 8 * e0 * eps_c) / A).to(dtp))
+                st["ma2"] = Coef(1.0, cell=(-(4 * e0 * eps_c - 2 * dt * e0 * eps_c * g
+                                              + e0 * (dt * dt * w * w + q * eps_c)) / A).to(dtp))
                 st["drude_active"] = (w != 0) | (g != 0)
             self.upml[c] = st
         self._init_chain_regions(prof)

@@ -47,3 +47,60 @@ def test_regional_chain_equals_full_chain(name):
         scale = max(float(b.F[0][o].abs().max()) for o in b.comps if o[0] == c[0]) + 1e-300
         err = float((x - y).abs().max())
         assert err <= 1e-9 * scale, (name, c, err, scale)
+
+
+def test_lorentz_regional_equals_full_chain():
+    cfg = dataclasses.replace(CASES["drude-upml"], dispersion="lorentz", lorentz_omega0_ratio=0.7)
+    a = _run(cfg, True)
+    b = _run(cfg, False)
+    for c in a.comps:
+        scale = max(float(b.F[0][o].abs().max()) for o in b.comps if o[0] == c[0]) + 1e-300
+        assert float((a.F[0][c] - b.F[0][c]).abs().max()) <= 1e-9 * scale
+
+
+def test_lorentz_zero_resonance_is_drude():
+    cfg = CASES["drude-upml"]
+    a = _run(dataclasses.replace(cfg, dispersion="lorentz", lorentz_omega0_ratio=0.0), True)
+    b = _run(cfg, True)
+    for c in a.comps:
+        assert torch.equal(a.F[0][c], b.F[0][c])
+    c = _run(dataclasses.replace(cfg, dispersion="lorentz", lorentz_omega0_ratio=0.8), True)
+    assert float((c.F[0]["Ez"] - b.F[0]["Ez"]).abs().max()) > 1e-6 * float(b.F[0]["Ez"].abs().max())
+
+
+def test_lorentz_ade_static_limit():
+    """The Lorentz recurrence driven by a constant D settles (gamma > 0) to the
+    static permittivity eps_s = eps + wp^2 / w0^2:  E -> D / (eps0 eps_s)."""
+    cfg = dataclasses.replace(CASES["drude-upml"], dispersion="lorentz", lorentz_omega0_ratio=0.3)
+    s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+    s.init_scheme()
+    s.init_grids()
+    st = s.upml["Ez"]
+    m = st["drude_active"]
+    idx = tuple(int(v) for v in torch.nonzero(m)[len(torch.nonzero(m)) // 2])
+    k = {n: float(st[n].cell[idx]) for n in ("b0", "b1", "b2", "ma1", "ma2")}
+    # recover this cell's material from the sampler
+    w, g = s.sampler.averaged_drude("Ez", electric=True)
+    eps = float(s.sampler.averaged("Ez", "eps")[idx])
+    wp, gam = float(w[idx]), float(g[idx])
+    w0 = cfg.lorentz_omega0_ratio * 2 * 3.141592653589793 * s.source_frequency
+    if gam == 0.0:
+        # undamped: add damping only for this check (same formulas)
+        gam = 0.05 / s.dt
+        dt = s.dt
+        from fdtd3d_amd.utils.constants import EPS0
+        q = dt * dt * w0 * w0
+        A = 4 * EPS0 * eps + 2 * dt * EPS0 * eps * gam + EPS0 * (dt * dt * wp * wp + q * eps)
+        k = {"b0": (4 + 2 * dt * gam + q) / A, "b1": (-8 + 2 * q) / A, "b2": (4 - 2 * dt * gam + q) / A,
+             "ma1": -(2 * EPS0 * (dt * dt * wp * wp + q * eps) - 8 * EPS0 * eps) / A,
+             "ma2": -(4 * EPS0 * eps - 2 * dt * EPS0 * eps * gam + EPS0 * (dt * dt * wp * wp + q * eps)) / A}
+    from fdtd3d_amd.utils.constants import EPS0
+    D = 1.0
+    e, e_prev = 0.0, 0.0
+    d_prev, d_cur = 0.0, 0.0
+    for _ in range(200000):
+        e_new = k["b0"] * D + k["b1"] * d_cur + k["b2"] * d_prev + k["ma1"] * e + k["ma2"] * e_prev
+        d_prev, d_cur = d_cur, D
+        e_prev, e = e, e_new
+    eps_s = eps + wp * wp / (w0 * w0)
+    assert abs(e * EPS0 * eps_s - 1.0) < 1e-6, (e * EPS0 * eps_s)
