@@ -121,7 +121,7 @@ class SchemeConfig:
             source=s.sourceType, gaussian_width=s.gaussianWidth, gaussian_delay=s.gaussianDelay,
             ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
-            dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio)
+            dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock)
 
 
 def _torch_dtype(name: str):

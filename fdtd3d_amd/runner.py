@@ -71,7 +71,11 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
                                        active_axes=active)
         if rank >= core.used_procs:
             raise SystemExit("rank %d is unused by topology %s" % (rank, core.topology))
-        domain = core.domain(rank, settings.bufferSize)
+        buf = settings.bufferSize
+        tb = max(1, settings.timeBlock)
+        if tb > 1 and cfg.scheme == "3d":
+            buf = tb  # blocked passes exchange tb-deep ghosts every tb steps
+        domain = core.domain(rank, buf, align_z=4 if tb > 1 else 1)
         halo = HaloExchanger(domain)
     scheme = YeeScheme(cfg, ops, domain, halo)
     return scheme, halo, core
@@ -101,8 +105,10 @@ def _report(settings: Settings, scheme, seconds: float, world: int, core, steps:
         out.write("Buffer size: %d\n" % settings.bufferSize)
     cells = cfg.size[0] * cfg.size[1] * cfg.size[2]
     mc = cells * steps / max(seconds, 1e-12) / 1e6
-    out.write("Backend: %s on %s, %s kernels\n" % (scheme.ops.name, scheme.device,
-                                                   "fused E+H" if getattr(scheme, "fused", False) else "split"))
+    kern = "fused E+H" if getattr(scheme, "fused", False) else "split"
+    if getattr(scheme, "tb", 1) > 1:
+        kern = "temporally blocked (%d steps per pass)" % scheme.tb
+    out.write("Backend: %s on %s, %s kernels\n" % (scheme.ops.name, scheme.device, kern))
     out.write("Throughput: %.1f Mcells/s\n" % mc)
     return mc
 
@@ -152,7 +158,11 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
                 halo.drain(s)
             save_checkpoint(s, settings.checkpointDir)
 
-    scheme.hooks.append(hook)
+    # only install the per-step hook when something is periodic: a hook-free
+    # run may advance several steps per kernel pass (--time-block)
+    if ((scheme.cfg.use_ntff and scheme.cfg.scheme == "3d") or settings.doSaveIntermediateRes
+            or (settings.checkpointDir and settings.checkpointStep > 0)):
+        scheme.hooks.append(hook)
     steps = max(0, settings.numTimeSteps - start_step)
 
     def sync():

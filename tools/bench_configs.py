@@ -27,6 +27,8 @@ CONFIGS = [
       "--dtype", "f64", "--warmup-steps", "10"]),
     ("3d-512-vacuum", "3D vacuum 512^3, point dipole, fp32",
      C512 + ["--time-steps", "200", "--scene", "vacuum"]),
+    ("3d-512-vacuum-tb2", "3D vacuum 512^3, point dipole, fp32, 2 steps per pass",
+     C512 + ["--time-steps", "200", "--scene", "vacuum", "--time-block", "2"]),
     ("3d-512-cpml-tfsf", "3D 512^3, CPML (10 cells) + TF/SF plane wave, fp32",
      C512 + ["--time-steps", "100", "--scene", "vacuum", "--use-pml", "--pml-type", "cpml", "--use-tfsf"]),
     ("3d-512-upml-tfsf", "3D 512^3, UPML (10 cells, reference D/B form) + TF/SF, fp32",
