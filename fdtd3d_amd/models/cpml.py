@@ -72,7 +72,18 @@ class CPML:
                     g = box_intersect(g, dom.allocated_global())
                     if box_empty(g):
                         continue
-                    lb = dom.to_local(g)
+                    # psi storage: the slab's range along the axis x the full
+                    # local extents of the other two (layout of yee3d_cpml.hip)
+                    lb0 = dom.to_local(g)
+                    plo, phi = [0, 0, 0], list(dom.shape)
+                    plo[axis], phi[axis] = lb0[0][axis], lb0[1][axis]
+                    if axis == 2 and dom.shape[2] % 4 == 0:
+                        # z slabs padded to whole float4 groups; the padding
+                        # cells have c = 0 and 1/kappa - 1 = 0, so their psi
+                        # stays 0 and adds nothing
+                        plo[2] = plo[2] & ~3
+                        phi[2] = min(dom.shape[2], (phi[2] + 3) & ~3)
+                    lb = (tuple(plo), tuple(phi))
                     n_loc = dom.shape[axis]
                     idx = torch.arange(n_loc, dtype=torch.float64) + dom.origin[axis] + m
                     if side == 0:
@@ -91,6 +102,44 @@ class CPML:
                     dev, dt_ = scheme.device, scheme.dtype
                     self.slabs[c].append(CPMLSlab(c, src, axis, sign, side, g, lb, bcoef.to(dev, dt_),
                                                   ccoef.to(dev, dt_), kinv.to(dev, dt_), scheme.planes, dev, dt_))
+
+    def kernel_table(self, kind: str, p: int):
+        """Term table of the fused CPML kernels (yee3d_cpml.hip) for the
+        components of ``kind`` and plane ``p``: per (component, axis) the low /
+        high psi slabs, their ranges along the axis, and one b / c / (1/kappa-1)
+        profile that selects the side's values inside each slab and the
+        identity (1, 0, 0) elsewhere."""
+        key = (kind, p)
+        cache = getattr(self, "_tables", None)
+        if cache is None:
+            cache = self._tables = {}
+        if key in cache:
+            return cache[key]
+        s = self.s
+        comps = s.e_comps if kind == "E" else s.h_comps
+        ptrs, ints, keep = [], [], []
+        for c in comps:
+            for a in range(3):
+                sl = [x for x in self.slabs[c] if x.axis == a]
+                psi = [None, None]
+                rng = [(0, 0), (0, 0)]
+                n = s.domain.shape[a]
+                b = torch.ones(n, dtype=s.dtype, device=s.device)
+                cc = torch.zeros(n, dtype=s.dtype, device=s.device)
+                kk = torch.zeros(n, dtype=s.dtype, device=s.device)
+                for x in sl:
+                    lo, hi = x.lbox[0][a], x.lbox[1][a]
+                    psi[x.side] = x.psi[p]
+                    rng[x.side] = (lo, hi)
+                    b[lo:hi] = x.b[lo:hi]
+                    cc[lo:hi] = x.c[lo:hi]
+                    kk[lo:hi] = x.kinv_m1[lo:hi]
+                keep += [b, cc, kk]
+                ptrs += [None if psi[0] is None else psi[0].data_ptr(), None if psi[1] is None else psi[1].data_ptr(),
+                         b.data_ptr(), cc.data_ptr(), kk.data_ptr()]
+                ints += [rng[0][0], rng[0][1], rng[1][0], rng[1][1]]
+        cache[key] = (ptrs, ints, keep)
+        return cache[key]
 
     def apply(self, kind: str, p: int, boxes) -> None:
         s = self.s

@@ -534,9 +534,13 @@ class YeeScheme:
                 for c in comps:
                     self._upml_region(kind, c, p, boxes[c])
                 continue
-            self.ops.curl_update(kind, boxes, F, F, self.cb)
-            if self.use_cpml:
-                self.cpml.apply(kind, p, boxes)
+            if self.use_cpml and getattr(self.ops, "fused_cpml_ok", lambda *a: False)(self):
+                # CPML folded into the update kernel (yee3d_cpml.hip)
+                self.ops.curl_update_cpml(kind, boxes, F, F, self.cb, self.cpml.kernel_table(kind, p))
+            else:
+                self.ops.curl_update(kind, boxes, F, F, self.cb)
+                if self.use_cpml:
+                    self.cpml.apply(kind, p, boxes)
             if self.cfg.use_tfsf:
                 inc = self.hinc[p] if kind == "E" else self.einc[p]
                 for c in comps:

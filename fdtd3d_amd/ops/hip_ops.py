@@ -584,3 +584,40 @@ class HipOps:
                                 c_int(shape[2]), _stream())
         _check(rc, "chain3d")
         self.launches += 1
+
+    # ------------------------------------------------------------ fused CPML
+    def fused_cpml_ok(self, scheme) -> bool:
+        return (self.vec4 and self.dtype == torch.float32 and scheme.cfg.scheme == "3d"
+                and scheme.domain.shape[2] % 4 == 0)
+
+    def curl_update_cpml(self, kind: str, boxes: Dict[str, Box], dst: Dict[str, torch.Tensor],
+                         src: Dict[str, torch.Tensor], cb: Dict[str, Coef], table) -> None:
+        """Plain 3D half step with the CPML convolution terms folded in
+        (yee3d_cpml.hip).  ``table`` = CPML.kernel_table(kind, plane)."""
+        names = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
+        other = ("Hx", "Hy", "Hz") if kind == "E" else ("Ex", "Ey", "Ez")
+        shape = tuple(dst[names[0]].shape)
+        for c in names:
+            self._check_tensor(dst[c], shape)
+            if not _empty(boxes[c]):
+                self._check_stencil_box(kind, c, boxes[c], shape)
+        for c in other:
+            self._check_tensor(src[c], shape)
+        if shape[2] % 4 != 0 or self.dtype != torch.float32:
+            raise HipError("fused CPML kernel needs fp32 and nz % 4 == 0")
+        per = [self._cell_or_none(cb[c]) for c in names]
+        if per[0] is not None:
+            per_p = [_ptr(self._scaled_cell(cb[c])) for c in names]
+            scal = 1.0
+        else:
+            per_p = [None, None, None]
+            scal = cb[names[0]].scalar
+            if any(cb[c].scalar != scal for c in names):
+                raise HipError("scalar coefficients must agree across components")
+        ptrs, ints, _keep = table
+        fn = self.fn("update_e3d_cpml_v4" if kind == "E" else "update_h3d_cpml_v4")
+        rc = fn(*[_ptr(dst[c]) for c in names], *[_ptr(src[c]) for c in other], *per_p, c_double(scal),
+                c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), _box_arr([boxes[c] for c in names]),
+                c_int(self.xchunk), (c_vp * len(ptrs))(*ptrs), (c_int * len(ints))(*ints), _stream())
+        _check(rc, "update_%s3d_cpml" % kind.lower())
+        self.launches += 1

@@ -61,6 +61,15 @@ def test_cpml_3d(gpu):
                          pml_size=(6, 6, 6), scene="vacuum", dtype="f32"), gpu, 5e-5)
 
 
+def test_cpml_fused_f32_sphere_tfsf(gpu):
+    """fp32 CPML folded into the float4 update kernels (yee3d_cpml.hip):
+    per-cell coefficients, z slabs straddling float4 lanes, kappa / alpha."""
+    compare(SchemeConfig(scheme="3d", size=(36, 40, 52), time_steps=30, use_pml=True, pml_type="cpml",
+                         use_tfsf=True, pml_size=(7, 6, 7), tfsf_size=(12, 12, 14), scene="sphere",
+                         sphere_radius=5, sphere_center=(18.5, 20.5, 26.5), dtype="f32", cpml_kappa_max=3.0,
+                         cpml_alpha_max=0.05), gpu, 5e-5)
+
+
 def test_cpml_tfsf_3d(gpu):
     compare(SchemeConfig(scheme="3d", size=(40, 40, 40), time_steps=25, use_pml=True, pml_type="cpml",
                          use_tfsf=True, pml_size=(6, 6, 6), tfsf_size=(12, 12, 12), scene="sphere",
