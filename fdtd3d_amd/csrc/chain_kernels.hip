@@ -8,42 +8,23 @@
 // runs the plain float4 kernels there and this kernel only on the chain
 // regions: one launch per region updates all three components of a kind, each
 // cell going through D -> [D1] -> E in registers (one read of every operand,
-// one write of every result; the generic path of generic_kernels.hip needs 4
-// launches and re-reads D / D1 / E between them).
+// one write of every result).
 //
-// Per component c (kind E; H is the mirror with forward differences):
+// Per component (kind E; H is the mirror with forward differences), with the
+// UPML coefficients in their factored form (profiles along the component's
+// axes aD / aCa / aCb, models/scheme.py _init_upml):
 //   curl = sg0 (s0[x] - s0[x - e_a0]) + sg1 (s1[x] - s1[x - e_a1])
-//   Dn   = caD D + cbD curl
-//   DRUDE: D1n = b0 Dn + b1 D + b2 Dp + ma1 D1 + ma2 D1p ;  (new, old) = (D1n, D1)
-//   else:                                                  (new, old) = (Dn, D)
-//   E    = caE E + cbE new + ccE old
-// Every coefficient is the factorised product of ops/coef.py (scalar x 1D
-// profiles x optional per-cell array).
+//   Dn   = caD[nD] D + cbD[nD] curl
+//   DRUDE: D1n = b0 Dn + b1 D + b2 Dp + ma1 D1 + ma2 D1p ; (new, old) = (D1n, D1)
+//   else:                                                 (new, old) = (Dn, D)
+//   E    = caE[nA] E + s cell ica[nA] (cbEa[nB] new + ccEa[nB] old)
+// Every operand is loaded before the first store, so one cell keeps ~20 loads
+// in flight (the generic Coef form, with a null check per factor, made the
+// compiler wait on each load).
 
 #include "common.h"
 
 namespace {
-
-template <typename T>
-struct CCoef {
-  T s;
-  const T* px;
-  const T* py;
-  const T* pz;
-  const T* cell;
-};
-
-template <typename T>
-__device__ __forceinline__ T cc_at(const CCoef<T>& c, int i, int j, int k, size_t off) {
-  T v = c.s;
-  if (c.px) v *= c.px[i];
-  if (c.py) v *= c.py[j];
-  if (c.pz) v *= c.pz[k];
-  if (c.cell) v *= c.cell[off];
-  return v;
-}
-
-enum { C_CAD, C_CBD, C_CAE, C_CBE, C_CCE, C_B0, C_B1, C_B2, C_MA1, C_MA2, C_N };
 
 template <typename T>
 struct ChainComp {
@@ -56,57 +37,99 @@ struct ChainComp {
   const T* D1p;
   const T* s0;
   const T* s1;
-  int a0, a1, sg0, sg1;
-  CCoef<T> c[C_N];
+  const T* caD;
+  const T* cbD;
+  const T* caE;
+  const T* ica;
+  const T* cbEa;
+  const T* ccEa;
+  const T* cell;  // per-cell 1/(eps eps0) or nullptr
+  const T* b0;
+  const T* b1;
+  const T* b2;
+  const T* ma1;
+  const T* ma2;
+  T s;
+  int a0, a1, sg0, sg1, aD, aA, aB;
   Box3 box;
 };
 
-template <typename T, bool DRUDE>
-__device__ __forceinline__ void chain_cell(const ChainComp<T>& q, int kind_e, const long long* stride, int i, int j,
-                                           int k, size_t off) {
-  if (!in_box(q.box, i, j, k)) return;
+template <typename T, bool DRUDE, bool CELL>
+__device__ __forceinline__ void chain_cell(const ChainComp<T>& q, bool kind_e, const long long* stride,
+                                           const int* n, size_t off) {
+  if (!in_box(q.box, n[0], n[1], n[2])) return;
   const long long s0 = stride[q.a0], s1 = stride[q.a1];
-  const T d0 = kind_e ? (q.s0[off] - q.s0[off - s0]) : (q.s0[off + s0] - q.s0[off]);
-  const T d1 = kind_e ? (q.s1[off] - q.s1[off - s1]) : (q.s1[off + s1] - q.s1[off]);
-  const T curl = (q.sg0 > 0 ? d0 : -d0) + (q.sg1 > 0 ? d1 : -d1);
+  // ---- every load first
+  const T x0 = q.s0[off], x1 = q.s1[off];
+  const T y0 = kind_e ? q.s0[off - s0] : q.s0[off + s0];
+  const T y1 = kind_e ? q.s1[off - s1] : q.s1[off + s1];
   const T D = q.D[off];
-  const T Dn = cc_at(q.c[C_CAD], i, j, k, off) * D + cc_at(q.c[C_CBD], i, j, k, off) * curl;
-  q.Dn[off] = Dn;
+  const T E = q.E[off];
+  const T caD = q.caD[n[q.aD]], cbD = q.cbD[n[q.aD]];
+  const T caE = q.caE[n[q.aA]], ica = q.ica[n[q.aA]];
+  const T cbEa = q.cbEa[n[q.aB]], ccEa = q.ccEa[n[q.aB]];
+  const T cell = CELL ? q.cell[off] : T(1);
+  T Dp = 0, D1 = 0, D1p = 0, b0 = 0, b1 = 0, b2 = 0, m1 = 0, m2 = 0;
+  if (DRUDE) {
+    Dp = q.Dp[off];
+    D1 = q.D1[off];
+    D1p = q.D1p[off];
+    b0 = q.b0[off];
+    b1 = q.b1[off];
+    b2 = q.b2[off];
+    m1 = q.ma1[off];
+    m2 = q.ma2[off];
+  }
+  // ---- compute
+  const T d0 = kind_e ? (x0 - y0) : (y0 - x0);
+  const T d1 = kind_e ? (x1 - y1) : (y1 - x1);
+  const T curl = (q.sg0 > 0 ? d0 : -d0) + (q.sg1 > 0 ? d1 : -d1);
+  const T Dn = caD * D + cbD * curl;
   T nw = Dn, old = D;
   if (DRUDE) {
-    const T D1 = q.D1[off];
-    const T D1n = cc_at(q.c[C_B0], i, j, k, off) * Dn + cc_at(q.c[C_B1], i, j, k, off) * D +
-                  cc_at(q.c[C_B2], i, j, k, off) * q.Dp[off] + cc_at(q.c[C_MA1], i, j, k, off) * D1 +
-                  cc_at(q.c[C_MA2], i, j, k, off) * q.D1p[off];
-    q.D1n[off] = D1n;
-    nw = D1n;
+    nw = b0 * Dn + b1 * D + b2 * Dp + m1 * D1 + m2 * D1p;
     old = D1;
   }
-  q.E[off] = cc_at(q.c[C_CAE], i, j, k, off) * q.E[off] + cc_at(q.c[C_CBE], i, j, k, off) * nw +
-             cc_at(q.c[C_CCE], i, j, k, off) * old;
+  const T En = caE * E + q.s * cell * ica * (cbEa * nw + ccEa * old);
+  // ---- stores
+  q.Dn[off] = Dn;
+  if (DRUDE) q.D1n[off] = nw;
+  q.E[off] = En;
 }
 
-template <typename T, bool DRUDE>
+// Thread mapping: the (y, z) cells of the launch box are flattened (z
+// fastest), so narrow boxes (a 10-cell z slab) still fill every lane and wide
+// rows stay coalesced; each thread walks CHX planes along x.
+constexpr int CHX = 8;
+
+template <typename T, bool DRUDE, bool CELL>
 __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q1, ChainComp<T> q2, int kind_e,
                                                  int ny, int nz, Box3 U) {
-  const int k = U.lo[2] + blockIdx.x * 64 + threadIdx.x;
-  const int j = U.lo[1] + blockIdx.y * 4 + threadIdx.y;
-  const int i = U.lo[0] + blockIdx.z;
-  if (k >= U.hi[2] || j >= U.hi[1]) return;
+  const int W = U.hi[2] - U.lo[2];
+  const int H = U.hi[1] - U.lo[1];
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)W * H) return;
+  int n[3];
+  n[1] = U.lo[1] + (int)(idx / W);
+  n[2] = U.lo[2] + (int)(idx % W);
+  const int i0 = U.lo[0] + (int)blockIdx.y * CHX;
+  const int i1 = min(i0 + CHX, U.hi[0]);
   const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
-  const size_t off = ((size_t)i * ny + j) * nz + k;
-  chain_cell<T, DRUDE>(q0, kind_e, stride, i, j, k, off);
-  chain_cell<T, DRUDE>(q1, kind_e, stride, i, j, k, off);
-  chain_cell<T, DRUDE>(q2, kind_e, stride, i, j, k, off);
+#pragma unroll 1
+  for (int i = i0; i < i1; ++i) {
+    n[0] = i;
+    const size_t off = ((size_t)i * ny + n[1]) * nz + n[2];
+    chain_cell<T, DRUDE, CELL>(q0, kind_e != 0, stride, n, off);
+    chain_cell<T, DRUDE, CELL>(q1, kind_e != 0, stride, n, off);
+    chain_cell<T, DRUDE, CELL>(q2, kind_e != 0, stride, n, off);
+  }
 }
 
-// pointer layout per component (see fdtd_chain3d_*)
-constexpr int CP_FIELDS = 9;                    // E Dn D Dp D1n D1 D1p s0 s1
-constexpr int CP_PER = CP_FIELDS + 4 * C_N;     // + (px py pz cell) per coefficient
-constexpr int CI_PER = 10;                      // a0 a1 sg0 sg1 box[6]
+constexpr int CP_PER = 21;  // pointers per component
+constexpr int CI_PER = 13;  // ints per component
 
 template <typename T>
-ChainComp<T> make_comp(const void* const* P, const double* S, const int* I) {
+ChainComp<T> make_comp(const void* const* P, double s, const int* I) {
   ChainComp<T> q;
   q.E = (T*)P[0];
   q.Dn = (T*)P[1];
@@ -117,15 +140,27 @@ ChainComp<T> make_comp(const void* const* P, const double* S, const int* I) {
   q.D1p = (const T*)P[6];
   q.s0 = (const T*)P[7];
   q.s1 = (const T*)P[8];
-  for (int n = 0; n < C_N; ++n) {
-    const void* const* p = P + CP_FIELDS + 4 * n;
-    q.c[n] = CCoef<T>{(T)S[n], (const T*)p[0], (const T*)p[1], (const T*)p[2], (const T*)p[3]};
-  }
+  q.caD = (const T*)P[9];
+  q.cbD = (const T*)P[10];
+  q.caE = (const T*)P[11];
+  q.ica = (const T*)P[12];
+  q.cbEa = (const T*)P[13];
+  q.ccEa = (const T*)P[14];
+  q.cell = (const T*)P[15];
+  q.b0 = (const T*)P[16];
+  q.b1 = (const T*)P[17];
+  q.b2 = (const T*)P[18];
+  q.ma1 = (const T*)P[19];
+  q.ma2 = (const T*)P[20];
+  q.s = (T)s;
   q.a0 = I[0];
   q.a1 = I[1];
   q.sg0 = I[2];
   q.sg1 = I[3];
-  q.box = make_box(I + 4);
+  q.aD = I[4];
+  q.aA = I[5];
+  q.aB = I[6];
+  q.box = make_box(I + 7);
   return q;
 }
 
@@ -134,25 +169,35 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
                  hipStream_t s) {
   ChainComp<T> q[3];
   Box3 U = {{0, 0, 0}, {0, 0, 0}};
+  bool cell = false;
   for (int c = 0; c < 3; ++c) {
-    q[c] = make_comp<T>(P + CP_PER * c, S + C_N * c, I + CI_PER * c);
+    q[c] = make_comp<T>(P + CP_PER * c, S[c], I + CI_PER * c);
+    if (!box_empty(q[c].box)) cell = cell || q[c].cell != nullptr;
     U = box_union(U, q[c].box);
   }
   if (box_empty(U)) return 0;
-  dim3 grid(cdiv(U.hi[2] - U.lo[2], 64), cdiv(U.hi[1] - U.lo[1], 4), (unsigned)(U.hi[0] - U.lo[0]));
-  if (drude)
-    k_chain3d<T, true><<<grid, dim3(64, 4), 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U);
-  else
-    k_chain3d<T, false><<<grid, dim3(64, 4), 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U);
+  for (int c = 0; c < 3; ++c)
+    if (!box_empty(q[c].box) && (q[c].cell != nullptr) != cell) return (int)hipErrorInvalidValue;
+  const long long cells = (long long)(U.hi[2] - U.lo[2]) * (U.hi[1] - U.lo[1]);
+  dim3 grid(cdiv(cells, 256), cdiv(U.hi[0] - U.lo[0], CHX));
+#define CH_LAUNCH(D, C) k_chain3d<T, D, C><<<grid, 256, 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U)
+  if (drude) {
+    if (cell) CH_LAUNCH(true, true);
+    else CH_LAUNCH(true, false);
+  } else {
+    if (cell) CH_LAUNCH(false, true);
+    else CH_LAUNCH(false, false);
+  }
+#undef CH_LAUNCH
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
 }  // namespace
 
 // One chain launch for the three components of a kind.  Per component c:
-// P[49c ..]: E Dn D Dp D1n D1 D1p s0 s1, then (px py pz cell) of caD cbD caE cbE
-// ccE b0 b1 b2 ma1 ma2; S[10c ..]: the coefficient scalars; I[10c ..]: curl axes
-// a0 a1, signs sg0 sg1, box lo[3] hi[3] (empty box: component skipped).
+// P[21c ..] = E Dn D Dp D1n D1 D1p s0 s1 caD cbD caE ica cbEa ccEa cell b0 b1 b2 ma1 ma2
+// (unused: nullptr), S[c] = scalar of the E-from-D term, I[13c ..] = curl axes
+// a0 a1, signs sg0 sg1, UPML axes aD aCa aCb, box lo[3] hi[3] (empty: skipped).
 FDTD_API int fdtd_chain3d_f32(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny,
                               int nz, void* s) {
   return launch_chain<float>(P, S, I, drude, kind_e, ny, nz, (hipStream_t)s);

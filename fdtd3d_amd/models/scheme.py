@@ -351,6 +351,14 @@ class YeeScheme:
                 "cbE": prof_coef(inv_mod_s, {aCb: cbE_a, aCa: inv_ca}, inv_mod),
                 "ccE": prof_coef(inv_mod_s, {aCb: ccE_a, aCa: inv_ca}, inv_mod),
             }
+            # the same coefficients in the factored form of the fused chain
+            # kernel (chain_kernels.hip): 1D profiles along aD / aCa / aCb, the
+            # scalar and the optional per-cell 1/(eps eps0) factor
+            st["prof"] = {"caD": caD.to(dtp).contiguous(), "cbD": cbD.to(dtp).contiguous(),
+                          "caE": caE.to(dtp).contiguous(), "ica": inv_ca.to(dtp).contiguous(),
+                          "cbEa": cbE_a.to(dtp).contiguous(), "ccEa": ccE_a.to(dtp).contiguous(),
+                          "s": float(inv_mod_s), "cell": None if inv_mod is None else inv_mod.to(dtp).contiguous(),
+                          "axes": (aD, aCa, aCb)}
             nlev = 3 if drude else 2
             st["D"] = [[self._zeros() for _ in range(nlev)] for _ in range(self.planes)]
             if drude:

@@ -530,20 +530,21 @@ class HipOps:
     tb_xchunk = 0
 
     # ------------------------------------------------------------ UPML chain
-    CHAIN_COEFS = ("caD", "cbD", "caE", "cbE", "ccE", "b0", "b1", "b2", "ma1", "ma2")
-
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
                      p: int, drude: bool) -> None:
-        """Fused UPML/Drude chain (chain_kernels.hip) of the components in
-        ``boxes`` (one launch).  ``upml[c]`` holds the coefficient set and the
-        D / D1 level lists of scheme._init_upml; new levels are written to
-        the last list entry."""
+        """Fused UPML/Drude chain (chain_kernels.hip) of the three components
+        of a kind (one launch).  ``upml[c]`` holds the factored coefficient
+        profiles (``prof``), the Drude cell coefficients and the D / D1 level
+        lists of scheme._init_upml; new levels go to the last list entry."""
         comps = list(boxes.keys())
+        if len(comps) != 3:
+            raise HipError("chain_update launches the three components of a kind together")
         shape = tuple(F[comps[0]].shape)
         P, S, I = [], [], []
         any_box = False
         for c in comps:
             st = upml[c]
+            pr = st["prof"]
             b = boxes[c]
             terms = self.layout.curl_terms(c)
             if len(terms) != 2:
@@ -552,33 +553,35 @@ class HipOps:
                 any_box = True
                 self._check_stencil_box(kind, c, b, shape)
             D = st["D"][p]
-            ptrs = [F[c], D[-1], D[0], D[1] if drude else None]
+            fields = [F[c], D[-1], D[0], D[1] if drude else None]
             if drude:
                 D1 = st["D1"][p]
-                ptrs += [D1[2], D1[0], D1[1]]
+                fields += [D1[2], D1[0], D1[1]]
             else:
-                ptrs += [None, None, None]
-            ptrs += [F[terms[0][0]], F[terms[1][0]]]
-            for t in ptrs:
+                fields += [None, None, None]
+            fields += [F[terms[0][0]], F[terms[1][0]]]
+            for t in fields:
                 if t is not None:
                     self._check_tensor(t, shape)
-            P += [None if t is None else t.data_ptr() for t in ptrs]
-            for name in self.CHAIN_COEFS:
-                k = st.get(name)
-                if k is None:
-                    S.append(0.0)
-                    P += [None] * 4
-                    continue
-                for t in (k.px, k.py, k.pz, k.cell):
-                    if t is not None:
-                        self._check_tensor(t)
-                S.append(float(k.scalar))
-                P += [None if t is None else t.data_ptr() for t in (k.px, k.py, k.pz, k.cell)]
-            I += [terms[0][1], terms[1][1], terms[0][2], terms[1][2]] + list(b[0]) + list(b[1])
+            aD, aA, aB = pr["axes"]
+            profs = [pr["caD"], pr["cbD"], pr["caE"], pr["ica"], pr["cbEa"], pr["ccEa"]]
+            for t, a in zip(profs, (aD, aD, aA, aA, aB, aB)):
+                self._check_tensor(t, (shape[a],))
+            cell = pr["cell"]
+            if cell is not None:
+                self._check_tensor(cell, shape)
+            dr = [None] * 5
+            if drude:
+                dr = [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")]
+                for n, t in zip(("b0", "b1", "b2", "ma1", "ma2"), dr):
+                    if st[n].scalar != 1.0 or t is None:
+                        raise HipError("Drude coefficient %s must be a plain per-cell array" % n)
+                    self._check_tensor(t, shape)
+            P += [None if t is None else t.data_ptr() for t in fields + profs + [cell] + dr]
+            S.append(float(pr["s"]))
+            I += [terms[0][1], terms[1][1], terms[0][2], terms[1][2], aD, aA, aB] + list(b[0]) + list(b[1])
         if not any_box:
             return
-        if len(comps) != 3:
-            raise HipError("chain_update launches the three components of a kind together")
         rc = self.fn("chain3d")((c_vp * len(P))(*P), (c_double * len(S))(*S), (c_int * len(I))(*I),
                                 c_int(1 if drude else 0), c_int(1 if kind == "E" else 0), c_int(shape[1]),
                                 c_int(shape[2]), _stream())
