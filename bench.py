@@ -66,6 +66,9 @@ def main(argv=None) -> int:
         device = "cuda:%d" % local
     if world > 1:
         dist.init_process_group("nccl" if device.startswith("cuda") else "gloo")
+        # establish the communicator with a collective before the first
+        # batched point-to-point exchange
+        dist.barrier()
 
     size = tuple(a.size)
     cfg = SchemeConfig(scheme="3d", size=size, time_steps=a.steps, scene="vacuum", dtype=a.dtype,

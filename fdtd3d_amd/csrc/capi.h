@@ -37,6 +37,11 @@ int fdtd_fused3d_v4_f32(const float* const* ein, const float* const* hin, float*
                         int nz, const int* boxes, int xchunk, long long src_off, int src_comp, double src_val,
                         void* s);
 
+int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
+                     const float* const* cbs, const float* const* dbs, double cb, double db, int nx, int ny, int nz,
+                     const int* boxes, const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
+                     void* stream);
+
 int fdtd_tmz_e_f32(float* ez, const float* hx, const float* hy, const float* cbz, double cb, int nx, int ny,
                    const int* box, int xchunk, void* s);
 int fdtd_tmz_h_f32(float* hx, float* hy, const float* ez, const float* dbx, const float* dby, double db, int nx,

@@ -10,6 +10,7 @@
 // asking this binary for them is an error, never a silent fallback.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -109,6 +110,17 @@ int fused(const double* const* ei, const double* const* hi, double* const* eo, d
           const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
           const int* bx, long long so, int sc, double sv, void* s, bool) {
   return fdtd_fused3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s);
+}
+// temporally blocked pass (fp32 float4 only; yee3d_tb.hip)
+int tb3d(const float* const* ei, const float* const* hi, float* const* eo, float* const* ho, const float* const* cbs,
+         const float* const* dbs, double cb, double db, int nx, int ny, int nz, const int* bx, int T,
+         const int* src, const double* vals, void* s) {
+  const int ob[6] = {0, 0, 0, nx, ny, nz};
+  return fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
+}
+int tb3d(const double* const*, const double* const*, double* const*, double* const*, const double* const*,
+         const double* const*, double, double, int, int, int, const int*, int, const int*, const double*, void*) {
+  return (int)hipErrorInvalidValue;
 }
 int setv(float* f, long long off, double v, void* s) { return fdtd_set_value_f32(f, off, v, s); }
 int setv(double* f, long long off, double v, void* s) { return fdtd_set_value_f64(f, off, v, s); }
@@ -234,12 +246,8 @@ int run(const fdtd::Settings& s) {
   auto cp = [&](Dev<T>* A, int c) -> const T* { return A[c].p; };
   (void)cp;
 
-  hipEvent_t e0, e1;
-  HIP_OK(hipEventCreate(&e0));
-  HIP_OK(hipEventCreate(&e1));
-  HIP_OK(hipEventRecord(e0, st));
-  const int steps = s.numTimeSteps;
-  for (int t = 0; t < steps; ++t) {
+  // one time step (t) through the configured kernels
+  auto step = [&](int t) {
     const double sv = src_val(t);
     if (scheme == "3d") {
       if (use_fused) {
@@ -274,7 +282,44 @@ int run(const fdtd::Settings& s) {
       K_OK(setv(F[2].p, src_off, sv, st));
       K_OK(h1d(F[4].p, F[2].p, C[4].p, percell ? 1.0 : db, boxes[24], boxes[27], st));
     }
-  }
+  };
+  // --time-block T: T steps per HBM pass through the blocked kernel
+  const int T_blk = (scheme == "3d" && use_fused && v4) ? std::max(1, std::min(4, s.timeBlock)) : 1;
+  auto advance = [&](int t0, int n) {
+    int t = t0;
+    while (n > 0) {
+      if (T_blk > 1 && n >= T_blk) {
+        const T* ei[3] = {F[0].p, F[1].p, F[2].p};
+        const T* hi[3] = {F[3].p, F[4].p, F[5].p};
+        T* eo[3] = {G[0].p, G[1].p, G[2].p};
+        T* ho[3] = {G[3].p, G[4].p, G[5].p};
+        const T* cbs[3] = {C[0].p, C[1].p, C[2].p};
+        const T* dbs[3] = {C[3].p, C[4].p, C[5].p};
+        const int src[4] = {sp[0], sp[1], sp[2], src_comp};
+        double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int l = 0; l < T_blk; ++l) vals[l] = src_val(t + l);
+        K_OK(tb3d(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, percell ? 1.0 : db, N[0], N[1], N[2], boxes, T_blk,
+                  src, vals, st));
+        for (int c = 0; c < 6; ++c) std::swap(F[c].p, G[c].p);
+        t += T_blk;
+        n -= T_blk;
+      } else {
+        step(t);
+        ++t;
+        --n;
+      }
+    }
+  };
+
+  const int steps = s.numTimeSteps;
+  const int warm = std::max(0, std::min(s.warmupSteps, steps));
+  advance(0, warm);  // untimed (they advance the simulation)
+  HIP_OK(hipStreamSynchronize(st));
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventRecord(e0, st));
+  advance(warm, steps - warm);
   HIP_OK(hipEventRecord(e1, st));
   HIP_OK(hipEventSynchronize(e1));
   HIP_OK(hipGetLastError());
@@ -290,15 +335,19 @@ int run(const fdtd::Settings& s) {
     std::printf("Grid size: %dx%d\n", N[0], N[1]);
   else
     std::printf("Grid size: %d\n", N[0]);
-  std::printf("Number of time steps: %d\n\n", steps);
+  const int timed = steps - warm;
+  std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", steps, timed, warm);
   std::printf("Value type: %s\n", Api<T>::name);
   std::printf("\n-------- Details --------\n");
   std::printf("Parallel grid: 0\n");
-  std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
-  std::printf("Throughput: %.1f Mcells/s\n", cells * (double)steps / sec / 1e6);
+  if (T_blk > 1)
+    std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", T_blk);
+  else
+    std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
+  std::printf("Throughput: %.1f Mcells/s\n", cells * (double)timed / sec / 1e6);
   if (s.doPrintJson)
-    std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f}\n", sec, steps,
-                cells * (double)steps / sec / 1e6);
+    std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f}\n", sec, timed,
+                cells * (double)timed / sec / 1e6);
 
   if (s.doSaveRes) {
     const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};

@@ -13,6 +13,8 @@ from fdtd3d_amd.runner import run as py_run
 CASES = {
     "3d_fused_vacuum": ["--3d", "--sizex", "28", "--sizey", "20", "--sizez", "24", "--time-steps", "12",
                         "--scene", "vacuum"],
+    "3d_tb2_vacuum": ["--3d", "--sizex", "28", "--sizey", "20", "--sizez", "24", "--time-steps", "13",
+                      "--scene", "vacuum", "--time-block", "2", "--warmup-steps", "3"],
     "3d_split_vacuum": ["--3d", "--sizex", "28", "--sizey", "20", "--sizez", "24", "--time-steps", "12",
                         "--scene", "vacuum", "--split-kernels"],
     "3d_fused_sphere": ["--3d", "--sizex", "32", "--same-size", "--time-steps", "15", "--scene", "sphere",
