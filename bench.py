@@ -10,10 +10,11 @@ sides; the slowest rank's time is used; rank 0 prints one JSON line.
 Scaling is *strong*: the global grid stays 1024^3 and is decomposed over the
 GPUs (2 -> 2x1x1, 4 -> 2x2x1, 8 -> 2x2x2 by the halo-surface optimiser).
 Every timed step is the full leapfrog: E and H updates of all cells, the hard
-source and (N>1) the RCCL halo exchange.  By default two leapfrog steps run
-per HBM pass (``--time-block 2``, the temporally blocked kernel
-``csrc/yee3d_tb.hip``; decomposed runs then exchange 2-deep ghosts every two
-steps); ``--time-block 1`` selects the single-pass fused kernel.  Odd step
+source and (N>1) the RCCL halo exchange.  By default four leapfrog steps run
+per HBM pass (``--time-block 4``, the temporally blocked kernel
+``csrc/yee3d_tb.hip``; decomposed runs then exchange 4-deep ghosts every four
+steps, overlapped with the interior pass); ``--time-block 1`` selects the
+single-pass fused kernel.  Odd step
 counts finish with one single-pass step, so exactly K steps are timed.  Fields start from zero plus the
 source -- the data dependence of the kernels is nil (pure streaming).
 """
@@ -40,7 +41,7 @@ def main(argv=None) -> int:
     ap.add_argument("--split", action="store_true", help="use the split E / H kernels instead of the fused one")
     ap.add_argument("--xchunk", type=int, default=0)
     ap.add_argument("--buffer-size", type=int, default=1, help="halo depth (deep halo when > 1)")
-    ap.add_argument("--time-block", type=int, default=2,
+    ap.add_argument("--time-block", type=int, default=4,
                     help="leapfrog steps per HBM pass (temporally blocked kernel); decomposed runs use a "
                          "halo of the same depth")
     ap.add_argument("--tb-xchunk", type=int, default=0, help="x planes per workgroup of the blocked kernel")

@@ -7,8 +7,9 @@
 // step, Source/Cuda/CudaInterface.cu:583-812).
 //
 // Tile (one workgroup, 16 waves = 1024 threads, one workgroup per CU):
-//   * z: a wave row of 64 lanes x float4 = 256 cells; lanes 0 and 63 are halo,
-//     lanes 1..62 (248 cells) are owned -> tiles advance by 248 cells.
+//   * z: a wave row of 64 lanes x V cells (V = 4: float4 lanes, 256 cells;
+//     V = 2 for T >= 3, halving the registers every level carries); HL =
+//     ceil(T / V) lanes at each end are halo, the rest are owned.
 //   * y: 16 rows (one per wave); T rows at each side are halo, 16-2T owned.
 //   * x: the workgroup streams planes X = i0-T .. i1+T-1 of its x chunk.
 // Level l (1..T) of iteration X computes E_l on plane X-l+1 and H_l on plane
@@ -26,15 +27,22 @@
 // updated redundantly at the inner levels but never stored.
 
 #include "common.h"
-#include "vec4.h"
 
 namespace {
 
 constexpr int TBW = 16;  // waves (y rows) per workgroup
-constexpr int TBZ = 248; // owned z cells per tile (lanes 1..62)
 
-struct F3 {
-  float4 x, y, z;
+template <int V>
+struct VT;
+template <>
+struct VT<2> {
+  typedef float f __attribute__((ext_vector_type(2)));
+  typedef unsigned u __attribute__((ext_vector_type(2)));
+};
+template <>
+struct VT<4> {
+  typedef float f __attribute__((ext_vector_type(4)));
+  typedef unsigned u __attribute__((ext_vector_type(4)));
 };
 
 struct TbSrc {
@@ -48,7 +56,6 @@ struct TbSrc {
 // x loop (24 VGPRs for 12 arrays) and spill.  Offsets past the descriptor's
 // size read 0 / drop the store, which is how rows and planes outside the
 // array are handled -- no per-lane load guards.
-typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 
 __device__ __forceinline__ Rsrc plane_rsrc(const float* base, int x, int nx, size_t plane) {
@@ -57,44 +64,74 @@ __device__ __forceinline__ Rsrc plane_rsrc(const float* base, int x, int nx, siz
                                            in ? (int)(plane * 4) : 0, 0x00020000);
 }
 
-__device__ __forceinline__ float4 bld(Rsrc r, unsigned boff) {
-  const v4f v = __builtin_amdgcn_raw_buffer_load_b128(r, boff, 0, 0);
-  return make_float4(v.x, v.y, v.z, v.w);
+template <int V>
+__device__ __forceinline__ typename VT<V>::f bld(Rsrc r, unsigned boff) {
+  if constexpr (V == 4)
+    return __builtin_bit_cast(typename VT<4>::f, __builtin_amdgcn_raw_buffer_load_b128(r, boff, 0, 0));
+  else
+    return __builtin_bit_cast(typename VT<2>::f, __builtin_amdgcn_raw_buffer_load_b64(r, boff, 0, 0));
 }
 
-__device__ __forceinline__ void bst(Rsrc r, unsigned boff, const float4& v, unsigned mask) {
-  if (mask == 0xFu) {
-    v4f t = {v.x, v.y, v.z, v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(t, r, boff, 0, 0);
+template <int V>
+__device__ __forceinline__ void bst(Rsrc r, unsigned boff, const typename VT<V>::f& v, unsigned mask) {
+  if (mask == (1u << V) - 1u) {
+    if constexpr (V == 4)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(typename VT<4>::u, v), r, boff, 0, 0);
+    else
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(typename VT<2>::u, v), r, boff, 0, 0);
   } else if (mask) {
     // the b32 builtin takes the raw bits (an implicit float->uint would convert)
-    if (mask & 1u) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.x), r, boff, 0, 0);
-    if (mask & 2u) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.y), r, boff + 4, 0, 0);
-    if (mask & 4u) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.z), r, boff + 8, 0, 0);
-    if (mask & 8u) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.w), r, boff + 12, 0, 0);
+#pragma unroll
+    for (int q = 0; q < V; ++q)
+      if (mask & (1u << q)) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), r, boff + 4 * q, 0, 0);
   }
 }
 
 __device__ __forceinline__ bool xin(const Box3& b, int x) { return x >= b.lo[0] && x < b.hi[0]; }
 
+// bit q set when element q of the lane's V-group (cells kb..kb+V-1) is in the box
+template <int V>
+__device__ __forceinline__ unsigned kmaskv(const Box3& b, int j, int kb) {
+  if (j < b.lo[1] || j >= b.hi[1]) return 0u;
+  unsigned m = 0;
+#pragma unroll
+  for (int e = 0; e < V; ++e) m |= ((kb + e >= b.lo[2]) && (kb + e < b.hi[2])) ? (1u << e) : 0u;
+  return m;
+}
+
 // elements of c whose bit is set in m, zero elsewhere
-__device__ __forceinline__ float4 cmask(const float4& c, unsigned m) {
-  return make_float4((m & 1u) ? c.x : 0.f, (m & 2u) ? c.y : 0.f, (m & 4u) ? c.z : 0.f, (m & 8u) ? c.w : 0.f);
+template <int V>
+__device__ __forceinline__ typename VT<V>::f cmask(typename VT<V>::f c, unsigned m) {
+#pragma unroll
+  for (int q = 0; q < V; ++q) c[q] = (m & (1u << q)) ? c[q] : 0.f;
+  return c;
 }
 
-// v + c * ((a - b) - (d - e))
-__device__ __forceinline__ float4 upd(const float4& v, const float4& c, const float4& a, const float4& b,
-                                      const float4& d, const float4& e) {
-  return make_float4(v.x + c.x * ((a.x - b.x) - (d.x - e.x)), v.y + c.y * ((a.y - b.y) - (d.y - e.y)),
-                     v.z + c.z * ((a.z - b.z) - (d.z - e.z)), v.w + c.w * ((a.w - b.w) - (d.w - e.w)));
+// z-1 / z+1 neighbours of a lane's V cells (s = the cell beyond the group)
+template <int V>
+__device__ __forceinline__ typename VT<V>::f zm1(const typename VT<V>::f& v, float s) {
+  typename VT<V>::f r;
+  r[0] = s;
+#pragma unroll
+  for (int q = 1; q < V; ++q) r[q] = v[q - 1];
+  return r;
+}
+template <int V>
+__device__ __forceinline__ typename VT<V>::f zp1(const typename VT<V>::f& v, float s) {
+  typename VT<V>::f r;
+#pragma unroll
+  for (int q = 0; q < V - 1; ++q) r[q] = v[q + 1];
+  r[V - 1] = s;
+  return r;
 }
 
-// z-1 / z+1 neighbours of a lane's 4 cells (s = the cell beyond the group)
-__device__ __forceinline__ float4 zm1(const float4& v, float s) { return make_float4(s, v.x, v.y, v.z); }
-__device__ __forceinline__ float4 zp1(const float4& v, float s) { return make_float4(v.y, v.z, v.w, s); }
+template <int V>
+struct F3 {
+  typename VT<V>::f x, y, z;
+};
 
-template <int T, bool PERCELL>
-__global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
+template <int T, int V, bool PERCELL>
+__global__ __launch_bounds__(64 * TBW) void k_tb3d(
     const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
     const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
     float* __restrict__ exo, float* __restrict__ eyo, float* __restrict__ ezo,
@@ -103,50 +140,84 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
     const float* __restrict__ dbx, const float* __restrict__ dby, const float* __restrict__ dbz, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv) {
-  __shared__ float4 sX[2][4][TBW][64];  // [buffer][field][row][lane]: 128 KiB
+  typedef typename VT<V>::f vec;
+  constexpr bool PF = V == 2;            // software prefetch of the next plane
+  constexpr int HL = (T + V - 1) / V;    // halo lanes per side
+  constexpr int TBZ = (64 - 2 * HL) * V; // owned z cells per tile
+  __shared__ vec sX[2][4][TBW][64];      // [buffer][field][row][lane]
   const int lane = threadIdx.x;
   const int w = threadIdx.y;
-  const int kb = (O.lo[2] & ~3) - 4 + TBZ * (int)blockIdx.x + 4 * lane;
+  const int kb = (O.lo[2] & ~(V - 1)) - HL * V + TBZ * (int)blockIdx.x + V * lane;
   const int j = O.lo[1] - T + (TBW - 2 * T) * (int)blockIdx.y + w;
   const int i0 = O.lo[0] + (int)blockIdx.z * xchunk;
   const int i1 = min(i0 + xchunk, O.hi[0]);
   const bool ld_ok = j >= 0 && j < ny && kb >= 0 && kb < nz;
-  const bool own = ld_ok && lane >= 1 && lane <= 62 && w >= T && w < TBW - T && j >= O.lo[1] && j < O.hi[1];
+  const bool own = ld_ok && lane >= HL && lane < 64 - HL && w >= T && w < TBW - T && j >= O.lo[1] && j < O.hi[1];
   const size_t plane = (size_t)ny * nz;
   // per-lane 32-bit offset inside a plane; plane bases are wave-uniform (SGPR)
   const unsigned row = ld_ok ? (unsigned)(j * nz + kb) * 4u : 0xF0000000u;  // byte offset (past end: reads 0)
   // element masks of the update boxes (all rows) and of the stored cells
-  const unsigned mex = ld_ok ? kmask(bex, j, kb) : 0u;
-  const unsigned mey = ld_ok ? kmask(bey, j, kb) : 0u;
-  const unsigned mez = ld_ok ? kmask(bez, j, kb) : 0u;
-  const unsigned mhx = ld_ok ? kmask(bhx, j, kb) : 0u;
-  const unsigned mhy = ld_ok ? kmask(bhy, j, kb) : 0u;
-  const unsigned mhz = ld_ok ? kmask(bhz, j, kb) : 0u;
-  const unsigned mo = own ? kmask(O, j, kb) : 0u;
-  const bool src_here = src_comp >= 0 && j == src_j && src_k >= kb && src_k < kb + 4;
+  const unsigned mex = ld_ok ? kmaskv<V>(bex, j, kb) : 0u;
+  const unsigned mey = ld_ok ? kmaskv<V>(bey, j, kb) : 0u;
+  const unsigned mez = ld_ok ? kmaskv<V>(bez, j, kb) : 0u;
+  const unsigned mhx = ld_ok ? kmaskv<V>(bhx, j, kb) : 0u;
+  const unsigned mhy = ld_ok ? kmaskv<V>(bhy, j, kb) : 0u;
+  const unsigned mhz = ld_ok ? kmaskv<V>(bhz, j, kb) : 0u;
+  const unsigned mo = own ? kmaskv<V>(O, j, kb) : 0u;
+  const bool src_here = src_comp >= 0 && j == src_j && src_k >= kb && src_k < kb + V;
   const int src_q = src_k - kb;
   const int rdn = w > 0 ? w - 1 : 0;
   const int rup = w < TBW - 1 ? w + 1 : TBW - 1;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const vec zero = (vec)(0.f);
+  const vec cbv = (vec)(cb), dbv = (vec)(db);
+  // float2 lanes: scalar coefficients masked by the (loop-invariant) y/z box
+  // masks once, per plane only the x-range test remains (a wave-uniform
+  // select); float4 lanes have no registers to spare and mask per plane
+  constexpr bool PREMASK = V == 2 && !PERCELL;
+  const vec mcex = PREMASK ? cmask<V>(cbv, mex) : zero, mcey = PREMASK ? cmask<V>(cbv, mey) : zero;
+  const vec mcez = PREMASK ? cmask<V>(cbv, mez) : zero, mchx = PREMASK ? cmask<V>(dbv, mhx) : zero;
+  const vec mchy = PREMASK ? cmask<V>(dbv, mhy) : zero, mchz = PREMASK ? cmask<V>(dbv, mhz) : zero;
+  // coefficient of one component on plane p: per-cell plane (PERCELL) or the
+  // scalar, zeroed outside the component's update box
+  auto coef = [&](const float* arr, const Box3& b, int p, unsigned m, const vec& pre, const vec& sc) -> vec {
+    const bool in = xin(b, p);
+    if (PERCELL) return cmask<V>(bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), row), in ? m : 0u);
+    if (PREMASK) return in ? pre : zero;
+    return cmask<V>(sc, in ? m : 0u);
+  };
 
   // carried state (see header): Hp[l] = H_l(X-1-l), Ep[l] = E_{l+1}(X-1-l)
-  F3 Hp[T], Ep[T];
+  F3<V> Hp[T], Ep[T];
 #pragma unroll
   for (int l = 0; l < T; ++l) {
-    Hp[l].x = Hp[l].y = Hp[l].z = z4;
-    Ep[l].x = Ep[l].y = Ep[l].z = z4;
+    Hp[l].x = Hp[l].y = Hp[l].z = zero;
+    Ep[l].x = Ep[l].y = Ep[l].z = zero;
   }
   int buf = 0;
 
+  // plane X's six fields; with PF the next plane is loaded before this one's
+  // levels run, so its HBM latency hides under the compute and barriers
+  // (float2 lanes have the registers for it)
+  auto load_plane = [&](int X, F3<V>& H, F3<V>& E) {
+    H.x = bld<V>(plane_rsrc(hxi, X, nx, plane), row);
+    H.y = bld<V>(plane_rsrc(hyi, X, nx, plane), row);
+    H.z = bld<V>(plane_rsrc(hzi, X, nx, plane), row);
+    E.x = bld<V>(plane_rsrc(exi, X, nx, plane), row);
+    E.y = bld<V>(plane_rsrc(eyi, X, nx, plane), row);
+    E.z = bld<V>(plane_rsrc(ezi, X, nx, plane), row);
+  };
+  F3<V> Hnx, Enx;
+  if (PF) load_plane(i0 - T, Hnx, Enx);
   for (int X = i0 - T; X <= i1 + T - 1; ++X) {
-    F3 Hc, Ec;
-    Hc.x = bld(plane_rsrc(hxi, X, nx, plane), row);
-    Hc.y = bld(plane_rsrc(hyi, X, nx, plane), row);
-    Hc.z = bld(plane_rsrc(hzi, X, nx, plane), row);
-    Ec.x = bld(plane_rsrc(exi, X, nx, plane), row);
-    Ec.y = bld(plane_rsrc(eyi, X, nx, plane), row);
-    Ec.z = bld(plane_rsrc(ezi, X, nx, plane), row);
-    F3 En;
+    F3<V> Hc, Ec;
+    if (PF) {
+      Hc = Hnx;
+      Ec = Enx;
+      load_plane(X + 1, Hnx, Enx);
+    } else {
+      load_plane(X, Hc, Ec);
+    }
+    F3<V> En;
 #pragma unroll
     for (int l = 0; l < T; ++l) {
       // ---- E_{l+1} on plane pe from H_l(pe) = Hc, H_l(pe-1) = Hp[l], E_l(pe) = Ec
@@ -158,44 +229,38 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
       sX[buf][2][w][lane] = Ep[l].x;
       sX[buf][3][w][lane] = Ep[l].z;
       __syncthreads();
-      const float4 hz_j = sX[buf][0][rdn][lane];
-      const float4 hx_j = sX[buf][1][rdn][lane];
-      const float4 ex_jn = sX[buf][2][rup][lane];
-      const float4 ez_jn = sX[buf][3][rup][lane];
+      const vec hz_j = sX[buf][0][rdn][lane];
+      const vec hx_j = sX[buf][1][rdn][lane];
+      const vec ex_jn = sX[buf][2][rup][lane];
+      const vec ez_jn = sX[buf][3][rup][lane];
       buf ^= 1;
-      const float hy_k0 = __shfl_up(Hc.y.w, 1, 64);
-      const float hx_k0 = __shfl_up(Hc.x.w, 1, 64);
+      const float hy_k0 = __shfl_up(Hc.y[V - 1], 1, 64);
+      const float hx_k0 = __shfl_up(Hc.x[V - 1], 1, 64);
       // coefficients are zeroed outside each component's update box, so the
-      // arithmetic is branch-free float4 work and untouched cells keep E_l
-      const float4 cex = cmask(PERCELL ? bld(plane_rsrc(cbx, xin(bex, pe) ? pe : -1, nx, plane), row) : make_float4(cb, cb, cb, cb),
-                               xin(bex, pe) ? mex : 0u);
-      En.x = upd(Ec.x, cex, Hc.z, hz_j, Hc.y, zm1(Hc.y, hy_k0));
-      const float4 cey = cmask(PERCELL ? bld(plane_rsrc(cby, xin(bey, pe) ? pe : -1, nx, plane), row) : make_float4(cb, cb, cb, cb),
-                               xin(bey, pe) ? mey : 0u);
-      En.y = upd(Ec.y, cey, Hc.x, zm1(Hc.x, hx_k0), Hc.z, Hp[l].z);
-      const float4 cez = cmask(PERCELL ? bld(plane_rsrc(cbz, xin(bez, pe) ? pe : -1, nx, plane), row) : make_float4(cb, cb, cb, cb),
-                               xin(bez, pe) ? mez : 0u);
-      En.z = upd(Ec.z, cez, Hc.y, Hp[l].y, Hc.x, hx_j);
+      // arithmetic is branch-free vector work and untouched cells keep E_l
+      const vec cex = coef(cbx, bex, pe, mex, mcex, cbv);
+      En.x = Ec.x + cex * ((Hc.z - hz_j) - (Hc.y - zm1<V>(Hc.y, hy_k0)));
+      const vec cey = coef(cby, bey, pe, mey, mcey, cbv);
+      En.y = Ec.y + cey * ((Hc.x - zm1<V>(Hc.x, hx_k0)) - (Hc.z - Hp[l].z));
+      const vec cez = coef(cbz, bez, pe, mez, mcez, cbv);
+      En.z = Ec.z + cez * ((Hc.y - Hp[l].y) - (Hc.x - hx_j));
       if (src_here && pe == src_i) {
-        if (src_comp == 0) f4set(En.x, src_q, sv.v[l]);
-        if (src_comp == 1) f4set(En.y, src_q, sv.v[l]);
-        if (src_comp == 2) f4set(En.z, src_q, sv.v[l]);
+        if (src_comp == 0) En.x[src_q] = sv.v[l];
+        if (src_comp == 1) En.y[src_q] = sv.v[l];
+        if (src_comp == 2) En.z[src_q] = sv.v[l];
       }
       // ---- H_{l+1} on plane ph = pe-1 from E_{l+1}(ph) = Ep[l], E_{l+1}(pe) = En,
       //      H_l(ph) = Hp[l]
       const int ph = pe - 1;
-      const float ey_k3 = __shfl_down(Ep[l].y.x, 1, 64);
-      const float ex_k3 = __shfl_down(Ep[l].x.x, 1, 64);
-      F3 Hn;
-      const float4 chx = cmask(PERCELL ? bld(plane_rsrc(dbx, xin(bhx, ph) ? ph : -1, nx, plane), row) : make_float4(db, db, db, db),
-                               xin(bhx, ph) ? mhx : 0u);
-      Hn.x = upd(Hp[l].x, chx, zp1(Ep[l].y, ey_k3), Ep[l].y, ez_jn, Ep[l].z);
-      const float4 chy = cmask(PERCELL ? bld(plane_rsrc(dby, xin(bhy, ph) ? ph : -1, nx, plane), row) : make_float4(db, db, db, db),
-                               xin(bhy, ph) ? mhy : 0u);
-      Hn.y = upd(Hp[l].y, chy, En.z, Ep[l].z, zp1(Ep[l].x, ex_k3), Ep[l].x);
-      const float4 chz = cmask(PERCELL ? bld(plane_rsrc(dbz, xin(bhz, ph) ? ph : -1, nx, plane), row) : make_float4(db, db, db, db),
-                               xin(bhz, ph) ? mhz : 0u);
-      Hn.z = upd(Hp[l].z, chz, ex_jn, Ep[l].x, En.y, Ep[l].y);
+      const float ey_k3 = __shfl_down(Ep[l].y[0], 1, 64);
+      const float ex_k3 = __shfl_down(Ep[l].x[0], 1, 64);
+      F3<V> Hn;
+      const vec chx = coef(dbx, bhx, ph, mhx, mchx, dbv);
+      Hn.x = Hp[l].x + chx * ((zp1<V>(Ep[l].y, ey_k3) - Ep[l].y) - (ez_jn - Ep[l].z));
+      const vec chy = coef(dby, bhy, ph, mhy, mchy, dbv);
+      Hn.y = Hp[l].y + chy * ((En.z - Ep[l].z) - (zp1<V>(Ep[l].x, ex_k3) - Ep[l].x));
+      const vec chz = coef(dbz, bhz, ph, mhz, mchz, dbv);
+      Hn.z = Hp[l].z + chz * ((ex_jn - Ep[l].x) - (En.y - Ep[l].y));
       // ---- rotate: next level reads E_{l+1}(X-l-1) and H_{l+1}(X-l-1)
       Ec = Ep[l];
       Ep[l] = En;
@@ -208,34 +273,50 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_v4(
     if (mo) {
       const int pe = X - T + 1;
       if (pe >= i0 && pe < i1) {
-        bst(plane_rsrc(exo, pe, nx, plane), row, En.x, mo);
-        bst(plane_rsrc(eyo, pe, nx, plane), row, En.y, mo);
-        bst(plane_rsrc(ezo, pe, nx, plane), row, En.z, mo);
+        bst<V>(plane_rsrc(exo, pe, nx, plane), row, En.x, mo);
+        bst<V>(plane_rsrc(eyo, pe, nx, plane), row, En.y, mo);
+        bst<V>(plane_rsrc(ezo, pe, nx, plane), row, En.z, mo);
       }
       const int ph = X - T;
       if (ph >= i0 && ph < i1) {
-        bst(plane_rsrc(hxo, ph, nx, plane), row, Hc.x, mo);
-        bst(plane_rsrc(hyo, ph, nx, plane), row, Hc.y, mo);
-        bst(plane_rsrc(hzo, ph, nx, plane), row, Hc.z, mo);
+        bst<V>(plane_rsrc(hxo, ph, nx, plane), row, Hc.x, mo);
+        bst<V>(plane_rsrc(hyo, ph, nx, plane), row, Hc.y, mo);
+        bst<V>(plane_rsrc(hzo, ph, nx, plane), row, Hc.z, mo);
       }
     }
   }
 }
 
-template <int T, bool PERCELL>
+template <int T, int V, bool PERCELL>
 int launch_tb(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
               const float* const* cbs, const float* const* dbs, float cb, float db, int nx, int ny, int nz,
               const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv, hipStream_t s) {
-  dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~3), TBZ), cdiv(O.hi[1] - O.lo[1], TBW - 2 * T),
+  constexpr int HL = (T + V - 1) / V;
+  constexpr int TBZ = (64 - 2 * HL) * V;
+  dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], TBW - 2 * T),
             cdiv(O.hi[0] - O.lo[0], xchunk));
-  k_tb3d_v4<T, PERCELL><<<grid, dim3(64, TBW), 0, s>>>(
+  k_tb3d<T, V, PERCELL><<<grid, dim3(64, TBW), 0, s>>>(
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2],
       cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], O,
       xchunk, src[0], src[1], src[2], src[3], sv);
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
+template <int T, int V>
+int launch_tb_pc(bool pc, const float* const* ein, const float* const* hin, float* const* eout,
+                 float* const* hout, const float* const* cbs, const float* const* dbs, float cb, float db, int nx,
+                 int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
+                 hipStream_t s) {
+  return pc ? launch_tb<T, V, true>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s)
+            : launch_tb<T, V, false>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s);
+}
+
+int g_tb_vec = 0;  // 0: automatic (float4 lanes for T <= 2, float2 above), else 2 / 4
+
 }  // namespace
+
+// lane width of the blocked kernel (tuning / tests): 0 = automatic, 2, 4
+FDTD_API void fdtd_set_tb_vec(int v) { g_tb_vec = (v == 2 || v == 4) ? v : 0; }
 
 // T fused leapfrog steps: reads ein/hin, writes eout/hout (distinct buffers)
 // on the output box `obox` (lo[3], hi[3]).  `boxes` = 6 update boxes
@@ -250,17 +331,19 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const Box3 O = make_box(obox);
   if (box_empty(O)) return 0;
-  if (xchunk <= 0) xchunk = 64;
+  if (xchunk <= 0) xchunk = steps <= 2 ? 64 : 256;  // measured at 1024^3 (tools/gpu_tb.sh)
   TbSrc sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
   hipStream_t s = (hipStream_t)stream;
   const bool pc = cbs[0] != nullptr;
-#define TB_CASE(TT)                                                                                              \
-  case TT:                                                                                                       \
-    return pc ? launch_tb<TT, true>(ein, hin, eout, hout, cbs, dbs, (float)cb, (float)db, nx, ny, nz, b, O,     \
-                                    xchunk, src, sv, s)                                                          \
-              : launch_tb<TT, false>(ein, hin, eout, hout, cbs, dbs, (float)cb, (float)db, nx, ny, nz, b, O,    \
-                                     xchunk, src, sv, s);
+  const int V = g_tb_vec ? g_tb_vec : (steps <= 2 ? 4 : 2);
+  const float fcb = (float)cb, fdb = (float)db;
+#define TB_CASE(TT)                                                                                          \
+  case TT:                                                                                                   \
+    return V == 4 ? launch_tb_pc<TT, 4>(pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, \
+                                        src, sv, s)                                                          \
+                  : launch_tb_pc<TT, 2>(pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, \
+                                        src, sv, s);
   switch (steps) {
     TB_CASE(1)
     TB_CASE(2)

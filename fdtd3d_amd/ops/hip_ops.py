@@ -520,6 +520,7 @@ class HipOps:
                 vals[l] = float(s[2])
             src = [idx[0], idx[1], idx[2], E.index(comp)]
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
+        self.lib.fdtd_set_tb_vec(c_int(self.tb_vec))
         rc = self.fn("tb3d_v4")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
                                 c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk),
@@ -528,6 +529,7 @@ class HipOps:
         self.launches += 1
 
     tb_xchunk = 0
+    tb_vec = 0  # lane width of the blocked kernel: 0 auto (4 for T <= 2, 2 above), 2 or 4
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],

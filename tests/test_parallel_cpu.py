@@ -100,6 +100,8 @@ CASES = [
                               time_block=2), 8, "xyz", 2),
     ("tb2-z2-pad", SchemeConfig(scheme="3d", size=(10, 12, 26), time_steps=6, scene="vacuum", use_fused=True,
                                 time_block=2), 2, "z", 2),
+    ("tb4-xy4", SchemeConfig(scheme="3d", size=(20, 22, 16), time_steps=11, scene="vacuum", use_fused=True,
+                             time_block=4), 4, "xy", 4),
     ("tb3-x2-sphere", SchemeConfig(scheme="3d", size=(22, 12, 16), time_steps=10, scene="sphere", sphere_radius=4,
                                    sphere_center=(11.0, 6.0, 8.0), use_fused=True, time_block=3), 2, "x", 3),
 ]

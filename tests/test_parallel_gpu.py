@@ -76,6 +76,8 @@ CASES = [
     # alignment padding (local nz = 34 + 2)
     ("tb2-xyz8", SchemeConfig(scheme="3d", size=(40, 36, 64), time_steps=11, scene="vacuum", dtype="f32",
                               use_fused=True, time_block=2), 8, "xyz", 2),
+    ("tb4-xy4", SchemeConfig(scheme="3d", size=(44, 40, 256), time_steps=13, scene="vacuum", dtype="f32",
+                             use_fused=True, time_block=4), 4, "xy", 4),
     ("tb2-z2-sphere", SchemeConfig(scheme="3d", size=(24, 30, 520), time_steps=8, scene="sphere", sphere_radius=9,
                                    sphere_center=(12.0, 15.0, 260.0), dtype="f32", use_fused=True, time_block=2),
      2, "z", 2),

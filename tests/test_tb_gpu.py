@@ -40,12 +40,14 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("vec", [0, 2, 4])
 @pytest.mark.parametrize("size,T,scene,obox,src", CASES)
-def test_tb_op_vs_torch(gpu, size, T, scene, obox, src):
+def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec):
     cfg = SchemeConfig(scheme="3d", size=size, scene=scene, sphere_radius=min(size) / 3.0,
                        sphere_center=tuple(v / 2.0 for v in size), dtype="f32", use_fused=True)
     a = _scheme(cfg, "hip", gpu, torch.float32)
     a.ops.tb_xchunk = 16
+    a.ops.tb_vec = vec
     b = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
     _randomize(a)
     _randomize(b)
@@ -67,13 +69,14 @@ def test_tb_op_vs_torch(gpu, size, T, scene, obox, src):
         assert err <= 2e-5 * (float(y.abs().max()) + 1.0), (c, err)
 
 
-def test_tb_scheme_matches_fused(gpu):
-    """Scheme-level: time_block=2 over 11 steps == 11 single fused steps."""
+@pytest.mark.parametrize("T", [2, 3, 4])
+def test_tb_scheme_matches_fused(gpu, T):
+    """Scheme-level: time_block=T over 11 steps == 11 single fused steps."""
     cfg = SchemeConfig(scheme="3d", size=(48, 40, 300), scene="vacuum", dtype="f32", use_fused=True,
                        time_steps=11)
-    a = _scheme(dataclasses.replace(cfg, time_block=2), "hip", gpu, torch.float32)
+    a = _scheme(dataclasses.replace(cfg, time_block=T), "hip", gpu, torch.float32)
     b = _scheme(cfg, "hip", gpu, torch.float32)
-    assert a.tb == 2
+    assert a.tb == T
     a.perform_steps()
     b.perform_steps()
     torch.cuda.synchronize()
