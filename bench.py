@@ -45,6 +45,9 @@ def main(argv=None) -> int:
                     help="leapfrog steps per HBM pass (temporally blocked kernel); decomposed runs use a "
                          "halo of the same depth")
     ap.add_argument("--tb-xchunk", type=int, default=0, help="x planes per workgroup of the blocked kernel")
+    ap.add_argument("--tb-vec", type=int, default=0, help="lane width of the blocked kernel (0 auto, 2, 4)")
+    ap.add_argument("--tb-rows", type=int, default=0, help="grid rows per wave of the blocked kernel (0 auto, 1, 2)")
+    ap.add_argument("--tb-xcd", type=int, default=0, help="XCD-aware tile order of the blocked kernel (1 on, 0 off)")
     a = ap.parse_args(argv)
 
     import torch
@@ -90,6 +93,8 @@ def main(argv=None) -> int:
     ops = make_ops(backend, None, device, dtype, **kw)
     if a.tb_xchunk:
         ops.tb_xchunk = a.tb_xchunk
+    if backend == "hip":
+        ops.tb_vec, ops.tb_rows, ops.tb_xcd = a.tb_vec, a.tb_rows, a.tb_xcd
     scheme = YeeScheme(cfg, ops, domain, halo)
     scheme.init_scheme()
     scheme.init_grids()

@@ -130,7 +130,7 @@ struct F3 {
   typename VT<V>::f x, y, z;
 };
 
-template <int T, int V, bool PERCELL>
+template <int T, int V, int R, bool PERCELL>
 __global__ __launch_bounds__(64 * TBW) void k_tb3d(
     const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
     const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
@@ -139,20 +139,38 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
     const float* __restrict__ cbx, const float* __restrict__ cby, const float* __restrict__ cbz,
     const float* __restrict__ dbx, const float* __restrict__ dby, const float* __restrict__ dbz, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
-    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv) {
+    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz) {
   typedef typename VT<V>::f vec;
   constexpr bool PF = V == 2;            // software prefetch of the next plane
+  constexpr int LW = 64 / R;             // lanes per grid row (R rows per wave)
+  constexpr int ROWS = TBW * R;          // y rows per workgroup
   constexpr int HL = (T + V - 1) / V;    // halo lanes per side
-  constexpr int TBZ = (64 - 2 * HL) * V; // owned z cells per tile
-  __shared__ vec sX[2][4][TBW][64];      // [buffer][field][row][lane]
-  const int lane = threadIdx.x;
-  const int w = threadIdx.y;
-  const int kb = (O.lo[2] & ~(V - 1)) - HL * V + TBZ * (int)blockIdx.x + V * lane;
-  const int j = O.lo[1] - T + (TBW - 2 * T) * (int)blockIdx.y + w;
-  const int i0 = O.lo[0] + (int)blockIdx.z * xchunk;
+  constexpr int TBZ = (LW - 2 * HL) * V; // owned z cells per tile
+  __shared__ vec sX[2][4][ROWS][LW];     // [buffer][field][row][lane]
+  const int lane = threadIdx.x % LW;     // z position inside the row
+  const int w = threadIdx.y * R + threadIdx.x / LW;  // row inside the workgroup
+  // tile of this workgroup.  XCD-aware order (cdna_hip_programming.md 5.5 T1):
+  // workgroups are dealt round-robin to the 8 XCDs, so remap the dispatch
+  // index so that each XCD gets a contiguous run of tiles, y fastest -- tiles
+  // adjacent in y then stream the same x planes at the same time on one L2
+  // and the 2T halo rows they share are L2 hits instead of HBM re-reads.
+  int tz = blockIdx.x, ty = blockIdx.y, tx = blockIdx.z;
+  if (xcd_swz) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy * (int)gridDim.z;
+    const int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int n8 = n & ~7;
+    const int q = p < n8 ? (p & 7) * (n8 >> 3) + (p >> 3) : p;
+    ty = q % gy;
+    tz = (q / gy) % gx;
+    tx = q / (gy * gx);
+  }
+  const int kb = (O.lo[2] & ~(V - 1)) - HL * V + TBZ * tz + V * lane;
+  const int j = O.lo[1] - T + (ROWS - 2 * T) * ty + w;
+  const int i0 = O.lo[0] + tx * xchunk;
   const int i1 = min(i0 + xchunk, O.hi[0]);
   const bool ld_ok = j >= 0 && j < ny && kb >= 0 && kb < nz;
-  const bool own = ld_ok && lane >= HL && lane < 64 - HL && w >= T && w < TBW - T && j >= O.lo[1] && j < O.hi[1];
+  const bool own = ld_ok && lane >= HL && lane < LW - HL && w >= T && w < ROWS - T && j >= O.lo[1] && j < O.hi[1];
   const size_t plane = (size_t)ny * nz;
   // per-lane 32-bit offset inside a plane; plane bases are wave-uniform (SGPR)
   const unsigned row = ld_ok ? (unsigned)(j * nz + kb) * 4u : 0xF0000000u;  // byte offset (past end: reads 0)
@@ -167,7 +185,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
   const bool src_here = src_comp >= 0 && j == src_j && src_k >= kb && src_k < kb + V;
   const int src_q = src_k - kb;
   const int rdn = w > 0 ? w - 1 : 0;
-  const int rup = w < TBW - 1 ? w + 1 : TBW - 1;
+  const int rup = w < ROWS - 1 ? w + 1 : ROWS - 1;
   const vec zero = (vec)(0.f);
   const vec cbv = (vec)(cb), dbv = (vec)(db);
   // float2 lanes: scalar coefficients masked by the (loop-invariant) y/z box
@@ -234,8 +252,8 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
       const vec ex_jn = sX[buf][2][rup][lane];
       const vec ez_jn = sX[buf][3][rup][lane];
       buf ^= 1;
-      const float hy_k0 = __shfl_up(Hc.y[V - 1], 1, 64);
-      const float hx_k0 = __shfl_up(Hc.x[V - 1], 1, 64);
+      const float hy_k0 = __shfl_up(Hc.y[V - 1], 1, LW);
+      const float hx_k0 = __shfl_up(Hc.x[V - 1], 1, LW);
       // coefficients are zeroed outside each component's update box, so the
       // arithmetic is branch-free vector work and untouched cells keep E_l
       const vec cex = coef(cbx, bex, pe, mex, mcex, cbv);
@@ -252,8 +270,8 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
       // ---- H_{l+1} on plane ph = pe-1 from E_{l+1}(ph) = Ep[l], E_{l+1}(pe) = En,
       //      H_l(ph) = Hp[l]
       const int ph = pe - 1;
-      const float ey_k3 = __shfl_down(Ep[l].y[0], 1, 64);
-      const float ex_k3 = __shfl_down(Ep[l].x[0], 1, 64);
+      const float ey_k3 = __shfl_down(Ep[l].y[0], 1, LW);
+      const float ex_k3 = __shfl_down(Ep[l].x[0], 1, LW);
       F3<V> Hn;
       const vec chx = coef(dbx, bhx, ph, mhx, mchx, dbv);
       Hn.x = Hp[l].x + chx * ((zp1<V>(Ep[l].y, ey_k3) - Ep[l].y) - (ez_jn - Ep[l].z));
@@ -287,36 +305,45 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
   }
 }
 
-template <int T, int V, bool PERCELL>
+int g_tb_vec = 0;   // 0: automatic (float4 lanes for T <= 2, float2 above), else 2 / 4
+int g_tb_rows = 0;  // rows per wave: 0 automatic (1), 1 / 2
+int g_tb_xcd = 0;   // XCD-aware tile order (measured: no gain, T=2 slower; off by default)
+
+template <int T, int V, int R, bool PERCELL>
 int launch_tb(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
               const float* const* cbs, const float* const* dbs, float cb, float db, int nx, int ny, int nz,
               const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv, hipStream_t s) {
   constexpr int HL = (T + V - 1) / V;
-  constexpr int TBZ = (64 - 2 * HL) * V;
-  dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], TBW - 2 * T),
+  constexpr int TBZ = (64 / R - 2 * HL) * V;
+  dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * T),
             cdiv(O.hi[0] - O.lo[0], xchunk));
-  k_tb3d<T, V, PERCELL><<<grid, dim3(64, TBW), 0, s>>>(
+  k_tb3d<T, V, R, PERCELL><<<grid, dim3(64, TBW), 0, s>>>(
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2],
       cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], O,
-      xchunk, src[0], src[1], src[2], src[3], sv);
+      xchunk, src[0], src[1], src[2], src[3], sv, g_tb_xcd);
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
-template <int T, int V>
+template <int T, int V, int R>
 int launch_tb_pc(bool pc, const float* const* ein, const float* const* hin, float* const* eout,
                  float* const* hout, const float* const* cbs, const float* const* dbs, float cb, float db, int nx,
                  int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
                  hipStream_t s) {
-  return pc ? launch_tb<T, V, true>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s)
-            : launch_tb<T, V, false>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s);
+  return pc ? launch_tb<T, V, R, true>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s)
+            : launch_tb<T, V, R, false>(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv,
+                                        s);
 }
 
-int g_tb_vec = 0;  // 0: automatic (float4 lanes for T <= 2, float2 above), else 2 / 4
 
 }  // namespace
 
 // lane width of the blocked kernel (tuning / tests): 0 = automatic, 2, 4
 FDTD_API void fdtd_set_tb_vec(int v) { g_tb_vec = (v == 2 || v == 4) ? v : 0; }
+// rows per wave of the blocked kernel: 0 = automatic, 1, 2 (2 rows of 32 lanes:
+// a 32-row tile, halving the y-halo re-reads of float2 lanes)
+FDTD_API void fdtd_set_tb_rows(int r) { g_tb_rows = (r == 1 || r == 2) ? r : 0; }
+// XCD-aware tile order of the blocked kernel (1 = on, default)
+FDTD_API void fdtd_set_tb_xcd(int on) { g_tb_xcd = on ? 1 : 0; }
 
 // T fused leapfrog steps: reads ein/hin, writes eout/hout (distinct buffers)
 // on the output box `obox` (lo[3], hi[3]).  `boxes` = 6 update boxes
@@ -338,12 +365,12 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   const bool pc = cbs[0] != nullptr;
   const int V = g_tb_vec ? g_tb_vec : (steps <= 2 ? 4 : 2);
   const float fcb = (float)cb, fdb = (float)db;
-#define TB_CASE(TT)                                                                                          \
-  case TT:                                                                                                   \
-    return V == 4 ? launch_tb_pc<TT, 4>(pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, \
-                                        src, sv, s)                                                          \
-                  : launch_tb_pc<TT, 2>(pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, \
-                                        src, sv, s);
+  const int R = g_tb_rows ? g_tb_rows : 1;  // 2 rows per wave measured slower (228k vs 245k, T=4)
+#define TB_ARGS pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, src, sv, s
+#define TB_CASE(TT)                                                                     \
+  case TT:                                                                              \
+    if (V == 4) return R == 2 ? launch_tb_pc<TT, 4, 2>(TB_ARGS) : launch_tb_pc<TT, 4, 1>(TB_ARGS); \
+    return R == 2 ? launch_tb_pc<TT, 2, 2>(TB_ARGS) : launch_tb_pc<TT, 2, 1>(TB_ARGS);
   switch (steps) {
     TB_CASE(1)
     TB_CASE(2)
@@ -351,5 +378,6 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
     TB_CASE(4)
   }
 #undef TB_CASE
+#undef TB_ARGS
   return (int)hipErrorInvalidValue;
 }

@@ -521,6 +521,8 @@ class HipOps:
             src = [idx[0], idx[1], idx[2], E.index(comp)]
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
         self.lib.fdtd_set_tb_vec(c_int(self.tb_vec))
+        self.lib.fdtd_set_tb_rows(c_int(self.tb_rows))
+        self.lib.fdtd_set_tb_xcd(c_int(self.tb_xcd))
         rc = self.fn("tb3d_v4")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
                                 c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk),
@@ -530,6 +532,8 @@ class HipOps:
 
     tb_xchunk = 0
     tb_vec = 0  # lane width of the blocked kernel: 0 auto (4 for T <= 2, 2 above), 2 or 4
+    tb_rows = 0  # grid rows per wave: 0 auto (1), 1 or 2
+    tb_xcd = 0  # XCD-aware tile order (off: measured no gain)
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],

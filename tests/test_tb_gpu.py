@@ -40,14 +40,16 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("vec", [0, 2, 4])
+@pytest.mark.parametrize("vec,rows,xcd", [(0, 0, 1), (0, 0, 0), (2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 0)])
 @pytest.mark.parametrize("size,T,scene,obox,src", CASES)
-def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec):
+def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec, rows, xcd):
     cfg = SchemeConfig(scheme="3d", size=size, scene=scene, sphere_radius=min(size) / 3.0,
                        sphere_center=tuple(v / 2.0 for v in size), dtype="f32", use_fused=True)
     a = _scheme(cfg, "hip", gpu, torch.float32)
     a.ops.tb_xchunk = 16
     a.ops.tb_vec = vec
+    a.ops.tb_rows = rows
+    a.ops.tb_xcd = xcd
     b = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
     _randomize(a)
     _randomize(b)
