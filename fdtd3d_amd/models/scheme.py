@@ -92,6 +92,7 @@ class SchemeConfig:
     cpml_kappa_max: float = 1.0
     cpml_alpha_max: float = 0.0
     time_block: int = 1                      # fused steps per HBM pass (temporal blocking, 3D vacuum/dielectric)
+    profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
     lorentz_omega0_ratio: float = 0.5        # Lorentz resonance / source frequency
 
@@ -121,7 +122,8 @@ class SchemeConfig:
             source=s.sourceType, gaussian_width=s.gaussianWidth, gaussian_delay=s.gaussianDelay,
             ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
-            dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock)
+            dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
+            profile_phases=s.doProfilePhases)
 
 
 def _torch_dtype(name: str):
@@ -162,6 +164,8 @@ class YeeScheme:
         self.timers: Dict[str, float] = {}
         self.hooks: List[Callable[["YeeScheme", int], None]] = []
         self.initialized = False
+        from ..utils.profiler import PhaseProfiler
+        self.prof = PhaseProfiler(self.device, cfg.profile_phases)
 
     # ================================================================ init
     def init_scheme(self, dx: Optional[float] = None, source_frequency: Optional[float] = None) -> None:
@@ -693,24 +697,34 @@ class YeeScheme:
             return
         deep = halo is not None and B > 1
         if deep and self.sub_step == 0:
-            halo.exchange_all(self)
+            with self.prof.phase("halo-deep"):
+                halo.exchange_all(self)
+        ph = self.prof.phase
         for p in range(self.planes):
             if cfg.use_tfsf:
-                self.ops.inc_step_e(self.einc[p], self.hinc[p], self.inc_ce, self.source_value(t, p))
+                with ph("incident-E"):
+                    self.ops.inc_step_e(self.einc[p], self.hinc[p], self.inc_ce, self.source_value(t, p))
+            with ph("E"):
+                if halo is not None and not deep:
+                    halo.finish_and_update(self, "E", p)
+                else:
+                    self._update("E", p)
+            with ph("source"):
+                self._apply_sources(t, p)
             if halo is not None and not deep:
-                halo.finish_and_update(self, "E", p)
-            else:
-                self._update("E", p)
-            self._apply_sources(t, p)
-            if halo is not None and not deep:
-                halo.start(self, "E", p)
+                with ph("halo-post"):
+                    halo.start(self, "E", p)
             if cfg.use_tfsf:
-                self.ops.inc_step_h(self.einc[p], self.hinc[p], self.inc_ch)
+                with ph("incident-H"):
+                    self.ops.inc_step_h(self.einc[p], self.hinc[p], self.inc_ch)
+            with ph("H"):
+                if halo is not None and not deep:
+                    halo.finish_and_update(self, "H", p)
+                else:
+                    self._update("H", p)
             if halo is not None and not deep:
-                halo.finish_and_update(self, "H", p)
-                halo.start(self, "H", p)
-            else:
-                self._update("H", p)
+                with ph("halo-post"):
+                    halo.start(self, "H", p)
         self.t += 1
         if deep:
             self.sub_step = (self.sub_step + 1) % B
@@ -728,7 +742,8 @@ class YeeScheme:
             self._fused_step_overlap(t)
             return
         if self.halo is not None and self.sub_step == 0:
-            self.halo.exchange_all(self)
+            with self.prof.phase("halo-deep"):
+                self.halo.exchange_all(self)
         wE = self.domain.window_fused("E", self.sub_step)
         wH = self.domain.window_fused("H", self.sub_step)
         boxes = {c: self.local_box(c, wE) for c in self.e_comps}
@@ -738,7 +753,8 @@ class YeeScheme:
             if self.point_source is not None and self.point_source[1] is not None:
                 comp, li, _ = self.point_source
                 src = (comp, li, self.source_value(t, p))
-            self.ops.fused_step(self.F[p], self.F_alt[p], boxes, self.cb, src)
+            with self.prof.phase("fused-E+H"):
+                self.ops.fused_step(self.F[p], self.F_alt[p], boxes, self.cb, src)
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
         self.t += 1
         if self.halo is not None:
@@ -885,7 +901,8 @@ class YeeScheme:
             srcs.append(sp)
         for p in range(self.planes):
             if not box_empty(outs[0]):
-                self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
+                with self.prof.phase("blocked-interior" if self.halo is not None else "blocked"):
+                    self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
         if self.halo is not None:
             side = None
             if self.device.type == "cuda":
@@ -895,12 +912,19 @@ class YeeScheme:
                     self._side_stream = side
                 # the side stream must see the previous pass's results
                 side.wait_stream(torch.cuda.current_stream(self.device))
-            self.halo.exchange_all(self, stream=side)
+            if side is not None and self.prof.enabled:
+                with torch.cuda.stream(side):
+                    with self.prof.phase("halo-overlapped"):
+                        self.halo.exchange_all(self)
+            else:
+                with self.prof.phase("halo-overlapped"):
+                    self.halo.exchange_all(self, stream=side)
             if side is not None:
                 torch.cuda.current_stream(self.device).wait_stream(side)
-            for ob in outs[1:]:
-                for p in range(self.planes):
-                    self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p])
+            with self.prof.phase("blocked-shells"):
+                for ob in outs[1:]:
+                    for p in range(self.planes):
+                        self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p])
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
         self.t += T

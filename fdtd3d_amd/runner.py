@@ -176,6 +176,7 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
         scheme.perform_steps(warm)
         steps -= warm
     sync()
+    scheme.prof.reset()  # phase timings cover the timed steps only
     t0 = time.perf_counter()
     scheme.perform_steps(steps)
     if halo is not None:
@@ -188,12 +189,17 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
         dump_fields(scheme, settings, scheme.t, "scattered-", scattered=True)
     if settings.checkpointDir:
         save_checkpoint(scheme, settings.checkpointDir)
+    phases = scheme.prof.summary() if scheme.prof.enabled else None
     if rank == 0:
         mc = _report(settings, scheme, seconds, world, core, steps, out)
+        if phases:
+            out.write(scheme.prof.report() + "\n")
         if settings.doPrintJson:
-            out.write(json.dumps({"seconds": seconds, "steps": steps, "mcells_per_s": mc,
-                                  "size": list(scheme.cfg.size), "ranks": world,
-                                  "backend": scheme.ops.name}) + "\n")
+            rec = {"seconds": seconds, "steps": steps, "mcells_per_s": mc, "size": list(scheme.cfg.size),
+                   "ranks": world, "backend": scheme.ops.name}
+            if phases:
+                rec["phases"] = phases
+            out.write(json.dumps(rec) + "\n")
     if dist is not None:
         dist.destroy_process_group()
     return EXIT_OK

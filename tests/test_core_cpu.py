@@ -317,3 +317,17 @@ def test_driver_end_to_end(tmp_path):
     rc = run(["--2d", "--2d-mode", "tez", "--sizex", "40", "--same-size", "--time-steps", "10"], out=io.StringIO())
     assert rc == 0
     assert run(["--help"], out=io.StringIO()) == 0
+
+
+def test_phase_profiler_report():
+    import io
+    from fdtd3d_amd.runner import run
+    out = io.StringIO()
+    assert run(["--3d", "--sizex", "16", "--same-size", "--time-steps", "4", "--use-pml", "--pml-sizex", "3",
+                "--same-size-pml", "--profile-phases", "--backend", "torch", "--device", "cpu", "--json"],
+               out=out) == 0
+    text = out.getvalue()
+    assert "Phase timings" in text
+    import json
+    rec = json.loads([l for l in text.splitlines() if l.startswith("{")][-1])
+    assert rec["phases"]["E"]["calls"] == 4 and rec["phases"]["H"]["calls"] == 4
