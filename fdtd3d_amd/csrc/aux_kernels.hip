@@ -23,6 +23,19 @@ __global__ void k_set_values(T* __restrict__ f, const long long* __restrict__ of
   if (t < n) f[offs[t]] = (T)v;
 }
 
+// Graph-replayable source: the value comes from a device table indexed by a
+// device step counter (+ the step's position inside the captured sequence),
+// so one captured HIP graph of G steps can be replayed for any G steps.
+template <typename T>
+__global__ void k_set_value_tab(T* __restrict__ f, long long off, const double* __restrict__ tab,
+                                const int* __restrict__ counter, int lag) {
+  if (threadIdx.x == 0) f[off] = (T)tab[*counter + lag];
+}
+
+__global__ void k_counter_add(int* counter, int n) {
+  if (threadIdx.x == 0) *counter += n;
+}
+
 // ---------------------------------------------------------------- halo boxes
 // Copy a strided box of `ncomp` fields into a packed buffer (pack) or back
 // (unpack).  One thread per element; the z run of each box row is contiguous
@@ -139,6 +152,11 @@ inline unsigned reduce_grid(long long n) {
     k_set_value<T><<<1, 64, 0, (hipStream_t)s>>>(f, off, v);                                                   \
     FDTD_RETURN_LAUNCH_STATUS();                                                                              \
   }                                                                                                           \
+  FDTD_API int fdtd_set_value_tab_##SUF(T* f, long long off, const double* tab, const int* counter, int lag,   \
+                                       void* s) {                                                             \
+    k_set_value_tab<T><<<1, 64, 0, (hipStream_t)s>>>(f, off, tab, counter, lag);                               \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
   FDTD_API int fdtd_set_values_##SUF(T* f, const long long* offs, int n, double v, void* s) {                 \
     if (n <= 0) return 0;                                                                                     \
     k_set_values<T><<<cdiv(n, 256), 256, 0, (hipStream_t)s>>>(f, offs, n, v);                                  \
@@ -182,5 +200,10 @@ inline unsigned reduce_grid(long long n) {
 
 FDTD_AUX_API(f32, float)
 FDTD_AUX_API(f64, double)
+
+FDTD_API int fdtd_counter_add(int* counter, int n, void* s) {
+  k_counter_add<<<1, 64, 0, (hipStream_t)s>>>(counter, n);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
 
 FDTD_API int fdtd_abi_version() { return 1; }

@@ -115,6 +115,19 @@ __global__ void k_inc_e(T* __restrict__ einc, const T* __restrict__ hinc, int n,
     einc[i] += c * (hinc[i - 1] - hinc[i]);
 }
 
+// graph-replayable variant: the source value from a device table (see
+// k_set_value_tab in aux_kernels.hip)
+template <typename T>
+__global__ void k_inc_e_tab(T* __restrict__ einc, const T* __restrict__ hinc, int n, T c,
+                            const double* __restrict__ tab, const int* __restrict__ counter, int lag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (i == 0)
+    einc[0] = (T)tab[*counter + lag];
+  else
+    einc[i] += c * (hinc[i - 1] - hinc[i]);
+}
+
 template <typename T>
 __global__ void k_inc_h(const T* __restrict__ einc, T* __restrict__ hinc, int n, T c) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -181,6 +194,11 @@ inline dim3 cell_grid(const Box3& b) {
   }                                                                                                           \
   FDTD_API int fdtd_inc_e_##SUF(T* einc, const T* hinc, int n, double c, double src, void* s) {               \
     k_inc_e<T><<<cdiv(n, 256), 256, 0, (hipStream_t)s>>>(einc, hinc, n, (T)c, src);                           \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_inc_e_tab_##SUF(T* einc, const T* hinc, int n, double c, const double* tab,               \
+                                   const int* counter, int lag, void* s) {                                    \
+    k_inc_e_tab<T><<<cdiv(n, 256), 256, 0, (hipStream_t)s>>>(einc, hinc, n, (T)c, tab, counter, lag);          \
     FDTD_RETURN_LAUNCH_STATUS();                                                                              \
   }                                                                                                           \
   FDTD_API int fdtd_inc_h_##SUF(const T* einc, T* hinc, int n, double c, void* s) {                           \

@@ -50,6 +50,8 @@ from .tfsf import build_tfsf_tables, incident_line_length
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
+GRAPH_STEPS = 60  # steps per captured HIP graph (a multiple of 6: D/D1 level rotations return to the start)
+
 
 @dataclass
 class SchemeConfig:
@@ -93,6 +95,7 @@ class SchemeConfig:
     cpml_alpha_max: float = 0.0
     time_block: int = 1                      # fused steps per HBM pass (temporal blocking, 3D vacuum/dielectric)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
+    use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
     lorentz_omega0_ratio: float = 0.5        # Lorentz resonance / source frequency
 
@@ -123,7 +126,7 @@ class SchemeConfig:
             ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
-            profile_phases=s.doProfilePhases)
+            profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
 def _torch_dtype(name: str):
@@ -256,6 +259,15 @@ class YeeScheme:
                       and not cfg.use_amp_mode)
         if self.fused:
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+        # HIP graph mode (--use-hip-graph): serial HIP runs capture GRAPH_STEPS
+        # steps once and replay them; sources read a device table, so the
+        # split kernels (separate source launch) are used
+        self.graph_mode = (cfg.use_hip_graph and self.device.type == "cuda" and self.ops.name == "hip"
+                           and self.halo is None and not cfg.use_amp_mode and not cfg.check_finite
+                           and not cfg.profile_phases)
+        self._graph_src = None
+        if self.graph_mode and self.fused:
+            self.fused = False
         # temporal blocking: T fused steps per pass (yee3d_tb.hip); decomposed
         # runs exchange T-deep ghosts every T steps (buffer size == T)
         T = max(1, int(cfg.time_block))
@@ -682,7 +694,11 @@ class YeeScheme:
         if self.point_source is not None:
             comp, li, _ = self.point_source
             if li is not None:
-                self.ops.set_value(self.F[p][comp], li, self.source_value(t, p))
+                if self._graph_src is not None:
+                    tab, counter, t0 = self._graph_src
+                    self.ops.set_value_tab(self.F[p][comp], li, tab[p], counter, t - t0)
+                else:
+                    self.ops.set_value(self.F[p][comp], li, self.source_value(t, p))
 
     in_amplitude = False
 
@@ -703,7 +719,11 @@ class YeeScheme:
         for p in range(self.planes):
             if cfg.use_tfsf:
                 with ph("incident-E"):
-                    self.ops.inc_step_e(self.einc[p], self.hinc[p], self.inc_ce, self.source_value(t, p))
+                    if self._graph_src is not None:
+                        tab, counter, t0 = self._graph_src
+                        self.ops.inc_step_e_tab(self.einc[p], self.hinc[p], self.inc_ce, tab[p], counter, t - t0)
+                    else:
+                        self.ops.inc_step_e(self.einc[p], self.hinc[p], self.inc_ce, self.source_value(t, p))
             with ph("E"):
                 if halo is not None and not deep:
                     halo.finish_and_update(self, "E", p)
@@ -848,6 +868,8 @@ class YeeScheme:
         blocked kernel where possible (no per-step hooks), single fused steps
         for the remainder."""
         T = self.tb
+        if self.graph_mode and not self.hooks and n >= GRAPH_STEPS:
+            n -= self._advance_graph(n)
         while n > 0:
             if T > 1 and n >= T and not self.hooks and self.sub_step == 0:
                 self._tb_step(T)
@@ -855,6 +877,34 @@ class YeeScheme:
             else:
                 self.step()
                 n -= 1
+
+    def _advance_graph(self, n: int) -> int:
+        """Capture GRAPH_STEPS steps into one HIP graph and replay it
+        ``n // GRAPH_STEPS`` times; returns the steps taken.  Sources read a
+        device table through a device step counter that the graph advances,
+        and GRAPH_STEPS is a multiple of 6, so the UPML / Drude level lists
+        (rotated every step) are back in place at the end of each replay."""
+        G = GRAPH_STEPS
+        reps = n // G
+        t0 = self.t
+        tab = torch.tensor([[self.source_value(t0 + i, p) for i in range(reps * G)] for p in range(self.planes)],
+                           dtype=torch.float64, device=self.device)
+        counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        graph = torch.cuda.CUDAGraph()
+        self._graph_src = (tab, counter, t0)
+        try:
+            with torch.cuda.graph(graph):
+                for _ in range(G):
+                    self.step()
+                self.ops.counter_add(counter, G)
+        finally:
+            self._graph_src = None
+        self.t = t0  # capture records the kernels, it does not run them
+        for _ in range(reps):
+            graph.replay()
+        self.t = t0 + reps * G
+        self._graph = (graph, tab, counter)  # keep alive until the stream has drained
+        return reps * G
 
     def _tb_regions(self, T: int):
         """(update boxes, [output boxes]) of a blocked pass, local indices.

@@ -173,10 +173,14 @@ def _layer(entries, device, dtype) -> List[TfsfTable]:
     layers = []
     for r in range(int(rank.max()) + 1):
         sel = rank == r
-        layers.append(TfsfTable(torch.as_tensor(flat[sel], device=device),
+        tab = TfsfTable(torch.as_tensor(flat[sel], device=device),
                                 torch.as_tensor(i0[sel], device=device),
                                 torch.as_tensor(w0[sel], device=device, dtype=dtype),
                                 torch.as_tensor(w1[sel], device=device, dtype=dtype),
                                 torch.as_tensor(cv[sel], device=device, dtype=dtype),
-                                torch.as_tensor(ijk[sel].astype(np.int32), device=device)))
+                                torch.as_tensor(ijk[sel].astype(np.int32), device=device))
+        # host-side bounds of the table (checked by the HIP op without a device sync)
+        tab.max_off = int(flat[sel].max()) if sel.any() else -1
+        tab.max_inc = int(i0[sel].max()) + 1 if sel.any() else -1
+        layers.append(tab)
     return layers

@@ -451,9 +451,12 @@ class HipOps:
     def tfsf_apply(self, target: torch.Tensor, table, inc: torch.Tensor, box: Box) -> None:
         if table.n == 0 or _empty(box):
             return
-        if int(table.off.max()) >= target.numel() if not hasattr(table, "_checked") else False:
-            raise HipError("TF/SF table targets outside the array")
-        table._checked = True
+        max_off = getattr(table, "max_off", None)
+        if max_off is None:  # tables built elsewhere: one (syncing) check, then cached
+            table.max_off = max_off = int(table.off.max())
+            table.max_inc = int(table.i0.max()) + 1
+        if max_off >= target.numel() or table.max_inc >= inc.numel():
+            raise HipError("TF/SF table reads or writes outside its arrays")
         rc = self.fn("tfsf_apply")(_ptr(target), _ptr(table.off), _ptr(table.i0), _ptr(table.w0), _ptr(table.w1),
                                    _ptr(table.coef), _ptr(table.ijk), c_int(table.n), _ptr(inc), _box_arr([box]),
                                    _stream())
@@ -630,3 +633,27 @@ class HipOps:
                 c_int(self.xchunk), (c_vp * len(ptrs))(*ptrs), (c_int * len(ints))(*ints), _stream())
         _check(rc, "update_%s3d_cpml" % kind.lower())
         self.launches += 1
+
+    # ------------------------------------------------------------ HIP graphs
+    def set_value_tab(self, t: torch.Tensor, idx: Sequence[int], tab: torch.Tensor, counter: torch.Tensor,
+                      lag: int) -> None:
+        """Hard source whose value is ``tab[counter + lag]`` (device table and
+        step counter): replayable inside a captured HIP graph."""
+        s = t.shape
+        for d in range(3):
+            if not (0 <= idx[d] < s[d]):
+                raise HipError("source index %s outside %s" % (idx, tuple(s)))
+        if tab.dtype != torch.float64 or counter.dtype != torch.int32:
+            raise HipError("source table must be float64 and the counter int32")
+        off = (idx[0] * s[1] + idx[1]) * s[2] + idx[2]
+        _check(self.fn("set_value_tab")(_ptr(t), c_ll(off), _ptr(tab), _ptr(counter), c_int(lag), _stream()),
+               "set_value_tab")
+        self.launches += 1
+
+    def inc_step_e_tab(self, einc: torch.Tensor, hinc: torch.Tensor, coef: float, tab: torch.Tensor,
+                       counter: torch.Tensor, lag: int) -> None:
+        _check(self.fn("inc_e_tab")(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(coef), _ptr(tab),
+                                    _ptr(counter), c_int(lag), _stream()), "inc_e_tab")
+
+    def counter_add(self, counter: torch.Tensor, n: int) -> None:
+        _check(self.lib.fdtd_counter_add(_ptr(counter), c_int(n), _stream()), "counter_add")

@@ -291,6 +291,10 @@ class TfsfTable:
         self.w1 = w1
         self.coef = coef
         self.ijk = ijk
+        # host-side bounds, so the HIP op validates without a device sync
+        # (required inside HIP graph capture)
+        self.max_off = int(off.max()) if off.numel() else -1
+        self.max_inc = int(i0.max()) + 1 if i0.numel() else -1
 
     @property
     def n(self) -> int:

@@ -108,6 +108,8 @@ def _report(settings: Settings, scheme, seconds: float, world: int, core, steps:
     kern = "fused E+H" if getattr(scheme, "fused", False) else "split"
     if getattr(scheme, "tb", 1) > 1:
         kern = "temporally blocked (%d steps per pass)" % scheme.tb
+    if getattr(scheme, "graph_mode", False):
+        kern += ", HIP graphs"
     out.write("Backend: %s on %s, %s kernels\n" % (scheme.ops.name, scheme.device, kern))
     out.write("Throughput: %.1f Mcells/s\n" % mc)
     return mc
