@@ -358,7 +358,22 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const Box3 O = make_box(obox);
   if (box_empty(O)) return 0;
-  if (xchunk <= 0) xchunk = steps <= 2 ? 64 : 256;  // measured at 1024^3 (tools/gpu_tb.sh)
+  if (xchunk <= 0) {
+    // longest x chunk (fewest re-read halo planes) that still gives >= 4
+    // workgroups per CU of the 256 (tail of the last wave of workgroups)
+    const int V = g_tb_vec ? g_tb_vec : (steps <= 2 ? 4 : 2);
+    const int R = g_tb_rows ? g_tb_rows : 1;
+    const int HL = (steps + V - 1) / V;
+    const long long gz = cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), (64 / R - 2 * HL) * V);
+    const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
+    xchunk = 32;
+    for (int c : {256, 128, 64}) {
+      if (gz * gy * (long long)cdiv(O.hi[0] - O.lo[0], c) >= 1024) {
+        xchunk = c;
+        break;
+      }
+    }
+  }
   TbSrc sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
   hipStream_t s = (hipStream_t)stream;

@@ -27,8 +27,11 @@ CONFIGS = [
       "--dtype", "f64", "--warmup-steps", "10"]),
     ("3d-512-vacuum", "3D vacuum 512^3, point dipole, fp32",
      C512 + ["--time-steps", "200", "--scene", "vacuum"]),
-    ("3d-512-vacuum-tb2", "3D vacuum 512^3, point dipole, fp32, 2 steps per pass",
-     C512 + ["--time-steps", "200", "--scene", "vacuum", "--time-block", "2"]),
+    ("1d-hip-graph", "1D vacuum, 10000 cells, Gaussian pulse, HIP graphs",
+     ["--1d", "--sizex", "10000", "--time-steps", "2000", "--scene", "vacuum", "--source", "gaussian",
+      "--dtype", "f64", "--warmup-steps", "60", "--use-hip-graph"]),
+    ("3d-512-vacuum-tb4", "3D vacuum 512^3, point dipole, fp32, 4 steps per pass",
+     C512 + ["--time-steps", "210", "--scene", "vacuum", "--time-block", "4"]),
     ("3d-512-cpml-tfsf", "3D 512^3, CPML (10 cells) + TF/SF plane wave, fp32",
      C512 + ["--time-steps", "100", "--scene", "vacuum", "--use-pml", "--pml-type", "cpml", "--use-tfsf"]),
     ("3d-512-upml-tfsf", "3D 512^3, UPML (10 cells, reference D/B form) + TF/SF, fp32",
@@ -41,6 +44,10 @@ CONFIGS = [
      C512 + ["--time-steps", "200", "--scene", "sphere", "--sphere-eps", "4",
              "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
              "--sphere-radius", "128"]),
+    ("3d-512-sphere-tb4", "3D 512^3 dielectric sphere (eps=4, r=128), fp32, 4 steps per pass",
+     C512 + ["--time-steps", "210", "--scene", "sphere", "--sphere-eps", "4",
+             "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
+             "--sphere-radius", "128", "--time-block", "4"]),
 ]
 
 
