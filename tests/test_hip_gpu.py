@@ -76,6 +76,17 @@ def test_cpml_tfsf_3d(gpu):
                          sphere_radius=6, sphere_center=(20.5, 20.5, 20.5), dtype="f64"), gpu, 1e-10)
 
 
+def test_chain_wide_upml_drude_f32(gpu):
+    """Chain boxes wider than a wave row in z (x / y slabs, the dispersive
+    box) and narrow z slabs in one run, fp32."""
+    compare(SchemeConfig(scheme="3d", size=(40, 36, 132), time_steps=14, use_pml=True, use_metamaterials=True,
+                         pml_size=(5, 5, 6), scene="drude-sphere", sphere_radius=9,
+                         sphere_center=(20.0, 18.0, 66.0), dtype="f32"), gpu, 5e-5)
+    compare(SchemeConfig(scheme="3d", size=(36, 40, 128), time_steps=14, use_pml=True, use_tfsf=True,
+                         pml_size=(6, 5, 6), tfsf_size=(10, 10, 12), scene="sphere", sphere_radius=7,
+                         sphere_center=(18.5, 20.5, 64.5), dtype="f32"), gpu, 5e-5)
+
+
 def test_drude_3d(gpu):
     compare(SchemeConfig(scheme="3d", size=(64, 64, 36), time_steps=12, use_pml=True, use_metamaterials=True,
                          pml_size=(5, 5, 5), dtype="f64"), gpu, 1e-10)

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Per-GPU compute cost of a decomposed blocked run, measured on ONE GPU.
+
+Runs one rank's sub-domain of an N-way decomposition through the scheme's
+blocked step (interior pass + T-thick shells + halo pack / unpack kernels)
+with a null transport (messages are not moved), and compares the time per
+step with the serial blocked kernel on the same number of cells.  The
+difference is the compute overhead of the decomposition (shell re-reads,
+pack / unpack) that RCCL transfers must hide under.
+
+    python tools/decomp_cost.py --size 1024 1024 1024 --world 8 --rank 3 --time-block 4
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class NullComm:
+    """Transport that completes every send / receive immediately (timing only)."""
+    backend = "null"
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+
+    def post(self, ops):
+        return []
+
+    def allreduce(self, v, op="sum"):
+        return v
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, nargs=3, default=[1024, 1024, 1024])
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=-1, help="-1: the rank with the most neighbours")
+    ap.add_argument("--axes", default="xy")
+    ap.add_argument("--time-block", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=16)
+    a = ap.parse_args()
+    import torch
+    from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+    from fdtd3d_amd.ops import make_ops
+    from fdtd3d_amd.parallel.halo import HaloExchanger
+    from fdtd3d_amd.parallel.topology import ParallelGridCore
+
+    T = a.time_block
+    size = tuple(a.size)
+    core = ParallelGridCore.create(size, a.world, a.axes)
+    rank = a.rank
+    if rank < 0:
+        def nn(r):
+            d = core.domain(r, T)
+            return sum((x >= 0) for pair in d.neighbors for x in pair)
+        rank = max(range(core.used_procs), key=nn)
+    dom = core.domain(rank, T, align_z=4)
+    cfg = SchemeConfig(scheme="3d", size=size, scene="vacuum", dtype="f32", use_fused=True, time_block=T)
+
+    def timed(domain, halo):
+        s = YeeScheme(cfg, make_ops("hip", None, "cuda:0", torch.float32), domain, halo)
+        s.init_scheme()
+        s.init_grids()
+        s.advance(2 * T)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.advance(a.steps)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / a.steps
+        del s
+        torch.cuda.empty_cache()
+        return dt
+
+    halo = HaloExchanger(dom, comm=NullComm(rank, a.world))
+    t_dec = timed(dom, halo)
+    own = dom.owned_shape
+    cells = own[0] * own[1] * own[2]
+    # serial reference on the rank's owned extent
+    from fdtd3d_amd.parallel.domain import Domain
+    cfg_serial = SchemeConfig(scheme="3d", size=tuple(own), scene="vacuum", dtype="f32", use_fused=True,
+                              time_block=T)
+    cfg, cfg_dec = cfg_serial, cfg
+    t_ser = timed(None, None)
+    print("topology %s rank %d owned %s neighbours %s" % ("x".join(map(str, core.topology)), rank, own,
+                                                        dom.neighbors))
+    print("decomposed step %.3f ms (%.0f Mcells/s per GPU), serial same cells %.3f ms (%.0f Mcells/s): "
+          "overhead %.1f%%" % (t_dec * 1e3, cells / t_dec / 1e6, t_ser * 1e3, cells / t_ser / 1e6,
+                               100 * (t_dec / t_ser - 1)))
+
+
+if __name__ == "__main__":
+    main()
