@@ -235,12 +235,20 @@ class YeeScheme:
 
         # ---- plain-update coefficients Cb = dt / (eps eps0 dx), Db = dt / (mu mu0 dx)
         self.cb: Dict[str, Coef] = {}
+        # uniform material of every component of a kind (e.g. mu = 1 in a
+        # dielectric or dispersive scene): scalar coefficients keep the
+        # kernels on their scalar fast path (the HIP ops need one form per kind)
+        uni = {c: self.mat[c] is None or bool((self.mat[c] == self.mat[c].flatten()[0]).all()) for c in self.comps}
         for c in self.comps:
             base = EPS0 if c[0] == "E" else MU0
-            if self.mat[c] is None:
+            m = self.mat[c]
+            kind_uniform = all(uni[o] for o in self.comps if o[0] == c[0])
+            if m is not None and kind_uniform:
+                self.cb[c] = Coef(dt / (base * dx) / float(m.flatten()[0]))
+            elif m is None:
                 self.cb[c] = Coef(dt / (base * dx))
             else:
-                self.cb[c] = Coef(dt / (base * dx), cell=(1.0 / self.mat[c]).to(self.dtype))
+                self.cb[c] = Coef(dt / (base * dx), cell=(1.0 / m).to(self.dtype))
 
         if self.use_upml_chain:
             self._init_upml()
@@ -405,6 +413,16 @@ class YeeScheme:
                 st["ma2"] = Coef(1.0, cell=(-(4 * e0 * eps_c - 2 * dt * e0 * eps_c * g
                                               + e0 * (dt * dt * w * w + q * eps_c)) / A).to(dtp))
                 st["drude_active"] = (w != 0) | (g != 0)
+                # the non-dispersive chain (E from D through 1/(eps eps0)) for the
+                # chain boxes with no dispersive cell (PML slabs away from the
+                # metamaterial): with w = g = 0 the ADE gives D1 = D/(eps eps0)
+                # exactly, so D1 and its five coefficient arrays are not needed
+                inv_e = 1.0 / (eps_c * base)
+                uniform = bool((inv_e == inv_e.flatten()[0]).all())
+                s_pl, cell_pl = (float(inv_e.flatten()[0]), None) if uniform else (1.0, inv_e.to(dtp).contiguous())
+                st["plain"] = {"cbE": prof_coef(s_pl, {aCb: cbE_a, aCa: inv_ca}, cell_pl),
+                               "ccE": prof_coef(s_pl, {aCb: ccE_a, aCa: inv_ca}, cell_pl),
+                               "prof": dict(st["prof"], s=s_pl, cell=cell_pl)}
             self.upml[c] = st
         self._init_chain_regions(prof)
 
@@ -459,13 +477,16 @@ class YeeScheme:
             plain_core = I
             plain = box_subtract(plain_core, Dbox) if not box_empty(plain_core) else [(C[0], C[0])] * 6
             chain = box_subtract(C, plain_core) + [box_intersect(plain_core, Dbox)]
-            per[c] = (plain, chain)
+            # which chain boxes need the dispersive (D1) form
+            drude = [cfg.use_metamaterials and (n == 6 or not box_empty(box_intersect(chain[n], Dbox)))
+                     for n in range(7)]
+            per[c] = (plain, chain, drude)
         regions = {}
         for kind, comps in (("E", self.e_comps), ("H", self.h_comps)):
             plain = [{c: per[c][0][n] for c in comps} for n in range(6)]
-            chain = [{c: per[c][1][n] for c in comps} for n in range(7)]
+            chain = [({c: per[c][1][n] for c in comps}, {c: per[c][2][n] for c in comps}) for n in range(7)]
             regions[kind] = {"plain": [r for r in plain if any(not box_empty(b) for b in r.values())],
-                             "chain": [r for r in chain if any(not box_empty(b) for b in r.values())]}
+                             "chain": [r for r in chain if any(not box_empty(b) for b in r[0].values())]}
         self.chain_regions = regions
 
     # ----------------------------------------------------------------- TF/SF
@@ -597,7 +618,7 @@ class YeeScheme:
                 for c in comps:
                     for tab in self.tfsf[c]:
                         self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
-        for r in reg["chain"]:
+        for r, dru in reg["chain"]:
             boxes = {c: dom.to_local(box_intersect(r[c], w)) for c in comps}
             if all(box_empty(b) for b in boxes.values()):
                 continue
@@ -610,8 +631,12 @@ class YeeScheme:
                     fast[c] = (b[0], b[0])
                 else:
                     fast[c] = b
-            if any(not box_empty(b) for b in fast.values()):
-                self.ops.chain_update(kind, fast, F, self.upml, p, self.cfg.use_metamaterials)
+            # one launch per form: dispersive chain / non-dispersive chain
+            for form in (True, False):
+                sel = {c: (fast[c] if dru[c] == form else (fast[c][0], fast[c][0])) for c in comps}
+                if any(not box_empty(b) for b in sel.values()):
+                    plain_form = self.cfg.use_metamaterials and not form
+                    self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form)
             for c in slow:
                 self._upml_region(kind, c, p, boxes[c])
 

@@ -234,12 +234,12 @@ class HipOps:
                 self._check_stencil_box("E" if c[0] == "E" else "H", c, b, shape)
         pe = [self._cell_or_none(cb[c]) for c in E]
         ph = [self._cell_or_none(cb[c]) for c in H]
-        percell = pe[0] is not None
-        if any((p is not None) != percell for p in pe + ph):
-            raise HipError("fused step: mixed scalar/per-cell coefficients")
+        percell = any(p is not None for p in pe + ph)
         if percell:
-            cbs = (c_vp * 3)(*[self._scaled_cell(cb[c]).data_ptr() for c in E])
-            dbs = (c_vp * 3)(*[self._scaled_cell(cb[c]).data_ptr() for c in H])
+            # one kernel form for both kinds: scalar coefficients of the other
+            # kind become constant arrays (cached)
+            cbs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in E])
+            dbs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in H])
             cbv, dbv = 1.0, 1.0
         else:
             cbs = (c_vp * 3)(None, None, None)
@@ -276,6 +276,17 @@ class HipOps:
         if cached is None:
             cached = (c.cell * c.scalar).to(self.dtype).contiguous()
             setattr(c, key, cached)
+        return cached
+
+    def _cell_array(self, c: Coef, shape) -> torch.Tensor:
+        """scalar*cell as a full array; a scalar coefficient becomes a
+        cached constant array (kernels with one per-cell form for E and H)."""
+        if c.cell is not None:
+            return self._scaled_cell(c)
+        cached = getattr(c, "_const_arr", None)
+        if cached is None or tuple(cached.shape) != tuple(shape):
+            cached = torch.full(tuple(shape), float(c.scalar), dtype=self.dtype, device=self.device)
+            c._const_arr = cached
         return cached
 
     def _cellp(self, c: Coef):
@@ -494,12 +505,10 @@ class HipOps:
                 raise HipError("output box %s outside array %s" % (obox, shape))
         pe = [self._cell_or_none(cb[c]) for c in E]
         ph = [self._cell_or_none(cb[c]) for c in H]
-        percell = pe[0] is not None
-        if any((p is not None) != percell for p in pe + ph):
-            raise HipError("tb_step: mixed scalar/per-cell coefficients")
+        percell = any(p is not None for p in pe + ph)
         if percell:
-            cbs = (c_vp * 3)(*[self._scaled_cell(cb[c]).data_ptr() for c in E])
-            dbs = (c_vp * 3)(*[self._scaled_cell(cb[c]).data_ptr() for c in H])
+            cbs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in E])
+            dbs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in H])
             cbv, dbv = 1.0, 1.0
         else:
             cbs = (c_vp * 3)(None, None, None)
@@ -540,7 +549,7 @@ class HipOps:
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
-                     p: int, drude: bool) -> None:
+                     p: int, drude: bool, plain_form: bool = False) -> None:
         """Fused UPML/Drude chain (chain_kernels.hip) of the three components
         of a kind (one launch).  ``upml[c]`` holds the factored coefficient
         profiles (``prof``), the Drude cell coefficients and the D / D1 level
@@ -553,7 +562,7 @@ class HipOps:
         any_box = False
         for c in comps:
             st = upml[c]
-            pr = st["prof"]
+            pr = st["plain"]["prof"] if plain_form else st["prof"]
             b = boxes[c]
             terms = self.layout.curl_terms(c)
             if len(terms) != 2:

@@ -135,7 +135,7 @@ class TorchOps:
                 fout[c][sl] = cur[c][sp]
 
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
-                     p: int, drude: bool) -> None:
+                     p: int, drude: bool, plain_form: bool = False) -> None:
         """Reference semantics of the fused UPML/Drude chain kernel
         (chain_kernels.hip): D -> [D1] -> E per cell of each box."""
         for c, box in boxes.items():
@@ -155,8 +155,9 @@ class TorchOps:
                        + st["ma2"].materialize(sl) * D1[1][sl])
                 D1[2][sl] = D1n
                 nw, old = D1n, D1[0][sl]
-            F[c][sl] = (st["caE"].materialize(sl) * F[c][sl] + st["cbE"].materialize(sl) * nw
-                        + st["ccE"].materialize(sl) * old)
+            cbE, ccE = (st["plain"]["cbE"], st["plain"]["ccE"]) if plain_form else (st["cbE"], st["ccE"])
+            F[c][sl] = (st["caE"].materialize(sl) * F[c][sl] + cbE.materialize(sl) * nw
+                        + ccE.materialize(sl) * old)
 
     def curl_general(self, kind: str, comp: str, box: Box, out: torch.Tensor, inp: torch.Tensor,
                      src: Dict[str, torch.Tensor], ca: Coef, cb: Coef) -> None:
