@@ -69,7 +69,9 @@ def main(argv=None) -> int:
         torch.cuda.set_device(local)
         device = "cuda:%d" % local
     if world > 1:
-        dist.init_process_group("nccl" if device.startswith("cuda") else "gloo")
+        from fdtd3d_amd.parallel.comm import init_process_group
+        init_process_group("nccl" if device.startswith("cuda") else "gloo",
+                           device if device.startswith("cuda") else None)
         # establish the communicator with a collective before the first
         # batched point-to-point exchange
         dist.barrier()
@@ -127,7 +129,7 @@ def main(argv=None) -> int:
     if rank == 0:
         par = "x".join(str(v) for v in topo)
         out = {
-            "metric": "Mcells/sec (whole node), 3D vacuum 1024^3 grid",
+            "metric": "Mcells/sec (whole node), 3D vacuum 1024^3 grid at 1/2/4/8 MI355X",
             "value": round(mcells, 1),
             "unit": "Mcells/s",
             "n_gpus": world,

@@ -874,7 +874,8 @@ class YeeScheme:
         if self.device.type == "cuda":
             side = getattr(self, "_side_stream", None)
             if side is None:
-                side = torch.cuda.Stream(device=self.device)
+                # high priority: its pack / unpack kernels get CUs next to the interior pass
+                side = torch.cuda.Stream(device=self.device, priority=-1)
                 self._side_stream = side
             side.wait_stream(torch.cuda.current_stream(self.device))
         self.halo.exchange_all(self, stream=side)
@@ -987,7 +988,7 @@ class YeeScheme:
             if self.device.type == "cuda":
                 side = getattr(self, "_side_stream", None)
                 if side is None:
-                    side = torch.cuda.Stream(device=self.device)
+                    side = torch.cuda.Stream(device=self.device, priority=-1)
                     self._side_stream = side
                 # the side stream must see the previous pass's results
                 side.wait_stream(torch.cuda.current_stream(self.device))

@@ -26,6 +26,22 @@ import torch.distributed as dist
 P2P = namedtuple("P2P", "send tensor peer tag")
 
 
+def init_process_group(backend: str, device=None) -> None:
+    """``torch.distributed`` init for the solver.  With ``nccl`` (RCCL) the
+    communication streams are created high-priority, so halo transfers that
+    overlap a long interior kernel get dispatched as soon as a CU has room;
+    ``device`` (already current) binds the communicator eagerly."""
+    if backend == "nccl":
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        kw = {"pg_options": opts}
+        if device is not None:
+            kw["device_id"] = torch.device(device)
+        dist.init_process_group("nccl", **kw)
+    else:
+        dist.init_process_group(backend)
+
+
 class _Done:
     def wait(self):
         return True

@@ -36,7 +36,8 @@ def _init_distributed(settings: Settings):
         backend = "nccl" if (torch.cuda.device_count() > 0 and settings.backend != "torch") else "gloo"
         if settings.device == "cpu":
             backend = "gloo"
-        dist.init_process_group(backend)
+        from .parallel.comm import init_process_group
+        init_process_group(backend)
     return dist, dist.get_rank(), dist.get_world_size()
 
 
