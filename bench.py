@@ -41,12 +41,16 @@ def main(argv=None) -> int:
     ap.add_argument("--split", action="store_true", help="use the split E / H kernels instead of the fused one")
     ap.add_argument("--xchunk", type=int, default=0)
     ap.add_argument("--buffer-size", type=int, default=1, help="halo depth (deep halo when > 1)")
-    ap.add_argument("--time-block", type=int, default=4,
+    ap.add_argument("--time-block", type=int, default=5,
                     help="leapfrog steps per HBM pass (temporally blocked kernel); decomposed runs use a "
                          "halo of the same depth")
     ap.add_argument("--tb-xchunk", type=int, default=0, help="x planes per workgroup of the blocked kernel")
     ap.add_argument("--tb-vec", type=int, default=0, help="lane width of the blocked kernel (0 auto, 2, 4)")
     ap.add_argument("--tb-rows", type=int, default=0, help="grid rows per wave of the blocked kernel (0 auto, 1, 2)")
+    ap.add_argument("--tb-mrows", type=int, default=0,
+                    help="adjacent y rows per wave of the blocked kernel (0 auto, 1 single-row kernel, 2)")
+    ap.add_argument("--tb-variant", type=int, default=-1,
+                    help="multi-row blocked kernel: bit 0 deferred stores, bit 1 two planes prefetched (-1 default)")
     ap.add_argument("--tb-xcd", type=int, default=0, help="XCD-aware tile order of the blocked kernel (1 on, 0 off)")
     a = ap.parse_args(argv)
 
@@ -96,7 +100,9 @@ def main(argv=None) -> int:
     if a.tb_xchunk:
         ops.tb_xchunk = a.tb_xchunk
     if backend == "hip":
-        ops.tb_vec, ops.tb_rows, ops.tb_xcd = a.tb_vec, a.tb_rows, a.tb_xcd
+        ops.tb_vec, ops.tb_rows, ops.tb_xcd, ops.tb_mrows = a.tb_vec, a.tb_rows, a.tb_xcd, a.tb_mrows
+        if a.tb_variant >= 0:
+            ops.tb_variant = a.tb_variant
     scheme = YeeScheme(cfg, ops, domain, halo)
     scheme.init_scheme()
     scheme.init_grids()

@@ -284,8 +284,8 @@ int run(const fdtd::Settings& s) {
     }
   };
   // --time-block T: T steps per HBM pass through the blocked kernel
-  const int T_req = s.timeBlock <= 0 ? 4 : s.timeBlock;  // 0: automatic (4 steps per pass)
-  const int T_blk = (scheme == "3d" && use_fused && v4) ? std::max(1, std::min(4, T_req)) : 1;
+  const int T_req = s.timeBlock <= 0 ? 5 : s.timeBlock;  // 0: automatic (5 steps per pass)
+  const int T_blk = (scheme == "3d" && use_fused && v4) ? std::max(1, std::min(fdtd_tb_max_steps(), T_req)) : 1;
   auto advance = [&](int t0, int n) {
     int t = t0;
     while (n > 0) {

@@ -35,6 +35,11 @@ constexpr int TBW = 16;  // waves (y rows) per workgroup
 template <int V>
 struct VT;
 template <>
+struct VT<1> {
+  typedef float f __attribute__((ext_vector_type(1)));
+  typedef unsigned u __attribute__((ext_vector_type(1)));
+};
+template <>
 struct VT<2> {
   typedef float f __attribute__((ext_vector_type(2)));
   typedef unsigned u __attribute__((ext_vector_type(2)));
@@ -44,6 +49,18 @@ struct VT<4> {
   typedef float f __attribute__((ext_vector_type(4)));
   typedef unsigned u __attribute__((ext_vector_type(4)));
 };
+
+// neighbour lanes through DPP wave shifts (one VALU op, usually folded into
+// the consuming v_sub as a _dpp modifier) instead of ds_bpermute round trips
+// through the LDS pipe: lane_up(v) on lane i = v of lane i-1 (wave_shr:1),
+// lane_dn(v) = v of lane i+1 (wave_shl:1); lanes shifted in from outside the
+// wave read 0 -- they are halo lanes of every tile.
+__device__ __forceinline__ float lane_up(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_dn(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
 
 struct TbSrc {
   float v[8];  // hard-source value applied after E update of level l
@@ -66,7 +83,9 @@ __device__ __forceinline__ Rsrc plane_rsrc(const float* base, int x, int nx, siz
 
 template <int V>
 __device__ __forceinline__ typename VT<V>::f bld(Rsrc r, unsigned boff) {
-  if constexpr (V == 4)
+  if constexpr (V == 1)
+    return __builtin_bit_cast(typename VT<1>::f, __builtin_amdgcn_raw_buffer_load_b32(r, boff, 0, 0));
+  else if constexpr (V == 4)
     return __builtin_bit_cast(typename VT<4>::f, __builtin_amdgcn_raw_buffer_load_b128(r, boff, 0, 0));
   else
     return __builtin_bit_cast(typename VT<2>::f, __builtin_amdgcn_raw_buffer_load_b64(r, boff, 0, 0));
@@ -75,11 +94,13 @@ __device__ __forceinline__ typename VT<V>::f bld(Rsrc r, unsigned boff) {
 template <int V>
 __device__ __forceinline__ void bst(Rsrc r, unsigned boff, const typename VT<V>::f& v, unsigned mask) {
   if (mask == (1u << V) - 1u) {
-    if constexpr (V == 4)
+    if constexpr (V == 1)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[0]), r, boff, 0, 0);
+    else if constexpr (V == 4)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(typename VT<4>::u, v), r, boff, 0, 0);
     else
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(typename VT<2>::u, v), r, boff, 0, 0);
-  } else if (mask) {
+  } else if (V > 1 && mask) {
     // the b32 builtin takes the raw bits (an implicit float->uint would convert)
 #pragma unroll
     for (int q = 0; q < V; ++q)
@@ -252,8 +273,8 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
       const vec ex_jn = sX[buf][2][rup][lane];
       const vec ez_jn = sX[buf][3][rup][lane];
       buf ^= 1;
-      const float hy_k0 = __shfl_up(Hc.y[V - 1], 1, LW);
-      const float hx_k0 = __shfl_up(Hc.x[V - 1], 1, LW);
+      const float hy_k0 = lane_up(Hc.y[V - 1]);
+      const float hx_k0 = lane_up(Hc.x[V - 1]);
       // coefficients are zeroed outside each component's update box, so the
       // arithmetic is branch-free vector work and untouched cells keep E_l
       const vec cex = coef(cbx, bex, pe, mex, mcex, cbv);
@@ -270,8 +291,8 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
       // ---- H_{l+1} on plane ph = pe-1 from E_{l+1}(ph) = Ep[l], E_{l+1}(pe) = En,
       //      H_l(ph) = Hp[l]
       const int ph = pe - 1;
-      const float ey_k3 = __shfl_down(Ep[l].y[0], 1, LW);
-      const float ex_k3 = __shfl_down(Ep[l].x[0], 1, LW);
+      const float ey_k3 = lane_dn(Ep[l].y[0]);
+      const float ex_k3 = lane_dn(Ep[l].x[0]);
       F3<V> Hn;
       const vec chx = coef(dbx, bhx, ph, mhx, mchx, dbv);
       Hn.x = Hp[l].x + chx * ((zp1<V>(Ep[l].y, ey_k3) - Ep[l].y) - (ez_jn - Ep[l].z));
@@ -305,6 +326,229 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Multi-row variant: every wave carries R ADJACENT y rows in registers (rows
+// R*w .. R*w+R-1 of the tile), so one workgroup spans 16R rows and the 2T
+// redundant halo rows are amortised over 16R instead of 16 (T=4: 8 of 16 rows
+// owned by the single-row kernel, 24 of 32 at R=2).  y neighbours inside a
+// wave's row group are registers; only the first / last row of the group goes
+// through LDS (the same 4 fields x 16 slots as above, one barrier per level).
+// Scalar lanes (V=1) keep the register footprint of the float2 single-row
+// kernel; the extra z halo lanes (T per side) cost less than the y rows saved.
+// Masks of the 7 boxes (6 update boxes + output box) for every row are packed
+// into one bit field (R*V <= 4).
+// PFD: planes loaded ahead (1 or 2).  DEFER: the results of plane X are
+// stored after plane X+1's prefetch is issued -- vmcnt counts loads and
+// stores together in issue order, so stores issued between two prefetches
+// would otherwise be waited for with the older prefetch.
+template <int T, int V, int R, bool PERCELL, int PFD, bool DEFER>
+__global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
+    const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
+    const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
+    float* __restrict__ exo, float* __restrict__ eyo, float* __restrict__ ezo,
+    float* __restrict__ hxo, float* __restrict__ hyo, float* __restrict__ hzo,
+    const float* __restrict__ cbx, const float* __restrict__ cby, const float* __restrict__ cbz,
+    const float* __restrict__ dbx, const float* __restrict__ dby, const float* __restrict__ dbz, float cb,
+    float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
+    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz) {
+  static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
+  typedef typename VT<V>::f vec;
+  constexpr int HL = (T + V - 1) / V;   // halo lanes per side
+  constexpr int TBZ = (64 - 2 * HL) * V; // owned z cells per tile
+  constexpr int ROWS = TBW * R;         // y rows per workgroup
+  constexpr unsigned VM = (1u << V) - 1u;
+  __shared__ vec sX[2][4][TBW][64];
+  const int lane = threadIdx.x;
+  const int w = threadIdx.y;
+  // Tile of this workgroup.  A row of a tile starts at an arbitrary z (the
+  // stride is the 64 - 2T owned cells), so its 64 cells straddle three
+  // 128-B lines, one shared with each z neighbour tile.  Workgroups are dealt
+  // round-robin to the 8 XCDs (own L2 each); with xcd_swz each XCD instead
+  // gets a contiguous run of tiles, z fastest, so z neighbours run together
+  // on one L2 and the shared lines are fetched from HBM once.
+  int tz = blockIdx.x, ty = blockIdx.y, tx = blockIdx.z;
+  if (xcd_swz) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy * (int)gridDim.z;
+    const int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int n8 = n & ~7;
+    const int q = p < n8 ? (p & 7) * (n8 >> 3) + (p >> 3) : p;
+    tz = q % gx;
+    ty = (q / gx) % gy;
+    tx = q / (gx * gy);
+  }
+  const int kb = (O.lo[2] & ~(V - 1)) - HL * V + TBZ * tz + V * lane;
+  const int jw = O.lo[1] - T + (ROWS - 2 * T) * ty + R * w;  // first row of this wave
+  const int i0 = O.lo[0] + tx * xchunk;
+  const int i1 = min(i0 + xchunk, O.hi[0]);
+  const bool kin = kb >= 0 && kb < nz;
+  const bool lane_own = lane >= HL && lane < 64 - HL;
+  const size_t plane = (size_t)ny * nz;
+  unsigned roff[R];
+  unsigned mbits = 0;  // bit (r*7 + n)*V + q: cell q of row r inside box n
+  const Box3* bx[7] = {&bex, &bey, &bez, &bhx, &bhy, &bhz, &O};
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = jw + r;
+    const int t = R * w + r;
+    const bool ld_ok = kin && j >= 0 && j < ny;
+    roff[r] = ld_ok ? (unsigned)(j * nz + kb) * 4u : 0xF0000000u;
+    const bool own = ld_ok && lane_own && t >= T && t < ROWS - T;
+#pragma unroll
+    for (int n = 0; n < 7; ++n) {
+      const bool ok = n < 6 ? ld_ok : own;
+      mbits |= (ok ? kmaskv<V>(*bx[n], j, kb) : 0u) << ((r * 7 + n) * V);
+    }
+  }
+  const int rdn = w > 0 ? w - 1 : 0;
+  const int rup = w < TBW - 1 ? w + 1 : TBW - 1;
+  const vec zero = (vec)(0.f);
+  const vec cbv = (vec)(cb), dbv = (vec)(db);
+  auto coef = [&](const float* arr, const Box3& b, int p, int r, int n, const vec& sc) -> vec {
+    const bool in = xin(b, p);
+    const unsigned m = in ? (mbits >> ((r * 7 + n) * V)) & VM : 0u;
+    if (PERCELL) return cmask<V>(bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]), m);
+    return cmask<V>(sc, m);
+  };
+
+  F3<V> Hp[T][R], Ep[T][R];
+#pragma unroll
+  for (int l = 0; l < T; ++l)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      Hp[l][r].x = Hp[l][r].y = Hp[l][r].z = zero;
+      Ep[l][r].x = Ep[l][r].y = Ep[l][r].z = zero;
+    }
+  int buf = 0;
+  auto load_plane = [&](int X, F3<V>* H, F3<V>* E) {
+    const Rsrc rhx = plane_rsrc(hxi, X, nx, plane), rhy = plane_rsrc(hyi, X, nx, plane);
+    const Rsrc rhz = plane_rsrc(hzi, X, nx, plane), rex = plane_rsrc(exi, X, nx, plane);
+    const Rsrc rey = plane_rsrc(eyi, X, nx, plane), rez = plane_rsrc(ezi, X, nx, plane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      H[r].x = bld<V>(rhx, roff[r]);
+      H[r].y = bld<V>(rhy, roff[r]);
+      H[r].z = bld<V>(rhz, roff[r]);
+      E[r].x = bld<V>(rex, roff[r]);
+      E[r].y = bld<V>(rey, roff[r]);
+      E[r].z = bld<V>(rez, roff[r]);
+    }
+  };
+  F3<V> Hnx[R], Enx[R], Hn2[R], En2[R];
+  load_plane(i0 - T, Hnx, Enx);
+  if (PFD == 2) load_plane(i0 - T + 1, Hn2, En2);
+  F3<V> Hs[R];  // DEFER: H_T of the previous plane, stored next trip
+  // stores of the results of trip X: E_T on plane X-T+1 (= Ep[T-1] until the
+  // next trip's last level), H_T on plane X-T
+  auto store_plane = [&](int X, const F3<V>* Es, const F3<V>* Hh) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned mo = (mbits >> ((r * 7 + 6) * V)) & VM;
+      if (mo) {
+        const int pe = X - T + 1;
+        if (pe >= i0 && pe < i1) {
+          bst<V>(plane_rsrc(exo, pe, nx, plane), roff[r], Es[r].x, mo);
+          bst<V>(plane_rsrc(eyo, pe, nx, plane), roff[r], Es[r].y, mo);
+          bst<V>(plane_rsrc(ezo, pe, nx, plane), roff[r], Es[r].z, mo);
+        }
+        const int ph = X - T;
+        if (ph >= i0 && ph < i1) {
+          bst<V>(plane_rsrc(hxo, ph, nx, plane), roff[r], Hh[r].x, mo);
+          bst<V>(plane_rsrc(hyo, ph, nx, plane), roff[r], Hh[r].y, mo);
+          bst<V>(plane_rsrc(hzo, ph, nx, plane), roff[r], Hh[r].z, mo);
+        }
+      }
+    }
+  };
+  for (int X = i0 - T; X <= i1 + T - 1; ++X) {
+    F3<V> Hc[R], Ec[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      Hc[r] = Hnx[r];
+      Ec[r] = Enx[r];
+      if (PFD == 2) {
+        Hnx[r] = Hn2[r];
+        Enx[r] = En2[r];
+      }
+    }
+    // next plane(s) in flight under this plane's levels
+    if (PFD == 2)
+      load_plane(X + 2, Hn2, En2);
+    else
+      load_plane(X + 1, Hnx, Enx);
+    if (DEFER && X > i0 - T) {
+      F3<V> Es[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) Es[r] = Ep[T - 1][r];
+      store_plane(X - 1, Es, Hs);
+    }
+    F3<V> En[R];
+#pragma unroll
+    for (int l = 0; l < T; ++l) {
+      const int pe = X - l;
+      sX[buf][0][w][lane] = Hc[R - 1].z;
+      sX[buf][1][w][lane] = Hc[R - 1].x;
+      sX[buf][2][w][lane] = Ep[l][0].x;
+      sX[buf][3][w][lane] = Ep[l][0].z;
+      __syncthreads();
+      const vec hz_dn = sX[buf][0][rdn][lane];
+      const vec hx_dn = sX[buf][1][rdn][lane];
+      const vec ex_up = sX[buf][2][rup][lane];
+      const vec ez_up = sX[buf][3][rup][lane];
+      buf ^= 1;
+      const bool src_plane = src_comp >= 0 && pe == src_i;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const vec hz_j = r == 0 ? hz_dn : Hc[r > 0 ? r - 1 : 0].z;
+        const vec hx_j = r == 0 ? hx_dn : Hc[r > 0 ? r - 1 : 0].x;
+        const float hy_k0 = lane_up(Hc[r].y[V - 1]);
+        const float hx_k0 = lane_up(Hc[r].x[V - 1]);
+        En[r].x = Ec[r].x + coef(cbx, bex, pe, r, 0, cbv) * ((Hc[r].z - hz_j) - (Hc[r].y - zm1<V>(Hc[r].y, hy_k0)));
+        En[r].y = Ec[r].y + coef(cby, bey, pe, r, 1, cbv) * ((Hc[r].x - zm1<V>(Hc[r].x, hx_k0)) - (Hc[r].z - Hp[l][r].z));
+        En[r].z = Ec[r].z + coef(cbz, bez, pe, r, 2, cbv) * ((Hc[r].y - Hp[l][r].y) - (Hc[r].x - hx_j));
+        if (src_plane && jw + r == src_j && src_k >= kb && src_k < kb + V) {
+          const int q = src_k - kb;
+          if (src_comp == 0) En[r].x[q] = sv.v[l];
+          if (src_comp == 1) En[r].y[q] = sv.v[l];
+          if (src_comp == 2) En[r].z[q] = sv.v[l];
+        }
+      }
+      const int ph = pe - 1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const vec ex_jn = r == R - 1 ? ex_up : Ep[l][r < R - 1 ? r + 1 : r].x;
+        const vec ez_jn = r == R - 1 ? ez_up : Ep[l][r < R - 1 ? r + 1 : r].z;
+        const float ey_k3 = lane_dn(Ep[l][r].y[0]);
+        const float ex_k3 = lane_dn(Ep[l][r].x[0]);
+        F3<V> Hn;
+        Hn.x = Hp[l][r].x + coef(dbx, bhx, ph, r, 3, dbv) *
+                                ((zp1<V>(Ep[l][r].y, ey_k3) - Ep[l][r].y) - (ez_jn - Ep[l][r].z));
+        Hn.y = Hp[l][r].y + coef(dby, bhy, ph, r, 4, dbv) *
+                                ((En[r].z - Ep[l][r].z) - (zp1<V>(Ep[l][r].x, ex_k3) - Ep[l][r].x));
+        Hn.z = Hp[l][r].z + coef(dbz, bhz, ph, r, 5, dbv) * ((ex_jn - Ep[l][r].x) - (En[r].y - Ep[l][r].y));
+        // later rows (r+1 ..) read only their own and higher rows' Ep, so
+        // row r rotates as soon as its H is done
+        Ec[r] = Ep[l][r];
+        Ep[l][r] = En[r];
+        Hp[l][r] = Hc[r];
+        Hc[r] = Hn;
+      }
+    }
+    if (DEFER) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) Hs[r] = Hc[r];
+    } else {
+      store_plane(X, En, Hc);
+    }
+  }
+  if (DEFER) {
+    F3<V> Es[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) Es[r] = Ep[T - 1][r];
+    store_plane(i1 + T - 1, Es, Hs);
+  }
+}
+
 int g_tb_vec = 0;   // 0: automatic (float4 lanes for T <= 2, float2 above), else 2 / 4
 int g_tb_rows = 0;  // rows per wave: 0 automatic (1), 1 / 2
 int g_tb_xcd = 0;   // XCD-aware tile order (measured: no gain, T=2 slower; off by default)
@@ -334,6 +578,49 @@ int launch_tb_pc(bool pc, const float* const* ein, const float* const* hin, floa
                                         s);
 }
 
+// two rows per wave from 4 steps per pass on (T=4: 246-267k vs 247-260k
+// Mcells/s single-row at 1024^3; T=3: 162k vs 207k, so single-row below)
+constexpr int MR_AUTO_ROWS = 2;
+int g_tb_mrows = 0;  // rows per wave of the multi-row kernel: 0 automatic, 1 = single-row kernel, 2 / 4
+
+int g_tb_mr_xcd = 1;   // multi-row kernel: XCD-contiguous tile order, z fastest (-16..20% HBM reads)
+int g_tb_variant = 0;  // multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched
+
+template <int T, int V, int R, bool PERCELL>
+int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
+                 const float* const* cbs, const float* const* dbs, float cb, float db, int nx, int ny, int nz,
+                 const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv, hipStream_t s) {
+  constexpr int HL = (T + V - 1) / V;
+  constexpr int TBZ = (64 - 2 * HL) * V;
+  dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * T),
+            cdiv(O.hi[0] - O.lo[0], xchunk));
+#define MR_LAUNCH(PFD, DEFER)                                                                                 \
+  k_tb3d_mr<T, V, R, PERCELL, PFD, DEFER><<<grid, dim3(64, TBW), 0, s>>>(                                   \
+      ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
+      cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
+      O, xchunk, src[0], src[1], src[2], src[3], sv, g_tb_mr_xcd)
+  switch (g_tb_variant & 3) {
+    case 0: MR_LAUNCH(1, false); break;
+    case 1: MR_LAUNCH(1, true); break;
+    case 2: MR_LAUNCH(2, false); break;
+    default: MR_LAUNCH(2, true); break;
+  }
+#undef MR_LAUNCH
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <int T>
+int launch_tb_mr_sel(int V, int R, bool pc, const float* const* ein, const float* const* hin, float* const* eout,
+                     float* const* hout, const float* const* cbs, const float* const* dbs, float cb, float db,
+                     int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src,
+                     const TbSrc& sv, hipStream_t s) {
+#define MR_ARGS ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s
+  // only scalar lanes with 2 rows per wave: R = 4 or float2 lanes at R = 2
+  // exceed 128 VGPRs and spill from T = 2 on
+  if (V == 1 && R == 2) return pc ? launch_tb_mr<T, 1, 2, true>(MR_ARGS) : launch_tb_mr<T, 1, 2, false>(MR_ARGS);
+#undef MR_ARGS
+  return (int)hipErrorInvalidValue;
+}
 
 }  // namespace
 
@@ -344,6 +631,17 @@ FDTD_API void fdtd_set_tb_vec(int v) { g_tb_vec = (v == 2 || v == 4) ? v : 0; }
 FDTD_API void fdtd_set_tb_rows(int r) { g_tb_rows = (r == 1 || r == 2) ? r : 0; }
 // XCD-aware tile order of the blocked kernel (1 = on, default)
 FDTD_API void fdtd_set_tb_xcd(int on) { g_tb_xcd = on ? 1 : 0; }
+// adjacent y rows carried per wave (k_tb3d_mr): 0 = automatic, 1 = the
+// single-row kernel, 2
+FDTD_API void fdtd_set_tb_mrows(int r) { g_tb_mrows = (r == 1 || r == 2) ? r : 0; }
+// multi-row kernel variant (tuning): bit 0 deferred stores, bit 1 two planes
+// prefetched, bit 2 XCD-contiguous tile order
+FDTD_API void fdtd_set_tb_variant(int v) {
+  g_tb_variant = v & 3;
+  g_tb_mr_xcd = (v >> 2) & 1;  // bit 2: XCD-contiguous tile order
+}
+// largest steps-per-pass the blocked kernels accept
+FDTD_API int fdtd_tb_max_steps() { return 6; }
 
 // T fused leapfrog steps: reads ein/hin, writes eout/hout (distinct buffers)
 // on the output box `obox` (lo[3], hi[3]).  `boxes` = 6 update boxes
@@ -353,11 +651,44 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
                               float* const* hout, const float* const* cbs, const float* const* dbs, double cb,
                               double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
                               int steps, const int* src, const double* src_vals, void* stream) {
-  if (nz % 4 != 0 || steps < 1 || steps > 4) return (int)hipErrorInvalidValue;
+  if (nz % 4 != 0 || steps < 1 || steps > 6) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const Box3 O = make_box(obox);
   if (box_empty(O)) return 0;
+  TbSrc sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
+  hipStream_t s = (hipStream_t)stream;
+  const bool pc = cbs[0] != nullptr;
+  const float fcb = (float)cb, fdb = (float)db;
+  // multi-row kernel: automatic from 4 steps on, required above 4
+  const int MR = g_tb_mrows ? g_tb_mrows : (steps >= 4 ? MR_AUTO_ROWS : 1);
+  if (MR > 1 || steps > 4) {
+    const int R = 2, V = 1;
+    if (xchunk <= 0) {
+      const int HL = (steps + V - 1) / V;
+      const long long gz = cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), (64 - 2 * HL) * V);
+      const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
+      xchunk = 32;
+      for (int c : {256, 128, 64}) {
+        if (gz * gy * (long long)cdiv(O.hi[0] - O.lo[0], c) >= 1024) {
+          xchunk = c;
+          break;
+        }
+      }
+    }
+#define MR_ARGS V, R, pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, src, sv, s
+    switch (steps) {
+      case 1: return launch_tb_mr_sel<1>(MR_ARGS);
+      case 2: return launch_tb_mr_sel<2>(MR_ARGS);
+      case 3: return launch_tb_mr_sel<3>(MR_ARGS);
+      case 4: return launch_tb_mr_sel<4>(MR_ARGS);
+      case 5: return launch_tb_mr_sel<5>(MR_ARGS);
+      case 6: return launch_tb_mr_sel<6>(MR_ARGS);
+    }
+#undef MR_ARGS
+    return (int)hipErrorInvalidValue;
+  }
   if (xchunk <= 0) {
     // longest x chunk (fewest re-read halo planes) that still gives >= 4
     // workgroups per CU of the 256 (tail of the last wave of workgroups)
@@ -374,12 +705,7 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
       }
     }
   }
-  TbSrc sv;
-  for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
-  hipStream_t s = (hipStream_t)stream;
-  const bool pc = cbs[0] != nullptr;
   const int V = g_tb_vec ? g_tb_vec : (steps <= 2 ? 4 : 2);
-  const float fcb = (float)cb, fdb = (float)db;
   const int R = g_tb_rows ? g_tb_rows : 1;  // 2 rows per wave measured slower (228k vs 245k, T=4)
 #define TB_ARGS pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, src, sv, s
 #define TB_CASE(TT)                                                                     \

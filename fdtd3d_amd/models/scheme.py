@@ -279,13 +279,14 @@ class YeeScheme:
         # temporal blocking: T fused steps per pass (yee3d_tb.hip); decomposed
         # runs exchange T-deep ghosts every T steps (buffer size == T)
         T = int(cfg.time_block)
-        if T <= 0:  # automatic: 4 steps per pass (measured best at 512^3 and 1024^3) for the HIP fp32 path
-            T = 4 if (self.ops.name == "hip" and self.dtype == torch.float32) else 1
+        if T <= 0:  # automatic: 5 steps per pass (measured best at 1024^3) for the HIP fp32 path
+            T = 5 if (self.ops.name == "hip" and self.dtype == torch.float32) else 1
             if self.halo is not None and self.domain.buffer_size != T:
                 T = 1
         self.tb = 1
         hip_ok = self.ops.name != "hip" or (self.dtype == torch.float32 and self.domain.shape[2] % 4 == 0)
-        if (T > 1 and self.fused and hasattr(self.ops, "tb_step") and hip_ok and T <= 4
+        if (T > 1 and self.fused and hasattr(self.ops, "tb_step") and hip_ok
+                and T <= getattr(self.ops, "tb_max_steps", 6)
                 and (self.halo is None or self.domain.buffer_size == T)):
             self.tb = T
         self.initialized = True

@@ -27,6 +27,7 @@ from .coef import Coef
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
 _LIB = None
+TB_MAX_STEPS = 6  # steps per pass of the blocked kernels (fdtd_tb_max_steps)
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libfdtd3d_hip.so")
 
 c_int = ctypes.c_int
@@ -486,8 +487,8 @@ class HipOps:
         ``sources`` = per-step list of (E component, local index, value) or
         None."""
         E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
-        if not (1 <= steps <= 4):
-            raise HipError("tb_step supports 1..4 steps per pass")
+        if not (1 <= steps <= TB_MAX_STEPS):
+            raise HipError("tb_step supports 1..%d steps per pass" % TB_MAX_STEPS)
         shape = tuple(fin["Ex"].shape)
         if self.dtype != torch.float32 or shape[2] % 4 != 0:
             raise HipError("tb_step needs fp32 fields with nz %% 4 == 0, got %s %s" % (self.dtype, shape))
@@ -535,6 +536,8 @@ class HipOps:
         self.lib.fdtd_set_tb_vec(c_int(self.tb_vec))
         self.lib.fdtd_set_tb_rows(c_int(self.tb_rows))
         self.lib.fdtd_set_tb_xcd(c_int(self.tb_xcd))
+        self.lib.fdtd_set_tb_mrows(c_int(self.tb_mrows))
+        self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
         rc = self.fn("tb3d_v4")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
                                 c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk),
@@ -542,10 +545,13 @@ class HipOps:
         _check(rc, "tb3d")
         self.launches += 1
 
+    tb_max_steps = TB_MAX_STEPS
     tb_xchunk = 0
     tb_vec = 0  # lane width of the blocked kernel: 0 auto (4 for T <= 2, 2 above), 2 or 4
     tb_rows = 0  # grid rows per wave: 0 auto (1), 1 or 2
     tb_xcd = 0  # XCD-aware tile order (off: measured no gain)
+    tb_variant = 4  # multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched, bit 2 XCD tile order
+    tb_mrows = 0  # adjacent y rows per wave (multi-row kernel): 0 auto, 1 single-row kernel, 2
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],

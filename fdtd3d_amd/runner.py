@@ -75,7 +75,7 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
         buf = settings.bufferSize
         tb = settings.timeBlock
         if tb <= 0:  # automatic: blocked passes on the fp32 3D fused path
-            tb = 4 if (cfg.scheme == "3d" and cfg.dtype == "f32" and backend == "hip" and cfg.use_fused
+            tb = 5 if (cfg.scheme == "3d" and cfg.dtype == "f32" and backend == "hip" and cfg.use_fused
                        and not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials or cfg.use_amp_mode)) else 1
         if tb > 1 and cfg.scheme == "3d":
             buf = tb  # blocked passes exchange tb-deep ghosts every tb steps

@@ -40,9 +40,21 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("vec,rows,xcd", [(0, 0, 1), (0, 0, 0), (2, 1, 1), (2, 2, 1), (4, 1, 1), (4, 2, 0)])
-@pytest.mark.parametrize("size,T,scene,obox,src", CASES)
-def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec, rows, xcd):
+CASES_MR = CASES + [
+    ((26, 70, 140), 5, "vacuum", None, True),       # 3 y tiles of the 2-row kernel, 3 z tiles
+    ((22, 40, 72), 6, "sphere", ((6, 6, 8), (16, 34, 64)), False),
+    ((20, 36, 68), 6, "vacuum", ((0, 0, 0), (20, 36, 68)), True),
+]
+
+
+@pytest.mark.parametrize("vec,rows,xcd,mrows,variant", [(0, 0, 1, 1, 0), (0, 0, 0, 1, 0), (2, 1, 1, 1, 0),
+                                                        (2, 2, 1, 1, 0), (4, 1, 1, 1, 0), (4, 2, 0, 1, 0),
+                                                        (0, 0, 0, 2, 0), (0, 0, 0, 2, 1), (0, 0, 0, 2, 2),
+                                                        (0, 0, 0, 2, 3), (0, 0, 0, 2, 4)])
+@pytest.mark.parametrize("size,T,scene,obox,src", CASES_MR)
+def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec, rows, xcd, mrows, variant):
+    if T > 4 and mrows != 2:
+        pytest.skip("the single-row kernel stops at 4 steps per pass")
     cfg = SchemeConfig(scheme="3d", size=size, scene=scene, sphere_radius=min(size) / 3.0,
                        sphere_center=tuple(v / 2.0 for v in size), dtype="f32", use_fused=True)
     a = _scheme(cfg, "hip", gpu, torch.float32)
@@ -50,6 +62,8 @@ def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec, rows, xcd):
     a.ops.tb_vec = vec
     a.ops.tb_rows = rows
     a.ops.tb_xcd = xcd
+    a.ops.tb_mrows = mrows
+    a.ops.tb_variant = variant
     b = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
     _randomize(a)
     _randomize(b)
@@ -71,7 +85,7 @@ def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec, rows, xcd):
         assert err <= 2e-5 * (float(y.abs().max()) + 1.0), (c, err)
 
 
-@pytest.mark.parametrize("T", [2, 3, 4])
+@pytest.mark.parametrize("T", [2, 3, 4, 5, 6])
 def test_tb_scheme_matches_fused(gpu, T):
     """Scheme-level: time_block=T over 11 steps == 11 single fused steps."""
     cfg = SchemeConfig(scheme="3d", size=(48, 40, 300), scene="vacuum", dtype="f32", use_fused=True,
