@@ -69,13 +69,17 @@ def main(argv=None) -> int:
         if rank == 0:
             print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
     backend, device = resolve_backend(a.backend, "auto")
+    # FDTD_BENCH_COMM=gloo rehearses the multi-rank path with several ranks on
+    # one GPU (RCCL refuses duplicate devices; gloo stages halos through host)
+    comm = os.environ.get("FDTD_BENCH_COMM", "nccl")
     if device == "cuda":
-        torch.cuda.set_device(local)
-        device = "cuda:%d" % local
+        dev_index = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_index)
+        device = "cuda:%d" % dev_index
     if world > 1:
         from fdtd3d_amd.parallel.comm import init_process_group
-        init_process_group("nccl" if device.startswith("cuda") else "gloo",
-                           device if device.startswith("cuda") else None)
+        use_nccl = device.startswith("cuda") and comm == "nccl"
+        init_process_group("nccl" if use_nccl else "gloo", device if use_nccl else None)
         # establish the communicator with a collective before the first
         # batched point-to-point exchange
         dist.barrier()

@@ -850,6 +850,23 @@ class YeeScheme:
         setattr(self, key, regions)
         return regions
 
+    def _fork_side_stream(self):
+        """High-priority side stream for the ghost exchange, ordered after
+        everything issued so far on the current stream (the pack must see the
+        previous pass's results) but NOT after the interior pass launched
+        next: that pass reads owned cells only (the ghosts it may touch lie
+        beyond its dependency cone) and writes the other buffer, so the
+        exchange runs concurrently with it.  None on the CPU."""
+        if self.device.type != "cuda":
+            return None
+        side = getattr(self, "_side_stream", None)
+        if side is None:
+            # high priority: its pack / unpack kernels get CUs next to the interior pass
+            side = torch.cuda.Stream(device=self.device, priority=-1)
+            self._side_stream = side
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        return side
+
     def _fused_step_overlap(self, t: int) -> None:
         """Decomposed fused step (``--buffer-size 1``): the interior update runs
         while the 1-deep ghost exchange (all axes, edges included) proceeds on
@@ -869,16 +886,9 @@ class YeeScheme:
                 src = (comp, li, self.source_value(t, p))
             srcs.append(src)
         interior = boxes_of(*regions[0])
+        side = self._fork_side_stream()
         for p in range(self.planes):
             self.ops.fused_step(self.F[p], self.F_alt[p], interior, self.cb, srcs[p])
-        side = None
-        if self.device.type == "cuda":
-            side = getattr(self, "_side_stream", None)
-            if side is None:
-                # high priority: its pack / unpack kernels get CUs next to the interior pass
-                side = torch.cuda.Stream(device=self.device, priority=-1)
-                self._side_stream = side
-            side.wait_stream(torch.cuda.current_stream(self.device))
         self.halo.exchange_all(self, stream=side)
         if side is not None:
             torch.cuda.current_stream(self.device).wait_stream(side)
@@ -980,19 +990,12 @@ class YeeScheme:
                 comp, li, _ = self.point_source
                 sp = [(comp, li, self.source_value(t + l, p)) for l in range(T)]
             srcs.append(sp)
+        side = self._fork_side_stream() if self.halo is not None else None
         for p in range(self.planes):
             if not box_empty(outs[0]):
                 with self.prof.phase("blocked-interior" if self.halo is not None else "blocked"):
                     self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
         if self.halo is not None:
-            side = None
-            if self.device.type == "cuda":
-                side = getattr(self, "_side_stream", None)
-                if side is None:
-                    side = torch.cuda.Stream(device=self.device, priority=-1)
-                    self._side_stream = side
-                # the side stream must see the previous pass's results
-                side.wait_stream(torch.cuda.current_stream(self.device))
             if side is not None and self.prof.enabled:
                 with torch.cuda.stream(side):
                     with self.prof.phase("halo-overlapped"):

@@ -18,14 +18,20 @@ MI355X, ``gloo`` on CPU):
   one-cell boundary slabs.  One message per neighbour per half step, no
   barriers.
 * ``buffer_size == B > 1`` -- *deep halo*.  Every ``B`` steps all state arrays
-  (fields and auxiliary UPML/Drude levels) exchange ``B``-deep ghosts, axis
-  after axis so that edges and corners are filled without 26 messages; the
+  (fields and auxiliary UPML/Drude levels) exchange ``B``-deep ghosts; the
   scheme computes redundantly in the ghost zone in between
-  (:meth:`fdtd3d_amd.parallel.domain.Domain.window`).
+  (:meth:`fdtd3d_amd.parallel.domain.Domain.window`).  Default ``direct``
+  mode: faces, edges and corners go straight to the face / edge / corner
+  neighbour (up to 26 messages, the reference's ``BUFFER_COUNT`` directions,
+  ``Source/Grid/BufferPosition.inc.h:8-61``) in ONE batched group -- a node's
+  8 GPUs are fully connected by xGMI, so every peer has its own link and one
+  round of concurrent transfers beats the ``sweep`` mode's three dependent
+  rounds (axis after axis, edges and corners relayed through the faces).
 """
 
 from __future__ import annotations
 
+import itertools
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -33,6 +39,7 @@ import torch.distributed as dist
 
 from .comm import P2P, DistComm
 from .domain import Domain, box_empty, box_intersect
+from .topology import coords_rank
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
@@ -50,7 +57,10 @@ def _face_components(layout, kind_needed: str, axis: int) -> List[str]:
 
 
 class HaloExchanger:
-    def __init__(self, domain: Domain, group=None, comm=None):
+    def __init__(self, domain: Domain, group=None, comm=None, mode: str = "direct"):
+        if mode not in ("direct", "sweep"):
+            raise ValueError("halo exchange mode must be direct or sweep")
+        self.mode = mode
         self.domain = domain
         self.group = group
         self.comm = comm if comm is not None else DistComm(group)
@@ -176,8 +186,9 @@ class HaloExchanger:
 
     # ------------------------------------------------------------ deep halo
     def exchange_all(self, scheme, stream=None) -> None:
-        """B-deep exchange of every state array, axis by axis (fills edges and
-        corners through the sequential sweep).  With ``stream`` the packing,
+        """B-deep exchange of every state array, edges and corners included
+        (``direct``: one batched round to up to 26 neighbours; ``sweep``: axis
+        by axis).  With ``stream`` the packing,
         RCCL transfers and unpacking are issued on that (side) stream so they
         overlap compute on the current stream."""
         if stream is not None:
@@ -187,6 +198,65 @@ class HaloExchanger:
             self._exchange_all(scheme)
 
     def _exchange_all(self, scheme) -> None:
+        if self.mode == "direct":
+            self._exchange_direct(scheme)
+        else:
+            self._exchange_sweep(scheme)
+
+    def deep_messages(self) -> List[Tuple[Tuple[int, int, int], int, Box, Box]]:
+        """(offset, peer, send box, recv box) of every neighbour of a direct
+        deep-halo exchange, global indices.  Along an axis the offset is
+        -1 (low side: send the first B owned layers, receive the B ghost
+        layers below), +1 (high side) or 0 (the owned range, which the peer
+        shares since it sits in the same rank column)."""
+        cached = getattr(self, "_deep_msgs", None)
+        if cached is not None:
+            return cached
+        d = self.domain
+        B = d.buffer_size
+        out = []
+        for off in itertools.product((-1, 0, 1), repeat=3):
+            if off == (0, 0, 0):
+                continue
+            c = [d.coords[a] + off[a] for a in range(3)]
+            if any(c[a] < 0 or c[a] >= d.topology[a] for a in range(3)):
+                continue
+            slo, shi, rlo, rhi = list(d.lo), list(d.hi), list(d.lo), list(d.hi)
+            for a in range(3):
+                if off[a] < 0:
+                    shi[a] = d.lo[a] + B
+                    rlo[a], rhi[a] = d.lo[a] - B, d.lo[a]
+                elif off[a] > 0:
+                    slo[a] = d.hi[a] - B
+                    rlo[a], rhi[a] = d.hi[a], d.hi[a] + B
+            out.append((off, coords_rank(c, d.topology), (tuple(slo), tuple(shi)), (tuple(rlo), tuple(rhi))))
+        self._deep_msgs = out
+        return out
+
+    def _exchange_direct(self, scheme) -> None:
+        ops = scheme.ops
+        tensors = scheme.state_tensors()
+        d = self.domain
+        ops_list, recvs = [], []
+        for off, peer, sg, rg in self.deep_messages():
+            sbox, rbox = d.to_local(sg), d.to_local(rg)
+            key = (off[0] + 1) * 9 + (off[1] + 1) * 3 + (off[2] + 1)
+            back = (-off[0] + 1) * 9 + (-off[1] + 1) * 3 + (-off[2] + 1)
+            sb = self._buf(("xs", key), _vol(sbox) * len(tensors), tensors[0])
+            _pack_many(ops, tensors, sbox, sb)
+            rb = self._buf(("xr", key), _vol(rbox) * len(tensors), tensors[0])
+            # the peer sends its message for offset -off with tag(-off)
+            ops_list.append(P2P(True, sb, peer, 300 + key))
+            ops_list.append(P2P(False, rb, peer, 300 + back))
+            recvs.append((rbox, rb))
+            self.bytes_sent += sb.numel() * sb.element_size()
+            self.messages += 1
+        for w in self._post(ops_list):
+            w.wait()
+        for rbox, rb in recvs:
+            _unpack_many(ops, tensors, rbox, rb)
+
+    def _exchange_sweep(self, scheme) -> None:
         d = self.domain
         B = d.buffer_size
         ops = scheme.ops

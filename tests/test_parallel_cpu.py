@@ -32,7 +32,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, cfg, topo_axes, buf, outdir):
+def _worker(rank, world, port, cfg, topo_axes, buf, outdir, mode="direct"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
@@ -41,7 +41,7 @@ def _worker(rank, world, port, cfg, topo_axes, buf, outdir):
         core = ParallelGridCore.create(cfg.size, world, topo_axes,
                                        active_axes=(0, 1, 2) if cfg.scheme == "3d" else ((0, 1) if cfg.scheme in ("tmz", "tez") else (0,)))
         dom = core.domain(rank, buf, align_z=4 if cfg.time_block > 1 else 1)
-        halo = HaloExchanger(dom)
+        halo = HaloExchanger(dom, mode=mode)
         s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64), dom, halo)
         s.init_scheme()
         s.init_grids()
@@ -61,9 +61,9 @@ def _worker(rank, world, port, cfg, topo_axes, buf, outdir):
         dist.destroy_process_group()
 
 
-def run_parallel(cfg, world, axes="xyz", buf=1):
+def run_parallel(cfg, world, axes="xyz", buf=1, mode="direct"):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), cfg, axes, buf, d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), cfg, axes, buf, d, mode), nprocs=world, join=True)
         return torch.load(os.path.join(d, "par.pt"), weights_only=True)
 
 
@@ -104,12 +104,20 @@ CASES = [
                              time_block=4), 4, "xy", 4),
     ("tb3-x2-sphere", SchemeConfig(scheme="3d", size=(22, 12, 16), time_steps=10, scene="sphere", sphere_radius=4,
                                    sphere_center=(11.0, 6.0, 8.0), use_fused=True, time_block=3), 2, "x", 3),
+    ("tb5-xy4", SchemeConfig(scheme="3d", size=(24, 26, 16), time_steps=12, scene="vacuum", use_fused=True,
+                             time_block=5), 4, "xy", 5),
+    # the axis-sweep deep-halo exchange (edges / corners relayed through faces)
+    ("sweep-deep-halo-xyz8-b2", SchemeConfig(scheme="3d", size=(16, 16, 16), time_steps=7, use_pml=True,
+                                             pml_size=(3, 3, 3)), 8, "xyz", 2, "sweep"),
+    ("sweep-tb4-xy4", SchemeConfig(scheme="3d", size=(20, 22, 16), time_steps=11, scene="vacuum", use_fused=True,
+                                   time_block=4), 4, "xy", 4, "sweep"),
 ]
 
 
-@pytest.mark.parametrize("name,cfg,world,axes,buf", CASES, ids=[c[0] for c in CASES])
-def test_decomposed_equals_serial(name, cfg, world, axes, buf):
-    par = run_parallel(cfg, world, axes, buf)
+@pytest.mark.parametrize("name,cfg,world,axes,buf,mode", [c if len(c) == 6 else c + ("direct",) for c in CASES],
+                         ids=[c[0] for c in CASES])
+def test_decomposed_equals_serial(name, cfg, world, axes, buf, mode):
+    par = run_parallel(cfg, world, axes, buf, mode)
     ser = run_serial(cfg)
     for p in range(ser.planes):
         for c in ser.comps:
