@@ -8,15 +8,17 @@ steps, then exactly K timed steps bracketed by barrier + device sync on both
 sides; the slowest rank's time is used; rank 0 prints one JSON line.
 
 Scaling is *strong*: the global grid stays 1024^3 and is decomposed over the
-GPUs (2 -> 2x1x1, 4 -> 2x2x1, 8 -> 2x2x2 by the halo-surface optimiser).
-Every timed step is the full leapfrog: E and H updates of all cells, the hard
-source and (N>1) the RCCL halo exchange.  By default four leapfrog steps run
-per HBM pass (``--time-block 4``, the temporally blocked kernel
-``csrc/yee3d_tb.hip``; decomposed runs then exchange 4-deep ghosts every four
-steps, overlapped with the interior pass); ``--time-block 1`` selects the
-single-pass fused kernel.  Odd step
-counts finish with one single-pass step, so exactly K steps are timed.  Fields start from zero plus the
-source -- the data dependence of the kernels is nil (pure streaming).
+GPUs on x and y (2 -> 2x1x1, 4 -> 2x2x1, 8 -> 4x2x1 by the halo-surface
+optimiser).  Every timed step is the full leapfrog: E and H updates of all
+cells, the hard source and (N>1) the RCCL halo exchange.  Several leapfrog
+steps run per HBM pass through the temporally blocked kernel
+(``csrc/yee3d_tb.hip``; automatic: 5 steps per pass, 4 when a rank's x or y
+extent is below 512); decomposed runs exchange T-deep ghosts with all face,
+edge and corner neighbours once per pass, overlapped with the interior pass.
+A step count that is not a multiple of T ends with one shorter pass, so
+exactly K steps are timed.  ``--time-block 1`` selects the single-pass fused
+kernel.  Fields start from zero plus the source -- the data dependence of the
+kernels is nil (pure streaming).
 """
 
 from __future__ import annotations
@@ -41,9 +43,9 @@ def main(argv=None) -> int:
     ap.add_argument("--split", action="store_true", help="use the split E / H kernels instead of the fused one")
     ap.add_argument("--xchunk", type=int, default=0)
     ap.add_argument("--buffer-size", type=int, default=1, help="halo depth (deep halo when > 1)")
-    ap.add_argument("--time-block", type=int, default=5,
-                    help="leapfrog steps per HBM pass (temporally blocked kernel); decomposed runs use a "
-                         "halo of the same depth")
+    ap.add_argument("--time-block", type=int, default=0,
+                    help="leapfrog steps per HBM pass (temporally blocked kernel; 0 automatic: 5, or 4 when a "
+                         "rank's x/y extent is below 512); decomposed runs use a halo of the same depth")
     ap.add_argument("--tb-xchunk", type=int, default=0, help="x planes per workgroup of the blocked kernel")
     ap.add_argument("--tb-vec", type=int, default=0, help="lane width of the blocked kernel (0 auto, 2, 4)")
     ap.add_argument("--tb-rows", type=int, default=0, help="grid rows per wave of the blocked kernel (0 auto, 1, 2)")
@@ -85,15 +87,25 @@ def main(argv=None) -> int:
         dist.barrier()
 
     size = tuple(a.size)
+    core = None
+    if world > 1:
+        # the blocked kernel tiles z in 54..60-cell rows, so a T-thick z shell
+        # would cost a whole tile row: decompose x and y only when blocking
+        core = ParallelGridCore.create(size, world, "xy" if a.time_block != 1 else "xyz")
+    if a.time_block <= 0:
+        # automatic: 5 steps per pass unless a rank's x or y extent drops
+        # below 512 (8 ranks on 1024^3: 4x2x1 -> 256x512x1024 per GPU), where
+        # the 5-deep ghosts and shells cost more than the saved HBM traffic
+        # (tools/decomp_cost.py: 8 ranks T=4 207-213k vs T=5 188-196k Mcells/s
+        # per GPU; 1-4 ranks T=5 ahead)
+        own = [size[d] // (core.topology[d] if core else 1) for d in range(3)]
+        a.time_block = 5 if min(own[0], own[1]) >= 512 else 4
     cfg = SchemeConfig(scheme="3d", size=size, time_steps=a.steps, scene="vacuum", dtype=a.dtype,
                        use_pml=False, use_tfsf=False, use_fused=not a.split, time_block=a.time_block)
     if a.time_block > 1 and world > 1:
         a.buffer_size = a.time_block
     dtype = torch.float32 if a.dtype == "f32" else torch.float64
     if world > 1:
-        # the blocked kernel tiles z in 248-cell rows, so a T-thick z shell would
-        # cost a whole tile row: decompose x and y only when blocking
-        core = ParallelGridCore.create(size, world, "xy" if a.time_block > 1 else "xyz")
         domain = core.domain(rank, a.buffer_size, align_z=4 if a.time_block > 1 else 1)
         halo = HaloExchanger(domain)
         topo = core.topology

@@ -549,6 +549,44 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   }
 }
 
+
+// x planes per workgroup.  A workgroup streams xchunk + 2T planes (T lead-in
+// and T drain planes are re-read), and every variant holds ONE 16-wave
+// workgroup per CU, so with uniform workgroups the pass takes
+// ceil(G / CUs) rounds of (xchunk + 2T) plane steps, G = (y, z tiles) x
+// ceil(nx / xchunk).  Pick the xchunk (nx split into k near-equal chunks)
+// minimising that: long chunks for big grids, many short ones for the thin
+// shells of a decomposed run (a 5-row y shell is 19 tiles: 13 chunks of 20
+// planes fill the chip in one round instead of one 266-plane workgroup per
+// tile).  1024^3, T=5: 512 planes (7 rounds) instead of 256 (14 rounds of
+// half the length, +2% tail).
+int g_num_cus = 0;
+int pick_xchunk(long long tiles_yz, int nxo, int T) {
+  if (g_num_cus <= 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus = n;
+    else
+      g_num_cus = 256;
+  }
+  if (nxo <= 0) return 1;
+  long long best_cost = -1;
+  int best = nxo;
+  for (int k = 1; k <= 256; ++k) {
+    const int xc = (nxo + k - 1) / k;
+    const long long chunks = (nxo + xc - 1) / xc;
+    const long long rounds = (tiles_yz * chunks + g_num_cus - 1) / g_num_cus;
+    const long long cost = rounds * (xc + 2LL * T);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best = xc;
+    }
+    if (xc == 1) break;
+  }
+  return best;
+}
+
 int g_tb_vec = 0;   // 0: automatic (float4 lanes for T <= 2, float2 above), else 2 / 4
 int g_tb_rows = 0;  // rows per wave: 0 automatic (1), 1 / 2
 int g_tb_xcd = 0;   // XCD-aware tile order (measured: no gain, T=2 slower; off by default)
@@ -669,13 +707,7 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
       const int HL = (steps + V - 1) / V;
       const long long gz = cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), (64 - 2 * HL) * V);
       const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
-      xchunk = 32;
-      for (int c : {256, 128, 64}) {
-        if (gz * gy * (long long)cdiv(O.hi[0] - O.lo[0], c) >= 1024) {
-          xchunk = c;
-          break;
-        }
-      }
+      xchunk = pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps);
     }
 #define MR_ARGS V, R, pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, src, sv, s
     switch (steps) {
@@ -690,20 +722,12 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
     return (int)hipErrorInvalidValue;
   }
   if (xchunk <= 0) {
-    // longest x chunk (fewest re-read halo planes) that still gives >= 4
-    // workgroups per CU of the 256 (tail of the last wave of workgroups)
     const int V = g_tb_vec ? g_tb_vec : (steps <= 2 ? 4 : 2);
     const int R = g_tb_rows ? g_tb_rows : 1;
     const int HL = (steps + V - 1) / V;
     const long long gz = cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), (64 / R - 2 * HL) * V);
     const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
-    xchunk = 32;
-    for (int c : {256, 128, 64}) {
-      if (gz * gy * (long long)cdiv(O.hi[0] - O.lo[0], c) >= 1024) {
-        xchunk = c;
-        break;
-      }
-    }
+    xchunk = pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps);
   }
   const int V = g_tb_vec ? g_tb_vec : (steps <= 2 ? 4 : 2);
   const int R = g_tb_rows ? g_tb_rows : 1;  // 2 rows per wave measured slower (228k vs 245k, T=4)

@@ -906,15 +906,18 @@ class YeeScheme:
 
     def advance(self, n: int) -> None:
         """``n`` leapfrog steps, ``self.tb`` at a time through the temporally
-        blocked kernel where possible (no per-step hooks), single fused steps
-        for the remainder."""
+        blocked kernel where possible (no per-step hooks; a tail shorter than
+        ``self.tb`` is one shorter pass), single fused steps otherwise."""
         T = self.tb
         if self.graph_mode and not self.hooks and n >= GRAPH_STEPS:
             n -= self._advance_graph(n)
         while n > 0:
-            if T > 1 and n >= T and not self.hooks and self.sub_step == 0:
-                self._tb_step(T)
-                n -= T
+            if T > 1 and not self.hooks and self.sub_step == 0:
+                # a short tail runs as one shorter blocked pass (its ghosts are
+                # T deep anyway), so the next call starts on a pass boundary
+                k = min(T, n)
+                self._tb_step(k)
+                n -= k
             else:
                 self.step()
                 n -= 1
@@ -953,10 +956,9 @@ class YeeScheme:
         interior (owned cells at least ``T`` from every neighbour -- needs no
         fresh ghost), then the ``T``-thick shell slabs peeled off axis by axis
         (disjoint), which run once the ghosts have arrived."""
-        key = "_tb_regions_cache"
-        cached = getattr(self, key, None)
-        if cached is not None:
-            return cached
+        cache = self.__dict__.setdefault("_tb_regions_cache", {})
+        if T in cache:
+            return cache[T]
         dom = self.domain
         upd = {c: self.local_box(c, dom.allocated_global()) for c in self.comps}
         lo, hi = list(dom.lo), list(dom.hi)
@@ -973,9 +975,8 @@ class YeeScheme:
                 shells.append((tuple(slo), tuple(shi)))
                 hi[a] -= T
         outs = [dom.to_local((tuple(lo), tuple(hi)))] + [dom.to_local(b) for b in shells if not box_empty(b)]
-        cached = (upd, outs)
-        setattr(self, key, cached)
-        return cached
+        cache[T] = (upd, outs)
+        return cache[T]
 
     def _tb_step(self, T: int) -> None:
         """``T`` steps in one blocked pass.  Decomposed runs overlap the

@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--rank", type=int, default=-1, help="-1: the rank with the most neighbours")
     ap.add_argument("--axes", default="xy")
-    ap.add_argument("--time-block", type=int, default=4)
+    ap.add_argument("--time-block", type=int, default=5)
+    ap.add_argument("--topology", type=int, nargs=3, default=None, help="force a rank grid (e.g. 4 2 1)")
     ap.add_argument("--steps", type=int, default=16)
     a = ap.parse_args()
     import torch
@@ -49,7 +50,10 @@ def main():
 
     T = a.time_block
     size = tuple(a.size)
-    core = ParallelGridCore.create(size, a.world, a.axes)
+    if a.topology:
+        core = ParallelGridCore.create(size, a.world, a.axes, requested=a.topology, optimal=False)
+    else:
+        core = ParallelGridCore.create(size, a.world, a.axes)
     rank = a.rank
     if rank < 0:
         def nn(r):
