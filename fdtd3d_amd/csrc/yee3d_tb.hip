@@ -700,7 +700,9 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   const bool pc = cbs[0] != nullptr;
   const float fcb = (float)cb, fdb = (float)db;
   // multi-row kernel: automatic from 4 steps on, required above 4
-  const int MR = g_tb_mrows ? g_tb_mrows : (steps >= 4 ? MR_AUTO_ROWS : 1);
+  // (per-cell coefficients: the single-row float2 kernel, whose coefficient
+  // loads are 8 B per lane; 512^3 sphere T=4 91k vs 85k Mcells/s multi-row)
+  const int MR = g_tb_mrows ? g_tb_mrows : (steps >= 4 && !pc ? MR_AUTO_ROWS : 1);
   if (MR > 1 || steps > 4) {
     const int R = 2, V = 1;
     if (xchunk <= 0) {

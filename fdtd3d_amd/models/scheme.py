@@ -279,8 +279,10 @@ class YeeScheme:
         # temporal blocking: T fused steps per pass (yee3d_tb.hip); decomposed
         # runs exchange T-deep ghosts every T steps (buffer size == T)
         T = int(cfg.time_block)
-        if T <= 0:  # automatic: 5 steps per pass (measured best at 1024^3) for the HIP fp32 path
-            T = 5 if (self.ops.name == "hip" and self.dtype == torch.float32) else 1
+        if T <= 0:  # automatic for the HIP fp32 path: 5 steps per pass (measured best at 1024^3),
+            # 4 with per-cell coefficients (the single-row kernel stops at 4)
+            percell = any(getattr(self.cb.get(c), "cell", None) is not None for c in self.comps)
+            T = (4 if percell else 5) if (self.ops.name == "hip" and self.dtype == torch.float32) else 1
             if self.halo is not None and self.domain.buffer_size != T:
                 T = 1
         self.tb = 1

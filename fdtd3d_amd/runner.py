@@ -75,8 +75,10 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
         buf = settings.bufferSize
         tb = settings.timeBlock
         if tb <= 0:  # automatic: blocked passes on the fp32 3D fused path
-            tb = 5 if (cfg.scheme == "3d" and cfg.dtype == "f32" and backend == "hip" and cfg.use_fused
-                       and not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials or cfg.use_amp_mode)) else 1
+            # (5 steps per pass with uniform materials, 4 with per-cell coefficients)
+            tb = (5 if cfg.scene == "vacuum" else 4) if (
+                cfg.scheme == "3d" and cfg.dtype == "f32" and backend == "hip" and cfg.use_fused
+                and not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials or cfg.use_amp_mode)) else 1
         if tb > 1 and cfg.scheme == "3d":
             buf = tb  # blocked passes exchange tb-deep ghosts every tb steps
         domain = core.domain(rank, buf, align_z=4 if tb > 1 else 1)
