@@ -101,15 +101,16 @@ __device__ __forceinline__ float4 comb(const float4& da, const float4& ca, const
                      (da.w + ca.w) - (db.w + cb_.w));
 }
 
-template <bool PERCELL>
+template <bool PERCELL, int LZ>
 __global__ __launch_bounds__(64 * TY) void k_update_e3d_cpml_v4(
     float* __restrict__ ex, float* __restrict__ ey, float* __restrict__ ez, const float* __restrict__ hx,
     const float* __restrict__ hy, const float* __restrict__ hz, const float* __restrict__ cbx,
     const float* __restrict__ cby, const float* __restrict__ cbz, float cb, int nx, int ny, int nz, Box3 bx,
     Box3 by, Box3 bz, Box3 bu, int xchunk, CpmlK P) {
-  const int lane = threadIdx.x;
-  const int kb = (bu.lo[2] & ~3) + 4 * (blockIdx.x * 64 + lane);
-  const int j = bu.lo[1] + blockIdx.y * TY + threadIdx.y;
+  // LZ lanes per z row, 64 / LZ rows per wave (LZ < 64 for z-thin boxes)
+  const int zl = threadIdx.x % LZ;
+  const int kb = (bu.lo[2] & ~3) + 4 * (blockIdx.x * LZ + zl);
+  const int j = bu.lo[1] + (blockIdx.y * TY + threadIdx.y) * (64 / LZ) + threadIdx.x / LZ;
   const bool act = (kb < bu.hi[2]) && (j < bu.hi[1]);
   const int i0 = bu.lo[0] + blockIdx.z * xchunk;
   const int i1 = min(i0 + xchunk, bu.hi[0]);
@@ -131,9 +132,9 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_cpml_v4(
       hyc = ld4(hy, off);
       hzc = ld4(hz, off);
     }
-    float hy_k0 = __shfl_up(hyc.w, 1, 64);
-    float hx_k0 = __shfl_up(hxc.w, 1, 64);
-    if (lane == 0 && act && kb > 0) {
+    float hy_k0 = __shfl_up(hyc.w, 1, LZ);
+    float hx_k0 = __shfl_up(hxc.w, 1, LZ);
+    if (zl == 0 && act && kb > 0) {
       hy_k0 = hy[off - 1];
       hx_k0 = hx[off - 1];
     }
@@ -175,15 +176,16 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_cpml_v4(
   }
 }
 
-template <bool PERCELL>
+template <bool PERCELL, int LZ>
 __global__ __launch_bounds__(64 * TY) void k_update_h3d_cpml_v4(
     float* __restrict__ hx, float* __restrict__ hy, float* __restrict__ hz, const float* __restrict__ ex,
     const float* __restrict__ ey, const float* __restrict__ ez, const float* __restrict__ dbx,
     const float* __restrict__ dby, const float* __restrict__ dbz, float db, int nx, int ny, int nz, Box3 bx,
     Box3 by, Box3 bz, Box3 bu, int xchunk, CpmlK P) {
-  const int lane = threadIdx.x;
-  const int kb = (bu.lo[2] & ~3) + 4 * (blockIdx.x * 64 + lane);
-  const int j = bu.lo[1] + blockIdx.y * TY + threadIdx.y;
+  // LZ lanes per z row, 64 / LZ rows per wave (LZ < 64 for z-thin boxes)
+  const int zl = threadIdx.x % LZ;
+  const int kb = (bu.lo[2] & ~3) + 4 * (blockIdx.x * LZ + zl);
+  const int j = bu.lo[1] + (blockIdx.y * TY + threadIdx.y) * (64 / LZ) + threadIdx.x / LZ;
   const bool act = (kb < bu.hi[2]) && (j < bu.hi[1]);
   const bool ld_ok = (kb < nz) && (j < ny);
   const int i0 = bu.lo[0] + blockIdx.z * xchunk;
@@ -208,9 +210,9 @@ __global__ __launch_bounds__(64 * TY) void k_update_h3d_cpml_v4(
         ez_n = ld4(ez, off + plane);
       }
     }
-    float ey_k3 = __shfl_down(ey_c.x, 1, 64);
-    float ex_k3 = __shfl_down(exc.x, 1, 64);
-    if (lane == 63 && act && kb + 4 < nz) {
+    float ey_k3 = __shfl_down(ey_c.x, 1, LZ);
+    float ex_k3 = __shfl_down(exc.x, 1, LZ);
+    if (zl == LZ - 1 && act && kb + 4 < nz) {
       ey_k3 = ey[off + 4];
       ex_k3 = ex[off + 4];
     }
@@ -272,10 +274,30 @@ CpmlK make_cpml(const void* const* P, const int* I) {
   return K;
 }
 
-inline dim3 grid_c(const Box3& bu, int xchunk) {
+// lanes per z row for a box: full 64-lane (256-cell) rows unless the box is
+// z-thin (PML / shell slabs normal to z), where short rows stacked 64 / LZ
+// per wave keep the lanes busy
+inline int lanes_z(const Box3& bu) {
   const int kspan = bu.hi[2] - (bu.lo[2] & ~3);
-  return dim3(cdiv(kspan, 256), cdiv(bu.hi[1] - bu.lo[1], TY), cdiv(bu.hi[0] - bu.lo[0], xchunk));
+  return kspan <= 32 ? 8 : (kspan <= 64 ? 16 : 64);
 }
+
+inline dim3 grid_c(const Box3& bu, int xchunk, int lz) {
+  const int kspan = bu.hi[2] - (bu.lo[2] & ~3);
+  return dim3(cdiv(kspan, 4 * lz), cdiv(bu.hi[1] - bu.lo[1], TY * (64 / lz)), cdiv(bu.hi[0] - bu.lo[0], xchunk));
+}
+
+// launch one split-kernel instantiation with the box's lane layout
+#define LAUNCH_LZ(KERNEL, PC, ...)                                                          \
+  do {                                                                                      \
+    const int lz_ = lanes_z(bu);                                                            \
+    if (lz_ == 8)                                                                           \
+      KERNEL<PC, 8><<<grid_c(bu, xchunk, 8), dim3(64, TY), 0, (hipStream_t)s>>>(__VA_ARGS__);   \
+    else if (lz_ == 16)                                                                     \
+      KERNEL<PC, 16><<<grid_c(bu, xchunk, 16), dim3(64, TY), 0, (hipStream_t)s>>>(__VA_ARGS__); \
+    else                                                                                    \
+      KERNEL<PC, 64><<<grid_c(bu, xchunk, 64), dim3(64, TY), 0, (hipStream_t)s>>>(__VA_ARGS__); \
+  } while (0)
 
 }  // namespace
 
@@ -292,11 +314,9 @@ FDTD_API int fdtd_update_e3d_cpml_v4_f32(float* ex, float* ey, float* ez, const 
   if (xchunk <= 0) xchunk = 16;
   const CpmlK K = make_cpml(cp, ci);
   if (cbx)
-    k_update_e3d_cpml_v4<true><<<grid_c(bu, xchunk), dim3(64, TY), 0, (hipStream_t)s>>>(
-        ex, ey, ez, hx, hy, hz, cbx, cby, cbz, (float)cb, nx, ny, nz, bx, by, bz, bu, xchunk, K);
+    LAUNCH_LZ(k_update_e3d_cpml_v4, true, ex, ey, ez, hx, hy, hz, cbx, cby, cbz, (float)cb, nx, ny, nz, bx, by, bz, bu, xchunk, K);
   else
-    k_update_e3d_cpml_v4<false><<<grid_c(bu, xchunk), dim3(64, TY), 0, (hipStream_t)s>>>(
-        ex, ey, ez, hx, hy, hz, cbx, cby, cbz, (float)cb, nx, ny, nz, bx, by, bz, bu, xchunk, K);
+    LAUNCH_LZ(k_update_e3d_cpml_v4, false, ex, ey, ez, hx, hy, hz, cbx, cby, cbz, (float)cb, nx, ny, nz, bx, by, bz, bu, xchunk, K);
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
@@ -311,10 +331,8 @@ FDTD_API int fdtd_update_h3d_cpml_v4_f32(float* hx, float* hy, float* hz, const 
   if (xchunk <= 0) xchunk = 16;
   const CpmlK K = make_cpml(cp, ci);
   if (dbx)
-    k_update_h3d_cpml_v4<true><<<grid_c(bu, xchunk), dim3(64, TY), 0, (hipStream_t)s>>>(
-        hx, hy, hz, ex, ey, ez, dbx, dby, dbz, (float)db, nx, ny, nz, bx, by, bz, bu, xchunk, K);
+    LAUNCH_LZ(k_update_h3d_cpml_v4, true, hx, hy, hz, ex, ey, ez, dbx, dby, dbz, (float)db, nx, ny, nz, bx, by, bz, bu, xchunk, K);
   else
-    k_update_h3d_cpml_v4<false><<<grid_c(bu, xchunk), dim3(64, TY), 0, (hipStream_t)s>>>(
-        hx, hy, hz, ex, ey, ez, dbx, dby, dbz, (float)db, nx, ny, nz, bx, by, bz, bu, xchunk, K);
+    LAUNCH_LZ(k_update_h3d_cpml_v4, false, hx, hy, hz, ex, ey, ez, dbx, dby, dbz, (float)db, nx, ny, nz, bx, by, bz, bu, xchunk, K);
   FDTD_RETURN_LAUNCH_STATUS();
 }

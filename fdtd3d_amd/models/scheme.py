@@ -94,6 +94,8 @@ class SchemeConfig:
     cpml_kappa_max: float = 1.0
     cpml_alpha_max: float = 0.0
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
+    hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
+                                             # (0 = auto: 4 on the HIP fp32 path, 1 = off)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
@@ -126,6 +128,7 @@ class SchemeConfig:
             ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
+            hybrid_block=s.hybridBlock,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
@@ -291,6 +294,8 @@ class YeeScheme:
                 and T <= getattr(self.ops, "tb_max_steps", 6)
                 and (self.halo is None or self.domain.buffer_size == T)):
             self.tb = T
+        self.hybrid = None
+        self._init_hybrid()
         self.initialized = True
         self.timers["init"] = time.perf_counter() - t0
 
@@ -570,16 +575,27 @@ class YeeScheme:
         w = self._window(kind)
         return {c: self.local_box(c, w) for c in comps}
 
-    def _update(self, kind: str, p: int, windows: Optional[Sequence[Box]] = None) -> None:
+    def _update(self, kind: str, p: int, windows: Optional[Sequence[Box]] = None, tfsf_once: bool = False) -> None:
         """Update all E (or H) components of plane ``p`` on the given global
-        windows (default: this sub-step's window)."""
+        windows (default: this sub-step's window).  ``tfsf_once``: apply the
+        E-form TF/SF corrections once over the whole grid after all windows
+        instead of per window (the hybrid shell: every target cell lies in
+        one of the windows, and per-window application costs a launch per
+        window, component and face)."""
         comps = self.e_comps if kind == "E" else self.h_comps
         F = self.F[p]
         if windows is None:
             windows = [self._window(kind)]
+        tfsf_here = self.cfg.use_tfsf and not tfsf_once
+        chain = self.use_upml_chain and getattr(self, "chain_regions", None) is not None
+        if chain and self.hybrid is not None and len(windows) > 1:
+            # hybrid shell: the chain boxes lie inside the shell, so each runs
+            # once, whole; only the plain slabs are cut to the shell windows
+            self._update_chain_regions(kind, p, None, tfsf_here, plain_windows=windows)
+            windows = []
         for w in windows:
-            if self.use_upml_chain and getattr(self, "chain_regions", None) is not None:
-                self._update_chain_regions(kind, p, w)
+            if chain:
+                self._update_chain_regions(kind, p, w, tfsf_here)
                 continue
             boxes = {c: self.local_box(c, w) for c in comps}
             if self.use_upml_chain:
@@ -593,16 +609,24 @@ class YeeScheme:
                 self.ops.curl_update(kind, boxes, F, F, self.cb)
                 if self.use_cpml:
                     self.cpml.apply(kind, p, boxes)
-            if self.cfg.use_tfsf:
+            if tfsf_here:
                 inc = self.hinc[p] if kind == "E" else self.einc[p]
                 for c in comps:
                     for tab in self.tfsf[c]:
                         self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
+        if self.cfg.use_tfsf and tfsf_once:
+            inc = self.hinc[p] if kind == "E" else self.einc[p]
+            alloc = self.domain.allocated_global()
+            for c in comps:
+                whole = self.local_box(c, alloc)
+                for tab in self.tfsf[c]:
+                    self.ops.tfsf_apply(F[c], tab, inc, whole)
         if self.use_upml_chain:
             for c in comps:
                 self._upml_rotate(c, p)
 
-    def _update_chain_regions(self, kind: str, p: int, w: Box) -> None:
+    def _update_chain_regions(self, kind: str, p: int, w: Optional[Box], tfsf_plain: bool = True,
+                              plain_windows: Optional[Sequence[Box]] = None) -> None:
         """UPML/Drude step on window ``w``: plain float4 Yee kernels on the
         plain slabs, the fused chain kernel on the chain boxes (components whose
         chain box holds TF/SF targets take the generic D-form path there)."""
@@ -612,17 +636,19 @@ class YeeScheme:
         tfsf = self.cfg.use_tfsf
         inc = (self.hinc[p] if kind == "E" else self.einc[p]) if tfsf else None
         reg = self.chain_regions[kind]
+        whole = dom.allocated_global()
         for r in reg["plain"]:
-            boxes = {c: dom.to_local(box_intersect(r[c], w)) for c in comps}
-            if all(box_empty(b) for b in boxes.values()):
-                continue
-            self.ops.curl_update(kind, boxes, F, F, self.cb)
-            if tfsf:
-                for c in comps:
-                    for tab in self.tfsf[c]:
-                        self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
+            for pw in (plain_windows if plain_windows is not None else [w]):
+                boxes = {c: dom.to_local(box_intersect(r[c], pw)) for c in comps}
+                if all(box_empty(b) for b in boxes.values()):
+                    continue
+                self.ops.curl_update(kind, boxes, F, F, self.cb)
+                if tfsf and tfsf_plain:
+                    for c in comps:
+                        for tab in self.tfsf[c]:
+                            self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
         for r, dru in reg["chain"]:
-            boxes = {c: dom.to_local(box_intersect(r[c], w)) for c in comps}
+            boxes = {c: dom.to_local(box_intersect(r[c], w if w is not None else whole)) for c in comps}
             if all(box_empty(b) for b in boxes.values()):
                 continue
             fast, slow = {}, []
@@ -733,9 +759,12 @@ class YeeScheme:
                     self.ops.set_value(self.F[p][comp], li, self.source_value(t, p))
 
     in_amplitude = False
+    _tfsf_once = False
 
-    def step(self) -> None:
-        """Advance one full leapfrog step."""
+    def step(self, windows: Optional[Sequence[Box]] = None) -> None:
+        """Advance one full leapfrog step (serial runs: optionally only on the
+        global ``windows``, disjoint boxes -- the stepped shell of a hybrid
+        blocked pass)."""
         t = self.t
         cfg = self.cfg
         B = self.domain.buffer_size
@@ -760,7 +789,7 @@ class YeeScheme:
                 if halo is not None and not deep:
                     halo.finish_and_update(self, "E", p)
                 else:
-                    self._update("E", p)
+                    self._update("E", p, windows, tfsf_once=windows is not None and self._tfsf_once)
             with ph("source"):
                 self._apply_sources(t, p)
             if halo is not None and not deep:
@@ -773,7 +802,7 @@ class YeeScheme:
                 if halo is not None and not deep:
                     halo.finish_and_update(self, "H", p)
                 else:
-                    self._update("H", p)
+                    self._update("H", p, windows, tfsf_once=windows is not None and self._tfsf_once)
             if halo is not None and not deep:
                 with ph("halo-post"):
                     halo.start(self, "H", p)
@@ -911,6 +940,12 @@ class YeeScheme:
         blocked kernel where possible (no per-step hooks; a tail shorter than
         ``self.tb`` is one shorter pass), single fused steps otherwise."""
         T = self.tb
+        if self.hybrid is not None and not self.hooks:
+            while n > 0:
+                k = min(self.hybrid["T"], n)
+                self._hybrid_step(k)
+                n -= k
+            return
         if self.graph_mode and not self.hooks and n >= GRAPH_STEPS:
             n -= self._advance_graph(n)
         while n > 0:
@@ -951,6 +986,166 @@ class YeeScheme:
         self.t = t0 + reps * G
         self._graph = (graph, tab, counter)  # keep alive until the stream has drained
         return reps * G
+
+    # ------------------------------------------------------ hybrid blocking
+    def _init_hybrid(self) -> None:
+        """Blocked core + stepped shell for 3D runs with absorbing layers,
+        TF/SF injection or dispersive media (serial HIP fp32 runs by default).
+
+        Every ``T`` steps: (1) the temporally blocked kernel advances the
+        *core* -- cells at least ``T + 2`` away from any PML / CPML slab,
+        TF/SF target cell and dispersive box -- by ``T`` steps in one HBM pass
+        (F -> F_alt); (2) the regular per-step kernels (UPML/Drude chain,
+        CPML, TF/SF corrections, sources) advance the *shell* (everything
+        else) plus a ``T + 1`` deep band into the core, in place in F: stale
+        values beyond the band corrupt at most ``T`` cells of it, all inside
+        the core, so the shell itself is exact; (3) the shell is copied into
+        F_alt and the buffers swap.  Bit-for-bit the same arithmetic as the
+        stepped run in both regions (the core's plain Yee update is what the
+        step kernels do there)."""
+        cfg = self.cfg
+        H = int(cfg.hybrid_block)
+        if H <= 0:
+            H = 4 if (self.ops.name == "hip" and self.dtype == torch.float32) else 1
+        if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme != "3d" or self.halo is not None
+                or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode
+                or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials)
+                or H > getattr(self.ops, "tb_max_steps", 6)):
+            return
+        if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
+            return
+        plan = self._hybrid_plan(H)
+        if plan is None:
+            return
+        if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.03 * self.cells():
+            # automatic mode: a large dispersive box splits the core into six
+            # slabs and moves its surroundings into the stepped shell -- slower
+            # than stepping everything (512^3 Drude sphere r=128: 37.8k vs 42k)
+            return
+        if not hasattr(self, "F_alt"):
+            self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+        self.hybrid = plan
+
+    def _hybrid_plan(self, T: int):
+        dom = self.domain
+        cfg = self.cfg
+        size = cfg.size
+        alloc = dom.allocated_global()
+        m = T + 2  # core margin to every irregular cell (staggering slack included)
+        lo, hi = [0, 0, 0], list(size)
+        for a in range(3):
+            edge = 0
+            if cfg.use_pml:
+                edge = max(edge, self.layout.pml_size[a])
+            if cfg.use_tfsf:
+                edge = max(edge, cfg.tfsf_size[a] + 1)
+            lo[a], hi[a] = edge + m, size[a] - edge - m
+        K = (tuple(lo), tuple(hi))
+        if box_empty(K):
+            return None
+        # dispersive boxes (chain boxes off the domain border) are cut out of the core
+        disp = []
+        if cfg.use_metamaterials and self.use_upml_chain:
+            for c in self.comps:
+                b = self._bbox_global(self.upml[c].get("drude_active"))
+                if not box_empty(b):
+                    disp.append(b)
+        D = None
+        for b in disp:
+            D = b if D is None else (tuple(min(D[0][d], b[0][d]) for d in range(3)),
+                                     tuple(max(D[1][d], b[1][d]) for d in range(3)))
+
+        def grow(b, n):
+            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
+
+        if D is not None:
+            Dm = box_intersect(grow(D, m), K)
+            couts = [b for b in box_subtract(K, Dm) if not box_empty(b)] if not box_empty(Dm) else [K]
+        else:
+            Dm = None
+            couts = [K]
+        couts = [b for b in couts if not box_empty(b)]
+        core_cells = sum(_vol(b) for b in couts)
+        if core_cells < 0.25 * size[0] * size[1] * size[2]:
+            return None
+        # verify: no irregular cell within T + 1 of an output box
+        irregular = []
+        if getattr(self, "chain_regions", None) is not None:
+            for kind in ("E", "H"):
+                for r, _ in self.chain_regions[kind]["chain"]:
+                    irregular += [b for b in r.values() if not box_empty(b)]
+        if self.use_cpml:
+            for slabs in self.cpml.slabs.values():
+                irregular += [sl.gbox for sl in slabs if not box_empty(sl.gbox)]
+        if self.use_upml_chain and getattr(self, "chain_regions", None) is None:
+            return None  # UPML without region split: every cell runs the chain
+        for ob in couts:
+            g = grow(ob, T + 1)
+            if any(not box_empty(box_intersect(g, b)) for b in irregular):
+                return None
+            if cfg.use_tfsf:
+                lg = dom.to_local(g)
+                for c in self.comps:
+                    for tab in self.tfsf[c]:
+                        if tab.n == 0:
+                            continue
+                        ijk = tab.ijk.view(-1, 3)
+                        inside = torch.ones(ijk.shape[0], dtype=torch.bool, device=ijk.device)
+                        for d in range(3):
+                            inside &= (ijk[:, d] >= lg[0][d]) & (ijk[:, d] < lg[1][d])
+                        if bool(inside.any()):
+                            return None
+        band = T + 1
+        Kb = (tuple(K[0][d] + band for d in range(3)), tuple(K[1][d] - band for d in range(3)))
+        if box_empty(Kb):
+            return None
+        shell_windows = [b for b in box_subtract(alloc, Kb) if not box_empty(b)]
+        if Dm is not None and not box_empty(Dm):
+            inner = box_intersect(grow(Dm, band), Kb)
+            if not box_empty(inner):
+                shell_windows.append(inner)
+        copy_boxes = [b for b in box_subtract(alloc, K) if not box_empty(b)]
+        if Dm is not None and not box_empty(Dm):
+            copy_boxes.append(Dm)
+        # TF/SF corrections once per half step, unless a component's TF/SF
+        # targets reach into a UPML chain box (D-form corrections there)
+        self._tfsf_once = bool(cfg.use_tfsf)
+        if cfg.use_tfsf and getattr(self, "chain_regions", None) is not None:
+            for kind in ("E", "H"):
+                for r, _ in self.chain_regions[kind]["chain"]:
+                    for c, b in r.items():
+                        tb = self.tfsf_bbox.get(c)
+                        if tb is not None and not box_empty(b) and not box_empty(box_intersect(dom.to_local(b), tb)):
+                            self._tfsf_once = False
+        upd = {c: self.local_box(c, alloc) for c in self.comps}
+        return {"T": T, "core": [dom.to_local(b) for b in couts], "shell": shell_windows,
+                "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
+                "cut_cells": _vol(Dm) if Dm is not None else 0}
+
+    def _hybrid_step(self, T: int) -> None:
+        hp = self.hybrid
+        t = self.t
+        srcs = []
+        for p in range(self.planes):
+            sp = None
+            if self.point_source is not None and self.point_source[1] is not None:
+                comp, li, _ = self.point_source
+                sp = [(comp, li, self.source_value(t + l, p)) for l in range(T)]
+            srcs.append(sp)
+        with self.prof.phase("blocked-core"):
+            for p in range(self.planes):
+                for ob in hp["core"]:
+                    self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
+        for _ in range(T):
+            self.step(hp["shell"])
+        with self.prof.phase("shell-copy"):
+            for p in range(self.planes):
+                for b in hp["copy"]:
+                    sl = tuple(slice(b[0][d], b[1][d]) for d in range(3))
+                    for c in self.comps:
+                        self.F_alt[p][c][sl] = self.F[p][c][sl]
+        for p in range(self.planes):
+            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
 
     def _tb_regions(self, T: int):
         """(update boxes, [output boxes]) of a blocked pass, local indices.
@@ -1091,3 +1286,9 @@ class YeeScheme:
         for v in self.cfg.size:
             n *= v
         return n
+
+
+def _vol(b: Box) -> int:
+    if box_empty(b):
+        return 0
+    return (b[1][0] - b[0][0]) * (b[1][1] - b[0][1]) * (b[1][2] - b[0][2])

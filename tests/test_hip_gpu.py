@@ -133,19 +133,35 @@ def test_fused_dielectric_complex_3d(gpu):
             1e-12)
 
 
-def test_vec4_windows_match_scalar(gpu):
+WINDOWS = {
+    # z span 37 -> 16 lanes per z row (4 rows per wave)
+    "mid": ({"Ex": ((2, 3, 5), (17, 21, 31)), "Ey": ((3, 1, 6), (19, 20, 33)), "Ez": ((1, 2, 1), (18, 22, 37))},
+            {"Hx": ((2, 3, 5), (17, 21, 31)), "Hy": ((3, 1, 6), (19, 20, 33)), "Hz": ((1, 2, 1), (18, 22, 38))}),
+    # z-thin slab (z span <= 32 -> 8 lanes per row, 8 rows per wave), high z end
+    "thin": ({"Ex": ((2, 3, 130), (17, 21, 149)), "Ey": ((3, 1, 131), (19, 20, 150)),
+              "Ez": ((1, 2, 129), (18, 22, 147))},
+             {"Hx": ((2, 3, 130), (17, 21, 150)), "Hy": ((3, 1, 131), (19, 20, 149)),
+              "Hz": ((1, 2, 129), (18, 22, 147))}),
+    # wide rows (64 lanes) with a partial last row
+    "wide": ({"Ex": ((2, 3, 5), (17, 21, 141)), "Ey": ((3, 1, 6), (19, 20, 143)), "Ez": ((1, 2, 1), (18, 22, 149))},
+             {"Hx": ((2, 3, 5), (17, 21, 141)), "Hy": ((3, 1, 6), (19, 20, 143)), "Hz": ((1, 2, 1), (18, 22, 148))}),
+}
+
+
+@pytest.mark.parametrize("win", sorted(WINDOWS))
+def test_vec4_windows_match_scalar(gpu, win):
     """float4 split kernels vs scalar split kernels on odd windows (box edges
-    not multiple of 4, lanes past the box feeding neighbours)."""
+    not multiple of 4, lanes past the box feeding neighbours, short z rows
+    stacked several per wave)."""
     from fdtd3d_amd.ops.hip_ops import HipOps
-    shape = (20, 24, 40)
+    shape = (20, 24, 152)
     torch.manual_seed(0)
     base = {c: torch.randn(shape, dtype=torch.float32, device=gpu) for c in
             ("Ex", "Ey", "Ez", "Hx", "Hy", "Hz")}
     from fdtd3d_amd.layout.yee import YeeLayout
     from fdtd3d_amd.ops.coef import Coef
     lay = YeeLayout(shape)
-    boxes_e = {"Ex": ((2, 3, 5), (17, 21, 31)), "Ey": ((3, 1, 6), (19, 20, 33)), "Ez": ((1, 2, 1), (18, 22, 37))}
-    boxes_h = {"Hx": ((2, 3, 5), (17, 21, 31)), "Hy": ((3, 1, 6), (19, 20, 33)), "Hz": ((1, 2, 1), (18, 22, 38))}
+    boxes_e, boxes_h = WINDOWS[win]
     cb = {c: Coef(0.3) for c in base}
     out = []
     for v4 in (False, True):

@@ -1,0 +1,52 @@
+"""Hybrid blocking on the GPU: blocked core (yee3d_tb.hip) + stepped shell
+(UPML chain / CPML / TF/SF kernels) vs the plain stepped HIP run, and vs the
+fp64 torch oracle."""
+import dataclasses
+
+import pytest
+import torch
+
+from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+from fdtd3d_amd.ops import make_ops
+
+pytestmark = pytest.mark.gpu
+
+BASE = dict(scheme="3d", size=(80, 72, 96), dtype="f32", pml_size=(5, 5, 5), tfsf_size=(8, 8, 8))
+
+CASES = [
+    ("upml-tfsf", dict(scene="vacuum", use_pml=True, use_tfsf=True, theta=40, phi=25, psi=15), 4, 13),
+    ("cpml-tfsf", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10, psi=5), 4, 12),
+    ("upml-point", dict(scene="vacuum", use_pml=True), 3, 10),
+    ("drude-upml", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, sphere_center=(40.0, 36.0, 48.0),
+                        sphere_radius=7.0), 4, 12),
+    ("sphere-cpml", dict(scene="sphere", use_pml=True, pml_type="cpml", sphere_center=(40.0, 36.0, 48.0),
+                         sphere_radius=10.0), 4, 9),
+]
+
+
+def _run(cfg, backend, device, dtype):
+    s = YeeScheme(cfg, make_ops(backend, None, device, dtype))
+    s.init_scheme()
+    s.init_grids()
+    s.perform_steps()
+    if device != "cpu":
+        torch.cuda.synchronize()
+    return s
+
+
+@pytest.mark.parametrize("name,extra,T,steps", CASES, ids=[c[0] for c in CASES])
+def test_hybrid_gpu(gpu, name, extra, T, steps):
+    cfg = SchemeConfig(time_steps=steps, **BASE, **extra)
+    hy = _run(dataclasses.replace(cfg, hybrid_block=T), "hip", gpu, torch.float32)
+    assert hy.hybrid is not None, "hybrid plan rejected"
+    st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, torch.float32)
+    assert st.hybrid is None
+    ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
+    for c in ref.comps:
+        r = ref.F[0][c]
+        # scale by the kind's largest component (a point Ez source leaves Hz ~ 0)
+        scale = max(float(ref.F[0][o].abs().max()) for o in ref.comps if o[0] == c[0]) + 1e-30
+        e_hy = float((hy.F[0][c].double().cpu() - st.F[0][c].double().cpu()).abs().max())
+        e_ref = float((hy.F[0][c].double().cpu() - r).abs().max())
+        assert e_hy <= 2e-5 * scale, (name, c, "hybrid vs stepped", e_hy, scale)
+        assert e_ref <= 2e-4 * scale, (name, c, "hybrid vs fp64 oracle", e_ref, scale)
