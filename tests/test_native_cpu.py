@@ -104,3 +104,26 @@ def test_cmake_configures_and_builds_host_runtime(tmp_path):
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert os.path.exists(os.path.join(b, "libfdtd3d_host.so"))
+
+
+def test_host_runtime_under_sanitizers(tmp_path):
+    """Host C++ runtime (settings parser, topology optimiser, DAT/BMP writers)
+    built with AddressSanitizer + UndefinedBehaviorSanitizer and exercised by
+    tests/native/host_selftest.cpp; any report aborts the run."""
+    import shutil
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(root, "fdtd3d_amd", "csrc")
+    exe = str(tmp_path / "host_selftest")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+           "-fno-sanitize-recover=all", "-I", csrc, os.path.join(root, "tests", "native", "host_selftest.cpp"),
+           os.path.join(csrc, "host_native.cpp"), os.path.join(csrc, "settings_native.cpp"), "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    # verify_asan_link_order=0: the environment may preload its own library ahead of the runtime
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "0 failed checks" in r.stdout
