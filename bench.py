@@ -100,6 +100,9 @@ def main(argv=None) -> int:
         # per GPU; 1-4 ranks T=5 ahead)
         own = [size[d] // (core.topology[d] if core else 1) for d in range(3)]
         a.time_block = 5 if min(own[0], own[1]) >= 512 else 4
+        if a.dtype == "f64":
+            from fdtd3d_amd.models.scheme import F64_AUTO_STEPS
+            a.time_block = F64_AUTO_STEPS
     cfg = SchemeConfig(scheme="3d", size=size, time_steps=a.steps, scene="vacuum", dtype=a.dtype,
                        use_pml=False, use_tfsf=False, use_fused=not a.split, time_block=a.time_block)
     if a.time_block > 1 and world > 1:

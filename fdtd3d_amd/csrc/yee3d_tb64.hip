@@ -1,0 +1,298 @@
+// Temporally blocked fp64 3D Yee kernel (the reference's default value type
+// is double, Source/Kernels/FieldValue.h:7-27).  Same wavefront as the fp32
+// multi-row kernel in yee3d_tb.hip (a level lags one x plane; y neighbours
+// between waves through a double-buffered LDS slot, one barrier per level; z
+// neighbours by DPP wave shifts), with scalar fp64 lanes: every carried
+// value takes two VGPRs, so one row per wave (two rows spill from T = 2 on):
+// 16-row x 64-lane tiles, T halo rows / lanes on each side.
+// A single-pass fp64 step moves >= 96 B/cell; T steps per pass read and write
+// the six fields once (plus the tile halos).
+
+#include "common.h"
+
+namespace {
+
+constexpr int TBW = 16;  // waves per workgroup
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ __forceinline__ Rsrc plane_rsrc64(const double* base, int x, int nx, size_t plane) {
+  const bool in = x >= 0 && x < nx;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)(in ? x : 0) * plane), (short)0,
+                                           in ? (int)(plane * 8) : 0, 0x00020000);
+}
+
+__device__ __forceinline__ double bld64(Rsrc r, unsigned boff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, boff, 0, 0));
+}
+
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void bst64(Rsrc r, unsigned boff, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, boff, 0, 0);
+}
+
+// DPP wave shifts of a double (two 32-bit halves): lane i gets lane i-1 (up)
+// or lane i+1 (dn); lanes shifted in from outside the wave read 0 (halo)
+__device__ __forceinline__ double lane_up64(double v) {
+  const u2 h = __builtin_bit_cast(u2, v);
+  u2 r;
+  r.x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)h.x, 0x138, 0xf, 0xf, false);
+  r.y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)h.y, 0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ double lane_dn64(double v) {
+  const u2 h = __builtin_bit_cast(u2, v);
+  u2 r;
+  r.x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)h.x, 0x130, 0xf, 0xf, false);
+  r.y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)h.y, 0x130, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, r);
+}
+
+__device__ __forceinline__ bool xin(const Box3& b, int x) { return x >= b.lo[0] && x < b.hi[0]; }
+__device__ __forceinline__ bool yzin(const Box3& b, int j, int k) {
+  return j >= b.lo[1] && j < b.hi[1] && k >= b.lo[2] && k < b.hi[2];
+}
+
+struct TbSrc64 {
+  double v[8];
+};
+
+struct F3d {
+  double x, y, z;
+};
+
+int g_num_cus64 = 0;
+
+// x chunk minimising rounds x (chunk + 2T) (same model as yee3d_tb.hip)
+int pick_xchunk64(long long tiles_yz, int nxo, int T) {
+  if (g_num_cus64 <= 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus64 = n;
+    else
+      g_num_cus64 = 256;
+  }
+  if (nxo <= 0) return 1;
+  long long best_cost = -1;
+  int best = nxo;
+  for (int k = 1; k <= 256; ++k) {
+    const int xc = (nxo + k - 1) / k;
+    const long long chunks = (nxo + xc - 1) / xc;
+    const long long rounds = (tiles_yz * chunks + g_num_cus64 - 1) / g_num_cus64;
+    const long long cost = rounds * (xc + 2LL * T);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best = xc;
+    }
+    if (xc == 1) break;
+  }
+  return best;
+}
+
+template <int T, int R, bool PERCELL>
+__global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
+    const double* __restrict__ exi, const double* __restrict__ eyi, const double* __restrict__ ezi,
+    const double* __restrict__ hxi, const double* __restrict__ hyi, const double* __restrict__ hzi,
+    double* __restrict__ exo, double* __restrict__ eyo, double* __restrict__ ezo,
+    double* __restrict__ hxo, double* __restrict__ hyo, double* __restrict__ hzo,
+    const double* __restrict__ cbx, const double* __restrict__ cby, const double* __restrict__ cbz,
+    const double* __restrict__ dbx, const double* __restrict__ dby, const double* __restrict__ dbz, double cb,
+    double db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
+    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc64 sv) {
+  constexpr int TBZ = 64 - 2 * T;  // owned z cells per tile
+  constexpr int ROWS = TBW * R;
+  __shared__ double sX[2][4][TBW][64];
+  const int lane = threadIdx.x;
+  const int w = threadIdx.y;
+  // XCD-contiguous tile order, z fastest (see yee3d_tb.hip)
+  int tz, ty, tx;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy * (int)gridDim.z;
+    const int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int n8 = n & ~7;
+    const int q = p < n8 ? (p & 7) * (n8 >> 3) + (p >> 3) : p;
+    tz = q % gx;
+    ty = (q / gx) % gy;
+    tx = q / (gx * gy);
+  }
+  const int k = O.lo[2] - T + TBZ * tz + lane;
+  const int jw = O.lo[1] - T + (ROWS - 2 * T) * ty + R * w;
+  const int i0 = O.lo[0] + tx * xchunk;
+  const int i1 = min(i0 + xchunk, O.hi[0]);
+  const bool kin = k >= 0 && k < nz;
+  const bool lane_own = lane >= T && lane < 64 - T;
+  const size_t plane = (size_t)ny * nz;
+  unsigned roff[R];
+  unsigned mbits = 0;  // bit r*7 + n: row r inside box n (n = 6: stored cells)
+  const Box3* bx[7] = {&bex, &bey, &bez, &bhx, &bhy, &bhz, &O};
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = jw + r;
+    const int t = R * w + r;
+    const bool ld_ok = kin && j >= 0 && j < ny;
+    roff[r] = ld_ok ? (unsigned)(j * nz + k) * 8u : 0xF0000000u;
+    const bool own = ld_ok && lane_own && t >= T && t < ROWS - T;
+#pragma unroll
+    for (int n = 0; n < 7; ++n) {
+      const bool ok = n < 6 ? ld_ok : own;
+      mbits |= (ok && yzin(*bx[n], j, k) ? 1u : 0u) << (r * 7 + n);
+    }
+  }
+  const int rdn = w > 0 ? w - 1 : 0;
+  const int rup = w < TBW - 1 ? w + 1 : TBW - 1;
+  auto coef = [&](const double* arr, const Box3& b, int p, int r, int n, double sc) -> double {
+    const bool in = xin(b, p) && ((mbits >> (r * 7 + n)) & 1u);
+    if (PERCELL) return in ? bld64(plane_rsrc64(arr, p, nx, plane), roff[r]) : 0.0;
+    return in ? sc : 0.0;
+  };
+  F3d Hp[T][R], Ep[T][R];
+#pragma unroll
+  for (int l = 0; l < T; ++l)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      Hp[l][r] = {0.0, 0.0, 0.0};
+      Ep[l][r] = {0.0, 0.0, 0.0};
+    }
+  int buf = 0;
+  auto load_plane = [&](int X, F3d* H, F3d* E) {
+    const Rsrc rhx = plane_rsrc64(hxi, X, nx, plane), rhy = plane_rsrc64(hyi, X, nx, plane);
+    const Rsrc rhz = plane_rsrc64(hzi, X, nx, plane), rex = plane_rsrc64(exi, X, nx, plane);
+    const Rsrc rey = plane_rsrc64(eyi, X, nx, plane), rez = plane_rsrc64(ezi, X, nx, plane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      H[r] = {bld64(rhx, roff[r]), bld64(rhy, roff[r]), bld64(rhz, roff[r])};
+      E[r] = {bld64(rex, roff[r]), bld64(rey, roff[r]), bld64(rez, roff[r])};
+    }
+  };
+  F3d Hnx[R], Enx[R];
+  load_plane(i0 - T, Hnx, Enx);
+  for (int X = i0 - T; X <= i1 + T - 1; ++X) {
+    F3d Hc[R], Ec[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      Hc[r] = Hnx[r];
+      Ec[r] = Enx[r];
+    }
+    load_plane(X + 1, Hnx, Enx);
+    F3d En[R];
+#pragma unroll
+    for (int l = 0; l < T; ++l) {
+      const int pe = X - l;
+      sX[buf][0][w][lane] = Hc[R - 1].z;
+      sX[buf][1][w][lane] = Hc[R - 1].x;
+      sX[buf][2][w][lane] = Ep[l][0].x;
+      sX[buf][3][w][lane] = Ep[l][0].z;
+      __syncthreads();
+      const double hz_dn = sX[buf][0][rdn][lane];
+      const double hx_dn = sX[buf][1][rdn][lane];
+      const double ex_up = sX[buf][2][rup][lane];
+      const double ez_up = sX[buf][3][rup][lane];
+      buf ^= 1;
+      const bool src_plane = src_comp >= 0 && pe == src_i;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double hz_j = r == 0 ? hz_dn : Hc[r > 0 ? r - 1 : 0].z;
+        const double hx_j = r == 0 ? hx_dn : Hc[r > 0 ? r - 1 : 0].x;
+        const double hy_k = lane_up64(Hc[r].y);
+        const double hx_k = lane_up64(Hc[r].x);
+        En[r].x = Ec[r].x + coef(cbx, bex, pe, r, 0, cb) * ((Hc[r].z - hz_j) - (Hc[r].y - hy_k));
+        En[r].y = Ec[r].y + coef(cby, bey, pe, r, 1, cb) * ((Hc[r].x - hx_k) - (Hc[r].z - Hp[l][r].z));
+        En[r].z = Ec[r].z + coef(cbz, bez, pe, r, 2, cb) * ((Hc[r].y - Hp[l][r].y) - (Hc[r].x - hx_j));
+        if (src_plane && jw + r == src_j && src_k == k) {
+          if (src_comp == 0) En[r].x = sv.v[l];
+          if (src_comp == 1) En[r].y = sv.v[l];
+          if (src_comp == 2) En[r].z = sv.v[l];
+        }
+      }
+      const int ph = pe - 1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double ex_jn = r == R - 1 ? ex_up : Ep[l][r < R - 1 ? r + 1 : r].x;
+        const double ez_jn = r == R - 1 ? ez_up : Ep[l][r < R - 1 ? r + 1 : r].z;
+        const double ey_k = lane_dn64(Ep[l][r].y);
+        const double ex_k = lane_dn64(Ep[l][r].x);
+        F3d Hn;
+        Hn.x = Hp[l][r].x + coef(dbx, bhx, ph, r, 3, db) * ((ey_k - Ep[l][r].y) - (ez_jn - Ep[l][r].z));
+        Hn.y = Hp[l][r].y + coef(dby, bhy, ph, r, 4, db) * ((En[r].z - Ep[l][r].z) - (ex_k - Ep[l][r].x));
+        Hn.z = Hp[l][r].z + coef(dbz, bhz, ph, r, 5, db) * ((ex_jn - Ep[l][r].x) - (En[r].y - Ep[l][r].y));
+        Ec[r] = Ep[l][r];
+        Ep[l][r] = En[r];
+        Hp[l][r] = Hc[r];
+        Hc[r] = Hn;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if ((mbits >> (r * 7 + 6)) & 1u) {
+        const int pe = X - T + 1;
+        if (pe >= i0 && pe < i1) {
+          bst64(plane_rsrc64(exo, pe, nx, plane), roff[r], En[r].x);
+          bst64(plane_rsrc64(eyo, pe, nx, plane), roff[r], En[r].y);
+          bst64(plane_rsrc64(ezo, pe, nx, plane), roff[r], En[r].z);
+        }
+        const int ph = X - T;
+        if (ph >= i0 && ph < i1) {
+          bst64(plane_rsrc64(hxo, ph, nx, plane), roff[r], Hc[r].x);
+          bst64(plane_rsrc64(hyo, ph, nx, plane), roff[r], Hc[r].y);
+          bst64(plane_rsrc64(hzo, ph, nx, plane), roff[r], Hc[r].z);
+        }
+      }
+    }
+  }
+}
+
+template <int T, int R>
+int launch_tb64(bool pc, const double* const* ein, const double* const* hin, double* const* eout,
+                double* const* hout, const double* const* cbs, const double* const* dbs, double cb, double db,
+                int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src,
+                const TbSrc64& sv, hipStream_t s) {
+  constexpr int TBZ = 64 - 2 * T;
+  const long long gz = cdiv(O.hi[2] - O.lo[2], TBZ);
+  const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * T);
+  if (xchunk <= 0) xchunk = pick_xchunk64(gz * gy, O.hi[0] - O.lo[0], T);
+  dim3 grid((unsigned)gz, (unsigned)gy, cdiv(O.hi[0] - O.lo[0], xchunk));
+#define TB64_ARGS                                                                                              \
+  ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2],      \
+      cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
+      O, xchunk, src[0], src[1], src[2], src[3], sv
+  if (pc)
+    k_tb3d_f64<T, R, true><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
+  else
+    k_tb3d_f64<T, R, false><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
+#undef TB64_ARGS
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+}  // namespace
+
+FDTD_API int fdtd_tb64_max_steps() { return 4; }
+
+// fp64 counterpart of fdtd_tb3d_v4_f32 (same arguments, double arrays), 1..4
+// steps per pass, any nz.
+FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, double* const* eout,
+                           double* const* hout, const double* const* cbs, const double* const* dbs, double cb,
+                           double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
+                           int steps, const int* src, const double* src_vals, void* stream) {
+  if (steps < 1 || steps > 4) return (int)hipErrorInvalidValue;
+  Box3 b[6];
+  for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
+  const Box3 O = make_box(obox);
+  if (box_empty(O)) return 0;
+  TbSrc64 sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? src_vals[l] : 0.0;
+  const bool pc = cbs[0] != nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  // one row per wave: two rows of fp64 state spill from T = 2 on
+#define TB64(TT) launch_tb64<TT, 1>(pc, ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s)
+  switch (steps) {
+    case 1: return TB64(1);
+    case 2: return TB64(2);
+    case 3: return TB64(3);
+    case 4: return TB64(4);
+  }
+#undef TB64
+  return (int)hipErrorInvalidValue;
+}

@@ -48,6 +48,8 @@ from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
 from ..utils import logging as log
 from .tfsf import build_tfsf_tables, incident_line_length
 
+F64_AUTO_STEPS = 4  # fp64 blocked kernel (yee3d_tb64.hip), 512^3: T=1 42.6k, 2 75.7k, 3 99.0k, 4 110k Mcells/s
+
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
 GRAPH_STEPS = 60  # steps per captured HIP graph (a multiple of 6: D/D1 level rotations return to the start)
@@ -285,11 +287,16 @@ class YeeScheme:
         if T <= 0:  # automatic for the HIP fp32 path: 5 steps per pass (measured best at 1024^3),
             # 4 with per-cell coefficients (the single-row kernel stops at 4)
             percell = any(getattr(self.cb.get(c), "cell", None) is not None for c in self.comps)
-            T = (4 if percell else 5) if (self.ops.name == "hip" and self.dtype == torch.float32) else 1
+            if self.ops.name != "hip":
+                T = 1
+            elif self.dtype == torch.float32:
+                T = 4 if percell else 5
+            else:
+                T = F64_AUTO_STEPS
             if self.halo is not None and self.domain.buffer_size != T:
                 T = 1
         self.tb = 1
-        hip_ok = self.ops.name != "hip" or (self.dtype == torch.float32 and self.domain.shape[2] % 4 == 0)
+        hip_ok = self.ops.name != "hip" or self.dtype == torch.float64 or self.domain.shape[2] % 4 == 0
         if (T > 1 and self.fused and hasattr(self.ops, "tb_step") and hip_ok
                 and T <= getattr(self.ops, "tb_max_steps", 6)
                 and (self.halo is None or self.domain.buffer_size == T)):
@@ -1006,13 +1013,13 @@ class YeeScheme:
         cfg = self.cfg
         H = int(cfg.hybrid_block)
         if H <= 0:
-            H = 4 if (self.ops.name == "hip" and self.dtype == torch.float32) else 1
+            H = (4 if self.dtype == torch.float32 else F64_AUTO_STEPS) if self.ops.name == "hip" else 1
         if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme != "3d" or self.halo is not None
                 or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode
                 or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials)
                 or H > getattr(self.ops, "tb_max_steps", 6)):
             return
-        if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
+        if self.ops.name == "hip" and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
             return
         plan = self._hybrid_plan(H)
         if plan is None:

@@ -28,6 +28,7 @@ Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
 _LIB = None
 TB_MAX_STEPS = 6  # steps per pass of the blocked kernels (fdtd_tb_max_steps)
+TB_MAX_STEPS_F64 = 4  # fp64 blocked kernel (fdtd_tb64_max_steps)
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libfdtd3d_hip.so")
 
 c_int = ctypes.c_int
@@ -487,11 +488,11 @@ class HipOps:
         ``sources`` = per-step list of (E component, local index, value) or
         None."""
         E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
-        if not (1 <= steps <= TB_MAX_STEPS):
-            raise HipError("tb_step supports 1..%d steps per pass" % TB_MAX_STEPS)
+        if not (1 <= steps <= self.tb_max_steps):
+            raise HipError("tb_step supports 1..%d steps per pass" % self.tb_max_steps)
         shape = tuple(fin["Ex"].shape)
-        if self.dtype != torch.float32 or shape[2] % 4 != 0:
-            raise HipError("tb_step needs fp32 fields with nz %% 4 == 0, got %s %s" % (self.dtype, shape))
+        if self.dtype == torch.float32 and shape[2] % 4 != 0:
+            raise HipError("fp32 tb_step needs nz %% 4 == 0, got %s" % (shape,))
         for c in E + H:
             self._check_tensor(fin[c], shape)
             self._check_tensor(fout[c], shape)
@@ -533,19 +534,24 @@ class HipOps:
                 vals[l] = float(s[2])
             src = [idx[0], idx[1], idx[2], E.index(comp)]
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
-        self.lib.fdtd_set_tb_vec(c_int(self.tb_vec))
-        self.lib.fdtd_set_tb_rows(c_int(self.tb_rows))
-        self.lib.fdtd_set_tb_xcd(c_int(self.tb_xcd))
-        self.lib.fdtd_set_tb_mrows(c_int(self.tb_mrows))
-        self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
-        rc = self.fn("tb3d_v4")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
+        if self.dtype == torch.float32:
+            self.lib.fdtd_set_tb_vec(c_int(self.tb_vec))
+            self.lib.fdtd_set_tb_rows(c_int(self.tb_rows))
+            self.lib.fdtd_set_tb_xcd(c_int(self.tb_xcd))
+            self.lib.fdtd_set_tb_mrows(c_int(self.tb_mrows))
+            self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
+        # fp32: yee3d_tb.hip (multi-row / single-row tiles); fp64: yee3d_tb64.hip
+        rc = self.fn("tb3d_v4" if self.dtype == torch.float32 else "tb3d")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
                                 c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk),
                                 c_int(steps), (c_int * 4)(*src), (c_double * 8)(*vals), _stream())
         _check(rc, "tb3d")
         self.launches += 1
 
-    tb_max_steps = TB_MAX_STEPS
+    @property
+    def tb_max_steps(self) -> int:
+        return TB_MAX_STEPS if self.dtype == torch.float32 else TB_MAX_STEPS_F64
+
     tb_xchunk = 0
     tb_vec = 0  # lane width of the blocked kernel: 0 auto (4 for T <= 2, 2 above), 2 or 4
     tb_rows = 0  # grid rows per wave: 0 auto (1), 1 or 2

@@ -76,8 +76,10 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
         tb = settings.timeBlock
         if tb <= 0:  # automatic: blocked passes on the fp32 3D fused path
             # (5 steps per pass with uniform materials, 4 with per-cell coefficients)
-            tb = (5 if cfg.scene == "vacuum" else 4) if (
-                cfg.scheme == "3d" and cfg.dtype == "f32" and backend == "hip" and cfg.use_fused
+            from .models.scheme import F64_AUTO_STEPS
+            per_dtype = (5 if cfg.scene == "vacuum" else 4) if cfg.dtype == "f32" else F64_AUTO_STEPS
+            tb = per_dtype if (
+                cfg.scheme == "3d" and backend == "hip" and cfg.use_fused
                 and not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials or cfg.use_amp_mode)) else 1
         if tb > 1 and cfg.scheme == "3d":
             buf = tb  # blocked passes exchange tb-deep ghosts every tb steps

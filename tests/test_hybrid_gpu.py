@@ -21,6 +21,7 @@ CASES = [
                         sphere_radius=7.0), 4, 12),
     ("sphere-cpml", dict(scene="sphere", use_pml=True, pml_type="cpml", sphere_center=(40.0, 36.0, 48.0),
                          sphere_radius=10.0), 4, 9),
+    ("upml-tfsf-f64", dict(scene="vacuum", use_pml=True, use_tfsf=True, theta=30, phi=40, psi=20, dtype="f64"), 4, 10),
 ]
 
 
@@ -36,10 +37,14 @@ def _run(cfg, backend, device, dtype):
 
 @pytest.mark.parametrize("name,extra,T,steps", CASES, ids=[c[0] for c in CASES])
 def test_hybrid_gpu(gpu, name, extra, T, steps):
-    cfg = SchemeConfig(time_steps=steps, **BASE, **extra)
-    hy = _run(dataclasses.replace(cfg, hybrid_block=T), "hip", gpu, torch.float32)
+    base = dict(BASE, **{k: v for k, v in extra.items() if k == "dtype"})
+    extra = {k: v for k, v in extra.items() if k != "dtype"}
+    cfg = SchemeConfig(time_steps=steps, **base, **extra)
+    dt = torch.float32 if cfg.dtype == "f32" else torch.float64
+    tol = 2e-5 if cfg.dtype == "f32" else 1e-12
+    hy = _run(dataclasses.replace(cfg, hybrid_block=T), "hip", gpu, dt)
     assert hy.hybrid is not None, "hybrid plan rejected"
-    st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, torch.float32)
+    st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, dt)
     assert st.hybrid is None
     ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
     for c in ref.comps:
@@ -48,5 +53,5 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
         scale = max(float(ref.F[0][o].abs().max()) for o in ref.comps if o[0] == c[0]) + 1e-30
         e_hy = float((hy.F[0][c].double().cpu() - st.F[0][c].double().cpu()).abs().max())
         e_ref = float((hy.F[0][c].double().cpu() - r).abs().max())
-        assert e_hy <= 2e-5 * scale, (name, c, "hybrid vs stepped", e_hy, scale)
-        assert e_ref <= 2e-4 * scale, (name, c, "hybrid vs fp64 oracle", e_ref, scale)
+        assert e_hy <= tol * scale, (name, c, "hybrid vs stepped", e_hy, scale)
+        assert e_ref <= 10 * tol * scale, (name, c, "hybrid vs fp64 oracle", e_ref, scale)

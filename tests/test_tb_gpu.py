@@ -100,3 +100,54 @@ def test_tb_scheme_matches_fused(gpu, T):
         x, y = a.F[0][c], b.F[0][c]
         err = float((x - y).abs().max())
         assert err <= 1e-6 * (float(y.abs().max()) + 1e-30), (c, err)
+
+
+F64_CASES = [
+    ((20, 30, 22), 2, "vacuum", None, True),
+    ((37, 29, 150), 3, "vacuum", None, True),      # 3 z tiles, 3 y tiles
+    ((40, 18, 61), 3, "sphere", None, False),      # per-cell coefficients, odd nz
+    ((24, 26, 28), 4, "vacuum", ((4, 4, 4), (20, 22, 24)), True),
+    ((20, 20, 36), 2, "vacuum", ((0, 0, 2), (20, 20, 4)), "shell"),
+]
+
+
+@pytest.mark.parametrize("size,T,scene,obox,src", F64_CASES)
+def test_tb_f64_vs_torch(gpu, size, T, scene, obox, src):
+    """fp64 blocked kernel (yee3d_tb64.hip) vs the fp64 torch oracle."""
+    cfg = SchemeConfig(scheme="3d", size=size, scene=scene, sphere_radius=min(size) / 3.0,
+                       sphere_center=tuple(v / 2.0 for v in size), dtype="f64", use_fused=True)
+    a = _scheme(cfg, "hip", gpu, torch.float64)
+    a.ops.tb_xchunk = 16
+    b = _scheme(cfg, "torch", "cpu", torch.float64)
+    _randomize(a)
+    _randomize(b)
+    upd = {c: a.local_box(c) for c in a.comps}
+    ob = obox if obox is not None else ((0, 0, 0), tuple(size))
+    srcs = None
+    if src == "shell":
+        srcs = [("Ez", (10, 10, 2), 0.5 + 0.25 * l) for l in range(T)]
+    elif src:
+        srcs = [("Ez", tuple(v // 2 for v in size), 0.5 + 0.25 * l) for l in range(T)]
+    a.ops.tb_step(a.F[0], a.F_alt[0], upd, ob, a.cb, T, srcs)
+    b.ops.tb_step(b.F[0], b.F_alt[0], upd, ob, b.cb, T, srcs)
+    torch.cuda.synchronize()
+    for c in a.comps:
+        x = a.F_alt[0][c].cpu()
+        y = b.F_alt[0][c]
+        err = float((x - y).abs().max())
+        assert err <= 1e-12 * (float(y.abs().max()) + 1.0), (c, err)
+
+
+@pytest.mark.parametrize("T", [2, 3, 4])
+def test_tb_f64_scheme_matches_fused(gpu, T):
+    cfg = SchemeConfig(scheme="3d", size=(40, 36, 90), scene="vacuum", dtype="f64", use_fused=True, time_steps=11)
+    a = _scheme(dataclasses.replace(cfg, time_block=T), "hip", gpu, torch.float64)
+    b = _scheme(cfg, "hip", gpu, torch.float64)
+    assert a.tb == T
+    a.perform_steps()
+    b.perform_steps()
+    torch.cuda.synchronize()
+    for c in a.comps:
+        x, y = a.F[0][c], b.F[0][c]
+        err = float((x - y).abs().max())
+        assert err <= 1e-12 * (float(y.abs().max()) + 1e-300), (c, err)
