@@ -42,6 +42,11 @@ int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, float* co
                      const int* boxes, const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
                      void* stream);
 int fdtd_tb_max_steps();
+int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, double* const* eout, double* const* hout,
+                  const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
+                  const int* boxes, const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
+                  void* stream);
+int fdtd_tb64_max_steps();
 
 int fdtd_tmz_e_f32(float* ez, const float* hx, const float* hy, const float* cbz, double cb, int nx, int ny,
                    const int* box, int xchunk, void* s);

@@ -111,16 +111,18 @@ int fused(const double* const* ei, const double* const* hi, double* const* eo, d
           const int* bx, long long so, int sc, double sv, void* s, bool) {
   return fdtd_fused3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s);
 }
-// temporally blocked pass (fp32 float4 only; yee3d_tb.hip)
+// temporally blocked pass (fp32: yee3d_tb.hip, fp64: yee3d_tb64.hip)
 int tb3d(const float* const* ei, const float* const* hi, float* const* eo, float* const* ho, const float* const* cbs,
          const float* const* dbs, double cb, double db, int nx, int ny, int nz, const int* bx, int T,
          const int* src, const double* vals, void* s) {
   const int ob[6] = {0, 0, 0, nx, ny, nz};
   return fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
 }
-int tb3d(const double* const*, const double* const*, double* const*, double* const*, const double* const*,
-         const double* const*, double, double, int, int, int, const int*, int, const int*, const double*, void*) {
-  return (int)hipErrorInvalidValue;
+int tb3d(const double* const* ei, const double* const* hi, double* const* eo, double* const* ho,
+         const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
+         const int* bx, int T, const int* src, const double* vals, void* s) {
+  const int ob[6] = {0, 0, 0, nx, ny, nz};
+  return fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
 }
 int setv(float* f, long long off, double v, void* s) { return fdtd_set_value_f32(f, off, v, s); }
 int setv(double* f, long long off, double v, void* s) { return fdtd_set_value_f64(f, off, v, s); }
@@ -284,8 +286,10 @@ int run(const fdtd::Settings& s) {
     }
   };
   // --time-block T: T steps per HBM pass through the blocked kernel
-  const int T_req = s.timeBlock <= 0 ? 5 : s.timeBlock;  // 0: automatic (5 steps per pass)
-  const int T_blk = (scheme == "3d" && use_fused && v4) ? std::max(1, std::min(fdtd_tb_max_steps(), T_req)) : 1;
+  // 0: automatic (5 steps per pass in fp32, 4 in fp64)
+  const int T_req = s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock;
+  const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
+  const int T_blk = (scheme == "3d" && use_fused && (v4 || sizeof(T) == 8)) ? std::max(1, std::min(T_max, T_req)) : 1;
   auto advance = [&](int t0, int n) {
     int t = t0;
     while (n > 0) {
