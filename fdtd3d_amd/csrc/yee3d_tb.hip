@@ -26,6 +26,8 @@
 // this launch stores) are separate: in a decomposed run the ghost layers are
 // updated redundantly at the inner levels but never stored.
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -108,7 +110,10 @@ __device__ __forceinline__ void bst(Rsrc r, unsigned boff, const typename VT<V>:
   }
 }
 
-__device__ __forceinline__ bool xin(const Box3& b, int x) { return x >= b.lo[0] && x < b.hi[0]; }
+// one unsigned compare (2 SALU) instead of two compares and an AND
+__device__ __forceinline__ bool xin(const Box3& b, int x) {
+  return (unsigned)(x - b.lo[0]) < (unsigned)(b.hi[0] - b.lo[0]);
+}
 
 // bit q set when element q of the lane's V-group (cells kb..kb+V-1) is in the box
 template <int V>
@@ -367,7 +372,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   // gets a contiguous run of tiles, z fastest, so z neighbours run together
   // on one L2 and the shared lines are fetched from HBM once.
   int tz = blockIdx.x, ty = blockIdx.y, tx = blockIdx.z;
-  if (xcd_swz) {
+  if (xcd_swz & 1) {
     const int gx = gridDim.x, gy = gridDim.y;
     const int n = gx * gy * (int)gridDim.z;
     const int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
@@ -404,8 +409,25 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   const int rup = w < TBW - 1 ? w + 1 : TBW - 1;
   const vec zero = (vec)(0.f);
   const vec cbv = (vec)(cb), dbv = (vec)(db);
+  // Tiles whose every lane and row lies inside all six update boxes in y / z
+  // (all but the tiles on the domain's y / z border) run a copy of the whole
+  // x loop in which a coefficient is just the x-range-selected scalar -- no
+  // per-element mask extraction and select (3 VALU per coefficient, ~40% of
+  // the kernel's VALU work).  The copy is of the OUTER loop, so the two
+  // versions never hold registers at the same time.
+  unsigned upd_bits = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) upd_bits |= ((1u << (6 * V)) - 1u) << (r * 7 * V);
+  const bool tile_all = __all((mbits & upd_bits) == upd_bits);
+
+  auto run = [&](auto allin_tag) {
+  constexpr bool ALLIN = decltype(allin_tag)::value;
   auto coef = [&](const float* arr, const Box3& b, int p, int r, int n, const vec& sc) -> vec {
     const bool in = xin(b, p);
+    if constexpr (ALLIN) {
+      if (PERCELL) return bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]);  // 0 outside the x range
+      return in ? sc : zero;
+    }
     const unsigned m = in ? (mbits >> ((r * 7 + n) * V)) & VM : 0u;
     if (PERCELL) return cmask<V>(bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]), m);
     return cmask<V>(sc, m);
@@ -547,6 +569,11 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
     for (int r = 0; r < R; ++r) Es[r] = Ep[T - 1][r];
     store_plane(i1 + T - 1, Es, Hs);
   }
+  };
+  if (tile_all && !(xcd_swz & 2))
+    run(std::true_type{});
+  else
+    run(std::false_type{});
 }
 
 
@@ -621,6 +648,7 @@ int launch_tb_pc(bool pc, const float* const* ein, const float* const* hin, floa
 constexpr int MR_AUTO_ROWS = 2;
 int g_tb_mrows = 0;  // rows per wave of the multi-row kernel: 0 automatic, 1 = single-row kernel, 2 / 4
 
+int g_tb_mr_noallin = 0;  // A/B knob: 1 = masked loop everywhere (no interior fast path)
 int g_tb_mr_xcd = 1;   // multi-row kernel: XCD-contiguous tile order, z fastest (-16..20% HBM reads)
 int g_tb_variant = 0;  // multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched
 
@@ -636,7 +664,7 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
   k_tb3d_mr<T, V, R, PERCELL, PFD, DEFER><<<grid, dim3(64, TBW), 0, s>>>(                                   \
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
-      O, xchunk, src[0], src[1], src[2], src[3], sv, g_tb_mr_xcd)
+      O, xchunk, src[0], src[1], src[2], src[3], sv, g_tb_mr_xcd | (g_tb_mr_noallin << 1))
   switch (g_tb_variant & 3) {
     case 0: MR_LAUNCH(1, false); break;
     case 1: MR_LAUNCH(1, true); break;
@@ -676,7 +704,8 @@ FDTD_API void fdtd_set_tb_mrows(int r) { g_tb_mrows = (r == 1 || r == 2) ? r : 0
 // prefetched, bit 2 XCD-contiguous tile order
 FDTD_API void fdtd_set_tb_variant(int v) {
   g_tb_variant = v & 3;
-  g_tb_mr_xcd = (v >> 2) & 1;  // bit 2: XCD-contiguous tile order
+  g_tb_mr_xcd = (v >> 2) & 1;      // bit 2: XCD-contiguous tile order
+  g_tb_mr_noallin = (v >> 3) & 1;  // bit 3: no interior fast path (A/B)
 }
 // largest steps-per-pass the blocked kernels accept
 FDTD_API int fdtd_tb_max_steps() { return 6; }
