@@ -45,24 +45,36 @@ struct FieldPtrs {
   T* p[8];
 };
 
+// Buffer layout [component][x][y][z].  grid.z walks (component, x plane) --
+// wave-uniform, so the field pointer is a scalar load -- and grid.x threads
+// walk the plane's (y, z) cells with ONE 32-bit divide each (the first
+// version decoded a 64-bit linear index per element with three 64-bit
+// divides, more instructions than the copy's memory time).
 template <typename T, bool PACK>
-__global__ void k_box_copy(FieldPtrs<T> fields, T* __restrict__ buf, int ncomp, int ny, int nz, Box3 b) {
+__global__ __launch_bounds__(256) void k_box_copy(FieldPtrs<T> fields, T* __restrict__ buf, int ny, int nz,
+                                                  Box3 b) {
   const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1], bz = b.hi[2] - b.lo[2];
-  const long long n = (long long)bx * by * bz;
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n * ncomp;
-       t += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(t / n);
-    long long r = t - (long long)c * n;
-    const int k = (int)(r % bz);
-    r /= bz;
-    const int j = (int)(r % by);
-    const int i = (int)(r / by);
-    const size_t off = ((size_t)(b.lo[0] + i) * ny + (b.lo[1] + j)) * nz + (b.lo[2] + k);
+  const int ci = blockIdx.z;  // component * bx + plane
+  const int c = ci / bx, i = ci - c * bx;
+  T* __restrict__ f = fields.p[c];
+  const int nyz = by * bz;
+  const size_t fplane = (size_t)(b.lo[0] + i) * ny;
+  const size_t bplane = (size_t)ci * nyz;
+  for (int jk = blockIdx.x * 256 + threadIdx.x; jk < nyz; jk += gridDim.x * 256) {
+    const int j = jk / bz, k = jk - j * bz;
+    const size_t off = (fplane + (b.lo[1] + j)) * nz + (b.lo[2] + k);
     if (PACK)
-      buf[t] = fields.p[c][off];
+      buf[bplane + jk] = f[off];
     else
-      fields.p[c][off] = buf[t];
+      f[off] = buf[bplane + jk];
   }
+}
+
+// grid of a box copy: up to 64 blocks of 256 threads per (component, plane)
+inline dim3 box_copy_grid(const Box3& b, int ncomp) {
+  const long long nyz = (long long)(b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]);
+  const long long per = (nyz + 255) / 256;
+  return dim3((unsigned)(per < 64 ? per : 64), 1, (unsigned)((b.hi[0] - b.lo[0]) * ncomp));
 }
 
 // ---------------------------------------------------------------- reductions
@@ -168,8 +180,8 @@ inline unsigned reduce_grid(long long n) {
     if (box_empty(b) || ncomp <= 0 || ncomp > 8) return ncomp > 8 ? (int)hipErrorInvalidValue : 0;             \
     FieldPtrs<T> fp;                                                                                          \
     for (int c = 0; c < ncomp; ++c) fp.p[c] = fields[c];                                                      \
-    long long n = (long long)(b.hi[0] - b.lo[0]) * (b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]) * ncomp;         \
-    k_box_copy<T, true><<<reduce_grid(n), 256, 0, (hipStream_t)s>>>(fp, buf, ncomp, ny, nz, b);            \
+    if ((long long)(b.hi[0] - b.lo[0]) * ncomp > 65535) return (int)hipErrorInvalidValue;                    \
+    k_box_copy<T, true><<<box_copy_grid(b, ncomp), 256, 0, (hipStream_t)s>>>(fp, buf, ny, nz, b);           \
     FDTD_RETURN_LAUNCH_STATUS();                                                                              \
   }                                                                                                           \
   FDTD_API int fdtd_box_unpack_##SUF(T* const* fields, const T* buf, int ncomp, int ny, int nz,                \
@@ -178,8 +190,8 @@ inline unsigned reduce_grid(long long n) {
     if (box_empty(b) || ncomp <= 0 || ncomp > 8) return ncomp > 8 ? (int)hipErrorInvalidValue : 0;             \
     FieldPtrs<T> fp;                                                                                          \
     for (int c = 0; c < ncomp; ++c) fp.p[c] = fields[c];                                                      \
-    long long n = (long long)(b.hi[0] - b.lo[0]) * (b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]) * ncomp;         \
-    k_box_copy<T, false><<<reduce_grid(n), 256, 0, (hipStream_t)s>>>(fp, (T*)buf, ncomp, ny, nz, b);       \
+    if ((long long)(b.hi[0] - b.lo[0]) * ncomp > 65535) return (int)hipErrorInvalidValue;                    \
+    k_box_copy<T, false><<<box_copy_grid(b, ncomp), 256, 0, (hipStream_t)s>>>(fp, (T*)buf, ny, nz, b);      \
     FDTD_RETURN_LAUNCH_STATUS();                                                                              \
   }                                                                                                           \
   FDTD_API int fdtd_box_maxabs_##SUF(const T* f, int ny, int nz, const int* box, unsigned int* out, void* s) { \

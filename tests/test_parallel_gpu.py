@@ -81,6 +81,12 @@ CASES = [
     ("tb2-z2-sphere", SchemeConfig(scheme="3d", size=(24, 30, 520), time_steps=8, scene="sphere", sphere_radius=9,
                                    sphere_center=(12.0, 15.0, 260.0), dtype="f32", use_fused=True, time_block=2),
      2, "z", 2),
+    # multi-row kernel (5 steps per pass, 5-deep ghosts, direct 26-neighbour exchange)
+    ("tb5-xy4", SchemeConfig(scheme="3d", size=(60, 56, 128), time_steps=13, scene="vacuum", dtype="f32",
+                             use_fused=True, time_block=5), 4, "xy", 5),
+    # fp64 blocked kernel
+    ("tb4-f64-xyz8", SchemeConfig(scheme="3d", size=(40, 36, 44), time_steps=10, scene="vacuum", dtype="f64",
+                                  use_fused=True, time_block=4), 8, "xyz", 4),
 ]
 
 
