@@ -1,0 +1,279 @@
+"""Temporal blocking of the 3D leapfrog (mixed into :class:`YeeScheme`).
+
+* ``_tb_step``: T leapfrog steps of plain 3D runs in ONE HBM pass through the
+  blocked kernels (``csrc/yee3d_tb.hip`` fp32, ``csrc/yee3d_tb64.hip`` fp64).
+  Decomposed runs exchange T-deep ghosts (faces, edges, corners) once per pass
+  on a high-priority side stream, overlapped with the interior pass, then
+  update the T-thick shells.
+* ``_hybrid_step``: runs with PML / TF-SF / dispersive media -- the blocked
+  kernel advances the core, the per-step kernels the shell plus a band.
+
+The reference has no counterpart: its only communication-avoiding scheme is
+the deep halo of ``--buffer-size`` (``Source/Grid/ParallelGrid.cpp:2161-2194,
+2365-2489``) with per-step CPU updates, and its CUDA path launches one kernel
+per component and step (``Source/Cuda/CudaInterface.cu:583-812``).
+"""
+
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from ..parallel.domain import box_empty, box_intersect, box_subtract, box_volume
+
+Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
+
+# automatic steps per pass of the fp64 blocked kernel (yee3d_tb64.hip);
+# 512^3: T=1 42.6k, 2 75.7k, 3 99.0k, 4 110k Mcells/s
+F64_AUTO_STEPS = 4
+
+
+class BlockedStepping:
+    """Blocked and hybrid passes of :class:`fdtd3d_amd.models.scheme.YeeScheme`
+    (uses its fields, ops, domain, halo, layout and per-step update methods)."""
+
+    _tfsf_once = False
+
+    def _fork_side_stream(self):
+        """High-priority side stream for the ghost exchange, ordered after
+        everything issued so far on the current stream (the pack must see the
+        previous pass's results) but NOT after the interior pass launched
+        next: that pass reads owned cells only (the ghosts it may touch lie
+        beyond its dependency cone) and writes the other buffer, so the
+        exchange runs concurrently with it.  None on the CPU."""
+        if self.device.type != "cuda":
+            return None
+        side = getattr(self, "_side_stream", None)
+        if side is None:
+            # high priority: its pack / unpack kernels get CUs next to the interior pass
+            side = torch.cuda.Stream(device=self.device, priority=-1)
+            self._side_stream = side
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        return side
+
+    # ------------------------------------------------------ hybrid blocking
+    def _init_hybrid(self) -> None:
+        """Blocked core + stepped shell for 3D runs with absorbing layers,
+        TF/SF injection or dispersive media (serial HIP fp32 runs by default).
+
+        Every ``T`` steps: (1) the temporally blocked kernel advances the
+        *core* -- cells at least ``T + 2`` away from any PML / CPML slab,
+        TF/SF target cell and dispersive box -- by ``T`` steps in one HBM pass
+        (F -> F_alt); (2) the regular per-step kernels (UPML/Drude chain,
+        CPML, TF/SF corrections, sources) advance the *shell* (everything
+        else) plus a ``T + 1`` deep band into the core, in place in F: stale
+        values beyond the band corrupt at most ``T`` cells of it, all inside
+        the core, so the shell itself is exact; (3) the shell is copied into
+        F_alt and the buffers swap.  Bit-for-bit the same arithmetic as the
+        stepped run in both regions (the core's plain Yee update is what the
+        step kernels do there)."""
+        cfg = self.cfg
+        H = int(cfg.hybrid_block)
+        if H <= 0:
+            H = (4 if self.dtype == torch.float32 else F64_AUTO_STEPS) if self.ops.name == "hip" else 1
+        if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme != "3d" or self.halo is not None
+                or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode
+                or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials)
+                or H > getattr(self.ops, "tb_max_steps", 6)):
+            return
+        if self.ops.name == "hip" and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
+            return
+        plan = self._hybrid_plan(H)
+        if plan is None:
+            return
+        if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.03 * self.cells():
+            # automatic mode: a large dispersive box splits the core into six
+            # slabs and moves its surroundings into the stepped shell -- slower
+            # than stepping everything (512^3 Drude sphere r=128: 37.8k vs 42k)
+            return
+        if not hasattr(self, "F_alt"):
+            self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+        self.hybrid = plan
+
+    def _hybrid_plan(self, T: int):
+        dom = self.domain
+        cfg = self.cfg
+        size = cfg.size
+        alloc = dom.allocated_global()
+        m = T + 2  # core margin to every irregular cell (staggering slack included)
+        lo, hi = [0, 0, 0], list(size)
+        for a in range(3):
+            edge = 0
+            if cfg.use_pml:
+                edge = max(edge, self.layout.pml_size[a])
+            if cfg.use_tfsf:
+                edge = max(edge, cfg.tfsf_size[a] + 1)
+            lo[a], hi[a] = edge + m, size[a] - edge - m
+        K = (tuple(lo), tuple(hi))
+        if box_empty(K):
+            return None
+        # dispersive boxes (chain boxes off the domain border) are cut out of the core
+        disp = []
+        if cfg.use_metamaterials and self.use_upml_chain:
+            for c in self.comps:
+                b = self._bbox_global(self.upml[c].get("drude_active"))
+                if not box_empty(b):
+                    disp.append(b)
+        D = None
+        for b in disp:
+            D = b if D is None else (tuple(min(D[0][d], b[0][d]) for d in range(3)),
+                                     tuple(max(D[1][d], b[1][d]) for d in range(3)))
+
+        def grow(b, n):
+            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
+
+        if D is not None:
+            Dm = box_intersect(grow(D, m), K)
+            couts = [b for b in box_subtract(K, Dm) if not box_empty(b)] if not box_empty(Dm) else [K]
+        else:
+            Dm = None
+            couts = [K]
+        couts = [b for b in couts if not box_empty(b)]
+        core_cells = sum(box_volume(b) for b in couts)
+        if core_cells < 0.25 * size[0] * size[1] * size[2]:
+            return None
+        # verify: no irregular cell within T + 1 of an output box
+        irregular = []
+        if getattr(self, "chain_regions", None) is not None:
+            for kind in ("E", "H"):
+                for r, _ in self.chain_regions[kind]["chain"]:
+                    irregular += [b for b in r.values() if not box_empty(b)]
+        if self.use_cpml:
+            for slabs in self.cpml.slabs.values():
+                irregular += [sl.gbox for sl in slabs if not box_empty(sl.gbox)]
+        if self.use_upml_chain and getattr(self, "chain_regions", None) is None:
+            return None  # UPML without region split: every cell runs the chain
+        for ob in couts:
+            g = grow(ob, T + 1)
+            if any(not box_empty(box_intersect(g, b)) for b in irregular):
+                return None
+            if cfg.use_tfsf:
+                lg = dom.to_local(g)
+                for c in self.comps:
+                    for tab in self.tfsf[c]:
+                        if tab.n == 0:
+                            continue
+                        ijk = tab.ijk.view(-1, 3)
+                        inside = torch.ones(ijk.shape[0], dtype=torch.bool, device=ijk.device)
+                        for d in range(3):
+                            inside &= (ijk[:, d] >= lg[0][d]) & (ijk[:, d] < lg[1][d])
+                        if bool(inside.any()):
+                            return None
+        band = T + 1
+        Kb = (tuple(K[0][d] + band for d in range(3)), tuple(K[1][d] - band for d in range(3)))
+        if box_empty(Kb):
+            return None
+        shell_windows = [b for b in box_subtract(alloc, Kb) if not box_empty(b)]
+        if Dm is not None and not box_empty(Dm):
+            inner = box_intersect(grow(Dm, band), Kb)
+            if not box_empty(inner):
+                shell_windows.append(inner)
+        copy_boxes = [b for b in box_subtract(alloc, K) if not box_empty(b)]
+        if Dm is not None and not box_empty(Dm):
+            copy_boxes.append(Dm)
+        # TF/SF corrections once per half step, unless a component's TF/SF
+        # targets reach into a UPML chain box (D-form corrections there)
+        self._tfsf_once = bool(cfg.use_tfsf)
+        if cfg.use_tfsf and getattr(self, "chain_regions", None) is not None:
+            for kind in ("E", "H"):
+                for r, _ in self.chain_regions[kind]["chain"]:
+                    for c, b in r.items():
+                        tb = self.tfsf_bbox.get(c)
+                        if tb is not None and not box_empty(b) and not box_empty(box_intersect(dom.to_local(b), tb)):
+                            self._tfsf_once = False
+        upd = {c: self.local_box(c, alloc) for c in self.comps}
+        return {"T": T, "core": [dom.to_local(b) for b in couts], "shell": shell_windows,
+                "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
+                "cut_cells": box_volume(Dm) if Dm is not None else 0}
+
+    def _pass_sources(self, t: int, T: int):
+        """Per plane: the hard point source's value at each of the pass's T
+        E half steps (None without a point source on this rank)."""
+        srcs = []
+        for p in range(self.planes):
+            sp = None
+            if self.point_source is not None and self.point_source[1] is not None:
+                comp, li, _ = self.point_source
+                sp = [(comp, li, self.source_value(t + l, p)) for l in range(T)]
+            srcs.append(sp)
+        return srcs
+
+    def _hybrid_step(self, T: int) -> None:
+        hp = self.hybrid
+        srcs = self._pass_sources(self.t, T)
+        with self.prof.phase("blocked-core"):
+            for p in range(self.planes):
+                for ob in hp["core"]:
+                    self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
+        for _ in range(T):
+            self.step(hp["shell"])
+        with self.prof.phase("shell-copy"):
+            for p in range(self.planes):
+                for b in hp["copy"]:
+                    sl = tuple(slice(b[0][d], b[1][d]) for d in range(3))
+                    for c in self.comps:
+                        self.F_alt[p][c][sl] = self.F[p][c][sl]
+        for p in range(self.planes):
+            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
+
+    # ----------------------------------------------------- plain blocking
+    def _tb_regions(self, T: int):
+        """(update boxes, [output boxes]) of a blocked pass, local indices.
+        Serial: one output box (the whole domain).  Decomposed: first the
+        interior (owned cells at least ``T`` from every neighbour -- needs no
+        fresh ghost), then the ``T``-thick shell slabs peeled off axis by axis
+        (disjoint), which run once the ghosts have arrived."""
+        cache = self.__dict__.setdefault("_tb_regions_cache", {})
+        if T in cache:
+            return cache[T]
+        dom = self.domain
+        upd = {c: self.local_box(c, dom.allocated_global()) for c in self.comps}
+        lo, hi = list(dom.lo), list(dom.hi)
+        shells = []
+        for a in range(3):
+            if dom.has_low(a):
+                slo, shi = list(lo), list(hi)
+                shi[a] = lo[a] + T
+                shells.append((tuple(slo), tuple(shi)))
+                lo[a] += T
+            if dom.has_high(a):
+                slo, shi = list(lo), list(hi)
+                slo[a] = hi[a] - T
+                shells.append((tuple(slo), tuple(shi)))
+                hi[a] -= T
+        outs = [dom.to_local((tuple(lo), tuple(hi)))] + [dom.to_local(b) for b in shells if not box_empty(b)]
+        cache[T] = (upd, outs)
+        return cache[T]
+
+    def _tb_step(self, T: int) -> None:
+        """``T`` steps in one blocked pass.  Decomposed runs overlap the
+        T-deep ghost exchange (side stream) with the interior pass and run the
+        shell slabs after it."""
+        upd, outs = self._tb_regions(T)
+        srcs = self._pass_sources(self.t, T)
+        side = self._fork_side_stream() if self.halo is not None else None
+        for p in range(self.planes):
+            if not box_empty(outs[0]):
+                with self.prof.phase("blocked-interior" if self.halo is not None else "blocked"):
+                    self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
+        if self.halo is not None:
+            if side is not None and self.prof.enabled:
+                with torch.cuda.stream(side):
+                    with self.prof.phase("halo-overlapped"):
+                        self.halo.exchange_all(self)
+            else:
+                with self.prof.phase("halo-overlapped"):
+                    self.halo.exchange_all(self, stream=side)
+            if side is not None:
+                torch.cuda.current_stream(self.device).wait_stream(side)
+            with self.prof.phase("blocked-shells"):
+                for ob in outs[1:]:
+                    for p in range(self.planes):
+                        self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p])
+        for p in range(self.planes):
+            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
+        self.t += T
+        if self.cfg.check_finite and (self.t // max(1, self.cfg.finite_check_step)
+                                      != (self.t - T) // max(1, self.cfg.finite_check_step)):
+            self.check_finite()
