@@ -47,6 +47,10 @@ int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, double* co
                   const int* boxes, const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
                   void* stream);
 int fdtd_tb64_max_steps();
+int fdtd_tb2d_f32(int mode, const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
+                  const float* const* cs, double cb, double db, int nx, int ny, const int* boxes, const int* obox,
+                  int xchunk, int steps, const int* src, const double* src_vals, void* stream);
+int fdtd_tb2d_max_steps();
 
 int fdtd_tmz_e_f32(float* ez, const float* hx, const float* hy, const float* cbz, double cb, int nx, int ny,
                    const int* box, int xchunk, void* s);

@@ -1,0 +1,266 @@
+// Temporally blocked 2D (TMz / TEz) Yee kernel: T leapfrog steps per HBM pass.
+//
+// The reference's 2D schemes update one component per sweep
+// (Source/Scheme/SchemeTMz.cpp:162-1309, SchemeTEz.cpp:109-1025; CUDA TMz:
+// Source/Cuda/CudaGlobalKernels.cu:5-153); a single-pass 2D step moves >= 24
+// B/cell (3 fields read + written) and the split E / H kernels 36 B.  Here a
+// wave owns a 256-cell run of one x row (64 lanes x float4 along the
+// contiguous y axis) and streams x; level l of iteration X updates E on row
+// X-l and H on row X-l-1 (the same one-row-per-level wavefront as the 3D
+// kernels), so T steps cost one read and one write of the three fields.
+// y neighbours come from the adjacent lane by DPP wave shifts; T halo cells
+// at each end of the run are recomputed redundantly.  Waves never talk to
+// each other: no LDS, no barriers.
+//
+//   TMz: Ez += cb ((Hy - Hy[x-1]) - (Hx - Hx[y-1])),  Hx += db (-(Ez[y+1] - Ez)),
+//        Hy += db (Ez[x+1] - Ez)                                      (Kernels.h:64-74)
+//   TEz: Ex += cb (Hz - Hz[y-1]),  Ey += cb (-(Hz - Hz[x-1])),
+//        Hz += db ((Ex[y+1] - Ex) - (Ey[x+1] - Ey))
+// Hard point source after the E half step on any of the three components
+// (an H source -- TEz's reference source is Hz -- is set before the H update).
+
+#include "common.h"
+
+namespace {
+
+constexpr int WPB = 4;  // independent waves per workgroup
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ __forceinline__ Rsrc row_rsrc(const float* base, int x, int nx, int ny) {
+  const bool in = x >= 0 && x < nx;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)(in ? x : 0) * ny), (short)0, in ? ny * 4 : 0,
+                                           0x00020000);
+}
+__device__ __forceinline__ f4v ld(Rsrc r, unsigned off) {
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void st(Rsrc r, unsigned off, const f4v& v, unsigned m) {
+  if (m == 0xFu) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, off, 0, 0);
+  } else if (m) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (m & (1u << q)) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), r, off + 4 * q, 0, 0);
+  }
+}
+__device__ __forceinline__ float up(float v) {  // value of lane - 1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dn(float v) {  // value of lane + 1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
+__device__ __forceinline__ f4v ym1(const f4v& v) { return f4v{up(v.w), v.x, v.y, v.z}; }
+__device__ __forceinline__ f4v yp1(const f4v& v) { return f4v{v.y, v.z, v.w, dn(v.x)}; }
+__device__ __forceinline__ unsigned ymask(const Box3& b, int x, int jb) {
+  if (x < b.lo[0] || x >= b.hi[0]) return 0u;
+  unsigned m = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) m |= (jb + e >= b.lo[1] && jb + e < b.hi[1]) ? (1u << e) : 0u;
+  return m;
+}
+__device__ __forceinline__ f4v sel(const f4v& c, unsigned m) {
+  return f4v{(m & 1u) ? c.x : 0.f, (m & 2u) ? c.y : 0.f, (m & 4u) ? c.z : 0.f, (m & 8u) ? c.w : 0.f};
+}
+
+struct Src2 {
+  float v[8];
+};
+
+// MODE 0 = TMz (E = {Ez}, H = {Hx, Hy}), 1 = TEz (E = {Ex, Ey}, H = {Hz}).
+// Arrays: e0 e1 (e1 unused in TMz), h0 h1 (h1 unused in TEz); boxes b[3] in
+// component order (TMz: Ez Hx Hy; TEz: Ex Ey Hz).
+template <int T, int MODE, bool PERCELL>
+__global__ __launch_bounds__(64 * WPB) void k_tb2d(const float* __restrict__ e0i, const float* __restrict__ e1i,
+                                                   const float* __restrict__ h0i, const float* __restrict__ h1i,
+                                                   float* __restrict__ e0o, float* __restrict__ e1o,
+                                                   float* __restrict__ h0o, float* __restrict__ h1o,
+                                                   const float* __restrict__ c0, const float* __restrict__ c1,
+                                                   const float* __restrict__ c2, float cb, float db, int nx, int ny,
+                                                   Box3 b0, Box3 b1, Box3 b2, Box3 O, int xchunk, int src_i,
+                                                   int src_j, int src_c, Src2 sv) {
+  constexpr int HL = (T + 3) / 4;        // halo lanes per side
+  constexpr int OWN = (64 - 2 * HL) * 4;  // owned cells per wave run
+  const int lane = threadIdx.x;
+  const int tile = blockIdx.x * WPB + threadIdx.y;
+  const int jb = (O.lo[1] & ~3) - 4 * HL + OWN * tile + 4 * lane;
+  if ((O.lo[1] & ~3) - 4 * HL + OWN * tile >= O.hi[1]) return;  // whole wave past the box (uniform)
+  const int i0 = O.lo[0] + (int)blockIdx.y * xchunk;
+  const int i1 = min(i0 + xchunk, O.hi[0]);
+  const bool ld_ok = jb >= 0 && jb < ny;
+  const unsigned off = ld_ok ? (unsigned)jb * 4u : 0xF0000000u;
+  const bool own = ld_ok && lane >= HL && lane < 64 - HL;
+  const bool src_hit = src_c >= 0 && src_j >= jb && src_j < jb + 4;
+  const f4v zero = {0.f, 0.f, 0.f, 0.f};
+  const f4v cbv = {cb, cb, cb, cb}, dbv = {db, db, db, db};
+  // coefficient of component n (0..2) on row x
+  auto coef = [&](const float* arr, const Box3& b, int x, const f4v& sc) -> f4v {
+    const unsigned m = ld_ok ? ymask(b, x, jb) : 0u;
+    if (PERCELL) return sel(ld(row_rsrc(arr, x, nx, ny), off), m);
+    return sel(sc, m);
+  };
+  // carried per level l: Hp = H_l(row X-1-l), Ep = E_{l+1}(row X-1-l)
+  f4v Hp0[T], Hp1[T], Ep0[T], Ep1[T];
+#pragma unroll
+  for (int l = 0; l < T; ++l) Hp0[l] = Hp1[l] = Ep0[l] = Ep1[l] = zero;
+  f4v nh0, nh1, ne0, ne1;  // next row in flight
+  auto load_row = [&](int X) {
+    nh0 = ld(row_rsrc(h0i, X, nx, ny), off);
+    ne0 = ld(row_rsrc(e0i, X, nx, ny), off);
+    if (MODE == 0) nh1 = ld(row_rsrc(h1i, X, nx, ny), off);
+    else ne1 = ld(row_rsrc(e1i, X, nx, ny), off);
+  };
+  load_row(i0 - T);
+  for (int X = i0 - T; X <= i1 + T - 1; ++X) {
+    f4v Hc0 = nh0, Hc1 = MODE == 0 ? nh1 : zero, Ec0 = ne0, Ec1 = MODE == 1 ? ne1 : zero;
+    load_row(X + 1);
+    f4v En0 = zero, En1 = zero;
+#pragma unroll
+    for (int l = 0; l < T; ++l) {
+      const int pe = X - l, ph = pe - 1;
+      if (MODE == 0) {
+        // Ez on row pe: Hc0 = Hx_l(pe), Hc1 = Hy_l(pe), Hp1 = Hy_l(pe-1)
+        En0 = Ec0 + coef(c0, b0, pe, cbv) * ((Hc1 - Hp1[l]) - (Hc0 - ym1(Hc0)));
+        if (src_c == 0 && pe == src_i && src_hit) En0[src_j - jb] = sv.v[l];
+        // hard Hx / Hy source on row ph before its H update (E of row pe above
+        // read the pre-source values)
+        f4v hx0 = Hp0[l], hy0 = Hp1[l];
+        if (src_c == 1 && ph == src_i && src_hit) hx0[src_j - jb] = sv.v[l];
+        if (src_c == 2 && ph == src_i && src_hit) hy0[src_j - jb] = sv.v[l];
+        // Hx, Hy on row ph: Ep0 = Ez_{l+1}(ph), En0 = Ez_{l+1}(pe)
+        const f4v hx = hx0 + coef(c1, b1, ph, dbv) * (-(yp1(Ep0[l]) - Ep0[l]));
+        const f4v hy = hy0 + coef(c2, b2, ph, dbv) * (En0 - Ep0[l]);
+        Ec0 = Ep0[l];
+        Ep0[l] = En0;
+        Hp0[l] = Hc0;
+        Hp1[l] = Hc1;
+        Hc0 = hx;
+        Hc1 = hy;
+      } else {
+        // Ex, Ey on row pe: Hc0 = Hz_l(pe), Hp0 = Hz_l(pe-1)
+        En0 = Ec0 + coef(c0, b0, pe, cbv) * (Hc0 - ym1(Hc0));
+        En1 = Ec1 + coef(c1, b1, pe, cbv) * (-(Hc0 - Hp0[l]));
+        // hard Hz source on row ph before its H update (the E update of row
+        // pe above read the pre-source Hz_l(ph) through Hp0)
+        f4v hz0 = Hp0[l];
+        if (src_c == 2 && ph == src_i && src_hit) hz0[src_j - jb] = sv.v[l];
+        if (src_c == 0 && pe == src_i && src_hit) En0[src_j - jb] = sv.v[l];
+        if (src_c == 1 && pe == src_i && src_hit) En1[src_j - jb] = sv.v[l];
+        // Hz on row ph: Ep0 = Ex_{l+1}(ph), Ep1 = Ey_{l+1}(ph), En1 = Ey_{l+1}(pe)
+        const f4v hz = hz0 + coef(c2, b2, ph, dbv) * ((yp1(Ep0[l]) - Ep0[l]) - (En1 - Ep1[l]));
+        Ec0 = Ep0[l];
+        Ec1 = Ep1[l];
+        Ep0[l] = En0;
+        Ep1[l] = En1;
+        Hp0[l] = Hc0;
+        Hc0 = hz;
+      }
+    }
+    // outputs: E_T on row X-T+1, H_T on row X-T
+    const int pe = X - T + 1, ph = X - T;
+    if (own) {
+      if (pe >= i0 && pe < i1) {
+        const unsigned m = ymask(O, pe, jb);
+        st(row_rsrc(e0o, pe, nx, ny), off, En0, m);
+        if (MODE == 1) st(row_rsrc(e1o, pe, nx, ny), off, En1, m);
+      }
+      if (ph >= i0 && ph < i1) {
+        const unsigned m = ymask(O, ph, jb);
+        st(row_rsrc(h0o, ph, nx, ny), off, Hc0, m);
+        if (MODE == 0) st(row_rsrc(h1o, ph, nx, ny), off, Hc1, m);
+      }
+    }
+  }
+}
+
+int g_num_cus2d = 0;
+
+int pick_xchunk2d(long long tiles, int nxo, int T) {
+  if (g_num_cus2d <= 0) {
+    int dev = 0, n = 0;
+    g_num_cus2d = (hipGetDevice(&dev) == hipSuccess &&
+                   hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                      ? n
+                      : 256;
+  }
+  // 4-wave workgroups, several per CU: aim at >= 8 workgroups per CU, then
+  // the longest chunk (fewest re-read lead-in rows)
+  const long long slots = 8LL * g_num_cus2d;
+  int best = nxo;
+  long long best_cost = -1;
+  for (int k = 1; k <= 512; ++k) {
+    const int xc = (nxo + k - 1) / k;
+    const long long chunks = (nxo + xc - 1) / xc;
+    const long long rounds = (tiles * chunks + slots - 1) / slots;
+    const long long cost = rounds * (xc + 2LL * T);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best = xc;
+    }
+    if (xc == 1) break;
+  }
+  return best;
+}
+
+template <int T, int MODE>
+int launch2d(bool pc, const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
+             const float* const* cs, float cb, float db, int nx, int ny, const Box3* b, const Box3& O, int xchunk,
+             const int* src, const Src2& sv, hipStream_t s) {
+  constexpr int HL = (T + 3) / 4;
+  constexpr int OWN = (64 - 2 * HL) * 4;
+  const long long tiles = cdiv(O.hi[1] - ((O.lo[1] & ~3) - 4 * HL) - 4 * HL, OWN);
+  if (xchunk <= 0) xchunk = pick_xchunk2d(cdiv(tiles, WPB), O.hi[0] - O.lo[0], T);
+  dim3 grid(cdiv(tiles, WPB), cdiv(O.hi[0] - O.lo[0], xchunk));
+#define K2D_ARGS                                                                                             \
+  ein[0], ein[1], hin[0], hin[1], eout[0], eout[1], hout[0], hout[1], cs[0], cs[1], cs[2], cb, db, nx, ny, b[0], \
+      b[1], b[2], O, xchunk, src[0], src[1], src[2], sv
+  if (pc)
+    k_tb2d<T, MODE, true><<<grid, dim3(64, WPB), 0, s>>>(K2D_ARGS);
+  else
+    k_tb2d<T, MODE, false><<<grid, dim3(64, WPB), 0, s>>>(K2D_ARGS);
+#undef K2D_ARGS
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <int MODE>
+int dispatch2d(int steps, bool pc, const float* const* ein, const float* const* hin, float* const* eout,
+               float* const* hout, const float* const* cs, float cb, float db, int nx, int ny, const Box3* b,
+               const Box3& O, int xchunk, const int* src, const Src2& sv, hipStream_t s) {
+#define C2D(TT) \
+  case TT: return launch2d<TT, MODE>(pc, ein, hin, eout, hout, cs, cb, db, nx, ny, b, O, xchunk, src, sv, s);
+  switch (steps) {
+    C2D(1) C2D(2) C2D(3) C2D(4) C2D(5) C2D(6) C2D(7) C2D(8)
+  }
+#undef C2D
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+FDTD_API int fdtd_tb2d_max_steps() { return 8; }
+
+// T (1..8) 2D leapfrog steps in one pass: mode 0 TMz (e = {Ez}, h = {Hx, Hy}),
+// 1 TEz (e = {Ex, Ey}, h = {Hz}); unused array slots may be null.  `cs` = 3
+// per-cell coefficient arrays in component order (all null: scalars cb / db),
+// `boxes` = 3 update boxes (lo[3] hi[3]) in component order, `obox` = cells
+// stored; `src` = {x, y, component 0..2 | -1} with one value per step.  ny
+// must be a multiple of 4 (float4 rows).
+FDTD_API int fdtd_tb2d_f32(int mode, const float* const* ein, const float* const* hin, float* const* eout,
+                           float* const* hout, const float* const* cs, double cb, double db, int nx, int ny,
+                           const int* boxes, const int* obox, int xchunk, int steps, const int* src,
+                           const double* src_vals, void* stream) {
+  if (ny % 4 != 0 || steps < 1 || steps > 8 || (mode != 0 && mode != 1)) return (int)hipErrorInvalidValue;
+  Box3 b[3];
+  for (int n = 0; n < 3; ++n) b[n] = make_box(boxes + 6 * n);
+  const Box3 O = make_box(obox);
+  if (O.hi[0] <= O.lo[0] || O.hi[1] <= O.lo[1]) return 0;
+  Src2 sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = (src[2] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
+  const bool pc = cs[0] != nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 0)
+    return dispatch2d<0>(steps, pc, ein, hin, eout, hout, cs, (float)cb, (float)db, nx, ny, b, O, xchunk, src, sv, s);
+  return dispatch2d<1>(steps, pc, ein, hin, eout, hout, cs, (float)cb, (float)db, nx, ny, b, O, xchunk, src, sv, s);
+}

@@ -27,6 +27,9 @@ Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 # automatic steps per pass of the fp64 blocked kernel (yee3d_tb64.hip);
 # 512^3: T=1 42.6k, 2 75.7k, 3 99.0k, 4 110k Mcells/s
 F64_AUTO_STEPS = 4
+# automatic steps per pass of the 2D TMz / TEz blocked kernel (yee2d_tb.hip);
+# 16384^2 fp32 TMz: T=1 119k, 5 851k, 6 1.01M, 7 1.11M, 8 1.06M Mcells/s
+TB2D_AUTO_STEPS = 7
 
 
 class BlockedStepping:

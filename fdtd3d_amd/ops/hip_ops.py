@@ -29,6 +29,8 @@ Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 _LIB = None
 TB_MAX_STEPS = 6  # steps per pass of the blocked kernels (fdtd_tb_max_steps)
 TB_MAX_STEPS_F64 = 4  # fp64 blocked kernel (fdtd_tb64_max_steps)
+TB2D_MAX_STEPS = 8  # 2D TMz / TEz blocked kernel, fp32 (fdtd_tb2d_max_steps)
+TB2D_MODES = {("Ez",): (0, ("Ez",), ("Hx", "Hy")), ("Ex", "Ey"): (1, ("Ex", "Ey"), ("Hz",))}
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libfdtd3d_hip.so")
 
 c_int = ctypes.c_int
@@ -487,6 +489,9 @@ class HipOps:
         give every stored cell ``steps`` valid layers of input around it.
         ``sources`` = per-step list of (E component, local index, value) or
         None."""
+        if len(fin) == 3:
+            self._tb2d_step(fin, fout, boxes, obox, cb, steps, sources)
+            return
         E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
         if not (1 <= steps <= self.tb_max_steps):
             raise HipError("tb_step supports 1..%d steps per pass" % self.tb_max_steps)
@@ -547,6 +552,66 @@ class HipOps:
                                 c_int(steps), (c_int * 4)(*src), (c_double * 8)(*vals), _stream())
         _check(rc, "tb3d")
         self.launches += 1
+
+    def _tb2d_step(self, fin, fout, boxes, obox, cb, steps, sources) -> None:
+        """2D (TMz / TEz) blocked pass (yee2d_tb.hip): fp32, (nx, ny, 1)
+        arrays with ny % 4 == 0; the point source may sit on any of the three
+        components (TEz's reference source is on Hz)."""
+        ecomps = tuple(c for c in ("Ex", "Ey", "Ez") if c in fin)
+        if ecomps not in TB2D_MODES or self.dtype != torch.float32:
+            raise HipError("2D tb_step: fp32 TMz (Ez, Hx, Hy) or TEz (Ex, Ey, Hz) only")
+        mode, E, H = TB2D_MODES[ecomps]
+        comps = E + H
+        if not (1 <= steps <= TB2D_MAX_STEPS):
+            raise HipError("2D tb_step supports 1..%d steps per pass" % TB2D_MAX_STEPS)
+        shape = tuple(fin[comps[0]].shape)
+        if len(shape) != 3 or shape[2] != 1 or shape[1] % 4 != 0:
+            raise HipError("2D tb_step needs (nx, ny, 1) arrays with ny %% 4 == 0, got %s" % (shape,))
+        for c in comps:
+            self._check_tensor(fin[c], shape)
+            self._check_tensor(fout[c], shape)
+            if fin[c].data_ptr() == fout[c].data_ptr():
+                raise HipError("tb_step needs distinct in/out buffers")
+            b = boxes[c]
+            for d in range(2):
+                if not _empty(b) and (b[0][d] < 0 or b[1][d] > shape[d]):
+                    raise HipError("update box %s of %s outside array %s" % (b, c, shape))
+        for d in range(2):
+            if obox[0][d] < 0 or obox[1][d] > shape[d]:
+                raise HipError("output box %s outside array %s" % (obox, shape))
+        if any(self._cell_or_none(cb[c]) is not None for c in comps):
+            cs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in comps])
+            cbv, dbv = 1.0, 1.0
+        else:
+            cs = (c_vp * 3)(None, None, None)
+            cbv, dbv = cb[E[0]].scalar, cb[H[0]].scalar
+            if any(cb[c].scalar != cbv for c in E) or any(cb[c].scalar != dbv for c in H):
+                raise HipError("tb_step: scalar coefficients must agree per kind")
+        src = [-1, -1, -1]
+        vals = [0.0] * 8
+        if sources is not None and any(s is not None for s in sources):
+            first = next(s for s in sources if s is not None)
+            comp, idx = first[0], tuple(first[1])
+            if comp not in comps:
+                raise HipError("2D tb_step: source component %s not in %s" % (comp, comps))
+            if not (0 <= idx[0] < shape[0] and 0 <= idx[1] < shape[1]):
+                raise HipError("source index outside array")
+            for l, s in enumerate(sources):
+                if s is None or s[0] != comp or tuple(s[1]) != idx:
+                    raise HipError("tb_step: the source must be the same point at every step")
+                vals[l] = float(s[2])
+            src = [idx[0], idx[1], comps.index(comp)]
+        two = lambda names, f: (c_vp * 2)(*([f[c].data_ptr() for c in names] + [None] * (2 - len(names))))
+        rc = self.lib.fdtd_tb2d_f32(c_int(mode), two(E, fin), two(H, fin), two(E, fout), two(H, fout), cs,
+                                    c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]),
+                                    _box_arr([boxes[c] for c in comps]), _box_arr([obox]), c_int(self.tb_xchunk),
+                                    c_int(steps), (c_int * 3)(*src), (c_double * 8)(*vals), _stream())
+        _check(rc, "tb2d")
+        self.launches += 1
+
+    @property
+    def tb2d_max_steps(self) -> int:
+        return TB2D_MAX_STEPS if self.dtype == torch.float32 else 0
 
     @property
     def tb_max_steps(self) -> int:
