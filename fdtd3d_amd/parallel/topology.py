@@ -146,11 +146,12 @@ class ParallelGridCore:
     def used_procs(self) -> int:
         return self.topology[0] * self.topology[1] * self.topology[2]
 
-    def domain(self, rank: int, buffer_size: int = 1, align_z: int = 1) -> Domain:
+    def domain(self, rank: int, buffer_size: int = 1, align_z: int = 1, align_axis: int = 2) -> Domain:
         """Sub-domain of ``rank``.  ``align_z`` > 1 pads the local allocation at
-        the high z end so that its z extent is a multiple of ``align_z`` (the
-        float4 kernels need nz % 4 == 0); padding cells are never owned,
-        exchanged or stored."""
+        the high end of ``align_axis`` (z; y for the 2D schemes, whose rows run
+        along y) so that its extent is a multiple of ``align_z`` (the float4
+        kernels need it % 4 == 0); padding cells are never owned, exchanged or
+        stored."""
         topo = self.topology
         c = rank_coords(rank, topo)
         lo, hi, nbr = [], [], []
@@ -171,8 +172,8 @@ class ParallelGridCore:
         gh = tuple(B if nbr[a][1] >= 0 else 0 for a in range(3))
         d = Domain(self.size, tuple(lo), tuple(hi), gl, gh, tuple(nbr), B, rank, c, topo)
         if align_z > 1:
-            nz = d.shape[2]
-            d.pad_hi = (0, 0, (-nz) % align_z)
+            n = d.shape[align_axis]
+            d.pad_hi = tuple((-n) % align_z if a == align_axis else 0 for a in range(3))
         return d
 
 

@@ -74,16 +74,22 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
             raise SystemExit("rank %d is unused by topology %s" % (rank, core.topology))
         buf = settings.bufferSize
         tb = settings.timeBlock
-        if tb <= 0:  # automatic: blocked passes on the fp32 3D fused path
-            # (5 steps per pass with uniform materials, 4 with per-cell coefficients)
-            from .models.scheme import F64_AUTO_STEPS
-            per_dtype = (5 if cfg.scene == "vacuum" else 4) if cfg.dtype == "f32" else F64_AUTO_STEPS
-            tb = per_dtype if (
-                cfg.scheme == "3d" and backend == "hip" and cfg.use_fused
-                and not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials or cfg.use_amp_mode)) else 1
-        if tb > 1 and cfg.scheme == "3d":
+        plain = (backend == "hip" and cfg.use_fused
+                 and not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials or cfg.use_amp_mode))
+        if tb <= 0:  # automatic: blocked passes on the plain 3D fused path
+            # (fp32: 5 steps per pass with uniform materials, 4 with per-cell
+            # coefficients) and the plain fp32 2D path
+            from .models.blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS
+            if cfg.scheme == "3d":
+                tb = ((5 if cfg.scene == "vacuum" else 4) if cfg.dtype == "f32" else F64_AUTO_STEPS) if plain else 1
+            elif cfg.scheme in ("tmz", "tez"):
+                tb = TB2D_AUTO_STEPS if plain and cfg.dtype == "f32" else 1
+            else:
+                tb = 1
+        if tb > 1 and cfg.scheme in ("3d", "tmz", "tez"):
             buf = tb  # blocked passes exchange tb-deep ghosts every tb steps
-        domain = core.domain(rank, buf, align_z=4 if tb > 1 else 1)
+        # float4 rows: z extent (3D) / y extent (2D) padded to a multiple of 4
+        domain = core.domain(rank, buf, align_z=4 if tb > 1 else 1, align_axis=2 if cfg.scheme == "3d" else 1)
         halo = HaloExchanger(domain)
     scheme = YeeScheme(cfg, ops, domain, halo)
     return scheme, halo, core

@@ -40,7 +40,8 @@ def _worker(rank, world, port, cfg, topo_axes, buf, outdir, mode="direct"):
     try:
         core = ParallelGridCore.create(cfg.size, world, topo_axes,
                                        active_axes=(0, 1, 2) if cfg.scheme == "3d" else ((0, 1) if cfg.scheme in ("tmz", "tez") else (0,)))
-        dom = core.domain(rank, buf, align_z=4 if cfg.time_block > 1 else 1)
+        dom = core.domain(rank, buf, align_z=4 if cfg.time_block > 1 else 1,
+                          align_axis=2 if cfg.scheme == "3d" else 1)
         halo = HaloExchanger(dom, mode=mode)
         s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64), dom, halo)
         s.init_scheme()
@@ -106,6 +107,11 @@ CASES = [
                                    sphere_center=(11.0, 6.0, 8.0), use_fused=True, time_block=3), 2, "x", 3),
     ("tb5-xy4", SchemeConfig(scheme="3d", size=(24, 26, 16), time_steps=12, scene="vacuum", use_fused=True,
                              time_block=5), 4, "xy", 5),
+    # 2D blocked passes (yee2d_tb.hip path): y extent padded to whole float4 rows
+    ("tmz-tb4-xy4", SchemeConfig(scheme="tmz", size=(40, 34, 1), time_steps=13, scene="vacuum", use_fused=True,
+                                 time_block=4), 4, "xy", 4),
+    ("tez-tb7-y2-complex", SchemeConfig(scheme="tez", size=(30, 50, 1), time_steps=16, scene="vacuum",
+                                        use_fused=True, complex_values=True, time_block=7), 2, "y", 7),
     # the axis-sweep deep-halo exchange (edges / corners relayed through faces)
     ("sweep-deep-halo-xyz8-b2", SchemeConfig(scheme="3d", size=(16, 16, 16), time_steps=7, use_pml=True,
                                              pml_size=(3, 3, 3)), 8, "xyz", 2, "sweep"),

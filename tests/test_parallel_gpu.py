@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 
 def run_threads(cfg, world, axes, buf, device):
-    core = ParallelGridCore.create(cfg.size, world, axes)
+    core = ParallelGridCore.create(cfg.size, world, axes, active_axes=(0, 1, 2) if cfg.scheme == "3d" else (0, 1))
     hub = LocalHub(world)
     dt = torch.float32 if cfg.dtype == "f32" else torch.float64
     schemes = [None] * world
@@ -32,7 +32,8 @@ def run_threads(cfg, world, axes, buf, device):
 
     def body(rank):
         try:
-            dom = core.domain(rank, buf, align_z=4 if cfg.time_block > 1 else 1)
+            dom = core.domain(rank, buf, align_z=4 if cfg.time_block > 1 else 1,
+                              align_axis=2 if cfg.scheme == "3d" else 1)
             halo = HaloExchanger(dom, comm=hub.comm(rank))
             s = YeeScheme(cfg, make_ops("hip", None, device, dt), dom, halo)
             s.init_scheme()
@@ -87,6 +88,11 @@ CASES = [
     # fp64 blocked kernel
     ("tb4-f64-xyz8", SchemeConfig(scheme="3d", size=(40, 36, 44), time_steps=10, scene="vacuum", dtype="f64",
                                   use_fused=True, time_block=4), 8, "xyz", 4),
+    # 2D blocked kernel (yee2d_tb.hip), local y extents padded to float4 rows
+    ("tmz-tb7-xy4", SchemeConfig(scheme="tmz", size=(300, 290, 1), time_steps=17, scene="vacuum", dtype="f32",
+                                 use_fused=True, time_block=7), 4, "xy", 7),
+    ("tez-tb6-y2", SchemeConfig(scheme="tez", size=(100, 522, 1), time_steps=15, scene="vacuum", dtype="f32",
+                                use_fused=True, time_block=6), 2, "y", 6),
 ]
 
 
