@@ -313,6 +313,16 @@ class YeeScheme(BlockedStepping):
                 and (self.halo is None or self.domain.buffer_size == T)):
             self.tb = T
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+        # 1D plain serial HIP runs: a whole advance() in one launch of the
+        # register-resident kernel (yee1d_res.hip) -- the per-step path is
+        # launch-bound at these sizes, HIP graphs included
+        self.res1d = (cfg.scheme == "1d" and self.ops.name == "hip" and cfg.use_fused
+                      and hasattr(self.ops, "resident_1d") and self.halo is None
+                      and not self.use_upml_chain and not self.use_cpml and not cfg.use_tfsf
+                      and not cfg.use_amp_mode and self.line_source is None
+                      and self.domain.shape[0] <= self.ops.resident_1d_max_cells())
+        if self.res1d:
+            self.graph_mode = False
         self.hybrid = None
         self._init_hybrid()
         self.initialized = True
@@ -585,6 +595,16 @@ class YeeScheme(BlockedStepping):
             return v if plane == 0 else 0.0
         arg = self.dt * t * 2 * PI * self.source_frequency
         return math.sin(arg) if plane == 0 else math.cos(arg)
+
+    def source_values(self, t0: int, n: int, plane: int) -> torch.Tensor:
+        """``source_value(t0 + s, plane)`` for s < n as one float64 tensor."""
+        cfg = self.cfg
+        t = torch.arange(t0, t0 + n, dtype=torch.float64)
+        if cfg.source == "gaussian":
+            v = torch.exp(-((t - cfg.gaussian_delay) / cfg.gaussian_width) ** 2)
+            return v if plane == 0 else torch.zeros_like(v)
+        arg = self.dt * t * 2 * PI * self.source_frequency
+        return torch.sin(arg) if plane == 0 else torch.cos(arg)
 
     # ================================================================ stepping
     def _window(self, kind: str) -> Box:
@@ -941,6 +961,9 @@ class YeeScheme(BlockedStepping):
         blocked kernel where possible (no per-step hooks; a tail shorter than
         ``self.tb`` is one shorter pass), single fused steps otherwise."""
         T = self.tb
+        if getattr(self, "res1d", False) and not self.hooks and n > 0:
+            self._resident_1d(n)
+            return
         if self.hybrid is not None and not self.hooks:
             while n > 0:
                 k = min(self.hybrid["T"], n)
@@ -959,6 +982,23 @@ class YeeScheme(BlockedStepping):
             else:
                 self.step()
                 n -= 1
+
+    def _resident_1d(self, n: int) -> None:
+        """``n`` 1D steps in one launch per plane (ops.resident_1d): per-step
+        source values go to the device as one table."""
+        boxes = {c: self.local_box(c, self._window(c[0])) for c in self.comps}
+        for p in range(self.planes):
+            vals, si = None, None
+            if self.point_source is not None and self.point_source[1] is not None:
+                comp, li, _ = self.point_source
+                fdtd_assert(comp == "Ez", "1D point source must drive Ez")
+                si = li[0]
+                vals = self.source_values(self.t, n, p).to(self.device, self.dtype)
+            with self.prof.phase("resident-1d"):
+                self.ops.resident_1d(self.F[p], boxes, self.cb, n, si, vals)
+        self.t += n
+        if self.cfg.check_finite:
+            self.check_finite()
 
     def _advance_graph(self, n: int) -> int:
         """Capture GRAPH_STEPS steps into one HIP graph and replay it

@@ -221,6 +221,43 @@ class HipOps:
         _check(rc, "%s %s update" % (scheme, kind))
         self.launches += 1
 
+    def resident_1d_max_cells(self) -> int:
+        return int(self.lib.fdtd_res1d_max_cells(c_int(self.dtype.itemsize)))
+
+    def resident_1d(self, F: Dict[str, torch.Tensor], boxes: Dict[str, Box], cb: Dict[str, Coef], nsteps: int,
+                    src_i: Optional[int] = None, vals: Optional[torch.Tensor] = None) -> None:
+        """``nsteps`` 1D leapfrog steps of (Ez, Hy) in place in ONE launch of
+        one register-resident workgroup (yee1d_res.hip); ``vals`` = device
+        tensor of the hard Ez source value at cell ``src_i`` for each step."""
+        ez, hy = F["Ez"], F["Hy"]
+        n = ez.numel()
+        self._check_tensor(ez, tuple(ez.shape))
+        self._check_tensor(hy, tuple(ez.shape))
+        if n > self.resident_1d_max_cells():
+            raise HipError("resident 1D kernel holds at most %d cells, got %d" % (self.resident_1d_max_cells(), n))
+        be, bh = boxes["Ez"], boxes["Hy"]
+        lim = lambda b: (b[0][0], b[1][0]) if not _empty(b) else (0, 0)
+        (elo, ehi), (hlo, hhi) = lim(be), lim(bh)
+        if (ehi > elo and (elo < 1 or ehi > n)) or (hhi > hlo and (hlo < 0 or hhi > n - 1)):
+            raise HipError("1D boxes %s / %s read outside %d cells" % (be, bh, n))
+        if self._cell_or_none(cb["Ez"]) is not None or self._cell_or_none(cb["Hy"]) is not None:
+            pe, ph = self._cell_array(cb["Ez"], tuple(ez.shape)), self._cell_array(cb["Hy"], tuple(ez.shape))
+            pe_p, ph_p, cbv, dbv = pe.data_ptr(), ph.data_ptr(), 1.0, 1.0
+        else:
+            pe_p, ph_p, cbv, dbv = None, None, cb["Ez"].scalar, cb["Hy"].scalar
+        vp = None
+        si = -1
+        if vals is not None:
+            if src_i is None or not (0 <= src_i < n) or vals.numel() < nsteps:
+                raise HipError("resident_1d: bad source (%s, %d values for %d steps)" % (src_i, vals.numel(), nsteps))
+            self._check_tensor(vals, tuple(vals.shape))
+            vp, si = vals.data_ptr(), int(src_i)
+        rc = self.fn("res1d")(c_vp(ez.data_ptr()), c_vp(hy.data_ptr()), c_vp(pe_p), c_vp(ph_p), c_double(cbv),
+                              c_double(dbv), c_int(n), (c_int * 4)(elo, ehi, hlo, hhi), c_int(nsteps), c_int(si),
+                              c_vp(vp), _stream())
+        _check(rc, "res1d")
+        self.launches += 1
+
     def fused_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
                    cb: Dict[str, Coef], source=None) -> None:
         """One fused E+H leapfrog step (yee3d.hip ``k_fused3d``): reads

@@ -109,6 +109,18 @@ class TorchOps:
                 sl = box_slices(b)
                 fout[c][sl] = tmp[c][sl]
 
+    def resident_1d(self, F: Dict[str, torch.Tensor], boxes: Dict[str, Box], cb: Dict[str, Coef], nsteps: int,
+                    src_i=None, vals=None) -> None:
+        """Reference semantics of the register-resident 1D kernel
+        (yee1d_res.hip): ``nsteps`` fused steps in place, hard Ez source
+        ``vals[s]`` at cell ``src_i``."""
+        for s in range(nsteps):
+            nxt = {c: F[c].clone() for c in F}
+            src = None if vals is None else ("Ez", (int(src_i), 0, 0), float(vals[s]))
+            self.fused_step(F, nxt, boxes, cb, src)
+            for c in F:
+                F[c].copy_(nxt[c])
+
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
                 obox: Box, cb: Dict[str, Coef], steps: int, sources=None) -> None:
         """Reference semantics of the temporally blocked kernel: ``steps``
