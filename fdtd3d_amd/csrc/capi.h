@@ -51,6 +51,15 @@ int fdtd_tb2d_f32(int mode, const float* const* ein, const float* const* hin, fl
                   const float* const* cs, double cb, double db, int nx, int ny, const int* boxes, const int* obox,
                   int xchunk, int steps, const int* src, const double* src_vals, void* stream);
 int fdtd_tb2d_max_steps();
+int fdtd_tb2d_f64(int mode, const double* const* ein, const double* const* hin, double* const* eout,
+                  double* const* hout, const double* const* cs, double cb, double db, int nx, int ny, const int* boxes,
+                  const int* obox, int xchunk, int steps, const int* src, const double* src_vals, void* stream);
+int fdtd_tb2d64_max_steps();
+int fdtd_res1d_f32(float* ez, float* hy, const float* cbz, const float* dby, double cb, double db, int n,
+                   const int* boxes, int nsteps, int src_i, const float* vals, void* s);
+int fdtd_res1d_f64(double* ez, double* hy, const double* cbz, const double* dby, double cb, double db, int n,
+                   const int* boxes, int nsteps, int src_i, const double* vals, void* s);
+int fdtd_res1d_max_cells(int elem_bytes);
 
 int fdtd_tmz_e_f32(float* ez, const float* hx, const float* hy, const float* cbz, double cb, int nx, int ny,
                    const int* box, int xchunk, void* s);

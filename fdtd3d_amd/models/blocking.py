@@ -30,6 +30,8 @@ F64_AUTO_STEPS = 4
 # automatic steps per pass of the 2D TMz / TEz blocked kernel (yee2d_tb.hip);
 # 16384^2 fp32 TMz: T=1 119k, 5 851k, 6 1.01M, 7 1.11M, 8 1.06M Mcells/s
 TB2D_AUTO_STEPS = 7
+# fp64: T=1 67k, 4 361k, 6 521k-638k, 7 701k, 8 630k Mcells/s
+TB2D_AUTO_STEPS_F64 = 7
 
 
 class BlockedStepping:

@@ -46,7 +46,7 @@ from ..parallel.domain import Domain, box_empty, box_intersect, box_subtract
 from ..utils.assertions import FdtdError, fdtd_assert
 from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
 from ..utils import logging as log
-from .blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, BlockedStepping
+from .blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64, BlockedStepping
 from .tfsf import build_tfsf_tables, incident_line_length
 
 
@@ -290,7 +290,7 @@ class YeeScheme(BlockedStepping):
             if self.ops.name != "hip":
                 T = 1
             elif cfg.scheme in ("tmz", "tez"):
-                T = TB2D_AUTO_STEPS
+                T = TB2D_AUTO_STEPS if self.dtype == torch.float32 else TB2D_AUTO_STEPS_F64
             elif self.dtype == torch.float32:
                 T = 4 if percell else 5
             else:
@@ -303,12 +303,12 @@ class YeeScheme(BlockedStepping):
                 and T <= getattr(self.ops, "tb_max_steps", 6)
                 and (self.halo is None or self.domain.buffer_size == T)):
             self.tb = T
-        # 2D (TMz / TEz) plain runs: the blocked pass of yee2d_tb.hip (fp32,
-        # ny % 4 == 0) or the generic oracle; F_alt is its ping-pong buffer
+        # 2D (TMz / TEz) plain runs: the blocked pass of yee2d_tb.hip (rows of
+        # whole 16-byte lanes) or the generic oracle; F_alt is its ping-pong buffer
         if (cfg.scheme in ("tmz", "tez") and T > 1 and cfg.use_fused and hasattr(self.ops, "tb_step")
                 and not self.use_upml_chain and not self.use_cpml and not cfg.use_tfsf and not cfg.use_amp_mode
                 and not self.graph_mode
-                and (self.ops.name != "hip" or (self.dtype == torch.float32 and self.domain.shape[1] % 4 == 0))
+                and (self.ops.name != "hip" or self.domain.shape[1] % (16 // self.dtype.itemsize) == 0)
                 and T <= getattr(self.ops, "tb2d_max_steps", 8)
                 and (self.halo is None or self.domain.buffer_size == T)):
             self.tb = T

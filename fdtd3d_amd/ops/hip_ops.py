@@ -30,6 +30,7 @@ _LIB = None
 TB_MAX_STEPS = 6  # steps per pass of the blocked kernels (fdtd_tb_max_steps)
 TB_MAX_STEPS_F64 = 4  # fp64 blocked kernel (fdtd_tb64_max_steps)
 TB2D_MAX_STEPS = 8  # 2D TMz / TEz blocked kernel, fp32 (fdtd_tb2d_max_steps)
+TB2D_MAX_STEPS_F64 = 8  # fp64 (fdtd_tb2d64_max_steps)
 TB2D_MODES = {("Ez",): (0, ("Ez",), ("Hx", "Hy")), ("Ex", "Ey"): (1, ("Ex", "Ey"), ("Hz",))}
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libfdtd3d_hip.so")
 
@@ -591,19 +592,21 @@ class HipOps:
         self.launches += 1
 
     def _tb2d_step(self, fin, fout, boxes, obox, cb, steps, sources) -> None:
-        """2D (TMz / TEz) blocked pass (yee2d_tb.hip): fp32, (nx, ny, 1)
-        arrays with ny % 4 == 0; the point source may sit on any of the three
-        components (TEz's reference source is on Hz)."""
+        """2D (TMz / TEz) blocked pass (yee2d_tb.hip): (nx, ny, 1) arrays
+        whose rows are whole 16-byte lanes (ny % 4 == 0 fp32, % 2 fp64); the
+        point source may sit on any of the three components (TEz's reference
+        source is on Hz)."""
         ecomps = tuple(c for c in ("Ex", "Ey", "Ez") if c in fin)
-        if ecomps not in TB2D_MODES or self.dtype != torch.float32:
-            raise HipError("2D tb_step: fp32 TMz (Ez, Hx, Hy) or TEz (Ex, Ey, Hz) only")
+        if ecomps not in TB2D_MODES:
+            raise HipError("2D tb_step: TMz (Ez, Hx, Hy) or TEz (Ex, Ey, Hz) only")
         mode, E, H = TB2D_MODES[ecomps]
         comps = E + H
-        if not (1 <= steps <= TB2D_MAX_STEPS):
-            raise HipError("2D tb_step supports 1..%d steps per pass" % TB2D_MAX_STEPS)
+        if not (1 <= steps <= self.tb2d_max_steps):
+            raise HipError("2D tb_step supports 1..%d steps per pass" % self.tb2d_max_steps)
         shape = tuple(fin[comps[0]].shape)
-        if len(shape) != 3 or shape[2] != 1 or shape[1] % 4 != 0:
-            raise HipError("2D tb_step needs (nx, ny, 1) arrays with ny %% 4 == 0, got %s" % (shape,))
+        vec = 16 // self.dtype.itemsize
+        if len(shape) != 3 or shape[2] != 1 or shape[1] % vec != 0:
+            raise HipError("2D tb_step needs (nx, ny, 1) arrays with ny %% %d == 0, got %s" % (vec, shape))
         for c in comps:
             self._check_tensor(fin[c], shape)
             self._check_tensor(fout[c], shape)
@@ -639,7 +642,7 @@ class HipOps:
                 vals[l] = float(s[2])
             src = [idx[0], idx[1], comps.index(comp)]
         two = lambda names, f: (c_vp * 2)(*([f[c].data_ptr() for c in names] + [None] * (2 - len(names))))
-        rc = self.lib.fdtd_tb2d_f32(c_int(mode), two(E, fin), two(H, fin), two(E, fout), two(H, fout), cs,
+        rc = self.fn("tb2d")(c_int(mode), two(E, fin), two(H, fin), two(E, fout), two(H, fout), cs,
                                     c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]),
                                     _box_arr([boxes[c] for c in comps]), _box_arr([obox]), c_int(self.tb_xchunk),
                                     c_int(steps), (c_int * 3)(*src), (c_double * 8)(*vals), _stream())
@@ -648,7 +651,7 @@ class HipOps:
 
     @property
     def tb2d_max_steps(self) -> int:
-        return TB2D_MAX_STEPS if self.dtype == torch.float32 else 0
+        return TB2D_MAX_STEPS if self.dtype == torch.float32 else TB2D_MAX_STEPS_F64
 
     @property
     def tb_max_steps(self) -> int:

@@ -78,12 +78,12 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
                  and not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials or cfg.use_amp_mode))
         if tb <= 0:  # automatic: blocked passes on the plain 3D fused path
             # (fp32: 5 steps per pass with uniform materials, 4 with per-cell
-            # coefficients) and the plain fp32 2D path
-            from .models.blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS
+            # coefficients) and the plain 2D path
+            from .models.blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64
             if cfg.scheme == "3d":
                 tb = ((5 if cfg.scene == "vacuum" else 4) if cfg.dtype == "f32" else F64_AUTO_STEPS) if plain else 1
             elif cfg.scheme in ("tmz", "tez"):
-                tb = TB2D_AUTO_STEPS if plain and cfg.dtype == "f32" else 1
+                tb = (TB2D_AUTO_STEPS if cfg.dtype == "f32" else TB2D_AUTO_STEPS_F64) if plain else 1
             else:
                 tb = 1
         if tb > 1 and cfg.scheme in ("3d", "tmz", "tez"):
