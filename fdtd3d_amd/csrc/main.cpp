@@ -124,6 +124,24 @@ int tb3d(const double* const* ei, const double* const* hi, double* const* eo, do
   const int ob[6] = {0, 0, 0, nx, ny, nz};
   return fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
 }
+int tb2d(int mode, const float* const* ei, const float* const* hi, float* const* eo, float* const* ho,
+         const float* const* cs, double cb, double db, int nx, int ny, const int* bx, const int* ob, int T,
+         const int* src, const double* vals, void* s) {
+  return fdtd_tb2d_f32(mode, ei, hi, eo, ho, cs, cb, db, nx, ny, bx, ob, 0, T, src, vals, s);
+}
+int tb2d(int mode, const double* const* ei, const double* const* hi, double* const* eo, double* const* ho,
+         const double* const* cs, double cb, double db, int nx, int ny, const int* bx, const int* ob, int T,
+         const int* src, const double* vals, void* s) {
+  return fdtd_tb2d_f64(mode, ei, hi, eo, ho, cs, cb, db, nx, ny, bx, ob, 0, T, src, vals, s);
+}
+int res1d(float* ez, float* hy, const float* ce, const float* ch, double cb, double db, int n, const int* bx, int steps,
+          int si, const float* vals, void* s) {
+  return fdtd_res1d_f32(ez, hy, ce, ch, cb, db, n, bx, steps, si, vals, s);
+}
+int res1d(double* ez, double* hy, const double* ce, const double* ch, double cb, double db, int n, const int* bx,
+          int steps, int si, const double* vals, void* s) {
+  return fdtd_res1d_f64(ez, hy, ce, ch, cb, db, n, bx, steps, si, vals, s);
+}
 int setv(float* f, long long off, double v, void* s) { return fdtd_set_value_f32(f, off, v, s); }
 int setv(double* f, long long off, double v, void* s) { return fdtd_set_value_f64(f, off, v, s); }
 int tmz_e(float* a, const float* b, const float* c, const float* d, double cb, int nx, int ny, const int* bx, void* s) {
@@ -181,7 +199,9 @@ int run(const fdtd::Settings& s) {
   const double freq = kC / s.sourceWaveLength;
   const bool vacuum = s.scene == "vacuum" || (s.scene == "reference" && dim != 3);
   const bool v4 = sizeof(T) == 4 && N[2] % 4 == 0 && dim == 3;
-  const bool use_fused = dim == 3 && !s.doUseSplitKernels;
+  // fused / blocked / resident kernels unless --split-kernels (3D fused E+H
+  // and blocked passes, 2D blocked passes, 1D one-launch resident run)
+  const bool use_fused = !s.doUseSplitKernels;
   hipStream_t st;
   HIP_OK(hipStreamCreate(&st));
 
@@ -290,9 +310,52 @@ int run(const fdtd::Settings& s) {
   const int T_req = s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock;
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
   const int T_blk = (scheme == "3d" && use_fused && (v4 || sizeof(T) == 8)) ? std::max(1, std::min(T_max, T_req)) : 1;
+  // 2D: yee2d_tb.hip passes (automatic 7 steps), rows of whole 16-byte lanes
+  const int T2_max = sizeof(T) == 4 ? fdtd_tb2d_max_steps() : fdtd_tb2d64_max_steps();
+  const int T2_blk = (dim == 2 && use_fused && N[1] % (16 / (int)sizeof(T)) == 0)
+                         ? std::max(1, std::min(T2_max, s.timeBlock <= 0 ? 7 : s.timeBlock))
+                         : 1;
+  // 1D: the whole run in one launch of the register-resident kernel
+  const bool res1 = dim == 1 && use_fused && N[0] <= fdtd_res1d_max_cells((int)sizeof(T));
   auto advance = [&](int t0, int n) {
     int t = t0;
+    if (res1 && n > 0) {
+      std::vector<T> hv(n);
+      for (int l = 0; l < n; ++l) hv[l] = (T)src_val(t + l);
+      Dev<T> dv;
+      dv.alloc(n);
+      HIP_OK(hipMemcpyAsync(dv.p, hv.data(), n * sizeof(T), hipMemcpyHostToDevice, st));
+      const int b1[4] = {boxes[12], boxes[15], boxes[24], boxes[27]};
+      K_OK(res1d(F[2].p, F[4].p, C[2].p, C[4].p, percell ? 1.0 : cb, percell ? 1.0 : db, N[0], b1, n, sp[0], dv.p,
+                 st));
+      HIP_OK(hipStreamSynchronize(st));  // the table is freed on return
+      return;
+    }
     while (n > 0) {
+      if (T2_blk > 1) {
+        // component order: TMz Ez Hx Hy, TEz Ex Ey Hz
+        const int ord[2][3] = {{2, 3, 4}, {0, 1, 5}};
+        const int m = scheme == "tmz" ? 0 : 1;
+        const int* o = ord[m];
+        const T* ei[2] = {F[o[0]].p, m ? F[o[1]].p : nullptr};
+        const T* hi[2] = {F[m ? o[2] : o[1]].p, m ? nullptr : F[o[2]].p};
+        T* eo[2] = {G[o[0]].p, m ? G[o[1]].p : nullptr};
+        T* ho[2] = {G[m ? o[2] : o[1]].p, m ? nullptr : G[o[2]].p};
+        const T* cs[3] = {C[o[0]].p, C[o[1]].p, C[o[2]].p};
+        int b2[18];
+        for (int q = 0; q < 3; ++q) std::memcpy(b2 + 6 * q, boxes + 6 * o[q], 6 * sizeof(int));
+        const int ob[6] = {0, 0, 0, N[0], N[1], 1};
+        const int src[3] = {sp[0], sp[1], m ? 2 : 0};
+        const int k = std::min(T2_blk, n);
+        double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
+        K_OK(tb2d(m, ei, hi, eo, ho, cs, percell ? 1.0 : cb, percell ? 1.0 : db, N[0], N[1], b2, ob, k, src, vals,
+                  st));
+        for (int q = 0; q < 3; ++q) std::swap(F[o[q]].p, G[o[q]].p);
+        t += k;
+        n -= k;
+        continue;
+      }
       if (T_blk > 1 && n >= T_blk) {
         const T* ei[3] = {F[0].p, F[1].p, F[2].p};
         const T* hi[3] = {F[3].p, F[4].p, F[5].p};
@@ -345,8 +408,10 @@ int run(const fdtd::Settings& s) {
   std::printf("Value type: %s\n", Api<T>::name);
   std::printf("\n-------- Details --------\n");
   std::printf("Parallel grid: 0\n");
-  if (T_blk > 1)
-    std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", T_blk);
+  if (T_blk > 1 || T2_blk > 1)
+    std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", std::max(T_blk, T2_blk));
+  else if (res1)
+    std::printf("Backend: native HIP, register-resident 1D kernel (one launch per run)\n");
   else
     std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
   std::printf("Throughput: %.1f Mcells/s\n", cells * (double)timed / sec / 1e6);

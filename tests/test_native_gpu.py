@@ -25,6 +25,15 @@ CASES = {
                "--scene", "vacuum"],
     "1d": ["--1d", "--sizex", "300", "--time-steps", "40", "--scene", "vacuum", "--source", "gaussian",
            "--gaussian-width", "8", "--gaussian-delay", "30"],
+    # blocked 2D passes (ny % 4 == 0; 23 steps = 4 passes of 5 + a tail of 3) and the per-step kernels
+    "2d_tmz_tb5": ["--2d", "--sizex", "60", "--sizey", "52", "--time-steps", "23", "--scene", "vacuum",
+                   "--time-block", "5"],
+    "2d_tez_tb": ["--2d", "--2d-mode", "tez", "--sizex", "44", "--sizey", "64", "--time-steps", "25",
+                  "--scene", "vacuum"],
+    "2d_tmz_split": ["--2d", "--sizex", "60", "--sizey", "52", "--time-steps", "25", "--scene", "vacuum",
+                     "--split-kernels"],
+    "1d_split": ["--1d", "--sizex", "300", "--time-steps", "40", "--scene", "vacuum", "--source", "gaussian",
+                 "--gaussian-width", "8", "--gaussian-delay", "30", "--split-kernels"],
 }
 
 COMPS = {"3d": ["Ex", "Ey", "Ez", "Hx", "Hy", "Hz"], "tmz": ["Ez", "Hx", "Hy"], "tez": ["Ex", "Ey", "Hz"],
