@@ -74,16 +74,26 @@ class BlockedStepping:
         stepped run in both regions (the core's plain Yee update is what the
         step kernels do there)."""
         cfg = self.cfg
+        two_d = cfg.scheme in ("tmz", "tez")
         H = int(cfg.hybrid_block)
         if H <= 0:
-            H = (4 if self.dtype == torch.float32 else F64_AUTO_STEPS) if self.ops.name == "hip" else 1
-        if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme != "3d" or self.halo is not None
+            if self.ops.name != "hip":
+                H = 1
+            elif two_d:
+                H = TB2D_AUTO_STEPS if self.dtype == torch.float32 else TB2D_AUTO_STEPS_F64
+            else:
+                H = 4 if self.dtype == torch.float32 else F64_AUTO_STEPS
+        hmax = getattr(self.ops, "tb2d_max_steps" if two_d else "tb_max_steps", 8 if two_d else 6)
+        if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme not in ("3d", "tmz", "tez") or self.halo is not None
                 or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode
-                or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials)
-                or H > getattr(self.ops, "tb_max_steps", 6)):
+                or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials) or H > hmax):
             return
-        if self.ops.name == "hip" and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
-            return
+        # fp32 3D rows are float4 along z, 2D rows 16-byte lanes along y
+        if self.ops.name == "hip":
+            if two_d and self.domain.shape[1] % (16 // self.dtype.itemsize) != 0:
+                return
+            if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
+                return
         plan = self._hybrid_plan(H)
         if plan is None:
             return
@@ -103,7 +113,10 @@ class BlockedStepping:
         alloc = dom.allocated_global()
         m = T + 2  # core margin to every irregular cell (staggering slack included)
         lo, hi = [0, 0, 0], list(size)
+        act = [self.layout.active(a) for a in range(3)]  # 2D: z is one cell, never cut
         for a in range(3):
+            if not act[a]:
+                continue
             edge = 0
             if cfg.use_pml:
                 edge = max(edge, self.layout.pml_size[a])
@@ -126,7 +139,8 @@ class BlockedStepping:
                                      tuple(max(D[1][d], b[1][d]) for d in range(3)))
 
         def grow(b, n):
-            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
+            return (tuple(b[0][d] - (n if act[d] else 0) for d in range(3)),
+                    tuple(b[1][d] + (n if act[d] else 0) for d in range(3)))
 
         if D is not None:
             Dm = box_intersect(grow(D, m), K)
@@ -148,7 +162,16 @@ class BlockedStepping:
             for slabs in self.cpml.slabs.values():
                 irregular += [sl.gbox for sl in slabs if not box_empty(sl.gbox)]
         if self.use_upml_chain and getattr(self, "chain_regions", None) is None:
-            return None  # UPML without region split: every cell runs the chain
+            if cfg.scheme == "3d":
+                return None  # 3D UPML without region split: every cell runs the chain
+            # 2D: the per-component UPML update runs on every cell; away from
+            # the PML slabs (sigma = 0) it reduces to the plain Yee update to
+            # round-off, and the core is cut T + 2 clear of the slabs above
+            for a in range(3):
+                if act[a] and cfg.use_pml and self.layout.pml_size[a] > 0:
+                    n = self.layout.pml_size[a]
+                    irregular.append(((0, 0, 0), tuple(n if d == a else size[d] for d in range(3))))
+                    irregular.append((tuple(size[a] - n if d == a else 0 for d in range(3)), tuple(size)))
         for ob in couts:
             g = grow(ob, T + 1)
             if any(not box_empty(box_intersect(g, b)) for b in irregular):
@@ -166,7 +189,7 @@ class BlockedStepping:
                         if bool(inside.any()):
                             return None
         band = T + 1
-        Kb = (tuple(K[0][d] + band for d in range(3)), tuple(K[1][d] - band for d in range(3)))
+        Kb = grow(K, -band)
         if box_empty(Kb):
             return None
         shell_windows = [b for b in box_subtract(alloc, Kb) if not box_empty(b)]
@@ -180,6 +203,8 @@ class BlockedStepping:
         # TF/SF corrections once per half step, unless a component's TF/SF
         # targets reach into a UPML chain box (D-form corrections there)
         self._tfsf_once = bool(cfg.use_tfsf)
+        if self.use_upml_chain and getattr(self, "chain_regions", None) is None:
+            self._tfsf_once = False  # 2D UPML: the per-window chain applies its D-form corrections
         if cfg.use_tfsf and getattr(self, "chain_regions", None) is not None:
             for kind in ("E", "H"):
                 for r, _ in self.chain_regions[kind]["chain"]:

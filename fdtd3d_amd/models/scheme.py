@@ -478,7 +478,7 @@ class YeeScheme(BlockedStepping):
         return self.domain.to_global((tuple(lo), tuple(hi)))
 
     def _init_chain_regions(self, prof) -> None:
-        """Region-local UPML/Drude chain (3D).  Where all three sigma values
+        """Region-local UPML/Drude chain (3D and 2D).  Where all sigma values
         of a component vanish and its Drude parameters are zero the chain is
         algebraically the plain Yee update (D' - D = (dt/dx) curl, E = D/(eps eps0)
         and, for Drude, D1 = D/(eps eps0) exactly), so each component's box is
@@ -486,7 +486,7 @@ class YeeScheme(BlockedStepping):
         (fused chain kernel): 6 PML slabs + the dispersive bounding box.  D / D1
         are only ever read in the chain boxes, which are static."""
         self.chain_regions = None
-        if self.cfg.scheme != "3d":
+        if self.cfg.scheme == "1d":
             return
         cfg = self.cfg
         dom = self.domain
@@ -699,6 +699,13 @@ class YeeScheme(BlockedStepping):
                     fast[c] = (b[0], b[0])
                 else:
                     fast[c] = b
+            if self.cfg.scheme != "3d":
+                # 2D: the chain boxes are the thin PML slabs (+ the dispersive
+                # box); the factored per-component chain runs there
+                for c in comps:
+                    if not box_empty(boxes[c]):
+                        self._upml_region(kind, c, p, boxes[c])
+                continue
             # one launch per form: dispersive chain / non-dispersive chain
             for form in (True, False):
                 sel = {c: (fast[c] if dru[c] == form else (fast[c][0], fast[c][0])) for c in comps}

@@ -24,6 +24,16 @@ CASES = [
 ]
 
 
+BASE2 = dict(size=(80, 76, 1), dtype="f64", pml_size=(5, 5, 1), tfsf_size=(9, 9, 1))
+CASES_2D = [
+    ("tmz-upml-tfsf", dict(scheme="tmz", scene="vacuum", use_pml=True, use_tfsf=True, phi=30), 4, 11),
+    ("tez-upml-point", dict(scheme="tez", scene="vacuum", use_pml=True), 5, 12),
+    ("tmz-cpml-tfsf", dict(scheme="tmz", scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=70), 7, 16),
+    ("tez-cpml-tfsf-complex", dict(scheme="tez", scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True,
+                                   complex_values=True), 3, 8),
+]
+
+
 def _run(cfg):
     s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
     s.init_scheme()
@@ -46,6 +56,24 @@ def test_hybrid_matches_stepped(name, extra, T, steps):
             scale = float(b.abs().max()) + 1e-300
             err = float((a - b).abs().max())
             assert err <= 1e-12 * scale, (name, c, err, scale)
+
+
+@pytest.mark.parametrize("name,extra,T,steps", CASES_2D, ids=[c[0] for c in CASES_2D])
+def test_hybrid_2d_matches_stepped(name, extra, T, steps):
+    """2D (TMz / TEz): blocked core (2D blocked kernel semantics) + stepped
+    shell == stepping everything."""
+    cfg = SchemeConfig(time_steps=steps, hybrid_block=1, **BASE2, **extra)
+    ref = _run(cfg)
+    assert ref.hybrid is None
+    hy = _run(dataclasses.replace(cfg, hybrid_block=T))
+    assert hy.hybrid is not None, "hybrid plan rejected"
+    for p in range(ref.planes):
+        for c in ref.comps:
+            a, b = hy.F[p][c], ref.F[p][c]
+            scale = float(b.abs().max()) + 1e-300
+            err = float((a - b).abs().max())
+            assert err <= 1e-12 * scale, (name, c, err, scale)
+    assert max(float(ref.F[0][c].abs().max()) for c in ref.comps) > 0
 
 
 def test_hybrid_checkpoint_resume(tmp_path):

@@ -22,6 +22,13 @@ CASES = [
     ("sphere-cpml", dict(scene="sphere", use_pml=True, pml_type="cpml", sphere_center=(40.0, 36.0, 48.0),
                          sphere_radius=10.0), 4, 9),
     ("upml-tfsf-f64", dict(scene="vacuum", use_pml=True, use_tfsf=True, theta=30, phi=40, psi=20, dtype="f64"), 4, 10),
+    # 2D: blocked core through yee2d_tb.hip
+    ("tmz-upml-tfsf", dict(scheme="tmz", size=(120, 104, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
+                           scene="vacuum", use_pml=True, use_tfsf=True, phi=30), 7, 23),
+    ("tez-cpml-tfsf", dict(scheme="tez", size=(96, 128, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
+                           scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=60), 5, 17),
+    ("tmz-upml-point-f64", dict(scheme="tmz", size=(150, 90, 1), pml_size=(8, 8, 1), scene="vacuum", use_pml=True,
+                                dtype="f64"), 6, 19),
 ]
 
 
@@ -37,8 +44,9 @@ def _run(cfg, backend, device, dtype):
 
 @pytest.mark.parametrize("name,extra,T,steps", CASES, ids=[c[0] for c in CASES])
 def test_hybrid_gpu(gpu, name, extra, T, steps):
-    base = dict(BASE, **{k: v for k, v in extra.items() if k == "dtype"})
-    extra = {k: v for k, v in extra.items() if k != "dtype"}
+    keys = ("dtype", "scheme", "size", "pml_size", "tfsf_size")
+    base = dict(BASE, **{k: v for k, v in extra.items() if k in keys})
+    extra = {k: v for k, v in extra.items() if k not in keys}
     cfg = SchemeConfig(time_steps=steps, **base, **extra)
     dt = torch.float32 if cfg.dtype == "f32" else torch.float64
     tol = 2e-5 if cfg.dtype == "f32" else 1e-12
