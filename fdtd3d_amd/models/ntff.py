@@ -39,13 +39,12 @@ from ..utils.constants import EPS0, MU0, PI
 ETA0 = math.sqrt(MU0 / EPS0)
 
 
-def _sample(F: torch.Tensor, comp: str, axis: int, x0: float, lo: Sequence[float], hi: Sequence[float]):
-    """Values of ``comp`` at the face-cell centres of the face ``axis = x0``
-    spanning ``[lo, hi)`` along the two other axes (centres at lo+0.5 ...).
-    Returns a 2D tensor (other axes in increasing order)."""
+def _sample_plan(comp: str, axis: int, x0: float, lo: Sequence[float], hi: Sequence[float]):
+    """Per axis (first index, count, offsets): averaging the Yee samples at
+    ``first + offset`` (0 or 0 and 1) gives ``comp`` at the face-cell
+    centres of the face ``axis = x0`` spanning ``[lo, hi)`` along the two
+    other axes (centres at lo+0.5 ...)."""
     m = MIN_COORD_FP[comp]
-    others = [a for a in range(3) if a != axis]
-    # for each axis: list of (index_start, count) slices whose average gives the target
     idx_sets = []
     for a in range(3):
         if a == axis:
@@ -61,25 +60,63 @@ def _sample(F: torch.Tensor, comp: str, axis: int, x0: float, lo: Sequence[float
             offs = [0, 1]
             base = int(math.floor(first))
         idx_sets.append((base, len(targets), offs))
+    return idx_sets
+
+
+def _plan_box(idx_sets):
+    """Global index box the samples of a plan read."""
+    return (tuple(b for b, _, _ in idx_sets), tuple(b + n + max(o) for b, n, o in idx_sets))
+
+
+def _sample_from(Fb: torch.Tensor, origin: Sequence[int], idx_sets, axis: int) -> torch.Tensor:
+    """Face-centre values from ``Fb``, the global box starting at ``origin``.
+    Returns a 2D tensor (other axes in increasing order)."""
     acc = None
     cnt = 0
     for ox in idx_sets[0][2]:
         for oy in idx_sets[1][2]:
             for oz in idx_sets[2][2]:
                 o = (ox, oy, oz)
-                sl = tuple(slice(idx_sets[a][0] + o[a], idx_sets[a][0] + o[a] + idx_sets[a][1]) for a in range(3))
-                v = F[sl]
+                sl = tuple(slice(idx_sets[a][0] - origin[a] + o[a], idx_sets[a][0] - origin[a] + o[a] + idx_sets[a][1])
+                           for a in range(3))
+                v = Fb[sl]
                 acc = v if acc is None else acc + v
                 cnt += 1
-    out = acc / cnt
-    return out.squeeze(axis)
+    return (acc / cnt).squeeze(axis)
 
 
-def ntff_power(fields_re: Dict[str, torch.Tensor], fields_im: Optional[Dict[str, torch.Tensor]], size, ntff,
-               dx: float, wavelength: float, theta: float, phis: torch.Tensor) -> torch.Tensor:
+def _sample(F: torch.Tensor, comp: str, axis: int, x0: float, lo: Sequence[float], hi: Sequence[float]):
+    """Face-centre values of ``comp`` from the full global array ``F``."""
+    return _sample_from(F, (0, 0, 0), _sample_plan(comp, axis, x0, lo, hi), axis)
+
+
+def _faces(size, ntff):
+    """(axis, x0, sign, lo, hi) of the six faces of the NTFF box."""
+    L = [float(ntff[a]) for a in range(3)]
+    R = [float(size[a] - ntff[a]) for a in range(3)]
+    return [(axis, x0, s, L, R) for axis in range(3) for x0, s in ((L[axis], -1.0), (R[axis], 1.0))]
+
+
+def ntff_requests(size, ntff) -> List[Tuple[str, Tuple]]:
+    """Every (component, global index box) the diagram reads: two-cell-thick
+    slabs around the six faces -- all a decomposed run has to gather (instead
+    of the whole grid)."""
+    req = []
+    for axis, x0, _, lo, hi in _faces(size, ntff):
+        for a in range(3):
+            if a == axis:
+                continue
+            for comp in ("H" + "xyz"[a], "E" + "xyz"[a]):
+                req.append((comp, _plan_box(_sample_plan(comp, axis, x0, lo, hi))))
+    return req
+
+
+def ntff_power(fields_re: Optional[Dict[str, torch.Tensor]], fields_im: Optional[Dict[str, torch.Tensor]], size, ntff,
+               dx: float, wavelength: float, theta: float, phis: torch.Tensor, boxes=None) -> torch.Tensor:
     """Normalised scattered power for every angle in ``phis`` (radians) at
-    polar angle ``theta``.  ``fields_*`` are full (gathered) global grids."""
-    dev = fields_re["Ex"].device
+    polar angle ``theta``.  ``fields_*`` are full global grids, or (``boxes``
+    given) dicts (component, box) -> the gathered ``ntff_requests`` slabs."""
+    dev = (fields_re["Ex"] if boxes is None else next(iter(fields_re.values()))).device
     cdt = torch.complex128
     k = 2 * PI / wavelength
     L = [float(ntff[a]) for a in range(3)]
@@ -89,10 +126,17 @@ def ntff_power(fields_re: Dict[str, torch.Tensor], fields_im: Optional[Dict[str,
     st, ct = math.sin(theta), math.cos(theta)
     rhat = torch.stack([st * torch.cos(phis), st * torch.sin(phis), torch.full_like(phis, ct)], dim=1)  # (A, 3)
 
-    def cplx(comp):
-        re = fields_re[comp].to(torch.float64)
-        im = fields_im[comp].to(torch.float64) if fields_im is not None else torch.zeros_like(re)
-        return re, im
+    def face(comp, axis, x0, lo, hi):
+        plan = _sample_plan(comp, axis, x0, lo, hi)
+        if boxes is None:
+            key, origin = comp, (0, 0, 0)
+        else:
+            key = (comp, _plan_box(plan))
+            origin = key[1][0]
+        re = _sample_from(fields_re[key].to(torch.float64), origin, plan, axis)
+        im = (_sample_from(fields_im[key].to(torch.float64), origin, plan, axis) if fields_im is not None
+              else torch.zeros_like(re))
+        return torch.complex(re, im)
 
     Nvec = torch.zeros(phis.numel(), 3, dtype=cdt, device=dev)
     Lvec = torch.zeros(phis.numel(), 3, dtype=cdt, device=dev)
@@ -103,12 +147,8 @@ def ntff_power(fields_re: Dict[str, torch.Tensor], fields_im: Optional[Dict[str,
             hi = [R[a] for a in range(3)]
             Ht, Et = {}, {}
             for a in others:
-                hc = "H" + "xyz"[a]
-                ec = "E" + "xyz"[a]
-                hr, hi_ = cplx(hc)
-                er, ei = cplx(ec)
-                Ht[a] = torch.complex(_sample(hr, hc, axis, x0, lo, hi), _sample(hi_, hc, axis, x0, lo, hi))
-                Et[a] = torch.complex(_sample(er, ec, axis, x0, lo, hi), _sample(ei, ec, axis, x0, lo, hi))
+                Ht[a] = face("H" + "xyz"[a], axis, x0, lo, hi)
+                Et[a] = face("E" + "xyz"[a], axis, x0, lo, hi)
             # n = s e_axis;  J = n x H ; M = -n x E
             a1, a2 = others  # cyclic order check: e_axis x e_a1 = +/- e_a2
             cyc = 1.0 if (a1 - axis) % 3 == 1 else -1.0
@@ -153,18 +193,24 @@ def ntff_report(scheme, t: int, out=None) -> Optional[torch.Tensor]:
     """Evaluate the diagram for the scheme's current fields (gathering a
     decomposed run on rank 0) and print the reference's report lines."""
     import sys
-    from ..parallel.halo import gather_field
+    from ..parallel.halo import gather_box
     out = out or sys.stdout
     comps = ("Ex", "Ey", "Ez", "Hx", "Hy", "Hz")
-    re = {c: gather_field(scheme, c, 0) if scheme.halo is not None else scheme.owned_field(c, 0) for c in comps}
-    im = None
-    if scheme.planes == 2:
-        im = {c: gather_field(scheme, c, 1) if scheme.halo is not None else scheme.owned_field(c, 1) for c in comps}
-    if re["Ex"] is None:
-        return None
     phis = reference_angles()
-    p = ntff_power(re, im, scheme.cfg.size, scheme.cfg.ntff_size, scheme.dx, scheme.wavelength,
-                   scheme.layout.theta, phis)
+    if scheme.halo is not None:
+        # decomposed: gather only the face slabs the diagram reads on rank 0
+        req = ntff_requests(scheme.cfg.size, scheme.cfg.ntff_size)
+        re = {key: gather_box(scheme, key[0], key[1], 0) for key in req}
+        im = {key: gather_box(scheme, key[0], key[1], 1) for key in req} if scheme.planes == 2 else None
+        if any(v is None for v in re.values()):
+            return None
+        p = ntff_power(re, im, scheme.cfg.size, scheme.cfg.ntff_size, scheme.dx, scheme.wavelength,
+                       scheme.layout.theta, phis, boxes=True)
+    else:
+        re = {c: scheme.owned_field(c, 0) for c in comps}
+        im = {c: scheme.owned_field(c, 1) for c in comps} if scheme.planes == 2 else None
+        p = ntff_power(re, im, scheme.cfg.size, scheme.cfg.ntff_size, scheme.dx, scheme.wavelength,
+                       scheme.layout.theta, phis)
     for a, v in zip(phis.tolist(), p.cpu().tolist()):
         out.write("=== t=%u, inc angle=%f; angle %f === %.17g \n" % (t, scheme.layout.phi, a, v))
     return p

@@ -334,6 +334,50 @@ def _unpack_many(ops, tensors, box, buf):
         ops.unpack(chunk, box, buf[i * n:(i + len(chunk)) * n])
 
 
+def gather_box(scheme, comp: str, box, plane: int = 0, dst: int = 0, group=None) -> Optional[torch.Tensor]:
+    """The global index box ``box`` of ``comp`` assembled on rank ``dst``
+    (None elsewhere): each rank sends only its owned part of the box (the
+    NTFF face slabs of a decomposed run, instead of whole-grid gathers)."""
+    from .topology import ParallelGridCore
+    d = scheme.domain
+    lo, hi = tuple(box[0]), tuple(box[1])
+    shape = tuple(hi[a] - lo[a] for a in range(3))
+
+    def part(dr):
+        plo = tuple(max(lo[a], dr.lo[a]) for a in range(3))
+        phi = tuple(min(hi[a], dr.hi[a]) for a in range(3))
+        return None if any(phi[a] <= plo[a] for a in range(3)) else (plo, phi)
+
+    own_full = scheme.owned_field(comp, plane)
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return own_full[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]].clone()
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    core = ParallelGridCore(tuple(d.global_size), world, tuple(d.topology))
+    mine = part(d)
+
+    def local(pp):
+        return own_full[tuple(slice(pp[0][a] - d.lo[a], pp[1][a] - d.lo[a]) for a in range(3))].contiguous()
+
+    if rank == dst:
+        out = torch.zeros(shape, dtype=own_full.dtype, device=own_full.device)
+        for r in range(core.used_procs):
+            pp = part(core.domain(r, d.buffer_size))
+            if pp is None:
+                continue
+            if r == rank:
+                blk = local(pp)
+            else:
+                blk = torch.empty(tuple(pp[1][a] - pp[0][a] for a in range(3)), dtype=own_full.dtype,
+                                  device=own_full.device)
+                dist.recv(blk, r, group=group, tag=201)
+            out[tuple(slice(pp[0][a] - lo[a], pp[1][a] - lo[a]) for a in range(3))] = blk
+        return out
+    if rank < core.used_procs and mine is not None:
+        dist.send(local(mine), dst, group=group, tag=201)
+    return None
+
+
 def gather_field(scheme, comp: str, plane: int = 0, dst: int = 0, group=None) -> Optional[torch.Tensor]:
     """Assemble the global array of ``comp`` on rank ``dst`` (None elsewhere).
 

@@ -132,3 +132,43 @@ def test_decomposed_equals_serial(name, cfg, world, axes, buf, mode):
             scale = float(b.abs().max()) + 1e-300
             err = float((a - b).abs().max())
             assert err <= 1e-12 * scale, (name, c, err, scale, par["topology"].tolist())
+
+
+def _ntff_worker(rank, world, port, cfg, axes, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import io
+        from fdtd3d_amd.models.ntff import ntff_report
+        core = ParallelGridCore.create(cfg.size, world, axes)
+        dom = core.domain(rank, 1)
+        s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64), dom, HaloExchanger(dom))
+        s.init_scheme()
+        s.init_grids()
+        s.perform_steps()
+        p = ntff_report(s, s.t, out=io.StringIO())
+        if rank == 0:
+            torch.save({"p": p}, os.path.join(outdir, "ntff.pt"))
+        else:
+            assert p is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,axes", [(4, "xyz"), (8, "xyz")])
+def test_decomposed_ntff_equals_serial(world, axes):
+    """The decomposed NTFF diagram gathers only the face slabs (gather_box)
+    and must equal the serial diagram."""
+    import io
+    from fdtd3d_amd.models.ntff import ntff_report
+    cfg = SchemeConfig(scheme="3d", size=(22, 20, 24), time_steps=14, scene="vacuum", use_pml=True,
+                       pml_size=(3, 3, 3), use_tfsf=True, tfsf_size=(5, 5, 5), ntff_size=(4, 4, 4),
+                       complex_values=True, theta=60, phi=30, psi=10)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ntff_worker, args=(world, _free_port(), cfg, axes, d), nprocs=world, join=True)
+        par = torch.load(os.path.join(d, "ntff.pt"), weights_only=True)["p"]
+    ser = ntff_report(run_serial(cfg), cfg.time_steps, out=io.StringIO())
+    assert float(ser.abs().max()) > 0
+    assert torch.allclose(par, ser, rtol=1e-10, atol=0), float((par - ser).abs().max())

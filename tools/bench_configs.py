@@ -25,6 +25,9 @@ CONFIGS = [
     ("1d-hip", "1D vacuum, 10000 cells, Gaussian pulse, HIP",
      ["--1d", "--sizex", "10000", "--time-steps", "2000", "--scene", "vacuum", "--source", "gaussian",
       "--dtype", "f64", "--warmup-steps", "10"]),
+    ("1d-hip-long", "1D vacuum, 10000 cells, Gaussian pulse, HIP, 100 000 steps (one resident launch)",
+     ["--1d", "--sizex", "10000", "--time-steps", "100000", "--scene", "vacuum", "--source", "gaussian",
+      "--dtype", "f64", "--warmup-steps", "10"]),
     ("3d-512-vacuum", "3D vacuum 512^3, point dipole, fp32",
      C512 + ["--time-steps", "200", "--scene", "vacuum"]),
     ("1d-hip-graph", "1D vacuum, 10000 cells, Gaussian pulse, HIP graphs",
@@ -44,6 +47,15 @@ CONFIGS = [
      C512 + ["--time-steps", "200", "--scene", "sphere", "--sphere-eps", "4",
              "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
              "--sphere-radius", "128"]),
+    ("2d-tmz-16k", "2D TMz 16384^2 vacuum, fp32 (blocked, 7 steps per pass)",
+     ["--2d", "--sizex", "16384", "--sizey", "16384", "--time-steps", "600", "--warmup-steps", "14", "--scene",
+      "vacuum", "--dtype", "f32"]),
+    ("2d-tmz-16k-f64", "2D TMz 16384^2 vacuum, fp64 (blocked, 7 steps per pass)",
+     ["--2d", "--sizex", "16384", "--sizey", "16384", "--time-steps", "600", "--warmup-steps", "14", "--scene",
+      "vacuum", "--dtype", "f64"]),
+    ("2d-tmz-8k-upml-tfsf", "2D TMz 8192^2, UPML + TF/SF, fp32 (hybrid blocking)",
+     ["--2d", "--sizex", "8192", "--sizey", "8192", "--time-steps", "210", "--warmup-steps", "14", "--scene",
+      "vacuum", "--use-pml", "--use-tfsf", "--dtype", "f32"]),
     ("3d-512-sphere-tb4", "3D 512^3 dielectric sphere (eps=4, r=128), fp32, 4 steps per pass",
      C512 + ["--time-steps", "210", "--scene", "sphere", "--sphere-eps", "4",
              "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
