@@ -30,9 +30,9 @@ CONFIGS = [
       "--dtype", "f64", "--warmup-steps", "10"]),
     ("3d-512-vacuum", "3D vacuum 512^3, point dipole, fp32",
      C512 + ["--time-steps", "200", "--scene", "vacuum"]),
-    ("1d-hip-graph", "1D vacuum, 10000 cells, Gaussian pulse, HIP graphs",
+    ("1d-hip-graph", "1D vacuum, 10000 cells, Gaussian pulse, HIP graphs of the per-step kernels",
      ["--1d", "--sizex", "10000", "--time-steps", "2000", "--scene", "vacuum", "--source", "gaussian",
-      "--dtype", "f64", "--warmup-steps", "60", "--use-hip-graph"]),
+      "--dtype", "f64", "--warmup-steps", "60", "--use-hip-graph", "--split-kernels"]),
     ("3d-512-vacuum-tb4", "3D vacuum 512^3, point dipole, fp32, 4 steps per pass",
      C512 + ["--time-steps", "210", "--scene", "vacuum", "--time-block", "4"]),
     ("3d-512-cpml-tfsf", "3D 512^3, CPML (10 cells) + TF/SF plane wave, fp32",
