@@ -46,4 +46,15 @@ static inline Box3 make_box(const int* lohi) {
 
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
+// x planes per workgroup of the x-streaming split kernels: 16 (measured best
+// on full grids), halved while the launch would hold fewer than 2048
+// workgroups -- thin shell / slab windows (hybrid blocking, PML slabs) would
+// otherwise leave most CUs idle.  `wg_per_chunk` = workgroups per x chunk.
+static inline int split_xchunk(int nxo, long long wg_per_chunk, int req) {
+  if (req > 0) return req;
+  int xc = 16;
+  while (xc > 2 && wg_per_chunk * (long long)cdiv(nxo, xc) < 2048) xc /= 2;
+  return xc;
+}
+
 #define FDTD_RETURN_LAUNCH_STATUS() return (int)hipGetLastError()

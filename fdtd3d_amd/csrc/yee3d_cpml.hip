@@ -311,7 +311,10 @@ FDTD_API int fdtd_update_e3d_cpml_v4_f32(float* ex, float* ey, float* ez, const 
   Box3 bx = make_box(boxes), by = make_box(boxes + 6), bz = make_box(boxes + 12);
   Box3 bu = box_union(box_union(bx, by), bz);
   if (box_empty(bu)) return 0;
-  if (xchunk <= 0) xchunk = 16;
+  {
+    const dim3 g1 = grid_c(bu, 1, lanes_z(bu));
+    xchunk = split_xchunk(bu.hi[0] - bu.lo[0], (long long)g1.x * g1.y, xchunk);
+  }
   const CpmlK K = make_cpml(cp, ci);
   if (cbx)
     LAUNCH_LZ(k_update_e3d_cpml_v4, true, ex, ey, ez, hx, hy, hz, cbx, cby, cbz, (float)cb, nx, ny, nz, bx, by, bz, bu, xchunk, K);
@@ -328,7 +331,10 @@ FDTD_API int fdtd_update_h3d_cpml_v4_f32(float* hx, float* hy, float* hz, const 
   Box3 bx = make_box(boxes), by = make_box(boxes + 6), bz = make_box(boxes + 12);
   Box3 bu = box_union(box_union(bx, by), bz);
   if (box_empty(bu)) return 0;
-  if (xchunk <= 0) xchunk = 16;
+  {
+    const dim3 g1 = grid_c(bu, 1, lanes_z(bu));
+    xchunk = split_xchunk(bu.hi[0] - bu.lo[0], (long long)g1.x * g1.y, xchunk);
+  }
   const CpmlK K = make_cpml(cp, ci);
   if (dbx)
     LAUNCH_LZ(k_update_h3d_cpml_v4, true, hx, hy, hz, ex, ey, ez, dbx, dby, dbz, (float)db, nx, ny, nz, bx, by, bz, bu, xchunk, K);

@@ -193,6 +193,8 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
         steps -= warm
     sync()
     scheme.prof.reset()  # phase timings cover the timed steps only
+    if halo is not None:
+        halo.bytes_sent = 0
     t0 = time.perf_counter()
     scheme.perform_steps(steps)
     if halo is not None:
@@ -215,6 +217,11 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
                    "ranks": world, "backend": scheme.ops.name}
             if phases:
                 rec["phases"] = phases
+            if halo is not None:
+                # rank 0's halo traffic over the timed steps (sent bytes; every
+                # rank receives as much as its neighbours send it)
+                rec["halo_gb_sent"] = halo.bytes_sent / 1e9
+                rec["halo_gb_per_s"] = halo.bytes_sent / 1e9 / seconds if seconds > 0 else 0.0
             out.write(json.dumps(rec) + "\n")
     if dist is not None:
         dist.destroy_process_group()
