@@ -50,10 +50,10 @@ static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b)
 // on full grids), halved while the launch would hold fewer than 2048
 // workgroups -- thin shell / slab windows (hybrid blocking, PML slabs) would
 // otherwise leave most CUs idle.  `wg_per_chunk` = workgroups per x chunk.
-static inline int split_xchunk(int nxo, long long wg_per_chunk, int req) {
+static inline int split_xchunk(int nxo, long long wg_per_chunk, int req, int base = 16, int min_xc = 2) {
   if (req > 0) return req;
-  int xc = 16;
-  while (xc > 2 && wg_per_chunk * (long long)cdiv(nxo, xc) < 2048) xc /= 2;
+  int xc = base;
+  while (xc > min_xc && wg_per_chunk * (long long)cdiv(nxo, xc) < 2048) xc /= 2;
   return xc;
 }
 

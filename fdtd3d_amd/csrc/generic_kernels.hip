@@ -40,14 +40,25 @@ struct Term {
   int sign;
 };
 
+// (j, k) of this thread in the box's y-z plane, k fastest: 256 threads walk
+// the flattened plane, so z-thin boxes (the 2D schemes' nz = 1) keep every
+// lane busy (grid: cell_grid).
+__device__ __forceinline__ bool plane_cell(const Box3& b, int& j, int& k) {
+  const unsigned kspan = (unsigned)(b.hi[2] - b.lo[2]);
+  const unsigned t = blockIdx.x * 256u + threadIdx.y * 64u + threadIdx.x;
+  const unsigned jj = t / kspan;
+  j = b.lo[1] + (int)jj;
+  k = b.lo[2] + (int)(t - jj * kspan);
+  return j < b.hi[1];
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_curl_general(T* __restrict__ out, const T* __restrict__ inp, Term<T> t0,
                                                       Term<T> t1, int nterms, int kind_e, Coef3<T> ca,
                                                       Coef3<T> cb, int ny, int nz, Box3 b) {
-  const int k = b.lo[2] + blockIdx.x * 64 + threadIdx.x;
-  const int j = b.lo[1] + blockIdx.y * 4 + threadIdx.y;
+  int j, k;
+  if (!plane_cell(b, j, k)) return;
   const int i = b.lo[0] + blockIdx.z;
-  if (k >= b.hi[2] || j >= b.hi[1]) return;
   const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
   const size_t off = ((size_t)i * ny + j) * nz + k;
   T acc = 0;
@@ -73,10 +84,9 @@ struct LinTerms {
 template <typename T>
 __global__ __launch_bounds__(256) void k_lincomb(T* __restrict__ out, LinTerms<T> terms, int nterms, int ny,
                                                  int nz, Box3 b) {
-  const int k = b.lo[2] + blockIdx.x * 64 + threadIdx.x;
-  const int j = b.lo[1] + blockIdx.y * 4 + threadIdx.y;
+  int j, k;
+  if (!plane_cell(b, j, k)) return;
   const int i = b.lo[0] + blockIdx.z;
-  if (k >= b.hi[2] || j >= b.hi[1]) return;
   const size_t off = ((size_t)i * ny + j) * nz + k;
   T v = 0;
 #pragma unroll
@@ -147,7 +157,8 @@ Coef3<T> coef_from(const double* s, const void* const* p) {
 }
 
 inline dim3 cell_grid(const Box3& b) {
-  return dim3(cdiv(b.hi[2] - b.lo[2], 64), cdiv(b.hi[1] - b.lo[1], 4), (unsigned)(b.hi[0] - b.lo[0]));
+  const long long plane = (long long)(b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]);
+  return dim3(cdiv(plane, 256), 1, (unsigned)(b.hi[0] - b.lo[0]));
 }
 
 }  // namespace
@@ -219,10 +230,9 @@ __global__ __launch_bounds__(256) void k_cpml(T* __restrict__ target, const T* _
                                               const T* __restrict__ bc, const T* __restrict__ cc,
                                               const T* __restrict__ kc, Coef3<T> cb, int ny, int nz, Box3 b,
                                               Box3 pb) {
-  const int k = b.lo[2] + blockIdx.x * 64 + threadIdx.x;
-  const int j = b.lo[1] + blockIdx.y * 4 + threadIdx.y;
+  int j, k;
+  if (!plane_cell(b, j, k)) return;
   const int i = b.lo[0] + blockIdx.z;
-  if (k >= b.hi[2] || j >= b.hi[1]) return;
   const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
   const size_t off = ((size_t)i * ny + j) * nz + k;
   const long long s = stride[axis];

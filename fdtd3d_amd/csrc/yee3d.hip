@@ -119,7 +119,8 @@ int launch_e3d(T* ex, T* ey, T* ez, const T* hx, const T* hy, const T* hz,
   Box3 bx = make_box(boxes), by = make_box(boxes + 6), bz = make_box(boxes + 12);
   Box3 bu = box_union(box_union(bx, by), bz);
   if (box_empty(bu)) return 0;
-  if (xchunk <= 0) xchunk = 32;
+  xchunk = split_xchunk(bu.hi[0] - bu.lo[0], (long long)cdiv(bu.hi[2] - bu.lo[2], TX) * cdiv(bu.hi[1] - bu.lo[1], TY),
+                        xchunk, 32);
   dim3 block(TX, TY, 1);
   dim3 grid(cdiv(bu.hi[2] - bu.lo[2], TX), cdiv(bu.hi[1] - bu.lo[1], TY), cdiv(bu.hi[0] - bu.lo[0], xchunk));
   if (cbx != nullptr) {
@@ -139,7 +140,8 @@ int launch_h3d(T* hx, T* hy, T* hz, const T* ex, const T* ey, const T* ez,
   Box3 bx = make_box(boxes), by = make_box(boxes + 6), bz = make_box(boxes + 12);
   Box3 bu = box_union(box_union(bx, by), bz);
   if (box_empty(bu)) return 0;
-  if (xchunk <= 0) xchunk = 32;
+  xchunk = split_xchunk(bu.hi[0] - bu.lo[0], (long long)cdiv(bu.hi[2] - bu.lo[2], TX) * cdiv(bu.hi[1] - bu.lo[1], TY),
+                        xchunk, 32);
   dim3 block(TX, TY, 1);
   dim3 grid(cdiv(bu.hi[2] - bu.lo[2], TX), cdiv(bu.hi[1] - bu.lo[1], TY), cdiv(bu.hi[0] - bu.lo[0], xchunk));
   if (dbx != nullptr) {

@@ -133,12 +133,21 @@ inline dim3 grid2d(const Box3& b, int xchunk) {
   return dim3(cdiv(b.hi[1] - b.lo[1], TX), cdiv(cdiv(b.hi[0] - b.lo[0], xchunk), TY), 1);
 }
 
+// rows per thread along x: 16, fewer on thin windows (hybrid shell, PML
+// slabs) until the launch holds >= 2048 workgroups
+inline int xchunk2d(const Box3& b, int req) {
+  if (req > 0) return req;
+  int xc = 16;
+  while (xc > 1 && (long long)cdiv(b.hi[1] - b.lo[1], TX) * cdiv(cdiv(b.hi[0] - b.lo[0], xc), TY) < 2048) xc /= 2;
+  return xc;
+}
+
 template <typename T>
 int tmz_e(T* ez, const T* hx, const T* hy, const T* cbz, double cb, int nx, int ny, const int* box, int xchunk,
           hipStream_t s) {
   Box3 bz = make_box(box);
   if (box_empty(bz)) return 0;
-  if (xchunk <= 0) xchunk = 16;
+  xchunk = xchunk2d(bz, xchunk);
   if (cbz)
     k_tmz_e<T, true><<<grid2d(bz, xchunk), dim3(TX, TY), 0, s>>>(ez, hx, hy, cbz, (T)cb, nx, ny, bz, xchunk);
   else
@@ -151,7 +160,7 @@ int tmz_h(T* hx, T* hy, const T* ez, const T* dbx, const T* dby, double db, int 
           int xchunk, hipStream_t s) {
   Box3 bx = make_box(boxes), by = make_box(boxes + 6), bu = box_union(bx, by);
   if (box_empty(bu)) return 0;
-  if (xchunk <= 0) xchunk = 16;
+  xchunk = xchunk2d(bu, xchunk);
   if (dbx)
     k_tmz_h<T, true><<<grid2d(bu, xchunk), dim3(TX, TY), 0, s>>>(hx, hy, ez, dbx, dby, (T)db, nx, ny, bx, by, bu,
                                                                  xchunk);
@@ -166,7 +175,7 @@ int tez_e(T* ex, T* ey, const T* hz, const T* cbx, const T* cby, double cb, int 
           int xchunk, hipStream_t s) {
   Box3 bx = make_box(boxes), by = make_box(boxes + 6), bu = box_union(bx, by);
   if (box_empty(bu)) return 0;
-  if (xchunk <= 0) xchunk = 16;
+  xchunk = xchunk2d(bu, xchunk);
   if (cbx)
     k_tez_e<T, true><<<grid2d(bu, xchunk), dim3(TX, TY), 0, s>>>(ex, ey, hz, cbx, cby, (T)cb, nx, ny, bx, by, bu,
                                                                  xchunk);
@@ -181,7 +190,7 @@ int tez_h(T* hz, const T* ex, const T* ey, const T* dbz, double db, int nx, int 
           hipStream_t s) {
   Box3 bz = make_box(box);
   if (box_empty(bz)) return 0;
-  if (xchunk <= 0) xchunk = 16;
+  xchunk = xchunk2d(bz, xchunk);
   if (dbz)
     k_tez_h<T, true><<<grid2d(bz, xchunk), dim3(TX, TY), 0, s>>>(hz, ex, ey, dbz, (T)db, nx, ny, bz, xchunk);
   else

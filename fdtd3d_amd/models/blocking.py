@@ -88,6 +88,12 @@ class BlockedStepping:
                 or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode
                 or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials) or H > hmax):
             return
+        if (two_d and int(cfg.hybrid_block) <= 0 and self.use_upml_chain and self.dtype == torch.float32
+                and self.ops.name == "hip"):
+            # measured 8192^2 TMz UPML + TF/SF fp32: stepped 88.7k > hybrid 77.1k
+            # Mcells/s (the thin shell's per-window launches cost as much as the
+            # whole stepped grid); fp64 and CPML gain (52.5k -> 72.9k, 106k -> 116k)
+            return
         # fp32 3D rows are float4 along z, 2D rows 16-byte lanes along y
         if self.ops.name == "hip":
             if two_d and self.domain.shape[1] % (16 // self.dtype.itemsize) != 0:
