@@ -12,8 +12,8 @@ GPUs on x and y (2 -> 2x1x1, 4 -> 2x2x1, 8 -> 4x2x1 by the halo-surface
 optimiser).  Every timed step is the full leapfrog: E and H updates of all
 cells, the hard source and (N>1) the RCCL halo exchange.  Several leapfrog
 steps run per HBM pass through the temporally blocked kernel
-(``csrc/yee3d_tb.hip``; automatic: 5 steps per pass on one GPU, 4 when
-decomposed); decomposed runs exchange T-deep ghosts with all face,
+(``csrc/yee3d_tb.hip``; automatic: 5 steps per pass on one and two GPUs, 4
+on more); decomposed runs exchange T-deep ghosts with all face,
 edge and corner neighbours once per pass, overlapped with the interior pass.
 A step count that is not a multiple of T ends with one shorter pass, so
 exactly K steps are timed.  ``--time-block 1`` selects the single-pass fused
@@ -44,8 +44,8 @@ def main(argv=None) -> int:
     ap.add_argument("--xchunk", type=int, default=0)
     ap.add_argument("--buffer-size", type=int, default=1, help="halo depth (deep halo when > 1)")
     ap.add_argument("--time-block", type=int, default=0,
-                    help="leapfrog steps per HBM pass (temporally blocked kernel; 0 automatic: 5 on one GPU, 4 "
-                         "decomposed); decomposed runs use a halo of the same depth")
+                    help="leapfrog steps per HBM pass (temporally blocked kernel; 0 automatic: 5 on one or two "
+                         "GPUs, 4 on more); decomposed runs use a halo of the same depth")
     ap.add_argument("--tb-xchunk", type=int, default=0, help="x planes per workgroup of the blocked kernel")
     ap.add_argument("--tb-vec", type=int, default=0, help="lane width of the blocked kernel (0 auto, 2, 4)")
     ap.add_argument("--tb-rows", type=int, default=0, help="grid rows per wave of the blocked kernel (0 auto, 1, 2)")
@@ -93,12 +93,13 @@ def main(argv=None) -> int:
         # would cost a whole tile row: decompose x and y only when blocking
         core = ParallelGridCore.create(size, world, "xy" if a.time_block != 1 else "xyz")
     if a.time_block <= 0:
-        # automatic: 5 steps per pass on one GPU, 4 when decomposed -- the
-        # 5-deep ghosts and shells cost more than the saved HBM traffic
+        # automatic: 5 steps per pass on one and two GPUs, 4 on more -- there
+        # the 5-deep ghosts and shells cost more than the saved HBM traffic
         # (tools/decomp_cost.py, per-GPU Mcells/s with a null transport on
-        # 1024^3: 2 ranks T=4 255k vs T=5 244k, 4 ranks 231k vs 213k, 8 ranks
-        # 213k vs 194k; one GPU T=5 ahead: 277-281k vs 260-267k)
-        a.time_block = 5 if world == 1 else 4
+        # 1024^3, three runs each: 2 ranks T=5 269-281k vs T=4 238-274k; 4
+        # ranks T=4 224-252k vs T=5 239-245k; 8 ranks T=4 229k vs T=5 221k;
+        # one GPU T=5 281-289k vs T=4 260-263k)
+        a.time_block = 5 if world <= 2 else 4
         if a.dtype == "f64":
             from fdtd3d_amd.models.scheme import F64_AUTO_STEPS
             a.time_block = F64_AUTO_STEPS

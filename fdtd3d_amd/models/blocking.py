@@ -59,8 +59,9 @@ class BlockedStepping:
 
     # ------------------------------------------------------ hybrid blocking
     def _init_hybrid(self) -> None:
-        """Blocked core + stepped shell for 3D runs with absorbing layers,
-        TF/SF injection or dispersive media (serial HIP fp32 runs by default).
+        """Blocked core + stepped shell for 3D and 2D runs with absorbing
+        layers, TF/SF injection or dispersive media (serial HIP runs by
+        default; the 2D core runs the yee2d_tb.hip kernel).
 
         Every ``T`` steps: (1) the temporally blocked kernel advances the
         *core* -- cells at least ``T + 2`` away from any PML / CPML slab,

@@ -581,7 +581,12 @@ class HipOps:
             self.lib.fdtd_set_tb_vec(c_int(self.tb_vec))
             self.lib.fdtd_set_tb_rows(c_int(self.tb_rows))
             self.lib.fdtd_set_tb_xcd(c_int(self.tb_xcd))
-            self.lib.fdtd_set_tb_mrows(c_int(self.tb_mrows))
+            mr = self.tb_mrows
+            if mr == 0 and self.tb_thin_single_row and steps <= 4 and obox[1][1] - obox[0][1] <= 8:
+                # thin y shells of a decomposed pass: the single-row kernel's
+                # 16-row tiles waste half as many rows as the 32-row multi-row tiles
+                mr = 1
+            self.lib.fdtd_set_tb_mrows(c_int(mr))
             self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
         # fp32: yee3d_tb.hip (multi-row / single-row tiles); fp64: yee3d_tb64.hip
         rc = self.fn("tb3d_v4" if self.dtype == torch.float32 else "tb3d")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
@@ -663,6 +668,7 @@ class HipOps:
     tb_xcd = 0  # XCD-aware tile order (off: measured no gain)
     tb_variant = 4  # multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched, bit 2 XCD tile order
     tb_mrows = 0  # adjacent y rows per wave (multi-row kernel): 0 auto, 1 single-row kernel, 2
+    tb_thin_single_row = True  # auto mode: output boxes <= 8 rows in y use the single-row kernel
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],

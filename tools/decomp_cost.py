@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--time-block", type=int, default=5)
     ap.add_argument("--topology", type=int, nargs=3, default=None, help="force a rank grid (e.g. 4 2 1)")
     ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--thin", type=int, default=1, help="thin y shells on the single-row kernel (T <= 4)")
     a = ap.parse_args()
     import torch
     from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
@@ -65,6 +66,7 @@ def main():
 
     def timed(domain, halo):
         s = YeeScheme(cfg, make_ops("hip", None, "cuda:0", torch.float32), domain, halo)
+        s.ops.tb_thin_single_row = bool(a.thin)
         s.init_scheme()
         s.init_grids()
         s.advance(2 * T)
