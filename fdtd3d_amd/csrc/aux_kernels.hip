@@ -38,8 +38,9 @@ __global__ void k_counter_add(int* counter, int n) {
 
 // ---------------------------------------------------------------- halo boxes
 // Copy a strided box of `ncomp` fields into a packed buffer (pack) or back
-// (unpack).  One thread per element; the z run of each box row is contiguous
-// in both the field and the buffer, so rows are coalesced.
+// (unpack).  One 16-byte vector (or one element on unaligned boxes) per
+// thread and iteration; the z run of each box row is contiguous in both the
+// field and the buffer, so rows are coalesced.
 template <typename T>
 struct FieldPtrs {
   T* p[8];
@@ -50,31 +51,64 @@ struct FieldPtrs {
 // walk the plane's (y, z) cells with ONE 32-bit divide each (the first
 // version decoded a 64-bit linear index per element with three 64-bit
 // divides, more instructions than the copy's memory time).
-template <typename T, bool PACK>
+template <typename T, bool PACK, int V>
 __global__ __launch_bounds__(256) void k_box_copy(FieldPtrs<T> fields, T* __restrict__ buf, int ny, int nz,
                                                   Box3 b) {
+  // V elements (16 bytes when V > 1) per thread and iteration
+  typedef T VT __attribute__((ext_vector_type(V)));
   const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1], bz = b.hi[2] - b.lo[2];
   const int ci = blockIdx.z;  // component * bx + plane
   const int c = ci / bx, i = ci - c * bx;
   T* __restrict__ f = fields.p[c];
-  const int nyz = by * bz;
+  const int bzv = bz / V, nyzv = by * bzv;
   const size_t fplane = (size_t)(b.lo[0] + i) * ny;
-  const size_t bplane = (size_t)ci * nyz;
-  for (int jk = blockIdx.x * 256 + threadIdx.x; jk < nyz; jk += gridDim.x * 256) {
-    const int j = jk / bz, k = jk - j * bz;
-    const size_t off = (fplane + (b.lo[1] + j)) * nz + (b.lo[2] + k);
-    if (PACK)
-      buf[bplane + jk] = f[off];
-    else
-      f[off] = buf[bplane + jk];
+  const size_t bplane = (size_t)ci * by * bz;
+  for (int jk = blockIdx.x * 256 + threadIdx.x; jk < nyzv; jk += gridDim.x * 256) {
+    const int j = jk / bzv, kv = jk - j * bzv;
+    const size_t off = (fplane + (b.lo[1] + j)) * nz + (b.lo[2] + kv * V);
+    const size_t boff = bplane + (size_t)jk * V;
+    if (V == 1) {
+      if (PACK)
+        buf[boff] = f[off];
+      else
+        f[off] = buf[boff];
+    } else {
+      if (PACK)
+        *reinterpret_cast<VT*>(buf + boff) = *reinterpret_cast<const VT*>(f + off);
+      else
+        *reinterpret_cast<VT*>(f + off) = *reinterpret_cast<const VT*>(buf + boff);
+    }
   }
 }
 
-// grid of a box copy: up to 64 blocks of 256 threads per (component, plane)
-inline dim3 box_copy_grid(const Box3& b, int ncomp) {
-  const long long nyz = (long long)(b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]);
+// grid of a box copy with V elements per thread: up to 1024 blocks of 256
+// threads per (component, plane)
+inline dim3 box_copy_grid(const Box3& b, int ncomp, int V) {
+  const long long nyz = (long long)(b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]) / V;
   const long long per = (nyz + 255) / 256;
-  return dim3((unsigned)(per < 64 ? per : 64), 1, (unsigned)((b.hi[0] - b.lo[0]) * ncomp));
+  return dim3((unsigned)(per < 1024 ? per : 1024), 1, (unsigned)((b.hi[0] - b.lo[0]) * ncomp));
+}
+
+// 16-byte vectors when every row run, row start and the buffer are aligned
+template <typename T>
+inline int box_copy_vec(const Box3& b, int nz, const void* buf, T* const* fields, int ncomp) {
+  constexpr int V = 16 / sizeof(T);
+  bool ok = (b.hi[2] - b.lo[2]) % V == 0 && b.lo[2] % V == 0 && nz % V == 0 && ((uintptr_t)buf & 15) == 0;
+  for (int c = 0; c < ncomp && ok; ++c) ok = ((uintptr_t)fields[c] & 15) == 0;
+  return ok ? V : 1;
+}
+
+template <typename T, bool PACK>
+int launch_box_copy(T* const* fields, T* buf, int ncomp, int ny, int nz, const Box3& b, hipStream_t s) {
+  FieldPtrs<T> fp;
+  for (int c = 0; c < ncomp; ++c) fp.p[c] = fields[c];
+  if ((long long)(b.hi[0] - b.lo[0]) * ncomp > 65535) return (int)hipErrorInvalidValue;
+  constexpr int VW = 16 / sizeof(T);
+  if (box_copy_vec<T>(b, nz, buf, fields, ncomp) == VW)
+    k_box_copy<T, PACK, VW><<<box_copy_grid(b, ncomp, VW), 256, 0, s>>>(fp, buf, ny, nz, b);
+  else
+    k_box_copy<T, PACK, 1><<<box_copy_grid(b, ncomp, 1), 256, 0, s>>>(fp, buf, ny, nz, b);
+  FDTD_RETURN_LAUNCH_STATUS();
 }
 
 // ---------------------------------------------------------------- reductions
@@ -178,21 +212,13 @@ inline unsigned reduce_grid(long long n) {
                                    void* s) {                                                                 \
     Box3 b = make_box(box);                                                                                   \
     if (box_empty(b) || ncomp <= 0 || ncomp > 8) return ncomp > 8 ? (int)hipErrorInvalidValue : 0;             \
-    FieldPtrs<T> fp;                                                                                          \
-    for (int c = 0; c < ncomp; ++c) fp.p[c] = fields[c];                                                      \
-    if ((long long)(b.hi[0] - b.lo[0]) * ncomp > 65535) return (int)hipErrorInvalidValue;                    \
-    k_box_copy<T, true><<<box_copy_grid(b, ncomp), 256, 0, (hipStream_t)s>>>(fp, buf, ny, nz, b);           \
-    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+    return launch_box_copy<T, true>(fields, buf, ncomp, ny, nz, b, (hipStream_t)s);                          \
   }                                                                                                           \
   FDTD_API int fdtd_box_unpack_##SUF(T* const* fields, const T* buf, int ncomp, int ny, int nz,                \
                                      const int* box, void* s) {                                               \
     Box3 b = make_box(box);                                                                                   \
     if (box_empty(b) || ncomp <= 0 || ncomp > 8) return ncomp > 8 ? (int)hipErrorInvalidValue : 0;             \
-    FieldPtrs<T> fp;                                                                                          \
-    for (int c = 0; c < ncomp; ++c) fp.p[c] = fields[c];                                                      \
-    if ((long long)(b.hi[0] - b.lo[0]) * ncomp > 65535) return (int)hipErrorInvalidValue;                    \
-    k_box_copy<T, false><<<box_copy_grid(b, ncomp), 256, 0, (hipStream_t)s>>>(fp, (T*)buf, ny, nz, b);      \
-    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+    return launch_box_copy<T, false>(fields, (T*)buf, ncomp, ny, nz, b, (hipStream_t)s);                    \
   }                                                                                                           \
   FDTD_API int fdtd_box_maxabs_##SUF(const T* f, int ny, int nz, const int* box, unsigned int* out, void* s) { \
     Box3 b = make_box(box);                                                                                   \
