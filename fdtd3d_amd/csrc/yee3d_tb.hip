@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
   // scalar, zeroed outside the component's update box
   auto coef = [&](const float* arr, const Box3& b, int p, unsigned m, const vec& pre, const vec& sc) -> vec {
     const bool in = xin(b, p);
-    if (PERCELL) return cmask<V>(bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), row), in ? m : 0u);
+    if (PERCELL && arr) return cmask<V>(bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), row), in ? m : 0u);
     if (PREMASK) return in ? pre : zero;
     return cmask<V>(sc, in ? m : 0u);
   };
@@ -425,11 +425,11 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   auto coef = [&](const float* arr, const Box3& b, int p, int r, int n, const vec& sc) -> vec {
     const bool in = xin(b, p);
     if constexpr (ALLIN) {
-      if (PERCELL) return bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]);  // 0 outside the x range
+      if (PERCELL && arr) return bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]);  // 0 outside the x range
       return in ? sc : zero;
     }
     const unsigned m = in ? (mbits >> ((r * 7 + n) * V)) & VM : 0u;
-    if (PERCELL) return cmask<V>(bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]), m);
+    if (PERCELL && arr) return cmask<V>(bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]), m);
     return cmask<V>(sc, m);
   };
 
@@ -726,7 +726,8 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   TbSrc sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
   hipStream_t s = (hipStream_t)stream;
-  const bool pc = cbs[0] != nullptr;
+  // per-cell coefficients of either kind (a null kind uses its scalar)
+  const bool pc = cbs[0] != nullptr || dbs[0] != nullptr;
   const float fcb = (float)cb, fdb = (float)db;
   // multi-row kernel: automatic from 4 steps on, required above 4
   // (per-cell coefficients: the single-row float2 kernel, whose coefficient

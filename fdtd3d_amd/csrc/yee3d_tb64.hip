@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
   const int rup = w < TBW - 1 ? w + 1 : TBW - 1;
   auto coef = [&](const double* arr, const Box3& b, int p, int r, int n, double sc) -> double {
     const bool in = xin(b, p) && ((mbits >> (r * 7 + n)) & 1u);
-    if (PERCELL) return in ? bld64(plane_rsrc64(arr, p, nx, plane), roff[r]) : 0.0;
+    if (PERCELL && arr) return in ? bld64(plane_rsrc64(arr, p, nx, plane), roff[r]) : 0.0;
     return in ? sc : 0.0;
   };
   F3d Hp[T][R], Ep[T][R];
@@ -283,7 +283,7 @@ FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, d
   if (box_empty(O)) return 0;
   TbSrc64 sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? src_vals[l] : 0.0;
-  const bool pc = cbs[0] != nullptr;
+  const bool pc = cbs[0] != nullptr || dbs[0] != nullptr;  // a null kind uses its scalar
   hipStream_t s = (hipStream_t)stream;
   // one row per wave: two rows of fp64 state spill from T = 2 on
 #define TB64(TT) launch_tb64<TT, 1>(pc, ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s)

@@ -552,9 +552,15 @@ class HipOps:
         ph = [self._cell_or_none(cb[c]) for c in H]
         percell = any(p is not None for p in pe + ph)
         if percell:
-            cbs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in E])
-            dbs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in H])
-            cbv, dbv = 1.0, 1.0
+            # a kind whose three coefficients are one scalar passes null arrays
+            # and its scalar (dielectric scenes: H reads no coefficient planes)
+            def kind_args(names, cells):
+                sc = cb[names[0]].scalar
+                if all(p is None for p in cells) and all(cb[c].scalar == sc for c in names):
+                    return (c_vp * 3)(None, None, None), sc
+                return (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in names]), 1.0
+            cbs, cbv = kind_args(E, pe)
+            dbs, dbv = kind_args(H, ph)
         else:
             cbs = (c_vp * 3)(None, None, None)
             dbs = (c_vp * 3)(None, None, None)
