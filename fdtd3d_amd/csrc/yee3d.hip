@@ -55,15 +55,15 @@ __global__ __launch_bounds__(TX * TY) void k_update_e3d(
     const T hyc = hy[off];
     const T hzc = hz[off];
     if (in_box(bx, i, j, k)) {
-      const T c = PERCELL ? cbx[off] : cb;
+      const T c = (PERCELL && cbx) ? cbx[off] : cb;
       ex[off] += c * ((hzc - hz[off - nz]) - (hyc - hy[off - 1]));
     }
     if (in_box(by, i, j, k)) {
-      const T c = PERCELL ? cby[off] : cb;
+      const T c = (PERCELL && cby) ? cby[off] : cb;
       ey[off] += c * ((hxc - hx[off - 1]) - (hzc - hz_m));
     }
     if (in_box(bz, i, j, k)) {
-      const T c = PERCELL ? cbz[off] : cb;
+      const T c = (PERCELL && cbz) ? cbz[off] : cb;
       ez[off] += c * ((hyc - hy_m) - (hxc - hx[off - nz]));
     }
     hz_m = hzc;
@@ -96,15 +96,15 @@ __global__ __launch_bounds__(TX * TY) void k_update_h3d(
       ez_n = ez[off + plane];
     }
     if (in_box(bx, i, j, k)) {
-      const T c = PERCELL ? dbx[off] : db;
+      const T c = (PERCELL && dbx) ? dbx[off] : db;
       hx[off] += c * ((ey[off + 1] - ey_c) - (ez[off + nz] - ez_c));
     }
     if (in_box(by, i, j, k)) {
-      const T c = PERCELL ? dby[off] : db;
+      const T c = (PERCELL && dby) ? dby[off] : db;
       hy[off] += c * ((ez_n - ez_c) - (ex[off + 1] - exc));
     }
     if (in_box(bz, i, j, k)) {
-      const T c = PERCELL ? dbz[off] : db;
+      const T c = (PERCELL && dbz) ? dbz[off] : db;
       hz[off] += c * ((ex[off + nz] - exc) - (ey_n - ey_c));
     }
     ey_c = ey_n;
@@ -251,15 +251,15 @@ __global__ __launch_bounds__(64 * (TY + 1)) void k_fused3d(
       eyn = eyi[off];
       ezn = ezi[off];
       if (in_box(bex, x, j, k)) {
-        const T c = PERCELL ? cbx[off] : cb;
+        const T c = (PERCELL && cbx) ? cbx[off] : cb;
         exn += c * ((hzc - hzi[off - nz]) - (hyc - hyi[off - 1]));
       }
       if (in_box(bey, x, j, k)) {
-        const T c = PERCELL ? cby[off] : cb;
+        const T c = (PERCELL && cby) ? cby[off] : cb;
         eyn += c * ((hxc - hxi[off - 1]) - (hzc - hzp));
       }
       if (in_box(bez, x, j, k)) {
-        const T c = PERCELL ? cbz[off] : cb;
+        const T c = (PERCELL && cbz) ? cbz[off] : cb;
         ezn += c * ((hyc - hyp) - (hxc - hxi[off - nz]));
       }
       if (src_comp >= 0 && (long long)off == src_off) {
@@ -286,11 +286,11 @@ __global__ __launch_bounds__(64 * (TY + 1)) void k_fused3d(
       T ex1 = exi[off], ey1 = eyi[off];
       hz_c1 = hzi[off];
       if (in_box(bex, x, j, k1)) {
-        const T c = PERCELL ? cbx[off] : cb;
+        const T c = (PERCELL && cbx) ? cbx[off] : cb;
         ex1 += c * ((hz_c1 - hzi[off - nz]) - (hyi[off] - hyi[off - 1]));
       }
       if (in_box(bey, x, j, k1)) {
-        const T c = PERCELL ? cby[off] : cb;
+        const T c = (PERCELL && cby) ? cby[off] : cb;
         ey1 += c * ((hxi[off] - hxi[off - 1]) - (hz_c1 - hz_p1));
       }
       if (src_comp >= 0 && (long long)off == src_off) {
@@ -312,15 +312,15 @@ __global__ __launch_bounds__(64 * (TY + 1)) void k_fused3d(
       const T ez_ip = sE[buf][2][w][lane], ey_ip = sE[buf][1][w][lane];
       T hxn = hxp, hyn = hyp, hzn = hzp;
       if (in_box(bhx, xm, j, k)) {
-        const T c = PERCELL ? dbx[off] : db;
+        const T c = (PERCELL && dbx) ? dbx[off] : db;
         hxn += c * ((ey_kp - ey_c) - (ez_jp - ez_c));
       }
       if (in_box(bhy, xm, j, k)) {
-        const T c = PERCELL ? dby[off] : db;
+        const T c = (PERCELL && dby) ? dby[off] : db;
         hyn += c * ((ez_ip - ez_c) - (ex_kp - ex_c));
       }
       if (in_box(bhz, xm, j, k)) {
-        const T c = PERCELL ? dbz[off] : db;
+        const T c = (PERCELL && dbz) ? dbz[off] : db;
         hzn += c * ((ex_jp - ex_c) - (ey_ip - ey_c));
       }
       if (in_box(bhx, xm, j, k)) hxo[off] = hxn;
@@ -346,7 +346,7 @@ int launch_fused(const T* const* ein, const T* const* hin, T* const* eout, T* co
   if (xchunk <= 0) xchunk = 32;
   dim3 block(64, TY + 1, 1);
   dim3 grid(cdiv(R.hi[2] - R.lo[2], 64), cdiv(R.hi[1] - R.lo[1], TY), cdiv(R.hi[0] - R.lo[0], xchunk));
-  if (cbs[0] != nullptr)
+  if (cbs[0] != nullptr || dbs[0] != nullptr)  // a null kind uses its scalar
     k_fused3d<T, true, TY><<<grid, block, 0, s>>>(ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1],
                                                   eout[2], hout[0], hout[1], hout[2], cbs[0], cbs[1], cbs[2], dbs[0],
                                                   dbs[1], dbs[2], (T)cb, (T)db, nx, ny, nz, b[0], b[1], b[2], b[3],

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_v4(
     if (xin_x && mx) {
       float4 e = ld4(ex, off);
       const float4 hz_j = ld4(hz, off - nz);
-      const float4 c4 = PERCELL ? ld4(cbx, off) : make_float4(cb, cb, cb, cb);
+      const float4 c4 = (PERCELL && cbx) ? ld4(cbx, off) : make_float4(cb, cb, cb, cb);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (mx & (1u << q)) {
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_v4(
     }
     if (xin_y && my) {
       float4 e = ld4(ey, off);
-      const float4 c4 = PERCELL ? ld4(cby, off) : make_float4(cb, cb, cb, cb);
+      const float4 c4 = (PERCELL && cby) ? ld4(cby, off) : make_float4(cb, cb, cb, cb);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (my & (1u << q)) {
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_v4(
     if (xin_z && mz) {
       float4 e = ld4(ez, off);
       const float4 hx_j = ld4(hx, off - nz);
-      const float4 c4 = PERCELL ? ld4(cbz, off) : make_float4(cb, cb, cb, cb);
+      const float4 c4 = (PERCELL && cbz) ? ld4(cbz, off) : make_float4(cb, cb, cb, cb);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (mz & (1u << q)) {
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_h3d_v4(
     if (xin_x && mx) {
       float4 h = ld4(hx, off);
       const float4 ez_j = ld4(ez, off + nz);
-      const float4 c4 = PERCELL ? ld4(dbx, off) : make_float4(db, db, db, db);
+      const float4 c4 = (PERCELL && dbx) ? ld4(dbx, off) : make_float4(db, db, db, db);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (mx & (1u << q)) {
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_h3d_v4(
     }
     if (xin_y && my) {
       float4 h = ld4(hy, off);
-      const float4 c4 = PERCELL ? ld4(dby, off) : make_float4(db, db, db, db);
+      const float4 c4 = (PERCELL && dby) ? ld4(dby, off) : make_float4(db, db, db, db);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (my & (1u << q)) {
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_h3d_v4(
     if (xin_z && mz) {
       float4 h = ld4(hz, off);
       const float4 ex_j = ld4(ex, off + nz);
-      const float4 c4 = PERCELL ? ld4(dbz, off) : make_float4(db, db, db, db);
+      const float4 c4 = (PERCELL && dbz) ? ld4(dbz, off) : make_float4(db, db, db, db);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (mz & (1u << q)) {
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
     if (inx) {
       if (mex && x >= bex.lo[0] && x < bex.hi[0]) {
         const float4 hz_j = ld4(hzi, off - nz);
-        const float4 c4 = PERCELL ? ld4(cbx, off) : make_float4(cb, cb, cb, cb);
+        const float4 c4 = (PERCELL && cbx) ? ld4(cbx, off) : make_float4(cb, cb, cb, cb);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (mex & (1u << q)) {
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
           }
       }
       if (mey && x >= bey.lo[0] && x < bey.hi[0]) {
-        const float4 c4 = PERCELL ? ld4(cby, off) : make_float4(cb, cb, cb, cb);
+        const float4 c4 = (PERCELL && cby) ? ld4(cby, off) : make_float4(cb, cb, cb, cb);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (mey & (1u << q)) {
@@ -278,7 +278,7 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
       }
       if (mez && x >= bez.lo[0] && x < bez.hi[0]) {
         const float4 hx_j = ld4(hxi, off - nz);
-        const float4 c4 = PERCELL ? ld4(cbz, off) : make_float4(cb, cb, cb, cb);
+        const float4 c4 = (PERCELL && cbz) ? ld4(cbz, off) : make_float4(cb, cb, cb, cb);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (mez & (1u << q))
@@ -308,11 +308,11 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
       ey1 = eyi[o1];
       hz_c1 = hzi[o1];
       if (x1in && x >= bex.lo[0] && x < bex.hi[0]) {
-        const float c = PERCELL ? cbx[o1] : cb;
+        const float c = (PERCELL && cbx) ? cbx[o1] : cb;
         ex1 += c * ((hz_c1 - hzi[o1 - nz]) - (hyi[o1] - hyc.w));
       }
       if (y1in && x >= bey.lo[0] && x < bey.hi[0]) {
-        const float c = PERCELL ? cby[o1] : cb;
+        const float c = (PERCELL && cby) ? cby[o1] : cb;
         ey1 += c * ((hxi[o1] - hxc.w) - (hz_c1 - hz_p1));
       }
       if (src_comp >= 0 && src_off == (long long)o1) {
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
       const float4 ez_jp = sE[pb][1][w + 1][lane];
       float4 hxn = hxp, hyn = hyp, hzn = hzp;
       if (mhx && xm >= bhx.lo[0] && xm < bhx.hi[0]) {
-        const float4 c4 = PERCELL ? ld4(dbx, o) : make_float4(db, db, db, db);
+        const float4 c4 = (PERCELL && dbx) ? ld4(dbx, o) : make_float4(db, db, db, db);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (mhx & (1u << q)) {
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
           }
       }
       if (mhy && xm >= bhy.lo[0] && xm < bhy.hi[0]) {
-        const float4 c4 = PERCELL ? ld4(dby, o) : make_float4(db, db, db, db);
+        const float4 c4 = (PERCELL && dby) ? ld4(dby, o) : make_float4(db, db, db, db);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (mhy & (1u << q)) {
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(64 * (FTY + 1)) void k_fused3d_v4(
           }
       }
       if (mhz && xm >= bhz.lo[0] && xm < bhz.hi[0]) {
-        const float4 c4 = PERCELL ? ld4(dbz, o) : make_float4(db, db, db, db);
+        const float4 c4 = (PERCELL && dbz) ? ld4(dbz, o) : make_float4(db, db, db, db);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (mhz & (1u << q))
@@ -439,7 +439,7 @@ static int launch_fused_v4(const float* const* ein, const float* const* hin, flo
   const int kspan = R.hi[2] - (R.lo[2] & ~3);
   dim3 grid(cdiv(kspan, 256), cdiv(R.hi[1] - R.lo[1], FTY), cdiv(R.hi[0] - R.lo[0], xchunk));
   dim3 block(64, FTY + 1);
-  if (cbs[0])
+  if (cbs[0] || dbs[0])  // a null kind uses its scalar
     k_fused3d_v4<true, FTY><<<grid, block, 0, (hipStream_t)s>>>(
         ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], cbs[0],
         cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], (float)cb, (float)db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],

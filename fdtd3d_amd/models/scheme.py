@@ -285,14 +285,16 @@ class YeeScheme(BlockedStepping):
         # runs exchange T-deep ghosts every T steps (buffer size == T)
         T = int(cfg.time_block)
         if T <= 0:  # automatic for the HIP fp32 path: 5 steps per pass (measured best at 1024^3),
-            # 4 with per-cell coefficients (the single-row kernel stops at 4)
+            # 2 with per-cell coefficients (float4 single-row kernel; 512^3 eps sphere, one box:
+            # T=2 122.8k, T=3 107.0k, T=4 117.3k Mcells/s -- the per-plane coefficient loads make
+            # the deeper passes VALU / issue bound)
             percell = any(getattr(self.cb.get(c), "cell", None) is not None for c in self.comps)
             if self.ops.name != "hip":
                 T = 1
             elif cfg.scheme in ("tmz", "tez"):
                 T = TB2D_AUTO_STEPS if self.dtype == torch.float32 else TB2D_AUTO_STEPS_F64
             elif self.dtype == torch.float32:
-                T = 4 if percell else 5
+                T = 2 if percell else 5
             else:
                 T = F64_AUTO_STEPS
             if self.halo is not None and self.domain.buffer_size != T:

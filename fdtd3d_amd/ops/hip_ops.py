@@ -278,11 +278,8 @@ class HipOps:
         ph = [self._cell_or_none(cb[c]) for c in H]
         percell = any(p is not None for p in pe + ph)
         if percell:
-            # one kernel form for both kinds: scalar coefficients of the other
-            # kind become constant arrays (cached)
-            cbs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in E])
-            dbs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in H])
-            cbv, dbv = 1.0, 1.0
+            cbs, cbv = self._kind_coef_args(cb, E, pe, shape)
+            dbs, dbv = self._kind_coef_args(cb, H, ph, shape)
         else:
             cbs = (c_vp * 3)(None, None, None)
             dbs = (c_vp * 3)(None, None, None)
@@ -330,6 +327,16 @@ class HipOps:
             cached = torch.full(tuple(shape), float(c.scalar), dtype=self.dtype, device=self.device)
             c._const_arr = cached
         return cached
+
+    def _kind_coef_args(self, cb: Dict[str, Coef], names, cells, shape):
+        """(3 array pointers, scalar) of one kind (E or H) for the per-cell
+        forms of the fused / blocked kernels.  A kind whose three
+        coefficients are one scalar passes null arrays and that scalar, so a
+        dielectric scene's H update reads no constant coefficient planes."""
+        sc = cb[names[0]].scalar
+        if all(p is None for p in cells) and all(cb[c].scalar == sc for c in names):
+            return (c_vp * 3)(None, None, None), sc
+        return (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in names]), 1.0
 
     def _cellp(self, c: Coef):
         self._cell_or_none(c)
@@ -552,15 +559,8 @@ class HipOps:
         ph = [self._cell_or_none(cb[c]) for c in H]
         percell = any(p is not None for p in pe + ph)
         if percell:
-            # a kind whose three coefficients are one scalar passes null arrays
-            # and its scalar (dielectric scenes: H reads no coefficient planes)
-            def kind_args(names, cells):
-                sc = cb[names[0]].scalar
-                if all(p is None for p in cells) and all(cb[c].scalar == sc for c in names):
-                    return (c_vp * 3)(None, None, None), sc
-                return (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in names]), 1.0
-            cbs, cbv = kind_args(E, pe)
-            dbs, dbv = kind_args(H, ph)
+            cbs, cbv = self._kind_coef_args(cb, E, pe, shape)
+            dbs, dbv = self._kind_coef_args(cb, H, ph, shape)
         else:
             cbs = (c_vp * 3)(None, None, None)
             dbs = (c_vp * 3)(None, None, None)
