@@ -1,24 +1,32 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mcells/s (whole node) of the 3D vacuum Yee leapfrog on a
-1024^3 grid, fp32, point-dipole source, on 1/2/4/8 MI355X (BASELINE.json).
+1024^3 grid, fp32, point-dipole source, random-init fields, on 1/2/4/8 MI355X
+(BASELINE.json).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
 launched under ``torch.distributed.run`` (one rank per GPU, RCCL).  W untimed
 steps, then exactly K timed steps bracketed by barrier + device sync on both
 sides; the slowest rank's time is used; rank 0 prints one JSON line.
 
-Scaling is *strong*: the global grid stays 1024^3 and is decomposed over the
-GPUs on x and y (2 -> 2x1x1, 4 -> 2x2x1, 8 -> 4x2x1 by the halo-surface
-optimiser).  Every timed step is the full leapfrog: E and H updates of all
-cells, the hard source and (N>1) the RCCL halo exchange.  Several leapfrog
-steps run per HBM pass through the temporally blocked kernel
-(``csrc/yee3d_tb.hip``; automatic: 5 steps per pass on one and two GPUs, 4
-on more); decomposed runs exchange T-deep ghosts with all face,
-edge and corner neighbours once per pass, overlapped with the interior pass.
-A step count that is not a multiple of T ends with one shorter pass, so
-exactly K steps are timed.  ``--time-block 1`` selects the single-pass fused
-kernel.  Fields start from zero plus the source -- the data dependence of the
-kernels is nil (pure streaming).
+Scaling is *strong*: the global grid (``--size``, default 1024^3) stays fixed
+and is decomposed over the GPUs (``--topology``: ``auto``, an axis set such as
+``xy`` / ``xyz`` for the halo-surface optimiser, or an explicit ``2x2x2``).
+Every timed step is the full leapfrog: E and H updates of all cells, the hard
+source and (N>1) the RCCL halo exchange.  Several leapfrog steps run per HBM
+pass through the temporally blocked kernel (``csrc/yee3d_tb.hip``;
+automatic: 5 steps per pass on one and two GPUs, 4 on more); decomposed runs
+exchange T-deep ghosts with all face, edge and corner neighbours once per
+pass, overlapped with the interior pass.  A step count that is not a multiple
+of T ends with one shorter pass, so exactly K steps are timed.
+
+Self-check: fields start from a deterministic hash of the *global* cell index
+(``utils/synthetic.py``), so every decomposition starts from the same state and
+must end in the same state; the JSON carries the all-reduced field energy
+(sum of E^2 + eta0^2 H^2 over owned cells, fp64) before and after, which
+``tests/test_bench_cpu.py`` checks against the serial run.  With
+``--fp64-companion`` (default on one GPU) the same measurement is repeated in
+fp64 -- the reference's default value type (``CMakeLists.txt:11``) -- and
+reported under ``"fp64"`` without changing the headline fields.
 """
 
 from __future__ import annotations
@@ -31,15 +39,161 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+HEADLINE_SIZE = (1024, 1024, 1024)
+
+
+def metric_name(size) -> str:
+    s = tuple(size)
+    if s[0] == s[1] == s[2]:
+        g = "%d^3" % s[0]
+    else:
+        g = "%dx%dx%d" % s
+    return "Mcells/sec (whole node), 3D vacuum %s grid at 1/2/4/8 MI355X" % g
+
+
+def parse_topology(spec: str, size, world: int, blocked: bool):
+    """Rank grid for ``--topology``: ``auto``, an axis set for the optimiser,
+    or an explicit ``AxBxC``."""
+    from fdtd3d_amd.parallel.topology import ParallelGridCore
+    spec = spec.lower()
+    if "x" in spec and spec.replace("x", "").isdigit():
+        t = tuple(int(v) for v in spec.split("x"))
+        if len(t) != 3 or t[0] * t[1] * t[2] != world:
+            raise SystemExit("--topology %s does not match %d ranks" % (spec, world))
+        return ParallelGridCore.create(size, world, "xyz", requested=t, optimal=False)
+    if spec == "auto":
+        # blocked passes: split x and y only.  The blocked kernel tiles z in
+        # 54-cell rows, so a T-thick z shell costs a whole tile row
+        # (tools/decomp_cost.py, profiles/decomp_r2.md)
+        spec = "xy" if blocked else "xyz"
+    return ParallelGridCore.create(size, world, spec)
+
+
+def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str, core):
+    """Build, warm up, time ``a.steps`` steps; returns a result dict (only
+    rank 0's is used)."""
+    import torch
+    import torch.distributed as dist
+
+    from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+    from fdtd3d_amd.models.blocking import auto_time_block
+    from fdtd3d_amd.ops import make_ops
+    from fdtd3d_amd.parallel.halo import HaloExchanger
+
+    size = tuple(a.size)
+    T = a.time_block
+    if T <= 0:
+        # automatic (models/blocking.py auto_time_block; the torch backend
+        # rehearses the HIP rule): 5 steps per pass on one and two GPUs, 4 on
+        # more -- there the 5-deep ghosts and shells cost more than the saved
+        # HBM traffic
+        T = auto_time_block("3d", dtype_name, "hip", False, world)
+    cfg = SchemeConfig(scheme="3d", size=size, time_steps=a.steps, scene="vacuum", dtype=dtype_name,
+                       use_pml=False, use_tfsf=False, use_fused=not a.split, time_block=T)
+    buf = T if (T > 1 and world > 1) else a.buffer_size
+    dtype = torch.float32 if dtype_name == "f32" else torch.float64
+    if world > 1:
+        domain = core.domain(rank, buf, align_z=4 if T > 1 else 1)
+        halo = HaloExchanger(domain)
+    else:
+        domain, halo = None, None
+    kw = {"xchunk": a.xchunk} if backend == "hip" else {}
+    ops = make_ops(backend, None, device, dtype, **kw)
+    if a.tb_xchunk:
+        ops.tb_xchunk = a.tb_xchunk
+    if backend == "hip":
+        ops.tb_vec, ops.tb_rows, ops.tb_xcd, ops.tb_mrows = a.tb_vec, a.tb_rows, a.tb_xcd, a.tb_mrows
+        if a.tb_variant >= 0:
+            ops.tb_variant = a.tb_variant
+    scheme = YeeScheme(cfg, ops, domain, halo)
+    scheme.init_scheme()
+    scheme.init_grids()
+    if a.init == "random":
+        scheme.randomize_fields(seed=a.seed)
+
+    def allsum(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=device if device.startswith("cuda") else "cpu")
+        dist.all_reduce(t)
+        return float(t.item())
+
+    def sync():
+        if device.startswith("cuda"):
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    energy0 = allsum(scheme.field_energy())
+    scheme.advance(a.warmup)
+    if halo is not None:
+        halo.drain(scheme)
+        # one ghost refresh outside the timed region (idempotent: the ghosts
+        # get the values they already hold) so that RCCL's lazily created
+        # peer connections exist even with --warmup 0
+        if scheme.tb > 1 or buf > 1:
+            halo.exchange_all(scheme)
+        halo.reset_timing()
+        halo.timing = True
+        halo.bytes_sent = 0
+    sync()
+    t0 = time.perf_counter()
+    scheme.advance(a.steps)
+    if halo is not None:
+        halo.drain(scheme)
+    if device.startswith("cuda"):
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    halo_ms, nex = 0.0, 0
+    if halo is not None:
+        halo_ms, nex = halo.exchange_ms(), halo.exchanges
+        halo.timing = False
+    if world > 1:
+        t = torch.tensor([dt, halo_ms / max(1, nex), halo_ms / max(1, nex)], dtype=torch.float64,
+                         device=device if device.startswith("cuda") else "cpu")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t)
+        dt = float(tmax[0].item())
+        halo_max, halo_mean = float(tmax[1].item()), float(t[2].item()) / world
+    else:
+        halo_max = halo_mean = 0.0
+    energy = allsum(scheme.field_energy())
+    cells = size[0] * size[1] * size[2]
+    res = {
+        "mcells": cells * a.steps / dt / 1e6,
+        "dt": dt,
+        "tb": scheme.tb,
+        "energy0": energy0,
+        "energy": energy,
+        "halo_bytes": halo.bytes_sent if halo else 0,
+        "halo_ms_per_pass_max": halo_max,
+        "halo_ms_per_pass_mean": halo_mean,
+        "exchanges": nex,
+    }
+    del scheme, halo, ops
+    if device.startswith("cuda"):
+        torch.cuda.empty_cache()
+    return res
+
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--size", type=int, nargs=3, default=[1024, 1024, 1024])
+    ap.add_argument("--size", type=int, nargs=3, default=list(HEADLINE_SIZE))
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--backend", default="auto")
+    ap.add_argument("--topology", default="auto",
+                    help="rank grid: auto, an axis set for the optimiser (x, xy, xyz, ...) or explicit AxBxC")
+    ap.add_argument("--init", default="random", choices=("random", "zero"),
+                    help="initial fields: hash of the global cell index (random) or zero")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--fp64-companion", default="auto", choices=("auto", "on", "off"),
+                    help="repeat the measurement in fp64 and report it under 'fp64' (auto: one GPU, fp32 runs)")
     ap.add_argument("--split", action="store_true", help="use the split E / H kernels instead of the fused one")
     ap.add_argument("--xchunk", type=int, default=0)
     ap.add_argument("--buffer-size", type=int, default=1, help="halo depth (deep halo when > 1)")
@@ -54,22 +208,19 @@ def main(argv=None) -> int:
     ap.add_argument("--tb-variant", type=int, default=-1,
                     help="multi-row blocked kernel: bit 0 deferred stores, bit 1 two planes prefetched (-1 default)")
     ap.add_argument("--tb-xcd", type=int, default=0, help="XCD-aware tile order of the blocked kernel (1 on, 0 off)")
+    ap.add_argument("--timeout", type=float, default=300.0, help="collective timeout (s): a hung exchange aborts")
     a = ap.parse_args(argv)
 
     import torch
     import torch.distributed as dist
 
-    from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
-    from fdtd3d_amd.ops import make_ops, resolve_backend
-    from fdtd3d_amd.parallel.halo import HaloExchanger
-    from fdtd3d_amd.parallel.topology import ParallelGridCore
+    from fdtd3d_amd.ops import resolve_backend
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if rank == 0:
-            print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
+    if world != a.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
     backend, device = resolve_backend(a.backend, "auto")
     # FDTD_BENCH_COMM=gloo rehearses the multi-rank path with several ranks on
     # one GPU (RCCL refuses duplicate devices; gloo stages halos through host)
@@ -81,96 +232,41 @@ def main(argv=None) -> int:
     if world > 1:
         from fdtd3d_amd.parallel.comm import init_process_group
         use_nccl = device.startswith("cuda") and comm == "nccl"
-        init_process_group("nccl" if use_nccl else "gloo", device if use_nccl else None)
+        init_process_group("nccl" if use_nccl else "gloo", device if use_nccl else None, timeout_s=a.timeout)
         # establish the communicator with a collective before the first
         # batched point-to-point exchange
         dist.barrier()
 
     size = tuple(a.size)
-    core = None
-    if world > 1:
-        # the blocked kernel tiles z in 54..60-cell rows, so a T-thick z shell
-        # would cost a whole tile row: decompose x and y only when blocking
-        core = ParallelGridCore.create(size, world, "xy" if a.time_block != 1 else "xyz")
-    if a.time_block <= 0:
-        # automatic: 5 steps per pass on one and two GPUs, 4 on more -- there
-        # the 5-deep ghosts and shells cost more than the saved HBM traffic
-        # (tools/decomp_cost.py, per-GPU Mcells/s with a null transport on
-        # 1024^3, three runs each: 2 ranks T=5 269-281k vs T=4 238-274k; 4
-        # ranks T=4 224-252k vs T=5 239-245k; 8 ranks T=4 229k vs T=5 221k;
-        # one GPU T=5 281-289k vs T=4 260-263k)
-        a.time_block = 5 if world <= 2 else 4
-        if a.dtype == "f64":
-            from fdtd3d_amd.models.scheme import F64_AUTO_STEPS
-            a.time_block = F64_AUTO_STEPS
-    cfg = SchemeConfig(scheme="3d", size=size, time_steps=a.steps, scene="vacuum", dtype=a.dtype,
-                       use_pml=False, use_tfsf=False, use_fused=not a.split, time_block=a.time_block)
-    if a.time_block > 1 and world > 1:
-        a.buffer_size = a.time_block
-    dtype = torch.float32 if a.dtype == "f32" else torch.float64
-    if world > 1:
-        domain = core.domain(rank, a.buffer_size, align_z=4 if a.time_block > 1 else 1)
-        halo = HaloExchanger(domain)
-        topo = core.topology
-    else:
-        domain, halo, topo = None, None, (1, 1, 1)
-    kw = {"xchunk": a.xchunk} if backend == "hip" else {}
-    ops = make_ops(backend, None, device, dtype, **kw)
-    if a.tb_xchunk:
-        ops.tb_xchunk = a.tb_xchunk
-    if backend == "hip":
-        ops.tb_vec, ops.tb_rows, ops.tb_xcd, ops.tb_mrows = a.tb_vec, a.tb_rows, a.tb_xcd, a.tb_mrows
-        if a.tb_variant >= 0:
-            ops.tb_variant = a.tb_variant
-    scheme = YeeScheme(cfg, ops, domain, halo)
-    scheme.init_scheme()
-    scheme.init_grids()
-
-    def sync():
-        if device.startswith("cuda"):
-            torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-
-    scheme.advance(a.warmup)
-    if halo is not None:
-        halo.drain(scheme)
-        # one ghost refresh outside the timed region (idempotent: the ghosts
-        # get the values they already hold) so that RCCL's lazily created
-        # peer connections exist even with --warmup 0
-        if scheme.tb > 1 or a.buffer_size > 1:
-            halo.exchange_all(scheme)
-    sync()
-    t0 = time.perf_counter()
-    scheme.advance(a.steps)
-    if halo is not None:
-        halo.drain(scheme)
-    if device.startswith("cuda"):
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=device if device.startswith("cuda") else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    cells = size[0] * size[1] * size[2]
-    mcells = cells * a.steps / dt / 1e6
+    core = parse_topology(a.topology, size, world, a.time_block != 1) if world > 1 else None
+    topo = core.topology if core is not None else (1, 1, 1)
+    res = run_one(a, a.dtype, world, rank, device, backend, core)
+    fp64 = None
+    companion = a.fp64_companion == "on" or (a.fp64_companion == "auto" and world == 1 and a.dtype == "f32"
+                                              and backend == "hip")
+    if companion:
+        try:
+            fp64 = run_one(a, "f64", world, rank, device, backend, core)
+        except Exception as e:  # the headline line must still be printed
+            fp64 = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0:
         par = "x".join(str(v) for v in topo)
+        cells = size[0] * size[1] * size[2]
         out = {
-            "metric": "Mcells/sec (whole node), 3D vacuum 1024^3 grid at 1/2/4/8 MI355X",
-            "value": round(mcells, 1),
+            "metric": metric_name(size),
+            "value": round(res["mcells"], 1),
             "unit": "Mcells/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(dt / a.steps * 1e3, 4),
+            "ms_per_step": round(res["dt"] / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32" if a.dtype == "f32" else "fp64",
-            "data": "synthetic (zero fields + hard point-dipole Ez source, vacuum)",
+            "data": ("synthetic (random-init fields: hash of the global cell index, + hard point-dipole Ez source, "
+                     "vacuum)" if a.init == "random" else "synthetic (zero fields + hard point-dipole Ez source, "
+                                                           "vacuum)"),
             "config": {
                 "model": "fdtd3d 3D Yee leapfrog, vacuum, point dipole (BASELINE.json headline)",
                 "grid": "%dx%dx%d" % size,
@@ -178,10 +274,20 @@ def main(argv=None) -> int:
                 "seq_len": cells,
                 "parallelism": "domain-decomposition %s (dp%d-equivalent ranks)" % (par, world),
                 "backend": backend,
-                "time_block": scheme.tb,
-                "halo_bytes_per_step": (halo.bytes_sent // max(1, a.steps + a.warmup)) if halo else 0,
+                "time_block": res["tb"],
+                "halo_bytes_per_step": res["halo_bytes"] // max(1, a.steps),
+                "halo_ms_per_pass_max": round(res["halo_ms_per_pass_max"], 4),
+                "halo_ms_per_pass_mean": round(res["halo_ms_per_pass_mean"], 4),
             },
+            "checksum": {"energy0": res["energy0"], "energy": res["energy"],
+                         "steps_total": a.warmup + a.steps},
         }
+        if fp64 is not None:
+            if "error" in fp64:
+                out["fp64"] = fp64
+            else:
+                out["fp64"] = {"value": round(fp64["mcells"], 1), "ms_per_step": round(fp64["dt"] / a.steps * 1e3, 4),
+                               "time_block": fp64["tb"], "energy": fp64["energy"]}
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -34,6 +34,33 @@ TB2D_AUTO_STEPS = 7
 TB2D_AUTO_STEPS_F64 = 7
 
 
+# automatic steps per pass of the fp32 3D blocked kernel: uniform media
+# (1024^3: T=5 281-289k vs T=4 260-263k Mcells/s on one GPU; decomposed over
+# more than two ranks T=4, whose ghosts and shells are thinner:
+# tools/decomp_cost.py 8 ranks T=4 229k vs T=5 221k per GPU) and per-cell
+# coefficients (512^3 eps sphere: T=2 122.8k, T=4 117.3k)
+F32_AUTO_STEPS = 5
+F32_AUTO_STEPS_MANY_RANKS = 4
+F32_AUTO_STEPS_PERCELL = 2
+
+
+def auto_time_block(scheme: str, dtype_name: str, backend: str, percell: bool, world: int = 1) -> int:
+    """Steps per pass of a plain (no PML / TF-SF / dispersion) run in
+    automatic mode -- ONE rule for the serial scheme, the decomposed driver
+    (which must size the ghost layers before the scheme exists) and bench.py."""
+    if backend != "hip":
+        return 1
+    if scheme in ("tmz", "tez"):
+        return TB2D_AUTO_STEPS if dtype_name == "f32" else TB2D_AUTO_STEPS_F64
+    if scheme != "3d":
+        return 1
+    if dtype_name != "f32":
+        return F64_AUTO_STEPS
+    if percell:
+        return F32_AUTO_STEPS_PERCELL
+    return F32_AUTO_STEPS if world <= 2 else F32_AUTO_STEPS_MANY_RANKS
+
+
 class BlockedStepping:
     """Blocked and hybrid passes of :class:`fdtd3d_amd.models.scheme.YeeScheme`
     (uses its fields, ops, domain, halo, layout and per-step update methods)."""

@@ -46,7 +46,7 @@ from ..parallel.domain import Domain, box_empty, box_intersect, box_subtract
 from ..utils.assertions import FdtdError, fdtd_assert
 from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
 from ..utils import logging as log
-from .blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64, BlockedStepping
+from .blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64, BlockedStepping, auto_time_block
 from .tfsf import build_tfsf_tables, incident_line_length
 
 
@@ -284,19 +284,13 @@ class YeeScheme(BlockedStepping):
         # temporal blocking: T fused steps per pass (yee3d_tb.hip); decomposed
         # runs exchange T-deep ghosts every T steps (buffer size == T)
         T = int(cfg.time_block)
-        if T <= 0:  # automatic for the HIP fp32 path: 5 steps per pass (measured best at 1024^3),
-            # 2 with per-cell coefficients (float4 single-row kernel; 512^3 eps sphere, one box:
-            # T=2 122.8k, T=3 107.0k, T=4 117.3k Mcells/s -- the per-plane coefficient loads make
-            # the deeper passes VALU / issue bound)
+        if T <= 0:  # automatic (models/blocking.py auto_time_block: one rule with the driver)
             percell = any(getattr(self.cb.get(c), "cell", None) is not None for c in self.comps)
-            if self.ops.name != "hip":
-                T = 1
-            elif cfg.scheme in ("tmz", "tez"):
-                T = TB2D_AUTO_STEPS if self.dtype == torch.float32 else TB2D_AUTO_STEPS_F64
-            elif self.dtype == torch.float32:
-                T = 2 if percell else 5
-            else:
-                T = F64_AUTO_STEPS
+            world = 1
+            if self.halo is not None:
+                t = self.domain.topology
+                world = t[0] * t[1] * t[2]
+            T = auto_time_block(cfg.scheme, cfg.dtype, self.ops.name, percell, world)
             if self.halo is not None and self.domain.buffer_size != T:
                 T = 1
         self.tb = 1
@@ -1109,3 +1103,37 @@ class YeeScheme(BlockedStepping):
         for v in self.cfg.size:
             n *= v
         return n
+
+    # ------------------------------------------------------- synthetic data
+    def randomize_fields(self, seed: int = 1) -> None:
+        """Pseudo-random E / H in [-1, 1) keyed by global cell index
+        (utils/synthetic.py): a decomposed run starts from the same fields as
+        a serial one.  The ping-pong buffer gets the same values, so cells a
+        pass never stores (PEC, padding) agree in both.  H is scaled by
+        1/eta0 so that E and H carry comparable energy."""
+        from ..utils.synthetic import hash_fill
+        eta0 = math.sqrt(MU0 / EPS0)
+        for p in range(self.planes):
+            for n, c in enumerate(self.comps):
+                hash_fill(self.F[p][c], self.domain.origin, self.cfg.size, seed * 64 + p * 8 + n)
+                if c[0] == "H":
+                    self.F[p][c].mul_(1.0 / eta0)
+                # cells a component never updates (PEC walls) stay zero: a
+                # frozen non-zero tangential E would drive H linearly forever
+                ub = self.local_box(c, self.domain.allocated_global())
+                keep = torch.zeros_like(self.F[p][c], dtype=torch.bool)
+                keep[ub[0][0]:ub[1][0], ub[0][1]:ub[1][1], ub[0][2]:ub[1][2]] = True
+                self.F[p][c].masked_fill_(~keep, 0.0)
+                alt = getattr(self, "F_alt", None)
+                if alt is not None:
+                    alt[p][c].copy_(self.F[p][c])
+
+    def field_energy(self) -> float:
+        """Vacuum field energy over this rank's owned cells in units of
+        eps0 * cell volume: sum of E^2 + eta0^2 H^2 (fp64) -- the bench
+        checksum (all-reduced by the caller)."""
+        from ..utils.synthetic import energy
+        box = self.domain.to_local(self.domain.owned_global())
+        eta2 = MU0 / EPS0
+        return sum(energy(self.F[p][c], box) * (eta2 if c[0] == "H" else 1.0)
+                   for p in range(self.planes) for c in self.comps)

@@ -26,20 +26,40 @@ import torch.distributed as dist
 P2P = namedtuple("P2P", "send tensor peer tag")
 
 
-def init_process_group(backend: str, device=None) -> None:
-    """``torch.distributed`` init for the solver.  With ``nccl`` (RCCL) the
-    communication streams are created high-priority, so halo transfers that
-    overlap a long interior kernel get dispatched as soon as a CU has room;
-    ``device`` (already current) binds the communicator eagerly."""
+DEFAULT_TIMEOUT_S = 300
+
+
+def nccl_init_kwargs(device=None, timeout_s: float = DEFAULT_TIMEOUT_S) -> dict:
+    """Keyword arguments of ``init_process_group`` for the ``nccl`` (RCCL)
+    backend: high-priority communication streams (halo transfers that overlap
+    a long interior kernel get dispatched as soon as a CU has room), the
+    device bound eagerly, and a collective timeout -- with the default
+    asynchronous error handling a hung exchange aborts the process (non-zero
+    exit) instead of hanging the job."""
+    import datetime
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    kw = {"pg_options": opts, "timeout": datetime.timedelta(seconds=float(timeout_s))}
+    if device is not None:
+        kw["device_id"] = torch.device(device)
+    return kw
+
+
+def init_process_group(backend: str, device=None, timeout_s: float = DEFAULT_TIMEOUT_S) -> None:
+    """``torch.distributed`` init for the solver (``nccl`` == RCCL over xGMI
+    on MI355X, ``gloo`` on the CPU), with a timeout on every collective."""
+    import datetime
     if backend == "nccl":
-        opts = dist.ProcessGroupNCCL.Options()
-        opts.is_high_priority_stream = True
-        kw = {"pg_options": opts}
-        if device is not None:
-            kw["device_id"] = torch.device(device)
-        dist.init_process_group("nccl", **kw)
+        dist.init_process_group("nccl", **nccl_init_kwargs(device, timeout_s))
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=float(timeout_s)))
+
+
+def build_p2p_ops(ops: List[P2P], group=None) -> list:
+    """``P2POp`` list of one batched RCCL group: every send and receive of
+    one exchange, so ``batch_isend_irecv`` issues them between one
+    ``ncclGroupStart`` / ``ncclGroupEnd`` pair (all xGMI links at once)."""
+    return [dist.P2POp(dist.isend if o.send else dist.irecv, o.tensor, o.peer, group, o.tag) for o in ops]
 
 
 class _Done:
@@ -66,8 +86,7 @@ class DistComm:
         if self.backend == "gloo" and ops[0].tensor.is_cuda:
             return self._post_staged(ops)
         if self.backend == "nccl":
-            p2p = [dist.P2POp(dist.isend if o.send else dist.irecv, o.tensor, o.peer, self.group, o.tag) for o in ops]
-            return dist.batch_isend_irecv(p2p)
+            return dist.batch_isend_irecv(build_p2p_ops(ops, self.group))
         works = []
         for o in ops:
             f = dist.isend if o.send else dist.irecv

@@ -69,6 +69,12 @@ class HaloExchanger:
         self.bufs: Dict[tuple, torch.Tensor] = {}
         self.bytes_sent = 0
         self.messages = 0
+        # exchange timing (bench / --json): HIP events on the exchange's
+        # stream around each deep exchange, wall clock on the CPU
+        self.timing = False
+        self._timed: List[tuple] = []
+        self._wall_s = 0.0
+        self.exchanges = 0
 
     # ------------------------------------------------------------ helpers
     def _buf(self, key, n, like: torch.Tensor) -> torch.Tensor:
@@ -193,9 +199,43 @@ class HaloExchanger:
         overlap compute on the current stream."""
         if stream is not None:
             with torch.cuda.stream(stream):
-                self._exchange_all(scheme)
+                self._timed_exchange(scheme)
         else:
+            self._timed_exchange(scheme)
+
+    def _timed_exchange(self, scheme) -> None:
+        self.exchanges += 1
+        if not self.timing:
             self._exchange_all(scheme)
+            return
+        dev = scheme.device
+        if getattr(dev, "type", str(dev)) == "cuda":
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            self._exchange_all(scheme)
+            b.record()
+            self._timed.append((a, b))
+        else:
+            import time
+            t0 = time.perf_counter()
+            self._exchange_all(scheme)
+            self._wall_s += time.perf_counter() - t0
+
+    def reset_timing(self) -> None:
+        self._timed = []
+        self._wall_s = 0.0
+        self.exchanges = 0
+
+    def exchange_ms(self) -> float:
+        """Total milliseconds of the timed exchanges since :meth:`reset_timing`
+        (pack + transfer + unpack, on the exchange's own stream: overlapped
+        with the interior pass, so this is latency, not added step time).
+        Synchronises the device."""
+        ms = self._wall_s * 1e3
+        for a, b in self._timed:
+            b.synchronize()
+            ms += a.elapsed_time(b)
+        return ms
 
     def _exchange_all(self, scheme) -> None:
         if self.mode == "direct":

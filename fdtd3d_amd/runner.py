@@ -76,16 +76,11 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
         tb = settings.timeBlock
         plain = (backend == "hip" and cfg.use_fused
                  and not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials or cfg.use_amp_mode))
-        if tb <= 0:  # automatic: blocked passes on the plain 3D fused path
-            # (fp32: 5 steps per pass with uniform materials, 4 with per-cell
-            # coefficients) and the plain 2D path
-            from .models.blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64
-            if cfg.scheme == "3d":
-                tb = ((5 if cfg.scene == "vacuum" else 4) if cfg.dtype == "f32" else F64_AUTO_STEPS) if plain else 1
-            elif cfg.scheme in ("tmz", "tez"):
-                tb = (TB2D_AUTO_STEPS if cfg.dtype == "f32" else TB2D_AUTO_STEPS_F64) if plain else 1
-            else:
-                tb = 1
+        if tb <= 0:  # automatic: the scheme's own rule (models/blocking.py auto_time_block)
+            from .layout.materials import Scene
+            from .models.blocking import auto_time_block
+            percell = not Scene(cfg.scene, cfg.scheme).is_vacuum(cfg.use_metamaterials)
+            tb = auto_time_block(cfg.scheme, cfg.dtype, backend, percell, world) if plain else 1
         if tb > 1 and cfg.scheme in ("3d", "tmz", "tez"):
             buf = tb  # blocked passes exchange tb-deep ghosts every tb steps
         # float4 rows: z extent (3D) / y extent (2D) padded to a multiple of 4
@@ -116,7 +111,8 @@ def _report(settings: Settings, scheme, seconds: float, world: int, core, steps:
         out.write("Number of processes: %d\n" % world)
         out.write("Parallel grid scheme: %s (topology %dx%dx%d)\n" % (
             settings.parallelBufferDimension.upper(), *core.topology))
-        out.write("Buffer size: %d\n" % settings.bufferSize)
+        # effective ghost depth: blocked passes exchange T-deep ghosts whatever --buffer-size says
+        out.write("Buffer size: %d\n" % scheme.domain.buffer_size)
     cells = cfg.size[0] * cfg.size[1] * cfg.size[2]
     mc = cells * steps / max(seconds, 1e-12) / 1e6
     kern = "fused E+H" if getattr(scheme, "fused", False) else "split"
