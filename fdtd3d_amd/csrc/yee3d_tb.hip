@@ -346,16 +346,17 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
 // stored after plane X+1's prefetch is issued -- vmcnt counts loads and
 // stores together in issue order, so stores issued between two prefetches
 // would otherwise be waited for with the older prefetch.
-template <int T, int V, int R, bool PERCELL, int PFD, bool DEFER>
+template <int T, int V, int R, int PC, int PFD, bool DEFER>
 __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
     const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
     const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
     float* __restrict__ exo, float* __restrict__ eyo, float* __restrict__ ezo,
     float* __restrict__ hxo, float* __restrict__ hyo, float* __restrict__ hzo,
-    const float* __restrict__ cbx, const float* __restrict__ cby, const float* __restrict__ cbz,
-    const float* __restrict__ dbx, const float* __restrict__ dby, const float* __restrict__ dbz, float cb,
+    const float4* __restrict__ ce4, const float4* __restrict__ ch4, Box3 BE, Box3 BH, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz) {
+  static_assert(V == 1 || !PC, "sparse per-cell coefficients: scalar lanes");
+  constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
   static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
   typedef typename VT<V>::f vec;
   constexpr int HL = (T + V - 1) / V;   // halo lanes per side
@@ -420,17 +421,72 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   for (int r = 0; r < R; ++r) upd_bits |= ((1u << (6 * V)) - 1u) << (r * 7 * V);
   const bool tile_all = __all((mbits & upd_bits) == upd_bits);
 
+  // Sparse per-cell coefficients (PC): the cells whose coefficient differs
+  // from the kind's scalar lie in a box (BE for E, BH for H) and the three
+  // components' values are one float4 per cell of that box (.w unused).  Each
+  // trip loads, for every level, one 12-byte vector per kind and row -- only
+  // on planes and waves that cross the box (wave-uniform tests), everything
+  // else runs on the scalar -- and issues those loads BEFORE the next plane's
+  // field prefetch: vmcnt retires loads in issue order, so a coefficient load
+  // issued after the prefetch would make its level wait for the prefetch too.
+  // Lanes outside the box in y / z read at an offset past the plane (0) and
+  // select the scalar.
+  unsigned eoff[R], hoff[R];
+  unsigned inb = 0;  // bit r: row r of this lane inside BE (y, z); bit R + r: inside BH
+  const int bez_n = BE.hi[2] - BE.lo[2], bhz_n = BH.hi[2] - BH.lo[2];
+  const size_t eplane = (size_t)(BE.hi[1] - BE.lo[1]) * bez_n * 16u;
+  const size_t hplane = (size_t)(BH.hi[1] - BH.lo[1]) * bhz_n * 16u;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = jw + r;
+    const bool ie = PCE && kin && j >= BE.lo[1] && j < BE.hi[1] && kb >= BE.lo[2] && kb < BE.hi[2];
+    const bool ih = PCH && kin && j >= BH.lo[1] && j < BH.hi[1] && kb >= BH.lo[2] && kb < BH.hi[2];
+    eoff[r] = ie ? (unsigned)((j - BE.lo[1]) * bez_n + (kb - BE.lo[2])) * 16u : 0xF0000000u;
+    hoff[r] = ih ? (unsigned)((j - BH.lo[1]) * bhz_n + (kb - BH.lo[2])) * 16u : 0xF0000000u;
+    inb |= (ie ? 1u : 0u) << r;
+    inb |= (ih ? 1u : 0u) << (R + r);
+  }
+  const bool wave_e = PCE && __any(inb & ((1u << R) - 1u));
+  const bool wave_h = PCH && __any(inb >> R);
+  typedef unsigned u3 __attribute__((ext_vector_type(3)));
+  auto coef_ld = [&](const float4* arr, const Box3& B, unsigned off, size_t pl, int p) -> u3 {
+    const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)arr + (size_t)(p - B.lo[0]) * pl),
+                                                      (short)0, (int)pl, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+  };
+  // RING: one per-cell kind; its coefficient planes X - l - RHS of the T
+  // levels of trip X sit in T LDS slots (each wave reads and writes only its
+  // own rows, so no barrier guards them)
+  constexpr bool RING = PC == 1 || PC == 2;
+  constexpr int NS = RING ? T : 1;
+  constexpr int RHS = PC == 2 ? 1 : 0;  // H levels run one plane behind E
+  __shared__ float sC[NS][3][RING ? ROWS : 1][64];
+  const Box3& RB = PC == 2 ? BH : BE;
+  const float4* rarr = PC == 2 ? ch4 : ce4;
+  const size_t rpl = PC == 2 ? hplane : eplane;
+  const unsigned* roffc = PC == 2 ? hoff : eoff;
+  const bool wave_r = PC == 2 ? wave_h : wave_e;
+  auto ring_slot = [&](int p) -> int { return (p + 64 * NS) % NS; };
+  if (RING && wave_r && xin(RB, i0 - T - RHS)) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u3 v = coef_ld(rarr, RB, roffc[r], rpl, i0 - T - RHS);
+      const int sl = ring_slot(i0 - T - RHS);
+      sC[sl][0][R * w + r][lane] = __uint_as_float(v.x);
+      sC[sl][1][R * w + r][lane] = __uint_as_float(v.y);
+      sC[sl][2][R * w + r][lane] = __uint_as_float(v.z);
+    }
+  }
+
   auto run = [&](auto allin_tag) {
   constexpr bool ALLIN = decltype(allin_tag)::value;
-  auto coef = [&](const float* arr, const Box3& b, int p, int r, int n, const vec& sc) -> vec {
+  // coefficient of component n (box b) of row r on plane p: the lane's value
+  // sc (scalar or per-cell) inside the update box, 0 outside
+  auto coef = [&](const Box3& b, int p, int r, int n, float sc) -> vec {
     const bool in = xin(b, p);
-    if constexpr (ALLIN) {
-      if (PERCELL && arr) return bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]);  // 0 outside the x range
-      return in ? sc : zero;
-    }
+    if constexpr (ALLIN) return in ? (vec)(sc) : zero;
     const unsigned m = in ? (mbits >> ((r * 7 + n) * V)) & VM : 0u;
-    if (PERCELL && arr) return cmask<V>(bld<V>(plane_rsrc(arr, in ? p : -1, nx, plane), roff[r]), m);
-    return cmask<V>(sc, m);
+    return cmask<V>((vec)(sc), m);
   };
 
   F3<V> Hp[T][R], Ep[T][R];
@@ -493,6 +549,49 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
         Enx[r] = En2[r];
       }
     }
+    // this trip's coefficients.  One per-cell kind (RING): the next trip's
+    // newest plane is loaded now and parked in the wave's own LDS ring slots
+    // at the end of the trip.  Both kinds: every level's plane into registers.
+    const int qn = X + 1 - RHS;  // ring: the plane the next trip's level 0 needs
+    const bool ring_ld = RING && wave_r && xin(RB, qn);
+    u3 RQ[R];
+    if (ring_ld) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) RQ[r] = coef_ld(rarr, RB, roffc[r], rpl, qn);
+    }
+    u3 CE[PC == 3 ? T : 1][R], CH[PC == 3 ? T : 1][R];
+    if (PC == 3 && wave_e) {
+#pragma unroll
+      for (int l = 0; l < T; ++l)
+        if (xin(BE, X - l))
+#pragma unroll
+          for (int r = 0; r < R; ++r) CE[PC == 3 ? l : 0][r] = coef_ld(ce4, BE, eoff[r], eplane, X - l);
+    }
+    if (PC == 3 && wave_h) {
+#pragma unroll
+      for (int l = 0; l < T; ++l)
+        if (xin(BH, X - l - 1))
+#pragma unroll
+          for (int r = 0; r < R; ++r) CH[PC == 3 ? l : 0][r] = coef_ld(ch4, BH, hoff[r], hplane, X - l - 1);
+    }
+    // the lane's three coefficients of a kind at level l, plane p (scalar off the box)
+    auto kcoef = [&](bool kind_e, int l, int p, int r) -> float3 {
+      const float sc = kind_e ? cb : db;
+      const bool wave = kind_e ? wave_e : wave_h;
+      const bool lane_in = (inb >> (kind_e ? r : R + r)) & 1u;
+      if constexpr (RING) {
+        if (kind_e == (bool)PCE && wave && xin(RB, p) && lane_in) {
+          const int sl = ring_slot(p);
+          return make_float3(sC[sl][0][R * w + r][lane], sC[sl][1][R * w + r][lane], sC[sl][2][R * w + r][lane]);
+        }
+      } else if constexpr (PC == 3) {
+        if (wave && xin(kind_e ? BE : BH, p) && lane_in) {
+          const u3 raw = kind_e ? CE[PC == 3 ? l : 0][r] : CH[PC == 3 ? l : 0][r];
+          return make_float3(__uint_as_float(raw.x), __uint_as_float(raw.y), __uint_as_float(raw.z));
+        }
+      }
+      return make_float3(sc, sc, sc);
+    };
     // next plane(s) in flight under this plane's levels
     if (PFD == 2)
       load_plane(X + 2, Hn2, En2);
@@ -525,9 +624,10 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
         const vec hx_j = r == 0 ? hx_dn : Hc[r > 0 ? r - 1 : 0].x;
         const float hy_k0 = lane_up(Hc[r].y[V - 1]);
         const float hx_k0 = lane_up(Hc[r].x[V - 1]);
-        En[r].x = Ec[r].x + coef(cbx, bex, pe, r, 0, cbv) * ((Hc[r].z - hz_j) - (Hc[r].y - zm1<V>(Hc[r].y, hy_k0)));
-        En[r].y = Ec[r].y + coef(cby, bey, pe, r, 1, cbv) * ((Hc[r].x - zm1<V>(Hc[r].x, hx_k0)) - (Hc[r].z - Hp[l][r].z));
-        En[r].z = Ec[r].z + coef(cbz, bez, pe, r, 2, cbv) * ((Hc[r].y - Hp[l][r].y) - (Hc[r].x - hx_j));
+        const float3 ce = kcoef(true, l, pe, r);
+        En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * ((Hc[r].z - hz_j) - (Hc[r].y - zm1<V>(Hc[r].y, hy_k0)));
+        En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * ((Hc[r].x - zm1<V>(Hc[r].x, hx_k0)) - (Hc[r].z - Hp[l][r].z));
+        En[r].z = Ec[r].z + coef(bez, pe, r, 2, ce.z) * ((Hc[r].y - Hp[l][r].y) - (Hc[r].x - hx_j));
         if (src_plane && jw + r == src_j && src_k >= kb && src_k < kb + V) {
           const int q = src_k - kb;
           if (src_comp == 0) En[r].x[q] = sv.v[l];
@@ -543,17 +643,28 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
         const float ey_k3 = lane_dn(Ep[l][r].y[0]);
         const float ex_k3 = lane_dn(Ep[l][r].x[0]);
         F3<V> Hn;
-        Hn.x = Hp[l][r].x + coef(dbx, bhx, ph, r, 3, dbv) *
+        const float3 ch = kcoef(false, l, ph, r);
+        Hn.x = Hp[l][r].x + coef(bhx, ph, r, 3, ch.x) *
                                 ((zp1<V>(Ep[l][r].y, ey_k3) - Ep[l][r].y) - (ez_jn - Ep[l][r].z));
-        Hn.y = Hp[l][r].y + coef(dby, bhy, ph, r, 4, dbv) *
+        Hn.y = Hp[l][r].y + coef(bhy, ph, r, 4, ch.y) *
                                 ((En[r].z - Ep[l][r].z) - (zp1<V>(Ep[l][r].x, ex_k3) - Ep[l][r].x));
-        Hn.z = Hp[l][r].z + coef(dbz, bhz, ph, r, 5, dbv) * ((ex_jn - Ep[l][r].x) - (En[r].y - Ep[l][r].y));
+        Hn.z = Hp[l][r].z + coef(bhz, ph, r, 5, ch.z) * ((ex_jn - Ep[l][r].x) - (En[r].y - Ep[l][r].y));
         // later rows (r+1 ..) read only their own and higher rows' Ep, so
         // row r rotates as soon as its H is done
         Ec[r] = Ep[l][r];
         Ep[l][r] = En[r];
         Hp[l][r] = Hc[r];
         Hc[r] = Hn;
+      }
+    }
+    if (ring_ld) {
+      // slot of plane qn = that of plane qn - T, read at this trip's last level
+      const int sl = ring_slot(qn);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        sC[sl][0][R * w + r][lane] = __uint_as_float(RQ[r].x);
+        sC[sl][1][R * w + r][lane] = __uint_as_float(RQ[r].y);
+        sC[sl][2][R * w + r][lane] = __uint_as_float(RQ[r].z);
       }
     }
     if (DEFER) {
@@ -651,39 +762,80 @@ int g_tb_mrows = 0;  // rows per wave of the multi-row kernel: 0 automatic, 1 = 
 int g_tb_mr_noallin = 0;  // A/B knob: 1 = masked loop everywhere (no interior fast path)
 int g_tb_mr_xcd = 1;   // multi-row kernel: XCD-contiguous tile order, z fastest (-16..20% HBM reads)
 int g_tb_variant = 0;  // multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched
+const int kNoBox[6] = {0, 0, 0, 0, 0, 0};
 
-template <int T, int V, int R, bool PERCELL>
+template <int T, int V, int R, int PC>
 int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
-                 const float* const* cbs, const float* const* dbs, float cb, float db, int nx, int ny, int nz,
-                 const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv, hipStream_t s) {
+                 const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
+                 int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
+                 hipStream_t s) {
   constexpr int HL = (T + V - 1) / V;
   constexpr int TBZ = (64 - 2 * HL) * V;
   dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * T),
             cdiv(O.hi[0] - O.lo[0], xchunk));
 #define MR_LAUNCH(PFD, DEFER)                                                                                 \
-  k_tb3d_mr<T, V, R, PERCELL, PFD, DEFER><<<grid, dim3(64, TBW), 0, s>>>(                                   \
+  k_tb3d_mr<T, V, R, PC, PFD, DEFER><<<grid, dim3(64, TBW), 0, s>>>(                                   \
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
-      cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
+      ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
       O, xchunk, src[0], src[1], src[2], src[3], sv, g_tb_mr_xcd | (g_tb_mr_noallin << 1))
-  switch (g_tb_variant & 3) {
-    case 0: MR_LAUNCH(1, false); break;
-    case 1: MR_LAUNCH(1, true); break;
-    case 2: MR_LAUNCH(2, false); break;
-    default: MR_LAUNCH(2, true); break;
+  if constexpr (PC != 0) {
+    MR_LAUNCH(1, false);  // tuning variants: uniform media only
+  } else {
+    switch (g_tb_variant & 3) {
+      case 0: MR_LAUNCH(1, false); break;
+      case 1: MR_LAUNCH(1, true); break;
+      case 2: MR_LAUNCH(2, false); break;
+      default: MR_LAUNCH(2, true); break;
+    }
   }
 #undef MR_LAUNCH
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
 template <int T>
-int launch_tb_mr_sel(int V, int R, bool pc, const float* const* ein, const float* const* hin, float* const* eout,
-                     float* const* hout, const float* const* cbs, const float* const* dbs, float cb, float db,
-                     int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src,
-                     const TbSrc& sv, hipStream_t s) {
-#define MR_ARGS ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s
-  // only scalar lanes with 2 rows per wave: R = 4 or float2 lanes at R = 2
+int launch_tb_mr_sel(int pc, const float* const* ein, const float* const* hin, float* const* eout,
+                     float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
+                     float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
+                     const int* src, const TbSrc& sv, hipStream_t s) {
+  // scalar lanes with 2 rows per wave: R = 4 or float2 lanes at R = 2
   // exceed 128 VGPRs and spill from T = 2 on
-  if (V == 1 && R == 2) return pc ? launch_tb_mr<T, 1, 2, true>(MR_ARGS) : launch_tb_mr<T, 1, 2, false>(MR_ARGS);
+#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s
+  // per-cell: one kind keeps T coefficient planes in LDS (24 KiB each, 160
+  // KiB per CU: T <= 5); both kinds keep them in registers (spill-free to T = 3)
+  if constexpr (T <= 5) {
+    switch (pc) {
+      case 1: return launch_tb_mr<T, 1, 2, 1>(MR_ARGS);
+      case 2: return launch_tb_mr<T, 1, 2, 2>(MR_ARGS);
+      case 3: return launch_tb_mr<T, 1, 2, 3>(MR_ARGS);
+    }
+  } else {
+    if (pc) return (int)hipErrorInvalidValue;
+  }
+  return launch_tb_mr<T, 1, 2, 0>(MR_ARGS);
+#undef MR_ARGS
+}
+
+// multi-row pass (scalar lanes, 2 rows per wave), uniform or sparse per-cell coefficients
+int tb_mr_dispatch(int pc, const float* const* ein, const float* const* hin, float* const* eout,
+                   float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
+                   float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, int steps,
+                   const int* src, const TbSrc& sv, hipStream_t s) {
+  const int R = 2, V = 1;
+  if (xchunk <= 0) {
+    const int HL = (steps + V - 1) / V;
+    const long long gz = cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), (64 - 2 * HL) * V);
+    const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
+    xchunk = pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps);
+  }
+#define MR_ARGS pc, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s
+  switch (steps) {
+    case 1: return launch_tb_mr_sel<1>(MR_ARGS);
+    case 2: return launch_tb_mr_sel<2>(MR_ARGS);
+    case 3: return launch_tb_mr_sel<3>(MR_ARGS);
+    case 4: return launch_tb_mr_sel<4>(MR_ARGS);
+    case 5: return launch_tb_mr_sel<5>(MR_ARGS);
+    case 6: return launch_tb_mr_sel<6>(MR_ARGS);
+  }
 #undef MR_ARGS
   return (int)hipErrorInvalidValue;
 }
@@ -729,30 +881,16 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   // per-cell coefficients of either kind (a null kind uses its scalar)
   const bool pc = cbs[0] != nullptr || dbs[0] != nullptr;
   const float fcb = (float)cb, fdb = (float)db;
-  // multi-row kernel: automatic from 4 steps on, required above 4
-  // (per-cell coefficients: the single-row float2 kernel, whose coefficient
-  // loads are 8 B per lane; 512^3 sphere T=4 91k vs 85k Mcells/s multi-row)
+  // multi-row kernel for uniform media: automatic from 4 steps on, required
+  // above 4 (full per-cell planes run on the single-row kernel; the sparse
+  // per-cell form is fdtd_tb3d_sparse_f32)
   const int MR = g_tb_mrows ? g_tb_mrows : (steps >= 4 && !pc ? MR_AUTO_ROWS : 1);
-  if (MR > 1 || steps > 4) {
-    const int R = 2, V = 1;
-    if (xchunk <= 0) {
-      const int HL = (steps + V - 1) / V;
-      const long long gz = cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), (64 - 2 * HL) * V);
-      const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
-      xchunk = pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps);
-    }
-#define MR_ARGS V, R, pc, ein, hin, eout, hout, cbs, dbs, fcb, fdb, nx, ny, nz, b, O, xchunk, src, sv, s
-    switch (steps) {
-      case 1: return launch_tb_mr_sel<1>(MR_ARGS);
-      case 2: return launch_tb_mr_sel<2>(MR_ARGS);
-      case 3: return launch_tb_mr_sel<3>(MR_ARGS);
-      case 4: return launch_tb_mr_sel<4>(MR_ARGS);
-      case 5: return launch_tb_mr_sel<5>(MR_ARGS);
-      case 6: return launch_tb_mr_sel<6>(MR_ARGS);
-    }
-#undef MR_ARGS
-    return (int)hipErrorInvalidValue;
+  if (!pc && (MR > 1 || steps > 4)) {
+    const Box3 nb = make_box(kNoBox);
+    return tb_mr_dispatch(0, ein, hin, eout, hout, nullptr, nullptr, nb, nb, fcb, fdb, nx, ny, nz, b, O, xchunk,
+                          steps, src, sv, s);
   }
+  if (steps > 4) return (int)hipErrorInvalidValue;
   if (xchunk <= 0) {
     const int V = g_tb_vec ? g_tb_vec : (steps <= 2 ? 4 : 2);
     const int R = g_tb_rows ? g_tb_rows : 1;
@@ -777,4 +915,29 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
 #undef TB_CASE
 #undef TB_ARGS
   return (int)hipErrorInvalidValue;
+}
+
+// T fused leapfrog steps with sparse per-cell coefficients (multi-row
+// kernel): ``ce4`` / ``ch4`` hold the E / H coefficients of the three
+// components as one float4 per cell of the box ``ebox`` / ``hbox`` (x-major,
+// z fastest, .w unused); every cell outside its kind's box -- and either kind
+// whose array is null -- uses the scalar ``cb`` / ``db``.  Other arguments as
+// fdtd_tb3d_v4_f32.
+FDTD_API int fdtd_tb3d_sparse_f32(const float* const* ein, const float* const* hin, float* const* eout,
+                                  float* const* hout, const void* ce4, const int* ebox, const void* ch4,
+                                  const int* hbox, double cb, double db, int nx, int ny, int nz, const int* boxes,
+                                  const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
+                                  void* stream) {
+  if (nz % 4 != 0 || steps < 1 || steps > 6) return (int)hipErrorInvalidValue;
+  Box3 b[6];
+  for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
+  const Box3 O = make_box(obox);
+  if (box_empty(O)) return 0;
+  const Box3 BE = make_box(ce4 ? ebox : kNoBox), BH = make_box(ch4 ? hbox : kNoBox);
+  TbSrc sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
+  const int pc = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0);
+  return tb_mr_dispatch(pc, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
+                        (const float4*)(box_empty(BH) ? nullptr : ch4), BE, BH, (float)cb, (float)db, nx, ny, nz, b,
+                        O, xchunk, steps, src, sv, (hipStream_t)stream);
 }

@@ -37,17 +37,22 @@ TB2D_AUTO_STEPS_F64 = 7
 # automatic steps per pass of the fp32 3D blocked kernel: uniform media
 # (1024^3: T=5 281-289k vs T=4 260-263k Mcells/s on one GPU; decomposed over
 # more than two ranks T=4, whose ghosts and shells are thinner:
-# tools/decomp_cost.py 8 ranks T=4 229k vs T=5 221k per GPU) and per-cell
-# coefficients (512^3 eps sphere: T=2 122.8k, T=4 117.3k)
+# tools/decomp_cost.py 8 ranks T=4 229k vs T=5 221k per GPU).  Per-cell
+# coefficients of one kind (dielectric or magnetic scenes) run the sparse
+# multi-row kernel with an LDS ring of coefficient planes (512^3 eps sphere:
+# T=3 160k, 4 188k, 5 203k Mcells/s); per-cell E AND H keep the planes in
+# registers, spill-free only to T=2.
 F32_AUTO_STEPS = 5
 F32_AUTO_STEPS_MANY_RANKS = 4
-F32_AUTO_STEPS_PERCELL = 2
+F32_AUTO_STEPS_PERCELL_BOTH = 2
 
 
-def auto_time_block(scheme: str, dtype_name: str, backend: str, percell: bool, world: int = 1) -> int:
+def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: int = 1) -> int:
     """Steps per pass of a plain (no PML / TF-SF / dispersion) run in
     automatic mode -- ONE rule for the serial scheme, the decomposed driver
-    (which must size the ghost layers before the scheme exists) and bench.py."""
+    (which must size the ghost layers before the scheme exists) and bench.py.
+    ``percell``: number of field kinds (E, H) with per-cell coefficients
+    (a bool counts as one)."""
     if backend != "hip":
         return 1
     if scheme in ("tmz", "tez"):
@@ -56,8 +61,8 @@ def auto_time_block(scheme: str, dtype_name: str, backend: str, percell: bool, w
         return 1
     if dtype_name != "f32":
         return F64_AUTO_STEPS
-    if percell:
-        return F32_AUTO_STEPS_PERCELL
+    if int(percell) >= 2:
+        return F32_AUTO_STEPS_PERCELL_BOTH
     return F32_AUTO_STEPS if world <= 2 else F32_AUTO_STEPS_MANY_RANKS
 
 

@@ -285,7 +285,8 @@ class YeeScheme(BlockedStepping):
         # runs exchange T-deep ghosts every T steps (buffer size == T)
         T = int(cfg.time_block)
         if T <= 0:  # automatic (models/blocking.py auto_time_block: one rule with the driver)
-            percell = any(getattr(self.cb.get(c), "cell", None) is not None for c in self.comps)
+            percell = sum(any(getattr(self.cb.get(c), "cell", None) is not None for c in self.comps if c[0] == k)
+                          for k in "EH")
             world = 1
             if self.halo is not None:
                 t = self.domain.topology

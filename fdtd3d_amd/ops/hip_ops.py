@@ -338,6 +338,44 @@ class HipOps:
             return (c_vp * 3)(None, None, None), sc
         return (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in names]), 1.0
 
+    def _sparse_kind(self, cb: Dict[str, Coef], names, shape):
+        """Sparse per-cell form of one kind's coefficients for the multi-row
+        blocked kernel: (float4 array over the box of cells whose value
+        differs from the kind's dominant value -- one (x, y, z, 0) vector per
+        cell --, that box, the dominant value).  A kind of one scalar gives
+        (None, empty box, scalar).  Cached on the kind's first Coef."""
+        sc = cb[names[0]].scalar
+        if all(cb[c].cell is None for c in names) and all(cb[c].scalar == sc for c in names):
+            return None, ((0, 0, 0), (0, 0, 0)), sc
+        cached = getattr(cb[names[0]], "_sparse4", None)
+        if cached is not None and cached[3] == tuple(shape):
+            return cached[:3]
+        arrs = [self._cell_array(cb[c], shape) for c in names]
+        flat = arrs[0].reshape(-1)
+        sample = flat[:: max(1, flat.numel() // (1 << 20))]
+        dom = float(torch.mode(sample).values)  # fp32 value, exact in a double
+        diff = (arrs[0] != dom) | (arrs[1] != dom) | (arrs[2] != dom)
+        lo, hi = [], []
+        for d in range(3):
+            other = tuple(a for a in range(3) if a != d)
+            nz = torch.nonzero(diff.any(dim=other)).view(-1)
+            if nz.numel() == 0:
+                lo, hi = [0, 0, 0], [0, 0, 0]
+                break
+            lo.append(int(nz[0]))
+            hi.append(int(nz[-1]) + 1)
+        box = (tuple(lo), tuple(hi))
+        if _empty(box):
+            out = (None, box, dom)
+        else:
+            sl = tuple(slice(lo[d], hi[d]) for d in range(3))
+            v = torch.zeros(tuple(hi[d] - lo[d] for d in range(3)) + (4,), dtype=self.dtype, device=self.device)
+            for n in range(3):
+                v[..., n] = arrs[n][sl]
+            out = (v.contiguous(), box, dom)
+        cb[names[0]]._sparse4 = out + (tuple(shape),)
+        return out
+
     def _cellp(self, c: Coef):
         self._cell_or_none(c)
         return None if c.cell is None else _ptr(self._scaled_cell(c))
@@ -583,6 +621,21 @@ class HipOps:
                 vals[l] = float(s[2])
             src = [idx[0], idx[1], idx[2], E.index(comp)]
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
+        if percell and self.dtype == torch.float32 and self.tb_sparse:
+            # sparse per-cell coefficients on the multi-row kernel
+            if steps > 5:
+                raise HipError("per-cell coefficients: at most 5 steps per pass")
+            ce, ebox, cbv = self._sparse_kind(cb, E, shape)
+            ch, hbox, dbv = self._sparse_kind(cb, H, shape)
+            self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
+            rc = self.lib.fdtd_tb3d_sparse_f32(
+                arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), _ptr(ce), _box_arr([ebox]), _ptr(ch),
+                _box_arr([hbox]), c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
+                _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk), c_int(steps),
+                (c_int * 4)(*src), (c_double * 8)(*vals), _stream())
+            _check(rc, "tb3d_sparse")
+            self.launches += 1
+            return
         if self.dtype == torch.float32:
             self.lib.fdtd_set_tb_vec(c_int(self.tb_vec))
             self.lib.fdtd_set_tb_rows(c_int(self.tb_rows))
@@ -675,6 +728,7 @@ class HipOps:
     tb_variant = 4  # multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched, bit 2 XCD tile order
     tb_mrows = 0  # adjacent y rows per wave (multi-row kernel): 0 auto, 1 single-row kernel, 2
     tb_thin_single_row = True  # auto mode: output boxes <= 8 rows in y use the single-row kernel
+    tb_sparse = True  # per-cell fp32 coefficients: sparse float4 boxes on the multi-row kernel
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],

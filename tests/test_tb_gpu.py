@@ -7,6 +7,7 @@ import torch
 
 from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
 from fdtd3d_amd.ops import make_ops
+from fdtd3d_amd.ops.coef import Coef
 
 pytestmark = pytest.mark.gpu
 
@@ -42,7 +43,7 @@ CASES = [
 
 CASES_MR = CASES + [
     ((26, 70, 140), 5, "vacuum", None, True),       # 3 y tiles of the 2-row kernel, 3 z tiles
-    ((22, 40, 72), 6, "sphere", ((6, 6, 8), (16, 34, 64)), False),
+    ((22, 40, 72), 5, "sphere", ((6, 6, 8), (16, 34, 64)), False),
     ((20, 36, 68), 6, "vacuum", ((0, 0, 0), (20, 36, 68)), True),
 ]
 
@@ -64,6 +65,7 @@ def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec, rows, xcd, mrows, v
     a.ops.tb_xcd = xcd
     a.ops.tb_mrows = mrows
     a.ops.tb_variant = variant
+    a.ops.tb_sparse = mrows != 1  # single-row runs keep the full per-cell planes
     b = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
     _randomize(a)
     _randomize(b)
@@ -78,6 +80,49 @@ def test_tb_op_vs_torch(gpu, size, T, scene, obox, src, vec, rows, xcd, mrows, v
     a.ops.tb_step(a.F[0], a.F_alt[0], upd, ob, a.cb, T, srcs)
     b.ops.tb_step(b.F[0], b.F_alt[0], upd, ob, b.cb, T, srcs)
     torch.cuda.synchronize()
+    for c in a.comps:
+        x = a.F_alt[0][c].double().cpu()
+        y = b.F_alt[0][c]
+        err = float((x - y).abs().max())
+        assert err <= 2e-5 * (float(y.abs().max()) + 1.0), (c, err)
+
+
+SPARSE_BOXES = [((6, 10, 30), (20, 37, 101)), ((0, 0, 0), (11, 50, 8)), ((25, 44, 128), (30, 50, 136))]
+
+
+@pytest.mark.parametrize("kinds", ["E", "H", "EH"])
+@pytest.mark.parametrize("T", [1, 3, 5])
+@pytest.mark.parametrize("box", SPARSE_BOXES)
+def test_tb_sparse_coefs(gpu, kinds, T, box):
+    """Sparse per-cell coefficients (float4 box arrays, multi-row kernel):
+    per-cell E only (dielectric), H only (magnetic, scalar E), or both; one
+    component of each per-cell kind stays scalar; boxes inside the grid, on
+    its low corner and on its high corner."""
+    size = (30, 50, 136)
+    cfg = SchemeConfig(scheme="3d", size=size, scene="vacuum", dtype="f32", use_fused=True)
+    a = _scheme(cfg, "hip", gpu, torch.float32)
+    b = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
+    g = torch.Generator().manual_seed(11)
+    sl = tuple(slice(box[0][d], box[1][d]) for d in range(3))
+    for c in ("Ex", "Ez", "Hy", "Hz"):
+        if c[0] not in kinds:
+            continue
+        cell = torch.ones(size, dtype=torch.float64)
+        cell[sl] = 0.3 + 0.7 * torch.rand(cell[sl].shape, generator=g, dtype=torch.float64)
+        cell32 = cell.float()
+        a.cb[c] = Coef(scalar=a.cb[c].scalar, cell=cell32.to(gpu))
+        b.cb[c] = Coef(scalar=b.cb[c].scalar, cell=cell32.double())
+    _randomize(a)
+    _randomize(b)
+    upd = {c: a.local_box(c) for c in a.comps}
+    ob = ((0, 0, 0), size)
+    srcs = [("Ez", (15, 25, 68), 0.5 + 0.25 * l) for l in range(T)]
+    a.ops.tb_step(a.F[0], a.F_alt[0], upd, ob, a.cb, T, srcs)
+    b.ops.tb_step(b.F[0], b.F_alt[0], upd, ob, b.cb, T, srcs)
+    torch.cuda.synchronize()
+    ce = a.cb["Ex"]._sparse4 if "E" in kinds else None
+    if ce is not None:
+        assert tuple(ce[1][0]) == box[0] and tuple(ce[1][1]) == box[1], ce[1]
     for c in a.comps:
         x = a.F_alt[0][c].double().cpu()
         y = b.F_alt[0][c]
