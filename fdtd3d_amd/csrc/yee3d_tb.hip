@@ -68,6 +68,52 @@ struct TbSrc {
   float v[8];  // hard-source value applied after E update of level l
 };
 
+// TF/SF plane-wave corrections folded into the blocked passes (fdtd3d_amd/
+// models/tfsf.py TfsfSets).  A set is one (component, TF/SF face) pair of the
+// reference's border tests (Scheme3D.cpp:138-208, YeeGridLayout.cpp:327-809):
+// a box of target cells, one cell thick across the face.  For an incident
+// direction along x or y the incident value a target sees depends on its
+// index along that axis only (`va`), so each pass precomputes, per level,
+// g = sign * projection * interpolated incident line at every index of a set
+// (k_tfsf_pass below) and the kernels add g to the target's curl before the
+// coefficient multiply -- from SCALAR loads (wave-uniform index), which do not
+// queue behind the vector prefetch.
+constexpr int TF_MAX_SETS = 24;
+struct TfSet {
+  int n;          // component 0..5 = Ex Ey Ez Hx Hy Hz
+  int fa;         // axis the face is perpendicular to
+  int lo[3], hi[3];
+  int va;         // table axis (0 x, 1 y)
+  int goff;       // first g entry of the set inside one level
+};
+// CPML convolution terms (fdtd3d_amd/models/cpml.py, layout of
+// yee3d_cpml.hip): per (component, term axis) the low / high psi slabs, their
+// ranges along the axis and the b / c / (1/kappa - 1) profiles (identity
+// outside the slabs).  psi index of a slab along x: ((i-lo) ny + j) nz + k;
+// along y: (i w + j-lo) nz + k; along z: (i ny + j) w + k-lo (w = hi - lo).
+struct CpmlTerm {
+  const float* psi[2];  // read (time n) ...
+  float* out[2];        // ... and written (time n + 1): ping-pong, because the
+                        // halo cells a tile recomputes belong to neighbour tiles
+                        // that may already have advanced them
+  int lo[2], hi[2];
+  const float* b;
+  const float* c;
+  const float* k;
+};
+struct CpmlDev {
+  CpmlTerm t[6][3];  // [Ex Ey Ez Hx Hy Hz][term axis]
+};
+// curl terms of each component: (axis, sign), Ex = +dHz/dy - dHy/dz etc.
+__device__ constexpr int kTermAxis[6][2] = {{1, 2}, {2, 0}, {0, 1}, {2, 1}, {0, 2}, {1, 0}};
+
+struct TfDev {
+  int nsets;
+  int ld;                   // g entries per level
+  int xpl[2][2];            // [E / H][low / high] x-face planes (-1: none)
+  TfSet s[TF_MAX_SETS];
+};
+
 // Memory access through buffer descriptors: one descriptor per (array, x
 // plane) built in SGPRs from the wave-uniform plane index, plus ONE 32-bit
 // per-lane byte offset shared by every array (buffer_load ... offen).  Flat
@@ -346,7 +392,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
 // stored after plane X+1's prefetch is issued -- vmcnt counts loads and
 // stores together in issue order, so stores issued between two prefetches
 // would otherwise be waited for with the older prefetch.
-template <int T, int V, int R, int PC, int PFD, bool DEFER>
+template <int T, int V, int R, int FX, int PFD, bool DEFER>
 __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
     const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
     const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
@@ -354,8 +400,15 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
     float* __restrict__ hxo, float* __restrict__ hyo, float* __restrict__ hzo,
     const float4* __restrict__ ce4, const float4* __restrict__ ch4, Box3 BE, Box3 BH, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
-    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz) {
-  static_assert(V == 1 || !PC, "sparse per-cell coefficients: scalar lanes");
+    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz,
+    const TfDev* __restrict__ tf, const float* __restrict__ gtab, const CpmlDev* __restrict__ cp) {
+  // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF,
+  // 8 CPML (single-step passes: the psi of a cell is read and written once)
+  constexpr int PC = FX & 3;
+  constexpr bool TFS = FX & 4;
+  constexpr bool CPM = FX & 8;
+  static_assert(!CPM || T == 1, "CPML: one step per pass");
+  static_assert(V == 1 || !FX, "sparse coefficients / TF/SF: scalar lanes");
   constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
   static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
   typedef typename VT<V>::f vec;
@@ -365,7 +418,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   constexpr unsigned VM = (1u << V) - 1u;
   __shared__ vec sX[2][4][TBW][64];
   const int lane = threadIdx.x;
-  const int w = threadIdx.y;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);  // one wave per y (SGPR)
   // Tile of this workgroup.  A row of a tile starts at an arbitrary z (the
   // stride is the 64 - 2T owned cells), so its 64 cells straddle three
   // 128-B lines, one shared with each z neighbour tile.  Workgroups are dealt
@@ -448,6 +501,123 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   }
   const bool wave_e = PCE && __any(inb & ((1u << R) - 1u));
   const bool wave_h = PCH && __any(inb >> R);
+  // TF/SF.  x-face sets (one plane each, all rows / lanes of the TF box) are
+  // rare per wave and go through scalar loads when a level hits their plane.
+  // y / z-face sets (one row or one lane column) touch few waves but every
+  // level of every trip of those waves, so each wave parks up to TF_SLOTS of
+  // them per kind in slots: slot metadata in VGPR lanes (read back with
+  // readlane at a compile-time lane), a per-lane bit per (slot, row) for the
+  // cells it covers, and per trip ONE vector load of the g values of every
+  // (slot, level, row) -- issued before the field prefetch, so the levels
+  // never wait behind it.
+  constexpr int TF_SLOTS = 6;                      // per kind
+  constexpr int TF_ENT = 2 * TF_SLOTS * T * R;     // g entries per trip (<= 128 for T <= 5)
+  static_assert(!TFS || TF_ENT <= 128, "TF/SF: at most 5 steps per pass");
+  unsigned tf_wx[2] = {0u, 0u};
+  unsigned tf_ov[2] = {0u, 0u};  // face sets beyond the slots: the scalar path every level
+  int tf_xe0 = -1, tf_xe1 = -1, tf_xh0 = -1, tf_xh1 = -1;  // x-face planes (E / H sets)
+  int tf_na0 = 0, tf_na1 = 0;                      // slots in use (E / H)
+  unsigned tf_lbits = 0;                           // bit slot * R + r: this lane in the slot's set, row r
+  int tf_mx = 0;                                   // lane s: x range of slot s (lo | hi << 16)
+  int tf_mn = 0;                                   // lane s: component of slot s
+  int tf_gb0 = 0, tf_gb1 = 0;                      // g index of entry lane / lane + 64 (plus X when va = 0)
+  bool tf_ok0 = false, tf_ok1 = false;
+  int tf_va = 0, tf_ld = 0;
+  if constexpr (TFS) {
+    const int ns = tf->nsets;
+    const int ld = tf->ld;
+    tf_ld = ld;
+    tf_va = tf->s[0].va;
+    int na[2] = {0, 0};
+    for (int si = 0; si < ns; ++si) {
+      const TfSet& S = tf->s[si];
+      unsigned rb = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int j = jw + r;
+        rb |= (kin && j >= S.lo[1] && j < S.hi[1] && kb >= S.lo[2] && kb < S.hi[2]) ? (1u << r) : 0u;
+      }
+      if (!__any(rb != 0u)) continue;
+      const int k = S.n < 3 ? 0 : 1;
+      if (S.fa == 0) {
+        tf_wx[0] |= k == 0 ? (1u << si) : 0u;
+        tf_wx[1] |= k == 1 ? (1u << si) : 0u;
+        continue;
+      }
+      const int a = k == 0 ? na[0] : na[1];
+      if (a >= TF_SLOTS) {
+        tf_ov[0] |= k == 0 ? (1u << si) : 0u;
+        tf_ov[1] |= k == 1 ? (1u << si) : 0u;
+        continue;
+      }
+      const int slot = k * TF_SLOTS + a;
+      if (k == 0) ++na[0]; else ++na[1];
+      tf_lbits |= rb << (slot * R);
+      if (lane == slot) {
+        tf_mx = S.lo[0] | (S.hi[0] << 16);
+        tf_mn = S.n;
+      }
+      // entries (slot, l, r) -> entry q = (slot * T + l) * R + r
+#pragma unroll
+      for (int l = 0; l < T; ++l)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int q = (slot * T + l) * R + r;
+          // level l: E sets on plane X - l, H sets on X - l - 1
+          const int base = l * ld + S.goff + (S.va == 0 ? -S.lo[0] - l - k : (jw + r) - S.lo[1]);
+          if (lane == q) { tf_gb0 = base; tf_ok0 = true; }
+          if (lane + 64 == q) { tf_gb1 = base; tf_ok1 = true; }
+        }
+    }
+    tf_na0 = na[0];
+    tf_na1 = na[1];
+    tf_xe0 = tf->xpl[0][0];
+    tf_xe1 = tf->xpl[0][1];
+    tf_xh0 = tf->xpl[1][0];
+    tf_xh1 = tf->xpl[1][1];
+  }
+  const bool tf_slots = TFS && (tf_na0 + tf_na1) > 0;
+  float tf_g0 = 0.f, tf_g1 = 0.f;  // this trip's g entries (lane q, q + 64)
+  // add the TF/SF corrections of kind k at level l, plane p, row r to the curls
+  auto tf_apply = [&](int k, int l, int p, int r, vec& c0, vec& c1, vec& c2) {
+    if constexpr (TFS) {
+      // y / z-face slots
+      if (tf_slots) {
+#pragma unroll
+        for (int a = 0; a < TF_SLOTS; ++a) {
+          if (a >= (k == 0 ? tf_na0 : tf_na1)) break;
+          const int slot = k * TF_SLOTS + a;
+          const int xr = __builtin_amdgcn_readlane(tf_mx, slot);
+          if ((unsigned)(p - (xr & 0xffff)) >= (unsigned)((xr >> 16) - (xr & 0xffff))) continue;
+          const int q = (slot * T + l) * R + r;
+          const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q < 64 ? tf_g0 : tf_g1), q & 63));
+          const float gl = ((tf_lbits >> (slot * R + r)) & 1u) ? g : 0.f;
+          const int c = __builtin_amdgcn_readlane(tf_mn, slot) - 3 * k;
+          c0 = c0 + (vec)(c == 0 ? gl : 0.f);
+          c1 = c1 + (vec)(c == 1 ? gl : 0.f);
+          c2 = c2 + (vec)(c == 2 ? gl : 0.f);
+        }
+      }
+      // x-face sets on their plane
+      const bool xp = k == 0 ? (p == tf_xe0 || p == tf_xe1) : (p == tf_xh0 || p == tf_xh1);
+      unsigned cand = (xp ? (k == 0 ? tf_wx[0] : tf_wx[1]) : 0u) | (k == 0 ? tf_ov[0] : tf_ov[1]);
+      const int j = jw + r;
+      while (cand) {
+        const int si = __builtin_ctz(cand);
+        cand &= cand - 1u;
+        const TfSet& S = tf->s[si];
+        if ((unsigned)(p - S.lo[0]) >= (unsigned)(S.hi[0] - S.lo[0]) || j < S.lo[1] || j >= S.hi[1]) continue;
+        const float g = gtab[l * tf->ld + S.goff + (S.va == 0 ? p - S.lo[0] : j - S.lo[1])];
+        // g on the set's lanes, 0 elsewhere, added to the set's component by
+        // selects (conditional adds make the compiler index a scratch array)
+        const float gl = (kb >= S.lo[2] && kb < S.hi[2]) ? g : 0.f;
+        const int c = S.n - 3 * k;
+        c0 = c0 + (vec)(c == 0 ? gl : 0.f);
+        c1 = c1 + (vec)(c == 1 ? gl : 0.f);
+        c2 = c2 + (vec)(c == 2 ? gl : 0.f);
+      }
+    }
+  };
   typedef unsigned u3 __attribute__((ext_vector_type(3)));
   auto coef_ld = [&](const float4* arr, const Box3& B, unsigned off, size_t pl, int p) -> u3 {
     const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)arr + (size_t)(p - B.lo[0]) * pl),
@@ -476,6 +646,83 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
       sC[sl][1][R * w + r][lane] = __uint_as_float(v.y);
       sC[sl][2][R * w + r][lane] = __uint_as_float(v.z);
     }
+  }
+
+  // CPML helpers (T = 1 single-step passes).  Terms are (component n, t):
+  // axis kTermAxis[n][t].  y terms: Ex.0 Ez.1 Hx.1 Hz.0; z terms: Ex.1 Ey.0
+  // Hx.0 Hy.1; x terms: the rest.
+  auto ytm_index = [](int n) -> int { return n == 0 ? 0 : (n == 2 ? 1 : (n == 3 ? 2 : 3)); };
+  auto ztm_index = [](int n) -> int { return n == 0 ? 0 : (n == 1 ? 1 : (n == 3 ? 2 : 3)); };
+  // slab side holding index v along the term's axis (-1: none)
+  auto side_of = [&](const CpmlTerm& tm, int v) -> int {
+    return (tm.psi[0] && v >= tm.lo[0] && v < tm.hi[0]) ? 0 : ((tm.psi[1] && v >= tm.lo[1] && v < tm.hi[1]) ? 1 : -1);
+  };
+  auto psi_side_x = [&](int n, int t, int pl) -> int {
+    return kTermAxis[n][t] == 0 ? side_of(cp->t[n][0], pl) : -1;
+  };
+  auto psi_side_y = [&](int n, int t, int j) -> int {
+    return kTermAxis[n][t] == 1 ? side_of(cp->t[n][1], j) : -1;
+  };
+  // descriptor of plane pl of the side-sd slab of term (n, t), read or written copy
+  auto psi_rsrc = [&](int n, int t, int sd, int pl, bool wr) -> Rsrc {
+    const int a = kTermAxis[n][t];
+    const CpmlTerm& tm = cp->t[n][a];
+    const int wd = tm.hi[sd] - tm.lo[sd];
+    const size_t pe_ = a == 0 ? (size_t)ny * nz : (a == 1 ? (size_t)wd * nz : (size_t)ny * wd);
+    const size_t first = a == 0 ? (size_t)(pl - tm.lo[sd]) * pe_ : (size_t)pl * pe_;
+    const float* base = wr ? tm.out[sd] : tm.psi[sd];
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(base + first), (short)0, (int)(pe_ * 4), 0x00020000);
+  };
+  // lane byte offset of row r in that plane (past the plane for lanes outside the slab)
+  auto psi_off = [&](int n, int t, int sd, int r) -> unsigned {
+    const int a = kTermAxis[n][t];
+    const CpmlTerm& tm = cp->t[n][a];
+    if (a == 0) return roff[r];
+    if (a == 1) return roff[r] - (unsigned)(tm.lo[sd] * nz) * 4u;  // sentinel offsets stay past the plane
+    const int j = jw + r;
+    const bool in = kin && j >= 0 && j < ny && kb >= tm.lo[sd] && kb < tm.hi[sd];
+    return in ? (unsigned)(j * (tm.hi[sd] - tm.lo[sd]) + (kb - tm.lo[sd])) * 4u : 0xF0000000u;
+  };
+  // wave-level activity of the 12 terms (bit 2n + t): x terms always (the
+  // plane decides per trip), y terms when a row of the wave lies in a slab,
+  // z terms when a lane does; z-term profiles per lane, y-term profiles of
+  // the wave's rows in LDS (uniform reads)
+  unsigned cpm_wave = 0;
+  float ZB[CPM ? 4 : 1], ZC[CPM ? 4 : 1], ZK[CPM ? 4 : 1];
+  __shared__ float sYP[CPM ? TBW : 1][CPM ? 4 * R * 3 : 1];
+  if constexpr (CPM) {
+#pragma unroll
+    for (int n = 0; n < 6; ++n)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int a = kTermAxis[n][t];
+        const CpmlTerm& tm = cp->t[n][a];
+        bool act = false;
+        if (a == 0) {
+          act = tm.psi[0] || tm.psi[1];
+        } else if (a == 1) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int j = jw + r;
+            const bool in = side_of(tm, j) >= 0;
+            act |= in;
+            const int q = (ytm_index(n) * R + r) * 3;
+            if (lane == 0) {
+              sYP[w][q] = in ? tm.b[j] : 1.f;
+              sYP[w][q + 1] = in ? tm.c[j] : 0.f;
+              sYP[w][q + 2] = in ? tm.k[j] : 0.f;
+            }
+          }
+        } else {
+          const bool in = kin && side_of(tm, kb) >= 0;
+          act = __any(in);
+          const int zi = ztm_index(n);
+          ZB[zi] = in ? tm.b[kb] : 1.f;
+          ZC[zi] = in ? tm.c[kb] : 0.f;
+          ZK[zi] = in ? tm.k[kb] : 0.f;
+        }
+        cpm_wave |= act ? (1u << (2 * n + t)) : 0u;
+      }
   }
 
   auto run = [&](auto allin_tag) {
@@ -592,6 +839,80 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
       }
       return make_float3(sc, sc, sc);
     };
+    // CPML: this trip's psi (E terms on plane X, H terms on X - 1), loaded
+    // before the prefetch (vmcnt order).  Slab membership is wave-uniform for
+    // x (plane) and y (row) terms and per lane for z terms; every access goes
+    // through a buffer descriptor of the slab plane with a 32-bit lane offset,
+    // and lanes outside a slab get an offset past the descriptor (reads 0,
+    // stores dropped) instead of a branch.
+    float PS[CPM ? 6 : 1][2][R];
+    if constexpr (CPM) {
+#pragma unroll
+      for (int n = 0; n < 6; ++n) {
+        const int pl = n < 3 ? X : X - 1;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int a = kTermAxis[n][t];
+#pragma unroll
+          for (int r = 0; r < R; ++r) PS[n][t][r] = 0.f;
+          if (!(cpm_wave >> (2 * n + t) & 1u) || pl < 0 || pl >= nx) continue;
+#pragma unroll
+          for (int sd = 0; sd < 2; ++sd) {
+            const int side_pl = psi_side_x(n, t, pl);
+            if (a == 0 && side_pl != sd) continue;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              if (a == 1 && psi_side_y(n, t, jw + r) != sd) continue;
+              const unsigned off = psi_off(n, t, sd, r);
+              PS[n][t][r] +=
+                  __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(psi_rsrc(n, t, sd, pl, false), off, 0, 0));
+            }
+          }
+        }
+      }
+    }
+    // psi update of term t of component n (plane pl, row r) from its raw
+    // difference d; returns the curl correction sign * ((1/kappa - 1) d + psi)
+    auto cpml = [&](int n, int t, int pl, int r, const vec& d) -> vec {
+      if constexpr (CPM) {
+        const int a = kTermAxis[n][t];
+        const int sg = t == 0 ? 1 : -1;
+        if (!(cpm_wave >> (2 * n + t) & 1u)) return zero;
+        float bb, cc, kk;
+        if (a == 0) {
+          if (psi_side_x(n, t, pl) < 0) return zero;
+          const CpmlTerm& tm = cp->t[n][0];
+          bb = tm.b[pl];
+          cc = tm.c[pl];
+          kk = tm.k[pl];
+        } else if (a == 1) {
+          if (psi_side_y(n, t, jw + r) < 0) return zero;
+          const int q = (ytm_index(n) * R + r) * 3;
+          bb = sYP[w][q];
+          cc = sYP[w][q + 1];
+          kk = sYP[w][q + 2];
+        } else {
+          const int zi = ztm_index(n);
+          bb = ZB[zi];
+          cc = ZC[zi];
+          kk = ZK[zi];
+        }
+        const float pn = bb * PS[n][t][r] + cc * d[0];
+        PS[n][t][r] = pn;
+        const float cr = kk * d[0] + pn;  // 0 off a z slab (identity profile, psi 0)
+        return (vec)(sg > 0 ? cr : -cr);
+      }
+      return zero;
+    };
+    if (tf_slots) {
+      // this trip's g entries of the face slots (va = 0: index moves with X)
+      // (entries of planes outside a set's x range are never used; their
+      // index is clamped into the table)
+      const int dx = tf_va == 0 ? X : 0;
+      const int last = T * tf_ld - 1;
+      tf_g0 = tf_ok0 ? gtab[min(max(tf_gb0 + dx, 0), last)] : 0.f;
+      if (TF_ENT > 64) tf_g1 = tf_ok1 ? gtab[min(max(tf_gb1 + dx, 0), last)] : 0.f;
+    }
     // next plane(s) in flight under this plane's levels
     if (PFD == 2)
       load_plane(X + 2, Hn2, En2);
@@ -625,9 +946,21 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
         const float hy_k0 = lane_up(Hc[r].y[V - 1]);
         const float hx_k0 = lane_up(Hc[r].x[V - 1]);
         const float3 ce = kcoef(true, l, pe, r);
-        En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * ((Hc[r].z - hz_j) - (Hc[r].y - zm1<V>(Hc[r].y, hy_k0)));
-        En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * ((Hc[r].x - zm1<V>(Hc[r].x, hx_k0)) - (Hc[r].z - Hp[l][r].z));
-        En[r].z = Ec[r].z + coef(bez, pe, r, 2, ce.z) * ((Hc[r].y - Hp[l][r].y) - (Hc[r].x - hx_j));
+        const vec dxy = Hc[r].z - hz_j, dxz = Hc[r].y - zm1<V>(Hc[r].y, hy_k0);
+        const vec dyz = Hc[r].x - zm1<V>(Hc[r].x, hx_k0), dyx = Hc[r].z - Hp[l][r].z;
+        const vec dzx = Hc[r].y - Hp[l][r].y, dzy = Hc[r].x - hx_j;
+        vec cx = dxy - dxz;
+        vec cy = dyz - dyx;
+        vec cz = dzx - dzy;
+        if constexpr (CPM) {
+          cx += cpml(0, 0, pe, r, dxy) + cpml(0, 1, pe, r, dxz);
+          cy += cpml(1, 0, pe, r, dyz) + cpml(1, 1, pe, r, dyx);
+          cz += cpml(2, 0, pe, r, dzx) + cpml(2, 1, pe, r, dzy);
+        }
+        tf_apply(0, l, pe, r, cx, cy, cz);
+        En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * cx;
+        En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * cy;
+        En[r].z = Ec[r].z + coef(bez, pe, r, 2, ce.z) * cz;
         if (src_plane && jw + r == src_j && src_k >= kb && src_k < kb + V) {
           const int q = src_k - kb;
           if (src_comp == 0) En[r].x[q] = sv.v[l];
@@ -644,17 +977,52 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
         const float ex_k3 = lane_dn(Ep[l][r].x[0]);
         F3<V> Hn;
         const float3 ch = kcoef(false, l, ph, r);
-        Hn.x = Hp[l][r].x + coef(bhx, ph, r, 3, ch.x) *
-                                ((zp1<V>(Ep[l][r].y, ey_k3) - Ep[l][r].y) - (ez_jn - Ep[l][r].z));
-        Hn.y = Hp[l][r].y + coef(bhy, ph, r, 4, ch.y) *
-                                ((En[r].z - Ep[l][r].z) - (zp1<V>(Ep[l][r].x, ex_k3) - Ep[l][r].x));
-        Hn.z = Hp[l][r].z + coef(bhz, ph, r, 5, ch.z) * ((ex_jn - Ep[l][r].x) - (En[r].y - Ep[l][r].y));
+        const vec gxz = zp1<V>(Ep[l][r].y, ey_k3) - Ep[l][r].y, gxy = ez_jn - Ep[l][r].z;
+        const vec gyx = En[r].z - Ep[l][r].z, gyz = zp1<V>(Ep[l][r].x, ex_k3) - Ep[l][r].x;
+        const vec gzy = ex_jn - Ep[l][r].x, gzx = En[r].y - Ep[l][r].y;
+        vec dx = gxz - gxy;
+        vec dy = gyx - gyz;
+        vec dz = gzy - gzx;
+        if constexpr (CPM) {
+          dx += cpml(3, 0, ph, r, gxz) + cpml(3, 1, ph, r, gxy);
+          dy += cpml(4, 0, ph, r, gyx) + cpml(4, 1, ph, r, gyz);
+          dz += cpml(5, 0, ph, r, gzy) + cpml(5, 1, ph, r, gzx);
+        }
+        tf_apply(1, l, ph, r, dx, dy, dz);
+        Hn.x = Hp[l][r].x + coef(bhx, ph, r, 3, ch.x) * dx;
+        Hn.y = Hp[l][r].y + coef(bhy, ph, r, 4, ch.y) * dy;
+        Hn.z = Hp[l][r].z + coef(bhz, ph, r, 5, ch.z) * dz;
         // later rows (r+1 ..) read only their own and higher rows' Ep, so
         // row r rotates as soon as its H is done
         Ec[r] = Ep[l][r];
         Ep[l][r] = En[r];
         Hp[l][r] = Hc[r];
         Hc[r] = Hn;
+      }
+    }
+    if constexpr (CPM) {
+      // psi of owned cells inside their component's update box
+#pragma unroll
+      for (int n = 0; n < 6; ++n) {
+        const int pl = n < 3 ? X : X - 1;
+        if (pl < i0 || pl >= i1 || !xin(*bx[n], pl)) continue;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int a = kTermAxis[n][t];
+          if (!(cpm_wave >> (2 * n + t) & 1u)) continue;
+#pragma unroll
+          for (int sd = 0; sd < 2; ++sd) {
+            if (a == 0 && psi_side_x(n, t, pl) != sd) continue;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              if (a == 1 && psi_side_y(n, t, jw + r) != sd) continue;
+              const bool st = ((mbits >> (r * 7 + 6)) & 1u) && ((mbits >> (r * 7 + n)) & 1u);
+              const unsigned off = st ? psi_off(n, t, sd, r) : 0xF0000000u;
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PS[n][t][r]), psi_rsrc(n, t, sd, pl, true), off,
+                                                    0, 0);
+            }
+          }
+        }
       }
     }
     if (ring_ld) {
@@ -764,21 +1132,21 @@ int g_tb_mr_xcd = 1;   // multi-row kernel: XCD-contiguous tile order, z fastest
 int g_tb_variant = 0;  // multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched
 const int kNoBox[6] = {0, 0, 0, 0, 0, 0};
 
-template <int T, int V, int R, int PC>
+template <int T, int V, int R, int FX>
 int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                  const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
                  int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
-                 hipStream_t s) {
+                 const TfDev* tf, const float* gtab, const CpmlDev* cp, hipStream_t s) {
   constexpr int HL = (T + V - 1) / V;
   constexpr int TBZ = (64 - 2 * HL) * V;
   dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * T),
             cdiv(O.hi[0] - O.lo[0], xchunk));
 #define MR_LAUNCH(PFD, DEFER)                                                                                 \
-  k_tb3d_mr<T, V, R, PC, PFD, DEFER><<<grid, dim3(64, TBW), 0, s>>>(                                   \
+  k_tb3d_mr<T, V, R, FX, PFD, DEFER><<<grid, dim3(64, TBW), 0, s>>>(                                        \
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
-      O, xchunk, src[0], src[1], src[2], src[3], sv, g_tb_mr_xcd | (g_tb_mr_noallin << 1))
-  if constexpr (PC != 0) {
+      O, xchunk, src[0], src[1], src[2], src[3], sv, g_tb_mr_xcd | (g_tb_mr_noallin << 1), tf, gtab, cp)
+  if constexpr (FX != 0) {
     MR_LAUNCH(1, false);  // tuning variants: uniform media only
   } else {
     switch (g_tb_variant & 3) {
@@ -793,33 +1161,55 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
 }
 
 template <int T>
-int launch_tb_mr_sel(int pc, const float* const* ein, const float* const* hin, float* const* eout,
+int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                      float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                      float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
-                     const int* src, const TbSrc& sv, hipStream_t s) {
+                     const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const CpmlDev* cp,
+                     hipStream_t s) {
   // scalar lanes with 2 rows per wave: R = 4 or float2 lanes at R = 2
   // exceed 128 VGPRs and spill from T = 2 on
-#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s
+#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, s
+  if constexpr (T == 1) {
+    // CPML single-step passes (hybrid shells)
+    switch (fx) {
+      case 8: return launch_tb_mr<T, 1, 2, 8>(MR_ARGS);
+      case 9: return launch_tb_mr<T, 1, 2, 9>(MR_ARGS);
+      case 10: return launch_tb_mr<T, 1, 2, 10>(MR_ARGS);
+      case 11: return launch_tb_mr<T, 1, 2, 11>(MR_ARGS);
+      case 12: return launch_tb_mr<T, 1, 2, 12>(MR_ARGS);
+      case 13: return launch_tb_mr<T, 1, 2, 13>(MR_ARGS);
+      case 14: return launch_tb_mr<T, 1, 2, 14>(MR_ARGS);
+      case 15: return launch_tb_mr<T, 1, 2, 15>(MR_ARGS);
+    }
+  } else {
+    if (fx & 8) return (int)hipErrorInvalidValue;
+  }
   // per-cell: one kind keeps T coefficient planes in LDS (24 KiB each, 160
-  // KiB per CU: T <= 5); both kinds keep them in registers (spill-free to T = 3)
+  // KiB per CU: T <= 5); both kinds keep them in registers (spill-free to T = 2)
   if constexpr (T <= 5) {
-    switch (pc) {
+    switch (fx) {
       case 1: return launch_tb_mr<T, 1, 2, 1>(MR_ARGS);
       case 2: return launch_tb_mr<T, 1, 2, 2>(MR_ARGS);
       case 3: return launch_tb_mr<T, 1, 2, 3>(MR_ARGS);
+      case 4: return launch_tb_mr<T, 1, 2, 4>(MR_ARGS);
+      case 5: return launch_tb_mr<T, 1, 2, 5>(MR_ARGS);
+      case 6: return launch_tb_mr<T, 1, 2, 6>(MR_ARGS);
+      case 7: return launch_tb_mr<T, 1, 2, 7>(MR_ARGS);
     }
   } else {
-    if (pc) return (int)hipErrorInvalidValue;
+    if (fx) return (int)hipErrorInvalidValue;
   }
   return launch_tb_mr<T, 1, 2, 0>(MR_ARGS);
 #undef MR_ARGS
 }
 
-// multi-row pass (scalar lanes, 2 rows per wave), uniform or sparse per-cell coefficients
-int tb_mr_dispatch(int pc, const float* const* ein, const float* const* hin, float* const* eout,
+// multi-row pass (scalar lanes, 2 rows per wave): uniform media, sparse
+// per-cell coefficients (fx bits 1 / 2), TF/SF corrections (fx bit 4)
+int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                    float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                    float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, int steps,
-                   const int* src, const TbSrc& sv, hipStream_t s) {
+                   const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const CpmlDev* cp,
+                   hipStream_t s) {
   const int R = 2, V = 1;
   if (xchunk <= 0) {
     const int HL = (steps + V - 1) / V;
@@ -827,7 +1217,7 @@ int tb_mr_dispatch(int pc, const float* const* ein, const float* const* hin, flo
     const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
     xchunk = pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps);
   }
-#define MR_ARGS pc, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s
+#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, s
   switch (steps) {
     case 1: return launch_tb_mr_sel<1>(MR_ARGS);
     case 2: return launch_tb_mr_sel<2>(MR_ARGS);
@@ -838,6 +1228,32 @@ int tb_mr_dispatch(int pc, const float* const* ein, const float* const* hin, flo
   }
 #undef MR_ARGS
   return (int)hipErrorInvalidValue;
+}
+
+// Incident line + TF/SF g tables of one blocked pass (one workgroup): for
+// each level l = 0..T-1 (step t + l) the E sets' values from the H line as
+// it stands, the line's E half step (hard source at index 0), the H sets'
+// values from the new E line, the line's H half step -- the order of the
+// stepped scheme (models/scheme.py step).  Only the first `reach` cells of
+// the line move: beyond the wave front every value is exactly 0.
+__global__ __launch_bounds__(1024) void k_tfsf_pass(float* __restrict__ einc, float* __restrict__ hinc, int n,
+                                                    float ce, float ch, TbSrc sv, int T, int reach, int nE, int nH,
+                                                    const int* __restrict__ I0, const float* __restrict__ W0,
+                                                    const float* __restrict__ W1, const float* __restrict__ C,
+                                                    float* __restrict__ gtab) {
+  const int tid = threadIdx.x;
+  const int ld = nE + nH;
+  const int m = min(n, reach);
+  for (int l = 0; l < T; ++l) {
+    for (int e = tid; e < nE; e += blockDim.x)
+      gtab[l * ld + e] = C[e] * (W0[e] * hinc[I0[e]] + W1[e] * hinc[I0[e] + 1]);
+    for (int i = tid; i < m; i += blockDim.x) einc[i] = i == 0 ? sv.v[l] : einc[i] + ce * (hinc[i - 1] - hinc[i]);
+    __syncthreads();
+    for (int e = nE + tid; e < ld; e += blockDim.x)
+      gtab[l * ld + e] = C[e] * (W0[e] * einc[I0[e]] + W1[e] * einc[I0[e] + 1]);
+    for (int i = tid; i < m && i < n - 1; i += blockDim.x) hinc[i] += ch * (einc[i] - einc[i + 1]);
+    __syncthreads();
+  }
 }
 
 }  // namespace
@@ -888,7 +1304,7 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   if (!pc && (MR > 1 || steps > 4)) {
     const Box3 nb = make_box(kNoBox);
     return tb_mr_dispatch(0, ein, hin, eout, hout, nullptr, nullptr, nb, nb, fcb, fdb, nx, ny, nz, b, O, xchunk,
-                          steps, src, sv, s);
+                          steps, src, sv, nullptr, nullptr, nullptr, s);
   }
   if (steps > 4) return (int)hipErrorInvalidValue;
   if (xchunk <= 0) {
@@ -917,18 +1333,22 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   return (int)hipErrorInvalidValue;
 }
 
-// T fused leapfrog steps with sparse per-cell coefficients (multi-row
-// kernel): ``ce4`` / ``ch4`` hold the E / H coefficients of the three
-// components as one float4 per cell of the box ``ebox`` / ``hbox`` (x-major,
-// z fastest, .w unused); every cell outside its kind's box -- and either kind
-// whose array is null -- uses the scalar ``cb`` / ``db``.  Other arguments as
-// fdtd_tb3d_v4_f32.
-FDTD_API int fdtd_tb3d_sparse_f32(const float* const* ein, const float* const* hin, float* const* eout,
-                                  float* const* hout, const void* ce4, const int* ebox, const void* ch4,
-                                  const int* hbox, double cb, double db, int nx, int ny, int nz, const int* boxes,
-                                  const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
-                                  void* stream) {
+// T fused leapfrog steps on the multi-row kernel with its extensions:
+// sparse per-cell coefficients -- ``ce4`` / ``ch4`` hold the E / H
+// coefficients of the three components as one float4 per cell of the box
+// ``ebox`` / ``hbox`` (x-major, z fastest, .w unused); every cell outside its
+// kind's box, and either kind whose array is null, uses the scalar ``cb`` /
+// ``db`` -- TF/SF corrections (``tf`` = device TfDev, ``gtab`` = the g
+// table of this pass's first level, from fdtd_tfsf_pass_f32; null: none) and,
+// for single-step passes, CPML (``cpml`` = device CpmlDev; null: none).
+// Other arguments as fdtd_tb3d_v4_f32.
+FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* const* eout,
+                               float* const* hout, const void* ce4, const int* ebox, const void* ch4,
+                               const int* hbox, double cb, double db, int nx, int ny, int nz, const int* boxes,
+                               const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
+                               const void* tf, const float* gtab, const void* cpml, void* stream) {
   if (nz % 4 != 0 || steps < 1 || steps > 6) return (int)hipErrorInvalidValue;
+  if (cpml && steps != 1) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const Box3 O = make_box(obox);
@@ -936,8 +1356,29 @@ FDTD_API int fdtd_tb3d_sparse_f32(const float* const* ein, const float* const* h
   const Box3 BE = make_box(ce4 ? ebox : kNoBox), BH = make_box(ch4 ? hbox : kNoBox);
   TbSrc sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
-  const int pc = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0);
-  return tb_mr_dispatch(pc, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
+  const int fx = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0) | (tf && gtab ? 4 : 0) |
+                 (cpml ? 8 : 0);
+  return tb_mr_dispatch(fx, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
                         (const float4*)(box_empty(BH) ? nullptr : ch4), BE, BH, (float)cb, (float)db, nx, ny, nz, b,
-                        O, xchunk, steps, src, sv, (hipStream_t)stream);
+                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, (const CpmlDev*)cpml,
+                        (hipStream_t)stream);
+}
+
+// size of the CpmlDev block the host fills (ABI check)
+FDTD_API int fdtd_cpmldev_size() { return (int)sizeof(CpmlDev); }
+
+// size of the TfDev block the host fills (ABI check)
+FDTD_API int fdtd_tfdev_size() { return (int)sizeof(TfDev); }
+
+// incident line advanced ``steps`` steps from step t (source value per step
+// in ``src_vals``) and the per-level g tables of the pass (k_tfsf_pass)
+FDTD_API int fdtd_tfsf_pass_f32(float* einc, float* hinc, int n, double ce, double ch, const double* src_vals,
+                                int steps, int reach, int nE, int nH, const int* I0, const float* W0,
+                                const float* W1, const float* C, float* gtab, void* stream) {
+  if (steps < 1 || steps > 8) return (int)hipErrorInvalidValue;
+  TbSrc sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = l < steps ? (float)src_vals[l] : 0.f;
+  k_tfsf_pass<<<1, 1024, 0, (hipStream_t)stream>>>(einc, hinc, n, (float)ce, (float)ch, sv, steps, reach, nE, nH,
+                                                   I0, W0, W1, C, gtab);
+  FDTD_RETURN_LAUNCH_STATUS();
 }

@@ -133,6 +133,14 @@ class BlockedStepping:
                 return
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
                 return
+        if self._hybrid2_ok():
+            plan = self._hybrid2_plan(H)
+            if plan is not None:
+                if not hasattr(self, "F_alt"):
+                    self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+                self.F_3 = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+                self.hybrid = plan
+                return
         plan = self._hybrid_plan(H)
         if plan is None:
             return
@@ -145,12 +153,104 @@ class BlockedStepping:
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
         self.hybrid = plan
 
+    # ------------------------------------------------ hybrid, single-pass shell
+    def _hybrid2_ok(self) -> bool:
+        """CPML / TF-SF runs whose every irregular term the fp32 multi-row
+        kernel applies itself: CPML psi (single-step passes), TF/SF sets
+        (incident direction along x or y), sparse per-cell coefficients."""
+        cfg = self.cfg
+        return (self.ops.name == "hip" and self.dtype == torch.float32 and cfg.scheme == "3d"
+                and self.halo is None and not self.use_upml_chain and not cfg.use_metamaterials
+                and not cfg.use_amp_mode and self.domain.shape[2] % 4 == 0
+                and (not cfg.use_tfsf or getattr(self, "tfsf_sets", None) is not None)
+                and (cfg.use_pml and self.use_cpml))
+
+    def _hybrid2_plan(self, T: int):
+        """Blocked core + single-pass shell with shrinking windows.
+
+        The core ``K`` (cells at least ``pml + T + 2`` from every face) takes
+        one ``T``-step blocked pass.  The shell -- everything else -- takes
+        ``T`` single-step passes of the same kernel with its CPML / TF-SF
+        terms, step ``s`` over ``alloc - K.shrink(T - s)``: each step's
+        window is one cell deeper into the core than the next needs, so
+        every shell value is exact without a stale band (the deep-halo
+        rule, reference ``ParallelGrid.cpp:2365-2489``).  Single-step passes
+        read one buffer and write another, so the shell ping-pongs between
+        ``F_alt`` and a third buffer while the core reads the untouched
+        ``F``."""
+        cfg = self.cfg
+        size = cfg.size
+        m = T + 2
+        lo, hi = [0, 0, 0], list(size)
+        for a in range(3):
+            edge = self.layout.pml_size[a] if cfg.use_pml else 0
+            lo[a], hi[a] = edge + m, size[a] - edge - m
+        K = (tuple(lo), tuple(hi))
+        if box_empty(K) or box_volume(K) < 0.25 * size[0] * size[1] * size[2]:
+            return None
+        # every CPML slab must stay T + 1 clear of the core
+        g = (tuple(lo[d] - T - 1 for d in range(3)), tuple(hi[d] + T + 1 for d in range(3)))
+        for slabs in self.cpml.slabs.values():
+            for sl in slabs:
+                if not box_empty(box_intersect(g, sl.gbox)):
+                    return None
+        alloc = self.domain.allocated_global()
+        windows = []
+        for st in range(1, T + 1):
+            d = T - st
+            Kd = (tuple(lo[a] + d for a in range(3)), tuple(hi[a] - d for a in range(3)))
+            windows.append([self.domain.to_local(b) for b in box_subtract(alloc, Kd) if not box_empty(b)])
+        upd = {c: self.local_box(c, alloc) for c in self.comps}
+        return {"T": T, "v2": True, "core": [self.domain.to_local(K)], "windows": windows, "upd": upd,
+                "core_cells": box_volume(K)}
+
+    def _hybrid2_step(self, T: int) -> None:
+        hp = self.hybrid
+        if T != hp["T"]:
+            # a short tail pass: its own (shallower) windows
+            hp = self.__dict__.setdefault("_hybrid2_tails", {}).get(T)
+            if hp is None:
+                hp = self._hybrid2_plan(T)
+                self._hybrid2_tails[T] = hp
+            if hp is None:
+                for _ in range(T):
+                    self.step()
+                return
+        srcs = self._pass_sources(self.t, T)
+        for p in range(self.planes):
+            tf = self._tfsf_pass(p, T)
+            P, Q, Z = self.F[p], self.F_alt[p], self.F_3[p]
+            cur = P
+            with self.prof.phase("shell"):
+                for st in range(1, T + 1):
+                    out = Q if st % 2 == 1 else Z
+                    sv = None if srcs[p] is None else [srcs[p][st - 1]]
+                    tfs = None if tf is None else (tf[0], tf[1], st - 1)
+                    cp = self.cpml.device_table(p) if self.use_cpml else None
+                    for b in hp["windows"][st - 1]:
+                        self.ops.tb_step(cur, out, hp["upd"], b, self.cb, 1, sv, tfsf=tfs, cpml=cp)
+                    if self.use_cpml:
+                        self.cpml.flip(p)
+                    cur = out
+            with self.prof.phase("blocked-core"):
+                for ob in hp["core"]:
+                    self.ops.tb_step(P, cur, hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf)
+            rest = [b for b in (Q, Z) if b is not cur]
+            self.F[p], self.F_alt[p], self.F_3[p] = cur, P, rest[0]
+        self.t += T
+        if self.cfg.check_finite and (self.t // max(1, self.cfg.finite_check_step)
+                                      != (self.t - T) // max(1, self.cfg.finite_check_step)):
+            self.check_finite()
+
     def _hybrid_plan(self, T: int):
         dom = self.domain
         cfg = self.cfg
         size = cfg.size
         alloc = dom.allocated_global()
         m = T + 2  # core margin to every irregular cell (staggering slack included)
+        # the fp32 blocked kernel applies TF/SF corrections itself (TfsfSets):
+        # TF/SF faces may then lie inside the core
+        in_kernel_tfsf = cfg.use_tfsf and getattr(self, "tfsf_sets", None) is not None
         lo, hi = [0, 0, 0], list(size)
         act = [self.layout.active(a) for a in range(3)]  # 2D: z is one cell, never cut
         for a in range(3):
@@ -159,7 +259,7 @@ class BlockedStepping:
             edge = 0
             if cfg.use_pml:
                 edge = max(edge, self.layout.pml_size[a])
-            if cfg.use_tfsf:
+            if cfg.use_tfsf and not in_kernel_tfsf:
                 edge = max(edge, cfg.tfsf_size[a] + 1)
             lo[a], hi[a] = edge + m, size[a] - edge - m
         K = (tuple(lo), tuple(hi))
@@ -215,7 +315,7 @@ class BlockedStepping:
             g = grow(ob, T + 1)
             if any(not box_empty(box_intersect(g, b)) for b in irregular):
                 return None
-            if cfg.use_tfsf:
+            if cfg.use_tfsf and not in_kernel_tfsf:
                 lg = dom.to_local(g)
                 for c in self.comps:
                     for tab in self.tfsf[c]:
@@ -256,6 +356,19 @@ class BlockedStepping:
                 "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
                 "cut_cells": box_volume(Dm) if Dm is not None else 0}
 
+    def _tfsf_pass(self, p: int, T: int, level0: int = 0):
+        """In-kernel TF/SF of a blocked pass starting at step ``self.t`` on
+        plane ``p``: advances the plane's incident line ``T`` steps and returns
+        the ``tfsf`` argument of ``ops.tb_step`` (None without in-kernel
+        TF/SF)."""
+        sets = getattr(self, "tfsf_sets", None)
+        if not self.cfg.use_tfsf or sets is None:
+            return None
+        vals = [self.source_value(self.t + l, p) for l in range(T)]
+        g = self.ops.tfsf_pass(self.einc[p], self.hinc[p], self.inc_ce, self.inc_ch, vals, self.t + T + 2, sets,
+                               slot=p)
+        return (sets, g, level0)
+
     def _pass_sources(self, t: int, T: int):
         """Per plane: the hard point source's value at each of the pass's T
         E half steps (None without a point source on this rank)."""
@@ -269,12 +382,27 @@ class BlockedStepping:
         return srcs
 
     def _hybrid_step(self, T: int) -> None:
+        if self.hybrid.get("v2"):
+            self._hybrid2_step(T)
+            return
         hp = self.hybrid
         srcs = self._pass_sources(self.t, T)
         with self.prof.phase("blocked-core"):
             for p in range(self.planes):
+                tf = None
+                if self.cfg.use_tfsf and getattr(self, "tfsf_sets", None) is not None:
+                    # the pass kernel advances the incident line for the core;
+                    # the stepped shell advances it again from the same state
+                    line0 = (self.einc[p].clone(), self.hinc[p].clone())
+                    tf = self._tfsf_pass(p, T)
                 for ob in hp["core"]:
-                    self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
+                    if tf is not None:
+                        self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf)
+                    else:
+                        self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
+                if tf is not None:
+                    self.einc[p].copy_(line0[0])
+                    self.hinc[p].copy_(line0[1])
         for _ in range(T):
             self.step(hp["shell"])
         with self.prof.phase("shell-copy"):
@@ -322,10 +450,14 @@ class BlockedStepping:
         upd, outs = self._tb_regions(T)
         srcs = self._pass_sources(self.t, T)
         side = self._fork_side_stream() if self.halo is not None else None
+        tfs = [self._tfsf_pass(p, T) for p in range(self.planes)] if self.cfg.use_tfsf else [None] * self.planes
         for p in range(self.planes):
             if not box_empty(outs[0]):
                 with self.prof.phase("blocked-interior" if self.halo is not None else "blocked"):
-                    self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
+                    if tfs[p] is not None:
+                        self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p], tfsf=tfs[p])
+                    else:
+                        self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
         if self.halo is not None:
             if side is not None and self.prof.enabled:
                 with torch.cuda.stream(side):
@@ -339,7 +471,10 @@ class BlockedStepping:
             with self.prof.phase("blocked-shells"):
                 for ob in outs[1:]:
                     for p in range(self.planes):
-                        self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p])
+                        if tfs[p] is not None:
+                            self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p], tfsf=tfs[p])
+                        else:
+                            self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p])
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
         self.t += T

@@ -47,7 +47,7 @@ from ..utils.assertions import FdtdError, fdtd_assert
 from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
 from ..utils import logging as log
 from .blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64, BlockedStepping, auto_time_block
-from .tfsf import build_tfsf_tables, incident_line_length
+from .tfsf import build_tfsf_sets, build_tfsf_tables, incident_line_length
 
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
@@ -270,7 +270,13 @@ class YeeScheme(BlockedStepping):
         self.fused = (cfg.use_fused and hasattr(self.ops, "fused_step") and cfg.scheme == "3d"
                       and not self.use_upml_chain and not self.use_cpml and not cfg.use_tfsf
                       and not cfg.use_amp_mode)
-        if self.fused:
+        # plain 3D runs with TF/SF injection: the fp32 blocked kernel applies
+        # the corrections itself (models/tfsf.py TfsfSets), so such serial runs
+        # take blocked passes like plain ones (single steps keep the tables)
+        self.tfsf_blocked = (cfg.use_tfsf and getattr(self, "tfsf_sets", None) is not None and cfg.use_fused
+                             and cfg.scheme == "3d" and not self.use_upml_chain and not self.use_cpml
+                             and not cfg.use_amp_mode and self.halo is None)
+        if self.fused or self.tfsf_blocked:
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
         # HIP graph mode (--use-hip-graph): serial HIP runs capture GRAPH_STEPS
         # steps once and replay them; sources read a device table, so the
@@ -296,7 +302,7 @@ class YeeScheme(BlockedStepping):
                 T = 1
         self.tb = 1
         hip_ok = self.ops.name != "hip" or self.dtype == torch.float64 or self.domain.shape[2] % 4 == 0
-        if (T > 1 and self.fused and hasattr(self.ops, "tb_step") and hip_ok
+        if (T > 1 and (self.fused or self.tfsf_blocked) and hasattr(self.ops, "tb_step") and hip_ok
                 and T <= getattr(self.ops, "tb_max_steps", 6)
                 and (self.halo is None or self.domain.buffer_size == T)):
             self.tb = T
@@ -542,6 +548,13 @@ class YeeScheme(BlockedStepping):
         if self.use_upml_chain:
             self.tfsf_D = build_tfsf_tables(self.layout, self.comps, self.domain.origin, self.domain.shape, boxes,
                                             {c: self.upml[c]["cbD"] for c in self.comps}, self.device, self.dtype, n)
+        # in-kernel form for the blocked passes (fp32 HIP, incident direction
+        # along x or y; models/tfsf.py TfsfSets)
+        self.tfsf_sets = None
+        if (self.ops.name == "hip" and self.dtype == torch.float32 and self.cfg.scheme == "3d"
+                and getattr(self.ops, "tfsf_sets_ok", False)):
+            self.tfsf_sets = build_tfsf_sets(self.layout, self.comps, self.domain.origin, self.domain.shape, boxes,
+                                             self.device, self.dtype, n)
         # local bounding box of each component's TF/SF targets
         self.tfsf_bbox = {}
         for c in self.comps:
@@ -1125,9 +1138,9 @@ class YeeScheme(BlockedStepping):
                 keep = torch.zeros_like(self.F[p][c], dtype=torch.bool)
                 keep[ub[0][0]:ub[1][0], ub[0][1]:ub[1][1], ub[0][2]:ub[1][2]] = True
                 self.F[p][c].masked_fill_(~keep, 0.0)
-                alt = getattr(self, "F_alt", None)
-                if alt is not None:
-                    alt[p][c].copy_(self.F[p][c])
+                for alt in (getattr(self, "F_alt", None), getattr(self, "F_3", None)):
+                    if alt is not None:
+                        alt[p][c].copy_(self.F[p][c])
 
     def field_energy(self) -> float:
         """Vacuum field energy over this rank's owned cells in units of

@@ -184,3 +184,141 @@ def _layer(entries, device, dtype) -> List[TfsfTable]:
         tab.max_inc = int(i0[sel].max()) + 1 if sel.any() else -1
         layers.append(tab)
     return layers
+
+
+class TfsfSets:
+    """TF/SF corrections in the form the blocked kernels apply them
+    (``csrc/yee3d_tb.hip`` TfDev): one *set* per (component, face) -- the box
+    of target cells the reference's border tests select
+    (``YeeGridLayout.cpp:327-809``), one cell thick across the face -- and,
+    per set, the incident-line interpolation (index ``i0``, weights ``w0``,
+    ``w1``) and ``sign * projection`` factor at every index along the table
+    axis ``va``.  Valid when the incident direction lies along x or y (the
+    reference default theta = 90, phi = 0 is +x): the incident value of a
+    target then depends on that one index.  Each blocked pass turns the
+    entries into per-level g values (``k_tfsf_pass``) that the kernel adds to
+    the target's curl, so ``E += Cb * (curl + g)`` equals the table path's
+    ``E += Cb * curl; E += Cb * g``."""
+
+    MAX_SETS = 24
+    INTS_PER_SET = 10
+
+    def __init__(self):
+        self.sets: List[dict] = []
+        self.i0 = self.w0 = self.w1 = self.c = None
+        self.n_e = self.n_h = 0
+        self.xpl = [[-1, -1], [-1, -1]]
+        self.dev = None  # int32 device block (TfDev)
+
+    @property
+    def ld(self) -> int:
+        return self.n_e + self.n_h
+
+    def struct_ints(self) -> np.ndarray:
+        v = [len(self.sets), self.ld, self.xpl[0][0], self.xpl[0][1], self.xpl[1][0], self.xpl[1][1]]
+        for s in self.sets:
+            v += [s["n"], s["fa"]] + list(s["lo"]) + list(s["hi"]) + [s["va"], s["goff"]]
+        v += [0] * (self.INTS_PER_SET * (self.MAX_SETS - len(self.sets)))
+        return np.asarray(v, dtype=np.int32)
+
+
+COMP_INDEX = {"Ex": 0, "Ey": 1, "Ez": 2, "Hx": 3, "Hy": 4, "Hz": 5}
+
+
+def build_tfsf_sets(layout: YeeLayout, comps: Sequence[str], origin: Sequence[int], shape: Sequence[int],
+                    boxes: Dict[str, Tuple], device, dtype, line_len: int) -> Optional[TfsfSets]:
+    """:class:`TfsfSets` of the local array ``shape`` at ``origin`` (targets
+    restricted to ``boxes``, as :func:`build_tfsf_tables`), or None when the
+    incident direction is not along x or y (3D only)."""
+    if layout.scheme != "3d":
+        return None
+    L, R = layout.tfsf_borders()
+    zero = layout.zero_inc_coord_fp()
+    dirv = layout.incident_direction()
+    tol = 1e-9
+    if abs(dirv[1]) < tol and abs(dirv[2]) < tol:
+        va = 0
+    elif abs(dirv[0]) < tol and abs(dirv[2]) < tol:
+        va = 1
+    else:
+        return None
+    out = TfsfSets()
+    ent = {"E": [], "H": []}
+    for kind in ("E", "H"):
+        for comp in comps:
+            if comp[0] != kind:
+                continue
+            box = boxes[comp]
+            if any(box[1][d] <= box[0][d] for d in range(3)):
+                continue
+            m = MIN_COORD_FP[comp]
+            for (s, axis, sign) in layout.curl_terms(comp):
+                for dname in "LRDUBF":
+                    if DIR_AXIS[dname] != axis or (comp, dname) not in TFSF_PREDICATES:
+                        continue
+                    pred = TFSF_PREDICATES[(comp, dname)]
+                    lo, hi = [], []
+                    for d in range(3):
+                        idx = np.arange(box[0][d], box[1][d])
+                        g = idx + origin[d] + m[d]
+                        sel = _axis_mask(g, pred[d], L[d], R[d]) if layout.active(d) else np.ones_like(g, bool)
+                        if not sel.any():
+                            break
+                        nzi = np.flatnonzero(sel)
+                        if nzi[-1] - nzi[0] + 1 != nzi.size:
+                            raise ValueError("TF/SF set is not a box")
+                        lo.append(int(idx[nzi[0]]))
+                        hi.append(int(idx[nzi[-1]]) + 1)
+                    if len(lo) < 3:
+                        continue
+                    if len(out.sets) >= TfsfSets.MAX_SETS:
+                        raise ValueError("too many TF/SF sets")
+                    low = DIR_LOW[dname]
+                    nb_off = (0 if low else -1) if kind == "E" else (0 if low else +1)
+                    ms = MIN_COORD_FP[s]
+                    a = np.arange(lo[va], hi[va])
+                    pos = []
+                    for d in range(3):
+                        base = a if d == va else np.full(a.shape, lo[d])
+                        pos.append(base + (nb_off if d == axis else 0) + origin[d] + ms[d])
+                    dd = sum((pos[d] - zero[d]) * dirv[d] for d in range(3))
+                    dd = dd - (0.5 if kind == "E" else 0.0)
+                    i0 = np.floor(dd).astype(np.int64)
+                    if (i0 < 0).any() or (i0 + 1 >= line_len).any():
+                        raise ValueError("TF/SF box does not fit the incident line")
+                    w1 = dd - i0
+                    tsign = -sign if low else sign
+                    cval = np.full(a.shape, tsign * layout.incident_projection(s))
+                    out.sets.append({"n": COMP_INDEX[comp], "fa": axis, "lo": tuple(lo), "hi": tuple(hi), "va": va,
+                                     "goff": 0, "kind": kind})
+                    ent[kind].append((i0, 1.0 - w1, w1, cval))
+    # E sets first: g index space [E entries | H entries]
+    goff = 0
+    parts = []
+    for kind in ("E", "H"):
+        k = 0 if kind == "E" else 1
+        planes = set()
+        for s_, e in zip([s for s in out.sets if s["kind"] == kind], ent[kind]):
+            s_["goff"] = goff
+            goff += e[0].size
+            parts.append(e)
+            if s_["fa"] == 0:
+                planes.add(s_["lo"][0])
+        planes = sorted(planes)
+        if len(planes) > 2:
+            raise ValueError("more than two TF/SF x-face planes per kind")
+        for q, pl in enumerate(planes):
+            out.xpl[k][q] = pl
+        if kind == "E":
+            out.n_e = goff
+    out.n_h = goff - out.n_e
+    out.sets.sort(key=lambda s_: 0 if s_["kind"] == "E" else 1)
+    if not parts:
+        return None
+    cat = lambda i: np.concatenate([p[i] for p in parts])
+    out.i0 = torch.as_tensor(cat(0).astype(np.int32), device=device)
+    out.w0 = torch.as_tensor(cat(1), device=device, dtype=dtype)
+    out.w1 = torch.as_tensor(cat(2), device=device, dtype=dtype)
+    out.c = torch.as_tensor(cat(3), device=device, dtype=dtype)
+    out.dev = torch.as_tensor(out.struct_ints(), device=device)
+    return out

@@ -562,8 +562,37 @@ class HipOps:
         self.launches += 1
 
     # ------------------------------------------------------ temporal blocking
+    tfsf_sets_ok = True  # the fp32 blocked kernel applies TfsfSets corrections
+
+    def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
+                  sets, slot: int = 0) -> torch.Tensor:
+        """Advance the incident line ``len(src_vals)`` steps and return the
+        g table of the pass (levels x sets.ld, yee3d_tb.hip k_tfsf_pass);
+        ``slot`` selects the table buffer (one per field plane)."""
+        T = len(src_vals)
+        if not (1 <= T <= 8) or self.dtype != torch.float32:
+            raise HipError("tfsf_pass: fp32, 1..8 steps")
+        if int(self.lib.fdtd_tfdev_size()) != 4 * sets.dev.numel():
+            raise HipError("TfDev layout mismatch (%d vs %d bytes)" % (self.lib.fdtd_tfdev_size(),
+                                                                       4 * sets.dev.numel()))
+        need = T * max(1, sets.ld)
+        tabs = sets.__dict__.setdefault("gtab", {})
+        g = tabs.get(slot)
+        if g is None or g.numel() < need:
+            g = tabs[slot] = torch.zeros(8 * max(1, sets.ld), dtype=torch.float32, device=self.device)
+        for t_ in (einc, hinc):
+            self._check_tensor(t_)
+        rc = self.lib.fdtd_tfsf_pass_f32(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(ce), c_double(ch),
+                                         (c_double * 8)(*(list(src_vals) + [0.0] * (8 - T))), c_int(T),
+                                         c_int(min(einc.numel(), reach)), c_int(sets.n_e), c_int(sets.n_h),
+                                         _ptr(sets.i0), _ptr(sets.w0), _ptr(sets.w1), _ptr(sets.c), _ptr(g),
+                                         _stream())
+        _check(rc, "tfsf_pass")
+        self.launches += 1
+        return g
+
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                obox: Box, cb: Dict[str, Coef], steps: int, sources=None) -> None:
+                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None, cpml=None) -> None:
         """``steps`` fused leapfrog steps in one HBM pass (yee3d_tb.hip).
 
         ``boxes`` are the update boxes (each component changes only there, at
@@ -621,19 +650,34 @@ class HipOps:
                 vals[l] = float(s[2])
             src = [idx[0], idx[1], idx[2], E.index(comp)]
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
-        if percell and self.dtype == torch.float32 and self.tb_sparse:
-            # sparse per-cell coefficients on the multi-row kernel
-            if steps > 5:
+        if tfsf is not None and self.dtype != torch.float32:
+            raise HipError("in-kernel TF/SF: fp32 only")
+        if cpml is not None:
+            if self.dtype != torch.float32 or steps != 1:
+                raise HipError("in-kernel CPML: fp32 single-step passes")
+            if int(self.lib.fdtd_cpmldev_size()) != cpml.numel():
+                raise HipError("CpmlDev layout mismatch")
+        if (percell and self.dtype == torch.float32 and self.tb_sparse) or tfsf is not None or cpml is not None:
+            # multi-row kernel with sparse per-cell coefficients / TF/SF sets
+            if percell and steps > 5:
                 raise HipError("per-cell coefficients: at most 5 steps per pass")
-            ce, ebox, cbv = self._sparse_kind(cb, E, shape)
-            ch, hbox, dbv = self._sparse_kind(cb, H, shape)
-            self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
-            rc = self.lib.fdtd_tb3d_sparse_f32(
+            if percell:
+                ce, ebox, cbv = self._sparse_kind(cb, E, shape)
+                ch, hbox, dbv = self._sparse_kind(cb, H, shape)
+            else:
+                ce = ch = None
+                ebox = hbox = ((0, 0, 0), (0, 0, 0))
+            tfp = gp = None
+            if tfsf is not None:
+                sets, gtab, level0 = tfsf
+                tfp = _ptr(sets.dev)
+                gp = c_vp(gtab.data_ptr() + 4 * level0 * sets.ld)
+            rc = self.lib.fdtd_tb3d_ext_f32(
                 arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), _ptr(ce), _box_arr([ebox]), _ptr(ch),
                 _box_arr([hbox]), c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk), c_int(steps),
-                (c_int * 4)(*src), (c_double * 8)(*vals), _stream())
-            _check(rc, "tb3d_sparse")
+                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _ptr(cpml), _stream())
+            _check(rc, "tb3d_ext")
             self.launches += 1
             return
         if self.dtype == torch.float32:

@@ -27,6 +27,14 @@ CASES = [
                            scene="vacuum", use_pml=True, use_tfsf=True, phi=30), 7, 23),
     ("tez-cpml-tfsf", dict(scheme="tez", size=(96, 128, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
                            scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=60), 5, 17),
+    # single-pass shell (CPML psi and TF/SF sets inside the multi-row kernel, shrinking windows)
+    ("cpml-tfsf-x", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 13),
+    ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0), 3, 11),
+    ("cpml-tfsf-sphere", dict(scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
+                              sphere_center=(40.0, 36.0, 48.0), sphere_radius=10.0), 4, 10),
+    ("cpml-point-T5", dict(scene="vacuum", use_pml=True, pml_type="cpml"), 5, 12),
+    ("cpml-tfsf-complex", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, complex_values=True),
+     2, 7),
     ("tmz-upml-point-f64", dict(scheme="tmz", size=(150, 90, 1), pml_size=(8, 8, 1), scene="vacuum", use_pml=True,
                                 dtype="f64"), 6, 19),
 ]
@@ -54,12 +62,53 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
     assert hy.hybrid is not None, "hybrid plan rejected"
     st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, dt)
     assert st.hybrid is None
+    if name.startswith(("cpml-tfsf-x", "cpml-tfsf-y", "cpml-tfsf-sphere", "cpml-point", "cpml-tfsf-complex",
+                        "sphere-cpml")):
+        assert hy.hybrid.get("v2"), "single-pass shell not selected"
     ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
-    for c in ref.comps:
-        r = ref.F[0][c]
-        # scale by the kind's largest component (a point Ez source leaves Hz ~ 0)
-        scale = max(float(ref.F[0][o].abs().max()) for o in ref.comps if o[0] == c[0]) + 1e-30
-        e_hy = float((hy.F[0][c].double().cpu() - st.F[0][c].double().cpu()).abs().max())
-        e_ref = float((hy.F[0][c].double().cpu() - r).abs().max())
-        assert e_hy <= tol * scale, (name, c, "hybrid vs stepped", e_hy, scale)
-        assert e_ref <= 10 * tol * scale, (name, c, "hybrid vs fp64 oracle", e_ref, scale)
+    for p in range(ref.planes):
+        for c in ref.comps:
+            r = ref.F[p][c]
+            # scale by the kind's largest component (a point Ez source leaves Hz ~ 0)
+            scale = max(float(ref.F[p][o].abs().max()) for o in ref.comps if o[0] == c[0]) + 1e-30
+            e_hy = float((hy.F[p][c].double().cpu() - st.F[p][c].double().cpu()).abs().max())
+            e_ref = float((hy.F[p][c].double().cpu() - r).abs().max())
+            assert e_hy <= tol * scale, (name, p, c, "hybrid vs stepped", e_hy, scale)
+            assert e_ref <= 10 * tol * scale, (name, p, c, "hybrid vs fp64 oracle", e_ref, scale)
+    if hy.use_cpml:
+        # the CPML auxiliaries advanced identically
+        # (psi is a convolution of field differences of the source kind: its
+        # absolute error is bounded like that kind's fields')
+        for c in hy.comps:
+            src_scale = max(float(ref.F[0][o].abs().max()) for o in ref.comps if o[0] != c[0]) + 1e-30
+            for a, b in zip(hy.cpml.slabs[c], st.cpml.slabs[c]):
+                x, y = a.psi[0].double().cpu(), b.psi[0].double().cpu()
+                err = float((x - y).abs().max())
+                assert err <= 1e-4 * float(y.abs().max()) + tol * src_scale, (name, c, "psi", err, src_scale)
+
+
+@pytest.mark.parametrize("T,tfsf", [(4, True), (3, False), (5, True)])
+def test_hybrid2_random_fields(gpu, T, tfsf):
+    """Single-pass shell on random initial fields: every CPML slab carries
+    field from the first step on, so the in-kernel psi terms are exercised."""
+    cfg = SchemeConfig(time_steps=2 * T + 1, **BASE, scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=tfsf)
+    runs = {}
+    for hb in (T, 1):
+        s = YeeScheme(dataclasses.replace(cfg, hybrid_block=hb), make_ops("hip", None, gpu, torch.float32))
+        s.init_scheme()
+        s.init_grids()
+        s.randomize_fields(seed=5)
+        s.perform_steps()
+        torch.cuda.synchronize()
+        runs[hb] = s
+    hy, st = runs[T], runs[1]
+    assert hy.hybrid is not None and hy.hybrid.get("v2")
+    for c in hy.comps:
+        x, y = hy.F[0][c].double().cpu(), st.F[0][c].double().cpu()
+        scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])
+        assert float((x - y).abs().max()) <= 2e-5 * scale, (c, float((x - y).abs().max()), scale)
+        src_scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] != c[0])
+        for a, b in zip(hy.cpml.slabs[c], st.cpml.slabs[c]):
+            err = float((a.psi[0].double() - b.psi[0].double()).abs().max())
+            assert err <= 2e-5 * src_scale, (c, "psi", err, src_scale)
+        assert max(float(b.psi[0].abs().max()) for b in st.cpml.slabs[c]) > 1e-3 * src_scale  # psi is live

@@ -19,6 +19,9 @@ run() {
 for n in ${CONFIGS:-cpml upml drude sphere}; do
   case $n in
     cpml) run cpml --scene vacuum --use-pml --pml-type cpml --use-tfsf ;;
+    cpml3) run cpml3 --scene vacuum --use-pml --pml-type cpml --use-tfsf --hybrid-block 3 ;;
+    cpml5) run cpml5 --scene vacuum --use-pml --pml-type cpml --use-tfsf --hybrid-block 5 ;;
+    cpmlsph) run cpmlsph --scene sphere --sphere-eps 4 $SPH --use-pml --pml-type cpml --use-tfsf ;;
     upml) run upml --scene vacuum --use-pml --use-tfsf ;;
     drude) run drude --scene drude-sphere --use-metamaterials --use-pml $SPH ;;
     sphere) run sphere --scene sphere --sphere-eps 4 $SPH ;;
@@ -26,6 +29,9 @@ for n in ${CONFIGS:-cpml upml drude sphere}; do
     sphere4) run sphere4 --scene sphere --sphere-eps 4 $SPH --time-block 4 ;;
     sphere5) run sphere5 --scene sphere --sphere-eps 4 $SPH --time-block 5 ;;
     vac) run vac --scene vacuum ;;
+    vac4) run vac4 --scene vacuum --time-block 4 ;;
+    tfsf4) run tfsf4 --scene vacuum --use-tfsf --time-block 4 ;;
+    tfsf5) run tfsf5 --scene vacuum --use-tfsf --time-block 5 ;;
   esac || exit 1
 done
 echo done
