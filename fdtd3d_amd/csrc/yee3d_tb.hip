@@ -419,6 +419,22 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   __shared__ vec sX[2][4][TBW][64];
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);  // one wave per y (SGPR)
+  // TF/SF and CPML tables live in LDS for the kernel's life: their fields are
+  // read in many branches, and scalar loads there serialise on scalar-cache
+  // misses (and spill SGPRs)
+  __shared__ unsigned sTFraw[TFS ? sizeof(TfDev) / 4 : 1];
+  __shared__ unsigned long long sCPraw[CPM ? sizeof(CpmlDev) / 8 : 1];
+  if constexpr (TFS) {
+    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(TfDev) / 4); q += 64 * TBW)
+      sTFraw[q] = ((const unsigned*)tf)[q];
+  }
+  if constexpr (CPM) {
+    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(CpmlDev) / 8); q += 64 * TBW)
+      sCPraw[q] = ((const unsigned long long*)cp)[q];
+  }
+  if constexpr (TFS || CPM) __syncthreads();
+  const TfDev& TF = *reinterpret_cast<const TfDev*>(sTFraw);
+  const CpmlDev& CP = *reinterpret_cast<const CpmlDev*>(sCPraw);
   // Tile of this workgroup.  A row of a tile starts at an arbitrary z (the
   // stride is the 64 - 2T owned cells), so its 64 cells straddle three
   // 128-B lines, one shared with each z neighbour tile.  Workgroups are dealt
@@ -524,13 +540,13 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   bool tf_ok0 = false, tf_ok1 = false;
   int tf_va = 0, tf_ld = 0;
   if constexpr (TFS) {
-    const int ns = tf->nsets;
-    const int ld = tf->ld;
+    const int ns = TF.nsets;
+    const int ld = TF.ld;
     tf_ld = ld;
-    tf_va = tf->s[0].va;
+    tf_va = TF.s[0].va;
     int na[2] = {0, 0};
     for (int si = 0; si < ns; ++si) {
-      const TfSet& S = tf->s[si];
+      const TfSet& S = TF.s[si];
       unsigned rb = 0;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -571,10 +587,10 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
     }
     tf_na0 = na[0];
     tf_na1 = na[1];
-    tf_xe0 = tf->xpl[0][0];
-    tf_xe1 = tf->xpl[0][1];
-    tf_xh0 = tf->xpl[1][0];
-    tf_xh1 = tf->xpl[1][1];
+    tf_xe0 = TF.xpl[0][0];
+    tf_xe1 = TF.xpl[0][1];
+    tf_xh0 = TF.xpl[1][0];
+    tf_xh1 = TF.xpl[1][1];
   }
   const bool tf_slots = TFS && (tf_na0 + tf_na1) > 0;
   float tf_g0 = 0.f, tf_g1 = 0.f;  // this trip's g entries (lane q, q + 64)
@@ -605,9 +621,9 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
       while (cand) {
         const int si = __builtin_ctz(cand);
         cand &= cand - 1u;
-        const TfSet& S = tf->s[si];
+        const TfSet& S = TF.s[si];
         if ((unsigned)(p - S.lo[0]) >= (unsigned)(S.hi[0] - S.lo[0]) || j < S.lo[1] || j >= S.hi[1]) continue;
-        const float g = gtab[l * tf->ld + S.goff + (S.va == 0 ? p - S.lo[0] : j - S.lo[1])];
+        const float g = gtab[l * TF.ld + S.goff + (S.va == 0 ? p - S.lo[0] : j - S.lo[1])];
         // g on the set's lanes, 0 elsewhere, added to the set's component by
         // selects (conditional adds make the compiler index a scratch array)
         const float gl = (kb >= S.lo[2] && kb < S.hi[2]) ? g : 0.f;
@@ -658,15 +674,15 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
     return (tm.psi[0] && v >= tm.lo[0] && v < tm.hi[0]) ? 0 : ((tm.psi[1] && v >= tm.lo[1] && v < tm.hi[1]) ? 1 : -1);
   };
   auto psi_side_x = [&](int n, int t, int pl) -> int {
-    return kTermAxis[n][t] == 0 ? side_of(cp->t[n][0], pl) : -1;
+    return kTermAxis[n][t] == 0 ? side_of(CP.t[n][0], pl) : -1;
   };
   auto psi_side_y = [&](int n, int t, int j) -> int {
-    return kTermAxis[n][t] == 1 ? side_of(cp->t[n][1], j) : -1;
+    return kTermAxis[n][t] == 1 ? side_of(CP.t[n][1], j) : -1;
   };
   // descriptor of plane pl of the side-sd slab of term (n, t), read or written copy
   auto psi_rsrc = [&](int n, int t, int sd, int pl, bool wr) -> Rsrc {
     const int a = kTermAxis[n][t];
-    const CpmlTerm& tm = cp->t[n][a];
+    const CpmlTerm& tm = CP.t[n][a];
     const int wd = tm.hi[sd] - tm.lo[sd];
     const size_t pe_ = a == 0 ? (size_t)ny * nz : (a == 1 ? (size_t)wd * nz : (size_t)ny * wd);
     const size_t first = a == 0 ? (size_t)(pl - tm.lo[sd]) * pe_ : (size_t)pl * pe_;
@@ -676,7 +692,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   // lane byte offset of row r in that plane (past the plane for lanes outside the slab)
   auto psi_off = [&](int n, int t, int sd, int r) -> unsigned {
     const int a = kTermAxis[n][t];
-    const CpmlTerm& tm = cp->t[n][a];
+    const CpmlTerm& tm = CP.t[n][a];
     if (a == 0) return roff[r];
     if (a == 1) return roff[r] - (unsigned)(tm.lo[sd] * nz) * 4u;  // sentinel offsets stay past the plane
     const int j = jw + r;
@@ -696,7 +712,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int a = kTermAxis[n][t];
-        const CpmlTerm& tm = cp->t[n][a];
+        const CpmlTerm& tm = CP.t[n][a];
         bool act = false;
         if (a == 0) {
           act = tm.psi[0] || tm.psi[1];
@@ -881,7 +897,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
         float bb, cc, kk;
         if (a == 0) {
           if (psi_side_x(n, t, pl) < 0) return zero;
-          const CpmlTerm& tm = cp->t[n][0];
+          const CpmlTerm& tm = CP.t[n][0];
           bb = tm.b[pl];
           cc = tm.c[pl];
           kk = tm.k[pl];

@@ -159,7 +159,8 @@ class BlockedStepping:
         kernel applies itself: CPML psi (single-step passes), TF/SF sets
         (incident direction along x or y), sparse per-cell coefficients."""
         cfg = self.cfg
-        return (self.ops.name == "hip" and self.dtype == torch.float32 and cfg.scheme == "3d"
+        return (getattr(cfg, "hybrid_shell", "stepped") == "single-pass"
+                and self.ops.name == "hip" and self.dtype == torch.float32 and cfg.scheme == "3d"
                 and self.halo is None and not self.use_upml_chain and not cfg.use_metamaterials
                 and not cfg.use_amp_mode and self.domain.shape[2] % 4 == 0
                 and (not cfg.use_tfsf or getattr(self, "tfsf_sets", None) is not None)
@@ -248,9 +249,10 @@ class BlockedStepping:
         size = cfg.size
         alloc = dom.allocated_global()
         m = T + 2  # core margin to every irregular cell (staggering slack included)
-        # the fp32 blocked kernel applies TF/SF corrections itself (TfsfSets):
-        # TF/SF faces may then lie inside the core
-        in_kernel_tfsf = cfg.use_tfsf and getattr(self, "tfsf_sets", None) is not None
+        # TF/SF faces stay in the stepped shell: the blocked kernel's TF/SF
+        # variant runs at about half the plain kernel's rate
+        # (profiles/tfsf_cpml_r2.md), more than the shell it would save
+        in_kernel_tfsf = False
         lo, hi = [0, 0, 0], list(size)
         act = [self.layout.active(a) for a in range(3)]  # 2D: z is one cell, never cut
         for a in range(3):
@@ -390,7 +392,7 @@ class BlockedStepping:
         with self.prof.phase("blocked-core"):
             for p in range(self.planes):
                 tf = None
-                if self.cfg.use_tfsf and getattr(self, "tfsf_sets", None) is not None:
+                if self.cfg.use_tfsf and self.hybrid.get("tfsf_in_core"):
                     # the pass kernel advances the incident line for the core;
                     # the stepped shell advances it again from the same state
                     line0 = (self.einc[p].clone(), self.hinc[p].clone())

@@ -98,6 +98,7 @@ class SchemeConfig:
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
+    hybrid_shell: str = "stepped"            # stepped | single-pass (models/blocking.py _hybrid2_plan)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
@@ -130,7 +131,7 @@ class SchemeConfig:
             ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
-            hybrid_block=s.hybridBlock,
+            hybrid_block=s.hybridBlock, hybrid_shell=s.hybridShell,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 

@@ -28,12 +28,12 @@ CASES = [
     ("tez-cpml-tfsf", dict(scheme="tez", size=(96, 128, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
                            scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=60), 5, 17),
     # single-pass shell (CPML psi and TF/SF sets inside the multi-row kernel, shrinking windows)
-    ("cpml-tfsf-x", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 13),
-    ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0), 3, 11),
-    ("cpml-tfsf-sphere", dict(scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
+    ("cpml-tfsf-x", dict(hybrid_shell="single-pass", scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 13),
+    ("cpml-tfsf-y", dict(hybrid_shell="single-pass", scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0), 3, 11),
+    ("cpml-tfsf-sphere", dict(hybrid_shell="single-pass", scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
                               sphere_center=(40.0, 36.0, 48.0), sphere_radius=10.0), 4, 10),
-    ("cpml-point-T5", dict(scene="vacuum", use_pml=True, pml_type="cpml"), 5, 12),
-    ("cpml-tfsf-complex", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, complex_values=True),
+    ("cpml-point-T5", dict(hybrid_shell="single-pass", scene="vacuum", use_pml=True, pml_type="cpml"), 5, 12),
+    ("cpml-tfsf-complex", dict(hybrid_shell="single-pass", scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, complex_values=True),
      2, 7),
     ("tmz-upml-point-f64", dict(scheme="tmz", size=(150, 90, 1), pml_size=(8, 8, 1), scene="vacuum", use_pml=True,
                                 dtype="f64"), 6, 19),
@@ -62,8 +62,7 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
     assert hy.hybrid is not None, "hybrid plan rejected"
     st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, dt)
     assert st.hybrid is None
-    if name.startswith(("cpml-tfsf-x", "cpml-tfsf-y", "cpml-tfsf-sphere", "cpml-point", "cpml-tfsf-complex",
-                        "sphere-cpml")):
+    if cfg.hybrid_shell == "single-pass":
         assert hy.hybrid.get("v2"), "single-pass shell not selected"
     ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
     for p in range(ref.planes):
@@ -91,7 +90,8 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
 def test_hybrid2_random_fields(gpu, T, tfsf):
     """Single-pass shell on random initial fields: every CPML slab carries
     field from the first step on, so the in-kernel psi terms are exercised."""
-    cfg = SchemeConfig(time_steps=2 * T + 1, **BASE, scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=tfsf)
+    cfg = SchemeConfig(time_steps=2 * T + 1, **BASE, scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=tfsf,
+                       hybrid_shell="single-pass")
     runs = {}
     for hb in (T, 1):
         s = YeeScheme(dataclasses.replace(cfg, hybrid_block=hb), make_ops("hip", None, gpu, torch.float32))
