@@ -392,8 +392,8 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d(
 // stored after plane X+1's prefetch is issued -- vmcnt counts loads and
 // stores together in issue order, so stores issued between two prefetches
 // would otherwise be waited for with the older prefetch.
-template <int T, int V, int R, int FX, int PFD, bool DEFER>
-__global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
+template <int T, int V, int R, int FX, int PFD, bool DEFER, int NW>
+__global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
     const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
     float* __restrict__ exo, float* __restrict__ eyo, float* __restrict__ ezo,
@@ -414,9 +414,9 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   typedef typename VT<V>::f vec;
   constexpr int HL = (T + V - 1) / V;   // halo lanes per side
   constexpr int TBZ = (64 - 2 * HL) * V; // owned z cells per tile
-  constexpr int ROWS = TBW * R;         // y rows per workgroup
+  constexpr int ROWS = NW * R;         // y rows per workgroup
   constexpr unsigned VM = (1u << V) - 1u;
-  __shared__ vec sX[2][4][TBW][64];
+  __shared__ vec sX[2][4][NW][64];
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);  // one wave per y (SGPR)
   // TF/SF and CPML tables live in LDS for the kernel's life: their fields are
@@ -425,11 +425,11 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   __shared__ unsigned sTFraw[TFS ? sizeof(TfDev) / 4 : 1];
   __shared__ unsigned long long sCPraw[CPM ? sizeof(CpmlDev) / 8 : 1];
   if constexpr (TFS) {
-    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(TfDev) / 4); q += 64 * TBW)
+    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(TfDev) / 4); q += 64 * NW)
       sTFraw[q] = ((const unsigned*)tf)[q];
   }
   if constexpr (CPM) {
-    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(CpmlDev) / 8); q += 64 * TBW)
+    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(CpmlDev) / 8); q += 64 * NW)
       sCPraw[q] = ((const unsigned long long*)cp)[q];
   }
   if constexpr (TFS || CPM) __syncthreads();
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
     }
   }
   const int rdn = w > 0 ? w - 1 : 0;
-  const int rup = w < TBW - 1 ? w + 1 : TBW - 1;
+  const int rup = w < NW - 1 ? w + 1 : NW - 1;
   const vec zero = (vec)(0.f);
   const vec cbv = (vec)(cb), dbv = (vec)(db);
   // Tiles whose every lane and row lies inside all six update boxes in y / z
@@ -705,7 +705,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
   // the wave's rows in LDS (uniform reads)
   unsigned cpm_wave = 0;
   float ZB[CPM ? 4 : 1], ZC[CPM ? 4 : 1], ZK[CPM ? 4 : 1];
-  __shared__ float sYP[CPM ? TBW : 1][CPM ? 4 * R * 3 : 1];
+  __shared__ float sYP[CPM ? NW : 1][CPM ? 4 * R * 3 : 1];
   if constexpr (CPM) {
 #pragma unroll
     for (int n = 0; n < 6; ++n)
@@ -1083,7 +1083,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_mr(
 // tile).  1024^3, T=5: 512 planes (7 rounds) instead of 256 (14 rounds of
 // half the length, +2% tail).
 int g_num_cus = 0;
-int pick_xchunk(long long tiles_yz, int nxo, int T) {
+int pick_xchunk(long long tiles_yz, int nxo, int T, int wg_per_cu = 1) {
   if (g_num_cus <= 0) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
@@ -1098,7 +1098,8 @@ int pick_xchunk(long long tiles_yz, int nxo, int T) {
   for (int k = 1; k <= 256; ++k) {
     const int xc = (nxo + k - 1) / k;
     const long long chunks = (nxo + xc - 1) / xc;
-    const long long rounds = (tiles_yz * chunks + g_num_cus - 1) / g_num_cus;
+    const long long slots = (long long)g_num_cus * wg_per_cu;
+    const long long rounds = (tiles_yz * chunks + slots - 1) / slots;
     const long long cost = rounds * (xc + 2LL * T);
     if (best_cost < 0 || cost < best_cost) {
       best_cost = cost;
@@ -1147,18 +1148,19 @@ int g_tb_mr_noallin = 0;  // A/B knob: 1 = masked loop everywhere (no interior f
 int g_tb_mr_xcd = 1;   // multi-row kernel: XCD-contiguous tile order, z fastest (-16..20% HBM reads)
 int g_tb_variant = 0;  // multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched
 const int kNoBox[6] = {0, 0, 0, 0, 0, 0};
+int g_tb_mr_shape = 0;  // plain multi-row kernel: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
 
-template <int T, int V, int R, int FX>
+template <int T, int V, int R, int FX, int NW = TBW>
 int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                  const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
                  int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
                  const TfDev* tf, const float* gtab, const CpmlDev* cp, hipStream_t s) {
   constexpr int HL = (T + V - 1) / V;
   constexpr int TBZ = (64 - 2 * HL) * V;
-  dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * T),
+  dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], NW * R - 2 * T),
             cdiv(O.hi[0] - O.lo[0], xchunk));
 #define MR_LAUNCH(PFD, DEFER)                                                                                 \
-  k_tb3d_mr<T, V, R, FX, PFD, DEFER><<<grid, dim3(64, TBW), 0, s>>>(                                        \
+  k_tb3d_mr<T, V, R, FX, PFD, DEFER, NW><<<grid, dim3(64, NW), 0, s>>>(                                     \
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
       O, xchunk, src[0], src[1], src[2], src[3], sv, g_tb_mr_xcd | (g_tb_mr_noallin << 1), tf, gtab, cp)
@@ -1215,6 +1217,10 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
   } else {
     if (fx) return (int)hipErrorInvalidValue;
   }
+  // plain: 16 waves x 2 rows (4 waves / SIMD, <= 128 VGPRs) or 8 waves x 4
+  // rows (2 waves / SIMD, <= 256 VGPRs: more rows of ILP per wave, half the
+  // LDS row exchanges); both a 32-row tile
+  if (g_tb_mr_shape == 1) return launch_tb_mr<T, 1, 4, 0, 8>(MR_ARGS);
   return launch_tb_mr<T, 1, 2, 0>(MR_ARGS);
 #undef MR_ARGS
 }
@@ -1231,7 +1237,8 @@ int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, flo
     const int HL = (steps + V - 1) / V;
     const long long gz = cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), (64 - 2 * HL) * V);
     const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
-    xchunk = pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps);
+    // the 8-wave shape fits two workgroups per CU
+    xchunk = pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) ? 2 : 1);
   }
 #define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, s
   switch (steps) {
@@ -1291,6 +1298,8 @@ FDTD_API void fdtd_set_tb_variant(int v) {
   g_tb_mr_xcd = (v >> 2) & 1;      // bit 2: XCD-contiguous tile order
   g_tb_mr_noallin = (v >> 3) & 1;  // bit 3: no interior fast path (A/B)
 }
+// plain multi-row tile shape (tuning): 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
+FDTD_API void fdtd_set_tb_mr_shape(int v) { g_tb_mr_shape = v == 1 ? 1 : 0; }
 // largest steps-per-pass the blocked kernels accept
 FDTD_API int fdtd_tb_max_steps() { return 6; }
 

@@ -691,6 +691,7 @@ class HipOps:
                 mr = 1
             self.lib.fdtd_set_tb_mrows(c_int(mr))
             self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
+            self.lib.fdtd_set_tb_mr_shape(c_int(self.tb_mr_shape))
         # fp32: yee3d_tb.hip (multi-row / single-row tiles); fp64: yee3d_tb64.hip
         rc = self.fn("tb3d_v4" if self.dtype == torch.float32 else "tb3d")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
                                 c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
@@ -773,6 +774,8 @@ class HipOps:
     tb_mrows = 0  # adjacent y rows per wave (multi-row kernel): 0 auto, 1 single-row kernel, 2
     tb_thin_single_row = True  # auto mode: output boxes <= 8 rows in y use the single-row kernel
     tb_sparse = True  # per-cell fp32 coefficients: sparse float4 boxes on the multi-row kernel
+    # plain multi-row tile shape: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows (two workgroups per CU)
+    tb_mr_shape = int(os.environ.get("FDTD3D_TB_MR_SHAPE", "0"))
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],

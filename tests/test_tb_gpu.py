@@ -196,3 +196,33 @@ def test_tb_f64_scheme_matches_fused(gpu, T):
         x, y = a.F[0][c], b.F[0][c]
         err = float((x - y).abs().max())
         assert err <= 1e-12 * (float(y.abs().max()) + 1e-300), (c, err)
+
+
+@pytest.mark.parametrize("size,T,scene,obox,src", [c for c in CASES_MR if c[2] == "vacuum"])
+@pytest.mark.parametrize("variant", [0, 4])
+def test_tb_mr_shape8(gpu, size, T, scene, obox, src, variant):
+    """8-wave x 4-row tiles of the plain multi-row kernel (two workgroups per
+    CU) vs the fp64 torch oracle."""
+    cfg = SchemeConfig(scheme="3d", size=size, scene=scene, dtype="f32", use_fused=True)
+    a = _scheme(cfg, "hip", gpu, torch.float32)
+    a.ops.tb_mrows = 2
+    a.ops.tb_mr_shape = 1
+    a.ops.tb_variant = variant
+    b = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
+    _randomize(a)
+    _randomize(b)
+    upd = {c: a.local_box(c) for c in a.comps}
+    ob = obox if obox is not None else ((0, 0, 0), tuple(size))
+    srcs = None
+    if src == "shell":
+        srcs = [("Ez", (10, 10, 2), 0.5 + 0.25 * l) for l in range(T)]
+    elif src:
+        srcs = [("Ez", tuple(v // 2 for v in size), 0.5 + 0.25 * l) for l in range(T)]
+    a.ops.tb_step(a.F[0], a.F_alt[0], upd, ob, a.cb, T, srcs)
+    b.ops.tb_step(b.F[0], b.F_alt[0], upd, ob, b.cb, T, srcs)
+    torch.cuda.synchronize()
+    for c in a.comps:
+        x = a.F_alt[0][c].double().cpu()
+        y = b.F_alt[0][c]
+        err = float((x - y).abs().max())
+        assert err <= 2e-5 * (float(y.abs().max()) + 1.0), (c, err)
