@@ -85,7 +85,7 @@ def scattered_field(scheme, comp: str, plane: int = 0) -> torch.Tensor:
 
 def dump_fields(scheme, settings, step: int, name_prefix: str = "", scattered: bool = False,
                 directory: Optional[str] = None) -> List[str]:
-    from ..parallel.halo import gather_field
+    from ..parallel.halo import gather_field, gather_owned
     directory = directory or settings.outputDir
     rank = scheme.domain.rank
     gather = settings.doGatherFullGrid and scheme.halo is not None
@@ -101,9 +101,7 @@ def dump_fields(scheme, settings, step: int, name_prefix: str = "", scattered: b
                     gl = scheme.domain.ghost_lo
                     s = scheme.domain.owned_shape
                     own = t[gl[0]:gl[0] + s[0], gl[1]:gl[1] + s[1], gl[2]:gl[2] + s[2]]
-                    saved = scheme.F[p][c]
-                    # temporarily view the scattered values through the gather path
-                    full = _gather_tensor(scheme, own)
+                    full = gather_owned(scheme, own)
                 else:
                     full = gather_field(scheme, c, p)
                 parts.append(full)
@@ -136,29 +134,6 @@ def dump_fields(scheme, settings, step: int, name_prefix: str = "", scattered: b
                 else:
                     files += d.dump_grid(re, im, dim=dim)
     return files
-
-
-def _gather_tensor(scheme, own: torch.Tensor):
-    import torch.distributed as dist
-    from ..parallel.topology import ParallelGridCore
-    if not dist.is_initialized():
-        return own.clone()
-    d = scheme.domain
-    rank = dist.get_rank()
-    core = ParallelGridCore(tuple(d.global_size), dist.get_world_size(), tuple(d.topology))
-    own = own.contiguous()
-    if rank == 0:
-        full = torch.zeros(tuple(d.global_size), dtype=own.dtype, device=own.device)
-        for r in range(core.used_procs):
-            dr = core.domain(r, d.buffer_size)
-            blk = own if r == 0 else torch.empty(dr.owned_shape, dtype=own.dtype, device=own.device)
-            if r:
-                dist.recv(blk, r, tag=201)
-            full[dr.lo[0]:dr.hi[0], dr.lo[1]:dr.hi[1], dr.lo[2]:dr.hi[2]] = blk
-        return full
-    if rank < core.used_procs:
-        dist.send(own, 0, tag=201)
-    return None
 
 
 def dump_materials(scheme, settings, directory: Optional[str] = None) -> List[str]:

@@ -32,6 +32,8 @@ import math
 from dataclasses import dataclass
 from typing import Dict, List, Sequence, Tuple
 
+from ..utils.coordinates import GridCoordinate, GridCoordinateFP3D
+
 E_COMPONENTS = ("Ex", "Ey", "Ez")
 H_COMPONENTS = ("Hx", "Hy", "Hz")
 ALL_COMPONENTS = E_COMPONENTS + H_COMPONENTS
@@ -165,9 +167,11 @@ class YeeLayout:
     def min_coord_fp(self, comp: str) -> Tuple[float, float, float]:
         return MIN_COORD_FP[comp]
 
-    def coord_fp(self, comp: str, idx: Sequence[int]) -> Tuple[float, ...]:
-        m = MIN_COORD_FP[comp]
-        return tuple(idx[a] + m[a] for a in range(3))
+    def coord_fp(self, comp: str, idx: Sequence[int]) -> GridCoordinate:
+        """Real (staggered) coordinate of cell ``idx`` of ``comp``: the
+        reference's ``getTotalPosition`` + ``getMinCoordFP``
+        (``YeeGridLayout.h:407-424``) as a 3D FP coordinate."""
+        return GridCoordinateFP3D(*idx) + GridCoordinateFP3D(*MIN_COORD_FP[comp])
 
     # ---------------------------------------------------------------- PML
     def pml_borders(self):
@@ -175,8 +179,11 @@ class YeeLayout:
         right = tuple(self.size[a] - self.pml_size[a] for a in range(3))
         return left, right
 
-    def is_in_pml(self, real: Sequence[float]) -> bool:
-        """``YeeGridLayout::isInPML`` (YeeGridLayout.cpp:255-279)."""
+    def is_in_pml(self, real) -> bool:
+        """``YeeGridLayout::isInPML`` (YeeGridLayout.cpp:255-279); ``real`` is
+        a :class:`GridCoordinate` or a sequence of 3 reals."""
+        if isinstance(real, GridCoordinate):
+            real = real.as_tuple()
         left, right = self.pml_borders()
         for a in self.axes:
             if left[a] != right[a] and (real[a] < left[a] or real[a] >= right[a]):

@@ -1057,13 +1057,16 @@ class YeeScheme(BlockedStepping):
     def amplitude_box(self, c: str) -> Box:
         """Computation box of ``c`` minus PML cells (Scheme3D.cpp:3016-3030)."""
         lo_g, hi_g = self._global_box(c)
-        m = self.layout.min_coord_fp(c)
-        left, right = self.layout.pml_borders()
+        lay = self.layout
+        left, right = lay.pml_borders()
+        # first / one-past-last index along each axis whose real coordinate
+        # lies outside the PML slabs (the reference's !isInPML per axis)
+        m0 = lay.coord_fp(c, (0, 0, 0))
         lo, hi = list(lo_g), list(hi_g)
-        for a in self.layout.axes:
+        for a in lay.axes:
             if left[a] != right[a]:
-                lo[a] = max(lo[a], int(math.ceil(left[a] - m[a])))
-                hi[a] = min(hi[a], int(math.ceil(right[a] - m[a])))
+                lo[a] = max(lo[a], int(math.ceil(left[a] - m0.c[a])))
+                hi[a] = min(hi[a], int(math.ceil(right[a] - m0.c[a])))
         b = box_intersect((tuple(lo), tuple(hi)), self.domain.owned_global())
         return self.domain.to_local(b)
 

@@ -424,9 +424,16 @@ def gather_field(scheme, comp: str, plane: int = 0, dst: int = 0, group=None) ->
     Replaces ``ParallelGrid::gatherFullGrid`` (ParallelGrid.cpp:2600-2845),
     which broadcast every rank's chunk to *all* ranks (O(P*N) traffic): here
     each rank sends only its owned block, once, to the destination."""
+    return gather_owned(scheme, scheme.owned_field(comp, plane), dst, group)
+
+
+def gather_owned(scheme, own: torch.Tensor, dst: int = 0, group=None) -> Optional[torch.Tensor]:
+    """Global array assembled on rank ``dst`` from every rank's owned block
+    ``own`` (any per-cell quantity laid out like the owned fields, e.g. the
+    scattered field of a dump); None on the other ranks."""
     from .topology import ParallelGridCore
     d = scheme.domain
-    own = scheme.owned_field(comp, plane).contiguous()
+    own = own.contiguous()
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return own.clone()
     rank = dist.get_rank(group)

@@ -114,7 +114,7 @@ def test_yee_layout_tables():
     L = YeeLayout((10, 12, 14))
     assert L.global_range("Ex") == ((0, 1, 1), (9, 12, 14))
     assert L.global_range("Hz") == ((0, 0, 1), (9, 11, 14))
-    assert L.coord_fp("Ey", (0, 0, 0)) == (0.5, 1.0, 0.5)
+    assert L.coord_fp("Ey", (0, 0, 0)).as_tuple() == (0.5, 1.0, 0.5)
     T = YeeLayout((10, 12, 1), scheme="tmz")
     assert T.components == ("Ez", "Hx", "Hy")
     assert T.global_range("Ez") == ((1, 1, 0), (10, 12, 1))
