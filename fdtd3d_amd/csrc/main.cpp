@@ -112,15 +112,23 @@ int fused(const double* const* ei, const double* const* hi, double* const* eo, d
   return fdtd_fused3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s);
 }
 // temporally blocked pass (fp32: yee3d_tb.hip, fp64: yee3d_tb64.hip)
+// fp32: a sparse float4 box of the E coefficients (ce4 over ebox, scalar cb
+// elsewhere, scalar db) takes the multi-row kernel; otherwise per-kind arrays
 int tb3d(const float* const* ei, const float* const* hi, float* const* eo, float* const* ho, const float* const* cbs,
          const float* const* dbs, double cb, double db, int nx, int ny, int nz, const int* bx, int T,
-         const int* src, const double* vals, void* s) {
+         const int* src, const double* vals, void* s, const void* ce4 = nullptr, const int* ebox = nullptr) {
   const int ob[6] = {0, 0, 0, nx, ny, nz};
+  if (ce4) {
+    const int none[6] = {0, 0, 0, 0, 0, 0};
+    return fdtd_tb3d_ext_f32(ei, hi, eo, ho, ce4, ebox, nullptr, none, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals,
+                             nullptr, nullptr, nullptr, s);
+  }
   return fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
 }
 int tb3d(const double* const* ei, const double* const* hi, double* const* eo, double* const* ho,
          const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
-         const int* bx, int T, const int* src, const double* vals, void* s) {
+         const int* bx, int T, const int* src, const double* vals, void* s, const void* = nullptr,
+         const int* = nullptr) {
   const int ob[6] = {0, 0, 0, nx, ny, nz};
   return fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
 }
@@ -212,6 +220,8 @@ int run(const fdtd::Settings& s) {
   if (scheme == "tez") present[0] = present[1] = present[5] = true;
   if (scheme == "1d") present[2] = present[4] = true;
   Dev<T> F[6], G[6], C[6];
+  Dev<float> CE4;  // fp32 3D per-cell: sparse E coefficients of the blocked kernel
+  int ebox[6] = {0, 0, 0, 0, 0, 0};
   for (int c = 0; c < 6; ++c)
     if (present[c]) {
       F[c].alloc(cells);
@@ -243,6 +253,31 @@ int run(const fdtd::Settings& s) {
           }
       C[c].alloc(cells);
       HIP_OK(hipMemcpy(C[c].p, host.data(), cells * sizeof(T), hipMemcpyHostToDevice));
+    }
+    if (sizeof(T) == 4 && dim == 3) {
+      // sparse form for the blocked kernel: the E coefficients of the cells
+      // around the sphere (its bounding box + 2 cells; every other cell has
+      // eps = 1 on both averaging points, i.e. exactly cb) as one float4 per
+      // cell; mu = 1, so H stays on the scalar db
+      for (int a = 0; a < 3; ++a) {
+        ebox[a] = std::max(0, (int)std::floor(ctr[a] - s.sphereRadius) - 2);
+        ebox[3 + a] = std::min(N[a], (int)std::ceil(ctr[a] + s.sphereRadius) + 3);
+      }
+      const size_t bn = (size_t)std::max(0, ebox[3] - ebox[0]) * std::max(0, ebox[4] - ebox[1]) *
+                        std::max(0, ebox[5] - ebox[2]);
+      if (bn > 0) {
+        std::vector<float> h4(4 * bn, 0.f);
+        size_t q = 0;
+        for (int i = ebox[0]; i < ebox[3]; ++i)
+          for (int j = ebox[1]; j < ebox[4]; ++j)
+            for (int k = ebox[2]; k < ebox[5]; ++k, ++q)
+              for (int c = 0; c < 3; ++c) {
+                const int di = c == 0, dj = c == 1, dk = c == 2;
+                h4[4 * q + c] = (float)(cb * 2.0 / (eps_at(i, j, k) + eps_at(i + di, j + dj, k + dk)));
+              }
+        CE4.alloc(4 * bn);
+        HIP_OK(hipMemcpy(CE4.p, h4.data(), 4 * bn * sizeof(float), hipMemcpyHostToDevice));
+      }
     }
   }
   int boxes[36];
@@ -366,8 +401,11 @@ int run(const fdtd::Settings& s) {
         const int src[4] = {sp[0], sp[1], sp[2], src_comp};
         double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int l = 0; l < T_blk; ++l) vals[l] = src_val(t + l);
-        K_OK(tb3d(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, percell ? 1.0 : db, N[0], N[1], N[2], boxes, T_blk,
-                  src, vals, st));
+        if (CE4.p)
+          K_OK(tb3d(ei, hi, eo, ho, cbs, dbs, cb, db, N[0], N[1], N[2], boxes, T_blk, src, vals, st, CE4.p, ebox));
+        else
+          K_OK(tb3d(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, percell ? 1.0 : db, N[0], N[1], N[2], boxes, T_blk,
+                    src, vals, st));
         for (int c = 0; c < 6; ++c) std::swap(F[c].p, G[c].p);
         t += T_blk;
         n -= T_blk;

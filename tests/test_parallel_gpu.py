@@ -38,7 +38,9 @@ def run_threads(cfg, world, axes, buf, device):
             s = YeeScheme(cfg, make_ops("hip", None, device, dt), dom, halo)
             s.init_scheme()
             s.init_grids()
-            assert s.tb == max(1, cfg.time_block)
+            # time_block 0: the automatic rule must pick the ghost depth the
+            # driver sized the domain for (models/blocking.py auto_time_block)
+            assert s.tb == (buf if cfg.time_block == 0 else max(1, cfg.time_block))
             s.perform_steps()
             halo.drain(s)
             torch.cuda.synchronize()
@@ -85,6 +87,10 @@ CASES = [
     # multi-row kernel (5 steps per pass, 5-deep ghosts, direct 26-neighbour exchange)
     ("tb5-xy4", SchemeConfig(scheme="3d", size=(60, 56, 128), time_steps=13, scene="vacuum", dtype="f32",
                              use_fused=True, time_block=5), 4, "xy", 5),
+    # automatic steps per pass on a dielectric (sparse per-cell) scene, 4 ranks -> T = 4
+    ("auto-sphere-xy4", SchemeConfig(scheme="3d", size=(48, 44, 128), time_steps=13, scene="sphere", sphere_radius=10,
+                                     sphere_center=(24.0, 20.0, 64.0), dtype="f32", use_fused=True, time_block=0),
+     4, "xy", 4),
     # fp64 blocked kernel
     ("tb4-f64-xyz8", SchemeConfig(scheme="3d", size=(40, 36, 44), time_steps=10, scene="vacuum", dtype="f64",
                                   use_fused=True, time_block=4), 8, "xyz", 4),

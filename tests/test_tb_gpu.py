@@ -226,3 +226,26 @@ def test_tb_mr_shape8(gpu, size, T, scene, obox, src, variant):
         y = b.F_alt[0][c]
         err = float((x - y).abs().max())
         assert err <= 2e-5 * (float(y.abs().max()) + 1.0), (c, err)
+
+
+def test_tb_bench_scale(gpu):
+    """The bench configuration itself: 1024^3 fp32 with the automatic x chunks
+    (512-plane chunks at T=5), 10 steps as two blocked passes == 10 fused
+    single steps, from random fields."""
+    cfg = SchemeConfig(scheme="3d", size=(1024, 1024, 1024), scene="vacuum", dtype="f32", use_fused=True,
+                       time_steps=10)
+    runs = []
+    for T in (5, 1):
+        s = _scheme(dataclasses.replace(cfg, time_block=T), "hip", gpu, torch.float32)
+        assert s.tb == T and s.ops.tb_xchunk == 0
+        s.randomize_fields(seed=2)
+        s.perform_steps()
+        torch.cuda.synchronize()
+        runs.append(s)
+    a, b = runs
+    for c in a.comps:
+        err = float((a.F[0][c] - b.F[0][c]).abs().max())
+        scale = max(float(b.F[0][o].abs().max()) for o in b.comps if o[0] == c[0])
+        assert err <= 1e-6 * scale, (c, err, scale)
+    del runs, a, b
+    torch.cuda.empty_cache()
