@@ -154,22 +154,25 @@ def ntff_power(fields_re: Optional[Dict[str, torch.Tensor]], fields_im: Optional
             cyc = 1.0 if (a1 - axis) % 3 == 1 else -1.0
             J = {a2: s * cyc * Ht[a1], a1: -s * cyc * Ht[a2]}
             M = {a2: -s * cyc * Et[a1], a1: s * cyc * Et[a2]}
-            # r' of face-cell centres (in metres, relative to the centre)
-            u = torch.arange(int(round(hi[a1] - lo[a1])), device=dev, dtype=torch.float64) + lo[a1] + 0.5
-            v = torch.arange(int(round(hi[a2] - lo[a2])), device=dev, dtype=torch.float64) + lo[a2] + 0.5
-            U, V = torch.meshgrid(u, v, indexing="ij")
-            coords = [None, None, None]
-            coords[axis] = torch.full_like(U, x0)
-            coords[a1] = U
-            coords[a2] = V
-            rp = torch.stack([(c - center).reshape(-1) for c in coords], dim=1) * dx  # (P, 3)
-            # fields carry exp(-i w t) (source sin + i cos = i exp(-i w t)), so the
-            # radiation kernel is exp(-i k r_hat . r')
-            phase = torch.exp(-1j * k * (rhat @ rp.T).to(cdt))  # (A, P)
-            for comp_axis, val in J.items():
-                Nvec[:, comp_axis] += phase @ val.reshape(-1) * (dx * dx)
-            for comp_axis, val in M.items():
-                Lvec[:, comp_axis] += phase @ val.reshape(-1) * (dx * dx)
+            # The phase exp(-i k r_hat . r') of a face-cell centre r' factors
+            # over the face's two axes: exp(-i k rh[axis] x0') exp(-i k rh[a1]
+            # u') exp(-i k rh[a2] v').  So each face sum is one batched GEMM
+            # over v (face values x v-phases) and a weighted sum over u --
+            # U V A complex multiply-adds on the BLAS path and (U + V) A
+            # exponentials, instead of U V A exponentials.  (Fields carry
+            # exp(-i w t): source sin + i cos = i exp(-i w t).)
+            nu, nv = int(round(hi[a1] - lo[a1])), int(round(hi[a2] - lo[a2]))
+            u = (torch.arange(nu, device=dev, dtype=torch.float64) + lo[a1] + 0.5 - center) * dx
+            v = (torch.arange(nv, device=dev, dtype=torch.float64) + lo[a2] + 0.5 - center) * dx
+            eu = torch.exp(-1j * k * torch.outer(rhat[:, a1], u).to(cdt))          # (A, U)
+            ev = torch.exp(-1j * k * torch.outer(rhat[:, a2], v).to(cdt))          # (A, V)
+            e0 = torch.exp(-1j * k * (rhat[:, axis] * ((x0 - center) * dx)).to(cdt)) * (dx * dx)  # (A,)
+            keys = [(Nvec, ca, val) for ca, val in J.items()] + [(Lvec, ca, val) for ca, val in M.items()]
+            vals = torch.stack([kv[2] for kv in keys])                              # (C, U, V)
+            t1 = torch.matmul(vals, ev.transpose(0, 1))                             # (C, U, A)
+            sums = (t1 * eu.transpose(0, 1).unsqueeze(0)).sum(dim=1) * e0           # (C, A)
+            for (acc, ca, _), sm in zip(keys, sums):
+                acc[:, ca] += sm
     cp, sp = torch.cos(phis).to(cdt), torch.sin(phis).to(cdt)
     N_th = Nvec[:, 0] * ct * cp + Nvec[:, 1] * ct * sp - Nvec[:, 2] * st
     N_ph = -Nvec[:, 0] * sp + Nvec[:, 1] * cp

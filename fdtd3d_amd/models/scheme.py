@@ -172,6 +172,11 @@ class YeeScheme(BlockedStepping):
         self.sub_step = 0
         self.timers: Dict[str, float] = {}
         self.hooks: List[Callable[["YeeScheme", int], None]] = []
+        # periodic work (NTFF, intermediate dumps, checkpoints): (period,
+        # offset, fn) fires fn(scheme, t) after step t when (t - offset) %
+        # period == 0.  Unlike per-step hooks these keep the blocked / hybrid
+        # passes: advance() ends a pass at every firing step.
+        self.periodic: List[Tuple[int, int, Callable[["YeeScheme", int], None]]] = []
         self.initialized = False
         from ..utils.profiler import PhaseProfiler
         self.prof = PhaseProfiler(self.device, cfg.profile_phases)
@@ -974,7 +979,31 @@ class YeeScheme(BlockedStepping):
         if self.cfg.check_finite and self.t % max(1, self.cfg.finite_check_step) == 0:
             self.check_finite()
 
+    def add_periodic(self, period: int, offset: int, fn: Callable[["YeeScheme", int], None]) -> None:
+        """Run ``fn(scheme, t)`` after every step ``t`` with ``(t - offset) %
+        period == 0`` (see ``self.periodic``)."""
+        self.periodic.append((max(1, int(period)), int(offset), fn))
+
+    def _next_periodic(self, t0: int, t1: int) -> int:
+        """First step in ``(t0, t1]`` at which periodic work fires (``t1`` if none)."""
+        nxt = t1
+        for period, off, _ in self.periodic:
+            t = t0 + 1 + ((off - (t0 + 1)) % period)
+            nxt = min(nxt, t)
+        return nxt
+
     def advance(self, n: int) -> None:
+        """``n`` leapfrog steps; blocked / hybrid passes end at every step at
+        which periodic work fires, which then runs between passes."""
+        end = self.t + n
+        while self.t < end:
+            nxt = self._next_periodic(self.t, end) if self.periodic else end
+            self._advance(nxt - self.t)
+            for period, off, fn in self.periodic:
+                if (self.t - off) % period == 0:
+                    fn(self, self.t)
+
+    def _advance(self, n: int) -> None:
         """``n`` leapfrog steps, ``self.tb`` at a time through the temporally
         blocked kernel where possible (no per-step hooks; a tail shorter than
         ``self.tb`` is one shorter pass), single fused steps otherwise."""

@@ -152,29 +152,32 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
         start_step = load_checkpoint(scheme, settings.loadFromFile)
         log.info("resumed from %s at step %d" % (settings.loadFromFile, start_step))
 
-    # periodic hooks (reference: NTFF every 100 steps, dumps every N steps)
-    def hook(s, t):
-        step_done = t - 1  # the reference evaluates after finishing step t-1 of its loop
-        if s.cfg.use_ntff and s.cfg.scheme == "3d" and step_done % max(1, s.cfg.ntff_step) == 0:
-            if halo is not None:
-                halo.drain(s)
-            ntff_report(s, step_done, out=out if rank == 0 else open(os.devnull, "w"))
-        if settings.doSaveIntermediateRes and t % max(1, settings.intermediateSaveStep) == 0:
-            if halo is not None:
-                halo.drain(s)
-            dump_fields(s, settings, t, "interm-")
-            if settings.doSaveScatteredFieldIntermediate:
-                dump_fields(s, settings, t, "interm-scattered-", scattered=True)
-        if settings.checkpointDir and settings.checkpointStep > 0 and t % settings.checkpointStep == 0:
-            if halo is not None:
-                halo.drain(s)
-            save_checkpoint(s, settings.checkpointDir)
+    # periodic work (reference: NTFF every 100 steps, dumps every N steps),
+    # run between blocked passes (YeeScheme.add_periodic)
+    def ntff_hook(s, t):
+        # the reference evaluates after finishing step t-1 of its loop
+        if halo is not None:
+            halo.drain(s)
+        ntff_report(s, t - 1, out=out if rank == 0 else open(os.devnull, "w"))
 
-    # only install the per-step hook when something is periodic: a hook-free
-    # run may advance several steps per kernel pass (--time-block)
-    if ((scheme.cfg.use_ntff and scheme.cfg.scheme == "3d") or settings.doSaveIntermediateRes
-            or (settings.checkpointDir and settings.checkpointStep > 0)):
-        scheme.hooks.append(hook)
+    def interm_hook(s, t):
+        if halo is not None:
+            halo.drain(s)
+        dump_fields(s, settings, t, "interm-")
+        if settings.doSaveScatteredFieldIntermediate:
+            dump_fields(s, settings, t, "interm-scattered-", scattered=True)
+
+    def checkpoint_hook(s, t):
+        if halo is not None:
+            halo.drain(s)
+        save_checkpoint(s, settings.checkpointDir)
+
+    if scheme.cfg.use_ntff and scheme.cfg.scheme == "3d":
+        scheme.add_periodic(scheme.cfg.ntff_step, 1, ntff_hook)
+    if settings.doSaveIntermediateRes:
+        scheme.add_periodic(settings.intermediateSaveStep, 0, interm_hook)
+    if settings.checkpointDir and settings.checkpointStep > 0:
+        scheme.add_periodic(settings.checkpointStep, 0, checkpoint_hook)
     steps = max(0, settings.numTimeSteps - start_step)
 
     def sync():

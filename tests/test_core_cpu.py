@@ -331,3 +331,24 @@ def test_phase_profiler_report():
     import json
     rec = json.loads([l for l in text.splitlines() if l.startswith("{")][-1])
     assert rec["phases"]["E"]["calls"] == 4 and rec["phases"]["H"]["calls"] == 4
+
+
+# ---------------------------------------------------------------- periodic work
+def test_periodic_hooks_fire_on_schedule():
+    """YeeScheme.add_periodic: fires after every step t with (t - offset) %
+    period == 0, across several advance() calls, in registration order."""
+    from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+    from fdtd3d_amd.ops import make_ops
+    cfg = SchemeConfig(scheme="3d", size=(8, 8, 8), dtype="f64", scene="vacuum", time_steps=0)
+    s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+    s.init_scheme()
+    s.init_grids()
+    seen = []
+    s.add_periodic(10, 1, lambda sc, t: seen.append(("a", t, sc.t)))
+    s.add_periodic(7, 0, lambda sc, t: seen.append(("b", t, sc.t)))
+    s.advance(12)
+    s.advance(13)
+    assert [x for x in seen if x[0] == "a"] == [("a", 1, 1), ("a", 11, 11), ("a", 21, 21)]
+    assert [x for x in seen if x[0] == "b"] == [("b", 7, 7), ("b", 14, 14), ("b", 21, 21)]
+    assert seen.index(("a", 21, 21)) < seen.index(("b", 21, 21))
+    assert s.t == 25

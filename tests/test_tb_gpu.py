@@ -249,3 +249,26 @@ def test_tb_bench_scale(gpu):
         assert err <= 1e-6 * scale, (c, err, scale)
     del runs, a, b
     torch.cuda.empty_cache()
+
+
+def test_tb_periodic_between_passes(gpu):
+    """Periodic work no longer forces single steps: a T=5 blocked run with
+    work every 7 steps (passes cut at 7, 14, ...) sees the same fields at each
+    firing as the fused single-step run, and still takes blocked passes."""
+    cfg = SchemeConfig(scheme="3d", size=(40, 36, 96), scene="vacuum", dtype="f32", use_fused=True, time_steps=23)
+    rec = {}
+    for T in (5, 1):
+        s = _scheme(dataclasses.replace(cfg, time_block=T), "hip", gpu, torch.float32)
+        s.randomize_fields(seed=4)
+        log = []
+        s.add_periodic(7, 0, lambda sc, t, log=log: log.append((t, sc.F[0]["Ez"].double().sum().item(),
+                                                              sc.F[0]["Hy"].double().abs().sum().item())))
+        launches0 = s.ops.launches
+        s.perform_steps()
+        torch.cuda.synchronize()
+        rec[T] = (log, s.ops.launches - launches0)
+    (la, na), (lb, nb) = rec[5], rec[1]
+    assert [x[0] for x in la] == [7, 14, 21] == [x[0] for x in lb]
+    for x, y in zip(la, lb):
+        assert abs(x[1] - y[1]) <= 1e-4 * (abs(y[1]) + 1) and abs(x[2] - y[2]) <= 1e-5 * y[2], (x, y)
+    assert na < nb  # blocked passes (7 = 5 + 2 per period), not 23 single steps
