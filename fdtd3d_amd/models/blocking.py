@@ -117,9 +117,13 @@ class BlockedStepping:
             else:
                 H = 4 if self.dtype == torch.float32 else F64_AUTO_STEPS
         hmax = getattr(self.ops, "tb2d_max_steps" if two_d else "tb_max_steps", 8 if two_d else 6)
-        if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme not in ("3d", "tmz", "tez") or self.halo is not None
+        if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme not in ("3d", "tmz", "tez")
                 or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode
                 or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials) or H > hmax):
+            return
+        if self.halo is not None and (cfg.scheme != "3d" or self.domain.buffer_size != H):
+            # decomposed: one T-deep exchange per pass feeds both the core and
+            # the deep-halo stepped shell, so the ghosts must be exactly T deep
             return
         if (two_d and int(cfg.hybrid_block) <= 0 and self.use_upml_chain and self.dtype == torch.float32
                 and self.ops.name == "hip"):
@@ -329,6 +333,10 @@ class BlockedStepping:
                             inside &= (ijk[:, d] >= lg[0][d]) & (ijk[:, d] < lg[1][d])
                         if bool(inside.any()):
                             return None
+        if self.halo is not None:
+            # decomposed: each rank's core is its owned part of the global core
+            couts = [box_intersect(b, dom.owned_global()) for b in couts]
+            couts = [b for b in couts if not box_empty(b)]
         band = T + 1
         Kb = grow(K, -band)
         if box_empty(Kb):
@@ -340,7 +348,11 @@ class BlockedStepping:
                 shell_windows.append(inner)
         copy_boxes = [b for b in box_subtract(alloc, K) if not box_empty(b)]
         if Dm is not None and not box_empty(Dm):
-            copy_boxes.append(Dm)
+            # (a decomposed run's dispersive box can reach past this rank's
+            # allocation: clip before turning it into local slices)
+            dma = box_intersect(Dm, alloc)
+            if not box_empty(dma):
+                copy_boxes.append(dma)
         # TF/SF corrections once per half step, unless a component's TF/SF
         # targets reach into a UPML chain box (D-form corrections there)
         self._tfsf_once = bool(cfg.use_tfsf)
@@ -389,6 +401,12 @@ class BlockedStepping:
             return
         hp = self.hybrid
         srcs = self._pass_sources(self.t, T)
+        if self.halo is not None:
+            # one T-deep exchange of every state array (aux included) feeds the
+            # core pass and the deep-halo shell steps; step() skips its own
+            with self.prof.phase("halo-deep"):
+                self.halo.exchange_all(self)
+            self._deep_fresh = True
         with self.prof.phase("blocked-core"):
             for p in range(self.planes):
                 tf = None

@@ -199,3 +199,9 @@ class CPML:
 
     def state_tensors(self, p: int) -> List[torch.Tensor]:
         return [sl.psi[p] for c in self.slabs for sl in self.slabs[c]]
+
+    def state_boxes(self, p: int):
+        """(global slab box, local index of psi[0, 0, 0]) per :meth:`state_tensors`
+        entry: the unpadded global box is the same on every rank, so the
+        two ends of a halo message clip it identically."""
+        return [(sl.gbox, sl.lbox[0]) for c in self.slabs for sl in self.slabs[c]]

@@ -641,12 +641,18 @@ class YeeScheme(BlockedStepping):
         F = self.F[p]
         if windows is None:
             windows = [self._window(kind)]
+        elif self.halo is not None:
+            # hybrid shell of a decomposed run: clip to this sub-step's deep-halo window
+            dw = self._window(kind)
+            windows = [b for b in (box_intersect(w, dw) for w in windows) if not box_empty(b)]
         tfsf_here = self.cfg.use_tfsf and not tfsf_once
         chain = self.use_upml_chain and getattr(self, "chain_regions", None) is not None
         if chain and self.hybrid is not None and len(windows) > 1:
             # hybrid shell: the chain boxes lie inside the shell, so each runs
             # once, whole; only the plain slabs are cut to the shell windows
-            self._update_chain_regions(kind, p, None, tfsf_here, plain_windows=windows)
+            # (decomposed: clipped to this sub-step's deep-halo window)
+            self._update_chain_regions(kind, p, None if self.halo is None else self._window(kind), tfsf_here,
+                                       plain_windows=windows)
             windows = []
         for w in windows:
             if chain:
@@ -805,6 +811,23 @@ class YeeScheme(BlockedStepping):
                 out += self.cpml.state_tensors(p)
         return out
 
+    def state_boxes(self) -> List[Optional[Tuple[Box, Tuple[int, int, int]]]]:
+        """Per :meth:`state_tensors` entry: None for arrays of the local field
+        shape, else (global box the array covers, local index of its first
+        element) -- the CPML psi slabs, whose ghost parts a deep-halo exchange
+        moves through the same messages."""
+        out = []
+        for p in range(self.planes):
+            out += [None] * len(self.comps)
+            if self.use_upml_chain:
+                for c in self.comps:
+                    out += [None] * len(self.upml[c]["D"][p])
+                    if self.cfg.use_metamaterials:
+                        out += [None] * len(self.upml[c]["D1"][p])
+            if self.use_cpml:
+                out += self.cpml.state_boxes(p)
+        return out
+
     def _apply_sources(self, t: int, p: int) -> None:
         if self.line_source is not None and self.cfg.use_amp_mode and self.in_amplitude:
             comp, offs = self.line_source
@@ -835,8 +858,11 @@ class YeeScheme(BlockedStepping):
             return
         deep = halo is not None and B > 1
         if deep and self.sub_step == 0:
-            with self.prof.phase("halo-deep"):
-                halo.exchange_all(self)
+            if getattr(self, "_deep_fresh", False):
+                self._deep_fresh = False  # a hybrid pass exchanged already
+            else:
+                with self.prof.phase("halo-deep"):
+                    halo.exchange_all(self)
         ph = self.prof.phase
         for p in range(self.planes):
             if cfg.use_tfsf:

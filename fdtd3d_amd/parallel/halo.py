@@ -275,32 +275,32 @@ class HaloExchanger:
 
     def _exchange_direct(self, scheme) -> None:
         ops = scheme.ops
-        tensors = scheme.state_tensors()
+        tensors, boxed = _split_state(scheme)
         d = self.domain
         ops_list, recvs = [], []
         for off, peer, sg, rg in self.deep_messages():
             sbox, rbox = d.to_local(sg), d.to_local(rg)
             key = (off[0] + 1) * 9 + (off[1] + 1) * 3 + (off[2] + 1)
             back = (-off[0] + 1) * 9 + (-off[1] + 1) * 3 + (-off[2] + 1)
-            sb = self._buf(("xs", key), _vol(sbox) * len(tensors), tensors[0])
-            _pack_many(ops, tensors, sbox, sb)
-            rb = self._buf(("xr", key), _vol(rbox) * len(tensors), tensors[0])
+            sb = self._buf(("xs", key), _msg_len(tensors, boxed, sg), tensors[0])
+            _pack_state(ops, tensors, boxed, sbox, sg, d, sb)
+            rb = self._buf(("xr", key), _msg_len(tensors, boxed, rg), tensors[0])
             # the peer sends its message for offset -off with tag(-off)
             ops_list.append(P2P(True, sb, peer, 300 + key))
             ops_list.append(P2P(False, rb, peer, 300 + back))
-            recvs.append((rbox, rb))
+            recvs.append((rbox, rg, rb))
             self.bytes_sent += sb.numel() * sb.element_size()
             self.messages += 1
         for w in self._post(ops_list):
             w.wait()
-        for rbox, rb in recvs:
-            _unpack_many(ops, tensors, rbox, rb)
+        for rbox, rg, rb in recvs:
+            _unpack_state(ops, tensors, boxed, rbox, rg, d, rb)
 
     def _exchange_sweep(self, scheme) -> None:
         d = self.domain
         B = d.buffer_size
         ops = scheme.ops
-        tensors = scheme.state_tensors()
+        tensors, boxed = _split_state(scheme)
         alloc_lo, alloc_hi = d.allocated_global()
         for a in range(3):
             lo_n, hi_n = d.neighbors[a]
@@ -316,29 +316,31 @@ class HaloExchanger:
             if lo_n >= 0:
                 sbox = box_along(d.lo[a], d.lo[a] + B)
                 rbox = box_along(d.lo[a] - B, d.lo[a])
-                sb = self._buf(("ds", a, 0), _vol(sbox) * len(tensors), tensors[0])
-                _pack_many(ops, tensors, sbox, sb)
-                rb = self._buf(("dr", a, 0), _vol(rbox) * len(tensors), tensors[0])
+                sg, rg = d.to_global(sbox), d.to_global(rbox)
+                sb = self._buf(("ds", a, 0), _msg_len(tensors, boxed, sg), tensors[0])
+                _pack_state(ops, tensors, boxed, sbox, sg, d, sb)
+                rb = self._buf(("dr", a, 0), _msg_len(tensors, boxed, rg), tensors[0])
                 ops_list.append(P2P(True,sb, lo_n,100 + 2 * a))
                 ops_list.append(P2P(False,rb, lo_n,101 + 2 * a))
-                recvs.append((rbox, rb))
+                recvs.append((rbox, rg, rb))
                 self.bytes_sent += sb.numel() * sb.element_size()
                 self.messages += 1
             if hi_n >= 0:
                 sbox = box_along(d.hi[a] - B, d.hi[a])
                 rbox = box_along(d.hi[a], d.hi[a] + B)
-                sb = self._buf(("ds", a, 1), _vol(sbox) * len(tensors), tensors[0])
-                _pack_many(ops, tensors, sbox, sb)
-                rb = self._buf(("dr", a, 1), _vol(rbox) * len(tensors), tensors[0])
+                sg, rg = d.to_global(sbox), d.to_global(rbox)
+                sb = self._buf(("ds", a, 1), _msg_len(tensors, boxed, sg), tensors[0])
+                _pack_state(ops, tensors, boxed, sbox, sg, d, sb)
+                rb = self._buf(("dr", a, 1), _msg_len(tensors, boxed, rg), tensors[0])
                 ops_list.append(P2P(True,sb, hi_n,101 + 2 * a))
                 ops_list.append(P2P(False,rb, hi_n,100 + 2 * a))
-                recvs.append((rbox, rb))
+                recvs.append((rbox, rg, rb))
                 self.bytes_sent += sb.numel() * sb.element_size()
                 self.messages += 1
             for w in self._post(ops_list):
                 w.wait()
-            for rbox, rb in recvs:
-                _unpack_many(ops, tensors, rbox, rb)
+            for rbox, rg, rb in recvs:
+                _unpack_state(ops, tensors, boxed, rbox, rg, d, rb)
 
     # ------------------------------------------------------------ collectives
     def allreduce_sum(self, v: int) -> int:
@@ -365,6 +367,59 @@ def _pack_many(ops, tensors, box, buf):
     for i in range(0, len(tensors), 8):
         chunk = tensors[i:i + 8]
         ops.pack(chunk, box, buf[i * n:(i + len(chunk)) * n])
+
+
+def _split_state(scheme):
+    """(arrays of the local field shape, [(array, global box it covers, local
+    index of its first element)]) of the scheme's state."""
+    ts = scheme.state_tensors()
+    bx = scheme.state_boxes() if hasattr(scheme, "state_boxes") else [None] * len(ts)
+    full = [t for t, b in zip(ts, bx) if b is None]
+    boxed = [(t, b[0], b[1]) for t, b in zip(ts, bx) if b is not None]
+    return full, boxed
+
+
+def _boxed_part(g: Box, cover: Box, first, d):
+    """Local box inside a boxed array (first element at local ``first``) of
+    the global message box ``g`` clipped to the array's global ``cover``."""
+    from .domain import box_intersect
+    c = box_intersect(g, cover)
+    if any(c[1][a] <= c[0][a] for a in range(3)):
+        return None
+    lc = d.to_local(c)
+    return (tuple(lc[0][a] - first[a] for a in range(3)), tuple(lc[1][a] - first[a] for a in range(3)))
+
+
+def _msg_len(full, boxed, g) -> int:
+    n = _vol(g) * len(full)
+    for t, cover, first in boxed:
+        from .domain import box_intersect
+        n += _vol(box_intersect(g, cover))
+    return n
+
+
+def _pack_state(ops, full, boxed, lbox, g, d, buf):
+    n = _vol(lbox) * len(full)
+    _pack_many(ops, full, lbox, buf[:n])
+    for t, cover, first in boxed:
+        b = _boxed_part(g, cover, first, d)
+        if b is None:
+            continue
+        m = _vol(b)
+        ops.pack([t], b, buf[n:n + m])
+        n += m
+
+
+def _unpack_state(ops, full, boxed, lbox, g, d, buf):
+    n = _vol(lbox) * len(full)
+    _unpack_many(ops, full, lbox, buf[:n])
+    for t, cover, first in boxed:
+        b = _boxed_part(g, cover, first, d)
+        if b is None:
+            continue
+        m = _vol(b)
+        ops.unpack([t], b, buf[n:n + m])
+        n += m
 
 
 def _unpack_many(ops, tensors, box, buf):

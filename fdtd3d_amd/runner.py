@@ -83,6 +83,13 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
             tb = auto_time_block(cfg.scheme, cfg.dtype, backend, percell, world) if plain else 1
         if tb > 1 and cfg.scheme in ("3d", "tmz", "tez"):
             buf = tb  # blocked passes exchange tb-deep ghosts every tb steps
+        hyb = (backend == "hip" and cfg.use_fused and cfg.scheme == "3d" and not cfg.use_amp_mode
+               and (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials) and settings.hybridBlock != 1)
+        if hyb:
+            # hybrid passes (models/blocking.py): blocked core + stepped shell,
+            # one hybridBlock-deep exchange per pass
+            from .models.blocking import F64_AUTO_STEPS
+            buf = settings.hybridBlock if settings.hybridBlock > 1 else (4 if cfg.dtype == "f32" else F64_AUTO_STEPS)
         # float4 rows: z extent (3D) / y extent (2D) padded to a multiple of 4
         domain = core.domain(rank, buf, align_z=4 if tb > 1 else 1, align_axis=2 if cfg.scheme == "3d" else 1)
         halo = HaloExchanger(domain)

@@ -47,6 +47,8 @@ def _worker(rank, world, port, cfg, topo_axes, buf, outdir, mode="direct"):
         s.init_scheme()
         s.init_grids()
         assert s.tb == max(1, cfg.time_block)
+        if cfg.hybrid_block > 1:
+            assert s.hybrid is not None, "hybrid pass not selected on rank %d" % rank
         s.perform_steps()
         halo.drain(s)
         res = {}
@@ -96,6 +98,26 @@ CASES = [
                                    sphere_center=(9.5, 8.5, 10.5), use_fused=True), 8, "xyz", 1),
     ("fused-xy4-b2", SchemeConfig(scheme="3d", size=(20, 20, 12), time_steps=9, scene="vacuum", use_fused=True,
                                   complex_values=True), 4, "xy", 2),
+    # hybrid passes in decomposed runs: blocked core (owned part of the global
+    # core) + deep-halo stepped shell, one T-deep exchange (aux state included)
+    ("hybrid-upml-tfsf-xy4-b3", SchemeConfig(scheme="3d", size=(80, 80, 80), time_steps=8, use_pml=True,
+                                             use_tfsf=True, pml_size=(4, 4, 4), tfsf_size=(8, 8, 8), theta=50,
+                                             phi=20, psi=30, hybrid_block=3), 4, "xy", 3),
+    ("hybrid-cpml-point-xyz8-b2", SchemeConfig(scheme="3d", size=(64, 64, 64), time_steps=7, use_pml=True,
+                                               pml_type="cpml", pml_size=(4, 4, 4), scene="vacuum",
+                                               hybrid_block=2), 8, "xyz", 2),
+    ("deep-drude-z2-b3", SchemeConfig(scheme="3d", size=(64, 64, 72), time_steps=7, use_pml=True,
+                                      use_metamaterials=True, scene="drude-sphere", sphere_radius=4,
+                                      sphere_center=(32.0, 32.0, 36.0), pml_size=(4, 4, 4), hybrid_block=1),
+     2, "z", 3),
+    ("hybrid-drude-off-z2-b3", SchemeConfig(scheme="3d", size=(64, 64, 72), time_steps=7, use_pml=True,
+                                            use_metamaterials=True, scene="drude-sphere", sphere_radius=4,
+                                            sphere_center=(32.0, 32.0, 20.0), pml_size=(4, 4, 4), hybrid_block=3),
+     2, "z", 3),
+    ("hybrid-drude-z2-b3", SchemeConfig(scheme="3d", size=(64, 64, 72), time_steps=7, use_pml=True,
+                                        use_metamaterials=True, scene="drude-sphere", sphere_radius=4,
+                                        sphere_center=(32.0, 32.0, 36.0), pml_size=(4, 4, 4), hybrid_block=3),
+     2, "z", 3),
     # temporal blocking: T steps per pass, T-deep ghosts exchanged every T steps
     ("tb2-xyz8", SchemeConfig(scheme="3d", size=(16, 18, 20), time_steps=9, scene="vacuum", use_fused=True,
                               time_block=2), 8, "xyz", 2),
@@ -131,6 +153,11 @@ def test_decomposed_equals_serial(name, cfg, world, axes, buf, mode):
             b = ser.F[p][c]
             scale = float(b.abs().max()) + 1e-300
             err = float((a - b).abs().max())
+            if err > 1e-12 * scale:
+                d = (a - b).abs()
+                zs = [(z, float(d[:, :, z].max())) for z in range(d.shape[2]) if float(d[:, :, z].max()) > 1e-12 * scale]
+                xs = [(x, float(d[x].max())) for x in range(d.shape[0]) if float(d[x].max()) > 1e-12 * scale]
+                print("ERRMAP", name, c, "z", zs[:12], "x", xs[:12])
             assert err <= 1e-12 * scale, (name, c, err, scale, par["topology"].tolist())
 
 
