@@ -128,13 +128,17 @@ def ntff_power(fields_re: Optional[Dict[str, torch.Tensor]], fields_im: Optional
 
     def face(comp, axis, x0, lo, hi):
         plan = _sample_plan(comp, axis, x0, lo, hi)
+        pb = _plan_box(plan)
         if boxes is None:
-            key, origin = comp, (0, 0, 0)
+            # slice the (thin) slab the face reads before any conversion: a
+            # whole-grid .to(float64) per face and component would dominate
+            sl = tuple(slice(pb[0][a], pb[1][a]) for a in range(3))
+            get = lambda f: f[comp][sl]
         else:
-            key = (comp, _plan_box(plan))
-            origin = key[1][0]
-        re = _sample_from(fields_re[key].to(torch.float64), origin, plan, axis)
-        im = (_sample_from(fields_im[key].to(torch.float64), origin, plan, axis) if fields_im is not None
+            get = lambda f: f[(comp, pb)]
+        origin = pb[0]
+        re = _sample_from(get(fields_re).to(torch.float64), origin, plan, axis)
+        im = (_sample_from(get(fields_im).to(torch.float64), origin, plan, axis) if fields_im is not None
               else torch.zeros_like(re))
         return torch.complex(re, im)
 

@@ -32,7 +32,7 @@ def run_threads(cfg, world, axes, buf, device):
 
     def body(rank):
         try:
-            dom = core.domain(rank, buf, align_z=4 if cfg.time_block > 1 else 1,
+            dom = core.domain(rank, buf, align_z=4 if (cfg.time_block > 1 or cfg.hybrid_block > 1) else 1,
                               align_axis=2 if cfg.scheme == "3d" else 1)
             halo = HaloExchanger(dom, comm=hub.comm(rank))
             s = YeeScheme(cfg, make_ops("hip", None, device, dt), dom, halo)
@@ -40,7 +40,10 @@ def run_threads(cfg, world, axes, buf, device):
             s.init_grids()
             # time_block 0: the automatic rule must pick the ghost depth the
             # driver sized the domain for (models/blocking.py auto_time_block)
-            assert s.tb == (buf if cfg.time_block == 0 else max(1, cfg.time_block))
+            if cfg.hybrid_block > 1:
+                assert s.hybrid is not None, "hybrid pass not selected"
+            else:
+                assert s.tb == (buf if cfg.time_block == 0 else max(1, cfg.time_block))
             s.perform_steps()
             halo.drain(s)
             torch.cuda.synchronize()
@@ -91,6 +94,14 @@ CASES = [
     ("auto-sphere-xy4", SchemeConfig(scheme="3d", size=(48, 44, 128), time_steps=13, scene="sphere", sphere_radius=10,
                                      sphere_center=(24.0, 20.0, 64.0), dtype="f32", use_fused=True, time_block=0),
      4, "xy", 4),
+    # hybrid passes on decomposed ranks (blocked core + deep-halo stepped shell)
+    ("hybrid-cpml-tfsf-xy4", SchemeConfig(scheme="3d", size=(96, 96, 96), time_steps=10, scene="vacuum", dtype="f32",
+                                          use_pml=True, pml_type="cpml", use_tfsf=True, pml_size=(5, 5, 5),
+                                          tfsf_size=(10, 10, 10), use_fused=True, hybrid_block=4), 4, "xy", 4),
+    ("hybrid-upml-drude-z2", SchemeConfig(scheme="3d", size=(80, 80, 96), time_steps=9, dtype="f32", use_pml=True,
+                                          use_metamaterials=True, scene="drude-sphere", sphere_radius=6,
+                                          sphere_center=(40.0, 40.0, 48.0), pml_size=(5, 5, 5), use_fused=True,
+                                          hybrid_block=3), 2, "z", 3),
     # fp64 blocked kernel
     ("tb4-f64-xyz8", SchemeConfig(scheme="3d", size=(40, 36, 44), time_steps=10, scene="vacuum", dtype="f64",
                                   use_fused=True, time_block=4), 8, "xyz", 4),
