@@ -45,9 +45,12 @@ TB2D_AUTO_STEPS_F64 = 7
 F32_AUTO_STEPS = 5
 F32_AUTO_STEPS_MANY_RANKS = 4
 F32_AUTO_STEPS_PERCELL_BOTH = 2
+# plain runs with in-kernel TF/SF (TfsfSets): 512^3 vacuum + TF/SF T=4 127k,
+# T=5 86k Mcells/s (the TF/SF variant spills at T=5)
+F32_AUTO_STEPS_TFSF = 4
 
 
-def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: int = 1) -> int:
+def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: int = 1, tfsf: bool = False) -> int:
     """Steps per pass of a plain (no PML / TF-SF / dispersion) run in
     automatic mode -- ONE rule for the serial scheme, the decomposed driver
     (which must size the ghost layers before the scheme exists) and bench.py.
@@ -63,6 +66,8 @@ def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: 
         return F64_AUTO_STEPS
     if int(percell) >= 2:
         return F32_AUTO_STEPS_PERCELL_BOTH
+    if tfsf:
+        return F32_AUTO_STEPS_TFSF
     return F32_AUTO_STEPS if world <= 2 else F32_AUTO_STEPS_MANY_RANKS
 
 

@@ -303,7 +303,8 @@ class YeeScheme(BlockedStepping):
             if self.halo is not None:
                 t = self.domain.topology
                 world = t[0] * t[1] * t[2]
-            T = auto_time_block(cfg.scheme, cfg.dtype, self.ops.name, percell, world)
+            T = auto_time_block(cfg.scheme, cfg.dtype, self.ops.name, percell, world,
+                                tfsf=bool(getattr(self, "tfsf_blocked", False)))
             if self.halo is not None and self.domain.buffer_size != T:
                 T = 1
         self.tb = 1

@@ -29,6 +29,10 @@ for n in ${CONFIGS:-cpml upml drude sphere}; do
     sphere4) run sphere4 --scene sphere --sphere-eps 4 $SPH --time-block 4 ;;
     sphere5) run sphere5 --scene sphere --sphere-eps 4 $SPH --time-block 5 ;;
     vac) run vac --scene vacuum ;;
+    cpmlpt) run cpmlpt --scene vacuum --use-pml --pml-type cpml ;;
+    drudecpml) run drudecpml --scene drude-sphere --use-metamaterials --use-pml --pml-type cpml $SPH ;;
+    drudecpmlh) run drudecpmlh --scene drude-sphere --use-metamaterials --use-pml --pml-type cpml $SPH --hybrid-block 4 ;;
+    drudeh) run drudeh --scene drude-sphere --use-metamaterials --use-pml $SPH --hybrid-block 4 ;;
     vac4) run vac4 --scene vacuum --time-block 4 ;;
     tfsf4) run tfsf4 --scene vacuum --use-tfsf --time-block 4 ;;
     tfsf5) run tfsf5 --scene vacuum --use-tfsf --time-block 5 ;;
