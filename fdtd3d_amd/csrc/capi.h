@@ -57,6 +57,7 @@ int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, double* co
                   const int* boxes, const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
                   void* stream);
 int fdtd_tb64_max_steps();
+void fdtd_set_tb64_shape(int half);
 int fdtd_tb2d_f32(int mode, const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                   const float* const* cs, double cb, double db, int nx, int ny, const int* boxes, const int* obox,
                   int xchunk, int steps, const int* src, const double* src_vals, void* stream);

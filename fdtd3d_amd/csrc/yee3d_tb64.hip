@@ -3,8 +3,13 @@
 // multi-row kernel in yee3d_tb.hip (a level lags one x plane; y neighbours
 // between waves through a double-buffered LDS slot, one barrier per level; z
 // neighbours by DPP wave shifts), with scalar fp64 lanes: every carried
-// value takes two VGPRs, so one row per wave (two rows spill from T = 2 on):
-// 16-row x 64-lane tiles, T halo rows / lanes on each side.
+// value takes two VGPRs, so one cell per lane (two cells spill from T = 2
+// on).  Default tiles are 32 x 32 (each wave holds two y rows of 32 z lanes,
+// HALF below); the 16-row x 64-lane shape stays selectable
+// (fdtd_set_tb64_shape).  T halo rows / lanes on each side, 1..5 steps.
+// 1024^3 vacuum, one MI355X (bench.py --dtype f64): 16 x 64 tiles T = 4
+// 105-109k Mcells/s; 32 x 32 tiles T = 4 114k; + stores deferred one plane
+// (no store-ack drain per plane) 120k; T = 5 116k.
 // A single-pass fp64 step moves >= 96 B/cell; T steps per pass read and write
 // the six fields once (plus the tile halos).
 
@@ -63,6 +68,7 @@ struct F3d {
 };
 
 int g_num_cus64 = 0;
+bool g_tb64_half = true;
 
 // x chunk minimising rounds x (chunk + 2T) (same model as yee3d_tb.hip)
 int pick_xchunk64(long long tiles_yz, int nxo, int T) {
@@ -91,7 +97,12 @@ int pick_xchunk64(long long tiles_yz, int nxo, int T) {
   return best;
 }
 
-template <int T, int R, bool PERCELL>
+// HALF: each wave holds two y rows of 32 z lanes (lanes 0-31 row 2w, 32-63
+// row 2w+1): 32 x 32 tiles instead of 16 x 64, so a larger share of the
+// tile is owned (T = 4: 24 x 24 of 32 x 32 = 56% against 8 x 56 of 16 x 64 =
+// 44%) for the same registers.  The z shift crosses the half boundary only
+// into halo lanes; y neighbours are one flat LDS row (32 lanes) apart.
+template <int T, int R, bool PERCELL, bool HALF>
 __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
     const double* __restrict__ exi, const double* __restrict__ eyi, const double* __restrict__ ezi,
     const double* __restrict__ hxi, const double* __restrict__ hyi, const double* __restrict__ hzi,
@@ -101,10 +112,14 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
     const double* __restrict__ dbx, const double* __restrict__ dby, const double* __restrict__ dbz, double cb,
     double db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc64 sv) {
-  constexpr int TBZ = 64 - 2 * T;  // owned z cells per tile
-  constexpr int ROWS = TBW * R;
+  constexpr int LW = HALF ? 32 : 64;  // z lanes per row
+  constexpr int TBZ = LW - 2 * T;       // owned z cells per tile
+  constexpr int ROWS = TBW * R * (HALF ? 2 : 1);
+  static_assert(!HALF || R == 1, "half-wave rows hold one row per half");
   __shared__ double sX[2][4][TBW][64];
   const int lane = threadIdx.x;
+  const int lz = HALF ? (lane & 31) : lane;
+  const int hr = HALF ? (lane >> 5) : 0;
   const int w = threadIdx.y;
   // XCD-contiguous tile order, z fastest (see yee3d_tb.hip)
   int tz, ty, tx;
@@ -118,12 +133,12 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
     ty = (q / gx) % gy;
     tx = q / (gx * gy);
   }
-  const int k = O.lo[2] - T + TBZ * tz + lane;
-  const int jw = O.lo[1] - T + (ROWS - 2 * T) * ty + R * w;
+  const int k = O.lo[2] - T + TBZ * tz + lz;
+  const int jw = O.lo[1] - T + (ROWS - 2 * T) * ty + (HALF ? 2 * w + hr : R * w);
   const int i0 = O.lo[0] + tx * xchunk;
   const int i1 = min(i0 + xchunk, O.hi[0]);
   const bool kin = k >= 0 && k < nz;
-  const bool lane_own = lane >= T && lane < 64 - T;
+  const bool lane_own = lz >= T && lz < LW - T;
   const size_t plane = (size_t)ny * nz;
   unsigned roff[R];
   unsigned mbits = 0;  // bit r*7 + n: row r inside box n (n = 6: stored cells)
@@ -131,7 +146,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int j = jw + r;
-    const int t = R * w + r;
+    const int t = HALF ? 2 * w + hr : R * w + r;
     const bool ld_ok = kin && j >= 0 && j < ny;
     roff[r] = ld_ok ? (unsigned)(j * nz + k) * 8u : 0xF0000000u;
     const bool own = ld_ok && lane_own && t >= T && t < ROWS - T;
@@ -167,6 +182,34 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
       E[r] = {bld64(rex, roff[r]), bld64(rey, roff[r]), bld64(rez, roff[r])};
     }
   };
+  // outputs of plane X are stored one plane late, after the next prefetch:
+  // the stores are issued unconditionally, masked by an out-of-range buffer
+  // offset (dropped by the descriptor), so the wait at the top of a plane
+  // covers loads and stores that were both issued a whole plane earlier
+  // (with stores in flight the compiler drains vmcnt: storing right before
+  // that wait stalled every plane on the write acknowledgements)
+  F3d Ed[R], Hd[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    Ed[r] = {0.0, 0.0, 0.0};
+    Hd[r] = {0.0, 0.0, 0.0};
+  }
+  auto store_out = [&](int Xs) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool own = (mbits >> (r * 7 + 6)) & 1u;
+      const int pe = Xs - T + 1;
+      const unsigned oe = own && pe >= i0 && pe < i1 ? roff[r] : 0xF0000000u;
+      bst64(plane_rsrc64(exo, pe, nx, plane), oe, Ed[r].x);
+      bst64(plane_rsrc64(eyo, pe, nx, plane), oe, Ed[r].y);
+      bst64(plane_rsrc64(ezo, pe, nx, plane), oe, Ed[r].z);
+      const int ph = Xs - T;
+      const unsigned oh = own && ph >= i0 && ph < i1 ? roff[r] : 0xF0000000u;
+      bst64(plane_rsrc64(hxo, ph, nx, plane), oh, Hd[r].x);
+      bst64(plane_rsrc64(hyo, ph, nx, plane), oh, Hd[r].y);
+      bst64(plane_rsrc64(hzo, ph, nx, plane), oh, Hd[r].z);
+    }
+  };
   F3d Hnx[R], Enx[R];
   load_plane(i0 - T, Hnx, Enx);
   for (int X = i0 - T; X <= i1 + T - 1; ++X) {
@@ -177,6 +220,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
       Ec[r] = Enx[r];
     }
     load_plane(X + 1, Hnx, Enx);
+    store_out(X - 1);  // the first plane's are out of [i0, i1): dropped
     F3d En[R];
 #pragma unroll
     for (int l = 0; l < T; ++l) {
@@ -186,10 +230,22 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
       sX[buf][2][w][lane] = Ep[l][0].x;
       sX[buf][3][w][lane] = Ep[l][0].z;
       __syncthreads();
-      const double hz_dn = sX[buf][0][rdn][lane];
-      const double hx_dn = sX[buf][1][rdn][lane];
-      const double ex_up = sX[buf][2][rup][lane];
-      const double ez_up = sX[buf][3][rup][lane];
+      double hz_dn, hx_dn, ex_up, ez_up;
+      if constexpr (HALF) {
+        // row j -/+ 1 is 32 lanes down / up in the flat [TBW * 64] slot
+        const int fl = w * 64 + lane;
+        const int fdn = fl >= 32 ? fl - 32 : fl;
+        const int fup = fl < TBW * 64 - 32 ? fl + 32 : fl;
+        hz_dn = (&sX[buf][0][0][0])[fdn];
+        hx_dn = (&sX[buf][1][0][0])[fdn];
+        ex_up = (&sX[buf][2][0][0])[fup];
+        ez_up = (&sX[buf][3][0][0])[fup];
+      } else {
+        hz_dn = sX[buf][0][rdn][lane];
+        hx_dn = sX[buf][1][rdn][lane];
+        ex_up = sX[buf][2][rup][lane];
+        ez_up = sX[buf][3][rup][lane];
+      }
       buf ^= 1;
       const bool src_plane = src_comp >= 0 && pe == src_i;
 #pragma unroll
@@ -226,32 +282,21 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      if ((mbits >> (r * 7 + 6)) & 1u) {
-        const int pe = X - T + 1;
-        if (pe >= i0 && pe < i1) {
-          bst64(plane_rsrc64(exo, pe, nx, plane), roff[r], En[r].x);
-          bst64(plane_rsrc64(eyo, pe, nx, plane), roff[r], En[r].y);
-          bst64(plane_rsrc64(ezo, pe, nx, plane), roff[r], En[r].z);
-        }
-        const int ph = X - T;
-        if (ph >= i0 && ph < i1) {
-          bst64(plane_rsrc64(hxo, ph, nx, plane), roff[r], Hc[r].x);
-          bst64(plane_rsrc64(hyo, ph, nx, plane), roff[r], Hc[r].y);
-          bst64(plane_rsrc64(hzo, ph, nx, plane), roff[r], Hc[r].z);
-        }
-      }
+      Ed[r] = En[r];
+      Hd[r] = Hc[r];
     }
   }
+  store_out(i1 + T - 1);
 }
 
-template <int T, int R>
+template <int T, int R, bool HALF>
 int launch_tb64(bool pc, const double* const* ein, const double* const* hin, double* const* eout,
                 double* const* hout, const double* const* cbs, const double* const* dbs, double cb, double db,
                 int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src,
                 const TbSrc64& sv, hipStream_t s) {
-  constexpr int TBZ = 64 - 2 * T;
+  constexpr int TBZ = (HALF ? 32 : 64) - 2 * T;
   const long long gz = cdiv(O.hi[2] - O.lo[2], TBZ);
-  const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * T);
+  const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R * (HALF ? 2 : 1) - 2 * T);
   if (xchunk <= 0) xchunk = pick_xchunk64(gz * gy, O.hi[0] - O.lo[0], T);
   dim3 grid((unsigned)gz, (unsigned)gy, cdiv(O.hi[0] - O.lo[0], xchunk));
 #define TB64_ARGS                                                                                              \
@@ -259,16 +304,20 @@ int launch_tb64(bool pc, const double* const* ein, const double* const* hin, dou
       cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
       O, xchunk, src[0], src[1], src[2], src[3], sv
   if (pc)
-    k_tb3d_f64<T, R, true><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
+    k_tb3d_f64<T, R, true, HALF><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
   else
-    k_tb3d_f64<T, R, false><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
+    k_tb3d_f64<T, R, false, HALF><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
 #undef TB64_ARGS
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
 }  // namespace
 
-FDTD_API int fdtd_tb64_max_steps() { return 4; }
+FDTD_API int fdtd_tb64_max_steps() { return 5; }
+
+// 1: two rows of 32 lanes per wave (32 x 32 tiles, default); 0: one row of
+// 64 lanes (16 x 64 tiles)
+FDTD_API void fdtd_set_tb64_shape(int half) { g_tb64_half = half != 0; }
 
 // fp64 counterpart of fdtd_tb3d_v4_f32 (same arguments, double arrays), 1..4
 // steps per pass, any nz.
@@ -276,7 +325,7 @@ FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, d
                            double* const* hout, const double* const* cbs, const double* const* dbs, double cb,
                            double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
                            int steps, const int* src, const double* src_vals, void* stream) {
-  if (steps < 1 || steps > 4) return (int)hipErrorInvalidValue;
+  if (steps < 1 || steps > 5) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const Box3 O = make_box(obox);
@@ -286,12 +335,24 @@ FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, d
   const bool pc = cbs[0] != nullptr || dbs[0] != nullptr;  // a null kind uses its scalar
   hipStream_t s = (hipStream_t)stream;
   // one row per wave: two rows of fp64 state spill from T = 2 on
-#define TB64(TT) launch_tb64<TT, 1>(pc, ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s)
-  switch (steps) {
-    case 1: return TB64(1);
-    case 2: return TB64(2);
-    case 3: return TB64(3);
-    case 4: return TB64(4);
+#define TB64(TT, HF) \
+  launch_tb64<TT, 1, HF>(pc, ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s)
+  if (g_tb64_half) {
+    switch (steps) {
+      case 1: return TB64(1, true);
+      case 2: return TB64(2, true);
+      case 3: return TB64(3, true);
+      case 4: return TB64(4, true);
+      case 5: return TB64(5, true);
+    }
+  } else {
+    switch (steps) {
+      case 1: return TB64(1, false);
+      case 2: return TB64(2, false);
+      case 3: return TB64(3, false);
+      case 4: return TB64(4, false);
+      case 5: return TB64(5, false);
+    }
   }
 #undef TB64
   return (int)hipErrorInvalidValue;

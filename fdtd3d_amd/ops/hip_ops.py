@@ -28,7 +28,7 @@ Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
 _LIB = None
 TB_MAX_STEPS = 6  # steps per pass of the blocked kernels (fdtd_tb_max_steps)
-TB_MAX_STEPS_F64 = 4  # fp64 blocked kernel (fdtd_tb64_max_steps)
+TB_MAX_STEPS_F64 = 5  # fp64 blocked kernel (fdtd_tb64_max_steps)
 TB2D_MAX_STEPS = 8  # 2D TMz / TEz blocked kernel, fp32 (fdtd_tb2d_max_steps)
 TB2D_MAX_STEPS_F64 = 8  # fp64 (fdtd_tb2d64_max_steps)
 TB2D_MODES = {("Ez",): (0, ("Ez",), ("Hx", "Hy")), ("Ex", "Ey"): (1, ("Ex", "Ey"), ("Hz",))}
@@ -692,6 +692,8 @@ class HipOps:
             self.lib.fdtd_set_tb_mrows(c_int(mr))
             self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
             self.lib.fdtd_set_tb_mr_shape(c_int(self.tb_mr_shape))
+        else:
+            self.lib.fdtd_set_tb64_shape(c_int(self.tb64_half))
         # fp32: yee3d_tb.hip (multi-row / single-row tiles); fp64: yee3d_tb64.hip
         rc = self.fn("tb3d_v4" if self.dtype == torch.float32 else "tb3d")(arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv),
                                 c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
@@ -776,6 +778,8 @@ class HipOps:
     tb_sparse = True  # per-cell fp32 coefficients: sparse float4 boxes on the multi-row kernel
     # plain multi-row tile shape: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows (two workgroups per CU)
     tb_mr_shape = int(os.environ.get("FDTD3D_TB_MR_SHAPE", "0"))
+    # fp64 tiles: 1 = two rows of 32 z lanes per wave (32 x 32), 0 = one row of 64 (16 x 64)
+    tb64_half = int(os.environ.get("FDTD3D_TB64_HALF", "1"))
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],

@@ -153,16 +153,21 @@ F64_CASES = [
     ((40, 18, 61), 3, "sphere", None, False),      # per-cell coefficients, odd nz
     ((24, 26, 28), 4, "vacuum", ((4, 4, 4), (20, 22, 24)), True),
     ((20, 20, 36), 2, "vacuum", ((0, 0, 2), (20, 20, 4)), "shell"),
+    ((30, 70, 75), 5, "vacuum", None, True),      # 3 x 4 half-wave tiles at T = 5
+    ((26, 41, 33), 5, "sphere", None, False),
 ]
 
 
+@pytest.mark.parametrize("half", [1, 0])
 @pytest.mark.parametrize("size,T,scene,obox,src", F64_CASES)
-def test_tb_f64_vs_torch(gpu, size, T, scene, obox, src):
-    """fp64 blocked kernel (yee3d_tb64.hip) vs the fp64 torch oracle."""
+def test_tb_f64_vs_torch(gpu, size, T, scene, obox, src, half):
+    """fp64 blocked kernel (yee3d_tb64.hip, both tile shapes) vs the fp64
+    torch oracle."""
     cfg = SchemeConfig(scheme="3d", size=size, scene=scene, sphere_radius=min(size) / 3.0,
                        sphere_center=tuple(v / 2.0 for v in size), dtype="f64", use_fused=True)
     a = _scheme(cfg, "hip", gpu, torch.float64)
     a.ops.tb_xchunk = 16
+    a.ops.tb64_half = half
     b = _scheme(cfg, "torch", "cpu", torch.float64)
     _randomize(a)
     _randomize(b)
@@ -183,7 +188,7 @@ def test_tb_f64_vs_torch(gpu, size, T, scene, obox, src):
         assert err <= 1e-12 * (float(y.abs().max()) + 1.0), (c, err)
 
 
-@pytest.mark.parametrize("T", [2, 3, 4])
+@pytest.mark.parametrize("T", [2, 3, 4, 5])
 def test_tb_f64_scheme_matches_fused(gpu, T):
     cfg = SchemeConfig(scheme="3d", size=(40, 36, 90), scene="vacuum", dtype="f64", use_fused=True, time_steps=11)
     a = _scheme(dataclasses.replace(cfg, time_block=T), "hip", gpu, torch.float64)

@@ -1,14 +1,14 @@
 #!/bin/bash
-# fp64 (the reference's default value type): blocked-kernel + hybrid tests, then runs.
+# fp64 blocked kernel: oracle tests, then 1024^3 throughput per tile shape and T
 set -o pipefail
-cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_tb_gpu.py tests/test_hybrid_gpu.py -x -q -k "f64" --timeout 120 --timeout-method thread > gpurun_out/pytest_f64.log 2>&1
-rc=$?; grep -E "FAIL|Error|assert" gpurun_out/pytest_f64.log | head; tail -2 gpurun_out/pytest_f64.log; [ $rc -ne 0 ] && exit $rc
-C512="--3d --sizex 512 --same-size --warmup-steps 8 --json"
-for args in "--time-steps 64 --scene vacuum" "--time-steps 40 --scene vacuum --use-pml --pml-type cpml --use-tfsf" \
-            "--time-steps 40 --scene vacuum --use-pml --use-tfsf" "--time-steps 40 --scene vacuum --use-pml --use-tfsf --hybrid-block 1"; do
-  timeout -k 10 200 python -m fdtd3d_amd $C512 $args > gpurun_out/f64.log 2>&1 || { tail -5 gpurun_out/f64.log; exit 1; }
-  echo "[f64 $args] $(grep -o '"mcells_per_s": [0-9.]*' gpurun_out/f64.log)"
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_tb_gpu.py -k f64 \
+  > gpurun_out/f64_tests.log 2>&1 || { tail -30 gpurun_out/f64_tests.log; exit 1; }
+tail -3 gpurun_out/f64_tests.log
+for half in 1 0; do
+  for T in 4 5; do
+    FDTD3D_TB64_HALF=$half timeout -k 10 200 python bench.py --dtype f64 --steps 20 --warmup 5 --time-block $T \
+      > gpurun_out/f64_h${half}_T$T.json 2> gpurun_out/f64_err.log || { tail gpurun_out/f64_err.log; exit 1; }
+    echo "half=$half T=$T $(cat gpurun_out/f64_h${half}_T$T.json)"
+  done
 done
-timeout -k 10 300 python bench.py --dtype f64 --steps 16 --warmup 4 > gpurun_out/bench_f64.log 2>&1 && cut -c1-200 gpurun_out/bench_f64.log
