@@ -779,13 +779,29 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   load_plane(i0 - T, Hnx, Enx);
   if (PFD == 2) load_plane(i0 - T + 1, Hn2, En2);
   F3<V> Hs[R];  // DEFER: H_T of the previous plane, stored next trip
+#pragma unroll
+  for (int r = 0; r < R; ++r) Hs[r] = F3<V>{};
   // stores of the results of trip X: E_T on plane X-T+1 (= Ep[T-1] until the
   // next trip's last level), H_T on plane X-T
   auto store_plane = [&](int X, const F3<V>* Es, const F3<V>* Hh) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const unsigned mo = (mbits >> ((r * 7 + 6) * V)) & VM;
-      if (mo) {
+      if constexpr (V == 1) {
+        // unconditional stores masked by an out-of-range offset (dropped by
+        // the descriptor): a fixed store count per trip keeps the compiler's
+        // vmcnt bookkeeping exact, so the next prefetch wait does not drain
+        // the stores (see DEFER)
+        const int pe = X - T + 1, ph = X - T;
+        const unsigned oe = mo && pe >= i0 && pe < i1 ? roff[r] : 0xF0000000u;
+        const unsigned oh = mo && ph >= i0 && ph < i1 ? roff[r] : 0xF0000000u;
+        bst<V>(plane_rsrc(exo, pe, nx, plane), oe, Es[r].x, 1u);
+        bst<V>(plane_rsrc(eyo, pe, nx, plane), oe, Es[r].y, 1u);
+        bst<V>(plane_rsrc(ezo, pe, nx, plane), oe, Es[r].z, 1u);
+        bst<V>(plane_rsrc(hxo, ph, nx, plane), oh, Hh[r].x, 1u);
+        bst<V>(plane_rsrc(hyo, ph, nx, plane), oh, Hh[r].y, 1u);
+        bst<V>(plane_rsrc(hzo, ph, nx, plane), oh, Hh[r].z, 1u);
+      } else if (mo) {
         const int pe = X - T + 1;
         if (pe >= i0 && pe < i1) {
           bst<V>(plane_rsrc(exo, pe, nx, plane), roff[r], Es[r].x, mo);
@@ -934,7 +950,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
       load_plane(X + 2, Hn2, En2);
     else
       load_plane(X + 1, Hnx, Enx);
-    if (DEFER && X > i0 - T) {
+    if (DEFER && (V == 1 || X > i0 - T)) {  // V = 1: the first trip's stores are dropped
       F3<V> Es[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) Es[r] = Ep[T - 1][r];
