@@ -111,6 +111,46 @@ int launch_box_copy(T* const* fields, T* buf, int ncomp, int ny, int nz, const B
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
+// Field-to-field copy of a box for `ncomp` component pairs (the hybrid
+// pass's shell copy): same (component, plane) x (y, z) walk as k_box_copy.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_box_xfer(FieldPtrs<T> src, FieldPtrs<T> dst, int ny, int nz, Box3 b) {
+  typedef T VT __attribute__((ext_vector_type(V)));
+  const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1], bz = b.hi[2] - b.lo[2];
+  const int ci = blockIdx.z;
+  const int c = ci / bx, i = ci - c * bx;
+  const T* __restrict__ f = src.p[c];
+  T* __restrict__ g = dst.p[c];
+  const int bzv = bz / V, nyzv = by * bzv;
+  const size_t fplane = (size_t)(b.lo[0] + i) * ny;
+  for (int jk = blockIdx.x * 256 + threadIdx.x; jk < nyzv; jk += gridDim.x * 256) {
+    const int j = jk / bzv, kv = jk - j * bzv;
+    const size_t off = (fplane + (b.lo[1] + j)) * nz + (b.lo[2] + kv * V);
+    if (V == 1)
+      g[off] = f[off];
+    else
+      *reinterpret_cast<VT*>(g + off) = *reinterpret_cast<const VT*>(f + off);
+  }
+}
+
+template <typename T>
+int launch_box_xfer(T* const* src, T* const* dst, int ncomp, int ny, int nz, const Box3& b, hipStream_t s) {
+  FieldPtrs<T> fs, fd;
+  constexpr int VW = 16 / sizeof(T);
+  bool vec = (b.hi[2] - b.lo[2]) % VW == 0 && b.lo[2] % VW == 0 && nz % VW == 0;
+  for (int c = 0; c < ncomp; ++c) {
+    fs.p[c] = src[c];
+    fd.p[c] = dst[c];
+    vec = vec && ((uintptr_t)src[c] & 15) == 0 && ((uintptr_t)dst[c] & 15) == 0;
+  }
+  if ((long long)(b.hi[0] - b.lo[0]) * ncomp > 65535) return (int)hipErrorInvalidValue;
+  if (vec)
+    k_box_xfer<T, VW><<<box_copy_grid(b, ncomp, VW), 256, 0, s>>>(fs, fd, ny, nz, b);
+  else
+    k_box_xfer<T, 1><<<box_copy_grid(b, ncomp, 1), 256, 0, s>>>(fs, fd, ny, nz, b);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
 // ---------------------------------------------------------------- reductions
 // max |f| over a box -> atomicMax on the float bit pattern (non-negative
 // floats order like their integer bits).  Used by the amplitude mode and the
@@ -219,6 +259,12 @@ inline unsigned reduce_grid(long long n) {
     Box3 b = make_box(box);                                                                                   \
     if (box_empty(b) || ncomp <= 0 || ncomp > 8) return ncomp > 8 ? (int)hipErrorInvalidValue : 0;             \
     return launch_box_copy<T, false>(fields, (T*)buf, ncomp, ny, nz, b, (hipStream_t)s);                    \
+  }                                                                                                           \
+  FDTD_API int fdtd_box_xfer_##SUF(T* const* src, T* const* dst, int ncomp, int ny, int nz, const int* box,     \
+                                   void* s) {                                                                 \
+    Box3 b = make_box(box);                                                                                   \
+    if (box_empty(b) || ncomp <= 0 || ncomp > 8) return ncomp > 8 ? (int)hipErrorInvalidValue : 0;             \
+    return launch_box_xfer<T>(src, dst, ncomp, ny, nz, b, (hipStream_t)s);                                   \
   }                                                                                                           \
   FDTD_API int fdtd_box_maxabs_##SUF(const T* f, int ny, int nz, const int* box, unsigned int* out, void* s) { \
     Box3 b = make_box(box);                                                                                   \

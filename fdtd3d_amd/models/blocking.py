@@ -342,15 +342,25 @@ class BlockedStepping:
             # decomposed: each rank's core is its owned part of the global core
             couts = [box_intersect(b, dom.owned_global()) for b in couts]
             couts = [b for b in couts if not box_empty(b)]
-        band = T + 1
-        Kb = grow(K, -band)
-        if box_empty(Kb):
+        def shell_windows(d):
+            # everything but the core cells deeper than d inside it
+            Kd = grow(K, -d)
+            if box_empty(Kd):
+                return None
+            ws = [b for b in box_subtract(alloc, Kd) if not box_empty(b)]
+            if Dm is not None and not box_empty(Dm):
+                inner = box_intersect(grow(Dm, d), Kd)
+                if not box_empty(inner):
+                    ws.append(inner)
+            return ws
+
+        # step s of the pass (0-based) advances the shell plus a band T - s
+        # deep into the core: the stale core beyond the band corrupts one
+        # more band cell per step, so after step s the band is exact to depth
+        # T - 1 - s, and after the last step the shell itself (depth 0)
+        shells = [shell_windows(T - s) for s in range(T)]
+        if shells[0] is None:
             return None
-        shell_windows = [b for b in box_subtract(alloc, Kb) if not box_empty(b)]
-        if Dm is not None and not box_empty(Dm):
-            inner = box_intersect(grow(Dm, band), Kb)
-            if not box_empty(inner):
-                shell_windows.append(inner)
         copy_boxes = [b for b in box_subtract(alloc, K) if not box_empty(b)]
         if Dm is not None and not box_empty(Dm):
             # (a decomposed run's dispersive box can reach past this rank's
@@ -371,7 +381,7 @@ class BlockedStepping:
                         if tb is not None and not box_empty(b) and not box_empty(box_intersect(dom.to_local(b), tb)):
                             self._tfsf_once = False
         upd = {c: self.local_box(c, alloc) for c in self.comps}
-        return {"T": T, "core": [dom.to_local(b) for b in couts], "shell": shell_windows,
+        return {"T": T, "core": [dom.to_local(b) for b in couts], "shell": shells[0], "shells": shells,
                 "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
                 "cut_cells": box_volume(Dm) if Dm is not None else 0}
 
@@ -428,14 +438,14 @@ class BlockedStepping:
                 if tf is not None:
                     self.einc[p].copy_(line0[0])
                     self.hinc[p].copy_(line0[1])
-        for _ in range(T):
-            self.step(hp["shell"])
+        for s in range(T):
+            self.step(hp["shells"][s])
         with self.prof.phase("shell-copy"):
             for p in range(self.planes):
+                src = [self.F[p][c] for c in self.comps]
+                dst = [self.F_alt[p][c] for c in self.comps]
                 for b in hp["copy"]:
-                    sl = tuple(slice(b[0][d], b[1][d]) for d in range(3))
-                    for c in self.comps:
-                        self.F_alt[p][c][sl] = self.F[p][c][sl]
+                    self.ops.copy_box(src, dst, b)
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
 

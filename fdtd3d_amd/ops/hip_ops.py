@@ -508,6 +508,25 @@ class HipOps:
         _check(rc, "box_unpack")
         self.launches += 1
 
+    def copy_box(self, src: Sequence[torch.Tensor], dst: Sequence[torch.Tensor], box: Box) -> None:
+        """dst[c][box] = src[c][box] for up to 8 component pairs, one launch
+        (aux_kernels.hip k_box_xfer)."""
+        if _empty(box) or not src:
+            return
+        if len(src) != len(dst) or len(src) > 8:
+            raise HipError("copy_box: 1..8 matching component pairs")
+        shape = tuple(src[0].shape)
+        for d in range(3):
+            if box[0][d] < 0 or box[1][d] > shape[d]:
+                raise HipError("copy box %s outside %s" % (box, shape))
+        for t in list(src) + list(dst):
+            self._check_tensor(t, shape)
+        rc = self.fn("box_xfer")((c_vp * len(src))(*[t.data_ptr() for t in src]),
+                                 (c_vp * len(dst))(*[t.data_ptr() for t in dst]), c_int(len(src)),
+                                 c_int(shape[1]), c_int(shape[2]), _box_arr([box]), _stream())
+        _check(rc, "box_xfer")
+        self.launches += 1
+
     # ------------------------------------------------------------ reductions
     def _scratch_u32(self):
         s = getattr(self, "_u32", None)
@@ -555,9 +574,14 @@ class HipOps:
             table.max_inc = int(table.i0.max()) + 1
         if max_off >= target.numel() or table.max_inc >= inc.numel():
             raise HipError("TF/SF table reads or writes outside its arrays")
+        bb = getattr(table, "bbox", None)
+        if bb is None:  # targets' bounding box: one (syncing) reduction, then cached
+            v = table.ijk.view(-1, 3)
+            table.bbox = bb = (tuple(int(x) for x in v.min(0).values), tuple(int(x) + 1 for x in v.max(0).values))
+        whole = all(box[0][d] <= bb[0][d] and bb[1][d] <= box[1][d] for d in range(3))
         rc = self.fn("tfsf_apply")(_ptr(target), _ptr(table.off), _ptr(table.i0), _ptr(table.w0), _ptr(table.w1),
-                                   _ptr(table.coef), _ptr(table.ijk), c_int(table.n), _ptr(inc), _box_arr([box]),
-                                   _stream())
+                                   _ptr(table.coef), None if whole else _ptr(table.ijk), c_int(table.n), _ptr(inc),
+                                   _box_arr([box]), _stream())
         _check(rc, "tfsf_apply")
         self.launches += 1
 

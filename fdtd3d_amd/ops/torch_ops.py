@@ -240,6 +240,12 @@ class TorchOps:
         for c, t in enumerate(tensors):
             t[sl] = buf[c * n:(c + 1) * n].view(t[sl].shape)
 
+    def copy_box(self, src: Sequence[torch.Tensor], dst: Sequence[torch.Tensor], box: Box) -> None:
+        """dst[c][box] = src[c][box] for every component pair."""
+        sl = box_slices(box)
+        for a, b in zip(src, dst):
+            b[sl] = a[sl]
+
     # ------------------------------------------------------------ reductions
     def maxabs(self, t: torch.Tensor, box: Box) -> float:
         if _empty(box):

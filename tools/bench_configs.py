@@ -56,6 +56,16 @@ CONFIGS = [
     ("2d-tmz-8k-upml-tfsf", "2D TMz 8192^2, UPML + TF/SF, fp32 (hybrid blocking)",
      ["--2d", "--sizex", "8192", "--sizey", "8192", "--time-steps", "210", "--warmup-steps", "14", "--scene",
       "vacuum", "--use-pml", "--use-tfsf", "--dtype", "f32"]),
+    ("3d-512-cpml-point", "3D 512^3, CPML (10 cells), point dipole, fp32",
+     C512 + ["--time-steps", "100", "--scene", "vacuum", "--use-pml", "--pml-type", "cpml"]),
+    ("3d-512-tfsf", "3D 512^3 vacuum + TF/SF plane wave, no PML, fp32 (in-kernel TF/SF, T=4)",
+     C512 + ["--time-steps", "200", "--scene", "vacuum", "--use-tfsf"]),
+    ("3d-512-ntff", "3D 512^3 vacuum, point dipole, NTFF diagram every 100 steps, fp32",
+     C512 + ["--time-steps", "210", "--scene", "vacuum", "--use-ntff", "--ntff-sizex", "15", "--ntff-sizey", "15",
+             "--ntff-sizez", "15"]),
+    ("3d-512-vacuum-f64", "3D vacuum 512^3, point dipole, fp64",
+     ["--3d", "--sizex", "512", "--same-size", "--dtype", "f64", "--warmup-steps", "10", "--time-steps", "200",
+      "--scene", "vacuum"]),
     ("3d-512-sphere-tb4", "3D 512^3 dielectric sphere (eps=4, r=128), fp32, 4 steps per pass",
      C512 + ["--time-steps", "210", "--scene", "sphere", "--sphere-eps", "4",
              "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",

@@ -14,6 +14,7 @@ run() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$name -o run -- python3 -m fdtd3d_amd $C512 "$@" > $O/$name.log 2>&1 || { echo "$name failed"; tail -5 $O/$name.log; return 1; }
   grep '^{' $O/$name.log | cut -c1-300
   python3 tools/prof_summary.py $(find $O/$name -name '*results.db' | head -1) --cells 134217728 > $O/$name.md 2>&1
+  python3 tools/prof_summary.py $(find $O/$name -name '*results.db' | head -1) --marker ${MARKER:-k_tb3d} --passes ${PASSES:-8} > $O/${name}_steady.md 2>&1
   rm -rf $O/$name
 }
 for n in ${CONFIGS:-cpml upml drude sphere}; do

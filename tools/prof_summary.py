@@ -43,12 +43,26 @@ def main(argv=None):
     ap.add_argument("db")
     ap.add_argument("--cells", type=float, default=0.0, help="cells per launch, for GB/s")
     ap.add_argument("--title", default="")
+    ap.add_argument("--marker", default="", help="kernel-name substring that starts each pass / step")
+    ap.add_argument("--passes", type=int, default=0,
+                    help="with --marker: only the kernels between the start of the (passes+1)-th last marker "
+                         "launch and the start of the last one (steady-state, init excluded)")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
+    where = ""
+    if a.marker and a.passes > 0:
+        names = c.execute("select k.start, coalesce(nullif(k.name, ''), s.kernel_name) from kernels k left join "
+                          "kernel_symbols s on s.kernel_id = k.kernel_id order by k.start").fetchall()
+        starts = [t for t, n in names if a.marker in demangle(n or "")]
+        if len(starts) > a.passes:
+            t0, t1 = starts[-a.passes - 1], starts[-1]
+            where = " where k.start >= %d and k.start < %d" % (t0, t1)
+            sys.stdout.write("window: %d passes, %.3f ms wall, %.3f ms per pass\n\n" % (
+                a.passes, (t1 - t0) / 1e6, (t1 - t0) / 1e6 / a.passes))
     rows = c.execute("select coalesce(nullif(k.name, ''), s.kernel_name), count(*), sum(k.duration), "
                      "avg(k.duration), min(k.duration), max(k.vgpr_count), max(k.sgpr_count), max(k.lds_size), "
-                     "max(k.scratch_size) from kernels k left join kernel_symbols s on s.kernel_id = k.kernel_id "
-                     "group by k.kernel_id order by sum(k.duration) desc").fetchall()
+                     "max(k.scratch_size) from kernels k left join kernel_symbols s on s.kernel_id = k.kernel_id"
+                     + where + " group by k.kernel_id order by sum(k.duration) desc").fetchall()
     rows = [(demangle(r[0] or "?"),) + tuple(r[1:]) for r in rows]
     total = sum(r[2] for r in rows) or 1
     out = sys.stdout
