@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tb2d(const F* __restrict__ e0i, co
   // coefficient of component n (0..2) on row x
   auto coef = [&](const F* arr, const Box3& b, int x, const V& sc) -> V {
     const unsigned m = ld_ok ? ymask<N>(b, x, jb) : 0u;
-    if (PERCELL) return sel(ld<F>(row_rsrc(arr, x, nx, ny), off), m);
+    if (PERCELL && arr) return sel(ld<F>(row_rsrc(arr, x, nx, ny), off), m);  // null: the kind's scalar
     return sel(sc, m);
   };
   // carried per level l: Hp = H_l(row X-1-l), Ep = E_{l+1}(row X-1-l)
@@ -311,7 +311,7 @@ int tb2d(int mode, const F* const* ein, const F* const* hin, F* const* eout, F* 
   if (O.hi[0] <= O.lo[0] || O.hi[1] <= O.lo[1]) return 0;
   Src2<F> sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[2] >= 0 && l < steps) ? (F)src_vals[l] : F(0);
-  const bool pc = cs[0] != nullptr;
+  const bool pc = cs[0] != nullptr || cs[1] != nullptr || cs[2] != nullptr;
   hipStream_t s = (hipStream_t)stream;
   if (mode == 0) return dispatch2d<F, 0>(steps, pc, ein, hin, eout, hout, cs, (F)cb, (F)db, nx, ny, b, O, xchunk, src, sv, s);
   return dispatch2d<F, 1>(steps, pc, ein, hin, eout, hout, cs, (F)cb, (F)db, nx, ny, b, O, xchunk, src, sv, s);
@@ -326,7 +326,8 @@ FDTD_API int fdtd_tb2d64_max_steps() { return max_steps2d<double>(); }
 // {Ez}, h = {Hx, Hy}), 1 TEz (e = {Ex, Ey}, h = {Hz}); unused array slots may
 // be null.  `cs` = 3 per-cell coefficient arrays in component order (all
 // null: scalars cb / db), `boxes` = 3 update boxes (lo[3] hi[3]) in component
-// order, `obox` = cells stored; `src` = {x, y, component 0..2 | -1} with one
+// order (a null array: that component uses its kind's scalar cb / db, so a
+// uniform kind streams no constant plane), `obox` = cells stored; `src` = {x, y, component 0..2 | -1} with one
 // value per step.  ny must be a multiple of 4 (fp32) / 2 (fp64): 16-byte rows.
 FDTD_API int fdtd_tb2d_f32(int mode, const float* const* ein, const float* const* hin, float* const* eout,
                            float* const* hout, const float* const* cs, double cb, double db, int nx, int ny,

@@ -754,14 +754,20 @@ class HipOps:
         for d in range(2):
             if obox[0][d] < 0 or obox[1][d] > shape[d]:
                 raise HipError("output box %s outside array %s" % (obox, shape))
-        if any(self._cell_or_none(cb[c]) is not None for c in comps):
-            cs = (c_vp * 3)(*[self._cell_array(cb[c], shape).data_ptr() for c in comps])
-            cbv, dbv = 1.0, 1.0
-        else:
-            cs = (c_vp * 3)(None, None, None)
-            cbv, dbv = cb[E[0]].scalar, cb[H[0]].scalar
-            if any(cb[c].scalar != cbv for c in E) or any(cb[c].scalar != dbv for c in H):
-                raise HipError("tb_step: scalar coefficients must agree per kind")
+        # per kind: per-cell arrays when any component of the kind has them,
+        # else null pointers and the kind's scalar (no constant planes streamed)
+        ptrs, sv = [], {}
+        for kind, names in (("E", E), ("H", H)):
+            if any(self._cell_or_none(cb[c]) is not None for c in names):
+                ptrs += [self._cell_array(cb[c], shape).data_ptr() for c in names]
+                sv[kind] = 1.0
+            else:
+                ptrs += [None] * len(names)
+                sv[kind] = cb[names[0]].scalar
+                if any(cb[c].scalar != sv[kind] for c in names):
+                    raise HipError("tb_step: scalar coefficients must agree per kind")
+        cs = (c_vp * 3)(*ptrs)
+        cbv, dbv = sv["E"], sv["H"]
         src = [-1, -1, -1]
         vals = [0.0] * 8
         if sources is not None and any(s is not None for s in sources):

@@ -90,3 +90,38 @@ def test_tb2d_scheme_matches_stepped(gpu, mode, T, dtype):
         x, y = a.F[0][c], b.F[0][c]
         err = float((x - y).abs().max())
         assert err <= (1e-5 if dtype == "f32" else 1e-12) * scale, (c, err, scale)
+
+
+@pytest.mark.parametrize("kinds", ["E", "H", "EH"])
+@pytest.mark.parametrize("mode", ["tmz", "tez"])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_tb2d_per_kind_coefs(gpu, mode, kinds, dtype):
+    """Per-cell coefficients on one kind only (the other kind passes null
+    arrays and its scalar: no constant planes) or on both, vs the torch
+    oracle."""
+    from fdtd3d_amd.ops.coef import Coef
+    nx, ny = 36, 264
+    dt = torch.float32 if dtype == "f32" else torch.float64
+    cfg = SchemeConfig(scheme=mode, size=(nx, ny, 1), scene="vacuum", dtype=dtype, use_fused=True)
+    a = _scheme(cfg, "hip", gpu, dt)
+    b = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
+    g = torch.Generator().manual_seed(5)
+    for c in a.comps:
+        if c[0] not in kinds:
+            continue
+        cell = 0.3 + 0.7 * torch.rand((nx, ny, 1), generator=g, dtype=torch.float64)
+        a.cb[c] = Coef(scalar=a.cb[c].scalar, cell=cell.to(dt).to(gpu))
+        b.cb[c] = Coef(scalar=b.cb[c].scalar, cell=cell.to(dt).double())
+    _randomize(a)
+    _randomize(b)
+    upd = {c: a.local_box(c) for c in a.comps}
+    ob = ((0, 0, 0), (nx, ny, 1))
+    T = 4
+    a.ops.tb_step(a.F[0], a.F_alt[0], upd, ob, a.cb, T, None)
+    b.ops.tb_step(b.F[0], b.F_alt[0], upd, ob, b.cb, T, None)
+    torch.cuda.synchronize()
+    for c in a.comps:
+        x = a.F_alt[0][c].double().cpu()
+        y = b.F_alt[0][c]
+        err = float((x - y).abs().max())
+        assert err <= (2e-5 if dtype == "f32" else 1e-12) * (float(y.abs().max()) + 1.0), (c, err)
