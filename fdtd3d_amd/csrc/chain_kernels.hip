@@ -49,6 +49,8 @@ struct ChainComp {
   const T* b2;
   const T* ma1;
   const T* ma2;
+  const unsigned char* id;  // Drude material index per cell (null: the five per-cell arrays)
+  const T* lut;             // id -> (b0, b1, b2, ma1, ma2)
   T s;
   int a0, a1, sg0, sg1, aD, aA, aB;
   Box3 box;
@@ -74,11 +76,23 @@ __device__ __forceinline__ void chain_cell(const ChainComp<T>& q, bool kind_e, c
     Dp = q.Dp[off];
     D1 = q.D1[off];
     D1p = q.D1p[off];
-    b0 = q.b0[off];
-    b1 = q.b1[off];
-    b2 = q.b2[off];
-    m1 = q.ma1[off];
-    m2 = q.ma2[off];
+    if (q.id) {
+      // material-ID + LUT: one byte per cell instead of 20 (a Drude scene
+      // holds a handful of distinct coefficient tuples: vacuum, the
+      // material and the averaged boundary cells)
+      const T* e = q.lut + 5 * (int)q.id[off];
+      b0 = e[0];
+      b1 = e[1];
+      b2 = e[2];
+      m1 = e[3];
+      m2 = e[4];
+    } else {
+      b0 = q.b0[off];
+      b1 = q.b1[off];
+      b2 = q.b2[off];
+      m1 = q.ma1[off];
+      m2 = q.ma2[off];
+    }
   }
   // ---- compute
   const T d0 = kind_e ? (x0 - y0) : (y0 - x0);
@@ -125,7 +139,7 @@ __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q
   }
 }
 
-constexpr int CP_PER = 21;  // pointers per component
+constexpr int CP_PER = 23;  // pointers per component
 constexpr int CI_PER = 13;  // ints per component
 
 template <typename T>
@@ -152,6 +166,8 @@ ChainComp<T> make_comp(const void* const* P, double s, const int* I) {
   q.b2 = (const T*)P[18];
   q.ma1 = (const T*)P[19];
   q.ma2 = (const T*)P[20];
+  q.id = (const unsigned char*)P[21];
+  q.lut = (const T*)P[22];
   q.s = (T)s;
   q.a0 = I[0];
   q.a1 = I[1];
@@ -195,8 +211,8 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
 }  // namespace
 
 // One chain launch for the three components of a kind.  Per component c:
-// P[21c ..] = E Dn D Dp D1n D1 D1p s0 s1 caD cbD caE ica cbEa ccEa cell b0 b1 b2 ma1 ma2
-// (unused: nullptr), S[c] = scalar of the E-from-D term, I[13c ..] = curl axes
+// P[23c ..] = E Dn D Dp D1n D1 D1p s0 s1 caD cbD caE ica cbEa ccEa cell b0 b1 b2 ma1 ma2 id lut
+// (unused: nullptr; a non-null id replaces b0 .. ma2 by lut[5 id ..]), S[c] = scalar of the E-from-D term, I[13c ..] = curl axes
 // a0 a1, signs sg0 sg1, UPML axes aD aCa aCb, box lo[3] hi[3] (empty: skipped).
 FDTD_API int fdtd_chain3d_f32(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny,
                               int nz, void* s) {

@@ -694,21 +694,45 @@ class YeeScheme(BlockedStepping):
         chain box holds TF/SF targets take the generic D-form path there)."""
         comps = self.e_comps if kind == "E" else self.h_comps
         F = self.F[p]
-        dom = self.domain
         tfsf = self.cfg.use_tfsf
         inc = (self.hinc[p] if kind == "E" else self.einc[p]) if tfsf else None
+        pws = tuple(plain_windows) if plain_windows is not None else None
+        key = (kind, w, pws)
+        cache = self.__dict__.setdefault("_chain_plan_cache", {})
+        plan = cache.get(key)
+        if plan is None:
+            # the launch list of this (kind, window set) is static: built once
+            # (the hybrid shell steps through T window sets every pass)
+            plan = cache[key] = self._chain_plan(kind, w, pws)
+        for boxes in plan["plain"]:
+            self.ops.curl_update(kind, boxes, F, F, self.cb)
+            if tfsf and tfsf_plain:
+                for c in comps:
+                    for tab in self.tfsf[c]:
+                        self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
+        for launches, slow in plan["chain"]:
+            for sel, form, plain_form in launches:
+                self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form)
+            for c, b in slow:
+                self._upml_region(kind, c, p, b)
+
+    def _chain_plan(self, kind: str, w: Optional[Box], pws) -> dict:
+        """Launches of one UPML/Drude step on window ``w`` (plain slabs cut to
+        ``pws`` when given): local plain boxes per launch, and per chain box
+        the fused chain launches (dispersive / non-dispersive form) plus the
+        components that take the generic D-form path (TF/SF targets inside)."""
+        comps = self.e_comps if kind == "E" else self.h_comps
+        dom = self.domain
+        tfsf = self.cfg.use_tfsf
         reg = self.chain_regions[kind]
         whole = dom.allocated_global()
+        plain = []
         for r in reg["plain"]:
-            for pw in (plain_windows if plain_windows is not None else [w]):
+            for pw in (pws if pws is not None else [w]):
                 boxes = {c: dom.to_local(box_intersect(r[c], pw)) for c in comps}
-                if all(box_empty(b) for b in boxes.values()):
-                    continue
-                self.ops.curl_update(kind, boxes, F, F, self.cb)
-                if tfsf and tfsf_plain:
-                    for c in comps:
-                        for tab in self.tfsf[c]:
-                            self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
+                if not all(box_empty(b) for b in boxes.values()):
+                    plain.append(boxes)
+        chain = []
         for r, dru in reg["chain"]:
             boxes = {c: dom.to_local(box_intersect(r[c], w if w is not None else whole)) for c in comps}
             if all(box_empty(b) for b in boxes.values()):
@@ -718,25 +742,23 @@ class YeeScheme(BlockedStepping):
                 b = boxes[c]
                 tb = self.tfsf_bbox.get(c) if tfsf else None
                 if tb is not None and not box_empty(b) and not box_empty(box_intersect(b, tb)):
-                    slow.append(c)
+                    slow.append((c, b))
                     fast[c] = (b[0], b[0])
                 else:
                     fast[c] = b
             if self.cfg.scheme != "3d":
                 # 2D: the chain boxes are the thin PML slabs (+ the dispersive
                 # box); the factored per-component chain runs there
-                for c in comps:
-                    if not box_empty(boxes[c]):
-                        self._upml_region(kind, c, p, boxes[c])
+                chain.append(([], [(c, boxes[c]) for c in comps if not box_empty(boxes[c])]))
                 continue
             # one launch per form: dispersive chain / non-dispersive chain
+            launches = []
             for form in (True, False):
                 sel = {c: (fast[c] if dru[c] == form else (fast[c][0], fast[c][0])) for c in comps}
                 if any(not box_empty(b) for b in sel.values()):
-                    plain_form = self.cfg.use_metamaterials and not form
-                    self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form)
-            for c in slow:
-                self._upml_region(kind, c, p, boxes[c])
+                    launches.append((sel, form, self.cfg.use_metamaterials and not form))
+            chain.append((launches, slow))
+        return {"plain": plain, "chain": chain}
 
     def _upml_region(self, kind: str, c: str, p: int, box: Box) -> None:
         F = self.F[p]

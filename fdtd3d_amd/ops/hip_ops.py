@@ -853,13 +853,16 @@ class HipOps:
             if cell is not None:
                 self._check_tensor(cell, shape)
             dr = [None] * 5
+            lut = (None, None)
             if drude:
                 dr = [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")]
                 for n, t in zip(("b0", "b1", "b2", "ma1", "ma2"), dr):
                     if st[n].scalar != 1.0 or t is None:
                         raise HipError("Drude coefficient %s must be a plain per-cell array" % n)
                     self._check_tensor(t, shape)
-            P += [None if t is None else t.data_ptr() for t in fields + profs + [cell] + dr]
+                if self.drude_lut:
+                    lut = self._drude_lut(st, dr, shape)
+            P += [None if t is None else t.data_ptr() for t in fields + profs + [cell] + dr + list(lut)]
             S.append(float(pr["s"]))
             I += [terms[0][1], terms[1][1], terms[0][2], terms[1][2], aD, aA, aB] + list(b[0]) + list(b[1])
         if not any_box:
@@ -869,6 +872,24 @@ class HipOps:
                                 c_int(shape[2]), _stream())
         _check(rc, "chain3d")
         self.launches += 1
+
+    drude_lut = True  # Drude chain: uint8 material index + coefficient table (falls back past 256 tuples)
+
+    def _drude_lut(self, st: dict, dr, shape):
+        """(uint8 id array, (n, 5) table) of a component's five Drude
+        coefficient arrays, built once per component (None, None when the
+        arrays hold more than 256 distinct tuples)."""
+        got = st.get("_drude_lut")
+        if got is None:
+            M = torch.stack([t.reshape(-1) for t in dr], 1)
+            tab, inv = torch.unique(M, dim=0, return_inverse=True)
+            if tab.shape[0] <= 256:
+                got = (inv.to(torch.uint8).reshape(shape).contiguous(), tab.contiguous())
+            else:
+                got = (None, None)
+            del M, inv
+            st["_drude_lut"] = got
+        return got
 
     # ------------------------------------------------------------ fused CPML
     def fused_cpml_ok(self, scheme) -> bool:

@@ -184,3 +184,26 @@ def test_fused_matches_split_bitwise(gpu):
     for c in a.comps:
         scale = float(a.F[0][c].abs().max()) + 1e-30
         assert float((a.F[0][c] - b.F[0][c]).abs().max()) <= 1e-6 * scale
+
+
+def test_drude_lut_bitwise(gpu):
+    """The Drude chain's material-ID + LUT coefficients (one byte per cell)
+    give bit-identical fields to the five per-cell coefficient arrays, and
+    the scene really compresses (a handful of tuples)."""
+    cfg = SchemeConfig(scheme="3d", size=(48, 40, 64), time_steps=10, use_pml=True, use_metamaterials=True,
+                       pml_size=(5, 5, 6), scene="drude-sphere", sphere_radius=10,
+                       sphere_center=(24.0, 20.0, 32.0), dtype="f32")
+    res = []
+    for lut in (True, False):
+        s = YeeScheme(cfg, make_ops("hip", None, gpu, torch.float32))
+        s.ops.drude_lut = lut
+        s.init_scheme()
+        s.init_grids()
+        s.perform_steps()
+        torch.cuda.synchronize()
+        if lut:
+            ids, tab = s.upml["Ez"]["_drude_lut"]
+            assert ids is not None and ids.dtype == torch.uint8 and 2 <= tab.shape[0] <= 8
+        res.append({c: s.F[0][c].cpu() for c in s.comps})
+    for c in res[0]:
+        assert torch.equal(res[0][c], res[1][c]), c
