@@ -335,6 +335,14 @@ class YeeScheme(BlockedStepping):
             self.graph_mode = False
         self.hybrid = None
         self._init_hybrid()
+        if (self.hybrid is None and cfg.scheme == "3d" and self.ops.name == "hip"
+                and getattr(self, "chain_regions", None) is not None and getattr(self, "_chain_prof", None) is not None):
+            # stepped 3D runs: the z PML slabs' chain boxes widened to whole
+            # 128-byte row segments (their 10-cell rows read a third of each
+            # line; the widened cells have sigma = 0, where the chain is the
+            # plain update algebraically).  Hybrid runs keep the exact slabs:
+            # their core must stay clear of every chain box.
+            self._init_chain_regions(self._chain_prof, z_align=128 // self.dtype.itemsize)
         self.initialized = True
         self.timers["init"] = time.perf_counter() - t0
 
@@ -487,7 +495,7 @@ class YeeScheme(BlockedStepping):
             hi.append(int(nzv.max()) + 1)
         return self.domain.to_global((tuple(lo), tuple(hi)))
 
-    def _init_chain_regions(self, prof) -> None:
+    def _init_chain_regions(self, prof, z_align: int = 1) -> None:
         """Region-local UPML/Drude chain (3D and 2D).  Where all sigma values
         of a component vanish and its Drude parameters are zero the chain is
         algebraically the plain Yee update (D' - D = (dt/dx) curl, E = D/(eps eps0)
@@ -496,6 +504,8 @@ class YeeScheme(BlockedStepping):
         (fused chain kernel): 6 PML slabs + the dispersive bounding box.  D / D1
         are only ever read in the chain boxes, which are static."""
         self.chain_regions = None
+        self._chain_prof = prof
+        self.__dict__.pop("_chain_plan_cache", None)
         if self.cfg.scheme == "1d":
             return
         cfg = self.cfg
@@ -515,6 +525,10 @@ class YeeScheme(BlockedStepping):
                     continue
                 zl, zh = int(zero.min()), int(zero.max()) + 1
                 fdtd_assert(bool((sv[zl:zh] == 0.0).all()), "sigma profile is not zero on one contiguous range")
+                if a == 2 and z_align > 1:
+                    # local z index rounded inward to whole row segments
+                    zl = -(-zl // z_align) * z_align
+                    zh = max(zl, zh // z_align * z_align)
                 lo[a] = max(lo[a], zl + dom.origin[a])
                 hi[a] = min(hi[a], zh + dom.origin[a])
             I = box_intersect(C, (tuple(lo), tuple(hi)))
