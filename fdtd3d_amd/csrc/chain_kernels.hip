@@ -51,16 +51,34 @@ struct ChainComp {
   const T* ma2;
   const unsigned char* id;  // Drude material index per cell (null: the five per-cell arrays)
   const T* lut;             // id -> (b0, b1, b2, ma1, ma2)
+  const T* pcell;           // plain part: per-cell (scaled) update coefficient, or null
   T s;
+  T pcb;                    // plain part: scalar update coefficient
   int a0, a1, sg0, sg1, aD, aA, aB;
   Box3 box;
+  Box3 pbox;                // plain Yee cells folded into this launch (empty: none)
 };
 
 template <typename T, bool DRUDE, bool CELL>
 __device__ __forceinline__ void chain_cell(const ChainComp<T>& q, bool kind_e, const long long* stride,
                                            const int* n, size_t off) {
-  if (!in_box(q.box, n[0], n[1], n[2])) return;
   const long long s0 = stride[q.a0], s1 = stride[q.a1];
+  if (!in_box(q.box, n[0], n[1], n[2])) {
+    // plain Yee cells of a thin box folded into the launch (the rows a z PML
+    // slab shares with the shell window next to it: one pass over whole
+    // 128-byte row segments instead of two partial ones).  Same expression
+    // as the float4 plain kernels: F + c * (d0 - d1).
+    if (!in_box(q.pbox, n[0], n[1], n[2])) return;
+    const T x0 = q.s0[off], x1 = q.s1[off];
+    const T y0 = kind_e ? q.s0[off - s0] : q.s0[off + s0];
+    const T y1 = kind_e ? q.s1[off - s1] : q.s1[off + s1];
+    const T c = q.pcell ? q.pcell[off] : q.pcb;
+    const T d0 = kind_e ? (x0 - y0) : (y0 - x0);
+    const T d1 = kind_e ? (x1 - y1) : (y1 - x1);
+    const T curl = (q.sg0 > 0 ? d0 : -d0) + (q.sg1 > 0 ? d1 : -d1);
+    q.E[off] = q.E[off] + c * curl;
+    return;
+  }
   // ---- every load first
   const T x0 = q.s0[off], x1 = q.s1[off];
   const T y0 = kind_e ? q.s0[off - s0] : q.s0[off + s0];
@@ -139,8 +157,8 @@ __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q
   }
 }
 
-constexpr int CP_PER = 23;  // pointers per component
-constexpr int CI_PER = 13;  // ints per component
+constexpr int CP_PER = 24;  // pointers per component
+constexpr int CI_PER = 19;  // ints per component
 
 template <typename T>
 ChainComp<T> make_comp(const void* const* P, double s, const int* I) {
@@ -168,6 +186,7 @@ ChainComp<T> make_comp(const void* const* P, double s, const int* I) {
   q.ma2 = (const T*)P[20];
   q.id = (const unsigned char*)P[21];
   q.lut = (const T*)P[22];
+  q.pcell = (const T*)P[23];
   q.s = (T)s;
   q.a0 = I[0];
   q.a1 = I[1];
@@ -177,6 +196,7 @@ ChainComp<T> make_comp(const void* const* P, double s, const int* I) {
   q.aA = I[5];
   q.aB = I[6];
   q.box = make_box(I + 7);
+  q.pbox = make_box(I + 13);
   return q;
 }
 
@@ -187,9 +207,11 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
   Box3 U = {{0, 0, 0}, {0, 0, 0}};
   bool cell = false;
   for (int c = 0; c < 3; ++c) {
-    q[c] = make_comp<T>(P + CP_PER * c, S[c], I + CI_PER * c);
+    q[c] = make_comp<T>(P + CP_PER * c, S[2 * c], I + CI_PER * c);
+    q[c].pcb = (T)S[2 * c + 1];
     if (!box_empty(q[c].box)) cell = cell || q[c].cell != nullptr;
     U = box_union(U, q[c].box);
+    U = box_union(U, q[c].pbox);
   }
   if (box_empty(U)) return 0;
   for (int c = 0; c < 3; ++c)
@@ -211,9 +233,11 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
 }  // namespace
 
 // One chain launch for the three components of a kind.  Per component c:
-// P[23c ..] = E Dn D Dp D1n D1 D1p s0 s1 caD cbD caE ica cbEa ccEa cell b0 b1 b2 ma1 ma2 id lut
-// (unused: nullptr; a non-null id replaces b0 .. ma2 by lut[5 id ..]), S[c] = scalar of the E-from-D term, I[13c ..] = curl axes
-// a0 a1, signs sg0 sg1, UPML axes aD aCa aCb, box lo[3] hi[3] (empty: skipped).
+// P[24c ..] = E Dn D Dp D1n D1 D1p s0 s1 caD cbD caE ica cbEa ccEa cell b0 b1 b2 ma1 ma2 id lut pcell
+// (unused: nullptr; a non-null id replaces b0 .. ma2 by lut[5 id ..]), S[2c] = scalar of the
+// E-from-D term, S[2c + 1] = plain-part coefficient, I[19c ..] = curl axes a0 a1, signs sg0
+// sg1, UPML axes aD aCa aCb, chain box lo[3] hi[3], plain box lo[3] hi[3] (empty: skipped;
+// the plain box holds cells updated F += c (curl) in the same launch).
 FDTD_API int fdtd_chain3d_f32(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny,
                               int nz, void* s) {
   return launch_chain<float>(P, S, I, drude, kind_e, ny, nz, (hipStream_t)s);

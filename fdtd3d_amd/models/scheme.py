@@ -720,15 +720,20 @@ class YeeScheme(BlockedStepping):
             plan = cache[key] = self._chain_plan(kind, w, pws)
         for boxes in plan["plain"]:
             self.ops.curl_update(kind, boxes, F, F, self.cb)
-            if tfsf and tfsf_plain:
+        for launches, slow in plan["chain"]:
+            for sel, form, plain_form, fold in launches:
+                if fold is None:
+                    self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form)
+                else:
+                    self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form, plain=fold, cb=self.cb)
+            for c, b in slow:
+                self._upml_region(kind, c, p, b)
+        if tfsf and tfsf_plain:
+            # corrections on every plain box (folded ones included), after all updates
+            for boxes in plan["plain"] + plan["folded"]:
                 for c in comps:
                     for tab in self.tfsf[c]:
                         self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
-        for launches, slow in plan["chain"]:
-            for sel, form, plain_form in launches:
-                self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form)
-            for c, b in slow:
-                self._upml_region(kind, c, p, b)
 
     def _chain_plan(self, kind: str, w: Optional[Box], pws) -> dict:
         """Launches of one UPML/Drude step on window ``w`` (plain slabs cut to
@@ -770,9 +775,41 @@ class YeeScheme(BlockedStepping):
             for form in (True, False):
                 sel = {c: (fast[c] if dru[c] == form else (fast[c][0], fast[c][0])) for c in comps}
                 if any(not box_empty(b) for b in sel.values()):
-                    launches.append((sel, form, self.cfg.use_metamaterials and not form))
+                    launches.append([sel, form, self.cfg.use_metamaterials and not form, None])
             chain.append((launches, slow))
-        return {"plain": plain, "chain": chain}
+        folded = []
+        if self.cfg.scheme == "3d" and getattr(self.ops, "chain_fold", False):
+            # a thin plain box on the z side of a non-dispersive chain box with
+            # the same or a narrower (x, y) footprint rides in that chain
+            # launch: the rows a z PML slab shares with a shell window are
+            # read once, whole
+            def fits(pb, cbx):
+                if box_empty(pb):
+                    return True
+                if box_empty(cbx) or pb[1][2] - pb[0][2] > 64:
+                    return False
+                if any(pb[0][d] < cbx[0][d] or pb[1][d] > cbx[1][d] for d in (0, 1)):
+                    return False
+                return pb[0][2] == cbx[1][2] or pb[1][2] == cbx[0][2]
+
+            keep = []
+            for boxes in plain:
+                host = None
+                for launches, _ in chain:
+                    for L in launches:
+                        if L[3] is None and not L[1] and all(fits(boxes[c], L[0][c]) for c in comps):
+                            host = L
+                            break
+                    if host is not None:
+                        break
+                if host is None:
+                    keep.append(boxes)
+                else:
+                    host[3] = {c: b for c, b in boxes.items() if not box_empty(b)}
+                    folded.append(boxes)
+            plain = keep
+        chain = [([tuple(L) for L in launches], slow) for launches, slow in chain]
+        return {"plain": plain, "chain": chain, "folded": folded}
 
     def _upml_region(self, kind: str, c: str, p: int, box: Box) -> None:
         F = self.F[p]

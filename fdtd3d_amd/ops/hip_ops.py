@@ -813,7 +813,8 @@ class HipOps:
 
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
-                     p: int, drude: bool, plain_form: bool = False) -> None:
+                     p: int, drude: bool, plain_form: bool = False, plain: Optional[Dict[str, Box]] = None,
+                     cb: Optional[Dict[str, Coef]] = None) -> None:
         """Fused UPML/Drude chain (chain_kernels.hip) of the three components
         of a kind (one launch).  ``upml[c]`` holds the factored coefficient
         profiles (``prof``), the Drude cell coefficients and the D / D1 level
@@ -862,9 +863,20 @@ class HipOps:
                     self._check_tensor(t, shape)
                 if self.drude_lut:
                     lut = self._drude_lut(st, dr, shape)
-            P += [None if t is None else t.data_ptr() for t in fields + profs + [cell] + dr + list(lut)]
-            S.append(float(pr["s"]))
-            I += [terms[0][1], terms[1][1], terms[0][2], terms[1][2], aD, aA, aB] + list(b[0]) + list(b[1])
+            # plain Yee cells folded into the launch (F += c curl; c scalar or scaled per cell)
+            pb = plain.get(c, ((0, 0, 0), (0, 0, 0))) if plain else ((0, 0, 0), (0, 0, 0))
+            pcell, pcb = None, 1.0
+            if not _empty(pb):
+                any_box = True
+                self._check_stencil_box(kind, c, pb, shape)
+                if self._cell_or_none(cb[c]) is not None:
+                    pcell = self._scaled_cell(cb[c])
+                else:
+                    pcb = float(cb[c].scalar)
+            P += [None if t is None else t.data_ptr() for t in fields + profs + [cell] + dr + list(lut) + [pcell]]
+            S += [float(pr["s"]), pcb]
+            I += ([terms[0][1], terms[1][1], terms[0][2], terms[1][2], aD, aA, aB] + list(b[0]) + list(b[1])
+                  + list(pb[0]) + list(pb[1]))
         if not any_box:
             return
         rc = self.fn("chain3d")((c_vp * len(P))(*P), (c_double * len(S))(*S), (c_int * len(I))(*I),
@@ -874,6 +886,7 @@ class HipOps:
         self.launches += 1
 
     drude_lut = True  # Drude chain: uint8 material index + coefficient table (falls back past 256 tuples)
+    chain_fold = True  # thin plain boxes next to a z PML slab ride in the slab's chain launch
 
     def _drude_lut(self, st: dict, dr, shape):
         """(uint8 id array, (n, 5) table) of a component's five Drude

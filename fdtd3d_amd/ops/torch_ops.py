@@ -146,10 +146,17 @@ class TorchOps:
                 sp = tuple(slice(s.start + 1, s.stop + 1) for s in sl)
                 fout[c][sl] = cur[c][sp]
 
+    chain_fold = True
+
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
-                     p: int, drude: bool, plain_form: bool = False) -> None:
+                     p: int, drude: bool, plain_form: bool = False, plain: Optional[Dict[str, Box]] = None,
+                     cb: Optional[Dict[str, Coef]] = None) -> None:
         """Reference semantics of the fused UPML/Drude chain kernel
-        (chain_kernels.hip): D -> [D1] -> E per cell of each box."""
+        (chain_kernels.hip): D -> [D1] -> E per cell of each box, plus the
+        plain Yee update on the folded ``plain`` boxes."""
+        if plain:
+            pb = {c: plain.get(c, ((0, 0, 0), (0, 0, 0))) for c in boxes}
+            self.curl_update(kind, pb, F, F, cb)
         for c, box in boxes.items():
             if _empty(box):
                 continue
