@@ -133,19 +133,55 @@ __global__ __launch_bounds__(256) void k_box_xfer(FieldPtrs<T> src, FieldPtrs<T>
   }
 }
 
+// Unaligned z range on rows of whole 16-byte vectors: aligned vector loads
+// over the covering groups, element stores only inside [lo, hi) (the cells
+// next to the box belong to someone else's output).
+template <typename T>
+__global__ __launch_bounds__(256) void k_box_xfer_m(FieldPtrs<T> src, FieldPtrs<T> dst, int ny, int nz, Box3 b) {
+  constexpr int V = 16 / sizeof(T);
+  typedef T VT __attribute__((ext_vector_type(V)));
+  const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1];
+  const int z0 = b.lo[2] & ~(V - 1);
+  const int ng = (b.hi[2] - z0 + V - 1) / V;  // vector groups per row
+  const int ci = blockIdx.z;
+  const int c = ci / bx, i = ci - c * bx;
+  const T* __restrict__ f = src.p[c];
+  T* __restrict__ g = dst.p[c];
+  const int nyzv = by * ng;
+  const size_t fplane = (size_t)(b.lo[0] + i) * ny;
+  for (int jk = blockIdx.x * 256 + threadIdx.x; jk < nyzv; jk += gridDim.x * 256) {
+    const int j = jk / ng, q = jk - j * ng;
+    const int k = z0 + q * V;
+    const size_t off = (fplane + (b.lo[1] + j)) * nz + k;
+    const VT v = *reinterpret_cast<const VT*>(f + off);
+    if (k >= b.lo[2] && k + V <= b.hi[2]) {
+      *reinterpret_cast<VT*>(g + off) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (k + e >= b.lo[2] && k + e < b.hi[2]) g[off + e] = v[e];
+    }
+  }
+}
+
 template <typename T>
 int launch_box_xfer(T* const* src, T* const* dst, int ncomp, int ny, int nz, const Box3& b, hipStream_t s) {
   FieldPtrs<T> fs, fd;
   constexpr int VW = 16 / sizeof(T);
   bool vec = (b.hi[2] - b.lo[2]) % VW == 0 && b.lo[2] % VW == 0 && nz % VW == 0;
+  bool vrow = nz % VW == 0;  // rows of whole vectors: masked vector path for unaligned boxes
   for (int c = 0; c < ncomp; ++c) {
     fs.p[c] = src[c];
     fd.p[c] = dst[c];
-    vec = vec && ((uintptr_t)src[c] & 15) == 0 && ((uintptr_t)dst[c] & 15) == 0;
+    const bool al = ((uintptr_t)src[c] & 15) == 0 && ((uintptr_t)dst[c] & 15) == 0;
+    vec = vec && al;
+    vrow = vrow && al;
   }
   if ((long long)(b.hi[0] - b.lo[0]) * ncomp > 65535) return (int)hipErrorInvalidValue;
   if (vec)
     k_box_xfer<T, VW><<<box_copy_grid(b, ncomp, VW), 256, 0, s>>>(fs, fd, ny, nz, b);
+  else if (vrow)
+    k_box_xfer_m<T><<<box_copy_grid(b, ncomp, VW), 256, 0, s>>>(fs, fd, ny, nz, b);
   else
     k_box_xfer<T, 1><<<box_copy_grid(b, ncomp, 1), 256, 0, s>>>(fs, fd, ny, nz, b);
   FDTD_RETURN_LAUNCH_STATUS();

@@ -153,10 +153,12 @@ class BlockedStepping:
         plan = self._hybrid_plan(H)
         if plan is None:
             return
-        if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.03 * self.cells():
-            # automatic mode: a large dispersive box splits the core into six
-            # slabs and moves its surroundings into the stepped shell -- slower
-            # than stepping everything (512^3 Drude sphere r=128: 37.8k vs 42k)
+        if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.5 * self.cells():
+            # automatic mode: a dispersive box over half the grid leaves too
+            # little core.  (512^3 Drude sphere r=128, the box an eighth of
+            # the grid: hybrid 51.7k vs stepped 45.7k Mcells/s once the Drude
+            # chain reads its coefficients through the material LUT; 37.8k vs
+            # 42k before)
             return
         if not hasattr(self, "F_alt"):
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]

@@ -43,3 +43,26 @@ def test_pack_unpack_vs_torch(gpu, dtype, box, buf_off):
         m = torch.ones(SHAPE, dtype=torch.bool, device=gpu)
         m[sl] = False
         assert float(d[m].abs().max()) == 0.0 if m.any() else True
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("box", [((1, 2, 0), (9, 11, 24)),      # aligned z: vector path
+                                 ((0, 3, 5), (7, 12, 18)),      # unaligned both ends: masked vectors
+                                 ((2, 0, 3), (5, 13, 4)),       # one cell in z
+                                 ((0, 0, 1), (10, 13, 23))])
+def test_copy_box_vs_torch(gpu, dtype, box):
+    """ops.copy_box (k_box_xfer / k_box_xfer_m): only the box changes, every
+    component pair."""
+    ops = make_ops("hip", None, gpu, dtype)
+    shape = (10, 13, 24)
+    g = torch.Generator().manual_seed(3)
+    src = [torch.rand(shape, generator=g, dtype=torch.float64).to(dtype).to(gpu) for _ in range(6)]
+    dst = [torch.rand(shape, generator=g, dtype=torch.float64).to(dtype).to(gpu) for _ in range(6)]
+    want = [d.clone() for d in dst]
+    sl = tuple(slice(box[0][d], box[1][d]) for d in range(3))
+    for a, b in zip(src, want):
+        b[sl] = a[sl]
+    ops.copy_box(src, dst, box)
+    torch.cuda.synchronize()
+    for a, b in zip(dst, want):
+        assert torch.equal(a, b)
