@@ -182,6 +182,9 @@ def _layer(entries, device, dtype) -> List[TfsfTable]:
         # host-side bounds of the table (checked by the HIP op without a device sync)
         tab.max_off = int(flat[sel].max()) if sel.any() else -1
         tab.max_inc = int(i0[sel].max()) + 1 if sel.any() else -1
+        if sel.any():  # targets' bounding box (lets the op skip the per-entry box test)
+            v = ijk[sel].reshape(-1, 3)
+            tab.bbox = (tuple(int(x) for x in v.min(0)), tuple(int(x) + 1 for x in v.max(0)))
         layers.append(tab)
     return layers
 

@@ -574,11 +574,8 @@ class HipOps:
             table.max_inc = int(table.i0.max()) + 1
         if max_off >= target.numel() or table.max_inc >= inc.numel():
             raise HipError("TF/SF table reads or writes outside its arrays")
-        bb = getattr(table, "bbox", None)
-        if bb is None:  # targets' bounding box: one (syncing) reduction, then cached
-            v = table.ijk.view(-1, 3)
-            table.bbox = bb = (tuple(int(x) for x in v.min(0).values), tuple(int(x) + 1 for x in v.max(0).values))
-        whole = all(box[0][d] <= bb[0][d] and bb[1][d] <= box[1][d] for d in range(3))
+        bb = getattr(table, "bbox", None)  # host-side, set where the table is built (no sync under capture)
+        whole = bb is not None and all(box[0][d] <= bb[0][d] and bb[1][d] <= box[1][d] for d in range(3))
         rc = self.fn("tfsf_apply")(_ptr(target), _ptr(table.off), _ptr(table.i0), _ptr(table.w0), _ptr(table.w1),
                                    _ptr(table.coef), None if whole else _ptr(table.ijk), c_int(table.n), _ptr(inc),
                                    _box_arr([box]), _stream())

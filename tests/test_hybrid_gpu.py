@@ -112,3 +112,42 @@ def test_hybrid2_random_fields(gpu, T, tfsf):
             err = float((a.psi[0].double() - b.psi[0].double()).abs().max())
             assert err <= 2e-5 * src_scale, (c, "psi", err, src_scale)
         assert max(float(b.psi[0].abs().max()) for b in st.cpml.slabs[c]) > 1e-3 * src_scale  # psi is live
+
+
+SCALE_CASES = [
+    ("cpml-tfsf-256", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True)),
+    ("upml-tfsf-256", dict(scene="vacuum", use_pml=True, use_tfsf=True)),
+    ("drude-256", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, sphere_center=(128.0, 128.0, 128.0),
+                       sphere_radius=64)),
+]
+
+
+@pytest.mark.parametrize("name,extra", SCALE_CASES, ids=[c[0] for c in SCALE_CASES])
+def test_hybrid_at_scale(gpu, name, extra):
+    """Bench-like configs at 256^3 (reference PML / TF-SF sizes, automatic
+    hybrid plan and T, random-init fields): two hybrid passes + one step
+    equal the stepped run of the same kernels.  (The fp64 torch oracle is
+    checked on the small cases above; at this size it would take minutes on
+    the CPU.)"""
+    cfg = SchemeConfig(scheme="3d", size=(256, 256, 256), time_steps=9, dtype="f32", **extra)
+    runs = []
+    for hb in (0, 1):
+        s = YeeScheme(dataclasses.replace(cfg, hybrid_block=hb), make_ops("hip", None, gpu, torch.float32))
+        s.init_scheme()
+        s.init_grids()
+        s.randomize_fields(seed=7)
+        if hb == 0:
+            assert s.hybrid is not None, "automatic hybrid plan rejected"
+        else:
+            assert s.hybrid is None
+        s.perform_steps()
+        torch.cuda.synchronize()
+        runs.append(s)
+    hy, st = runs
+    for c in hy.comps:
+        scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0]) + 1e-30
+        err = float((hy.F[0][c] - st.F[0][c]).abs().max())
+        assert err <= 2e-5 * scale, (name, c, err, scale)
+        del scale
+    del runs, hy, st
+    torch.cuda.empty_cache()
