@@ -116,6 +116,54 @@ __global__ void k_tfsf_apply(T* __restrict__ target, const long long* __restrict
   target[off[e]] += coef[e] * (w0[e] * inc[p] + w1[e] * inc[p + 1]);
 }
 
+// Scattered field of a TF/SF run (Scheme3D.cpp:2593-2747): inside the TF box
+// the total field minus the incident plane wave, interpolated from the 1D
+// line at the component's position (fp64 position and weights, the same
+// expression as io/dump.py's torch path), outside the box the field itself.
+struct ScatGeom {
+  double m[3];     // component offset inside the cell (MIN_COORD_FP)
+  double zero[3];  // incident line origin
+  double dir[3];   // propagation direction
+  double L[3], R[3];
+  double proj;     // the component's share of the incident wave
+  double shift;    // 0.5 for H (the line's H points sit half a cell later)
+  int org[3];      // global index of local cell 0
+  int act;         // bit a: axis a bounds the TF box
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_scattered(const T* __restrict__ f, T* __restrict__ out,
+                                                   const T* __restrict__ line, int nline, int nx, int ny, int nz,
+                                                   ScatGeom g) {
+  const long long n = (long long)nx * ny * nz;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(t % nz);
+    const long long r = t / nz;
+    const int j = (int)(r % ny);
+    const int i = (int)(r / ny);
+    const double x = i + g.org[0] + g.m[0], y = j + g.org[1] + g.m[1], z = k + g.org[2] + g.m[2];
+    bool inside = true;
+    if (g.act & 1) inside = inside && x > g.L[0] && x < g.R[0];
+    if (g.act & 2) inside = inside && y > g.L[1] && y < g.R[1];
+    if (g.act & 4) inside = inside && z > g.L[2] && z < g.R[2];
+    const T v = f[t];
+    if (!inside) {
+      out[t] = v;
+      continue;
+    }
+    // explicitly rounded operations (no FMA contraction): the same value as
+    // the torch expression, so the interpolation index never flips
+    double d = __dadd_rn(__dadd_rn(__dmul_rn(x - g.zero[0], g.dir[0]), __dmul_rn(y - g.zero[1], g.dir[1])),
+                         __dmul_rn(z - g.zero[2], g.dir[2]));
+    d = d - g.shift;
+    long long i0 = (long long)floor(d);
+    i0 = i0 < 0 ? 0 : (i0 > nline - 2 ? nline - 2 : i0);
+    const double w1 = d - (double)i0;
+    const double li = __dadd_rn(__dmul_rn(1.0 - w1, (double)line[i0]), __dmul_rn(w1, (double)line[i0 + 1]));
+    out[t] = v - (T)__dmul_rn(li, g.proj);
+  }
+}
+
 // 1D incident line (Scheme3D.cpp:25-82)
 template <typename T>
 __global__ void k_inc_e(T* __restrict__ einc, const T* __restrict__ hinc, int n, T c, double src) {
@@ -203,6 +251,28 @@ inline dim3 cell_grid(const Box3& b) {
     Box3 b = make_box(box);                                                                                   \
     if (n <= 0 || box_empty(b)) return 0;                                                                     \
     k_tfsf_apply<T><<<cdiv(n, 256), 256, 0, (hipStream_t)s>>>(target, off, i0, w0, w1, coef, ijk, n, inc, b);  \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_scattered_##SUF(const T* f, T* out, const T* line, int nline, int nx, int ny, int nz,      \
+                                    const double* geo, const int* igeo, void* s) {                            \
+    ScatGeom g;                                                                                               \
+    for (int a = 0; a < 3; ++a) {                                                                             \
+      g.m[a] = geo[a];                                                                                        \
+      g.zero[a] = geo[3 + a];                                                                                 \
+      g.dir[a] = geo[6 + a];                                                                                  \
+      g.L[a] = geo[9 + a];                                                                                    \
+      g.R[a] = geo[12 + a];                                                                                   \
+      g.org[a] = igeo[a];                                                                                     \
+    }                                                                                                         \
+    g.proj = geo[15];                                                                                         \
+    g.shift = geo[16];                                                                                        \
+    g.act = igeo[3];                                                                                          \
+    const long long n = (long long)nx * ny * nz;                                                              \
+    if (n <= 0) return 0;                                                                                     \
+    if (nline < 2) return (int)hipErrorInvalidValue;                                                          \
+    const long long blocks = (n + 255) / 256;                                                                 \
+    k_scattered<T><<<(unsigned)(blocks < 65536 ? blocks : 65536), 256, 0, (hipStream_t)s>>>(f, out, line, nline, \
+                                                                                            nx, ny, nz, g);   \
     FDTD_RETURN_LAUNCH_STATUS();                                                                              \
   }                                                                                                           \
   FDTD_API int fdtd_inc_e_##SUF(T* einc, const T* hinc, int n, double c, double src, void* s) {               \

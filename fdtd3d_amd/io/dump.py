@@ -64,11 +64,29 @@ def incident_field(scheme, comp: str, plane: int = 0) -> Optional[torch.Tensor]:
 
 def scattered_field(scheme, comp: str, plane: int = 0) -> torch.Tensor:
     """Total field minus the incident field inside the TF box (outside it the
-    grid already holds the scattered field) -- ``Scheme3D.cpp:2593-2747``."""
+    grid already holds the scattered field) -- ``Scheme3D.cpp:2593-2747``.
+    HIP: one kernel pass (``ops.scattered``); torch: the expression below."""
+    f = scheme.F[plane][comp]
+    if not scheme.cfg.use_tfsf:
+        return f
+    if hasattr(scheme.ops, "scattered"):
+        lay = scheme.layout
+        L, R = lay.tfsf_borders()
+        act = 0
+        for a in lay.axes:
+            act |= 1 << a
+        geo = (list(MIN_COORD_FP[comp]) + list(lay.zero_inc_coord_fp()) + list(lay.incident_direction())
+               + [float(v) for v in L] + [float(v) for v in R]
+               + [float(lay.incident_projection(comp)), 0.5 if comp[0] == "H" else 0.0])
+        line = scheme.einc[plane] if comp[0] == "E" else scheme.hinc[plane]
+        return scheme.ops.scattered(f, line, geo, list(scheme.domain.origin) + [act])
+    return scattered_field_torch(scheme, comp, plane)
+
+
+def scattered_field_torch(scheme, comp: str, plane: int = 0) -> torch.Tensor:
+    """Torch expression of :func:`scattered_field` (any backend / device)."""
     f = scheme.F[plane][comp]
     inc = incident_field(scheme, comp, plane)
-    if inc is None:
-        return f
     L, R = scheme.layout.tfsf_borders()
     m = MIN_COORD_FP[comp]
     o = scheme.domain.origin

@@ -582,6 +582,20 @@ class HipOps:
         _check(rc, "tfsf_apply")
         self.launches += 1
 
+    def scattered(self, f: torch.Tensor, line: torch.Tensor, geo: Sequence[float], igeo: Sequence[int]) -> torch.Tensor:
+        """Scattered field of a TF/SF run in one pass (generic_kernels.hip
+        k_scattered): ``geo`` = m[3] zero[3] dir[3] L[3] R[3] proj shift,
+        ``igeo`` = origin[3] active-axis bits."""
+        self._check_tensor(f)
+        self._check_tensor(line)
+        out = torch.empty_like(f)
+        s = f.shape
+        rc = self.fn("scattered")(_ptr(f), _ptr(out), _ptr(line), c_int(line.numel()), c_int(s[0]), c_int(s[1]),
+                                  c_int(s[2]), (c_double * 17)(*geo), (c_int * 4)(*igeo), _stream())
+        _check(rc, "scattered")
+        self.launches += 1
+        return out
+
     # ------------------------------------------------------ temporal blocking
     tfsf_sets_ok = True  # the fp32 blocked kernel applies TfsfSets corrections
 
