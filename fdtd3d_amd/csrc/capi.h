@@ -22,6 +22,17 @@ int fdtd_update_h3d_f64(double* hx, double* hy, double* hz, const double* ex, co
 int fdtd_update_e3d_v4_f32(float* ex, float* ey, float* ez, const float* hx, const float* hy, const float* hz,
                            const float* cbx, const float* cby, const float* cbz, double cb, int nx, int ny, int nz,
                            const int* boxes, int xchunk, void* stream);
+// float4 split E / H updates with the CPML convolution terms folded in
+// (yee3d_cpml.hip): cp = 9 x {psi_lo, psi_hi, b, c, 1/kappa - 1} per
+// (component, axis), ci = 9 x {lo0, hi0, lo1, hi1}
+int fdtd_update_e3d_cpml_v4_f32(float* ex, float* ey, float* ez, const float* hx, const float* hy, const float* hz,
+                                const float* cbx, const float* cby, const float* cbz, double cb, int nx, int ny,
+                                int nz, const int* boxes, int xchunk, const void* const* cp, const int* ci,
+                                void* stream);
+int fdtd_update_h3d_cpml_v4_f32(float* hx, float* hy, float* hz, const float* ex, const float* ey, const float* ez,
+                                const float* dbx, const float* dby, const float* dbz, double db, int nx, int ny,
+                                int nz, const int* boxes, int xchunk, const void* const* cp, const int* ci,
+                                void* stream);
 int fdtd_update_h3d_v4_f32(float* hx, float* hy, float* hz, const float* ex, const float* ey, const float* ez,
                            const float* dbx, const float* dby, const float* dbz, double db, int nx, int ny, int nz,
                            const int* boxes, int xchunk, void* stream);

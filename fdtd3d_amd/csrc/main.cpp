@@ -4,10 +4,11 @@
 //
 // Covers the plain Yee solvers (1D, 2D TMz/TEz, 3D) on one GPU with the
 // vacuum / dielectric-sphere scenes and the hard point source, fp32 or fp64,
-// fused or split 3D kernels, DAT/BMP output of the final fields.  Absorbing
-// layers, TF/SF, dispersive media, NTFF, amplitude mode and multi-GPU runs go
-// through the Python driver (python -m fdtd3d_amd), which shares the kernels;
-// asking this binary for them is an error, never a silent fallback.
+// fused or split 3D kernels, CPML absorbing layers in 3D fp32 (--use-pml
+// --pml-type cpml), DAT/BMP output of the final fields.  UPML, TF/SF,
+// dispersive media, NTFF, amplitude mode and multi-GPU runs go through the
+// Python driver (python -m fdtd3d_amd), which shares the kernels; asking this
+// binary for them is an error, never a silent fallback.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -195,6 +196,106 @@ int h1d(double* a, const double* b, const double* c, double db, int lo, int hi, 
   return fdtd_1d_h_f64(a, b, c, db, lo, hi, s);
 }
 
+// CPML (3D, fp32 float4 kernels): profiles, psi slabs and the per-kind term
+// tables of yee3d_cpml.hip -- the same slabs and profiles as
+// fdtd3d_amd/models/cpml.py (polynomial grading m = 4, R = 1e-8, kappa and
+// alpha from --cpml-kappa-max / --cpml-alpha-max, each component's own
+// staggered position).
+struct NativeCpml {
+  std::vector<Dev<float>*> keep;       // psi slabs and profile arrays
+  std::vector<const void*> P[2];       // per kind (E, H): 9 x 5 pointers
+  std::vector<int> I[2];               // per kind: 9 x 4 ints
+  ~NativeCpml() {
+    for (auto* d : keep) delete d;
+  }
+  float* upload(const std::vector<float>& h) {
+    auto* d = new Dev<float>();
+    d->alloc(h.size());
+    HIP_OK(hipMemcpy(d->p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    keep.push_back(d);
+    return d->p;
+  }
+  float* zeros(size_t n) {
+    auto* d = new Dev<float>();
+    d->alloc(n);
+    keep.push_back(d);
+    return d->p;
+  }
+};
+
+void setup_cpml(NativeCpml& cp, const fdtd::Settings& s, const fdtd::Int3& N, const std::vector<int>& active,
+                double dt, double dx) {
+  // staggered offset of each component inside its cell (layout/yee.py MIN_COORD_FP)
+  static const double mco[6][3] = {{1.0, 0.5, 0.5}, {0.5, 1.0, 0.5}, {0.5, 0.5, 1.0},
+                                   {0.5, 1.0, 1.0}, {1.0, 0.5, 1.0}, {1.0, 1.0, 0.5}};
+  const int Ps[3] = {s.pmlSizeX, s.pmlSizeY, s.pmlSizeZ};
+  const double eta = std::sqrt(kMu0 / kEps0);
+  const double kmax = s.cpmlKappaMax, amax = s.cpmlAlphaMax;
+  for (int kind = 0; kind < 2; ++kind) {
+    cp.P[kind].assign(45, nullptr);
+    cp.I[kind].assign(36, 0);
+    for (int cc = 0; cc < 3; ++cc) {
+      const int c = 3 * kind + cc;
+      fdtd::Int3 glo, ghi;
+      fdtd::global_range(c, N, active, glo, ghi);
+      for (int a = 0; a < 3; ++a) {
+        // a component's two curl terms differentiate along the other two axes
+        const int P = Ps[a];
+        if (a == cc || P <= 0 || std::find(active.begin(), active.end(), a) == active.end()) continue;
+        const int n = N[a];
+        const double m = mco[c][a];
+        const double sig_max = -(4 + 1) * std::log(1e-8) / (2 * eta * P * dx);
+        std::vector<float> b(n, 1.f), cv(n, 0.f), kk(n, 0.f);
+        const void* psi[2] = {nullptr, nullptr};
+        int rng[2][2] = {{0, 0}, {0, 0}};
+        for (int side = 0; side < 2; ++side) {
+          int lo = glo[a], hi = ghi[a];
+          if (side == 0)
+            hi = std::min(hi, (int)std::ceil(P - m));
+          else
+            lo = std::max(lo, (int)std::floor(N[a] - P - m) + 1);
+          bool empty = hi <= lo;
+          for (int d = 0; d < 3; ++d) empty = empty || ghi[d] <= glo[d];
+          if (empty) continue;
+          if (a == 2 && N[2] % 4 == 0) {  // z slabs padded to whole float4 groups (c = 0 there)
+            lo &= ~3;
+            hi = std::min(N[2], (hi + 3) & ~3);
+          }
+          for (int v = lo; v < hi; ++v) {
+            const double idx = v + m;
+            double depth = side == 0 ? (P - idx) / P : (idx - (N[a] - P)) / P;
+            depth = std::min(1.0, std::max(0.0, depth));
+            const double d4 = depth * depth * depth * depth;
+            const double sig = sig_max * d4, kap = 1.0 + (kmax - 1.0) * d4, alp = amax * (1.0 - depth);
+            const double bc = std::exp(-(sig / kap + alp) * dt / kEps0);
+            const double den = sig * kap + kap * kap * alp;
+            b[v] = (float)bc;
+            cv[v] = (float)(den > 0 ? sig / den * (bc - 1.0) : 0.0);
+            kk[v] = (float)(1.0 / kap - 1.0);
+          }
+          // psi storage: the slab's range along a x the full extents of the other two
+          size_t vol = (size_t)(hi - lo);
+          for (int d = 0; d < 3; ++d)
+            if (d != a) vol *= (size_t)N[d];
+          psi[side] = cp.zeros(vol);
+          rng[side][0] = lo;
+          rng[side][1] = hi;
+        }
+        const int t = 3 * cc + a;
+        cp.P[kind][5 * t] = psi[0];
+        cp.P[kind][5 * t + 1] = psi[1];
+        cp.P[kind][5 * t + 2] = cp.upload(b);
+        cp.P[kind][5 * t + 3] = cp.upload(cv);
+        cp.P[kind][5 * t + 4] = cp.upload(kk);
+        cp.I[kind][4 * t] = rng[0][0];
+        cp.I[kind][4 * t + 1] = rng[0][1];
+        cp.I[kind][4 * t + 2] = rng[1][0];
+        cp.I[kind][4 * t + 3] = rng[1][1];
+      }
+    }
+  }
+}
+
 template <typename T>
 int run(const fdtd::Settings& s) {
   const int dim = s.dimension;
@@ -209,7 +310,9 @@ int run(const fdtd::Settings& s) {
   const bool v4 = sizeof(T) == 4 && N[2] % 4 == 0 && dim == 3;
   // fused / blocked / resident kernels unless --split-kernels (3D fused E+H
   // and blocked passes, 2D blocked passes, 1D one-launch resident run)
-  const bool use_fused = !s.doUseSplitKernels;
+  // CPML runs step through the float4 split kernels with the psi terms folded in
+  const bool cpml = s.doUsePML;
+  const bool use_fused = !s.doUseSplitKernels && !cpml;
   hipStream_t st;
   HIP_OK(hipStreamCreate(&st));
 
@@ -300,8 +403,8 @@ int run(const fdtd::Settings& s) {
     if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
     return std::sin(dt * t * 2 * kPi * freq);
   };
-  auto cp = [&](Dev<T>* A, int c) -> const T* { return A[c].p; };
-  (void)cp;
+  NativeCpml cpt;
+  if (cpml) setup_cpml(cpt, s, N, active, dt, dx);
 
   // one time step (t) through the configured kernels
   auto step = [&](int t) {
@@ -317,6 +420,16 @@ int run(const fdtd::Settings& s) {
         K_OK(fused(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, percell ? 1.0 : db, N[0], N[1], N[2], boxes,
                    src_off, src_comp, sv, st, v4));
         for (int c = 0; c < 6; ++c) std::swap(F[c].p, G[c].p);
+      } else if (cpml) {
+        if constexpr (sizeof(T) == 4) {
+          K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p,
+                                           percell ? 1.0 : cb, N[0], N[1], N[2], boxes, 0, cpt.P[0].data(),
+                                           cpt.I[0].data(), st));
+          K_OK(setv(F[src_comp].p, src_off, sv, st));
+          K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p,
+                                           percell ? 1.0 : db, N[0], N[1], N[2], boxes + 18, 0, cpt.P[1].data(),
+                                           cpt.I[1].data(), st));
+        }
       } else {
         K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, percell ? 1.0 : cb, N[0],
                  N[1], N[2], boxes, 0, st, v4));
@@ -450,6 +563,8 @@ int run(const fdtd::Settings& s) {
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", std::max(T_blk, T2_blk));
   else if (res1)
     std::printf("Backend: native HIP, register-resident 1D kernel (one launch per run)\n");
+  else if (cpml)
+    std::printf("Backend: native HIP, split float4 kernels with the CPML terms folded in\n");
   else
     std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
   std::printf("Throughput: %.1f Mcells/s\n", cells * (double)timed / sec / 1e6);
@@ -498,12 +613,16 @@ int main(int argc, char** argv) {
     std::fprintf(stdout, "ERROR: %s\n", s.message.c_str());
     return 1;
   }
-  if (s.doUsePML || s.doUseTFSF || s.doUseMetamaterials || s.doUseNTFF || s.doUseAmplitudeMode ||
+  // CPML absorbing layers: 3D fp32 with whole float4 z rows (the folded float4 kernels)
+  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && s.dimension == 3 && s.valueType == "f32" &&
+                       s.sizeZ % 4 == 0;
+  if ((s.doUsePML && !cpml_ok) || s.doUseTFSF || s.doUseMetamaterials || s.doUseNTFF || s.doUseAmplitudeMode ||
       s.doUseComplexFieldValues || s.doUseParallelGrid || s.doUseDoubleMaterialPrecision ||
       !s.loadFromFile.empty()) {
     std::fprintf(stderr,
-                 "fdtd3d (native): PML, TF/SF, metamaterials, NTFF, amplitude mode, complex fields, "
-                 "parallel grids and resume run through the Python driver: python -m fdtd3d_amd <same options>\n");
+                 "fdtd3d (native): UPML, CPML outside 3D fp32 float4 rows, TF/SF, metamaterials, NTFF, amplitude "
+                 "mode, complex fields, parallel grids and resume run through the Python driver: "
+                 "python -m fdtd3d_amd <same options>\n");
     return 2;
   }
   int ndev = 0;
