@@ -259,7 +259,20 @@ class BlockedStepping:
         cfg = self.cfg
         size = cfg.size
         alloc = dom.allocated_global()
-        m = T + 2  # core margin to every irregular cell (staggering slack included)
+        # core margin to every irregular cell: T + 1 clears the stencil reach
+        # of a T-step pass (checked below; T + 2 when a staggered component's
+        # irregular box sticks out one cell further)
+        for m in (T + 1, T + 2):
+            plan = self._hybrid_plan_m(T, m)
+            if plan is not None:
+                return plan
+        return None
+
+    def _hybrid_plan_m(self, T: int, m: int):
+        dom = self.domain
+        cfg = self.cfg
+        size = cfg.size
+        alloc = dom.allocated_global()
         # TF/SF faces stay in the stepped shell: the blocked kernel's TF/SF
         # variant runs at about half the plain kernel's rate
         # (profiles/tfsf_cpml_r2.md), more than the shell it would save
