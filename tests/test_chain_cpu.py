@@ -104,3 +104,49 @@ def test_lorentz_ade_static_limit():
         e_prev, e = e, e_new
     eps_s = eps + wp * wp / (w0 * w0)
     assert abs(e * EPS0 * eps_s - 1.0) < 1e-6, (e * EPS0 * eps_s)
+
+
+@pytest.mark.parametrize("w0_ratio", [0.0, 0.5])
+def test_ade_natural_modes_match_continuous_medium(w0_ratio):
+    """Analytic dispersive check of the ADE discretisation (no fixture in the
+    reference pins it).  With D held constant the recurrence of a dispersive
+    cell, x(n+1) = ma1 x(n) + ma2 x(n-1), must reproduce the continuous
+    medium's free response E'' + g E' + (wp^2/eps + w0^2) E = 0 (Drude: w0 = 0,
+    Lorentz): the roots r of r^2 - ma1 r - ma2 = 0 are exp(s dt) with
+    s = -g/2 +- i sqrt(wp^2/eps + w0^2 - g^2/4), to second order in the step.
+    The cell's coefficients come from the scheme (scheme.py _init_upml),
+    its wp / g / eps from the material sampler; a damping g is added if the
+    scene has none, with the same coefficient formulas."""
+    import cmath
+    import math
+    from fdtd3d_amd.utils.constants import EPS0
+    cfg = dataclasses.replace(CASES["drude-upml"], dispersion="lorentz" if w0_ratio else "drude",
+                              lorentz_omega0_ratio=w0_ratio)
+    s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+    s.init_scheme()
+    s.init_grids()
+    st = s.upml["Ez"]
+    nz = torch.nonzero(st["drude_active"])
+    idx = tuple(int(v) for v in nz[len(nz) // 2])
+    w, g = s.sampler.averaged_drude("Ez", electric=True)
+    eps = float(s.sampler.averaged("Ez", "eps")[idx])
+    wp, gam = float(w[idx]), float(g[idx])
+    dt = s.dt
+    w0 = w0_ratio * 2 * math.pi * s.source_frequency
+    m1, m2 = float(st["ma1"].cell[idx]), float(st["ma2"].cell[idx])
+    if gam == 0.0:
+        gam = 0.02 / dt
+        q = dt * dt * w0 * w0
+        A = 4 * EPS0 * eps + 2 * dt * EPS0 * eps * gam + EPS0 * (dt * dt * wp * wp + q * eps)
+        m1 = -(2 * EPS0 * (dt * dt * wp * wp + q * eps) - 8 * EPS0 * eps) / A
+        m2 = -(4 * EPS0 * eps - 2 * dt * EPS0 * eps * gam + EPS0 * (dt * dt * wp * wp + q * eps)) / A
+    wn2 = wp * wp / eps + w0 * w0
+    assert wn2 * dt * dt < 0.25, "step too coarse for the check"
+    disc = cmath.sqrt(m1 * m1 + 4 * m2)
+    r = (m1 + disc) / 2 if (m1 + disc).imag >= 0 else (m1 - disc) / 2
+    s_num = cmath.log(r) / dt
+    s_ana = complex(-gam / 2, math.sqrt(max(wn2 - gam * gam / 4, 0.0)))
+    # bilinear (trapezoidal) map: relative error O((|s| dt)^2)
+    tol = 0.05 * abs(s_ana) * dt * abs(s_ana) * dt + 1e-9
+    assert abs(s_num.imag - s_ana.imag) <= max(tol, 1e-3) * abs(s_ana), (s_num, s_ana)
+    assert abs(s_num.real - s_ana.real) <= max(tol, 1e-3) * abs(s_ana), (s_num, s_ana)
