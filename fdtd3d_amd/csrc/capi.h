@@ -33,6 +33,17 @@ int fdtd_update_h3d_cpml_v4_f32(float* hx, float* hy, float* hz, const float* ex
                                 const float* dbx, const float* dby, const float* dbz, double db, int nx, int ny,
                                 int nz, const int* boxes, int xchunk, const void* const* cp, const int* ci,
                                 void* stream);
+// TF/SF: 1D incident line steps and the table-driven corrections
+// (generic_kernels.hip; ijk may be null when the box holds every target)
+int fdtd_inc_e_f32(float* einc, const float* hinc, int n, double c, double src, void* stream);
+int fdtd_inc_e_f64(double* einc, const double* hinc, int n, double c, double src, void* stream);
+int fdtd_inc_h_f32(const float* einc, float* hinc, int n, double c, void* stream);
+int fdtd_inc_h_f64(const double* einc, double* hinc, int n, double c, void* stream);
+int fdtd_tfsf_apply_f32(float* target, const long long* off, const long long* i0, const float* w0, const float* w1,
+                        const float* coef, const int* ijk, int n, const float* inc, const int* box, void* stream);
+int fdtd_tfsf_apply_f64(double* target, const long long* off, const long long* i0, const double* w0,
+                        const double* w1, const double* coef, const int* ijk, int n, const double* inc,
+                        const int* box, void* stream);
 int fdtd_update_h3d_v4_f32(float* hx, float* hy, float* hz, const float* ex, const float* ey, const float* ez,
                            const float* dbx, const float* dby, const float* dbz, double db, int nx, int ny, int nz,
                            const int* boxes, int xchunk, void* stream);

@@ -5,8 +5,9 @@
 // Covers the plain Yee solvers (1D, 2D TMz/TEz, 3D) on one GPU with the
 // vacuum / dielectric-sphere scenes and the hard point source, fp32 or fp64,
 // fused or split 3D kernels, CPML absorbing layers in 3D fp32 (--use-pml
-// --pml-type cpml), DAT/BMP output of the final fields.  UPML, TF/SF,
-// dispersive media, NTFF, amplitude mode and multi-GPU runs go through the
+// --pml-type cpml) and TF/SF plane waves in 3D, DAT/BMP output of the final
+// fields.  UPML, 2D TF/SF, dispersive media, NTFF, amplitude mode and
+// multi-GPU runs go through the
 // Python driver (python -m fdtd3d_amd), which shares the kernels; asking this
 // binary for them is an error, never a silent fallback.
 #include <hip/hip_runtime.h>
@@ -296,6 +297,238 @@ void setup_cpml(NativeCpml& cp, const fdtd::Settings& s, const fdtd::Int3& N, co
   }
 }
 
+// ------------------------------------------------------------------ TF/SF
+// Plane-wave injection through a total-field / scattered-field box, 3D: the
+// 1D incident line (k_inc_e / k_inc_h) and per-component correction tables
+// applied after each half step (k_tfsf_apply) -- the tables of
+// fdtd3d_amd/models/tfsf.py build_tfsf_tables, built here on the host.
+
+// numerical phase velocity of a plane wave on the Yee grid (Taflove;
+// reference Approximation.cpp:212-269, layout/approximation.py)
+double phase_velocity_3d(double delta, double wl, double courant, double nl, double theta, double phi) {
+  const double half = kPi / 2;
+  if (theta == half && (phi == 0.0 || phi == half || phi == kPi || phi == 3 * half))
+    return kC * kPi / (nl * std::asin(std::sin(kPi * courant / nl) / courant));
+  if (theta == half && (phi == kPi / 4 || phi == 3 * kPi / 4 || phi == 5 * kPi / 4 || phi == 7 * kPi / 4)) {
+    const double s2 = std::sqrt(2.0);
+    return kC * kPi / (nl * s2 * std::asin(std::sin(kPi * courant / nl) / (courant * s2)));
+  }
+  const double acc = 1e-7;  // Approximation.cpp:7
+  double k = 2 * kPi, kp = k + acc;
+  const double nd = delta / wl;
+  const double A = nd * std::sin(theta) * std::cos(phi) / 2, B = nd * std::sin(theta) * std::sin(phi) / 2;
+  const double C = nd * std::cos(theta) / 2;
+  const double D = std::pow(std::sin(kPi * courant / nl), 2) / (courant * courant);
+  for (int it = 0; (kp - k) * (kp - k) >= acc && it < 1000; ++it) {
+    kp = k;
+    const double f = std::pow(std::sin(A * k), 2) + std::pow(std::sin(B * k), 2) + std::pow(std::sin(C * k), 2) - D;
+    const double df = A * std::sin(2 * A * k) + B * std::sin(2 * B * k) + C * std::sin(2 * C * k);
+    k -= f / df;
+  }
+  return kC * 2 * kPi / k;
+}
+
+// (component, direction) -> per-axis open interval (ref lo, offset, ref hi,
+// offset), ref 0 = the box's left border L, 1 = its right border R; directions
+// L R D U B F (x low / high, y low / high, z low / high) -- models/tfsf.py
+struct TfsfPred {
+  int comp, dir;
+  struct {
+    int ra;
+    double oa;
+    int rb;
+    double ob;
+  } iv[3];
+};
+const TfsfPred kTfsfPred[24] = {
+    {0, 2, {{0, -0.5, 1, 0.5}, {0, -1.0, 0, 0.0}, {0, 0.0, 1, 0.0}}},
+    {0, 3, {{0, -0.5, 1, 0.5}, {1, 0.0, 1, 1.0}, {0, 0.0, 1, 0.0}}},
+    {0, 4, {{0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {0, -1.0, 0, 0.0}}},
+    {0, 5, {{0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {1, 0.0, 1, 1.0}}},
+    {1, 0, {{0, -1.0, 0, 0.0}, {0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
+    {1, 1, {{1, 0.0, 1, 1.0}, {0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
+    {1, 4, {{0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}, {0, -1.0, 0, 0.0}}},
+    {1, 5, {{0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}, {1, 0.0, 1, 1.0}}},
+    {2, 0, {{0, -1.0, 0, 0.0}, {0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}}},
+    {2, 1, {{1, 0.0, 1, 1.0}, {0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}}},
+    {2, 2, {{0, 0.0, 1, 0.0}, {0, -1.0, 0, 0.0}, {0, -0.5, 1, 0.5}}},
+    {2, 3, {{0, 0.0, 1, 0.0}, {1, 0.0, 1, 1.0}, {0, -0.5, 1, 0.5}}},
+    {3, 2, {{0, 0.0, 1, 0.0}, {0, -0.5, 0, 0.5}, {0, -0.5, 1, 0.5}}},
+    {3, 3, {{0, 0.0, 1, 0.0}, {1, -0.5, 1, 0.5}, {0, -0.5, 1, 0.5}}},
+    {3, 4, {{0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}, {0, -0.5, 0, 0.5}}},
+    {3, 5, {{0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}, {1, -0.5, 1, 0.5}}},
+    {4, 0, {{0, -0.5, 0, 0.5}, {0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}}},
+    {4, 1, {{1, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}}},
+    {4, 4, {{0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {0, -0.5, 0, 0.5}}},
+    {4, 5, {{0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {1, -0.5, 1, 0.5}}},
+    {5, 0, {{0, -0.5, 0, 0.5}, {0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
+    {5, 1, {{1, -0.5, 1, 0.5}, {0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
+    {5, 2, {{0, -0.5, 1, 0.5}, {0, -0.5, 0, 0.5}, {0, 0.0, 1, 0.0}}},
+    {5, 3, {{0, -0.5, 1, 0.5}, {1, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
+};
+// curl terms (source component, derivative axis, sign) of each component (layout/yee.py CURL_TERMS)
+const int kCurl[6][2][3] = {{{5, 1, +1}, {4, 2, -1}}, {{3, 2, +1}, {5, 0, -1}}, {{4, 0, +1}, {3, 1, -1}},
+                            {{1, 2, +1}, {2, 1, -1}}, {{2, 0, +1}, {0, 2, -1}}, {{0, 1, +1}, {1, 0, -1}}};
+// staggered offset of each component inside its cell (layout/yee.py MIN_COORD_FP)
+const double kMinFP[6][3] = {{1.0, 0.5, 0.5}, {0.5, 1.0, 0.5}, {0.5, 0.5, 1.0},
+                             {0.5, 1.0, 1.0}, {1.0, 0.5, 1.0}, {1.0, 1.0, 0.5}};
+
+template <typename T>
+struct TfsfLayer {
+  Dev<long long> off, i0;
+  Dev<T> w0, w1, coef;
+  int n = 0;
+};
+
+template <typename T>
+struct NativeTfsf {
+  std::vector<TfsfLayer<T>*> tab[6];
+  Dev<T> einc, hinc;
+  int nline = 0;
+  double ce = 0, ch = 0;
+  ~NativeTfsf() {
+    for (auto& v : tab)
+      for (auto* l : v) delete l;
+  }
+};
+
+// incident-wave projection onto a component (YeeGridLayout.cpp:811-845)
+double inc_projection(int c, double t, double p, double q) {
+  switch (c) {
+    case 0: return std::cos(q) * std::sin(p) - std::sin(q) * std::cos(t) * std::cos(p);
+    case 1: return -std::cos(q) * std::cos(p) - std::sin(q) * std::cos(t) * std::sin(p);
+    case 2: return std::sin(q) * std::sin(t);
+    case 3: return std::sin(q) * std::sin(p) + std::cos(q) * std::cos(t) * std::cos(p);
+    case 4: return -std::sin(q) * std::cos(p) + std::cos(q) * std::cos(t) * std::sin(p);
+    default: return -(std::cos(q) * std::sin(t));
+  }
+}
+
+template <typename T>
+bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N, const int* boxes,
+                const Dev<T>* Cc, double cb, double db, double dt, double dx, double freq) {
+  const double th = s.incidentWaveAngle1 * (kPi / 180.0), ph = s.incidentWaveAngle2 * (kPi / 180.0);
+  const double ps = s.incidentWaveAngle3 * (kPi / 180.0);
+  if (!(th >= 0 && th <= kPi / 2 + 1e-12 && ph >= 0 && ph <= kPi / 2 + 1e-12)) {
+    std::fprintf(stderr, "fdtd3d (native): TF/SF incident angles must lie in [0, 90] degrees\n");
+    return false;
+  }
+  const double wl = kC / freq, nl = wl / dx, courant = s.courantNum;
+  const double rel = phase_velocity_3d(dx, wl, courant, nl, kPi / 2, 0.0) /
+                     phase_velocity_3d(dx, wl, courant, nl, th, ph);
+  tf.ce = dt / (rel * kEps0 * dx);
+  tf.ch = dt / (rel * kMu0 * dx);
+  tf.nline = 100 * (N[0] + N[1] + N[2]);
+  tf.einc.alloc(tf.nline);
+  tf.hinc.alloc(tf.nline);
+  const double L[3] = {(double)s.tfsfSizeX, (double)s.tfsfSizeY, (double)s.tfsfSizeZ};
+  const double R[3] = {N[0] - L[0], N[1] - L[1], N[2] - L[2]};
+  const double dir[3] = {std::sin(th) * std::cos(ph), std::sin(th) * std::sin(ph), std::cos(th)};
+  const double zero[3] = {L[0] - 2.5 * std::sin(th) * std::cos(ph), L[1] - 2.5 * std::sin(th) * std::sin(ph),
+                          L[2] - 2.5 * std::cos(th)};
+  const int dir_axis[6] = {0, 0, 1, 1, 2, 2};
+  const bool dir_low[6] = {true, false, true, false, true, false};
+  std::vector<T> hc((size_t)N[0] * N[1] * N[2]);
+  for (int c = 0; c < 6; ++c) {
+    const int* bx = boxes + 6 * c;
+    if (bx[3] <= bx[0] || bx[4] <= bx[1] || bx[5] <= bx[2]) continue;
+    const bool kind_e = c < 3;
+    const bool pc = Cc[c].p != nullptr;
+    if (pc) HIP_OK(hipMemcpy(hc.data(), Cc[c].p, hc.size() * sizeof(T), hipMemcpyDeviceToHost));
+    struct Ent {
+      long long flat, i0;
+      double w0, w1, cv;
+      size_t seq;
+    };
+    std::vector<Ent> ents;
+    for (int t = 0; t < 2; ++t) {
+      const int src = kCurl[c][t][0], axis = kCurl[c][t][1], sign = kCurl[c][t][2];
+      const double proj = inc_projection(src, th, ph, ps);
+      for (int d = 0; d < 6; ++d) {
+        if (dir_axis[d] != axis) continue;
+        const TfsfPred* pr = nullptr;
+        for (const auto& q : kTfsfPred)
+          if (q.comp == c && q.dir == d) pr = &q;
+        if (!pr) continue;
+        std::vector<int> sel[3];
+        for (int a = 0; a < 3; ++a) {
+          const double lo = (pr->iv[a].ra ? R[a] : L[a]) + pr->iv[a].oa;
+          const double hi = (pr->iv[a].rb ? R[a] : L[a]) + pr->iv[a].ob;
+          for (int v = bx[a]; v < bx[3 + a]; ++v) {
+            const double g = v + kMinFP[c][a];
+            if (g > lo && g < hi) sel[a].push_back(v);
+          }
+        }
+        const int nb = kind_e ? (dir_low[d] ? 0 : -1) : (dir_low[d] ? 0 : 1);
+        const int tsign = dir_low[d] ? -sign : sign;
+        for (int i : sel[0])
+          for (int j : sel[1])
+            for (int k : sel[2]) {
+              int ni[3] = {i, j, k};
+              ni[axis] += nb;
+              double dd = 0.0;
+              for (int a = 0; a < 3; ++a) dd += (ni[a] + kMinFP[src][a] - zero[a]) * dir[a];
+              dd -= kind_e ? 0.5 : 0.0;
+              const long long i0 = (long long)std::floor(dd);
+              if (i0 < 0 || i0 + 1 >= tf.nline) {
+                std::fprintf(stderr, "fdtd3d (native): TF/SF box does not fit the incident line\n");
+                return false;
+              }
+              const long long flat = ((long long)i * N[1] + j) * N[2] + k;
+              const double cf = pc ? (double)hc[flat] : (kind_e ? cb : db);
+              const double w1 = dd - (double)i0;
+              ents.push_back({flat, i0, 1.0 - w1, w1, cf * tsign * proj, ents.size()});
+            }
+      }
+    }
+    if (ents.empty()) continue;
+    // layers of unique targets (k_tfsf_apply has no atomics): stable order, the
+    // r-th entry of a target goes to layer r
+    std::stable_sort(ents.begin(), ents.end(), [](const Ent& a, const Ent& b) { return a.flat < b.flat; });
+    std::vector<int> rank(ents.size(), 0);
+    int maxr = 0;
+    for (size_t q = 1; q < ents.size(); ++q)
+      if (ents[q].flat == ents[q - 1].flat) maxr = std::max(maxr, rank[q] = rank[q - 1] + 1);
+    for (int r = 0; r <= maxr; ++r) {
+      std::vector<long long> off, i0;
+      std::vector<T> w0, w1, cv;
+      for (size_t q = 0; q < ents.size(); ++q)
+        if (rank[q] == r) {
+          off.push_back(ents[q].flat);
+          i0.push_back(ents[q].i0);
+          w0.push_back((T)ents[q].w0);
+          w1.push_back((T)ents[q].w1);
+          cv.push_back((T)ents[q].cv);
+        }
+      auto* l = new TfsfLayer<T>();
+      l->n = (int)off.size();
+      l->off.alloc(off.size());
+      l->i0.alloc(i0.size());
+      l->w0.alloc(w0.size());
+      l->w1.alloc(w1.size());
+      l->coef.alloc(cv.size());
+      HIP_OK(hipMemcpy(l->off.p, off.data(), off.size() * sizeof(long long), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(l->i0.p, i0.data(), i0.size() * sizeof(long long), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(l->w0.p, w0.data(), w0.size() * sizeof(T), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(l->w1.p, w1.data(), w1.size() * sizeof(T), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(l->coef.p, cv.data(), cv.size() * sizeof(T), hipMemcpyHostToDevice));
+      tf.tab[c].push_back(l);
+    }
+  }
+  return true;
+}
+
+int inc_e(float* e, const float* h, int n, double c, double v, void* s) { return fdtd_inc_e_f32(e, h, n, c, v, s); }
+int inc_e(double* e, const double* h, int n, double c, double v, void* s) { return fdtd_inc_e_f64(e, h, n, c, v, s); }
+int inc_h(const float* e, float* h, int n, double c, void* s) { return fdtd_inc_h_f32(e, h, n, c, s); }
+int inc_h(const double* e, double* h, int n, double c, void* s) { return fdtd_inc_h_f64(e, h, n, c, s); }
+int tfsf_apply(float* t, const TfsfLayer<float>& l, const float* inc, const int* box, void* s) {
+  return fdtd_tfsf_apply_f32(t, l.off.p, l.i0.p, l.w0.p, l.w1.p, l.coef.p, nullptr, l.n, inc, box, s);
+}
+int tfsf_apply(double* t, const TfsfLayer<double>& l, const double* inc, const int* box, void* s) {
+  return fdtd_tfsf_apply_f64(t, l.off.p, l.i0.p, l.w0.p, l.w1.p, l.coef.p, nullptr, l.n, inc, box, s);
+}
+
 template <typename T>
 int run(const fdtd::Settings& s) {
   const int dim = s.dimension;
@@ -310,9 +543,11 @@ int run(const fdtd::Settings& s) {
   const bool v4 = sizeof(T) == 4 && N[2] % 4 == 0 && dim == 3;
   // fused / blocked / resident kernels unless --split-kernels (3D fused E+H
   // and blocked passes, 2D blocked passes, 1D one-launch resident run)
-  // CPML runs step through the float4 split kernels with the psi terms folded in
+  // CPML runs step through the float4 split kernels with the psi terms folded
+  // in; TF/SF runs apply their corrections between the split half steps
   const bool cpml = s.doUsePML;
-  const bool use_fused = !s.doUseSplitKernels && !cpml;
+  const bool tfsf = s.doUseTFSF;
+  const bool use_fused = !s.doUseSplitKernels && !cpml && !tfsf;
   hipStream_t st;
   HIP_OK(hipStreamCreate(&st));
 
@@ -405,6 +640,14 @@ int run(const fdtd::Settings& s) {
   };
   NativeCpml cpt;
   if (cpml) setup_cpml(cpt, s, N, active, dt, dx);
+  NativeTfsf<T> tft;
+  if (tfsf && !setup_tfsf(tft, s, N, boxes, C, percell ? 1.0 : cb, percell ? 1.0 : db, dt, dx, freq)) return 1;
+  const bool point_src = !tfsf || s.doUsePointSource;
+  const int whole[6] = {0, 0, 0, N[0], N[1], N[2]};
+  auto tfsf_kind = [&](int kind) {
+    for (int c = 3 * kind; c < 3 * kind + 3; ++c)
+      for (auto* l : tft.tab[c]) K_OK(tfsf_apply(F[c].p, *l, kind == 0 ? tft.hinc.p : tft.einc.p, whole, st));
+  };
 
   // one time step (t) through the configured kernels
   auto step = [&](int t) {
@@ -420,22 +663,32 @@ int run(const fdtd::Settings& s) {
         K_OK(fused(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, percell ? 1.0 : db, N[0], N[1], N[2], boxes,
                    src_off, src_comp, sv, st, v4));
         for (int c = 0; c < 6; ++c) std::swap(F[c].p, G[c].p);
-      } else if (cpml) {
-        if constexpr (sizeof(T) == 4) {
-          K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p,
-                                           percell ? 1.0 : cb, N[0], N[1], N[2], boxes, 0, cpt.P[0].data(),
-                                           cpt.I[0].data(), st));
-          K_OK(setv(F[src_comp].p, src_off, sv, st));
-          K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p,
-                                           percell ? 1.0 : db, N[0], N[1], N[2], boxes + 18, 0, cpt.P[1].data(),
-                                           cpt.I[1].data(), st));
-        }
       } else {
-        K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, percell ? 1.0 : cb, N[0],
-                 N[1], N[2], boxes, 0, st, v4));
-        K_OK(setv(F[src_comp].p, src_off, sv, st));
-        K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, percell ? 1.0 : db, N[0],
-                 N[1], N[2], boxes + 18, 0, st, v4));
+        // split half steps: [incident line E] E update [TF/SF on E] [source]
+        // [incident line H] H update [TF/SF on H] -- the order of scheme.step
+        if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
+        if (cpml) {
+          if constexpr (sizeof(T) == 4)
+            K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p,
+                                             percell ? 1.0 : cb, N[0], N[1], N[2], boxes, 0, cpt.P[0].data(),
+                                             cpt.I[0].data(), st));
+        } else {
+          K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, percell ? 1.0 : cb,
+                   N[0], N[1], N[2], boxes, 0, st, v4));
+        }
+        if (tfsf) tfsf_kind(0);
+        if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));
+        if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
+        if (cpml) {
+          if constexpr (sizeof(T) == 4)
+            K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p,
+                                             percell ? 1.0 : db, N[0], N[1], N[2], boxes + 18, 0, cpt.P[1].data(),
+                                             cpt.I[1].data(), st));
+        } else {
+          K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, percell ? 1.0 : db,
+                   N[0], N[1], N[2], boxes + 18, 0, st, v4));
+        }
+        if (tfsf) tfsf_kind(1);
       }
     } else if (scheme == "tmz") {
       K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], boxes + 12, st));
@@ -563,8 +816,9 @@ int run(const fdtd::Settings& s) {
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", std::max(T_blk, T2_blk));
   else if (res1)
     std::printf("Backend: native HIP, register-resident 1D kernel (one launch per run)\n");
-  else if (cpml)
-    std::printf("Backend: native HIP, split float4 kernels with the CPML terms folded in\n");
+  else if (cpml || tfsf)
+    std::printf("Backend: native HIP, split kernels%s%s\n", cpml ? " with the CPML terms folded in" : "",
+                tfsf ? " + TF/SF corrections" : "");
   else
     std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
   std::printf("Throughput: %.1f Mcells/s\n", cells * (double)timed / sec / 1e6);
@@ -616,12 +870,15 @@ int main(int argc, char** argv) {
   // CPML absorbing layers: 3D fp32 with whole float4 z rows (the folded float4 kernels)
   const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && s.dimension == 3 && s.valueType == "f32" &&
                        s.sizeZ % 4 == 0;
-  if ((s.doUsePML && !cpml_ok) || s.doUseTFSF || s.doUseMetamaterials || s.doUseNTFF || s.doUseAmplitudeMode ||
+  // TF/SF plane waves: 3D (any precision), also combined with the CPML
+  const bool tfsf_ok = s.doUseTFSF && s.dimension == 3;
+  if ((s.doUsePML && !cpml_ok) || (s.doUseTFSF && !tfsf_ok) || s.doUseMetamaterials || s.doUseNTFF ||
+      s.doUseAmplitudeMode ||
       s.doUseComplexFieldValues || s.doUseParallelGrid || s.doUseDoubleMaterialPrecision ||
       !s.loadFromFile.empty()) {
     std::fprintf(stderr,
-                 "fdtd3d (native): UPML, CPML outside 3D fp32 float4 rows, TF/SF, metamaterials, NTFF, amplitude "
-                 "mode, complex fields, parallel grids and resume run through the Python driver: "
+                 "fdtd3d (native): UPML, CPML outside 3D fp32 float4 rows, TF/SF outside 3D, metamaterials, NTFF, "
+                 "amplitude mode, complex fields, parallel grids and resume run through the Python driver: "
                  "python -m fdtd3d_amd <same options>\n");
     return 2;
   }

@@ -83,7 +83,7 @@ def test_native_executable_cli(host):
     assert r.returncode == 0 and "Version" in r.stdout
     r = subprocess.run([exe, "--no-such-flag"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2
-    r = subprocess.run([exe, "--use-tfsf"], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([exe, "--2d", "--use-tfsf"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "python -m fdtd3d_amd" in r.stderr
     # CPML runs natively in 3D fp32 only; UPML and fp64 CPML go to the Python driver
     for argv in (["--3d", "--use-pml"], ["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f64"],

@@ -42,8 +42,17 @@ CASES = {
                              "--sphere-radius", "5", "--sphere-eps", "3", "--use-pml", "--pml-type", "cpml",
                              "--pml-sizex", "6", "--same-size-pml", "--cpml-kappa-max", "3",
                              "--cpml-alpha-max", "0.05"],
+    # TF/SF plane wave (oblique incidence; fp32 and fp64), and CPML + TF/SF (BASELINE config 3, fp32)
+    "3d_tfsf": ["--3d", "--sizex", "36", "--sizey", "32", "--sizez", "40", "--time-steps", "30", "--scene", "sphere",
+                "--sphere-center-x", "18", "--sphere-center-y", "16", "--sphere-center-z", "20", "--sphere-radius",
+                "4", "--sphere-eps", "2", "--use-tfsf", "--tfsf-sizex", "8", "--tfsf-sizey", "7", "--tfsf-sizez", "9",
+                "--angle-teta", "50", "--angle-phi", "30", "--angle-psi", "20"],
+    "3d_cpml_tfsf": ["--3d", "--sizex", "40", "--same-size", "--time-steps", "30", "--scene", "vacuum",
+                     "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6", "--same-size-pml", "--use-tfsf",
+                     "--tfsf-sizex", "10", "--same-size-tfsf", "--angle-teta", "60", "--angle-phi", "10",
+                     "--angle-psi", "5"],
 }
-FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa"}
+FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf"}
 
 COMPS = {"3d": ["Ex", "Ey", "Ez", "Hx", "Hy", "Hz"], "tmz": ["Ez", "Hx", "Hy"], "tez": ["Ex", "Ey", "Hz"],
          "1d": ["Ez", "Hy"]}
