@@ -27,6 +27,11 @@ Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 # automatic steps per pass of the fp64 blocked kernel (yee3d_tb64.hip);
 # 512^3: T=1 42.6k, 2 75.7k, 3 99.0k, 4 110k Mcells/s
 F64_AUTO_STEPS = 4
+# automatic steps per hybrid pass (fp32): 512^3 CPML + TF/SF 79.2k / 75.5k /
+# 74.5k Mcells/s at T = 5 / 4 / 3, UPML + TF/SF 70.9k / 67.9k / 66.6k, Drude
+# sphere 53.5k / 52.1k / 49.3k, CPML point 99.4k / 95.0k / 80.2k: the faster
+# T = 5 core outweighs the one-cell deeper band
+HYBRID_AUTO_STEPS = 5
 # automatic steps per pass of the 2D TMz / TEz blocked kernel (yee2d_tb.hip);
 # 16384^2 fp32 TMz: T=1 119k, 5 851k, 6 1.01M, 7 1.11M, 8 1.06M Mcells/s
 TB2D_AUTO_STEPS = 7
@@ -120,7 +125,7 @@ class BlockedStepping:
             elif two_d:
                 H = TB2D_AUTO_STEPS if self.dtype == torch.float32 else TB2D_AUTO_STEPS_F64
             else:
-                H = 4 if self.dtype == torch.float32 else F64_AUTO_STEPS
+                H = HYBRID_AUTO_STEPS if self.dtype == torch.float32 else F64_AUTO_STEPS
         hmax = getattr(self.ops, "tb2d_max_steps" if two_d else "tb_max_steps", 8 if two_d else 6)
         if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme not in ("3d", "tmz", "tez")
                 or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode

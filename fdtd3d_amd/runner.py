@@ -88,8 +88,9 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
         if hyb:
             # hybrid passes (models/blocking.py): blocked core + stepped shell,
             # one hybridBlock-deep exchange per pass
-            from .models.blocking import F64_AUTO_STEPS
-            buf = settings.hybridBlock if settings.hybridBlock > 1 else (4 if cfg.dtype == "f32" else F64_AUTO_STEPS)
+            from .models.blocking import F64_AUTO_STEPS, HYBRID_AUTO_STEPS
+            buf = settings.hybridBlock if settings.hybridBlock > 1 else (HYBRID_AUTO_STEPS if cfg.dtype == "f32"
+                                                                          else F64_AUTO_STEPS)
         # float4 rows: z extent (3D) / y extent (2D) padded to a multiple of 4
         domain = core.domain(rank, buf, align_z=4 if (tb > 1 or hyb) else 1,
                              align_axis=2 if cfg.scheme == "3d" else 1)
