@@ -292,7 +292,11 @@ class BlockedStepping:
                 edge = max(edge, self.layout.pml_size[a])
             if cfg.use_tfsf and not in_kernel_tfsf:
                 edge = max(edge, cfg.tfsf_size[a] + 1)
-            lo[a], hi[a] = edge + m, size[a] - edge - m
+            if edge > 0:
+                lo[a], hi[a] = edge + m, size[a] - edge - m
+            # else: nothing irregular along this axis but the domain border,
+            # which the blocked kernel handles itself (a Drude sphere in
+            # vacuum without PML: the core reaches the faces)
         K = (tuple(lo), tuple(hi))
         if box_empty(K):
             return None
@@ -362,9 +366,15 @@ class BlockedStepping:
             # decomposed: each rank's core is its owned part of the global core
             couts = [box_intersect(b, dom.owned_global()) for b in couts]
             couts = [b for b in couts if not box_empty(b)]
+        def shrink_inner(b, n):
+            # shrink by n only the sides that lie inside the domain (a side
+            # on the domain border has no shell beyond it)
+            return (tuple(b[0][d] + (n if act[d] and b[0][d] > 0 else 0) for d in range(3)),
+                    tuple(b[1][d] - (n if act[d] and b[1][d] < size[d] else 0) for d in range(3)))
+
         def shell_windows(d):
             # everything but the core cells deeper than d inside it
-            Kd = grow(K, -d)
+            Kd = shrink_inner(K, d)
             if box_empty(Kd):
                 return None
             ws = [b for b in box_subtract(alloc, Kd) if not box_empty(b)]

@@ -21,6 +21,11 @@ CASES = [
     ("sphere-cpml", dict(scene="sphere", use_pml=True, pml_type="cpml", sphere_center=(36.0, 36.0, 36.0),
                          sphere_radius=9.0), 2, 6),
     ("upml-tfsf-complex", dict(scene="vacuum", use_pml=True, use_tfsf=True, complex_values=True), 3, 7),
+    # no PML / TF-SF: the core reaches the domain faces (only the dispersive box is stepped)
+    ("drude-nopml", dict(scene="drude-sphere", use_metamaterials=True, sphere_center=(36.0, 36.0, 36.0),
+                         sphere_radius=6.0), 3, 8),
+    ("drude-nopml-face", dict(scene="drude-sphere", use_metamaterials=True, sphere_center=(9.0, 30.0, 40.0),
+                              sphere_radius=6.0), 4, 9),
 ]
 
 

@@ -22,6 +22,11 @@ CASES = [
     ("sphere-cpml", dict(scene="sphere", use_pml=True, pml_type="cpml", sphere_center=(40.0, 36.0, 48.0),
                          sphere_radius=10.0), 4, 9),
     ("upml-tfsf-f64", dict(scene="vacuum", use_pml=True, use_tfsf=True, theta=30, phi=40, psi=20, dtype="f64"), 4, 10),
+    # no PML: the blocked core reaches the domain faces around the dispersive box
+    ("drude-nopml", dict(scene="drude-sphere", use_metamaterials=True, sphere_center=(40.0, 36.0, 48.0),
+                         sphere_radius=7.0), 5, 12),
+    ("drude-nopml-face", dict(scene="drude-sphere", use_metamaterials=True, sphere_center=(9.0, 30.0, 60.0),
+                              sphere_radius=6.0), 4, 11),
     # 2D: blocked core through yee2d_tb.hip
     ("tmz-upml-tfsf", dict(scheme="tmz", size=(120, 104, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
                            scene="vacuum", use_pml=True, use_tfsf=True, phi=30), 7, 23),
@@ -119,6 +124,8 @@ SCALE_CASES = [
     ("upml-tfsf-256", dict(scene="vacuum", use_pml=True, use_tfsf=True)),
     ("drude-256", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, sphere_center=(128.0, 128.0, 128.0),
                        sphere_radius=64)),
+    ("drude-256-nopml", dict(scene="drude-sphere", use_metamaterials=True, sphere_center=(128.0, 128.0, 128.0),
+                             sphere_radius=64)),
 ]
 
 

@@ -43,6 +43,10 @@ CONFIGS = [
      C512 + ["--time-steps", "100", "--scene", "drude-sphere", "--use-metamaterials", "--use-pml",
              "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
              "--sphere-radius", "128"]),
+    ("3d-512-drude-nopml", "3D 512^3 Drude sphere (r=128) in vacuum, no PML (BASELINE config 4 as named), fp32",
+     C512 + ["--time-steps", "100", "--scene", "drude-sphere", "--use-metamaterials",
+             "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
+             "--sphere-radius", "128"]),
     ("3d-512-sphere", "3D 512^3 dielectric sphere (eps=4, r=128), fp32",
      C512 + ["--time-steps", "200", "--scene", "sphere", "--sphere-eps", "4",
              "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
