@@ -229,9 +229,44 @@ __device__ __forceinline__ void chain_finish(const ChainComp<T>& q, bool kind_e,
 // rows stay coalesced; each thread walks CHX planes along x.
 constexpr int CHX = 8;
 
+// Plain Yee update of one component of one cell (mode 2 of chain_finish):
+// the cells of a dispersive box outside the material's per-row z range.
+template <typename T>
+__device__ __forceinline__ ChainIn<T> plain_load(const ChainComp<T>& q, bool kind_e, const long long* stride,
+                                                 const int* n, size_t off) {
+  ChainIn<T> v;
+  v.mode = in_box(q.box, n[0], n[1], n[2]) ? 2 : 0;
+  if (v.mode == 0) return v;
+  const long long s0 = pick3(q.a0, stride[0], stride[1], stride[2]);
+  const long long s1 = pick3(q.a1, stride[0], stride[1], stride[2]);
+  v.x0 = q.s0[off];
+  v.x1 = q.s1[off];
+  v.y0 = kind_e ? q.s0[off - s0] : q.s0[off + s0];
+  v.y1 = kind_e ? q.s1[off - s1] : q.s1[off + s1];
+  v.E = q.E[off];
+  v.cell = q.pcell ? q.pcell[off] : q.pcb;
+  return v;
+}
+
+// Per-row z range of the dispersive cells of a box (local indices): rows
+// (x, y) of [lo0, lo0 + nx) x [lo1, lo1 + ny) hold int2 (z0, z1); cells of the
+// launch outside their row's range run the plain update.  The split is a
+// static property of the cell (the same in every window set), so a cell's D /
+// D1 history is either always advanced or never read.
+struct RowRanges {
+  const int2* r;
+  int lo0, lo1, nx, ny;
+};
+
+__device__ __forceinline__ int2 row_range(const RowRanges& rr, int x, int y) {
+  const int tx = x - rr.lo0, ty = y - rr.lo1;
+  if (tx < 0 || ty < 0 || tx >= rr.nx || ty >= rr.ny) return make_int2(0, 0);
+  return rr.r[(size_t)tx * rr.ny + ty];
+}
+
 template <typename T, bool DRUDE, bool CELL>
 __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q1, ChainComp<T> q2, int kind_e,
-                                                 int ny, int nz, Box3 U) {
+                                                 int ny, int nz, Box3 U, RowRanges rr) {
   const int W = U.hi[2] - U.lo[2];
   const int H = U.hi[1] - U.lo[1];
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -242,16 +277,31 @@ __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q
   const int i0 = U.lo[0] + (int)blockIdx.y * CHX;
   const int i1 = min(i0 + CHX, U.hi[0]);
   const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
+  // dispersive launches with a row table: the next plane's range is loaded
+  // one trip ahead, so the path decision never waits on its own load
+  int2 nxt = make_int2(0, 0x7fffffff);
+  if (DRUDE && rr.r && i0 < i1) nxt = row_range(rr, i0, n[1]);
 #pragma unroll 1
   for (int i = i0; i < i1; ++i) {
     n[0] = i;
     const size_t off = ((size_t)i * ny + n[1]) * nz + n[2];
     if constexpr (DRUDE) {
-      // the dispersive form holds twice the operands: one component at a
-      // time (all three in flight spill: measured 47k vs 51k Mcells/s)
-      chain_cell<T, DRUDE, CELL>(q0, kind_e != 0, stride, n, off);
-      chain_cell<T, DRUDE, CELL>(q1, kind_e != 0, stride, n, off);
-      chain_cell<T, DRUDE, CELL>(q2, kind_e != 0, stride, n, off);
+      const int2 cur = nxt;
+      if (rr.r && i + 1 < i1) nxt = row_range(rr, i + 1, n[1]);
+      if (n[2] >= cur.x && n[2] < cur.y) {
+        // the dispersive form holds twice the operands: one component at a
+        // time (all three in flight spill: measured 47k vs 51k Mcells/s)
+        chain_cell<T, DRUDE, CELL>(q0, kind_e != 0, stride, n, off);
+        chain_cell<T, DRUDE, CELL>(q1, kind_e != 0, stride, n, off);
+        chain_cell<T, DRUDE, CELL>(q2, kind_e != 0, stride, n, off);
+      } else {
+        const ChainIn<T> v0 = plain_load<T>(q0, kind_e != 0, stride, n, off);
+        const ChainIn<T> v1 = plain_load<T>(q1, kind_e != 0, stride, n, off);
+        const ChainIn<T> v2 = plain_load<T>(q2, kind_e != 0, stride, n, off);
+        chain_finish<T, DRUDE>(q0, kind_e != 0, v0, off);
+        chain_finish<T, DRUDE>(q1, kind_e != 0, v1, off);
+        chain_finish<T, DRUDE>(q2, kind_e != 0, v2, off);
+      }
     } else {
       // all three components' loads before the first store (UPML + TF/SF
       // 512^3: 69.6k vs 67.0k Mcells/s)
@@ -310,7 +360,7 @@ ChainComp<T> make_comp(const void* const* P, double s, const int* I) {
 
 template <typename T>
 int launch_chain(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny, int nz,
-                 hipStream_t s) {
+                 RowRanges rr, hipStream_t s) {
   ChainComp<T> q[3];
   Box3 U = {{0, 0, 0}, {0, 0, 0}};
   bool cell = false;
@@ -326,7 +376,7 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
     if (!box_empty(q[c].box) && (q[c].cell != nullptr) != cell) return (int)hipErrorInvalidValue;
   const long long cells = (long long)(U.hi[2] - U.lo[2]) * (U.hi[1] - U.lo[1]);
   dim3 grid(cdiv(cells, 256), cdiv(U.hi[0] - U.lo[0], CHX));
-#define CH_LAUNCH(D, C) k_chain3d<T, D, C><<<grid, 256, 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U)
+#define CH_LAUNCH(D, C) k_chain3d<T, D, C><<<grid, 256, 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U, rr)
   if (drude) {
     if (cell) CH_LAUNCH(true, true);
     else CH_LAUNCH(true, false);
@@ -348,10 +398,26 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
 // the plain box holds cells updated F += c (curl) in the same launch).
 FDTD_API int fdtd_chain3d_f32(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny,
                               int nz, void* s) {
-  return launch_chain<float>(P, S, I, drude, kind_e, ny, nz, (hipStream_t)s);
+  return launch_chain<float>(P, S, I, drude, kind_e, ny, nz, RowRanges{nullptr, 0, 0, 0, 0}, (hipStream_t)s);
 }
 
 FDTD_API int fdtd_chain3d_f64(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny,
                               int nz, void* s) {
-  return launch_chain<double>(P, S, I, drude, kind_e, ny, nz, (hipStream_t)s);
+  return launch_chain<double>(P, S, I, drude, kind_e, ny, nz, RowRanges{nullptr, 0, 0, 0, 0}, (hipStream_t)s);
+}
+
+// Dispersive launch over a box with no PML (sigma = 0): rows = int2 (z0, z1)
+// per (x, y) of [R[0], R[0] + R[2]) x [R[1], R[1] + R[3]); cells outside their
+// row's range take the plain update with the per-component plain coefficient
+// (P[24c + 23] per cell or S[2c + 1]).
+FDTD_API int fdtd_chain3d_rows_f32(const void* const* P, const double* S, const int* I, int kind_e, int ny, int nz,
+                                   const void* rows, const int* R, void* s) {
+  return launch_chain<float>(P, S, I, 1, kind_e, ny, nz, RowRanges{(const int2*)rows, R[0], R[1], R[2], R[3]},
+                             (hipStream_t)s);
+}
+
+FDTD_API int fdtd_chain3d_rows_f64(const void* const* P, const double* S, const int* I, int kind_e, int ny, int nz,
+                                   const void* rows, const int* R, void* s) {
+  return launch_chain<double>(P, S, I, 1, kind_e, ny, nz, RowRanges{(const int2*)rows, R[0], R[1], R[2], R[3]},
+                              (hipStream_t)s);
 }

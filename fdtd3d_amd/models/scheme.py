@@ -168,6 +168,9 @@ class YeeScheme(BlockedStepping):
         self.planes = 2 if cfg.complex_values else 1
         self.use_upml_chain = (cfg.use_pml and cfg.pml_type == "upml") or cfg.use_metamaterials
         self.use_cpml = cfg.use_pml and cfg.pml_type == "cpml" and not cfg.use_metamaterials
+        if cfg.use_pml and cfg.pml_type == "cpml" and cfg.use_metamaterials:
+            log.log(0, "--pml-type cpml with --use-metamaterials: the absorbing layers run the UPML D/B form "
+                       "(the dispersive chain carries D; reference Scheme3D.cpp:266-416)")
         self.t = 0
         self.sub_step = 0
         self.timers: Dict[str, float] = {}
@@ -512,6 +515,8 @@ class YeeScheme(BlockedStepping):
         dom = self.domain
         alloc = dom.allocated_global()
         per = {}
+        sigma0 = {}  # per component: the box where every sigma vanishes (global)
+        self._chain_sigma0 = sigma0
         for c in self.comps:
             C = box_intersect(self._global_box(c), alloc)
             lo, hi = list(C[0]), list(C[1])
@@ -534,6 +539,7 @@ class YeeScheme(BlockedStepping):
             I = box_intersect(C, (tuple(lo), tuple(hi)))
             if box_empty(I):
                 I = (C[0], C[0])
+            sigma0[c] = I
             Dbox = self._bbox_global(self.upml[c].get("drude_active"))
             plain_core = I
             plain = box_subtract(plain_core, Dbox) if not box_empty(plain_core) else [(C[0], C[0])] * 6
@@ -721,8 +727,10 @@ class YeeScheme(BlockedStepping):
         for boxes in plan["plain"]:
             self.ops.curl_update(kind, boxes, F, F, self.cb)
         for launches, slow in plan["chain"]:
-            for sel, form, plain_form, fold in launches:
-                if fold is None:
+            for sel, form, plain_form, fold, rows in launches:
+                if rows is not None:
+                    self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form, cb=self.cb, rows=rows)
+                elif fold is None:
                     self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form)
                 else:
                     self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form, plain=fold, cb=self.cb)
@@ -775,7 +783,8 @@ class YeeScheme(BlockedStepping):
             for form in (True, False):
                 sel = {c: (fast[c] if dru[c] == form else (fast[c][0], fast[c][0])) for c in comps}
                 if any(not box_empty(b) for b in sel.values()):
-                    launches.append([sel, form, self.cfg.use_metamaterials and not form, None])
+                    rows = self._drude_rows(kind) if form and self._sigma0_launch(sel) else None
+                    launches.append([sel, form, self.cfg.use_metamaterials and not form, None, rows])
             chain.append((launches, slow))
         folded = []
         if self.cfg.scheme == "3d" and getattr(self.ops, "chain_fold", False):
@@ -810,6 +819,55 @@ class YeeScheme(BlockedStepping):
             plain = keep
         chain = [([tuple(L) for L in launches], slow) for launches, slow in chain]
         return {"plain": plain, "chain": chain, "folded": folded}
+
+    def _sigma0_launch(self, sel: Dict[str, Box]) -> bool:
+        """True when every (local) box of a chain launch lies where all sigma
+        vanish: there the chain collapses to the plain update away from the
+        dispersive cells."""
+        if not getattr(self.ops, "chain_rows", False) or not self.cfg.use_metamaterials:
+            return False
+        for c, b in sel.items():
+            if box_empty(b):
+                continue
+            z = self.domain.to_local(self._chain_sigma0[c])
+            if box_empty(z) or any(b[0][d] < z[0][d] or b[1][d] > z[1][d] for d in range(3)):
+                return False
+        return True
+
+    def _drude_rows(self, kind: str):
+        """Per local row (x, y): the z range [z0, z1) holding every dispersive
+        cell of the kind's components (int32 ``(nx, ny, 2)`` over the rows'
+        bounding box, plus its origin).  Dispersive chain launches on sigma = 0
+        boxes run the chain inside the ranges only and the plain update on the
+        rest of the box: ~half of a sphere's bounding box, whose D / D1 levels
+        are then never touched (reference: every cell of the grid runs the
+        ADE sweep, Scheme3D.cpp:326-364)."""
+        cache = self.__dict__.setdefault("_drude_rows_cache", {})
+        if kind in cache:
+            return cache[kind]
+        comps = self.e_comps if kind == "E" else self.h_comps
+        m = None
+        for c in comps:
+            a = self.upml[c].get("drude_active")
+            if a is not None:
+                m = a.clone() if m is None else (m | a)
+        if m is None or not bool(m.any()):
+            cache[kind] = None
+            return None
+        rows_any = m.any(dim=2)
+        xs = torch.nonzero(rows_any.any(dim=1)).flatten()
+        ys = torch.nonzero(rows_any.any(dim=0)).flatten()
+        x0, x1, y0, y1 = int(xs.min()), int(xs.max()) + 1, int(ys.min()), int(ys.max()) + 1
+        sub = m[x0:x1, y0:y1, :].to(torch.int8)
+        nz = sub.shape[2]
+        has = sub.any(dim=2)
+        first = torch.argmax(sub, dim=2)
+        last = nz - 1 - torch.argmax(torch.flip(sub, dims=(2,)), dim=2)
+        z0 = torch.where(has, first, torch.zeros_like(first))
+        z1 = torch.where(has, last + 1, torch.zeros_like(last))
+        tab = torch.stack([z0, z1], dim=-1).to(torch.int32).contiguous()
+        cache[kind] = (tab, x0, y0)
+        return cache[kind]
 
     def _upml_region(self, kind: str, c: str, p: int, box: Box) -> None:
         F = self.F[p]

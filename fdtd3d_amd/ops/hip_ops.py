@@ -825,11 +825,17 @@ class HipOps:
     # ------------------------------------------------------------ UPML chain
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
                      p: int, drude: bool, plain_form: bool = False, plain: Optional[Dict[str, Box]] = None,
-                     cb: Optional[Dict[str, Coef]] = None) -> None:
+                     cb: Optional[Dict[str, Coef]] = None, rows=None) -> None:
         """Fused UPML/Drude chain (chain_kernels.hip) of the three components
         of a kind (one launch).  ``upml[c]`` holds the factored coefficient
         profiles (``prof``), the Drude cell coefficients and the D / D1 level
-        lists of scheme._init_upml; new levels go to the last list entry."""
+        lists of scheme._init_upml; new levels go to the last list entry.
+        ``rows`` (dispersive launches on sigma = 0 boxes): ``(table, lo0, lo1)``
+        with ``table`` int32 ``(nx, ny, 2)`` = per local row (x, y) the z range
+        of the dispersive cells; the rest of the box takes the plain update
+        with ``cb`` (the plain scheme's coefficients)."""
+        if rows is not None and (not drude or cb is None):
+            raise HipError("chain_update rows: dispersive launches with the plain coefficients only")
         comps = list(boxes.keys())
         if len(comps) != 3:
             raise HipError("chain_update launches the three components of a kind together")
@@ -877,9 +883,10 @@ class HipOps:
             # plain Yee cells folded into the launch (F += c curl; c scalar or scaled per cell)
             pb = plain.get(c, ((0, 0, 0), (0, 0, 0))) if plain else ((0, 0, 0), (0, 0, 0))
             pcell, pcb = None, 1.0
-            if not _empty(pb):
-                any_box = True
-                self._check_stencil_box(kind, c, pb, shape)
+            if not _empty(pb) or rows is not None:
+                if not _empty(pb):
+                    any_box = True
+                    self._check_stencil_box(kind, c, pb, shape)
                 if self._cell_or_none(cb[c]) is not None:
                     pcell = self._scaled_cell(cb[c])
                 else:
@@ -890,12 +897,25 @@ class HipOps:
                   + list(pb[0]) + list(pb[1]))
         if not any_box:
             return
+        if rows is not None:
+            tab, lo0, lo1 = rows
+            if (tab.device.type != "cuda" or tab.dtype != torch.int32 or not tab.is_contiguous() or tab.dim() != 3
+                    or tab.shape[2] != 2):
+                raise HipError("chain_update rows: contiguous int32 (nx, ny, 2) device table expected")
+            R = (c_int * 4)(int(lo0), int(lo1), int(tab.shape[0]), int(tab.shape[1]))
+            rc = self.fn("chain3d_rows")((c_vp * len(P))(*P), (c_double * len(S))(*S), (c_int * len(I))(*I),
+                                         c_int(1 if kind == "E" else 0), c_int(shape[1]), c_int(shape[2]),
+                                         c_vp(tab.data_ptr()), R, _stream())
+            _check(rc, "chain3d_rows")
+            self.launches += 1
+            return
         rc = self.fn("chain3d")((c_vp * len(P))(*P), (c_double * len(S))(*S), (c_int * len(I))(*I),
                                 c_int(1 if drude else 0), c_int(1 if kind == "E" else 0), c_int(shape[1]),
                                 c_int(shape[2]), _stream())
         _check(rc, "chain3d")
         self.launches += 1
 
+    chain_rows = True  # dispersive chain launches on sigma = 0 boxes: chain inside the per-row material range only
     drude_lut = True  # Drude chain: uint8 material index + coefficient table (falls back past 256 tuples)
     chain_fold = True  # thin plain boxes next to a z PML slab ride in the slab's chain launch
 

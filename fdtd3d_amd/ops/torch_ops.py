@@ -58,6 +58,7 @@ def cb_pad(cb: Dict[str, Coef]) -> Dict[str, Coef]:
 
 class TorchOps:
     name = "torch"
+    chain_rows = True  # same launch plan as the HIP backend (row-range dispersive split)
 
     def __init__(self, layout: YeeLayout, device, dtype):
         self.layout = layout
@@ -150,33 +151,60 @@ class TorchOps:
 
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
                      p: int, drude: bool, plain_form: bool = False, plain: Optional[Dict[str, Box]] = None,
-                     cb: Optional[Dict[str, Coef]] = None) -> None:
+                     cb: Optional[Dict[str, Coef]] = None, rows=None) -> None:
         """Reference semantics of the fused UPML/Drude chain kernel
         (chain_kernels.hip): D -> [D1] -> E per cell of each box, plus the
-        plain Yee update on the folded ``plain`` boxes."""
+        plain Yee update on the folded ``plain`` boxes.  ``rows`` (dispersive
+        launches): ``(table, lo0, lo1)``, per local row (x, y) the z range of
+        the cells that run the chain; the other cells of the boxes take the
+        plain update ``F += cb curl`` (their D / D1 levels are left alone)."""
         if plain:
             pb = {c: plain.get(c, ((0, 0, 0), (0, 0, 0))) for c in boxes}
             self.curl_update(kind, pb, F, F, cb)
+        new = []
         for c, box in boxes.items():
             if _empty(box):
                 continue
             st = upml[c]
             sl = box_slices(box)
             curl = self.curl(kind, c, sl, F)
+            mask = None if rows is None else self._row_mask(rows, box)
             D = st["D"][p]
             Dn = st["caD"].materialize(sl) * D[0][sl] + st["cbD"].materialize(sl) * curl
-            D[-1][sl] = Dn
             nw, old = Dn, D[0][sl]
+            upd = [(D[-1], Dn)]
             if drude:
                 D1 = st["D1"][p]
                 D1n = (st["b0"].materialize(sl) * Dn + st["b1"].materialize(sl) * D[0][sl]
                        + st["b2"].materialize(sl) * D[1][sl] + st["ma1"].materialize(sl) * D1[0][sl]
                        + st["ma2"].materialize(sl) * D1[1][sl])
-                D1[2][sl] = D1n
+                upd.append((D1[2], D1n))
                 nw, old = D1n, D1[0][sl]
             cbE, ccE = (st["plain"]["cbE"], st["plain"]["ccE"]) if plain_form else (st["cbE"], st["ccE"])
-            F[c][sl] = (st["caE"].materialize(sl) * F[c][sl] + cbE.materialize(sl) * nw
-                        + ccE.materialize(sl) * old)
+            En = st["caE"].materialize(sl) * F[c][sl] + cbE.materialize(sl) * nw + ccE.materialize(sl) * old
+            if mask is not None:
+                En = torch.where(mask, En, F[c][sl] + cb[c].materialize(sl) * curl)
+                upd = [(t, torch.where(mask, v, t[sl])) for t, v in upd]
+            new.append((c, sl, En, upd))
+        # every component reads the other kind only: the stores can follow in any order
+        for c, sl, En, upd in new:
+            for t, v in upd:
+                t[sl] = v
+            F[c][sl] = En
+
+    @staticmethod
+    def _row_mask(rows, box: Box) -> torch.Tensor:
+        """Boolean mask over ``box``: z inside the row's dispersive range."""
+        tab, lo0, lo1 = rows
+        nx, ny = tab.shape[0], tab.shape[1]
+        X = torch.arange(box[0][0], box[1][0], device=tab.device) - lo0
+        Y = torch.arange(box[0][1], box[1][1], device=tab.device) - lo1
+        okx = (X >= 0) & (X < nx)
+        oky = (Y >= 0) & (Y < ny)
+        r = tab[X.clamp(0, nx - 1)][:, Y.clamp(0, ny - 1)]  # (bx, by, 2)
+        ok = (okx[:, None] & oky[None, :])[..., None]
+        Z = torch.arange(box[0][2], box[1][2], device=tab.device)[None, None, :]
+        return ok & (Z >= r[..., 0:1]) & (Z < r[..., 1:2])
 
     def curl_general(self, kind: str, comp: str, box: Box, out: torch.Tensor, inp: torch.Tensor,
                      src: Dict[str, torch.Tensor], ca: Coef, cb: Coef) -> None:

@@ -150,3 +150,37 @@ def test_ade_natural_modes_match_continuous_medium(w0_ratio):
     tol = 0.05 * abs(s_ana) * dt * abs(s_ana) * dt + 1e-9
     assert abs(s_num.imag - s_ana.imag) <= max(tol, 1e-3) * abs(s_ana), (s_num, s_ana)
     assert abs(s_num.real - s_ana.real) <= max(tol, 1e-3) * abs(s_ana), (s_num, s_ana)
+
+
+@pytest.mark.parametrize("pml", [False, True])
+def test_drude_row_split_matches_full_chain(pml, monkeypatch):
+    """Dispersive chain launches on sigma = 0 boxes run the ADE only inside
+    each row's material z range and the plain update elsewhere: the same
+    fields as running the chain on the whole bounding box (the chain collapses
+    to the plain update where omega = gamma = 0, D tracking the increments),
+    from random initial fields."""
+    from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+    from fdtd3d_amd.ops import make_ops
+    from fdtd3d_amd.ops.torch_ops import TorchOps
+
+    cfg = SchemeConfig(scheme="3d", size=(40, 36, 44), dtype="f64", time_steps=7, scene="drude-sphere",
+                       use_metamaterials=True, use_pml=pml, pml_size=(4, 4, 4), sphere_center=(20.0, 17.0, 23.0),
+                       sphere_radius=8.0)
+    runs = []
+    for rows in (True, False):
+        monkeypatch.setattr(TorchOps, "chain_rows", rows)
+        s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+        s.init_scheme()
+        s.init_grids()
+        s.randomize_fields(seed=3)
+        s.perform_steps()
+        used = any(L[4] is not None for plan in s._chain_plan_cache.values() for ls, _ in plan["chain"] for L in ls)
+        assert used == rows
+        runs.append(s)
+    a, b = runs
+    tab = a._drude_rows("E")[0]
+    filled = float((tab[..., 1] - tab[..., 0]).sum())
+    assert 0 < filled < 0.8 * tab.shape[0] * tab.shape[1] * 16  # the ranges are tighter than the box
+    for c in a.comps:
+        scale = float(b.F[0][c].abs().max())
+        assert float((a.F[0][c] - b.F[0][c]).abs().max()) <= 1e-12 * scale, c

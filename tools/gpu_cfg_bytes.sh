@@ -27,6 +27,7 @@ for n in ${CONFIGS:-cpml upml drude}; do
     cpml) run cpml --scene vacuum --use-pml --pml-type cpml --use-tfsf ;;
     upml) run upml --scene vacuum --use-pml --use-tfsf ;;
     drude) run drude --scene drude-sphere --use-metamaterials --use-pml $SPH ;;
+    drudenopml) run drudenopml --scene drude-sphere --use-metamaterials $SPH ;;
     sphere) run sphere --scene sphere --sphere-eps 4 $SPH ;;
     vac) run vac --scene vacuum ;;
   esac || exit 1

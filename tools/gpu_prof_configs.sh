@@ -25,6 +25,7 @@ for n in ${CONFIGS:-cpml upml drude sphere}; do
     cpmlsph) run cpmlsph --scene sphere --sphere-eps 4 $SPH --use-pml --pml-type cpml --use-tfsf ;;
     upml) run upml --scene vacuum --use-pml --use-tfsf ;;
     drude) run drude --scene drude-sphere --use-metamaterials --use-pml $SPH ;;
+    drudenopml) run drudenopml --scene drude-sphere --use-metamaterials $SPH ;;
     sphere) run sphere --scene sphere --sphere-eps 4 $SPH ;;
     sphere3) run sphere3 --scene sphere --sphere-eps 4 $SPH --time-block 3 ;;
     sphere4) run sphere4 --scene sphere --sphere-eps 4 $SPH --time-block 4 ;;
