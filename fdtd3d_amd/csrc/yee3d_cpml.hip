@@ -279,7 +279,14 @@ CpmlK make_cpml(const void* const* P, const int* I) {
 // per wave keep the lanes busy
 inline int lanes_z(const Box3& bu) {
   const int kspan = bu.hi[2] - (bu.lo[2] & ~3);
-  return kspan <= 32 ? 8 : (kspan <= 64 ? 16 : 64);
+  // the widest row layout whose padding wastes at most 15% of the lanes (a
+  // 272-cell window row: 256-cell rows run 2 x 256 = 53% busy, 32-cell rows
+  // 9 x 32 = 94%); thin rows fall through to the 32-cell layout
+  for (int lz = 64; lz > 8; lz /= 4) {
+    const int seg = 4 * lz;
+    if (20 * kspan >= 17 * (cdiv(kspan, seg) * seg)) return lz;
+  }
+  return 8;
 }
 
 inline dim3 grid_c(const Box3& bu, int xchunk, int lz) {
