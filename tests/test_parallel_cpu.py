@@ -118,6 +118,12 @@ CASES = [
                                         use_metamaterials=True, scene="drude-sphere", sphere_radius=4,
                                         sphere_center=(32.0, 32.0, 36.0), pml_size=(4, 4, 4), hybrid_block=3),
      2, "z", 3),
+    # no PML: the core reaches the domain faces; the dispersive box straddles
+    # the rank boundary (per-row material ranges on both ranks)
+    ("hybrid-drude-nopml-xy4-b3", SchemeConfig(scheme="3d", size=(48, 44, 40), time_steps=8,
+                                               use_metamaterials=True, scene="drude-sphere", sphere_radius=5,
+                                               sphere_center=(24.0, 22.0, 20.0), hybrid_block=3),
+     4, "xy", 3),
     # temporal blocking: T steps per pass, T-deep ghosts exchanged every T steps
     ("tb2-xyz8", SchemeConfig(scheme="3d", size=(16, 18, 20), time_steps=9, scene="vacuum", use_fused=True,
                               time_block=2), 8, "xyz", 2),
