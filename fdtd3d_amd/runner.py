@@ -52,7 +52,12 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
     cfg = SchemeConfig.from_settings(settings)
     backend, device = resolve_backend(settings.backend, settings.device)
     if device.startswith("cuda"):
-        n = max(1, min(settings.numCudaGPUs, torch.cuda.device_count()))
+        avail = max(1, torch.cuda.device_count())
+        n = max(1, min(settings.numCudaGPUs, avail))
+        if world > 1 and settings.numCudaGPUs <= 1 and avail > 1:
+            # default --num-cuda-gpus 1 under torchrun on a multi-GPU node: one
+            # rank per GPU (RCCL refuses two ranks on one device)
+            n = avail
         local = int(os.environ.get("LOCAL_RANK", rank))
         dev_index = local % n
         torch.cuda.set_device(dev_index)
