@@ -116,6 +116,40 @@ __global__ void k_tfsf_apply(T* __restrict__ target, const long long* __restrict
   target[off[e]] += coef[e] * (w0[e] * inc[p] + w1[e] * inc[p + 1]);
 }
 
+// All whole-grid TF/SF tables of one half step in ONE launch (the hybrid
+// shell applies its corrections once per half step): up to TFM tables, each
+// starting on a fresh block (block-uniform table index), compact entries --
+// int32 target offset and line index, the weights folded into the
+// coefficient (a0 = coef w0, a1 = coef w1): 16 instead of 28 bytes per fp32
+// entry.  Different tables of one launch write different arrays or, for the
+// layers of one component, are applied by separate launches (the caller
+// groups them), so no two entries of a launch share a target.
+constexpr int TFM = 8;
+
+template <typename T>
+struct TfMulti {
+  T* target[TFM];
+  const int* off[TFM];
+  const int* i0[TFM];
+  const T* a0[TFM];
+  const T* a1[TFM];
+  int n[TFM];
+  int bstart[TFM + 1];
+  int count;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_tfsf_apply_many(TfMulti<T> m, const T* __restrict__ inc) {
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < m.count && b >= m.bstart[t + 1]) ++t;
+  const int e = (b - m.bstart[t]) * 256 + threadIdx.x;
+  if (e >= m.n[t]) return;
+  const int p = m.i0[t][e];
+  const int o = m.off[t][e];
+  m.target[t][o] += m.a0[t][e] * inc[p] + m.a1[t][e] * inc[p + 1];
+}
+
 // Scattered field of a TF/SF run (Scheme3D.cpp:2593-2747): inside the TF box
 // the total field minus the incident plane wave, interpolated from the 1D
 // line at the component's position (fp64 position and weights, the same
@@ -243,6 +277,28 @@ inline dim3 cell_grid(const Box3& b) {
       }                                                                                                       \
     }                                                                                                         \
     k_lincomb<T><<<cell_grid(b), dim3(64, 4), 0, (hipStream_t)s>>>(out, lt, nterms, ny, nz, b);               \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }                                                                                                           \
+  FDTD_API int fdtd_tfsf_apply_many_##SUF(void* const* P, const int* N, int count, const T* inc, void* s) {    \
+    if (count <= 0) return 0;                                                                                 \
+    if (count > TFM) return (int)hipErrorInvalidValue;                                                        \
+    TfMulti<T> m;                                                                                             \
+    int blocks = 0;                                                                                           \
+    for (int t = 0; t < TFM; ++t) {                                                                           \
+      const bool on = t < count;                                                                              \
+      m.target[t] = on ? (T*)P[5 * t] : nullptr;                                                              \
+      m.off[t] = on ? (const int*)P[5 * t + 1] : nullptr;                                                     \
+      m.i0[t] = on ? (const int*)P[5 * t + 2] : nullptr;                                                      \
+      m.a0[t] = on ? (const T*)P[5 * t + 3] : nullptr;                                                        \
+      m.a1[t] = on ? (const T*)P[5 * t + 4] : nullptr;                                                        \
+      m.n[t] = on ? N[t] : 0;                                                                                 \
+      m.bstart[t] = blocks;                                                                                   \
+      if (on) blocks += (int)cdiv(N[t], 256);                                                                 \
+    }                                                                                                         \
+    m.bstart[TFM] = blocks;                                                                                   \
+    m.count = count;                                                                                          \
+    if (blocks == 0) return 0;                                                                                \
+    k_tfsf_apply_many<T><<<blocks, 256, 0, (hipStream_t)s>>>(m, inc);                                         \
     FDTD_RETURN_LAUNCH_STATUS();                                                                              \
   }                                                                                                           \
   FDTD_API int fdtd_tfsf_apply_##SUF(T* target, const long long* off, const long long* i0, const T* w0,      \

@@ -699,10 +699,19 @@ class YeeScheme(BlockedStepping):
         if self.cfg.use_tfsf and tfsf_once:
             inc = self.hinc[p] if kind == "E" else self.einc[p]
             alloc = self.domain.allocated_global()
+            many = []
             for c in comps:
                 whole = self.local_box(c, alloc)
                 for tab in self.tfsf[c]:
-                    self.ops.tfsf_apply(F[c], tab, inc, whole)
+                    bb = getattr(tab, "bbox", None)
+                    if (hasattr(self.ops, "tfsf_apply_many") and bb is not None
+                            and all(whole[0][d] <= bb[0][d] and bb[1][d] <= whole[1][d] for d in range(3))):
+                        many.append((F[c], tab))  # every target inside the update range
+                    else:
+                        self.ops.tfsf_apply(F[c], tab, inc, whole)
+            if many:
+                # the rest of the half step's tables in one or two launches
+                self.ops.tfsf_apply_many(many, inc)
         if self.use_upml_chain:
             for c in comps:
                 self._upml_rotate(c, p)

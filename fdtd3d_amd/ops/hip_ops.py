@@ -582,6 +582,57 @@ class HipOps:
         _check(rc, "tfsf_apply")
         self.launches += 1
 
+    def _tfsf_compact(self, table):
+        """int32 offsets / line indices and folded weights (coef w0, coef w1)
+        of a correction table, built once (None past 2^31 elements)."""
+        cmp = getattr(table, "_compact", None)
+        if cmp is None:
+            if table.max_off >= 2 ** 31 - 1 or table.max_inc >= 2 ** 31 - 1:
+                table._compact = False
+                return None
+            c = table.coef.double()
+            cmp = (table.off.to(torch.int32).contiguous(), table.i0.to(torch.int32).contiguous(),
+                   (c * table.w0.double()).to(self.dtype).contiguous(), (c * table.w1.double()).to(self.dtype).contiguous())
+            table._compact = cmp
+        return cmp or None
+
+    def tfsf_apply_many(self, items, inc: torch.Tensor) -> None:
+        """Whole-grid TF/SF corrections of several (target, table) pairs in as
+        few launches as possible (generic_kernels.hip k_tfsf_apply_many, at most
+        8 tables a launch, the layers of one target in successive launches, in
+        order)."""
+        launches = []
+        for target, tab in items:
+            if tab.n == 0:
+                continue
+            if getattr(tab, "max_off", None) is None:
+                tab.max_off = int(tab.off.max())
+                tab.max_inc = int(tab.i0.max()) + 1
+            if tab.max_off >= target.numel() or tab.max_inc >= inc.numel():
+                raise HipError("TF/SF table reads or writes outside its arrays")
+            self._check_tensor(target)
+            cmp = self._tfsf_compact(tab)
+            if cmp is None:
+                self.tfsf_apply(target, tab, inc, ((0, 0, 0), tuple(target.shape)))
+                continue
+            ptr = target.data_ptr()
+            for L in launches:  # first fit: a launch never holds one target twice
+                if len(L) < 8 and all(t.data_ptr() != ptr for t, _, _ in L):
+                    L.append((target, tab, cmp))
+                    break
+            else:
+                launches.append([(target, tab, cmp)])
+        self._check_tensor(inc)
+        for L in launches:
+            P, N = [], []
+            for target, tab, cmp in L:
+                P += [target.data_ptr()] + [t.data_ptr() for t in cmp]
+                N.append(int(tab.n))
+            rc = self.fn("tfsf_apply_many")((c_vp * len(P))(*P), (c_int * len(N))(*N), c_int(len(L)), _ptr(inc),
+                                            _stream())
+            _check(rc, "tfsf_apply_many")
+            self.launches += 1
+
     def scattered(self, f: torch.Tensor, line: torch.Tensor, geo: Sequence[float], igeo: Sequence[int]) -> torch.Tensor:
         """Scattered field of a TF/SF run in one pass (generic_kernels.hip
         k_scattered): ``geo`` = m[3] zero[3] dir[3] L[3] R[3] proj shift,

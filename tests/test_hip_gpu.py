@@ -241,3 +241,34 @@ def test_drude_row_split_gpu(gpu, pml):
         scale = max(float(res[2][o].abs().max()) for o in res[2] if o[0] == c[0])
         assert float((res[0][c] - res[1][c]).abs().max()) <= 2e-5 * scale, (c, "rows vs whole box")
         assert float((res[0][c] - res[2][c]).abs().max()) <= 2e-5 * scale, (c, "rows vs fp64 oracle")
+
+
+def test_tfsf_apply_many_vs_tables(gpu):
+    """The merged TF/SF launch (int32 offsets, folded weights, first-fit
+    grouping: the layers of one component in successive launches) applies
+    the same corrections as one launch per table."""
+    cfg = SchemeConfig(scheme="3d", size=(40, 36, 44), time_steps=1, use_tfsf=True, scene="vacuum", dtype="f32",
+                       tfsf_size=(6, 7, 8), theta=35, phi=20, psi=10)
+    s = YeeScheme(cfg, make_ops("hip", None, gpu, torch.float32))
+    s.init_scheme()
+    s.init_grids()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    inc = torch.randn(s.einc[0].numel(), generator=g).to(gpu)
+    for kind, comps in (("E", s.e_comps), ("H", s.h_comps)):
+        base = {c: torch.randn(s.F[0][c].shape, generator=g).to(gpu) for c in comps}
+        a = {c: base[c].clone() for c in comps}
+        b = {c: base[c].clone() for c in comps}
+        items = []
+        for c in comps:
+            for tab in s.tfsf[c]:
+                s.ops.tfsf_apply(a[c], tab, inc, ((0, 0, 0), tuple(a[c].shape)))
+                items.append((b[c], tab))
+        assert len(items) > 3
+        n0 = s.ops.launches
+        s.ops.tfsf_apply_many(items, inc)
+        assert s.ops.launches - n0 < len(items)
+        torch.cuda.synchronize()
+        for c in comps:
+            d = float((a[c] - b[c]).abs().max())
+            assert d <= 1e-5 * float(base[c].abs().max()), (kind, c, d)
+            assert float((a[c] - base[c]).abs().max()) > 0  # corrections landed
