@@ -23,6 +23,7 @@
 // compiler wait on each load).
 
 #include "common.h"
+#include "vec4.h"
 
 namespace {
 
@@ -315,6 +316,116 @@ __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q
   }
 }
 
+// ---------------------------------------------------------------------------
+// float4 form of the non-dispersive chain (fp32, z rows of 4-cell groups):
+// each thread owns 4 consecutive z cells of one (y, x-run), 16-byte loads and
+// stores; per element the cell is a chain cell (its component's box), a
+// folded plain cell (pbox) or skipped.  A z-derivative neighbour comes from
+// the thread's own float4 plus one scalar load (guarded at the array ends).
+__device__ __forceinline__ float4 bcast4(float v) { return make_float4(v, v, v, v); }
+
+// a factored profile value along `axis` for the 4 cells (z: 4 values)
+__device__ __forceinline__ float4 prof4(const float* p, int axis, int i, int j, int k) {
+  if (axis == 2) return ld4(p, (size_t)k);
+  return bcast4(p[axis == 0 ? i : j]);
+}
+
+__device__ __forceinline__ void chain_v4(const ChainComp<float>& q, bool kind_e, const long long* stride, int i, int j,
+                                         int k, int nz, size_t off) {
+  unsigned mc = kmask(q.box, j, k), mp = kmask(q.pbox, j, k);
+  if (i < q.box.lo[0] || i >= q.box.hi[0]) mc = 0u;
+  if (i < q.pbox.lo[0] || i >= q.pbox.hi[0]) mp = 0u;
+  mp &= ~mc;
+  if ((mc | mp) == 0u) return;
+  const long long s0 = pick3(q.a0, stride[0], stride[1], stride[2]);
+  const long long s1 = pick3(q.a1, stride[0], stride[1], stride[2]);
+  const float4 x0 = ld4(q.s0, off), x1 = ld4(q.s1, off);
+  float4 y0, y1;
+  if (q.a0 != 2) {
+    y0 = ld4(q.s0, kind_e ? off - s0 : off + s0);
+  } else if (kind_e) {
+    y0 = make_float4(k > 0 ? q.s0[off - 1] : 0.f, x0.x, x0.y, x0.z);
+  } else {
+    y0 = make_float4(x0.y, x0.z, x0.w, k + 4 < nz ? q.s0[off + 4] : 0.f);
+  }
+  if (q.a1 != 2) {
+    y1 = ld4(q.s1, kind_e ? off - s1 : off + s1);
+  } else if (kind_e) {
+    y1 = make_float4(k > 0 ? q.s1[off - 1] : 0.f, x1.x, x1.y, x1.z);
+  } else {
+    y1 = make_float4(x1.y, x1.z, x1.w, k + 4 < nz ? q.s1[off + 4] : 0.f);
+  }
+  const float4 E = ld4(q.E, off);
+  float4 D = bcast4(0.f), caD = D, cbD = D, caE = D, ica = D, cbEa = D, ccEa = D, cell = bcast4(1.f);
+  if (mc) {
+    D = ld4(q.D, off);
+    caD = prof4(q.caD, q.aD, i, j, k);
+    cbD = prof4(q.cbD, q.aD, i, j, k);
+    caE = prof4(q.caE, q.aA, i, j, k);
+    ica = prof4(q.ica, q.aA, i, j, k);
+    cbEa = prof4(q.cbEa, q.aB, i, j, k);
+    ccEa = prof4(q.ccEa, q.aB, i, j, k);
+    if (q.cell) cell = ld4(q.cell, off);
+  }
+  const float4 pc = mp ? (q.pcell ? ld4(q.pcell, off) : bcast4(q.pcb)) : bcast4(0.f);
+  float4 Dn = D, En = E;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float d0 = kind_e ? (f4(x0, e) - f4(y0, e)) : (f4(y0, e) - f4(x0, e));
+    const float d1 = kind_e ? (f4(x1, e) - f4(y1, e)) : (f4(y1, e) - f4(x1, e));
+    const float curl = (q.sg0 > 0 ? d0 : -d0) + (q.sg1 > 0 ? d1 : -d1);
+    if (mc & (1u << e)) {
+      const float dn = f4(caD, e) * f4(D, e) + f4(cbD, e) * curl;
+      f4set(Dn, e, dn);
+      f4set(En, e, f4(caE, e) * f4(E, e) +
+                       q.s * f4(cell, e) * f4(ica, e) * (f4(cbEa, e) * dn + f4(ccEa, e) * f4(D, e)));
+    } else if (mp & (1u << e)) {
+      f4set(En, e, f4(E, e) + f4(pc, e) * curl);
+    }
+  }
+  st4m(q.Dn, off, Dn, mc);
+  st4m(q.E, off, En, mc | mp);
+}
+
+__global__ __launch_bounds__(256) void k_chain3d_v4(ChainComp<float> q0, ChainComp<float> q1, ChainComp<float> q2,
+                                                    int kind_e, int ny, int nz, Box3 U) {
+  const int W4 = (U.hi[2] - U.lo[2]) >> 2;
+  const int H = U.hi[1] - U.lo[1];
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)W4 * H) return;
+  const int j = U.lo[1] + (int)(idx / W4);
+  const int k = U.lo[2] + 4 * (int)(idx % W4);
+  const int i0 = U.lo[0] + (int)blockIdx.y * CHX;
+  const int i1 = min(i0 + CHX, U.hi[0]);
+  const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
+#pragma unroll 1
+  for (int i = i0; i < i1; ++i) {
+    const size_t off = ((size_t)i * ny + j) * nz + k;
+    chain_v4(q0, kind_e != 0, stride, i, j, k, nz, off);
+    chain_v4(q1, kind_e != 0, stride, i, j, k, nz, off);
+    chain_v4(q2, kind_e != 0, stride, i, j, k, nz, off);
+  }
+}
+
+// off by default: measured slower than one cell per thread (512^3 UPML + TF/SF
+// 58.1k vs 71.3k, Drude + UPML 46.2k vs 55.4k Mcells/s): A-B knob (fdtd_set_chain_v4)
+static bool g_chain_v4 = false;
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// every array the float4 chain touches 16-byte aligned (z rows of nz % 4 == 0)
+template <typename T>
+bool chain_v4_ok(const ChainComp<T>* q, int nz) {
+  if (sizeof(T) != 4 || (nz & 3) != 0 || !g_chain_v4) return false;
+  for (int c = 0; c < 3; ++c) {
+    const void* ps[] = {q[c].E, q[c].Dn, q[c].D, q[c].s0, q[c].s1, q[c].caD, q[c].cbD, q[c].caE, q[c].ica,
+                        q[c].cbEa, q[c].ccEa, q[c].cell, q[c].pcell};
+    for (const void* p : ps)
+      if (p && !al16(p)) return false;
+  }
+  return true;
+}
+
 constexpr int CP_PER = 24;  // pointers per component
 constexpr int CI_PER = 19;  // ints per component
 
@@ -374,6 +485,19 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
   if (box_empty(U)) return 0;
   for (int c = 0; c < 3; ++c)
     if (!box_empty(q[c].box) && (q[c].cell != nullptr) != cell) return (int)hipErrorInvalidValue;
+  if constexpr (sizeof(T) == 4) {
+    if (!drude && chain_v4_ok(q, nz)) {
+      // 4-cell z groups: the union box widened to whole groups (per-element
+      // box tests keep the cells outside every component's boxes untouched)
+      Box3 U4 = U;
+      U4.lo[2] &= ~3;
+      U4.hi[2] = (U4.hi[2] + 3) & ~3;
+      const long long groups = (long long)((U4.hi[2] - U4.lo[2]) >> 2) * (U4.hi[1] - U4.lo[1]);
+      dim3 g4(cdiv(groups, 256), cdiv(U4.hi[0] - U4.lo[0], CHX));
+      k_chain3d_v4<<<g4, 256, 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U4);
+      FDTD_RETURN_LAUNCH_STATUS();
+    }
+  }
   const long long cells = (long long)(U.hi[2] - U.lo[2]) * (U.hi[1] - U.lo[1]);
   dim3 grid(cdiv(cells, 256), cdiv(U.hi[0] - U.lo[0], CHX));
 #define CH_LAUNCH(D, C) k_chain3d<T, D, C><<<grid, 256, 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U, rr)
@@ -405,6 +529,8 @@ FDTD_API int fdtd_chain3d_f64(const void* const* P, const double* S, const int* 
                               int nz, void* s) {
   return launch_chain<double>(P, S, I, drude, kind_e, ny, nz, RowRanges{nullptr, 0, 0, 0, 0}, (hipStream_t)s);
 }
+
+FDTD_API void fdtd_set_chain_v4(int on) { g_chain_v4 = on != 0; }
 
 // Dispersive launch over a box with no PML (sigma = 0): rows = int2 (z0, z1)
 // per (x, y) of [R[0], R[0] + R[2]) x [R[1], R[1] + R[3]); cells outside their

@@ -274,3 +274,39 @@ def test_tfsf_apply_many_vs_tables(gpu):
             assert corr > 0  # corrections landed
             # fp32 round-off of (coef w0) inc0 + (coef w1) inc1 vs coef (w0 inc0 + w1 inc1)
             assert d <= 1e-5 * max(corr, float(base[c].abs().max())), (kind, c, d, corr)
+
+
+@pytest.mark.parametrize("hb", [1, 3])
+def test_chain_v4_vs_scalar(gpu, hb):
+    """Non-dispersive UPML chain in 4-cell z groups (chain_kernels.hip
+    k_chain3d_v4, per-element box / folded-plain masks) vs the one-cell-per-
+    thread kernel, stepped (z slabs widened to 32-cell rows) and hybrid (thin
+    plain boxes folded into the z slab launches), from random fields, and vs
+    the fp64 torch oracle."""
+    from fdtd3d_amd.ops.hip_ops import load_library
+    lib = load_library()
+    cfg = SchemeConfig(scheme="3d", size=(72, 64, 128), time_steps=7, use_pml=True, use_tfsf=True, scene="vacuum",
+                       pml_size=(5, 6, 7), tfsf_size=(8, 8, 8), theta=30, phi=20, psi=10, dtype="f32",
+                       hybrid_block=hb)
+    res = []
+    try:
+        for backend, dev, dt, v4 in (("hip", gpu, torch.float32, 1), ("hip", gpu, torch.float32, 0),
+                                     ("torch", "cpu", torch.float64, 1)):
+            lib.fdtd_set_chain_v4(v4)
+            c = dataclasses.replace(cfg, dtype="f32" if dt == torch.float32 else "f64",
+                                    hybrid_block=hb if backend == "hip" else 1)
+            s = YeeScheme(c, make_ops(backend, None, dev, dt))
+            s.init_scheme()
+            s.init_grids()
+            s.randomize_fields(seed=4)
+            s.perform_steps()
+            if backend == "hip":
+                torch.cuda.synchronize()
+                assert (s.hybrid is not None) == (hb > 1)
+            res.append({k: s.F[0][k].double().cpu() for k in s.comps})
+    finally:
+        lib.fdtd_set_chain_v4(0)  # the library default (measured slower, kept as a knob)
+    for k in res[0]:
+        scale = max(float(res[2][o].abs().max()) for o in res[2] if o[0] == k[0])
+        assert float((res[0][k] - res[1][k]).abs().max()) <= 2e-5 * scale, (k, "v4 vs scalar")
+        assert float((res[0][k] - res[2][k]).abs().max()) <= 2e-5 * scale, (k, "v4 vs fp64 oracle")
