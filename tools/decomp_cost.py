@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--topology", type=int, nargs=3, default=None, help="force a rank grid (e.g. 4 2 1)")
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--thin", type=int, default=1, help="thin y shells on the single-row kernel (T <= 4)")
+    ap.add_argument("--physics", default="vacuum", choices=("vacuum", "cpml-tfsf", "upml-tfsf", "cpml"),
+                    help="non-vacuum: hybrid passes (blocked owned core + deep-halo stepped shell), per-GPU "
+                         "Mcells/s only")
     a = ap.parse_args()
     import torch
     from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
@@ -63,12 +66,18 @@ def main():
         rank = max(range(core.used_procs), key=nn)
     dom = core.domain(rank, T, align_z=4)
     cfg = SchemeConfig(scheme="3d", size=size, scene="vacuum", dtype="f32", use_fused=True, time_block=T)
+    if a.physics != "vacuum":
+        cfg = SchemeConfig(scheme="3d", size=size, scene="vacuum", dtype="f32", use_pml=True,
+                           pml_type="upml" if a.physics.startswith("upml") else "cpml",
+                           use_tfsf=a.physics.endswith("tfsf"), hybrid_block=T)
 
     def timed(domain, halo):
         s = YeeScheme(cfg, make_ops("hip", None, "cuda:0", torch.float32), domain, halo)
         s.ops.tb_thin_single_row = bool(a.thin)
         s.init_scheme()
         s.init_grids()
+        if a.physics != "vacuum":
+            print("hybrid pass: %s (ghost depth %d)" % (s.hybrid is not None, s.domain.buffer_size if s.domain else 0))
         s.advance(2 * T)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -83,6 +92,13 @@ def main():
     t_dec = timed(dom, halo)
     own = dom.owned_shape
     cells = own[0] * own[1] * own[2]
+    if a.physics != "vacuum":
+        glob = size[0] * size[1] * size[2]
+        print("%s %s: topology %s rank %d owned %s neighbours %s: decomposed step %.3f ms, %.0f Mcells/s per "
+              "GPU (x %d GPUs = %.0f if the exchange hides under the interior pass)"
+              % (a.physics, "x".join(map(str, size)), "x".join(map(str, core.topology)), rank, own, dom.neighbors,
+                 t_dec * 1e3, cells / t_dec / 1e6, a.world, glob / t_dec / 1e6))
+        return
     # serial reference on the rank's owned extent
     from fdtd3d_amd.parallel.domain import Domain
     cfg_serial = SchemeConfig(scheme="3d", size=tuple(own), scene="vacuum", dtype="f32", use_fused=True,
