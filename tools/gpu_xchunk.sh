@@ -13,3 +13,7 @@ for sz in "1024 1024 1024" "2048 1024 1024" "512 512 512" "512 512 1024"; do
 done
 v=$(timeout -k 10 150 python bench.py --fp64-companion off --steps 40 --size 512 512 1024 --tb-xchunk 512 2>/dev/null | val) || exit 1
 echo "[512 512 1024, 512-plane chunks] $v"
+for args in "" "--tb-xchunk 256" "--tb-xchunk 128"; do
+  v=$(timeout -k 10 150 python bench.py --dtype f64 --fp64-companion off --steps 24 $args 2>/dev/null | val) || exit 1
+  echo "[f64 1024^3 $args] $v"
+done
