@@ -860,7 +860,7 @@ class HipOps:
     def tb_max_steps(self) -> int:
         return TB_MAX_STEPS if self.dtype == torch.float32 else TB_MAX_STEPS_F64
 
-    tb_xchunk = 0
+    tb_xchunk = int(os.environ.get("FDTD3D_TB_XCHUNK", "0"))  # x planes per blocked workgroup: 0 automatic
     tb_vec = 0  # lane width of the blocked kernel: 0 auto (4 for T <= 2, 2 above), 2 or 4
     tb_rows = 0  # grid rows per wave: 0 auto (1), 1 or 2
     tb_xcd = 0  # XCD-aware tile order (off: measured no gain)
