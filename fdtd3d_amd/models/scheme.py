@@ -483,6 +483,10 @@ class YeeScheme(BlockedStepping):
                                "prof": dict(st["prof"], s=s_pl, cell=cell_pl)}
             self.upml[c] = st
         self._init_chain_regions(prof)
+        if cfg.use_metamaterials and getattr(self.ops, "chain_rows", False) and cfg.scheme == "3d":
+            # row tables built now (host syncs), never under a HIP graph capture
+            for kind in ("E", "H"):
+                self._drude_rows(kind)
 
     def _bbox_global(self, mask: torch.Tensor) -> Box:
         """Global bounding box of the True cells of a local mask (empty box
