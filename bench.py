@@ -81,6 +81,8 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
     from fdtd3d_amd.parallel.halo import HaloExchanger
 
     size = tuple(a.size)
+    if device.startswith("cuda"):
+        torch.cuda.reset_peak_memory_stats()
     T = a.time_block
     if T <= 0:
         # automatic (models/blocking.py auto_time_block; the torch backend
@@ -136,6 +138,9 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
         halo.reset_timing()
         halo.timing = True
         halo.bytes_sent = 0
+        # per-pass main-stream breakdown (interior / exchange wait / shell)
+        from fdtd3d_amd.models.blocking import PassTimer
+        scheme.pass_timer = PassTimer(scheme.device)
     sync()
     t0 = time.perf_counter()
     scheme.advance(a.steps)
@@ -150,14 +155,29 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
     if halo is not None:
         halo_ms, nex = halo.exchange_ms(), halo.exchanges
         halo.timing = False
+    per_rank = []
     if world > 1:
-        t = torch.tensor([dt, halo_ms / max(1, nex), halo_ms / max(1, nex)], dtype=torch.float64,
-                         device=device if device.startswith("cuda") else "cpu")
+        tdev = device if device.startswith("cuda") else "cpu"
+        t = torch.tensor([dt, halo_ms / max(1, nex), halo_ms / max(1, nex)], dtype=torch.float64, device=tdev)
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t)
         dt = float(tmax[0].item())
         halo_max, halo_mean = float(tmax[1].item()), float(t[2].item()) / world
+        # every rank's pass breakdown, so an 8-GPU record says which rank
+        # waited on its exchange and for how long
+        bd = scheme.pass_timer.summary() if scheme.pass_timer is not None else {}
+        scheme.pass_timer = None
+        mine = torch.tensor([bd.get("passes", 0), bd.get("interior_ms", 0.0), bd.get("exchange_wait_ms", 0.0),
+                             bd.get("shell_ms", 0.0), halo_ms / max(1, nex)], dtype=torch.float64, device=tdev)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        for r, v in enumerate(allv):
+            v = v.cpu().tolist()
+            n = max(1.0, v[0])
+            per_rank.append({"rank": r, "passes": int(v[0]), "interior_ms": round(v[1] / n, 4),
+                             "exchange_wait_ms": round(v[2] / n, 4), "shell_ms": round(v[3] / n, 4),
+                             "exchange_ms": round(v[4], 4)})
     else:
         halo_max = halo_mean = 0.0
     energy = allsum(scheme.field_energy())
@@ -172,6 +192,8 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
         "halo_ms_per_pass_max": halo_max,
         "halo_ms_per_pass_mean": halo_mean,
         "exchanges": nex,
+        "per_rank": per_rank,
+        "max_mem_gb": (torch.cuda.max_memory_allocated() / 1e9) if device.startswith("cuda") else 0.0,
     }
     del scheme, halo, ops
     if device.startswith("cuda"):
@@ -281,7 +303,14 @@ def main(argv=None) -> int:
             },
             "checksum": {"energy0": res["energy0"], "energy": res["energy"],
                          "steps_total": a.warmup + a.steps},
+            "max_mem_gb_rank0": round(res["max_mem_gb"], 2),
         }
+        if res["per_rank"]:
+            # ms per pass on each rank's main stream: interior (overlapped with
+            # the exchange on the side stream), exchange_wait (the part of the
+            # exchange the interior did not hide), shell; exchange_ms = the
+            # exchange's own duration on the side stream
+            out["per_rank"] = res["per_rank"]
         if fp64 is not None:
             if "error" in fp64:
                 out["fp64"] = fp64

@@ -1,0 +1,550 @@
+// Single-step fused E+H passes over the SHELL of a hybrid pass (fp32, 3D).
+//
+// A hybrid pass (models/blocking.py) advances the core of the grid -- every
+// cell at least PML + T + 2 (TF/SF box + T + 3 with a plane wave) away from
+// the faces -- T steps at a time through the temporally blocked kernel
+// (yee3d_tb.hip), and the shell around it one step at a time over windows
+// that shrink by one cell per step (the deep-halo rule of the reference's
+// ParallelGrid.cpp:2365-2489, applied to the core boundary).  This kernel
+// is that single step: E^{n+1} and H^{n+1} in ONE pass (read E^n, H^n once,
+// write both once: 48 B/cell against 72 B for separate E and H kernels),
+// over a work list of shell boxes in one launch, with the CPML convolution
+// terms (models/cpml.py) of the absorbing layers folded in.  The reference
+// updates its UPML cells with three sweeps per component
+// (Scheme3D.cpp:266-416); its CUDA path has no absorbing layer at all.
+//
+// Tile: 16 waves x 64 lanes.  Lanes run along z: LW = 64 lanes per grid row,
+// or LW = 32 (two grid rows per wave) for boxes at most 30 cells deep in z --
+// the z shell slabs -- where 64-lane rows would leave half the lanes idle.
+// Every lane group carries R = 2 adjacent y rows in registers; the first /
+// last row of a group exchanges its y neighbours through a double-buffered
+// LDS slot (one barrier per plane); z neighbours come through DPP lane
+// shifts (lanes shifted in across a row-group boundary are halo lanes).  The
+// workgroup streams x: trip X loads plane X, computes E^{n+1}(X) from H^n(X),
+// H^n(X-1) (carried) and H^{n+1}(X-1) from E^{n+1}(X-1) (carried) and
+// E^{n+1}(X).  One halo lane / row per side: halo cells are recomputed by the
+// neighbour tile, so the CPML psi of a step is read from one copy and written
+// to the other (models/cpml.py flip).
+//
+// CPML (models/cpml.py: psi = b psi + c d, curl += sign ((1/kappa - 1) d +
+// psi)) is specialised per launch by the set AX of axes whose absorbing slab
+// the launch's boxes touch (bit 0 x, 1 y, 2 z): a face slab carries 4 of the
+// 12 terms, the interior band none; edges and corners take all axes.  A
+// term's slab side is wave-uniform along x (plane) and, for 64-lane rows,
+// along y (row); along z it is per lane.  Loads past a buffer descriptor read
+// 0 and stores past it are dropped: lanes outside a slab use such offsets.
+//
+// TF/SF corrections are NOT in this kernel: they are additive, so the host
+// adds Cb g to the E targets of the input buffer before the pass and Db g to
+// the H targets of the output after it (models/blocking.py _hybrid2_step).
+
+#include "common.h"
+
+namespace {
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ __forceinline__ float sh_up(float v) {  // lane i <- lane i-1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float sh_dn(float v) {  // lane i <- lane i+1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ Rsrc mk_rs(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ Rsrc plane_rs(const float* base, int x, int nx, size_t plane) {
+  const bool in = x >= 0 && x < nx;
+  return mk_rs(base + (size_t)(in ? x : 0) * plane, in ? (unsigned)(plane * 4) : 0u);
+}
+__device__ __forceinline__ float ldf(Rsrc r, unsigned off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void stf(Rsrc r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+
+constexpr unsigned kBad = 0xF0000000u;  // byte offset past every descriptor
+
+// one (component, term axis) of the CPML: the layout of models/cpml.py
+// device_table (and yee3d_tb.hip CpmlDev)
+struct ShTerm {
+  const float* psi[2];  // low / high slab, read (time n)
+  float* out[2];        // written (time n + 1)
+  int lo[2], hi[2];     // slab ranges along the axis (local; z padded to float4 groups)
+  const float* b;
+  const float* c;
+  const float* k;       // 1 / kappa - 1
+};
+struct ShCpml {
+  ShTerm t[6][3];  // [Ex Ey Ez Hx Hy Hz][axis]
+};
+
+// curl terms of each component: (axis of term 0, axis of term 1); the curl is
+// +d0 - d1 (Ex = dHz/dy - dHy/dz, ..., Hx = dEy/dz - dEz/dy, ...)
+__device__ constexpr int kAx[6][2] = {{1, 2}, {2, 0}, {0, 1}, {2, 1}, {0, 2}, {1, 0}};
+
+constexpr int SH_MAX = 64;  // boxes per launch
+struct ShList {
+  int n;
+  int first[SH_MAX + 1];  // first workgroup of each box; first[n] = grid size
+  int tz[SH_MAX], ty[SH_MAX], xc[SH_MAX];
+  Box3 box[SH_MAX];
+};
+
+constexpr int SNW = 16;  // waves per workgroup
+constexpr int SR = 2;    // rows per lane group
+
+template <int AX, bool KAP, int LW>
+__global__ __launch_bounds__(64 * SNW) void k_shell1(
+    const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
+    const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
+    float* __restrict__ exo, float* __restrict__ eyo, float* __restrict__ ezo, float* __restrict__ hxo,
+    float* __restrict__ hyo, float* __restrict__ hzo, float cb, float db, int nx, int ny, int nz, Box3 bex,
+    Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, ShList L, int src_i, int src_j, int src_k, int src_comp,
+    float src_v, const ShCpml* __restrict__ cp) {
+  constexpr int G = 64 / LW;         // lane groups (grid rows) per wave
+  constexpr int NS = SNW * G;        // lane groups per workgroup
+  constexpr int ROWS = NS * SR;      // y rows per tile
+  constexpr bool CPX = AX & 1, CPY = AX & 2, CPZ = AX & 4;
+  __shared__ float sX[2][4][NS][LW];
+  __shared__ ShTerm sT[AX ? 18 : 1];
+  const int lane = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);
+  const int g = LW == 64 ? 0 : lane / LW;
+  const int li = LW == 64 ? lane : lane % LW;
+  const int slot = w * G + g;
+  if constexpr (AX != 0) {
+    const unsigned* src = (const unsigned*)cp;
+    unsigned* dst = (unsigned*)sT;
+    for (int q = lane + 64 * w; q < (int)(sizeof(ShTerm) * 18 / 4); q += 64 * SNW) dst[q] = src[q];
+    __syncthreads();
+  }
+  // ---- box and tile of this workgroup (wave-uniform)
+  // (static indices only: a dynamic index into the by-value list would copy
+  // it to scratch)
+  const int bid = blockIdx.x;
+  Box3 O = L.box[0];
+  int first = 0, ntz = L.tz[0], nty = L.ty[0], xc = L.xc[0];
+#pragma unroll
+  for (int q = 1; q < SH_MAX; ++q)
+    if (q < L.n && bid >= L.first[q]) {
+      O = L.box[q];
+      first = L.first[q];
+      ntz = L.tz[q];
+      nty = L.ty[q];
+      xc = L.xc[q];
+    }
+  const int loc = bid - first;
+  const int tz = loc % ntz, ty = (loc / ntz) % nty, tx = loc / (ntz * nty);
+  const int i0 = O.lo[0] + tx * xc, i1 = min(i0 + xc, O.hi[0]);
+  const int kb = O.lo[2] - 1 + (LW - 2) * tz + li;
+  const int jr0 = O.lo[1] - 1 + (ROWS - 2) * ty + slot * SR;
+  const bool kin = kb >= 0 && kb < nz;
+  const size_t plane = (size_t)ny * nz;
+  unsigned roff[SR];
+  unsigned mbits = 0;  // bit r*7 + n: row r inside update box n (6 = stored)
+  const Box3* bx[7] = {&bex, &bey, &bez, &bhx, &bhy, &bhz, &O};
+#pragma unroll
+  for (int r = 0; r < SR; ++r) {
+    const int j = jr0 + r, t = slot * SR + r;
+    const bool ok = kin && j >= 0 && j < ny;
+    roff[r] = ok ? (unsigned)(j * nz + kb) * 4u : kBad;
+    const bool own = ok && li >= 1 && li < LW - 1 && t >= 1 && t < ROWS - 1;
+#pragma unroll
+    for (int n = 0; n < 7; ++n) {
+      const Box3& b = *bx[n];
+      const bool in = (n < 6 ? ok : own) && j >= b.lo[1] && j < b.hi[1] && kb >= b.lo[2] && kb < b.hi[2];
+      mbits |= (in ? 1u : 0u) << (r * 7 + n);
+    }
+  }
+  const int rdn = slot > 0 ? slot - 1 : 0;
+  const int rup = slot < NS - 1 ? slot + 1 : NS - 1;
+  auto coef = [&](int n, int r, int p, float sc) -> float {
+    const Box3& b = *bx[n];
+    const bool in = (unsigned)(p - b.lo[0]) < (unsigned)(b.hi[0] - b.lo[0]) && ((mbits >> (r * 7 + n)) & 1u);
+    return in ? sc : 0.f;
+  };
+
+  // ---- CPML: per-lane z offsets / profiles, per-row y offsets (tile constants)
+  // E terms (n < 3) sit at plane X, H terms at X - 1.
+  // y slab psi: ((i w + j - lo) nz + k); z slab psi: ((i ny + j) w + k - lo)
+  unsigned yoff[2][2][SR], zoff[2][2][SR];  // [kind][side][row]
+  bool yany[2][2] = {{false, false}, {false, false}}, zany[2][2] = {{false, false}, {false, false}};
+  float zb[4], zc[4], zk[4];                // z terms Ex.1 Ey.0 Hx.0 Hy.1: profile at this lane
+  if constexpr (CPY) {
+#pragma unroll
+    for (int kd = 0; kd < 2; ++kd) {
+      const ShTerm& tm = sT[(kd == 0 ? 0 : 3) * 3 + 1];  // Ex / Hx y terms define the slab rows of the kind
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+          const int j = jr0 + r;
+          const bool in = tm.psi[sd] && kin && j >= tm.lo[sd] && j < tm.hi[sd];
+          yoff[kd][sd][r] = in ? (unsigned)((j - tm.lo[sd]) * nz + kb) * 4u : kBad;
+          any |= in;
+        }
+        yany[kd][sd] = __any(any);
+      }
+    }
+  }
+  if constexpr (CPZ) {
+#pragma unroll
+    for (int kd = 0; kd < 2; ++kd) {
+      const ShTerm& tm = sT[(kd == 0 ? 0 : 3) * 3 + 2];  // Ex / Hx z terms
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        const bool in = tm.psi[sd] && kin && kb >= tm.lo[sd] && kb < tm.hi[sd];
+        const int wd = tm.hi[sd] - tm.lo[sd];
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+          const int j = jr0 + r;
+          zoff[kd][sd][r] = in && j >= 0 && j < ny ? (unsigned)(j * wd + kb - tm.lo[sd]) * 4u : kBad;
+        }
+        zany[kd][sd] = __any(in);
+      }
+    }
+    const int zn[4] = {0, 1, 3, 4};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const ShTerm& tm = sT[zn[q] * 3 + 2];
+      const bool in = kin && ((tm.psi[0] && kb >= tm.lo[0] && kb < tm.hi[0]) ||
+                              (tm.psi[1] && kb >= tm.lo[1] && kb < tm.hi[1]));
+      zb[q] = in ? tm.b[kb] : 1.f;
+      zc[q] = in ? tm.c[kb] : 0.f;
+      zk[q] = in && KAP ? tm.k[kb] : 0.f;
+    }
+  }
+
+  // psi of term (n, t) on plane pl, row r: descriptor of the side that holds
+  // this cell (x: by plane, y / z: both sides, offsets select) -- loaded into
+  // ps[...] before the trip's field prefetch, updated and stored after use
+  auto psi_load = [&](int n, int t, int pl, int r) -> float {
+    const int a = kAx[n][t];
+    const ShTerm& tm = sT[n * 3 + a];
+    const int kd = n < 3 ? 0 : 1;
+    float v = 0.f;
+    if (pl < 0 || pl >= nx) return 0.f;
+    if (a == 0) {
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+        if (tm.psi[sd] && pl >= tm.lo[sd] && pl < tm.hi[sd])
+          v = ldf(mk_rs(tm.psi[sd] + (size_t)(pl - tm.lo[sd]) * plane, (unsigned)(plane * 4)), roff[r]);
+    } else if (a == 1) {
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+        if (yany[kd][sd]) {
+          const size_t pp = (size_t)(tm.hi[sd] - tm.lo[sd]) * nz;
+          v += ldf(mk_rs(tm.psi[sd] + (size_t)pl * pp, (unsigned)(pp * 4)), yoff[kd][sd][r]);
+        }
+    } else {
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+        if (zany[kd][sd]) {
+          const size_t pp = (size_t)ny * (tm.hi[sd] - tm.lo[sd]);
+          v += ldf(mk_rs(tm.psi[sd] + (size_t)pl * pp, (unsigned)(pp * 4)), zoff[kd][sd][r]);
+        }
+    }
+    return v;
+  };
+  // psi update of term (n, t) at plane pl, row r from the raw difference d:
+  // returns the curl correction, stores the new psi for stored cells of the
+  // component's update box
+  auto psi_step = [&](int n, int t, int pl, int r, float ps, float d) -> float {
+    const int a = kAx[n][t];
+    const ShTerm& tm = sT[n * 3 + a];
+    const int kd = n < 3 ? 0 : 1;
+    const bool st = ((mbits >> (r * 7 + 6)) & 1u) && ((mbits >> (r * 7 + n)) & 1u) &&
+                    (unsigned)(pl - bx[n]->lo[0]) < (unsigned)(bx[n]->hi[0] - bx[n]->lo[0]);
+    float b = 1.f, c = 0.f, k = 0.f;
+    float r_ = 0.f;
+    if (a == 0) {
+      if (pl < 0 || pl >= nx) return 0.f;
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+        if (tm.psi[sd] && pl >= tm.lo[sd] && pl < tm.hi[sd]) {
+          b = tm.b[pl];
+          c = tm.c[pl];
+          if (KAP) k = tm.k[pl];
+          const float pn = b * ps + c * d;
+          stf(mk_rs(tm.out[sd] + (size_t)(pl - tm.lo[sd]) * plane, (unsigned)(plane * 4)), st ? roff[r] : kBad, pn);
+          r_ = k * d + pn;
+        }
+      return r_;
+    } else if (a == 1) {
+      const int j = jr0 + r;
+      bool any = false;
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) any |= yany[kd][sd];
+      if (!any) return 0.f;
+      const bool in = (tm.psi[0] && j >= tm.lo[0] && j < tm.hi[0]) || (tm.psi[1] && j >= tm.lo[1] && j < tm.hi[1]);
+      if (in) {
+        b = tm.b[j];
+        c = tm.c[j];
+        if (KAP) k = tm.k[j];
+      }
+      const float pn = b * ps + c * d;
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+        if (yany[kd][sd]) {
+          const size_t pp = (size_t)(tm.hi[sd] - tm.lo[sd]) * nz;
+          stf(mk_rs(tm.out[sd] + (size_t)pl * pp, (unsigned)(pp * 4)), st ? yoff[kd][sd][r] : kBad, pn);
+        }
+      return in ? k * d + pn : 0.f;
+    } else {
+      const int q = n == 0 ? 0 : (n == 1 ? 1 : (n == 3 ? 2 : 3));
+      bool any = false;
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) any |= zany[kd][sd];
+      if (!any) return 0.f;
+      const float pn = zb[q] * ps + zc[q] * d;
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+        if (zany[kd][sd]) {
+          const size_t pp = (size_t)ny * (tm.hi[sd] - tm.lo[sd]);
+          stf(mk_rs(tm.out[sd] + (size_t)pl * pp, (unsigned)(pp * 4)), st ? zoff[kd][sd][r] : kBad, pn);
+        }
+      return zk[q] * d + pn;  // 0 off the slab (b 1, c 0, k 0, psi 0)
+    }
+  };
+  // which terms this launch carries: term (n, t) iff its axis is in AX
+  auto term_on = [](int n, int t) -> bool { return (AX >> kAx[n][t]) & 1; };
+
+  float Hp[SR][3], Ep[SR][3];  // H^n(X-1) and E^{n+1}(X-1)
+#pragma unroll
+  for (int r = 0; r < SR; ++r)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) Hp[r][q] = Ep[r][q] = 0.f;
+  float Hn_[SR][3], En_[SR][3];  // next plane (prefetched)
+  auto load_plane = [&](int X, float (*H)[3], float (*E)[3]) {
+    const Rsrc a = plane_rs(hxi, X, nx, plane), b = plane_rs(hyi, X, nx, plane), c = plane_rs(hzi, X, nx, plane);
+    const Rsrc d = plane_rs(exi, X, nx, plane), e = plane_rs(eyi, X, nx, plane), f = plane_rs(ezi, X, nx, plane);
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      H[r][0] = ldf(a, roff[r]);
+      H[r][1] = ldf(b, roff[r]);
+      H[r][2] = ldf(c, roff[r]);
+      E[r][0] = ldf(d, roff[r]);
+      E[r][1] = ldf(e, roff[r]);
+      E[r][2] = ldf(f, roff[r]);
+    }
+  };
+  load_plane(i0 - 1, Hn_, En_);
+  int buf = 0;
+  for (int X = i0 - 1; X <= i1; ++X) {
+    float Hc[SR][3], Ec[SR][3];
+#pragma unroll
+    for (int r = 0; r < SR; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        Hc[r][q] = Hn_[r][q];
+        Ec[r][q] = En_[r][q];
+      }
+    // this trip's psi (before the prefetch: vmcnt retires in issue order)
+    float PS[6][2][SR];
+#pragma unroll
+    for (int n = 0; n < 6; ++n)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < SR; ++r) PS[n][t][r] = (AX && term_on(n, t)) ? psi_load(n, t, n < 3 ? X : X - 1, r) : 0.f;
+    load_plane(X + 1, Hn_, En_);
+    // y neighbours: H(X) of the group's last row for the group above, E^{n+1}(X-1)
+    // of its first row for the group below
+    sX[buf][0][slot][li] = Hc[SR - 1][2];
+    sX[buf][1][slot][li] = Hc[SR - 1][0];
+    sX[buf][2][slot][li] = Ep[0][0];
+    sX[buf][3][slot][li] = Ep[0][2];
+    __syncthreads();
+    const float hz_dn = sX[buf][0][rdn][li], hx_dn = sX[buf][1][rdn][li];
+    const float ex_up = sX[buf][2][rup][li], ez_up = sX[buf][3][rup][li];
+    buf ^= 1;
+    float En[SR][3];
+    // ---- E^{n+1} on plane X
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      const float hz_j = r == 0 ? hz_dn : Hc[r > 0 ? r - 1 : 0][2];
+      const float hx_j = r == 0 ? hx_dn : Hc[r > 0 ? r - 1 : 0][0];
+      const float hy_k = sh_up(Hc[r][1]), hx_k = sh_up(Hc[r][0]);
+      const float dxy = Hc[r][2] - hz_j, dxz = Hc[r][1] - hy_k;
+      const float dyz = Hc[r][0] - hx_k, dyx = Hc[r][2] - Hp[r][2];
+      const float dzx = Hc[r][1] - Hp[r][1], dzy = Hc[r][0] - hx_j;
+      float cx = dxy - dxz, cy = dyz - dyx, cz = dzx - dzy;
+      if constexpr (AX != 0) {
+        if (term_on(0, 0)) cx += psi_step(0, 0, X, r, PS[0][0][r], dxy);
+        if (term_on(0, 1)) cx -= psi_step(0, 1, X, r, PS[0][1][r], dxz);
+        if (term_on(1, 0)) cy += psi_step(1, 0, X, r, PS[1][0][r], dyz);
+        if (term_on(1, 1)) cy -= psi_step(1, 1, X, r, PS[1][1][r], dyx);
+        if (term_on(2, 0)) cz += psi_step(2, 0, X, r, PS[2][0][r], dzx);
+        if (term_on(2, 1)) cz -= psi_step(2, 1, X, r, PS[2][1][r], dzy);
+      }
+      En[r][0] = Ec[r][0] + coef(0, r, X, cb) * cx;
+      En[r][1] = Ec[r][1] + coef(1, r, X, cb) * cy;
+      En[r][2] = Ec[r][2] + coef(2, r, X, cb) * cz;
+      if (src_comp >= 0 && X == src_i && jr0 + r == src_j && kb == src_k) {
+        if (src_comp == 0) En[r][0] = src_v;
+        if (src_comp == 1) En[r][1] = src_v;
+        if (src_comp == 2) En[r][2] = src_v;
+      }
+    }
+    // ---- H^{n+1} on plane X - 1
+    float Hn[SR][3];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      const float ex_j = r == SR - 1 ? ex_up : Ep[r < SR - 1 ? r + 1 : r][0];
+      const float ez_j = r == SR - 1 ? ez_up : Ep[r < SR - 1 ? r + 1 : r][2];
+      const float ey_k = sh_dn(Ep[r][1]), ex_k = sh_dn(Ep[r][0]);
+      const float gxz = ey_k - Ep[r][1], gxy = ez_j - Ep[r][2];
+      const float gyx = En[r][2] - Ep[r][2], gyz = ex_k - Ep[r][0];
+      const float gzy = ex_j - Ep[r][0], gzx = En[r][1] - Ep[r][1];
+      float dx = gxz - gxy, dy = gyx - gyz, dz = gzy - gzx;
+      if constexpr (AX != 0) {
+        if (term_on(3, 0)) dx += psi_step(3, 0, X - 1, r, PS[3][0][r], gxz);
+        if (term_on(3, 1)) dx -= psi_step(3, 1, X - 1, r, PS[3][1][r], gxy);
+        if (term_on(4, 0)) dy += psi_step(4, 0, X - 1, r, PS[4][0][r], gyx);
+        if (term_on(4, 1)) dy -= psi_step(4, 1, X - 1, r, PS[4][1][r], gyz);
+        if (term_on(5, 0)) dz += psi_step(5, 0, X - 1, r, PS[5][0][r], gzy);
+        if (term_on(5, 1)) dz -= psi_step(5, 1, X - 1, r, PS[5][1][r], gzx);
+      }
+      Hn[r][0] = Hp[r][0] + coef(3, r, X - 1, db) * dx;
+      Hn[r][1] = Hp[r][1] + coef(4, r, X - 1, db) * dy;
+      Hn[r][2] = Hp[r][2] + coef(5, r, X - 1, db) * dz;
+    }
+    // ---- stores: E^{n+1}(X), H^{n+1}(X-1) of the tile's own cells
+    const bool se = X >= i0 && X < i1, sh = X - 1 >= i0 && X - 1 < i1;
+    const Rsrc rex = plane_rs(exo, X, nx, plane), rey = plane_rs(eyo, X, nx, plane), rez = plane_rs(ezo, X, nx, plane);
+    const Rsrc rhx = plane_rs(hxo, X - 1, nx, plane), rhy = plane_rs(hyo, X - 1, nx, plane);
+    const Rsrc rhz = plane_rs(hzo, X - 1, nx, plane);
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      const bool mo = (mbits >> (r * 7 + 6)) & 1u;
+      const unsigned oe = mo && se ? roff[r] : kBad, oh = mo && sh ? roff[r] : kBad;
+      stf(rex, oe, En[r][0]);
+      stf(rey, oe, En[r][1]);
+      stf(rez, oe, En[r][2]);
+      stf(rhx, oh, Hn[r][0]);
+      stf(rhy, oh, Hn[r][1]);
+      stf(rhz, oh, Hn[r][2]);
+    }
+#pragma unroll
+    for (int r = 0; r < SR; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        Hp[r][q] = Hc[r][q];
+        Ep[r][q] = En[r][q];
+      }
+  }
+}
+
+template <int AX, bool KAP, int LW>
+int launch_shell(const float* const* fi, float* const* fo, float cb, float db, int nx, int ny, int nz,
+                 const Box3* b, const ShList& L, const int* src, float sv, const ShCpml* cp, hipStream_t s) {
+  k_shell1<AX, KAP, LW><<<L.first[L.n], dim3(64, SNW), 0, s>>>(
+      fi[0], fi[1], fi[2], fi[3], fi[4], fi[5], fo[0], fo[1], fo[2], fo[3], fo[4], fo[5], cb, db, nx, ny, nz, b[0],
+      b[1], b[2], b[3], b[4], b[5], L, src[0], src[1], src[2], src[3], sv, cp);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <int AX>
+int launch_shell_ax(bool kap, int lw, const float* const* fi, float* const* fo, float cb, float db, int nx, int ny,
+                    int nz, const Box3* b, const ShList& L, const int* src, float sv, const ShCpml* cp,
+                    hipStream_t s) {
+  if (lw == 32)
+    return kap ? launch_shell<AX, true, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, s)
+               : launch_shell<AX, false, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, s);
+  return kap ? launch_shell<AX, true, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, s)
+             : launch_shell<AX, false, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, s);
+}
+
+}  // namespace
+
+// One step of the shell: reads fin (Ex Ey Ez Hx Hy Hz), writes fout on the
+// `nwin` output boxes `wins` (6 ints each, local; disjoint) -- cells of a box
+// outside a component's update box (`boxes`, 6 x 6 ints) are stored
+// unchanged.  `ax[w]` = CPML axes of box w (bit 0 x, 1 y, 2 z: the absorbing
+// slabs it may touch; 0 = none; any superset is correct), `cpml` = device
+// CpmlDev block of models/cpml.py (psi read from psi[p], written to the alt
+// copy; null when no box has CPML axes), `kap` = some 1/kappa - 1 is non-zero.
+// `src` = {i, j, k, comp} of a hard E point source (comp -1: none), value
+// `src_val`.  Boxes at most 30 cells deep in z run 32-lane rows.
+FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double cb, double db, int nx, int ny,
+                             int nz, const int* boxes, int nwin, const int* wins, const int* ax, const int* src,
+                             double src_val, const void* cpml, int kap, void* stream) {
+  if (nwin < 0 || (cpml == nullptr && nwin > 0)) {
+    for (int w = 0; w < nwin; ++w)
+      if (ax[w]) return (int)hipErrorInvalidValue;
+  }
+  Box3 b[6];
+  for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
+  const hipStream_t s = (hipStream_t)stream;
+  // group the boxes by (CPML class, lane width); classes: none, x, y, z, all
+  const int classes[5] = {0, 1, 2, 4, 7};
+  for (int ci = 0; ci < 5; ++ci) {
+    for (int lw : {64, 32}) {
+      ShList L;
+      L.n = 0;
+      long long work = 0;
+      Box3 pend[256];
+      int np = 0;
+      for (int wi = 0; wi < nwin; ++wi) {
+        const Box3 o = make_box(wins + 6 * wi);
+        if (box_empty(o)) continue;
+        const int a = ax[wi];
+        const int cls = a == 0 ? 0 : ((a == 1 || a == 2 || a == 4) ? a : 7);
+        if (cls != classes[ci]) continue;
+        const int zl = o.hi[2] - o.lo[2];
+        if ((zl <= 30) != (lw == 32)) continue;
+        if (np >= 256) return (int)hipErrorInvalidValue;
+        pend[np++] = o;
+      }
+      if (np == 0) continue;
+      const int ROWS = SNW * (64 / lw) * SR;
+      for (int q = 0; q < np; ++q) {
+        const Box3& o = pend[q];
+        work += (long long)cdiv(o.hi[2] - o.lo[2], lw - 2) * cdiv(o.hi[1] - o.lo[1], ROWS - 2) * (o.hi[0] - o.lo[0]);
+      }
+      // x chunk: about 1024 workgroups per launch, at least 16 planes (two
+      // re-read lead-in / drain planes per chunk)
+      int xc = (int)((work + 1023) / 1024);
+      xc = xc < 16 ? 16 : (xc > 512 ? 512 : xc);
+      int q = 0;
+      while (q < np) {
+        L.n = 0;
+        int first = 0;
+        while (q < np && L.n < SH_MAX) {
+          const Box3& o = pend[q++];
+          const int k = L.n++;
+          L.box[k] = o;
+          L.tz[k] = (int)cdiv(o.hi[2] - o.lo[2], lw - 2);
+          L.ty[k] = (int)cdiv(o.hi[1] - o.lo[1], ROWS - 2);
+          L.xc[k] = xc;
+          L.first[k] = first;
+          first += L.tz[k] * L.ty[k] * (int)cdiv(o.hi[0] - o.lo[0], xc);
+        }
+        L.first[L.n] = first;
+        const ShCpml* cp = (const ShCpml*)cpml;
+        int rc = 0;
+        switch (classes[ci]) {
+          case 0: rc = launch_shell_ax<0>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
+                                          (float)src_val, cp, s); break;
+          case 1: rc = launch_shell_ax<1>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
+                                          (float)src_val, cp, s); break;
+          case 2: rc = launch_shell_ax<2>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
+                                          (float)src_val, cp, s); break;
+          case 4: rc = launch_shell_ax<4>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
+                                          (float)src_val, cp, s); break;
+          default: rc = launch_shell_ax<7>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
+                                           (float)src_val, cp, s); break;
+        }
+        if (rc) return rc;
+      }
+    }
+  }
+  return 0;
+}
+
+// size of the CPML block (ABI check against models/cpml.py device_table)
+FDTD_API int fdtd_shell_cpml_size() { return (int)sizeof(ShCpml); }

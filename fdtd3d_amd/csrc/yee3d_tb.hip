@@ -26,6 +26,8 @@
 // this launch stores) are separate: in a decomposed run the ghost layers are
 // updated redundantly at the inner levels but never stored.
 
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -448,9 +450,29 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     const int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
     const int n8 = n & ~7;
     const int q = p < n8 ? (p & 7) * (n8 >> 3) + (p >> 3) : p;
-    tz = q % gx;
-    ty = (q / gx) % gy;
-    tx = q / (gx * gy);
+    const int pz = (xcd_swz >> 8) & 0xff, py = (xcd_swz >> 16) & 0xff;
+    if (pz > 0 && py > 0) {
+      // patch order: an XCD's run of tiles is dealt in PZ x PY (z x y)
+      // patches, so the ~32 workgroups one XCD holds at a time form a compact
+      // block whose y AND z neighbours stream the same planes on the same L2
+      // (a tile shares 2T of its rows with each y neighbour, 2T lanes with
+      // each z neighbour).  Bands of PY tile rows; the last band and the last
+      // patch of a band may be narrower.
+      tx = q / (gx * gy);
+      const int r = q - tx * gx * gy;
+      const int band = r / (py * gx);
+      const int h = min(py, gy - band * py);
+      const int rb = r - band * py * gx;
+      const int col = rb / (pz * h);
+      const int wdt = min(pz, gx - col * pz);
+      const int e = rb - col * pz * h;
+      tz = col * pz + e % wdt;
+      ty = band * py + e / wdt;
+    } else {
+      tz = q % gx;
+      ty = (q / gx) % gy;
+      tx = q / (gx * gy);
+    }
   }
   const int kb = (O.lo[2] & ~(V - 1)) - HL * V + TBZ * tz + V * lane;
   const int jw = O.lo[1] - T + (ROWS - 2 * T) * ty + R * w;  // first row of this wave
@@ -1177,6 +1199,19 @@ int g_tb_mrows = 0;  // rows per wave of the multi-row kernel: 0 automatic, 1 = 
 
 int g_tb_mr_noallin = 0;  // A/B knob: 1 = masked loop everywhere (no interior fast path)
 int g_tb_mr_xcd = 1;   // multi-row kernel: XCD-contiguous tile order, z fastest (-16..20% HBM reads)
+// patch order of the XCD-contiguous tile run (k_tb3d_mr): (pz << 8) | (py << 16),
+// 0 = z fastest; FDTD3D_TB_PATCH="PZxPY" (e.g. 4x8) at first use
+int g_tb_patch = -1;
+int tb_patch_bits() {
+  if (g_tb_patch < 0) {
+    g_tb_patch = 0;
+    const char* e = getenv("FDTD3D_TB_PATCH");
+    int pz = 0, py = 0;
+    if (e && sscanf(e, "%dx%d", &pz, &py) == 2 && pz > 0 && py > 0 && pz < 256 && py < 256)
+      g_tb_patch = (pz << 8) | (py << 16);
+  }
+  return g_tb_patch;
+}
 int g_tb_variant = 0;  // multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched
 const int kNoBox[6] = {0, 0, 0, 0, 0, 0};
 int g_tb_mr_shape = 0;  // plain multi-row kernel: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
@@ -1194,7 +1229,8 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
   k_tb3d_mr<T, V, R, FX, PFD, DEFER, NW><<<grid, dim3(64, NW), 0, s>>>(                                     \
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
-      O, xchunk, src[0], src[1], src[2], src[3], sv, g_tb_mr_xcd | (g_tb_mr_noallin << 1), tf, gtab, cp)
+      O, xchunk, src[0], src[1], src[2], src[3], sv,                                                       \
+      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, cp)
   if constexpr (FX != 0) {
     MR_LAUNCH(1, false);  // tuning variants: uniform media only
   } else {
@@ -1328,6 +1364,10 @@ FDTD_API void fdtd_set_tb_variant(int v) {
   g_tb_variant = v & 3;
   g_tb_mr_xcd = (v >> 2) & 1;      // bit 2: XCD-contiguous tile order
   g_tb_mr_noallin = (v >> 3) & 1;  // bit 3: no interior fast path (A/B)
+}
+// patch order of the multi-row kernel's XCD tile run: pz x py tiles (0: z fastest)
+FDTD_API void fdtd_set_tb_patch(int pz, int py) {
+  g_tb_patch = (pz > 0 && py > 0 && pz < 256 && py < 256) ? ((pz << 8) | (py << 16)) : 0;
 }
 // plain multi-row tile shape (tuning): 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
 FDTD_API void fdtd_set_tb_mr_shape(int v) { g_tb_mr_shape = v == 1 ? 1 : 0; }

@@ -63,6 +63,13 @@ class Scene:
             return True
         return False
 
+    def percell_kinds(self, metamaterials: bool) -> int:
+        """Number of field kinds (E, H) whose plain update coefficient varies
+        per cell -- the count ``models/blocking.py auto_time_block`` takes (the
+        scheme derives the same count from its coefficients).  Every scene has
+        mu = 1, so at most the E kind."""
+        return 0 if self.is_vacuum(metamaterials) else 1
+
     def eps(self, x, y, z, mod: float) -> torch.Tensor:
         if self.kind in ("vacuum", "drude-sphere") or (self.kind == "reference" and self.scheme != "3d"):
             return torch.ones_like(x)

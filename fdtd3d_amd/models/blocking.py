@@ -76,11 +76,116 @@ def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: 
     return F32_AUTO_STEPS if world <= 2 else F32_AUTO_STEPS_MANY_RANKS
 
 
+def _cut_pieces(b: Box, cuts):
+    """``b`` split at the CPML slab cuts of every axis: [(box, axes bits)],
+    bit a set when the piece lies in an absorbing slab along axis a."""
+    pieces = [(b, 0)]
+    for a in range(3):
+        if cuts[a] is None:
+            continue
+        lo_c, hi_c = cuts[a]
+        nxt = []
+        for pb, ax in pieces:
+            for s_lo, s_hi, slab in ((None, lo_c, True), (lo_c, hi_c, False), (hi_c, None, True)):
+                l0 = pb[0][a] if s_lo is None else max(pb[0][a], s_lo)
+                h0 = pb[1][a] if s_hi is None else min(pb[1][a], s_hi)
+                if h0 <= l0:
+                    continue
+                lo, hi = list(pb[0]), list(pb[1])
+                lo[a], hi[a] = l0, h0
+                nxt.append(((tuple(lo), tuple(hi)), ax | ((1 << a) if slab else 0)))
+        pieces = nxt
+    return [(pb, ax) for pb, ax in pieces if not box_empty(pb)]
+
+
+def _merge_pieces(pieces):
+    """Merge pieces of the same CPML class whose union is a box (fewer,
+    larger boxes per shell launch)."""
+    out = list(pieces)
+    changed = True
+    while changed:
+        changed = False
+        for i in range(len(out)):
+            for j in range(i + 1, len(out)):
+                (a, ca), (b, cb_) = out[i], out[j]
+                if ca != cb_:
+                    continue
+                for d in range(3):
+                    same = all(a[0][e] == b[0][e] and a[1][e] == b[1][e] for e in range(3) if e != d)
+                    if same and (a[1][d] == b[0][d] or b[1][d] == a[0][d]):
+                        lo = tuple(min(a[0][e], b[0][e]) for e in range(3))
+                        hi = tuple(max(a[1][e], b[1][e]) for e in range(3))
+                        out[i] = ((lo, hi), ca)
+                        del out[j]
+                        changed = True
+                        break
+                if changed:
+                    break
+            if changed:
+                break
+    return out
+
+
+class PassTimer:
+    """Per-pass breakdown of decomposed blocked / hybrid passes on the main
+    stream: ``interior`` (the pass part that needs no fresh ghost, issued
+    while the exchange runs on the side stream), ``exchange_wait`` (main
+    stream blocked on the side stream after the interior: the part of the
+    exchange the interior did not hide) and ``shell`` (the parts that read
+    the fresh ghosts).  HIP events on the GPU, wall clock on the CPU (where
+    the gloo exchange is synchronous and lands in ``exchange_wait``)."""
+
+    def __init__(self, device):
+        self.cuda = getattr(device, "type", str(device)) == "cuda"
+        self.passes: list = []
+        self._cur = None
+
+    def mark(self, name: str) -> None:
+        if name == "start":
+            self._cur = []
+            self.passes.append(self._cur)
+        if self._cur is None:
+            return
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._cur.append((name, ev))
+        else:
+            import time
+            self._cur.append((name, time.perf_counter()))
+
+    def summary(self) -> dict:
+        """Totals in ms over the recorded passes (synchronises the device)."""
+        out = {"passes": len(self.passes), "interior_ms": 0.0, "exchange_wait_ms": 0.0, "shell_ms": 0.0}
+        keys = {"interior": "interior_ms", "wait": "exchange_wait_ms", "end": "shell_ms"}
+        for marks in self.passes:
+            for (_, a), (name, b) in zip(marks, marks[1:]):
+                if self.cuda:
+                    b.synchronize()
+                    ms = a.elapsed_time(b)
+                else:
+                    ms = (b - a) * 1e3
+                if name in keys:
+                    out[keys[name]] += ms
+        return out
+
+
 class BlockedStepping:
     """Blocked and hybrid passes of :class:`fdtd3d_amd.models.scheme.YeeScheme`
     (uses its fields, ops, domain, halo, layout and per-step update methods)."""
 
     _tfsf_once = False
+    pass_timer = None  # PassTimer of decomposed passes (bench.py / --json), None: off
+    _skip_side_wait = False  # tests only: drop the main stream's wait on the exchange (negative control)
+
+    def _mark(self, name: str) -> None:
+        if self.pass_timer is not None:
+            self.pass_timer.mark(name)
+
+    def _join_side(self, side) -> None:
+        """Main stream waits for the ghost exchange issued on ``side``."""
+        if side is not None and not self._skip_side_wait:
+            torch.cuda.current_stream(self.device).wait_stream(side)
 
     def _fork_side_stream(self):
         """High-priority side stream for the ghost exchange, ordered after
@@ -171,55 +276,123 @@ class BlockedStepping:
 
     # ------------------------------------------------ hybrid, single-pass shell
     def _hybrid2_ok(self) -> bool:
-        """CPML / TF-SF runs whose every irregular term the fp32 multi-row
-        kernel applies itself: CPML psi (single-step passes), TF/SF sets
-        (incident direction along x or y), sparse per-cell coefficients."""
+        """Runs whose shell the fused single-step shell kernel can advance
+        (csrc/yee3d_shell.hip): 3D serial CPML (no UPML / dispersive chain),
+        uniform media (scalar coefficients), plane waves through the TF/SF
+        tables.  ``hybrid_shell`` = auto / single-pass selects it, stepped
+        keeps the per-step kernels."""
         cfg = self.cfg
-        return (getattr(cfg, "hybrid_shell", "stepped") == "single-pass"
-                and self.ops.name == "hip" and self.dtype == torch.float32 and cfg.scheme == "3d"
-                and self.halo is None and not self.use_upml_chain and not cfg.use_metamaterials
-                and not cfg.use_amp_mode and self.domain.shape[2] % 4 == 0
-                and (not cfg.use_tfsf or getattr(self, "tfsf_sets", None) is not None)
-                and (cfg.use_pml and self.use_cpml))
+        mode = getattr(cfg, "hybrid_shell", "auto")
+        if mode not in ("auto", "single-pass") or not hasattr(self.ops, "shell_step"):
+            return False
+        if (cfg.scheme != "3d" or self.halo is not None or self.use_upml_chain or cfg.use_metamaterials
+                or cfg.use_amp_mode or not (cfg.use_pml and self.use_cpml)):
+            return False
+        if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
+            return False
+        if any(getattr(self.cb[c], "cell", None) is not None for c in self.comps):
+            return False  # per-cell coefficients: the stepped shell
+        # the kernel shares one slab geometry per (kind, axis): the terms of
+        # a kind along y / z must have the same psi slab ranges
+        by = {}
+        for c, slabs in self.cpml.slabs.items():
+            for sl in slabs:
+                key = (c[0], sl.axis, sl.side)
+                rng = (sl.lbox[0][sl.axis], sl.lbox[1][sl.axis])
+                if by.setdefault(key, rng) != rng:
+                    return False
+        return True
 
     def _hybrid2_plan(self, T: int):
         """Blocked core + single-pass shell with shrinking windows.
 
-        The core ``K`` (cells at least ``pml + T + 2`` from every face) takes
-        one ``T``-step blocked pass.  The shell -- everything else -- takes
-        ``T`` single-step passes of the same kernel with its CPML / TF-SF
-        terms, step ``s`` over ``alloc - K.shrink(T - s)``: each step's
-        window is one cell deeper into the core than the next needs, so
-        every shell value is exact without a stale band (the deep-halo
-        rule, reference ``ParallelGrid.cpp:2365-2489``).  Single-step passes
-        read one buffer and write another, so the shell ping-pongs between
-        ``F_alt`` and a third buffer while the core reads the untouched
-        ``F``."""
+        The core ``K`` -- cells at least ``T + 2`` from every CPML slab and
+        TF/SF target -- takes one ``T``-step blocked pass of the plain kernel.
+        The shell -- everything else -- takes ``T`` fused single steps
+        (``ops.shell_step``), step ``s`` over ``alloc - K.shrink(T - s)``:
+        each step's window is one cell deeper into the core than the next
+        needs, so every shell value is exact without a stale band (the
+        deep-halo rule, reference ``ParallelGrid.cpp:2365-2489``).
+        Single-step passes read one buffer and write another, so the shell
+        ping-pongs between ``F_alt`` and a third buffer while the core reads
+        the untouched ``F``.  Each window is cut at the CPML slab boundaries
+        into boxes tagged with the axes whose slab they touch (the kernel's
+        per-launch specialisation)."""
         cfg = self.cfg
         size = cfg.size
         m = T + 2
         lo, hi = [0, 0, 0], list(size)
         for a in range(3):
             edge = self.layout.pml_size[a] if cfg.use_pml else 0
+            if cfg.use_tfsf:
+                edge = max(edge, cfg.tfsf_size[a] + 1)
             lo[a], hi[a] = edge + m, size[a] - edge - m
         K = (tuple(lo), tuple(hi))
         if box_empty(K) or box_volume(K) < 0.25 * size[0] * size[1] * size[2]:
             return None
-        # every CPML slab must stay T + 1 clear of the core
+        # every CPML slab and TF/SF target must stay T + 1 clear of the core
+        # (its dependency cone; also keeps the host-side TF/SF additions to
+        # the shell's input buffer out of what the core pass reads)
         g = (tuple(lo[d] - T - 1 for d in range(3)), tuple(hi[d] + T + 1 for d in range(3)))
         for slabs in self.cpml.slabs.values():
             for sl in slabs:
                 if not box_empty(box_intersect(g, sl.gbox)):
                     return None
+        if cfg.use_tfsf:
+            lg = self.domain.to_local(g)
+            for c in self.comps:
+                for tab in self.tfsf[c]:
+                    if tab.n == 0:
+                        continue
+                    ijk = tab.ijk.view(-1, 3)
+                    inside = torch.ones(ijk.shape[0], dtype=torch.bool, device=ijk.device)
+                    for d in range(3):
+                        inside &= (ijk[:, d] >= lg[0][d]) & (ijk[:, d] < lg[1][d])
+                    if bool(inside.any()):
+                        return None
         alloc = self.domain.allocated_global()
+        cuts = self._cpml_cuts()
         windows = []
         for st in range(1, T + 1):
             d = T - st
             Kd = (tuple(lo[a] + d for a in range(3)), tuple(hi[a] - d for a in range(3)))
-            windows.append([self.domain.to_local(b) for b in box_subtract(alloc, Kd) if not box_empty(b)])
+            boxes = [self.domain.to_local(b) for b in box_subtract(alloc, Kd) if not box_empty(b)]
+            windows.append(_merge_pieces([pc for b in boxes for pc in _cut_pieces(b, cuts)]))
         upd = {c: self.local_box(c, alloc) for c in self.comps}
         return {"T": T, "v2": True, "core": [self.domain.to_local(K)], "windows": windows, "upd": upd,
                 "core_cells": box_volume(K)}
+
+    def _cpml_cuts(self):
+        """Per axis (low cut, high cut) of the CPML slabs, local indices:
+        cells below the low cut or at / above the high cut may carry that
+        axis's psi terms (None: no slab along the axis)."""
+        cuts = [None, None, None]
+        n = self.domain.shape
+        for slabs in self.cpml.slabs.values():
+            for sl in slabs:
+                a = sl.axis
+                b = self.domain.to_local(sl.gbox)
+                lo_c, hi_c = cuts[a] if cuts[a] is not None else (0, n[a])
+                if sl.side == 0:
+                    lo_c = max(lo_c, b[1][a])
+                else:
+                    hi_c = min(hi_c, b[0][a])
+                cuts[a] = (lo_c, hi_c)
+        return cuts
+
+    def _tfsf_kind(self, kind: str, p: int, F) -> None:
+        """Every TF/SF correction of ``kind`` on plane ``p``'s fields ``F``
+        (coefficient Cb / Db, incident H for E targets, E for H targets), in
+        as few launches as the backend allows."""
+        comps = self.e_comps if kind == "E" else self.h_comps
+        inc = self.hinc[p] if kind == "E" else self.einc[p]
+        whole = ((0, 0, 0), tuple(self.domain.shape))
+        if hasattr(self.ops, "tfsf_apply_many"):
+            self.ops.tfsf_apply_many([(F[c], tab) for c in comps for tab in self.tfsf[c]], inc)
+        else:
+            for c in comps:
+                for tab in self.tfsf[c]:
+                    self.ops.tfsf_apply(F[c], tab, inc, whole)
 
     def _hybrid2_step(self, T: int) -> None:
         hp = self.hybrid
@@ -234,24 +407,34 @@ class BlockedStepping:
                     self.step()
                 return
         srcs = self._pass_sources(self.t, T)
+        tfsf = self.cfg.use_tfsf
+        kappa = getattr(self.cfg, "cpml_kappa_max", 1.0) != 1.0
         for p in range(self.planes):
-            tf = self._tfsf_pass(p, T)
             P, Q, Z = self.F[p], self.F_alt[p], self.F_3[p]
             cur = P
             with self.prof.phase("shell"):
                 for st in range(1, T + 1):
                     out = Q if st % 2 == 1 else Z
-                    sv = None if srcs[p] is None else [srcs[p][st - 1]]
-                    tfs = None if tf is None else (tf[0], tf[1], st - 1)
-                    cp = self.cpml.device_table(p) if self.use_cpml else None
-                    for b in hp["windows"][st - 1]:
-                        self.ops.tb_step(cur, out, hp["upd"], b, self.cb, 1, sv, tfsf=tfs, cpml=cp)
-                    if self.use_cpml:
-                        self.cpml.flip(p)
+                    t = self.t + st - 1
+                    if tfsf:
+                        # incident line E half step, then the E corrections
+                        # added to the INPUT (additive: E + Cb g + Cb curl)
+                        self.ops.inc_step_e(self.einc[p], self.hinc[p], self.inc_ce, self.source_value(t, p))
+                        self._tfsf_kind("E", p, cur)
+                    sv = None if srcs[p] is None else srcs[p][st - 1]
+                    cp = self.cpml.shell_arg(p, self.ops)
+                    pieces = hp["windows"][st - 1]
+                    self.ops.shell_step(cur, out, hp["upd"], [b for b, _ in pieces], [a for _, a in pieces],
+                                        self.cb, sv, cpml=cp, kappa=kappa)
+                    self.cpml.flip(p)
+                    if tfsf:
+                        # incident line H half step, H corrections on the OUTPUT
+                        self.ops.inc_step_h(self.einc[p], self.hinc[p], self.inc_ch)
+                        self._tfsf_kind("H", p, out)
                     cur = out
             with self.prof.phase("blocked-core"):
                 for ob in hp["core"]:
-                    self.ops.tb_step(P, cur, hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf)
+                    self.ops.tb_step(P, cur, hp["upd"], ob, self.cb, T, srcs[p])
             rest = [b for b in (Q, Z) if b is not cur]
             self.F[p], self.F_alt[p], self.F_3[p] = cur, P, rest[0]
         self.t += T
@@ -446,30 +629,59 @@ class BlockedStepping:
             return
         hp = self.hybrid
         srcs = self._pass_sources(self.t, T)
+        side = None
+        core_now, core_later = hp["core"], []
         if self.halo is not None:
             # one T-deep exchange of every state array (aux included) feeds the
-            # core pass and the deep-halo shell steps; step() skips its own
+            # core pass and the deep-halo shell steps; step() skips its own.
+            # It runs on the side stream while the core cells at least T from
+            # every neighbour (no fresh ghost in their dependency cone) are
+            # advanced; the rest of the core and the stepped shell follow.
+            core_now, core_later = self._hybrid_core_split(T)
+            side = self._fork_side_stream()
+            self._mark("start")
             with self.prof.phase("halo-deep"):
-                self.halo.exchange_all(self)
+                self.halo.exchange_all(self, stream=side)
             self._deep_fresh = True
-        with self.prof.phase("blocked-core"):
+            # the fresh ghosts are T deep: the shell steps of this pass use
+            # the deep-halo windows from sub-step 0, whatever an earlier
+            # shorter pass (periodic work, a tail) left behind
+            self.sub_step = 0
+        tfs = []
+        for p in range(self.planes):
+            tf = None
+            if self.cfg.use_tfsf and self.hybrid.get("tfsf_in_core"):
+                # the pass kernel advances the incident line for the core;
+                # the stepped shell advances it again from the same state
+                line0 = (self.einc[p].clone(), self.hinc[p].clone())
+                tf = (self._tfsf_pass(p, T), line0)
+            tfs.append(tf)
+
+        def core(boxes):
             for p in range(self.planes):
-                tf = None
-                if self.cfg.use_tfsf and self.hybrid.get("tfsf_in_core"):
-                    # the pass kernel advances the incident line for the core;
-                    # the stepped shell advances it again from the same state
-                    line0 = (self.einc[p].clone(), self.hinc[p].clone())
-                    tf = self._tfsf_pass(p, T)
-                for ob in hp["core"]:
+                tf = tfs[p][0] if tfs[p] is not None else None
+                for ob in boxes:
                     if tf is not None:
                         self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf)
                     else:
                         self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
-                if tf is not None:
-                    self.einc[p].copy_(line0[0])
-                    self.hinc[p].copy_(line0[1])
+
+        with self.prof.phase("blocked-core"):
+            core(core_now)
+        if self.halo is not None:
+            self._mark("interior")
+            self._join_side(side)
+            self._mark("wait")
+            with self.prof.phase("blocked-core"):
+                core(core_later)
+        for p in range(self.planes):
+            if tfs[p] is not None:
+                self.einc[p].copy_(tfs[p][1][0])
+                self.hinc[p].copy_(tfs[p][1][1])
         for s in range(T):
             self.step(hp["shells"][s])
+        if self.halo is not None:
+            self._mark("end")
         with self.prof.phase("shell-copy"):
             for p in range(self.planes):
                 src = [self.F[p][c] for c in self.comps]
@@ -478,6 +690,34 @@ class BlockedStepping:
                     self.ops.copy_box(src, dst, b)
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
+
+    def _hybrid_core_split(self, T: int):
+        """(core boxes that need no fresh ghost, the rest) of a decomposed
+        hybrid pass, local indices: the interior is the owned box shrunk by
+        ``T`` on every side with a neighbour (a T-step pass reads T cells
+        beyond its output box), the rest are the slabs between it and the
+        rank border, which wait for the exchange."""
+        cache = self.__dict__.setdefault("_hybrid_split_cache", {})
+        if T in cache:
+            return cache[T]
+        dom = self.domain
+        lo, hi = list(dom.lo), list(dom.hi)
+        for a in range(3):
+            if dom.has_low(a):
+                lo[a] += T
+            if dom.has_high(a):
+                hi[a] -= T
+        inner = dom.to_local((tuple(lo), tuple(hi)))
+        now, later = [], []
+        for b in self.hybrid["core"]:
+            i = box_intersect(b, inner)
+            if not box_empty(i):
+                now.append(i)
+                later += [r for r in box_subtract(b, i) if not box_empty(r)]
+            else:
+                later.append(b)
+        cache[T] = (now, later)
+        return cache[T]
 
     # ----------------------------------------------------- plain blocking
     def _tb_regions(self, T: int):
@@ -516,6 +756,8 @@ class BlockedStepping:
         srcs = self._pass_sources(self.t, T)
         side = self._fork_side_stream() if self.halo is not None else None
         tfs = [self._tfsf_pass(p, T) for p in range(self.planes)] if self.cfg.use_tfsf else [None] * self.planes
+        if self.halo is not None:
+            self._mark("start")
         for p in range(self.planes):
             if not box_empty(outs[0]):
                 with self.prof.phase("blocked-interior" if self.halo is not None else "blocked"):
@@ -524,6 +766,7 @@ class BlockedStepping:
                     else:
                         self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
         if self.halo is not None:
+            self._mark("interior")
             if side is not None and self.prof.enabled:
                 with torch.cuda.stream(side):
                     with self.prof.phase("halo-overlapped"):
@@ -531,8 +774,8 @@ class BlockedStepping:
             else:
                 with self.prof.phase("halo-overlapped"):
                     self.halo.exchange_all(self, stream=side)
-            if side is not None:
-                torch.cuda.current_stream(self.device).wait_stream(side)
+            self._join_side(side)
+            self._mark("wait")
             with self.prof.phase("blocked-shells"):
                 for ob in outs[1:]:
                     for p in range(self.planes):
@@ -540,6 +783,7 @@ class BlockedStepping:
                             self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p], tfsf=tfs[p])
                         else:
                             self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p])
+            self._mark("end")
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
         self.t += T

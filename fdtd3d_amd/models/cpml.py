@@ -177,6 +177,13 @@ class CPML:
         cache[key] = (dev, keep)
         return dev
 
+    def shell_arg(self, p: int, ops):
+        """The ``cpml`` argument of ``ops.shell_step`` for plane ``p``: the
+        device block on the HIP backend, (self, p) for the torch oracle."""
+        if ops.name == "hip":
+            return self.device_table(p)
+        return (self, p)
+
     def flip(self, p: int) -> None:
         """The copy the last single-step pass wrote becomes plane ``p``'s psi."""
         self.__dict__.pop("_tables", None)

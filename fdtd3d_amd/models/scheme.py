@@ -53,6 +53,7 @@ from .tfsf import build_tfsf_sets, build_tfsf_tables, incident_line_length
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
 GRAPH_STEPS = 60  # steps per captured HIP graph (a multiple of 6: D/D1 level rotations return to the start)
+TFSF_MAX_STEPS = 5  # steps per pass of the blocked kernel's in-kernel TF/SF variant (yee3d_tb.hip TF_ENT)
 
 
 @dataclass
@@ -98,7 +99,7 @@ class SchemeConfig:
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
-    hybrid_shell: str = "stepped"            # stepped | single-pass (models/blocking.py _hybrid2_plan)
+    hybrid_shell: str = "auto"               # auto | stepped | single-pass (models/blocking.py _hybrid2_plan)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
@@ -310,6 +311,11 @@ class YeeScheme(BlockedStepping):
                                 tfsf=bool(getattr(self, "tfsf_blocked", False)))
             if self.halo is not None and self.domain.buffer_size != T:
                 T = 1
+        if self.tfsf_blocked and T > TFSF_MAX_STEPS:
+            # the in-kernel TF/SF variant of the blocked kernel exists for T <= 5
+            # (yee3d_tb.hip TF_ENT); a longer request runs 5-step passes
+            log.log(1, "--time-block %d with TF/SF: %d steps per pass" % (T, TFSF_MAX_STEPS))
+            T = TFSF_MAX_STEPS
         self.tb = 1
         hip_ok = self.ops.name != "hip" or self.dtype == torch.float64 or self.domain.shape[2] % 4 == 0
         if (T > 1 and (self.fused or self.tfsf_blocked) and hasattr(self.ops, "tb_step") and hip_ok
@@ -487,6 +493,13 @@ class YeeScheme(BlockedStepping):
             # row tables built now (host syncs), never under a HIP graph capture
             for kind in ("E", "H"):
                 self._drude_rows(kind)
+        if (cfg.use_metamaterials and cfg.scheme == "3d" and getattr(self.ops, "drude_lut", False)
+                and hasattr(self.ops, "_drude_lut")):
+            # the uint8 material index + coefficient table too (torch.unique
+            # syncs the host): built here, not lazily inside a graph capture
+            for c in self.comps:
+                st = self.upml[c]
+                self.ops._drude_lut(st, [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")], self.domain.shape)
 
     def _bbox_global(self, mask: torch.Tensor) -> Box:
         """Global bounding box of the True cells of a local mask (empty box

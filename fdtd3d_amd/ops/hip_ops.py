@@ -788,6 +788,60 @@ class HipOps:
         _check(rc, "tb3d")
         self.launches += 1
 
+    shell_ok = True  # fused single-step shell kernel (yee3d_shell.hip) present
+
+    def shell_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                   windows: Sequence[Box], ax: Sequence[int], cb: Dict[str, Coef], source=None, cpml=None,
+                   kappa: bool = False) -> None:
+        """One fused E+H leapfrog step (yee3d_shell.hip) of the shell boxes
+        ``windows`` (local, disjoint): reads ``fin``, writes ``fout`` there.
+        ``ax[w]`` = the CPML axes of box ``w`` (bit 0 x, 1 y, 2 z), ``cpml`` =
+        ``CPML.device_table(p)`` (psi read from the current copy, written to the
+        other: call ``CPML.flip`` after), ``source`` = (E component, local
+        index, value) of a hard point source or None.  fp32, scalar
+        coefficients per kind."""
+        E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
+        if self.dtype != torch.float32:
+            raise HipError("shell_step: fp32 only")
+        shape = tuple(fin["Ex"].shape)
+        for c in E + H:
+            self._check_tensor(fin[c], shape)
+            self._check_tensor(fout[c], shape)
+            if fin[c].data_ptr() == fout[c].data_ptr():
+                raise HipError("shell_step needs distinct in/out buffers")
+            if self._cell_or_none(cb[c]) is not None:
+                raise HipError("shell_step: scalar coefficients only")
+        cbv, dbv = cb["Ex"].scalar, cb["Hx"].scalar
+        if any(cb[c].scalar != cbv for c in E) or any(cb[c].scalar != dbv for c in H):
+            raise HipError("shell_step: scalar coefficients must agree per kind")
+        wins = [w for w in windows]
+        if len(wins) != len(ax) or len(wins) > 64 * 10:
+            raise HipError("shell_step: one CPML class per window")
+        for w in wins:
+            for d in range(3):
+                if not _empty(w) and (w[0][d] < 0 or w[1][d] > shape[d]):
+                    raise HipError("shell window %s outside array %s" % (w, shape))
+        if any(ax) and cpml is None:
+            raise HipError("shell_step: CPML windows without a CPML table")
+        if cpml is not None and int(self.lib.fdtd_shell_cpml_size()) != cpml.numel():
+            raise HipError("shell CPML block layout mismatch")
+        src = [-1, -1, -1, -1]
+        val = 0.0
+        if source is not None:
+            comp, idx, val = source[0], tuple(source[1]), float(source[2])
+            if comp not in E or any(not (0 <= idx[d] < shape[d]) for d in range(3)):
+                raise HipError("shell_step: E point source inside the array only")
+            src = [idx[0], idx[1], idx[2], E.index(comp)]
+        arr = (c_vp * 6)(*[fin[c].data_ptr() for c in E + H])
+        out = (c_vp * 6)(*[fout[c].data_ptr() for c in E + H])
+        rc = self.lib.fdtd_shell1_f32(arr, out, c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]),
+                                      c_int(shape[2]), _box_arr([boxes[c] for c in E + H]), c_int(len(wins)),
+                                      _box_arr(wins) if wins else (c_int * 1)(0), (c_int * max(1, len(ax)))(*ax),
+                                      (c_int * 4)(*src), c_double(val), _ptr(cpml), c_int(1 if kappa else 0),
+                                      _stream())
+        _check(rc, "shell1")
+        self.launches += 1
+
     def _tb2d_step(self, fin, fout, boxes, obox, cb, steps, sources) -> None:
         """2D (TMz / TEz) blocked pass (yee2d_tb.hip): (nx, ny, 1) arrays
         whose rows are whole 16-byte lanes (ny % 4 == 0 fp32, % 2 fp64); the

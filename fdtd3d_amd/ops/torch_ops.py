@@ -147,6 +147,44 @@ class TorchOps:
                 sp = tuple(slice(s.start + 1, s.stop + 1) for s in sl)
                 fout[c][sl] = cur[c][sp]
 
+    def shell_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                   windows, ax, cb: Dict[str, Coef], source=None, cpml=None, kappa: bool = False) -> None:
+        """Reference semantics of the fused single-step shell kernel
+        (yee3d_shell.hip): one leapfrog step of every update box from ``fin``
+        (CPML psi read from ``psi[p]``, written to ``psi_alt[p]``; ``cpml`` =
+        (CPML, p)), of which only the ``windows`` are stored to ``fout``.
+        ``ax`` (the kernel's per-box CPML class) does not change the result."""
+        tmp = {c: fin[c].clone() for c in fin}
+        e = {c: b for c, b in boxes.items() if c[0] == "E"}
+        h = {c: b for c, b in boxes.items() if c[0] == "H"}
+        cp, p = cpml if cpml is not None else (None, 0)
+
+        def psi_terms(kind, src):
+            if cp is None:
+                return
+            for c, box in (e if kind == "E" else h).items():
+                for sl in cp.slabs[c]:
+                    if getattr(sl, "psi_alt", None) is None:
+                        sl.psi_alt = [torch.zeros_like(x) for x in sl.psi]
+                    sl.psi_alt[p].copy_(sl.psi[p])
+                    b = box_intersect_(box, sl.lbox)
+                    self.cpml_apply(kind, tmp[c], src[sl.src], sl.axis, sl.sign, sl.psi_alt[p], sl.lbox, b, sl.b,
+                                    sl.c, sl.kinv_m1, cb[c])
+
+        self.curl_update("E", e, tmp, fin, cb)
+        psi_terms("E", fin)
+        if source is not None:
+            comp, idx, val = source
+            tmp[comp][tuple(idx)] = val
+        self.curl_update("H", h, tmp, tmp, cb)
+        psi_terms("H", tmp)
+        for w in windows:
+            if _empty(w):
+                continue
+            sl = box_slices(w)
+            for c in fout:
+                fout[c][sl] = tmp[c][sl]
+
     chain_fold = True
 
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],

@@ -143,12 +143,26 @@ class _LocalRecv:
         self.q, self.dst = q, dst
 
     def wait(self):
-        src = self.q.get(timeout=120)
+        src, ev = self.q.get(timeout=120)
+        if ev is not None:
+            # stream-ordered like RCCL's work.wait(): the receiver's CURRENT
+            # stream waits for the sender's snapshot, the host does not -- a
+            # consumer that forgets to order its stream after this one reads
+            # stale ghosts (tests/test_parallel_gpu.py negative control)
+            cur = torch.cuda.current_stream(self.dst.device)
+            cur.wait_event(ev)
+            src.record_stream(cur)  # the snapshot's memory lives until the copy ran
         self.dst.copy_(src)
         return True
 
 
 class LocalComm:
+    """In-process transport with RCCL's ordering semantics: a send snapshots
+    the buffer on the sender's current stream and publishes it with an event;
+    a receive's ``wait()`` makes the receiver's current stream wait on that
+    event.  Nothing synchronises the host, so a missing stream dependency on
+    either side shows up as wrong fields instead of being hidden by a
+    device-wide sync."""
     backend = "local"
 
     def __init__(self, hub: LocalHub, rank: int):
@@ -161,10 +175,11 @@ class LocalComm:
         for o in ops:
             if o.send:
                 snap = o.tensor.clone()
+                ev = None
                 if snap.is_cuda:
-                    # the receiver runs on another thread/stream: publish only finished data
-                    torch.cuda.current_stream(snap.device).synchronize()
-                self.hub.box(self.rank, o.peer, o.tag).put(snap)
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(snap.device))
+                self.hub.box(self.rank, o.peer, o.tag).put((snap, ev))
                 works.append(_Done())
             else:
                 works.append(_LocalRecv(self.hub.box(o.peer, self.rank, o.tag), o.tensor))

@@ -293,8 +293,14 @@ class HaloExchanger:
             self.messages += 1
         for w in self._post(ops_list):
             w.wait()
+        if self.debug_delay_cycles and tensors[0].is_cuda:
+            # tests: hold the unpack back on the exchange's stream so that a
+            # consumer not ordered after it deterministically reads old ghosts
+            torch.cuda._sleep(int(self.debug_delay_cycles))
         for rbox, rg, rb in recvs:
             _unpack_state(ops, tensors, boxed, rbox, rg, d, rb)
+
+    debug_delay_cycles = 0
 
     def _exchange_sweep(self, scheme) -> None:
         d = self.domain

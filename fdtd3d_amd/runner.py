@@ -26,18 +26,40 @@ from .utils import logging as log
 from .utils.settings import (EXIT_BREAK_ARG_PARSING, EXIT_OK, Settings, setup_from_cmd)
 
 
+def select_device_index(settings: Settings, local_rank: int, world: int, avail: int) -> int:
+    """GPU of this rank: ``local_rank % n`` with ``n`` = ``--num-cuda-gpus``
+    clipped to the visible devices (reference bug #11 fixed); under torchrun
+    with the default ``--num-cuda-gpus 1`` on a multi-GPU node one rank per GPU
+    (RCCL refuses two ranks on one device)."""
+    avail = max(1, avail)
+    n = max(1, min(settings.numCudaGPUs, avail))
+    if world > 1 and settings.numCudaGPUs <= 1 and avail > 1:
+        n = avail
+    return local_rank % n
+
+
 def _init_distributed(settings: Settings):
+    """Process group of a torchrun launch.  The rank's GPU is bound BEFORE
+    ``init_process_group`` (``device_id`` = eager RCCL communicator on the
+    right device), and a barrier establishes the communicator before the
+    first batched point-to-point exchange -- the order ``bench.py`` uses."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return None, 0, 1
     if not dist.is_initialized():
-        backend = "nccl" if (torch.cuda.device_count() > 0 and settings.backend != "torch") else "gloo"
-        if settings.device == "cpu":
-            backend = "gloo"
+        use_gpu = (torch.cuda.device_count() > 0 and settings.backend != "torch" and settings.device != "cpu")
+        backend = "nccl" if use_gpu else "gloo"
+        device = None
+        if use_gpu:
+            local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+            idx = select_device_index(settings, local, world, torch.cuda.device_count())
+            torch.cuda.set_device(idx)
+            device = "cuda:%d" % idx
         from .parallel.comm import init_process_group
-        init_process_group(backend)
+        init_process_group(backend, device)
+        dist.barrier()
     return dist, dist.get_rank(), dist.get_world_size()
 
 
@@ -52,14 +74,8 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
     cfg = SchemeConfig.from_settings(settings)
     backend, device = resolve_backend(settings.backend, settings.device)
     if device.startswith("cuda"):
-        avail = max(1, torch.cuda.device_count())
-        n = max(1, min(settings.numCudaGPUs, avail))
-        if world > 1 and settings.numCudaGPUs <= 1 and avail > 1:
-            # default --num-cuda-gpus 1 under torchrun on a multi-GPU node: one
-            # rank per GPU (RCCL refuses two ranks on one device)
-            n = avail
         local = int(os.environ.get("LOCAL_RANK", rank))
-        dev_index = local % n
+        dev_index = select_device_index(settings, local, world, torch.cuda.device_count())
         torch.cuda.set_device(dev_index)
         device = "cuda:%d" % dev_index
     dtype = torch.float32 if cfg.dtype == "f32" else torch.float64
@@ -84,7 +100,7 @@ def build(settings: Settings, rank: int = 0, world: int = 1):
         if tb <= 0:  # automatic: the scheme's own rule (models/blocking.py auto_time_block)
             from .layout.materials import Scene
             from .models.blocking import auto_time_block
-            percell = not Scene(cfg.scene, cfg.scheme).is_vacuum(cfg.use_metamaterials)
+            percell = Scene(cfg.scene, cfg.scheme).percell_kinds(cfg.use_metamaterials)
             tb = auto_time_block(cfg.scheme, cfg.dtype, backend, percell, world) if plain else 1
         if tb > 1 and cfg.scheme in ("3d", "tmz", "tez"):
             buf = tb  # blocked passes exchange tb-deep ghosts every tb steps
@@ -208,6 +224,9 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
     scheme.prof.reset()  # phase timings cover the timed steps only
     if halo is not None:
         halo.bytes_sent = 0
+        if settings.doPrintJson:
+            from .models.blocking import PassTimer
+            scheme.pass_timer = PassTimer(scheme.device)
     t0 = time.perf_counter()
     scheme.perform_steps(steps)
     if halo is not None:
@@ -221,6 +240,10 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
     if settings.checkpointDir:
         save_checkpoint(scheme, settings.checkpointDir)
     phases = scheme.prof.summary() if scheme.prof.enabled else None
+    breakdown = None
+    if scheme.pass_timer is not None:
+        breakdown = scheme.pass_timer.summary()
+        scheme.pass_timer = None
     if rank == 0:
         mc = _report(settings, scheme, seconds, world, core, steps, out)
         if phases:
@@ -230,6 +253,10 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
                    "ranks": world, "backend": scheme.ops.name}
             if phases:
                 rec["phases"] = phases
+            if breakdown is not None:
+                rec["rank0_passes"] = breakdown  # decomposed passes: interior / exchange wait / shell ms
+            if scheme.device.type == "cuda":
+                rec["max_mem_gb"] = torch.cuda.max_memory_allocated(scheme.device) / 1e9
             if halo is not None:
                 # rank 0's halo traffic over the timed steps (sent bytes; every
                 # rank receives as much as its neighbours send it)

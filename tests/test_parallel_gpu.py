@@ -23,7 +23,14 @@ from fdtd3d_amd.parallel.topology import ParallelGridCore
 pytestmark = pytest.mark.gpu
 
 
-def run_threads(cfg, world, axes, buf, device):
+def run_threads(cfg, world, axes, buf, device, delay_cycles=0, skip_side_wait=False, split=None,
+                random_init=False):
+    """Decomposed run with one thread per rank, each on its OWN main stream
+    (like one process per GPU): the in-process transport orders streams with
+    events only, so every cross-stream dependency must be explicit.
+    ``delay_cycles`` holds every ghost unpack back on the exchange stream;
+    ``skip_side_wait`` drops the main stream's wait on it (negative control);
+    ``split`` = (steps, ...) runs perform_steps in pieces (passes cut short)."""
     core = ParallelGridCore.create(cfg.size, world, axes, active_axes=(0, 1, 2) if cfg.scheme == "3d" else (0, 1))
     hub = LocalHub(world)
     dt = torch.float32 if cfg.dtype == "f32" else torch.float64
@@ -32,20 +39,30 @@ def run_threads(cfg, world, axes, buf, device):
 
     def body(rank):
         try:
-            dom = core.domain(rank, buf, align_z=4 if (cfg.time_block > 1 or cfg.hybrid_block > 1) else 1,
-                              align_axis=2 if cfg.scheme == "3d" else 1)
-            halo = HaloExchanger(dom, comm=hub.comm(rank))
-            s = YeeScheme(cfg, make_ops("hip", None, device, dt), dom, halo)
-            s.init_scheme()
-            s.init_grids()
-            # time_block 0: the automatic rule must pick the ghost depth the
-            # driver sized the domain for (models/blocking.py auto_time_block)
-            if cfg.hybrid_block > 1:
-                assert s.hybrid is not None, "hybrid pass not selected"
-            else:
-                assert s.tb == (buf if cfg.time_block == 0 else max(1, cfg.time_block))
-            s.perform_steps()
-            halo.drain(s)
+            stream = torch.cuda.Stream(device=device)
+            with torch.cuda.stream(stream):
+                dom = core.domain(rank, buf, align_z=4 if (cfg.time_block > 1 or cfg.hybrid_block > 1) else 1,
+                                  align_axis=2 if cfg.scheme == "3d" else 1)
+                halo = HaloExchanger(dom, comm=hub.comm(rank))
+                halo.debug_delay_cycles = delay_cycles
+                s = YeeScheme(cfg, make_ops("hip", None, device, dt), dom, halo)
+                s._skip_side_wait = skip_side_wait
+                s.init_scheme()
+                s.init_grids()
+                # time_block 0: the automatic rule must pick the ghost depth the
+                # driver sized the domain for (models/blocking.py auto_time_block)
+                if cfg.hybrid_block > 1:
+                    assert s.hybrid is not None, "hybrid pass not selected"
+                else:
+                    assert s.tb == (buf if cfg.time_block == 0 else max(1, cfg.time_block))
+                if random_init:
+                    s.randomize_fields()
+                if split:
+                    for n in split:
+                        s.perform_steps(n)
+                else:
+                    s.perform_steps()
+                halo.drain(s)
             torch.cuda.synchronize()
             schemes[rank] = s
         except BaseException as e:  # surface thread failures in the test
@@ -113,17 +130,61 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("name,cfg,world,axes,buf", CASES, ids=[c[0] for c in CASES])
-def test_gpu_decomposed_equals_serial(gpu, name, cfg, world, axes, buf):
-    par = run_threads(cfg, world, axes, buf, gpu)
+def _serial(cfg, gpu, random_init=False):
     dt = torch.float32 if cfg.dtype == "f32" else torch.float64
     s = YeeScheme(cfg, make_ops("hip", None, gpu, dt))
     s.init_scheme()
     s.init_grids()
+    if random_init:
+        s.randomize_fields()
     s.perform_steps()
+    return s
+
+
+def _max_rel_err(par, s):
+    worst = 0.0
+    for c in s.comps:
+        b = s.F[0][c].double().cpu()
+        scale = max(float(s.F[0][o].abs().max()) for o in s.comps if o[0] == c[0]) + 1e-30
+        worst = max(worst, float((par[c] - b).abs().max()) / scale)
+    return worst
+
+
+@pytest.mark.parametrize("name,cfg,world,axes,buf", CASES, ids=[c[0] for c in CASES])
+def test_gpu_decomposed_equals_serial(gpu, name, cfg, world, axes, buf):
+    par = run_threads(cfg, world, axes, buf, gpu)
+    s = _serial(cfg, gpu)
     for c in s.comps:
         a = par[c]
         b = s.F[0][c].double().cpu()
         scale = max(float(s.F[0][o].abs().max()) for o in s.comps if o[0] == c[0]) + 1e-30
         err = float((a - b).abs().max())
         assert err <= 1e-6 * scale, (name, c, err, scale)
+
+
+# the exchange overlapped with the interior / core pass on the side stream
+STREAM_CASES = [c for c in CASES if c[0] in ("tb5-xy4", "hybrid-cpml-tfsf-xy4", "hybrid-upml-drude-z2")]
+DELAY = 40_000_000  # GPU clock cycles of torch.cuda._sleep before every ghost unpack (~20 ms)
+
+
+@pytest.mark.parametrize("name,cfg,world,axes,buf", STREAM_CASES, ids=[c[0] for c in STREAM_CASES])
+def test_gpu_side_stream_order(gpu, name, cfg, world, axes, buf):
+    """Every unpack is held back ~20 ms on the side stream: the decomposed
+    result still equals the serial one (the main stream waits for the
+    exchange) -- and with that wait removed it does NOT (negative control:
+    proves the test sees a missing stream dependency)."""
+    s = _serial(cfg, gpu, random_init=True)
+    ok = run_threads(cfg, world, axes, buf, gpu, delay_cycles=DELAY, random_init=True)
+    assert _max_rel_err(ok, s) <= 1e-5, name
+    bad = run_threads(cfg, world, axes, buf, gpu, delay_cycles=DELAY, skip_side_wait=True, random_init=True)
+    assert _max_rel_err(bad, s) > 1e-3, "%s: a missing side-stream wait went unnoticed" % name
+
+
+def test_gpu_hybrid_split_passes(gpu):
+    """Decomposed hybrid run advanced in pieces that are not multiples of T
+    (passes cut short, as periodic work does): equals one serial run
+    (the deep-halo sub-step must restart with every exchange)."""
+    name, cfg, world, axes, buf = [c for c in CASES if c[0] == "hybrid-cpml-tfsf-xy4"][0]
+    s = _serial(cfg, gpu, random_init=True)
+    par = run_threads(cfg, world, axes, buf, gpu, split=(2, 4, 3, 1), random_init=True)
+    assert _max_rel_err(par, s) <= 1e-5

@@ -1,0 +1,106 @@
+"""Fused single-step shell kernel (csrc/yee3d_shell.hip) against the torch
+reference of the same step (ops/torch_ops.py ``shell_step``) in fp64: fields
+inside the windows, CPML psi written to the alternate copy, cells outside the
+windows left alone.  (GPU only.)"""
+import dataclasses
+
+import pytest
+import torch
+
+from fdtd3d_amd.models.blocking import _cut_pieces, _merge_pieces
+from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+from fdtd3d_amd.ops import make_ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _scheme(cfg, backend, device, dtype):
+    s = YeeScheme(cfg, make_ops(backend, None, device, dtype))
+    s.init_scheme()
+    s.init_grids()
+    return s
+
+
+def _live_state(cfg, gpu):
+    """A stepped CPML run from random fields: live psi in every slab."""
+    s = _scheme(cfg, "hip", gpu, torch.float32)
+    s.randomize_fields(seed=11)
+    s.perform_steps(3)
+    torch.cuda.synchronize()
+    return s
+
+
+CASES = [
+    # (name, size, pml, kappa, windows: "all" = the whole domain cut at the slabs, "shell" = a hybrid shell window)
+    ("all-64", (40, 36, 48), (5, 5, 5), 1.0, "all"),
+    ("all-kappa", (40, 36, 48), (5, 5, 5), 3.0, "all"),
+    ("shell", (64, 60, 72), (6, 6, 6), 1.0, "shell"),
+    ("thin-z-nopml-z", (44, 40, 28), (5, 5, 0), 1.0, "all"),
+]
+
+
+@pytest.mark.parametrize("name,size,pml,kappa,mode", CASES, ids=[c[0] for c in CASES])
+def test_shell_step_vs_torch(gpu, name, size, pml, kappa, mode):
+    cfg = SchemeConfig(scheme="3d", size=size, time_steps=3, dtype="f32", scene="vacuum", use_pml=True,
+                       pml_type="cpml", pml_size=pml, hybrid_block=1, cpml_kappa_max=kappa)
+    s = _live_state(cfg, gpu)
+    alloc = ((0, 0, 0), tuple(s.domain.shape))
+    cuts = s._cpml_cuts()
+    if mode == "all":
+        boxes = [alloc]
+    else:
+        from fdtd3d_amd.parallel.domain import box_subtract
+        K = ((14, 13, 15), (size[0] - 12, size[1] - 14, size[2] - 13))
+        boxes = [b for b in box_subtract(alloc, K) if all(b[1][d] > b[0][d] for d in range(3))]
+    pieces = _merge_pieces([pc for b in boxes for pc in _cut_pieces(b, cuts)])
+    assert any(a == 0 for _, a in pieces) and any(a for _, a in pieces)
+    upd = {c: s.local_box(c, s.domain.allocated_global()) for c in s.comps}
+    src = ("Ez", (size[0] // 3, size[1] // 2, 3), 0.75)  # inside a z slab: hard source next to CPML terms
+    # fp64 torch reference on copies of the state
+    ref = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
+    fin_r = {c: s.F[0][c].double().cpu() for c in s.comps}
+    for c in s.comps:
+        for a, b in zip(ref.cpml.slabs[c], s.cpml.slabs[c]):
+            a.psi[0].copy_(b.psi[0].double().cpu())
+    out_r = {c: torch.full_like(fin_r[c], 7.0) for c in s.comps}
+    ref.ops.shell_step(fin_r, out_r, upd, [b for b, _ in pieces], [a for _, a in pieces], ref.cb, src,
+                       cpml=(ref.cpml, 0), kappa=kappa != 1.0)
+    # the kernel
+    out = {c: torch.full_like(s.F[0][c], 7.0) for c in s.comps}
+    s.ops.shell_step(s.F[0], out, upd, [b for b, _ in pieces], [a for _, a in pieces], s.cb, src,
+                     cpml=s.cpml.device_table(0), kappa=kappa != 1.0)
+    torch.cuda.synchronize()
+    for c in s.comps:
+        scale = max(float(fin_r[o].abs().max()) for o in s.comps if o[0] == c[0])
+        err = float((out[c].double().cpu() - out_r[c]).abs().max())
+        assert err <= 2e-5 * scale, (name, c, err, scale)
+    # psi: the kernel wrote the alternate copy
+    for c in s.comps:
+        src_scale = max(float(fin_r[o].abs().max()) for o in s.comps if o[0] != c[0])
+        for a, b in zip(ref.cpml.slabs[c], s.cpml.slabs[c]):
+            x, y = b.psi_alt[0].double().cpu(), a.psi_alt[0]
+            err = float((x - y).abs().max())
+            assert err <= 2e-5 * src_scale + 1e-4 * float(y.abs().max()), (name, c, "psi", err)
+        assert max(float(a.psi_alt[0].abs().max()) for a in ref.cpml.slabs[c]) > 0 or not ref.cpml.slabs[c]
+
+
+def test_shell_hybrid_selected_and_exact(gpu):
+    """The automatic hybrid plan of a CPML + TF/SF run takes the single-pass
+    shell, and two passes + a tail step equal the stepped run (random fields)."""
+    cfg = SchemeConfig(scheme="3d", size=(96, 88, 104), time_steps=11, dtype="f32", scene="vacuum", use_pml=True,
+                       pml_type="cpml", use_tfsf=True, pml_size=(6, 6, 6), tfsf_size=(9, 9, 9), theta=70, phi=20,
+                       psi=40)
+    runs = []
+    for hb in (0, 1):
+        s = _scheme(dataclasses.replace(cfg, hybrid_block=hb), "hip", gpu, torch.float32)
+        s.randomize_fields(seed=4)
+        if hb == 0:
+            assert s.hybrid is not None and s.hybrid.get("v2"), "single-pass shell not selected"
+        s.perform_steps()
+        torch.cuda.synchronize()
+        runs.append(s)
+    hy, st = runs
+    for c in hy.comps:
+        scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])
+        err = float((hy.F[0][c] - st.F[0][c]).abs().max())
+        assert err <= 2e-5 * scale, (c, err, scale)
