@@ -260,6 +260,50 @@ __global__ __launch_bounds__(256) void k_amplitude_update(const T* __restrict__ 
   if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(changed, cnt);
 }
 
+// All components of a kind at once (blockIdx.y = component), accumulating
+// into a device counter the host reads once per amplitude check period
+// instead of once per component and step.
+struct AmpSet {
+  const void* f[6];
+  void* amp[6];
+  Box3 b[6];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_amplitude_many(AmpSet a, int ny, int nz, double accuracy,
+                                                        unsigned int* __restrict__ changed) {
+  const int c = blockIdx.y;
+  const T* __restrict__ f = (const T*)a.f[c];
+  T* __restrict__ amp = (T*)a.amp[c];
+  const Box3 b = a.b[c];
+  const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1], bz = b.hi[2] - b.lo[2];
+  const long long n = (bx > 0 && by > 0 && bz > 0) ? (long long)bx * by * bz : 0;
+  unsigned int cnt = 0;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(t % bz);
+    const long long r = t / bz;
+    const int j = (int)(r % by);
+    const int i = (int)(r / by);
+    const size_t off = ((size_t)(b.lo[0] + i) * ny + (b.lo[1] + j)) * nz + (b.lo[2] + k);
+    const T v = f[off] < T(0) ? -f[off] : f[off];
+    const T am = amp[off];
+    if (v >= am) {
+      T acc = v - am;
+      if (am != T(0))
+        acc /= am;
+      else if (v != T(0))
+        acc /= v;
+      if (acc > (T)accuracy) {
+        cnt++;
+        amp[off] = v;
+      }
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(changed, cnt);
+}
+
 inline unsigned reduce_grid(long long n) {
   long long g = (n + 255) / 256;
   if (g > 4096) g = 4096;
@@ -320,6 +364,39 @@ inline unsigned reduce_grid(long long n) {
 
 FDTD_AUX_API(f32, float)
 FDTD_AUX_API(f64, double)
+
+template <typename T>
+int amplitude_many(const void* const* f, void* const* amp, int ncomp, int ny, int nz, const int* boxes,
+                   double accuracy, unsigned int* changed, hipStream_t s) {
+  if (ncomp <= 0 || ncomp > 6) return (int)hipErrorInvalidValue;
+  AmpSet a;
+  long long nmax = 0;
+  for (int c = 0; c < 6; ++c) {
+    a.f[c] = c < ncomp ? f[c] : nullptr;
+    a.amp[c] = c < ncomp ? amp[c] : nullptr;
+    a.b[c] = c < ncomp ? make_box(boxes + 6 * c) : Box3{{0, 0, 0}, {0, 0, 0}};
+    if (c < ncomp && !box_empty(a.b[c])) {
+      const Box3& b = a.b[c];
+      const long long n = (long long)(b.hi[0] - b.lo[0]) * (b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]);
+      nmax = n > nmax ? n : nmax;
+    }
+  }
+  if (nmax == 0) return 0;
+  k_amplitude_many<T><<<dim3(reduce_grid(nmax), ncomp), 256, 0, s>>>(a, ny, nz, accuracy, changed);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+// amplitude update of up to 6 components in one launch, the count of changed
+// cells ADDED to *changed (no reset, no host read: models/scheme.py reads a
+// whole check period's counters at once)
+FDTD_API int fdtd_amplitude_many_f32(const void* const* f, void* const* amp, int ncomp, int ny, int nz,
+                                     const int* boxes, double accuracy, unsigned int* changed, void* s) {
+  return amplitude_many<float>(f, amp, ncomp, ny, nz, boxes, accuracy, changed, (hipStream_t)s);
+}
+FDTD_API int fdtd_amplitude_many_f64(const void* const* f, void* const* amp, int ncomp, int ny, int nz,
+                                     const int* boxes, double accuracy, unsigned int* changed, void* s) {
+  return amplitude_many<double>(f, amp, ncomp, ny, nz, boxes, accuracy, changed, (hipStream_t)s);
+}
 
 FDTD_API int fdtd_counter_add(int* counter, int n, void* s) {
   k_counter_add<<<1, 64, 0, (hipStream_t)s>>>(counter, n);

@@ -81,6 +81,49 @@ struct ShCpml {
   ShTerm t[6][3];  // [Ex Ey Ez Hx Hy Hz][axis]
 };
 
+// UPML in the reference's D/B form (Scheme3D.cpp:266-416, models/scheme.py
+// _init_upml) over the shell, with the D (B) levels stored only where some
+// sigma is non-zero: the 6 disjoint boxes of alloc minus the all-sigma-zero
+// core I (x slabs over the whole y, z extent; y slabs over I's x range; z
+// slabs over I's x, y ranges -- models/upml.py UPMLRegions).  Per component,
+// with its profiles as (a, b) pairs per axis -- (caD, cbD) along aD, (caE,
+// ica) along aCa, (cbEa, ccEa) along aCb:
+//   Dn = caD D + cbD curl ;  E = caE E + s ica (cbEa Dn + ccEa D)
+// D is read from one copy and written to the other (halo cells are
+// recomputed by neighbour tiles); cells of no box run the same formula with
+// D = 0, which is the plain update where every sigma vanishes.
+struct ShUpml {
+  int blo[6][3], bhi[6][3];   // D storage boxes (local): x-lo, x-hi, y-lo, y-hi, z-lo, z-hi
+  const float* d[6][6];       // [component][box] D^n
+  float* dn[6][6];            // [component][box] D^{n+1}
+  const float2* pr[6][3];     // [component][axis] profile pairs over the local extent
+  float s[6];                 // scalar of the E-from-D term
+  int pad;
+};
+// Dispersive box (AX == 9): Drude / Lorentz media in the reference's chain
+// form (Kernels.h:103-107, Scheme3D.cpp:326-364; models/scheme.py
+// _init_upml) on the bounding box of the dispersive cells, where every sigma
+// vanishes (caD = caE = 1 etc. as scalars).  Per component with dispersion:
+// three D and D1 levels over the box (cur, prev, next -- the next level is
+// the one no tile reads this step), a uint8 material index + 1 (0: the cell
+// lies outside its row's material range and takes the plain update, exactly
+// the row split of the stepped chain) and the (b0, b1, b2, ma1, ma2) table:
+//   Dn = caD D + cbD curl ; D1n = b0 Dn + b1 D + b2 Dp + ma1 D1 + ma2 D1p
+//   E  = caE E + sica (cbEa D1n + ccEa D1)
+constexpr int SH_LUT = 16;  // coefficient tuples per component (more: stepped shell)
+struct ShDrude {
+  int lo[3], hi[3];
+  const float* d[6][3];       // [component][cur, prev, next]
+  const float* d1[6][3];
+  const unsigned char* id[6]; // null: no dispersion in this component (plain update)
+  const float* lut[6];        // (nlut, 5)
+  float caD[6], cbD[6], caE[6], sica[6], cbEa[6], ccEa[6];
+  int nlut[6];
+};
+
+// (aD, aCa, aCb) per component (layout/yee.py UPML_AXES)
+__device__ constexpr int kUp[6][3] = {{1, 2, 0}, {2, 0, 1}, {0, 1, 2}, {1, 2, 0}, {2, 0, 1}, {0, 1, 2}};
+
 // curl terms of each component: (axis of term 0, axis of term 1); the curl is
 // +d0 - d1 (Ex = dHz/dy - dHy/dz, ..., Hx = dEy/dz - dEz/dy, ...)
 __device__ constexpr int kAx[6][2] = {{1, 2}, {2, 0}, {0, 1}, {2, 1}, {0, 2}, {1, 0}};
@@ -103,24 +146,49 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
     float* __restrict__ exo, float* __restrict__ eyo, float* __restrict__ ezo, float* __restrict__ hxo,
     float* __restrict__ hyo, float* __restrict__ hzo, float cb, float db, int nx, int ny, int nz, Box3 bex,
     Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, ShList L, int src_i, int src_j, int src_k, int src_comp,
-    float src_v, const ShCpml* __restrict__ cp) {
+    float src_v, const ShCpml* __restrict__ cp, const ShUpml* __restrict__ up, const ShDrude* __restrict__ dr) {
   constexpr int G = 64 / LW;         // lane groups (grid rows) per wave
   constexpr int NS = SNW * G;        // lane groups per workgroup
   constexpr int ROWS = NS * SR;      // y rows per tile
-  constexpr bool CPX = AX & 1, CPY = AX & 2, CPZ = AX & 4;
+  constexpr bool UP = AX == 8;       // UPML launch (no CPML terms)
+  constexpr bool DR = AX == 9;       // dispersive-box launch
+  constexpr bool CPX = AX < 8 && (AX & 1), CPY = AX < 8 && (AX & 2), CPZ = AX < 8 && (AX & 4);
+  constexpr bool CPM = AX < 8 && AX != 0;
   __shared__ float sX[2][4][NS][LW];
-  __shared__ ShTerm sT[AX ? 18 : 1];
+  __shared__ ShTerm sT[CPM ? 18 : 1];
+  __shared__ ShUpml sU[1];
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);
   const int g = LW == 64 ? 0 : lane / LW;
   const int li = LW == 64 ? lane : lane % LW;
   const int slot = w * G + g;
-  if constexpr (AX != 0) {
+  if constexpr (CPM) {
     const unsigned* src = (const unsigned*)cp;
     unsigned* dst = (unsigned*)sT;
     for (int q = lane + 64 * w; q < (int)(sizeof(ShTerm) * 18 / 4); q += 64 * SNW) dst[q] = src[q];
     __syncthreads();
   }
+  if constexpr (UP) {
+    const unsigned* src = (const unsigned*)up;
+    unsigned* dst = (unsigned*)sU;
+    for (int q = lane + 64 * w; q < (int)(sizeof(ShUpml) / 4); q += 64 * SNW) dst[q] = src[q];
+    __syncthreads();
+  }
+  const ShUpml& U = sU[0];
+  __shared__ ShDrude sD[1];
+  __shared__ float sL[DR ? 6 : 1][DR ? SH_LUT * 5 : 1];
+  if constexpr (DR) {
+    const unsigned* src = (const unsigned*)dr;
+    unsigned* dst = (unsigned*)sD;
+    for (int q = lane + 64 * w; q < (int)(sizeof(ShDrude) / 4); q += 64 * SNW) dst[q] = src[q];
+    __syncthreads();
+    for (int q = lane + 64 * w; q < 6 * SH_LUT * 5; q += 64 * SNW) {
+      const int n = q / (SH_LUT * 5), e = q % (SH_LUT * 5);
+      sL[n][e] = (sD[0].id[n] && e < 5 * sD[0].nlut[n]) ? sD[0].lut[n][e] : 0.f;
+    }
+    __syncthreads();
+  }
+  const ShDrude& DB = sD[0];
   // ---- box and tile of this workgroup (wave-uniform)
   // (static indices only: a dynamic index into the by-value list would copy
   // it to scratch)
@@ -257,7 +325,9 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
     const int a = kAx[n][t];
     const ShTerm& tm = sT[n * 3 + a];
     const int kd = n < 3 ? 0 : 1;
-    const bool st = ((mbits >> (r * 7 + 6)) & 1u) && ((mbits >> (r * 7 + n)) & 1u) &&
+    // own cells only: halo planes / rows / lanes (recomputed here, owned by a
+    // neighbour tile or chunk) must not write the psi copy
+    const bool st = ((mbits >> (r * 7 + 6)) & 1u) && ((mbits >> (r * 7 + n)) & 1u) && pl >= i0 && pl < i1 &&
                     (unsigned)(pl - bx[n]->lo[0]) < (unsigned)(bx[n]->hi[0] - bx[n]->lo[0]);
     float b = 1.f, c = 0.f, k = 0.f;
     float r_ = 0.f;
@@ -311,7 +381,126 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
     }
   };
   // which terms this launch carries: term (n, t) iff its axis is in AX
-  auto term_on = [](int n, int t) -> bool { return (AX >> kAx[n][t]) & 1; };
+  auto term_on = [](int n, int t) -> bool { return CPM && ((AX >> kAx[n][t]) & 1); };
+
+  // ---- UPML: D box offsets of the tile's rows / lanes (y and z boxes:
+  // per-lane offsets, kBad off the box), z profile pairs of the lane
+  unsigned uyo[2][SR], uzo[2][SR];  // [lo / hi box][row]
+  bool uy_any[2] = {false, false}, uz_any[2] = {false, false};
+  __shared__ float2 sUz[UP ? 6 : 1][UP ? LW : 1];  // z profile pairs of the tile's lanes
+  if constexpr (UP) {
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      const int qy = 2 + sd, qz = 4 + sd;
+      bool ay = false, az = false;
+#pragma unroll
+      for (int r = 0; r < SR; ++r) {
+        const int j = jr0 + r;
+        const bool iny = kin && j >= U.blo[qy][1] && j < U.bhi[qy][1] && kb >= U.blo[qy][2] && kb < U.bhi[qy][2];
+        uyo[sd][r] = iny ? (unsigned)((j - U.blo[qy][1]) * (U.bhi[qy][2] - U.blo[qy][2]) + kb - U.blo[qy][2]) * 4u
+                         : kBad;
+        const bool inz = kin && j >= U.blo[qz][1] && j < U.bhi[qz][1] && kb >= U.blo[qz][2] && kb < U.bhi[qz][2];
+        uzo[sd][r] = inz ? (unsigned)((j - U.blo[qz][1]) * (U.bhi[qz][2] - U.blo[qz][2]) + kb - U.blo[qz][2]) * 4u
+                         : kBad;
+        ay |= iny;
+        az |= inz;
+      }
+      uy_any[sd] = __any(ay);
+      uz_any[sd] = __any(az);
+    }
+    if (w == 0 && g == 0) {
+#pragma unroll
+      for (int n = 0; n < 6; ++n) sUz[n][li] = kin ? U.pr[n][2][kb] : make_float2(1.f, 0.f);
+    }
+    __syncthreads();
+  }
+  // descriptor of plane pl of D storage box q of component n (read / written copy)
+  auto ud_rs = [&](int n, int q, int pl, bool wr) -> Rsrc {
+    const size_t pp = (size_t)(U.bhi[q][1] - U.blo[q][1]) * (U.bhi[q][2] - U.blo[q][2]);
+    const bool in = pl >= U.blo[q][0] && pl < U.bhi[q][0];
+    const float* base = wr ? (const float*)U.dn[n][q] : U.d[n][q];
+    return mk_rs(base + (size_t)(in ? pl - U.blo[q][0] : 0) * pp, in ? (unsigned)(pp * 4) : 0u);
+  };
+  // x box holding plane pl (-1: none); x boxes span the whole y / z extent
+  auto ux_box = [&](int pl) -> int {
+    return (pl >= U.blo[0][0] && pl < U.bhi[0][0]) ? 0 : ((pl >= U.blo[1][0] && pl < U.bhi[1][0]) ? 1 : -1);
+  };
+  // D of component n at plane pl, row r (0 outside every box)
+  auto ud_load = [&](int n, int pl, int r) -> float {
+    const int xb = ux_box(pl);
+    if (xb >= 0) return ldf(ud_rs(n, xb, pl, false), roff[r]);
+    float v = 0.f;
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      if (uy_any[sd]) v += ldf(ud_rs(n, 2 + sd, pl, false), uyo[sd][r]);
+      if (uz_any[sd]) v += ldf(ud_rs(n, 4 + sd, pl, false), uzo[sd][r]);
+    }
+    return v;
+  };
+  auto ud_store = [&](int n, int pl, int r, float v, bool st) {
+    const int xb = ux_box(pl);
+    if (xb >= 0) {
+      stf(ud_rs(n, xb, pl, true), st ? roff[r] : kBad, v);
+      return;
+    }
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      if (uy_any[sd]) stf(ud_rs(n, 2 + sd, pl, true), st ? uyo[sd][r] : kBad, v);
+      if (uz_any[sd]) stf(ud_rs(n, 4 + sd, pl, true), st ? uzo[sd][r] : kBad, v);
+    }
+  };
+  // profile pair of component n along axis a at plane pl / row r / this lane
+  auto upair = [&](int n, int a, int pl, int r) -> float2 {
+    if (a == 0) return U.pr[n][0][pl];
+    if (a == 1) {
+      const int j = jr0 + r;
+      return (j >= 0 && j < ny) ? U.pr[n][1][j] : make_float2(1.f, 0.f);
+    }
+    return sUz[UP ? n : 0][UP ? li : 0];
+  };
+  // the UPML update of component n (E kind n < 3 on plane X, H on X - 1) from
+  // its raw curl; returns the new field value
+  auto upml = [&](int n, int pl, int r, float f, float curl, float Dv, bool upd, bool st) -> float {
+    const float2 pD = upair(n, kUp[n][0], pl, r), pA = upair(n, kUp[n][1], pl, r);
+    const float2 pB = upair(n, kUp[n][2], pl, r);
+    const float Dn = pD.x * Dv + pD.y * curl;
+    const float fn = pA.x * f + U.s[n] * pA.y * (pB.x * Dn + pB.y * Dv);
+    ud_store(n, pl, r, Dn, upd && st);
+    return upd ? fn : f;
+  };
+
+  // ---- dispersive box: element offset of each row's lane inside the box
+  // (~0u off the box: byte / float loads past the descriptor read 0 = plain)
+  unsigned dbo[SR];
+  if constexpr (DR) {
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      const int j = jr0 + r;
+      const bool in = kin && j >= DB.lo[1] && j < DB.hi[1] && kb >= DB.lo[2] && kb < DB.hi[2];
+      dbo[r] = in ? (unsigned)((j - DB.lo[1]) * (DB.hi[2] - DB.lo[2]) + kb - DB.lo[2]) : 0x3C000000u;
+    }
+  }
+  auto db_rs = [&](const void* base, int pl, unsigned esz) -> Rsrc {
+    const size_t pp = (size_t)(DB.hi[1] - DB.lo[1]) * (DB.hi[2] - DB.lo[2]);
+    const bool in = base && pl >= DB.lo[0] && pl < DB.hi[0];
+    return mk_rs((const char*)base + (in ? (size_t)(pl - DB.lo[0]) * pp * esz : 0), in ? (unsigned)(pp * esz) : 0u);
+  };
+  // dispersive update of component n on plane pl, row r (plain where id = 0)
+  auto drude = [&](int n, int pl, int r, float f, float curl, float pc, bool upd, bool st) -> float {
+    const unsigned id = DB.id[n] ? __builtin_amdgcn_raw_buffer_load_b8(db_rs(DB.id[n], pl, 1), dbo[r], 0, 0) : 0u;
+    if (id == 0u) return f + (upd ? pc : 0.f) * curl;
+    const unsigned o = dbo[r] * 4u;
+    const float D = ldf(db_rs(DB.d[n][0], pl, 4), o), Dp = ldf(db_rs(DB.d[n][1], pl, 4), o);
+    const float D1 = ldf(db_rs(DB.d1[n][0], pl, 4), o), D1p = ldf(db_rs(DB.d1[n][1], pl, 4), o);
+    const float* e = &sL[DR ? n : 0][DR ? 5 * (id - 1) : 0];
+    const float Dn = DB.caD[n] * D + DB.cbD[n] * curl;
+    const float D1n = e[0] * Dn + e[1] * D + e[2] * Dp + e[3] * D1 + e[4] * D1p;
+    const float fn = DB.caE[n] * f + DB.sica[n] * (DB.cbEa[n] * D1n + DB.ccEa[n] * D1);
+    const bool w_ = upd && st;
+    stf(db_rs(DB.d[n][2], pl, 4), w_ ? o : kBad, Dn);
+    stf(db_rs(DB.d1[n][2], pl, 4), w_ ? o : kBad, D1n);
+    return upd ? fn : f;
+  };
 
   float Hp[SR][3], Ep[SR][3];  // H^n(X-1) and E^{n+1}(X-1)
 #pragma unroll
@@ -350,7 +539,16 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < SR; ++r) PS[n][t][r] = (AX && term_on(n, t)) ? psi_load(n, t, n < 3 ? X : X - 1, r) : 0.f;
+        for (int r = 0; r < SR; ++r) PS[n][t][r] = term_on(n, t) ? psi_load(n, t, n < 3 ? X : X - 1, r) : 0.f;
+    float DV[UP ? 6 : 1][SR];
+    if constexpr (UP) {
+#pragma unroll
+      for (int n = 0; n < 6; ++n)
+#pragma unroll
+        for (int r = 0; r < SR; ++r)
+          DV[n][r] = (n < 3 ? (X >= 0 && X < nx) : (X - 1 >= 0 && X - 1 < nx)) ? ud_load(n, n < 3 ? X : X - 1, r)
+                                                                             : 0.f;
+    }
     load_plane(X + 1, Hn_, En_);
     // y neighbours: H(X) of the group's last row for the group above, E^{n+1}(X-1)
     // of its first row for the group below
@@ -373,7 +571,7 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
       const float dyz = Hc[r][0] - hx_k, dyx = Hc[r][2] - Hp[r][2];
       const float dzx = Hc[r][1] - Hp[r][1], dzy = Hc[r][0] - hx_j;
       float cx = dxy - dxz, cy = dyz - dyx, cz = dzx - dzy;
-      if constexpr (AX != 0) {
+      if constexpr (CPM) {
         if (term_on(0, 0)) cx += psi_step(0, 0, X, r, PS[0][0][r], dxy);
         if (term_on(0, 1)) cx -= psi_step(0, 1, X, r, PS[0][1][r], dxz);
         if (term_on(1, 0)) cy += psi_step(1, 0, X, r, PS[1][0][r], dyz);
@@ -381,9 +579,21 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
         if (term_on(2, 0)) cz += psi_step(2, 0, X, r, PS[2][0][r], dzx);
         if (term_on(2, 1)) cz -= psi_step(2, 1, X, r, PS[2][1][r], dzy);
       }
-      En[r][0] = Ec[r][0] + coef(0, r, X, cb) * cx;
-      En[r][1] = Ec[r][1] + coef(1, r, X, cb) * cy;
-      En[r][2] = Ec[r][2] + coef(2, r, X, cb) * cz;
+      if constexpr (UP) {
+        const bool se_ = (mbits >> (r * 7 + 6)) & 1u && X >= i0 && X < i1;
+        En[r][0] = upml(0, X, r, Ec[r][0], cx, DV[0][r], coef(0, r, X, 1.f) != 0.f, se_);
+        En[r][1] = upml(1, X, r, Ec[r][1], cy, DV[1][r], coef(1, r, X, 1.f) != 0.f, se_);
+        En[r][2] = upml(2, X, r, Ec[r][2], cz, DV[2][r], coef(2, r, X, 1.f) != 0.f, se_);
+      } else if constexpr (DR) {
+        const bool se_ = (mbits >> (r * 7 + 6)) & 1u && X >= i0 && X < i1;
+        En[r][0] = drude(0, X, r, Ec[r][0], cx, cb, coef(0, r, X, 1.f) != 0.f, se_);
+        En[r][1] = drude(1, X, r, Ec[r][1], cy, cb, coef(1, r, X, 1.f) != 0.f, se_);
+        En[r][2] = drude(2, X, r, Ec[r][2], cz, cb, coef(2, r, X, 1.f) != 0.f, se_);
+      } else {
+        En[r][0] = Ec[r][0] + coef(0, r, X, cb) * cx;
+        En[r][1] = Ec[r][1] + coef(1, r, X, cb) * cy;
+        En[r][2] = Ec[r][2] + coef(2, r, X, cb) * cz;
+      }
       if (src_comp >= 0 && X == src_i && jr0 + r == src_j && kb == src_k) {
         if (src_comp == 0) En[r][0] = src_v;
         if (src_comp == 1) En[r][1] = src_v;
@@ -401,7 +611,7 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
       const float gyx = En[r][2] - Ep[r][2], gyz = ex_k - Ep[r][0];
       const float gzy = ex_j - Ep[r][0], gzx = En[r][1] - Ep[r][1];
       float dx = gxz - gxy, dy = gyx - gyz, dz = gzy - gzx;
-      if constexpr (AX != 0) {
+      if constexpr (CPM) {
         if (term_on(3, 0)) dx += psi_step(3, 0, X - 1, r, PS[3][0][r], gxz);
         if (term_on(3, 1)) dx -= psi_step(3, 1, X - 1, r, PS[3][1][r], gxy);
         if (term_on(4, 0)) dy += psi_step(4, 0, X - 1, r, PS[4][0][r], gyx);
@@ -409,9 +619,21 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
         if (term_on(5, 0)) dz += psi_step(5, 0, X - 1, r, PS[5][0][r], gzy);
         if (term_on(5, 1)) dz -= psi_step(5, 1, X - 1, r, PS[5][1][r], gzx);
       }
-      Hn[r][0] = Hp[r][0] + coef(3, r, X - 1, db) * dx;
-      Hn[r][1] = Hp[r][1] + coef(4, r, X - 1, db) * dy;
-      Hn[r][2] = Hp[r][2] + coef(5, r, X - 1, db) * dz;
+      if constexpr (UP) {
+        const bool sh_ = (mbits >> (r * 7 + 6)) & 1u && X - 1 >= i0 && X - 1 < i1;
+        Hn[r][0] = upml(3, X - 1, r, Hp[r][0], dx, DV[3][r], coef(3, r, X - 1, 1.f) != 0.f, sh_);
+        Hn[r][1] = upml(4, X - 1, r, Hp[r][1], dy, DV[4][r], coef(4, r, X - 1, 1.f) != 0.f, sh_);
+        Hn[r][2] = upml(5, X - 1, r, Hp[r][2], dz, DV[5][r], coef(5, r, X - 1, 1.f) != 0.f, sh_);
+      } else if constexpr (DR) {
+        const bool sh_ = (mbits >> (r * 7 + 6)) & 1u && X - 1 >= i0 && X - 1 < i1;
+        Hn[r][0] = drude(3, X - 1, r, Hp[r][0], dx, db, coef(3, r, X - 1, 1.f) != 0.f, sh_);
+        Hn[r][1] = drude(4, X - 1, r, Hp[r][1], dy, db, coef(4, r, X - 1, 1.f) != 0.f, sh_);
+        Hn[r][2] = drude(5, X - 1, r, Hp[r][2], dz, db, coef(5, r, X - 1, 1.f) != 0.f, sh_);
+      } else {
+        Hn[r][0] = Hp[r][0] + coef(3, r, X - 1, db) * dx;
+        Hn[r][1] = Hp[r][1] + coef(4, r, X - 1, db) * dy;
+        Hn[r][2] = Hp[r][2] + coef(5, r, X - 1, db) * dz;
+      }
     }
     // ---- stores: E^{n+1}(X), H^{n+1}(X-1) of the tile's own cells
     const bool se = X >= i0 && X < i1, sh = X - 1 >= i0 && X - 1 < i1;
@@ -441,22 +663,27 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
 
 template <int AX, bool KAP, int LW>
 int launch_shell(const float* const* fi, float* const* fo, float cb, float db, int nx, int ny, int nz,
-                 const Box3* b, const ShList& L, const int* src, float sv, const ShCpml* cp, hipStream_t s) {
+                 const Box3* b, const ShList& L, const int* src, float sv, const ShCpml* cp, const ShUpml* up,
+                 const ShDrude* dr, hipStream_t s) {
   k_shell1<AX, KAP, LW><<<L.first[L.n], dim3(64, SNW), 0, s>>>(
       fi[0], fi[1], fi[2], fi[3], fi[4], fi[5], fo[0], fo[1], fo[2], fo[3], fo[4], fo[5], cb, db, nx, ny, nz, b[0],
-      b[1], b[2], b[3], b[4], b[5], L, src[0], src[1], src[2], src[3], sv, cp);
+      b[1], b[2], b[3], b[4], b[5], L, src[0], src[1], src[2], src[3], sv, cp, up, dr);
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
 template <int AX>
 int launch_shell_ax(bool kap, int lw, const float* const* fi, float* const* fo, float cb, float db, int nx, int ny,
                     int nz, const Box3* b, const ShList& L, const int* src, float sv, const ShCpml* cp,
-                    hipStream_t s) {
+                    const ShUpml* up, const ShDrude* dr, hipStream_t s) {
+  if constexpr (AX == 8 || AX == 9 || AX == 0) {  // no kappa term: one variant
+    if (lw == 32) return launch_shell<AX, false, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s);
+    return launch_shell<AX, false, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s);
+  }
   if (lw == 32)
-    return kap ? launch_shell<AX, true, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, s)
-               : launch_shell<AX, false, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, s);
-  return kap ? launch_shell<AX, true, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, s)
-             : launch_shell<AX, false, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, s);
+    return kap ? launch_shell<AX, true, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s)
+               : launch_shell<AX, false, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s);
+  return kap ? launch_shell<AX, true, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s)
+             : launch_shell<AX, false, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s);
 }
 
 }  // namespace
@@ -464,25 +691,30 @@ int launch_shell_ax(bool kap, int lw, const float* const* fi, float* const* fo, 
 // One step of the shell: reads fin (Ex Ey Ez Hx Hy Hz), writes fout on the
 // `nwin` output boxes `wins` (6 ints each, local; disjoint) -- cells of a box
 // outside a component's update box (`boxes`, 6 x 6 ints) are stored
-// unchanged.  `ax[w]` = CPML axes of box w (bit 0 x, 1 y, 2 z: the absorbing
-// slabs it may touch; 0 = none; any superset is correct), `cpml` = device
-// CpmlDev block of models/cpml.py (psi read from psi[p], written to the alt
-// copy; null when no box has CPML axes), `kap` = some 1/kappa - 1 is non-zero.
-// `src` = {i, j, k, comp} of a hard E point source (comp -1: none), value
-// `src_val`.  Boxes at most 30 cells deep in z run 32-lane rows.
+// unchanged.  `ax[w]` = absorbing-layer axes of box w (bit 0 x, 1 y, 2 z: the
+// slabs it may touch; 0 = none; any superset is correct).  CPML runs pass
+// `cpml` = device CpmlDev block of models/cpml.py (psi read from psi[p],
+// written to the alt copy) and `kap` = some 1/kappa - 1 is non-zero; UPML
+// runs pass `upml` = device ShUpml block of models/upml.py (every box with
+// ax != 0 runs the D/B chain).  `src` = {i, j, k, comp} of a hard E point
+// source (comp -1: none), value `src_val`.  Boxes at most 30 cells deep in z
+// run 32-lane rows.
 FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double cb, double db, int nx, int ny,
                              int nz, const int* boxes, int nwin, const int* wins, const int* ax, const int* src,
-                             double src_val, const void* cpml, int kap, void* stream) {
-  if (nwin < 0 || (cpml == nullptr && nwin > 0)) {
-    for (int w = 0; w < nwin; ++w)
-      if (ax[w]) return (int)hipErrorInvalidValue;
+                             double src_val, const void* cpml, int kap, const void* upml, const void* drude,
+                             void* stream) {
+  if (nwin < 0 || (cpml && upml)) return (int)hipErrorInvalidValue;
+  for (int w = 0; w < nwin; ++w) {
+    if ((ax[w] & 8) && !drude) return (int)hipErrorInvalidValue;
+    if ((ax[w] & 7) && !cpml && !upml) return (int)hipErrorInvalidValue;
   }
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const hipStream_t s = (hipStream_t)stream;
-  // group the boxes by (CPML class, lane width); classes: none, x, y, z, all
-  const int classes[5] = {0, 1, 2, 4, 7};
-  for (int ci = 0; ci < 5; ++ci) {
+  // group the boxes by (class, lane width); classes: none, CPML x, y, z,
+  // CPML all axes (edges, corners), UPML
+  const int classes[7] = {0, 1, 2, 4, 7, 8, 9};
+  for (int ci = 0; ci < 7; ++ci) {
     for (int lw : {64, 32}) {
       ShList L;
       L.n = 0;
@@ -493,7 +725,7 @@ FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double
         const Box3 o = make_box(wins + 6 * wi);
         if (box_empty(o)) continue;
         const int a = ax[wi];
-        const int cls = a == 0 ? 0 : ((a == 1 || a == 2 || a == 4) ? a : 7);
+        const int cls = a == 0 ? 0 : ((a & 8) ? 9 : (upml ? 8 : ((a == 1 || a == 2 || a == 4) ? a : 7)));
         if (cls != classes[ci]) continue;
         const int zl = o.hi[2] - o.lo[2];
         if ((zl <= 30) != (lw == 32)) continue;
@@ -526,19 +758,21 @@ FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double
         }
         L.first[L.n] = first;
         const ShCpml* cp = (const ShCpml*)cpml;
+        const ShUpml* up = (const ShUpml*)upml;
+        const ShDrude* dr = (const ShDrude*)drude;
+        const float fc = (float)cb, fd = (float)db, sv = (float)src_val;
         int rc = 0;
+#define SH_CASE(A) rc = launch_shell_ax<A>(kap != 0, lw, fin, fout, fc, fd, nx, ny, nz, b, L, src, sv, cp, up, dr, s)
         switch (classes[ci]) {
-          case 0: rc = launch_shell_ax<0>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
-                                          (float)src_val, cp, s); break;
-          case 1: rc = launch_shell_ax<1>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
-                                          (float)src_val, cp, s); break;
-          case 2: rc = launch_shell_ax<2>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
-                                          (float)src_val, cp, s); break;
-          case 4: rc = launch_shell_ax<4>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
-                                          (float)src_val, cp, s); break;
-          default: rc = launch_shell_ax<7>(kap, lw, fin, fout, (float)cb, (float)db, nx, ny, nz, b, L, src,
-                                           (float)src_val, cp, s); break;
+          case 0: SH_CASE(0); break;
+          case 1: SH_CASE(1); break;
+          case 2: SH_CASE(2); break;
+          case 4: SH_CASE(4); break;
+          case 7: SH_CASE(7); break;
+          case 8: SH_CASE(8); break;
+          default: SH_CASE(9); break;
         }
+#undef SH_CASE
         if (rc) return rc;
       }
     }
@@ -548,3 +782,9 @@ FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double
 
 // size of the CPML block (ABI check against models/cpml.py device_table)
 FDTD_API int fdtd_shell_cpml_size() { return (int)sizeof(ShCpml); }
+
+// size of the UPML block (ABI check against models/upml.py)
+FDTD_API int fdtd_shell_upml_size() { return (int)sizeof(ShUpml); }
+
+// size of the dispersive-box block (ABI check against models/upml.py DrudeBox)
+FDTD_API int fdtd_shell_drude_size() { return (int)sizeof(ShDrude); }

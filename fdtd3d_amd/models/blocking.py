@@ -77,13 +77,17 @@ def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: 
 
 
 def _cut_pieces(b: Box, cuts):
-    """``b`` split at the CPML slab cuts of every axis: [(box, axes bits)],
-    bit a set when the piece lies in an absorbing slab along axis a."""
+    """``b`` split at the absorbing-slab cuts of every axis: [(box, axes
+    bits)], bit a set when the piece may touch a slab along axis a.  The
+    high-side cut moves one cell down: a tile recomputes its halo cells with
+    its own specialisation, and the H update of the last cell below a high
+    slab reads the new E of the first slab cell (H^{n+1} needs E^{n+1} at
+    +1 along every axis; E^{n+1} needs only H^n, so the low side is exact)."""
     pieces = [(b, 0)]
     for a in range(3):
         if cuts[a] is None:
             continue
-        lo_c, hi_c = cuts[a]
+        lo_c, hi_c = cuts[a][0], cuts[a][1] - 1
         nxt = []
         for pb, ax in pieces:
             for s_lo, s_hi, slab in ((None, lo_c, True), (lo_c, hi_c, False), (hi_c, None, True)):
@@ -96,6 +100,17 @@ def _cut_pieces(b: Box, cuts):
                 nxt.append(((tuple(lo), tuple(hi)), ax | ((1 << a) if slab else 0)))
         pieces = nxt
     return [(pb, ax) for pb, ax in pieces if not box_empty(pb)]
+
+
+def _cut_box(b: Box, box: Box):
+    """``b`` split at a dispersive box: [(piece, 8)] for the part within
+    [box.lo - 1, box.hi) on every axis (the cell below the box's low face
+    updates H from the box's new E), [(piece, 0)] for the rest."""
+    lo = tuple(box[0][d] - 1 for d in range(3))
+    inner = (tuple(max(b[0][d], lo[d]) for d in range(3)), tuple(min(b[1][d], box[1][d]) for d in range(3)))
+    if box_empty(inner):
+        return [(b, 0)]
+    return [(inner, 8)] + [(r, 0) for r in box_subtract(b, inner) if not box_empty(r)]
 
 
 def _merge_pieces(pieces):
@@ -252,9 +267,12 @@ class BlockedStepping:
                 return
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
                 return
-        if self._hybrid2_ok():
+        if self._hybrid2_ok() and self._hybrid2_regions():
             plan = self._hybrid2_plan(H)
-            if plan is not None:
+            if plan is None:
+                self.upml_regions = None
+                self.drude_box = None
+            else:
                 if not hasattr(self, "F_alt"):
                     self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
                 self.F_3 = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
@@ -277,17 +295,26 @@ class BlockedStepping:
     # ------------------------------------------------ hybrid, single-pass shell
     def _hybrid2_ok(self) -> bool:
         """Runs whose shell the fused single-step shell kernel can advance
-        (csrc/yee3d_shell.hip): 3D serial CPML (no UPML / dispersive chain),
-        uniform media (scalar coefficients), plane waves through the TF/SF
-        tables.  ``hybrid_shell`` = auto / single-pass selects it, stepped
-        keeps the per-step kernels."""
+        (csrc/yee3d_shell.hip): 3D serial runs with CPML, UPML (D/B form),
+        dispersive (Drude / Lorentz) boxes inside the all-sigma-zero core, or
+        plane waves in an open box; uniform background media (scalar
+        coefficients); plane waves through the TF/SF tables.  ``hybrid_shell``
+        = auto / single-pass selects it, stepped keeps the per-step kernels."""
         cfg = self.cfg
         mode = getattr(cfg, "hybrid_shell", "auto")
         if mode not in ("auto", "single-pass") or not hasattr(self.ops, "shell_step"):
             return False
-        if (cfg.scheme != "3d" or self.halo is not None or self.use_upml_chain or cfg.use_metamaterials
-                or cfg.use_amp_mode or not (cfg.use_pml and self.use_cpml)):
+        if cfg.scheme != "3d" or self.halo is not None or cfg.use_amp_mode:
             return False
+        upml = cfg.use_pml and self.use_upml_chain
+        if not ((cfg.use_pml and self.use_cpml) or upml or (not cfg.use_pml and (cfg.use_tfsf or
+                                                                               cfg.use_metamaterials))):
+            return False
+        if self.use_upml_chain:
+            for c in self.comps:
+                st = self.upml[c]
+                if st["prof"]["cell"] is not None or ("plain" in st and st["plain"]["prof"]["cell"] is not None):
+                    return False
         if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
             return False
         if any(getattr(self.cb[c], "cell", None) is not None for c in self.comps):
@@ -295,7 +322,7 @@ class BlockedStepping:
         # the kernel shares one slab geometry per (kind, axis): the terms of
         # a kind along y / z must have the same psi slab ranges
         by = {}
-        for c, slabs in self.cpml.slabs.items():
+        for c, slabs in (self.cpml.slabs.items() if self.use_cpml else ()):
             for sl in slabs:
                 key = (c[0], sl.axis, sl.side)
                 rng = (sl.lbox[0][sl.axis], sl.lbox[1][sl.axis])
@@ -303,21 +330,45 @@ class BlockedStepping:
                     return False
         return True
 
+    def _hybrid2_regions(self) -> bool:
+        """Region-local UPML / dispersive state of the single-pass shell
+        (models/upml.py); False when the run does not fit it."""
+        cfg = self.cfg
+        self.upml_regions = None
+        self.drude_box = None
+        try:
+            if cfg.use_pml and self.use_upml_chain:
+                from .upml import UPMLRegions
+                self.upml_regions = UPMLRegions(self)
+            if cfg.use_metamaterials:
+                from .upml import DrudeBox
+                self.drude_box = DrudeBox(self)
+                if self.upml_regions is not None:
+                    I, B = self.upml_regions.core, self.drude_box.box
+                    if box_intersect(I, B) != B:
+                        raise ValueError("dispersive box reaches an absorbing layer")
+        except ValueError:
+            self.upml_regions = None
+            self.drude_box = None
+            return False
+        return True
+
     def _hybrid2_plan(self, T: int):
         """Blocked core + single-pass shell with shrinking windows.
 
-        The core ``K`` -- cells at least ``T + 2`` from every CPML slab and
-        TF/SF target -- takes one ``T``-step blocked pass of the plain kernel.
-        The shell -- everything else -- takes ``T`` fused single steps
-        (``ops.shell_step``), step ``s`` over ``alloc - K.shrink(T - s)``:
-        each step's window is one cell deeper into the core than the next
-        needs, so every shell value is exact without a stale band (the
-        deep-halo rule, reference ``ParallelGrid.cpp:2365-2489``).
-        Single-step passes read one buffer and write another, so the shell
-        ping-pongs between ``F_alt`` and a third buffer while the core reads
-        the untouched ``F``.  Each window is cut at the CPML slab boundaries
-        into boxes tagged with the axes whose slab they touch (the kernel's
-        per-launch specialisation)."""
+        The core -- cells at least ``T + 2`` from every absorbing-layer cell,
+        TF/SF target and dispersive cell -- takes one ``T``-step blocked pass
+        of the plain kernel (``K``, minus the dispersive box grown by
+        ``T + 2``).  The shell -- everything else -- takes ``T`` fused single
+        steps (``ops.shell_step``), step ``s`` over ``alloc`` minus the core
+        shrunk by ``T - s`` on its inner sides: each step's window is one cell
+        deeper into the core than the next needs, so every shell value is
+        exact without a stale band (the deep-halo rule, reference
+        ``ParallelGrid.cpp:2365-2489``).  Single-step passes read one buffer
+        and write another, so the shell ping-pongs between ``F_alt`` and a
+        third buffer while the core reads the untouched ``F``.  Each window
+        is cut at the absorbing-slab and dispersive-box boundaries into boxes
+        tagged with the kernel's specialisation (axes bits; 8 = dispersive)."""
         cfg = self.cfg
         size = cfg.size
         m = T + 2
@@ -326,41 +377,88 @@ class BlockedStepping:
             edge = self.layout.pml_size[a] if cfg.use_pml else 0
             if cfg.use_tfsf:
                 edge = max(edge, cfg.tfsf_size[a] + 1)
-            lo[a], hi[a] = edge + m, size[a] - edge - m
+            if edge > 0:
+                lo[a], hi[a] = edge + m, size[a] - edge - m
         K = (tuple(lo), tuple(hi))
-        if box_empty(K) or box_volume(K) < 0.25 * size[0] * size[1] * size[2]:
+        if box_empty(K):
             return None
-        # every CPML slab and TF/SF target must stay T + 1 clear of the core
-        # (its dependency cone; also keeps the host-side TF/SF additions to
-        # the shell's input buffer out of what the core pass reads)
-        g = (tuple(lo[d] - T - 1 for d in range(3)), tuple(hi[d] + T + 1 for d in range(3)))
-        for slabs in self.cpml.slabs.values():
-            for sl in slabs:
-                if not box_empty(box_intersect(g, sl.gbox)):
-                    return None
-        if cfg.use_tfsf:
-            lg = self.domain.to_local(g)
-            for c in self.comps:
-                for tab in self.tfsf[c]:
-                    if tab.n == 0:
-                        continue
-                    ijk = tab.ijk.view(-1, 3)
-                    inside = torch.ones(ijk.shape[0], dtype=torch.bool, device=ijk.device)
-                    for d in range(3):
-                        inside &= (ijk[:, d] >= lg[0][d]) & (ijk[:, d] < lg[1][d])
-                    if bool(inside.any()):
+        dom = self.domain
+        alloc = dom.allocated_global()
+        dbox = getattr(self, "drude_box", None)
+        Dm = None
+        couts = [K]
+        if dbox is not None:
+            B = dom.to_global(dbox.box)
+            Dm = box_intersect((tuple(B[0][d] - m for d in range(3)), tuple(B[1][d] + m for d in range(3))), K)
+            if not box_empty(Dm):
+                couts = [b for b in box_subtract(K, Dm) if not box_empty(b)]
+        core_cells = sum(box_volume(b) for b in couts)
+        if core_cells < 0.25 * size[0] * size[1] * size[2]:
+            return None
+
+        def grow(b, n):
+            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
+
+        # every irregular cell must stay T + 1 clear of the core (its
+        # dependency cone; also keeps the host-side TF/SF additions to the
+        # shell's input buffer out of what the core pass reads)
+        ureg = getattr(self, "upml_regions", None)
+        for ob in couts:
+            g = grow(ob, T + 1)
+            for slabs in (self.cpml.slabs.values() if self.use_cpml else ()):
+                for sl in slabs:
+                    if not box_empty(box_intersect(g, sl.gbox)):
                         return None
-        alloc = self.domain.allocated_global()
+            lg = dom.to_local(g)
+            if ureg is not None and box_intersect(lg, ureg.core) != box_intersect(lg, dom.to_local(alloc)):
+                return None  # the core's cone must see no UPML cell
+            if dbox is not None and not box_empty(box_intersect(lg, dbox.box)):
+                return None
+            if cfg.use_tfsf and self._tfsf_targets_in(lg):
+                return None
+        if cfg.use_tfsf and (ureg is not None or dbox is not None):
+            # E-form corrections only where the update is the plain one
+            if ureg is not None and self._tfsf_targets_in(ureg.core, outside=True):
+                return None
+            if dbox is not None and self._tfsf_targets_in(grow(dbox.box, 1)):
+                return None
         cuts = self._cpml_cuts()
+
+        def shrink_inner(b, n):
+            return (tuple(b[0][d] + (n if b[0][d] > 0 else 0) for d in range(3)),
+                    tuple(b[1][d] - (n if b[1][d] < size[d] else 0) for d in range(3)))
+
         windows = []
         for st in range(1, T + 1):
             d = T - st
-            Kd = (tuple(lo[a] + d for a in range(3)), tuple(hi[a] - d for a in range(3)))
-            boxes = [self.domain.to_local(b) for b in box_subtract(alloc, Kd) if not box_empty(b)]
-            windows.append(_merge_pieces([pc for b in boxes for pc in _cut_pieces(b, cuts)]))
+            Kd = shrink_inner(K, d)
+            pieces = []
+            for b in box_subtract(alloc, Kd):
+                if not box_empty(b):
+                    pieces += _cut_pieces(dom.to_local(b), cuts)
+            if Dm is not None and not box_empty(Dm):
+                inner = box_intersect(grow(Dm, d), Kd)
+                if not box_empty(inner):
+                    pieces += _cut_box(dom.to_local(inner), dbox.box)
+            windows.append(_merge_pieces(pieces))
         upd = {c: self.local_box(c, alloc) for c in self.comps}
-        return {"T": T, "v2": True, "core": [self.domain.to_local(K)], "windows": windows, "upd": upd,
-                "core_cells": box_volume(K)}
+        return {"T": T, "v2": True, "core": [dom.to_local(b) for b in couts], "windows": windows, "upd": upd,
+                "core_cells": core_cells}
+
+    def _tfsf_targets_in(self, lbox: Box, outside: bool = False) -> bool:
+        """True when some TF/SF target lies inside the local box (``outside``:
+        outside it)."""
+        for c in self.comps:
+            for tab in self.tfsf[c]:
+                if tab.n == 0:
+                    continue
+                ijk = tab.ijk.view(-1, 3)
+                inside = torch.ones(ijk.shape[0], dtype=torch.bool, device=ijk.device)
+                for d in range(3):
+                    inside &= (ijk[:, d] >= lbox[0][d]) & (ijk[:, d] < lbox[1][d])
+                if bool((~inside if outside else inside).any()):
+                    return True
+        return False
 
     def _cpml_cuts(self):
         """Per axis (low cut, high cut) of the CPML slabs, local indices:
@@ -368,7 +466,12 @@ class BlockedStepping:
         axis's psi terms (None: no slab along the axis)."""
         cuts = [None, None, None]
         n = self.domain.shape
-        for slabs in self.cpml.slabs.values():
+        ureg = getattr(self, "upml_regions", None)
+        if ureg is not None:
+            # the D boxes: everything outside the all-sigma-zero core
+            I = ureg.core
+            return [(I[0][a], I[1][a]) if (I[0][a] > 0 or I[1][a] < n[a]) else None for a in range(3)]
+        for slabs in (self.cpml.slabs.values() if self.use_cpml else ()):
             for sl in slabs:
                 a = sl.axis
                 b = self.domain.to_local(sl.gbox)
@@ -422,11 +525,20 @@ class BlockedStepping:
                         self.ops.inc_step_e(self.einc[p], self.hinc[p], self.inc_ce, self.source_value(t, p))
                         self._tfsf_kind("E", p, cur)
                     sv = None if srcs[p] is None else srcs[p][st - 1]
-                    cp = self.cpml.shell_arg(p, self.ops)
+                    cp = self.cpml.shell_arg(p, self.ops) if self.use_cpml else None
+                    ureg = getattr(self, "upml_regions", None)
                     pieces = hp["windows"][st - 1]
+                    dbox = getattr(self, "drude_box", None)
                     self.ops.shell_step(cur, out, hp["upd"], [b for b, _ in pieces], [a for _, a in pieces],
-                                        self.cb, sv, cpml=cp, kappa=kappa)
-                    self.cpml.flip(p)
+                                        self.cb, sv, cpml=cp, kappa=kappa,
+                                        upml=None if ureg is None else ureg.shell_arg(p, self.ops),
+                                        drude=None if dbox is None else dbox.shell_arg(p, self.ops))
+                    if self.use_cpml:
+                        self.cpml.flip(p)
+                    if ureg is not None:
+                        ureg.flip(p)
+                    if dbox is not None:
+                        dbox.rotate(p)
                     if tfsf:
                         # incident line H half step, H corrections on the OUTPUT
                         self.ops.inc_step_h(self.einc[p], self.hinc[p], self.inc_ch)

@@ -104,6 +104,7 @@ class SchemeConfig:
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
     lorentz_omega0_ratio: float = 0.5        # Lorentz resonance / source frequency
+    amplitude_check_steps: int = 8           # amplitude mode: steps between host reads of the changed counts
 
     @classmethod
     def from_settings(cls, s) -> "SchemeConfig":
@@ -132,6 +133,7 @@ class SchemeConfig:
             ntff_step=s.ntffStep, check_finite=s.doCheckFinite, finite_check_step=s.finiteCheckStep,
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
+            amplitude_check_steps=s.amplitudeCheckSteps,
             hybrid_block=s.hybridBlock, hybrid_shell=s.hybridShell,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
@@ -344,6 +346,8 @@ class YeeScheme(BlockedStepping):
             self.graph_mode = False
         self.hybrid = None
         self._init_hybrid()
+        if self.use_upml_chain and not (self.hybrid is not None and self.hybrid.get("v2")):
+            self._alloc_upml_levels()
         if (self.hybrid is None and cfg.scheme == "3d" and self.ops.name == "hip"
                 and getattr(self, "chain_regions", None) is not None and getattr(self, "_chain_prof", None) is not None):
             # stepped 3D runs: the z PML slabs' chain boxes widened to whole
@@ -451,10 +455,13 @@ class YeeScheme(BlockedStepping):
                           "cbEa": cbE_a.to(dtp).contiguous(), "ccEa": ccE_a.to(dtp).contiguous(),
                           "s": float(inv_mod_s), "cell": None if inv_mod is None else inv_mod.to(dtp).contiguous(),
                           "axes": (aD, aCa, aCb)}
-            nlev = 3 if drude else 2
-            st["D"] = [[self._zeros() for _ in range(nlev)] for _ in range(self.planes)]
+            # D (3 levels with Drude) and D1 levels: allocated once the time
+            # stepping is known (init_grids): full-grid arrays for the chain
+            # kernels, region-local boxes for the single-pass shell
+            st["nlev"] = 3 if drude else 2
+            st["D"] = None
             if drude:
-                st["D1"] = [[self._zeros() for _ in range(3)] for _ in range(self.planes)]
+                st["D1"] = None
                 eps_c = self.sampler.averaged(c, "eps" if c[0] == "E" else "mu")
                 w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
                 e0 = base
@@ -500,6 +507,16 @@ class YeeScheme(BlockedStepping):
             for c in self.comps:
                 st = self.upml[c]
                 self.ops._drude_lut(st, [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")], self.domain.shape)
+
+    def _alloc_upml_levels(self) -> None:
+        """Full-grid D / D1 levels of the chain kernels (the stepped shell and
+        stepped runs read them by global cell index)."""
+        for c in self.comps:
+            st = self.upml[c]
+            if st["D"] is None:
+                st["D"] = [[self._zeros() for _ in range(st["nlev"])] for _ in range(self.planes)]
+            if "D1" in st and st["D1"] is None:
+                st["D1"] = [[self._zeros() for _ in range(3)] for _ in range(self.planes)]
 
     def _bbox_global(self, mask: torch.Tensor) -> Box:
         """Global bounding box of the True cells of a local mask (empty box
@@ -935,7 +952,12 @@ class YeeScheme(BlockedStepping):
             sfx = "" if p == 0 else "-im"
             for c in self.comps:
                 out[c + sfx] = self.F[p][c]
-            if self.use_upml_chain:
+            if self.use_upml_chain and self.hybrid is not None and self.hybrid.get("v2"):
+                if getattr(self, "upml_regions", None) is not None:
+                    out.update(self.upml_regions.named(p, sfx))
+                if getattr(self, "drude_box", None) is not None:
+                    out.update(self.drude_box.named(p, sfx))
+            elif self.use_upml_chain:
                 for c in self.comps:
                     for lv, t in enumerate(self.upml[c]["D"][p]):
                         out["%s%s-aux%d%s" % ("D" if c[0] == "E" else "B", c[1], lv, sfx)] = t
@@ -960,7 +982,12 @@ class YeeScheme(BlockedStepping):
         out = []
         for p in range(self.planes):
             out += [self.F[p][c] for c in self.comps]
-            if self.use_upml_chain:
+            if self.use_upml_chain and self.hybrid is not None and self.hybrid.get("v2"):
+                if getattr(self, "upml_regions", None) is not None:
+                    out += list(self.upml_regions.named(p, "").values())
+                if getattr(self, "drude_box", None) is not None:
+                    out += list(self.drude_box.named(p, "").values())
+            elif self.use_upml_chain:
                 for c in self.comps:
                     out += list(self.upml[c]["D"][p])
                     if self.cfg.use_metamaterials:
@@ -977,7 +1004,15 @@ class YeeScheme(BlockedStepping):
         out = []
         for p in range(self.planes):
             out += [None] * len(self.comps)
-            if self.use_upml_chain:
+            if self.use_upml_chain and self.hybrid is not None and self.hybrid.get("v2"):
+                ur = getattr(self, "upml_regions", None)
+                if ur is not None:
+                    for c in self.comps:
+                        out += [(self.domain.to_global(b), b[0]) for b in ur.boxes if not box_empty(b)]
+                dbx = getattr(self, "drude_box", None)
+                if dbx is not None:
+                    out += [(self.domain.to_global(dbx.box), dbx.box[0])] * len(dbx.named(p, ""))
+            elif self.use_upml_chain:
                 for c in self.comps:
                     out += [None] * len(self.upml[c]["D"][p])
                     if self.cfg.use_metamaterials:
@@ -1291,20 +1326,32 @@ class YeeScheme(BlockedStepping):
         documented intent.  Returns the number of steps taken."""
         fdtd_assert(self.planes == 1, "amplitude mode needs real field values (reference asserts the same)")
         self.in_amplitude = True
+        K = max(1, int(getattr(self.cfg, "amplitude_check_steps", 8)))
+        boxes = [self.amplitude_box(c) for c in self.comps]
+        counts = torch.zeros(K, dtype=torch.int32, device=self.device)
         taken = 0
         try:
-            for _ in range(self.cfg.amplitude_steps):
-                self.step()
-                taken += 1
-                changed = 0
-                for c in self.comps:
-                    changed += self.ops.amplitude_update(self.F[0][c], self.amp[0][c], self.amplitude_box(c),
-                                                         ACCURACY)
+            # the changed-cell counts of K steps accumulate on the device (one
+            # fused launch per step, no host sync) and are read back once per
+            # period; the run stops at the end of the period in which a step
+            # changed no amplitude (K = 1: the check after every step)
+            while taken < self.cfg.amplitude_steps:
+                n = min(K, self.cfg.amplitude_steps - taken)
+                counts.zero_()
+                for s_ in range(n):
+                    self.step()
+                    self.ops.amplitude_update_many([self.F[0][c] for c in self.comps],
+                                                   [self.amp[0][c] for c in self.comps], boxes, ACCURACY,
+                                                   counts[s_:s_ + 1])
+                got = [int(v) for v in counts[:n].cpu()]
                 if self.halo is not None:
-                    changed = self.halo.allreduce_sum(changed)
-                if changed == 0 and taken > 1:
-                    self.amplitude_converged = True
-                    return taken
+                    got = [self.halo.allreduce_sum(v) for v in got]
+                for s_ in range(n):
+                    if got[s_] == 0 and taken + s_ + 1 > 1:
+                        self.amplitude_converged = True
+                        self.amplitude_stable_step = taken + s_ + 1
+                        return taken + n
+                taken += n
             self.amplitude_converged = False
             log.log(0, "amplitude mode: stable state not reached after %d steps" % taken)
             return taken

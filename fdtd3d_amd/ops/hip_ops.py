@@ -557,6 +557,29 @@ class HipOps:
         _check(rc, "amplitude_update")
         return int(s.item())
 
+    def amplitude_update_many(self, fields: Sequence[torch.Tensor], amps: Sequence[torch.Tensor],
+                              boxes: Sequence[Box], accuracy: float, counter: torch.Tensor) -> None:
+        """Amplitude update of several components in one launch; the number
+        of changed cells is ADDED to the device int32 ``counter`` (one
+        element) -- no host synchronisation."""
+        shape = tuple(fields[0].shape)
+        for f, a in zip(fields, amps):
+            self._check_tensor(f, shape)
+            self._check_tensor(a, shape)
+        for b in boxes:
+            for d in range(3):
+                if not _empty(b) and (b[0][d] < 0 or b[1][d] > shape[d]):
+                    raise HipError("amplitude box %s outside array %s" % (b, shape))
+        if counter.device.type != "cuda" or counter.dtype != torch.int32 or counter.numel() < 1:
+            raise HipError("amplitude counter: one int32 on the device")
+        n = len(fields)
+        rc = self.fn("amplitude_many")((c_vp * n)(*[f.data_ptr() for f in fields]),
+                                       (c_vp * n)(*[a.data_ptr() for a in amps]), c_int(n), c_int(shape[1]),
+                                       c_int(shape[2]), _box_arr(boxes), c_double(accuracy),
+                                       c_vp(counter.data_ptr()), _stream())
+        _check(rc, "amplitude_many")
+        self.launches += 1
+
     # ----------------------------------------------------------------- TF/SF
     def inc_step_e(self, einc: torch.Tensor, hinc: torch.Tensor, coef: float, source: float) -> None:
         _check(self.fn("inc_e")(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(coef), c_double(source),
@@ -792,7 +815,7 @@ class HipOps:
 
     def shell_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
                    windows: Sequence[Box], ax: Sequence[int], cb: Dict[str, Coef], source=None, cpml=None,
-                   kappa: bool = False) -> None:
+                   kappa: bool = False, upml=None, drude=None) -> None:
         """One fused E+H leapfrog step (yee3d_shell.hip) of the shell boxes
         ``windows`` (local, disjoint): reads ``fin``, writes ``fout`` there.
         ``ax[w]`` = the CPML axes of box ``w`` (bit 0 x, 1 y, 2 z), ``cpml`` =
@@ -821,10 +844,20 @@ class HipOps:
             for d in range(3):
                 if not _empty(w) and (w[0][d] < 0 or w[1][d] > shape[d]):
                     raise HipError("shell window %s outside array %s" % (w, shape))
-        if any(ax) and cpml is None:
-            raise HipError("shell_step: CPML windows without a CPML table")
+        if any(a & 8 for a in ax) and drude is None:
+            raise HipError("shell_step: dispersive-box windows without a dispersive table")
+        if drude is not None and int(self.lib.fdtd_shell_drude_size()) != drude.numel():
+            raise HipError("shell dispersive block layout mismatch (%d vs %d bytes)"
+                           % (self.lib.fdtd_shell_drude_size(), drude.numel()))
+        if any(a & 7 for a in ax) and cpml is None and upml is None:
+            raise HipError("shell_step: absorbing-layer windows without a CPML / UPML table")
+        if cpml is not None and upml is not None:
+            raise HipError("shell_step: CPML or UPML, not both")
         if cpml is not None and int(self.lib.fdtd_shell_cpml_size()) != cpml.numel():
             raise HipError("shell CPML block layout mismatch")
+        if upml is not None and int(self.lib.fdtd_shell_upml_size()) != upml.numel():
+            raise HipError("shell UPML block layout mismatch (%d vs %d bytes)"
+                           % (self.lib.fdtd_shell_upml_size(), upml.numel()))
         src = [-1, -1, -1, -1]
         val = 0.0
         if source is not None:
@@ -838,7 +871,7 @@ class HipOps:
                                       c_int(shape[2]), _box_arr([boxes[c] for c in E + H]), c_int(len(wins)),
                                       _box_arr(wins) if wins else (c_int * 1)(0), (c_int * max(1, len(ax)))(*ax),
                                       (c_int * 4)(*src), c_double(val), _ptr(cpml), c_int(1 if kappa else 0),
-                                      _stream())
+                                      _ptr(upml), _ptr(drude), _stream())
         _check(rc, "shell1")
         self.launches += 1
 

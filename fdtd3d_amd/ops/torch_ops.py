@@ -22,7 +22,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from ..layout.yee import YeeLayout
+from ..layout.yee import UPML_AXES, YeeLayout
 from .coef import Coef
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
@@ -148,13 +148,45 @@ class TorchOps:
                 fout[c][sl] = cur[c][sp]
 
     def shell_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                   windows, ax, cb: Dict[str, Coef], source=None, cpml=None, kappa: bool = False) -> None:
+                   windows, ax, cb: Dict[str, Coef], source=None, cpml=None, kappa: bool = False,
+                   upml=None, drude=None) -> None:
         """Reference semantics of the fused single-step shell kernel
         (yee3d_shell.hip): one leapfrog step of every update box from ``fin``
         (CPML psi read from ``psi[p]``, written to ``psi_alt[p]``; ``cpml`` =
-        (CPML, p)), of which only the ``windows`` are stored to ``fout``.
-        ``ax`` (the kernel's per-box CPML class) does not change the result."""
+        (CPML, p); UPML D read from / written to the two copies of ``upml`` =
+        (UPMLRegions, p) inside its D boxes), of which only the ``windows``
+        are stored to ``fout``.  ``ax`` (the kernel's per-box class) does not
+        change the result."""
         tmp = {c: fin[c].clone() for c in fin}
+        ureg, up = upml if upml is not None else (None, 0)
+
+        def upml_kind(kind, src):
+            if ureg is None:
+                return
+            rd, wr = ureg.cur[up], 1 - ureg.cur[up]
+            for c, box in (e if kind == "E" else h).items():
+                aD, aA, aB = UPML_AXES[c]
+                for q, qb in enumerate(ureg.boxes):
+                    sub = box_intersect_(box, qb)
+                    if _empty(sub):
+                        continue
+                    sl = box_slices(sub)
+                    curl = self.curl(kind, c, sl, src)
+                    dsl = tuple(slice(sub[0][d] - qb[0][d], sub[1][d] - qb[0][d]) for d in range(3))
+
+                    def pair(a):
+                        v = ureg.pairs[c][a][sl[a]]
+                        shape = [1, 1, 1]
+                        shape[a] = -1
+                        return v[:, 0].view(shape), v[:, 1].view(shape)
+
+                    caD, cbD = pair(aD)
+                    caE, ica = pair(aA)
+                    cbEa, ccEa = pair(aB)
+                    D = ureg.D[up][c][rd][q][dsl]
+                    Dn = caD * D + cbD * curl
+                    tmp[c][sl] = caE * fin[c][sl] + ureg.scal[c] * ica * (cbEa * Dn + ccEa * D)
+                    ureg.D[up][c][wr][q][dsl] = Dn
         e = {c: b for c, b in boxes.items() if c[0] == "E"}
         h = {c: b for c, b in boxes.items() if c[0] == "H"}
         cp, p = cpml if cpml is not None else (None, 0)
@@ -171,13 +203,48 @@ class TorchOps:
                     self.cpml_apply(kind, tmp[c], src[sl.src], sl.axis, sl.sign, sl.psi_alt[p], sl.lbox, b, sl.b,
                                     sl.c, sl.kinv_m1, cb[c])
 
+        dbox, dp = drude if drude is not None else (None, 0)
+
+        def drude_kind(kind, src):
+            # dispersive box: the chain where the material index is set, the
+            # plain update (already in tmp) elsewhere
+            if dbox is None:
+                return
+            B = dbox.box
+            for c, box in (e if kind == "E" else h).items():
+                if c not in dbox.ids:
+                    continue
+                sub = box_intersect_(box, B)
+                if _empty(sub):
+                    continue
+                sl = box_slices(sub)
+                bsl = tuple(slice(sub[0][d] - B[0][d], sub[1][d] - B[0][d]) for d in range(3))
+                curl = self.curl(kind, c, sl, src)
+                ids = dbox.ids[c][bsl].long()
+                m = ids > 0
+                lut = dbox.lut[c].to(curl.dtype)
+                co = lut[(ids - 1).clamp(min=0)]  # (..., 5)
+                caD, cbD, caE, sica, cbEa, ccEa = dbox.scal[c]
+                Dl, D1l = dbox.D[dp][c], dbox.D1[dp][c]
+                D, Dp, D1, D1p = Dl[0][bsl], Dl[1][bsl], D1l[0][bsl], D1l[1][bsl]
+                Dn = caD * D + cbD * curl
+                D1n = co[..., 0] * Dn + co[..., 1] * D + co[..., 2] * Dp + co[..., 3] * D1 + co[..., 4] * D1p
+                En = caE * fin[c][sl] + sica * (cbEa * D1n + ccEa * D1)
+                tmp[c][sl] = torch.where(m, En, tmp[c][sl])
+                Dl[2][bsl] = torch.where(m, Dn, Dl[2][bsl])
+                D1l[2][bsl] = torch.where(m, D1n, D1l[2][bsl])
+
         self.curl_update("E", e, tmp, fin, cb)
         psi_terms("E", fin)
+        upml_kind("E", fin)
+        drude_kind("E", fin)
         if source is not None:
             comp, idx, val = source
             tmp[comp][tuple(idx)] = val
         self.curl_update("H", h, tmp, tmp, cb)
         psi_terms("H", tmp)
+        upml_kind("H", tmp)
+        drude_kind("H", tmp)
         for w in windows:
             if _empty(w):
                 continue
@@ -327,6 +394,12 @@ class TorchOps:
         if torch.isnan(v).any():
             return float("inf")
         return float(v.max())
+
+    def amplitude_update_many(self, fields, amps, boxes, accuracy: float, counter: torch.Tensor) -> None:
+        """Several components' amplitude updates; the changed count is added
+        to ``counter`` (semantics of the HIP kernel)."""
+        for f, a, b in zip(fields, amps, boxes):
+            counter += self.amplitude_update(f, a, b, accuracy)
 
     def amplitude_update(self, f: torch.Tensor, amp: torch.Tensor, box: Box, accuracy: float) -> int:
         """Running max-|f| with the reference's convergence test

@@ -159,7 +159,9 @@ def test_gpu_decomposed_equals_serial(gpu, name, cfg, world, axes, buf):
         b = s.F[0][c].double().cpu()
         scale = max(float(s.F[0][o].abs().max()) for o in s.comps if o[0] == c[0]) + 1e-30
         err = float((a - b).abs().max())
-        assert err <= 1e-6 * scale, (name, c, err, scale)
+        # the serial hybrid may run the single-pass shell kernel while the
+        # decomposed ranks run the stepped shell: fp32 rounding of two kernels
+        assert err <= (5e-6 if name.startswith("hybrid") else 1e-6) * scale, (name, c, err, scale)
 
 
 # the exchange overlapped with the interior / core pass on the side stream

@@ -142,3 +142,25 @@ def test_tfsf_leakage_3d():
     outside = max(float(ez[7:9, 7:33, 7:33].abs().max()), float(ez[31:33, 7:33, 7:33].abs().max()))
     assert inside > 0.3
     assert outside < 0.05 * inside, (outside, inside)
+
+
+def test_amplitude_check_period():
+    """Amplitude mode with the changed counts read back once per 8 steps
+    finds the same first stable step as a check after every step, and stops
+    at the end of that period (reference intent of Scheme3D.cpp:2945-3333)."""
+    import torch
+    from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+    from fdtd3d_amd.ops import make_ops
+    res = {}
+    for k in (1, 8):
+        cfg = SchemeConfig(scheme="3d", size=(16, 16, 16), time_steps=60, amplitude_steps=300, use_amp_mode=True,
+                           scene="vacuum", dtype="f64", use_pml=True, pml_size=(4, 4, 4), amplitude_check_steps=k)
+        s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+        s.init_scheme()
+        s.init_grids()
+        s.advance(cfg.time_steps)
+        taken = s.perform_amplitude_steps()
+        res[k] = (taken, getattr(s, "amplitude_stable_step", None), s.amplitude_converged)
+    assert res[1][2] and res[8][2], res
+    assert res[1][1] == res[8][1] == res[1][0], res
+    assert res[8][0] == -(-res[8][1] // 8) * 8, res

@@ -104,3 +104,34 @@ def test_shell_hybrid_selected_and_exact(gpu):
         scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])
         err = float((hy.F[0][c] - st.F[0][c]).abs().max())
         assert err <= 2e-5 * scale, (c, err, scale)
+
+
+@pytest.mark.parametrize("name,extra", [
+    ("tfsf-oblique-open", dict(theta=60, phi=20, psi=30)),
+    ("cpml-point-kappa", dict(use_pml=True, pml_type="cpml", pml_size=(5, 4, 6), use_tfsf=False,
+                              cpml_kappa_max=4.0)),
+    ("cpml-tfsf-x-T5", dict(use_pml=True, pml_type="cpml", pml_size=(6, 6, 6))),
+    ("upml-tfsf-oblique", dict(use_pml=True, pml_size=(4, 5, 6), tfsf_size=(9, 9, 9), theta=60, phi=20, psi=30)),
+    ("upml-point", dict(use_pml=True, pml_size=(6, 6, 6), use_tfsf=False)),
+])
+def test_single_pass_shell_gpu(gpu, name, extra):
+    """HIP single-pass hybrid (shell kernel + TF/SF tables + blocked core)
+    == HIP stepped run, from random fields."""
+    kw = dict(scheme="3d", size=(96, 88, 96), dtype="f32", tfsf_size=(8, 8, 8), scene="vacuum", use_tfsf=True,
+              time_steps=12)
+    kw.update(extra)
+    cfg = SchemeConfig(**kw)
+    runs = []
+    for hb in (0, 1):
+        s = _scheme(dataclasses.replace(cfg, hybrid_block=hb), "hip", gpu, torch.float32)
+        if hb == 0:
+            assert s.hybrid is not None and s.hybrid.get("v2"), "single-pass shell not selected"
+        s.randomize_fields(seed=9)
+        s.perform_steps()
+        torch.cuda.synchronize()
+        runs.append(s)
+    hy, st = runs
+    for c in hy.comps:
+        scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])
+        err = float((hy.F[0][c] - st.F[0][c]).abs().max())
+        assert err <= 2e-5 * scale, (name, c, err, scale)
