@@ -38,6 +38,8 @@
 // adds Cb g to the E targets of the input buffer before the pass and Db g to
 // the H targets of the output after it (models/blocking.py _hybrid2_step).
 
+#include <cstring>
+#include <cstdlib>
 #include "common.h"
 
 namespace {
@@ -128,7 +130,7 @@ __device__ constexpr int kUp[6][3] = {{1, 2, 0}, {2, 0, 1}, {0, 1, 2}, {1, 2, 0}
 // +d0 - d1 (Ex = dHz/dy - dHy/dz, ..., Hx = dEy/dz - dEz/dy, ...)
 __device__ constexpr int kAx[6][2] = {{1, 2}, {2, 0}, {0, 1}, {2, 1}, {0, 2}, {1, 0}};
 
-constexpr int SH_MAX = 64;  // boxes per launch
+constexpr int SH_MAX = 32;  // boxes per launch
 struct ShList {
   int n;
   int first[SH_MAX + 1];  // first workgroup of each box; first[n] = grid size
@@ -136,17 +138,26 @@ struct ShList {
   Box3 box[SH_MAX];
 };
 
-constexpr int SNW = 16;  // waves per workgroup
+// the CPML / UPML / dispersive block of a launch travels BY VALUE in the
+// kernel arguments: kernarg loads are invariant, so the compiler keeps the
+// psi / D descriptors in SGPRs (or re-reads them at will) instead of reloading
+// them from global memory after every buffer store that might alias them --
+// a dependent scalar-load chain per term and trip
+union ShAux {
+  ShCpml c;
+  ShUpml u;
+  ShDrude d;
+};
 constexpr int SR = 2;    // rows per lane group
 
-template <int AX, bool KAP, int LW>
+template <int AX, bool KAP, int LW, int SNW>
 __global__ __launch_bounds__(64 * SNW) void k_shell1(
     const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
     const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
     float* __restrict__ exo, float* __restrict__ eyo, float* __restrict__ ezo, float* __restrict__ hxo,
     float* __restrict__ hyo, float* __restrict__ hzo, float cb, float db, int nx, int ny, int nz, Box3 bex,
     Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, ShList L, int src_i, int src_j, int src_k, int src_comp,
-    float src_v, const ShCpml* __restrict__ cp, const ShUpml* __restrict__ up, const ShDrude* __restrict__ dr) {
+    float src_v, const ShAux A) {
   constexpr int G = 64 / LW;         // lane groups (grid rows) per wave
   constexpr int NS = SNW * G;        // lane groups per workgroup
   constexpr int ROWS = NS * SR;      // y rows per tile
@@ -155,40 +166,27 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
   constexpr bool CPX = AX < 8 && (AX & 1), CPY = AX < 8 && (AX & 2), CPZ = AX < 8 && (AX & 4);
   constexpr bool CPM = AX < 8 && AX != 0;
   __shared__ float sX[2][4][NS][LW];
-  __shared__ ShTerm sT[CPM ? 18 : 1];
-  __shared__ ShUpml sU[1];
+  // the CPML / UPML / dispersive blocks are read straight from (constant)
+  // global memory with wave-uniform addresses: scalar loads into SGPRs, so
+  // the psi / D descriptors built from them need no waterfall loop (an LDS
+  // copy would hand the pointers back in VGPRs)
+  const ShTerm* sT = &A.c.t[0][0];
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);
   const int g = LW == 64 ? 0 : lane / LW;
   const int li = LW == 64 ? lane : lane % LW;
   const int slot = w * G + g;
-  if constexpr (CPM) {
-    const unsigned* src = (const unsigned*)cp;
-    unsigned* dst = (unsigned*)sT;
-    for (int q = lane + 64 * w; q < (int)(sizeof(ShTerm) * 18 / 4); q += 64 * SNW) dst[q] = src[q];
-    __syncthreads();
-  }
-  if constexpr (UP) {
-    const unsigned* src = (const unsigned*)up;
-    unsigned* dst = (unsigned*)sU;
-    for (int q = lane + 64 * w; q < (int)(sizeof(ShUpml) / 4); q += 64 * SNW) dst[q] = src[q];
-    __syncthreads();
-  }
-  const ShUpml& U = sU[0];
-  __shared__ ShDrude sD[1];
+  const ShUpml& U = A.u;    // UPML launches only
+  const ShDrude& DB = A.d;  // dispersive launches only
   __shared__ float sL[DR ? 6 : 1][DR ? SH_LUT * 5 : 1];
   if constexpr (DR) {
-    const unsigned* src = (const unsigned*)dr;
-    unsigned* dst = (unsigned*)sD;
-    for (int q = lane + 64 * w; q < (int)(sizeof(ShDrude) / 4); q += 64 * SNW) dst[q] = src[q];
-    __syncthreads();
+    // the coefficient tuples ARE indexed per lane (by material id): LDS
     for (int q = lane + 64 * w; q < 6 * SH_LUT * 5; q += 64 * SNW) {
       const int n = q / (SH_LUT * 5), e = q % (SH_LUT * 5);
-      sL[n][e] = (sD[0].id[n] && e < 5 * sD[0].nlut[n]) ? sD[0].lut[n][e] : 0.f;
+      sL[n][e] = (DB.id[n] && e < 5 * DB.nlut[n]) ? DB.lut[n][e] : 0.f;
     }
     __syncthreads();
   }
-  const ShDrude& DB = sD[0];
   // ---- box and tile of this workgroup (wave-uniform)
   // (static indices only: a dynamic index into the by-value list would copy
   // it to scratch)
@@ -661,29 +659,45 @@ __global__ __launch_bounds__(64 * SNW) void k_shell1(
   }
 }
 
-template <int AX, bool KAP, int LW>
+template <int AX, bool KAP, int LW, int NW>
 int launch_shell(const float* const* fi, float* const* fo, float cb, float db, int nx, int ny, int nz,
-                 const Box3* b, const ShList& L, const int* src, float sv, const ShCpml* cp, const ShUpml* up,
-                 const ShDrude* dr, hipStream_t s) {
-  k_shell1<AX, KAP, LW><<<L.first[L.n], dim3(64, SNW), 0, s>>>(
+                 const Box3* b, const ShList& L, const int* src, float sv, const ShAux& A, hipStream_t s) {
+  k_shell1<AX, KAP, LW, NW><<<L.first[L.n], dim3(64, NW), 0, s>>>(
       fi[0], fi[1], fi[2], fi[3], fi[4], fi[5], fo[0], fo[1], fo[2], fo[3], fo[4], fo[5], cb, db, nx, ny, nz, b[0],
-      b[1], b[2], b[3], b[4], b[5], L, src[0], src[1], src[2], src[3], sv, cp, up, dr);
+      b[1], b[2], b[3], b[4], b[5], L, src[0], src[1], src[2], src[3], sv, A);
   FDTD_RETURN_LAUNCH_STATUS();
+}
+
+template <int AX, int NW>
+int launch_shell_nw(bool kap, int lw, const float* const* fi, float* const* fo, float cb, float db, int nx, int ny,
+                    int nz, const Box3* b, const ShList& L, const int* src, float sv, const ShAux& A, hipStream_t s) {
+  if constexpr (AX == 8 || AX == 9 || AX == 0) {  // no kappa term: one variant
+    if (lw == 32) return launch_shell<AX, false, 32, NW>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, A, s);
+    return launch_shell<AX, false, 64, NW>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, A, s);
+  } else {
+    if (lw == 32)
+      return kap ? launch_shell<AX, true, 32, NW>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, A, s)
+                 : launch_shell<AX, false, 32, NW>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, A, s);
+    return kap ? launch_shell<AX, true, 64, NW>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, A, s)
+               : launch_shell<AX, false, 64, NW>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, A, s);
+  }
+}
+
+// waves per workgroup (tuning): FDTD3D_SHELL_WAVES = 8 or 16 (default)
+int shell_waves() {
+  static int w = -1;
+  if (w < 0) {
+    const char* e = getenv("FDTD3D_SHELL_WAVES");
+    w = (e && atoi(e) == 8) ? 8 : 16;
+  }
+  return w;
 }
 
 template <int AX>
 int launch_shell_ax(bool kap, int lw, const float* const* fi, float* const* fo, float cb, float db, int nx, int ny,
-                    int nz, const Box3* b, const ShList& L, const int* src, float sv, const ShCpml* cp,
-                    const ShUpml* up, const ShDrude* dr, hipStream_t s) {
-  if constexpr (AX == 8 || AX == 9 || AX == 0) {  // no kappa term: one variant
-    if (lw == 32) return launch_shell<AX, false, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s);
-    return launch_shell<AX, false, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s);
-  }
-  if (lw == 32)
-    return kap ? launch_shell<AX, true, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s)
-               : launch_shell<AX, false, 32>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s);
-  return kap ? launch_shell<AX, true, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s)
-             : launch_shell<AX, false, 64>(fi, fo, cb, db, nx, ny, nz, b, L, src, sv, cp, up, dr, s);
+                    int nz, const Box3* b, const ShList& L, const int* src, float sv, const ShAux& A, hipStream_t s) {
+  if (shell_waves() == 8) return launch_shell_nw<AX, 8>(kap, lw, fi, fo, cb, db, nx, ny, nz, b, L, src, sv, A, s);
+  return launch_shell_nw<AX, 16>(kap, lw, fi, fo, cb, db, nx, ny, nz, b, L, src, sv, A, s);
 }
 
 }  // namespace
@@ -693,10 +707,11 @@ int launch_shell_ax(bool kap, int lw, const float* const* fi, float* const* fo, 
 // outside a component's update box (`boxes`, 6 x 6 ints) are stored
 // unchanged.  `ax[w]` = absorbing-layer axes of box w (bit 0 x, 1 y, 2 z: the
 // slabs it may touch; 0 = none; any superset is correct).  CPML runs pass
-// `cpml` = device CpmlDev block of models/cpml.py (psi read from psi[p],
-// written to the alt copy) and `kap` = some 1/kappa - 1 is non-zero; UPML
-// runs pass `upml` = device ShUpml block of models/upml.py (every box with
-// ax != 0 runs the D/B chain).  `src` = {i, j, k, comp} of a hard E point
+// `cpml` = the CpmlDev block of models/cpml.py host_table, in HOST memory
+// (psi read from psi[p], written to the alt copy) and `kap` = some
+// 1/kappa - 1 is non-zero; UPML runs pass `upml` = the host ShUpml block of
+// models/upml.py (every box with ax != 0 runs the D/B chain), dispersive
+// boxes `drude` = the host ShDrude block.  `src` = {i, j, k, comp} of a hard E point
 // source (comp -1: none), value `src_val`.  Boxes at most 30 cells deep in z
 // run 32-lane rows.
 FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double cb, double db, int nx, int ny,
@@ -711,10 +726,16 @@ FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const hipStream_t s = (hipStream_t)stream;
+  // the tables arrive as HOST bytes (models/cpml.py host_table, models/upml.py)
+  ShAux aux;
+  memset(&aux, 0, sizeof(aux));
+  if (cpml) memcpy(&aux.c, cpml, sizeof(ShCpml));
+  if (upml) memcpy(&aux.u, upml, sizeof(ShUpml));
+  if (drude) memcpy(&aux.d, drude, sizeof(ShDrude));
   // group the boxes by (class, lane width); classes: none, CPML x, y, z,
-  // CPML all axes (edges, corners), UPML
-  const int classes[7] = {0, 1, 2, 4, 7, 8, 9};
-  for (int ci = 0; ci < 7; ++ci) {
+  // the two-axis edges (xy, xz, yz), the corners (xyz), UPML, dispersive
+  const int classes[10] = {0, 1, 2, 4, 3, 5, 6, 7, 8, 9};
+  for (int ci = 0; ci < 10; ++ci) {
     for (int lw : {64, 32}) {
       ShList L;
       L.n = 0;
@@ -725,7 +746,7 @@ FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double
         const Box3 o = make_box(wins + 6 * wi);
         if (box_empty(o)) continue;
         const int a = ax[wi];
-        const int cls = a == 0 ? 0 : ((a & 8) ? 9 : (upml ? 8 : ((a == 1 || a == 2 || a == 4) ? a : 7)));
+        const int cls = a == 0 ? 0 : ((a & 8) ? 9 : (upml ? 8 : (a & 7)));
         if (cls != classes[ci]) continue;
         const int zl = o.hi[2] - o.lo[2];
         if ((zl <= 30) != (lw == 32)) continue;
@@ -733,7 +754,7 @@ FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double
         pend[np++] = o;
       }
       if (np == 0) continue;
-      const int ROWS = SNW * (64 / lw) * SR;
+      const int ROWS = shell_waves() * (64 / lw) * SR;
       for (int q = 0; q < np; ++q) {
         const Box3& o = pend[q];
         work += (long long)cdiv(o.hi[2] - o.lo[2], lw - 2) * cdiv(o.hi[1] - o.lo[1], ROWS - 2) * (o.hi[0] - o.lo[0]);
@@ -757,17 +778,17 @@ FDTD_API int fdtd_shell1_f32(const float* const* fin, float* const* fout, double
           first += L.tz[k] * L.ty[k] * (int)cdiv(o.hi[0] - o.lo[0], xc);
         }
         L.first[L.n] = first;
-        const ShCpml* cp = (const ShCpml*)cpml;
-        const ShUpml* up = (const ShUpml*)upml;
-        const ShDrude* dr = (const ShDrude*)drude;
         const float fc = (float)cb, fd = (float)db, sv = (float)src_val;
         int rc = 0;
-#define SH_CASE(A) rc = launch_shell_ax<A>(kap != 0, lw, fin, fout, fc, fd, nx, ny, nz, b, L, src, sv, cp, up, dr, s)
+#define SH_CASE(C) rc = launch_shell_ax<C>(kap != 0, lw, fin, fout, fc, fd, nx, ny, nz, b, L, src, sv, aux, s)
         switch (classes[ci]) {
           case 0: SH_CASE(0); break;
           case 1: SH_CASE(1); break;
           case 2: SH_CASE(2); break;
           case 4: SH_CASE(4); break;
+          case 3: SH_CASE(3); break;
+          case 5: SH_CASE(5); break;
+          case 6: SH_CASE(6); break;
           case 7: SH_CASE(7); break;
           case 8: SH_CASE(8); break;
           default: SH_CASE(9); break;

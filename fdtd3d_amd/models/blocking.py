@@ -76,18 +76,26 @@ def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: 
     return F32_AUTO_STEPS if world <= 2 else F32_AUTO_STEPS_MANY_RANKS
 
 
-def _cut_pieces(b: Box, cuts):
+def _cut_pieces(b: Box, cuts, keep=()):
     """``b`` split at the absorbing-slab cuts of every axis: [(box, axes
     bits)], bit a set when the piece may touch a slab along axis a.  The
     high-side cut moves one cell down: a tile recomputes its halo cells with
     its own specialisation, and the H update of the last cell below a high
     slab reads the new E of the first slab cell (H^{n+1} needs E^{n+1} at
-    +1 along every axis; E^{n+1} needs only H^n, so the low side is exact)."""
+    +1 along every axis; E^{n+1} needs only H^n, so the low side is exact).
+    Axes in ``keep`` are not cut (the piece keeps its slab cells and the band
+    beyond them in one box: a thin face of the shell stays one tile deep
+    instead of two part-filled ones); their bit is set when ``b`` reaches a
+    slab."""
     pieces = [(b, 0)]
     for a in range(3):
         if cuts[a] is None:
             continue
         lo_c, hi_c = cuts[a][0], cuts[a][1] - 1
+        if a in keep:
+            if b[0][a] < lo_c or b[1][a] > hi_c:
+                pieces = [(pb, ax | (1 << a)) for pb, ax in pieces]
+            continue
         nxt = []
         for pb, ax in pieces:
             for s_lo, s_hi, slab in ((None, lo_c, True), (lo_c, hi_c, False), (hi_c, None, True)):
@@ -298,11 +306,16 @@ class BlockedStepping:
         (csrc/yee3d_shell.hip): 3D serial runs with CPML, UPML (D/B form),
         dispersive (Drude / Lorentz) boxes inside the all-sigma-zero core, or
         plane waves in an open box; uniform background media (scalar
-        coefficients); plane waves through the TF/SF tables.  ``hybrid_shell``
-        = auto / single-pass selects it, stepped keeps the per-step kernels."""
+        coefficients); plane waves through the TF/SF tables.  Opt-in
+        (``hybrid_shell`` = single-pass): measured at 512^3 (round 3,
+        ``tools/shell_micro.py``, ``profiles/configs_r3.md``) the fused
+        single-step shell kernel is issue-bound on the thin shell faces
+        (20-54 Gcells/s, a 0.2 ms floor per two-axis edge launch) and the whole
+        runs are 1.7-1.9x slower than the stepped shell (CPML + TF/SF 48.5k
+        vs 84.7k Mcells/s), so ``auto`` keeps the stepped shell."""
         cfg = self.cfg
         mode = getattr(cfg, "hybrid_shell", "auto")
-        if mode not in ("auto", "single-pass") or not hasattr(self.ops, "shell_step"):
+        if mode != "single-pass" or not hasattr(self.ops, "shell_step"):
             return False
         if cfg.scheme != "3d" or self.halo is not None or cfg.use_amp_mode:
             return False
@@ -435,7 +448,10 @@ class BlockedStepping:
             pieces = []
             for b in box_subtract(alloc, Kd):
                 if not box_empty(b):
-                    pieces += _cut_pieces(dom.to_local(b), cuts)
+                    # the face normal of this part of the shell (the axes
+                    # along which it lies wholly outside the hole) is not cut
+                    normal = [a for a in range(3) if b[1][a] <= Kd[0][a] or b[0][a] >= Kd[1][a]]
+                    pieces += _cut_pieces(dom.to_local(b), cuts, keep=normal)
             if Dm is not None and not box_empty(Dm):
                 inner = box_intersect(grow(Dm, d), Kd)
                 if not box_empty(inner):

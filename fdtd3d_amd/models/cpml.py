@@ -141,6 +141,13 @@ class CPML:
         cache[key] = (ptrs, ints, keep)
         return cache[key]
 
+    def host_table(self, p: int) -> torch.Tensor:
+        """The :meth:`device_table` block as HOST bytes: the shell kernel
+        (yee3d_shell.hip) takes it by value in its kernel arguments."""
+        self.device_table(p)
+        key = (p,) + tuple(sl.psi[p].data_ptr() for c in self.s.comps for sl in self.slabs[c])
+        return self.__dict__["_dev"][key][2]
+
     def device_table(self, p: int) -> torch.Tensor:
         """CpmlDev block of plane ``p`` for the single-step blocked kernel
         (yee3d_tb.hip): per component (Ex..Hz) and term axis the psi slab
@@ -173,15 +180,16 @@ class CPML:
                 o1 = alt_of.get(pp[1], 0) if pp[1] else 0
                 raw += struct.pack("<QQQQiiiiQQQ", pp[0] or 0, pp[1] or 0, o0, o1, lo0, lo1, hi0, hi1, pp[2] or 0,
                                    pp[3] or 0, pp[4] or 0)
-        dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(s.device)
-        cache[key] = (dev, keep)
+        host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        dev = host.to(s.device)
+        cache[key] = (dev, keep, host)
         return dev
 
     def shell_arg(self, p: int, ops):
         """The ``cpml`` argument of ``ops.shell_step`` for plane ``p``: the
         device block on the HIP backend, (self, p) for the torch oracle."""
         if ops.name == "hip":
-            return self.device_table(p)
+            return self.host_table(p)
         return (self, p)
 
     def flip(self, p: int) -> None:

@@ -71,9 +71,10 @@ class UPMLRegions:
         return n
 
     # ------------------------------------------------------------- kernel
-    def device_table(self, p: int) -> torch.Tensor:
-        """ShUpml block (csrc/yee3d_shell.hip) of plane ``p``: boxes, D^n /
-        D^{n+1} pointers per (component, box), profile pairs, scalars."""
+    def host_table(self, p: int) -> torch.Tensor:
+        """ShUpml block (csrc/yee3d_shell.hip) of plane ``p`` as host bytes
+        (the kernel takes it by value): boxes, D^n / D^{n+1} pointers per
+        (component, box), profile pairs, scalars."""
         s = self.s
         rd, wr = self.cur[p], 1 - self.cur[p]
         key = (p, rd)
@@ -93,12 +94,12 @@ class UPMLRegions:
         raw = struct.pack("<36i", *ints) + struct.pack("<%dQ" % (36 + 36 + 18), *(d + dn + pr))
         raw += struct.pack("<6fi", *[self.scal[c] for c in comps], 0)
         raw += b"\0" * ((-len(raw)) % 8)
-        dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(s.device)
-        cache[key] = dev
-        return dev
+        host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        cache[key] = host
+        return host
 
     def shell_arg(self, p: int, ops):
-        return self.device_table(p) if ops.name == "hip" else (self, p)
+        return self.host_table(p) if ops.name == "hip" else (self, p)
 
     def flip(self, p: int) -> None:
         self.cur[p] = 1 - self.cur[p]
@@ -201,7 +202,8 @@ class DrudeBox:
         b = self.box
         return (b[1][0] - b[0][0]) * (b[1][1] - b[0][1]) * (b[1][2] - b[0][2])
 
-    def device_table(self, p: int) -> torch.Tensor:
+    def host_table(self, p: int) -> torch.Tensor:
+        """ShDrude block (csrc/yee3d_shell.hip) of plane ``p``, host bytes."""
         s = self.s
         comps = list(s.comps)
         key = (p,) + tuple(self.D[p][c][0].data_ptr() for c in comps if c in self.D[p])
@@ -222,12 +224,12 @@ class DrudeBox:
         nl = [int(self.lut[c].shape[0]) if c in self.lut else 0 for c in comps]
         raw = struct.pack("<6i", *ints) + struct.pack("<48Q", *ptr) + struct.pack("<36f", *fl)
         raw += struct.pack("<6i", *nl)
-        dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(s.device)
-        cache[key] = dev
-        return dev
+        host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        cache[key] = host
+        return host
 
     def shell_arg(self, p: int, ops):
-        return self.device_table(p) if ops.name == "hip" else (self, p)
+        return self.host_table(p) if ops.name == "hip" else (self, p)
 
     def rotate(self, p: int) -> None:
         """next -> cur -> prev (the stepped chain's level rotation)."""

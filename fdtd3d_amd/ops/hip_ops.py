@@ -819,8 +819,9 @@ class HipOps:
         """One fused E+H leapfrog step (yee3d_shell.hip) of the shell boxes
         ``windows`` (local, disjoint): reads ``fin``, writes ``fout`` there.
         ``ax[w]`` = the CPML axes of box ``w`` (bit 0 x, 1 y, 2 z), ``cpml`` =
-        ``CPML.device_table(p)`` (psi read from the current copy, written to the
-        other: call ``CPML.flip`` after), ``source`` = (E component, local
+        ``CPML.host_table(p)`` (host bytes, passed by value to the kernel; psi
+        read from the current copy, written to the other: call ``CPML.flip``
+        after), ``source`` = (E component, local
         index, value) of a hard point source or None.  fp32, scalar
         coefficients per kind."""
         E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
@@ -853,6 +854,9 @@ class HipOps:
             raise HipError("shell_step: absorbing-layer windows without a CPML / UPML table")
         if cpml is not None and upml is not None:
             raise HipError("shell_step: CPML or UPML, not both")
+        for name, t in (("CPML", cpml), ("UPML", upml), ("dispersive", drude)):
+            if t is not None and (t.is_cuda or t.dtype != torch.uint8 or not t.is_contiguous()):
+                raise HipError("shell_step: the %s block must be host bytes (host_table)" % name)
         if cpml is not None and int(self.lib.fdtd_shell_cpml_size()) != cpml.numel():
             raise HipError("shell CPML block layout mismatch")
         if upml is not None and int(self.lib.fdtd_shell_upml_size()) != upml.numel():

@@ -119,12 +119,12 @@ def test_hybrid_checkpoint_resume(tmp_path):
 ])
 def test_single_pass_shell_matches_stepped(name, extra):
     """The single-pass shell (fused step kernel semantics, TF/SF tables added
-    around it, shrinking windows cut at the CPML slabs) is selected
-    automatically and reproduces the stepped run from random fields, through
-    two full passes and a short tail (incidence at any angle: reference
+    around it, shrinking windows cut at the CPML slabs), when asked for,
+    reproduces the stepped run from random fields, through two full passes
+    and a short tail (incidence at any angle: reference
     YeeGridLayout.cpp:327-809)."""
     kw = dict(scheme="3d", size=(96, 88, 96), dtype="f64", tfsf_size=(8, 8, 8), scene="vacuum", use_tfsf=True,
-              time_steps=11)
+              time_steps=11, hybrid_shell="single-pass")
     kw.update(extra)
     cfg = SchemeConfig(hybrid_block=4, **kw)
     runs = []
@@ -146,3 +146,15 @@ def test_single_pass_shell_matches_stepped(name, extra):
         b = st.F[0][c]
         err = float((hy.F[0][c] - b).abs().max())
         assert err <= 1e-12 * float(b.abs().max()), (name, c, err)
+
+
+def test_auto_hybrid_keeps_stepped_shell():
+    """``hybrid_shell`` = auto takes the stepped shell (the faster one at
+    512^3, models/blocking.py _hybrid2_ok); single-pass must be asked for."""
+    kw = dict(scheme="3d", size=(96, 88, 96), dtype="f64", pml_size=(6, 6, 6), tfsf_size=(8, 8, 8), scene="vacuum",
+              use_pml=True, pml_type="cpml", use_tfsf=True, time_steps=4, hybrid_block=4)
+    for mode, v2 in (("auto", False), ("stepped", False), ("single-pass", True)):
+        s = YeeScheme(SchemeConfig(hybrid_shell=mode, **kw), make_ops("torch", None, "cpu", torch.float64))
+        s.init_scheme()
+        s.init_grids()
+        assert s.hybrid is not None and bool(s.hybrid.get("v2")) == v2, mode

@@ -68,7 +68,7 @@ def test_shell_step_vs_torch(gpu, name, size, pml, kappa, mode):
     # the kernel
     out = {c: torch.full_like(s.F[0][c], 7.0) for c in s.comps}
     s.ops.shell_step(s.F[0], out, upd, [b for b, _ in pieces], [a for _, a in pieces], s.cb, src,
-                     cpml=s.cpml.device_table(0), kappa=kappa != 1.0)
+                     cpml=s.cpml.host_table(0), kappa=kappa != 1.0)
     torch.cuda.synchronize()
     for c in s.comps:
         scale = max(float(fin_r[o].abs().max()) for o in s.comps if o[0] == c[0])
@@ -85,11 +85,11 @@ def test_shell_step_vs_torch(gpu, name, size, pml, kappa, mode):
 
 
 def test_shell_hybrid_selected_and_exact(gpu):
-    """The automatic hybrid plan of a CPML + TF/SF run takes the single-pass
-    shell, and two passes + a tail step equal the stepped run (random fields)."""
+    """A CPML + TF/SF run asking for the single-pass shell gets it, and two
+    passes + a tail step equal the stepped run (random fields)."""
     cfg = SchemeConfig(scheme="3d", size=(96, 88, 104), time_steps=11, dtype="f32", scene="vacuum", use_pml=True,
                        pml_type="cpml", use_tfsf=True, pml_size=(6, 6, 6), tfsf_size=(9, 9, 9), theta=70, phi=20,
-                       psi=40)
+                       psi=40, hybrid_shell="single-pass")
     runs = []
     for hb in (0, 1):
         s = _scheme(dataclasses.replace(cfg, hybrid_block=hb), "hip", gpu, torch.float32)
@@ -118,7 +118,7 @@ def test_single_pass_shell_gpu(gpu, name, extra):
     """HIP single-pass hybrid (shell kernel + TF/SF tables + blocked core)
     == HIP stepped run, from random fields."""
     kw = dict(scheme="3d", size=(96, 88, 96), dtype="f32", tfsf_size=(8, 8, 8), scene="vacuum", use_tfsf=True,
-              time_steps=12)
+              time_steps=12, hybrid_shell="single-pass")
     kw.update(extra)
     cfg = SchemeConfig(**kw)
     runs = []

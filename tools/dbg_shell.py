@@ -53,7 +53,7 @@ def case(name, size, pml_type, pml, mode, steps=3):
     cp_r = (ref.cpml, 0) if s.use_cpml else None
     ref.ops.shell_step(fin, out_r, upd, [b for b, _ in pieces], [a for _, a in pieces], ref.cb, None, cpml=cp_r)
     out = {c: torch.full_like(s.F[0][c], 7.0) for c in s.comps}
-    cp = s.cpml.device_table(0) if s.use_cpml else None
+    cp = s.cpml.host_table(0) if s.use_cpml else None
     ax = [a for _, a in pieces] if s.use_cpml else [0] * len(pieces)
     s.ops.shell_step(s.F[0], out, upd, [b for b, _ in pieces], ax, s.cb, None, cpml=cp)
     torch.cuda.synchronize()
@@ -129,7 +129,7 @@ def pass_case(T=3, size=(80, 72, 96)):
         ref.ops.shell_step(fin, out_r, hp["upd"], [b for b, _ in pieces], [a for _, a in pieces], ref.cb, None,
                            cpml=(ref.cpml, 0))
         s.ops.shell_step(cur, out, hp["upd"], [b for b, _ in pieces], [a for _, a in pieces], s.cb, None,
-                         cpml=s.cpml.device_table(0))
+                         cpml=s.cpml.host_table(0))
         s.cpml.flip(0)
         torch.cuda.synchronize()
         msg = []
