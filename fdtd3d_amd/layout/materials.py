@@ -83,6 +83,24 @@ class Scene:
     def mu(self, x, y, z, mod: float) -> torch.Tensor:
         return torch.ones_like(x)
 
+    def uniform(self, name: str) -> Optional[float]:
+        """The value of material ``name`` when it is the same everywhere in
+        this scene (None: it varies) -- lets the scheme keep a scalar instead
+        of evaluating and averaging a full fp64 grid (8 GB per array at
+        1024^3)."""
+        two_d_ref = self.kind == "reference" and self.scheme != "3d"
+        if name == "eps":
+            return 1.0 if self.kind in ("vacuum", "drude-sphere") or two_d_ref else None
+        if name == "mu":
+            return 1.0
+        if name in ("gamma_e", "gamma_m"):
+            return 0.0
+        if name == "omega_pe":
+            return None if self.kind in ("drude-sphere", "reference") else 0.0
+        if name == "omega_pm":
+            return None if self.kind == "reference" else 0.0
+        raise ValueError("unknown material %r" % name)
+
     def omega_pe(self, x, y, z, mod: float) -> torch.Tensor:
         w = SQRT2_F32 * 2 * math.pi * self.source_frequency
         if self.kind == "drude-sphere":
@@ -180,6 +198,15 @@ class MaterialSampler:
         w = self._points(comp, self.grid("omega_pe" if electric else "omega_pm"))
         g = self._points(comp, self.grid("gamma_e" if electric else "gamma_m"))
         return approximate_drude(w, g)
+
+    def uniform(self, name: str) -> Optional[float]:
+        return self.scene.uniform(name)
+
+    def free(self) -> None:
+        """Drop the cached eps-layout grids (recomputed on demand, e.g. by a
+        material dump): they are only needed while the coefficients are
+        built."""
+        self._cache.clear()
 
 
 def _dedupe_points(comp, pts, act, double):

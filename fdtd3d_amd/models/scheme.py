@@ -138,6 +138,21 @@ class SchemeConfig:
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
+def _drude_coefs(dt: float, e0: float, eps, w, g, q: float):
+    """(b0, b1, b2, ma1, ma2) of the second-order dispersive ADE D -> D1
+    (reference Drude form, Kernels.h:103-107; Lorentz with w0 > 0 via ``q`` =
+    dt^2 w0^2) -- elementwise over tensors / floats of eps, omega_p, gamma."""
+    A = 4 * e0 * eps + 2 * dt * e0 * eps * g + e0 * (dt * dt * w * w + q * eps)
+    b0 = (4 + 2 * dt * g + q) / A
+    b1 = (-8.0 + 2 * q) / A
+    b2 = (4 - 2 * dt * g + q) / A
+    ma1 = -(2 * e0 * (dt * dt * w * w + q * eps) - 8 * e0 * eps) / A
+    ma2 = -(4 * e0 * eps - 2 * dt * e0 * eps * g + e0 * (dt * dt * w * w + q * eps)) / A
+    if not isinstance(b1, torch.Tensor):
+        b1 = torch.full_like(A, b1)
+    return b0, b1, b2, ma1, ma2
+
+
 def _torch_dtype(name: str):
     return {"f32": torch.float32, "f64": torch.float64}[name]
 
@@ -232,6 +247,8 @@ class YeeScheme(BlockedStepping):
         t0 = time.perf_counter()
         dom = self.domain
         shape = dom.shape
+        self.mem_plan = self.capacity_plan()
+        self._check_capacity(self.mem_plan)
         self.F: List[Dict[str, torch.Tensor]] = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
 
         self.scene = Scene(cfg.scene, cfg.scheme, self.source_frequency, cfg.sphere_eps, cfg.sphere_radius,
@@ -243,12 +260,15 @@ class YeeScheme(BlockedStepping):
         dt, dx = self.dt, self.dx
 
         # ---- per-component material (relative eps / mu at the component)
+        # (None = vacuum; a material the scene holds uniformly at 1 -- mu
+        # everywhere, eps of a Drude sphere -- is never evaluated on the grid)
         self.mat: Dict[str, Optional[torch.Tensor]] = {}
         for c in self.comps:
-            if vacuum:
+            name = "eps" if c[0] == "E" else "mu"
+            if vacuum or sampler.uniform(name) == 1.0:
                 self.mat[c] = None
             else:
-                self.mat[c] = sampler.averaged(c, "eps" if c[0] == "E" else "mu")
+                self.mat[c] = sampler.averaged(c, name)
 
         # ---- plain-update coefficients Cb = dt / (eps eps0 dx), Db = dt / (mu mu0 dx)
         self.cb: Dict[str, Coef] = {}
@@ -356,8 +376,64 @@ class YeeScheme(BlockedStepping):
             # plain update algebraically).  Hybrid runs keep the exact slabs:
             # their core must stay clear of every chain box.
             self._init_chain_regions(self._chain_prof, z_align=128 // self.dtype.itemsize)
+        # the eps-layout material grids (fp64, 8 B per cell and material) and
+        # the averaged materials only feed the coefficients built above
+        self.sampler.free()
+        self.mat = {c: None for c in self.comps}
         self.initialized = True
         self.timers["init"] = time.perf_counter() - t0
+
+    # -------------------------------------------------------------- capacity
+    def capacity_plan(self) -> Dict[str, int]:
+        """Bytes this rank's scheme will hold resident, by array family,
+        estimated before anything is allocated (the layout rules of
+        init_grids): field sets, UPML D levels (two; three for dispersive
+        components), Drude D1 levels + uint8 index, CPML psi slabs, amplitude
+        maxima -- and the transient peak of the material setup (a few fp64
+        grids).  Per-cell figures at 1024^3 fp32: fields 24 B per set, a
+        Drude + UPML run 150 B in all."""
+        cfg = self.cfg
+        n = self.domain.shape
+        cells = n[0] * n[1] * n[2]  # this rank's allocated region (ghosts included)
+        isz = 4 if cfg.dtype == "f32" else 8
+        planes = self.planes
+        plan = {"fields": 6 * isz * cells * planes}
+        scene = Scene(cfg.scene, cfg.scheme)
+        blocked = cfg.use_fused and cfg.scheme in ("3d", "tmz", "tez") and self.ops.name == "hip"
+        if blocked or cfg.use_tfsf:
+            plan["fields_pingpong"] = plan["fields"]
+        if cfg.use_amp_mode:
+            plan["amplitude"] = plan["fields"]
+        if self.use_upml_chain:
+            disp_e = cfg.use_metamaterials and scene.uniform("omega_pe") != 0.0
+            disp_h = cfg.use_metamaterials and scene.uniform("omega_pm") != 0.0
+            nd = 3 * (disp_e + disp_h)  # dispersive components
+            plan["upml_D"] = isz * cells * planes * (3 * nd + 2 * (6 - nd))
+            if nd:
+                plan["drude_D1"] = 3 * isz * cells * planes * nd
+                lean = self.ops.name == "hip" and cfg.scheme == "3d"
+                plan["drude_coef"] = cells * nd * (2 if lean else 1 + 5 * isz)
+        if self.use_cpml:
+            pml = self.layout.pml_size
+            slab = sum(2 * pml[a] * (cells // max(1, n[a])) for a in range(3) if self.layout.active(a))
+            plan["cpml_psi"] = 2 * 4 * isz * slab * planes  # ~4 terms per slab cell, two copies
+        plan["init_transient"] = 4 * 8 * cells if not scene.is_vacuum(cfg.use_metamaterials) else 0
+        return plan
+
+    def _check_capacity(self, plan: Dict[str, int]) -> None:
+        """Fail before allocating when the plan cannot fit the device (a
+        1024^3 run that would die half-initialised after minutes of setup)."""
+        if self.device.type != "cuda":
+            return
+        free, total = torch.cuda.mem_get_info(self.device)
+        need = sum(plan.values())
+        log.info("capacity plan %.1f GB (%s) of %.1f GB free" % (
+            need / 1e9, ", ".join("%s %.1f" % (k, v / 1e9) for k, v in plan.items() if v), free / 1e9))
+        if need > 0.97 * free:
+            raise FdtdError("grid %s needs about %.1f GB on this device (%s) but %.1f GB are free: use more ranks "
+                            "(--manual-topology / torchrun) or a smaller grid"
+                            % (tuple(self.domain.shape), need / 1e9,
+                               ", ".join("%s %.1f GB" % (k, v / 1e9) for k, v in plan.items() if v), free / 1e9))
 
     # ------------------------------------------------------------------ UPML
     def _sigma_profiles(self) -> Dict[int, torch.Tensor]:
@@ -455,15 +531,20 @@ class YeeScheme(BlockedStepping):
                           "cbEa": cbE_a.to(dtp).contiguous(), "ccEa": ccE_a.to(dtp).contiguous(),
                           "s": float(inv_mod_s), "cell": None if inv_mod is None else inv_mod.to(dtp).contiguous(),
                           "axes": (aD, aCa, aCb)}
-            # D (3 levels with Drude) and D1 levels: allocated once the time
-            # stepping is known (init_grids): full-grid arrays for the chain
-            # kernels, region-local boxes for the single-pass shell
-            st["nlev"] = 3 if drude else 2
+            # D (3 levels for a dispersive component) and D1 levels: allocated
+            # once the time stepping is known (init_grids): full-grid arrays
+            # for the chain kernels, region-local boxes for the single-pass
+            # shell.  A component without any dispersive cell (H in an
+            # electric Drude scene) keeps two D levels and no D1 at all: its
+            # chain boxes all take the non-dispersive form.
+            st["nlev"] = 2
             st["D"] = None
             if drude:
-                st["D1"] = None
-                eps_c = self.sampler.averaged(c, "eps" if c[0] == "E" else "mu")
-                w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
+                name = "eps" if c[0] == "E" else "mu"
+                ue = self.sampler.uniform(name)
+                eps_c = ue if ue is not None else self.sampler.averaged(c, name)
+                wname, gname = ("omega_pe", "gamma_e") if c[0] == "E" else ("omega_pm", "gamma_m")
+                uw, ug = self.sampler.uniform(wname), self.sampler.uniform(gname)
                 e0 = base
                 # second-order ADE  D -> D1 (= E) of the dispersive permittivity,
                 # bilinear in the non-derivative terms (reference Drude form,
@@ -476,21 +557,49 @@ class YeeScheme(BlockedStepping):
                 if cfg.dispersion == "lorentz":
                     w0 = cfg.lorentz_omega0_ratio * 2 * PI * self.source_frequency
                 q = dt * dt * w0 * w0
-                A = 4 * e0 * eps_c + 2 * dt * e0 * eps_c * g + e0 * (dt * dt * w * w + q * eps_c)
-                st["b0"] = Coef(1.0, cell=((4 + 2 * dt * g + q) / A).to(dtp))
-                st["b1"] = Coef(1.0, cell=((-8.0 + 2 * q) / A).to(dtp))
-                st["b2"] = Coef(1.0, cell=((4 - 2 * dt * g + q) / A).to(dtp))
-                st["ma1"] = Coef(1.0, cell=(-(2 * e0 * (dt * dt * w * w + q * eps_c) - 8 * e0 * eps_c) / A).to(dtp))
-                st["ma2"] = Coef(1.0, cell=(-(4 * e0 * eps_c - 2 * dt * e0 * eps_c * g
-                                              + e0 * (dt * dt * w * w + q * eps_c)) / A).to(dtp))
-                st["drude_active"] = (w != 0) | (g != 0)
+                if uw == 0.0 and ug == 0.0:
+                    active = None
+                else:
+                    w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
+                    active = (w != 0) | (g != 0)
+                    if not bool(active.any()):
+                        active = None
+                if active is not None:
+                    st["nlev"] = 3
+                    st["D1"] = None
+                    st["drude_active"] = active
+                    lean = (ue is not None and ug is not None and cfg.scheme == "3d"
+                            and getattr(self.ops, "drude_lut", False) and hasattr(self.ops, "_drude_lut"))
+                    if lean:
+                        # coefficients are a function of omega_p alone here (eps
+                        # and gamma uniform): the uint8 index + table straight from
+                        # the distinct omega values, no per-cell coefficient arrays
+                        # (5 x 4 B per cell and component; torch.unique over those
+                        # would need ~10x that transiently at 1024^3)
+                        uniq, inv = torch.unique(w, return_inverse=True)
+                        lean = uniq.numel() <= 256
+                        if lean:
+                            tab = torch.stack(_drude_coefs(dt, e0, eps_c, uniq, ug, q), 1).to(dtp).contiguous()
+                            st["_drude_lut"] = (inv.to(torch.uint8).contiguous(), tab)
+                            for n in ("b0", "b1", "b2", "ma1", "ma2"):
+                                st[n] = Coef(1.0)  # cell: self._drude_cells(c) on demand
+                        del uniq, inv
+                    if not lean:
+                        for n, v in zip(("b0", "b1", "b2", "ma1", "ma2"), _drude_coefs(dt, e0, eps_c, w, g, q)):
+                            st[n] = Coef(1.0, cell=v.to(dtp))
+                    del w, g
                 # the non-dispersive chain (E from D through 1/(eps eps0)) for the
                 # chain boxes with no dispersive cell (PML slabs away from the
                 # metamaterial): with w = g = 0 the ADE gives D1 = D/(eps eps0)
                 # exactly, so D1 and its five coefficient arrays are not needed
-                inv_e = 1.0 / (eps_c * base)
-                uniform = bool((inv_e == inv_e.flatten()[0]).all())
-                s_pl, cell_pl = (float(inv_e.flatten()[0]), None) if uniform else (1.0, inv_e.to(dtp).contiguous())
+                if not isinstance(eps_c, torch.Tensor):
+                    s_pl, cell_pl = 1.0 / (eps_c * base), None
+                else:
+                    inv_e = 1.0 / (eps_c * base)
+                    uniform = bool((inv_e == inv_e.flatten()[0]).all())
+                    s_pl, cell_pl = ((float(inv_e.flatten()[0]), None) if uniform
+                                     else (1.0, inv_e.to(dtp).contiguous()))
+                    del inv_e
                 st["plain"] = {"cbE": prof_coef(s_pl, {aCb: cbE_a, aCa: inv_ca}, cell_pl),
                                "ccE": prof_coef(s_pl, {aCb: ccE_a, aCa: inv_ca}, cell_pl),
                                "prof": dict(st["prof"], s=s_pl, cell=cell_pl)}
@@ -506,7 +615,21 @@ class YeeScheme(BlockedStepping):
             # syncs the host): built here, not lazily inside a graph capture
             for c in self.comps:
                 st = self.upml[c]
-                self.ops._drude_lut(st, [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")], self.domain.shape)
+                if "D1" in st and "_drude_lut" not in st:
+                    self.ops._drude_lut(st, [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")],
+                                        self.domain.shape)
+
+    def _drude_cells(self, c: str) -> None:
+        """Per-cell Drude coefficient arrays of component ``c`` rebuilt from
+        its uint8 index + table (the lean initialisation keeps only those) for
+        the paths that take them per cell (generic D-form boxes, the
+        single-pass shell's dispersive box)."""
+        st = self.upml[c]
+        if st["b0"].cell is not None or st.get("_drude_lut") is None:
+            return
+        ids, tab = st["_drude_lut"]
+        for q, n in enumerate(("b0", "b1", "b2", "ma1", "ma2")):
+            st[n] = Coef(1.0, cell=tab[:, q][ids.long()].contiguous())
 
     def _alloc_upml_levels(self) -> None:
         """Full-grid D / D1 levels of the chain kernels (the stepped shell and
@@ -923,22 +1046,28 @@ class YeeScheme(BlockedStepping):
             inc = self.hinc[p] if kind == "E" else self.einc[p]
             for tab in self.tfsf_D[c]:
                 self.ops.tfsf_apply(Dn, tab, inc, box)
-        if self.cfg.use_metamaterials:
+        if st.get("D1") is not None:
+            self._drude_cells(c)
             D1 = st["D1"][p]
             D1n, D1c, D1p = D1[2], D1[0], D1[1]
             Dp = D[1]
             self.ops.lincomb(D1n, box, [(st["b0"], Dn), (st["b1"], Dc), (st["b2"], Dp),
                                         (st["ma1"], D1c), (st["ma2"], D1p)])
             src_new, src_old = D1n, D1c
+            cbE, ccE = st["cbE"], st["ccE"]
         else:
             src_new, src_old = Dn, Dc
-        self.ops.lincomb(F[c], box, [(st["caE"], F[c]), (st["cbE"], src_new), (st["ccE"], src_old)])
+            # a non-dispersive component of a metamaterial run: E from D
+            # through 1/(eps eps0) (the plain form; D1 = D/(eps eps0) exactly)
+            pl = st.get("plain")
+            cbE, ccE = (pl["cbE"], pl["ccE"]) if pl is not None else (st["cbE"], st["ccE"])
+        self.ops.lincomb(F[c], box, [(st["caE"], F[c]), (cbE, src_new), (ccE, src_old)])
 
     def _upml_rotate(self, c: str, p: int) -> None:
         """new -> cur -> prev (the reference's ``nextTimeStep`` shift)."""
         st = self.upml[c]
         D = st["D"][p]
-        if self.cfg.use_metamaterials:
+        if len(D) == 3:
             D[0], D[1], D[2] = D[2], D[0], D[1]
             D1 = st["D1"][p]
             D1[0], D1[1], D1[2] = D1[2], D1[0], D1[1]
@@ -961,7 +1090,7 @@ class YeeScheme(BlockedStepping):
                 for c in self.comps:
                     for lv, t in enumerate(self.upml[c]["D"][p]):
                         out["%s%s-aux%d%s" % ("D" if c[0] == "E" else "B", c[1], lv, sfx)] = t
-                    if self.cfg.use_metamaterials:
+                    if self.upml[c].get("D1") is not None:
                         for lv, t in enumerate(self.upml[c]["D1"][p]):
                             out["%s1%s-aux%d%s" % ("D" if c[0] == "E" else "B", c[1], lv, sfx)] = t
             if self.use_cpml:
@@ -990,7 +1119,7 @@ class YeeScheme(BlockedStepping):
             elif self.use_upml_chain:
                 for c in self.comps:
                     out += list(self.upml[c]["D"][p])
-                    if self.cfg.use_metamaterials:
+                    if self.upml[c].get("D1") is not None:
                         out += list(self.upml[c]["D1"][p])
             if self.use_cpml:
                 out += self.cpml.state_tensors(p)
@@ -1015,7 +1144,7 @@ class YeeScheme(BlockedStepping):
             elif self.use_upml_chain:
                 for c in self.comps:
                     out += [None] * len(self.upml[c]["D"][p])
-                    if self.cfg.use_metamaterials:
+                    if self.upml[c].get("D1") is not None:
                         out += [None] * len(self.upml[c]["D1"][p])
             if self.use_cpml:
                 out += self.cpml.state_boxes(p)

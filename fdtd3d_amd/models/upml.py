@@ -174,6 +174,7 @@ class DrudeBox:
             cb_ = boxes[c]
             own[tuple(slice(cb_[0][d] - B[0][d], cb_[1][d] - B[0][d]) for d in range(3))] = True
             use = own & in_range[c[0]].to(dev)
+            scheme._drude_cells(c)
             M = torch.stack([st[n].cell[sl].reshape(-1) for n in ("b0", "b1", "b2", "ma1", "ma2")], 1)
             tab, inv = torch.unique(M, dim=0, return_inverse=True)
             if tab.shape[0] > self.MAX_LUT:

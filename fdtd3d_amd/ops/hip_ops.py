@@ -1015,13 +1015,23 @@ class HipOps:
             dr = [None] * 5
             lut = (None, None)
             if drude:
-                dr = [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")]
-                for n, t in zip(("b0", "b1", "b2", "ma1", "ma2"), dr):
-                    if st[n].scalar != 1.0 or t is None:
-                        raise HipError("Drude coefficient %s must be a plain per-cell array" % n)
-                    self._check_tensor(t, shape)
-                if self.drude_lut:
-                    lut = self._drude_lut(st, dr, shape)
+                pre = st.get("_drude_lut")
+                if self.drude_lut and pre is not None and pre[0] is not None:
+                    # built at initialisation (scheme._init_upml): index + table only
+                    lut = pre
+                    ids, tab = lut
+                    if (ids.device.type != "cuda" or ids.dtype != torch.uint8 or tuple(ids.shape) != shape
+                            or not ids.is_contiguous() or tab.dtype != self.dtype or tab.dim() != 2
+                            or tab.shape[1] != 5 or tab.device.type != "cuda"):
+                        raise HipError("Drude index / table of %s malformed" % c)
+                else:
+                    dr = [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")]
+                    for n, t in zip(("b0", "b1", "b2", "ma1", "ma2"), dr):
+                        if st[n].scalar != 1.0 or t is None:
+                            raise HipError("Drude coefficient %s must be a plain per-cell array" % n)
+                        self._check_tensor(t, shape)
+                    if self.drude_lut:
+                        lut = self._drude_lut(st, dr, shape)
             # plain Yee cells folded into the launch (F += c curl; c scalar or scaled per cell)
             pb = plain.get(c, ((0, 0, 0), (0, 0, 0))) if plain else ((0, 0, 0), (0, 0, 0))
             pcell, pcb = None, 1.0

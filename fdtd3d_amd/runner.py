@@ -257,6 +257,7 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
                 rec["rank0_passes"] = breakdown  # decomposed passes: interior / exchange wait / shell ms
             if scheme.device.type == "cuda":
                 rec["max_mem_gb"] = torch.cuda.max_memory_allocated(scheme.device) / 1e9
+                rec["mem_plan_gb"] = round(sum(getattr(scheme, "mem_plan", {}).values()) / 1e9, 2)
             if halo is not None:
                 # rank 0's halo traffic over the timed steps (sent bytes; every
                 # rank receives as much as its neighbours send it)

@@ -206,6 +206,9 @@ def test_drude_lut_bitwise(gpu):
         if lut:
             ids, tab = s.upml["Ez"]["_drude_lut"]
             assert ids is not None and ids.dtype == torch.uint8 and 2 <= tab.shape[0] <= 8
+            # lean initialisation: no per-cell coefficient arrays, no D1 for H
+            assert s.upml["Ez"]["b0"].cell is None
+            assert s.upml["Hx"].get("D1") is None and len(s.upml["Hx"]["D"][0]) == 2
         res.append({c: s.F[0][c].cpu() for c in s.comps})
     for c in res[0]:
         assert torch.equal(res[0][c], res[1][c]), c

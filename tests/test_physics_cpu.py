@@ -164,3 +164,30 @@ def test_amplitude_check_period():
     assert res[1][2] and res[8][2], res
     assert res[1][1] == res[8][1] == res[1][0], res
     assert res[8][0] == -(-res[8][1] // 8) * 8, res
+
+
+def test_capacity_plan_drude_upml():
+    """The capacity plan of a Drude sphere + UPML run (scheme.capacity_plan):
+    two field sets on the HIP path, three D levels + D1 for the three
+    dispersive E components only, two D levels for H -- and the resident
+    arrays of the torch run match the plan's UPML / D1 terms."""
+    import torch
+    from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
+    from fdtd3d_amd.ops import make_ops
+    cfg = SchemeConfig(scheme="3d", size=(40, 36, 32), dtype="f32", use_pml=True, use_metamaterials=True,
+                       scene="drude-sphere", sphere_radius=7, sphere_center=(20.0, 18.0, 16.0), time_steps=2)
+    s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float32))
+    s.init_scheme()
+    s.init_grids()
+    cells = 40 * 36 * 32
+    plan = s.mem_plan
+    assert plan["fields"] == 24 * cells
+    assert plan["upml_D"] == 4 * cells * (3 * 3 + 2 * 3)
+    assert plan["drude_D1"] == 3 * 4 * cells * 3
+    d = sum(t.numel() * 4 for c in s.comps for t in s.upml[c]["D"][0])
+    d1 = sum(t.numel() * 4 for c in s.comps if s.upml[c].get("D1") is not None for t in s.upml[c]["D1"][0])
+    assert d == plan["upml_D"] and d1 == plan["drude_D1"]
+    assert all(s.upml[c].get("D1") is None for c in s.h_comps)
+    # the material grids are released once the coefficients exist
+    assert not s.sampler._cache and all(v is None for v in s.mat.values())
+    s.perform_steps()
