@@ -269,39 +269,46 @@ struct AmpSet {
   Box3 b[6];
 };
 
+// one cell of every component per thread: a 3D grid over the union of the
+// component boxes (z lanes, 4 rows per workgroup, one x plane per grid
+// slice), no index division; per-wave count reduction, one atomic per wave
 template <typename T>
-__global__ __launch_bounds__(256) void k_amplitude_many(AmpSet a, int ny, int nz, double accuracy,
-                                                        unsigned int* __restrict__ changed) {
-  const int c = blockIdx.y;
-  const T* __restrict__ f = (const T*)a.f[c];
-  T* __restrict__ amp = (T*)a.amp[c];
-  const Box3 b = a.b[c];
-  const int bx = b.hi[0] - b.lo[0], by = b.hi[1] - b.lo[1], bz = b.hi[2] - b.lo[2];
-  const long long n = (bx > 0 && by > 0 && bz > 0) ? (long long)bx * by * bz : 0;
+__global__ __launch_bounds__(256) void k_amplitude_many(AmpSet a, int ncomp, Box3 u, int ny, int nz,
+                                                        double accuracy, unsigned int* __restrict__ changed) {
+  const int k = u.lo[2] + blockIdx.x * 64 + threadIdx.x;
+  const int j = u.lo[1] + blockIdx.y * 4 + threadIdx.y;
+  const int i = u.lo[0] + blockIdx.z;
   unsigned int cnt = 0;
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n;
-       t += (long long)gridDim.x * blockDim.x) {
-    const int k = (int)(t % bz);
-    const long long r = t / bz;
-    const int j = (int)(r % by);
-    const int i = (int)(r / by);
-    const size_t off = ((size_t)(b.lo[0] + i) * ny + (b.lo[1] + j)) * nz + (b.lo[2] + k);
-    const T v = f[off] < T(0) ? -f[off] : f[off];
-    const T am = amp[off];
-    if (v >= am) {
-      T acc = v - am;
-      if (am != T(0))
-        acc /= am;
-      else if (v != T(0))
-        acc /= v;
-      if (acc > (T)accuracy) {
-        cnt++;
-        amp[off] = v;
+  if (k < u.hi[2] && j < u.hi[1]) {
+    const size_t off = ((size_t)i * ny + j) * nz + k;
+    const T acc_t = (T)accuracy;
+    // every component's field and running maximum loaded before the first
+    // store (a store through one amp pointer could alias the next loads, which
+    // otherwise serialises six memory round trips per cell)
+    T fv[6], am[6];
+    bool in[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const Box3& b = a.b[c];
+      in[c] = c < ncomp && i >= b.lo[0] && i < b.hi[0] && j >= b.lo[1] && j < b.hi[1] && k >= b.lo[2] &&
+              k < b.hi[2];
+      fv[c] = in[c] ? ((const T*)a.f[c])[off] : T(0);
+      am[c] = in[c] ? ((const T*)a.amp[c])[off] : T(0);
+    }
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const T v = fv[c] < T(0) ? -fv[c] : fv[c];
+      if (in[c] && v >= am[c]) {
+        const T den = am[c] != T(0) ? am[c] : (v != T(0) ? v : T(1));
+        if ((v - am[c]) / den > acc_t) {
+          cnt++;
+          ((T*)a.amp[c])[off] = v;
+        }
       }
     }
   }
   for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
-  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(changed, cnt);
+  if (threadIdx.x == 0 && cnt) atomicAdd(changed, cnt);
 }
 
 inline unsigned reduce_grid(long long n) {
@@ -382,7 +389,16 @@ int amplitude_many(const void* const* f, void* const* amp, int ncomp, int ny, in
     }
   }
   if (nmax == 0) return 0;
-  k_amplitude_many<T><<<dim3(reduce_grid(nmax), ncomp), 256, 0, s>>>(a, ny, nz, accuracy, changed);
+  Box3 u = {{0, 0, 0}, {0, 0, 0}};
+  bool first = true;
+  for (int c = 0; c < ncomp; ++c) {
+    if (box_empty(a.b[c])) continue;
+    u = first ? a.b[c] : box_union(u, a.b[c]);
+    first = false;
+  }
+  const dim3 grid((unsigned)cdiv(u.hi[2] - u.lo[2], 64), (unsigned)cdiv(u.hi[1] - u.lo[1], 4),
+                  (unsigned)(u.hi[0] - u.lo[0]));
+  k_amplitude_many<T><<<grid, dim3(64, 4), 0, s>>>(a, ncomp, u, ny, nz, accuracy, changed);
   FDTD_RETURN_LAUNCH_STATUS();
 }
 

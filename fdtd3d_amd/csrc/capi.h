@@ -33,6 +33,12 @@ int fdtd_update_h3d_cpml_v4_f32(float* hx, float* hy, float* hz, const float* ex
                                 const float* dbx, const float* dby, const float* dbz, double db, int nx, int ny,
                                 int nz, const int* boxes, int xchunk, const void* const* cp, const int* ci,
                                 void* stream);
+// fused UPML / Drude chain of the three components of a kind (chain_kernels.hip):
+// P = 24 pointers, S = 2 scalars, I = 19 ints per component (layout there)
+int fdtd_chain3d_f32(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny, int nz,
+                     void* stream);
+int fdtd_chain3d_f64(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny, int nz,
+                     void* stream);
 // TF/SF: 1D incident line steps and the table-driven corrections
 // (generic_kernels.hip; ijk may be null when the box holds every target)
 int fdtd_inc_e_f32(float* einc, const float* hinc, int n, double c, double src, void* stream);

@@ -5,10 +5,12 @@
 // Covers the plain Yee solvers (1D, 2D TMz/TEz, 3D) on one GPU with the
 // vacuum / dielectric-sphere scenes and the hard point source, fp32 or fp64,
 // fused or split 3D kernels, CPML absorbing layers in 3D fp32 (--use-pml
-// --pml-type cpml) and TF/SF plane waves in 3D, DAT/BMP output of the final
-// fields.  UPML, 2D TF/SF, dispersive media, NTFF, amplitude mode and
-// multi-GPU runs go through the
-// Python driver (python -m fdtd3d_amd), which shares the kernels; asking this
+// --pml-type cpml), the UPML in the reference's D/B form and Drude / Lorentz
+// spheres (--use-metamaterials, scene drude-sphere) in 3D through the fused
+// chain kernel, TF/SF plane waves in 3D, the NTFF scattered power diagram
+// (--use-ntff) and DAT/BMP output of the final fields (native_physics.h).
+// 2D TF/SF / PML, amplitude mode and multi-GPU runs go through the Python
+// driver (python -m fdtd3d_amd), which shares the kernels; asking this
 // binary for them is an error, never a silent fallback.
 #include <hip/hip_runtime.h>
 
@@ -22,6 +24,7 @@
 
 #include "capi.h"
 #include "host_native.h"
+#include "native_physics.h"
 #include "settings_native.h"
 
 namespace {
@@ -539,15 +542,18 @@ int run(const fdtd::Settings& s) {
   const double dx = s.gridStep, courant = s.courantNum;
   const double dt = dx * courant / kC;
   const double freq = kC / s.sourceWaveLength;
-  const bool vacuum = s.scene == "vacuum" || (s.scene == "reference" && dim != 3);
+  // eps = 1 everywhere (a Drude sphere's eps_inf is 1 too: layout/materials.py Scene.eps)
+  const bool vacuum = s.scene == "vacuum" || s.scene == "drude-sphere" || (s.scene == "reference" && dim != 3);
   const bool v4 = sizeof(T) == 4 && N[2] % 4 == 0 && dim == 3;
   // fused / blocked / resident kernels unless --split-kernels (3D fused E+H
   // and blocked passes, 2D blocked passes, 1D one-launch resident run)
   // CPML runs step through the float4 split kernels with the psi terms folded
   // in; TF/SF runs apply their corrections between the split half steps
-  const bool cpml = s.doUsePML;
+  const bool upml = (s.doUsePML && s.pmlType == "upml") || s.doUseMetamaterials;  // the D/B chain
+  const bool cpml = s.doUsePML && !upml;
   const bool tfsf = s.doUseTFSF;
-  const bool use_fused = !s.doUseSplitKernels && !cpml && !tfsf;
+  const bool ntff = s.doUseNTFF && dim == 3;
+  const bool use_fused = !s.doUseSplitKernels && !cpml && !tfsf && !upml;
   hipStream_t st;
   HIP_OK(hipStreamCreate(&st));
 
@@ -640,6 +646,32 @@ int run(const fdtd::Settings& s) {
   };
   NativeCpml cpt;
   if (cpml) setup_cpml(cpt, s, N, active, dt, dx);
+  native_phys::Upml<T> upt;
+  if (upml) {
+    native_phys::UpmlScene sc;
+    sc.pml[0] = s.pmlSizeX;
+    sc.pml[1] = s.pmlSizeY;
+    sc.pml[2] = s.pmlSizeZ;
+    sc.use_pml = s.doUsePML;
+    sc.metamaterials = s.doUseMetamaterials;
+    sc.lorentz = s.dispersion == "lorentz";
+    sc.lorentz_ratio = s.lorentzOmega0Ratio;
+    sc.freq = freq;
+    sc.sphere_eps = s.scene == "sphere";
+    sc.drude_sphere = s.scene == "drude-sphere";
+    sc.ctr[0] = s.sphereCenterX;
+    sc.ctr[1] = s.sphereCenterY;
+    sc.ctr[2] = s.sphereCenterZ;
+    sc.radius = s.sphereRadius;
+    sc.eps_in = s.sphereEps;
+    native_phys::setup_upml<T>(upt, N, sc, dt, dx);
+  }
+  T* Fp[6];
+  auto fptrs = [&]() {
+    for (int c = 0; c < 6; ++c) Fp[c] = F[c].p;
+  };
+  int (*chain_fn)(const void* const*, const double*, const int*, int, int, int, int, void*) =
+      sizeof(T) == 4 ? fdtd_chain3d_f32 : fdtd_chain3d_f64;
   NativeTfsf<T> tft;
   if (tfsf && !setup_tfsf(tft, s, N, boxes, C, percell ? 1.0 : cb, percell ? 1.0 : db, dt, dx, freq)) return 1;
   const bool point_src = !tfsf || s.doUsePointSource;
@@ -667,7 +699,10 @@ int run(const fdtd::Settings& s) {
         // split half steps: [incident line E] E update [TF/SF on E] [source]
         // [incident line H] H update [TF/SF on H] -- the order of scheme.step
         if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
-        if (cpml) {
+        if (upml) {
+          fptrs();
+          K_OK(native_phys::upml_kind<T>(upt, Fp, boxes, 0, N[1], N[2], st, chain_fn));
+        } else if (cpml) {
           if constexpr (sizeof(T) == 4)
             K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p,
                                              percell ? 1.0 : cb, N[0], N[1], N[2], boxes, 0, cpt.P[0].data(),
@@ -679,7 +714,10 @@ int run(const fdtd::Settings& s) {
         if (tfsf) tfsf_kind(0);
         if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));
         if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
-        if (cpml) {
+        if (upml) {
+          fptrs();
+          K_OK(native_phys::upml_kind<T>(upt, Fp, boxes, 1, N[1], N[2], st, chain_fn));
+        } else if (cpml) {
           if constexpr (sizeof(T) == 4)
             K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p,
                                              percell ? 1.0 : db, N[0], N[1], N[2], boxes + 18, 0, cpt.P[1].data(),
@@ -783,15 +821,44 @@ int run(const fdtd::Settings& s) {
     }
   };
 
+  // NTFF diagram after every step t with (t - 1) % ntffStep == 0, for the
+  // fields of step t - 1 (the Python driver's periodic hook, runner.py)
+  const int nstep = std::max(1, s.ntffStep);
+  const int nbox[3] = {s.ntffSizeX, s.ntffSizeY, s.ntffSizeZ};
+  auto ntff_report = [&](int t) {
+    HIP_OK(hipStreamSynchronize(st));
+    fptrs();
+    const std::vector<double> phis = native_phys::reference_angles();
+    const std::vector<double> p =
+        native_phys::ntff_power<T>(Fp, N, nbox, dx, s.sourceWaveLength, s.incidentWaveAngle1 * (kPi / 180.0), phis);
+    for (size_t q = 0; q < phis.size(); ++q)
+      std::printf("=== t=%u, inc angle=%f; angle %f === %.17g \n", (unsigned)t, s.incidentWaveAngle2 * (kPi / 180.0),
+                  phis[q], p[q]);
+  };
+  auto run_steps = [&](int t0, int n) {
+    if (!ntff) {
+      advance(t0, n);
+      return;
+    }
+    int t = t0;
+    const int end = t0 + n;
+    while (t < end) {
+      const int nxt = std::min(end, t + 1 + ((1 - (t + 1)) % nstep + nstep) % nstep);
+      advance(t, nxt - t);
+      t = nxt;
+      if ((t - 1) % nstep == 0) ntff_report(t - 1);
+    }
+  };
+
   const int steps = s.numTimeSteps;
   const int warm = std::max(0, std::min(s.warmupSteps, steps));
-  advance(0, warm);  // untimed (they advance the simulation)
+  run_steps(0, warm);  // untimed (they advance the simulation)
   HIP_OK(hipStreamSynchronize(st));
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, st));
-  advance(warm, steps - warm);
+  run_steps(warm, steps - warm);
   HIP_OK(hipEventRecord(e1, st));
   HIP_OK(hipEventSynchronize(e1));
   HIP_OK(hipGetLastError());
@@ -816,9 +883,9 @@ int run(const fdtd::Settings& s) {
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", std::max(T_blk, T2_blk));
   else if (res1)
     std::printf("Backend: native HIP, register-resident 1D kernel (one launch per run)\n");
-  else if (cpml || tfsf)
-    std::printf("Backend: native HIP, split kernels%s%s\n", cpml ? " with the CPML terms folded in" : "",
-                tfsf ? " + TF/SF corrections" : "");
+  else if (cpml || tfsf || upml)
+    std::printf("Backend: native HIP, split kernels%s%s%s\n", cpml ? " with the CPML terms folded in" : "",
+                upml ? " with the UPML / dispersive chain" : "", tfsf ? " + TF/SF corrections" : "");
   else
     std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
   std::printf("Throughput: %.1f Mcells/s\n", cells * (double)timed / sec / 1e6);
@@ -868,18 +935,25 @@ int main(int argc, char** argv) {
     return 1;
   }
   // CPML absorbing layers: 3D fp32 with whole float4 z rows (the folded float4 kernels)
-  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && s.dimension == 3 && s.valueType == "f32" &&
-                       s.sizeZ % 4 == 0;
-  // TF/SF plane waves: 3D (any precision), also combined with the CPML
-  const bool tfsf_ok = s.doUseTFSF && s.dimension == 3;
-  if ((s.doUsePML && !cpml_ok) || (s.doUseTFSF && !tfsf_ok) || s.doUseMetamaterials || s.doUseNTFF ||
-      s.doUseAmplitudeMode ||
-      s.doUseComplexFieldValues || s.doUseParallelGrid || s.doUseDoubleMaterialPrecision ||
+  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && !s.doUseMetamaterials && s.dimension == 3 &&
+                       s.valueType == "f32" && s.sizeZ % 4 == 0;
+  // UPML (D/B chain) and Drude / Lorentz spheres: 3D, any precision
+  const bool upml_ok = s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials) && s.dimension == 3;
+  const bool meta_ok = !s.doUseMetamaterials || (s.dimension == 3 && s.scene == "drude-sphere");
+  // TF/SF plane waves: 3D (any precision), with the CPML or the UPML; with the
+  // UPML the corrections take the E form, exact where every sigma vanishes:
+  // the TF/SF box must lie inside the absorbing layers' interior
+  bool tfsf_ok = s.doUseTFSF && s.dimension == 3;
+  if (tfsf_ok && s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials))
+    tfsf_ok = s.tfsfSizeX > s.pmlSizeX + 1 && s.tfsfSizeY > s.pmlSizeY + 1 && s.tfsfSizeZ > s.pmlSizeZ + 1;
+  const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
+  if ((s.doUsePML && !cpml_ok && !upml_ok) || (s.doUseTFSF && !tfsf_ok) || !meta_ok || !ntff_ok ||
+      s.doUseAmplitudeMode || s.doUseComplexFieldValues || s.doUseParallelGrid || s.doUseDoubleMaterialPrecision ||
       !s.loadFromFile.empty()) {
     std::fprintf(stderr,
-                 "fdtd3d (native): UPML, CPML outside 3D fp32 float4 rows, TF/SF outside 3D, metamaterials, NTFF, "
-                 "amplitude mode, complex fields, parallel grids and resume run through the Python driver: "
-                 "python -m fdtd3d_amd <same options>\n");
+                 "fdtd3d (native): CPML outside 3D fp32 float4 rows, PML / TF/SF / NTFF outside 3D, TF/SF boxes "
+                 "reaching the UPML, metamaterials outside the drude-sphere scene, amplitude mode, complex fields, "
+                 "parallel grids and resume run through the Python driver: python -m fdtd3d_amd <same options>\n");
     return 2;
   }
   int ndev = 0;

@@ -51,6 +51,25 @@ CASES = {
                      "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6", "--same-size-pml", "--use-tfsf",
                      "--tfsf-sizex", "10", "--same-size-tfsf", "--angle-teta", "60", "--angle-phi", "10",
                      "--angle-psi", "5"],
+    # UPML in the reference's D/B form (fused chain kernel) + oblique TF/SF, a dielectric sphere with the
+    # UPML (per-cell 1/(eps eps0) in the chain), Drude and Lorentz spheres + UPML (uint8 index + table)
+    "3d_upml_tfsf": ["--3d", "--sizex", "36", "--sizey", "32", "--sizez", "40", "--time-steps", "30",
+                     "--scene", "vacuum", "--use-pml", "--pml-sizex", "5", "--pml-sizey", "4", "--pml-sizez", "6",
+                     "--use-tfsf", "--tfsf-sizex", "9", "--tfsf-sizey", "8", "--tfsf-sizez", "10",
+                     "--angle-teta", "60", "--angle-phi", "20", "--angle-psi", "30"],
+    "3d_upml_sphere": ["--3d", "--sizex", "32", "--same-size", "--time-steps", "24", "--scene", "sphere",
+                       "--sphere-center-x", "16", "--sphere-center-y", "16", "--sphere-center-z", "16",
+                       "--sphere-radius", "5", "--sphere-eps", "3", "--use-pml", "--pml-sizex", "5",
+                       "--same-size-pml"],
+    "3d_drude_upml": ["--3d", "--sizex", "40", "--sizey", "36", "--sizez", "32", "--time-steps", "24",
+                      "--scene", "drude-sphere", "--use-metamaterials", "--use-pml", "--pml-sizex", "5",
+                      "--same-size-pml", "--sphere-center-x", "20", "--sphere-center-y", "18",
+                      "--sphere-center-z", "16", "--sphere-radius", "7"],
+    "3d_lorentz_upml_tfsf": ["--3d", "--sizex", "40", "--same-size", "--time-steps", "24", "--scene",
+                             "drude-sphere", "--use-metamaterials", "--dispersion", "lorentz", "--lorentz-omega0",
+                             "0.7", "--use-pml", "--pml-sizex", "5", "--same-size-pml", "--sphere-center-x", "20",
+                             "--sphere-center-y", "20", "--sphere-center-z", "20", "--sphere-radius", "6",
+                             "--use-tfsf", "--tfsf-sizex", "9", "--same-size-tfsf"],
 }
 FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf"}
 
@@ -102,3 +121,40 @@ def test_native_driver_matches_python(case, dtype, tmp_path, gpu):
         for c, (err, _) in errs.items():
             if c[0] == kind:
                 assert err <= tol * peak + 1e-300, (c, err, peak)
+
+
+NTFF_ARGV = ["--3d", "--sizex", "40", "--same-size", "--time-steps", "31", "--scene", "sphere", "--sphere-center-x",
+             "20", "--sphere-center-y", "20", "--sphere-center-z", "20", "--sphere-radius", "5", "--sphere-eps", "3",
+             "--use-pml", "--pml-sizex", "5", "--same-size-pml", "--use-tfsf", "--tfsf-sizex", "9",
+             "--same-size-tfsf", "--use-ntff", "--ntff-sizex", "12", "--same-size-ntff", "--ntff-step", "10"]
+
+
+def _ntff_lines(text):
+    out = []
+    for line in text.splitlines():
+        if line.startswith("=== t="):
+            head, val = line.rsplit("===", 1)
+            out.append((head.strip(), float(val)))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_native_ntff_matches_python(dtype, gpu):
+    """The native driver's NTFF scattered power diagram (native_physics.h) at
+    the reference's angles and report steps against the Python driver's
+    (models/ntff.py) on the torch CPU backend, same UPML + TF/SF + sphere run."""
+    exe = native.executable()
+    assert os.path.exists(exe)
+    r = subprocess.run([exe] + NTFF_ARGV + ["--dtype", dtype], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    buf = io.StringIO()
+    assert py_run(NTFF_ARGV + ["--dtype", "f64", "--backend", "torch", "--device", "cpu"], out=buf) == 0
+    a, b = _ntff_lines(r.stdout), _ntff_lines(buf.getvalue())
+    assert len(a) == len(b) == 4 * 181, (len(a), len(b))  # t = 0, 10, 20, 30
+    assert [h for h, _ in a] == [h for h, _ in b]
+    peak = max(abs(v) for _, v in b)
+    assert peak > 0
+    tol = 1e-9 if dtype == "f64" else 2e-4
+    for (h, x), (_, y) in zip(a, b):
+        assert abs(x - y) <= tol * peak, (h, x, y, peak)
