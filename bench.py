@@ -36,6 +36,7 @@ import json
 import os
 import sys
 import time
+T_START = time.perf_counter()
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -107,11 +108,20 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
         ops.tb_vec, ops.tb_rows, ops.tb_xcd, ops.tb_mrows = a.tb_vec, a.tb_rows, a.tb_xcd, a.tb_mrows
         if a.tb_variant >= 0:
             ops.tb_variant = a.tb_variant
+    trace = os.environ.get("FDTD3D_BENCH_TRACE") == "1"  # phase lines on stderr (profiler runs)
+
+    def phase(msg):
+        if trace:
+            print("[bench %.1fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+    phase("ops ready")
     scheme = YeeScheme(cfg, ops, domain, halo)
     scheme.init_scheme()
     scheme.init_grids()
+    phase("grids ready")
     if a.init == "random":
         scheme.randomize_fields(seed=a.seed)
+    phase("fields initialised")
 
     def allsum(v: float) -> float:
         if world == 1:
@@ -127,6 +137,7 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
             dist.barrier()
 
     energy0 = allsum(scheme.field_energy())
+    phase("warmup")
     scheme.advance(a.warmup)
     if halo is not None:
         halo.drain(scheme)
@@ -142,6 +153,7 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
         from fdtd3d_amd.models.blocking import PassTimer
         scheme.pass_timer = PassTimer(scheme.device)
     sync()
+    phase("timed steps")
     t0 = time.perf_counter()
     scheme.advance(a.steps)
     if halo is not None:

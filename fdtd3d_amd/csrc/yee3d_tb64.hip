@@ -13,6 +13,9 @@
 // A single-pass fp64 step moves >= 96 B/cell; T steps per pass read and write
 // the six fields once (plus the tile halos).
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
     const double* __restrict__ cbx, const double* __restrict__ cby, const double* __restrict__ cbz,
     const double* __restrict__ dbx, const double* __restrict__ dby, const double* __restrict__ dbz, double cb,
     double db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
-    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc64 sv) {
+    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc64 sv, int patch) {
   constexpr int LW = HALF ? 32 : 64;  // z lanes per row
   constexpr int TBZ = LW - 2 * T;       // owned z cells per tile
   constexpr int ROWS = TBW * R * (HALF ? 2 : 1);
@@ -129,9 +132,26 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
     const int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
     const int n8 = n & ~7;
     const int q = p < n8 ? (p & 7) * (n8 >> 3) + (p >> 3) : p;
-    tz = q % gx;
-    ty = (q / gx) % gy;
-    tx = q / (gx * gy);
+    const int pz = patch & 0xff, py = (patch >> 8) & 0xff;
+    if (pz > 0 && py > 0) {
+      // patch order (yee3d_tb.hip k_tb3d_mr): an XCD's run of tiles in PZ x
+      // PY blocks, so a tile's y neighbours -- 2T shared rows, a quarter of
+      // a 32-row fp64 tile -- stream the same planes on the same L2
+      tx = q / (gx * gy);
+      const int r = q - tx * gx * gy;
+      const int band = r / (py * gx);
+      const int h = min(py, gy - band * py);
+      const int rb = r - band * py * gx;
+      const int col = rb / (pz * h);
+      const int wdt = min(pz, gx - col * pz);
+      const int e = rb - col * pz * h;
+      tz = col * pz + e % wdt;
+      ty = band * py + e / wdt;
+    } else {
+      tz = q % gx;
+      ty = (q / gx) % gy;
+      tx = q / (gx * gy);
+    }
   }
   const int k = O.lo[2] - T + TBZ * tz + lz;
   const int jw = O.lo[1] - T + (ROWS - 2 * T) * ty + (HALF ? 2 * w + hr : R * w);
@@ -289,6 +309,20 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
   store_out(i1 + T - 1);
 }
 
+// patch order of the XCD tile run: pz | (py << 8), 0 = z fastest;
+// FDTD3D_TB64_PATCH="PZxPY" at first use, fdtd_set_tb64_patch
+int g_tb64_patch = -1;
+int tb64_patch() {
+  if (g_tb64_patch < 0) {
+    g_tb64_patch = 0;
+    const char* e = getenv("FDTD3D_TB64_PATCH");
+    int pz = 0, py = 0;
+    if (e && sscanf(e, "%dx%d", &pz, &py) == 2 && pz > 0 && py > 0 && pz < 256 && py < 256)
+      g_tb64_patch = pz | (py << 8);
+  }
+  return g_tb64_patch;
+}
+
 template <int T, int R, bool HALF>
 int launch_tb64(bool pc, const double* const* ein, const double* const* hin, double* const* eout,
                 double* const* hout, const double* const* cbs, const double* const* dbs, double cb, double db,
@@ -302,7 +336,7 @@ int launch_tb64(bool pc, const double* const* ein, const double* const* hin, dou
 #define TB64_ARGS                                                                                              \
   ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2],      \
       cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
-      O, xchunk, src[0], src[1], src[2], src[3], sv
+      O, xchunk, src[0], src[1], src[2], src[3], sv, tb64_patch()
   if (pc)
     k_tb3d_f64<T, R, true, HALF><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
   else
@@ -318,6 +352,11 @@ FDTD_API int fdtd_tb64_max_steps() { return 5; }
 // 1: two rows of 32 lanes per wave (32 x 32 tiles, default); 0: one row of
 // 64 lanes (16 x 64 tiles)
 FDTD_API void fdtd_set_tb64_shape(int half) { g_tb64_half = half != 0; }
+
+// patch order of the fp64 kernel's XCD tile run: pz x py tiles (0: z fastest)
+FDTD_API void fdtd_set_tb64_patch(int pz, int py) {
+  g_tb64_patch = (pz > 0 && py > 0 && pz < 256 && py < 256) ? (pz | (py << 8)) : 0;
+}
 
 // fp64 counterpart of fdtd_tb3d_v4_f32 (same arguments, double arrays), 1..4
 // steps per pass, any nz.

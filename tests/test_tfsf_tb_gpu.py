@@ -55,7 +55,19 @@ def test_tfsf_blocked(gpu, name, extra, T, steps):
         assert float((bl.einc[p] - st.einc[p]).abs().max()) <= 1e-6 * (float(st.einc[p].abs().max()) + 1e-30)
 
 
-def test_tfsf_sets_oblique_falls_back(gpu):
-    cfg = SchemeConfig(time_steps=4, **BASE, scene="vacuum", theta=60.0, phi=20.0, time_block=4)
+def test_tfsf_oblique_takes_hybrid_passes(gpu):
+    """Oblique incidence (theta 60, phi 20): the incident index of a target is
+    not a function of one axis, so there are no in-kernel TF/SF sets -- the
+    run takes hybrid passes instead (blocked core, stepped shell carrying the
+    TF/SF tables of any angle, reference YeeGridLayout.cpp:327-845) and
+    matches the fp64 oracle through two passes and a tail."""
+    cfg = SchemeConfig(scheme="3d", size=(96, 88, 96), dtype="f32", tfsf_size=(8, 8, 8), use_tfsf=True,
+                       use_fused=True, scene="vacuum", theta=60.0, phi=20.0, psi=30.0, time_steps=13)
     s = _run(cfg, "hip", gpu, torch.float32)
-    assert s.tfsf_sets is None and not s.tfsf_blocked and s.tb == 1
+    assert s.tfsf_sets is None and not s.tfsf_blocked
+    assert s.hybrid is not None and s.hybrid["T"] > 1 and s.hybrid["core_cells"] > 0.25 * s.cells()
+    ref = _run(dataclasses.replace(cfg, use_fused=False, dtype="f64"), "torch", "cpu", torch.float64)
+    for c in ref.comps:
+        scale = max(float(ref.F[0][o].abs().max()) for o in ref.comps if o[0] == c[0]) + 1e-30
+        err = float((s.F[0][c].double().cpu() - ref.F[0][c]).abs().max())
+        assert err <= 2e-5 * scale, (c, err, scale)
