@@ -3,6 +3,7 @@
 // can be captured into HIP graphs together with the stencil kernels.
 
 #include "common.h"
+#include "vec4.h"
 
 namespace {
 
@@ -311,6 +312,48 @@ __global__ __launch_bounds__(256) void k_amplitude_many(AmpSet a, int ncomp, Box
   if (threadIdx.x == 0 && cnt) atomicAdd(changed, cnt);
 }
 
+// fp32 float4 form (rows of whole 16-byte groups, nz % 4 == 0): four cells of
+// every component per thread, 16-byte loads, masked stores of the changed
+// maxima -- the amplitude update is a pure streaming pass (read f and amp,
+// write the grown amp), so the vector width is its bandwidth
+__global__ __launch_bounds__(256) void k_amplitude_many_v4(AmpSet a, int ncomp, Box3 u, int ny, int nz,
+                                                           float accuracy, unsigned int* __restrict__ changed) {
+  const int kb = (u.lo[2] & ~3) + 4 * (blockIdx.x * 64 + threadIdx.x);
+  const int j = u.lo[1] + blockIdx.y * 4 + threadIdx.y;
+  const int i = u.lo[0] + blockIdx.z;
+  unsigned int cnt = 0;
+  if (kb < u.hi[2] && j < u.hi[1]) {
+    const size_t off = ((size_t)i * ny + j) * nz + kb;
+    float4 fv[6], am[6];
+    unsigned m[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const Box3& b = a.b[c];
+      m[c] = (c < ncomp && i >= b.lo[0] && i < b.hi[0]) ? kmask(b, j, kb) : 0u;
+      fv[c] = m[c] ? ld4((const float*)a.f[c], off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      am[c] = m[c] ? ld4((const float*)a.amp[c], off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      unsigned w = 0;
+      float4 nv = am[c];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float f = f4(fv[c], e), v = f < 0.f ? -f : f, old = f4(am[c], e);
+        const float den = old != 0.f ? old : (v != 0.f ? v : 1.f);
+        if (((m[c] >> e) & 1u) && v >= old && (v - old) / den > accuracy) {
+          w |= 1u << e;
+          f4set(nv, e, v);
+          cnt++;
+        }
+      }
+      st4m((float*)a.amp[c], off, nv, w);
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+  if (threadIdx.x == 0 && cnt) atomicAdd(changed, cnt);
+}
+
 inline unsigned reduce_grid(long long n) {
   long long g = (n + 255) / 256;
   if (g > 4096) g = 4096;
@@ -395,6 +438,16 @@ int amplitude_many(const void* const* f, void* const* amp, int ncomp, int ny, in
     if (box_empty(a.b[c])) continue;
     u = first ? a.b[c] : box_union(u, a.b[c]);
     first = false;
+  }
+  if (sizeof(T) == 4 && nz % 4 == 0) {
+    bool al = true;
+    for (int c = 0; c < ncomp; ++c) al = al && ((uintptr_t)a.f[c] % 16 == 0) && ((uintptr_t)a.amp[c] % 16 == 0);
+    if (al) {
+      const int kspan = u.hi[2] - (u.lo[2] & ~3);
+      const dim3 g4((unsigned)cdiv(kspan, 256), (unsigned)cdiv(u.hi[1] - u.lo[1], 4), (unsigned)(u.hi[0] - u.lo[0]));
+      k_amplitude_many_v4<<<g4, dim3(64, 4), 0, s>>>(a, ncomp, u, ny, nz, (float)accuracy, changed);
+      FDTD_RETURN_LAUNCH_STATUS();
+    }
   }
   const dim3 grid((unsigned)cdiv(u.hi[2] - u.lo[2], 64), (unsigned)cdiv(u.hi[1] - u.lo[1], 4),
                   (unsigned)(u.hi[0] - u.lo[0]));
