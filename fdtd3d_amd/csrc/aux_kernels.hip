@@ -472,4 +472,4 @@ FDTD_API int fdtd_counter_add(int* counter, int n, void* s) {
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
-FDTD_API int fdtd_abi_version() { return 1; }
+FDTD_API int fdtd_abi_version() { return 2; }

@@ -109,6 +109,20 @@ struct CpmlDev {
 // curl terms of each component: (axis, sign), Ex = +dHz/dy - dHy/dz etc.
 __device__ constexpr int kTermAxis[6][2] = {{1, 2}, {2, 0}, {0, 1}, {2, 1}, {0, 2}, {1, 0}};
 
+// the CPML table travels by value in the kernel arguments (CPML variants
+// only): its pointers and profile reads are then wave-uniform scalar loads --
+// SGPR descriptors, no waterfall loop, and profile loads that wait on the
+// scalar counter instead of queueing behind the vector prefetch (a copy in
+// LDS hands every field back in VGPRs)
+template <bool ON>
+struct CpArg {
+  int unused;
+};
+template <>
+struct CpArg<true> {
+  CpmlDev d;
+};
+
 struct TfDev {
   int nsets;
   int ld;                   // g entries per level
@@ -403,13 +417,14 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     const float4* __restrict__ ce4, const float4* __restrict__ ch4, Box3 BE, Box3 BH, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz,
-    const TfDev* __restrict__ tf, const float* __restrict__ gtab, const CpmlDev* __restrict__ cp) {
+    const TfDev* __restrict__ tf, const float* __restrict__ gtab, const CpArg<(FX & 8) != 0> cpv,
+    float* __restrict__ pscr) {
   // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF,
-  // 8 CPML (single-step passes: the psi of a cell is read and written once)
+  // 8 CPML.  A CPML pass of T > 1 steps hands each level's psi to the next
+  // level through `pscr`, thread-private scratch (see the level loop)
   constexpr int PC = FX & 3;
   constexpr bool TFS = FX & 4;
   constexpr bool CPM = FX & 8;
-  static_assert(!CPM || T == 1, "CPML: one step per pass");
   static_assert(V == 1 || !FX, "sparse coefficients / TF/SF: scalar lanes");
   constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
   static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
@@ -421,22 +436,23 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   __shared__ vec sX[2][4][NW][64];
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);  // one wave per y (SGPR)
-  // TF/SF and CPML tables live in LDS for the kernel's life: their fields are
-  // read in many branches, and scalar loads there serialise on scalar-cache
-  // misses (and spill SGPRs)
+  // the TF/SF table lives in LDS for the kernel's life: its fields are read in
+  // many branches (with dynamic set indices)
   __shared__ unsigned sTFraw[TFS ? sizeof(TfDev) / 4 : 1];
-  __shared__ unsigned long long sCPraw[CPM ? sizeof(CpmlDev) / 8 : 1];
+  __shared__ unsigned long long sCPraw[1];  // stand-in table of the non-CPML variants (never read)
   if constexpr (TFS) {
     for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(TfDev) / 4); q += 64 * NW)
       sTFraw[q] = ((const unsigned*)tf)[q];
   }
-  if constexpr (CPM) {
-    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(CpmlDev) / 8); q += 64 * NW)
-      sCPraw[q] = ((const unsigned long long*)cp)[q];
-  }
-  if constexpr (TFS || CPM) __syncthreads();
+  if constexpr (TFS) __syncthreads();
   const TfDev& TF = *reinterpret_cast<const TfDev*>(sTFraw);
-  const CpmlDev& CP = *reinterpret_cast<const CpmlDev*>(sCPraw);
+  auto cp_ref = [&]() -> const CpmlDev& {
+    if constexpr (CPM)
+      return cpv.d;
+    else
+      return *reinterpret_cast<const CpmlDev*>(sCPraw);
+  };
+  const CpmlDev& CP = cp_ref();
   // Tile of this workgroup.  A row of a tile starts at an arbitrary z (the
   // stride is the 64 - 2T owned cells), so its 64 cells straddle three
   // 128-B lines, one shared with each z neighbour tile.  Workgroups are dealt
@@ -686,7 +702,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     }
   }
 
-  // CPML helpers (T = 1 single-step passes).  Terms are (component n, t):
+  // CPML helpers.  Terms are (component n, t):
   // axis kTermAxis[n][t].  y terms: Ex.0 Ez.1 Hx.1 Hz.0; z terms: Ex.1 Ey.0
   // Hx.0 Hy.1; x terms: the rest.
   auto ytm_index = [](int n) -> int { return n == 0 ? 0 : (n == 2 ? 1 : (n == 3 ? 2 : 3)); };
@@ -762,6 +778,29 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         cpm_wave |= act ? (1u << (2 * n + t)) : 0u;
       }
   }
+  // Multi-step CPML: level l of trip X advances the psi of plane X - l (E
+  // terms; H terms X - l - 1), and level l + 1 of trip X + 1 advances the same
+  // cells again -- in the same lane of the same wave.  So the hand-off between
+  // levels is thread-private: level l stores its psi in slot (X & 1, l) of
+  // this thread's scratch column, the next trip's level l + 1 loads it back
+  // (agent-scope loads: L1 bypassed, the thread's own store is in L2).  The
+  // trip parity keeps this trip's level l from overwriting what its level
+  // l + 1 has yet to read.  Level 0 reads
+  // the slab arrays (psi at time n), level T - 1 writes the other copy (n + T)
+  // for owned cells only.  Slots are slot-major across all threads of the
+  // launch, so a wave's 64 lanes touch one contiguous 256-B run.
+  const unsigned scr_nth = gridDim.x * gridDim.y * gridDim.z * NW * 64u;
+  const unsigned scr_tid =
+      ((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * NW + w) * 64u + lane;
+  const Rsrc scr_rs = __builtin_amdgcn_make_buffer_rsrc((void*)pscr, (short)0, CPM && T > 1 && pscr ? -1 : 0,
+                                                        0x00020000);
+  // (xcd_swz bit 24, tuning: plain loads that may hit L1 instead of agent-scope ones)
+  const bool scr_l1 = (xcd_swz >> 24) & 1;
+  // per-lane part of a slot address (one VGPR) + wave-uniform slot base (soffset)
+  const unsigned scr_voff = scr_tid * 4u;
+  auto scr_soff = [&](int par, int l, int n, int t, int r) -> int {
+    return (int)((unsigned)((((par * (T - 1) + l) * 6 + n) * 2 + t) * R + r) * scr_nth * 4u);
+  };
 
   auto run = [&](auto allin_tag) {
   constexpr bool ALLIN = decltype(allin_tag)::value;
@@ -982,6 +1021,26 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
 #pragma unroll
     for (int l = 0; l < T; ++l) {
       const int pe = X - l;
+      if constexpr (CPM && T > 1) {
+        if (l > 0) {
+          // this level's psi: written by level l - 1 on the previous trip
+#pragma unroll
+          for (int n = 0; n < 6; ++n) {
+            const int pl = n < 3 ? pe : pe - 1;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              if (!(cpm_wave >> (2 * n + t) & 1u)) continue;
+              if (kTermAxis[n][t] == 0 && psi_side_x(n, t, pl) < 0) continue;
+#pragma unroll
+              for (int r = 0; r < R; ++r) {
+                const int so = scr_soff((X - 1) & 1, l - 1, n, t, r);
+                PS[n][t][r] = __uint_as_float(scr_l1 ? __builtin_amdgcn_raw_buffer_load_b32(scr_rs, scr_voff, so, 0)
+                                                     : __builtin_amdgcn_raw_buffer_load_b32(scr_rs, scr_voff, so, 16));
+              }
+            }
+          }
+        }
+      }
       sX[buf][0][w][lane] = Hc[R - 1].z;
       sX[buf][1][w][lane] = Hc[R - 1].x;
       sX[buf][2][w][lane] = Ep[l][0].x;
@@ -1053,12 +1112,30 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         Hp[l][r] = Hc[r];
         Hc[r] = Hn;
       }
+      if constexpr (CPM && T > 1) {
+        if (l < T - 1) {
+#pragma unroll
+          for (int n = 0; n < 6; ++n) {
+            const int pl = n < 3 ? pe : pe - 1;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              if (!(cpm_wave >> (2 * n + t) & 1u)) continue;
+              if (kTermAxis[n][t] == 0 && psi_side_x(n, t, pl) < 0) continue;
+#pragma unroll
+              for (int r = 0; r < R; ++r)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PS[n][t][r]), scr_rs, scr_voff,
+                                                      scr_soff(X & 1, l, n, t, r), 0);
+            }
+          }
+        }
+      }
     }
     if constexpr (CPM) {
-      // psi of owned cells inside their component's update box
+      // psi of owned cells inside their component's update box (the last
+      // level's planes)
 #pragma unroll
       for (int n = 0; n < 6; ++n) {
-        const int pl = n < 3 ? X : X - 1;
+        const int pl = n < 3 ? X - T + 1 : X - T;
         if (pl < i0 || pl >= i1 || !xin(*bx[n], pl)) continue;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -1213,6 +1290,15 @@ int tb_patch_bits() {
   return g_tb_patch;
 }
 int g_tb_variant = 0;  // multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched
+// multi-step CPML scratch loads: 0 agent scope (default), 1 plain (FDTD3D_CPML_SCR_L1=1, tuning)
+int cpml_scr_l1() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FDTD3D_CPML_SCR_L1");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v;
+}
 const int kNoBox[6] = {0, 0, 0, 0, 0, 0};
 int g_tb_mr_shape = 0;  // plain multi-row kernel: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
 
@@ -1220,17 +1306,21 @@ template <int T, int V, int R, int FX, int NW = TBW>
 int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                  const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
                  int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
-                 const TfDev* tf, const float* gtab, const CpmlDev* cp, hipStream_t s) {
+                 const TfDev* tf, const float* gtab, const CpmlDev* cp, float* pscr, hipStream_t s) {
   constexpr int HL = (T + V - 1) / V;
   constexpr int TBZ = (64 - 2 * HL) * V;
   dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], NW * R - 2 * T),
             cdiv(O.hi[0] - O.lo[0], xchunk));
+  CpArg<(FX & 8) != 0> cpv{};
+  if constexpr ((FX & 8) != 0) cpv.d = *cp;
 #define MR_LAUNCH(PFD, DEFER)                                                                                 \
   k_tb3d_mr<T, V, R, FX, PFD, DEFER, NW><<<grid, dim3(64, NW), 0, s>>>(                                     \
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
       O, xchunk, src[0], src[1], src[2], src[3], sv,                                                       \
-      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, cp)
+      (g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1)) |          \
+          (cpml_scr_l1() << 24),                                                                           \
+      tf, gtab, cpv, pscr)
   if constexpr (FX != 0) {
     MR_LAUNCH(1, false);  // tuning variants: uniform media only
   } else {
@@ -1245,15 +1335,18 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
+// tile of the multi-step CPML passes: CPML_NW waves x CPML_R rows
+constexpr int CPML_NW = 8, CPML_R = 2;
+
 template <int T>
 int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                      float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                      float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
                      const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const CpmlDev* cp,
-                     hipStream_t s) {
+                     float* pscr, hipStream_t s) {
   // scalar lanes with 2 rows per wave: R = 4 or float2 lanes at R = 2
   // exceed 128 VGPRs and spill from T = 2 on
-#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, s
+#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, pscr, s
   if constexpr (T == 1) {
     // CPML single-step passes (hybrid shells)
     switch (fx) {
@@ -1266,6 +1359,13 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
       case 14: return launch_tb_mr<T, 1, 2, 14>(MR_ARGS);
       case 15: return launch_tb_mr<T, 1, 2, 15>(MR_ARGS);
     }
+  } else if constexpr (T <= 5) {
+    // multi-step CPML (+ TF/SF) passes over the shell boxes of a hybrid run
+    switch (fx) {
+      case 8: return launch_tb_mr<T, 1, CPML_R, 8, CPML_NW>(MR_ARGS);
+      case 12: return launch_tb_mr<T, 1, CPML_R, 12, CPML_NW>(MR_ARGS);
+    }
+    if (fx & 8) return (int)hipErrorInvalidValue;
   } else {
     if (fx & 8) return (int)hipErrorInvalidValue;
   }
@@ -1292,22 +1392,35 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
 #undef MR_ARGS
 }
 
+// automatic x chunk of a multi-row pass over output box O
+int tb_mr_xchunk(int fx, const Box3& O, int steps) {
+  const bool cpm = (fx & 8) && steps > 1;
+  const int R = cpm ? CPML_R : 2, NW = cpm ? CPML_NW : TBW;
+  const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
+  const long long gy = cdiv(O.hi[1] - O.lo[1], NW * R - 2 * steps);
+  // the 8-wave shape fits two workgroups per CU
+  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) || cpm ? 2 : 1);
+}
+
+// bytes of thread-private psi scratch a multi-step CPML pass needs (0: none)
+long long tb_mr_scratch_bytes(int fx, const Box3& O, int steps, int xchunk) {
+  if (!(fx & 8) || steps <= 1 || box_empty(O)) return 0;
+  if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
+  const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
+  const long long gy = cdiv(O.hi[1] - O.lo[1], CPML_NW * CPML_R - 2 * steps);
+  const long long gx = cdiv(O.hi[0] - O.lo[0], xchunk);
+  return 2LL * (steps - 1) * 12 * CPML_R * gz * gy * gx * CPML_NW * 64 * 4;
+}
+
 // multi-row pass (scalar lanes, 2 rows per wave): uniform media, sparse
 // per-cell coefficients (fx bits 1 / 2), TF/SF corrections (fx bit 4)
 int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                    float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                    float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, int steps,
                    const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const CpmlDev* cp,
-                   hipStream_t s) {
-  const int R = 2, V = 1;
-  if (xchunk <= 0) {
-    const int HL = (steps + V - 1) / V;
-    const long long gz = cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), (64 - 2 * HL) * V);
-    const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R - 2 * steps);
-    // the 8-wave shape fits two workgroups per CU
-    xchunk = pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) ? 2 : 1);
-  }
-#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, s
+                   float* pscr, hipStream_t s) {
+  if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
+#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, pscr, s
   switch (steps) {
     case 1: return launch_tb_mr_sel<1>(MR_ARGS);
     case 2: return launch_tb_mr_sel<2>(MR_ARGS);
@@ -1400,7 +1513,7 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   if (!pc && (MR > 1 || steps > 4)) {
     const Box3 nb = make_box(kNoBox);
     return tb_mr_dispatch(0, ein, hin, eout, hout, nullptr, nullptr, nb, nb, fcb, fdb, nx, ny, nz, b, O, xchunk,
-                          steps, src, sv, nullptr, nullptr, nullptr, s);
+                          steps, src, sv, nullptr, nullptr, nullptr, nullptr, s);
   }
   if (steps > 4) return (int)hipErrorInvalidValue;
   if (xchunk <= 0) {
@@ -1436,15 +1549,18 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
 // kind's box, and either kind whose array is null, uses the scalar ``cb`` /
 // ``db`` -- TF/SF corrections (``tf`` = device TfDev, ``gtab`` = the g
 // table of this pass's first level, from fdtd_tfsf_pass_f32; null: none) and,
-// for single-step passes, CPML (``cpml`` = device CpmlDev; null: none).
+// CPML (``cpml`` = the CpmlDev block as HOST bytes, passed by value to the
+// kernel; passes of more than one step need ``pscr``, ``pscr_bytes`` >=
+// fdtd_tb3d_cpml_scratch_bytes; null: none).
 // Other arguments as fdtd_tb3d_v4_f32.
 FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* const* eout,
                                float* const* hout, const void* ce4, const int* ebox, const void* ch4,
                                const int* hbox, double cb, double db, int nx, int ny, int nz, const int* boxes,
                                const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
-                               const void* tf, const float* gtab, const void* cpml, void* stream) {
+                               const void* tf, const float* gtab, const void* cpml, void* pscr,
+                               long long pscr_bytes, void* stream) {
   if (nz % 4 != 0 || steps < 1 || steps > 6) return (int)hipErrorInvalidValue;
-  if (cpml && steps != 1) return (int)hipErrorInvalidValue;
+  if (cpml && steps > 5) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const Box3 O = make_box(obox);
@@ -1454,10 +1570,24 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
   const int fx = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0) | (tf && gtab ? 4 : 0) |
                  (cpml ? 8 : 0);
+  if ((fx & 8) && steps > 1) {
+    // multi-step CPML: uniform media only; the caller's scratch must cover the launch
+    if (fx & 3) return (int)hipErrorInvalidValue;
+    if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
+    if (!pscr || pscr_bytes < tb_mr_scratch_bytes(fx, O, steps, xchunk) ||
+        tb_mr_scratch_bytes(fx, O, steps, xchunk) > 0xFFFFFFFFLL)
+      return (int)hipErrorInvalidValue;
+  }
   return tb_mr_dispatch(fx, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
                         (const float4*)(box_empty(BH) ? nullptr : ch4), BE, BH, (float)cb, (float)db, nx, ny, nz, b,
-                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, (const CpmlDev*)cpml,
+                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, (const CpmlDev*)cpml, (float*)pscr,
                         (hipStream_t)stream);
+}
+
+// scratch bytes fdtd_tb3d_ext_f32 needs for a CPML pass of ``steps`` steps
+// over output box ``obox`` (TF/SF on or off; 0 for single-step passes)
+FDTD_API long long fdtd_tb3d_cpml_scratch_bytes(const int* obox, int xchunk, int steps, int tfsf) {
+  return tb_mr_scratch_bytes(8 | (tfsf ? 4 : 0), make_box(obox), steps, xchunk);
 }
 
 // size of the CpmlDev block the host fills (ABI check)

@@ -55,6 +55,10 @@ F32_AUTO_STEPS_PERCELL_BOTH = 2
 F32_AUTO_STEPS_TFSF = 4
 
 
+# hybrid_shell modes that take the blocked shell (_hybrid3_plan) when the run fits it
+BLOCKED_SHELL_MODES = ("blocked",)
+
+
 def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: int = 1, tfsf: bool = False) -> int:
     """Steps per pass of a plain (no PML / TF-SF / dispersion) run in
     automatic mode -- ONE rule for the serial scheme, the decomposed driver
@@ -275,6 +279,13 @@ class BlockedStepping:
                 return
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
                 return
+        if self._hybrid3_ok():
+            plan = self._hybrid3_plan(H)
+            if plan is not None:
+                if not hasattr(self, "F_alt"):
+                    self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+                self.hybrid = plan
+                return
         if self._hybrid2_ok() and self._hybrid2_regions():
             plan = self._hybrid2_plan(H)
             if plan is None:
@@ -299,6 +310,104 @@ class BlockedStepping:
         if not hasattr(self, "F_alt"):
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
         self.hybrid = plan
+
+    # ------------------------------------------------ hybrid, blocked shell
+    def _hybrid3_ok(self) -> bool:
+        """Runs whose shell takes blocked passes too (``hybrid_shell`` auto or
+        blocked): serial fp32 3D HIP runs with CPML absorbing layers and / or
+        TF/SF plane waves along x or y (in-kernel TfsfSets), uniform media.
+        The CPML variant of the blocked kernel carries psi through the pass's
+        levels (csrc/yee3d_tb.hip, thread-private hand-off)."""
+        cfg = self.cfg
+        mode = getattr(cfg, "hybrid_shell", "auto")
+        if mode not in BLOCKED_SHELL_MODES or self.ops.name != "hip" or not hasattr(self.ops, "tb_step"):
+            return False
+        if cfg.scheme != "3d" or self.halo is not None or cfg.use_amp_mode or cfg.use_metamaterials:
+            return False
+        if self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0:
+            return False
+        if cfg.use_pml and (not self.use_cpml or self.use_upml_chain):
+            return False
+        if cfg.use_tfsf and getattr(self, "tfsf_sets", None) is None:
+            return False
+        if not (self.use_cpml or cfg.use_tfsf):
+            return False
+        return not any(getattr(self.cb[c], "cell", None) is not None for c in self.comps)
+
+    def _hybrid3_plan(self, T: int):
+        """Every cell advances ``T`` steps per pass in ONE blocked launch per
+        box, all reading ``F`` and writing ``F_alt``: the plain kernel on the
+        core (cells at least ``T + 1`` -- ``T + 2`` when staggering needs it --
+        from every CPML slab cell and TF/SF target, so its dependency cone
+        holds only plain cells) and the CPML + TF/SF variant on the six shell
+        boxes around it.  No stepped band, no shell copy: a shell box's cone
+        reaches into the core, where the variant's update is the plain one."""
+        cfg = self.cfg
+        size = cfg.size
+        dom = self.domain
+        alloc = dom.allocated_global()
+
+        def grow(b, n):
+            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
+
+        K = None
+        for m in (T + 1, T + 2):
+            lo, hi = [0, 0, 0], list(size)
+            for a in range(3):
+                edge = 0
+                if cfg.use_pml:
+                    edge = max(edge, self.layout.pml_size[a])
+                if cfg.use_tfsf:
+                    edge = max(edge, cfg.tfsf_size[a] + 1)
+                if edge > 0:
+                    lo[a], hi[a] = edge + m, size[a] - edge - m
+            cand = (tuple(lo), tuple(hi))
+            if box_empty(cand):
+                return None
+            g = grow(cand, T + 1)
+            if self.use_cpml and any(not box_empty(box_intersect(g, sl.gbox))
+                                     for slabs in self.cpml.slabs.values() for sl in slabs):
+                continue
+            if cfg.use_tfsf and self._tfsf_targets_in(dom.to_local(g)):
+                continue
+            K = cand
+            break
+        if K is None:
+            return None
+        shell = [dom.to_local(b) for b in box_subtract(alloc, K) if not box_empty(b)]
+        upd = {c: self.local_box(c, alloc) for c in self.comps}
+        return {"T": T, "v3": True, "core": [dom.to_local(K)], "shell": shell, "upd": upd,
+                "core_cells": box_volume(K)}
+
+    def _hybrid3_step(self, T: int) -> None:
+        hp = self.hybrid
+        if T != hp["T"]:
+            tails = self.__dict__.setdefault("_hybrid3_tails", {})
+            if T not in tails:
+                tails[T] = self._hybrid3_plan(T)
+            hp = tails[T]
+            if hp is None:
+                for _ in range(T):
+                    self.step()
+                return
+        srcs = self._pass_sources(self.t, T)
+        for p in range(self.planes):
+            tf = self._tfsf_pass(p, T)
+            cp = self.cpml.host_table(p) if self.use_cpml else None
+            P, Q = self.F[p], self.F_alt[p]
+            with self.prof.phase("blocked-core"):
+                for ob in hp["core"]:
+                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p])
+            with self.prof.phase("blocked-shell"):
+                for ob in hp["shell"]:
+                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf, cpml=cp)
+            if self.use_cpml:
+                self.cpml.flip(p)
+            self.F[p], self.F_alt[p] = Q, P
+        self.t += T
+        if self.cfg.check_finite and (self.t // max(1, self.cfg.finite_check_step)
+                                      != (self.t - T) // max(1, self.cfg.finite_check_step)):
+            self.check_finite()
 
     # ------------------------------------------------ hybrid, single-pass shell
     def _hybrid2_ok(self) -> bool:
@@ -752,6 +861,9 @@ class BlockedStepping:
         return srcs
 
     def _hybrid_step(self, T: int) -> None:
+        if self.hybrid.get("v3"):
+            self._hybrid3_step(T)
+            return
         if self.hybrid.get("v2"):
             self._hybrid2_step(T)
             return

@@ -562,7 +562,13 @@ class YeeScheme(BlockedStepping):
                 else:
                     w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
                     active = (w != 0) | (g != 0)
-                    if not bool(active.any()):
+                    local = bool(active.any())
+                    # decomposed: a rank without dispersive cells of c still
+                    # keeps the dispersive state arrays when another rank has
+                    # some (every rank must exchange the same message list)
+                    if self.halo is not None:
+                        local = self.halo.allreduce_max(1.0 if local else 0.0) > 0
+                    if not local:
                         active = None
                 if active is not None:
                     st["nlev"] = 3

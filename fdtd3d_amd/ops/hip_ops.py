@@ -761,11 +761,20 @@ class HipOps:
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
         if tfsf is not None and self.dtype != torch.float32:
             raise HipError("in-kernel TF/SF: fp32 only")
+        pscr, pscr_bytes = None, 0
         if cpml is not None:
-            if self.dtype != torch.float32 or steps != 1:
-                raise HipError("in-kernel CPML: fp32 single-step passes")
-            if int(self.lib.fdtd_cpmldev_size()) != cpml.numel():
-                raise HipError("CpmlDev layout mismatch")
+            if self.dtype != torch.float32 or steps > 5:
+                raise HipError("in-kernel CPML: fp32, at most 5 steps per pass")
+            if int(self.lib.fdtd_cpmldev_size()) != cpml.numel() or cpml.device.type != "cpu":
+                raise HipError("cpml: the CpmlDev block as host bytes (CPML.host_table)")
+            if steps > 1:
+                if percell:
+                    raise HipError("multi-step CPML passes: uniform media only")
+                # thread-private psi hand-off between the pass's levels
+                f = self.lib.fdtd_tb3d_cpml_scratch_bytes
+                f.restype = ctypes.c_longlong
+                pscr_bytes = int(f(_box_arr([obox]), c_int(self.tb_xchunk), c_int(steps), c_int(tfsf is not None)))
+                pscr = self._scratch(pscr_bytes)
         if (percell and self.dtype == torch.float32 and self.tb_sparse) or tfsf is not None or cpml is not None:
             # multi-row kernel with sparse per-cell coefficients / TF/SF sets
             if percell and steps > 5:
@@ -785,7 +794,8 @@ class HipOps:
                 arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), _ptr(ce), _box_arr([ebox]), _ptr(ch),
                 _box_arr([hbox]), c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk), c_int(steps),
-                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _ptr(cpml), _stream())
+                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _ptr(cpml), _ptr(pscr),
+                ctypes.c_longlong(pscr_bytes), _stream())
             _check(rc, "tb3d_ext")
             self.launches += 1
             return
@@ -810,6 +820,16 @@ class HipOps:
                                 c_int(steps), (c_int * 4)(*src), (c_double * 8)(*vals), _stream())
         _check(rc, "tb3d")
         self.launches += 1
+
+    def _scratch(self, nbytes: int) -> Optional[torch.Tensor]:
+        """Device scratch of at least ``nbytes`` bytes, reused by every launch
+        on this ops object (stream-ordered: launches of one stream only)."""
+        if nbytes <= 0:
+            return None
+        buf = getattr(self, "_scr", None)
+        if buf is None or buf.numel() * 4 < nbytes:
+            buf = self._scr = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=self.device)
+        return buf
 
     shell_ok = True  # fused single-step shell kernel (yee3d_shell.hip) present
 

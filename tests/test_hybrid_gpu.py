@@ -160,3 +160,39 @@ def test_hybrid_at_scale(gpu, name, extra):
         del scale
     del runs, hy, st
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("T,tfsf,point,size", [(5, True, False, (96, 88, 96)), (4, True, True, (80, 72, 96)),
+                                               (3, False, True, (72, 80, 64)), (2, True, False, (64, 64, 128)),
+                                               (5, False, True, (112, 96, 100))])
+def test_hybrid3_blocked_shell(gpu, T, tfsf, point, size):
+    """Blocked shell (every box one T-step launch: the CPML + TF/SF variant
+    of the multi-row kernel carries psi through the pass's levels) vs the
+    stepped run, from random fields so every slab carries field from step 1;
+    2T + 1 steps = two passes and a one-step tail."""
+    cfg = SchemeConfig(time_steps=2 * T + 1, scheme="3d", size=size, dtype="f32", pml_size=(5, 6, 7),
+                       tfsf_size=(9, 10, 11), scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=tfsf,
+                       hybrid_shell="blocked")
+    if point:
+        cfg = dataclasses.replace(cfg, use_point_source=True)
+    runs = {}
+    for hb in (T, 1):
+        s = YeeScheme(dataclasses.replace(cfg, hybrid_block=hb), make_ops("hip", None, gpu, torch.float32))
+        s.init_scheme()
+        s.init_grids()
+        s.randomize_fields(seed=11)
+        s.perform_steps()
+        torch.cuda.synchronize()
+        runs[hb] = s
+    hy, st = runs[T], runs[1]
+    assert hy.hybrid is not None and hy.hybrid.get("v3"), "blocked shell not selected"
+    assert st.hybrid is None
+    for c in hy.comps:
+        x, y = hy.F[0][c].double().cpu(), st.F[0][c].double().cpu()
+        scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])
+        assert float((x - y).abs().max()) <= 2e-5 * scale, (c, float((x - y).abs().max()), scale)
+        src_scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] != c[0])
+        for a, b in zip(hy.cpml.slabs[c], st.cpml.slabs[c]):
+            err = float((a.psi[0].double() - b.psi[0].double()).abs().max())
+            assert err <= 2e-5 * src_scale, (c, "psi", err, src_scale)
+        assert max(float(b.psi[0].abs().max()) for b in st.cpml.slabs[c]) > 1e-3 * src_scale  # psi is live

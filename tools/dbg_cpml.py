@@ -34,7 +34,7 @@ b.F_alt = [{c: torch.zeros_like(b.F[0][c]) for c in b.comps}]
 a.step()
 alloc = b.domain.allocated_global()
 upd = {c: b.local_box(c, alloc) for c in b.comps}
-b.ops.tb_step(b.F[0], b.F_alt[0], upd, ((0, 0, 0), cfg.size), b.cb, 1, None, cpml=b.cpml.device_table(0))
+b.ops.tb_step(b.F[0], b.F_alt[0], upd, ((0, 0, 0), cfg.size), b.cb, 1, None, cpml=b.cpml.host_table(0))
 torch.cuda.synchronize()
 for c in a.comps:
     d = (a.F[0][c] - b.F_alt[0][c]).double().cpu()

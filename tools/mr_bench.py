@@ -37,7 +37,7 @@ def main():
     wins = {"whole": whole, "xwin": ((0, 0, 0), (t, n, n)), "ywin": ((t, 0, 0), (n - t, t, n)),
             "zwin": ((t, t, 0), (n - t, n - t, t)), "core": ((16, 16, 16), (n - 16, n - 16, n - 16))}
     g = s._tfsf_pass(0, 5)
-    cp = s.cpml.device_table(0)
+    cp = s.cpml.host_table(0)
     cases = []
     for T in (1, 4):
         for name, box in wins.items():
