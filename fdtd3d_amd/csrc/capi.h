@@ -74,7 +74,7 @@ int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* c
                       const void* ce4, const int* ebox, const void* ch4, const int* hbox, double cb, double db,
                       int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk, int steps,
                       const int* src, const double* src_vals, const void* tf, const float* gtab, const void* cpml,
-                      void* pscr, long long pscr_bytes, void* stream);
+                      int cpml_axes, void* pscr, long long pscr_bytes, void* stream);
 long long fdtd_tb3d_cpml_scratch_bytes(const int* obox, int xchunk, int steps, int tfsf);
 int fdtd_tfdev_size();
 int fdtd_cpmldev_size();

@@ -1,0 +1,1041 @@
+// Multi-row temporally blocked fp32 3D Yee kernel (k_tb3d_mr) and its
+// launcher, shared by yee3d_tb.hip (plain / TF-SF / sparse per-cell variants,
+// the host API) and yee3d_tb_cpml.hip (the multi-step CPML variants, a
+// translation unit of their own so the two compile in parallel).
+#pragma once
+
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+
+namespace tb3d {
+
+constexpr int TBW = 16;  // waves (y rows) per workgroup
+
+template <int V>
+struct VT;
+template <>
+struct VT<1> {
+  typedef float f __attribute__((ext_vector_type(1)));
+  typedef unsigned u __attribute__((ext_vector_type(1)));
+};
+template <>
+struct VT<2> {
+  typedef float f __attribute__((ext_vector_type(2)));
+  typedef unsigned u __attribute__((ext_vector_type(2)));
+};
+template <>
+struct VT<4> {
+  typedef float f __attribute__((ext_vector_type(4)));
+  typedef unsigned u __attribute__((ext_vector_type(4)));
+};
+
+// neighbour lanes through DPP wave shifts (one VALU op, usually folded into
+// the consuming v_sub as a _dpp modifier) instead of ds_bpermute round trips
+// through the LDS pipe: lane_up(v) on lane i = v of lane i-1 (wave_shr:1),
+// lane_dn(v) = v of lane i+1 (wave_shl:1); lanes shifted in from outside the
+// wave read 0 -- they are halo lanes of every tile.
+__device__ __forceinline__ float lane_up(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_dn(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
+
+struct TbSrc {
+  float v[8];  // hard-source value applied after E update of level l
+};
+
+// TF/SF plane-wave corrections folded into the blocked passes (fdtd3d_amd/
+// models/tfsf.py TfsfSets).  A set is one (component, TF/SF face) pair of the
+// reference's border tests (Scheme3D.cpp:138-208, YeeGridLayout.cpp:327-809):
+// a box of target cells, one cell thick across the face.  For an incident
+// direction along x or y the incident value a target sees depends on its
+// index along that axis only (`va`), so each pass precomputes, per level,
+// g = sign * projection * interpolated incident line at every index of a set
+// (k_tfsf_pass below) and the kernels add g to the target's curl before the
+// coefficient multiply -- from SCALAR loads (wave-uniform index), which do not
+// queue behind the vector prefetch.
+constexpr int TF_MAX_SETS = 24;
+struct TfSet {
+  int n;          // component 0..5 = Ex Ey Ez Hx Hy Hz
+  int fa;         // axis the face is perpendicular to
+  int lo[3], hi[3];
+  int va;         // table axis (0 x, 1 y)
+  int goff;       // first g entry of the set inside one level
+};
+// CPML convolution terms (fdtd3d_amd/models/cpml.py, layout of
+// yee3d_cpml.hip): per (component, term axis) the low / high psi slabs, their
+// ranges along the axis and the b / c / (1/kappa - 1) profiles (identity
+// outside the slabs).  psi index of a slab along x: ((i-lo) ny + j) nz + k;
+// along y: (i w + j-lo) nz + k; along z: (i ny + j) w + k-lo (w = hi - lo).
+struct CpmlTerm {
+  const float* psi[2];  // read (time n) ...
+  float* out[2];        // ... and written (time n + 1): ping-pong, because the
+                        // halo cells a tile recomputes belong to neighbour tiles
+                        // that may already have advanced them
+  int lo[2], hi[2];
+  const float* b;
+  const float* c;
+  const float* k;
+};
+struct CpmlDev {
+  CpmlTerm t[6][3];  // [Ex Ey Ez Hx Hy Hz][term axis]
+};
+// curl terms of each component: (axis, sign), Ex = +dHz/dy - dHy/dz etc.
+__device__ constexpr int kTermAxis[6][2] = {{1, 2}, {2, 0}, {0, 1}, {2, 1}, {0, 2}, {1, 0}};
+
+// the CPML table travels by value in the kernel arguments: its pointers and
+// profile reads are then wave-uniform scalar loads from the kernarg segment --
+// SGPR descriptors, no waterfall loop, and profile loads that wait on the
+// scalar counter instead of queueing behind the vector prefetch (a copy in
+// LDS, or any generic-pointer view of the argument, hands every field back in
+// VGPRs).  The non-CPML variants carry it unread.
+
+struct TfDev {
+  int nsets;
+  int ld;                   // g entries per level
+  int xpl[2][2];            // [E / H][low / high] x-face planes (-1: none)
+  TfSet s[TF_MAX_SETS];
+};
+
+// Memory access through buffer descriptors: one descriptor per (array, x
+// plane) built in SGPRs from the wave-uniform plane index, plus ONE 32-bit
+// per-lane byte offset shared by every array (buffer_load ... offen).  Flat
+// 64-bit addressing would keep a per-lane pointer per array live across the
+// x loop (24 VGPRs for 12 arrays) and spill.  Offsets past the descriptor's
+// size read 0 / drop the store, which is how rows and planes outside the
+// array are handled -- no per-lane load guards.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+// wave-uniform read of a table the kernel never writes, through the constant
+// address space: a scalar load (s_load, lgkm counter) -- a plain global load
+// of the same uniform address is a vector load that waits behind the plane
+// prefetch
+__device__ __forceinline__ float cload(const float* p, int i) {
+  return ((const __attribute__((address_space(4))) float*)p)[i];
+}
+
+__device__ __forceinline__ Rsrc plane_rsrc(const float* base, int x, int nx, size_t plane) {
+  const bool in = x >= 0 && x < nx;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)(in ? x : 0) * plane), (short)0,
+                                           in ? (int)(plane * 4) : 0, 0x00020000);
+}
+
+template <int V>
+__device__ __forceinline__ typename VT<V>::f bld(Rsrc r, unsigned boff) {
+  if constexpr (V == 1)
+    return __builtin_bit_cast(typename VT<1>::f, __builtin_amdgcn_raw_buffer_load_b32(r, boff, 0, 0));
+  else if constexpr (V == 4)
+    return __builtin_bit_cast(typename VT<4>::f, __builtin_amdgcn_raw_buffer_load_b128(r, boff, 0, 0));
+  else
+    return __builtin_bit_cast(typename VT<2>::f, __builtin_amdgcn_raw_buffer_load_b64(r, boff, 0, 0));
+}
+
+template <int V>
+__device__ __forceinline__ void bst(Rsrc r, unsigned boff, const typename VT<V>::f& v, unsigned mask) {
+  if (mask == (1u << V) - 1u) {
+    if constexpr (V == 1)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[0]), r, boff, 0, 0);
+    else if constexpr (V == 4)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(typename VT<4>::u, v), r, boff, 0, 0);
+    else
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(typename VT<2>::u, v), r, boff, 0, 0);
+  } else if (V > 1 && mask) {
+    // the b32 builtin takes the raw bits (an implicit float->uint would convert)
+#pragma unroll
+    for (int q = 0; q < V; ++q)
+      if (mask & (1u << q)) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), r, boff + 4 * q, 0, 0);
+  }
+}
+
+// one unsigned compare (2 SALU) instead of two compares and an AND
+__device__ __forceinline__ bool xin(const Box3& b, int x) {
+  return (unsigned)(x - b.lo[0]) < (unsigned)(b.hi[0] - b.lo[0]);
+}
+
+// bit q set when element q of the lane's V-group (cells kb..kb+V-1) is in the box
+template <int V>
+__device__ __forceinline__ unsigned kmaskv(const Box3& b, int j, int kb) {
+  if (j < b.lo[1] || j >= b.hi[1]) return 0u;
+  unsigned m = 0;
+#pragma unroll
+  for (int e = 0; e < V; ++e) m |= ((kb + e >= b.lo[2]) && (kb + e < b.hi[2])) ? (1u << e) : 0u;
+  return m;
+}
+
+// elements of c whose bit is set in m, zero elsewhere
+template <int V>
+__device__ __forceinline__ typename VT<V>::f cmask(typename VT<V>::f c, unsigned m) {
+#pragma unroll
+  for (int q = 0; q < V; ++q) c[q] = (m & (1u << q)) ? c[q] : 0.f;
+  return c;
+}
+
+// z-1 / z+1 neighbours of a lane's V cells (s = the cell beyond the group)
+template <int V>
+__device__ __forceinline__ typename VT<V>::f zm1(const typename VT<V>::f& v, float s) {
+  typename VT<V>::f r;
+  r[0] = s;
+#pragma unroll
+  for (int q = 1; q < V; ++q) r[q] = v[q - 1];
+  return r;
+}
+template <int V>
+__device__ __forceinline__ typename VT<V>::f zp1(const typename VT<V>::f& v, float s) {
+  typename VT<V>::f r;
+#pragma unroll
+  for (int q = 0; q < V - 1; ++q) r[q] = v[q + 1];
+  r[V - 1] = s;
+  return r;
+}
+
+template <int V>
+struct F3 {
+  typename VT<V>::f x, y, z;
+};
+
+// ---------------------------------------------------------------------------
+// Multi-row variant: every wave carries R ADJACENT y rows in registers (rows
+// R*w .. R*w+R-1 of the tile), so one workgroup spans 16R rows and the 2T
+// redundant halo rows are amortised over 16R instead of 16 (T=4: 8 of 16 rows
+// owned by the single-row kernel, 24 of 32 at R=2).  y neighbours inside a
+// wave's row group are registers; only the first / last row of the group goes
+// through LDS (the same 4 fields x 16 slots as above, one barrier per level).
+// Scalar lanes (V=1) keep the register footprint of the float2 single-row
+// kernel; the extra z halo lanes (T per side) cost less than the y rows saved.
+// Masks of the 7 boxes (6 update boxes + output box) for every row are packed
+// into one bit field (R*V <= 4).
+// PFD: planes loaded ahead (1 or 2).  DEFER: the results of plane X are
+// stored after plane X+1's prefetch is issued -- vmcnt counts loads and
+// stores together in issue order, so stores issued between two prefetches
+// would otherwise be waited for with the older prefetch.
+template <int T, int V, int R, int FX, int PFD, bool DEFER, int NW>
+__global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
+    const float* __restrict__ exi, const float* __restrict__ eyi, const float* __restrict__ ezi,
+    const float* __restrict__ hxi, const float* __restrict__ hyi, const float* __restrict__ hzi,
+    float* __restrict__ exo, float* __restrict__ eyo, float* __restrict__ ezo,
+    float* __restrict__ hxo, float* __restrict__ hyo, float* __restrict__ hzo,
+    const float4* __restrict__ ce4, const float4* __restrict__ ch4, Box3 BE, Box3 BH, float cb,
+    float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
+    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz,
+    const TfDev* __restrict__ tf, const float* __restrict__ gtab, const CpmlDev CP,
+    float* __restrict__ pscr) {
+  // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF,
+  // 8 / 16 / 32 CPML terms along x / y / z (a launch over a shell box carries
+  // only the axes whose slabs its dependency cone reaches).  A CPML pass of
+  // T > 1 steps hands each level's psi to the next level through `pscr`,
+  // thread-private scratch (see the level loop)
+  constexpr int PC = FX & 3;
+  constexpr bool TFS = FX & 4;
+  constexpr int CAX = (FX >> 3) & 7;
+  constexpr bool CPM = CAX != 0;
+  static_assert(V == 1 || !FX, "sparse coefficients / TF/SF: scalar lanes");
+  constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
+  static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
+  typedef typename VT<V>::f vec;
+  constexpr int HL = (T + V - 1) / V;   // halo lanes per side
+  constexpr int TBZ = (64 - 2 * HL) * V; // owned z cells per tile
+  constexpr int ROWS = NW * R;         // y rows per workgroup
+  constexpr unsigned VM = (1u << V) - 1u;
+  __shared__ vec sX[2][4][NW][64];
+  const int lane = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);  // one wave per y (SGPR)
+  // the TF/SF table lives in LDS for the kernel's life: its fields are read in
+  // many branches (with dynamic set indices)
+  __shared__ unsigned sTFraw[TFS ? sizeof(TfDev) / 4 : 1];
+  if constexpr (TFS) {
+    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(TfDev) / 4); q += 64 * NW)
+      sTFraw[q] = ((const unsigned*)tf)[q];
+  }
+  if constexpr (TFS) __syncthreads();
+  const TfDev& TF = *reinterpret_cast<const TfDev*>(sTFraw);
+
+  // Tile of this workgroup.  A row of a tile starts at an arbitrary z (the
+  // stride is the 64 - 2T owned cells), so its 64 cells straddle three
+  // 128-B lines, one shared with each z neighbour tile.  Workgroups are dealt
+  // round-robin to the 8 XCDs (own L2 each); with xcd_swz each XCD instead
+  // gets a contiguous run of tiles, z fastest, so z neighbours run together
+  // on one L2 and the shared lines are fetched from HBM once.
+  int tz = blockIdx.x, ty = blockIdx.y, tx = blockIdx.z;
+  if (xcd_swz & 1) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy * (int)gridDim.z;
+    const int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int n8 = n & ~7;
+    const int q = p < n8 ? (p & 7) * (n8 >> 3) + (p >> 3) : p;
+    const int pz = (xcd_swz >> 8) & 0xff, py = (xcd_swz >> 16) & 0xff;
+    if (pz > 0 && py > 0) {
+      // patch order: an XCD's run of tiles is dealt in PZ x PY (z x y)
+      // patches, so the ~32 workgroups one XCD holds at a time form a compact
+      // block whose y AND z neighbours stream the same planes on the same L2
+      // (a tile shares 2T of its rows with each y neighbour, 2T lanes with
+      // each z neighbour).  Bands of PY tile rows; the last band and the last
+      // patch of a band may be narrower.
+      tx = q / (gx * gy);
+      const int r = q - tx * gx * gy;
+      const int band = r / (py * gx);
+      const int h = min(py, gy - band * py);
+      const int rb = r - band * py * gx;
+      const int col = rb / (pz * h);
+      const int wdt = min(pz, gx - col * pz);
+      const int e = rb - col * pz * h;
+      tz = col * pz + e % wdt;
+      ty = band * py + e / wdt;
+    } else {
+      tz = q % gx;
+      ty = (q / gx) % gy;
+      tx = q / (gx * gy);
+    }
+  }
+  const int kb = (O.lo[2] & ~(V - 1)) - HL * V + TBZ * tz + V * lane;
+  const int jw = O.lo[1] - T + (ROWS - 2 * T) * ty + R * w;  // first row of this wave
+  const int i0 = O.lo[0] + tx * xchunk;
+  const int i1 = min(i0 + xchunk, O.hi[0]);
+  const bool kin = kb >= 0 && kb < nz;
+  const bool lane_own = lane >= HL && lane < 64 - HL;
+  const size_t plane = (size_t)ny * nz;
+  unsigned roff[R];
+  unsigned mbits = 0;  // bit (r*7 + n)*V + q: cell q of row r inside box n
+  const Box3* bx[7] = {&bex, &bey, &bez, &bhx, &bhy, &bhz, &O};
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = jw + r;
+    const int t = R * w + r;
+    const bool ld_ok = kin && j >= 0 && j < ny;
+    roff[r] = ld_ok ? (unsigned)(j * nz + kb) * 4u : 0xF0000000u;
+    const bool own = ld_ok && lane_own && t >= T && t < ROWS - T;
+#pragma unroll
+    for (int n = 0; n < 7; ++n) {
+      const bool ok = n < 6 ? ld_ok : own;
+      mbits |= (ok ? kmaskv<V>(*bx[n], j, kb) : 0u) << ((r * 7 + n) * V);
+    }
+  }
+  const int rdn = w > 0 ? w - 1 : 0;
+  const int rup = w < NW - 1 ? w + 1 : NW - 1;
+  const vec zero = (vec)(0.f);
+  const vec cbv = (vec)(cb), dbv = (vec)(db);
+  // Tiles whose every lane and row lies inside all six update boxes in y / z
+  // (all but the tiles on the domain's y / z border) run a copy of the whole
+  // x loop in which a coefficient is just the x-range-selected scalar -- no
+  // per-element mask extraction and select (3 VALU per coefficient, ~40% of
+  // the kernel's VALU work).  The copy is of the OUTER loop, so the two
+  // versions never hold registers at the same time.
+  unsigned upd_bits = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) upd_bits |= ((1u << (6 * V)) - 1u) << (r * 7 * V);
+  const bool tile_all = __all((mbits & upd_bits) == upd_bits);
+
+  // Sparse per-cell coefficients (PC): the cells whose coefficient differs
+  // from the kind's scalar lie in a box (BE for E, BH for H) and the three
+  // components' values are one float4 per cell of that box (.w unused).  Each
+  // trip loads, for every level, one 12-byte vector per kind and row -- only
+  // on planes and waves that cross the box (wave-uniform tests), everything
+  // else runs on the scalar -- and issues those loads BEFORE the next plane's
+  // field prefetch: vmcnt retires loads in issue order, so a coefficient load
+  // issued after the prefetch would make its level wait for the prefetch too.
+  // Lanes outside the box in y / z read at an offset past the plane (0) and
+  // select the scalar.
+  unsigned eoff[R], hoff[R];
+  unsigned inb = 0;  // bit r: row r of this lane inside BE (y, z); bit R + r: inside BH
+  const int bez_n = BE.hi[2] - BE.lo[2], bhz_n = BH.hi[2] - BH.lo[2];
+  const size_t eplane = (size_t)(BE.hi[1] - BE.lo[1]) * bez_n * 16u;
+  const size_t hplane = (size_t)(BH.hi[1] - BH.lo[1]) * bhz_n * 16u;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = jw + r;
+    const bool ie = PCE && kin && j >= BE.lo[1] && j < BE.hi[1] && kb >= BE.lo[2] && kb < BE.hi[2];
+    const bool ih = PCH && kin && j >= BH.lo[1] && j < BH.hi[1] && kb >= BH.lo[2] && kb < BH.hi[2];
+    eoff[r] = ie ? (unsigned)((j - BE.lo[1]) * bez_n + (kb - BE.lo[2])) * 16u : 0xF0000000u;
+    hoff[r] = ih ? (unsigned)((j - BH.lo[1]) * bhz_n + (kb - BH.lo[2])) * 16u : 0xF0000000u;
+    inb |= (ie ? 1u : 0u) << r;
+    inb |= (ih ? 1u : 0u) << (R + r);
+  }
+  const bool wave_e = PCE && __any(inb & ((1u << R) - 1u));
+  const bool wave_h = PCH && __any(inb >> R);
+  // TF/SF.  x-face sets (one plane each, all rows / lanes of the TF box) are
+  // rare per wave and go through scalar loads when a level hits their plane.
+  // y / z-face sets (one row or one lane column) touch few waves but every
+  // level of every trip of those waves, so each wave parks up to TF_SLOTS of
+  // them per kind in slots: slot metadata in VGPR lanes (read back with
+  // readlane at a compile-time lane), a per-lane bit per (slot, row) for the
+  // cells it covers, and per trip ONE vector load of the g values of every
+  // (slot, level, row) -- issued before the field prefetch, so the levels
+  // never wait behind it.
+  constexpr int TF_SLOTS = 6;                      // per kind
+  constexpr int TF_ENT = 2 * TF_SLOTS * T * R;     // g entries per trip (<= 128 for T <= 5)
+  static_assert(!TFS || TF_ENT <= 128, "TF/SF: at most 5 steps per pass");
+  unsigned tf_wx[2] = {0u, 0u};
+  unsigned tf_ov[2] = {0u, 0u};  // face sets beyond the slots: the scalar path every level
+  int tf_xe0 = -1, tf_xe1 = -1, tf_xh0 = -1, tf_xh1 = -1;  // x-face planes (E / H sets)
+  int tf_na0 = 0, tf_na1 = 0;                      // slots in use (E / H)
+  unsigned tf_lbits = 0;                           // bit slot * R + r: this lane in the slot's set, row r
+  int tf_mx = 0;                                   // lane s: x range of slot s (lo | hi << 16)
+  int tf_mn = 0;                                   // lane s: component of slot s
+  int tf_gb0 = 0, tf_gb1 = 0;                      // g index of entry lane / lane + 64 (plus X when va = 0)
+  bool tf_ok0 = false, tf_ok1 = false;
+  int tf_va = 0, tf_ld = 0;
+  if constexpr (TFS) {
+    const int ns = TF.nsets;
+    const int ld = TF.ld;
+    tf_ld = ld;
+    tf_va = TF.s[0].va;
+    int na[2] = {0, 0};
+    for (int si = 0; si < ns; ++si) {
+      const TfSet& S = TF.s[si];
+      unsigned rb = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int j = jw + r;
+        rb |= (kin && j >= S.lo[1] && j < S.hi[1] && kb >= S.lo[2] && kb < S.hi[2]) ? (1u << r) : 0u;
+      }
+      if (!__any(rb != 0u)) continue;
+      const int k = S.n < 3 ? 0 : 1;
+      if (S.fa == 0) {
+        tf_wx[0] |= k == 0 ? (1u << si) : 0u;
+        tf_wx[1] |= k == 1 ? (1u << si) : 0u;
+        continue;
+      }
+      const int a = k == 0 ? na[0] : na[1];
+      if (a >= TF_SLOTS) {
+        tf_ov[0] |= k == 0 ? (1u << si) : 0u;
+        tf_ov[1] |= k == 1 ? (1u << si) : 0u;
+        continue;
+      }
+      const int slot = k * TF_SLOTS + a;
+      if (k == 0) ++na[0]; else ++na[1];
+      tf_lbits |= rb << (slot * R);
+      if (lane == slot) {
+        tf_mx = S.lo[0] | (S.hi[0] << 16);
+        tf_mn = S.n;
+      }
+      // entries (slot, l, r) -> entry q = (slot * T + l) * R + r
+#pragma unroll
+      for (int l = 0; l < T; ++l)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int q = (slot * T + l) * R + r;
+          // level l: E sets on plane X - l, H sets on X - l - 1
+          const int base = l * ld + S.goff + (S.va == 0 ? -S.lo[0] - l - k : (jw + r) - S.lo[1]);
+          if (lane == q) { tf_gb0 = base; tf_ok0 = true; }
+          if (lane + 64 == q) { tf_gb1 = base; tf_ok1 = true; }
+        }
+    }
+    tf_na0 = na[0];
+    tf_na1 = na[1];
+    tf_xe0 = TF.xpl[0][0];
+    tf_xe1 = TF.xpl[0][1];
+    tf_xh0 = TF.xpl[1][0];
+    tf_xh1 = TF.xpl[1][1];
+  }
+  const bool tf_slots = TFS && (tf_na0 + tf_na1) > 0;
+  float tf_g0 = 0.f, tf_g1 = 0.f;  // this trip's g entries (lane q, q + 64)
+  // add the TF/SF corrections of kind k at level l, plane p, row r to the curls
+  auto tf_apply = [&](int k, int l, int p, int r, vec& c0, vec& c1, vec& c2) {
+    if constexpr (TFS) {
+      // y / z-face slots
+      if (tf_slots) {
+#pragma unroll
+        for (int a = 0; a < TF_SLOTS; ++a) {
+          if (a >= (k == 0 ? tf_na0 : tf_na1)) break;
+          const int slot = k * TF_SLOTS + a;
+          const int xr = __builtin_amdgcn_readlane(tf_mx, slot);
+          if ((unsigned)(p - (xr & 0xffff)) >= (unsigned)((xr >> 16) - (xr & 0xffff))) continue;
+          const int q = (slot * T + l) * R + r;
+          const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q < 64 ? tf_g0 : tf_g1), q & 63));
+          const float gl = ((tf_lbits >> (slot * R + r)) & 1u) ? g : 0.f;
+          const int c = __builtin_amdgcn_readlane(tf_mn, slot) - 3 * k;
+          c0 = c0 + (vec)(c == 0 ? gl : 0.f);
+          c1 = c1 + (vec)(c == 1 ? gl : 0.f);
+          c2 = c2 + (vec)(c == 2 ? gl : 0.f);
+        }
+      }
+      // x-face sets on their plane
+      const bool xp = k == 0 ? (p == tf_xe0 || p == tf_xe1) : (p == tf_xh0 || p == tf_xh1);
+      unsigned cand = (xp ? (k == 0 ? tf_wx[0] : tf_wx[1]) : 0u) | (k == 0 ? tf_ov[0] : tf_ov[1]);
+      const int j = jw + r;
+      while (cand) {
+        const int si = __builtin_ctz(cand);
+        cand &= cand - 1u;
+        const TfSet& S = TF.s[si];
+        if ((unsigned)(p - S.lo[0]) >= (unsigned)(S.hi[0] - S.lo[0]) || j < S.lo[1] || j >= S.hi[1]) continue;
+        const float g = gtab[l * TF.ld + S.goff + (S.va == 0 ? p - S.lo[0] : j - S.lo[1])];
+        // g on the set's lanes, 0 elsewhere, added to the set's component by
+        // selects (conditional adds make the compiler index a scratch array)
+        const float gl = (kb >= S.lo[2] && kb < S.hi[2]) ? g : 0.f;
+        const int c = S.n - 3 * k;
+        c0 = c0 + (vec)(c == 0 ? gl : 0.f);
+        c1 = c1 + (vec)(c == 1 ? gl : 0.f);
+        c2 = c2 + (vec)(c == 2 ? gl : 0.f);
+      }
+    }
+  };
+  typedef unsigned u3 __attribute__((ext_vector_type(3)));
+  auto coef_ld = [&](const float4* arr, const Box3& B, unsigned off, size_t pl, int p) -> u3 {
+    const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)arr + (size_t)(p - B.lo[0]) * pl),
+                                                      (short)0, (int)pl, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+  };
+  // RING: one per-cell kind; its coefficient planes X - l - RHS of the T
+  // levels of trip X sit in T LDS slots (each wave reads and writes only its
+  // own rows, so no barrier guards them)
+  constexpr bool RING = PC == 1 || PC == 2;
+  constexpr int NS = RING ? T : 1;
+  constexpr int RHS = PC == 2 ? 1 : 0;  // H levels run one plane behind E
+  __shared__ float sC[NS][3][RING ? ROWS : 1][64];
+  const Box3& RB = PC == 2 ? BH : BE;
+  const float4* rarr = PC == 2 ? ch4 : ce4;
+  const size_t rpl = PC == 2 ? hplane : eplane;
+  const unsigned* roffc = PC == 2 ? hoff : eoff;
+  const bool wave_r = PC == 2 ? wave_h : wave_e;
+  auto ring_slot = [&](int p) -> int { return (p + 64 * NS) % NS; };
+  if (RING && wave_r && xin(RB, i0 - T - RHS)) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u3 v = coef_ld(rarr, RB, roffc[r], rpl, i0 - T - RHS);
+      const int sl = ring_slot(i0 - T - RHS);
+      sC[sl][0][R * w + r][lane] = __uint_as_float(v.x);
+      sC[sl][1][R * w + r][lane] = __uint_as_float(v.y);
+      sC[sl][2][R * w + r][lane] = __uint_as_float(v.z);
+    }
+  }
+
+  // CPML helpers.  Terms are (component n, t):
+  // axis kTermAxis[n][t].  y terms: Ex.0 Ez.1 Hx.1 Hz.0; z terms: Ex.1 Ey.0
+  // Hx.0 Hy.1; x terms: the rest.
+  auto ytm_index = [](int n) -> int { return n == 0 ? 0 : (n == 2 ? 1 : (n == 3 ? 2 : 3)); };
+  auto ztm_index = [](int n) -> int { return n == 0 ? 0 : (n == 1 ? 1 : (n == 3 ? 2 : 3)); };
+  // slab side holding index v along the term's axis (-1: none)
+  auto side_of = [&](const CpmlTerm& tm, int v) -> int {
+    return (tm.psi[0] && v >= tm.lo[0] && v < tm.hi[0]) ? 0 : ((tm.psi[1] && v >= tm.lo[1] && v < tm.hi[1]) ? 1 : -1);
+  };
+  auto psi_side_x = [&](int n, int t, int pl) -> int {
+    return kTermAxis[n][t] == 0 ? side_of(CP.t[n][0], pl) : -1;
+  };
+  auto psi_side_y = [&](int n, int t, int j) -> int {
+    return kTermAxis[n][t] == 1 ? side_of(CP.t[n][1], j) : -1;
+  };
+  // descriptor of plane pl of the side-sd slab of term (n, t), read or written
+  // copy; an empty one (every access dropped / reads 0) for sd < 0 or a plane
+  // outside the grid -- so every psi access is issued unconditionally and the
+  // compiler's vmcnt bookkeeping never has to drain the plane prefetch
+  auto psi_rsrc = [&](int n, int t, int sd, int pl, bool wr) -> Rsrc {
+    const int a = kTermAxis[n][t];
+    const CpmlTerm& tm = CP.t[n][a];
+    const bool ok = sd >= 0 && pl >= 0 && pl < nx;
+    const int s_ = sd > 0 ? 1 : 0;
+    const int wd = tm.hi[s_] - tm.lo[s_];
+    const size_t pe_ = a == 0 ? (size_t)ny * nz : (a == 1 ? (size_t)wd * nz : (size_t)ny * wd);
+    const size_t first = ok ? (a == 0 ? (size_t)(pl - tm.lo[s_]) * pe_ : (size_t)pl * pe_) : 0;
+    const float* base = wr ? tm.out[s_] : tm.psi[s_];
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(base + first), (short)0, ok ? (int)(pe_ * 4) : 0, 0x00020000);
+  };
+  // lane byte offset of row r in that plane (past the plane for lanes outside the slab)
+  auto psi_off = [&](int n, int t, int sd, int r) -> unsigned {
+    const int a = kTermAxis[n][t];
+    const CpmlTerm& tm = CP.t[n][a];
+    if (a == 0) return roff[r];
+    if (a == 1) return roff[r] - (unsigned)(tm.lo[sd] * nz) * 4u;  // sentinel offsets stay past the plane
+    const int j = jw + r;
+    const bool in = kin && j >= 0 && j < ny && kb >= tm.lo[sd] && kb < tm.hi[sd];
+    return in ? (unsigned)(j * (tm.hi[sd] - tm.lo[sd]) + (kb - tm.lo[sd])) * 4u : 0xF0000000u;
+  };
+  // wave-level activity of the 12 terms (bit 2n + t): x terms always (the
+  // plane decides per trip), y terms when a row of the wave lies in a slab,
+  // z terms when a lane does; z-term profiles per lane, y-term profiles of
+  // the wave's rows in LDS (uniform reads)
+  unsigned cpm_wave = 0;
+  // term (n, t) compiled into this variant (its axis is one of CAX) and live in this wave
+  auto act = [&](int n, int t) -> bool { return ((CAX >> kTermAxis[n][t]) & 1) && ((cpm_wave >> (2 * n + t)) & 1u); };
+  float ZB[CPM ? 4 : 1], ZC[CPM ? 4 : 1], ZK[CPM ? 4 : 1];
+  __shared__ float sYP[CPM ? NW : 1][CPM ? 4 * R * 3 : 1];
+  if constexpr (CPM) {
+#pragma unroll
+    for (int n = 0; n < 6; ++n)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int a = kTermAxis[n][t];
+        if (!((CAX >> a) & 1)) continue;
+        const CpmlTerm& tm = CP.t[n][a];
+        bool live = false;
+        if (a == 0) {
+          live = tm.psi[0] || tm.psi[1];
+        } else if (a == 1) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int j = jw + r;
+            const bool in = side_of(tm, j) >= 0;
+            live |= in;
+            const int q = (ytm_index(n) * R + r) * 3;
+            if (lane == 0) {
+              sYP[w][q] = in ? tm.b[j] : 1.f;
+              sYP[w][q + 1] = in ? tm.c[j] : 0.f;
+              sYP[w][q + 2] = in ? tm.k[j] : 0.f;
+            }
+          }
+        } else {
+          const bool in = kin && side_of(tm, kb) >= 0;
+          live = __any(in);
+          const int zi = ztm_index(n);
+          ZB[zi] = in ? tm.b[kb] : 1.f;
+          ZC[zi] = in ? tm.c[kb] : 0.f;
+          ZK[zi] = in ? tm.k[kb] : 0.f;
+        }
+        cpm_wave |= live ? (1u << (2 * n + t)) : 0u;
+      }
+  }
+  // Multi-step CPML: level l of trip X advances the psi of plane X - l (E
+  // terms; H terms X - l - 1), and level l + 1 of trip X + 1 advances the same
+  // cells again -- in the same lane of the same wave.  So the hand-off between
+  // levels is thread-private: level l stores its psi in slot (X & 1, l) of
+  // this thread's scratch column, the next trip's level l + 1 loads it back
+  // (agent-scope loads: L1 bypassed, the thread's own store is in L2).  The
+  // trip parity keeps this trip's level l from overwriting what its level
+  // l + 1 has yet to read.  Level 0 reads
+  // the slab arrays (psi at time n), level T - 1 writes the other copy (n + T)
+  // for owned cells only.  Slots are slot-major across all threads of the
+  // launch, so a wave's 64 lanes touch one contiguous 256-B run.
+  const unsigned scr_nth = gridDim.x * gridDim.y * gridDim.z * NW * 64u;
+  const unsigned scr_tid =
+      ((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * NW + w) * 64u + lane;
+  // (descriptor built at each use from the kernel argument: a descriptor
+  // value carried across the loop is taken for divergent and waterfalled)
+  auto scr_rs = [&]() -> Rsrc { return __builtin_amdgcn_make_buffer_rsrc((void*)pscr, (short)0, -1, 0x00020000); };
+  // per-lane part of a slot address (one VGPR) + wave-uniform slot base (soffset)
+  const unsigned scr_voff = scr_tid * 4u;
+  auto scr_soff = [&](int par, int l, int n, int t, int r) -> int {
+    return (int)((unsigned)((((par * (T - 1) + l) * 6 + n) * 2 + t) * R + r) * scr_nth * 4u);
+  };
+
+  auto run = [&](auto allin_tag) {
+  constexpr bool ALLIN = decltype(allin_tag)::value;
+  // coefficient of component n (box b) of row r on plane p: the lane's value
+  // sc (scalar or per-cell) inside the update box, 0 outside
+  auto coef = [&](const Box3& b, int p, int r, int n, float sc) -> vec {
+    const bool in = xin(b, p);
+    if constexpr (ALLIN) return in ? (vec)(sc) : zero;
+    const unsigned m = in ? (mbits >> ((r * 7 + n) * V)) & VM : 0u;
+    return cmask<V>((vec)(sc), m);
+  };
+
+  F3<V> Hp[T][R], Ep[T][R];
+#pragma unroll
+  for (int l = 0; l < T; ++l)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      Hp[l][r].x = Hp[l][r].y = Hp[l][r].z = zero;
+      Ep[l][r].x = Ep[l][r].y = Ep[l][r].z = zero;
+    }
+  int buf = 0;
+  auto load_plane = [&](int X, F3<V>* H, F3<V>* E) {
+    const Rsrc rhx = plane_rsrc(hxi, X, nx, plane), rhy = plane_rsrc(hyi, X, nx, plane);
+    const Rsrc rhz = plane_rsrc(hzi, X, nx, plane), rex = plane_rsrc(exi, X, nx, plane);
+    const Rsrc rey = plane_rsrc(eyi, X, nx, plane), rez = plane_rsrc(ezi, X, nx, plane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      H[r].x = bld<V>(rhx, roff[r]);
+      H[r].y = bld<V>(rhy, roff[r]);
+      H[r].z = bld<V>(rhz, roff[r]);
+      E[r].x = bld<V>(rex, roff[r]);
+      E[r].y = bld<V>(rey, roff[r]);
+      E[r].z = bld<V>(rez, roff[r]);
+    }
+  };
+  F3<V> Hnx[R], Enx[R], Hn2[R], En2[R];
+  load_plane(i0 - T, Hnx, Enx);
+  if (PFD == 2) load_plane(i0 - T + 1, Hn2, En2);
+  F3<V> Hs[R];  // DEFER: H_T of the previous plane, stored next trip
+#pragma unroll
+  for (int r = 0; r < R; ++r) Hs[r] = F3<V>{};
+  // stores of the results of trip X: E_T on plane X-T+1 (= Ep[T-1] until the
+  // next trip's last level), H_T on plane X-T
+  auto store_plane = [&](int X, const F3<V>* Es, const F3<V>* Hh) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned mo = (mbits >> ((r * 7 + 6) * V)) & VM;
+      if constexpr (V == 1) {
+        // unconditional stores masked by an out-of-range offset (dropped by
+        // the descriptor): a fixed store count per trip keeps the compiler's
+        // vmcnt bookkeeping exact, so the next prefetch wait does not drain
+        // the stores (see DEFER)
+        const int pe = X - T + 1, ph = X - T;
+        const unsigned oe = mo && pe >= i0 && pe < i1 ? roff[r] : 0xF0000000u;
+        const unsigned oh = mo && ph >= i0 && ph < i1 ? roff[r] : 0xF0000000u;
+        bst<V>(plane_rsrc(exo, pe, nx, plane), oe, Es[r].x, 1u);
+        bst<V>(plane_rsrc(eyo, pe, nx, plane), oe, Es[r].y, 1u);
+        bst<V>(plane_rsrc(ezo, pe, nx, plane), oe, Es[r].z, 1u);
+        bst<V>(plane_rsrc(hxo, ph, nx, plane), oh, Hh[r].x, 1u);
+        bst<V>(plane_rsrc(hyo, ph, nx, plane), oh, Hh[r].y, 1u);
+        bst<V>(plane_rsrc(hzo, ph, nx, plane), oh, Hh[r].z, 1u);
+      } else if (mo) {
+        const int pe = X - T + 1;
+        if (pe >= i0 && pe < i1) {
+          bst<V>(plane_rsrc(exo, pe, nx, plane), roff[r], Es[r].x, mo);
+          bst<V>(plane_rsrc(eyo, pe, nx, plane), roff[r], Es[r].y, mo);
+          bst<V>(plane_rsrc(ezo, pe, nx, plane), roff[r], Es[r].z, mo);
+        }
+        const int ph = X - T;
+        if (ph >= i0 && ph < i1) {
+          bst<V>(plane_rsrc(hxo, ph, nx, plane), roff[r], Hh[r].x, mo);
+          bst<V>(plane_rsrc(hyo, ph, nx, plane), roff[r], Hh[r].y, mo);
+          bst<V>(plane_rsrc(hzo, ph, nx, plane), roff[r], Hh[r].z, mo);
+        }
+      }
+    }
+  };
+  for (int X = i0 - T; X <= i1 + T - 1; ++X) {
+    F3<V> Hc[R], Ec[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      Hc[r] = Hnx[r];
+      Ec[r] = Enx[r];
+      if (PFD == 2) {
+        Hnx[r] = Hn2[r];
+        Enx[r] = En2[r];
+      }
+    }
+    // this trip's coefficients.  One per-cell kind (RING): the next trip's
+    // newest plane is loaded now and parked in the wave's own LDS ring slots
+    // at the end of the trip.  Both kinds: every level's plane into registers.
+    const int qn = X + 1 - RHS;  // ring: the plane the next trip's level 0 needs
+    const bool ring_ld = RING && wave_r && xin(RB, qn);
+    u3 RQ[R];
+    if (ring_ld) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) RQ[r] = coef_ld(rarr, RB, roffc[r], rpl, qn);
+    }
+    u3 CE[PC == 3 ? T : 1][R], CH[PC == 3 ? T : 1][R];
+    if (PC == 3 && wave_e) {
+#pragma unroll
+      for (int l = 0; l < T; ++l)
+        if (xin(BE, X - l))
+#pragma unroll
+          for (int r = 0; r < R; ++r) CE[PC == 3 ? l : 0][r] = coef_ld(ce4, BE, eoff[r], eplane, X - l);
+    }
+    if (PC == 3 && wave_h) {
+#pragma unroll
+      for (int l = 0; l < T; ++l)
+        if (xin(BH, X - l - 1))
+#pragma unroll
+          for (int r = 0; r < R; ++r) CH[PC == 3 ? l : 0][r] = coef_ld(ch4, BH, hoff[r], hplane, X - l - 1);
+    }
+    // the lane's three coefficients of a kind at level l, plane p (scalar off the box)
+    auto kcoef = [&](bool kind_e, int l, int p, int r) -> float3 {
+      const float sc = kind_e ? cb : db;
+      const bool wave = kind_e ? wave_e : wave_h;
+      const bool lane_in = (inb >> (kind_e ? r : R + r)) & 1u;
+      if constexpr (RING) {
+        if (kind_e == (bool)PCE && wave && xin(RB, p) && lane_in) {
+          const int sl = ring_slot(p);
+          return make_float3(sC[sl][0][R * w + r][lane], sC[sl][1][R * w + r][lane], sC[sl][2][R * w + r][lane]);
+        }
+      } else if constexpr (PC == 3) {
+        if (wave && xin(kind_e ? BE : BH, p) && lane_in) {
+          const u3 raw = kind_e ? CE[PC == 3 ? l : 0][r] : CH[PC == 3 ? l : 0][r];
+          return make_float3(__uint_as_float(raw.x), __uint_as_float(raw.y), __uint_as_float(raw.z));
+        }
+      }
+      return make_float3(sc, sc, sc);
+    };
+    // CPML: every psi value this trip's levels advance -- level l: E terms
+    // on plane X - l, H terms on X - l - 1 -- loaded before the prefetch
+    // (vmcnt retires in issue order): level 0 from the slab arrays (time n),
+    // levels >= 1 from the thread's scratch slots the previous trip's level
+    // l - 1 wrote.  Slab membership is wave-uniform for x (plane) and y (row)
+    // terms and per lane for z terms; lanes / rows / planes outside a slab get
+    // an empty descriptor or an offset past it (reads 0) instead of a branch.
+    float PSL[CPM ? T : 1][CPM ? 6 : 1][2][R];
+    if constexpr (CPM) {
+#pragma unroll
+      for (int l = 0; l < T; ++l)
+#pragma unroll
+        for (int n = 0; n < 6; ++n)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int a = kTermAxis[n][t];
+            if (!((CAX >> a) & 1)) continue;
+            const int pl = (n < 3 ? X : X - 1) - l;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              float v = 0.f;
+              if (l > 0) {
+                v = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(scr_rs(), scr_voff, scr_soff((X - 1) & 1, l - 1, n, t, r), 16));
+              } else if (a == 0) {
+                v = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(psi_rsrc(n, t, psi_side_x(n, t, pl), pl, false), roff[r], 0, 0));
+              } else if (a == 1) {
+                const int sd = psi_side_y(n, t, jw + r);
+                v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(psi_rsrc(n, t, sd, pl, false),
+                                                                         psi_off(n, t, sd > 0 ? 1 : 0, r), 0, 0));
+              } else {
+#pragma unroll
+                for (int sd = 0; sd < 2; ++sd)
+                  v += __uint_as_float(
+                      __builtin_amdgcn_raw_buffer_load_b32(psi_rsrc(n, t, sd, pl, false), psi_off(n, t, sd, r), 0, 0));
+              }
+              PSL[CPM ? l : 0][CPM ? n : 0][t][r] = v;
+            }
+          }
+    }
+    // psi update of term t of component n (plane pl, row r) from its raw
+    // difference d; returns the curl correction sign * ((1/kappa - 1) d + psi)
+    auto cpml = [&](int l, int n, int t, int pl, int r, const vec& d) -> vec {
+      if constexpr (CPM) {
+        const int a = kTermAxis[n][t];
+        const int sg = t == 0 ? 1 : -1;
+        if (!act(n, t)) return zero;
+        float bb, cc, kk;
+        if (a == 0) {
+          if (psi_side_x(n, t, pl) < 0) return zero;
+          const CpmlTerm& tm = CP.t[n][0];
+          bb = cload(tm.b, pl);
+          cc = cload(tm.c, pl);
+          kk = cload(tm.k, pl);
+        } else if (a == 1) {
+          if (psi_side_y(n, t, jw + r) < 0) return zero;
+          const int q = (ytm_index(n) * R + r) * 3;
+          bb = sYP[w][q];
+          cc = sYP[w][q + 1];
+          kk = sYP[w][q + 2];
+        } else {
+          const int zi = ztm_index(n);
+          bb = ZB[zi];
+          cc = ZC[zi];
+          kk = ZK[zi];
+        }
+        const float pn = bb * PSL[CPM ? l : 0][CPM ? n : 0][t][r] + cc * d[0];
+        PSL[CPM ? l : 0][CPM ? n : 0][t][r] = pn;
+        const float cr = kk * d[0] + pn;  // 0 off a z slab (identity profile, psi 0)
+        return (vec)(sg > 0 ? cr : -cr);
+      }
+      return zero;
+    };
+    if (tf_slots) {
+      // this trip's g entries of the face slots (va = 0: index moves with X)
+      // (entries of planes outside a set's x range are never used; their
+      // index is clamped into the table)
+      const int dx = tf_va == 0 ? X : 0;
+      const int last = T * tf_ld - 1;
+      tf_g0 = tf_ok0 ? gtab[min(max(tf_gb0 + dx, 0), last)] : 0.f;
+      if (TF_ENT > 64) tf_g1 = tf_ok1 ? gtab[min(max(tf_gb1 + dx, 0), last)] : 0.f;
+    }
+    // next plane(s) in flight under this plane's levels
+    if (PFD == 2)
+      load_plane(X + 2, Hn2, En2);
+    else
+      load_plane(X + 1, Hnx, Enx);
+    if (DEFER && (V == 1 || X > i0 - T)) {  // V = 1: the first trip's stores are dropped
+      F3<V> Es[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) Es[r] = Ep[T - 1][r];
+      store_plane(X - 1, Es, Hs);
+    }
+    F3<V> En[R];
+#pragma unroll
+    for (int l = 0; l < T; ++l) {
+      const int pe = X - l;
+      sX[buf][0][w][lane] = Hc[R - 1].z;
+      sX[buf][1][w][lane] = Hc[R - 1].x;
+      sX[buf][2][w][lane] = Ep[l][0].x;
+      sX[buf][3][w][lane] = Ep[l][0].z;
+      __syncthreads();
+      const vec hz_dn = sX[buf][0][rdn][lane];
+      const vec hx_dn = sX[buf][1][rdn][lane];
+      const vec ex_up = sX[buf][2][rup][lane];
+      const vec ez_up = sX[buf][3][rup][lane];
+      buf ^= 1;
+      const bool src_plane = src_comp >= 0 && pe == src_i;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const vec hz_j = r == 0 ? hz_dn : Hc[r > 0 ? r - 1 : 0].z;
+        const vec hx_j = r == 0 ? hx_dn : Hc[r > 0 ? r - 1 : 0].x;
+        const float hy_k0 = lane_up(Hc[r].y[V - 1]);
+        const float hx_k0 = lane_up(Hc[r].x[V - 1]);
+        const float3 ce = kcoef(true, l, pe, r);
+        const vec dxy = Hc[r].z - hz_j, dxz = Hc[r].y - zm1<V>(Hc[r].y, hy_k0);
+        const vec dyz = Hc[r].x - zm1<V>(Hc[r].x, hx_k0), dyx = Hc[r].z - Hp[l][r].z;
+        const vec dzx = Hc[r].y - Hp[l][r].y, dzy = Hc[r].x - hx_j;
+        vec cx = dxy - dxz;
+        vec cy = dyz - dyx;
+        vec cz = dzx - dzy;
+        if constexpr (CPM) {
+          cx += cpml(l, 0, 0, pe, r, dxy) + cpml(l, 0, 1, pe, r, dxz);
+          cy += cpml(l, 1, 0, pe, r, dyz) + cpml(l, 1, 1, pe, r, dyx);
+          cz += cpml(l, 2, 0, pe, r, dzx) + cpml(l, 2, 1, pe, r, dzy);
+        }
+        tf_apply(0, l, pe, r, cx, cy, cz);
+        En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * cx;
+        En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * cy;
+        En[r].z = Ec[r].z + coef(bez, pe, r, 2, ce.z) * cz;
+        if (src_plane && jw + r == src_j && src_k >= kb && src_k < kb + V) {
+          const int q = src_k - kb;
+          if (src_comp == 0) En[r].x[q] = sv.v[l];
+          if (src_comp == 1) En[r].y[q] = sv.v[l];
+          if (src_comp == 2) En[r].z[q] = sv.v[l];
+        }
+      }
+      const int ph = pe - 1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const vec ex_jn = r == R - 1 ? ex_up : Ep[l][r < R - 1 ? r + 1 : r].x;
+        const vec ez_jn = r == R - 1 ? ez_up : Ep[l][r < R - 1 ? r + 1 : r].z;
+        const float ey_k3 = lane_dn(Ep[l][r].y[0]);
+        const float ex_k3 = lane_dn(Ep[l][r].x[0]);
+        F3<V> Hn;
+        const float3 ch = kcoef(false, l, ph, r);
+        const vec gxz = zp1<V>(Ep[l][r].y, ey_k3) - Ep[l][r].y, gxy = ez_jn - Ep[l][r].z;
+        const vec gyx = En[r].z - Ep[l][r].z, gyz = zp1<V>(Ep[l][r].x, ex_k3) - Ep[l][r].x;
+        const vec gzy = ex_jn - Ep[l][r].x, gzx = En[r].y - Ep[l][r].y;
+        vec dx = gxz - gxy;
+        vec dy = gyx - gyz;
+        vec dz = gzy - gzx;
+        if constexpr (CPM) {
+          dx += cpml(l, 3, 0, ph, r, gxz) + cpml(l, 3, 1, ph, r, gxy);
+          dy += cpml(l, 4, 0, ph, r, gyx) + cpml(l, 4, 1, ph, r, gyz);
+          dz += cpml(l, 5, 0, ph, r, gzy) + cpml(l, 5, 1, ph, r, gzx);
+        }
+        tf_apply(1, l, ph, r, dx, dy, dz);
+        Hn.x = Hp[l][r].x + coef(bhx, ph, r, 3, ch.x) * dx;
+        Hn.y = Hp[l][r].y + coef(bhy, ph, r, 4, ch.y) * dy;
+        Hn.z = Hp[l][r].z + coef(bhz, ph, r, 5, ch.z) * dz;
+        // later rows (r+1 ..) read only their own and higher rows' Ep, so
+        // row r rotates as soon as its H is done
+        Ec[r] = Ep[l][r];
+        Ep[l][r] = En[r];
+        Hp[l][r] = Hc[r];
+        Hc[r] = Hn;
+      }
+      if constexpr (CPM && T > 1) {
+        // this level's psi to the thread's slot for the next trip's level l + 1
+        if (l < T - 1) {
+#pragma unroll
+          for (int n = 0; n < 6; ++n)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              if (!((CAX >> kTermAxis[n][t]) & 1)) continue;
+#pragma unroll
+              for (int r = 0; r < R; ++r)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PSL[CPM ? l : 0][CPM ? n : 0][t][r]), scr_rs(),
+                                                      scr_voff, scr_soff(X & 1, l, n, t, r), 0);
+            }
+        }
+      }
+    }
+    if constexpr (CPM) {
+      // the last level's psi of owned cells inside their component's update
+      // box to the slab arrays (time n + T); every store issued, the rest
+      // dropped by the descriptor
+#pragma unroll
+      for (int n = 0; n < 6; ++n) {
+        const int pl = n < 3 ? X - T + 1 : X - T;
+        const bool xok = pl >= i0 && pl < i1 && xin(*bx[n], pl);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int a = kTermAxis[n][t];
+          if (!((CAX >> a) & 1)) continue;
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const bool st = xok && ((mbits >> (r * 7 + 6)) & 1u) && ((mbits >> (r * 7 + n)) & 1u);
+            const float v = PSL[CPM ? T - 1 : 0][CPM ? n : 0][t][r];
+            if (a == 0) {
+              const int sd = xok ? psi_side_x(n, t, pl) : -1;
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), psi_rsrc(n, t, sd, pl, true),
+                                                    st ? roff[r] : 0xF0000000u, 0, 0);
+            } else if (a == 1) {
+              const int sd = xok ? psi_side_y(n, t, jw + r) : -1;
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), psi_rsrc(n, t, sd, pl, true),
+                                                    st ? psi_off(n, t, sd > 0 ? 1 : 0, r) : 0xF0000000u, 0, 0);
+            } else {
+#pragma unroll
+              for (int sd = 0; sd < 2; ++sd)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), psi_rsrc(n, t, xok ? sd : -1, pl, true),
+                                                      st ? psi_off(n, t, sd, r) : 0xF0000000u, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    if (ring_ld) {
+      // slot of plane qn = that of plane qn - T, read at this trip's last level
+      const int sl = ring_slot(qn);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        sC[sl][0][R * w + r][lane] = __uint_as_float(RQ[r].x);
+        sC[sl][1][R * w + r][lane] = __uint_as_float(RQ[r].y);
+        sC[sl][2][R * w + r][lane] = __uint_as_float(RQ[r].z);
+      }
+    }
+    if (DEFER) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) Hs[r] = Hc[r];
+    } else {
+      store_plane(X, En, Hc);
+    }
+  }
+  if (DEFER) {
+    F3<V> Es[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) Es[r] = Ep[T - 1][r];
+    store_plane(i1 + T - 1, Es, Hs);
+  }
+  };
+  if (tile_all && !(xcd_swz & 2))
+    run(std::true_type{});
+  else
+    run(std::false_type{});
+}
+
+
+// host-side knobs of the multi-row launches (defined in yee3d_tb.hip)
+extern int g_tb_mr_noallin;
+extern int g_tb_mr_xcd;
+extern int g_tb_variant;
+int tb_patch_bits();
+int cpml_scr_l1();
+
+// tile of the multi-step CPML passes: CPML_NW waves x CPML_R rows
+constexpr int CPML_NW = 8, CPML_R = 2;
+
+template <int T, int V, int R, int FX, int NW = TBW>
+int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
+                 const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
+                 int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
+                 const TfDev* tf, const float* gtab, const CpmlDev* cp, float* pscr, hipStream_t s) {
+  constexpr int HL = (T + V - 1) / V;
+  constexpr int TBZ = (64 - 2 * HL) * V;
+  dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], NW * R - 2 * T),
+            cdiv(O.hi[0] - O.lo[0], xchunk));
+  CpmlDev cpv{};
+  if constexpr (((FX >> 3) & 7) != 0) cpv = *cp;
+#define MR_LAUNCH(PFD, DEFER)                                                                                 \
+  k_tb3d_mr<T, V, R, FX, PFD, DEFER, NW><<<grid, dim3(64, NW), 0, s>>>(                                     \
+      ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
+      ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
+      O, xchunk, src[0], src[1], src[2], src[3], sv,                                                       \
+      (g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1)) |          \
+          (cpml_scr_l1() << 24),                                                                           \
+      tf, gtab, cpv, pscr)
+  if constexpr (FX != 0) {
+    MR_LAUNCH(1, false);  // tuning variants: uniform media only
+  } else {
+    switch (g_tb_variant & 3) {
+      case 0: MR_LAUNCH(1, false); break;
+      case 1: MR_LAUNCH(1, true); break;
+      case 2: MR_LAUNCH(2, false); break;
+      default: MR_LAUNCH(2, true); break;
+    }
+  }
+#undef MR_LAUNCH
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+// multi-step (T > 1) CPML passes, TF/SF on or off (yee3d_tb_cpml.hip)
+int launch_tb_mr_cpml(int T, int fx, const float* const* ein, const float* const* hin, float* const* eout,
+                      float* const* hout, float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O,
+                      int xchunk, const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab,
+                      const CpmlDev* cp, float* pscr, hipStream_t s);
+
+}  // namespace tb3d

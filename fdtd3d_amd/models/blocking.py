@@ -374,7 +374,38 @@ class BlockedStepping:
             break
         if K is None:
             return None
-        shell = [dom.to_local(b) for b in box_subtract(alloc, K) if not box_empty(b)]
+        if self.use_cpml and T not in getattr(self.ops, "tb_cpml_steps", ()):
+            return None
+        # shell pieces by class: the CPML axes whose slabs a piece's
+        # dependency cone reaches (cuts T + 1 beyond each slab), and whether
+        # it reaches a TF/SF target -- each class is its own kernel variant
+        slabs = [sl for sls in (self.cpml.slabs.values() if self.use_cpml else ()) for sl in sls]
+        cuts = []
+        for a in range(3):
+            lo_e = max([sl.gbox[1][a] for sl in slabs if sl.axis == a and sl.side == 0], default=None)
+            hi_s = min([sl.gbox[0][a] for sl in slabs if sl.axis == a and sl.side == 1], default=None)
+            cuts.append([c for c in ((lo_e + T + 1) if lo_e is not None else None,
+                                     (hi_s - T - 1) if hi_s is not None else None) if c is not None])
+        pieces = [b for b in box_subtract(alloc, K) if not box_empty(b)]
+        for a in range(3):
+            nxt = []
+            for b in pieces:
+                edges = sorted({b[0][a], b[1][a]} | {c for c in cuts[a] if b[0][a] < c < b[1][a]})
+                for lo_, hi_ in zip(edges, edges[1:]):
+                    lo, hi = list(b[0]), list(b[1])
+                    lo[a], hi[a] = lo_, hi_
+                    nxt.append((tuple(lo), tuple(hi)))
+            pieces = nxt
+        classed = []
+        for b in pieces:
+            g = grow(b, T + 1)
+            ax = 0
+            for sl in slabs:
+                if not box_empty(box_intersect(g, sl.gbox)):
+                    ax |= 1 << sl.axis
+            tf = bool(cfg.use_tfsf and self._tfsf_targets_in(dom.to_local(g)))
+            classed.append((b, ax | (8 if tf else 0)))
+        shell = [(dom.to_local(b), c) for b, c in _merge_pieces(classed)]
         upd = {c: self.local_box(c, alloc) for c in self.comps}
         return {"T": T, "v3": True, "core": [dom.to_local(K)], "shell": shell, "upd": upd,
                 "core_cells": box_volume(K)}
@@ -399,8 +430,10 @@ class BlockedStepping:
                 for ob in hp["core"]:
                     self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p])
             with self.prof.phase("blocked-shell"):
-                for ob in hp["shell"]:
-                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf, cpml=cp)
+                for ob, cls in hp["shell"]:
+                    cax = cls & 7
+                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf if cls & 8 else None,
+                                     cpml=cp if cax else None, cpml_axes=cax)
             if self.use_cpml:
                 self.cpml.flip(p)
             self.F[p], self.F_alt[p] = Q, P

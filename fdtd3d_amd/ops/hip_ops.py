@@ -672,6 +672,7 @@ class HipOps:
 
     # ------------------------------------------------------ temporal blocking
     tfsf_sets_ok = True  # the fp32 blocked kernel applies TfsfSets corrections
+    tb_cpml_steps = (1, 4, 5)  # steps per pass of the in-kernel CPML variants (yee3d_tb_cpml.hip)
 
     def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
                   sets, slot: int = 0) -> torch.Tensor:
@@ -701,7 +702,8 @@ class HipOps:
         return g
 
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None, cpml=None) -> None:
+                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None, cpml=None,
+                cpml_axes: int = 0) -> None:
         """``steps`` fused leapfrog steps in one HBM pass (yee3d_tb.hip).
 
         ``boxes`` are the update boxes (each component changes only there, at
@@ -709,7 +711,10 @@ class HipOps:
         never reads outside the arrays whatever the boxes, but the caller must
         give every stored cell ``steps`` valid layers of input around it.
         ``sources`` = per-step list of (E component, local index, value) or
-        None."""
+        None.  ``cpml`` = ``CPML.host_table(p)`` (psi read from ``psi[p]``,
+        written to the other copy: ``CPML.flip`` after the pass), with
+        ``cpml_axes`` the axes (bits) whose slabs the box's dependency cone
+        reaches (0: all); multi-step CPML passes take 4 or 5 steps."""
         if len(fin) == 3:
             self._tb2d_step(fin, fout, boxes, obox, cb, steps, sources)
             return
@@ -763,8 +768,8 @@ class HipOps:
             raise HipError("in-kernel TF/SF: fp32 only")
         pscr, pscr_bytes = None, 0
         if cpml is not None:
-            if self.dtype != torch.float32 or steps > 5:
-                raise HipError("in-kernel CPML: fp32, at most 5 steps per pass")
+            if self.dtype != torch.float32 or steps not in self.tb_cpml_steps:
+                raise HipError("in-kernel CPML: fp32, %s steps per pass" % (self.tb_cpml_steps,))
             if int(self.lib.fdtd_cpmldev_size()) != cpml.numel() or cpml.device.type != "cpu":
                 raise HipError("cpml: the CpmlDev block as host bytes (CPML.host_table)")
             if steps > 1:
@@ -794,7 +799,7 @@ class HipOps:
                 arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), _ptr(ce), _box_arr([ebox]), _ptr(ch),
                 _box_arr([hbox]), c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk), c_int(steps),
-                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _ptr(cpml), _ptr(pscr),
+                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _ptr(cpml), c_int(int(cpml_axes)), _ptr(pscr),
                 ctypes.c_longlong(pscr_bytes), _stream())
             _check(rc, "tb3d_ext")
             self.launches += 1

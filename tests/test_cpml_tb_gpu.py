@@ -27,7 +27,7 @@ def _where(d):
 PML = {"x": (6, 0, 0), "y": (0, 6, 0), "z": (0, 0, 6), "xyz": (5, 6, 7)}
 
 
-@pytest.mark.parametrize("T", [1, 2, 3, 5])
+@pytest.mark.parametrize("T", [1, 4, 5])
 @pytest.mark.parametrize("axes", ["x", "y", "z", "xyz"])
 @pytest.mark.parametrize("tfsf", [False, True])
 def test_cpml_pass_vs_stepped(gpu, T, axes, tfsf):
@@ -44,7 +44,10 @@ def test_cpml_pass_vs_stepped(gpu, T, axes, tfsf):
     out = {c: torch.zeros_like(b.F[0][c]) for c in b.comps}
     tf = b._tfsf_pass(0, T) if tfsf else None
     srcs = b._pass_sources(b.t, T)[0]
-    b.ops.tb_step(b.F[0], out, upd, ((0, 0, 0), cfg.size), b.cb, T, srcs, tfsf=tf, cpml=b.cpml.host_table(0))
+    # the whole grid's cone reaches every slab: the class of the configured axes
+    cax = sum(1 << a for a in range(3) if PML[axes][a] > 0)
+    b.ops.tb_step(b.F[0], out, upd, ((0, 0, 0), cfg.size), b.cb, T, srcs, tfsf=tf, cpml=b.cpml.host_table(0),
+                  cpml_axes=cax)
     b.cpml.flip(0)
     torch.cuda.synchronize()
     bad = []

@@ -163,7 +163,7 @@ def test_hybrid_at_scale(gpu, name, extra):
 
 
 @pytest.mark.parametrize("T,tfsf,point,size", [(5, True, False, (96, 88, 96)), (4, True, True, (80, 72, 96)),
-                                               (3, False, True, (72, 80, 64)), (2, True, False, (64, 64, 128)),
+                                               (4, False, True, (72, 80, 64)), (5, True, False, (64, 64, 128)),
                                                (5, False, True, (112, 96, 100))])
 def test_hybrid3_blocked_shell(gpu, T, tfsf, point, size):
     """Blocked shell (every box one T-step launch: the CPML + TF/SF variant
@@ -187,6 +187,7 @@ def test_hybrid3_blocked_shell(gpu, T, tfsf, point, size):
     hy, st = runs[T], runs[1]
     assert hy.hybrid is not None and hy.hybrid.get("v3"), "blocked shell not selected"
     assert st.hybrid is None
+    assert len({cls for _, cls in hy.hybrid["shell"]}) >= 3  # face / edge / corner classes
     for c in hy.comps:
         x, y = hy.F[0][c].double().cpu(), st.F[0][c].double().cpu()
         scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--only", default="", help="run only the cases whose name contains this")
     a = ap.parse_args()
     n = a.n
     cfg = SchemeConfig(scheme="3d", size=(n, n, n), dtype="f32", scene="vacuum", use_pml=True, pml_type="cpml",
@@ -39,20 +40,22 @@ def main():
     g = s._tfsf_pass(0, 5)
     cp = s.cpml.host_table(0)
     cases = []
-    for T in (1, 4):
-        for name, box in wins.items():
-            if T == 4 and name != "core" and name != "whole":
-                continue
-            cases.append(("T%d plain %s" % (T, name), T, box, None, None))
-            cases.append(("T%d tfsf  %s" % (T, name), T, box, g, None))
-            if T == 1:
-                cases.append(("T1 cpml  %s" % name, 1, box, None, cp))
-                cases.append(("T1 cp+tf %s" % name, 1, box, g, cp))
+    cls = {"core": 0, "xwin": 1, "ywin": 2, "zwin": 4}
+    for T in (1, 4, 5):
+        cases.append(("T%d plain core" % T, T, wins["core"], None, None, 0))
+        cases.append(("T%d tfsf  core" % T, T, wins["core"], g, None, 0))
+        for name in ("core", "xwin", "ywin", "zwin"):
+            cases.append(("T%d cpml  %s" % (T, name), T, wins[name], None, cp, 7))
+            if T > 1 and name != "core":
+                cases.append(("T%d cpml  %s class %d" % (T, name, cls[name]), T, wins[name], None, cp, cls[name]))
+        cases.append(("T%d cp+tf xwin" % T, T, wins["xwin"], g, cp, 1 if T > 1 else 7))
+    if a.only:
+        cases = [c for c in cases if a.only in c[0]]
     res = {c[0]: [] for c in cases}
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rnd in range(a.rounds):
-        for name, T, box, tf, cpd in cases:
-            kw = {}
+        for name, T, box, tf, cpd, cax in cases:
+            kw = {"cpml_axes": cax} if cpd is not None else {}
             if tf is not None:
                 kw["tfsf"] = tf
             if cpd is not None:
@@ -64,7 +67,7 @@ def main():
             ev1.record()
             torch.cuda.synchronize()
             res[name].append(ev0.elapsed_time(ev1) / 3)
-    for name, T, box, tf, cpd in cases:
+    for name, T, box, tf, cpd, cax in cases:
         cells = 1
         for d in range(3):
             cells *= box[1][d] - box[0][d]
