@@ -99,7 +99,7 @@ class SchemeConfig:
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
-    hybrid_shell: str = "auto"               # auto | stepped | single-pass (models/blocking.py _hybrid2_plan)
+    hybrid_shell: str = "auto"               # auto | stepped | single-pass | blocked (models/blocking.py)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
@@ -357,7 +357,8 @@ class YeeScheme(BlockedStepping):
         # 1D plain serial HIP runs: a whole advance() in one launch of the
         # register-resident kernel (yee1d_res.hip) -- the per-step path is
         # launch-bound at these sizes, HIP graphs included
-        self.res1d = (cfg.scheme == "1d" and self.ops.name == "hip" and cfg.use_fused
+        # (the torch backend on the CPU runs the host library's native loop)
+        self.res1d = (cfg.scheme == "1d" and (self.ops.name == "hip" or self.device.type == "cpu") and cfg.use_fused
                       and hasattr(self.ops, "resident_1d") and self.halo is None
                       and not self.use_upml_chain and not self.use_cpml and not cfg.use_tfsf
                       and not cfg.use_amp_mode and self.line_source is None

@@ -110,17 +110,61 @@ class TorchOps:
                 sl = box_slices(b)
                 fout[c][sl] = tmp[c][sl]
 
+    def resident_1d_max_cells(self) -> int:
+        return 1 << 30
+
     def resident_1d(self, F: Dict[str, torch.Tensor], boxes: Dict[str, Box], cb: Dict[str, Coef], nsteps: int,
                     src_i=None, vals=None) -> None:
         """Reference semantics of the register-resident 1D kernel
         (yee1d_res.hip): ``nsteps`` fused steps in place, hard Ez source
-        ``vals[s]`` at cell ``src_i``."""
+        ``vals[s]`` at cell ``src_i``.  CPU tensors run the native loop of
+        the host library (csrc/host_yee1d.cpp); the torch ops below are the
+        oracle it is tested against."""
+        if self._res1d_native(F, boxes, cb, nsteps, src_i, vals):
+            return
         for s in range(nsteps):
             nxt = {c: F[c].clone() for c in F}
             src = None if vals is None else ("Ez", (int(src_i), 0, 0), float(vals[s]))
             self.fused_step(F, nxt, boxes, cb, src)
             for c in F:
                 F[c].copy_(nxt[c])
+
+    native_1d = True  # CPU 1D runs take the host library's loop (False: the torch oracle)
+
+    def _res1d_native(self, F, boxes, cb, nsteps, src_i, vals) -> bool:
+        ez, hy = F["Ez"], F["Hy"]
+        if (not self.native_1d or ez.device.type != "cpu" or ez.dtype not in (torch.float32, torch.float64)
+                or not ez.is_contiguous() or not hy.is_contiguous() or hy.dtype != ez.dtype):
+            return False
+        try:
+            from ..native import load_host_library
+            lib = load_host_library(build_if_missing=False)
+            fn = getattr(lib, "fdtd_res1d_cpu_%s" % ("f64" if ez.dtype == torch.float64 else "f32"))
+        except (OSError, AttributeError):
+            return False
+        import ctypes
+        n = ez.numel()
+        whole = tuple(slice(0, d) for d in ez.shape)
+
+        def cell(c):  # per-cell array of a coefficient with profiles / cells, None for a scalar
+            if all(getattr(c, a) is None for a in ("cell", "px", "py", "pz")):
+                return None
+            v = c.materialize(whole)
+            v = torch.as_tensor(v, dtype=ez.dtype).expand(ez.shape)
+            return v.contiguous().reshape(-1)
+        pe, ph = cell(cb["Ez"]), cell(cb["Hy"])
+        lim = lambda b: (b[0][0], b[1][0]) if not _empty(b) else (0, 0)
+        (elo, ehi), (hlo, hhi) = lim(boxes["Ez"]), lim(boxes["Hy"])
+        v = None
+        if vals is not None:
+            v = vals.to("cpu", ez.dtype).contiguous()
+        ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
+        fn.restype = ctypes.c_int
+        fn(ptr(ez), ptr(hy), ptr(pe), ptr(ph), ctypes.c_double(cb["Ez"].scalar if pe is None else 1.0),
+           ctypes.c_double(cb["Hy"].scalar if ph is None else 1.0), ctypes.c_int(n),
+           (ctypes.c_int * 4)(elo, ehi, hlo, hhi), ctypes.c_int(nsteps),
+           ctypes.c_int(-1 if src_i is None else int(src_i)), ptr(v))
+        return True
 
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
                 obox: Box, cb: Dict[str, Coef], steps: int, sources=None) -> None:
