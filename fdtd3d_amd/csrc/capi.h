@@ -75,7 +75,7 @@ int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* c
                       int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk, int steps,
                       const int* src, const double* src_vals, const void* tf, const float* gtab, const void* cpml,
                       int cpml_axes, void* pscr, long long pscr_bytes, void* stream);
-long long fdtd_tb3d_cpml_scratch_bytes(const int* obox, int xchunk, int steps, int tfsf);
+long long fdtd_tb3d_cpml_scratch_bytes(const int* obox, int xchunk, int steps, int tfsf, int cpml_axes);
 int fdtd_tfdev_size();
 int fdtd_cpmldev_size();
 int fdtd_tfsf_pass_f32(float* einc, float* hinc, int n, double ce, double ch, const double* src_vals, int steps,

@@ -232,6 +232,11 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   constexpr bool TFS = FX & 4;
   constexpr int CAX = (FX >> 3) & 7;
   constexpr bool CPM = CAX != 0;
+  // single-axis (face) CPML classes of 16-wave multi-step passes hand psi from
+  // level to level through LDS (4 terms x (T - 1) levels x the tile, 32 KiB
+  // per level) instead of registers / scratch: the register footprint of the
+  // plain kernel, 4 waves per SIMD and 32-row tiles
+  constexpr bool LPS = CPM && T > 1 && NW == 16 && (CAX == 1 || CAX == 2 || CAX == 4);
   static_assert(V == 1 || !FX, "sparse coefficients / TF/SF: scalar lanes");
   constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
   static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
@@ -551,6 +556,11 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   auto act = [&](int n, int t) -> bool { return ((CAX >> kTermAxis[n][t]) & 1) && ((cpm_wave >> (2 * n + t)) & 1u); };
   float ZB[CPM ? 4 : 1], ZC[CPM ? 4 : 1], ZK[CPM ? 4 : 1];
   __shared__ float sYP[CPM ? NW : 1][CPM ? 4 * R * 3 : 1];
+  __shared__ float sPS[LPS ? T - 1 : 1][LPS ? 4 : 1][LPS ? NW * R : 1][64];
+  // slot of component n's term among the 4 terms of a face class (axis LA):
+  // one per component off the axis, E first
+  constexpr int LA = CAX == 1 ? 0 : (CAX == 2 ? 1 : 2);
+  auto lps_q = [](int n) -> int { return (n / 3) * 2 + ((n % 3) < LA ? (n % 3) : (n % 3) - 1); };
   if constexpr (CPM) {
 #pragma unroll
     for (int n = 0; n < 6; ++n)
@@ -746,7 +756,10 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     // l - 1 wrote.  Slab membership is wave-uniform for x (plane) and y (row)
     // terms and per lane for z terms; lanes / rows / planes outside a slab get
     // an empty descriptor or an offset past it (reads 0) instead of a branch.
-    float PSL[CPM ? T : 1][CPM ? 6 : 1][2][R];
+    float PSL[CPM ? (LPS ? 1 : T) : 1][CPM ? 6 : 1][2][R];
+    // psi of level l of term (n, t), row r (LDS hand-off: one register set
+    // that every level updates in place)
+    auto psl = [&](int l, int n, int t, int r) -> float& { return PSL[CPM && !LPS ? l : 0][CPM ? n : 0][t][r]; };
     if constexpr (CPM) {
 #pragma unroll
       for (int l = 0; l < T; ++l)
@@ -759,6 +772,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
             const int pl = (n < 3 ? X : X - 1) - l;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
+              if (LPS && l > 0) continue;
               float v = 0.f;
               if (l > 0) {
                 v = __uint_as_float(
@@ -776,7 +790,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
                   v += __uint_as_float(
                       __builtin_amdgcn_raw_buffer_load_b32(psi_rsrc(n, t, sd, pl, false), psi_off(n, t, sd, r), 0, 0));
               }
-              PSL[CPM ? l : 0][CPM ? n : 0][t][r] = v;
+              psl(l, n, t, r) = v;
             }
           }
     }
@@ -806,8 +820,8 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
           cc = ZC[zi];
           kk = ZK[zi];
         }
-        const float pn = bb * PSL[CPM ? l : 0][CPM ? n : 0][t][r] + cc * d[0];
-        PSL[CPM ? l : 0][CPM ? n : 0][t][r] = pn;
+        const float pn = bb * psl(l, n, t, r) + cc * d[0];
+        psl(l, n, t, r) = pn;
         const float cr = kk * d[0] + pn;  // 0 off a z slab (identity profile, psi 0)
         return (vec)(sg > 0 ? cr : -cr);
       }
@@ -908,7 +922,26 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         Hp[l][r] = Hc[r];
         Hc[r] = Hn;
       }
-      if constexpr (CPM && T > 1) {
+      if constexpr (LPS) {
+        // swap with the thread's LDS slot of level l: it holds psi^{l+1} of
+        // plane X - l - 1 (this trip's level l + 1 input, written by level l
+        // one trip ago) and takes this level's result for the next trip
+        if (l < T - 1) {
+#pragma unroll
+          for (int n = 0; n < 6; ++n)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              if (!((CAX >> kTermAxis[n][t]) & 1)) continue;
+#pragma unroll
+              for (int r = 0; r < R; ++r) {
+                float& slot = sPS[LPS ? l : 0][LPS ? lps_q(n) : 0][R * w + r][lane];
+                const float nxt = slot;
+                slot = psl(l, n, t, r);
+                psl(l, n, t, r) = nxt;
+              }
+            }
+        }
+      } else if constexpr (CPM && T > 1) {
         // this level's psi to the thread's slot for the next trip's level l + 1
         if (l < T - 1) {
 #pragma unroll
@@ -918,7 +951,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
               if (!((CAX >> kTermAxis[n][t]) & 1)) continue;
 #pragma unroll
               for (int r = 0; r < R; ++r)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(PSL[CPM ? l : 0][CPM ? n : 0][t][r]), scr_rs(),
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(psl(l, n, t, r)), scr_rs(),
                                                       scr_voff, scr_soff(X & 1, l, n, t, r), 0);
             }
         }
@@ -939,7 +972,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             const bool st = xok && ((mbits >> (r * 7 + 6)) & 1u) && ((mbits >> (r * 7 + n)) & 1u);
-            const float v = PSL[CPM ? T - 1 : 0][CPM ? n : 0][t][r];
+            const float v = psl(T - 1, n, t, r);
             if (a == 0) {
               const int sd = xok ? psi_side_x(n, t, pl) : -1;
               __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), psi_rsrc(n, t, sd, pl, true),
@@ -1031,6 +1064,15 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
 #undef MR_LAUNCH
   FDTD_RETURN_LAUNCH_STATUS();
 }
+
+// tile of a multi-step CPML pass: face classes at 4 steps hand psi through
+// LDS in the plain 16-wave x 2-row tile; the rest carry it in registers and
+// thread-private scratch in CPML_NW-wave tiles
+inline bool cpml_lds(int fx, int steps) {
+  const int cax = (fx >> 3) & 7;
+  return steps == 4 && (cax == 1 || cax == 2 || cax == 4);
+}
+inline int cpml_nw(int fx, int steps) { return cpml_lds(fx, steps) ? 16 : CPML_NW; }
 
 // multi-step (T > 1) CPML passes, TF/SF on or off (yee3d_tb_cpml.hip)
 int launch_tb_mr_cpml(int T, int fx, const float* const* ein, const float* const* hin, float* const* eout,

@@ -388,16 +388,16 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
 // automatic x chunk of a multi-row pass over output box O
 int tb_mr_xchunk(int fx, const Box3& O, int steps) {
   const bool cpm = (fx & 56) && steps > 1;
-  const int R = cpm ? CPML_R : 2, NW = cpm ? CPML_NW : TBW;
+  const int R = cpm ? CPML_R : 2, NW = cpm ? cpml_nw(fx, steps) : TBW;
   const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
   const long long gy = cdiv(O.hi[1] - O.lo[1], NW * R - 2 * steps);
   // the 8-wave shape fits two workgroups per CU
-  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) || cpm ? 2 : 1);
+  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) || (cpm && NW == 8) ? 2 : 1);
 }
 
 // bytes of thread-private psi scratch a multi-step CPML pass needs (0: none)
 long long tb_mr_scratch_bytes(int fx, const Box3& O, int steps, int xchunk) {
-  if (!(fx & 56) || steps <= 1 || box_empty(O)) return 0;
+  if (!(fx & 56) || steps <= 1 || box_empty(O) || cpml_lds(fx, steps)) return 0;
   if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
   const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
   const long long gy = cdiv(O.hi[1] - O.lo[1], CPML_NW * CPML_R - 2 * steps);
@@ -570,8 +570,8 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
     // multi-step CPML: uniform media only; the caller's scratch must cover the launch
     if (fx & 3) return (int)hipErrorInvalidValue;
     if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
-    if (!pscr || pscr_bytes < tb_mr_scratch_bytes(fx, O, steps, xchunk) ||
-        tb_mr_scratch_bytes(fx, O, steps, xchunk) > 0xFFFFFFFFLL)
+    const long long need = tb_mr_scratch_bytes(fx, O, steps, xchunk);
+    if ((need > 0 && !pscr) || pscr_bytes < need || need > 0xFFFFFFFFLL)
       return (int)hipErrorInvalidValue;
   }
   return tb_mr_dispatch(fx, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
@@ -582,8 +582,9 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
 
 // scratch bytes fdtd_tb3d_ext_f32 needs for a CPML pass of ``steps`` steps
 // over output box ``obox`` (TF/SF on or off; 0 for single-step passes)
-FDTD_API long long fdtd_tb3d_cpml_scratch_bytes(const int* obox, int xchunk, int steps, int tfsf) {
-  return tb_mr_scratch_bytes(56 | (tfsf ? 4 : 0), make_box(obox), steps, xchunk);
+FDTD_API long long fdtd_tb3d_cpml_scratch_bytes(const int* obox, int xchunk, int steps, int tfsf, int cpml_axes) {
+  const int cax = (cpml_axes & 7) ? (cpml_axes & 7) : 7;
+  return tb_mr_scratch_bytes((cax << 3) | (tfsf ? 4 : 0), make_box(obox), steps, xchunk);
 }
 
 // size of the CpmlDev block the host fills (ABI check)

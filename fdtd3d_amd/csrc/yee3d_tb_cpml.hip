@@ -21,6 +21,22 @@ int cpml_sel(int fx, const float* const* ein, const float* const* hin, float* co
   case F:                                                                                                     \
     return launch_tb_mr<T, 1, CPML_R, F, CPML_NW>(ein, hin, eout, hout, nullptr, nullptr, nb, nb, cb, db, nx, ny, \
                                                   nz, b, O, xchunk, src, sv, tf, gtab, cp, pscr, s);
+  if constexpr (T == 4) {
+    // face classes: psi through LDS, the plain kernel's 16-wave x 2-row tile
+#define FACE_CASE(F)                                                                                          \
+  case F:                                                                                                     \
+    return launch_tb_mr<T, 1, 2, F, 16>(ein, hin, eout, hout, nullptr, nullptr, nb, nb, cb, db, nx, ny, nz, b, O, \
+                                        xchunk, src, sv, tf, gtab, cp, pscr, s);
+    switch (fx) {
+      FACE_CASE(8)
+      FACE_CASE(12)
+      FACE_CASE(16)
+      FACE_CASE(20)
+      FACE_CASE(32)
+      FACE_CASE(36)
+    }
+#undef FACE_CASE
+  }
   switch (fx) {
     CPML_CASE(8)
     CPML_CASE(12)

@@ -280,7 +280,9 @@ class BlockedStepping:
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
                 return
         if self._hybrid3_ok():
-            plan = self._hybrid3_plan(H)
+            # automatic T: 4, where the face classes hand psi through LDS
+            # (csrc/tb3d_mr.h LPS) in the plain kernel's tile
+            plan = self._hybrid3_plan(H if int(cfg.hybrid_block) > 0 or not self.use_cpml else 4)
             if plan is not None:
                 if not hasattr(self, "F_alt"):
                     self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]

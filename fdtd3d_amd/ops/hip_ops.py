@@ -778,7 +778,8 @@ class HipOps:
                 # thread-private psi hand-off between the pass's levels
                 f = self.lib.fdtd_tb3d_cpml_scratch_bytes
                 f.restype = ctypes.c_longlong
-                pscr_bytes = int(f(_box_arr([obox]), c_int(self.tb_xchunk), c_int(steps), c_int(tfsf is not None)))
+                pscr_bytes = int(f(_box_arr([obox]), c_int(self.tb_xchunk), c_int(steps), c_int(tfsf is not None),
+                                   c_int(int(cpml_axes))))
                 pscr = self._scratch(pscr_bytes)
         if (percell and self.dtype == torch.float32 and self.tb_sparse) or tfsf is not None or cpml is not None:
             # multi-row kernel with sparse per-cell coefficients / TF/SF sets

@@ -12,7 +12,7 @@ grep -E "passed|failed|^E " $O/tests.log | cut -c1-300 | head -20
 timeout -k 10 300 python -u tools/mr_bench.py --n 512 --rounds 3 > $O/mr.log 2>&1 || { tail -5 $O/mr.log; exit 1; }
 grep -v amdgpu.ids $O/mr.log
 C512="--3d --sizex 512 --same-size --dtype f32 --warmup-steps 10 --time-steps 40 --json"
-for T in 5 4; do
+for T in 4; do
 timeout -k 10 240 python -m fdtd3d_amd $C512 --scene vacuum --use-pml --pml-type cpml --use-tfsf --hybrid-shell blocked --hybrid-block $T > $O/cfg$T.log 2>&1 || { tail -5 $O/cfg$T.log; exit 1; }
 echo "cpml_tfsf T$T $(grep '^{' $O/cfg$T.log | cut -c1-100)"
 done
