@@ -544,7 +544,7 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
 // table of this pass's first level, from fdtd_tfsf_pass_f32; null: none) and,
 // CPML (``cpml`` = the CpmlDev block as HOST bytes, passed by value to the
 // kernel, ``cpml_axes`` = the axes whose terms the launch carries, 0 = all;
-// passes of more than one step -- 4 or 5 -- need ``pscr``, ``pscr_bytes`` >=
+// 1 or 4 steps per pass; 4-step passes of multi-axis classes need ``pscr``, ``pscr_bytes`` >=
 // fdtd_tb3d_cpml_scratch_bytes; null: none).
 // Other arguments as fdtd_tb3d_v4_f32.
 FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* const* eout,
@@ -554,7 +554,7 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
                                const void* tf, const float* gtab, const void* cpml, int cpml_axes, void* pscr,
                                long long pscr_bytes, void* stream) {
   if (nz % 4 != 0 || steps < 1 || steps > 6) return (int)hipErrorInvalidValue;
-  if (cpml && (steps > 5 || (steps > 1 && steps < 4))) return (int)hipErrorInvalidValue;
+  if (cpml && steps != 1 && steps != 4) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const Box3 O = make_box(obox);

@@ -1,6 +1,7 @@
 // Multi-step CPML variants of the multi-row blocked kernel (tb3d_mr.h):
-// one instantiation per (steps per pass, CPML axes of the box's dependency
-// cone, TF/SF on / off), in a translation unit of their own.  A hybrid pass
+// one instantiation per (CPML axes of the box's dependency cone, TF/SF on /
+// off) at 4 steps per pass (5 measured no faster and doubles the build), in a
+// translation unit of their own.  A hybrid pass
 // (models/blocking.py _hybrid3_plan) advances every shell box T steps with
 // the variant of its class while the plain kernel advances the core.
 
@@ -65,7 +66,6 @@ int launch_tb_mr_cpml(int T, int fx, const float* const* ein, const float* const
                       const CpmlDev* cp, float* pscr, hipStream_t s) {
   switch (T) {
     case 4: return cpml_sel<4>(fx, ein, hin, eout, hout, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, pscr, s);
-    case 5: return cpml_sel<5>(fx, ein, hin, eout, hout, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, pscr, s);
   }
   return (int)hipErrorInvalidValue;
 }

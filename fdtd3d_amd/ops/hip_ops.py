@@ -672,7 +672,7 @@ class HipOps:
 
     # ------------------------------------------------------ temporal blocking
     tfsf_sets_ok = True  # the fp32 blocked kernel applies TfsfSets corrections
-    tb_cpml_steps = (1, 4, 5)  # steps per pass of the in-kernel CPML variants (yee3d_tb_cpml.hip)
+    tb_cpml_steps = (1, 4)  # steps per pass of the in-kernel CPML variants (yee3d_tb_cpml.hip)
 
     def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
                   sets, slot: int = 0) -> torch.Tensor:

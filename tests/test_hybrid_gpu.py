@@ -162,9 +162,9 @@ def test_hybrid_at_scale(gpu, name, extra):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("T,tfsf,point,size", [(5, True, False, (96, 88, 96)), (4, True, True, (80, 72, 96)),
-                                               (4, False, True, (72, 80, 64)), (5, True, False, (64, 64, 128)),
-                                               (5, False, True, (112, 96, 100))])
+@pytest.mark.parametrize("T,tfsf,point,size", [(4, True, False, (96, 88, 96)), (4, True, True, (80, 72, 96)),
+                                               (4, False, True, (72, 80, 64)), (4, True, False, (64, 64, 128)),
+                                               (4, False, True, (112, 96, 100))])
 def test_hybrid3_blocked_shell(gpu, T, tfsf, point, size):
     """Blocked shell (every box one T-step launch: the CPML + TF/SF variant
     of the multi-row kernel carries psi through the pass's levels) vs the

@@ -41,7 +41,7 @@ def main():
     cp = s.cpml.host_table(0)
     cases = []
     cls = {"core": 0, "xwin": 1, "ywin": 2, "zwin": 4}
-    for T in (1, 4, 5):
+    for T in (1, 4):
         cases.append(("T%d plain core" % T, T, wins["core"], None, None, 0))
         cases.append(("T%d tfsf  core" % T, T, wins["core"], g, None, 0))
         for name in ("core", "xwin", "ywin", "zwin"):
