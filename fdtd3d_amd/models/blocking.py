@@ -56,7 +56,7 @@ F32_AUTO_STEPS_TFSF = 4
 
 
 # hybrid_shell modes that take the blocked shell (_hybrid3_plan) when the run fits it
-BLOCKED_SHELL_MODES = ("blocked",)
+BLOCKED_SHELL_MODES = ("blocked", "mixed")
 
 
 def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: int = 1, tfsf: bool = False) -> int:
@@ -282,7 +282,10 @@ class BlockedStepping:
         if self._hybrid3_ok():
             # automatic T: 4, where the face classes hand psi through LDS
             # (csrc/tb3d_mr.h LPS) in the plain kernel's tile
-            plan = self._hybrid3_plan(H if int(cfg.hybrid_block) > 0 or not self.use_cpml else 4)
+            T3 = H if int(cfg.hybrid_block) > 0 or not self.use_cpml else 4
+            plan = self._hybrid3_plan(T3)
+            if plan is not None and getattr(cfg, "hybrid_shell", "auto") == "mixed" and self.use_cpml:
+                plan = self._hybrid4_plan(plan)
             if plan is not None:
                 if not hasattr(self, "F_alt"):
                     self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
@@ -411,6 +414,101 @@ class BlockedStepping:
         upd = {c: self.local_box(c, alloc) for c in self.comps}
         return {"T": T, "v3": True, "core": [dom.to_local(K)], "shell": shell, "upd": upd,
                 "core_cells": box_volume(K)}
+
+    def _hybrid4_plan(self, p3):
+        """Mixed shell: the pieces of a blocked-shell plan whose class runs
+        near the plain kernel's rate -- no CPML in the cone (plain / TF-SF
+        variants) or one x / y face (psi through LDS) -- take blocked
+        launches like the core; the rest (z faces, edges, corners) is stepped
+        in place in F over windows grown ``T - s`` cells into the blocked
+        pieces at step ``s`` (the band rule of ``_hybrid_plan``), then copied
+        to F_alt.  The blocked face pieces' psi (written to the other copy)
+        is copied back over the band's in-place psi afterwards."""
+        T = p3["T"]
+        dom = self.domain
+        alloc = dom.allocated_global()
+        blocked, stepped = [], []
+        for b, cls in p3["shell"]:
+            (blocked if (cls & 7) in (0, 1, 2) else stepped).append((b, cls))
+        if not stepped:
+            return p3
+
+        def grow(b, n):
+            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
+
+        def disjoint_union(boxes):
+            out = []
+            for b in boxes:
+                pieces = [box_intersect(b, alloc)]
+                for o in out:
+                    nxt = []
+                    for q in pieces:
+                        nxt += [r for r in box_subtract(q, o) if not box_empty(r)] if not box_empty(
+                            box_intersect(q, o)) else [q]
+                    pieces = nxt
+                out += [q for q in pieces if not box_empty(q)]
+            return out
+
+        sg = [dom.to_global(b) for b, _ in stepped]
+        # step s (0-based) advances the stepped pieces plus a band T - s deep
+        windows = [disjoint_union([grow(b, T - s) for b in sg]) for s in range(T)]
+        fixes = []
+        for b, cls in blocked:
+            a = {1: 0, 2: 1}.get(cls & 7)
+            if a is None:
+                continue
+            for c in self.comps:
+                for sl in self.cpml.slabs[c]:
+                    if sl.axis != a:
+                        continue
+                    i = box_intersect(b, sl.lbox)
+                    if not box_empty(i):
+                        fixes.append((sl, tuple(slice(i[0][d] - sl.lbox[0][d], i[1][d] - sl.lbox[0][d])
+                                                for d in range(3))))
+        self._tfsf_once = bool(self.cfg.use_tfsf)
+        return dict(p3, v3=False, v4=True, shell=blocked, windows=windows, copy=[b for b, _ in stepped],
+                    psi_fix=fixes)
+
+    def _hybrid4_step(self, T: int) -> None:
+        hp = self.hybrid
+        if T != hp["T"]:
+            for _ in range(T):
+                self.step()
+            return
+        srcs = self._pass_sources(self.t, T)
+        for p in range(self.planes):
+            line0 = None
+            if self.cfg.use_tfsf:
+                # the blocked launches' g tables advance the incident line T
+                # steps; the stepped windows advance it again from here
+                line0 = (self.einc[p].clone(), self.hinc[p].clone())
+            tf = self._tfsf_pass(p, T)
+            cp = self.cpml.host_table(p)
+            P, Q = self.F[p], self.F_alt[p]
+            with self.prof.phase("blocked-core"):
+                for ob in hp["core"]:
+                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p])
+                for ob, cls in hp["shell"]:
+                    cax = cls & 7
+                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf if cls & 8 else None,
+                                     cpml=cp if cax else None, cpml_axes=cax)
+            if line0 is not None:
+                self.einc[p].copy_(line0[0])
+                self.hinc[p].copy_(line0[1])
+        for s in range(T):
+            self.step(hp["windows"][s])
+        with self.prof.phase("shell-copy"):
+            for p in range(self.planes):
+                src = [self.F[p][c] for c in self.comps]
+                dst = [self.F_alt[p][c] for c in self.comps]
+                for b in hp["copy"]:
+                    self.ops.copy_box(src, dst, b)
+                # the blocked face pieces' psi (level T, other copy) over the
+                # stepped band's in-place values
+                for sl, sub in hp["psi_fix"]:
+                    sl.psi[p][sub] = sl.psi_alt[p][sub]
+        for p in range(self.planes):
+            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
 
     def _hybrid3_step(self, T: int) -> None:
         hp = self.hybrid
@@ -896,6 +994,9 @@ class BlockedStepping:
         return srcs
 
     def _hybrid_step(self, T: int) -> None:
+        if self.hybrid.get("v4"):
+            self._hybrid4_step(T)
+            return
         if self.hybrid.get("v3"):
             self._hybrid3_step(T)
             return

@@ -165,14 +165,15 @@ def test_hybrid_at_scale(gpu, name, extra):
 @pytest.mark.parametrize("T,tfsf,point,size", [(4, True, False, (96, 88, 96)), (4, True, True, (80, 72, 96)),
                                                (4, False, True, (72, 80, 64)), (4, True, False, (64, 64, 128)),
                                                (4, False, True, (112, 96, 100))])
-def test_hybrid3_blocked_shell(gpu, T, tfsf, point, size):
+@pytest.mark.parametrize("mode", ["blocked", "mixed"])
+def test_hybrid3_blocked_shell(gpu, T, tfsf, point, size, mode):
     """Blocked shell (every box one T-step launch: the CPML + TF/SF variant
     of the multi-row kernel carries psi through the pass's levels) vs the
     stepped run, from random fields so every slab carries field from step 1;
     2T + 1 steps = two passes and a one-step tail."""
     cfg = SchemeConfig(time_steps=2 * T + 1, scheme="3d", size=size, dtype="f32", pml_size=(5, 6, 7),
                        tfsf_size=(9, 10, 11), scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=tfsf,
-                       hybrid_shell="blocked")
+                       hybrid_shell=mode)
     if point:
         cfg = dataclasses.replace(cfg, use_point_source=True)
     runs = {}
@@ -185,9 +186,12 @@ def test_hybrid3_blocked_shell(gpu, T, tfsf, point, size):
         torch.cuda.synchronize()
         runs[hb] = s
     hy, st = runs[T], runs[1]
-    assert hy.hybrid is not None and hy.hybrid.get("v3"), "blocked shell not selected"
+    assert hy.hybrid is not None and hy.hybrid.get("v4" if mode == "mixed" else "v3"), "plan not selected"
     assert st.hybrid is None
-    assert len({cls for _, cls in hy.hybrid["shell"]}) >= 3  # face / edge / corner classes
+    if mode == "blocked":
+        assert len({cls for _, cls in hy.hybrid["shell"]}) >= 3  # face / edge / corner classes
+    else:
+        assert hy.hybrid["copy"] and hy.hybrid["psi_fix"]  # stepped pieces and blocked faces
     for c in hy.comps:
         x, y = hy.F[0][c].double().cpu(), st.F[0][c].double().cpu()
         scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])
