@@ -99,7 +99,7 @@ class SchemeConfig:
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
-    hybrid_shell: str = "auto"               # auto | stepped | single-pass | blocked (models/blocking.py)
+    hybrid_shell: str = "auto"               # auto | stepped | single-pass | blocked | mixed (models/blocking.py)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
