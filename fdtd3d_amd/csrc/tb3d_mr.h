@@ -1027,7 +1027,6 @@ extern int g_tb_mr_noallin;
 extern int g_tb_mr_xcd;
 extern int g_tb_variant;
 int tb_patch_bits();
-int cpml_scr_l1();
 
 // tile of the multi-step CPML passes: CPML_NW waves x CPML_R rows
 constexpr int CPML_NW = 8, CPML_R = 2;
@@ -1048,9 +1047,8 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
       O, xchunk, src[0], src[1], src[2], src[3], sv,                                                       \
-      (g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1)) |          \
-          (cpml_scr_l1() << 24),                                                                           \
-      tf, gtab, cpv, pscr)
+      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, cpv, \
+      pscr)
   if constexpr (FX != 0) {
     MR_LAUNCH(1, false);  // tuning variants: uniform media only
   } else {

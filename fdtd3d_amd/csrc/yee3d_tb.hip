@@ -51,15 +51,6 @@ int tb_patch_bits() {
   return g_tb_patch;
 }
 int g_tb_variant = 0;  // multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched
-// multi-step CPML scratch loads: 0 agent scope (default), 1 plain (FDTD3D_CPML_SCR_L1=1, tuning)
-int cpml_scr_l1() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("FDTD3D_CPML_SCR_L1");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v;
-}
 }  // namespace tb3d
 
 namespace {
