@@ -416,20 +416,49 @@ class BlockedStepping:
                 "core_cells": box_volume(K)}
 
     def _hybrid4_plan(self, p3):
-        """Mixed shell: the pieces of a blocked-shell plan whose class runs
-        near the plain kernel's rate -- no CPML in the cone (plain / TF-SF
-        variants) or one x / y face (psi through LDS) -- take blocked
-        launches like the core; the rest (z faces, edges, corners) is stepped
-        in place in F over windows grown ``T - s`` cells into the blocked
-        pieces at step ``s`` (the band rule of ``_hybrid_plan``), then copied
-        to F_alt.  The blocked face pieces' psi (written to the other copy)
-        is copied back over the band's in-place psi afterwards."""
+        """Mixed shell: the core and the x / y faces (one CPML axis in their
+        cone: psi through LDS, csrc/tb3d_mr.h LPS, + in-kernel TF/SF) take
+        blocked launches; the rest -- the z slabs over the whole x / y
+        extent and the x-y edge columns -- is stepped in place in F over
+        windows grown ``T - s`` cells into the blocked pieces at step ``s``
+        (the band rule of ``_hybrid_plan``), then copied to F_alt.  The
+        blocked faces' psi (written to the other copy) is copied back over
+        the band's in-place psi afterwards."""
         T = p3["T"]
         dom = self.domain
         alloc = dom.allocated_global()
-        blocked, stepped = [], []
-        for b, cls in p3["shell"]:
-            (blocked if (cls & 7) in (0, 1, 2) else stepped).append((b, cls))
+        # geometry: the x faces (x outside the core's range, y / z inside it)
+        # and the y faces (x / z inside, y outside) are blocked; the z slabs
+        # (whole x / y extent) and the x-y edge columns are stepped -- few,
+        # large stepped windows
+        K = dom.to_global(p3["core"][0])
+        faces = []
+        for a in (0, 1):
+            for lo_, hi_ in ((alloc[0][a], K[0][a]), (K[1][a], alloc[1][a])):
+                if hi_ <= lo_:
+                    continue
+                lo, hi = list(K[0]), list(K[1])
+                lo[a], hi[a] = lo_, hi_
+                if a == 1:
+                    lo[0], hi[0] = K[0][0], K[1][0]
+                faces.append(((tuple(lo), tuple(hi)), a))
+        slabs = [sl for sls in self.cpml.slabs.values() for sl in sls]
+        blocked = []
+        for b, a in faces:
+            g = (tuple(b[0][d] - T - 1 for d in range(3)), tuple(b[1][d] + T + 1 for d in range(3)))
+            ax = 0
+            for sl in slabs:
+                if not box_empty(box_intersect(g, sl.gbox)):
+                    ax |= 1 << sl.axis
+            if ax != 1 << a:
+                return p3  # a face's cone reaches another axis's slab: the blocked plan
+            tf = bool(self.cfg.use_tfsf and self._tfsf_targets_in(dom.to_local(g)))
+            blocked.append((dom.to_local(b), ax | (8 if tf else 0)))
+        rest = [alloc]
+        for b in [K] + [dom.to_global(f) for f, _ in blocked]:
+            rest = [r for q in rest for r in (box_subtract(q, b) if not box_empty(box_intersect(q, b)) else [q])
+                    if not box_empty(r)]
+        stepped = [(dom.to_local(r), 7) for r in rest]
         if not stepped:
             return p3
 
