@@ -213,6 +213,68 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
     return res
 
 
+# BASELINE.json physics configs timed next to the headline on one GPU
+# (``--physics-companion``): the driver's own record then carries them.  The
+# command lines are the ones tools/bench_configs.py uses (reference scenes:
+# zero fields, plane wave / dipole sources, default 10-cell layers and
+# TF/SF distance 20).
+PHYSICS_CONFIGS = (
+    ("cpml_tfsf_512", "3D 512^3 CPML (10 cells) + TF/SF plane wave, fp32 (BASELINE config 3)",
+     ["--3d", "--sizex", "512", "--same-size", "--dtype", "f32", "--scene", "vacuum", "--use-pml",
+      "--pml-type", "cpml", "--use-tfsf"]),
+    ("drude_upml_512", "3D 512^3 Drude sphere r=128 + UPML, fp32 (BASELINE config 4 with absorbing layers)",
+     ["--3d", "--sizex", "512", "--same-size", "--dtype", "f32", "--scene", "drude-sphere", "--use-metamaterials",
+      "--use-pml", "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
+      "--sphere-radius", "128"]),
+)
+
+
+def physics_args(args, n: int):
+    """A physics config's command line on an n^3 grid (sphere scaled along)."""
+    out = list(args)
+    for i, v in enumerate(out):
+        if i and out[i - 1] == "--sizex":
+            out[i] = str(n)
+        elif i and out[i - 1].startswith("--sphere-"):
+            out[i] = str(int(v) * n // 512)
+    return out
+
+
+def run_physics(args, steps: int, warmup: int) -> dict:
+    """One physics config through the regular driver path (runner.build):
+    ``warmup`` untimed steps, then ``steps`` timed steps between device syncs."""
+    import torch
+    from fdtd3d_amd.runner import build
+    from fdtd3d_amd.utils.settings import setup_from_cmd
+
+    status, settings = setup_from_cmd(list(args) + ["--time-steps", str(warmup + steps)], out=open(os.devnull, "w"))
+    if status != 0:
+        raise RuntimeError("bad physics config %s" % " ".join(args))
+    scheme, _, _ = build(settings)
+    scheme.init_scheme()
+    scheme.init_grids()
+    scheme.perform_steps(warmup)
+    cuda = scheme.device.type == "cuda"
+    if cuda:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    scheme.perform_steps(steps)
+    if cuda:
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    size = scheme.cfg.size
+    res = {"value": round(size[0] * size[1] * size[2] * steps / dt / 1e6, 1),
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+           "hybrid": ("v3" if scheme.hybrid.get("v3") else "stepped-shell") if getattr(scheme, "hybrid", None)
+           else "none",
+           "energy": scheme.field_energy(),
+           "max_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2) if cuda else 0.0}
+    del scheme
+    if cuda:
+        torch.cuda.empty_cache()
+    return res
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +290,11 @@ def main(argv=None) -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--fp64-companion", default="auto", choices=("auto", "on", "off"),
                     help="repeat the measurement in fp64 and report it under 'fp64' (auto: one GPU, fp32 runs)")
+    ap.add_argument("--physics-companion", default="auto", choices=("auto", "on", "off"),
+                    help="also time the 512^3 CPML + TF/SF and Drude + UPML configs (10 steps each) and report them "
+                         "under 'physics' (auto: one GPU, fp32 runs)")
+    ap.add_argument("--physics-steps", type=int, default=10)
+    ap.add_argument("--physics-size", type=int, default=512, help="edge of the physics configs' cubic grid")
     ap.add_argument("--split", action="store_true", help="use the split E / H kernels instead of the fused one")
     ap.add_argument("--xchunk", type=int, default=0)
     ap.add_argument("--buffer-size", type=int, default=1, help="halo depth (deep halo when > 1)")
@@ -283,6 +350,16 @@ def main(argv=None) -> int:
             fp64 = run_one(a, "f64", world, rank, device, backend, core)
         except Exception as e:  # the headline line must still be printed
             fp64 = {"error": "%s: %s" % (type(e).__name__, e)}
+    physics = None
+    if a.physics_companion == "on" or (a.physics_companion == "auto" and world == 1 and a.dtype == "f32"
+                                       and backend == "hip"):
+        physics = {}
+        for name, desc, args in PHYSICS_CONFIGS:
+            try:
+                physics[name] = dict(run_physics(physics_args(args, a.physics_size), a.physics_steps, 5),
+                                     desc=desc)
+            except Exception as e:  # the headline line must still be printed
+                physics[name] = {"error": "%s: %s" % (type(e).__name__, e), "desc": desc}
     if rank == 0:
         par = "x".join(str(v) for v in topo)
         cells = size[0] * size[1] * size[2]
@@ -329,6 +406,8 @@ def main(argv=None) -> int:
             else:
                 out["fp64"] = {"value": round(fp64["mcells"], 1), "ms_per_step": round(fp64["dt"] / a.steps * 1e3, 4),
                                "time_block": fp64["tb"], "energy": fp64["energy"]}
+        if physics is not None:
+            out["physics"] = physics
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
