@@ -248,6 +248,8 @@ def run_physics(args, steps: int, warmup: int) -> dict:
     from fdtd3d_amd.utils.settings import setup_from_cmd
 
     status, settings = setup_from_cmd(list(args) + ["--time-steps", str(warmup + steps)], out=open(os.devnull, "w"))
+    if torch.cuda.is_available():
+        torch.cuda.reset_peak_memory_stats()
     if status != 0:
         raise RuntimeError("bad physics config %s" % " ".join(args))
     scheme, _, _ = build(settings)
@@ -265,8 +267,7 @@ def run_physics(args, steps: int, warmup: int) -> dict:
     size = scheme.cfg.size
     res = {"value": round(size[0] * size[1] * size[2] * steps / dt / 1e6, 1),
            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
-           "hybrid": ("v3" if scheme.hybrid.get("v3") else "stepped-shell") if getattr(scheme, "hybrid", None)
-           else "none",
+           "hybrid": scheme.hybrid.get("kind", "stepped-shell") if getattr(scheme, "hybrid", None) else "none",
            "energy": scheme.field_energy(),
            "max_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2) if cuda else 0.0}
     del scheme

@@ -58,7 +58,18 @@ struct ChainComp {
   int a0, a1, sg0, sg1, aD, aA, aB;
   Box3 box;
   Box3 pbox;                // plain Yee cells folded into this launch (empty: none)
+  Box3 dbox;                // storage box of the D / D1 levels (empty: full-grid arrays)
 };
+
+// index of cell n in the D / D1 levels: region-local storage over the
+// component's chain box (models/regions.py) or the full-grid offset
+template <typename T>
+__device__ __forceinline__ size_t aux_off(const ChainComp<T>& q, const int* n, size_t off) {
+  if (q.dbox.hi[0] <= q.dbox.lo[0]) return off;
+  return ((size_t)(n[0] - q.dbox.lo[0]) * (q.dbox.hi[1] - q.dbox.lo[1]) + (n[1] - q.dbox.lo[1])) *
+             (q.dbox.hi[2] - q.dbox.lo[2]) +
+         (n[2] - q.dbox.lo[2]);
+}
 
 // One component of one cell in one go (the dispersive form: see the kernel).
 template <typename T, bool DRUDE, bool CELL>
@@ -82,10 +93,11 @@ __device__ __forceinline__ void chain_cell(const ChainComp<T>& q, bool kind_e, c
     return;
   }
   // ---- every load first
+  const size_t da = aux_off(q, n, off);
   const T x0 = q.s0[off], x1 = q.s1[off];
   const T y0 = kind_e ? q.s0[off - s0] : q.s0[off + s0];
   const T y1 = kind_e ? q.s1[off - s1] : q.s1[off + s1];
-  const T D = q.D[off];
+  const T D = q.D[da];
   const T E = q.E[off];
   const T caD = q.caD[n[q.aD]], cbD = q.cbD[n[q.aD]];
   const T caE = q.caE[n[q.aA]], ica = q.ica[n[q.aA]];
@@ -93,9 +105,9 @@ __device__ __forceinline__ void chain_cell(const ChainComp<T>& q, bool kind_e, c
   const T cell = CELL ? q.cell[off] : T(1);
   T Dp = 0, D1 = 0, D1p = 0, b0 = 0, b1 = 0, b2 = 0, m1 = 0, m2 = 0;
   if (DRUDE) {
-    Dp = q.Dp[off];
-    D1 = q.D1[off];
-    D1p = q.D1p[off];
+    Dp = q.Dp[da];
+    D1 = q.D1[da];
+    D1p = q.D1p[da];
     if (q.id) {
       // material-ID + LUT: one byte per cell instead of 20 (a Drude scene
       // holds a handful of distinct coefficient tuples: vacuum, the
@@ -126,8 +138,8 @@ __device__ __forceinline__ void chain_cell(const ChainComp<T>& q, bool kind_e, c
   }
   const T En = caE * E + q.s * cell * ica * (cbEa * nw + ccEa * old);
   // ---- stores
-  q.Dn[off] = Dn;
-  if (DRUDE) q.D1n[off] = nw;
+  q.Dn[da] = Dn;
+  if (DRUDE) q.D1n[da] = nw;
   q.E[off] = En;
 }
 
@@ -145,6 +157,7 @@ __device__ __forceinline__ V pick3(int a, V x, V y, V z) {
 template <typename T>
 struct ChainIn {
   int mode;  // 0 skip, 1 chain, 2 plain (folded box)
+  size_t da; // index into the D / D1 levels
   T x0, x1, y0, y1, D, E, caD, cbD, caE, ica, cbEa, ccEa, cell, Dp, D1, D1p, b0, b1, b2, m1, m2;
 };
 
@@ -168,7 +181,8 @@ __device__ __forceinline__ ChainIn<T> chain_load(const ChainComp<T>& q, bool kin
     v.cell = q.pcell ? q.pcell[off] : q.pcb;
     return v;
   }
-  v.D = q.D[off];
+  v.da = aux_off(q, n, off);
+  v.D = q.D[v.da];
   const int nD = pick3(q.aD, n[0], n[1], n[2]), nA = pick3(q.aA, n[0], n[1], n[2]);
   const int nB = pick3(q.aB, n[0], n[1], n[2]);
   v.caD = q.caD[nD];
@@ -179,9 +193,9 @@ __device__ __forceinline__ ChainIn<T> chain_load(const ChainComp<T>& q, bool kin
   v.ccEa = q.ccEa[nB];
   v.cell = CELL ? q.cell[off] : T(1);
   if (DRUDE) {
-    v.Dp = q.Dp[off];
-    v.D1 = q.D1[off];
-    v.D1p = q.D1p[off];
+    v.Dp = q.Dp[v.da];
+    v.D1 = q.D1[v.da];
+    v.D1p = q.D1p[v.da];
     if (q.id) {
       // material-ID + LUT: one byte per cell instead of 20 (a Drude scene
       // holds a handful of distinct coefficient tuples: vacuum, the
@@ -220,8 +234,8 @@ __device__ __forceinline__ void chain_finish(const ChainComp<T>& q, bool kind_e,
     old = v.D1;
   }
   const T En = v.caE * v.E + q.s * v.cell * v.ica * (v.cbEa * nw + v.ccEa * old);
-  q.Dn[off] = Dn;
-  if (DRUDE) q.D1n[off] = nw;
+  q.Dn[v.da] = Dn;
+  if (DRUDE) q.D1n[v.da] = nw;
   q.E[off] = En;
 }
 
@@ -418,6 +432,7 @@ template <typename T>
 bool chain_v4_ok(const ChainComp<T>* q, int nz) {
   if (sizeof(T) != 4 || (nz & 3) != 0 || !g_chain_v4) return false;
   for (int c = 0; c < 3; ++c) {
+    if (!box_empty(q[c].dbox)) return false;  // the float4 form indexes full-grid levels
     const void* ps[] = {q[c].E, q[c].Dn, q[c].D, q[c].s0, q[c].s1, q[c].caD, q[c].cbD, q[c].caE, q[c].ica,
                         q[c].cbEa, q[c].ccEa, q[c].cell, q[c].pcell};
     for (const void* p : ps)
@@ -427,7 +442,7 @@ bool chain_v4_ok(const ChainComp<T>* q, int nz) {
 }
 
 constexpr int CP_PER = 24;  // pointers per component
-constexpr int CI_PER = 19;  // ints per component
+constexpr int CI_PER = 25;  // ints per component
 
 template <typename T>
 ChainComp<T> make_comp(const void* const* P, double s, const int* I) {
@@ -466,6 +481,7 @@ ChainComp<T> make_comp(const void* const* P, double s, const int* I) {
   q.aB = I[6];
   q.box = make_box(I + 7);
   q.pbox = make_box(I + 13);
+  q.dbox = make_box(I + 19);
   return q;
 }
 
@@ -483,8 +499,13 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
     U = box_union(U, q[c].pbox);
   }
   if (box_empty(U)) return 0;
-  for (int c = 0; c < 3; ++c)
+  for (int c = 0; c < 3; ++c) {
     if (!box_empty(q[c].box) && (q[c].cell != nullptr) != cell) return (int)hipErrorInvalidValue;
+    // region-local levels: every chain cell inside the storage box
+    if (!box_empty(q[c].box) && !box_empty(q[c].dbox))
+      for (int d = 0; d < 3; ++d)
+        if (q[c].box.lo[d] < q[c].dbox.lo[d] || q[c].box.hi[d] > q[c].dbox.hi[d]) return (int)hipErrorInvalidValue;
+  }
   if constexpr (sizeof(T) == 4) {
     if (!drude && chain_v4_ok(q, nz)) {
       // 4-cell z groups: the union box widened to whole groups (per-element
@@ -519,7 +540,9 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
 // (unused: nullptr; a non-null id replaces b0 .. ma2 by lut[5 id ..]), S[2c] = scalar of the
 // E-from-D term, S[2c + 1] = plain-part coefficient, I[19c ..] = curl axes a0 a1, signs sg0
 // sg1, UPML axes aD aCa aCb, chain box lo[3] hi[3], plain box lo[3] hi[3] (empty: skipped;
-// the plain box holds cells updated F += c (curl) in the same launch).
+// the plain box holds cells updated F += c (curl) in the same launch), storage box of the D /
+// D1 levels lo[3] hi[3] (empty: full-grid levels; else they hold that box only, x-major, z
+// fastest, and the chain box must lie inside it).
 FDTD_API int fdtd_chain3d_f32(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny,
                               int nz, void* s) {
   return launch_chain<float>(P, S, I, drude, kind_e, ny, nz, RowRanges{nullptr, 0, 0, 0, 0}, (hipStream_t)s);

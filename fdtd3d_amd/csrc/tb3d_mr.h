@@ -1,7 +1,6 @@
 // Multi-row temporally blocked fp32 3D Yee kernel (k_tb3d_mr) and its
-// launcher, shared by yee3d_tb.hip (plain / TF-SF / sparse per-cell variants,
-// the host API) and yee3d_tb_cpml.hip (the multi-step CPML variants, a
-// translation unit of their own so the two compile in parallel).
+// launcher (yee3d_tb.hip holds the host API): plain, sparse per-cell
+// coefficient, TF/SF and boundary-history variants.
 #pragma once
 
 #include <cstdio>
@@ -55,9 +54,10 @@ struct TbSrc {
 // direction along x or y the incident value a target sees depends on its
 // index along that axis only (`va`), so each pass precomputes, per level,
 // g = sign * projection * interpolated incident line at every index of a set
-// (k_tfsf_pass below) and the kernels add g to the target's curl before the
-// coefficient multiply -- from SCALAR loads (wave-uniform index), which do not
-// queue behind the vector prefetch.
+// (k_tfsf_pass in yee3d_tb.hip) and the kernel adds g to the target's curl
+// before the coefficient multiply.  The table and the g values are read
+// through the constant address space: wave-uniform scalar loads that wait on
+// the scalar counter, never behind the vector plane prefetch.
 constexpr int TF_MAX_SETS = 24;
 struct TfSet {
   int n;          // component 0..5 = Ex Ey Ez Hx Hy Hz
@@ -66,40 +66,26 @@ struct TfSet {
   int va;         // table axis (0 x, 1 y)
   int goff;       // first g entry of the set inside one level
 };
-// CPML convolution terms (fdtd3d_amd/models/cpml.py, layout of
-// yee3d_cpml.hip): per (component, term axis) the low / high psi slabs, their
-// ranges along the axis and the b / c / (1/kappa - 1) profiles (identity
-// outside the slabs).  psi index of a slab along x: ((i-lo) ny + j) nz + k;
-// along y: (i w + j-lo) nz + k; along z: (i ny + j) w + k-lo (w = hi - lo).
-struct CpmlTerm {
-  const float* psi[2];  // read (time n) ...
-  float* out[2];        // ... and written (time n + 1): ping-pong, because the
-                        // halo cells a tile recomputes belong to neighbour tiles
-                        // that may already have advanced them
-  int lo[2], hi[2];
-  const float* b;
-  const float* c;
-  const float* k;
-};
-struct CpmlDev {
-  CpmlTerm t[6][3];  // [Ex Ey Ez Hx Hy Hz][term axis]
-};
-// curl terms of each component: (axis, sign), Ex = +dHz/dy - dHy/dz etc.
-__device__ constexpr int kTermAxis[6][2] = {{1, 2}, {2, 0}, {0, 1}, {2, 1}, {0, 2}, {1, 0}};
-
-// the CPML table travels by value in the kernel arguments: its pointers and
-// profile reads are then wave-uniform scalar loads from the kernarg segment --
-// SGPR descriptors, no waterfall loop, and profile loads that wait on the
-// scalar counter instead of queueing behind the vector prefetch (a copy in
-// LDS, or any generic-pointer view of the argument, hands every field back in
-// VGPRs).  The non-CPML variants carry it unread.
-
 struct TfDev {
   int nsets;
   int ld;                   // g entries per level
   int xpl[2][2];            // [E / H][low / high] x-face planes (-1: none)
   TfSet s[TF_MAX_SETS];
 };
+typedef const __attribute__((address_space(4))) TfDev* TfC;
+
+// Boundary history (feature bit 8) of a hybrid pass whose stepped shell has
+// no band (models/blocking.py, "history shell"): the owned cells of the
+// output box O on its three LOW faces store E after every level, those on
+// its three HIGH faces H after every level but the last.  A shell cell next
+// to O reads exactly these values at the intermediate time levels (E^{n+1}
+// from H^{n+1/2} at i and i-1, H from E at i and i+1), so the stepped shell
+// never recomputes core cells.  Layout, element units: ((kind * T + l) * 3
+// + axis) * 2 + slot) * hls + cell, kind 0 = E / low faces, 1 = H / high
+// faces, slot = the two components off the face axis (x: y z, y: x z, z: x
+// y), cell = the face cell's index in the full array's plane of that
+// orientation: x face j * nz + k, y face i * nz + k, z face i * ny + j (hls
+// >= the largest of ny nz, nx nz, nx ny).
 
 // Memory access through buffer descriptors: one descriptor per (array, x
 // plane) built in SGPRs from the wave-uniform plane index, plus ONE 32-bit
@@ -221,23 +207,13 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     const float4* __restrict__ ce4, const float4* __restrict__ ch4, Box3 BE, Box3 BH, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz,
-    const TfDev* __restrict__ tf, const float* __restrict__ gtab, const CpmlDev CP,
-    float* __restrict__ pscr) {
+    const TfDev* __restrict__ tf, const float* __restrict__ gtab, float* __restrict__ hist, int hls) {
   // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF,
-  // 8 / 16 / 32 CPML terms along x / y / z (a launch over a shell box carries
-  // only the axes whose slabs its dependency cone reaches).  A CPML pass of
-  // T > 1 steps hands each level's psi to the next level through `pscr`,
-  // thread-private scratch (see the level loop)
+  // 8 boundary history
   constexpr int PC = FX & 3;
   constexpr bool TFS = FX & 4;
-  constexpr int CAX = (FX >> 3) & 7;
-  constexpr bool CPM = CAX != 0;
-  // single-axis (face) CPML classes of 16-wave multi-step passes hand psi from
-  // level to level through LDS (4 terms x (T - 1) levels x the tile, 32 KiB
-  // per level) instead of registers / scratch: the register footprint of the
-  // plain kernel, 4 waves per SIMD and 32-row tiles
-  constexpr bool LPS = CPM && T > 1 && NW == 16 && (CAX == 1 || CAX == 2 || CAX == 4);
-  static_assert(V == 1 || !FX, "sparse coefficients / TF/SF: scalar lanes");
+  constexpr bool HIS = FX & 8;
+  static_assert(V == 1 || !FX, "sparse coefficients / TF/SF / history: scalar lanes");
   constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
   static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
   typedef typename VT<V>::f vec;
@@ -248,15 +224,6 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   __shared__ vec sX[2][4][NW][64];
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);  // one wave per y (SGPR)
-  // the TF/SF table lives in LDS for the kernel's life: its fields are read in
-  // many branches (with dynamic set indices)
-  __shared__ unsigned sTFraw[TFS ? sizeof(TfDev) / 4 : 1];
-  if constexpr (TFS) {
-    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(TfDev) / 4); q += 64 * NW)
-      sTFraw[q] = ((const unsigned*)tf)[q];
-  }
-  if constexpr (TFS) __syncthreads();
-  const TfDev& TF = *reinterpret_cast<const TfDev*>(sTFraw);
 
   // Tile of this workgroup.  A row of a tile starts at an arbitrary z (the
   // stride is the 64 - 2T owned cells), so its 64 cells straddle three
@@ -360,123 +327,109 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   }
   const bool wave_e = PCE && __any(inb & ((1u << R) - 1u));
   const bool wave_h = PCH && __any(inb >> R);
-  // TF/SF.  x-face sets (one plane each, all rows / lanes of the TF box) are
-  // rare per wave and go through scalar loads when a level hits their plane.
-  // y / z-face sets (one row or one lane column) touch few waves but every
-  // level of every trip of those waves, so each wave parks up to TF_SLOTS of
-  // them per kind in slots: slot metadata in VGPR lanes (read back with
-  // readlane at a compile-time lane), a per-lane bit per (slot, row) for the
-  // cells it covers, and per trip ONE vector load of the g values of every
-  // (slot, level, row) -- issued before the field prefetch, so the levels
-  // never wait behind it.
-  constexpr int TF_SLOTS = 6;                      // per kind
-  constexpr int TF_ENT = 2 * TF_SLOTS * T * R;     // g entries per trip (<= 128 for T <= 5)
-  static_assert(!TFS || TF_ENT <= 128, "TF/SF: at most 5 steps per pass");
-  unsigned tf_wx[2] = {0u, 0u};
-  unsigned tf_ov[2] = {0u, 0u};  // face sets beyond the slots: the scalar path every level
-  int tf_xe0 = -1, tf_xe1 = -1, tf_xh0 = -1, tf_xh1 = -1;  // x-face planes (E / H sets)
-  int tf_na0 = 0, tf_na1 = 0;                      // slots in use (E / H)
-  unsigned tf_lbits = 0;                           // bit slot * R + r: this lane in the slot's set, row r
-  int tf_mx = 0;                                   // lane s: x range of slot s (lo | hi << 16)
-  int tf_mn = 0;                                   // lane s: component of slot s
-  int tf_gb0 = 0, tf_gb1 = 0;                      // g index of entry lane / lane + 64 (plus X when va = 0)
-  bool tf_ok0 = false, tf_ok1 = false;
-  int tf_va = 0, tf_ld = 0;
+
+  // TF/SF.  Per kind, the sets whose y / z extent this wave's rows and lanes
+  // meet are found once: y / z-face sets (a row or a lane column, every
+  // level of every trip inside their x range) in tf_face, x-face sets (one
+  // plane, all rows / lanes of the TF box) in tf_xs, added to the candidates
+  // only on a level whose plane is one of the kind's two x-face planes.  A
+  // wave away from every face therefore pays two scalar compares per level;
+  // a candidate costs a few scalar loads (set bounds, its g value) and one
+  // select + add per row.
+  const TfC TFc = (TfC)tf;
+  unsigned tf_face[2] = {0u, 0u}, tf_xs[2] = {0u, 0u};
+  int tf_xp[2][2] = {{-1, -1}, {-1, -1}};
+  int tf_ld = 0;
   if constexpr (TFS) {
-    const int ns = TF.nsets;
-    const int ld = TF.ld;
-    tf_ld = ld;
-    tf_va = TF.s[0].va;
-    int na[2] = {0, 0};
+    const int ns = TFc->nsets;
+    tf_ld = TFc->ld;
     for (int si = 0; si < ns; ++si) {
-      const TfSet& S = TF.s[si];
-      unsigned rb = 0;
+      const int lo1 = TFc->s[si].lo[1], hi1 = TFc->s[si].hi[1];
+      const int lo2 = TFc->s[si].lo[2], hi2 = TFc->s[si].hi[2];
+      bool rows = false;
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int j = jw + r;
-        rb |= (kin && j >= S.lo[1] && j < S.hi[1] && kb >= S.lo[2] && kb < S.hi[2]) ? (1u << r) : 0u;
-      }
-      if (!__any(rb != 0u)) continue;
-      const int k = S.n < 3 ? 0 : 1;
-      if (S.fa == 0) {
-        tf_wx[0] |= k == 0 ? (1u << si) : 0u;
-        tf_wx[1] |= k == 1 ? (1u << si) : 0u;
-        continue;
-      }
-      const int a = k == 0 ? na[0] : na[1];
-      if (a >= TF_SLOTS) {
-        tf_ov[0] |= k == 0 ? (1u << si) : 0u;
-        tf_ov[1] |= k == 1 ? (1u << si) : 0u;
-        continue;
-      }
-      const int slot = k * TF_SLOTS + a;
-      if (k == 0) ++na[0]; else ++na[1];
-      tf_lbits |= rb << (slot * R);
-      if (lane == slot) {
-        tf_mx = S.lo[0] | (S.hi[0] << 16);
-        tf_mn = S.n;
-      }
-      // entries (slot, l, r) -> entry q = (slot * T + l) * R + r
-#pragma unroll
-      for (int l = 0; l < T; ++l)
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int q = (slot * T + l) * R + r;
-          // level l: E sets on plane X - l, H sets on X - l - 1
-          const int base = l * ld + S.goff + (S.va == 0 ? -S.lo[0] - l - k : (jw + r) - S.lo[1]);
-          if (lane == q) { tf_gb0 = base; tf_ok0 = true; }
-          if (lane + 64 == q) { tf_gb1 = base; tf_ok1 = true; }
-        }
+      for (int r = 0; r < R; ++r) rows |= jw + r >= lo1 && jw + r < hi1;
+      if (!rows || !__any(kin && kb >= lo2 && kb < hi2)) continue;
+      const int k = TFc->s[si].n < 3 ? 0 : 1;
+      if (TFc->s[si].fa == 0)
+        tf_xs[k] |= 1u << si;
+      else
+        tf_face[k] |= 1u << si;
     }
-    tf_na0 = na[0];
-    tf_na1 = na[1];
-    tf_xe0 = TF.xpl[0][0];
-    tf_xe1 = TF.xpl[0][1];
-    tf_xh0 = TF.xpl[1][0];
-    tf_xh1 = TF.xpl[1][1];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      tf_xp[k][0] = TFc->xpl[k][0];
+      tf_xp[k][1] = TFc->xpl[k][1];
+    }
   }
-  const bool tf_slots = TFS && (tf_na0 + tf_na1) > 0;
-  float tf_g0 = 0.f, tf_g1 = 0.f;  // this trip's g entries (lane q, q + 64)
   // add the TF/SF corrections of kind k at level l, plane p, row r to the curls
   auto tf_apply = [&](int k, int l, int p, int r, vec& c0, vec& c1, vec& c2) {
     if constexpr (TFS) {
-      // y / z-face slots
-      if (tf_slots) {
-#pragma unroll
-        for (int a = 0; a < TF_SLOTS; ++a) {
-          if (a >= (k == 0 ? tf_na0 : tf_na1)) break;
-          const int slot = k * TF_SLOTS + a;
-          const int xr = __builtin_amdgcn_readlane(tf_mx, slot);
-          if ((unsigned)(p - (xr & 0xffff)) >= (unsigned)((xr >> 16) - (xr & 0xffff))) continue;
-          const int q = (slot * T + l) * R + r;
-          const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q < 64 ? tf_g0 : tf_g1), q & 63));
-          const float gl = ((tf_lbits >> (slot * R + r)) & 1u) ? g : 0.f;
-          const int c = __builtin_amdgcn_readlane(tf_mn, slot) - 3 * k;
-          c0 = c0 + (vec)(c == 0 ? gl : 0.f);
-          c1 = c1 + (vec)(c == 1 ? gl : 0.f);
-          c2 = c2 + (vec)(c == 2 ? gl : 0.f);
-        }
-      }
-      // x-face sets on their plane
-      const bool xp = k == 0 ? (p == tf_xe0 || p == tf_xe1) : (p == tf_xh0 || p == tf_xh1);
-      unsigned cand = (xp ? (k == 0 ? tf_wx[0] : tf_wx[1]) : 0u) | (k == 0 ? tf_ov[0] : tf_ov[1]);
+      unsigned cand = tf_face[k];
+      if (p == tf_xp[k][0] || p == tf_xp[k][1]) cand |= tf_xs[k];
       const int j = jw + r;
       while (cand) {
         const int si = __builtin_ctz(cand);
         cand &= cand - 1u;
-        const TfSet& S = TF.s[si];
-        if ((unsigned)(p - S.lo[0]) >= (unsigned)(S.hi[0] - S.lo[0]) || j < S.lo[1] || j >= S.hi[1]) continue;
-        const float g = gtab[l * TF.ld + S.goff + (S.va == 0 ? p - S.lo[0] : j - S.lo[1])];
+        const int lo0 = TFc->s[si].lo[0], hi0 = TFc->s[si].hi[0];
+        const int lo1 = TFc->s[si].lo[1], hi1 = TFc->s[si].hi[1];
+        if ((unsigned)(p - lo0) >= (unsigned)(hi0 - lo0) || j < lo1 || j >= hi1) continue;
+        const int gi = l * tf_ld + TFc->s[si].goff + (TFc->s[si].va == 0 ? p - lo0 : j - lo1);
+        const float g = cload(gtab, gi);
         // g on the set's lanes, 0 elsewhere, added to the set's component by
         // selects (conditional adds make the compiler index a scratch array)
-        const float gl = (kb >= S.lo[2] && kb < S.hi[2]) ? g : 0.f;
-        const int c = S.n - 3 * k;
+        const float gl = (kb >= TFc->s[si].lo[2] && kb < TFc->s[si].hi[2]) ? g : 0.f;
+        const int c = TFc->s[si].n - 3 * k;
         c0 = c0 + (vec)(c == 0 ? gl : 0.f);
         c1 = c1 + (vec)(c == 1 ? gl : 0.f);
         c2 = c2 + (vec)(c == 2 ? gl : 0.f);
       }
     }
   };
+
+  // Boundary history (HIS): wave-uniform tests pick the few waves / levels
+  // that own a face cell of O (x faces: one plane; y faces: one row; z
+  // faces: one lane of the tiles at either z end); the stores are issued
+  // behind those branches, lanes off the face dropped by the offset.  Face
+  // layers are indexed like the full array's planes (x face j * nz + k, y
+  // face i * nz + k, z face i * ny + j), so the x / y offsets are the row
+  // offset roff plus a wave-uniform term: no per-lane state lives across
+  // the x loop.
+  const bool hz_lo = HIS && __any(lane_own && kb == O.lo[2]);
+  const bool hz_hi = HIS && __any(lane_own && kb == O.hi[2] - 1);
+  auto hrs = [&]() -> Rsrc { return __builtin_amdgcn_make_buffer_rsrc((void*)hist, (short)0, -1, 0x00020000); };
+  // slot offset (bytes) of (kind, level, axis, component slot).  The layer
+  // stride goes through an empty asm at every use: hoisted out of the x
+  // loop, the 12 T slot offsets would each hold an SGPR for the whole kernel
+  // (spilled to VGPR lanes, which then spill the field registers)
+  auto hso = [&](int kind, int l, int a, int q) -> int {
+    int h4 = hls * 4;
+    asm volatile("" : "+s"(h4));
+    return (((kind * T + l) * 3 + a) * 2 + q) * h4;
+  };
+  // store the two off-axis components of (x, y, z) for the face of axis a
+  auto hput = [&](int kind, int l, int a, unsigned off, const vec& vx, const vec& vy, const vec& vz) {
+    const vec& v0 = a == 0 ? vy : vx;
+    const vec& v1 = a == 2 ? vy : vz;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v0[0]), hrs(), off, hso(kind, l, a, 0), 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v1[0]), hrs(), off, hso(kind, l, a, 1), 0);
+  };
+  // face cells of kind `kind` (0: E on the low faces, 1: H on the high faces)
+  // on plane p, row r at level l
+  auto hist_store = [&](int kind, int l, int p, int r, const vec& vx, const vec& vy, const vec& vz) {
+    if constexpr (HIS) {
+      if (p < i0 || p >= i1) return;
+      const int j = jw + r;
+      const bool own = ((mbits >> ((r * 7 + 6) * V)) & 1u) != 0u;
+      if (p == (kind == 0 ? O.lo[0] : O.hi[0] - 1)) hput(kind, l, 0, own ? roff[r] : 0xF0000000u, vx, vy, vz);
+      if (j == (kind == 0 ? O.lo[1] : O.hi[1] - 1))
+        hput(kind, l, 1, own ? roff[r] + (unsigned)((p - j) * nz) * 4u : 0xF0000000u, vx, vy, vz);
+      if (kind == 0 ? hz_lo : hz_hi)
+        hput(kind, l, 2, own && kb == (kind == 0 ? O.lo[2] : O.hi[2] - 1) ? (unsigned)(p * ny + j) * 4u : 0xF0000000u,
+             vx, vy, vz);
+    }
+  };
+
   typedef unsigned u3 __attribute__((ext_vector_type(3)));
   auto coef_ld = [&](const float4* arr, const Box3& B, unsigned off, size_t pl, int p) -> u3 {
     const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)arr + (size_t)(p - B.lo[0]) * pl),
@@ -506,118 +459,6 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
       sC[sl][2][R * w + r][lane] = __uint_as_float(v.z);
     }
   }
-
-  // CPML helpers.  Terms are (component n, t):
-  // axis kTermAxis[n][t].  y terms: Ex.0 Ez.1 Hx.1 Hz.0; z terms: Ex.1 Ey.0
-  // Hx.0 Hy.1; x terms: the rest.
-  auto ytm_index = [](int n) -> int { return n == 0 ? 0 : (n == 2 ? 1 : (n == 3 ? 2 : 3)); };
-  auto ztm_index = [](int n) -> int { return n == 0 ? 0 : (n == 1 ? 1 : (n == 3 ? 2 : 3)); };
-  // slab side holding index v along the term's axis (-1: none)
-  auto side_of = [&](const CpmlTerm& tm, int v) -> int {
-    return (tm.psi[0] && v >= tm.lo[0] && v < tm.hi[0]) ? 0 : ((tm.psi[1] && v >= tm.lo[1] && v < tm.hi[1]) ? 1 : -1);
-  };
-  auto psi_side_x = [&](int n, int t, int pl) -> int {
-    return kTermAxis[n][t] == 0 ? side_of(CP.t[n][0], pl) : -1;
-  };
-  auto psi_side_y = [&](int n, int t, int j) -> int {
-    return kTermAxis[n][t] == 1 ? side_of(CP.t[n][1], j) : -1;
-  };
-  // descriptor of plane pl of the side-sd slab of term (n, t), read or written
-  // copy; an empty one (every access dropped / reads 0) for sd < 0 or a plane
-  // outside the grid -- so every psi access is issued unconditionally and the
-  // compiler's vmcnt bookkeeping never has to drain the plane prefetch
-  auto psi_rsrc = [&](int n, int t, int sd, int pl, bool wr) -> Rsrc {
-    const int a = kTermAxis[n][t];
-    const CpmlTerm& tm = CP.t[n][a];
-    const bool ok = sd >= 0 && pl >= 0 && pl < nx;
-    const int s_ = sd > 0 ? 1 : 0;
-    const int wd = tm.hi[s_] - tm.lo[s_];
-    const size_t pe_ = a == 0 ? (size_t)ny * nz : (a == 1 ? (size_t)wd * nz : (size_t)ny * wd);
-    const size_t first = ok ? (a == 0 ? (size_t)(pl - tm.lo[s_]) * pe_ : (size_t)pl * pe_) : 0;
-    const float* base = wr ? tm.out[s_] : tm.psi[s_];
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(base + first), (short)0, ok ? (int)(pe_ * 4) : 0, 0x00020000);
-  };
-  // lane byte offset of row r in that plane (past the plane for lanes outside the slab)
-  auto psi_off = [&](int n, int t, int sd, int r) -> unsigned {
-    const int a = kTermAxis[n][t];
-    const CpmlTerm& tm = CP.t[n][a];
-    if (a == 0) return roff[r];
-    if (a == 1) return roff[r] - (unsigned)(tm.lo[sd] * nz) * 4u;  // sentinel offsets stay past the plane
-    const int j = jw + r;
-    const bool in = kin && j >= 0 && j < ny && kb >= tm.lo[sd] && kb < tm.hi[sd];
-    return in ? (unsigned)(j * (tm.hi[sd] - tm.lo[sd]) + (kb - tm.lo[sd])) * 4u : 0xF0000000u;
-  };
-  // wave-level activity of the 12 terms (bit 2n + t): x terms always (the
-  // plane decides per trip), y terms when a row of the wave lies in a slab,
-  // z terms when a lane does; z-term profiles per lane, y-term profiles of
-  // the wave's rows in LDS (uniform reads)
-  unsigned cpm_wave = 0;
-  // term (n, t) compiled into this variant (its axis is one of CAX) and live in this wave
-  auto act = [&](int n, int t) -> bool { return ((CAX >> kTermAxis[n][t]) & 1) && ((cpm_wave >> (2 * n + t)) & 1u); };
-  float ZB[CPM ? 4 : 1], ZC[CPM ? 4 : 1], ZK[CPM ? 4 : 1];
-  __shared__ float sYP[CPM ? NW : 1][CPM ? 4 * R * 3 : 1];
-  __shared__ float sPS[LPS ? T - 1 : 1][LPS ? 4 : 1][LPS ? NW * R : 1][64];
-  // slot of component n's term among the 4 terms of a face class (axis LA):
-  // one per component off the axis, E first
-  constexpr int LA = CAX == 1 ? 0 : (CAX == 2 ? 1 : 2);
-  auto lps_q = [](int n) -> int { return (n / 3) * 2 + ((n % 3) < LA ? (n % 3) : (n % 3) - 1); };
-  if constexpr (CPM) {
-#pragma unroll
-    for (int n = 0; n < 6; ++n)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int a = kTermAxis[n][t];
-        if (!((CAX >> a) & 1)) continue;
-        const CpmlTerm& tm = CP.t[n][a];
-        bool live = false;
-        if (a == 0) {
-          live = tm.psi[0] || tm.psi[1];
-        } else if (a == 1) {
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int j = jw + r;
-            const bool in = side_of(tm, j) >= 0;
-            live |= in;
-            const int q = (ytm_index(n) * R + r) * 3;
-            if (lane == 0) {
-              sYP[w][q] = in ? tm.b[j] : 1.f;
-              sYP[w][q + 1] = in ? tm.c[j] : 0.f;
-              sYP[w][q + 2] = in ? tm.k[j] : 0.f;
-            }
-          }
-        } else {
-          const bool in = kin && side_of(tm, kb) >= 0;
-          live = __any(in);
-          const int zi = ztm_index(n);
-          ZB[zi] = in ? tm.b[kb] : 1.f;
-          ZC[zi] = in ? tm.c[kb] : 0.f;
-          ZK[zi] = in ? tm.k[kb] : 0.f;
-        }
-        cpm_wave |= live ? (1u << (2 * n + t)) : 0u;
-      }
-  }
-  // Multi-step CPML: level l of trip X advances the psi of plane X - l (E
-  // terms; H terms X - l - 1), and level l + 1 of trip X + 1 advances the same
-  // cells again -- in the same lane of the same wave.  So the hand-off between
-  // levels is thread-private: level l stores its psi in slot (X & 1, l) of
-  // this thread's scratch column, the next trip's level l + 1 loads it back
-  // (agent-scope loads: L1 bypassed, the thread's own store is in L2).  The
-  // trip parity keeps this trip's level l from overwriting what its level
-  // l + 1 has yet to read.  Level 0 reads
-  // the slab arrays (psi at time n), level T - 1 writes the other copy (n + T)
-  // for owned cells only.  Slots are slot-major across all threads of the
-  // launch, so a wave's 64 lanes touch one contiguous 256-B run.
-  const unsigned scr_nth = gridDim.x * gridDim.y * gridDim.z * NW * 64u;
-  const unsigned scr_tid =
-      ((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * NW + w) * 64u + lane;
-  // (descriptor built at each use from the kernel argument: a descriptor
-  // value carried across the loop is taken for divergent and waterfalled)
-  auto scr_rs = [&]() -> Rsrc { return __builtin_amdgcn_make_buffer_rsrc((void*)pscr, (short)0, -1, 0x00020000); };
-  // per-lane part of a slot address (one VGPR) + wave-uniform slot base (soffset)
-  const unsigned scr_voff = scr_tid * 4u;
-  auto scr_soff = [&](int par, int l, int n, int t, int r) -> int {
-    return (int)((unsigned)((((par * (T - 1) + l) * 6 + n) * 2 + t) * R + r) * scr_nth * 4u);
-  };
 
   auto run = [&](auto allin_tag) {
   constexpr bool ALLIN = decltype(allin_tag)::value;
@@ -749,93 +590,6 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
       }
       return make_float3(sc, sc, sc);
     };
-    // CPML: every psi value this trip's levels advance -- level l: E terms
-    // on plane X - l, H terms on X - l - 1 -- loaded before the prefetch
-    // (vmcnt retires in issue order): level 0 from the slab arrays (time n),
-    // levels >= 1 from the thread's scratch slots the previous trip's level
-    // l - 1 wrote.  Slab membership is wave-uniform for x (plane) and y (row)
-    // terms and per lane for z terms; lanes / rows / planes outside a slab get
-    // an empty descriptor or an offset past it (reads 0) instead of a branch.
-    float PSL[CPM ? (LPS ? 1 : T) : 1][CPM ? 6 : 1][2][R];
-    // psi of level l of term (n, t), row r (LDS hand-off: one register set
-    // that every level updates in place)
-    auto psl = [&](int l, int n, int t, int r) -> float& { return PSL[CPM && !LPS ? l : 0][CPM ? n : 0][t][r]; };
-    if constexpr (CPM) {
-#pragma unroll
-      for (int l = 0; l < T; ++l)
-#pragma unroll
-        for (int n = 0; n < 6; ++n)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            const int a = kTermAxis[n][t];
-            if (!((CAX >> a) & 1)) continue;
-            const int pl = (n < 3 ? X : X - 1) - l;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-              if (LPS && l > 0) continue;
-              float v = 0.f;
-              if (l > 0) {
-                v = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(scr_rs(), scr_voff, scr_soff((X - 1) & 1, l - 1, n, t, r), 16));
-              } else if (a == 0) {
-                v = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(psi_rsrc(n, t, psi_side_x(n, t, pl), pl, false), roff[r], 0, 0));
-              } else if (a == 1) {
-                const int sd = psi_side_y(n, t, jw + r);
-                v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(psi_rsrc(n, t, sd, pl, false),
-                                                                         psi_off(n, t, sd > 0 ? 1 : 0, r), 0, 0));
-              } else {
-#pragma unroll
-                for (int sd = 0; sd < 2; ++sd)
-                  v += __uint_as_float(
-                      __builtin_amdgcn_raw_buffer_load_b32(psi_rsrc(n, t, sd, pl, false), psi_off(n, t, sd, r), 0, 0));
-              }
-              psl(l, n, t, r) = v;
-            }
-          }
-    }
-    // psi update of term t of component n (plane pl, row r) from its raw
-    // difference d; returns the curl correction sign * ((1/kappa - 1) d + psi)
-    auto cpml = [&](int l, int n, int t, int pl, int r, const vec& d) -> vec {
-      if constexpr (CPM) {
-        const int a = kTermAxis[n][t];
-        const int sg = t == 0 ? 1 : -1;
-        if (!act(n, t)) return zero;
-        float bb, cc, kk;
-        if (a == 0) {
-          if (psi_side_x(n, t, pl) < 0) return zero;
-          const CpmlTerm& tm = CP.t[n][0];
-          bb = cload(tm.b, pl);
-          cc = cload(tm.c, pl);
-          kk = cload(tm.k, pl);
-        } else if (a == 1) {
-          if (psi_side_y(n, t, jw + r) < 0) return zero;
-          const int q = (ytm_index(n) * R + r) * 3;
-          bb = sYP[w][q];
-          cc = sYP[w][q + 1];
-          kk = sYP[w][q + 2];
-        } else {
-          const int zi = ztm_index(n);
-          bb = ZB[zi];
-          cc = ZC[zi];
-          kk = ZK[zi];
-        }
-        const float pn = bb * psl(l, n, t, r) + cc * d[0];
-        psl(l, n, t, r) = pn;
-        const float cr = kk * d[0] + pn;  // 0 off a z slab (identity profile, psi 0)
-        return (vec)(sg > 0 ? cr : -cr);
-      }
-      return zero;
-    };
-    if (tf_slots) {
-      // this trip's g entries of the face slots (va = 0: index moves with X)
-      // (entries of planes outside a set's x range are never used; their
-      // index is clamped into the table)
-      const int dx = tf_va == 0 ? X : 0;
-      const int last = T * tf_ld - 1;
-      tf_g0 = tf_ok0 ? gtab[min(max(tf_gb0 + dx, 0), last)] : 0.f;
-      if (TF_ENT > 64) tf_g1 = tf_ok1 ? gtab[min(max(tf_gb1 + dx, 0), last)] : 0.f;
-    }
     // next plane(s) in flight under this plane's levels
     if (PFD == 2)
       load_plane(X + 2, Hn2, En2);
@@ -875,11 +629,6 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         vec cx = dxy - dxz;
         vec cy = dyz - dyx;
         vec cz = dzx - dzy;
-        if constexpr (CPM) {
-          cx += cpml(l, 0, 0, pe, r, dxy) + cpml(l, 0, 1, pe, r, dxz);
-          cy += cpml(l, 1, 0, pe, r, dyz) + cpml(l, 1, 1, pe, r, dyx);
-          cz += cpml(l, 2, 0, pe, r, dzx) + cpml(l, 2, 1, pe, r, dzy);
-        }
         tf_apply(0, l, pe, r, cx, cy, cz);
         En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * cx;
         En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * cy;
@@ -890,6 +639,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
           if (src_comp == 1) En[r].y[q] = sv.v[l];
           if (src_comp == 2) En[r].z[q] = sv.v[l];
         }
+        hist_store(0, l, pe, r, En[r].x, En[r].y, En[r].z);
       }
       const int ph = pe - 1;
 #pragma unroll
@@ -906,89 +656,17 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         vec dx = gxz - gxy;
         vec dy = gyx - gyz;
         vec dz = gzy - gzx;
-        if constexpr (CPM) {
-          dx += cpml(l, 3, 0, ph, r, gxz) + cpml(l, 3, 1, ph, r, gxy);
-          dy += cpml(l, 4, 0, ph, r, gyx) + cpml(l, 4, 1, ph, r, gyz);
-          dz += cpml(l, 5, 0, ph, r, gzy) + cpml(l, 5, 1, ph, r, gzx);
-        }
         tf_apply(1, l, ph, r, dx, dy, dz);
         Hn.x = Hp[l][r].x + coef(bhx, ph, r, 3, ch.x) * dx;
         Hn.y = Hp[l][r].y + coef(bhy, ph, r, 4, ch.y) * dy;
         Hn.z = Hp[l][r].z + coef(bhz, ph, r, 5, ch.z) * dz;
+        if (l < T - 1) hist_store(1, l, ph, r, Hn.x, Hn.y, Hn.z);
         // later rows (r+1 ..) read only their own and higher rows' Ep, so
         // row r rotates as soon as its H is done
         Ec[r] = Ep[l][r];
         Ep[l][r] = En[r];
         Hp[l][r] = Hc[r];
         Hc[r] = Hn;
-      }
-      if constexpr (LPS) {
-        // swap with the thread's LDS slot of level l: it holds psi^{l+1} of
-        // plane X - l - 1 (this trip's level l + 1 input, written by level l
-        // one trip ago) and takes this level's result for the next trip
-        if (l < T - 1) {
-#pragma unroll
-          for (int n = 0; n < 6; ++n)
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-              if (!((CAX >> kTermAxis[n][t]) & 1)) continue;
-#pragma unroll
-              for (int r = 0; r < R; ++r) {
-                float& slot = sPS[LPS ? l : 0][LPS ? lps_q(n) : 0][R * w + r][lane];
-                const float nxt = slot;
-                slot = psl(l, n, t, r);
-                psl(l, n, t, r) = nxt;
-              }
-            }
-        }
-      } else if constexpr (CPM && T > 1) {
-        // this level's psi to the thread's slot for the next trip's level l + 1
-        if (l < T - 1) {
-#pragma unroll
-          for (int n = 0; n < 6; ++n)
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-              if (!((CAX >> kTermAxis[n][t]) & 1)) continue;
-#pragma unroll
-              for (int r = 0; r < R; ++r)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(psl(l, n, t, r)), scr_rs(),
-                                                      scr_voff, scr_soff(X & 1, l, n, t, r), 0);
-            }
-        }
-      }
-    }
-    if constexpr (CPM) {
-      // the last level's psi of owned cells inside their component's update
-      // box to the slab arrays (time n + T); every store issued, the rest
-      // dropped by the descriptor
-#pragma unroll
-      for (int n = 0; n < 6; ++n) {
-        const int pl = n < 3 ? X - T + 1 : X - T;
-        const bool xok = pl >= i0 && pl < i1 && xin(*bx[n], pl);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int a = kTermAxis[n][t];
-          if (!((CAX >> a) & 1)) continue;
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const bool st = xok && ((mbits >> (r * 7 + 6)) & 1u) && ((mbits >> (r * 7 + n)) & 1u);
-            const float v = psl(T - 1, n, t, r);
-            if (a == 0) {
-              const int sd = xok ? psi_side_x(n, t, pl) : -1;
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), psi_rsrc(n, t, sd, pl, true),
-                                                    st ? roff[r] : 0xF0000000u, 0, 0);
-            } else if (a == 1) {
-              const int sd = xok ? psi_side_y(n, t, jw + r) : -1;
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), psi_rsrc(n, t, sd, pl, true),
-                                                    st ? psi_off(n, t, sd > 0 ? 1 : 0, r) : 0xF0000000u, 0, 0);
-            } else {
-#pragma unroll
-              for (int sd = 0; sd < 2; ++sd)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), psi_rsrc(n, t, xok ? sd : -1, pl, true),
-                                                      st ? psi_off(n, t, sd, r) : 0xF0000000u, 0, 0);
-            }
-          }
-        }
       }
     }
     if (ring_ld) {
@@ -1028,27 +706,22 @@ extern int g_tb_mr_xcd;
 extern int g_tb_variant;
 int tb_patch_bits();
 
-// tile of the multi-step CPML passes: CPML_NW waves x CPML_R rows
-constexpr int CPML_NW = 8, CPML_R = 2;
-
 template <int T, int V, int R, int FX, int NW = TBW>
 int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                  const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
                  int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
-                 const TfDev* tf, const float* gtab, const CpmlDev* cp, float* pscr, hipStream_t s) {
+                 const TfDev* tf, const float* gtab, float* hist, int hls, hipStream_t s) {
   constexpr int HL = (T + V - 1) / V;
   constexpr int TBZ = (64 - 2 * HL) * V;
   dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], NW * R - 2 * T),
             cdiv(O.hi[0] - O.lo[0], xchunk));
-  CpmlDev cpv{};
-  if constexpr (((FX >> 3) & 7) != 0) cpv = *cp;
 #define MR_LAUNCH(PFD, DEFER)                                                                                 \
   k_tb3d_mr<T, V, R, FX, PFD, DEFER, NW><<<grid, dim3(64, NW), 0, s>>>(                                     \
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
       O, xchunk, src[0], src[1], src[2], src[3], sv,                                                       \
-      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, cpv, \
-      pscr)
+      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, hist, \
+      hls)
   if constexpr (FX != 0) {
     MR_LAUNCH(1, false);  // tuning variants: uniform media only
   } else {
@@ -1063,19 +736,12 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
-// tile of a multi-step CPML pass: face classes at 4 steps hand psi through
-// LDS in the plain 16-wave x 2-row tile; the rest carry it in registers and
-// thread-private scratch in CPML_NW-wave tiles
-inline bool cpml_lds(int fx, int steps) {
-  const int cax = (fx >> 3) & 7;
-  return steps == 4 && (cax == 1 || cax == 2 || cax == 4);
-}
-inline int cpml_nw(int fx, int steps) { return cpml_lds(fx, steps) ? 16 : CPML_NW; }
-
-// multi-step (T > 1) CPML passes, TF/SF on or off (yee3d_tb_cpml.hip)
-int launch_tb_mr_cpml(int T, int fx, const float* const* ein, const float* const* hin, float* const* eout,
-                      float* const* hout, float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O,
-                      int xchunk, const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab,
-                      const CpmlDev* cp, float* pscr, hipStream_t s);
+// boundary-history passes (fx bit 8, with any of bits 1 / 2 / 4; T <= 5),
+// compiled in yee3d_tb_hist.hip
+int launch_tb_mr_hist(int T, int fx, const float* const* ein, const float* const* hin, float* const* eout,
+                      float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
+                      float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
+                      const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, float* hist, int hls,
+                      hipStream_t s);
 
 }  // namespace tb3d

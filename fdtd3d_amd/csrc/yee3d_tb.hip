@@ -328,31 +328,11 @@ template <int T>
 int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                      float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                      float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
-                     const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const CpmlDev* cp,
-                     float* pscr, hipStream_t s) {
-  // scalar lanes with 2 rows per wave: R = 4 or float2 lanes at R = 2
-  // exceed 128 VGPRs and spill from T = 2 on
-#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, pscr, s
-  if constexpr (T == 1) {
-    // CPML single-step passes: every axis's terms (56 = x | y | z)
-    switch (fx) {
-      case 56: return launch_tb_mr<T, 1, 2, 56>(MR_ARGS);
-      case 57: return launch_tb_mr<T, 1, 2, 57>(MR_ARGS);
-      case 58: return launch_tb_mr<T, 1, 2, 58>(MR_ARGS);
-      case 59: return launch_tb_mr<T, 1, 2, 59>(MR_ARGS);
-      case 60: return launch_tb_mr<T, 1, 2, 60>(MR_ARGS);
-      case 61: return launch_tb_mr<T, 1, 2, 61>(MR_ARGS);
-      case 62: return launch_tb_mr<T, 1, 2, 62>(MR_ARGS);
-      case 63: return launch_tb_mr<T, 1, 2, 63>(MR_ARGS);
-    }
-    if (fx & 56) return (int)hipErrorInvalidValue;
-  } else {
-    // multi-step CPML (+ TF/SF) passes over the shell boxes of a hybrid run
-    if (fx & 56)
-      return (fx & 3) ? (int)hipErrorInvalidValue
-                      : launch_tb_mr_cpml(T, fx, ein, hin, eout, hout, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf,
-                                          gtab, cp, pscr, s);
-  }
+                     const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, float* hist, int hls,
+                     hipStream_t s) {
+#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, hist, hls, s
+  // boundary-history variants: their own translation unit (yee3d_tb_hist.hip)
+  if (fx & 8) return launch_tb_mr_hist(T, fx, MR_ARGS);
   // per-cell: one kind keeps T coefficient planes in LDS (24 KiB each, 160
   // KiB per CU: T <= 5); both kinds keep them in registers (spill-free to T = 2)
   if constexpr (T <= 5) {
@@ -378,33 +358,22 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
 
 // automatic x chunk of a multi-row pass over output box O
 int tb_mr_xchunk(int fx, const Box3& O, int steps) {
-  const bool cpm = (fx & 56) && steps > 1;
-  const int R = cpm ? CPML_R : 2, NW = cpm ? cpml_nw(fx, steps) : TBW;
   const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
-  const long long gy = cdiv(O.hi[1] - O.lo[1], NW * R - 2 * steps);
+  const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * 2 - 2 * steps);
   // the 8-wave shape fits two workgroups per CU
-  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) || (cpm && NW == 8) ? 2 : 1);
-}
-
-// bytes of thread-private psi scratch a multi-step CPML pass needs (0: none)
-long long tb_mr_scratch_bytes(int fx, const Box3& O, int steps, int xchunk) {
-  if (!(fx & 56) || steps <= 1 || box_empty(O) || cpml_lds(fx, steps)) return 0;
-  if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
-  const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
-  const long long gy = cdiv(O.hi[1] - O.lo[1], CPML_NW * CPML_R - 2 * steps);
-  const long long gx = cdiv(O.hi[0] - O.lo[0], xchunk);
-  return 2LL * (steps - 1) * 12 * CPML_R * gz * gy * gx * CPML_NW * 64 * 4;
+  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) ? 2 : 1);
 }
 
 // multi-row pass (scalar lanes, 2 rows per wave): uniform media, sparse
-// per-cell coefficients (fx bits 1 / 2), TF/SF corrections (fx bit 4)
+// per-cell coefficients (fx bits 1 / 2), TF/SF corrections (fx bit 4),
+// boundary history (fx bit 8)
 int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                    float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                    float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, int steps,
-                   const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const CpmlDev* cp,
-                   float* pscr, hipStream_t s) {
+                   const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, float* hist, int hls,
+                   hipStream_t s) {
   if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
-#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, cp, pscr, s
+#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, hist, hls, s
   switch (steps) {
     case 1: return launch_tb_mr_sel<1>(MR_ARGS);
     case 2: return launch_tb_mr_sel<2>(MR_ARGS);
@@ -497,7 +466,7 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   if (!pc && (MR > 1 || steps > 4)) {
     const Box3 nb = make_box(kNoBox);
     return tb_mr_dispatch(0, ein, hin, eout, hout, nullptr, nullptr, nb, nb, fcb, fdb, nx, ny, nz, b, O, xchunk,
-                          steps, src, sv, nullptr, nullptr, nullptr, nullptr, s);
+                          steps, src, sv, nullptr, nullptr, nullptr, 0, s);
   }
   if (steps > 4) return (int)hipErrorInvalidValue;
   if (xchunk <= 0) {
@@ -526,26 +495,25 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   return (int)hipErrorInvalidValue;
 }
 
+FDTD_API long long fdtd_tb3d_hist_floats(int nx, int ny, int nz, int steps, int* hls);
+
 // T fused leapfrog steps on the multi-row kernel with its extensions:
 // sparse per-cell coefficients -- ``ce4`` / ``ch4`` hold the E / H
 // coefficients of the three components as one float4 per cell of the box
 // ``ebox`` / ``hbox`` (x-major, z fastest, .w unused); every cell outside its
 // kind's box, and either kind whose array is null, uses the scalar ``cb`` /
 // ``db`` -- TF/SF corrections (``tf`` = device TfDev, ``gtab`` = the g
-// table of this pass's first level, from fdtd_tfsf_pass_f32; null: none) and,
-// CPML (``cpml`` = the CpmlDev block as HOST bytes, passed by value to the
-// kernel, ``cpml_axes`` = the axes whose terms the launch carries, 0 = all;
-// 1 or 4 steps per pass; 4-step passes of multi-axis classes need ``pscr``, ``pscr_bytes`` >=
-// fdtd_tb3d_cpml_scratch_bytes; null: none).
-// Other arguments as fdtd_tb3d_v4_f32.
+// table of this pass's first level, from fdtd_tfsf_pass_f32; null: none) and
+// the boundary history of the output box (``hist``: at least
+// fdtd_tb3d_hist_floats(nx, ny, nz, steps) floats, ``hls`` = its layer stride
+// from the same call; null: none; tb3d_mr.h).  Other arguments as fdtd_tb3d_v4_f32.
 FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* const* eout,
                                float* const* hout, const void* ce4, const int* ebox, const void* ch4,
                                const int* hbox, double cb, double db, int nx, int ny, int nz, const int* boxes,
                                const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
-                               const void* tf, const float* gtab, const void* cpml, int cpml_axes, void* pscr,
-                               long long pscr_bytes, void* stream) {
+                               const void* tf, const float* gtab, float* hist, long long hist_floats, int hls,
+                               void* stream) {
   if (nz % 4 != 0 || steps < 1 || steps > 6) return (int)hipErrorInvalidValue;
-  if (cpml && steps != 1 && steps != 4) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
   const Box3 O = make_box(obox);
@@ -553,33 +521,30 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
   const Box3 BE = make_box(ce4 ? ebox : kNoBox), BH = make_box(ch4 ? hbox : kNoBox);
   TbSrc sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
-  // CPML variants: the axes whose terms the box's dependency cone needs (0: all)
-  const int cax = (cpml_axes & 7) ? (cpml_axes & 7) : 7;
   const int fx = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0) | (tf && gtab ? 4 : 0) |
-                 (cpml ? (steps > 1 ? cax : 7) << 3 : 0);
-  if ((fx & 56) && steps > 1) {
-    // multi-step CPML: uniform media only; the caller's scratch must cover the launch
-    if (fx & 3) return (int)hipErrorInvalidValue;
-    if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
-    const long long need = tb_mr_scratch_bytes(fx, O, steps, xchunk);
-    if ((need > 0 && !pscr) || pscr_bytes < need || need > 0xFFFFFFFFLL)
+                 (hist ? 8 : 0);
+  if (hist) {
+    // the layer stride must cover every face plane of the array, the buffer every slot
+    int need = 0;
+    fdtd_tb3d_hist_floats(nx, ny, nz, steps, &need);
+    if (hls < need || hist_floats < 12LL * steps * hls || 12LL * steps * hls * 4 > 0x7FFFFFFFLL || steps > 5)
       return (int)hipErrorInvalidValue;
   }
   return tb_mr_dispatch(fx, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
                         (const float4*)(box_empty(BH) ? nullptr : ch4), BE, BH, (float)cb, (float)db, nx, ny, nz, b,
-                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, (const CpmlDev*)cpml, (float*)pscr,
-                        (hipStream_t)stream);
+                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, hist, hls, (hipStream_t)stream);
 }
 
-// scratch bytes fdtd_tb3d_ext_f32 needs for a CPML pass of ``steps`` steps
-// over output box ``obox`` (TF/SF on or off; 0 for single-step passes)
-FDTD_API long long fdtd_tb3d_cpml_scratch_bytes(const int* obox, int xchunk, int steps, int tfsf, int cpml_axes) {
-  const int cax = (cpml_axes & 7) ? (cpml_axes & 7) : 7;
-  return tb_mr_scratch_bytes((cax << 3) | (tfsf ? 4 : 0), make_box(obox), steps, xchunk);
+// floats of the boundary history of a ``steps``-step pass over an
+// (nx, ny, nz) array (12 * steps face layers) and, in ``hls``, the layer
+// stride (the largest face plane)
+FDTD_API long long fdtd_tb3d_hist_floats(int nx, int ny, int nz, int steps, int* hls) {
+  long long m = (long long)ny * nz;
+  if ((long long)nx * nz > m) m = (long long)nx * nz;
+  if ((long long)nx * ny > m) m = (long long)nx * ny;
+  *hls = (int)m;
+  return 12LL * steps * m;
 }
-
-// size of the CpmlDev block the host fills (ABI check)
-FDTD_API int fdtd_cpmldev_size() { return (int)sizeof(CpmlDev); }
 
 // size of the TfDev block the host fills (ABI check)
 FDTD_API int fdtd_tfdev_size() { return (int)sizeof(TfDev); }

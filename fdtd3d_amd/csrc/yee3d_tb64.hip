@@ -105,8 +105,8 @@ int pick_xchunk64(long long tiles_yz, int nxo, int T) {
 // tile is owned (T = 4: 24 x 24 of 32 x 32 = 56% against 8 x 56 of 16 x 64 =
 // 44%) for the same registers.  The z shift crosses the half boundary only
 // into halo lanes; y neighbours are one flat LDS row (32 lanes) apart.
-template <int T, int R, bool PERCELL, bool HALF>
-__global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
+template <int T, int R, bool PERCELL, bool HALF, int NW>
+__global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
     const double* __restrict__ exi, const double* __restrict__ eyi, const double* __restrict__ ezi,
     const double* __restrict__ hxi, const double* __restrict__ hyi, const double* __restrict__ hzi,
     double* __restrict__ exo, double* __restrict__ eyo, double* __restrict__ ezo,
@@ -117,9 +117,9 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc64 sv, int patch) {
   constexpr int LW = HALF ? 32 : 64;  // z lanes per row
   constexpr int TBZ = LW - 2 * T;       // owned z cells per tile
-  constexpr int ROWS = TBW * R * (HALF ? 2 : 1);
+  constexpr int ROWS = NW * R * (HALF ? 2 : 1);
   static_assert(!HALF || R == 1, "half-wave rows hold one row per half");
-  __shared__ double sX[2][4][TBW][64];
+  __shared__ double sX[2][4][NW][64];
   const int lane = threadIdx.x;
   const int lz = HALF ? (lane & 31) : lane;
   const int hr = HALF ? (lane >> 5) : 0;
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
     }
   }
   const int rdn = w > 0 ? w - 1 : 0;
-  const int rup = w < TBW - 1 ? w + 1 : TBW - 1;
+  const int rup = w < NW - 1 ? w + 1 : NW - 1;
   auto coef = [&](const double* arr, const Box3& b, int p, int r, int n, double sc) -> double {
     const bool in = xin(b, p) && ((mbits >> (r * 7 + n)) & 1u);
     if (PERCELL && arr) return in ? bld64(plane_rsrc64(arr, p, nx, plane), roff[r]) : 0.0;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64 * TBW) void k_tb3d_f64(
         // row j -/+ 1 is 32 lanes down / up in the flat [TBW * 64] slot
         const int fl = w * 64 + lane;
         const int fdn = fl >= 32 ? fl - 32 : fl;
-        const int fup = fl < TBW * 64 - 32 ? fl + 32 : fl;
+        const int fup = fl < NW * 64 - 32 ? fl + 32 : fl;
         hz_dn = (&sX[buf][0][0][0])[fdn];
         hx_dn = (&sX[buf][1][0][0])[fdn];
         ex_up = (&sX[buf][2][0][0])[fup];
@@ -323,14 +323,14 @@ int tb64_patch() {
   return g_tb64_patch;
 }
 
-template <int T, int R, bool HALF>
+template <int T, int R, bool HALF, int NW = TBW>
 int launch_tb64(bool pc, const double* const* ein, const double* const* hin, double* const* eout,
                 double* const* hout, const double* const* cbs, const double* const* dbs, double cb, double db,
                 int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src,
                 const TbSrc64& sv, hipStream_t s) {
   constexpr int TBZ = (HALF ? 32 : 64) - 2 * T;
   const long long gz = cdiv(O.hi[2] - O.lo[2], TBZ);
-  const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * R * (HALF ? 2 : 1) - 2 * T);
+  const long long gy = cdiv(O.hi[1] - O.lo[1], NW * R * (HALF ? 2 : 1) - 2 * T);
   if (xchunk <= 0) xchunk = pick_xchunk64(gz * gy, O.hi[0] - O.lo[0], T);
   dim3 grid((unsigned)gz, (unsigned)gy, cdiv(O.hi[0] - O.lo[0], xchunk));
 #define TB64_ARGS                                                                                              \
@@ -338,9 +338,9 @@ int launch_tb64(bool pc, const double* const* ein, const double* const* hin, dou
       cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
       O, xchunk, src[0], src[1], src[2], src[3], sv, tb64_patch()
   if (pc)
-    k_tb3d_f64<T, R, true, HALF><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
+    k_tb3d_f64<T, R, true, HALF, NW><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
   else
-    k_tb3d_f64<T, R, false, HALF><<<grid, dim3(64, TBW), 0, s>>>(TB64_ARGS);
+    k_tb3d_f64<T, R, false, HALF, NW><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
 #undef TB64_ARGS
   FDTD_RETURN_LAUNCH_STATUS();
 }

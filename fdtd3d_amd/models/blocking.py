@@ -55,9 +55,6 @@ F32_AUTO_STEPS_PERCELL_BOTH = 2
 F32_AUTO_STEPS_TFSF = 4
 
 
-# hybrid_shell modes that take the blocked shell (_hybrid3_plan) when the run fits it
-BLOCKED_SHELL_MODES = ("blocked", "mixed")
-
 
 def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: int = 1, tfsf: bool = False) -> int:
     """Steps per pass of a plain (no PML / TF-SF / dispersion) run in
@@ -78,79 +75,6 @@ def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: 
     if tfsf:
         return F32_AUTO_STEPS_TFSF
     return F32_AUTO_STEPS if world <= 2 else F32_AUTO_STEPS_MANY_RANKS
-
-
-def _cut_pieces(b: Box, cuts, keep=()):
-    """``b`` split at the absorbing-slab cuts of every axis: [(box, axes
-    bits)], bit a set when the piece may touch a slab along axis a.  The
-    high-side cut moves one cell down: a tile recomputes its halo cells with
-    its own specialisation, and the H update of the last cell below a high
-    slab reads the new E of the first slab cell (H^{n+1} needs E^{n+1} at
-    +1 along every axis; E^{n+1} needs only H^n, so the low side is exact).
-    Axes in ``keep`` are not cut (the piece keeps its slab cells and the band
-    beyond them in one box: a thin face of the shell stays one tile deep
-    instead of two part-filled ones); their bit is set when ``b`` reaches a
-    slab."""
-    pieces = [(b, 0)]
-    for a in range(3):
-        if cuts[a] is None:
-            continue
-        lo_c, hi_c = cuts[a][0], cuts[a][1] - 1
-        if a in keep:
-            if b[0][a] < lo_c or b[1][a] > hi_c:
-                pieces = [(pb, ax | (1 << a)) for pb, ax in pieces]
-            continue
-        nxt = []
-        for pb, ax in pieces:
-            for s_lo, s_hi, slab in ((None, lo_c, True), (lo_c, hi_c, False), (hi_c, None, True)):
-                l0 = pb[0][a] if s_lo is None else max(pb[0][a], s_lo)
-                h0 = pb[1][a] if s_hi is None else min(pb[1][a], s_hi)
-                if h0 <= l0:
-                    continue
-                lo, hi = list(pb[0]), list(pb[1])
-                lo[a], hi[a] = l0, h0
-                nxt.append(((tuple(lo), tuple(hi)), ax | ((1 << a) if slab else 0)))
-        pieces = nxt
-    return [(pb, ax) for pb, ax in pieces if not box_empty(pb)]
-
-
-def _cut_box(b: Box, box: Box):
-    """``b`` split at a dispersive box: [(piece, 8)] for the part within
-    [box.lo - 1, box.hi) on every axis (the cell below the box's low face
-    updates H from the box's new E), [(piece, 0)] for the rest."""
-    lo = tuple(box[0][d] - 1 for d in range(3))
-    inner = (tuple(max(b[0][d], lo[d]) for d in range(3)), tuple(min(b[1][d], box[1][d]) for d in range(3)))
-    if box_empty(inner):
-        return [(b, 0)]
-    return [(inner, 8)] + [(r, 0) for r in box_subtract(b, inner) if not box_empty(r)]
-
-
-def _merge_pieces(pieces):
-    """Merge pieces of the same CPML class whose union is a box (fewer,
-    larger boxes per shell launch)."""
-    out = list(pieces)
-    changed = True
-    while changed:
-        changed = False
-        for i in range(len(out)):
-            for j in range(i + 1, len(out)):
-                (a, ca), (b, cb_) = out[i], out[j]
-                if ca != cb_:
-                    continue
-                for d in range(3):
-                    same = all(a[0][e] == b[0][e] and a[1][e] == b[1][e] for e in range(3) if e != d)
-                    if same and (a[1][d] == b[0][d] or b[1][d] == a[0][d]):
-                        lo = tuple(min(a[0][e], b[0][e]) for e in range(3))
-                        hi = tuple(max(a[1][e], b[1][e]) for e in range(3))
-                        out[i] = ((lo, hi), ca)
-                        del out[j]
-                        changed = True
-                        break
-                if changed:
-                    break
-            if changed:
-                break
-    return out
 
 
 class PassTimer:
@@ -279,30 +203,9 @@ class BlockedStepping:
                 return
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
                 return
-        if self._hybrid3_ok():
-            # automatic T: 4, where the face classes hand psi through LDS
-            # (csrc/tb3d_mr.h LPS) in the plain kernel's tile
-            T3 = H if int(cfg.hybrid_block) > 0 or not self.use_cpml else 4
-            plan = self._hybrid3_plan(T3)
-            if plan is not None and getattr(cfg, "hybrid_shell", "auto") == "mixed" and self.use_cpml:
-                plan = self._hybrid4_plan(plan)
-            if plan is not None:
-                if not hasattr(self, "F_alt"):
-                    self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
-                self.hybrid = plan
-                return
-        if self._hybrid2_ok() and self._hybrid2_regions():
-            plan = self._hybrid2_plan(H)
-            if plan is None:
-                self.upml_regions = None
-                self.drude_box = None
-            else:
-                if not hasattr(self, "F_alt"):
-                    self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
-                self.F_3 = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
-                self.hybrid = plan
-                return
-        plan = self._hybrid_plan(H)
+        plan = self._hybrid_hist_plan(H) if self._hybrid_hist_ok() else None
+        if plan is None:
+            plan = self._hybrid_plan(H)
         if plan is None:
             return
         if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.5 * self.cells():
@@ -315,422 +218,6 @@ class BlockedStepping:
         if not hasattr(self, "F_alt"):
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
         self.hybrid = plan
-
-    # ------------------------------------------------ hybrid, blocked shell
-    def _hybrid3_ok(self) -> bool:
-        """Runs whose shell takes blocked passes too (``hybrid_shell`` auto or
-        blocked): serial fp32 3D HIP runs with CPML absorbing layers and / or
-        TF/SF plane waves along x or y (in-kernel TfsfSets), uniform media.
-        The CPML variant of the blocked kernel carries psi through the pass's
-        levels (csrc/yee3d_tb.hip, thread-private hand-off)."""
-        cfg = self.cfg
-        mode = getattr(cfg, "hybrid_shell", "auto")
-        if mode not in BLOCKED_SHELL_MODES or self.ops.name != "hip" or not hasattr(self.ops, "tb_step"):
-            return False
-        if cfg.scheme != "3d" or self.halo is not None or cfg.use_amp_mode or cfg.use_metamaterials:
-            return False
-        if self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0:
-            return False
-        if cfg.use_pml and (not self.use_cpml or self.use_upml_chain):
-            return False
-        if cfg.use_tfsf and getattr(self, "tfsf_sets", None) is None:
-            return False
-        if not (self.use_cpml or cfg.use_tfsf):
-            return False
-        return not any(getattr(self.cb[c], "cell", None) is not None for c in self.comps)
-
-    def _hybrid3_plan(self, T: int):
-        """Every cell advances ``T`` steps per pass in ONE blocked launch per
-        box, all reading ``F`` and writing ``F_alt``: the plain kernel on the
-        core (cells at least ``T + 1`` -- ``T + 2`` when staggering needs it --
-        from every CPML slab cell and TF/SF target, so its dependency cone
-        holds only plain cells) and the CPML + TF/SF variant on the six shell
-        boxes around it.  No stepped band, no shell copy: a shell box's cone
-        reaches into the core, where the variant's update is the plain one."""
-        cfg = self.cfg
-        size = cfg.size
-        dom = self.domain
-        alloc = dom.allocated_global()
-
-        def grow(b, n):
-            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
-
-        K = None
-        for m in (T + 1, T + 2):
-            lo, hi = [0, 0, 0], list(size)
-            for a in range(3):
-                edge = 0
-                if cfg.use_pml:
-                    edge = max(edge, self.layout.pml_size[a])
-                if cfg.use_tfsf:
-                    edge = max(edge, cfg.tfsf_size[a] + 1)
-                if edge > 0:
-                    lo[a], hi[a] = edge + m, size[a] - edge - m
-            cand = (tuple(lo), tuple(hi))
-            if box_empty(cand):
-                return None
-            g = grow(cand, T + 1)
-            if self.use_cpml and any(not box_empty(box_intersect(g, sl.gbox))
-                                     for slabs in self.cpml.slabs.values() for sl in slabs):
-                continue
-            if cfg.use_tfsf and self._tfsf_targets_in(dom.to_local(g)):
-                continue
-            K = cand
-            break
-        if K is None:
-            return None
-        if self.use_cpml and T not in getattr(self.ops, "tb_cpml_steps", ()):
-            return None
-        # shell pieces by class: the CPML axes whose slabs a piece's
-        # dependency cone reaches (cuts T + 1 beyond each slab), and whether
-        # it reaches a TF/SF target -- each class is its own kernel variant
-        slabs = [sl for sls in (self.cpml.slabs.values() if self.use_cpml else ()) for sl in sls]
-        cuts = []
-        for a in range(3):
-            lo_e = max([sl.gbox[1][a] for sl in slabs if sl.axis == a and sl.side == 0], default=None)
-            hi_s = min([sl.gbox[0][a] for sl in slabs if sl.axis == a and sl.side == 1], default=None)
-            cuts.append([c for c in ((lo_e + T + 1) if lo_e is not None else None,
-                                     (hi_s - T - 1) if hi_s is not None else None) if c is not None])
-        pieces = [b for b in box_subtract(alloc, K) if not box_empty(b)]
-        for a in range(3):
-            nxt = []
-            for b in pieces:
-                edges = sorted({b[0][a], b[1][a]} | {c for c in cuts[a] if b[0][a] < c < b[1][a]})
-                for lo_, hi_ in zip(edges, edges[1:]):
-                    lo, hi = list(b[0]), list(b[1])
-                    lo[a], hi[a] = lo_, hi_
-                    nxt.append((tuple(lo), tuple(hi)))
-            pieces = nxt
-        classed = []
-        for b in pieces:
-            g = grow(b, T + 1)
-            ax = 0
-            for sl in slabs:
-                if not box_empty(box_intersect(g, sl.gbox)):
-                    ax |= 1 << sl.axis
-            tf = bool(cfg.use_tfsf and self._tfsf_targets_in(dom.to_local(g)))
-            classed.append((b, ax | (8 if tf else 0)))
-        shell = [(dom.to_local(b), c) for b, c in _merge_pieces(classed)]
-        upd = {c: self.local_box(c, alloc) for c in self.comps}
-        return {"T": T, "v3": True, "core": [dom.to_local(K)], "shell": shell, "upd": upd,
-                "core_cells": box_volume(K)}
-
-    def _hybrid4_plan(self, p3):
-        """Mixed shell: the core and the x / y faces (one CPML axis in their
-        cone: psi through LDS, csrc/tb3d_mr.h LPS, + in-kernel TF/SF) take
-        blocked launches; the rest -- the z slabs over the whole x / y
-        extent and the x-y edge columns -- is stepped in place in F over
-        windows grown ``T - s`` cells into the blocked pieces at step ``s``
-        (the band rule of ``_hybrid_plan``), then copied to F_alt.  The
-        blocked faces' psi (written to the other copy) is copied back over
-        the band's in-place psi afterwards."""
-        T = p3["T"]
-        dom = self.domain
-        alloc = dom.allocated_global()
-        # geometry: the x faces (x outside the core's range, y / z inside it)
-        # and the y faces (x / z inside, y outside) are blocked; the z slabs
-        # (whole x / y extent) and the x-y edge columns are stepped -- few,
-        # large stepped windows
-        K = dom.to_global(p3["core"][0])
-        faces = []
-        for a in (0, 1):
-            for lo_, hi_ in ((alloc[0][a], K[0][a]), (K[1][a], alloc[1][a])):
-                if hi_ <= lo_:
-                    continue
-                lo, hi = list(K[0]), list(K[1])
-                lo[a], hi[a] = lo_, hi_
-                if a == 1:
-                    lo[0], hi[0] = K[0][0], K[1][0]
-                faces.append(((tuple(lo), tuple(hi)), a))
-        slabs = [sl for sls in self.cpml.slabs.values() for sl in sls]
-        blocked = []
-        for b, a in faces:
-            g = (tuple(b[0][d] - T - 1 for d in range(3)), tuple(b[1][d] + T + 1 for d in range(3)))
-            ax = 0
-            for sl in slabs:
-                if not box_empty(box_intersect(g, sl.gbox)):
-                    ax |= 1 << sl.axis
-            if ax != 1 << a:
-                return p3  # a face's cone reaches another axis's slab: the blocked plan
-            tf = bool(self.cfg.use_tfsf and self._tfsf_targets_in(dom.to_local(g)))
-            blocked.append((dom.to_local(b), ax | (8 if tf else 0)))
-        rest = [alloc]
-        for b in [K] + [dom.to_global(f) for f, _ in blocked]:
-            rest = [r for q in rest for r in (box_subtract(q, b) if not box_empty(box_intersect(q, b)) else [q])
-                    if not box_empty(r)]
-        stepped = [(dom.to_local(r), 7) for r in rest]
-        if not stepped:
-            return p3
-
-        def grow(b, n):
-            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
-
-        def disjoint_union(boxes):
-            out = []
-            for b in boxes:
-                pieces = [box_intersect(b, alloc)]
-                for o in out:
-                    nxt = []
-                    for q in pieces:
-                        nxt += [r for r in box_subtract(q, o) if not box_empty(r)] if not box_empty(
-                            box_intersect(q, o)) else [q]
-                    pieces = nxt
-                out += [q for q in pieces if not box_empty(q)]
-            return out
-
-        sg = [dom.to_global(b) for b, _ in stepped]
-        # step s (0-based) advances the stepped pieces plus a band T - s deep
-        windows = [disjoint_union([grow(b, T - s) for b in sg]) for s in range(T)]
-        fixes = []
-        for b, cls in blocked:
-            a = {1: 0, 2: 1}.get(cls & 7)
-            if a is None:
-                continue
-            for c in self.comps:
-                for sl in self.cpml.slabs[c]:
-                    if sl.axis != a:
-                        continue
-                    i = box_intersect(b, sl.lbox)
-                    if not box_empty(i):
-                        fixes.append((sl, tuple(slice(i[0][d] - sl.lbox[0][d], i[1][d] - sl.lbox[0][d])
-                                                for d in range(3))))
-        self._tfsf_once = bool(self.cfg.use_tfsf)
-        return dict(p3, v3=False, v4=True, shell=blocked, windows=windows, copy=[b for b, _ in stepped],
-                    psi_fix=fixes)
-
-    def _hybrid4_step(self, T: int) -> None:
-        hp = self.hybrid
-        if T != hp["T"]:
-            for _ in range(T):
-                self.step()
-            return
-        srcs = self._pass_sources(self.t, T)
-        for p in range(self.planes):
-            line0 = None
-            if self.cfg.use_tfsf:
-                # the blocked launches' g tables advance the incident line T
-                # steps; the stepped windows advance it again from here
-                line0 = (self.einc[p].clone(), self.hinc[p].clone())
-            tf = self._tfsf_pass(p, T)
-            cp = self.cpml.host_table(p)
-            P, Q = self.F[p], self.F_alt[p]
-            with self.prof.phase("blocked-core"):
-                for ob in hp["core"]:
-                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p])
-                for ob, cls in hp["shell"]:
-                    cax = cls & 7
-                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf if cls & 8 else None,
-                                     cpml=cp if cax else None, cpml_axes=cax)
-            if line0 is not None:
-                self.einc[p].copy_(line0[0])
-                self.hinc[p].copy_(line0[1])
-        for s in range(T):
-            self.step(hp["windows"][s])
-        with self.prof.phase("shell-copy"):
-            for p in range(self.planes):
-                src = [self.F[p][c] for c in self.comps]
-                dst = [self.F_alt[p][c] for c in self.comps]
-                for b in hp["copy"]:
-                    self.ops.copy_box(src, dst, b)
-                # the blocked face pieces' psi (level T, other copy) over the
-                # stepped band's in-place values
-                for sl, sub in hp["psi_fix"]:
-                    sl.psi[p][sub] = sl.psi_alt[p][sub]
-        for p in range(self.planes):
-            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
-
-    def _hybrid3_step(self, T: int) -> None:
-        hp = self.hybrid
-        if T != hp["T"]:
-            tails = self.__dict__.setdefault("_hybrid3_tails", {})
-            if T not in tails:
-                tails[T] = self._hybrid3_plan(T)
-            hp = tails[T]
-            if hp is None:
-                for _ in range(T):
-                    self.step()
-                return
-        srcs = self._pass_sources(self.t, T)
-        for p in range(self.planes):
-            tf = self._tfsf_pass(p, T)
-            cp = self.cpml.host_table(p) if self.use_cpml else None
-            P, Q = self.F[p], self.F_alt[p]
-            with self.prof.phase("blocked-core"):
-                for ob in hp["core"]:
-                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p])
-            with self.prof.phase("blocked-shell"):
-                for ob, cls in hp["shell"]:
-                    cax = cls & 7
-                    self.ops.tb_step(P, Q, hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf if cls & 8 else None,
-                                     cpml=cp if cax else None, cpml_axes=cax)
-            if self.use_cpml:
-                self.cpml.flip(p)
-            self.F[p], self.F_alt[p] = Q, P
-        self.t += T
-        if self.cfg.check_finite and (self.t // max(1, self.cfg.finite_check_step)
-                                      != (self.t - T) // max(1, self.cfg.finite_check_step)):
-            self.check_finite()
-
-    # ------------------------------------------------ hybrid, single-pass shell
-    def _hybrid2_ok(self) -> bool:
-        """Runs whose shell the fused single-step shell kernel can advance
-        (csrc/yee3d_shell.hip): 3D serial runs with CPML, UPML (D/B form),
-        dispersive (Drude / Lorentz) boxes inside the all-sigma-zero core, or
-        plane waves in an open box; uniform background media (scalar
-        coefficients); plane waves through the TF/SF tables.  Opt-in
-        (``hybrid_shell`` = single-pass): measured at 512^3 (round 3,
-        ``tools/shell_micro.py``, ``profiles/configs_r3.md``) the fused
-        single-step shell kernel is issue-bound on the thin shell faces
-        (20-54 Gcells/s, a 0.2 ms floor per two-axis edge launch) and the whole
-        runs are 1.7-1.9x slower than the stepped shell (CPML + TF/SF 48.5k
-        vs 84.7k Mcells/s), so ``auto`` keeps the stepped shell."""
-        cfg = self.cfg
-        mode = getattr(cfg, "hybrid_shell", "auto")
-        if mode != "single-pass" or not hasattr(self.ops, "shell_step"):
-            return False
-        if cfg.scheme != "3d" or self.halo is not None or cfg.use_amp_mode:
-            return False
-        upml = cfg.use_pml and self.use_upml_chain
-        if not ((cfg.use_pml and self.use_cpml) or upml or (not cfg.use_pml and (cfg.use_tfsf or
-                                                                               cfg.use_metamaterials))):
-            return False
-        if self.use_upml_chain:
-            for c in self.comps:
-                st = self.upml[c]
-                if st["prof"]["cell"] is not None or ("plain" in st and st["plain"]["prof"]["cell"] is not None):
-                    return False
-        if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
-            return False
-        if any(getattr(self.cb[c], "cell", None) is not None for c in self.comps):
-            return False  # per-cell coefficients: the stepped shell
-        # the kernel shares one slab geometry per (kind, axis): the terms of
-        # a kind along y / z must have the same psi slab ranges
-        by = {}
-        for c, slabs in (self.cpml.slabs.items() if self.use_cpml else ()):
-            for sl in slabs:
-                key = (c[0], sl.axis, sl.side)
-                rng = (sl.lbox[0][sl.axis], sl.lbox[1][sl.axis])
-                if by.setdefault(key, rng) != rng:
-                    return False
-        return True
-
-    def _hybrid2_regions(self) -> bool:
-        """Region-local UPML / dispersive state of the single-pass shell
-        (models/upml.py); False when the run does not fit it."""
-        cfg = self.cfg
-        self.upml_regions = None
-        self.drude_box = None
-        try:
-            if cfg.use_pml and self.use_upml_chain:
-                from .upml import UPMLRegions
-                self.upml_regions = UPMLRegions(self)
-            if cfg.use_metamaterials:
-                from .upml import DrudeBox
-                self.drude_box = DrudeBox(self)
-                if self.upml_regions is not None:
-                    I, B = self.upml_regions.core, self.drude_box.box
-                    if box_intersect(I, B) != B:
-                        raise ValueError("dispersive box reaches an absorbing layer")
-        except ValueError:
-            self.upml_regions = None
-            self.drude_box = None
-            return False
-        return True
-
-    def _hybrid2_plan(self, T: int):
-        """Blocked core + single-pass shell with shrinking windows.
-
-        The core -- cells at least ``T + 2`` from every absorbing-layer cell,
-        TF/SF target and dispersive cell -- takes one ``T``-step blocked pass
-        of the plain kernel (``K``, minus the dispersive box grown by
-        ``T + 2``).  The shell -- everything else -- takes ``T`` fused single
-        steps (``ops.shell_step``), step ``s`` over ``alloc`` minus the core
-        shrunk by ``T - s`` on its inner sides: each step's window is one cell
-        deeper into the core than the next needs, so every shell value is
-        exact without a stale band (the deep-halo rule, reference
-        ``ParallelGrid.cpp:2365-2489``).  Single-step passes read one buffer
-        and write another, so the shell ping-pongs between ``F_alt`` and a
-        third buffer while the core reads the untouched ``F``.  Each window
-        is cut at the absorbing-slab and dispersive-box boundaries into boxes
-        tagged with the kernel's specialisation (axes bits; 8 = dispersive)."""
-        cfg = self.cfg
-        size = cfg.size
-        m = T + 2
-        lo, hi = [0, 0, 0], list(size)
-        for a in range(3):
-            edge = self.layout.pml_size[a] if cfg.use_pml else 0
-            if cfg.use_tfsf:
-                edge = max(edge, cfg.tfsf_size[a] + 1)
-            if edge > 0:
-                lo[a], hi[a] = edge + m, size[a] - edge - m
-        K = (tuple(lo), tuple(hi))
-        if box_empty(K):
-            return None
-        dom = self.domain
-        alloc = dom.allocated_global()
-        dbox = getattr(self, "drude_box", None)
-        Dm = None
-        couts = [K]
-        if dbox is not None:
-            B = dom.to_global(dbox.box)
-            Dm = box_intersect((tuple(B[0][d] - m for d in range(3)), tuple(B[1][d] + m for d in range(3))), K)
-            if not box_empty(Dm):
-                couts = [b for b in box_subtract(K, Dm) if not box_empty(b)]
-        core_cells = sum(box_volume(b) for b in couts)
-        if core_cells < 0.25 * size[0] * size[1] * size[2]:
-            return None
-
-        def grow(b, n):
-            return (tuple(b[0][d] - n for d in range(3)), tuple(b[1][d] + n for d in range(3)))
-
-        # every irregular cell must stay T + 1 clear of the core (its
-        # dependency cone; also keeps the host-side TF/SF additions to the
-        # shell's input buffer out of what the core pass reads)
-        ureg = getattr(self, "upml_regions", None)
-        for ob in couts:
-            g = grow(ob, T + 1)
-            for slabs in (self.cpml.slabs.values() if self.use_cpml else ()):
-                for sl in slabs:
-                    if not box_empty(box_intersect(g, sl.gbox)):
-                        return None
-            lg = dom.to_local(g)
-            if ureg is not None and box_intersect(lg, ureg.core) != box_intersect(lg, dom.to_local(alloc)):
-                return None  # the core's cone must see no UPML cell
-            if dbox is not None and not box_empty(box_intersect(lg, dbox.box)):
-                return None
-            if cfg.use_tfsf and self._tfsf_targets_in(lg):
-                return None
-        if cfg.use_tfsf and (ureg is not None or dbox is not None):
-            # E-form corrections only where the update is the plain one
-            if ureg is not None and self._tfsf_targets_in(ureg.core, outside=True):
-                return None
-            if dbox is not None and self._tfsf_targets_in(grow(dbox.box, 1)):
-                return None
-        cuts = self._cpml_cuts()
-
-        def shrink_inner(b, n):
-            return (tuple(b[0][d] + (n if b[0][d] > 0 else 0) for d in range(3)),
-                    tuple(b[1][d] - (n if b[1][d] < size[d] else 0) for d in range(3)))
-
-        windows = []
-        for st in range(1, T + 1):
-            d = T - st
-            Kd = shrink_inner(K, d)
-            pieces = []
-            for b in box_subtract(alloc, Kd):
-                if not box_empty(b):
-                    # the face normal of this part of the shell (the axes
-                    # along which it lies wholly outside the hole) is not cut
-                    normal = [a for a in range(3) if b[1][a] <= Kd[0][a] or b[0][a] >= Kd[1][a]]
-                    pieces += _cut_pieces(dom.to_local(b), cuts, keep=normal)
-            if Dm is not None and not box_empty(Dm):
-                inner = box_intersect(grow(Dm, d), Kd)
-                if not box_empty(inner):
-                    pieces += _cut_box(dom.to_local(inner), dbox.box)
-            windows.append(_merge_pieces(pieces))
-        upd = {c: self.local_box(c, alloc) for c in self.comps}
-        return {"T": T, "v2": True, "core": [dom.to_local(b) for b in couts], "windows": windows, "upd": upd,
-                "core_cells": core_cells}
 
     def _tfsf_targets_in(self, lbox: Box, outside: bool = False) -> bool:
         """True when some TF/SF target lies inside the local box (``outside``:
@@ -747,100 +234,6 @@ class BlockedStepping:
                     return True
         return False
 
-    def _cpml_cuts(self):
-        """Per axis (low cut, high cut) of the CPML slabs, local indices:
-        cells below the low cut or at / above the high cut may carry that
-        axis's psi terms (None: no slab along the axis)."""
-        cuts = [None, None, None]
-        n = self.domain.shape
-        ureg = getattr(self, "upml_regions", None)
-        if ureg is not None:
-            # the D boxes: everything outside the all-sigma-zero core
-            I = ureg.core
-            return [(I[0][a], I[1][a]) if (I[0][a] > 0 or I[1][a] < n[a]) else None for a in range(3)]
-        for slabs in (self.cpml.slabs.values() if self.use_cpml else ()):
-            for sl in slabs:
-                a = sl.axis
-                b = self.domain.to_local(sl.gbox)
-                lo_c, hi_c = cuts[a] if cuts[a] is not None else (0, n[a])
-                if sl.side == 0:
-                    lo_c = max(lo_c, b[1][a])
-                else:
-                    hi_c = min(hi_c, b[0][a])
-                cuts[a] = (lo_c, hi_c)
-        return cuts
-
-    def _tfsf_kind(self, kind: str, p: int, F) -> None:
-        """Every TF/SF correction of ``kind`` on plane ``p``'s fields ``F``
-        (coefficient Cb / Db, incident H for E targets, E for H targets), in
-        as few launches as the backend allows."""
-        comps = self.e_comps if kind == "E" else self.h_comps
-        inc = self.hinc[p] if kind == "E" else self.einc[p]
-        whole = ((0, 0, 0), tuple(self.domain.shape))
-        if hasattr(self.ops, "tfsf_apply_many"):
-            self.ops.tfsf_apply_many([(F[c], tab) for c in comps for tab in self.tfsf[c]], inc)
-        else:
-            for c in comps:
-                for tab in self.tfsf[c]:
-                    self.ops.tfsf_apply(F[c], tab, inc, whole)
-
-    def _hybrid2_step(self, T: int) -> None:
-        hp = self.hybrid
-        if T != hp["T"]:
-            # a short tail pass: its own (shallower) windows
-            hp = self.__dict__.setdefault("_hybrid2_tails", {}).get(T)
-            if hp is None:
-                hp = self._hybrid2_plan(T)
-                self._hybrid2_tails[T] = hp
-            if hp is None:
-                for _ in range(T):
-                    self.step()
-                return
-        srcs = self._pass_sources(self.t, T)
-        tfsf = self.cfg.use_tfsf
-        kappa = getattr(self.cfg, "cpml_kappa_max", 1.0) != 1.0
-        for p in range(self.planes):
-            P, Q, Z = self.F[p], self.F_alt[p], self.F_3[p]
-            cur = P
-            with self.prof.phase("shell"):
-                for st in range(1, T + 1):
-                    out = Q if st % 2 == 1 else Z
-                    t = self.t + st - 1
-                    if tfsf:
-                        # incident line E half step, then the E corrections
-                        # added to the INPUT (additive: E + Cb g + Cb curl)
-                        self.ops.inc_step_e(self.einc[p], self.hinc[p], self.inc_ce, self.source_value(t, p))
-                        self._tfsf_kind("E", p, cur)
-                    sv = None if srcs[p] is None else srcs[p][st - 1]
-                    cp = self.cpml.shell_arg(p, self.ops) if self.use_cpml else None
-                    ureg = getattr(self, "upml_regions", None)
-                    pieces = hp["windows"][st - 1]
-                    dbox = getattr(self, "drude_box", None)
-                    self.ops.shell_step(cur, out, hp["upd"], [b for b, _ in pieces], [a for _, a in pieces],
-                                        self.cb, sv, cpml=cp, kappa=kappa,
-                                        upml=None if ureg is None else ureg.shell_arg(p, self.ops),
-                                        drude=None if dbox is None else dbox.shell_arg(p, self.ops))
-                    if self.use_cpml:
-                        self.cpml.flip(p)
-                    if ureg is not None:
-                        ureg.flip(p)
-                    if dbox is not None:
-                        dbox.rotate(p)
-                    if tfsf:
-                        # incident line H half step, H corrections on the OUTPUT
-                        self.ops.inc_step_h(self.einc[p], self.hinc[p], self.inc_ch)
-                        self._tfsf_kind("H", p, out)
-                    cur = out
-            with self.prof.phase("blocked-core"):
-                for ob in hp["core"]:
-                    self.ops.tb_step(P, cur, hp["upd"], ob, self.cb, T, srcs[p])
-            rest = [b for b in (Q, Z) if b is not cur]
-            self.F[p], self.F_alt[p], self.F_3[p] = cur, P, rest[0]
-        self.t += T
-        if self.cfg.check_finite and (self.t // max(1, self.cfg.finite_check_step)
-                                      != (self.t - T) // max(1, self.cfg.finite_check_step)):
-            self.check_finite()
-
     def _hybrid_plan(self, T: int):
         dom = self.domain
         cfg = self.cfg
@@ -855,15 +248,14 @@ class BlockedStepping:
                 return plan
         return None
 
-    def _hybrid_plan_m(self, T: int, m: int):
+    def _hybrid_plan_m(self, T: int, m: int, in_kernel_tfsf: bool = False):
+        """Hybrid plan with core margin ``m``; ``in_kernel_tfsf``: the core
+        pass applies the TF/SF corrections itself (TfsfSets), so the TF/SF
+        faces may lie inside the core (the history-shell plan)."""
         dom = self.domain
         cfg = self.cfg
         size = cfg.size
         alloc = dom.allocated_global()
-        # TF/SF faces stay in the stepped shell: the blocked kernel's TF/SF
-        # variant runs at about half the plain kernel's rate
-        # (profiles/tfsf_cpml_r2.md), more than the shell it would save
-        in_kernel_tfsf = False
         lo, hi = [0, 0, 0], list(size)
         act = [self.layout.active(a) for a in range(3)]  # 2D: z is one cell, never cut
         for a in range(3):
@@ -997,6 +389,85 @@ class BlockedStepping:
                 "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
                 "cut_cells": box_volume(Dm) if Dm is not None else 0}
 
+    # ------------------------------------------------ hybrid, history shell
+    def _hybrid_hist_ok(self) -> bool:
+        """Serial 3D runs whose core pass can record its boundary history
+        (fp32 HIP: the multi-row kernel's feature bit 8; the torch oracle in
+        any precision), with TF/SF through TfsfSets when on."""
+        cfg = self.cfg
+        if cfg.scheme != "3d" or self.halo is not None or not hasattr(self.ops, "hist_buffer"):
+            return False
+        if self.ops.name == "hip" and self.dtype != torch.float32:
+            return False
+        if getattr(self.ops, "tb_max_hist_steps", 5) < 1:
+            return False
+        if cfg.use_tfsf and getattr(self, "tfsf_sets", None) is None:
+            return False
+        return True
+
+    def _hybrid_hist_plan(self, T: int):
+        """History shell: the blocked core pass (TF/SF corrections inside it)
+        also records E on its boxes' low faces and H on their high faces at
+        every level (``ops.tb_step(hist=...)``); the stepped shell then
+        advances ONLY the shell -- no band of core cells -- reading those face
+        values (``ops.hist_apply`` before each half step) wherever its
+        stencil reaches into the core.  Every shell value is the stepped
+        run's: the cells next to the core see the core's exact intermediate
+        levels."""
+        if T > getattr(self.ops, "tb_max_hist_steps", 5):
+            return None
+        plan = None
+        for m in (T + 1, T + 2):
+            plan = self._hybrid_plan_m(T, m, in_kernel_tfsf=True)
+            if plan is not None:
+                break
+        if plan is None:
+            return None
+        shell = [self.domain.to_global(b) for b in plan["copy"]]
+        tf_shell = bool(self.cfg.use_tfsf) and any(self._tfsf_targets_in(b) for b in plan["copy"])
+        shape = tuple(self.domain.shape)
+        hist = [[self.ops.hist_buffer(shape, T) for _ in plan["core"]] for _ in range(self.planes)]
+        return dict(plan, kind="history-shell", shells=[shell] * T, shell=shell, hist=hist,
+                    shell_tfsf=tf_shell, tfsf_in_core=bool(self.cfg.use_tfsf))
+
+    def _hybrid_hist_step(self, T: int) -> None:
+        hp = self.hybrid
+        srcs = self._pass_sources(self.t, T)
+        cores = hp["core"]
+        for p in range(self.planes):
+            tf, line0 = None, None
+            if self.cfg.use_tfsf:
+                if hp["shell_tfsf"]:
+                    # the shell steps the incident line again from here
+                    line0 = (self.einc[p].clone(), self.hinc[p].clone())
+                tf = self._tfsf_pass(p, T)
+            with self.prof.phase("blocked-core"):
+                for ob, hb in zip(cores, hp["hist"][p]):
+                    self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf,
+                                     hist=hb)
+            if line0 is not None:
+                self.einc[p].copy_(line0[0])
+                self.hinc[p].copy_(line0[1])
+        for s_ in range(T):
+            def pre(kind, p, s_=s_):
+                # E half step s reads H_s of the core's high faces (in F
+                # already for s = 0), the H half step E_{s+1} of its low faces
+                if kind == "E" and s_ == 0:
+                    return
+                with self.prof.phase("history"):
+                    for ob, hb in zip(cores, hp["hist"][p]):
+                        self.ops.hist_apply(self.F[p], hb, ob, T, "H" if kind == "E" else "E",
+                                            s_ - 1 if kind == "E" else s_)
+            self.step(hp["shell"], pre=pre, tfsf=hp["shell_tfsf"])
+        with self.prof.phase("shell-copy"):
+            for p in range(self.planes):
+                src = [self.F[p][c] for c in self.comps]
+                dst = [self.F_alt[p][c] for c in self.comps]
+                for b in hp["copy"]:
+                    self.ops.copy_box(src, dst, b)
+        for p in range(self.planes):
+            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
+
     def _tfsf_pass(self, p: int, T: int, level0: int = 0):
         """In-kernel TF/SF of a blocked pass starting at step ``self.t`` on
         plane ``p``: advances the plane's incident line ``T`` steps and returns
@@ -1023,14 +494,8 @@ class BlockedStepping:
         return srcs
 
     def _hybrid_step(self, T: int) -> None:
-        if self.hybrid.get("v4"):
-            self._hybrid4_step(T)
-            return
-        if self.hybrid.get("v3"):
-            self._hybrid3_step(T)
-            return
-        if self.hybrid.get("v2"):
-            self._hybrid2_step(T)
+        if self.hybrid.get("kind") == "history-shell":
+            self._hybrid_hist_step(T)
             return
         hp = self.hybrid
         srcs = self._pass_sources(self.t, T)

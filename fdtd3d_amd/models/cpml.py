@@ -141,64 +141,6 @@ class CPML:
         cache[key] = (ptrs, ints, keep)
         return cache[key]
 
-    def host_table(self, p: int) -> torch.Tensor:
-        """The :meth:`device_table` block as HOST bytes: the shell kernel
-        (yee3d_shell.hip) takes it by value in its kernel arguments."""
-        self.device_table(p)
-        key = (p,) + tuple(sl.psi[p].data_ptr() for c in self.s.comps for sl in self.slabs[c])
-        return self.__dict__["_dev"][key][2]
-
-    def device_table(self, p: int) -> torch.Tensor:
-        """CpmlDev block of plane ``p`` for the single-step blocked kernel
-        (yee3d_tb.hip): per component (Ex..Hz) and term axis the psi slab
-        pointers -- read from ``psi[p]``, written to a second copy, since the
-        kernel recomputes halo cells whose psi a neighbour tile may already
-        have advanced --, their ranges and the profile pointers of
-        :meth:`kernel_table`.  After the pass call :meth:`flip` (the written
-        copy becomes ``psi[p]``)."""
-        import struct
-        s = self.s
-        slabs = [sl for c in s.comps for sl in self.slabs[c]]
-        for sl in slabs:
-            if getattr(sl, "psi_alt", None) is None:
-                sl.psi_alt = [torch.zeros_like(x) for x in sl.psi]
-        key = (p,) + tuple(sl.psi[p].data_ptr() for sl in slabs)
-        cache = self.__dict__.setdefault("_dev", {})
-        if key in cache:
-            return cache[key][0]
-        alt_of = {sl.psi[p].data_ptr(): sl.psi_alt[p].data_ptr() for sl in slabs}
-        self.__dict__.pop("_tables", None)  # kernel_table pointers follow psi[p]
-        raw = b""
-        keep = []  # profile tensors the block points at
-        for kind in ("E", "H"):
-            ptrs, ints, kk_ = self.kernel_table(kind, p)
-            keep.append(kk_)
-            for q in range(9):  # 3 components x 3 axes
-                pp = ptrs[5 * q:5 * q + 5]
-                lo0, hi0, lo1, hi1 = ints[4 * q:4 * q + 4]
-                o0 = alt_of.get(pp[0], 0) if pp[0] else 0
-                o1 = alt_of.get(pp[1], 0) if pp[1] else 0
-                raw += struct.pack("<QQQQiiiiQQQ", pp[0] or 0, pp[1] or 0, o0, o1, lo0, lo1, hi0, hi1, pp[2] or 0,
-                                   pp[3] or 0, pp[4] or 0)
-        host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
-        dev = host.to(s.device)
-        cache[key] = (dev, keep, host)
-        return dev
-
-    def shell_arg(self, p: int, ops):
-        """The ``cpml`` argument of ``ops.shell_step`` for plane ``p``: the
-        device block on the HIP backend, (self, p) for the torch oracle."""
-        if ops.name == "hip":
-            return self.host_table(p)
-        return (self, p)
-
-    def flip(self, p: int) -> None:
-        """The copy the last single-step pass wrote becomes plane ``p``'s psi."""
-        self.__dict__.pop("_tables", None)
-        for c in self.s.comps:
-            for sl in self.slabs[c]:
-                sl.psi[p], sl.psi_alt[p] = sl.psi_alt[p], sl.psi[p]
-
     def apply(self, kind: str, p: int, boxes) -> None:
         s = self.s
         F = s.F[p]

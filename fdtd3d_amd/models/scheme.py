@@ -42,6 +42,7 @@ from ..layout.yee import (E_COMPONENTS, H_COMPONENTS, MATERIAL_STENCIL, MATERIAL
                           YeeLayout)
 from ..layout.approximation import approximate_material
 from ..ops.coef import Coef
+from .regions import RegionLevel
 from ..parallel.domain import Domain, box_empty, box_intersect, box_subtract
 from ..utils.assertions import FdtdError, fdtd_assert
 from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
@@ -99,7 +100,6 @@ class SchemeConfig:
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
-    hybrid_shell: str = "auto"               # auto | stepped | single-pass | blocked | mixed (models/blocking.py)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
     dispersion: str = "drude"                # drude | lorentz (metamaterial regions)
@@ -134,7 +134,7 @@ class SchemeConfig:
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
             amplitude_check_steps=s.amplitudeCheckSteps,
-            hybrid_block=s.hybridBlock, hybrid_shell=s.hybridShell,
+            hybrid_block=s.hybridBlock,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
@@ -367,8 +367,6 @@ class YeeScheme(BlockedStepping):
             self.graph_mode = False
         self.hybrid = None
         self._init_hybrid()
-        if self.use_upml_chain and not (self.hybrid is not None and self.hybrid.get("v2")):
-            self._alloc_upml_levels()
         if (self.hybrid is None and cfg.scheme == "3d" and self.ops.name == "hip"
                 and getattr(self, "chain_regions", None) is not None and getattr(self, "_chain_prof", None) is not None):
             # stepped 3D runs: the z PML slabs' chain boxes widened to whole
@@ -377,6 +375,9 @@ class YeeScheme(BlockedStepping):
             # plain update algebraically).  Hybrid runs keep the exact slabs:
             # their core must stay clear of every chain box.
             self._init_chain_regions(self._chain_prof, z_align=128 // self.dtype.itemsize)
+        if self.use_upml_chain:
+            # after the chain boxes are final: region-local levels cover them
+            self._alloc_upml_levels()
         # the eps-layout material grids (fp64, 8 B per cell and material) and
         # the averaged materials only feed the coefficients built above
         self.sampler.free()
@@ -409,9 +410,36 @@ class YeeScheme(BlockedStepping):
             disp_e = cfg.use_metamaterials and scene.uniform("omega_pe") != 0.0
             disp_h = cfg.use_metamaterials and scene.uniform("omega_pm") != 0.0
             nd = 3 * (disp_e + disp_h)  # dispersive components
-            plan["upml_D"] = isz * cells * planes * (3 * nd + 2 * (6 - nd))
+            aux = disp = cells
+            if (cfg.scheme == "3d" and self.halo is None and getattr(self.ops, "region_aux", False)
+                    and not (cfg.use_tfsf and cfg.use_pml and min(cfg.tfsf_size) <= max(self.layout.pml_size))):
+                # region-local levels (models/regions.py): the PML slabs (one
+                # cell of staggering slack per side) and the dispersive box
+                inner = 1
+                for a in range(3):
+                    p_ = self.layout.pml_size[a] + 1 if cfg.use_pml and self.layout.active(a) else 0
+                    inner *= max(0, n[a] - 2 * p_)
+                slabs = cells - inner
+                disp = 0
+                if cfg.use_metamaterials:
+                    if cfg.scene == "drude-sphere":
+                        r = int(math.ceil(cfg.sphere_radius)) + 2
+                        lo = [int(cfg.sphere_center[a]) - r for a in range(3)]
+                        hi = [int(cfg.sphere_center[a]) + r + 1 for a in range(3)]
+                        disp = 1
+                        for a in range(3):
+                            disp *= max(0, min(n[a], hi[a]) - max(0, lo[a]))
+                        # D1 also lives in the PML slabs the dispersive box reaches
+                        pml = [self.layout.pml_size[a] + 1 if cfg.use_pml else 0 for a in range(3)]
+                        if any(lo[a] < pml[a] or hi[a] > n[a] - pml[a] for a in range(3)):
+                            disp += slabs
+                    else:
+                        disp = cells  # (the reference scene's small boxes: bounded by the grid)
+                aux = min(cells, slabs + disp)
+                disp = min(cells, disp)
+            plan["upml_D"] = isz * aux * planes * (3 * nd + 2 * (6 - nd))
             if nd:
-                plan["drude_D1"] = 3 * isz * cells * planes * nd
+                plan["drude_D1"] = 3 * isz * disp * planes * nd
                 lean = self.ops.name == "hip" and cfg.scheme == "3d"
                 plan["drude_coef"] = cells * nd * (2 if lean else 1 + 5 * isz)
         if self.use_cpml:
@@ -639,14 +667,53 @@ class YeeScheme(BlockedStepping):
             st[n] = Coef(1.0, cell=tab[:, q][ids.long()].contiguous())
 
     def _alloc_upml_levels(self) -> None:
-        """Full-grid D / D1 levels of the chain kernels (the stepped shell and
-        stepped runs read them by global cell index)."""
+        """D / D1 levels of the chain kernels: region-local (models/regions.py:
+        D over each component's chain boxes -- the PML slabs and the
+        dispersive box -- D1 over the chain boxes that hold dispersive cells)
+        where every launch is a fused chain launch, full-grid otherwise (2D,
+        the generic D-form path of TF/SF targets inside a chain box)."""
+        reg = self._upml_region_boxes()
+        self.upml_regional = reg is not None
         for c in self.comps:
             st = self.upml[c]
             if st["D"] is None:
-                st["D"] = [[self._zeros() for _ in range(st["nlev"])] for _ in range(self.planes)]
+                if reg is not None:
+                    st["D"] = [[RegionLevel(reg[c][0], self.dtype, self.device) for _ in range(st["nlev"])]
+                               for _ in range(self.planes)]
+                else:
+                    st["D"] = [[self._zeros() for _ in range(st["nlev"])] for _ in range(self.planes)]
             if "D1" in st and st["D1"] is None:
-                st["D1"] = [[self._zeros() for _ in range(3)] for _ in range(self.planes)]
+                if reg is not None:
+                    st["D1"] = [[RegionLevel(reg[c][1], self.dtype, self.device) for _ in range(3)]
+                                for _ in range(self.planes)]
+                else:
+                    st["D1"] = [[self._zeros() for _ in range(3)] for _ in range(self.planes)]
+
+    def _upml_region_boxes(self):
+        """Per component (D boxes, D1 boxes), local, for region-local levels;
+        None when the run needs full-grid levels."""
+        if (self.cfg.scheme != "3d" or getattr(self, "chain_regions", None) is None or self.halo is not None
+                or not getattr(self.ops, "region_aux", False)):
+            # (decomposed runs keep full-grid levels: their z-aligned chain
+            # boxes differ per rank, the halo messages of boxed arrays assume
+            # the same cover on both ends)
+            return None
+        dom = self.domain
+        out = {c: ([], []) for c in self.comps}
+        for kind, comps in (("E", self.e_comps), ("H", self.h_comps)):
+            for r, dru in self.chain_regions[kind]["chain"]:
+                for c in comps:
+                    b = dom.to_local(r[c])
+                    if box_empty(b):
+                        continue
+                    if self.cfg.use_tfsf:
+                        tb = self.tfsf_bbox.get(c)
+                        if tb is not None and not box_empty(box_intersect(b, tb)):
+                            return None  # TF/SF targets in a chain box: the generic full-grid D form
+                    out[c][0].append(b)
+                    if dru[c]:
+                        out[c][1].append(b)
+        return out
 
     def _bbox_global(self, mask: torch.Tensor) -> Box:
         """Global bounding box of the True cells of a local mask (empty box
@@ -719,6 +786,13 @@ class YeeScheme(BlockedStepping):
             regions[kind] = {"plain": [r for r in plain if any(not box_empty(b) for b in r.values())],
                              "chain": [r for r in chain if any(not box_empty(b) for b in r[0].values())]}
         self.chain_regions = regions
+        if getattr(self, "upml_regional", False):
+            # region-local levels follow the (new) chain boxes
+            for c in self.comps:
+                self.upml[c]["D"] = None
+                if "D1" in self.upml[c]:
+                    self.upml[c]["D1"] = None
+            self._alloc_upml_levels()
 
     # ----------------------------------------------------------------- TF/SF
     def _init_tfsf(self) -> None:
@@ -742,10 +816,12 @@ class YeeScheme(BlockedStepping):
         # in-kernel form for the blocked passes (fp32 HIP, incident direction
         # along x or y; models/tfsf.py TfsfSets)
         self.tfsf_sets = None
-        if (self.ops.name == "hip" and self.dtype == torch.float32 and self.cfg.scheme == "3d"
-                and getattr(self.ops, "tfsf_sets_ok", False)):
+        if (self.cfg.scheme == "3d" and getattr(self.ops, "tfsf_sets_ok", False)
+                and (self.ops.name != "hip" or self.dtype == torch.float32)):
             self.tfsf_sets = build_tfsf_sets(self.layout, self.comps, self.domain.origin, self.domain.shape, boxes,
                                              self.device, self.dtype, n)
+            if self.tfsf_sets is not None:
+                self.tfsf_sets.tables = self.tfsf  # the torch oracle's blocked pass applies these
         # local bounding box of each component's TF/SF targets
         self.tfsf_bbox = {}
         for c in self.comps:
@@ -815,7 +891,8 @@ class YeeScheme(BlockedStepping):
         w = self._window(kind)
         return {c: self.local_box(c, w) for c in comps}
 
-    def _update(self, kind: str, p: int, windows: Optional[Sequence[Box]] = None, tfsf_once: bool = False) -> None:
+    def _update(self, kind: str, p: int, windows: Optional[Sequence[Box]] = None, tfsf_once: bool = False,
+                tfsf: bool = True) -> None:
         """Update all E (or H) components of plane ``p`` on the given global
         windows (default: this sub-step's window).  ``tfsf_once``: apply the
         E-form TF/SF corrections once over the whole grid after all windows
@@ -830,7 +907,8 @@ class YeeScheme(BlockedStepping):
             # hybrid shell of a decomposed run: clip to this sub-step's deep-halo window
             dw = self._window(kind)
             windows = [b for b in (box_intersect(w, dw) for w in windows) if not box_empty(b)]
-        tfsf_here = self.cfg.use_tfsf and not tfsf_once
+        use_tfsf = self.cfg.use_tfsf and tfsf
+        tfsf_here = use_tfsf and not tfsf_once
         chain = self.use_upml_chain and getattr(self, "chain_regions", None) is not None
         if chain and self.hybrid is not None and len(windows) > 1:
             # hybrid shell: the chain boxes lie inside the shell, so each runs
@@ -860,7 +938,7 @@ class YeeScheme(BlockedStepping):
                 for c in comps:
                     for tab in self.tfsf[c]:
                         self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
-        if self.cfg.use_tfsf and tfsf_once:
+        if use_tfsf and tfsf_once:
             inc = self.hinc[p] if kind == "E" else self.einc[p]
             alloc = self.domain.allocated_global()
             many = []
@@ -1088,18 +1166,18 @@ class YeeScheme(BlockedStepping):
             sfx = "" if p == 0 else "-im"
             for c in self.comps:
                 out[c + sfx] = self.F[p][c]
-            if self.use_upml_chain and self.hybrid is not None and self.hybrid.get("v2"):
-                if getattr(self, "upml_regions", None) is not None:
-                    out.update(self.upml_regions.named(p, sfx))
-                if getattr(self, "drude_box", None) is not None:
-                    out.update(self.drude_box.named(p, sfx))
-            elif self.use_upml_chain:
+            if self.use_upml_chain:
                 for c in self.comps:
-                    for lv, t in enumerate(self.upml[c]["D"][p]):
-                        out["%s%s-aux%d%s" % ("D" if c[0] == "E" else "B", c[1], lv, sfx)] = t
+                    lists = [("%s%s" % ("D" if c[0] == "E" else "B", c[1]), self.upml[c]["D"][p])]
                     if self.upml[c].get("D1") is not None:
-                        for lv, t in enumerate(self.upml[c]["D1"][p]):
-                            out["%s1%s-aux%d%s" % ("D" if c[0] == "E" else "B", c[1], lv, sfx)] = t
+                        lists.append(("%s1%s" % ("D" if c[0] == "E" else "B", c[1]), self.upml[c]["D1"][p]))
+                    for base, levels in lists:
+                        for lv, t in enumerate(levels):
+                            if isinstance(t, RegionLevel):
+                                for q, part in enumerate(t.data):
+                                    out["%s-aux%d-r%d%s" % (base, lv, q, sfx)] = part
+                            else:
+                                out["%s-aux%d%s" % (base, lv, sfx)] = t
             if self.use_cpml:
                 for c, slabs in self.cpml.slabs.items():
                     for n, sl in enumerate(slabs):
@@ -1118,16 +1196,11 @@ class YeeScheme(BlockedStepping):
         out = []
         for p in range(self.planes):
             out += [self.F[p][c] for c in self.comps]
-            if self.use_upml_chain and self.hybrid is not None and self.hybrid.get("v2"):
-                if getattr(self, "upml_regions", None) is not None:
-                    out += list(self.upml_regions.named(p, "").values())
-                if getattr(self, "drude_box", None) is not None:
-                    out += list(self.drude_box.named(p, "").values())
-            elif self.use_upml_chain:
+            if self.use_upml_chain:
                 for c in self.comps:
-                    out += list(self.upml[c]["D"][p])
-                    if self.upml[c].get("D1") is not None:
-                        out += list(self.upml[c]["D1"][p])
+                    for levels in (self.upml[c]["D"][p], self.upml[c].get("D1") and self.upml[c]["D1"][p]):
+                        for t in (levels or ()):
+                            out += list(t.data) if isinstance(t, RegionLevel) else [t]
             if self.use_cpml:
                 out += self.cpml.state_tensors(p)
         return out
@@ -1140,19 +1213,14 @@ class YeeScheme(BlockedStepping):
         out = []
         for p in range(self.planes):
             out += [None] * len(self.comps)
-            if self.use_upml_chain and self.hybrid is not None and self.hybrid.get("v2"):
-                ur = getattr(self, "upml_regions", None)
-                if ur is not None:
-                    for c in self.comps:
-                        out += [(self.domain.to_global(b), b[0]) for b in ur.boxes if not box_empty(b)]
-                dbx = getattr(self, "drude_box", None)
-                if dbx is not None:
-                    out += [(self.domain.to_global(dbx.box), dbx.box[0])] * len(dbx.named(p, ""))
-            elif self.use_upml_chain:
+            if self.use_upml_chain:
                 for c in self.comps:
-                    out += [None] * len(self.upml[c]["D"][p])
-                    if self.upml[c].get("D1") is not None:
-                        out += [None] * len(self.upml[c]["D1"][p])
+                    for levels in (self.upml[c]["D"][p], self.upml[c].get("D1") and self.upml[c]["D1"][p]):
+                        for t in (levels or ()):
+                            if isinstance(t, RegionLevel):
+                                out += [(self.domain.to_global(b), b[0]) for b in t.boxes]
+                            else:
+                                out.append(None)
             if self.use_cpml:
                 out += self.cpml.state_boxes(p)
         return out
@@ -1174,10 +1242,14 @@ class YeeScheme(BlockedStepping):
 
     in_amplitude = False
 
-    def step(self, windows: Optional[Sequence[Box]] = None) -> None:
+    def step(self, windows: Optional[Sequence[Box]] = None, pre: Optional[Callable] = None,
+             tfsf: bool = True) -> None:
         """Advance one full leapfrog step (serial runs: optionally only on the
         global ``windows``, disjoint boxes -- the stepped shell of a hybrid
-        blocked pass)."""
+        blocked pass).  ``pre(kind, p)`` runs before each half step's update
+        (the history shell writes the core's face values there); ``tfsf`` =
+        False skips the incident line and the TF/SF corrections (a shell with
+        no TF/SF target whose core pass advanced the line)."""
         t = self.t
         cfg = self.cfg
         B = self.domain.buffer_size
@@ -1193,8 +1265,9 @@ class YeeScheme(BlockedStepping):
                 with self.prof.phase("halo-deep"):
                     halo.exchange_all(self)
         ph = self.prof.phase
+        use_tfsf = cfg.use_tfsf and tfsf
         for p in range(self.planes):
-            if cfg.use_tfsf:
+            if use_tfsf:
                 with ph("incident-E"):
                     if self._graph_src is not None:
                         tab, counter, t0 = self._graph_src
@@ -1205,20 +1278,24 @@ class YeeScheme(BlockedStepping):
                 if halo is not None and not deep:
                     halo.finish_and_update(self, "E", p)
                 else:
-                    self._update("E", p, windows, tfsf_once=windows is not None and self._tfsf_once)
+                    if pre is not None:
+                        pre("E", p)
+                    self._update("E", p, windows, tfsf_once=windows is not None and self._tfsf_once, tfsf=tfsf)
             with ph("source"):
                 self._apply_sources(t, p)
             if halo is not None and not deep:
                 with ph("halo-post"):
                     halo.start(self, "E", p)
-            if cfg.use_tfsf:
+            if use_tfsf:
                 with ph("incident-H"):
                     self.ops.inc_step_h(self.einc[p], self.hinc[p], self.inc_ch)
             with ph("H"):
                 if halo is not None and not deep:
                     halo.finish_and_update(self, "H", p)
                 else:
-                    self._update("H", p, windows, tfsf_once=windows is not None and self._tfsf_once)
+                    if pre is not None:
+                        pre("H", p)
+                    self._update("H", p, windows, tfsf_once=windows is not None and self._tfsf_once, tfsf=tfsf)
             if halo is not None and not deep:
                 with ph("halo-post"):
                     halo.start(self, "H", p)
@@ -1538,7 +1615,7 @@ class YeeScheme(BlockedStepping):
                 keep = torch.zeros_like(self.F[p][c], dtype=torch.bool)
                 keep[ub[0][0]:ub[1][0], ub[0][1]:ub[1][1], ub[0][2]:ub[1][2]] = True
                 self.F[p][c].masked_fill_(~keep, 0.0)
-                for alt in (getattr(self, "F_alt", None), getattr(self, "F_3", None)):
+                for alt in (getattr(self, "F_alt", None),):
                     if alt is not None:
                         alt[p][c].copy_(self.F[p][c])
 

@@ -22,6 +22,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..layout.yee import YeeLayout
+from ..models.regions import RegionLevel
 from .coef import Coef
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
@@ -672,7 +673,41 @@ class HipOps:
 
     # ------------------------------------------------------ temporal blocking
     tfsf_sets_ok = True  # the fp32 blocked kernel applies TfsfSets corrections
-    tb_cpml_steps = (1, 4)  # steps per pass of the in-kernel CPML variants (yee3d_tb_cpml.hip)
+
+    def hist_floats(self, shape, steps: int):
+        """(floats, layer stride) of the boundary history of a ``steps``-step
+        pass over an array of ``shape`` (fdtd_tb3d_hist_floats)."""
+        hls = c_int(0)
+        f = self.lib.fdtd_tb3d_hist_floats
+        f.restype = ctypes.c_longlong
+        n = int(f(c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), c_int(steps), ctypes.byref(hls)))
+        return n, int(hls.value)
+
+    def hist_buffer(self, shape, steps: int):
+        """A boundary-history buffer for :meth:`tb_step` (``hist``)."""
+        n, hls = self.hist_floats(shape, steps)
+        return torch.zeros(n, dtype=torch.float32, device=self.device), hls
+
+    def hist_apply(self, F: Dict[str, torch.Tensor], hist, obox: Box, steps: int, kind: str, level: int) -> None:
+        """Write level ``level`` of the history (kind "E": E on the low faces
+        of ``obox``, "H": H on its high faces) into the fields ``F``
+        (aux_kernels.hip k_hist_apply)."""
+        comps = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
+        shape = tuple(F[comps[0]].shape)
+        for c in comps:
+            self._check_tensor(F[c], shape)
+        for d in range(3):
+            if obox[0][d] < 0 or obox[1][d] > shape[d]:
+                raise HipError("hist_apply: box %s outside array %s" % (obox, shape))
+        hbuf, hls = hist
+        if hbuf.numel() < 12 * steps * hls:
+            raise HipError("hist_apply: history buffer too small")
+        rc = self.lib.fdtd_hist_apply_f32((c_vp * 3)(*[F[c].data_ptr() for c in comps]), _ptr(hbuf),
+                                          c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), _box_arr([obox]),
+                                          c_int(steps), c_int(hls), c_int(0 if kind == "E" else 1), c_int(level),
+                                          _stream())
+        _check(rc, "hist_apply")
+        self.launches += 1
 
     def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
                   sets, slot: int = 0) -> torch.Tensor:
@@ -702,8 +737,7 @@ class HipOps:
         return g
 
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None, cpml=None,
-                cpml_axes: int = 0) -> None:
+                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None, hist=None) -> None:
         """``steps`` fused leapfrog steps in one HBM pass (yee3d_tb.hip).
 
         ``boxes`` are the update boxes (each component changes only there, at
@@ -711,10 +745,10 @@ class HipOps:
         never reads outside the arrays whatever the boxes, but the caller must
         give every stored cell ``steps`` valid layers of input around it.
         ``sources`` = per-step list of (E component, local index, value) or
-        None.  ``cpml`` = ``CPML.host_table(p)`` (psi read from ``psi[p]``,
-        written to the other copy: ``CPML.flip`` after the pass), with
-        ``cpml_axes`` the axes (bits) whose slabs the box's dependency cone
-        reaches (0: all); multi-step CPML passes take 4 or 5 steps."""
+        None.  ``tfsf`` = (TfsfSets, g table, first level) from
+        ``tfsf_pass``.  ``hist`` = a buffer from :meth:`hist_buffer`: the
+        pass also records E on the output box's low faces and H on its high
+        faces after every level (read back with :meth:`hist_apply`)."""
         if len(fin) == 3:
             self._tb2d_step(fin, fout, boxes, obox, cb, steps, sources)
             return
@@ -766,22 +800,16 @@ class HipOps:
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
         if tfsf is not None and self.dtype != torch.float32:
             raise HipError("in-kernel TF/SF: fp32 only")
-        pscr, pscr_bytes = None, 0
-        if cpml is not None:
-            if self.dtype != torch.float32 or steps not in self.tb_cpml_steps:
-                raise HipError("in-kernel CPML: fp32, %s steps per pass" % (self.tb_cpml_steps,))
-            if int(self.lib.fdtd_cpmldev_size()) != cpml.numel() or cpml.device.type != "cpu":
-                raise HipError("cpml: the CpmlDev block as host bytes (CPML.host_table)")
-            if steps > 1:
-                if percell:
-                    raise HipError("multi-step CPML passes: uniform media only")
-                # thread-private psi hand-off between the pass's levels
-                f = self.lib.fdtd_tb3d_cpml_scratch_bytes
-                f.restype = ctypes.c_longlong
-                pscr_bytes = int(f(_box_arr([obox]), c_int(self.tb_xchunk), c_int(steps), c_int(tfsf is not None),
-                                   c_int(int(cpml_axes))))
-                pscr = self._scratch(pscr_bytes)
-        if (percell and self.dtype == torch.float32 and self.tb_sparse) or tfsf is not None or cpml is not None:
+        if hist is not None:
+            if self.dtype != torch.float32 or steps > 5:
+                raise HipError("boundary history: fp32, at most 5 steps per pass")
+            hbuf, hls = hist
+            need, want = self.hist_floats(shape, steps)
+            self._check_tensor(hbuf)
+            if hls != want or hbuf.numel() < need:
+                raise HipError("history buffer too small for %s x %d steps" % (shape, steps))
+        if ((percell and self.dtype == torch.float32 and self.tb_sparse) or tfsf is not None
+                or hist is not None):
             # multi-row kernel with sparse per-cell coefficients / TF/SF sets
             if percell and steps > 5:
                 raise HipError("per-cell coefficients: at most 5 steps per pass")
@@ -800,8 +828,9 @@ class HipOps:
                 arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), _ptr(ce), _box_arr([ebox]), _ptr(ch),
                 _box_arr([hbox]), c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk), c_int(steps),
-                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _ptr(cpml), c_int(int(cpml_axes)), _ptr(pscr),
-                ctypes.c_longlong(pscr_bytes), _stream())
+                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _ptr(None if hist is None else hist[0]),
+                ctypes.c_longlong(0 if hist is None else hist[0].numel()), c_int(0 if hist is None else hist[1]),
+                _stream())
             _check(rc, "tb3d_ext")
             self.launches += 1
             return
@@ -825,84 +854,6 @@ class HipOps:
                                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk),
                                 c_int(steps), (c_int * 4)(*src), (c_double * 8)(*vals), _stream())
         _check(rc, "tb3d")
-        self.launches += 1
-
-    def _scratch(self, nbytes: int) -> Optional[torch.Tensor]:
-        """Device scratch of at least ``nbytes`` bytes, reused by every launch
-        on this ops object (stream-ordered: launches of one stream only)."""
-        if nbytes <= 0:
-            return None
-        buf = getattr(self, "_scr", None)
-        if buf is None or buf.numel() * 4 < nbytes:
-            buf = self._scr = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=self.device)
-        return buf
-
-    shell_ok = True  # fused single-step shell kernel (yee3d_shell.hip) present
-
-    def shell_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                   windows: Sequence[Box], ax: Sequence[int], cb: Dict[str, Coef], source=None, cpml=None,
-                   kappa: bool = False, upml=None, drude=None) -> None:
-        """One fused E+H leapfrog step (yee3d_shell.hip) of the shell boxes
-        ``windows`` (local, disjoint): reads ``fin``, writes ``fout`` there.
-        ``ax[w]`` = the CPML axes of box ``w`` (bit 0 x, 1 y, 2 z), ``cpml`` =
-        ``CPML.host_table(p)`` (host bytes, passed by value to the kernel; psi
-        read from the current copy, written to the other: call ``CPML.flip``
-        after), ``source`` = (E component, local
-        index, value) of a hard point source or None.  fp32, scalar
-        coefficients per kind."""
-        E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
-        if self.dtype != torch.float32:
-            raise HipError("shell_step: fp32 only")
-        shape = tuple(fin["Ex"].shape)
-        for c in E + H:
-            self._check_tensor(fin[c], shape)
-            self._check_tensor(fout[c], shape)
-            if fin[c].data_ptr() == fout[c].data_ptr():
-                raise HipError("shell_step needs distinct in/out buffers")
-            if self._cell_or_none(cb[c]) is not None:
-                raise HipError("shell_step: scalar coefficients only")
-        cbv, dbv = cb["Ex"].scalar, cb["Hx"].scalar
-        if any(cb[c].scalar != cbv for c in E) or any(cb[c].scalar != dbv for c in H):
-            raise HipError("shell_step: scalar coefficients must agree per kind")
-        wins = [w for w in windows]
-        if len(wins) != len(ax) or len(wins) > 64 * 10:
-            raise HipError("shell_step: one CPML class per window")
-        for w in wins:
-            for d in range(3):
-                if not _empty(w) and (w[0][d] < 0 or w[1][d] > shape[d]):
-                    raise HipError("shell window %s outside array %s" % (w, shape))
-        if any(a & 8 for a in ax) and drude is None:
-            raise HipError("shell_step: dispersive-box windows without a dispersive table")
-        if drude is not None and int(self.lib.fdtd_shell_drude_size()) != drude.numel():
-            raise HipError("shell dispersive block layout mismatch (%d vs %d bytes)"
-                           % (self.lib.fdtd_shell_drude_size(), drude.numel()))
-        if any(a & 7 for a in ax) and cpml is None and upml is None:
-            raise HipError("shell_step: absorbing-layer windows without a CPML / UPML table")
-        if cpml is not None and upml is not None:
-            raise HipError("shell_step: CPML or UPML, not both")
-        for name, t in (("CPML", cpml), ("UPML", upml), ("dispersive", drude)):
-            if t is not None and (t.is_cuda or t.dtype != torch.uint8 or not t.is_contiguous()):
-                raise HipError("shell_step: the %s block must be host bytes (host_table)" % name)
-        if cpml is not None and int(self.lib.fdtd_shell_cpml_size()) != cpml.numel():
-            raise HipError("shell CPML block layout mismatch")
-        if upml is not None and int(self.lib.fdtd_shell_upml_size()) != upml.numel():
-            raise HipError("shell UPML block layout mismatch (%d vs %d bytes)"
-                           % (self.lib.fdtd_shell_upml_size(), upml.numel()))
-        src = [-1, -1, -1, -1]
-        val = 0.0
-        if source is not None:
-            comp, idx, val = source[0], tuple(source[1]), float(source[2])
-            if comp not in E or any(not (0 <= idx[d] < shape[d]) for d in range(3)):
-                raise HipError("shell_step: E point source inside the array only")
-            src = [idx[0], idx[1], idx[2], E.index(comp)]
-        arr = (c_vp * 6)(*[fin[c].data_ptr() for c in E + H])
-        out = (c_vp * 6)(*[fout[c].data_ptr() for c in E + H])
-        rc = self.lib.fdtd_shell1_f32(arr, out, c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]),
-                                      c_int(shape[2]), _box_arr([boxes[c] for c in E + H]), c_int(len(wins)),
-                                      _box_arr(wins) if wins else (c_int * 1)(0), (c_int * max(1, len(ax)))(*ax),
-                                      (c_int * 4)(*src), c_double(val), _ptr(cpml), c_int(1 if kappa else 0),
-                                      _ptr(upml), _ptr(drude), _stream())
-        _check(rc, "shell1")
         self.launches += 1
 
     def _tb2d_step(self, fin, fout, boxes, obox, cb, steps, sources) -> None:
@@ -1021,16 +972,32 @@ class HipOps:
                 any_box = True
                 self._check_stencil_box(kind, c, b, shape)
             D = st["D"][p]
-            fields = [F[c], D[-1], D[0], D[1] if drude else None]
+            aux = [D[-1], D[0], D[1] if drude else None]
             if drude:
                 D1 = st["D1"][p]
-                fields += [D1[2], D1[0], D1[1]]
+                aux += [D1[2], D1[0], D1[1]]
             else:
-                fields += [None, None, None]
-            fields += [F[terms[0][0]], F[terms[1][0]]]
-            for t in fields:
-                if t is not None:
-                    self._check_tensor(t, shape)
+                aux += [None, None, None]
+            dbox = ((0, 0, 0), (0, 0, 0))
+            if isinstance(D[0], RegionLevel):
+                # region-local levels (models/regions.py): the parts holding this launch's box
+                parts = [None if t is None else t.part(b) for t in aux]
+                boxes_ = {pt[1] for pt in parts if pt is not None and pt[0] is not None}
+                if len(boxes_) > 1:
+                    raise HipError("chain_update: D / D1 parts of %s in different storage boxes" % c)
+                dbox = boxes_.pop() if boxes_ else dbox
+                aux = [None if pt is None else pt[0] for pt in parts]
+                dshape = tuple(dbox[1][d] - dbox[0][d] for d in range(3))
+                for t in aux:
+                    if t is not None:
+                        self._check_tensor(t, dshape)
+            else:
+                for t in aux:
+                    if t is not None:
+                        self._check_tensor(t, shape)
+            fields = [F[c]] + aux + [F[terms[0][0]], F[terms[1][0]]]
+            for t in (F[c], F[terms[0][0]], F[terms[1][0]]):
+                self._check_tensor(t, shape)
             aD, aA, aB = pr["axes"]
             profs = [pr["caD"], pr["cbD"], pr["caE"], pr["ica"], pr["cbEa"], pr["ccEa"]]
             for t, a in zip(profs, (aD, aD, aA, aA, aB, aB)):
@@ -1072,7 +1039,7 @@ class HipOps:
             P += [None if t is None else t.data_ptr() for t in fields + profs + [cell] + dr + list(lut) + [pcell]]
             S += [float(pr["s"]), pcb]
             I += ([terms[0][1], terms[1][1], terms[0][2], terms[1][2], aD, aA, aB] + list(b[0]) + list(b[1])
-                  + list(pb[0]) + list(pb[1]))
+                  + list(pb[0]) + list(pb[1]) + list(dbox[0]) + list(dbox[1]))
         if not any_box:
             return
         if rows is not None:
@@ -1096,6 +1063,7 @@ class HipOps:
     chain_rows = True  # dispersive chain launches on sigma = 0 boxes: chain inside the per-row material range only
     drude_lut = True  # Drude chain: uint8 material index + coefficient table (falls back past 256 tuples)
     chain_fold = True  # thin plain boxes next to a z PML slab ride in the slab's chain launch
+    region_aux = True  # chain launches address region-local D / D1 levels (models/regions.py)
 
     def _drude_lut(self, st: dict, dr, shape):
         """(uint8 id array, (n, 5) table) of a component's five Drude

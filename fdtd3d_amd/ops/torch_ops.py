@@ -23,6 +23,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..layout.yee import UPML_AXES, YeeLayout
+from ..models.regions import RegionLevel
 from .coef import Coef
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
@@ -59,6 +60,7 @@ def cb_pad(cb: Dict[str, Coef]) -> Dict[str, Coef]:
 class TorchOps:
     name = "torch"
     chain_rows = True  # same launch plan as the HIP backend (row-range dispersive split)
+    region_aux = True  # chain_update addresses region-local D / D1 levels (models/regions.py)
 
     def __init__(self, layout: YeeLayout, device, dtype):
         self.layout = layout
@@ -167,22 +169,38 @@ class TorchOps:
         return True
 
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                obox: Box, cb: Dict[str, Coef], steps: int, sources=None) -> None:
+                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None, hist=None) -> None:
         """Reference semantics of the temporally blocked kernel: ``steps``
         fused steps on the update boxes (reads outside the arrays count as
         zero, like the kernel's unloaded rows), then only ``obox`` ∩ each
-        component's box is written to ``fout``."""
+        component's box is written to ``fout``.  ``tfsf`` = (TfsfSets, g
+        table, first level): each level adds coef * g to the set's target
+        cells after the curl update (the kernel adds g to the curl); ``hist``
+        = (buffer, layer stride): E on the low faces of ``obox`` after every
+        level, H on its high faces after every level but the last (layout of
+        csrc/tb3d_mr.h)."""
         pad = {c: torch.nn.functional.pad(fin[c], (1, 1, 1, 1, 1, 1)) for c in fin}
         shifted = {c: ((b[0][0] + 1, b[0][1] + 1, b[0][2] + 1), (b[1][0] + 1, b[1][1] + 1, b[1][2] + 1))
                    for c, b in boxes.items()}
+        cbp = cb_pad(cb)
+        e = {c: b for c, b in shifted.items() if c[0] == "E"}
+        h = {c: b for c, b in shifted.items() if c[0] == "H"}
         cur = pad
         for l in range(steps):
             nxt = {c: cur[c].clone() for c in cur}
-            src = None
+            self.curl_update("E", e, nxt, cur, cbp)
             if sources is not None and sources[l] is not None:
                 comp, idx, val = sources[l]
-                src = (comp, tuple(i + 1 for i in idx), val)
-            self.fused_step(cur, nxt, shifted, cb_pad(cb), src)
+                nxt[comp][tuple(i + 1 for i in idx)] = val
+            if tfsf is not None:
+                self._tfsf_level(nxt, tfsf, l, "E", shifted, cbp)
+            if hist is not None:
+                self._hist_record(nxt, hist, obox, steps, "E", l)
+            self.curl_update("H", h, nxt, nxt, cbp)
+            if tfsf is not None:
+                self._tfsf_level(nxt, tfsf, l, "H", shifted, cbp)
+            if hist is not None and l < steps - 1:
+                self._hist_record(nxt, hist, obox, steps, "H", l)
             cur = nxt
         for c, b in boxes.items():
             ob = box_intersect_(b, obox)
@@ -191,112 +209,106 @@ class TorchOps:
                 sp = tuple(slice(s.start + 1, s.stop + 1) for s in sl)
                 fout[c][sl] = cur[c][sp]
 
-    def shell_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                   windows, ax, cb: Dict[str, Coef], source=None, cpml=None, kappa: bool = False,
-                   upml=None, drude=None) -> None:
-        """Reference semantics of the fused single-step shell kernel
-        (yee3d_shell.hip): one leapfrog step of every update box from ``fin``
-        (CPML psi read from ``psi[p]``, written to ``psi_alt[p]``; ``cpml`` =
-        (CPML, p); UPML D read from / written to the two copies of ``upml`` =
-        (UPMLRegions, p) inside its D boxes), of which only the ``windows``
-        are stored to ``fout``.  ``ax`` (the kernel's per-box class) does not
-        change the result."""
-        tmp = {c: fin[c].clone() for c in fin}
-        ureg, up = upml if upml is not None else (None, 0)
-
-        def upml_kind(kind, src):
-            if ureg is None:
-                return
-            rd, wr = ureg.cur[up], 1 - ureg.cur[up]
-            for c, box in (e if kind == "E" else h).items():
-                aD, aA, aB = UPML_AXES[c]
-                for q, qb in enumerate(ureg.boxes):
-                    sub = box_intersect_(box, qb)
-                    if _empty(sub):
-                        continue
-                    sl = box_slices(sub)
-                    curl = self.curl(kind, c, sl, src)
-                    dsl = tuple(slice(sub[0][d] - qb[0][d], sub[1][d] - qb[0][d]) for d in range(3))
-
-                    def pair(a):
-                        v = ureg.pairs[c][a][sl[a]]
-                        shape = [1, 1, 1]
-                        shape[a] = -1
-                        return v[:, 0].view(shape), v[:, 1].view(shape)
-
-                    caD, cbD = pair(aD)
-                    caE, ica = pair(aA)
-                    cbEa, ccEa = pair(aB)
-                    D = ureg.D[up][c][rd][q][dsl]
-                    Dn = caD * D + cbD * curl
-                    tmp[c][sl] = caE * fin[c][sl] + ureg.scal[c] * ica * (cbEa * Dn + ccEa * D)
-                    ureg.D[up][c][wr][q][dsl] = Dn
-        e = {c: b for c, b in boxes.items() if c[0] == "E"}
-        h = {c: b for c, b in boxes.items() if c[0] == "H"}
-        cp, p = cpml if cpml is not None else (None, 0)
-
-        def psi_terms(kind, src):
-            if cp is None:
-                return
-            for c, box in (e if kind == "E" else h).items():
-                for sl in cp.slabs[c]:
-                    if getattr(sl, "psi_alt", None) is None:
-                        sl.psi_alt = [torch.zeros_like(x) for x in sl.psi]
-                    sl.psi_alt[p].copy_(sl.psi[p])
-                    b = box_intersect_(box, sl.lbox)
-                    self.cpml_apply(kind, tmp[c], src[sl.src], sl.axis, sl.sign, sl.psi_alt[p], sl.lbox, b, sl.b,
-                                    sl.c, sl.kinv_m1, cb[c])
-
-        dbox, dp = drude if drude is not None else (None, 0)
-
-        def drude_kind(kind, src):
-            # dispersive box: the chain where the material index is set, the
-            # plain update (already in tmp) elsewhere
-            if dbox is None:
-                return
-            B = dbox.box
-            for c, box in (e if kind == "E" else h).items():
-                if c not in dbox.ids:
+    def _tfsf_level(self, F, tfsf, l: int, kind: str, boxes, cb) -> None:
+        """TF/SF corrections of level ``l`` of a blocked pass on fields padded
+        by one cell: the E-form tables of the stepped path (``sets.tables``,
+        models/scheme.py ``_init_tfsf``) applied from the incident line as it
+        stood at that level (recorded by :meth:`tfsf_pass`), so a blocked
+        pass is bit-for-bit the stepped arithmetic."""
+        sets, g, level0 = tfsf
+        hin, ein = g.lines[level0 + l]
+        inc = hin if kind == "E" else ein
+        shape = tuple(F["Ex"].shape)
+        for c in (("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")):
+            for tab in sets.tables.get(c, ()):
+                if tab.n == 0:
                     continue
-                sub = box_intersect_(box, B)
-                if _empty(sub):
-                    continue
-                sl = box_slices(sub)
-                bsl = tuple(slice(sub[0][d] - B[0][d], sub[1][d] - B[0][d]) for d in range(3))
-                curl = self.curl(kind, c, sl, src)
-                ids = dbox.ids[c][bsl].long()
-                m = ids > 0
-                lut = dbox.lut[c].to(curl.dtype)
-                co = lut[(ids - 1).clamp(min=0)]  # (..., 5)
-                caD, cbD, caE, sica, cbEa, ccEa = dbox.scal[c]
-                Dl, D1l = dbox.D[dp][c], dbox.D1[dp][c]
-                D, Dp, D1, D1p = Dl[0][bsl], Dl[1][bsl], D1l[0][bsl], D1l[1][bsl]
-                Dn = caD * D + cbD * curl
-                D1n = co[..., 0] * Dn + co[..., 1] * D + co[..., 2] * Dp + co[..., 3] * D1 + co[..., 4] * D1p
-                En = caE * fin[c][sl] + sica * (cbEa * D1n + ccEa * D1)
-                tmp[c][sl] = torch.where(m, En, tmp[c][sl])
-                Dl[2][bsl] = torch.where(m, Dn, Dl[2][bsl])
-                D1l[2][bsl] = torch.where(m, D1n, D1l[2][bsl])
+                off = tab.__dict__.setdefault("_pad_off", {}).get(shape)
+                if off is None:
+                    ijk = tab.ijk.long() + 1
+                    off = tab._pad_off[shape] = (ijk[:, 0] * shape[1] + ijk[:, 1]) * shape[2] + ijk[:, 2]
+                v = (inc[tab.i0] * tab.w0 + inc[tab.i0 + 1] * tab.w1) * tab.coef
+                F[c].view(-1).index_add_(0, off, v.to(F[c].dtype))
 
-        self.curl_update("E", e, tmp, fin, cb)
-        psi_terms("E", fin)
-        upml_kind("E", fin)
-        drude_kind("E", fin)
-        if source is not None:
-            comp, idx, val = source
-            tmp[comp][tuple(idx)] = val
-        self.curl_update("H", h, tmp, tmp, cb)
-        psi_terms("H", tmp)
-        upml_kind("H", tmp)
-        drude_kind("H", tmp)
-        for w in windows:
-            if _empty(w):
-                continue
-            sl = box_slices(w)
-            for c in fout:
-                fout[c][sl] = tmp[c][sl]
+    @staticmethod
+    def _hist_slot(hist, steps: int, kind: int, l: int, a: int, q: int):
+        buf, hls = hist
+        o = ((((kind * steps + l) * 3 + a) * 2 + q) * hls)
+        return buf[o:o + hls]
 
-    chain_fold = True
+    def _hist_record(self, F, hist, obox: Box, steps: int, kind: str, l: int) -> None:
+        """Face values of one level into the history (F padded by one cell)."""
+        k = 0 if kind == "E" else 1
+        comps = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
+        n = tuple(F[comps[0]].shape[d] - 2 for d in range(3))
+        lo, hi = obox
+        f = [lo[d] if k == 0 else hi[d] - 1 for d in range(3)]
+        for a in range(3):
+            rng = [slice(lo[d] + 1, hi[d] + 1) for d in range(3)]
+            rng[a] = f[a] + 1
+            o = [d for d in range(3) if d != a]
+            for q, cq in enumerate(o):
+                v = F[comps[cq]][tuple(rng)]
+                lay = self._hist_slot(hist, steps, k, l, a, q)[:n[o[0]] * n[o[1]]].view(n[o[0]], n[o[1]])
+                lay[lo[o[0]]:hi[o[0]], lo[o[1]]:hi[o[1]]] = v.to(lay.dtype)
+
+    def hist_floats(self, shape, steps: int):
+        hls = max(shape[1] * shape[2], shape[0] * shape[2], shape[0] * shape[1])
+        return 12 * steps * hls, hls
+
+    def hist_buffer(self, shape, steps: int):
+        n, hls = self.hist_floats(shape, steps)
+        return torch.zeros(n, dtype=self.dtype, device=self.device), hls
+
+    def hist_apply(self, F: Dict[str, torch.Tensor], hist, obox: Box, steps: int, kind: str, level: int) -> None:
+        """Level ``level`` of the history into ``F`` (csrc/aux_kernels.hip
+        k_hist_apply)."""
+        k = 0 if kind == "E" else 1
+        comps = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
+        n = tuple(F[comps[0]].shape)
+        lo, hi = obox
+        f = [lo[d] if k == 0 else hi[d] - 1 for d in range(3)]
+        for a in range(3):
+            rng = [slice(lo[d], hi[d]) for d in range(3)]
+            rng[a] = f[a]
+            o = [d for d in range(3) if d != a]
+            for q, cq in enumerate(o):
+                lay = self._hist_slot(hist, steps, k, level, a, q)[:n[o[0]] * n[o[1]]].view(n[o[0]], n[o[1]])
+                F[comps[cq]][tuple(rng)] = lay[lo[o[0]]:hi[o[0]], lo[o[1]]:hi[o[1]]].to(F[comps[cq]].dtype)
+
+    tfsf_sets_ok = True  # tb_step applies TfsfSets corrections (the blocked kernel's form)
+
+    def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
+                  sets, slot: int = 0) -> torch.Tensor:
+        """Reference semantics of k_tfsf_pass (yee3d_tb.hip): the incident
+        line advanced ``len(src_vals)`` steps, the per-level g table of the
+        pass returned (levels x sets.ld)."""
+        T = len(src_vals)
+        n = einc.numel()
+        m = min(n, reach)
+        ld = sets.ld
+        g = torch.zeros(max(8, T) * max(1, ld), dtype=einc.dtype, device=einc.device)
+        i0 = sets.i0.long()
+        w0, w1, cc = sets.w0.to(einc.dtype), sets.w1.to(einc.dtype), sets.c.to(einc.dtype)
+        ne = sets.n_e
+        g.lines = []  # (H line before, E line after) each level's E half step: _tfsf_level
+        for l in range(T):
+            hin = hinc.clone()
+            if ne:
+                g[l * ld:l * ld + ne] = cc[:ne] * (w0[:ne] * hinc[i0[:ne]] + w1[:ne] * hinc[i0[:ne] + 1])
+            if m > 0:
+                new = einc[:m].clone()
+                if m > 1:
+                    new[1:m] = einc[1:m] + ce * (hinc[0:m - 1] - hinc[1:m])
+                new[0] = src_vals[l]
+                einc[:m] = new
+            g.lines.append((hin, einc.clone()))
+            if ld > ne:
+                g[l * ld + ne:(l + 1) * ld] = cc[ne:] * (w0[ne:] * einc[i0[ne:]] + w1[ne:] * einc[i0[ne:] + 1])
+            mh = min(m, n - 1)
+            if mh > 0:
+                hinc[:mh] += ch * (einc[:mh] - einc[1:mh + 1])
+        return g
 
     def chain_update(self, kind: str, boxes: Dict[str, Box], F: Dict[str, torch.Tensor], upml: Dict[str, dict],
                      p: int, drude: bool, plain_form: bool = False, plain: Optional[Dict[str, Box]] = None,
@@ -318,27 +330,31 @@ class TorchOps:
             sl = box_slices(box)
             curl = self.curl(kind, c, sl, F)
             mask = None if rows is None else self._row_mask(rows, box)
+
+            def lv(t, box=box, sl=sl):
+                # full-grid level or region-local one (models/regions.py)
+                return t.view(box) if isinstance(t, RegionLevel) else t[sl]
             D = st["D"][p]
-            Dn = st["caD"].materialize(sl) * D[0][sl] + st["cbD"].materialize(sl) * curl
-            nw, old = Dn, D[0][sl]
-            upd = [(D[-1], Dn)]
+            Dn = st["caD"].materialize(sl) * lv(D[0]) + st["cbD"].materialize(sl) * curl
+            nw, old = Dn, lv(D[0])
+            upd = [(lv(D[-1]), Dn)]
             if drude:
                 D1 = st["D1"][p]
-                D1n = (st["b0"].materialize(sl) * Dn + st["b1"].materialize(sl) * D[0][sl]
-                       + st["b2"].materialize(sl) * D[1][sl] + st["ma1"].materialize(sl) * D1[0][sl]
-                       + st["ma2"].materialize(sl) * D1[1][sl])
-                upd.append((D1[2], D1n))
-                nw, old = D1n, D1[0][sl]
+                D1n = (st["b0"].materialize(sl) * Dn + st["b1"].materialize(sl) * lv(D[0])
+                       + st["b2"].materialize(sl) * lv(D[1]) + st["ma1"].materialize(sl) * lv(D1[0])
+                       + st["ma2"].materialize(sl) * lv(D1[1]))
+                upd.append((lv(D1[2]), D1n))
+                nw, old = D1n, lv(D1[0])
             cbE, ccE = (st["plain"]["cbE"], st["plain"]["ccE"]) if plain_form else (st["cbE"], st["ccE"])
             En = st["caE"].materialize(sl) * F[c][sl] + cbE.materialize(sl) * nw + ccE.materialize(sl) * old
             if mask is not None:
                 En = torch.where(mask, En, F[c][sl] + cb[c].materialize(sl) * curl)
-                upd = [(t, torch.where(mask, v, t[sl])) for t, v in upd]
+                upd = [(t, torch.where(mask, v, t)) for t, v in upd]
             new.append((c, sl, En, upd))
         # every component reads the other kind only: the stores can follow in any order
         for c, sl, En, upd in new:
             for t, v in upd:
-                t[sl] = v
+                t.copy_(v)
             F[c][sl] = En
 
     @staticmethod

@@ -11,7 +11,10 @@ from fdtd3d_amd.ops import make_ops
 
 
 def _run(cfg, regional: bool):
-    s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+    ops = make_ops("torch", None, "cpu", torch.float64)
+    if not regional:
+        ops.region_aux = False  # full-grid D / D1 levels for the every-cell chain
+    s = YeeScheme(cfg, ops)
     s.init_scheme()
     s.init_grids()
     if not regional:

@@ -110,51 +110,52 @@ def test_hybrid_checkpoint_resume(tmp_path):
         assert torch.equal(full.F[0][c], resumed.F[0][c]), c
 
 
-@pytest.mark.parametrize("name,extra", [
-    ("cpml-tfsf-oblique", dict(use_pml=True, pml_type="cpml", pml_size=(4, 4, 4), theta=60, phi=20, psi=30)),
-    ("tfsf-oblique-open", dict(theta=60, phi=20, psi=30)),
-    ("cpml-point-kappa", dict(use_pml=True, pml_type="cpml", pml_size=(5, 4, 6), use_tfsf=False, cpml_kappa_max=4.0)),
-    ("upml-tfsf-oblique", dict(use_pml=True, pml_size=(4, 5, 6), tfsf_size=(9, 9, 9), theta=60, phi=20, psi=30)),
-    ("upml-point", dict(use_pml=True, pml_size=(6, 6, 6), use_tfsf=False)),
-])
-def test_single_pass_shell_matches_stepped(name, extra):
-    """The single-pass shell (fused step kernel semantics, TF/SF tables added
-    around it, shrinking windows cut at the CPML slabs), when asked for,
-    reproduces the stepped run from random fields, through two full passes
-    and a short tail (incidence at any angle: reference
-    YeeGridLayout.cpp:327-809)."""
-    kw = dict(scheme="3d", size=(96, 88, 96), dtype="f64", tfsf_size=(8, 8, 8), scene="vacuum", use_tfsf=True,
-              time_steps=11, hybrid_shell="single-pass")
+HIST_CASES = [
+    # TF/SF along +x (the reference default) and +y: in-kernel TfsfSets, the
+    # TF/SF faces inside the core
+    ("cpml-tfsf-x", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 11),
+    ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90), 3, 10),
+    ("upml-tfsf-x", dict(scene="vacuum", use_pml=True, use_tfsf=True), 5, 12),
+    ("cpml-point", dict(scene="vacuum", use_pml=True, pml_type="cpml"), 5, 11),
+    ("drude-upml", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, sphere_center=(36.0, 36.0, 36.0),
+                        sphere_radius=6.0), 3, 8),
+    ("drude-nopml-face", dict(scene="drude-sphere", use_metamaterials=True, sphere_center=(9.0, 30.0, 40.0),
+                              sphere_radius=6.0), 4, 9),
+    ("sphere-cpml-tfsf", dict(scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
+                              sphere_center=(36.0, 36.0, 36.0), sphere_radius=9.0), 3, 7),
+    ("cpml-tfsf-complex", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, complex_values=True),
+     3, 7),
+    # TF/SF faces inside the stepped shell (distance 2 < PML 4 + margin)
+    ("cpml-tfsf-near", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, tfsf_size=(2, 2, 2)), 3, 8),
+]
+
+
+@pytest.mark.parametrize("name,extra,T,steps", HIST_CASES, ids=[c[0] for c in HIST_CASES])
+def test_history_shell_matches_stepped(name, extra, T, steps):
+    """History shell (models/blocking.py ``_hybrid_hist_plan``): the core
+    pass records its face values at every level, the stepped shell advances
+    no core cell -- and the run equals stepping everything, from random
+    fields, through full passes and a short tail."""
+    kw = dict(BASE)
     kw.update(extra)
-    cfg = SchemeConfig(hybrid_block=4, **kw)
+    cfg = SchemeConfig(time_steps=steps, hybrid_block=1, **kw)
     runs = []
-    for hb in (4, 1):
+    for hb in (T, 1):
         s = YeeScheme(dataclasses.replace(cfg, hybrid_block=hb), make_ops("torch", None, "cpu", torch.float64))
         s.init_scheme()
         s.init_grids()
         if hb > 1:
-            assert s.hybrid is not None and s.hybrid.get("v2"), "single-pass shell not selected"
-        s.randomize_fields(seed=3)
+            assert s.hybrid is not None and s.hybrid.get("kind") == "history-shell", "history shell not selected"
+            assert len(s.hybrid["shell"]) == len(s.hybrid["copy"])
+        s.randomize_fields(seed=5)
         s.perform_steps()
         runs.append(s)
     hy, st = runs
-    if hy.use_upml_chain:
-        # the UPML auxiliaries live in the boxes around the all-sigma-zero core only
-        assert hy.upml_regions is not None and all(hy.upml[c]["D"] is None for c in hy.comps)
-        assert hy.upml_regions.cells() < 0.5 * hy.cells()
-    for c in st.comps:
-        b = st.F[0][c]
-        err = float((hy.F[0][c] - b).abs().max())
-        assert err <= 1e-12 * float(b.abs().max()), (name, c, err)
-
-
-def test_auto_hybrid_keeps_stepped_shell():
-    """``hybrid_shell`` = auto takes the stepped shell (the faster one at
-    512^3, models/blocking.py _hybrid2_ok); single-pass must be asked for."""
-    kw = dict(scheme="3d", size=(96, 88, 96), dtype="f64", pml_size=(6, 6, 6), tfsf_size=(8, 8, 8), scene="vacuum",
-              use_pml=True, pml_type="cpml", use_tfsf=True, time_steps=4, hybrid_block=4)
-    for mode, v2 in (("auto", False), ("stepped", False), ("single-pass", True)):
-        s = YeeScheme(SchemeConfig(hybrid_shell=mode, **kw), make_ops("torch", None, "cpu", torch.float64))
-        s.init_scheme()
-        s.init_grids()
-        assert s.hybrid is not None and bool(s.hybrid.get("v2")) == v2, mode
+    for p in range(st.planes):
+        for c in st.comps:
+            b = st.F[p][c]
+            scale = max(float(st.F[p][o].abs().max()) for o in st.comps if o[0] == c[0]) + 1e-300
+            err = float((hy.F[p][c] - b).abs().max())
+            assert err <= 1e-12 * scale, (name, c, err, scale)
+    if st.cfg.use_tfsf:
+        assert torch.equal(hy.einc[0], st.einc[0]) and torch.equal(hy.hinc[0], st.hinc[0])

@@ -32,13 +32,14 @@ CASES = [
                            scene="vacuum", use_pml=True, use_tfsf=True, phi=30), 7, 23),
     ("tez-cpml-tfsf", dict(scheme="tez", size=(96, 128, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
                            scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=60), 5, 17),
-    # single-pass shell (CPML psi and TF/SF sets inside the multi-row kernel, shrinking windows)
-    ("cpml-tfsf-x", dict(hybrid_shell="single-pass", scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 13),
-    ("cpml-tfsf-y", dict(hybrid_shell="single-pass", scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0), 3, 11),
-    ("cpml-tfsf-sphere", dict(hybrid_shell="single-pass", scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
+    # history shell (TF/SF along x / y inside the core pass, no band)
+    ("cpml-tfsf-x", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 13),
+    ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0), 3, 11),
+    ("cpml-tfsf-sphere", dict(scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
                               sphere_center=(40.0, 36.0, 48.0), sphere_radius=10.0), 4, 10),
-    ("cpml-point-T5", dict(hybrid_shell="single-pass", scene="vacuum", use_pml=True, pml_type="cpml"), 5, 12),
-    ("cpml-tfsf-complex", dict(hybrid_shell="single-pass", scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, complex_values=True),
+    ("cpml-point-T5", dict(scene="vacuum", use_pml=True, pml_type="cpml"), 5, 12),
+    ("upml-tfsf-x-T5", dict(scene="vacuum", use_pml=True, use_tfsf=True), 5, 12),
+    ("cpml-tfsf-complex", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, complex_values=True),
      2, 7),
     ("tmz-upml-point-f64", dict(scheme="tmz", size=(150, 90, 1), pml_size=(8, 8, 1), scene="vacuum", use_pml=True,
                                 dtype="f64"), 6, 19),
@@ -67,9 +68,8 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
     assert hy.hybrid is not None, "hybrid plan rejected"
     st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, dt)
     assert st.hybrid is None
-    if cfg.hybrid_shell == "single-pass" and cfg.scene != "sphere":
-        # (per-cell coefficients keep the stepped shell)
-        assert hy.hybrid.get("v2"), "single-pass shell not selected"
+    if cfg.scheme == "3d" and cfg.dtype == "f32" and (not cfg.use_tfsf or hy.tfsf_sets is not None):
+        assert hy.hybrid.get("kind") == "history-shell", "history shell not selected"
     ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
     for p in range(ref.planes):
         for c in ref.comps:
@@ -92,24 +92,31 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
                 assert err <= 1e-4 * float(y.abs().max()) + tol * src_scale, (name, c, "psi", err, src_scale)
 
 
-@pytest.mark.parametrize("T,tfsf", [(4, True), (3, False), (5, True)])
-def test_hybrid2_random_fields(gpu, T, tfsf):
-    """Single-pass shell on random initial fields: every CPML slab carries
-    field from the first step on, so the in-kernel psi terms are exercised."""
-    base = dict(BASE, size=(96, 88, 96)) if T >= 5 else BASE  # the core must keep >= 25% of the cells
-    cfg = SchemeConfig(time_steps=2 * T + 1, **base, scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=tfsf,
-                       hybrid_shell="single-pass")
+@pytest.mark.parametrize("T,tfsf,point,size,phi", [(4, True, False, (96, 88, 96), 0.0),
+                                                   (5, True, True, (80, 72, 96), 0.0),
+                                                   (4, False, True, (72, 80, 64), 0.0),
+                                                   (3, True, False, (64, 64, 128), 90.0),
+                                                   (5, False, True, (112, 96, 100), 0.0)])
+def test_history_shell_random_fields(gpu, T, tfsf, point, size, phi):
+    """History shell from random fields (every face and slab carries field
+    from step 1): the core pass's face history and in-kernel TF/SF against
+    the stepped run; 2T + 1 steps = two passes and a one-step tail."""
+    cfg = SchemeConfig(time_steps=2 * T + 1, scheme="3d", size=size, dtype="f32", pml_size=(5, 6, 7),
+                       tfsf_size=(9, 10, 11), scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=tfsf, phi=phi)
+    if point:
+        cfg = dataclasses.replace(cfg, use_point_source=True)
     runs = {}
     for hb in (T, 1):
         s = YeeScheme(dataclasses.replace(cfg, hybrid_block=hb), make_ops("hip", None, gpu, torch.float32))
         s.init_scheme()
         s.init_grids()
-        s.randomize_fields(seed=5)
+        s.randomize_fields(seed=11)
         s.perform_steps()
         torch.cuda.synchronize()
         runs[hb] = s
     hy, st = runs[T], runs[1]
-    assert hy.hybrid is not None and hy.hybrid.get("v2")
+    assert hy.hybrid is not None and hy.hybrid.get("kind") == "history-shell", "history shell not selected"
+    assert st.hybrid is None
     for c in hy.comps:
         x, y = hy.F[0][c].double().cpu(), st.F[0][c].double().cpu()
         scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])
@@ -118,7 +125,27 @@ def test_hybrid2_random_fields(gpu, T, tfsf):
         for a, b in zip(hy.cpml.slabs[c], st.cpml.slabs[c]):
             err = float((a.psi[0].double() - b.psi[0].double()).abs().max())
             assert err <= 2e-5 * src_scale, (c, "psi", err, src_scale)
-        assert max(float(b.psi[0].abs().max()) for b in st.cpml.slabs[c]) > 1e-3 * src_scale  # psi is live
+
+
+def test_history_negative_control(gpu):
+    """Without the history write-back the shell next to the core reads stale
+    face values: the run must then differ from the stepped one (the test
+    above would catch a history that does nothing)."""
+    cfg = SchemeConfig(time_steps=9, scheme="3d", size=(80, 72, 96), dtype="f32", pml_size=(5, 5, 5),
+                       tfsf_size=(8, 8, 8), scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True)
+    runs = {}
+    for hb in (4, 1):
+        s = YeeScheme(dataclasses.replace(cfg, hybrid_block=hb), make_ops("hip", None, gpu, torch.float32))
+        s.init_scheme()
+        s.init_grids()
+        if hb > 1:
+            s.ops.hist_apply = lambda *a, **k: None
+        s.randomize_fields(seed=3)
+        s.perform_steps()
+        torch.cuda.synchronize()
+        runs[hb] = s
+    err = max(float((runs[4].F[0][c] - runs[1].F[0][c]).abs().max()) for c in runs[1].comps)
+    assert err > 1e-3, err
 
 
 SCALE_CASES = [
@@ -160,44 +187,3 @@ def test_hybrid_at_scale(gpu, name, extra):
         del scale
     del runs, hy, st
     torch.cuda.empty_cache()
-
-
-@pytest.mark.parametrize("T,tfsf,point,size", [(4, True, False, (96, 88, 96)), (4, True, True, (80, 72, 96)),
-                                               (4, False, True, (72, 80, 64)), (4, True, False, (64, 64, 128)),
-                                               (4, False, True, (112, 96, 100))])
-@pytest.mark.parametrize("mode", ["blocked", "mixed"])
-def test_hybrid3_blocked_shell(gpu, T, tfsf, point, size, mode):
-    """Blocked shell (every box one T-step launch: the CPML + TF/SF variant
-    of the multi-row kernel carries psi through the pass's levels) vs the
-    stepped run, from random fields so every slab carries field from step 1;
-    2T + 1 steps = two passes and a one-step tail."""
-    cfg = SchemeConfig(time_steps=2 * T + 1, scheme="3d", size=size, dtype="f32", pml_size=(5, 6, 7),
-                       tfsf_size=(9, 10, 11), scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=tfsf,
-                       hybrid_shell=mode)
-    if point:
-        cfg = dataclasses.replace(cfg, use_point_source=True)
-    runs = {}
-    for hb in (T, 1):
-        s = YeeScheme(dataclasses.replace(cfg, hybrid_block=hb), make_ops("hip", None, gpu, torch.float32))
-        s.init_scheme()
-        s.init_grids()
-        s.randomize_fields(seed=11)
-        s.perform_steps()
-        torch.cuda.synchronize()
-        runs[hb] = s
-    hy, st = runs[T], runs[1]
-    assert hy.hybrid is not None and hy.hybrid.get("v4" if mode == "mixed" else "v3"), "plan not selected"
-    assert st.hybrid is None
-    if mode == "blocked":
-        assert len({cls for _, cls in hy.hybrid["shell"]}) >= 3  # face / edge / corner classes
-    else:
-        assert hy.hybrid["copy"] and hy.hybrid["psi_fix"]  # stepped pieces and blocked faces
-    for c in hy.comps:
-        x, y = hy.F[0][c].double().cpu(), st.F[0][c].double().cpu()
-        scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0])
-        assert float((x - y).abs().max()) <= 2e-5 * scale, (c, float((x - y).abs().max()), scale)
-        src_scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] != c[0])
-        for a, b in zip(hy.cpml.slabs[c], st.cpml.slabs[c]):
-            err = float((a.psi[0].double() - b.psi[0].double()).abs().max())
-            assert err <= 2e-5 * src_scale, (c, "psi", err, src_scale)
-        assert max(float(b.psi[0].abs().max()) for b in st.cpml.slabs[c]) > 1e-3 * src_scale  # psi is live

@@ -1,14 +1,22 @@
 #!/usr/bin/env python3
-"""Per-GPU compute cost of a decomposed blocked run, measured on ONE GPU.
+"""Per-GPU cost of a decomposed blocked run, measured on ONE GPU.
 
 Runs one rank's sub-domain of an N-way decomposition through the scheme's
 blocked step (interior pass + T-thick shells + halo pack / unpack kernels)
-with a null transport (messages are not moved), and compares the time per
-step with the serial blocked kernel on the same number of cells.  The
-difference is the compute overhead of the decomposition (shell re-reads,
-pack / unpack) that RCCL transfers must hide under.
+and compares the time per step with the serial blocked kernel on the same
+number of cells.  Transports:
 
-    python tools/decomp_cost.py --size 1024 1024 1024 --world 8 --rank 3 --time-block 4
+* ``null`` -- messages are not moved (the compute overhead of the
+  decomposition: shell re-reads, pack / unpack);
+* ``loopback`` -- every receive buffer is filled by a device-to-device copy
+  of a send buffer of the same size on the exchange's side stream, plus
+  (``--link-gbs``) a spin kernel for the wire time of the largest message
+  over one xGMI link: real pack, copy and unpack kernels that must find CUs
+  next to the interior pass.  The per-pass breakdown (``PassTimer``:
+  interior, exchange wait, shell) says how much of the exchange the interior
+  pass hides.  (Fields are not meaningful: timing only.)
+
+    python tools/decomp_cost.py --size 1024 1024 1024 --world 8 --topology 4 2 1 --transport loopback
 """
 import argparse
 import os
@@ -32,6 +40,56 @@ class NullComm:
         return v
 
 
+class LoopbackComm:
+    """Loopback transport (timing only): a receive is filled from a send
+    buffer of the same size by a device copy on the current (side) stream;
+    with ``link_gbs`` a spin kernel then stands in for the wire time of the
+    largest message (every neighbour has its own xGMI link)."""
+    backend = "loopback"
+
+    def __init__(self, rank, world, link_gbs=0.0):
+        self.rank, self.world = rank, world
+        self.link_gbs = link_gbs
+        self.bytes = 0
+        self._cyc_per_us = None
+
+    def _spin(self, us):
+        import torch
+        if self._cyc_per_us is None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record()
+            torch.cuda._sleep(1000000)
+            b.record()
+            b.synchronize()
+            self._cyc_per_us = 1000000 / (a.elapsed_time(b) * 1e3)
+        torch.cuda._sleep(max(1, int(us * self._cyc_per_us)))
+
+    def post(self, ops):
+        sends = {}
+        for o in ops:
+            if o.send:
+                sends.setdefault(o.tensor.numel(), []).append(o.tensor)
+        big = 0
+        for o in ops:
+            if o.send:
+                continue
+            pool = sends.get(o.tensor.numel())
+            if pool:
+                o.tensor.copy_(pool[-1])
+            else:
+                o.tensor.zero_()
+            nb = o.tensor.numel() * o.tensor.element_size()
+            self.bytes += nb
+            big = max(big, nb)
+        if self.link_gbs > 0 and big:
+            self._spin(big / (self.link_gbs * 1e3))
+        return []
+
+    def allreduce(self, v, op="sum"):
+        return v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, nargs=3, default=[1024, 1024, 1024])
@@ -42,6 +100,9 @@ def main():
     ap.add_argument("--topology", type=int, nargs=3, default=None, help="force a rank grid (e.g. 4 2 1)")
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--thin", type=int, default=1, help="thin y shells on the single-row kernel (T <= 4)")
+    ap.add_argument("--transport", default="null", choices=("null", "loopback"))
+    ap.add_argument("--link-gbs", type=float, default=0.0,
+                    help="loopback: emulate the wire time of the largest message at this xGMI link rate (GB/s)")
     ap.add_argument("--physics", default="vacuum", choices=("vacuum", "cpml-tfsf", "upml-tfsf", "cpml"),
                     help="non-vacuum: hybrid passes (blocked owned core + deep-halo stepped shell), per-GPU "
                          "Mcells/s only")
@@ -71,6 +132,8 @@ def main():
                            pml_type="upml" if a.physics.startswith("upml") else "cpml",
                            use_tfsf=a.physics.endswith("tfsf"), hybrid_block=T)
 
+    breakdown = {}
+
     def timed(domain, halo):
         s = YeeScheme(cfg, make_ops("hip", None, "cuda:0", torch.float32), domain, halo)
         s.ops.tb_thin_single_row = bool(a.thin)
@@ -80,16 +143,39 @@ def main():
             print("hybrid pass: %s (ghost depth %d)" % (s.hybrid is not None, s.domain.buffer_size if s.domain else 0))
         s.advance(2 * T)
         torch.cuda.synchronize()
+        if halo is not None:
+            from fdtd3d_amd.models.blocking import PassTimer
+            s.pass_timer = PassTimer(s.device)
+            halo.reset_timing()
+            halo.timing = True
+            if hasattr(halo.comm, "bytes"):
+                halo.comm.bytes = 0
         t0 = time.perf_counter()
         s.advance(a.steps)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
+        if halo is not None:
+            bd = s.pass_timer.summary()
+            n = max(1, bd["passes"])
+            breakdown.update({k: bd[k] / n for k in ("interior_ms", "exchange_wait_ms", "shell_ms")})
+            breakdown["exchange_ms"] = halo.exchange_ms() / max(1, halo.exchanges)
+            breakdown["passes"] = bd["passes"]
+            s.pass_timer = None
+            halo.timing = False
         del s
         torch.cuda.empty_cache()
         return dt
 
-    halo = HaloExchanger(dom, comm=NullComm(rank, a.world))
+    comm = (LoopbackComm(rank, a.world, a.link_gbs) if a.transport == "loopback" else NullComm(rank, a.world))
+    halo = HaloExchanger(dom, comm=comm)
     t_dec = timed(dom, halo)
+    if breakdown:
+        wait_frac = breakdown["exchange_wait_ms"] / max(1e-9, breakdown["interior_ms"])
+        print("per pass (%s transport%s): interior %.3f ms, exchange (side stream) %.3f ms, exchange wait %.3f ms "
+              "(%.1f%% of the interior), shell %.3f ms; %d passes, %.1f MB moved per pass"
+              % (a.transport, ", %.0f GB/s links" % a.link_gbs if a.link_gbs else "", breakdown["interior_ms"],
+                 breakdown["exchange_ms"], breakdown["exchange_wait_ms"], 100 * wait_frac, breakdown["shell_ms"],
+                 breakdown["passes"], getattr(comm, "bytes", 0) / 1e6 / max(1, breakdown["passes"])))
     own = dom.owned_shape
     cells = own[0] * own[1] * own[2]
     if a.physics != "vacuum":
