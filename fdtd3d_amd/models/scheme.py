@@ -586,11 +586,25 @@ class YeeScheme(BlockedStepping):
                 if cfg.dispersion == "lorentz":
                     w0 = cfg.lorentz_omega0_ratio * 2 * PI * self.source_frequency
                 q = dt * dt * w0 * w0
+                lean = (ue is not None and ug is not None and cfg.scheme == "3d"
+                        and getattr(self.ops, "drude_lut", False) and hasattr(self.ops, "_drude_lut"))
+                lut = None
                 if uw == 0.0 and ug == 0.0:
                     active = None
-                else:
-                    w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
-                    active = (w != 0) | (g != 0)
+                elif lean:
+                    # eps and gamma uniform: the coefficients are a function of
+                    # omega_p alone -- the uint8 index + table built slab by
+                    # slab (_drude_index), never a full-grid fp64 omega grid
+                    active, lut = self._drude_index(c, dt, e0, eps_c, ug, q, dtp)
+                    if lut is None:
+                        lean = False  # more than 256 distinct tuples: per-cell arrays
+                if uw == 0.0 and ug == 0.0:
+                    pass
+                elif not lean or lut is not None:
+                    w = g = None
+                    if lut is None:
+                        w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
+                        active = (w != 0) | (g != 0)
                     local = bool(active.any())
                     # decomposed: a rank without dispersive cells of c still
                     # keeps the dispersive state arrays when another rank has
@@ -599,29 +613,19 @@ class YeeScheme(BlockedStepping):
                         local = self.halo.allreduce_max(1.0 if local else 0.0) > 0
                     if not local:
                         active = None
-                if active is not None:
-                    st["nlev"] = 3
-                    st["D1"] = None
-                    st["drude_active"] = active
-                    lean = (ue is not None and ug is not None and cfg.scheme == "3d"
-                            and getattr(self.ops, "drude_lut", False) and hasattr(self.ops, "_drude_lut"))
-                    if lean:
-                        # coefficients are a function of omega_p alone here (eps
-                        # and gamma uniform): the uint8 index + table straight from
-                        # the distinct omega values, no per-cell coefficient arrays
-                        # (5 x 4 B per cell and component; torch.unique over those
-                        # would need ~10x that transiently at 1024^3)
-                        uniq, inv = torch.unique(w, return_inverse=True)
-                        lean = uniq.numel() <= 256
-                        if lean:
-                            tab = torch.stack(_drude_coefs(dt, e0, eps_c, uniq, ug, q), 1).to(dtp).contiguous()
-                            st["_drude_lut"] = (inv.to(torch.uint8).contiguous(), tab)
+                    if active is not None:
+                        st["nlev"] = 3
+                        st["D1"] = None
+                        st["drude_active"] = active
+                        if lut is not None:
+                            st["_drude_lut"] = lut
                             for n in ("b0", "b1", "b2", "ma1", "ma2"):
                                 st[n] = Coef(1.0)  # cell: self._drude_cells(c) on demand
-                        del uniq, inv
-                    if not lean:
-                        for n, v in zip(("b0", "b1", "b2", "ma1", "ma2"), _drude_coefs(dt, e0, eps_c, w, g, q)):
-                            st[n] = Coef(1.0, cell=v.to(dtp))
+                        else:
+                            if w is None:
+                                w, g = self.sampler.averaged_drude(c, electric=(c[0] == "E"))
+                            for n, v in zip(("b0", "b1", "b2", "ma1", "ma2"), _drude_coefs(dt, e0, eps_c, w, g, q)):
+                                st[n] = Coef(1.0, cell=v.to(dtp))
                     del w, g
                 # the non-dispersive chain (E from D through 1/(eps eps0)) for the
                 # chain boxes with no dispersive cell (PML slabs away from the
@@ -653,6 +657,46 @@ class YeeScheme(BlockedStepping):
                 if "D1" in st and "_drude_lut" not in st:
                     self.ops._drude_lut(st, [st[n].cell for n in ("b0", "b1", "b2", "ma1", "ma2")],
                                         self.domain.shape)
+
+    def _drude_index(self, c: str, dt: float, e0: float, eps_c, ug: float, q: float, dtp,
+                     slab_cells: int = 1 << 24):
+        """(active mask, (uint8 index, coefficient table)) of the dispersive
+        component ``c`` with uniform eps and gamma: omega_p is sampled and
+        averaged over x slabs of the local region (MaterialSampler on each
+        slab), so the transient is a slab of fp64 grids instead of several
+        full ones (1024^3: ~35 GB).  Pass 1 collects the distinct omega
+        values, pass 2 maps every cell to its table row.  (None for the
+        table when there are more than 256 distinct values.)"""
+        dom = self.domain
+        shape = tuple(dom.shape)
+        electric = c[0] == "E"
+        cells = shape[1] * shape[2]
+        xc = max(1, min(shape[0], slab_cells // max(1, cells)))  # ~16M cells per slab
+
+        def slabs():
+            for x0 in range(0, shape[0], xc):
+                n = min(xc, shape[0] - x0)
+                smp = MaterialSampler(self.layout, self.scene, (dom.origin[0] + x0, dom.origin[1], dom.origin[2]),
+                                      (n, shape[1], shape[2]), self.device)
+                w, _ = smp.averaged_drude(c, electric)
+                yield x0, n, w
+                del smp, w
+
+        active = torch.zeros(shape, dtype=torch.bool, device=self.device)
+        uniq = None
+        for x0, n, w in slabs():
+            # (a uniform non-zero gamma makes every cell dispersive, like
+            # approximate_drude's (w != 0) | (g != 0))
+            active[x0:x0 + n] = (w != 0) if ug == 0.0 else True
+            u = torch.unique(w)
+            uniq = u if uniq is None else torch.unique(torch.cat([uniq, u]))
+            if uniq.numel() > 256:
+                return active, None
+        ids = torch.empty(shape, dtype=torch.uint8, device=self.device)
+        for x0, n, w in slabs():
+            ids[x0:x0 + n] = torch.searchsorted(uniq, w).to(torch.uint8)
+        tab = torch.stack(_drude_coefs(dt, e0, eps_c, uniq, ug, q), 1).to(dtp).contiguous()
+        return active, (ids.contiguous(), tab)
 
     def _drude_cells(self, c: str) -> None:
         """Per-cell Drude coefficient arrays of component ``c`` rebuilt from

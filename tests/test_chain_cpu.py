@@ -187,3 +187,26 @@ def test_drude_row_split_matches_full_chain(pml, monkeypatch):
     for c in a.comps:
         scale = float(b.F[0][c].abs().max())
         assert float((a.F[0][c] - b.F[0][c]).abs().max()) <= 1e-12 * scale, c
+
+
+def test_drude_index_slabs_match_cells():
+    """The lean Drude init (scheme._drude_index: omega_p sampled slab by
+    slab, uint8 index + coefficient table) gives every dispersive cell the
+    coefficients of the per-cell arrays built from the full-grid sampling;
+    slabs of 3 x planes here, so the slab walk and the cross-slab union of
+    the distinct values are exercised."""
+    from fdtd3d_amd.utils.constants import EPS0
+    cfg = dataclasses.replace(CASES["drude-upml"], time_steps=0)
+    s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+    s.init_scheme()
+    s.init_grids()
+    st = s.upml["Ez"]
+    shape = tuple(s.domain.shape)
+    active, lut = s._drude_index("Ez", s.dt, EPS0, 1.0, 0.0, 0.0, torch.float64,
+                                 slab_cells=3 * shape[1] * shape[2])
+    assert lut is not None
+    ids, tab = lut
+    assert torch.equal(active, st["drude_active"])
+    for q, n in enumerate(("b0", "b1", "b2", "ma1", "ma2")):
+        got = tab[:, q][ids.long()]
+        assert torch.allclose(got[active], st[n].cell[active], rtol=1e-12, atol=0), n

@@ -127,6 +127,10 @@ HIST_CASES = [
      3, 7),
     # TF/SF faces inside the stepped shell (distance 2 < PML 4 + margin)
     ("cpml-tfsf-near", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, tfsf_size=(2, 2, 2)), 3, 8),
+    # non-cubic grid, unequal layers: every face layer a different shape
+    ("cpml-tfsf-box", dict(size=(64, 80, 56), pml_size=(4, 6, 5), scene="vacuum", use_pml=True, pml_type="cpml",
+                           use_tfsf=True, tfsf_size=(7, 9, 8)), 4, 9),
+    ("upml-point-box", dict(size=(60, 52, 76), pml_size=(5, 4, 6), scene="vacuum", use_pml=True), 3, 8),
 ]
 
 
