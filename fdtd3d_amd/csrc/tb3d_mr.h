@@ -397,22 +397,25 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   // the x loop.
   const bool hz_lo = HIS && __any(lane_own && kb == O.lo[2]);
   const bool hz_hi = HIS && __any(lane_own && kb == O.hi[2] - 1);
-  auto hrs = [&]() -> Rsrc { return __builtin_amdgcn_make_buffer_rsrc((void*)hist, (short)0, -1, 0x00020000); };
-  // slot offset (bytes) of (kind, level, axis, component slot).  The layer
-  // stride goes through an empty asm at every use: hoisted out of the x
-  // loop, the 12 T slot offsets would each hold an SGPR for the whole kernel
+  // descriptor of one face layer (kind, level, axis, component slot): the
+  // slot offset in the 64-bit base, the layer's size as the record count, so
+  // the out-of-range lane offset of a cell off the face (0xF0000000) is
+  // dropped by the range check like every masked store of this kernel.  The
+  // layer stride goes through an empty asm at every use: hoisted out of the x
+  // loop, the 12 T slot bases would each hold SGPRs for the whole kernel
   // (spilled to VGPR lanes, which then spill the field registers)
-  auto hso = [&](int kind, int l, int a, int q) -> int {
-    int h4 = hls * 4;
-    asm volatile("" : "+s"(h4));
-    return (((kind * T + l) * 3 + a) * 2 + q) * h4;
+  auto hrs = [&](int kind, int l, int a, int q) -> Rsrc {
+    int ls = hls;
+    asm volatile("" : "+s"(ls));
+    const size_t slot = (size_t)((((kind * T + l) * 3 + a) * 2 + q)) * (size_t)ls;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(hist + slot), (short)0, ls * 4, 0x00020000);
   };
   // store the two off-axis components of (x, y, z) for the face of axis a
   auto hput = [&](int kind, int l, int a, unsigned off, const vec& vx, const vec& vy, const vec& vz) {
     const vec& v0 = a == 0 ? vy : vx;
     const vec& v1 = a == 2 ? vy : vz;
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v0[0]), hrs(), off, hso(kind, l, a, 0), 0);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v1[0]), hrs(), off, hso(kind, l, a, 1), 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v0[0]), hrs(kind, l, a, 0), off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v1[0]), hrs(kind, l, a, 1), off, 0, 0);
   };
   // face cells of kind `kind` (0: E on the low faces, 1: H on the high faces)
   // on plane p, row r at level l

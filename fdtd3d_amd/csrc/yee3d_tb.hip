@@ -527,7 +527,8 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
     // the layer stride must cover every face plane of the array, the buffer every slot
     int need = 0;
     fdtd_tb3d_hist_floats(nx, ny, nz, steps, &need);
-    if (hls < need || hist_floats < 12LL * steps * hls || 12LL * steps * hls * 4 > 0x7FFFFFFFLL || steps > 5)
+    // (one layer per buffer descriptor: its byte size must fit the 32-bit record count)
+    if (hls < need || hist_floats < 12LL * steps * hls || (long long)hls * 4 > 0x7FFFFFFFLL || steps > 5)
       return (int)hipErrorInvalidValue;
   }
   return tb_mr_dispatch(fx, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
