@@ -473,55 +473,3 @@ FDTD_API int fdtd_counter_add(int* counter, int n, void* s) {
 }
 
 FDTD_API int fdtd_abi_version() { return 2; }
-
-// Boundary history of a blocked core pass (tb3d_mr.h, feature bit 8) written
-// back into the fields the stepped shell reads: level `level` of kind `kind`
-// (0: E on the output box's three low faces, 1: H on its three high faces),
-// the two off-axis components of each face.  One launch per shell half step
-// (models/blocking.py history shell); blockIdx.y = face axis.
-__global__ __launch_bounds__(256) void k_hist_apply(float* __restrict__ f0, float* __restrict__ f1,
-                                                    float* __restrict__ f2, const float* __restrict__ hist, int ny,
-                                                    int nz, Box3 O, int T, int hls, int kind, int level) {
-  const int a = blockIdx.y;
-  const int kx = O.hi[0] - O.lo[0], ky = O.hi[1] - O.lo[1], kz = O.hi[2] - O.lo[2];
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int fx = kind == 0 ? O.lo[0] : O.hi[0] - 1;
-  const int fy = kind == 0 ? O.lo[1] : O.hi[1] - 1;
-  const int fz = kind == 0 ? O.lo[2] : O.hi[2] - 1;
-  int i, j, k;
-  long long cell;
-  if (a == 0) {
-    if (t >= (long long)ky * kz) return;
-    i = fx, j = O.lo[1] + (int)(t / kz), k = O.lo[2] + (int)(t % kz);
-    cell = (long long)j * nz + k;
-  } else if (a == 1) {
-    if (t >= (long long)kx * kz) return;
-    i = O.lo[0] + (int)(t / kz), j = fy, k = O.lo[2] + (int)(t % kz);
-    cell = (long long)i * nz + k;
-  } else {
-    if (t >= (long long)kx * ky) return;
-    i = O.lo[0] + (int)(t / ky), j = O.lo[1] + (int)(t % ky), k = fz;
-    cell = (long long)i * ny + j;
-  }
-  const size_t off = ((size_t)i * ny + j) * nz + k;
-  const size_t s0 = ((size_t)((kind * T + level) * 3 + a) * 2) * hls + cell;
-  float* c0 = a == 0 ? f1 : f0;
-  float* c1 = a == 2 ? f1 : f2;
-  c0[off] = hist[s0];
-  c1[off] = hist[s0 + hls];
-}
-
-FDTD_API int fdtd_hist_apply_f32(float* const* f, const float* hist, int nx, int ny, int nz, const int* obox, int steps,
-                                 int hls, int kind, int level, void* s) {
-  const Box3 O = make_box(obox);
-  if (box_empty(O) || kind < 0 || kind > 1 || level < 0 || level >= steps) return (int)hipErrorInvalidValue;
-  if (O.lo[0] < 0 || O.lo[1] < 0 || O.lo[2] < 0 || O.hi[0] > nx || O.hi[1] > ny || O.hi[2] > nz)
-    return (int)hipErrorInvalidValue;
-  const long long kx = O.hi[0] - O.lo[0], ky = O.hi[1] - O.lo[1], kz = O.hi[2] - O.lo[2];
-  long long m = ky * kz;
-  if (kx * kz > m) m = kx * kz;
-  if (kx * ky > m) m = kx * ky;
-  const dim3 grid((unsigned)cdiv(m, 256), 3);
-  k_hist_apply<<<grid, 256, 0, (hipStream_t)s>>>(f[0], f[1], f[2], hist, ny, nz, O, steps, hls, kind, level);
-  FDTD_RETURN_LAUNCH_STATUS();
-}

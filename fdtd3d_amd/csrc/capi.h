@@ -73,11 +73,7 @@ int fdtd_tb_max_steps();
 int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                       const void* ce4, const int* ebox, const void* ch4, const int* hbox, double cb, double db,
                       int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk, int steps,
-                      const int* src, const double* src_vals, const void* tf, const float* gtab, float* hist,
-                      long long hist_floats, int hls, void* stream);
-long long fdtd_tb3d_hist_floats(int nx, int ny, int nz, int steps, int* hls);
-int fdtd_hist_apply_f32(float* const* f, const float* hist, int nx, int ny, int nz, const int* obox, int steps,
-                        int hls, int kind, int level, void* stream);
+                      const int* src, const double* src_vals, const void* tf, const float* gtab, void* stream);
 int fdtd_tfdev_size();
 int fdtd_tfsf_pass_f32(float* einc, float* hinc, int n, double ce, double ch, const double* src_vals, int steps,
                        int reach, int nE, int nH, const int* I0, const float* W0, const float* W1, const float* C,

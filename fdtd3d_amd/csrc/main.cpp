@@ -126,7 +126,7 @@ int tb3d(const float* const* ei, const float* const* hi, float* const* eo, float
   if (ce4) {
     const int none[6] = {0, 0, 0, 0, 0, 0};
     return fdtd_tb3d_ext_f32(ei, hi, eo, ho, ce4, ebox, nullptr, none, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals,
-                             nullptr, nullptr, nullptr, 0, 0, s);
+                             nullptr, nullptr, s);
   }
   return fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
 }

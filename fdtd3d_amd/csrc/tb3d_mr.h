@@ -1,6 +1,6 @@
 // Multi-row temporally blocked fp32 3D Yee kernel (k_tb3d_mr) and its
 // launcher (yee3d_tb.hip holds the host API): plain, sparse per-cell
-// coefficient, TF/SF and boundary-history variants.
+// coefficient and TF/SF variants.
 #pragma once
 
 #include <cstdio>
@@ -54,10 +54,9 @@ struct TbSrc {
 // direction along x or y the incident value a target sees depends on its
 // index along that axis only (`va`), so each pass precomputes, per level,
 // g = sign * projection * interpolated incident line at every index of a set
-// (k_tfsf_pass in yee3d_tb.hip) and the kernel adds g to the target's curl
-// before the coefficient multiply.  The table and the g values are read
-// through the constant address space: wave-uniform scalar loads that wait on
-// the scalar counter, never behind the vector plane prefetch.
+// (k_tfsf_pass in yee3d_tb.hip) and the kernels add g to the target's curl
+// before the coefficient multiply -- from SCALAR loads (wave-uniform index),
+// which do not queue behind the vector prefetch.
 constexpr int TF_MAX_SETS = 24;
 struct TfSet {
   int n;          // component 0..5 = Ex Ey Ez Hx Hy Hz
@@ -72,20 +71,6 @@ struct TfDev {
   int xpl[2][2];            // [E / H][low / high] x-face planes (-1: none)
   TfSet s[TF_MAX_SETS];
 };
-typedef const __attribute__((address_space(4))) TfDev* TfC;
-
-// Boundary history (feature bit 8) of a hybrid pass whose stepped shell has
-// no band (models/blocking.py, "history shell"): the owned cells of the
-// output box O on its three LOW faces store E after every level, those on
-// its three HIGH faces H after every level but the last.  A shell cell next
-// to O reads exactly these values at the intermediate time levels (E^{n+1}
-// from H^{n+1/2} at i and i-1, H from E at i and i+1), so the stepped shell
-// never recomputes core cells.  Layout, element units: ((kind * T + l) * 3
-// + axis) * 2 + slot) * hls + cell, kind 0 = E / low faces, 1 = H / high
-// faces, slot = the two components off the face axis (x: y z, y: x z, z: x
-// y), cell = the face cell's index in the full array's plane of that
-// orientation: x face j * nz + k, y face i * nz + k, z face i * ny + j (hls
-// >= the largest of ny nz, nx nz, nx ny).
 
 // Memory access through buffer descriptors: one descriptor per (array, x
 // plane) built in SGPRs from the wave-uniform plane index, plus ONE 32-bit
@@ -207,13 +192,11 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     const float4* __restrict__ ce4, const float4* __restrict__ ch4, Box3 BE, Box3 BH, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz,
-    const TfDev* __restrict__ tf, const float* __restrict__ gtab, float* __restrict__ hist, int hls) {
-  // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF,
-  // 8 boundary history
+    const TfDev* __restrict__ tf, const float* __restrict__ gtab) {
+  // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF
   constexpr int PC = FX & 3;
   constexpr bool TFS = FX & 4;
-  constexpr bool HIS = FX & 8;
-  static_assert(V == 1 || !FX, "sparse coefficients / TF/SF / history: scalar lanes");
+  static_assert(V == 1 || !FX, "sparse coefficients / TF/SF: scalar lanes");
   constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
   static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
   typedef typename VT<V>::f vec;
@@ -224,6 +207,15 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   __shared__ vec sX[2][4][NW][64];
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);  // one wave per y (SGPR)
+  // the TF/SF table lives in LDS for the kernel's life: its fields are read in
+  // many branches (with dynamic set indices)
+  __shared__ unsigned sTFraw[TFS ? sizeof(TfDev) / 4 : 1];
+  if constexpr (TFS) {
+    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(TfDev) / 4); q += 64 * NW)
+      sTFraw[q] = ((const unsigned*)tf)[q];
+  }
+  if constexpr (TFS) __syncthreads();
+  const TfDev& TF = *reinterpret_cast<const TfDev*>(sTFraw);
 
   // Tile of this workgroup.  A row of a tile starts at an arbitrary z (the
   // stride is the 64 - 2T owned cells), so its 64 cells straddle three
@@ -328,111 +320,123 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   const bool wave_e = PCE && __any(inb & ((1u << R) - 1u));
   const bool wave_h = PCH && __any(inb >> R);
 
-  // TF/SF.  Per kind, the sets whose y / z extent this wave's rows and lanes
-  // meet are found once: y / z-face sets (a row or a lane column, every
-  // level of every trip inside their x range) in tf_face, x-face sets (one
-  // plane, all rows / lanes of the TF box) in tf_xs, added to the candidates
-  // only on a level whose plane is one of the kind's two x-face planes.  A
-  // wave away from every face therefore pays two scalar compares per level;
-  // a candidate costs a few scalar loads (set bounds, its g value) and one
-  // select + add per row.
-  const TfC TFc = (TfC)tf;
-  unsigned tf_face[2] = {0u, 0u}, tf_xs[2] = {0u, 0u};
-  int tf_xp[2][2] = {{-1, -1}, {-1, -1}};
-  int tf_ld = 0;
+  // TF/SF.  x-face sets (one plane each, all rows / lanes of the TF box) are
+  // rare per wave and go through scalar loads when a level hits their plane.
+  // y / z-face sets (one row or one lane column) touch few waves but every
+  // level of every trip of those waves, so each wave parks up to TF_SLOTS of
+  // them per kind in slots: slot metadata in VGPR lanes (read back with
+  // readlane at a compile-time lane), a per-lane bit per (slot, row) for the
+  // cells it covers, and per trip ONE vector load of the g values of every
+  // (slot, level, row) -- issued before the field prefetch, so the levels
+  // never wait behind it.
+  constexpr int TF_SLOTS = 6;                      // per kind
+  constexpr int TF_ENT = 2 * TF_SLOTS * T * R;     // g entries per trip (<= 128 for T <= 5)
+  static_assert(!TFS || TF_ENT <= 128, "TF/SF: at most 5 steps per pass");
+  unsigned tf_wx[2] = {0u, 0u};
+  unsigned tf_ov[2] = {0u, 0u};  // face sets beyond the slots: the scalar path every level
+  int tf_xe0 = -1, tf_xe1 = -1, tf_xh0 = -1, tf_xh1 = -1;  // x-face planes (E / H sets)
+  int tf_na0 = 0, tf_na1 = 0;                      // slots in use (E / H)
+  unsigned tf_lbits = 0;                           // bit slot * R + r: this lane in the slot's set, row r
+  int tf_mx = 0;                                   // lane s: x range of slot s (lo | hi << 16)
+  int tf_mn = 0;                                   // lane s: component of slot s
+  int tf_gb0 = 0, tf_gb1 = 0;                      // g index of entry lane / lane + 64 (plus X when va = 0)
+  bool tf_ok0 = false, tf_ok1 = false;
+  int tf_va = 0, tf_ld = 0;
   if constexpr (TFS) {
-    const int ns = TFc->nsets;
-    tf_ld = TFc->ld;
+    const int ns = TF.nsets;
+    const int ld = TF.ld;
+    tf_ld = ld;
+    tf_va = TF.s[0].va;
+    int na[2] = {0, 0};
     for (int si = 0; si < ns; ++si) {
-      const int lo1 = TFc->s[si].lo[1], hi1 = TFc->s[si].hi[1];
-      const int lo2 = TFc->s[si].lo[2], hi2 = TFc->s[si].hi[2];
-      bool rows = false;
+      const TfSet& S = TF.s[si];
+      unsigned rb = 0;
 #pragma unroll
-      for (int r = 0; r < R; ++r) rows |= jw + r >= lo1 && jw + r < hi1;
-      if (!rows || !__any(kin && kb >= lo2 && kb < hi2)) continue;
-      const int k = TFc->s[si].n < 3 ? 0 : 1;
-      if (TFc->s[si].fa == 0)
-        tf_xs[k] |= 1u << si;
-      else
-        tf_face[k] |= 1u << si;
-    }
+      for (int r = 0; r < R; ++r) {
+        const int j = jw + r;
+        rb |= (kin && j >= S.lo[1] && j < S.hi[1] && kb >= S.lo[2] && kb < S.hi[2]) ? (1u << r) : 0u;
+      }
+      if (!__any(rb != 0u)) continue;
+      const int k = S.n < 3 ? 0 : 1;
+      if (S.fa == 0) {
+        tf_wx[0] |= k == 0 ? (1u << si) : 0u;
+        tf_wx[1] |= k == 1 ? (1u << si) : 0u;
+        continue;
+      }
+      const int a = k == 0 ? na[0] : na[1];
+      if (a >= TF_SLOTS) {
+        tf_ov[0] |= k == 0 ? (1u << si) : 0u;
+        tf_ov[1] |= k == 1 ? (1u << si) : 0u;
+        continue;
+      }
+      const int slot = k * TF_SLOTS + a;
+      if (k == 0) ++na[0]; else ++na[1];
+      tf_lbits |= rb << (slot * R);
+      if (lane == slot) {
+        tf_mx = S.lo[0] | (S.hi[0] << 16);
+        tf_mn = S.n;
+      }
+      // entries (slot, l, r) -> entry q = (slot * T + l) * R + r
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      tf_xp[k][0] = TFc->xpl[k][0];
-      tf_xp[k][1] = TFc->xpl[k][1];
+      for (int l = 0; l < T; ++l)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int q = (slot * T + l) * R + r;
+          // level l: E sets on plane X - l, H sets on X - l - 1
+          const int base = l * ld + S.goff + (S.va == 0 ? -S.lo[0] - l - k : (jw + r) - S.lo[1]);
+          if (lane == q) { tf_gb0 = base; tf_ok0 = true; }
+          if (lane + 64 == q) { tf_gb1 = base; tf_ok1 = true; }
+        }
     }
+    tf_na0 = na[0];
+    tf_na1 = na[1];
+    tf_xe0 = TF.xpl[0][0];
+    tf_xe1 = TF.xpl[0][1];
+    tf_xh0 = TF.xpl[1][0];
+    tf_xh1 = TF.xpl[1][1];
   }
+  const bool tf_slots = TFS && (tf_na0 + tf_na1) > 0;
+  float tf_g0 = 0.f, tf_g1 = 0.f;  // this trip's g entries (lane q, q + 64)
   // add the TF/SF corrections of kind k at level l, plane p, row r to the curls
   auto tf_apply = [&](int k, int l, int p, int r, vec& c0, vec& c1, vec& c2) {
     if constexpr (TFS) {
-      unsigned cand = tf_face[k];
-      if (p == tf_xp[k][0] || p == tf_xp[k][1]) cand |= tf_xs[k];
+      // y / z-face slots
+      if (tf_slots) {
+#pragma unroll
+        for (int a = 0; a < TF_SLOTS; ++a) {
+          if (a >= (k == 0 ? tf_na0 : tf_na1)) break;
+          const int slot = k * TF_SLOTS + a;
+          const int xr = __builtin_amdgcn_readlane(tf_mx, slot);
+          if ((unsigned)(p - (xr & 0xffff)) >= (unsigned)((xr >> 16) - (xr & 0xffff))) continue;
+          const int q = (slot * T + l) * R + r;
+          const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q < 64 ? tf_g0 : tf_g1), q & 63));
+          const float gl = ((tf_lbits >> (slot * R + r)) & 1u) ? g : 0.f;
+          const int c = __builtin_amdgcn_readlane(tf_mn, slot) - 3 * k;
+          c0 = c0 + (vec)(c == 0 ? gl : 0.f);
+          c1 = c1 + (vec)(c == 1 ? gl : 0.f);
+          c2 = c2 + (vec)(c == 2 ? gl : 0.f);
+        }
+      }
+      // x-face sets on their plane
+      const bool xp = k == 0 ? (p == tf_xe0 || p == tf_xe1) : (p == tf_xh0 || p == tf_xh1);
+      unsigned cand = (xp ? (k == 0 ? tf_wx[0] : tf_wx[1]) : 0u) | (k == 0 ? tf_ov[0] : tf_ov[1]);
       const int j = jw + r;
       while (cand) {
         const int si = __builtin_ctz(cand);
         cand &= cand - 1u;
-        const int lo0 = TFc->s[si].lo[0], hi0 = TFc->s[si].hi[0];
-        const int lo1 = TFc->s[si].lo[1], hi1 = TFc->s[si].hi[1];
-        if ((unsigned)(p - lo0) >= (unsigned)(hi0 - lo0) || j < lo1 || j >= hi1) continue;
-        const int gi = l * tf_ld + TFc->s[si].goff + (TFc->s[si].va == 0 ? p - lo0 : j - lo1);
-        const float g = cload(gtab, gi);
+        const TfSet& S = TF.s[si];
+        if ((unsigned)(p - S.lo[0]) >= (unsigned)(S.hi[0] - S.lo[0]) || j < S.lo[1] || j >= S.hi[1]) continue;
+        const float g = gtab[l * TF.ld + S.goff + (S.va == 0 ? p - S.lo[0] : j - S.lo[1])];
         // g on the set's lanes, 0 elsewhere, added to the set's component by
         // selects (conditional adds make the compiler index a scratch array)
-        const float gl = (kb >= TFc->s[si].lo[2] && kb < TFc->s[si].hi[2]) ? g : 0.f;
-        const int c = TFc->s[si].n - 3 * k;
+        const float gl = (kb >= S.lo[2] && kb < S.hi[2]) ? g : 0.f;
+        const int c = S.n - 3 * k;
         c0 = c0 + (vec)(c == 0 ? gl : 0.f);
         c1 = c1 + (vec)(c == 1 ? gl : 0.f);
         c2 = c2 + (vec)(c == 2 ? gl : 0.f);
       }
     }
   };
-
-  // Boundary history (HIS): wave-uniform tests pick the few waves / levels
-  // that own a face cell of O (x faces: one plane; y faces: one row; z
-  // faces: one lane of the tiles at either z end); the stores are issued
-  // behind those branches, lanes off the face dropped by the offset.  Face
-  // layers are indexed like the full array's planes (x face j * nz + k, y
-  // face i * nz + k, z face i * ny + j), so the x / y offsets are the row
-  // offset roff plus a wave-uniform term: no per-lane state lives across
-  // the x loop.
-  const bool hz_lo = HIS && __any(lane_own && kb == O.lo[2]);
-  const bool hz_hi = HIS && __any(lane_own && kb == O.hi[2] - 1);
-  // descriptor of one face layer (kind, level, axis, component slot): the
-  // slot offset in the 64-bit base, the layer's size as the record count, so
-  // the out-of-range lane offset of a cell off the face (0xF0000000) is
-  // dropped by the range check like every masked store of this kernel.  The
-  // layer stride goes through an empty asm at every use: hoisted out of the x
-  // loop, the 12 T slot bases would each hold SGPRs for the whole kernel
-  // (spilled to VGPR lanes, which then spill the field registers)
-  auto hrs = [&](int kind, int l, int a, int q) -> Rsrc {
-    int ls = hls;
-    asm volatile("" : "+s"(ls));
-    const size_t slot = (size_t)((((kind * T + l) * 3 + a) * 2 + q)) * (size_t)ls;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(hist + slot), (short)0, ls * 4, 0x00020000);
-  };
-  // store the two off-axis components of (x, y, z) for the face of axis a
-  auto hput = [&](int kind, int l, int a, unsigned off, const vec& vx, const vec& vy, const vec& vz) {
-    const vec& v0 = a == 0 ? vy : vx;
-    const vec& v1 = a == 2 ? vy : vz;
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v0[0]), hrs(kind, l, a, 0), off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v1[0]), hrs(kind, l, a, 1), off, 0, 0);
-  };
-  // face cells of kind `kind` (0: E on the low faces, 1: H on the high faces)
-  // on plane p, row r at level l
-  auto hist_store = [&](int kind, int l, int p, int r, const vec& vx, const vec& vy, const vec& vz) {
-    if constexpr (HIS) {
-      if (p < i0 || p >= i1) return;
-      const int j = jw + r;
-      const bool own = ((mbits >> ((r * 7 + 6) * V)) & 1u) != 0u;
-      if (p == (kind == 0 ? O.lo[0] : O.hi[0] - 1)) hput(kind, l, 0, own ? roff[r] : 0xF0000000u, vx, vy, vz);
-      if (j == (kind == 0 ? O.lo[1] : O.hi[1] - 1))
-        hput(kind, l, 1, own ? roff[r] + (unsigned)((p - j) * nz) * 4u : 0xF0000000u, vx, vy, vz);
-      if (kind == 0 ? hz_lo : hz_hi)
-        hput(kind, l, 2, own && kb == (kind == 0 ? O.lo[2] : O.hi[2] - 1) ? (unsigned)(p * ny + j) * 4u : 0xF0000000u,
-             vx, vy, vz);
-    }
-  };
-
   typedef unsigned u3 __attribute__((ext_vector_type(3)));
   auto coef_ld = [&](const float4* arr, const Box3& B, unsigned off, size_t pl, int p) -> u3 {
     const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)arr + (size_t)(p - B.lo[0]) * pl),
@@ -593,6 +597,15 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
       }
       return make_float3(sc, sc, sc);
     };
+    if (tf_slots) {
+      // this trip's g entries of the face slots (va = 0: index moves with X)
+      // (entries of planes outside a set's x range are never used; their
+      // index is clamped into the table)
+      const int dx = tf_va == 0 ? X : 0;
+      const int last = T * tf_ld - 1;
+      tf_g0 = tf_ok0 ? gtab[min(max(tf_gb0 + dx, 0), last)] : 0.f;
+      if (TF_ENT > 64) tf_g1 = tf_ok1 ? gtab[min(max(tf_gb1 + dx, 0), last)] : 0.f;
+    }
     // next plane(s) in flight under this plane's levels
     if (PFD == 2)
       load_plane(X + 2, Hn2, En2);
@@ -642,7 +655,6 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
           if (src_comp == 1) En[r].y[q] = sv.v[l];
           if (src_comp == 2) En[r].z[q] = sv.v[l];
         }
-        hist_store(0, l, pe, r, En[r].x, En[r].y, En[r].z);
       }
       const int ph = pe - 1;
 #pragma unroll
@@ -663,7 +675,6 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         Hn.x = Hp[l][r].x + coef(bhx, ph, r, 3, ch.x) * dx;
         Hn.y = Hp[l][r].y + coef(bhy, ph, r, 4, ch.y) * dy;
         Hn.z = Hp[l][r].z + coef(bhz, ph, r, 5, ch.z) * dz;
-        if (l < T - 1) hist_store(1, l, ph, r, Hn.x, Hn.y, Hn.z);
         // later rows (r+1 ..) read only their own and higher rows' Ep, so
         // row r rotates as soon as its H is done
         Ec[r] = Ep[l][r];
@@ -713,7 +724,7 @@ template <int T, int V, int R, int FX, int NW = TBW>
 int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                  const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
                  int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
-                 const TfDev* tf, const float* gtab, float* hist, int hls, hipStream_t s) {
+                 const TfDev* tf, const float* gtab, hipStream_t s) {
   constexpr int HL = (T + V - 1) / V;
   constexpr int TBZ = (64 - 2 * HL) * V;
   dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], NW * R - 2 * T),
@@ -723,8 +734,7 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
       O, xchunk, src[0], src[1], src[2], src[3], sv,                                                       \
-      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, hist, \
-      hls)
+      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab)
   if constexpr (FX != 0) {
     MR_LAUNCH(1, false);  // tuning variants: uniform media only
   } else {
@@ -738,13 +748,5 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
 #undef MR_LAUNCH
   FDTD_RETURN_LAUNCH_STATUS();
 }
-
-// boundary-history passes (fx bit 8, with any of bits 1 / 2 / 4; T <= 5),
-// compiled in yee3d_tb_hist.hip
-int launch_tb_mr_hist(int T, int fx, const float* const* ein, const float* const* hin, float* const* eout,
-                      float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
-                      float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
-                      const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, float* hist, int hls,
-                      hipStream_t s);
 
 }  // namespace tb3d

@@ -328,11 +328,8 @@ template <int T>
 int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                      float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                      float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
-                     const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, float* hist, int hls,
-                     hipStream_t s) {
-#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, hist, hls, s
-  // boundary-history variants: their own translation unit (yee3d_tb_hist.hip)
-  if (fx & 8) return launch_tb_mr_hist(T, fx, MR_ARGS);
+                     const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, hipStream_t s) {
+#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, s
   // per-cell: one kind keeps T coefficient planes in LDS (24 KiB each, 160
   // KiB per CU: T <= 5); both kinds keep them in registers (spill-free to T = 2)
   if constexpr (T <= 5) {
@@ -365,15 +362,13 @@ int tb_mr_xchunk(int fx, const Box3& O, int steps) {
 }
 
 // multi-row pass (scalar lanes, 2 rows per wave): uniform media, sparse
-// per-cell coefficients (fx bits 1 / 2), TF/SF corrections (fx bit 4),
-// boundary history (fx bit 8)
+// per-cell coefficients (fx bits 1 / 2), TF/SF corrections (fx bit 4)
 int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                    float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                    float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, int steps,
-                   const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, float* hist, int hls,
-                   hipStream_t s) {
+                   const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, hipStream_t s) {
   if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
-#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, hist, hls, s
+#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, s
   switch (steps) {
     case 1: return launch_tb_mr_sel<1>(MR_ARGS);
     case 2: return launch_tb_mr_sel<2>(MR_ARGS);
@@ -466,7 +461,7 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   if (!pc && (MR > 1 || steps > 4)) {
     const Box3 nb = make_box(kNoBox);
     return tb_mr_dispatch(0, ein, hin, eout, hout, nullptr, nullptr, nb, nb, fcb, fdb, nx, ny, nz, b, O, xchunk,
-                          steps, src, sv, nullptr, nullptr, nullptr, 0, s);
+                          steps, src, sv, nullptr, nullptr, s);
   }
   if (steps > 4) return (int)hipErrorInvalidValue;
   if (xchunk <= 0) {
@@ -495,24 +490,19 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   return (int)hipErrorInvalidValue;
 }
 
-FDTD_API long long fdtd_tb3d_hist_floats(int nx, int ny, int nz, int steps, int* hls);
-
 // T fused leapfrog steps on the multi-row kernel with its extensions:
 // sparse per-cell coefficients -- ``ce4`` / ``ch4`` hold the E / H
 // coefficients of the three components as one float4 per cell of the box
 // ``ebox`` / ``hbox`` (x-major, z fastest, .w unused); every cell outside its
 // kind's box, and either kind whose array is null, uses the scalar ``cb`` /
-// ``db`` -- TF/SF corrections (``tf`` = device TfDev, ``gtab`` = the g
-// table of this pass's first level, from fdtd_tfsf_pass_f32; null: none) and
-// the boundary history of the output box (``hist``: at least
-// fdtd_tb3d_hist_floats(nx, ny, nz, steps) floats, ``hls`` = its layer stride
-// from the same call; null: none; tb3d_mr.h).  Other arguments as fdtd_tb3d_v4_f32.
+// ``db`` -- and TF/SF corrections (``tf`` = device TfDev, ``gtab`` = the g
+// table of this pass's first level, from fdtd_tfsf_pass_f32; null: none).
+// Other arguments as fdtd_tb3d_v4_f32.
 FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* const* eout,
                                float* const* hout, const void* ce4, const int* ebox, const void* ch4,
                                const int* hbox, double cb, double db, int nx, int ny, int nz, const int* boxes,
                                const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
-                               const void* tf, const float* gtab, float* hist, long long hist_floats, int hls,
-                               void* stream) {
+                               const void* tf, const float* gtab, void* stream) {
   if (nz % 4 != 0 || steps < 1 || steps > 6) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
@@ -521,30 +511,10 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
   const Box3 BE = make_box(ce4 ? ebox : kNoBox), BH = make_box(ch4 ? hbox : kNoBox);
   TbSrc sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
-  const int fx = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0) | (tf && gtab ? 4 : 0) |
-                 (hist ? 8 : 0);
-  if (hist) {
-    // the layer stride must cover every face plane of the array, the buffer every slot
-    int need = 0;
-    fdtd_tb3d_hist_floats(nx, ny, nz, steps, &need);
-    // (one layer per buffer descriptor: its byte size must fit the 32-bit record count)
-    if (hls < need || hist_floats < 12LL * steps * hls || (long long)hls * 4 > 0x7FFFFFFFLL || steps > 5)
-      return (int)hipErrorInvalidValue;
-  }
+  const int fx = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0) | (tf && gtab ? 4 : 0);
   return tb_mr_dispatch(fx, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
                         (const float4*)(box_empty(BH) ? nullptr : ch4), BE, BH, (float)cb, (float)db, nx, ny, nz, b,
-                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, hist, hls, (hipStream_t)stream);
-}
-
-// floats of the boundary history of a ``steps``-step pass over an
-// (nx, ny, nz) array (12 * steps face layers) and, in ``hls``, the layer
-// stride (the largest face plane)
-FDTD_API long long fdtd_tb3d_hist_floats(int nx, int ny, int nz, int steps, int* hls) {
-  long long m = (long long)ny * nz;
-  if ((long long)nx * nz > m) m = (long long)nx * nz;
-  if ((long long)nx * ny > m) m = (long long)nx * ny;
-  *hls = (int)m;
-  return 12LL * steps * m;
+                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, (hipStream_t)stream);
 }
 
 // size of the TfDev block the host fills (ABI check)

@@ -203,9 +203,7 @@ class BlockedStepping:
                 return
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
                 return
-        plan = self._hybrid_hist_plan(H) if self._hybrid_hist_ok() else None
-        if plan is None:
-            plan = self._hybrid_plan(H)
+        plan = self._hybrid_plan(H)
         if plan is None:
             return
         if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.5 * self.cells():
@@ -251,7 +249,7 @@ class BlockedStepping:
     def _hybrid_plan_m(self, T: int, m: int, in_kernel_tfsf: bool = False):
         """Hybrid plan with core margin ``m``; ``in_kernel_tfsf``: the core
         pass applies the TF/SF corrections itself (TfsfSets), so the TF/SF
-        faces may lie inside the core (the history-shell plan)."""
+        faces may lie inside the core."""
         dom = self.domain
         cfg = self.cfg
         size = cfg.size
@@ -324,18 +322,8 @@ class BlockedStepping:
             g = grow(ob, T + 1)
             if any(not box_empty(box_intersect(g, b)) for b in irregular):
                 return None
-            if cfg.use_tfsf and not in_kernel_tfsf:
-                lg = dom.to_local(g)
-                for c in self.comps:
-                    for tab in self.tfsf[c]:
-                        if tab.n == 0:
-                            continue
-                        ijk = tab.ijk.view(-1, 3)
-                        inside = torch.ones(ijk.shape[0], dtype=torch.bool, device=ijk.device)
-                        for d in range(3):
-                            inside &= (ijk[:, d] >= lg[0][d]) & (ijk[:, d] < lg[1][d])
-                        if bool(inside.any()):
-                            return None
+            if cfg.use_tfsf and not in_kernel_tfsf and self._tfsf_targets_in(dom.to_local(g)):
+                return None
         if self.halo is not None:
             # decomposed: each rank's core is its owned part of the global core
             couts = [box_intersect(b, dom.owned_global()) for b in couts]
@@ -389,85 +377,6 @@ class BlockedStepping:
                 "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
                 "cut_cells": box_volume(Dm) if Dm is not None else 0}
 
-    # ------------------------------------------------ hybrid, history shell
-    def _hybrid_hist_ok(self) -> bool:
-        """Serial 3D runs whose core pass can record its boundary history
-        (fp32 HIP: the multi-row kernel's feature bit 8; the torch oracle in
-        any precision), with TF/SF through TfsfSets when on."""
-        cfg = self.cfg
-        if cfg.scheme != "3d" or self.halo is not None or not hasattr(self.ops, "hist_buffer"):
-            return False
-        if self.ops.name == "hip" and self.dtype != torch.float32:
-            return False
-        if getattr(self.ops, "tb_max_hist_steps", 5) < 1:
-            return False
-        if cfg.use_tfsf and getattr(self, "tfsf_sets", None) is None:
-            return False
-        return True
-
-    def _hybrid_hist_plan(self, T: int):
-        """History shell: the blocked core pass (TF/SF corrections inside it)
-        also records E on its boxes' low faces and H on their high faces at
-        every level (``ops.tb_step(hist=...)``); the stepped shell then
-        advances ONLY the shell -- no band of core cells -- reading those face
-        values (``ops.hist_apply`` before each half step) wherever its
-        stencil reaches into the core.  Every shell value is the stepped
-        run's: the cells next to the core see the core's exact intermediate
-        levels."""
-        if T > getattr(self.ops, "tb_max_hist_steps", 5):
-            return None
-        plan = None
-        for m in (T + 1, T + 2):
-            plan = self._hybrid_plan_m(T, m, in_kernel_tfsf=True)
-            if plan is not None:
-                break
-        if plan is None:
-            return None
-        shell = [self.domain.to_global(b) for b in plan["copy"]]
-        tf_shell = bool(self.cfg.use_tfsf) and any(self._tfsf_targets_in(b) for b in plan["copy"])
-        shape = tuple(self.domain.shape)
-        hist = [[self.ops.hist_buffer(shape, T) for _ in plan["core"]] for _ in range(self.planes)]
-        return dict(plan, kind="history-shell", shells=[shell] * T, shell=shell, hist=hist,
-                    shell_tfsf=tf_shell, tfsf_in_core=bool(self.cfg.use_tfsf))
-
-    def _hybrid_hist_step(self, T: int) -> None:
-        hp = self.hybrid
-        srcs = self._pass_sources(self.t, T)
-        cores = hp["core"]
-        for p in range(self.planes):
-            tf, line0 = None, None
-            if self.cfg.use_tfsf:
-                if hp["shell_tfsf"]:
-                    # the shell steps the incident line again from here
-                    line0 = (self.einc[p].clone(), self.hinc[p].clone())
-                tf = self._tfsf_pass(p, T)
-            with self.prof.phase("blocked-core"):
-                for ob, hb in zip(cores, hp["hist"][p]):
-                    self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf,
-                                     hist=hb)
-            if line0 is not None:
-                self.einc[p].copy_(line0[0])
-                self.hinc[p].copy_(line0[1])
-        for s_ in range(T):
-            def pre(kind, p, s_=s_):
-                # E half step s reads H_s of the core's high faces (in F
-                # already for s = 0), the H half step E_{s+1} of its low faces
-                if kind == "E" and s_ == 0:
-                    return
-                with self.prof.phase("history"):
-                    for ob, hb in zip(cores, hp["hist"][p]):
-                        self.ops.hist_apply(self.F[p], hb, ob, T, "H" if kind == "E" else "E",
-                                            s_ - 1 if kind == "E" else s_)
-            self.step(hp["shell"], pre=pre, tfsf=hp["shell_tfsf"])
-        with self.prof.phase("shell-copy"):
-            for p in range(self.planes):
-                src = [self.F[p][c] for c in self.comps]
-                dst = [self.F_alt[p][c] for c in self.comps]
-                for b in hp["copy"]:
-                    self.ops.copy_box(src, dst, b)
-        for p in range(self.planes):
-            self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
-
     def _tfsf_pass(self, p: int, T: int, level0: int = 0):
         """In-kernel TF/SF of a blocked pass starting at step ``self.t`` on
         plane ``p``: advances the plane's incident line ``T`` steps and returns
@@ -494,9 +403,6 @@ class BlockedStepping:
         return srcs
 
     def _hybrid_step(self, T: int) -> None:
-        if self.hybrid.get("kind") == "history-shell":
-            self._hybrid_hist_step(T)
-            return
         hp = self.hybrid
         srcs = self._pass_sources(self.t, T)
         side = None

@@ -935,8 +935,7 @@ class YeeScheme(BlockedStepping):
         w = self._window(kind)
         return {c: self.local_box(c, w) for c in comps}
 
-    def _update(self, kind: str, p: int, windows: Optional[Sequence[Box]] = None, tfsf_once: bool = False,
-                tfsf: bool = True) -> None:
+    def _update(self, kind: str, p: int, windows: Optional[Sequence[Box]] = None, tfsf_once: bool = False) -> None:
         """Update all E (or H) components of plane ``p`` on the given global
         windows (default: this sub-step's window).  ``tfsf_once``: apply the
         E-form TF/SF corrections once over the whole grid after all windows
@@ -951,7 +950,7 @@ class YeeScheme(BlockedStepping):
             # hybrid shell of a decomposed run: clip to this sub-step's deep-halo window
             dw = self._window(kind)
             windows = [b for b in (box_intersect(w, dw) for w in windows) if not box_empty(b)]
-        use_tfsf = self.cfg.use_tfsf and tfsf
+        use_tfsf = self.cfg.use_tfsf
         tfsf_here = use_tfsf and not tfsf_once
         chain = self.use_upml_chain and getattr(self, "chain_regions", None) is not None
         if chain and self.hybrid is not None and len(windows) > 1:
@@ -1286,14 +1285,10 @@ class YeeScheme(BlockedStepping):
 
     in_amplitude = False
 
-    def step(self, windows: Optional[Sequence[Box]] = None, pre: Optional[Callable] = None,
-             tfsf: bool = True) -> None:
+    def step(self, windows: Optional[Sequence[Box]] = None) -> None:
         """Advance one full leapfrog step (serial runs: optionally only on the
         global ``windows``, disjoint boxes -- the stepped shell of a hybrid
-        blocked pass).  ``pre(kind, p)`` runs before each half step's update
-        (the history shell writes the core's face values there); ``tfsf`` =
-        False skips the incident line and the TF/SF corrections (a shell with
-        no TF/SF target whose core pass advanced the line)."""
+        blocked pass)."""
         t = self.t
         cfg = self.cfg
         B = self.domain.buffer_size
@@ -1309,7 +1304,7 @@ class YeeScheme(BlockedStepping):
                 with self.prof.phase("halo-deep"):
                     halo.exchange_all(self)
         ph = self.prof.phase
-        use_tfsf = cfg.use_tfsf and tfsf
+        use_tfsf = cfg.use_tfsf
         for p in range(self.planes):
             if use_tfsf:
                 with ph("incident-E"):
@@ -1322,9 +1317,7 @@ class YeeScheme(BlockedStepping):
                 if halo is not None and not deep:
                     halo.finish_and_update(self, "E", p)
                 else:
-                    if pre is not None:
-                        pre("E", p)
-                    self._update("E", p, windows, tfsf_once=windows is not None and self._tfsf_once, tfsf=tfsf)
+                    self._update("E", p, windows, tfsf_once=windows is not None and self._tfsf_once)
             with ph("source"):
                 self._apply_sources(t, p)
             if halo is not None and not deep:
@@ -1337,9 +1330,7 @@ class YeeScheme(BlockedStepping):
                 if halo is not None and not deep:
                     halo.finish_and_update(self, "H", p)
                 else:
-                    if pre is not None:
-                        pre("H", p)
-                    self._update("H", p, windows, tfsf_once=windows is not None and self._tfsf_once, tfsf=tfsf)
+                    self._update("H", p, windows, tfsf_once=windows is not None and self._tfsf_once)
             if halo is not None and not deep:
                 with ph("halo-post"):
                     halo.start(self, "H", p)

@@ -674,41 +674,6 @@ class HipOps:
     # ------------------------------------------------------ temporal blocking
     tfsf_sets_ok = True  # the fp32 blocked kernel applies TfsfSets corrections
 
-    def hist_floats(self, shape, steps: int):
-        """(floats, layer stride) of the boundary history of a ``steps``-step
-        pass over an array of ``shape`` (fdtd_tb3d_hist_floats)."""
-        hls = c_int(0)
-        f = self.lib.fdtd_tb3d_hist_floats
-        f.restype = ctypes.c_longlong
-        n = int(f(c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), c_int(steps), ctypes.byref(hls)))
-        return n, int(hls.value)
-
-    def hist_buffer(self, shape, steps: int):
-        """A boundary-history buffer for :meth:`tb_step` (``hist``)."""
-        n, hls = self.hist_floats(shape, steps)
-        return torch.zeros(n, dtype=torch.float32, device=self.device), hls
-
-    def hist_apply(self, F: Dict[str, torch.Tensor], hist, obox: Box, steps: int, kind: str, level: int) -> None:
-        """Write level ``level`` of the history (kind "E": E on the low faces
-        of ``obox``, "H": H on its high faces) into the fields ``F``
-        (aux_kernels.hip k_hist_apply)."""
-        comps = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
-        shape = tuple(F[comps[0]].shape)
-        for c in comps:
-            self._check_tensor(F[c], shape)
-        for d in range(3):
-            if obox[0][d] < 0 or obox[1][d] > shape[d]:
-                raise HipError("hist_apply: box %s outside array %s" % (obox, shape))
-        hbuf, hls = hist
-        if hbuf.numel() < 12 * steps * hls:
-            raise HipError("hist_apply: history buffer too small")
-        rc = self.lib.fdtd_hist_apply_f32((c_vp * 3)(*[F[c].data_ptr() for c in comps]), _ptr(hbuf),
-                                          c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), _box_arr([obox]),
-                                          c_int(steps), c_int(hls), c_int(0 if kind == "E" else 1), c_int(level),
-                                          _stream())
-        _check(rc, "hist_apply")
-        self.launches += 1
-
     def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
                   sets, slot: int = 0) -> torch.Tensor:
         """Advance the incident line ``len(src_vals)`` steps and return the
@@ -737,7 +702,7 @@ class HipOps:
         return g
 
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None, hist=None) -> None:
+                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None) -> None:
         """``steps`` fused leapfrog steps in one HBM pass (yee3d_tb.hip).
 
         ``boxes`` are the update boxes (each component changes only there, at
@@ -746,9 +711,7 @@ class HipOps:
         give every stored cell ``steps`` valid layers of input around it.
         ``sources`` = per-step list of (E component, local index, value) or
         None.  ``tfsf`` = (TfsfSets, g table, first level) from
-        ``tfsf_pass``.  ``hist`` = a buffer from :meth:`hist_buffer`: the
-        pass also records E on the output box's low faces and H on its high
-        faces after every level (read back with :meth:`hist_apply`)."""
+        ``tfsf_pass``."""
         if len(fin) == 3:
             self._tb2d_step(fin, fout, boxes, obox, cb, steps, sources)
             return
@@ -800,16 +763,7 @@ class HipOps:
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
         if tfsf is not None and self.dtype != torch.float32:
             raise HipError("in-kernel TF/SF: fp32 only")
-        if hist is not None:
-            if self.dtype != torch.float32 or steps > 5:
-                raise HipError("boundary history: fp32, at most 5 steps per pass")
-            hbuf, hls = hist
-            need, want = self.hist_floats(shape, steps)
-            self._check_tensor(hbuf)
-            if hls != want or hbuf.numel() < need:
-                raise HipError("history buffer too small for %s x %d steps" % (shape, steps))
-        if ((percell and self.dtype == torch.float32 and self.tb_sparse) or tfsf is not None
-                or hist is not None):
+        if (percell and self.dtype == torch.float32 and self.tb_sparse) or tfsf is not None:
             # multi-row kernel with sparse per-cell coefficients / TF/SF sets
             if percell and steps > 5:
                 raise HipError("per-cell coefficients: at most 5 steps per pass")
@@ -828,9 +782,7 @@ class HipOps:
                 arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), _ptr(ce), _box_arr([ebox]), _ptr(ch),
                 _box_arr([hbox]), c_double(cbv), c_double(dbv), c_int(shape[0]), c_int(shape[1]), c_int(shape[2]),
                 _box_arr([boxes[c] for c in E + H]), _box_arr([obox]), c_int(self.tb_xchunk), c_int(steps),
-                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _ptr(None if hist is None else hist[0]),
-                ctypes.c_longlong(0 if hist is None else hist[0].numel()), c_int(0 if hist is None else hist[1]),
-                _stream())
+                (c_int * 4)(*src), (c_double * 8)(*vals), tfp, gp, _stream())
             _check(rc, "tb3d_ext")
             self.launches += 1
             return

@@ -169,16 +169,13 @@ class TorchOps:
         return True
 
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
-                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None, hist=None) -> None:
+                obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None) -> None:
         """Reference semantics of the temporally blocked kernel: ``steps``
         fused steps on the update boxes (reads outside the arrays count as
         zero, like the kernel's unloaded rows), then only ``obox`` ∩ each
         component's box is written to ``fout``.  ``tfsf`` = (TfsfSets, g
         table, first level): each level adds coef * g to the set's target
-        cells after the curl update (the kernel adds g to the curl); ``hist``
-        = (buffer, layer stride): E on the low faces of ``obox`` after every
-        level, H on its high faces after every level but the last (layout of
-        csrc/tb3d_mr.h)."""
+        cells after the curl update (the kernel adds g to the curl)."""
         pad = {c: torch.nn.functional.pad(fin[c], (1, 1, 1, 1, 1, 1)) for c in fin}
         shifted = {c: ((b[0][0] + 1, b[0][1] + 1, b[0][2] + 1), (b[1][0] + 1, b[1][1] + 1, b[1][2] + 1))
                    for c, b in boxes.items()}
@@ -194,13 +191,9 @@ class TorchOps:
                 nxt[comp][tuple(i + 1 for i in idx)] = val
             if tfsf is not None:
                 self._tfsf_level(nxt, tfsf, l, "E", shifted, cbp)
-            if hist is not None:
-                self._hist_record(nxt, hist, obox, steps, "E", l)
             self.curl_update("H", h, nxt, nxt, cbp)
             if tfsf is not None:
                 self._tfsf_level(nxt, tfsf, l, "H", shifted, cbp)
-            if hist is not None and l < steps - 1:
-                self._hist_record(nxt, hist, obox, steps, "H", l)
             cur = nxt
         for c, b in boxes.items():
             ob = box_intersect_(b, obox)
@@ -229,52 +222,6 @@ class TorchOps:
                     off = tab._pad_off[shape] = (ijk[:, 0] * shape[1] + ijk[:, 1]) * shape[2] + ijk[:, 2]
                 v = (inc[tab.i0] * tab.w0 + inc[tab.i0 + 1] * tab.w1) * tab.coef
                 F[c].view(-1).index_add_(0, off, v.to(F[c].dtype))
-
-    @staticmethod
-    def _hist_slot(hist, steps: int, kind: int, l: int, a: int, q: int):
-        buf, hls = hist
-        o = ((((kind * steps + l) * 3 + a) * 2 + q) * hls)
-        return buf[o:o + hls]
-
-    def _hist_record(self, F, hist, obox: Box, steps: int, kind: str, l: int) -> None:
-        """Face values of one level into the history (F padded by one cell)."""
-        k = 0 if kind == "E" else 1
-        comps = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
-        n = tuple(F[comps[0]].shape[d] - 2 for d in range(3))
-        lo, hi = obox
-        f = [lo[d] if k == 0 else hi[d] - 1 for d in range(3)]
-        for a in range(3):
-            rng = [slice(lo[d] + 1, hi[d] + 1) for d in range(3)]
-            rng[a] = f[a] + 1
-            o = [d for d in range(3) if d != a]
-            for q, cq in enumerate(o):
-                v = F[comps[cq]][tuple(rng)]
-                lay = self._hist_slot(hist, steps, k, l, a, q)[:n[o[0]] * n[o[1]]].view(n[o[0]], n[o[1]])
-                lay[lo[o[0]]:hi[o[0]], lo[o[1]]:hi[o[1]]] = v.to(lay.dtype)
-
-    def hist_floats(self, shape, steps: int):
-        hls = max(shape[1] * shape[2], shape[0] * shape[2], shape[0] * shape[1])
-        return 12 * steps * hls, hls
-
-    def hist_buffer(self, shape, steps: int):
-        n, hls = self.hist_floats(shape, steps)
-        return torch.zeros(n, dtype=self.dtype, device=self.device), hls
-
-    def hist_apply(self, F: Dict[str, torch.Tensor], hist, obox: Box, steps: int, kind: str, level: int) -> None:
-        """Level ``level`` of the history into ``F`` (csrc/aux_kernels.hip
-        k_hist_apply)."""
-        k = 0 if kind == "E" else 1
-        comps = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
-        n = tuple(F[comps[0]].shape)
-        lo, hi = obox
-        f = [lo[d] if k == 0 else hi[d] - 1 for d in range(3)]
-        for a in range(3):
-            rng = [slice(lo[d], hi[d]) for d in range(3)]
-            rng[a] = f[a]
-            o = [d for d in range(3) if d != a]
-            for q, cq in enumerate(o):
-                lay = self._hist_slot(hist, steps, k, level, a, q)[:n[o[0]] * n[o[1]]].view(n[o[0]], n[o[1]])
-                F[comps[cq]][tuple(rng)] = lay[lo[o[0]]:hi[o[0]], lo[o[1]]:hi[o[1]]].to(F[comps[cq]].dtype)
 
     tfsf_sets_ok = True  # tb_step applies TfsfSets corrections (the blocked kernel's form)
 

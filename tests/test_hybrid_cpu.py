@@ -110,9 +110,8 @@ def test_hybrid_checkpoint_resume(tmp_path):
         assert torch.equal(full.F[0][c], resumed.F[0][c]), c
 
 
-HIST_CASES = [
-    # TF/SF along +x (the reference default) and +y: in-kernel TfsfSets, the
-    # TF/SF faces inside the core
+RANDOM_CASES = [
+    # TF/SF along +x (the reference default) and +y
     ("cpml-tfsf-x", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 11),
     ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90), 3, 10),
     ("upml-tfsf-x", dict(scene="vacuum", use_pml=True, use_tfsf=True), 5, 12),
@@ -129,17 +128,17 @@ HIST_CASES = [
     ("cpml-tfsf-near", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, tfsf_size=(2, 2, 2)), 3, 8),
     # non-cubic grid, unequal layers: every face layer a different shape
     ("cpml-tfsf-box", dict(size=(64, 80, 56), pml_size=(4, 6, 5), scene="vacuum", use_pml=True, pml_type="cpml",
-                           use_tfsf=True, tfsf_size=(7, 9, 8)), 4, 9),
+                           use_tfsf=True, tfsf_size=(5, 6, 5)), 4, 9),
     ("upml-point-box", dict(size=(60, 52, 76), pml_size=(5, 4, 6), scene="vacuum", use_pml=True), 3, 8),
 ]
 
 
-@pytest.mark.parametrize("name,extra,T,steps", HIST_CASES, ids=[c[0] for c in HIST_CASES])
-def test_history_shell_matches_stepped(name, extra, T, steps):
-    """History shell (models/blocking.py ``_hybrid_hist_plan``): the core
-    pass records its face values at every level, the stepped shell advances
-    no core cell -- and the run equals stepping everything, from random
-    fields, through full passes and a short tail."""
+@pytest.mark.parametrize("name,extra,T,steps", RANDOM_CASES, ids=[c[0] for c in RANDOM_CASES])
+def test_hybrid_random_fields_match_stepped(name, extra, T, steps):
+    """Hybrid passes (blocked core + stepped shell with its shrinking band,
+    models/blocking.py ``_hybrid_plan``) from random fields -- every slab
+    and face carries field from step 1 -- through full passes and a short
+    tail equal stepping everything, on cubic and non-cubic grids."""
     kw = dict(BASE)
     kw.update(extra)
     cfg = SchemeConfig(time_steps=steps, hybrid_block=1, **kw)
@@ -149,8 +148,7 @@ def test_history_shell_matches_stepped(name, extra, T, steps):
         s.init_scheme()
         s.init_grids()
         if hb > 1:
-            assert s.hybrid is not None and s.hybrid.get("kind") == "history-shell", "history shell not selected"
-            assert len(s.hybrid["shell"]) == len(s.hybrid["copy"])
+            assert s.hybrid is not None, "hybrid plan rejected"
         s.randomize_fields(seed=5)
         s.perform_steps()
         runs.append(s)
