@@ -99,6 +99,7 @@ class SchemeConfig:
     cpml_alpha_max: float = 0.0
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
+    hybrid_tfsf: str = "auto"                # hybrid + TF/SF: faces in the blocked core ("core"), the shell, or auto
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
@@ -134,7 +135,7 @@ class SchemeConfig:
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
             amplitude_check_steps=s.amplitudeCheckSteps,
-            hybrid_block=s.hybridBlock,
+            hybrid_block=s.hybridBlock, hybrid_tfsf=s.hybridTfsf,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 

@@ -33,7 +33,9 @@ TB_MAX_STEPS_F64 = 5  # fp64 blocked kernel (fdtd_tb64_max_steps)
 TB2D_MAX_STEPS = 8  # 2D TMz / TEz blocked kernel, fp32 (fdtd_tb2d_max_steps)
 TB2D_MAX_STEPS_F64 = 8  # fp64 (fdtd_tb2d64_max_steps)
 TB2D_MODES = {("Ez",): (0, ("Ez",), ("Hx", "Hy")), ("Ex", "Ey"): (1, ("Ex", "Ey"), ("Hz",))}
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libfdtd3d_hip.so")
+# FDTD3D_HIP_LIB: another build of the library (A/B kernel measurements)
+_LIB_PATH = os.environ.get("FDTD3D_HIP_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                            "libfdtd3d_hip.so")
 
 c_int = ctypes.c_int
 c_ll = ctypes.c_longlong

@@ -38,6 +38,7 @@ CASES = [
     ("cpml-tfsf-sphere", dict(scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
                               sphere_center=(40.0, 36.0, 48.0), sphere_radius=10.0), 4, 10),
     ("cpml-point-T5", dict(scene="vacuum", use_pml=True, pml_type="cpml"), 5, 12),
+    ("cpml-tfsf-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, hybrid_tfsf="core"), 4, 13),
     ("upml-tfsf-x-T5", dict(scene="vacuum", use_pml=True, use_tfsf=True), 5, 12),
     ("cpml-tfsf-complex", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, complex_values=True),
      2, 7),
@@ -91,9 +92,9 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
 
 
 @pytest.mark.parametrize("T,tfsf,point,size,phi", [(4, True, False, (96, 88, 96), 0.0),
-                                                   (5, True, True, (80, 72, 96), 0.0),
+                                                   (5, True, True, (112, 104, 112), 0.0),
                                                    (4, False, True, (72, 80, 64), 0.0),
-                                                   (3, True, False, (64, 64, 128), 90.0),
+                                                   (3, True, False, (80, 80, 128), 90.0),
                                                    (5, False, True, (112, 96, 100), 0.0)])
 def test_hybrid_random_fields(gpu, T, tfsf, point, size, phi):
     """Hybrid passes from random fields (every face and slab carries field
