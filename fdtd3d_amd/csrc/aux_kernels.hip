@@ -268,6 +268,8 @@ struct AmpSet {
   const void* f[6];
   void* amp[6];
   Box3 b[6];
+  long long xs;  // x stride of the amp arrays (elements): the maxima of one x plane of all
+                 // components are contiguous (models/scheme.py; tb3d_mr.h AmpDev)
 };
 
 // one cell of every component per thread: a 3D grid over the union of the
@@ -282,6 +284,7 @@ __global__ __launch_bounds__(256) void k_amplitude_many(AmpSet a, int ncomp, Box
   unsigned int cnt = 0;
   if (k < u.hi[2] && j < u.hi[1]) {
     const size_t off = ((size_t)i * ny + j) * nz + k;
+    const size_t aoff = (size_t)i * a.xs + (size_t)j * nz + k;
     const T acc_t = (T)accuracy;
     // every component's field and running maximum loaded before the first
     // store (a store through one amp pointer could alias the next loads, which
@@ -294,7 +297,7 @@ __global__ __launch_bounds__(256) void k_amplitude_many(AmpSet a, int ncomp, Box
       in[c] = c < ncomp && i >= b.lo[0] && i < b.hi[0] && j >= b.lo[1] && j < b.hi[1] && k >= b.lo[2] &&
               k < b.hi[2];
       fv[c] = in[c] ? ((const T*)a.f[c])[off] : T(0);
-      am[c] = in[c] ? ((const T*)a.amp[c])[off] : T(0);
+      am[c] = in[c] ? ((const T*)a.amp[c])[aoff] : T(0);
     }
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
@@ -303,7 +306,7 @@ __global__ __launch_bounds__(256) void k_amplitude_many(AmpSet a, int ncomp, Box
         const T den = am[c] != T(0) ? am[c] : (v != T(0) ? v : T(1));
         if ((v - am[c]) / den > acc_t) {
           cnt++;
-          ((T*)a.amp[c])[off] = v;
+          ((T*)a.amp[c])[aoff] = v;
         }
       }
     }
@@ -324,6 +327,7 @@ __global__ __launch_bounds__(256) void k_amplitude_many_v4(AmpSet a, int ncomp, 
   unsigned int cnt = 0;
   if (kb < u.hi[2] && j < u.hi[1]) {
     const size_t off = ((size_t)i * ny + j) * nz + kb;
+    const size_t aoff = (size_t)i * a.xs + (size_t)j * nz + kb;
     float4 fv[6], am[6];
     unsigned m[6];
 #pragma unroll
@@ -331,7 +335,7 @@ __global__ __launch_bounds__(256) void k_amplitude_many_v4(AmpSet a, int ncomp, 
       const Box3& b = a.b[c];
       m[c] = (c < ncomp && i >= b.lo[0] && i < b.hi[0]) ? kmask(b, j, kb) : 0u;
       fv[c] = m[c] ? ld4((const float*)a.f[c], off) : make_float4(0.f, 0.f, 0.f, 0.f);
-      am[c] = m[c] ? ld4((const float*)a.amp[c], off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      am[c] = m[c] ? ld4((const float*)a.amp[c], aoff) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
@@ -347,7 +351,7 @@ __global__ __launch_bounds__(256) void k_amplitude_many_v4(AmpSet a, int ncomp, 
           cnt++;
         }
       }
-      st4m((float*)a.amp[c], off, nv, w);
+      st4m((float*)a.amp[c], aoff, nv, w);
     }
   }
   for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
@@ -417,9 +421,10 @@ FDTD_AUX_API(f64, double)
 
 template <typename T>
 int amplitude_many(const void* const* f, void* const* amp, int ncomp, int ny, int nz, const int* boxes,
-                   double accuracy, unsigned int* changed, hipStream_t s) {
+                   long long amp_xs, double accuracy, unsigned int* changed, hipStream_t s) {
   if (ncomp <= 0 || ncomp > 6) return (int)hipErrorInvalidValue;
   AmpSet a;
+  a.xs = amp_xs > 0 ? amp_xs : (long long)ny * nz;
   long long nmax = 0;
   for (int c = 0; c < 6; ++c) {
     a.f[c] = c < ncomp ? f[c] : nullptr;
@@ -458,13 +463,16 @@ int amplitude_many(const void* const* f, void* const* amp, int ncomp, int ny, in
 // amplitude update of up to 6 components in one launch, the count of changed
 // cells ADDED to *changed (no reset, no host read: models/scheme.py reads a
 // whole check period's counters at once)
+// ``amp_xs``: x stride of the amp arrays in elements (0: ny * nz, contiguous)
 FDTD_API int fdtd_amplitude_many_f32(const void* const* f, void* const* amp, int ncomp, int ny, int nz,
-                                     const int* boxes, double accuracy, unsigned int* changed, void* s) {
-  return amplitude_many<float>(f, amp, ncomp, ny, nz, boxes, accuracy, changed, (hipStream_t)s);
+                                     const int* boxes, long long amp_xs, double accuracy, unsigned int* changed,
+                                     void* s) {
+  return amplitude_many<float>(f, amp, ncomp, ny, nz, boxes, amp_xs, accuracy, changed, (hipStream_t)s);
 }
 FDTD_API int fdtd_amplitude_many_f64(const void* const* f, void* const* amp, int ncomp, int ny, int nz,
-                                     const int* boxes, double accuracy, unsigned int* changed, void* s) {
-  return amplitude_many<double>(f, amp, ncomp, ny, nz, boxes, accuracy, changed, (hipStream_t)s);
+                                     const int* boxes, long long amp_xs, double accuracy, unsigned int* changed,
+                                     void* s) {
+  return amplitude_many<double>(f, amp, ncomp, ny, nz, boxes, amp_xs, accuracy, changed, (hipStream_t)s);
 }
 
 FDTD_API int fdtd_counter_add(int* counter, int n, void* s) {

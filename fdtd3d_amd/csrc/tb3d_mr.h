@@ -72,6 +72,29 @@ struct TfDev {
   TfSet s[TF_MAX_SETS];
 };
 
+// Amplitude (steady-state) mode folded into the blocked passes (feature bit
+// 8; reference Scheme3D.cpp:2945-3333, models/scheme.py
+// perform_amplitude_steps): at every level each owned cell inside its
+// component's amplitude box compares |f| with its running maximum a and, when
+// |f| >= a and (|f| - a) / a > acc, sets a = |f| and counts one change for
+// that level (step) -- the arithmetic of k_amplitude_many, level by level.  A
+// cell's levels run in T consecutive trips of the same lane, so a hands from
+// level to level through a per-thread LDS slot (T - 1 slots x 6 components x
+// the 32 x 64 tile: 96 KiB at T = 3); level 0 reads it from memory (prefetched
+// a trip ahead), the last level writes it back.  The changed counts of each
+// level accumulate per lane and go to ``counts[l]`` with one atomic per wave
+// and level at the end.  The amplitude mode's hard source is a z line
+// (src_k .. k1 - 1).
+struct AmpDev {
+  float* a;          // running maxima of |Ex| .. |Hz|, [x][component][y][z]: ONE buffer descriptor
+                     // per x plane covers all six (SGPRs are this kernel's scarce resource)
+  Box3 b[6];         // amplitude boxes (computation box minus PML, local): y / z at setup
+  int xr[6];         // their x ranges, lo | hi << 16 (the per-plane test)
+  unsigned* counts;  // changed cells per level of the pass
+  float acc;         // relative growth that counts as a change
+  int k1;            // the source's z line: src_k .. k1 - 1
+};
+
 // Memory access through buffer descriptors: one descriptor per (array, x
 // plane) built in SGPRs from the wave-uniform plane index, plus ONE 32-bit
 // per-lane byte offset shared by every array (buffer_load ... offen).  Flat
@@ -192,10 +215,13 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     const float4* __restrict__ ce4, const float4* __restrict__ ch4, Box3 BE, Box3 BH, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz,
-    const TfDev* __restrict__ tf, const float* __restrict__ gtab) {
-  // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF
+    const TfDev* __restrict__ tf, const float* __restrict__ gtab, AmpDev amp) {
+  // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF,
+  // 8 amplitude mode (alone; T <= 3: its LDS hand-off)
   constexpr int PC = FX & 3;
   constexpr bool TFS = FX & 4;
+  constexpr bool AMP = FX & 8;
+  static_assert(!AMP || (FX == 8 && V == 1 && T <= 3), "amplitude mode: scalar lanes, alone, T <= 3");
   static_assert(V == 1 || !FX, "sparse coefficients / TF/SF: scalar lanes");
   constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
   static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
@@ -319,6 +345,81 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   }
   const bool wave_e = PCE && __any(inb & ((1u << R) - 1u));
   const bool wave_h = PCH && __any(inb >> R);
+
+  // amplitude mode: bit r * 6 + c -- row r of this lane is an owned cell of
+  // the output box inside component c's amplitude box (y / z; x per plane)
+  unsigned ambits = 0;
+  constexpr int AS = AMP ? T - 1 : 1;
+  __shared__ float sA[AS > 0 ? AS : 1][AMP ? 6 : 1][AMP ? ROWS : 1][AMP ? 64 : 1];
+  float aPre[AMP ? 6 : 1][R], aPend[AMP ? 6 : 1][R];
+  unsigned acnt[AMP ? T : 1];
+  if constexpr (AMP) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int j = jw + r;
+      const bool own = (mbits >> ((r * 7 + 6) * V)) & 1u;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const Box3& ab = amp.b[c];
+        const bool in = own && j >= ab.lo[1] && j < ab.hi[1] && kb >= ab.lo[2] && kb < ab.hi[2];
+        ambits |= (in ? 1u : 0u) << (r * 6 + c);
+        aPre[c][r] = aPend[c][r] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < T; ++l) acnt[l] = 0u;
+  }
+  // the six maxima of x plane p (offset c * plane * 4 + roff)
+  auto amp_rsrc = [&](int p) -> Rsrc { return plane_rsrc(amp.a, p, nx, 6 * plane); };
+  // level-0 maxima of the next trip (E on plane X + 1, H on plane X)
+  auto amp_prefetch = [&](int X) {
+    if constexpr (AMP) {
+      const Rsrc re = amp_rsrc(X + 1), rh = amp_rsrc(X);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          // the component's plane offset rides in the instruction's SGPR offset
+          aPre[c][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+              c < 3 ? re : rh, ((ambits >> (r * 6 + c)) & 1u) ? roff[r] : 0xF0000000u, c * 4 * (int)plane, 0));
+      }
+    }
+  };
+  // level l of kind k (0 E, 1 H) on plane p, row r: compare, count, hand on
+  auto amp_level = [&](int k, int l, int p, int r, const F3<V>& f) {
+    if constexpr (AMP) {
+      const bool pin = p >= i0 && p < i1;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int c = 3 * k + q;
+        const float fv = q == 0 ? f.x[0] : (q == 1 ? f.y[0] : f.z[0]);
+        const float v = fabsf(fv);
+        const int xr = amp.xr[c];
+        const bool in = pin && ((ambits >> (r * 6 + c)) & 1u) &&
+                        (unsigned)(p - (xr & 0xffff)) < (unsigned)((xr >> 16) - (xr & 0xffff));
+        float& slot = sA[l > 0 ? l - 1 : 0][c][R * w + r][lane];
+        // carried values hold a negated maximum once a level of this pass
+        // changed it (maxima are >= 0): only those are written back
+        const float raw = l == 0 ? aPre[c][r] : slot;
+        const bool dirty = l > 0 && (__float_as_uint(raw) >> 31);
+        const float old = fabsf(raw);
+        const float den = old != 0.f ? old : (v != 0.f ? v : 1.f);
+        // (v - old) / den > acc without the division (den > 0)
+        const bool ch = in && v >= old && (v - old) > amp.acc * den;
+        const float nv = ch ? v : old;
+        acnt[l] += ch ? 1u : 0u;
+        // the slot of level l - 1 now takes this trip's level l - 1 result
+        // (plane p + 1), read by level l of the next trip
+        if (l > 0) slot = aPend[c][r];
+        if (l < T - 1) {
+          aPend[c][r] = (dirty || ch) ? -nv : nv;
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv), amp_rsrc(p),
+                                                (in && (dirty || ch)) ? roff[r] : 0xF0000000u, c * 4 * (int)plane, 0);
+        }
+      }
+    }
+  };
 
   // TF/SF.  x-face sets (one plane each, all rows / lanes of the TF box) are
   // rare per wave and go through scalar loads when a level hits their plane.
@@ -649,12 +750,14 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * cx;
         En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * cy;
         En[r].z = Ec[r].z + coef(bez, pe, r, 2, ce.z) * cz;
-        if (src_plane && jw + r == src_j && src_k >= kb && src_k < kb + V) {
-          const int q = src_k - kb;
+        if (src_plane && jw + r == src_j &&
+            (AMP ? (kb >= src_k && kb < amp.k1) : (src_k >= kb && src_k < kb + V))) {
+          const int q = AMP ? 0 : src_k - kb;
           if (src_comp == 0) En[r].x[q] = sv.v[l];
           if (src_comp == 1) En[r].y[q] = sv.v[l];
           if (src_comp == 2) En[r].z[q] = sv.v[l];
         }
+        amp_level(0, l, pe, r, En[r]);
       }
       const int ph = pe - 1;
 #pragma unroll
@@ -675,6 +778,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         Hn.x = Hp[l][r].x + coef(bhx, ph, r, 3, ch.x) * dx;
         Hn.y = Hp[l][r].y + coef(bhy, ph, r, 4, ch.y) * dy;
         Hn.z = Hp[l][r].z + coef(bhz, ph, r, 5, ch.z) * dz;
+        amp_level(1, l, ph, r, Hn);
         // later rows (r+1 ..) read only their own and higher rows' Ep, so
         // row r rotates as soon as its H is done
         Ec[r] = Ep[l][r];
@@ -682,6 +786,8 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         Hp[l][r] = Hc[r];
         Hc[r] = Hn;
       }
+      // the next trip's level-0 maxima, in flight under the remaining levels
+      if (AMP && l == 0) amp_prefetch(X);
     }
     if (ring_ld) {
       // slot of plane qn = that of plane qn - T, read at this trip's last level
@@ -711,6 +817,15 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     run(std::true_type{});
   else
     run(std::false_type{});
+  if constexpr (AMP) {
+#pragma unroll
+    for (int l = 0; l < T; ++l) {
+      unsigned v = acnt[l];
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+      if (lane == 0 && v) atomicAdd(amp.counts + l, v);
+    }
+  }
 }
 
 
@@ -724,7 +839,7 @@ template <int T, int V, int R, int FX, int NW = TBW>
 int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                  const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
                  int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
-                 const TfDev* tf, const float* gtab, hipStream_t s) {
+                 const TfDev* tf, const float* gtab, const AmpDev& amp, hipStream_t s) {
   constexpr int HL = (T + V - 1) / V;
   constexpr int TBZ = (64 - 2 * HL) * V;
   dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], NW * R - 2 * T),
@@ -734,7 +849,7 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
       O, xchunk, src[0], src[1], src[2], src[3], sv,                                                       \
-      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab)
+      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, amp)
   if constexpr (FX != 0) {
     MR_LAUNCH(1, false);  // tuning variants: uniform media only
   } else {

@@ -328,8 +328,18 @@ template <int T>
 int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                      float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                      float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
-                     const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, hipStream_t s) {
-#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, s
+                     const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const AmpDev& amp,
+                     hipStream_t s) {
+#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, amp, s
+  // amplitude mode: uniform media, T <= 3 (tb3d_mr.h AmpDev)
+  if (fx == 8) {
+    if constexpr (T <= 3) {
+      // 16 waves x 2 rows; the 8 x 4 shape (tuning knob 1) needs 200-256 VGPRs
+      if (g_tb_mr_shape == 1) return launch_tb_mr<T, 1, 4, 8, 8>(MR_ARGS);
+      return launch_tb_mr<T, 1, 2, 8>(MR_ARGS);
+    }
+    return (int)hipErrorInvalidValue;
+  }
   // per-cell: one kind keeps T coefficient planes in LDS (24 KiB each, 160
   // KiB per CU: T <= 5); both kinds keep them in registers (spill-free to T = 2)
   if constexpr (T <= 5) {
@@ -366,9 +376,10 @@ int tb_mr_xchunk(int fx, const Box3& O, int steps) {
 int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, float* const* eout,
                    float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                    float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, int steps,
-                   const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, hipStream_t s) {
+                   const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const AmpDev& amp,
+                   hipStream_t s) {
   if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
-#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, s
+#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, amp, s
   switch (steps) {
     case 1: return launch_tb_mr_sel<1>(MR_ARGS);
     case 2: return launch_tb_mr_sel<2>(MR_ARGS);
@@ -461,7 +472,7 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   if (!pc && (MR > 1 || steps > 4)) {
     const Box3 nb = make_box(kNoBox);
     return tb_mr_dispatch(0, ein, hin, eout, hout, nullptr, nullptr, nb, nb, fcb, fdb, nx, ny, nz, b, O, xchunk,
-                          steps, src, sv, nullptr, nullptr, s);
+                          steps, src, sv, nullptr, nullptr, AmpDev{}, s);
   }
   if (steps > 4) return (int)hipErrorInvalidValue;
   if (xchunk <= 0) {
@@ -514,7 +525,49 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
   const int fx = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0) | (tf && gtab ? 4 : 0);
   return tb_mr_dispatch(fx, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
                         (const float4*)(box_empty(BH) ? nullptr : ch4), BE, BH, (float)cb, (float)db, nx, ny, nz, b,
-                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, (hipStream_t)stream);
+                        O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, AmpDev{}, (hipStream_t)stream);
+}
+
+// T <= 3 fused leapfrog steps with the amplitude (steady-state) update of
+// every level folded in (tb3d_mr.h AmpDev; uniform media, scalar
+// coefficients): ``amp`` = the six running-maximum arrays (field shape, the
+// planes of one [x][6][y][z] buffer: x stride 6 ny nz),
+// ``aboxes`` = their six amplitude boxes, ``counts`` = T uint32 counters that
+// receive the changed cells of each level (added to), ``accuracy`` the
+// relative growth that counts.  ``src`` = {i, j, k0, comp, k1}: a hard E
+// source on the z line k0 .. k1 - 1 (comp -1: none).  Other arguments as
+// fdtd_tb3d_v4_f32.
+FDTD_API int fdtd_tb3d_amp_f32(const float* const* ein, const float* const* hin, float* const* eout,
+                               float* const* hout, double cb, double db, int nx, int ny, int nz, const int* boxes,
+                               const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
+                               float* const* amp, const int* aboxes, double accuracy, unsigned* counts,
+                               void* stream) {
+  if (nz % 4 != 0 || steps < 1 || steps > 3 || !counts) return (int)hipErrorInvalidValue;
+  Box3 b[6];
+  for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
+  const Box3 O = make_box(obox);
+  if (box_empty(O)) return 0;
+  TbSrc sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
+  // the six arrays are the component planes of one [x][6][y][z] buffer
+  const long long plane = (long long)ny * nz;
+  // (the component offset rides in the instruction's SGPR offset: keep it
+  // far below the 0xF0000000 "no access" lane offset)
+  if (6 * plane * 4 >= (1ll << 28)) return (int)hipErrorInvalidValue;
+  AmpDev A;
+  A.a = amp[0];
+  for (int c = 0; c < 6; ++c) {
+    if (!amp[c] || amp[c] != amp[0] + c * plane) return (int)hipErrorInvalidValue;
+    A.b[c] = make_box(aboxes + 6 * c);
+    if (A.b[c].lo[0] < 0 || A.b[c].hi[0] >= 65536) return (int)hipErrorInvalidValue;
+    A.xr[c] = A.b[c].lo[0] | (A.b[c].hi[0] << 16);
+  }
+  A.counts = counts;
+  A.acc = (float)accuracy;
+  A.k1 = src[4];
+  const Box3 nb = make_box(kNoBox);
+  return tb_mr_dispatch(8, ein, hin, eout, hout, nullptr, nullptr, nb, nb, (float)cb, (float)db, nx, ny, nz, b, O,
+                        xchunk, steps, src, sv, nullptr, nullptr, A, (hipStream_t)stream);
 }
 
 // size of the TfDev block the host fills (ABI check)

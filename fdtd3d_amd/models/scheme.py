@@ -46,6 +46,12 @@ from .regions import RegionLevel
 from ..parallel.domain import Domain, box_empty, box_intersect, box_subtract
 from ..utils.assertions import FdtdError, fdtd_assert
 from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
+
+# steps per blocked amplitude pass (csrc/tb3d_mr.h AmpDev: T - 1 levels of
+# running maxima in LDS, <= 3).  fp32, check every 32 steps: 256^3 T = 3 67.3k,
+# T = 2 64.3k, per step 37.3k Mcells/s; 512^3 79.7k / 76.2k / 45.2k
+# (profiles/amplitude_r4.md)
+AMP_TB_STEPS = 3
 from ..utils import logging as log
 from .blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64, BlockedStepping, auto_time_block
 from .tfsf import build_tfsf_sets, build_tfsf_tables, incident_line_length
@@ -297,7 +303,15 @@ class YeeScheme(BlockedStepping):
             self._init_tfsf()
         self._init_source()
         if cfg.use_amp_mode:
-            self.amp = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+            # one [x][component][y][z] buffer per plane: the maxima of one x
+            # plane of all components are contiguous, so the blocked amplitude
+            # kernel reads them through ONE buffer descriptor per plane
+            # (csrc/tb3d_mr.h AmpDev); each component is a strided view
+            self.amp = []
+            sh = tuple(self.domain.shape)
+            for _ in range(self.planes):
+                big = torch.zeros((sh[0], len(self.comps), sh[1], sh[2]), dtype=self.dtype, device=self.device)
+                self.amp.append({c: big[:, n] for n, c in enumerate(self.comps)})
         # fused E+H kernel (ping-pong buffers): plain 3D updates with at most a
         # hard E point source
         self.fused = (cfg.use_fused and hasattr(self.ops, "fused_step") and cfg.scheme == "3d"
@@ -909,6 +923,12 @@ class YeeScheme(BlockedStepping):
                     s = self.domain.shape
                     offs.append((li2[0] * s[1] + li2[1]) * s[2] + li2[2])
             self.line_source = ("Ez", torch.as_tensor(offs, dtype=torch.int64, device=self.device))
+            # the same line as (component, i, j, k0, k1) for the blocked
+            # amplitude passes (serial runs: the whole line is local)
+            self.line_box = None
+            li0 = self.domain.local_index((size[0] // 8, size[1] // 2, lo))
+            if self.halo is None and li0 is not None and hi > lo:
+                self.line_box = ("Ez", li0[0], li0[1], li0[2], li0[2] + hi - lo)
 
     def source_value(self, t: int, plane: int) -> float:
         cfg = self.cfg
@@ -1578,23 +1598,35 @@ class YeeScheme(BlockedStepping):
         K = max(1, int(getattr(self.cfg, "amplitude_check_steps", 8)))
         boxes = [self.amplitude_box(c) for c in self.comps]
         counts = torch.zeros(K, dtype=torch.int32, device=self.device)
+        self.amplitude_counts = []  # changed cells of every step taken
         taken = 0
         try:
             # the changed-cell counts of K steps accumulate on the device (one
             # fused launch per step, no host sync) and are read back once per
             # period; the run stops at the end of the period in which a step
             # changed no amplitude (K = 1: the check after every step)
+            T = self._amp_blocked_steps()
             while taken < self.cfg.amplitude_steps:
                 n = min(K, self.cfg.amplitude_steps - taken)
                 counts.zero_()
-                for s_ in range(n):
+                s_ = 0
+                while s_ < n:
+                    if T > 1 and n - s_ >= 2:
+                        # blocked pass with the amplitude update of every step
+                        # folded in (csrc/tb3d_mr.h AmpDev)
+                        k = min(T, n - s_)
+                        self._amp_tb_step(k, boxes, counts[s_:s_ + k])
+                        s_ += k
+                        continue
                     self.step()
                     self.ops.amplitude_update_many([self.F[0][c] for c in self.comps],
                                                    [self.amp[0][c] for c in self.comps], boxes, ACCURACY,
                                                    counts[s_:s_ + 1])
+                    s_ += 1
                 got = [int(v) for v in counts[:n].cpu()]
                 if self.halo is not None:
                     got = [self.halo.allreduce_sum(v) for v in got]
+                self.amplitude_counts += got
                 for s_ in range(n):
                     if got[s_] == 0 and taken + s_ + 1 > 1:
                         self.amplitude_converged = True
@@ -1606,6 +1638,32 @@ class YeeScheme(BlockedStepping):
             return taken
         finally:
             self.in_amplitude = False
+
+    def _amp_blocked_steps(self) -> int:
+        """Steps per blocked amplitude pass (1: per-step stepping).  Serial
+        3D runs of uniform media without PML, TF/SF, dispersive media or
+        hooks, whose ops fold the amplitude update into the blocked kernel."""
+        cfg = self.cfg
+        if (cfg.scheme != "3d" or self.halo is not None or self.planes != 1 or cfg.use_pml or cfg.use_tfsf
+                or cfg.use_metamaterials or self.hooks or not hasattr(self.ops, "tb_amp_step")
+                or getattr(self, "line_box", None) is None or cfg.check_finite):
+            return 1
+        if any(getattr(self.cb.get(c), "cell", None) is not None for c in self.comps):
+            return 1
+        if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
+            return 1
+        T = min(AMP_TB_STEPS, getattr(self.ops, "tb_amp_max_steps", 1))
+        if T > 1 and not hasattr(self, "F_alt"):
+            self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+        return T
+
+    def _amp_tb_step(self, T: int, aboxes, counts: torch.Tensor) -> None:
+        upd, outs = self._tb_regions(T)
+        vals = [self.source_value(self.t + l, 0) for l in range(T)]
+        self.ops.tb_amp_step(self.F[0], self.F_alt[0], upd, outs[0], self.cb, T, self.line_box, vals,
+                             [self.amp[0][c] for c in self.comps], aboxes, ACCURACY, counts)
+        self.F[0], self.F_alt[0] = self.F_alt[0], self.F[0]
+        self.t += T
 
     # -------------------------------------------------------------- checks
     def check_finite(self) -> None:

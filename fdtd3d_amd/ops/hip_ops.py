@@ -560,15 +560,28 @@ class HipOps:
         _check(rc, "amplitude_update")
         return int(s.item())
 
+    def _check_amp(self, amps: Sequence[torch.Tensor], shape) -> int:
+        """Running-maximum arrays: the field shape, rows contiguous, one x
+        stride for all (models/scheme.py keeps the six components of an x plane
+        together); returns that stride."""
+        xs = amps[0].stride(0)
+        for a in amps:
+            if a.device.type != "cuda" or a.dtype != self.dtype or tuple(a.shape) != tuple(shape):
+                raise HipError("amplitude array %s/%s %s vs field shape %s" % (a.device, a.dtype, tuple(a.shape),
+                                                                              tuple(shape)))
+            if a.stride() != (xs, shape[2], 1) or xs < shape[1] * shape[2]:
+                raise HipError("amplitude arrays need strides (xs, nz, 1), got %s" % (a.stride(),))
+        return xs
+
     def amplitude_update_many(self, fields: Sequence[torch.Tensor], amps: Sequence[torch.Tensor],
                               boxes: Sequence[Box], accuracy: float, counter: torch.Tensor) -> None:
         """Amplitude update of several components in one launch; the number
         of changed cells is ADDED to the device int32 ``counter`` (one
         element) -- no host synchronisation."""
         shape = tuple(fields[0].shape)
-        for f, a in zip(fields, amps):
+        xs = self._check_amp(amps, shape)
+        for f in fields:
             self._check_tensor(f, shape)
-            self._check_tensor(a, shape)
         for b in boxes:
             for d in range(3):
                 if not _empty(b) and (b[0][d] < 0 or b[1][d] > shape[d]):
@@ -578,7 +591,7 @@ class HipOps:
         n = len(fields)
         rc = self.fn("amplitude_many")((c_vp * n)(*[f.data_ptr() for f in fields]),
                                        (c_vp * n)(*[a.data_ptr() for a in amps]), c_int(n), c_int(shape[1]),
-                                       c_int(shape[2]), _box_arr(boxes), c_double(accuracy),
+                                       c_int(shape[2]), _box_arr(boxes), ctypes.c_longlong(xs), c_double(accuracy),
                                        c_vp(counter.data_ptr()), _stream())
         _check(rc, "amplitude_many")
         self.launches += 1
@@ -702,6 +715,66 @@ class HipOps:
         _check(rc, "tfsf_pass")
         self.launches += 1
         return g
+
+    tb_amp_max_steps = 3  # amplitude passes: the kernel's LDS hand-off holds T - 1 levels
+
+    def tb_amp_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                    obox: Box, cb: Dict[str, Coef], steps: int, line, vals, amps: Sequence[torch.Tensor],
+                    aboxes: Sequence[Box], accuracy: float, counts: torch.Tensor) -> None:
+        """``steps`` (<= 3) fused leapfrog steps with the amplitude update of
+        every step folded in (tb3d_mr.h AmpDev, fdtd_tb3d_amp_f32): the
+        running maxima ``amps`` (Ex .. Hz, one allocation, equally spaced) of
+        the cells of ``obox`` inside ``aboxes`` advance level by level, and
+        ``counts[l]`` (int32, device) gets the changed cells of step l added.
+        ``line`` = (E component, i, j, k0, k1) of the hard z-line source, or
+        None; ``vals`` its value per step.  Uniform media only."""
+        E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
+        if self.dtype != torch.float32 or not (1 <= steps <= self.tb_amp_max_steps):
+            raise HipError("amplitude passes: fp32, 1..%d steps" % self.tb_amp_max_steps)
+        shape = tuple(fin["Ex"].shape)
+        if shape[2] % 4 != 0:
+            raise HipError("fp32 tb_amp_step needs nz %% 4 == 0, got %s" % (shape,))
+        for c in E + H:
+            self._check_tensor(fin[c], shape)
+            self._check_tensor(fout[c], shape)
+            if fin[c].data_ptr() == fout[c].data_ptr():
+                raise HipError("tb_amp_step needs distinct in/out buffers")
+            if self._cell_or_none(cb[c]) is not None:
+                raise HipError("tb_amp_step: uniform media only")
+        for bx in list(boxes.values()) + [obox] + list(aboxes):
+            for d in range(3):
+                if not _empty(bx) and (bx[0][d] < 0 or bx[1][d] > shape[d]):
+                    raise HipError("box %s outside array %s" % (bx, shape))
+        cbv, dbv = cb["Ex"].scalar, cb["Hx"].scalar
+        if any(cb[c].scalar != cbv for c in E) or any(cb[c].scalar != dbv for c in H):
+            raise HipError("tb_amp_step: scalar coefficients must agree per kind")
+        xs = self._check_amp(amps, shape)
+        plane = shape[1] * shape[2]
+        es = amps[0].element_size()
+        if xs != 6 * plane or 6 * plane * es >= 2 ** 28:
+            raise HipError("amplitude passes need the six arrays interleaved per x plane (x stride 6 ny nz)")
+        for n, a in enumerate(amps):
+            if a.data_ptr() != amps[0].data_ptr() + n * plane * es:
+                raise HipError("amplitude arrays must be the planes of one [x][6][y][z] allocation")
+        if counts.device.type != "cuda" or counts.dtype != torch.int32 or counts.numel() < steps:
+            raise HipError("amplitude counts: %d int32 on the device" % steps)
+        src = [-1, -1, -1, -1, -1]
+        v8 = [0.0] * 8
+        if line is not None:
+            comp, i, j, k0, k1 = line
+            if comp not in E or not (0 <= i < shape[0] and 0 <= j < shape[1] and 0 <= k0 <= k1 <= shape[2]):
+                raise HipError("tb_amp_step: bad line source %s" % (line,))
+            src = [i, j, k0, E.index(comp), k1]
+            v8[:steps] = [float(v) for v in vals[:steps]]
+        arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
+        rc = self.lib.fdtd_tb3d_amp_f32(
+            arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), c_double(cbv), c_double(dbv), c_int(shape[0]),
+            c_int(shape[1]), c_int(shape[2]), _box_arr([boxes[c] for c in E + H]), _box_arr([obox]),
+            c_int(self.tb_xchunk), c_int(steps), (c_int * 5)(*src), (c_double * 8)(*v8),
+            (c_vp * 6)(*[a.data_ptr() for a in amps]), _box_arr(list(aboxes)), c_double(accuracy),
+            c_vp(counts.data_ptr()), _stream())
+        _check(rc, "tb3d_amp")
+        self.launches += 1
 
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
                 obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None) -> None:

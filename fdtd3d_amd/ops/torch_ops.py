@@ -202,6 +202,46 @@ class TorchOps:
                 sp = tuple(slice(s.start + 1, s.stop + 1) for s in sl)
                 fout[c][sl] = cur[c][sp]
 
+    tb_amp_max_steps = 3
+
+    def tb_amp_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                    obox: Box, cb: Dict[str, Coef], steps: int, line, vals, amps, aboxes, accuracy: float,
+                    counts: torch.Tensor) -> None:
+        """Reference semantics of the amplitude pass (csrc/tb3d_mr.h AmpDev):
+        the fused steps of :meth:`tb_step` with, after each, the amplitude
+        update (:meth:`amplitude_update`) of the cells of ``obox`` inside
+        ``aboxes`` -- ``counts[l]`` += the changed cells of step l -- and the
+        hard source on the z line ``line`` = (E component, i, j, k0, k1)."""
+        pad = {c: torch.nn.functional.pad(fin[c], (1, 1, 1, 1, 1, 1)) for c in fin}
+        shifted = {c: ((b[0][0] + 1, b[0][1] + 1, b[0][2] + 1), (b[1][0] + 1, b[1][1] + 1, b[1][2] + 1))
+                   for c, b in boxes.items()}
+        cbp = cb_pad(cb)
+        e = {c: b for c, b in shifted.items() if c[0] == "E"}
+        h = {c: b for c, b in shifted.items() if c[0] == "H"}
+        comps = ("Ex", "Ey", "Ez", "Hx", "Hy", "Hz")
+        cur = pad
+        for l in range(steps):
+            nxt = {c: cur[c].clone() for c in cur}
+            self.curl_update("E", e, nxt, cur, cbp)
+            if line is not None:
+                comp, i, j, k0, k1 = line
+                nxt[comp][i + 1, j + 1, k0 + 1:k1 + 1] = float(vals[l])
+            self.curl_update("H", h, nxt, nxt, cbp)
+            cur = nxt
+            for c, a, ab in zip(comps, amps, aboxes):
+                b = box_intersect_(ab, obox)
+                if _empty(b):
+                    continue
+                view = {c: cur[c][tuple(slice(b[0][d] + 1, b[1][d] + 1) for d in range(3))]}
+                n = self.amplitude_update(view[c], a[box_slices(b)], ((0, 0, 0), tuple(view[c].shape)), accuracy)
+                counts[l] += n
+        # the whole output box of every component, like the kernel (the line
+        # source may sit outside its component's update box)
+        sl = box_slices(obox)
+        sp = tuple(slice(s_.start + 1, s_.stop + 1) for s_ in sl)
+        for c in boxes:
+            fout[c][sl] = cur[c][sp]
+
     def _tfsf_level(self, F, tfsf, l: int, kind: str, boxes, cb) -> None:
         """TF/SF corrections of level ``l`` of a blocked pass on fields padded
         by one cell: the E-form tables of the stepped path (``sets.tables``,

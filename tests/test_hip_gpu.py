@@ -138,6 +138,40 @@ def test_amplitude_mode_3d_f32_vector(gpu):
     assert getattr(a, "amplitude_stable_step", None) == getattr(b, "amplitude_stable_step", None)
 
 
+@pytest.mark.parametrize("T", [2, 3])
+def test_amplitude_blocked_passes(gpu, T, monkeypatch):
+    """Amplitude mode on blocked passes (csrc/tb3d_mr.h AmpDev: the update
+    of every step folded into the pass, maxima handed from level to level in
+    LDS) against per-step stepping with the separate amplitude kernel: the
+    same maxima, fields and per-step changed counts (fp32; counts may differ
+    by the few cells whose growth sits at the threshold within round-off)."""
+    import fdtd3d_amd.models.scheme as sch
+    cfg = SchemeConfig(scheme="3d", size=(48, 40, 64), time_steps=10, amplitude_steps=45, use_amp_mode=True,
+                       scene="vacuum", dtype="f32", amplitude_check_steps=8)
+    runs = {}
+    for t in (T, 1):
+        monkeypatch.setattr(sch, "AMP_TB_STEPS", t)
+        s = YeeScheme(cfg, make_ops("hip", None, gpu, torch.float32))
+        s.init_scheme()
+        s.init_grids()
+        assert s._amp_blocked_steps() == t
+        s.advance(cfg.time_steps)
+        s.perform_amplitude_steps()
+        torch.cuda.synchronize()
+        runs[t] = s
+    a, b = runs[T], runs[1]
+    assert len(a.amplitude_counts) == len(b.amplitude_counts) == 45
+    tot = sum(b.amplitude_counts)
+    assert tot > 1000
+    assert sum(abs(x - y) for x, y in zip(a.amplitude_counts, b.amplitude_counts)) <= 1e-3 * tot + 5, \
+        (a.amplitude_counts, b.amplitude_counts)
+    for c in a.comps:
+        scale = max(float(b.amp[0][o].abs().max()) for o in b.comps if o[0] == c[0]) + 1e-30
+        assert float((a.amp[0][c] - b.amp[0][c]).abs().max()) <= 2e-5 * scale, c
+        fs = max(float(b.F[0][o].abs().max()) for o in b.comps if o[0] == c[0]) + 1e-30
+        assert float((a.F[0][c] - b.F[0][c]).abs().max()) <= 2e-5 * fs, c
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 def test_fused_vacuum_3d(gpu, dtype):
     compare(SchemeConfig(scheme="3d", size=(50, 37, 131), time_steps=21, scene="vacuum", dtype=dtype,

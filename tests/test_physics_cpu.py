@@ -197,3 +197,30 @@ def test_capacity_plan_drude_upml():
     # the material grids are released once the coefficients exist
     assert not s.sampler._cache and all(v is None for v in s.mat.values())
     s.perform_steps()
+
+
+def test_amplitude_blocked_passes_match_stepped(monkeypatch):
+    """Amplitude mode on blocked passes (the amplitude update of every step
+    folded into the pass, csrc/tb3d_mr.h AmpDev; torch oracle of
+    ``tb_amp_step``) equals per-step stepping with the separate update: same
+    first stable step, same counts, same maxima and fields (fp64, bitwise
+    arithmetic of the same single steps)."""
+    import fdtd3d_amd.models.scheme as sch
+    res = {}
+    for T in (1, 2, 3):
+        monkeypatch.setattr(sch, "AMP_TB_STEPS", T)
+        cfg = SchemeConfig(scheme="3d", size=(20, 16, 24), time_steps=6, amplitude_steps=400, use_amp_mode=True,
+                           scene="vacuum", dtype="f64", amplitude_check_steps=8)
+        s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
+        s.init_scheme()
+        s.init_grids()
+        assert s._amp_blocked_steps() == T
+        s.advance(cfg.time_steps)
+        taken = s.perform_amplitude_steps()
+        res[T] = (taken, s.amplitude_converged, getattr(s, "amplitude_stable_step", None),
+                  {c: s.amp[0][c].clone() for c in s.comps}, {c: s.F[0][c].clone() for c in s.comps})
+    for T in (2, 3):
+        assert res[T][:3] == res[1][:3], (T, res[T][:3], res[1][:3])
+        for c in res[1][3]:
+            assert torch.allclose(res[T][3][c], res[1][3][c], rtol=1e-12, atol=0), c
+            assert torch.allclose(res[T][4][c], res[1][4][c], rtol=1e-12, atol=1e-300), c

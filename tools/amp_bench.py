@@ -35,14 +35,22 @@ def main():
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     dt = sys.argv[3] if len(sys.argv) > 3 else "f32"
     base = dict(scheme="3d", size=(n, n, n), dtype=dt, scene="vacuum", time_steps=steps)
+    import fdtd3d_amd.models.scheme as sch
     rows = []
-    for K in (1, 8, 32):
-        s = mk(SchemeConfig(use_amp_mode=True, amplitude_steps=steps, amplitude_check_steps=K, **base))
-        s.cfg.amplitude_steps = 10
-        s.perform_amplitude_steps()  # warm-up
-        s.cfg.amplitude_steps = steps
-        ms = timed(s.perform_amplitude_steps, steps)
-        rows.append(("amplitude mode, check every %d steps" % K, ms))
+    for T in (1, 2, 3):
+        # T = 1: per-step stepping + the separate amplitude kernel; T > 1:
+        # blocked passes with the amplitude update folded in (tb3d_mr.h AmpDev)
+        sch.AMP_TB_STEPS = T
+        for K in ((1, 8, 32) if T == 1 else (8, 32)):
+            s = mk(SchemeConfig(use_amp_mode=True, amplitude_steps=steps, amplitude_check_steps=K, **base))
+            s.cfg.amplitude_steps = 12
+            s.perform_amplitude_steps()  # warm-up
+            s.cfg.amplitude_steps = steps
+            ms = timed(s.perform_amplitude_steps, steps)
+            rows.append(("amplitude mode, %s, check every %d steps"
+                         % ("per-step" if T == 1 else "blocked T = %d" % T, K), ms))
+            del s
+    sch.AMP_TB_STEPS = 3
     s = mk(SchemeConfig(use_amp_mode=True, **base))
     s.advance(5)
     ms = timed(lambda: s.advance(steps), steps)
