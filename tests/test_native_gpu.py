@@ -51,6 +51,15 @@ CASES = {
                      "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6", "--same-size-pml", "--use-tfsf",
                      "--tfsf-sizex", "10", "--same-size-tfsf", "--angle-teta", "60", "--angle-phi", "10",
                      "--angle-psi", "5"],
+    # hybrid passes (blocked core + stepped CPML / TF/SF shell, csrc/main.cpp hybrid_pass): grids large
+    # enough for the core to hold a quarter of the cells; 23 steps = 4 passes of 5 + a 3-step tail
+    "3d_cpml_tfsf_hybrid": ["--3d", "--sizex", "104", "--same-size", "--time-steps", "23", "--scene", "vacuum",
+                            "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6", "--same-size-pml", "--use-tfsf",
+                            "--tfsf-sizex", "10", "--same-size-tfsf", "--angle-teta", "60", "--angle-phi", "10",
+                            "--angle-psi", "5"],
+    "3d_cpml_point_hybrid": ["--3d", "--sizex", "72", "--sizey", "76", "--sizez", "80", "--time-steps", "17",
+                             "--scene", "vacuum", "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6",
+                             "--pml-sizey", "7", "--pml-sizez", "5", "--hybrid-block", "4"],
     # UPML in the reference's D/B form (fused chain kernel) + oblique TF/SF, a dielectric sphere with the
     # UPML (per-cell 1/(eps eps0) in the chain), Drude and Lorentz spheres + UPML (uint8 index + table)
     "3d_upml_tfsf": ["--3d", "--sizex", "36", "--sizey", "32", "--sizez", "40", "--time-steps", "30",
@@ -71,7 +80,7 @@ CASES = {
                              "--sphere-center-y", "20", "--sphere-center-z", "20", "--sphere-radius", "6",
                              "--use-tfsf", "--tfsf-sizex", "9", "--same-size-tfsf"],
 }
-FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf"}
+FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf", "3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid"}
 
 COMPS = {"3d": ["Ex", "Ey", "Ez", "Hx", "Hy", "Hz"], "tmz": ["Ez", "Hx", "Hy"], "tez": ["Ex", "Ey", "Hz"],
          "1d": ["Ez", "Hy"]}
@@ -104,6 +113,7 @@ def test_native_driver_matches_python(case, dtype, tmp_path, gpu):
     r = subprocess.run([exe] + argv + ["--output-dir", str(nd)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Mcells/s" in r.stdout
+    assert ("hybrid passes" in r.stdout) == case.endswith("_hybrid"), r.stdout
     assert py_run(argv[:-4] + ["--dtype", "f64", "--save-res", "--save-as-dat", "--backend", "torch",
                                "--device", "cpu", "--output-dir", str(pd)], out=io.StringIO()) == 0
     shape, scheme = _shape(argv)
