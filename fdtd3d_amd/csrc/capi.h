@@ -34,7 +34,9 @@ int fdtd_update_h3d_cpml_v4_f32(float* hx, float* hy, float* hz, const float* ex
                                 int nz, const int* boxes, int xchunk, const void* const* cp, const int* ci,
                                 void* stream);
 // fused UPML / Drude chain of the three components of a kind (chain_kernels.hip):
-// P = 24 pointers, S = 2 scalars, I = 19 ints per component (layout there)
+// P = 24 pointers, S = 2 scalars, I = 25 ints per component (layout there)
+int fdtd_chain_ints_per_comp();
+int fdtd_chain_ptrs_per_comp();
 int fdtd_chain3d_f32(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny, int nz,
                      void* stream);
 int fdtd_chain3d_f64(const void* const* P, const double* S, const int* I, int drude, int kind_e, int ny, int nz,
@@ -127,4 +129,32 @@ int fdtd_1d_h_f64(double* hy, const double* ez, const double* dby, double db, in
 
 int fdtd_set_value_f32(float* f, long long off, double v, void* s);
 int fdtd_set_value_f64(double* f, long long off, double v, void* s);
+int fdtd_set_values_f32(float* f, const long long* offs, int n, double v, void* s);
+int fdtd_set_values_f64(double* f, const long long* offs, int n, double v, void* s);
+
+// generic building blocks (generic_kernels.hip): factored coefficients =
+// scalar x (px, py, pz, cell) pointers; the 2D UPML chain and the CPML slabs
+int fdtd_curl_general_f32(float* out, const float* inp, const float* const* srcs, const int* axes, const int* signs,
+                          int nterms, int kind_e, double ca_s, const void* const* ca_p, double cb_s,
+                          const void* const* cb_p, int ny, int nz, const int* box, void* s);
+int fdtd_curl_general_f64(double* out, const double* inp, const double* const* srcs, const int* axes,
+                          const int* signs, int nterms, int kind_e, double ca_s, const void* const* ca_p, double cb_s,
+                          const void* const* cb_p, int ny, int nz, const int* box, void* s);
+int fdtd_lincomb_f32(float* out, int nterms, const double* scalars, const void* const* ptrs, const float* const* xs,
+                     int ny, int nz, const int* box, void* s);
+int fdtd_lincomb_f64(double* out, int nterms, const double* scalars, const void* const* ptrs, const double* const* xs,
+                     int ny, int nz, const int* box, void* s);
+int fdtd_cpml_apply_f32(float* target, const float* src, float* psi, int axis, int sign, int kind_e, const float* bc,
+                        const float* cc, const float* kc, double cb_s, const void* const* cb_p, int ny, int nz,
+                        const int* box, const int* psi_box, void* s);
+int fdtd_cpml_apply_f64(double* target, const double* src, double* psi, int axis, int sign, int kind_e,
+                        const double* bc, const double* cc, const double* kc, double cb_s, const void* const* cb_p,
+                        int ny, int nz, const int* box, const int* psi_box, void* s);
+
+// amplitude mode (aux_kernels.hip): running maxima of up to 6 components, the
+// changed-cell count ADDED to *changed
+int fdtd_amplitude_many_f32(const void* const* f, void* const* amp, int ncomp, int ny, int nz, const int* boxes,
+                            long long amp_xs, double accuracy, unsigned int* changed, void* s);
+int fdtd_amplitude_many_f64(const void* const* f, void* const* amp, int ncomp, int ny, int nz, const int* boxes,
+                            long long amp_xs, double accuracy, unsigned int* changed, void* s);
 }

@@ -538,7 +538,7 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
 // One chain launch for the three components of a kind.  Per component c:
 // P[24c ..] = E Dn D Dp D1n D1 D1p s0 s1 caD cbD caE ica cbEa ccEa cell b0 b1 b2 ma1 ma2 id lut pcell
 // (unused: nullptr; a non-null id replaces b0 .. ma2 by lut[5 id ..]), S[2c] = scalar of the
-// E-from-D term, S[2c + 1] = plain-part coefficient, I[19c ..] = curl axes a0 a1, signs sg0
+// E-from-D term, S[2c + 1] = plain-part coefficient, I[25c ..] = curl axes a0 a1, signs sg0
 // sg1, UPML axes aD aCa aCb, chain box lo[3] hi[3], plain box lo[3] hi[3] (empty: skipped;
 // the plain box holds cells updated F += c (curl) in the same launch), storage box of the D /
 // D1 levels lo[3] hi[3] (empty: full-grid levels; else they hold that box only, x-major, z
@@ -554,6 +554,10 @@ FDTD_API int fdtd_chain3d_f64(const void* const* P, const double* S, const int* 
 }
 
 FDTD_API void fdtd_set_chain_v4(int on) { g_chain_v4 = on != 0; }
+
+// layout of the chain launch tables (checked by the callers that build them)
+FDTD_API int fdtd_chain_ints_per_comp() { return CI_PER; }
+FDTD_API int fdtd_chain_ptrs_per_comp() { return CP_PER; }
 
 // Dispersive launch over a box with no PML (sigma = 0): rows = int2 (z0, z1)
 // per (x, y) of [R[0], R[0] + R[2]) x [R[1], R[1] + R[3]); cells outside their

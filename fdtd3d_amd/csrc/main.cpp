@@ -10,12 +10,17 @@
 // spheres (--use-metamaterials, scene drude-sphere) in 3D through the fused
 // chain kernel, TF/SF plane waves in 3D, the NTFF scattered power diagram
 // (--use-ntff) and DAT/BMP output of the final fields (native_physics.h).
-// 2D TF/SF / PML, amplitude mode and multi-GPU runs go through the Python
-// driver (python -m fdtd3d_amd), which shares the kernels; asking this
-// binary for them is an error, never a silent fallback.
+// 2D CPML / UPML and TF/SF (generic slab and chain kernels), and amplitude mode
+// (running maxima folded into blocked passes for 3D vacuum fp32, a fused
+// amplitude kernel after each step otherwise).  Multi-GPU runs, complex
+// fields and resume go through the Python driver (python -m fdtd3d_amd),
+// which shares the kernels; asking this binary for them is an error, never a
+// silent fallback.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <new>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -201,6 +206,42 @@ int h1d(float* a, const float* b, const float* c, double db, int lo, int hi, voi
 }
 int h1d(double* a, const double* b, const double* c, double db, int lo, int hi, void* s) {
   return fdtd_1d_h_f64(a, b, c, db, lo, hi, s);
+}
+int setvs(float* f, const long long* o, int n, double v, void* s) { return fdtd_set_values_f32(f, o, n, v, s); }
+int setvs(double* f, const long long* o, int n, double v, void* s) { return fdtd_set_values_f64(f, o, n, v, s); }
+int curl_gen(float* out, const float* inp, const float* const* srcs, const int* axes, const int* signs, int nt,
+             int ke, const void* const* ca, const void* const* cbp, int ny, int nz, const int* box, void* s) {
+  return fdtd_curl_general_f32(out, inp, srcs, axes, signs, nt, ke, 1.0, ca, 1.0, cbp, ny, nz, box, s);
+}
+int curl_gen(double* out, const double* inp, const double* const* srcs, const int* axes, const int* signs, int nt,
+             int ke, const void* const* ca, const void* const* cbp, int ny, int nz, const int* box, void* s) {
+  return fdtd_curl_general_f64(out, inp, srcs, axes, signs, nt, ke, 1.0, ca, 1.0, cbp, ny, nz, box, s);
+}
+int lincomb(float* out, int nt, const double* sc, const void* const* p, const float* const* xs, int ny, int nz,
+            const int* box, void* s) {
+  return fdtd_lincomb_f32(out, nt, sc, p, xs, ny, nz, box, s);
+}
+int lincomb(double* out, int nt, const double* sc, const void* const* p, const double* const* xs, int ny, int nz,
+            const int* box, void* s) {
+  return fdtd_lincomb_f64(out, nt, sc, p, xs, ny, nz, box, s);
+}
+int cpml_apply(float* t, const float* src, float* psi, int axis, int sign, int ke, const float* b, const float* c,
+               const float* k, double cbs, const void* const* cbp, int ny, int nz, const int* box, const int* pb,
+               void* s) {
+  return fdtd_cpml_apply_f32(t, src, psi, axis, sign, ke, b, c, k, cbs, cbp, ny, nz, box, pb, s);
+}
+int cpml_apply(double* t, const double* src, double* psi, int axis, int sign, int ke, const double* b,
+               const double* c, const double* k, double cbs, const void* const* cbp, int ny, int nz, const int* box,
+               const int* pb, void* s) {
+  return fdtd_cpml_apply_f64(t, src, psi, axis, sign, ke, b, c, k, cbs, cbp, ny, nz, box, pb, s);
+}
+int amp_many(const float* const* f, float* const* a, int n, int ny, int nz, const int* bx, long long xs, double acc,
+             unsigned* cnt, void* s) {
+  return fdtd_amplitude_many_f32((const void* const*)f, (void* const*)a, n, ny, nz, bx, xs, acc, cnt, s);
+}
+int amp_many(const double* const* f, double* const* a, int n, int ny, int nz, const int* bx, long long xs,
+             double acc, unsigned* cnt, void* s) {
+  return fdtd_amplitude_many_f64((const void* const*)f, (void* const*)a, n, ny, nz, bx, xs, acc, cnt, s);
 }
 
 // CPML (3D, fp32 float4 kernels): profiles, psi slabs and the per-kind term
@@ -421,6 +462,161 @@ const int kCurl[6][2][3] = {{{5, 1, +1}, {4, 2, -1}}, {{3, 2, +1}, {5, 0, -1}}, 
 const double kMinFP[6][3] = {{1.0, 0.5, 0.5}, {0.5, 1.0, 0.5}, {0.5, 0.5, 1.0},
                              {0.5, 1.0, 1.0}, {1.0, 0.5, 1.0}, {1.0, 1.0, 0.5}};
 
+// ------------------------------------------------------------- 2D PML
+// Absorbing layers of the 2D schemes (TMz / TEz, fp32 / fp64) on the generic
+// one-thread-per-cell kernels of generic_kernels.hip, whose flattened (y, z)
+// plane keeps every lane busy at nz = 1:
+//  * CPML: the plain 2D update runs on every cell, then each (component, curl
+//    term, side) slab updates its psi and adds its term (models/cpml.py);
+//  * UPML (the reference's 2D PML, SchemeTMz.cpp:1896-1945): every component
+//    runs the D/B chain on its update box -- D_new = caD D + cbD curl
+//    (curl_general), E = caE E + s cell ica (cbEa D_new + ccEa D) (lincomb),
+//    the factored profiles of models/scheme.py _init_upml; where every sigma
+//    vanishes this is the plain update to round-off.
+template <typename T>
+struct Slab2d {
+  int comp, src, axis, sign;
+  int box[6], pbox[6];
+  T *psi, *b, *c, *k;
+};
+
+template <typename T>
+struct Pml2d {
+  std::vector<void*> keep;
+  std::vector<Slab2d<T>> slabs;
+  // UPML: D levels [cur, new] and the coefficient pointer sets per component
+  T* D[6][2] = {};
+  const void* ca[6][4] = {};
+  const void* cbp[6][4] = {};
+  const void* lin[6][12] = {};
+  double s[6] = {};
+  ~Pml2d() {
+    for (void* p : keep) (void)hipFree(p);
+  }
+};
+
+template <typename T>
+void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, const std::vector<int>& active,
+                  const bool* present, double dt, double dx) {
+  const int Ps[3] = {s.pmlSizeX, s.pmlSizeY, 0};
+  const double eta = std::sqrt(kMu0 / kEps0);
+  const double kmax = s.cpmlKappaMax, amax = s.cpmlAlphaMax;
+  for (int c = 0; c < 6; ++c) {
+    if (!present[c]) continue;
+    fdtd::Int3 glo, ghi;
+    fdtd::global_range(c, N, active, glo, ghi);
+    for (int t = 0; t < 2; ++t) {
+      const int src = kCurl[c][t][0], axis = kCurl[c][t][1], sign = kCurl[c][t][2];
+      if (!present[src] || axis >= 2 || Ps[axis] <= 0) continue;
+      const int Pa = Ps[axis], n = N[axis];
+      const double m = kMinFP[c][axis];
+      const double sig_max = -(4 + 1) * std::log(1e-8) / (2 * eta * Pa * dx);
+      for (int side = 0; side < 2; ++side) {
+        int lo = glo[axis], hi = ghi[axis];
+        if (side == 0)
+          hi = std::min(hi, (int)std::ceil(Pa - m));
+        else
+          lo = std::max(lo, (int)std::floor(n - Pa - m) + 1);
+        bool empty = hi <= lo;
+        for (int d = 0; d < 3; ++d) empty = empty || ghi[d] <= glo[d];
+        if (empty) continue;
+        // profiles over the whole axis with this side's clamped depth (models/cpml.py)
+        std::vector<T> b(n), cv(n), kk(n);
+        for (int v = 0; v < n; ++v) {
+          const double idx = v + m;
+          double depth = side == 0 ? (Pa - idx) / Pa : (idx - (n - Pa)) / Pa;
+          depth = std::min(1.0, std::max(0.0, depth));
+          const double d4 = depth * depth * depth * depth;
+          const double sig = sig_max * d4, kap = 1.0 + (kmax - 1.0) * d4, alp = amax * (1.0 - depth);
+          const double bc = std::exp(-(sig / kap + alp) * dt / kEps0);
+          const double den = sig * kap + kap * kap * alp;
+          b[v] = (T)bc;
+          cv[v] = (T)(den > 0 ? sig / den * (bc - 1.0) : 0.0);
+          kk[v] = (T)(1.0 / kap - 1.0);
+        }
+        Slab2d<T> sl;
+        sl.comp = c;
+        sl.src = src;
+        sl.axis = axis;
+        sl.sign = sign;
+        size_t vol = 1;
+        for (int d = 0; d < 3; ++d) {
+          sl.box[d] = d == axis ? lo : glo[d];
+          sl.box[3 + d] = d == axis ? hi : ghi[d];
+          sl.pbox[d] = d == axis ? lo : 0;
+          sl.pbox[3 + d] = d == axis ? hi : N[d];
+          vol *= (size_t)(sl.pbox[3 + d] - sl.pbox[d]);
+        }
+        sl.psi = native_phys::dev_zeros<T>(vol, P.keep);
+        sl.b = native_phys::dev_upload(b, P.keep);
+        sl.c = native_phys::dev_upload(cv, P.keep);
+        sl.k = native_phys::dev_upload(kk, P.keep);
+        P.slabs.push_back(sl);
+      }
+    }
+  }
+}
+
+// 2D UPML coefficients; ``cell_inv`` (optional, per present E component):
+// 1 / (eps eps0) per cell of a dielectric scene
+template <typename T>
+void setup_upml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, const bool* present, double dt,
+                  double dx, std::vector<T>* cell_inv) {
+  const size_t cells = (size_t)N[0] * N[1] * N[2];
+  std::vector<double> sig[3];
+  const int pml[3] = {s.pmlSizeX, s.pmlSizeY, 0};
+  for (int a = 0; a < 3; ++a) sig[a] = native_phys::sigma_profile(N[a] + 1, pml[a], dx);
+  for (int c = 0; c < 6; ++c) {
+    if (!present[c]) continue;
+    const int aD = native_phys::kUpmlAxes[c][0], aA = native_phys::kUpmlAxes[c][1], aB = native_phys::kUpmlAxes[c][2];
+    auto avg = [&](int a) {
+      std::vector<double> out(N[a]);
+      double v[4];
+      for (int n = 0; n < N[a]; ++n) {
+        for (int p = 0; p < native_phys::kStencilN[c]; ++p) v[p] = sig[a][n + native_phys::kStencil[c][p][a]];
+        out[n] = native_phys::approx_mean(v, native_phys::kStencilN[c]);
+      }
+      return out;
+    };
+    const std::vector<double> sD = avg(aD), sA = avg(aA), sB = avg(aB);
+    const double two = 2 * kEps0;
+    std::vector<T> caD(N[aD]), cbD(N[aD]), caE(N[aA]), ica(N[aA]), cbEa(N[aB]), ccEa(N[aB]);
+    for (int n = 0; n < N[aD]; ++n) {
+      caD[n] = (T)((two - sD[n] * dt) / (two + sD[n] * dt));
+      cbD[n] = (T)((two * dt / dx) / (two + sD[n] * dt));
+    }
+    for (int n = 0; n < N[aA]; ++n) {
+      caE[n] = (T)((two - sA[n] * dt) / (two + sA[n] * dt));
+      ica[n] = (T)(1.0 / (two + sA[n] * dt));
+    }
+    for (int n = 0; n < N[aB]; ++n) {
+      cbEa[n] = (T)(two + sB[n] * dt);
+      ccEa[n] = (T)(-(two - sB[n] * dt));
+    }
+    const T* cell = nullptr;
+    P.s[c] = 1.0 / (c < 3 ? kEps0 : kMu0);
+    if (cell_inv && c < 3 && !cell_inv[c].empty()) {
+      cell = native_phys::dev_upload(cell_inv[c], P.keep);
+      P.s[c] = 1.0;
+    }
+    P.ca[c][aD] = native_phys::dev_upload(caD, P.keep);
+    P.cbp[c][aD] = native_phys::dev_upload(cbD, P.keep);
+    const T* caEd = native_phys::dev_upload(caE, P.keep);
+    const T* icad = native_phys::dev_upload(ica, P.keep);
+    const T* cbEd = native_phys::dev_upload(cbEa, P.keep);
+    const T* ccEd = native_phys::dev_upload(ccEa, P.keep);
+    // lincomb terms: (caE, E), (s ica cbEa cell, D_new), (s ica ccEa cell, D)
+    P.lin[c][aA] = caEd;
+    P.lin[c][4 + aA] = icad;
+    P.lin[c][4 + aB] = cbEd;
+    P.lin[c][4 + 3] = cell;
+    P.lin[c][8 + aA] = icad;
+    P.lin[c][8 + aB] = ccEd;
+    P.lin[c][8 + 3] = cell;
+    for (int l = 0; l < 2; ++l) P.D[c][l] = native_phys::dev_zeros<T>(cells, P.keep);
+  }
+}
+
 template <typename T>
 struct TfsfLayer {
   Dev<long long> off, i0;
@@ -454,8 +650,12 @@ double inc_projection(int c, double t, double p, double q) {
 
 template <typename T>
 bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N, const int* boxes,
-                const Dev<T>* Cc, double cb, double db, double dt, double dx, double freq) {
-  const double th = s.incidentWaveAngle1 * (kPi / 180.0), ph = s.incidentWaveAngle2 * (kPi / 180.0);
+                const Dev<T>* Cc, double cb, double db, double dt, double dx, double freq, int dim,
+                const bool* present) {
+  // 2D (TMz / TEz): propagation in the xy plane, theta = pi / 2, the line
+  // 100 (Nx + Ny) long (SchemeTMz.h:186), z never bounds the TF box
+  const bool d2 = dim == 2;
+  const double th = d2 ? kPi / 2 : s.incidentWaveAngle1 * (kPi / 180.0), ph = s.incidentWaveAngle2 * (kPi / 180.0);
   const double ps = s.incidentWaveAngle3 * (kPi / 180.0);
   if (!(th >= 0 && th <= kPi / 2 + 1e-12 && ph >= 0 && ph <= kPi / 2 + 1e-12)) {
     std::fprintf(stderr, "fdtd3d (native): TF/SF incident angles must lie in [0, 90] degrees\n");
@@ -466,14 +666,14 @@ bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N,
                      phase_velocity_3d(dx, wl, courant, nl, th, ph);
   tf.ce = dt / (rel * kEps0 * dx);
   tf.ch = dt / (rel * kMu0 * dx);
-  tf.nline = 100 * (N[0] + N[1] + N[2]);
+  tf.nline = 100 * (N[0] + N[1] + (d2 ? 0 : N[2]));
   tf.einc.alloc(tf.nline);
   tf.hinc.alloc(tf.nline);
   const double L[3] = {(double)s.tfsfSizeX, (double)s.tfsfSizeY, (double)s.tfsfSizeZ};
   const double R[3] = {N[0] - L[0], N[1] - L[1], N[2] - L[2]};
-  const double dir[3] = {std::sin(th) * std::cos(ph), std::sin(th) * std::sin(ph), std::cos(th)};
+  const double dir[3] = {std::sin(th) * std::cos(ph), std::sin(th) * std::sin(ph), d2 ? 0.0 : std::cos(th)};
   const double zero[3] = {L[0] - 2.5 * std::sin(th) * std::cos(ph), L[1] - 2.5 * std::sin(th) * std::sin(ph),
-                          L[2] - 2.5 * std::cos(th)};
+                          d2 ? 0.0 : L[2] - 2.5 * std::cos(th)};
   const int dir_axis[6] = {0, 0, 1, 1, 2, 2};
   const bool dir_low[6] = {true, false, true, false, true, false};
   std::vector<T> hc((size_t)N[0] * N[1] * N[2]);
@@ -491,6 +691,7 @@ bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N,
     std::vector<Ent> ents;
     for (int t = 0; t < 2; ++t) {
       const int src = kCurl[c][t][0], axis = kCurl[c][t][1], sign = kCurl[c][t][2];
+      if (!present[src] || axis >= dim) continue;  // the scheme's own curl terms only
       const double proj = inc_projection(src, th, ph, ps);
       for (int d = 0; d < 6; ++d) {
         if (dir_axis[d] != axis) continue;
@@ -504,7 +705,7 @@ bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N,
           const double hi = (pr->iv[a].rb ? R[a] : L[a]) + pr->iv[a].ob;
           for (int v = bx[a]; v < bx[3 + a]; ++v) {
             const double g = v + kMinFP[c][a];
-            if (g > lo && g < hi) sel[a].push_back(v);
+            if (a >= dim || (g > lo && g < hi)) sel[a].push_back(v);
           }
         }
         const int nb = kind_e ? (dir_low[d] ? 0 : -1) : (dir_low[d] ? 0 : 1);
@@ -598,7 +799,11 @@ int run(const fdtd::Settings& s) {
   const bool cpml = s.doUsePML && !upml;
   const bool tfsf = s.doUseTFSF;
   const bool ntff = s.doUseNTFF && dim == 3;
-  const bool use_fused = !s.doUseSplitKernels && !cpml && !tfsf && !upml;
+  // amplitude mode (Scheme3D.cpp:2945-3333): split kernels for the regular
+  // steps (the Python driver's choice), then steps with the running maxima
+  // until a step changes none; 3D vacuum fp32 folds them into blocked passes
+  const bool amp = s.doUseAmplitudeMode;
+  const bool use_fused = !s.doUseSplitKernels && !cpml && !tfsf && !upml && !amp;
   hipStream_t st;
   HIP_OK(hipStreamCreate(&st));
 
@@ -690,9 +895,31 @@ int run(const fdtd::Settings& s) {
     return std::sin(dt * t * 2 * kPi * freq);
   };
   NativeCpml cpt;
-  if (cpml) setup_cpml(cpt, s, N, active, dt, dx);
+  if (cpml && dim == 3) setup_cpml(cpt, s, N, active, dt, dx);
   native_phys::Upml<T> upt;
-  if (upml) {
+  Pml2d<T> p2;
+  if (dim == 2 && cpml) setup_cpml2d(p2, s, N, active, present, dt, dx);
+  if (dim == 2 && upml) {
+    // per-cell 1 / (eps eps0) of a dielectric scene (E components; the
+    // 2-point averages of the plain coefficients above)
+    std::vector<T> inv[3];
+    if (percell) {
+      const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
+      for (int c = 0; c < 3; ++c) {
+        if (!present[c]) continue;
+        inv[c].resize(cells);
+        const int di = c == 0, dj = c == 1;
+        for (int i = 0; i < N[0]; ++i)
+          for (int j = 0; j < N[1]; ++j) {
+            const double a = sphere_eps(i + 0.5, j + 0.5, ctr[2], ctr, s.sphereRadius, s.sphereEps);
+            const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, ctr[2], ctr, s.sphereRadius, s.sphereEps);
+            inv[c][(size_t)i * N[1] + j] = (T)(1.0 / ((a + b) / 2.0 * kEps0));
+          }
+      }
+    }
+    setup_upml2d(p2, s, N, present, dt, dx, inv);
+  }
+  if (upml && dim == 3) {
     native_phys::UpmlScene sc;
     sc.pml[0] = s.pmlSizeX;
     sc.pml[1] = s.pmlSizeY;
@@ -718,13 +945,68 @@ int run(const fdtd::Settings& s) {
   int (*chain_fn)(const void* const*, const double*, const int*, int, int, int, int, void*) =
       sizeof(T) == 4 ? fdtd_chain3d_f32 : fdtd_chain3d_f64;
   NativeTfsf<T> tft;
-  if (tfsf && !setup_tfsf(tft, s, N, boxes, C, percell ? 1.0 : cb, percell ? 1.0 : db, dt, dx, freq)) return 1;
+  if (tfsf && !setup_tfsf(tft, s, N, boxes, C, percell ? 1.0 : cb, percell ? 1.0 : db, dt, dx, freq, dim, present))
+    return 1;
   const bool point_src = !tfsf || s.doUsePointSource;
   const int whole[6] = {0, 0, 0, N[0], N[1], N[2]};
   auto tfsf_kind = [&](int kind) {
     for (int c = 3 * kind; c < 3 * kind + 3; ++c)
       for (auto* l : tft.tab[c]) K_OK(tfsf_apply(F[c].p, *l, kind == 0 ? tft.hinc.p : tft.einc.p, whole, st));
   };
+
+  // 2D absorbing layers of one kind (0 = E) after / instead of the plain update
+  auto pml2d_cpml = [&](int kind) {
+    for (const Slab2d<T>& sl : p2.slabs) {
+      if ((sl.comp < 3) != (kind == 0)) continue;
+      const void* cp[4] = {nullptr, nullptr, nullptr, percell ? (const void*)C[sl.comp].p : nullptr};
+      K_OK(cpml_apply(F[sl.comp].p, F[sl.src].p, sl.psi, sl.axis, sl.sign, kind == 0 ? 1 : 0, sl.b, sl.c, sl.k,
+                      percell ? 1.0 : (kind == 0 ? cb : db), cp, N[1], N[2], sl.box, sl.pbox, st));
+    }
+  };
+  auto pml2d_upml = [&](int kind) {
+    for (int c = 3 * kind; c < 3 * kind + 3; ++c) {
+      if (!present[c]) continue;
+      const T* srcs[2];
+      int axes[2], signs[2], nt = 0;
+      for (int q = 0; q < 2; ++q) {
+        const int sc = kCurl[c][q][0], ax = kCurl[c][q][1];
+        if (!present[sc] || ax >= 2) continue;
+        srcs[nt] = F[sc].p;
+        axes[nt] = ax;
+        signs[nt++] = kCurl[c][q][2];
+      }
+      K_OK(curl_gen(p2.D[c][1], p2.D[c][0], srcs, axes, signs, nt, kind == 0 ? 1 : 0, p2.ca[c], p2.cbp[c], N[1],
+                    N[2], boxes + 6 * c, st));
+      const double sc3[3] = {1.0, p2.s[c], p2.s[c]};
+      const T* xs[3] = {F[c].p, p2.D[c][1], p2.D[c][0]};
+      K_OK(lincomb(F[c].p, 3, sc3, p2.lin[c], xs, N[1], N[2], boxes + 6 * c, st));
+      std::swap(p2.D[c][0], p2.D[c][1]);
+    }
+  };
+  // amplitude mode state: running maxima of every component, one [x][6][y][z]
+  // buffer (the layout of the blocked amplitude kernel), per-step changed
+  // counts, the Ez z-line source at (Nx/8, Ny/2, k outside the z PML) of 3D
+  // runs (Scheme3D.cpp:2995-3013)
+  bool amp_phase = false;
+  Dev<T> AMP;
+  Dev<unsigned> CNT;
+  Dev<long long> LINE;
+  int line_n = 0, line_k0 = 0;
+  const size_t plane = (size_t)N[1] * N[2];
+  if (amp) {
+    AMP.alloc((size_t)N[0] * 6 * plane);
+    CNT.alloc(std::max(1, s.amplitudeCheckSteps));
+    if (dim == 3 && point_src) {
+      line_k0 = s.doUsePML ? s.pmlSizeZ : 0;
+      std::vector<long long> offs;
+      for (int k = line_k0; k < N[2] - line_k0; ++k) offs.push_back(((long long)(N[0] / 8) * N[1] + N[1] / 2) * N[2] + k);
+      line_n = (int)offs.size();
+      if (line_n > 0) {
+        LINE.alloc(offs.size());
+        HIP_OK(hipMemcpy(LINE.p, offs.data(), offs.size() * sizeof(long long), hipMemcpyHostToDevice));
+      }
+    }
+  }
 
   // one time step (t) through the configured kernels
   auto step = [&](int t) {
@@ -757,7 +1039,12 @@ int run(const fdtd::Settings& s) {
                    N[0], N[1], N[2], boxes, 0, st, v4));
         }
         if (tfsf) tfsf_kind(0);
-        if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));
+        if (point_src) {
+          if (amp_phase && line_n > 0)  // the amplitude mode's Ez z-line replaces the point source
+            K_OK(setvs(F[2].p, LINE.p, line_n, sv, st));
+          else
+            K_OK(setv(F[src_comp].p, src_off, sv, st));
+        }
         if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
         if (upml) {
           fptrs();
@@ -773,16 +1060,32 @@ int run(const fdtd::Settings& s) {
         }
         if (tfsf) tfsf_kind(1);
       }
-    } else if (scheme == "tmz") {
-      K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], boxes + 12, st));
-      K_OK(setv(F[2].p, src_off, sv, st));
-      int hb[12];
-      std::memcpy(hb, boxes + 18, 12 * sizeof(int));
-      K_OK(tmz_h(F[3].p, F[4].p, F[2].p, C[3].p, C[4].p, percell ? 1.0 : db, N[0], N[1], hb, st));
-    } else if (scheme == "tez") {
-      K_OK(tez_e(F[0].p, F[1].p, F[5].p, C[0].p, C[1].p, percell ? 1.0 : cb, N[0], N[1], boxes, st));
-      K_OK(setv(F[5].p, src_off, sv, st));  // hard source between the E and H updates
-      K_OK(tez_h(F[5].p, F[0].p, F[1].p, C[5].p, percell ? 1.0 : db, N[0], N[1], boxes + 30, st));
+    } else if (scheme == "tmz" || scheme == "tez") {
+      // [incident line E] E update (+ CPML slabs | UPML chain) [TF/SF on E]
+      // [source] [incident line H] H update [TF/SF on H]
+      const bool tm = scheme == "tmz";
+      if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
+      if (upml)
+        pml2d_upml(0);
+      else if (tm)
+        K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], boxes + 12, st));
+      else
+        K_OK(tez_e(F[0].p, F[1].p, F[5].p, C[0].p, C[1].p, percell ? 1.0 : cb, N[0], N[1], boxes, st));
+      if (cpml) pml2d_cpml(0);
+      if (tfsf) tfsf_kind(0);
+      if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));  // hard source between the E and H updates
+      if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
+      if (upml) {
+        pml2d_upml(1);
+      } else if (tm) {
+        int hb[12];
+        std::memcpy(hb, boxes + 18, 12 * sizeof(int));
+        K_OK(tmz_h(F[3].p, F[4].p, F[2].p, C[3].p, C[4].p, percell ? 1.0 : db, N[0], N[1], hb, st));
+      } else {
+        K_OK(tez_h(F[5].p, F[0].p, F[1].p, C[5].p, percell ? 1.0 : db, N[0], N[1], boxes + 30, st));
+      }
+      if (cpml) pml2d_cpml(1);
+      if (tfsf) tfsf_kind(1);
     } else {
       K_OK(e1d(F[2].p, F[4].p, C[2].p, percell ? 1.0 : cb, boxes[12], boxes[15], st));
       K_OK(setv(F[2].p, src_off, sv, st));
@@ -812,7 +1115,8 @@ int run(const fdtd::Settings& s) {
   IBox hcore = {{0, 0, 0}, {0, 0, 0}};
   std::vector<IBox> hshell[8], hcopy;
   int T_h = 1;
-  if (scheme == "3d" && sizeof(T) == 4 && v4 && cpml && !percell && T_h_req > 1 && T_h_req <= fdtd_tb_max_steps()) {
+  if (scheme == "3d" && sizeof(T) == 4 && v4 && cpml && !percell && !amp && T_h_req > 1 &&
+      T_h_req <= fdtd_tb_max_steps()) {
     const int pml[3] = {s.pmlSizeX, s.pmlSizeY, s.pmlSizeZ};
     const int tfs[3] = {s.tfsfSizeX, s.tfsfSizeY, s.tfsfSizeZ};
     IBox K;
@@ -1003,6 +1307,92 @@ int run(const fdtd::Settings& s) {
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, st));
   run_steps(warm, steps - warm);
+  // amplitude mode (models/scheme.py perform_amplitude_steps): check periods
+  // of K steps whose changed-cell counts accumulate on the device, read once
+  // per period; the run ends with the period in which a step (after the
+  // first) changed no running maximum, or after --amplitude-time-steps steps
+  int t_end = steps, amp_taken = 0, amp_stable = -1;
+  if (amp) {
+    amp_phase = true;
+    const int K = std::max(1, s.amplitudeCheckSteps);
+    // amplitude box per component: its update box minus the PML cells
+    // (Scheme3D.cpp:3016-3030); only present components
+    int ab[36] = {}, na = 0;
+    const T* af[6];
+    T* aa[6];
+    for (int c = 0; c < 6; ++c) {
+      int* b = ab + 6 * c;
+      for (int q = 0; q < 6; ++q) b[q] = boxes[6 * c + q];
+      const int left[3] = {s.doUsePML ? s.pmlSizeX : 0, s.doUsePML ? s.pmlSizeY : 0, s.doUsePML ? s.pmlSizeZ : 0};
+      for (int a : active) {
+        const int right = N[a] - left[a];
+        if (left[a] == right) continue;
+        b[a] = std::max(b[a], (int)std::ceil(left[a] - kMinFP[c][a]));
+        b[3 + a] = std::min(b[3 + a], (int)std::ceil(right - kMinFP[c][a]));
+      }
+    }
+    int abp[36];
+    for (int c = 0; c < 6; ++c)
+      if (present[c]) {
+        af[na] = F[c].p;
+        aa[na] = AMP.p + c * plane;
+        std::memcpy(abp + 6 * na, ab + 6 * c, 6 * sizeof(int));
+        ++na;
+      }
+    // blocked passes with the amplitude update folded in (tb3d_mr.h AmpDev):
+    // 3D vacuum fp32 float4 rows, no absorbing layer / TF/SF / NTFF
+    const int Ta = (scheme == "3d" && sizeof(T) == 4 && v4 && !percell && !cpml && !upml && !tfsf && !ntff &&
+                    line_n > 0 && !s.doUseSplitKernels)
+                       ? 3
+                       : 1;
+    if (Ta > 1)
+      for (int c = 0; c < 6; ++c)
+        if (!G[c].p) G[c].alloc(cells);
+    std::vector<unsigned> got(K);
+    int t = steps;
+    bool done = false;
+    while (!done && amp_taken < s.numAmplitudeTimeSteps) {
+      const int n = std::min(K, s.numAmplitudeTimeSteps - amp_taken);
+      HIP_OK(hipMemsetAsync(CNT.p, 0, K * sizeof(unsigned), st));
+      int q = 0;
+      while (q < n) {
+        if (Ta > 1 && n - q >= 2) {
+          if constexpr (sizeof(T) == 4) {
+            const int k = std::min(Ta, n - q);
+            const T* ei[3] = {F[0].p, F[1].p, F[2].p};
+            const T* hi[3] = {F[3].p, F[4].p, F[5].p};
+            T* eo[3] = {G[0].p, G[1].p, G[2].p};
+            T* ho[3] = {G[3].p, G[4].p, G[5].p};
+            const int ob[6] = {0, 0, 0, N[0], N[1], N[2]};
+            const int src5[5] = {N[0] / 8, N[1] / 2, line_k0, 2, line_k0 + line_n};
+            double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
+            K_OK(fdtd_tb3d_amp_f32(ei, hi, eo, ho, cb, db, N[0], N[1], N[2], boxes, ob, 0, k, src5, vals, aa, ab,
+                                   0.001, CNT.p + q, st));
+            for (int c = 0; c < 6; ++c) std::swap(F[c].p, G[c].p);
+            for (int c = 0; c < 6; ++c) af[c] = F[c].p;
+            q += k;
+            t += k;
+            continue;
+          }
+        }
+        step(t);
+        K_OK(amp_many(af, aa, na, N[1], N[2], abp, (long long)(6 * plane), 0.001, CNT.p + q, st));
+        ++q;
+        ++t;
+      }
+      HIP_OK(hipMemcpyAsync(got.data(), CNT.p, n * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      for (int r = 0; r < n && !done; ++r)
+        if (got[r] == 0 && amp_taken + r + 1 > 1) {
+          amp_stable = amp_taken + r + 1;
+          done = true;
+        }
+      amp_taken += n;
+    }
+    amp_phase = false;
+    t_end = t;
+  }
   HIP_OK(hipEventRecord(e1, st));
   HIP_OK(hipEventSynchronize(e1));
   HIP_OK(hipGetLastError());
@@ -1018,8 +1408,8 @@ int run(const fdtd::Settings& s) {
     std::printf("Grid size: %dx%d\n", N[0], N[1]);
   else
     std::printf("Grid size: %d\n", N[0]);
-  const int timed = steps - warm;
-  std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", steps, timed, warm);
+  const int timed = steps - warm + amp_taken;
+  std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", t_end, timed, warm);
   std::printf("Value type: %s\n", Api<T>::name);
   std::printf("\n-------- Details --------\n");
   std::printf("Parallel grid: 0\n");
@@ -1036,6 +1426,12 @@ int run(const fdtd::Settings& s) {
   else
     std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
   std::printf("Throughput: %.1f Mcells/s\n", cells * (double)timed / sec / 1e6);
+  if (amp) {
+    if (amp_stable > 0)
+      std::printf("Amplitude mode: stable after %d steps (%d amplitude steps taken)\n", amp_stable, amp_taken);
+    else
+      std::printf("Amplitude mode: stable state not reached after %d steps\n", amp_taken);
+  }
   if (s.doPrintJson)
     std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f}\n", sec, timed,
                 cells * (double)timed / sec / 1e6);
@@ -1046,7 +1442,7 @@ int run(const fdtd::Settings& s) {
     for (int c = 0; c < 6; ++c) {
       if (!present[c]) continue;
       HIP_OK(hipMemcpy(host.data(), F[c].p, cells * sizeof(T), hipMemcpyDeviceToHost));
-      const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
+      const std::string base = fdtd::grid_file_name(t_end, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
       if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), cells * sizeof(T));
       if (s.saveAsBMP || !s.saveAsDAT) {
         // middle slice along z (3D) or the plane (2D) / line (1D)
@@ -1064,7 +1460,267 @@ int run(const fdtd::Settings& s) {
   return 0;
 }
 
+// ------------------------------------------------------------ multi-GPU
+// --parallel-grid: the 3D grid split into x slabs over P ranks, all driven
+// by this one process (rank r on device r % devices; --topology-sizex P, or
+// one rank per visible GPU).  x is the slowest axis, so a rank's T ghost
+// planes on each side are contiguous: no pack / unpack kernels, one
+// device-to-device (xGMI peer) copy per field and side.  Every T steps each
+// rank runs the temporally blocked kernel over its owned planes (reading the
+// T-deep ghosts, the pass's dependency cone), then pulls its neighbours'
+// fresh boundary planes on its own stream; events order the passes and the
+// pulls across streams (a rank's next pass waits for its neighbours' pulls
+// from the buffer it is about to overwrite).  Point-to-point and nearest-
+// neighbour only, the shape of the node's xGMI links.  Plain Yee media
+// (vacuum / dielectric sphere) with the point source; the reference's MPI
+// grid: Source/Grid/ParallelGrid.cpp:1600-1823 (exchange), :2161-2194.
+template <typename T>
+struct XRank {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr, copied = nullptr;
+  int lo = 0, hi = 0, gl = 0, gh = 0, x0 = 0, nx = 0;
+  Dev<T> F[6], G[6], C[6];
+  int boxes[36];
+};
+
+template <typename T>
+int run_multi(const fdtd::Settings& s) {
+  fdtd::Int3 N = {s.sizeX, s.sizeY, s.sizeZ};
+  const std::vector<int> active = {0, 1, 2};
+  const double dx = s.gridStep, courant = s.courantNum;
+  const double dt = dx * courant / kC;
+  const double freq = kC / s.sourceWaveLength;
+  const double cb = dt / (kEps0 * dx), db = dt / (kMu0 * dx);
+  const bool percell = s.scene != "vacuum";
+  int ndev = 0;
+  HIP_OK(hipGetDeviceCount(&ndev));
+  const int P = s.topologySizeX > 1 ? s.topologySizeX : ndev;
+  const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
+  const int TB = std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
+  if (sizeof(T) == 4 && N[2] % 4 != 0) {
+    std::fprintf(stderr, "fdtd3d (native): fp32 parallel grids need sizez %% 4 == 0 (float4 rows)\n");
+    return 2;
+  }
+  if (N[0] / P < TB) {
+    std::fprintf(stderr, "fdtd3d (native): %d x planes over %d ranks leave fewer than %d planes per rank\n", N[0], P,
+                 TB);
+    return 2;
+  }
+  const size_t plane = (size_t)N[1] * N[2];
+  std::vector<XRank<T>> R(P);
+  for (int r = 0, x = 0; r < P; ++r) {
+    XRank<T>& q = R[r];
+    q.dev = r % ndev;
+    q.lo = x;
+    q.hi = x + N[0] / P + (r < N[0] % P ? 1 : 0);
+    x = q.hi;
+    q.gl = r > 0 ? TB : 0;
+    q.gh = r < P - 1 ? TB : 0;
+    q.x0 = q.lo - q.gl;
+    q.nx = q.hi - q.lo + q.gl + q.gh;
+    HIP_OK(hipSetDevice(q.dev));
+    HIP_OK(hipStreamCreate(&q.st));
+    HIP_OK(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&q.copied, hipEventDisableTiming));
+    const size_t n = (size_t)q.nx * plane;
+    for (int c = 0; c < 6; ++c) {
+      q.F[c].alloc(n);
+      q.G[c].alloc(n);
+    }
+    // update boxes in local indices: the global range of each component
+    // clipped to the rank's planes (ghosts included)
+    for (int c = 0; c < 6; ++c) {
+      fdtd::Int3 glo, ghi;
+      fdtd::global_range(c, N, active, glo, ghi);
+      q.boxes[6 * c] = std::max(glo[0], q.x0) - q.x0;
+      q.boxes[6 * c + 3] = std::min(ghi[0], q.x0 + q.nx) - q.x0;
+      for (int a = 1; a < 3; ++a) {
+        q.boxes[6 * c + a] = glo[a];
+        q.boxes[6 * c + 3 + a] = ghi[a];
+      }
+    }
+    if (percell) {
+      // per-cell E coefficients of the dielectric sphere (2-point eps
+      // averages, as the single-rank path), H on the scalar db
+      const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
+      std::vector<T> host(n);
+      for (int c = 0; c < 3; ++c) {
+        const int di = c == 0, dj = c == 1, dk = c == 2;
+        for (int li = 0; li < q.nx; ++li)
+          for (int j = 0; j < N[1]; ++j)
+            for (int k = 0; k < N[2]; ++k) {
+              const int i = q.x0 + li;
+              const double a = sphere_eps(i + 0.5, j + 0.5, k + 0.5, ctr, s.sphereRadius, s.sphereEps);
+              const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, k + dk + 0.5, ctr, s.sphereRadius, s.sphereEps);
+              host[((size_t)li * N[1] + j) * N[2] + k] = (T)(cb * 2.0 / (a + b));
+            }
+        q.C[c].alloc(n);
+        HIP_OK(hipMemcpy(q.C[c].p, host.data(), n * sizeof(T), hipMemcpyHostToDevice));
+      }
+    }
+  }
+  // peer access between neighbouring devices (xGMI)
+  for (int r = 0; r + 1 < P; ++r)
+    if (R[r].dev != R[r + 1].dev) {
+      for (int d = 0; d < 2; ++d) {
+        const int a = R[r + d].dev, b = R[r + 1 - d].dev;
+        int ok = 0;
+        HIP_OK(hipDeviceCanAccessPeer(&ok, a, b));
+        if (ok) {
+          HIP_OK(hipSetDevice(a));
+          const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
+        }
+      }
+    }
+  (void)hipGetLastError();
+  const fdtd::Int3 sp = {N[0] / 2, N[1] / 2, N[2] / 2};
+  auto src_val = [&](int t) {
+    if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
+    return std::sin(dt * t * 2 * kPi * freq);
+  };
+  bool first = true;
+  // k steps on every rank, then the ghost pulls
+  auto pass = [&](int t, int k) {
+    for (int r = 0; r < P; ++r) {
+      XRank<T>& q = R[r];
+      HIP_OK(hipSetDevice(q.dev));
+      if (!first) {
+        // the neighbours' pulls from this rank's (old) F are done before the
+        // pass overwrites it as its output buffer
+        if (r > 0) HIP_OK(hipStreamWaitEvent(q.st, R[r - 1].copied, 0));
+        if (r < P - 1) HIP_OK(hipStreamWaitEvent(q.st, R[r + 1].copied, 0));
+      }
+      const T* ei[3] = {q.F[0].p, q.F[1].p, q.F[2].p};
+      const T* hi[3] = {q.F[3].p, q.F[4].p, q.F[5].p};
+      T* eo[3] = {q.G[0].p, q.G[1].p, q.G[2].p};
+      T* ho[3] = {q.G[3].p, q.G[4].p, q.G[5].p};
+      const T* cbs[3] = {q.C[0].p, q.C[1].p, q.C[2].p};
+      const T* dbs[3] = {nullptr, nullptr, nullptr};
+      const bool own = sp[0] >= q.lo && sp[0] < q.hi;
+      const int src[4] = {sp[0] - q.x0, sp[1], sp[2], own ? 2 : -1};
+      double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
+      const int ob[6] = {q.lo - q.x0, 0, 0, q.hi - q.x0, N[1], N[2]};
+      if constexpr (sizeof(T) == 4)
+        K_OK(fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.nx, N[1], N[2], q.boxes, ob, 0, k,
+                              src, vals, q.st));
+      else
+        K_OK(fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.nx, N[1], N[2], q.boxes, ob, 0, k, src,
+                           vals, q.st));
+      for (int c = 0; c < 6; ++c) std::swap(q.F[c].p, q.G[c].p);
+      HIP_OK(hipEventRecord(q.done, q.st));
+    }
+    for (int r = 0; r < P; ++r) {
+      XRank<T>& q = R[r];
+      HIP_OK(hipSetDevice(q.dev));
+      for (int side = 0; side < 2; ++side) {
+        const int nb = side == 0 ? r - 1 : r + 1;
+        if (nb < 0 || nb >= P) continue;
+        const XRank<T>& o = R[nb];
+        HIP_OK(hipStreamWaitEvent(q.st, o.done, 0));
+        // low ghosts <- the lower neighbour's top T owned planes; high ghosts
+        // <- the upper neighbour's bottom T owned planes
+        const int src_x = side == 0 ? o.hi - TB : o.lo;
+        const int dst_x = side == 0 ? q.lo - TB : q.hi;
+        const size_t bytes = (size_t)TB * plane * sizeof(T);
+        for (int c = 0; c < 6; ++c) {
+          T* dst = q.F[c].p + (size_t)(dst_x - q.x0) * plane;
+          const T* srcp = o.F[c].p + (size_t)(src_x - o.x0) * plane;
+          if (o.dev == q.dev)
+            HIP_OK(hipMemcpyAsync(dst, srcp, bytes, hipMemcpyDeviceToDevice, q.st));
+          else
+            HIP_OK(hipMemcpyPeerAsync(dst, q.dev, srcp, o.dev, bytes, q.st));
+        }
+      }
+      HIP_OK(hipEventRecord(q.copied, q.st));
+    }
+    first = false;
+  };
+  auto advance = [&](int t0, int n) {
+    int t = t0;
+    while (n > 0) {
+      const int k = std::min(TB, n);
+      pass(t, k);
+      t += k;
+      n -= k;
+    }
+  };
+  auto sync_all = [&]() {
+    for (int r = 0; r < P; ++r) {
+      HIP_OK(hipSetDevice(R[r].dev));
+      HIP_OK(hipStreamSynchronize(R[r].st));
+    }
+  };
+  const int steps = s.numTimeSteps;
+  const int warm = std::max(0, std::min(s.warmupSteps, steps));
+  advance(0, warm);
+  sync_all();
+  const auto c0 = std::chrono::steady_clock::now();
+  advance(warm, steps - warm);
+  sync_all();
+  HIP_OK(hipGetLastError());
+  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+  const double cells = (double)N[0] * N[1] * N[2];
+  const int timed = steps - warm;
+  std::printf("Total time = %f seconds\n", sec);
+  std::printf("Dimension: 3\n");
+  std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);
+  std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", steps, timed, warm);
+  std::printf("Value type: %s\n", Api<T>::name);
+  std::printf("\n-------- Details --------\n");
+  std::printf("Parallel grid: 1\n");
+  std::printf("Number of processes: %d (ranks of one process on %d device%s)\n", P, std::min(P, ndev),
+              std::min(P, ndev) > 1 ? "s" : "");
+  std::printf("Parallel grid scheme: X (topology %dx1x1)\n", P);
+  std::printf("Buffer size: %d\n", TB);
+  std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), x-slab ghost planes by peer copies\n",
+              TB);
+  std::printf("Throughput: %.1f Mcells/s\n", cells * timed / sec / 1e6);
+  if (s.doPrintJson)
+    std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f, \"ranks\": %d}\n", sec, timed,
+                cells * timed / sec / 1e6, P);
+  if (s.doSaveRes) {
+    const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
+    std::vector<T> host((size_t)N[0] * plane);
+    for (int c = 0; c < 6; ++c) {
+      for (int r = 0; r < P; ++r) {
+        const XRank<T>& q = R[r];
+        HIP_OK(hipSetDevice(q.dev));
+        HIP_OK(hipMemcpy(host.data() + (size_t)q.lo * plane, q.F[c].p + (size_t)q.gl * plane,
+                         (size_t)(q.hi - q.lo) * plane * sizeof(T), hipMemcpyDeviceToHost));
+      }
+      const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
+      if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), host.size() * sizeof(T));
+      if (s.saveAsBMP || !s.saveAsDAT) {
+        const int kz = N[2] / 2;
+        std::vector<double> v((size_t)N[0] * N[1]);
+        for (int i = 0; i < N[0]; ++i)
+          for (int j = 0; j < N[1]; ++j) v[(size_t)i * N[1] + j] = host[((size_t)i * N[1] + j) * N[2] + kz];
+        fdtd::write_bmp(base + std::to_string(kz) + "-Re.bmp", v, N[0], N[1], s.dumperPalette);
+      }
+    }
+  }
+  for (auto& q : R) {
+    HIP_OK(hipSetDevice(q.dev));
+    for (int c = 0; c < 6; ++c) {
+      q.F[c].~Dev<T>();
+      new (&q.F[c]) Dev<T>();
+      q.G[c].~Dev<T>();
+      new (&q.G[c]) Dev<T>();
+      q.C[c].~Dev<T>();
+      new (&q.C[c]) Dev<T>();
+    }
+    HIP_OK(hipEventDestroy(q.done));
+    HIP_OK(hipEventDestroy(q.copied));
+    HIP_OK(hipStreamDestroy(q.st));
+  }
+  return 0;
+}
+
 }  // namespace
+
 
 int main(int argc, char** argv) {
   fdtd::Settings s;
@@ -1081,26 +1737,36 @@ int main(int argc, char** argv) {
     std::fprintf(stdout, "ERROR: %s\n", s.message.c_str());
     return 1;
   }
-  // CPML absorbing layers: 3D fp32 with whole float4 z rows (the folded float4 kernels)
-  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && !s.doUseMetamaterials && s.dimension == 3 &&
-                       s.valueType == "f32" && s.sizeZ % 4 == 0;
-  // UPML (D/B chain) and Drude / Lorentz spheres: 3D, any precision
-  const bool upml_ok = s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials) && s.dimension == 3;
+  // CPML absorbing layers: 3D fp32 with whole float4 z rows (the folded
+  // float4 kernels), 2D in either precision (generic slab kernels)
+  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && !s.doUseMetamaterials &&
+                       ((s.dimension == 3 && s.valueType == "f32" && s.sizeZ % 4 == 0) || s.dimension == 2);
+  // UPML (D/B chain) and Drude / Lorentz spheres: 3D, any precision; the 2D UPML without dispersive media
+  const bool upml_ok = s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials) &&
+                       (s.dimension == 3 || (s.dimension == 2 && !s.doUseMetamaterials));
   const bool meta_ok = !s.doUseMetamaterials || (s.dimension == 3 && s.scene == "drude-sphere");
-  // TF/SF plane waves: 3D (any precision), with the CPML or the UPML; with the
-  // UPML the corrections take the E form, exact where every sigma vanishes:
-  // the TF/SF box must lie inside the absorbing layers' interior
-  bool tfsf_ok = s.doUseTFSF && s.dimension == 3;
+  // TF/SF plane waves: 3D and 2D (any precision), with the CPML or the UPML;
+  // with the UPML the corrections take the E form, exact where every sigma
+  // vanishes: the TF/SF box must lie inside the absorbing layers' interior
+  bool tfsf_ok = s.doUseTFSF && s.dimension >= 2;
   if (tfsf_ok && s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials))
-    tfsf_ok = s.tfsfSizeX > s.pmlSizeX + 1 && s.tfsfSizeY > s.pmlSizeY + 1 && s.tfsfSizeZ > s.pmlSizeZ + 1;
+    tfsf_ok = s.tfsfSizeX > s.pmlSizeX + 1 && s.tfsfSizeY > s.pmlSizeY + 1 &&
+              (s.dimension == 2 || s.tfsfSizeZ > s.pmlSizeZ + 1);
   const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
-  if ((s.doUsePML && !cpml_ok && !upml_ok) || (s.doUseTFSF && !tfsf_ok) || !meta_ok || !ntff_ok ||
-      s.doUseAmplitudeMode || s.doUseComplexFieldValues || s.doUseParallelGrid || s.doUseDoubleMaterialPrecision ||
-      !s.loadFromFile.empty()) {
+  // amplitude mode: any scheme, not with the NTFF diagram
+  const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
+  // parallel grids: 3D plain media (vacuum / dielectric sphere) with the point source, x slabs
+  const bool par_ok = !s.doUseParallelGrid ||
+                      (s.dimension == 3 && !s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials &&
+                       !s.doUseAmplitudeMode && !s.doUseNTFF && (s.scene == "vacuum" || s.scene == "sphere") &&
+                       s.topologySizeY <= 1 && s.topologySizeZ <= 1 && !s.doUseSplitKernels);
+  if ((s.doUsePML && !cpml_ok && !upml_ok) || (s.doUseTFSF && !tfsf_ok) || !meta_ok || !ntff_ok || !amp_ok ||
+      !par_ok || s.doUseComplexFieldValues || s.doUseDoubleMaterialPrecision || !s.loadFromFile.empty()) {
     std::fprintf(stderr,
-                 "fdtd3d (native): CPML outside 3D fp32 float4 rows, PML / TF/SF / NTFF outside 3D, TF/SF boxes "
-                 "reaching the UPML, metamaterials outside the drude-sphere scene, amplitude mode, complex fields, "
-                 "parallel grids and resume run through the Python driver: python -m fdtd3d_amd <same options>\n");
+                 "fdtd3d (native): CPML in 3D outside fp32 float4 rows, PML / TF/SF in 1D, TF/SF boxes reaching "
+                 "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "
+                 "grids beyond 3D plain media split along x, complex fields and resume run through the Python "
+                 "driver: python -m fdtd3d_amd <same options>\n");
     return 2;
   }
   int ndev = 0;
@@ -1109,6 +1775,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "no HIP device\n");
     return 1;
   }
+  if (s.doUseParallelGrid) return s.valueType == "f32" ? run_multi<float>(s) : run_multi<double>(s);
   HIP_OK(hipSetDevice(0 % (s.numCudaGPUs > 0 ? s.numCudaGPUs : 1)));
   return s.valueType == "f32" ? run<float>(s) : run<double>(s);
 }

@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "capi.h"
 #include "host_native.h"
 
 namespace native_phys {
@@ -260,9 +261,10 @@ void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt,
 template <typename T>
 int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int nz, void* stream,
               int (*chain)(const void* const*, const double*, const int*, int, int, int, int, void*)) {
+  if (fdtd_chain_ints_per_comp() != 25 || fdtd_chain_ptrs_per_comp() != 24) return (int)hipErrorInvalidValue;
   const void* P[72] = {};
   double S[6] = {};
-  int I[57] = {};
+  int I[75] = {};  // 25 per component (chain_kernels.hip CI_PER); plain and storage boxes empty
   int drude = 0;
   for (int cc = 0; cc < 3; ++cc) {
     const int c = 3 * kind + cc;
@@ -287,7 +289,7 @@ int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int n
     p[22] = U.lut[c];
     S[2 * cc] = U.s[c];
     S[2 * cc + 1] = 1.0;
-    int* in = I + 19 * cc;
+    int* in = I + 25 * cc;
     in[0] = kCurlT[c][0][1];
     in[1] = kCurlT[c][1][1];
     in[2] = kCurlT[c][0][2];

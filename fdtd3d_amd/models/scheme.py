@@ -1568,7 +1568,7 @@ class YeeScheme(BlockedStepping):
         n = self.cfg.time_steps if n is None else n
         self.advance(n)
         if self.cfg.use_amp_mode:
-            self.perform_amplitude_steps()
+            self.amplitude_taken = self.perform_amplitude_steps()
 
     # ------------------------------------------------------------ amplitude
     def amplitude_box(self, c: str) -> Box:

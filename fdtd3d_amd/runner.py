@@ -218,7 +218,7 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
 
     warm = min(max(0, settings.warmupSteps), steps)
     if warm:
-        scheme.perform_steps(warm)
+        scheme.advance(warm)  # regular steps only: amplitude mode follows the timed ones
         steps -= warm
     sync()
     scheme.prof.reset()  # phase timings cover the timed steps only
@@ -228,7 +228,9 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
             from .models.blocking import PassTimer
             scheme.pass_timer = PassTimer(scheme.device)
     t0 = time.perf_counter()
+    t_start = scheme.t
     scheme.perform_steps(steps)
+    steps = scheme.t - t_start  # amplitude mode: its steps count as timed steps too
     if halo is not None:
         halo.drain(scheme)
     sync()
@@ -246,6 +248,13 @@ def run(argv: Optional[List[str]] = None, out=sys.stdout) -> int:
         scheme.pass_timer = None
     if rank == 0:
         mc = _report(settings, scheme, seconds, world, core, steps, out)
+        if scheme.cfg.use_amp_mode:
+            taken = getattr(scheme, "amplitude_taken", 0)
+            if getattr(scheme, "amplitude_converged", False):
+                out.write("Amplitude mode: stable after %d steps (%d amplitude steps taken)\n"
+                          % (scheme.amplitude_stable_step, taken))
+            else:
+                out.write("Amplitude mode: stable state not reached after %d steps\n" % taken)
         if phases:
             out.write(scheme.prof.report() + "\n")
         if settings.doPrintJson:

@@ -83,13 +83,16 @@ def test_native_executable_cli(host):
     assert r.returncode == 0 and "Version" in r.stdout
     r = subprocess.run([exe, "--no-such-flag"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2
-    r = subprocess.run([exe, "--2d", "--use-tfsf"], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([exe, "--1d", "--use-tfsf"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "python -m fdtd3d_amd" in r.stderr
-    # CPML runs natively in 3D fp32 only, the UPML / Drude chain and NTFF in 3D; fp64 CPML, 2D absorbing
-    # layers, metamaterials outside the drude-sphere scene and amplitude mode go to the Python driver
-    for argv in (["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f64"],
-                 ["--2d", "--use-pml", "--pml-type", "cpml"], ["--2d", "--use-pml"], ["--2d", "--use-ntff"],
-                 ["--3d", "--use-metamaterials", "--use-pml", "--scene", "reference"], ["--3d", "--use-amp-mode"],
+    # CPML runs natively in 3D fp32 and in 2D, the UPML in 3D and 2D, the Drude chain and NTFF in 3D, parallel
+    # grids for 3D plain media; fp64 3D CPML, 2D metamaterials, metamaterials outside the drude-sphere scene,
+    # amplitude mode with NTFF and parallel grids with physics go to the Python driver
+    for argv in (["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f64"], ["--2d", "--use-ntff"],
+                 ["--2d", "--use-pml", "--use-metamaterials"],
+                 ["--3d", "--use-metamaterials", "--use-pml", "--scene", "reference"],
+                 ["--3d", "--use-amp-mode", "--use-ntff"], ["--3d", "--parallel-grid", "--use-pml"],
+                 ["--2d", "--parallel-grid"],
                  ["--3d", "--use-pml", "--use-tfsf", "--pml-sizex", "10", "--tfsf-sizex", "8"]):
         r = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=60)
         assert r.returncode == 2 and "python -m fdtd3d_amd" in r.stderr, argv

@@ -79,8 +79,37 @@ CASES = {
                              "0.7", "--use-pml", "--pml-sizex", "5", "--same-size-pml", "--sphere-center-x", "20",
                              "--sphere-center-y", "20", "--sphere-center-z", "20", "--sphere-radius", "6",
                              "--use-tfsf", "--tfsf-sizex", "9", "--same-size-tfsf"],
+    # 2D absorbing layers and TF/SF (generic slab / chain kernels, csrc/main.cpp Pml2d): the reference's
+    # UPML with an oblique plane wave, the CPML with kappa / alpha, dielectric cylinders (per-cell coefficients)
+    "2d_tmz_upml_tfsf": ["--2d", "--sizex", "60", "--sizey", "52", "--time-steps", "30", "--scene", "vacuum",
+                         "--use-pml", "--pml-sizex", "6", "--pml-sizey", "5", "--use-tfsf", "--tfsf-sizex", "10",
+                         "--tfsf-sizey", "9", "--angle-phi", "30"],
+    "2d_tez_cpml": ["--2d", "--2d-mode", "tez", "--sizex", "60", "--sizey", "52", "--time-steps", "30",
+                    "--scene", "vacuum", "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6", "--pml-sizey", "7",
+                    "--cpml-kappa-max", "2", "--cpml-alpha-max", "0.05"],
+    "2d_tmz_cpml_tfsf_sphere": ["--2d", "--sizex", "64", "--sizey", "56", "--time-steps", "30", "--scene", "sphere",
+                                "--sphere-center-x", "32", "--sphere-center-y", "28", "--sphere-radius", "7",
+                                "--sphere-eps", "3", "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6",
+                                "--same-size-pml", "--use-tfsf", "--tfsf-sizex", "11", "--tfsf-sizey", "10",
+                                "--angle-phi", "20", "--angle-psi", "90"],
+    "2d_tez_upml_sphere": ["--2d", "--2d-mode", "tez", "--sizex", "56", "--sizey", "60", "--time-steps", "30",
+                           "--scene", "sphere", "--sphere-center-x", "28", "--sphere-center-y", "30",
+                           "--sphere-radius", "6", "--sphere-eps", "4", "--use-pml", "--pml-sizex", "5",
+                           "--pml-sizey", "6"],
+    # amplitude mode: 3D vacuum (fp32: blocked passes with the running maxima folded in), CPML (per step),
+    # 2D with the CPML until the stable state (fp64: the same converged step as the Python driver)
+    "3d_amp": ["--3d", "--sizex", "32", "--sizey", "28", "--sizez", "24", "--time-steps", "6", "--scene", "vacuum",
+               "--use-amp-mode", "--amplitude-time-steps", "20"],
+    "3d_amp_cpml": ["--3d", "--sizex", "32", "--sizey", "28", "--sizez", "24", "--time-steps", "5", "--scene",
+                    "vacuum", "--use-amp-mode", "--amplitude-time-steps", "13", "--use-pml", "--pml-type", "cpml",
+                    "--pml-sizex", "5", "--same-size-pml"],
+    "2d_tmz_amp_cpml": ["--2d", "--sizex", "60", "--sizey", "52", "--time-steps", "10", "--scene", "vacuum",
+                        "--use-amp-mode", "--amplitude-time-steps", "300", "--use-pml", "--pml-type", "cpml"],
 }
-FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf", "3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid"}
+FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf", "3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid",
+             "3d_amp_cpml"}
+# the converged step depends on running-maximum comparisons at round-off level: fp64 only
+FP64_ONLY = {"2d_tmz_amp_cpml"}
 
 COMPS = {"3d": ["Ex", "Ey", "Ez", "Hx", "Hy", "Hz"], "tmz": ["Ez", "Hx", "Hy"], "tez": ["Ex", "Ey", "Hz"],
          "1d": ["Ez", "Hy"]}
@@ -106,6 +135,8 @@ def test_native_driver_matches_python(case, dtype, tmp_path, gpu):
     assert os.path.exists(exe), "native fdtd3d executable missing (run python -m fdtd3d_amd.ops.build)"
     if case in FP32_ONLY and dtype != "f32":
         pytest.skip("native CPML: fp32 float4 kernels")
+    if case in FP64_ONLY and dtype != "f64":
+        pytest.skip("converged amplitude step compared in fp64")
     argv = CASES[case] + ["--dtype", dtype, "--save-res", "--save-as-dat"]
     nd, pd = tmp_path / "native", tmp_path / "py"
     nd.mkdir()
@@ -114,10 +145,18 @@ def test_native_driver_matches_python(case, dtype, tmp_path, gpu):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Mcells/s" in r.stdout
     assert ("hybrid passes" in r.stdout) == case.endswith("_hybrid"), r.stdout
+    pbuf = io.StringIO()
     assert py_run(argv[:-4] + ["--dtype", "f64", "--save-res", "--save-as-dat", "--backend", "torch",
-                               "--device", "cpu", "--output-dir", str(pd)], out=io.StringIO()) == 0
+                               "--device", "cpu", "--output-dir", str(pd)], out=pbuf) == 0
     shape, scheme = _shape(argv)
     steps = int(argv[argv.index("--time-steps") + 1])
+    if "--use-amp-mode" in argv:
+        # the same amplitude steps (and converged step) in both drivers
+        na = [l for l in r.stdout.splitlines() if l.startswith("Amplitude mode:")]
+        pa = [l for l in pbuf.getvalue().splitlines() if l.startswith("Amplitude mode:")]
+        assert na and na == pa, (na, pa)
+        steps += int(na[0].split("after ")[1].split()[0]) if "not reached" in na[0] else \
+            int(na[0].split("(")[1].split()[0])
     ndt = np.float32 if dtype == "f32" else np.float64
     errs = {}
     for c in COMPS[scheme]:
@@ -168,3 +207,52 @@ def test_native_ntff_matches_python(dtype, gpu):
     tol = 1e-9 if dtype == "f64" else 2e-4
     for (h, x), (_, y) in zip(a, b):
         assert abs(x - y) <= tol * peak, (h, x, y, peak)
+
+
+# x-slab parallel grids of the native driver (csrc/main.cpp run_multi): 3 / 4 ranks of one process on one
+# GPU (ghost planes by device copies; peer xGMI copies on a multi-GPU node), 23 steps = 4 passes + a tail
+MULTI = {
+    "f32_vacuum_3ranks": ["--3d", "--sizex", "40", "--sizey", "24", "--sizez", "32", "--time-steps", "23",
+                          "--scene", "vacuum", "--parallel-grid", "--topology-sizex", "3", "--dtype", "f32"],
+    "f64_sphere_4ranks": ["--3d", "--sizex", "36", "--sizey", "20", "--sizez", "24", "--time-steps", "23",
+                          "--scene", "sphere", "--sphere-center-x", "17", "--sphere-center-y", "10",
+                          "--sphere-center-z", "12", "--sphere-radius", "5", "--sphere-eps", "3", "--parallel-grid",
+                          "--topology-sizex", "4", "--time-block", "3", "--dtype", "f64"],
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(MULTI))
+def test_native_parallel_grid_matches_python(case, tmp_path, gpu):
+    exe = native.executable()
+    argv = MULTI[case] + ["--save-res", "--save-as-dat"]
+    nd, pd = tmp_path / "native", tmp_path / "py"
+    nd.mkdir()
+    pd.mkdir()
+    r = subprocess.run([exe] + argv + ["--output-dir", str(nd)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Parallel grid: 1" in r.stdout and "x-slab ghost planes" in r.stdout, r.stdout
+    ranks = int(argv[argv.index("--topology-sizex") + 1])
+    assert "Number of processes: %d" % ranks in r.stdout
+    serial = [a for a in argv if a not in ("--parallel-grid",)]
+    i = serial.index("--topology-sizex")
+    serial = serial[:i] + serial[i + 2:]
+    i = serial.index("--dtype")
+    dtype = serial[i + 1]
+    serial = serial[:i] + serial[i + 2:]
+    assert py_run(serial + ["--dtype", "f64", "--backend", "torch", "--device", "cpu", "--output-dir", str(pd)],
+                  out=io.StringIO()) == 0
+    shape, _ = _shape(argv)
+    ndt = np.float32 if dtype == "f32" else np.float64
+    for kind in "EH":
+        errs = []
+        for c in ("x", "y", "z"):
+            name = "current[23]_rank-0_%s%s.dat" % (kind, c)
+            a = np.fromfile(nd / name, dtype=ndt).astype(np.float64).reshape(shape)
+            b = np.fromfile(pd / name, dtype=np.float64).reshape(shape)
+            errs.append((np.abs(a - b).max(), np.abs(b).max()))
+        peak = max(e[1] for e in errs)
+        assert peak > 0
+        tol = 1e-11 if dtype == "f64" else 2e-5
+        for err, _ in errs:
+            assert err <= tol * peak, (kind, err, peak)
