@@ -1598,8 +1598,10 @@ int run_multi(const fdtd::Settings& s) {
       T* ho[3] = {q.G[3].p, q.G[4].p, q.G[5].p};
       const T* cbs[3] = {q.C[0].p, q.C[1].p, q.C[2].p};
       const T* dbs[3] = {nullptr, nullptr, nullptr};
-      const bool own = sp[0] >= q.lo && sp[0] < q.hi;
-      const int src[4] = {sp[0] - q.x0, sp[1], sp[2], own ? 2 : -1};
+      // every rank whose planes (ghosts included) hold the source plane sets
+      // the hard source: a neighbour's redundant ghost-plane levels need it
+      const bool has = sp[0] >= q.x0 && sp[0] < q.x0 + q.nx;
+      const int src[4] = {sp[0] - q.x0, sp[1], sp[2], has ? 2 : -1};
       double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
       const int ob[6] = {q.lo - q.x0, 0, 0, q.hi - q.x0, N[1], N[2]};

@@ -210,7 +210,8 @@ def test_native_ntff_matches_python(dtype, gpu):
 
 
 # x-slab parallel grids of the native driver (csrc/main.cpp run_multi): 3 / 4 ranks of one process on one
-# GPU (ghost planes by device copies; peer xGMI copies on a multi-GPU node), 23 steps = 4 passes + a tail
+# GPU (ghost planes by device copies; peer xGMI copies on a multi-GPU node), 23 steps = passes + a tail;
+# the 4-rank case puts the source on a rank's first plane (its lower neighbour's ghosts hold it too)
 MULTI = {
     "f32_vacuum_3ranks": ["--3d", "--sizex", "40", "--sizey", "24", "--sizez", "32", "--time-steps", "23",
                           "--scene", "vacuum", "--parallel-grid", "--topology-sizex", "3", "--dtype", "f32"],
