@@ -106,6 +106,7 @@ class SchemeConfig:
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
     hybrid_tfsf: str = "auto"                # hybrid + TF/SF: faces in the blocked core ("core"), the shell, or auto
+    shell_streams: int = 0                   # hybrid shell: streams for the independent window launches (0 auto)
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
@@ -141,7 +142,7 @@ class SchemeConfig:
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
             amplitude_check_steps=s.amplitudeCheckSteps,
-            hybrid_block=s.hybridBlock, hybrid_tfsf=s.hybridTfsf,
+            hybrid_block=s.hybridBlock, hybrid_tfsf=s.hybridTfsf, shell_streams=s.shellStreams,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
@@ -981,15 +982,15 @@ class YeeScheme(BlockedStepping):
             self._update_chain_regions(kind, p, None if self.halo is None else self._window(kind), tfsf_here,
                                        plain_windows=windows)
             windows = []
-        for w in windows:
+        def one(w):
             if chain:
                 self._update_chain_regions(kind, p, w, tfsf_here)
-                continue
+                return
             boxes = {c: self.local_box(c, w) for c in comps}
             if self.use_upml_chain:
                 for c in comps:
                     self._upml_region(kind, c, p, boxes[c])
-                continue
+                return
             if self.use_cpml and getattr(self.ops, "fused_cpml_ok", lambda *a: False)(self):
                 # CPML folded into the update kernel (yee3d_cpml.hip)
                 self.ops.curl_update_cpml(kind, boxes, F, F, self.cb, self.cpml.kernel_table(kind, p))
@@ -1002,6 +1003,14 @@ class YeeScheme(BlockedStepping):
                 for c in comps:
                     for tab in self.tfsf[c]:
                         self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
+
+        if len(windows) > 1 and not tfsf_here and self.hybrid is not None:
+            # the hybrid shell's windows are disjoint: their launches of a half
+            # step are independent and run side by side on several streams
+            self._par_launches([(lambda w=w: one(w)) for w in windows])
+        else:
+            for w in windows:
+                one(w)
         if use_tfsf and tfsf_once:
             inc = self.hinc[p] if kind == "E" else self.einc[p]
             alloc = self.domain.allocated_global()
@@ -1022,6 +1031,38 @@ class YeeScheme(BlockedStepping):
             for c in comps:
                 self._upml_rotate(c, p)
 
+    def _par_launches(self, fns) -> None:
+        """Run independent launch callables round-robin on ``--shell-streams``
+        HIP streams (the current one first), joined back into the current
+        stream: the tail of one small window launch overlaps the next instead
+        of idling CUs.  Serial runs on the HIP path only."""
+        n = int(getattr(self.cfg, "shell_streams", 0))
+        if n <= 0:
+            n = 3 if self.ops.name == "hip" else 1
+        if n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda":
+            for f in fns:
+                f()
+            return
+        main = torch.cuda.current_stream(self.device)
+        pool = self.__dict__.get("_shell_pool")
+        if pool is None or len(pool) < n - 1:
+            pool = self._shell_pool = [torch.cuda.Stream(device=self.device) for _ in range(n - 1)]
+        pool = pool[:n - 1]
+        used = set()
+        for q, f in enumerate(fns):
+            k = q % n
+            if k == 0:
+                f()
+                continue
+            s = pool[k - 1]
+            if k not in used:
+                s.wait_stream(main)
+                used.add(k)
+            with torch.cuda.stream(s):
+                f()
+        for k in used:
+            main.wait_stream(pool[k - 1])
+
     def _update_chain_regions(self, kind: str, p: int, w: Optional[Box], tfsf_plain: bool = True,
                               plain_windows: Optional[Sequence[Box]] = None) -> None:
         """UPML/Drude step on window ``w``: plain float4 Yee kernels on the
@@ -1039,18 +1080,29 @@ class YeeScheme(BlockedStepping):
             # the launch list of this (kind, window set) is static: built once
             # (the hybrid shell steps through T window sets every pass)
             plan = cache[key] = self._chain_plan(kind, w, pws)
-        for boxes in plan["plain"]:
-            self.ops.curl_update(kind, boxes, F, F, self.cb)
+        fns = [(lambda boxes=boxes: self.ops.curl_update(kind, boxes, F, F, self.cb)) for boxes in plan["plain"]]
+        slow_all = []
         for launches, slow in plan["chain"]:
             for sel, form, plain_form, fold, rows in launches:
                 if rows is not None:
-                    self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form, cb=self.cb, rows=rows)
+                    fns.append(lambda sel=sel, form=form, pf=plain_form, rows=rows: self.ops.chain_update(
+                        kind, sel, F, self.upml, p, form, pf, cb=self.cb, rows=rows))
                 elif fold is None:
-                    self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form)
+                    fns.append(lambda sel=sel, form=form, pf=plain_form: self.ops.chain_update(
+                        kind, sel, F, self.upml, p, form, pf))
                 else:
-                    self.ops.chain_update(kind, sel, F, self.upml, p, form, plain_form, plain=fold, cb=self.cb)
-            for c, b in slow:
-                self._upml_region(kind, c, p, b)
+                    fns.append(lambda sel=sel, form=form, pf=plain_form, fold=fold: self.ops.chain_update(
+                        kind, sel, F, self.upml, p, form, pf, plain=fold, cb=self.cb))
+            slow_all += slow
+        if plain_windows is not None and self.hybrid is not None and not slow_all:
+            # hybrid shell: plain slabs and chain boxes are disjoint -- their
+            # launches run side by side on several streams
+            self._par_launches(fns)
+        else:
+            for f in fns:
+                f()
+        for c, b in slow_all:
+            self._upml_region(kind, c, p, b)
         if tfsf and tfsf_plain:
             # corrections on every plain box (folded ones included), after all updates
             for boxes in plan["plain"] + plan["folded"]:

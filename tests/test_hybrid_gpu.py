@@ -44,6 +44,12 @@ CASES = [
      2, 7),
     ("tmz-upml-point-f64", dict(scheme="tmz", size=(150, 90, 1), pml_size=(8, 8, 1), scene="vacuum", use_pml=True,
                                 dtype="f64"), 6, 19),
+    # the shell's window launches run on several streams (--shell-streams auto = 3); the in-order single-stream
+    # form stays covered
+    ("cpml-tfsf-inorder", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10, psi=5,
+                               shell_streams=1), 4, 12),
+    ("drude-upml-inorder", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True,
+                                sphere_center=(40.0, 36.0, 48.0), sphere_radius=7.0, shell_streams=1), 4, 12),
 ]
 
 
