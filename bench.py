@@ -222,6 +222,9 @@ PHYSICS_CONFIGS = (
     ("cpml_tfsf_512", "3D 512^3 CPML (10 cells) + TF/SF plane wave, fp32 (BASELINE config 3)",
      ["--3d", "--sizex", "512", "--same-size", "--dtype", "f32", "--scene", "vacuum", "--use-pml",
       "--pml-type", "cpml", "--use-tfsf"]),
+    ("drude_512", "3D 512^3 Drude sphere r=128 in vacuum, no absorbing layer, fp32 (BASELINE config 4 as named)",
+     ["--3d", "--sizex", "512", "--same-size", "--dtype", "f32", "--scene", "drude-sphere", "--use-metamaterials",
+      "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256", "--sphere-radius", "128"]),
     ("drude_upml_512", "3D 512^3 Drude sphere r=128 + UPML, fp32 (BASELINE config 4 with absorbing layers)",
      ["--3d", "--sizex", "512", "--same-size", "--dtype", "f32", "--scene", "drude-sphere", "--use-metamaterials",
       "--use-pml", "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
