@@ -6,6 +6,8 @@
 // the Python/C++ host code maps global computation ranges to local boxes.
 #pragma once
 
+#include <cstdlib>
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -50,10 +52,27 @@ static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b)
 // on full grids), halved while the launch would hold fewer than 2048
 // workgroups -- thin shell / slab windows (hybrid blocking, PML slabs) would
 // otherwise leave most CUs idle.  `wg_per_chunk` = workgroups per x chunk.
-static inline int split_xchunk(int nxo, long long wg_per_chunk, int req, int base = 16, int min_xc = 2) {
+// x planes per workgroup of the split (per-step) kernels: halve from `base`
+// until the launch has FDTD3D_SPLIT_WGS workgroups (default 2048), not below
+// FDTD3D_SPLIT_MINXC planes (default 2) -- read once per library at first use
+static inline int split_param(int which) {
+  static const int wgs = [] {
+    const char* e = getenv("FDTD3D_SPLIT_WGS");
+    return e && atoi(e) > 0 ? atoi(e) : 2048;
+  }();
+  static const int mxc = [] {
+    const char* e = getenv("FDTD3D_SPLIT_MINXC");
+    return e && atoi(e) > 0 ? atoi(e) : 2;
+  }();
+  return which ? mxc : wgs;
+}
+
+static inline int split_xchunk(int nxo, long long wg_per_chunk, int req, int base = 16, int min_xc = 0) {
   if (req > 0) return req;
+  if (min_xc <= 0) min_xc = split_param(1);
+  const long long target = split_param(0);
   int xc = base;
-  while (xc > min_xc && wg_per_chunk * (long long)cdiv(nxo, xc) < 2048) xc /= 2;
+  while (xc > min_xc && wg_per_chunk * (long long)cdiv(nxo, xc) < target) xc /= 2;
   return xc;
 }
 
