@@ -1350,9 +1350,10 @@ int run(const fdtd::Settings& s) {
         if (!G[c].p) G[c].alloc(cells);
     std::vector<unsigned> got(K);
     int t = steps;
-    bool done = false;
-    while (!done && amp_taken < s.numAmplitudeTimeSteps) {
-      const int n = std::min(K, s.numAmplitudeTimeSteps - amp_taken);
+    // one check period of n steps: blocked amplitude passes where they apply,
+    // per-step stepping + the fused amplitude kernel otherwise; returns the
+    // per-step changed counts
+    auto period = [&](int n) {
       HIP_OK(hipMemsetAsync(CNT.p, 0, K * sizeof(unsigned), st));
       int q = 0;
       while (q < n) {
@@ -1383,12 +1384,79 @@ int run(const fdtd::Settings& s) {
       }
       HIP_OK(hipMemcpyAsync(got.data(), CNT.p, n * sizeof(unsigned), hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
-      for (int r = 0; r < n && !done; ++r)
-        if (got[r] == 0 && amp_taken + r + 1 > 1) {
-          amp_stable = amp_taken + r + 1;
-          done = true;
+    };
+    // every array that carries state between steps, in logical order (the
+    // current F / D level lists, whatever the pointer swaps did): the
+    // near-convergence snapshot (models/scheme.py perform_amplitude_steps)
+    auto state = [&]() {
+      std::vector<std::pair<void*, size_t>> v;
+      for (int c = 0; c < 6; ++c)
+        if (present[c]) v.push_back({F[c].p, cells * sizeof(T)});
+      v.push_back({AMP.p, (size_t)N[0] * 6 * plane * sizeof(T)});
+      if (tfsf) {
+        v.push_back({tft.einc.p, (size_t)tft.nline * sizeof(T)});
+        v.push_back({tft.hinc.p, (size_t)tft.nline * sizeof(T)});
+      }
+      for (auto* d : cpt.keep) v.push_back({d->p, d->n * sizeof(float)});
+      for (const Slab2d<T>& sl : p2.slabs)
+        v.push_back({sl.psi, (size_t)(sl.pbox[3] - sl.pbox[0]) * (sl.pbox[4] - sl.pbox[1]) * (sl.pbox[5] - sl.pbox[2]) *
+                                 sizeof(T)});
+      for (int c = 0; c < 6; ++c) {
+        for (int l = 0; l < 2; ++l)
+          if (p2.D[c][l]) v.push_back({p2.D[c][l], cells * sizeof(T)});
+        for (T* d : upt.D[c]) v.push_back({d, cells * sizeof(T)});
+        for (T* d : upt.D1[c]) v.push_back({d, cells * sizeof(T)});
+      }
+      return v;
+    };
+    long long acells = 0;
+    for (int c = 0; c < na; ++c) {
+      const int* b = abp + 6 * c;
+      acells += (long long)std::max(0, b[3] - b[0]) * std::max(0, b[4] - b[1]) * std::max(0, b[5] - b[2]);
+    }
+    const long long near = std::max(1LL, (long long)(0.02 * (double)acells));
+    Dev<char> SNAP;
+    long long last = -1;
+    bool done = false;
+    while (!done && amp_taken < s.numAmplitudeTimeSteps) {
+      int n = std::min(K, s.numAmplitudeTimeSteps - amp_taken);
+      int t_snap = -1;
+      if (n > 1 && last >= 0 && last <= near) {
+        const auto v = state();
+        size_t total = 0;
+        for (const auto& e : v) total += e.second;
+        if (!SNAP.p) SNAP.alloc(total);
+        size_t o = 0;
+        for (const auto& e : v) {
+          HIP_OK(hipMemcpyAsync(SNAP.p + o, e.first, e.second, hipMemcpyDeviceToDevice, st));
+          o += e.second;
         }
+        t_snap = t;
+      }
+      period(n);
+      int first = -1;
+      for (int r = 0; r < n && first < 0; ++r)
+        if (got[r] == 0 && amp_taken + r + 1 > 1) first = r;
+      if (first < 0) {
+        last = got[n - 1];
+        amp_taken += n;
+        continue;
+      }
+      amp_stable = amp_taken + first + 1;
+      if (first + 1 < n && t_snap >= 0) {
+        // back to the period's start, then exactly the steps up to the stable one
+        const auto v = state();
+        size_t o = 0;
+        for (const auto& e : v) {
+          HIP_OK(hipMemcpyAsync(e.first, SNAP.p + o, e.second, hipMemcpyDeviceToDevice, st));
+          o += e.second;
+        }
+        t = t_snap;
+        n = first + 1;
+        period(n);
+      }
       amp_taken += n;
+      done = true;
     }
     amp_phase = false;
     t_end = t;

@@ -1639,52 +1639,90 @@ class YeeScheme(BlockedStepping):
         b = box_intersect((tuple(lo), tuple(hi)), self.domain.owned_global())
         return self.domain.to_local(b)
 
+    # the stop is exact (at the stable step, not at the end of its check
+    # period) whenever the period before it ended with at most this share of
+    # the amplitude cells changing: that period starts from a snapshot
+    AMP_SNAPSHOT_SHARE = 0.02
+
     def perform_amplitude_steps(self) -> int:
         """Steady-state mode: keep stepping until no cell's running max |f|
         grows by more than ``ACCURACY`` (relative), or until
         ``amplitude_steps`` extra steps.  The reference loop never sets its
         stable flag (``Scheme3D.cpp:2945-3291``); this implements the
-        documented intent.  Returns the number of steps taken."""
+        documented intent.  Returns the number of steps taken.
+
+        The changed-cell counts of ``--amplitude-check-steps`` K steps
+        accumulate on the device and are read once per period.  Near
+        convergence (the previous period's last count at most
+        ``AMP_SNAPSHOT_SHARE`` of the amplitude cells) a period starts from a
+        snapshot of the whole state; when one of its steps changes nothing,
+        the state goes back to the snapshot and exactly the steps up to the
+        stable one are replayed -- the run stops where K = 1 would.  A period
+        that drops to zero without a snapshot ends the run at its end (logged)."""
         fdtd_assert(self.planes == 1, "amplitude mode needs real field values (reference asserts the same)")
         self.in_amplitude = True
         K = max(1, int(getattr(self.cfg, "amplitude_check_steps", 8)))
         boxes = [self.amplitude_box(c) for c in self.comps]
         counts = torch.zeros(K, dtype=torch.int32, device=self.device)
         self.amplitude_counts = []  # changed cells of every step taken
+        cells = sum(max(0, b[1][0] - b[0][0]) * max(0, b[1][1] - b[0][1]) * max(0, b[1][2] - b[0][2]) for b in boxes)
+        if self.halo is not None:
+            cells = self.halo.allreduce_sum(cells)
+        near = max(1, int(self.AMP_SNAPSHOT_SHARE * cells))
         taken = 0
+        T = self._amp_blocked_steps()
+
+        def period(n):
+            counts.zero_()
+            s_ = 0
+            while s_ < n:
+                if T > 1 and n - s_ >= 2:
+                    # blocked pass with the amplitude update of every step
+                    # folded in (csrc/tb3d_mr.h AmpDev)
+                    k = min(T, n - s_)
+                    self._amp_tb_step(k, boxes, counts[s_:s_ + k])
+                    s_ += k
+                    continue
+                self.step()
+                self.ops.amplitude_update_many([self.F[0][c] for c in self.comps],
+                                               [self.amp[0][c] for c in self.comps], boxes, ACCURACY,
+                                               counts[s_:s_ + 1])
+                s_ += 1
+            got = [int(v) for v in counts[:n].cpu()]
+            if self.halo is not None:
+                got = [self.halo.allreduce_sum(v) for v in got]
+            return got
+
         try:
-            # the changed-cell counts of K steps accumulate on the device (one
-            # fused launch per step, no host sync) and are read back once per
-            # period; the run stops at the end of the period in which a step
-            # changed no amplitude (K = 1: the check after every step)
-            T = self._amp_blocked_steps()
+            last = None
             while taken < self.cfg.amplitude_steps:
                 n = min(K, self.cfg.amplitude_steps - taken)
-                counts.zero_()
-                s_ = 0
-                while s_ < n:
-                    if T > 1 and n - s_ >= 2:
-                        # blocked pass with the amplitude update of every step
-                        # folded in (csrc/tb3d_mr.h AmpDev)
-                        k = min(T, n - s_)
-                        self._amp_tb_step(k, boxes, counts[s_:s_ + k])
-                        s_ += k
-                        continue
-                    self.step()
-                    self.ops.amplitude_update_many([self.F[0][c] for c in self.comps],
-                                                   [self.amp[0][c] for c in self.comps], boxes, ACCURACY,
-                                                   counts[s_:s_ + 1])
-                    s_ += 1
-                got = [int(v) for v in counts[:n].cpu()]
-                if self.halo is not None:
-                    got = [self.halo.allreduce_sum(v) for v in got]
+                snap = None
+                if n > 1 and last is not None and last <= near:
+                    snap = ({k: v.clone() for k, v in self.named_state().items()}, self.t, self.sub_step)
+                got = period(n)
+                first = next((s_ for s_ in range(n) if got[s_] == 0 and taken + s_ + 1 > 1), None)
+                if first is None:
+                    self.amplitude_counts += got
+                    last = got[-1]
+                    taken += n
+                    continue
+                self.amplitude_converged = True
+                self.amplitude_stable_step = taken + first + 1
+                if first + 1 < n:
+                    if snap is None:
+                        log.log(0, "amplitude mode: stable at step %d, the run ends with its check period (%d steps)"
+                                % (taken + first + 1, taken + n))
+                    else:
+                        # back to the period's start, then exactly the steps up to the stable one
+                        state, t0, sub0 = snap
+                        for k, v in self.named_state().items():
+                            v.copy_(state[k])
+                        self.t, self.sub_step = t0, sub0
+                        got = period(first + 1)
+                        n = first + 1
                 self.amplitude_counts += got
-                for s_ in range(n):
-                    if got[s_] == 0 and taken + s_ + 1 > 1:
-                        self.amplitude_converged = True
-                        self.amplitude_stable_step = taken + s_ + 1
-                        return taken + n
-                taken += n
+                return taken + n
             self.amplitude_converged = False
             log.log(0, "amplitude mode: stable state not reached after %d steps" % taken)
             return taken

@@ -144,15 +144,17 @@ def test_tfsf_leakage_3d():
     assert outside < 0.05 * inside, (outside, inside)
 
 
-def test_amplitude_check_period():
+def test_amplitude_check_period(monkeypatch):
     """Amplitude mode with the changed counts read back once per 8 steps
-    finds the same first stable step as a check after every step, and stops
-    at the end of that period (reference intent of Scheme3D.cpp:2945-3333)."""
+    finds the same first stable step as a check after every step and, from a
+    near-convergence snapshot, stops exactly there with the same fields
+    (reference intent of Scheme3D.cpp:2945-3333); without a snapshot the run
+    ends with the stable step's check period."""
     import torch
     from fdtd3d_amd.models.scheme import SchemeConfig, YeeScheme
     from fdtd3d_amd.ops import make_ops
-    res = {}
-    for k in (1, 8):
+
+    def run(k):
         cfg = SchemeConfig(scheme="3d", size=(16, 16, 16), time_steps=60, amplitude_steps=300, use_amp_mode=True,
                            scene="vacuum", dtype="f64", use_pml=True, pml_size=(4, 4, 4), amplitude_check_steps=k)
         s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
@@ -160,10 +162,20 @@ def test_amplitude_check_period():
         s.init_grids()
         s.advance(cfg.time_steps)
         taken = s.perform_amplitude_steps()
-        res[k] = (taken, getattr(s, "amplitude_stable_step", None), s.amplitude_converged)
-    assert res[1][2] and res[8][2], res
-    assert res[1][1] == res[8][1] == res[1][0], res
-    assert res[8][0] == -(-res[8][1] // 8) * 8, res
+        return s, (taken, getattr(s, "amplitude_stable_step", None), s.amplitude_converged)
+
+    s1, r1 = run(1)
+    s8, r8 = run(8)
+    assert r1[2] and r8[2], (r1, r8)
+    assert r1[1] == r8[1] == r1[0] == r8[0], (r1, r8)
+    assert s1.t == s8.t and s1.amplitude_counts == s8.amplitude_counts
+    for c in s1.comps:
+        assert torch.equal(s1.F[0][c], s8.F[0][c]), c
+        assert torch.equal(s1.amp[0][c], s8.amp[0][c]), c
+    # no snapshot: the run ends with the period of the stable step
+    monkeypatch.setattr(YeeScheme, "AMP_SNAPSHOT_SHARE", 0.0)
+    s0, r0 = run(8)
+    assert r0[1] == r1[1] and r0[0] in (r1[1], -(-r1[1] // 8) * 8), (r0, r1)
 
 
 def test_capacity_plan_drude_upml():
