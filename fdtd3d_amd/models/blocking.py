@@ -191,12 +191,10 @@ class BlockedStepping:
             # decomposed: one T-deep exchange per pass feeds both the core and
             # the deep-halo stepped shell, so the ghosts must be exactly T deep
             return
-        if (two_d and int(cfg.hybrid_block) <= 0 and self.use_upml_chain and self.dtype == torch.float32
-                and self.ops.name == "hip"):
-            # measured 8192^2 TMz UPML + TF/SF fp32: stepped 88.7k > hybrid 77.1k
-            # Mcells/s (the thin shell's per-window launches cost as much as the
-            # whole stepped grid); fp64 and CPML gain (52.5k -> 72.9k, 106k -> 116k)
-            return
+        # (2D UPML fp32 used to step everything: the hybrid shell's per-window
+        # launches cost as much as the whole stepped grid -- 77.1k vs 88.7k at
+        # 8192^2 TMz + TF/SF -- until the 2D passes replayed from HIP graphs:
+        # 158k, profiles/graph2d_r4.md)
         # fp32 3D rows are float4 along z, 2D rows 16-byte lanes along y
         if self.ops.name == "hip":
             if two_d and self.domain.shape[1] % (16 // self.dtype.itemsize) != 0:

@@ -1039,7 +1039,8 @@ class YeeScheme(BlockedStepping):
         n = int(getattr(self.cfg, "shell_streams", 0))
         if n <= 0:
             n = 3 if self.ops.name == "hip" else 1
-        if n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda":
+        if (n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda"
+                or getattr(self, "_capturing", False)):
             for f in fns:
                 f()
             return
@@ -1552,6 +1553,8 @@ class YeeScheme(BlockedStepping):
             self._resident_1d(n)
             return
         if self.hybrid is not None and not self.hooks:
+            if self._hybrid_graph_ok(n):
+                n -= self._hybrid_graph(n)
             while n > 0:
                 k = min(self.hybrid["T"], n)
                 self._hybrid_step(k)
@@ -1569,6 +1572,57 @@ class YeeScheme(BlockedStepping):
             else:
                 self.step()
                 n -= 1
+
+    def _hybrid_graph_ok(self, n: int) -> bool:
+        """2D hybrid passes replay from a HIP graph: their stepped shell is a
+        few thin strips, so a step is ~30 small launches whose host cost (not
+        the GPU) bounds the rate.  Needs: serial HIP run, no periodic work, no
+        point source in the core pass (its values go in as launch
+        arguments), UPML levels that return to place after two passes."""
+        hp = self.hybrid
+        if (hp is None or self.cfg.scheme not in ("tmz", "tez") or self.halo is not None or self.hooks
+                or self.ops.name != "hip" or self.device.type != "cuda" or self.prof.enabled
+                or not hasattr(self.ops, "inc_step_e_tab") or not hasattr(self.ops, "counter_add")):
+            return False
+        if self.point_source is not None and self.point_source[1] is not None:
+            return False
+        if self.use_upml_chain and any(self.upml[c].get("nlev", 2) != 2 for c in self.comps):
+            return False
+        return n >= 4 * hp["T"]
+
+    def _hybrid_graph(self, n: int) -> int:
+        """Capture two hybrid passes (2T steps: the buffers swap back) into one
+        HIP graph and replay it; the shell's incident-line source values come
+        from a device table through a step counter the graph advances (the
+        ``_graph_src`` path of :meth:`step`).  Returns the steps taken."""
+        T = self.hybrid["T"]
+        # one pass outside the graph first: first-use set-up (table checks,
+        # compact TF/SF tables) may synchronise, which a capture must not
+        self._hybrid_step(T)
+        n -= T
+        G = 2 * T
+        reps = n // G
+        t0 = self.t
+        tab = torch.tensor([[self.source_value(t0 + i, p) for i in range(reps * G)] for p in range(self.planes)],
+                           dtype=torch.float64, device=self.device)
+        counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        graph = torch.cuda.CUDAGraph()
+        self._graph_src = (tab, counter, t0)
+        self._capturing = True
+        try:
+            with torch.cuda.graph(graph):
+                self._hybrid_step(T)
+                self._hybrid_step(T)
+                self.ops.counter_add(counter, G)
+        finally:
+            self._graph_src = None
+            self._capturing = False
+        self.t = t0  # capture records the kernels, it does not run them
+        for _ in range(reps):
+            graph.replay()
+        self.t = t0 + reps * G
+        self._graph = (graph, tab, counter)  # keep alive until the stream has drained
+        return T + reps * G
 
     def _resident_1d(self, n: int) -> None:
         """``n`` 1D steps in one launch per plane (ops.resident_1d): per-step

@@ -44,6 +44,11 @@ CASES = [
      2, 7),
     ("tmz-upml-point-f64", dict(scheme="tmz", size=(150, 90, 1), pml_size=(8, 8, 1), scene="vacuum", use_pml=True,
                                 dtype="f64"), 6, 19),
+    # 2D passes long enough to replay from a HIP graph (one warm pass, graphs of two passes, a tail)
+    ("tmz-cpml-tfsf-graph", dict(scheme="tmz", size=(120, 104, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
+                                 scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=30), 5, 37),
+    ("tez-upml-tfsf-graph", dict(scheme="tez", size=(96, 128, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
+                                 scene="vacuum", use_pml=True, use_tfsf=True, phi=60), 4, 30),
     # the shell's window launches run on several streams (--shell-streams auto = 3); the in-order single-stream
     # form stays covered
     ("cpml-tfsf-inorder", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10, psi=5,
@@ -73,6 +78,8 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
     tol = 2e-5 if cfg.dtype == "f32" else 1e-12
     hy = _run(dataclasses.replace(cfg, hybrid_block=T), "hip", gpu, dt)
     assert hy.hybrid is not None, "hybrid plan rejected"
+    if name.endswith("-graph"):
+        assert getattr(hy, "_graph", None) is not None, "no graph replay"
     st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, dt)
     assert st.hybrid is None
     ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
