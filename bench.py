@@ -297,7 +297,10 @@ def main(argv=None) -> int:
     ap.add_argument("--physics-companion", default="auto", choices=("auto", "on", "off"),
                     help="also time the 512^3 CPML + TF/SF and Drude + UPML configs (10 steps each) and report them "
                          "under 'physics' (auto: one GPU, fp32 runs)")
-    ap.add_argument("--physics-steps", type=int, default=10)
+    ap.add_argument("--physics-steps", type=int, default=30)
+    ap.add_argument("--physics-warmup", type=int, default=45,
+                    help="untimed steps before the physics configs' timed ones (hybrid passes capture their HIP "
+                         "graph there)")
     ap.add_argument("--physics-size", type=int, default=512, help="edge of the physics configs' cubic grid")
     ap.add_argument("--split", action="store_true", help="use the split E / H kernels instead of the fused one")
     ap.add_argument("--xchunk", type=int, default=0)
@@ -360,7 +363,7 @@ def main(argv=None) -> int:
         physics = {}
         for name, desc, args in PHYSICS_CONFIGS:
             try:
-                physics[name] = dict(run_physics(physics_args(args, a.physics_size), a.physics_steps, 5),
+                physics[name] = dict(run_physics(physics_args(args, a.physics_size), a.physics_steps, a.physics_warmup),
                                      desc=desc)
             except Exception as e:  # the headline line must still be printed
                 physics[name] = {"error": "%s: %s" % (type(e).__name__, e), "desc": desc}

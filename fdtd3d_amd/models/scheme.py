@@ -107,6 +107,7 @@ class SchemeConfig:
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
     hybrid_tfsf: str = "auto"                # hybrid + TF/SF: faces in the blocked core ("core"), the shell, or auto
     shell_streams: int = 0                   # hybrid shell: streams for the independent window launches (0 auto)
+    hybrid_graph: str = "auto"               # hybrid passes replayed from HIP graphs (auto / off)
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
@@ -142,7 +143,7 @@ class SchemeConfig:
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
             amplitude_check_steps=s.amplitudeCheckSteps,
-            hybrid_block=s.hybridBlock, hybrid_tfsf=s.hybridTfsf, shell_streams=s.shellStreams,
+            hybrid_block=s.hybridBlock, hybrid_tfsf=s.hybridTfsf, shell_streams=s.shellStreams, hybrid_graph=s.hybridGraph,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
@@ -1039,8 +1040,7 @@ class YeeScheme(BlockedStepping):
         n = int(getattr(self.cfg, "shell_streams", 0))
         if n <= 0:
             n = 3 if self.ops.name == "hip" else 1
-        if (n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda"
-                or getattr(self, "_capturing", False)):
+        if n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda":
             for f in fns:
                 f()
             return
@@ -1553,8 +1553,9 @@ class YeeScheme(BlockedStepping):
             self._resident_1d(n)
             return
         if self.hybrid is not None and not self.hooks:
-            if self._hybrid_graph_ok(n):
-                n -= self._hybrid_graph(n)
+            P = self._hybrid_graph_passes()
+            if P and n >= (P + 2) * self.hybrid["T"]:
+                n -= self._hybrid_graph(n, P)
             while n > 0:
                 k = min(self.hybrid["T"], n)
                 self._hybrid_step(k)
@@ -1573,56 +1574,83 @@ class YeeScheme(BlockedStepping):
                 self.step()
                 n -= 1
 
-    def _hybrid_graph_ok(self, n: int) -> bool:
-        """2D hybrid passes replay from a HIP graph: their stepped shell is a
-        few thin strips, so a step is ~30 small launches whose host cost (not
-        the GPU) bounds the rate.  Needs: serial HIP run, no periodic work, no
-        point source in the core pass (its values go in as launch
-        arguments), UPML levels that return to place after two passes."""
+    def _hybrid_graph_passes(self) -> int:
+        """Hybrid passes per HIP graph (0: no graph).  A 2D pass's stepped
+        shell is a few thin strips, so a step is ~30 small launches whose host
+        cost (not the GPU) bounds the rate.  (3D passes are GPU-bound: graphs
+        measured no faster with the capture done in the warm-up and 13-30%
+        slower with it in the timed run, profiles/graph2d_r4.md.)  Needs: 2D,
+        serial HIP run, no
+        periodic work, no point source inside a core box (the core pass takes
+        its values as launch arguments), and a pass count after which the
+        field buffers (2) and the UPML / Drude level lists (2 or 3 levels) are
+        back in place."""
         hp = self.hybrid
         if (hp is None or self.cfg.scheme not in ("tmz", "tez") or self.halo is not None or self.hooks
                 or self.ops.name != "hip" or self.device.type != "cuda" or self.prof.enabled
-                or not hasattr(self.ops, "inc_step_e_tab") or not hasattr(self.ops, "counter_add")):
-            return False
+                or not hasattr(self.ops, "inc_step_e_tab") or not hasattr(self.ops, "counter_add")
+                or getattr(self.cfg, "hybrid_graph", "auto") == "off" or hp.get("tfsf_in_core")):
+            return 0
         if self.point_source is not None and self.point_source[1] is not None:
-            return False
-        if self.use_upml_chain and any(self.upml[c].get("nlev", 2) != 2 for c in self.comps):
-            return False
-        return n >= 4 * hp["T"]
+            li = self.point_source[1]
+            if any(all(b[0][d] <= li[d] < b[1][d] for d in range(3)) for b in hp["core"]):
+                return 0
+        levels = {2}
+        if self.use_upml_chain:
+            levels |= {self.upml[c].get("nlev", 2) for c in self.comps}
+        T = hp["T"]
+        for P in range(2, 13, 2):
+            if all((P * T) % L == 0 for L in levels):
+                return P
+        return 0
 
-    def _hybrid_graph(self, n: int) -> int:
-        """Capture two hybrid passes (2T steps: the buffers swap back) into one
-        HIP graph and replay it; the shell's incident-line source values come
-        from a device table through a step counter the graph advances (the
-        ``_graph_src`` path of :meth:`step`).  Returns the steps taken."""
+    def _hybrid_graph(self, n: int, P: int) -> int:
+        """Replay ``P`` hybrid passes at a time from one HIP graph; the shell's
+        sources (incident line, point source) read a device table through a
+        step counter the graph advances (the ``_graph_src`` path of
+        :meth:`step`).  The graph is captured once and kept while its buffers
+        are the current ones (same field-buffer parity, table long enough);
+        later calls refill the table and reset the counter.  Returns the
+        steps taken."""
         T = self.hybrid["T"]
-        # one pass outside the graph first: first-use set-up (table checks,
-        # compact TF/SF tables) may synchronise, which a capture must not
-        self._hybrid_step(T)
-        n -= T
-        G = 2 * T
+        taken = 0
+        if not getattr(self, "_hybrid_warm", False):
+            # one pass outside any graph first: first-use set-up (table
+            # checks, compact TF/SF tables) may synchronise, which a capture
+            # must not
+            self._hybrid_step(T)
+            self._hybrid_warm = True
+            n -= T
+            taken += T
+        G = P * T
         reps = n // G
+        if reps == 0:
+            return taken
         t0 = self.t
-        tab = torch.tensor([[self.source_value(t0 + i, p) for i in range(reps * G)] for p in range(self.planes)],
-                           dtype=torch.float64, device=self.device)
-        counter = torch.zeros(1, dtype=torch.int32, device=self.device)
-        graph = torch.cuda.CUDAGraph()
-        self._graph_src = (tab, counter, t0)
-        self._capturing = True
-        try:
-            with torch.cuda.graph(graph):
-                self._hybrid_step(T)
-                self._hybrid_step(T)
-                self.ops.counter_add(counter, G)
-        finally:
-            self._graph_src = None
-            self._capturing = False
-        self.t = t0  # capture records the kernels, it does not run them
+        vals = torch.tensor([[self.source_value(t0 + i, p) for i in range(reps * G)] for p in range(self.planes)],
+                            dtype=torch.float64)
+        key = (P, T, tuple(self.F[p][self.comps[0]].data_ptr() for p in range(self.planes)))
+        g = self.__dict__.get("_hgraph")
+        if g is None or g["key"] != key or g["reps"] < reps:
+            tab = torch.zeros((self.planes, reps * G), dtype=torch.float64, device=self.device)
+            counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+            graph = torch.cuda.CUDAGraph()
+            self._graph_src = (tab, counter, t0)
+            try:
+                with torch.cuda.graph(graph):
+                    for _ in range(P):
+                        self._hybrid_step(T)
+                    self.ops.counter_add(counter, G)
+            finally:
+                self._graph_src = None
+            self.t = t0  # capture records the kernels, it does not run them
+            g = self._hgraph = {"key": key, "reps": reps, "graph": graph, "tab": tab, "counter": counter}
+        g["tab"][:, :reps * G].copy_(vals)
+        g["counter"].zero_()
         for _ in range(reps):
-            graph.replay()
+            g["graph"].replay()
         self.t = t0 + reps * G
-        self._graph = (graph, tab, counter)  # keep alive until the stream has drained
-        return T + reps * G
+        return taken + reps * G
 
     def _resident_1d(self, n: int) -> None:
         """``n`` 1D steps in one launch per plane (ops.resident_1d): per-step

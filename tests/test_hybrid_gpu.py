@@ -79,7 +79,7 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
     hy = _run(dataclasses.replace(cfg, hybrid_block=T), "hip", gpu, dt)
     assert hy.hybrid is not None, "hybrid plan rejected"
     if name.endswith("-graph"):
-        assert getattr(hy, "_graph", None) is not None, "no graph replay"
+        assert getattr(hy, "_hgraph", None) is not None, "no graph replay"
     st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, dt)
     assert st.hybrid is None
     ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
