@@ -963,6 +963,16 @@ int run(const fdtd::Settings& s) {
                       percell ? 1.0 : (kind == 0 ? cb : db), cp, N[1], N[2], sl.box, sl.pbox, st));
     }
   };
+  // 2D UPML half step: the D/B chain on the four PML strips (one cell of
+  // staggering slack inside), the plain 2D kernel on the inner box, where
+  // every sigma vanishes and the chain is the plain update to round-off (the
+  // strips' D levels are the only ones ever read)
+  const int ppx = s.pmlSizeX + 1, ppy = s.pmlSizeY + 1;
+  const IBox inner2 = {{ppx, ppy, 0}, {N[0] - ppx, N[1] - ppy, N[2]}};
+  const IBox strips2[4] = {{{0, 0, 0}, {std::min(ppx, N[0]), N[1], N[2]}},
+                           {{std::max(0, N[0] - ppx), 0, 0}, {N[0], N[1], N[2]}},
+                           {{ppx, 0, 0}, {N[0] - ppx, std::min(ppy, N[1]), N[2]}},
+                           {{ppx, std::max(0, N[1] - ppy), 0}, {N[0] - ppx, N[1], N[2]}}};
   auto pml2d_upml = [&](int kind) {
     for (int c = 3 * kind; c < 3 * kind + 3; ++c) {
       if (!present[c]) continue;
@@ -975,12 +985,48 @@ int run(const fdtd::Settings& s) {
         axes[nt] = ax;
         signs[nt++] = kCurl[c][q][2];
       }
-      K_OK(curl_gen(p2.D[c][1], p2.D[c][0], srcs, axes, signs, nt, kind == 0 ? 1 : 0, p2.ca[c], p2.cbp[c], N[1],
-                    N[2], boxes + 6 * c, st));
+      IBox ub;
+      for (int a = 0; a < 3; ++a) {
+        ub.lo[a] = boxes[6 * c + a];
+        ub.hi[a] = boxes[6 * c + 3 + a];
+      }
       const double sc3[3] = {1.0, p2.s[c], p2.s[c]};
       const T* xs[3] = {F[c].p, p2.D[c][1], p2.D[c][0]};
-      K_OK(lincomb(F[c].p, 3, sc3, p2.lin[c], xs, N[1], N[2], boxes + 6 * c, st));
+      for (const IBox& sb : strips2) {
+        const IBox b = box_and(sb, ub);
+        if (b.empty()) continue;
+        const int bx[6] = {b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2]};
+        K_OK(curl_gen(p2.D[c][1], p2.D[c][0], srcs, axes, signs, nt, kind == 0 ? 1 : 0, p2.ca[c], p2.cbp[c], N[1],
+                      N[2], bx, st));
+        K_OK(lincomb(F[c].p, 3, sc3, p2.lin[c], xs, N[1], N[2], bx, st));
+      }
       std::swap(p2.D[c][0], p2.D[c][1]);
+    }
+    // the inner box through the plain kernels (per-component boxes clipped)
+    int ib[36];
+    for (int c = 0; c < 6; ++c) {
+      IBox ub;
+      for (int a = 0; a < 3; ++a) {
+        ub.lo[a] = boxes[6 * c + a];
+        ub.hi[a] = boxes[6 * c + 3 + a];
+      }
+      const IBox b = box_and(ub, inner2);
+      for (int a = 0; a < 3; ++a) {
+        ib[6 * c + a] = b.empty() ? 0 : b.lo[a];
+        ib[6 * c + 3 + a] = b.empty() ? 0 : b.hi[a];
+      }
+    }
+    const bool tm = scheme == "tmz";
+    if (kind == 0) {
+      if (tm)
+        K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], ib + 12, st));
+      else
+        K_OK(tez_e(F[0].p, F[1].p, F[5].p, C[0].p, C[1].p, percell ? 1.0 : cb, N[0], N[1], ib, st));
+    } else {
+      if (tm)
+        K_OK(tmz_h(F[3].p, F[4].p, F[2].p, C[3].p, C[4].p, percell ? 1.0 : db, N[0], N[1], ib + 18, st));
+      else
+        K_OK(tez_h(F[5].p, F[0].p, F[1].p, C[5].p, percell ? 1.0 : db, N[0], N[1], ib + 30, st));
     }
   };
   // amplitude mode state: running maxima of every component, one [x][6][y][z]
