@@ -942,6 +942,54 @@ int run(const fdtd::Settings& s) {
   auto fptrs = [&]() {
     for (int c = 0; c < 6; ++c) Fp[c] = F[c].p;
   };
+  // 3D UPML / Drude: the chain only where it differs from the plain update --
+  // the PML slabs (one cell of staggering slack) and the dispersive sphere's
+  // box -- and the plain float4 kernels on the rest (models/scheme.py
+  // _init_chain_regions; the chain with every sigma and omega zero IS the
+  // plain update to round-off, and only chain cells read their D levels)
+  std::vector<IBox> chain_regs, plain_regs;
+  if (upml && dim == 3) {
+    const IBox whole = {{0, 0, 0}, {N[0], N[1], N[2]}};
+    const int pp[3] = {s.doUsePML ? s.pmlSizeX + 1 : 0, s.doUsePML ? s.pmlSizeY + 1 : 0,
+                       s.doUsePML ? s.pmlSizeZ + 1 : 0};
+    const IBox inner = {{pp[0], pp[1], pp[2]}, {N[0] - pp[0], N[1] - pp[1], N[2] - pp[2]}};
+    IBox dbox = {{0, 0, 0}, {0, 0, 0}};
+    if (s.doUseMetamaterials) {
+      const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
+      for (int a = 0; a < 3; ++a) {
+        dbox.lo[a] = std::max(0, (int)std::floor(ctr[a] - s.sphereRadius) - 2);
+        dbox.hi[a] = std::min(N[a], (int)std::ceil(ctr[a] + s.sphereRadius) + 3);
+      }
+    }
+    bool inside = !inner.empty();
+    for (int a = 0; a < 3 && !dbox.empty(); ++a)
+      inside = inside && dbox.lo[a] >= inner.lo[a] && dbox.hi[a] <= inner.hi[a];
+    if (!inside) {
+      chain_regs.push_back(whole);
+    } else {
+      if (s.doUsePML) chain_regs = box_minus(whole, inner);
+      if (!dbox.empty()) {
+        chain_regs.push_back(dbox);
+        plain_regs = box_minus(inner, dbox);
+      } else {
+        plain_regs.push_back(inner);
+      }
+    }
+  }
+  auto clip36 = [&](const IBox& r, int* out) {
+    for (int c = 0; c < 6; ++c) {
+      IBox b;
+      for (int a = 0; a < 3; ++a) {
+        b.lo[a] = boxes[6 * c + a];
+        b.hi[a] = boxes[6 * c + 3 + a];
+      }
+      b = box_and(b, r);
+      for (int a = 0; a < 3; ++a) {
+        out[6 * c + a] = b.empty() ? 0 : b.lo[a];
+        out[6 * c + 3 + a] = b.empty() ? 0 : b.hi[a];
+      }
+    }
+  };
   int (*chain_fn)(const void* const*, const double*, const int*, int, int, int, int, void*) =
       sizeof(T) == 4 ? fdtd_chain3d_f32 : fdtd_chain3d_f64;
   NativeTfsf<T> tft;
@@ -1054,6 +1102,25 @@ int run(const fdtd::Settings& s) {
     }
   }
 
+  auto upml_regions = [&](int kind) {
+    fptrs();
+    int rb[36];
+    for (const IBox& r : chain_regs) {
+      clip36(r, rb);
+      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false));
+    }
+    native_phys::upml_rotate(upt, kind);
+    for (const IBox& r : plain_regs) {
+      clip36(r, rb);
+      if (kind == 0)
+        K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, percell ? 1.0 : cb, N[0],
+                 N[1], N[2], rb, 0, st, v4));
+      else
+        K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, percell ? 1.0 : db, N[0],
+                 N[1], N[2], rb + 18, 0, st, v4));
+    }
+  };
+
   // one time step (t) through the configured kernels
   auto step = [&](int t) {
     const double sv = src_val(t);
@@ -1073,8 +1140,7 @@ int run(const fdtd::Settings& s) {
         // [incident line H] H update [TF/SF on H] -- the order of scheme.step
         if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
         if (upml) {
-          fptrs();
-          K_OK(native_phys::upml_kind<T>(upt, Fp, boxes, 0, N[1], N[2], st, chain_fn));
+          upml_regions(0);
         } else if (cpml) {
           if constexpr (sizeof(T) == 4)
             K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p,
@@ -1093,8 +1159,7 @@ int run(const fdtd::Settings& s) {
         }
         if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
         if (upml) {
-          fptrs();
-          K_OK(native_phys::upml_kind<T>(upt, Fp, boxes, 1, N[1], N[2], st, chain_fn));
+          upml_regions(1);
         } else if (cpml) {
           if constexpr (sizeof(T) == 4)
             K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p,

@@ -258,9 +258,32 @@ void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt,
 
 // one chain launch for the three components of a kind (kind 0 = E): the whole
 // update boxes; dispersive components take the ADE form
+// level rotation of a kind's components: new -> cur (-> prev)
+template <typename T>
+void upml_rotate(Upml<T>& U, int kind) {
+  for (int cc = 0; cc < 3; ++cc) {
+    const int c = 3 * kind + cc;
+    std::vector<T*>& D = U.D[c];
+    if (D.size() == 3) {
+      T* n = D[2];
+      D[2] = D[1];
+      D[1] = D[0];
+      D[0] = n;
+      std::vector<T*>& E1 = U.D1[c];
+      T* n1 = E1[2];
+      E1[2] = E1[1];
+      E1[1] = E1[0];
+      E1[0] = n1;
+    } else if (D.size() == 2) {
+      std::swap(D[0], D[1]);
+    }
+  }
+}
+
 template <typename T>
 int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int nz, void* stream,
-              int (*chain)(const void* const*, const double*, const int*, int, int, int, int, void*)) {
+              int (*chain)(const void* const*, const double*, const int*, int, int, int, int, void*),
+              bool rotate = true) {
   if (fdtd_chain_ints_per_comp() != 25 || fdtd_chain_ptrs_per_comp() != 24) return (int)hipErrorInvalidValue;
   const void* P[72] = {};
   double S[6] = {};
@@ -304,24 +327,7 @@ int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int n
     if (U.disp[3 * kind + cc] != (drude != 0)) return (int)hipErrorInvalidValue;
   const int rc = chain(P, S, I, drude, kind == 0 ? 1 : 0, ny, nz, stream);
   if (rc) return rc;
-  // level rotation: new -> cur (-> prev)
-  for (int cc = 0; cc < 3; ++cc) {
-    const int c = 3 * kind + cc;
-    std::vector<T*>& D = U.D[c];
-    if (D.size() == 3) {
-      T* n = D[2];
-      D[2] = D[1];
-      D[1] = D[0];
-      D[0] = n;
-      std::vector<T*>& E1 = U.D1[c];
-      T* n1 = E1[2];
-      E1[2] = E1[1];
-      E1[1] = E1[0];
-      E1[0] = n1;
-    } else {
-      std::swap(D[0], D[1]);
-    }
-  }
+  if (rotate) upml_rotate(U, kind);
   return 0;
 }
 
