@@ -1226,9 +1226,12 @@ int run(const fdtd::Settings& s) {
   IBox hcore = {{0, 0, 0}, {0, 0, 0}};
   std::vector<IBox> hshell[8], hcopy;
   int T_h = 1;
-  if (scheme == "3d" && sizeof(T) == 4 && v4 && cpml && !percell && !amp && T_h_req > 1 &&
+  // (UPML runs without dispersive media too: the chain slabs run whole in
+  // every shell step, the plain kernels on the windows' inner parts)
+  const bool upml_h = upml && s.doUsePML && !s.doUseMetamaterials && plain_regs.size() == 1;
+  if (scheme == "3d" && sizeof(T) == 4 && v4 && (cpml || upml_h) && !percell && !amp && T_h_req > 1 &&
       T_h_req <= fdtd_tb_max_steps()) {
-    const int pml[3] = {s.pmlSizeX, s.pmlSizeY, s.pmlSizeZ};
+    const int pml[3] = {s.pmlSizeX + (upml ? 1 : 0), s.pmlSizeY + (upml ? 1 : 0), s.pmlSizeZ + (upml ? 1 : 0)};
     const int tfs[3] = {s.tfsfSizeX, s.tfsfSizeY, s.tfsfSizeZ};
     IBox K;
     for (int a = 0; a < 3; ++a) {
@@ -1267,6 +1270,29 @@ int run(const fdtd::Settings& s) {
       }
     }
   };
+  // UPML shell half step: the chain slabs whole (they lie inside every
+  // step's windows), the plain kernels on the windows' parts in the inner box
+  auto upml_shell = [&](int kind, const std::vector<IBox>& wins) {
+    fptrs();
+    int rb[36];
+    for (const IBox& r : chain_regs) {
+      clip36(r, rb);
+      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false));
+    }
+    native_phys::upml_rotate(upt, kind);
+    for (const IBox& w : wins)
+      for (const IBox& pr : plain_regs) {
+        const IBox b = box_and(w, pr);
+        if (b.empty()) continue;
+        clip36(b, rb);
+        if (kind == 0)
+          K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, cb, N[0], N[1], N[2], rb, 0,
+                   st, v4));
+        else
+          K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, db, N[0], N[1], N[2],
+                   rb + 18, 0, st, v4));
+      }
+  };
   auto hybrid_pass = [&](int t) {
     if constexpr (sizeof(T) == 4) {
       const T* ei[3] = {F[0].p, F[1].p, F[2].p};
@@ -1286,18 +1312,28 @@ int run(const fdtd::Settings& s) {
         const double sv = src_val(t + q);
         int wb[18];
         if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
-        for (const IBox& w : hshell[q]) {
-          window_boxes(w, 0, wb);
-          K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, nullptr, nullptr, nullptr,
-                                           cb, N[0], N[1], N[2], wb, 0, cpt.P[0].data(), cpt.I[0].data(), st));
+        if (upml) {
+          upml_shell(0, hshell[q]);
+        } else {
+          for (const IBox& w : hshell[q]) {
+            window_boxes(w, 0, wb);
+            K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, nullptr, nullptr,
+                                             nullptr, cb, N[0], N[1], N[2], wb, 0, cpt.P[0].data(), cpt.I[0].data(),
+                                             st));
+          }
         }
         if (tfsf) tfsf_kind(0);
         if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));
         if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
-        for (const IBox& w : hshell[q]) {
-          window_boxes(w, 3, wb);
-          K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, nullptr, nullptr, nullptr,
-                                           db, N[0], N[1], N[2], wb, 0, cpt.P[1].data(), cpt.I[1].data(), st));
+        if (upml) {
+          upml_shell(1, hshell[q]);
+        } else {
+          for (const IBox& w : hshell[q]) {
+            window_boxes(w, 3, wb);
+            K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, nullptr, nullptr,
+                                             nullptr, db, N[0], N[1], N[2], wb, 0, cpt.P[1].data(), cpt.I[1].data(),
+                                             st));
+          }
         }
         if (tfsf) tfsf_kind(1);
       }
@@ -1593,8 +1629,8 @@ int run(const fdtd::Settings& s) {
   std::printf("\n-------- Details --------\n");
   std::printf("Parallel grid: 0\n");
   if (T_h > 1)
-    std::printf("Backend: native HIP, hybrid passes (blocked core, %d steps per pass; stepped CPML%s shell)\n", T_h,
-                tfsf ? " + TF/SF" : "");
+    std::printf("Backend: native HIP, hybrid passes (blocked core, %d steps per pass; stepped %s%s shell)\n", T_h,
+                upml ? "UPML" : "CPML", tfsf ? " + TF/SF" : "");
   else if (T_blk > 1 || T2_blk > 1)
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", std::max(T_blk, T2_blk));
   else if (res1)

@@ -60,6 +60,14 @@ CASES = {
     "3d_cpml_point_hybrid": ["--3d", "--sizex", "72", "--sizey", "76", "--sizez", "80", "--time-steps", "17",
                              "--scene", "vacuum", "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6",
                              "--pml-sizey", "7", "--pml-sizez", "5", "--hybrid-block", "4"],
+    # hybrid passes with the UPML (chain slabs whole in every shell step, plain kernels on the windows' inner
+    # parts)
+    "3d_upml_tfsf_hybrid": ["--3d", "--sizex", "104", "--same-size", "--time-steps", "23", "--scene", "vacuum",
+                            "--use-pml", "--pml-sizex", "5", "--same-size-pml", "--use-tfsf", "--tfsf-sizex", "10",
+                            "--same-size-tfsf", "--angle-teta", "50", "--angle-phi", "20", "--angle-psi", "10"],
+    "3d_upml_point_hybrid": ["--3d", "--sizex", "72", "--sizey", "76", "--sizez", "80", "--time-steps", "17",
+                             "--scene", "vacuum", "--use-pml", "--pml-sizex", "6", "--pml-sizey", "7", "--pml-sizez",
+                             "5", "--hybrid-block", "4"],
     # UPML in the reference's D/B form (fused chain kernel) + oblique TF/SF, a dielectric sphere with the
     # UPML (per-cell 1/(eps eps0) in the chain), Drude and Lorentz spheres + UPML (uint8 index + table)
     "3d_upml_tfsf": ["--3d", "--sizex", "36", "--sizey", "32", "--sizez", "40", "--time-steps", "30",
@@ -107,7 +115,7 @@ CASES = {
                         "--use-amp-mode", "--amplitude-time-steps", "300", "--use-pml", "--pml-type", "cpml"],
 }
 FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf", "3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid",
-             "3d_amp_cpml"}
+             "3d_amp_cpml", "3d_upml_tfsf_hybrid", "3d_upml_point_hybrid"}
 # the converged step depends on running-maximum comparisons at round-off level: fp64 only
 FP64_ONLY = {"2d_tmz_amp_cpml"}
 
