@@ -948,6 +948,7 @@ int run(const fdtd::Settings& s) {
   // _init_chain_regions; the chain with every sigma and omega zero IS the
   // plain update to round-off, and only chain cells read their D levels)
   std::vector<IBox> chain_regs, plain_regs;
+  std::vector<bool> chain_disp;  // per chain region: holds dispersive cells (the Drude form runs there)
   if (upml && dim == 3) {
     const IBox whole = {{0, 0, 0}, {N[0], N[1], N[2]}};
     const int pp[3] = {s.doUsePML ? s.pmlSizeX + 1 : 0, s.doUsePML ? s.pmlSizeY + 1 : 0,
@@ -966,10 +967,13 @@ int run(const fdtd::Settings& s) {
       inside = inside && dbox.lo[a] >= inner.lo[a] && dbox.hi[a] <= inner.hi[a];
     if (!inside) {
       chain_regs.push_back(whole);
+      chain_disp.push_back(true);
     } else {
       if (s.doUsePML) chain_regs = box_minus(whole, inner);
+      chain_disp.assign(chain_regs.size(), false);
       if (!dbox.empty()) {
         chain_regs.push_back(dbox);
+        chain_disp.push_back(true);
         plain_regs = box_minus(inner, dbox);
       } else {
         plain_regs.push_back(inner);
@@ -1105,9 +1109,9 @@ int run(const fdtd::Settings& s) {
   auto upml_regions = [&](int kind) {
     fptrs();
     int rb[36];
-    for (const IBox& r : chain_regs) {
-      clip36(r, rb);
-      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false));
+    for (size_t q = 0; q < chain_regs.size(); ++q) {
+      clip36(chain_regs[q], rb);
+      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false, !chain_disp[q]));
     }
     native_phys::upml_rotate(upt, kind);
     for (const IBox& r : plain_regs) {
@@ -1223,35 +1227,78 @@ int run(const fdtd::Settings& s) {
   // (stale core values corrupt one band cell per step, so the shell itself
   // stays exact), copied into G, and the buffers swap.
   const int T_h_req = s.hybridBlock == 0 ? 5 : s.hybridBlock;
-  IBox hcore = {{0, 0, 0}, {0, 0, 0}};
-  std::vector<IBox> hshell[8], hcopy;
+  std::vector<IBox> hcores, hshell[8], hcopy;
   int T_h = 1;
   // (UPML runs without dispersive media too: the chain slabs run whole in
   // every shell step, the plain kernels on the windows' inner parts)
   const bool upml_h = upml && s.doUsePML && !s.doUseMetamaterials && plain_regs.size() == 1;
-  if (scheme == "3d" && sizeof(T) == 4 && v4 && (cpml || upml_h) && !percell && !amp && T_h_req > 1 &&
+  // Drude / Lorentz sphere (+ UPML): the dispersive box is cut out of the core
+  // (grown by T + 2) and stepped with the shell, chain whole every step
+  IBox dbox_h = {{0, 0, 0}, {0, 0, 0}};
+  if (upml && s.doUseMetamaterials && !chain_regs.empty() && !plain_regs.empty()) dbox_h = chain_regs.back();
+  const bool drude_h = !dbox_h.empty();
+  if (scheme == "3d" && sizeof(T) == 4 && v4 && (cpml || upml_h || drude_h) && !percell && !amp && T_h_req > 1 &&
       T_h_req <= fdtd_tb_max_steps()) {
-    const int pml[3] = {s.pmlSizeX + (upml ? 1 : 0), s.pmlSizeY + (upml ? 1 : 0), s.pmlSizeZ + (upml ? 1 : 0)};
+    const int Th = T_h_req;
+    const int pml[3] = {s.doUsePML ? s.pmlSizeX + (upml ? 1 : 0) : 0, s.doUsePML ? s.pmlSizeY + (upml ? 1 : 0) : 0,
+                        s.doUsePML ? s.pmlSizeZ + (upml ? 1 : 0) : 0};
     const int tfs[3] = {s.tfsfSizeX, s.tfsfSizeY, s.tfsfSizeZ};
+    const IBox alloc = {{0, 0, 0}, {N[0], N[1], N[2]}};
     IBox K;
     for (int a = 0; a < 3; ++a) {
       const int edge = std::max(pml[a], tfsf ? tfs[a] + 1 : 0);
-      K.lo[a] = edge + T_h_req + 2;
-      K.hi[a] = N[a] - edge - T_h_req - 2;
+      // nothing irregular along an axis but the domain border: the core
+      // reaches the faces (the blocked kernel handles them itself)
+      K.lo[a] = edge > 0 ? edge + Th + 2 : 0;
+      K.hi[a] = edge > 0 ? N[a] - edge - Th - 2 : N[a];
     }
-    if (!K.empty() && K.volume() >= (long long)cells / 4) {
-      T_h = T_h_req;
-      hcore = K;
-      const IBox alloc = {{0, 0, 0}, {N[0], N[1], N[2]}};
-      for (int q = 0; q < T_h; ++q) {
-        IBox Kd = K;
-        for (int a = 0; a < 3; ++a) {
-          Kd.lo[a] += T_h - q;
-          Kd.hi[a] -= T_h - q;
-        }
-        hshell[q] = box_minus(alloc, Kd);
+    auto grow = [&](const IBox& b, int n) {
+      IBox g = b;
+      for (int a = 0; a < 3; ++a) {
+        g.lo[a] -= n;
+        g.hi[a] += n;
       }
-      hcopy = box_minus(alloc, K);
+      return g;
+    };
+    auto shrink_inner = [&](const IBox& b, int n) {
+      IBox r = b;
+      for (int a = 0; a < 3; ++a) {
+        if (r.lo[a] > 0) r.lo[a] += n;
+        if (r.hi[a] < N[a]) r.hi[a] -= n;
+      }
+      return r;
+    };
+    IBox Dm = {{0, 0, 0}, {0, 0, 0}};
+    bool ok = !K.empty();
+    if (ok && drude_h) {
+      Dm = box_and(grow(dbox_h, Th + 2), K);
+      // the dispersive box runs whole in every shell step: inside every window set
+      const IBox KT = shrink_inner(K, Th);
+      for (int a = 0; a < 3; ++a) ok = ok && dbox_h.lo[a] >= KT.lo[a] && dbox_h.hi[a] <= KT.hi[a];
+    }
+    std::vector<IBox> cores;
+    if (ok) cores = Dm.empty() ? std::vector<IBox>{K} : box_minus(K, Dm);
+    long long vol = 0;
+    for (const IBox& b : cores) vol += b.volume();
+    if (ok && vol >= (long long)cells / 4) {
+      T_h = Th;
+      hcores = cores;
+      for (int q = 0; q < T_h; ++q) {
+        const IBox Kd = shrink_inner(K, T_h - q);
+        hshell[q] = box_minus(alloc, Kd);
+        if (!Dm.empty()) {
+          const IBox w = box_and(grow(Dm, T_h - q), Kd);
+          if (!w.empty()) hshell[q].push_back(w);
+        }
+        std::vector<IBox> keep;
+        for (const IBox& w : hshell[q])
+          if (!w.empty()) keep.push_back(w);
+        hshell[q] = keep;
+      }
+      hcopy.clear();
+      for (const IBox& b : box_minus(alloc, K))
+        if (!b.empty()) hcopy.push_back(b);
+      if (!Dm.empty()) hcopy.push_back(box_and(Dm, alloc));
       for (int c = 0; c < 6; ++c)
         if (present[c] && !G[c].p) G[c].alloc(cells);
     }
@@ -1275,9 +1322,9 @@ int run(const fdtd::Settings& s) {
   auto upml_shell = [&](int kind, const std::vector<IBox>& wins) {
     fptrs();
     int rb[36];
-    for (const IBox& r : chain_regs) {
-      clip36(r, rb);
-      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false));
+    for (size_t q = 0; q < chain_regs.size(); ++q) {
+      clip36(chain_regs[q], rb);
+      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false, !chain_disp[q]));
     }
     native_phys::upml_rotate(upt, kind);
     for (const IBox& w : wins)
@@ -1300,14 +1347,16 @@ int run(const fdtd::Settings& s) {
       T* eo[3] = {G[0].p, G[1].p, G[2].p};
       T* ho[3] = {G[3].p, G[4].p, G[5].p};
       const T* none3[3] = {nullptr, nullptr, nullptr};
-      bool in_core = true;
-      for (int a = 0; a < 3; ++a) in_core = in_core && sp[a] >= hcore.lo[a] && sp[a] < hcore.hi[a];
-      const int src[4] = {sp[0], sp[1], sp[2], point_src && in_core ? src_comp : -1};
       double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int l = 0; l < T_h; ++l) vals[l] = src_val(t + l);
-      const int ob[6] = {hcore.lo[0], hcore.lo[1], hcore.lo[2], hcore.hi[0], hcore.hi[1], hcore.hi[2]};
-      K_OK(tb3d(ei, hi, eo, ho, none3, none3, cb, db, N[0], N[1], N[2], boxes, T_h, src, vals, st, nullptr, nullptr,
-                ob));
+      for (const IBox& hc : hcores) {
+        bool in_core = true;
+        for (int a = 0; a < 3; ++a) in_core = in_core && sp[a] >= hc.lo[a] && sp[a] < hc.hi[a];
+        const int src[4] = {sp[0], sp[1], sp[2], point_src && in_core ? src_comp : -1};
+        const int ob[6] = {hc.lo[0], hc.lo[1], hc.lo[2], hc.hi[0], hc.hi[1], hc.hi[2]};
+        K_OK(tb3d(ei, hi, eo, ho, none3, none3, cb, db, N[0], N[1], N[2], boxes, T_h, src, vals, st, nullptr, nullptr,
+                  ob));
+      }
       for (int q = 0; q < T_h; ++q) {
         const double sv = src_val(t + q);
         int wb[18];

@@ -283,7 +283,10 @@ void upml_rotate(Upml<T>& U, int kind) {
 template <typename T>
 int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int nz, void* stream,
               int (*chain)(const void* const*, const double*, const int*, int, int, int, int, void*),
-              bool rotate = true) {
+              bool rotate = true, bool plain_form = false) {
+  // plain_form: dispersive components take the non-dispersive chain (E from D
+  // through 1/eps0) -- the launches over boxes without dispersive cells (the
+  // PML slabs around an interior sphere)
   if (fdtd_chain_ints_per_comp() != 25 || fdtd_chain_ptrs_per_comp() != 24) return (int)hipErrorInvalidValue;
   const void* P[72] = {};
   double S[6] = {};
@@ -292,7 +295,7 @@ int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int n
   for (int cc = 0; cc < 3; ++cc) {
     const int c = 3 * kind + cc;
     const void** p = P + 24 * cc;
-    const bool d = U.disp[c];
+    const bool d = U.disp[c] && !plain_form;
     drude = drude || d;
     std::vector<T*>& D = U.D[c];
     p[0] = F[c];
@@ -310,7 +313,7 @@ int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int n
     p[15] = U.cell[c];
     p[21] = U.ids[c];
     p[22] = U.lut[c];
-    S[2 * cc] = U.s[c];
+    S[2 * cc] = (U.disp[c] && !d) ? 1.0 / (c < 3 ? kEps0 : kMu0) : U.s[c];
     S[2 * cc + 1] = 1.0;
     int* in = I + 25 * cc;
     in[0] = kCurlT[c][0][1];
@@ -324,7 +327,7 @@ int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int n
   }
   // a kind launches in one form: every component dispersive, or none
   for (int cc = 0; cc < 3; ++cc)
-    if (U.disp[3 * kind + cc] != (drude != 0)) return (int)hipErrorInvalidValue;
+    if ((U.disp[3 * kind + cc] && !plain_form) != (drude != 0)) return (int)hipErrorInvalidValue;
   const int rc = chain(P, S, I, drude, kind == 0 ? 1 : 0, ny, nz, stream);
   if (rc) return rc;
   if (rotate) upml_rotate(U, kind);

@@ -68,6 +68,15 @@ CASES = {
     "3d_upml_point_hybrid": ["--3d", "--sizex", "72", "--sizey", "76", "--sizez", "80", "--time-steps", "17",
                              "--scene", "vacuum", "--use-pml", "--pml-sizex", "6", "--pml-sizey", "7", "--pml-sizez",
                              "5", "--hybrid-block", "4"],
+    # hybrid passes around a Drude sphere (the dispersive box cut out of the core, its chain whole in every
+    # shell step), with the UPML and without absorbing layers (the core reaches the domain faces)
+    "3d_drude_upml_hybrid": ["--3d", "--sizex", "96", "--sizey", "88", "--sizez", "92", "--time-steps", "23",
+                             "--scene", "drude-sphere", "--use-metamaterials", "--use-pml", "--pml-sizex", "5",
+                             "--same-size-pml", "--sphere-center-x", "48", "--sphere-center-y", "44",
+                             "--sphere-center-z", "46", "--sphere-radius", "6"],
+    "3d_drude_hybrid": ["--3d", "--sizex", "80", "--same-size", "--time-steps", "17", "--scene", "drude-sphere",
+                        "--use-metamaterials", "--sphere-center-x", "40", "--sphere-center-y", "38",
+                        "--sphere-center-z", "41", "--sphere-radius", "7", "--hybrid-block", "4"],
     # UPML in the reference's D/B form (fused chain kernel) + oblique TF/SF, a dielectric sphere with the
     # UPML (per-cell 1/(eps eps0) in the chain), Drude and Lorentz spheres + UPML (uint8 index + table)
     "3d_upml_tfsf": ["--3d", "--sizex", "36", "--sizey", "32", "--sizez", "40", "--time-steps", "30",
@@ -115,7 +124,7 @@ CASES = {
                         "--use-amp-mode", "--amplitude-time-steps", "300", "--use-pml", "--pml-type", "cpml"],
 }
 FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf", "3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid",
-             "3d_amp_cpml", "3d_upml_tfsf_hybrid", "3d_upml_point_hybrid"}
+             "3d_amp_cpml", "3d_upml_tfsf_hybrid", "3d_upml_point_hybrid", "3d_drude_upml_hybrid", "3d_drude_hybrid"}
 # the converged step depends on running-maximum comparisons at round-off level: fp64 only
 FP64_ONLY = {"2d_tmz_amp_cpml"}
 
