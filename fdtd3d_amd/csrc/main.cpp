@@ -1237,8 +1237,10 @@ int run(const fdtd::Settings& s) {
   IBox dbox_h = {{0, 0, 0}, {0, 0, 0}};
   if (upml && s.doUseMetamaterials && !chain_regs.empty() && !plain_regs.empty()) dbox_h = chain_regs.back();
   const bool drude_h = !dbox_h.empty();
-  if (scheme == "3d" && sizeof(T) == 4 && v4 && (cpml || upml_h || drude_h) && !percell && !amp && T_h_req > 1 &&
-      T_h_req <= fdtd_tb_max_steps()) {
+  // TF/SF without absorbing layers: the shell is the TF/SF band on the plain kernels
+  const bool tfsf_h = tfsf && !s.doUsePML && !upml;
+  if (scheme == "3d" && sizeof(T) == 4 && v4 && (cpml || upml_h || drude_h || tfsf_h) && !percell && !amp &&
+      T_h_req > 1 && T_h_req <= fdtd_tb_max_steps()) {
     const int Th = T_h_req;
     const int pml[3] = {s.doUsePML ? s.pmlSizeX + (upml ? 1 : 0) : 0, s.doUsePML ? s.pmlSizeY + (upml ? 1 : 0) : 0,
                         s.doUsePML ? s.pmlSizeZ + (upml ? 1 : 0) : 0};
@@ -1363,6 +1365,13 @@ int run(const fdtd::Settings& s) {
         if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
         if (upml) {
           upml_shell(0, hshell[q]);
+        } else if (!cpml) {
+          for (const IBox& w : hshell[q]) {
+            int rb[36];
+            clip36(w, rb);
+            K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, cb, N[0], N[1], N[2],
+                     rb, 0, st, v4));
+          }
         } else {
           for (const IBox& w : hshell[q]) {
             window_boxes(w, 0, wb);
@@ -1376,6 +1385,13 @@ int run(const fdtd::Settings& s) {
         if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
         if (upml) {
           upml_shell(1, hshell[q]);
+        } else if (!cpml) {
+          for (const IBox& w : hshell[q]) {
+            int rb[36];
+            clip36(w, rb);
+            K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, db, N[0], N[1], N[2],
+                     rb + 18, 0, st, v4));
+          }
         } else {
           for (const IBox& w : hshell[q]) {
             window_boxes(w, 3, wb);
@@ -1679,7 +1695,7 @@ int run(const fdtd::Settings& s) {
   std::printf("Parallel grid: 0\n");
   if (T_h > 1)
     std::printf("Backend: native HIP, hybrid passes (blocked core, %d steps per pass; stepped %s%s shell)\n", T_h,
-                upml ? "UPML" : "CPML", tfsf ? " + TF/SF" : "");
+                upml ? "UPML" : (cpml ? "CPML" : "plain"), tfsf ? " + TF/SF" : "");
   else if (T_blk > 1 || T2_blk > 1)
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", std::max(T_blk, T2_blk));
   else if (res1)

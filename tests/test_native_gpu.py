@@ -68,6 +68,10 @@ CASES = {
     "3d_upml_point_hybrid": ["--3d", "--sizex", "72", "--sizey", "76", "--sizez", "80", "--time-steps", "17",
                              "--scene", "vacuum", "--use-pml", "--pml-sizex", "6", "--pml-sizey", "7", "--pml-sizez",
                              "5", "--hybrid-block", "4"],
+    # TF/SF without absorbing layers: hybrid passes with the TF/SF band in the stepped shell
+    "3d_tfsf_hybrid": ["--3d", "--sizex", "100", "--sizey", "96", "--sizez", "104", "--time-steps", "23", "--scene",
+                       "vacuum", "--use-tfsf", "--tfsf-sizex", "9", "--tfsf-sizey", "8", "--tfsf-sizez", "10",
+                       "--angle-teta", "40", "--angle-phi", "25", "--angle-psi", "15"],
     # hybrid passes around a Drude sphere (the dispersive box cut out of the core, its chain whole in every
     # shell step), with the UPML and without absorbing layers (the core reaches the domain faces)
     "3d_drude_upml_hybrid": ["--3d", "--sizex", "96", "--sizey", "88", "--sizez", "92", "--time-steps", "23",
@@ -124,7 +128,8 @@ CASES = {
                         "--use-amp-mode", "--amplitude-time-steps", "300", "--use-pml", "--pml-type", "cpml"],
 }
 FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf", "3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid",
-             "3d_amp_cpml", "3d_upml_tfsf_hybrid", "3d_upml_point_hybrid", "3d_drude_upml_hybrid", "3d_drude_hybrid"}
+             "3d_amp_cpml", "3d_upml_tfsf_hybrid", "3d_upml_point_hybrid", "3d_drude_upml_hybrid", "3d_drude_hybrid",
+             "3d_tfsf_hybrid"}
 # the converged step depends on running-maximum comparisons at round-off level: fp64 only
 FP64_ONLY = {"2d_tmz_amp_cpml"}
 
