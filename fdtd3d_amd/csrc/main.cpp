@@ -20,7 +20,6 @@
 
 #include <algorithm>
 #include <chrono>
-#include <new>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -77,9 +76,12 @@ struct Dev {
     HIP_OK(hipMalloc(&p, n * sizeof(T)));
     HIP_OK(hipMemset(p, 0, n * sizeof(T)));
   }
-  ~Dev() {
+  void reset() {
     if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
   }
+  ~Dev() { reset(); }
 };
 
 template <typename T>
@@ -1986,13 +1988,10 @@ int run_multi(const fdtd::Settings& s) {
   }
   for (auto& q : R) {
     HIP_OK(hipSetDevice(q.dev));
-    for (int c = 0; c < 6; ++c) {
-      q.F[c].~Dev<T>();
-      new (&q.F[c]) Dev<T>();
-      q.G[c].~Dev<T>();
-      new (&q.G[c]) Dev<T>();
-      q.C[c].~Dev<T>();
-      new (&q.C[c]) Dev<T>();
+    for (int c = 0; c < 6; ++c) {  // freed with the rank's device current
+      q.F[c].reset();
+      q.G[c].reset();
+      q.C[c].reset();
     }
     HIP_OK(hipEventDestroy(q.done));
     HIP_OK(hipEventDestroy(q.copied));
