@@ -515,11 +515,12 @@ class BlockedStepping:
         if self.halo is not None:
             self._mark("end")
         with self.prof.phase("shell-copy"):
+            fns = []
             for p in range(self.planes):
                 src = [self.F[p][c] for c in self.comps]
                 dst = [self.F_alt[p][c] for c in self.comps]
-                for b in hp["copy"]:
-                    self.ops.copy_box(src, dst, b)
+                fns += [(lambda b=b, src=src, dst=dst: self.ops.copy_box(src, dst, b)) for b in hp["copy"]]
+            self._par_launches(fns)  # disjoint boxes: side by side on the shell streams
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
 
