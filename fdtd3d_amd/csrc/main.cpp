@@ -209,6 +209,12 @@ int h1d(float* a, const float* b, const float* c, double db, int lo, int hi, voi
 int h1d(double* a, const double* b, const double* c, double db, int lo, int hi, void* s) {
   return fdtd_1d_h_f64(a, b, c, db, lo, hi, s);
 }
+int xfer(float* const* a, float* const* b, int n, int ny, int nz, const int* bx, void* s) {
+  return fdtd_box_xfer_f32(a, b, n, ny, nz, bx, s);
+}
+int xfer(double* const* a, double* const* b, int n, int ny, int nz, const int* bx, void* s) {
+  return fdtd_box_xfer_f64(a, b, n, ny, nz, bx, s);
+}
 int setvs(float* f, const long long* o, int n, double v, void* s) { return fdtd_set_values_f32(f, o, n, v, s); }
 int setvs(double* f, const long long* o, int n, double v, void* s) { return fdtd_set_values_f64(f, o, n, v, s); }
 int curl_gen(float* out, const float* inp, const float* const* srcs, const int* axes, const int* signs, int nt,
@@ -1027,7 +1033,37 @@ int run(const fdtd::Settings& s) {
                            {{std::max(0, N[0] - ppx), 0, 0}, {N[0], N[1], N[2]}},
                            {{ppx, 0, 0}, {N[0] - ppx, std::min(ppy, N[1]), N[2]}},
                            {{ppx, std::max(0, N[1] - ppy), 0}, {N[0] - ppx, N[1], N[2]}}};
-  auto pml2d_upml = [&](int kind) {
+  // the plain 2D kernels of one kind over the per-component update boxes
+  // clipped to `region`
+  auto plain2d = [&](int kind, const IBox& region) {
+    int ib[36];
+    for (int c = 0; c < 6; ++c) {
+      IBox ub;
+      for (int a = 0; a < 3; ++a) {
+        ub.lo[a] = boxes[6 * c + a];
+        ub.hi[a] = boxes[6 * c + 3 + a];
+      }
+      const IBox b = box_and(ub, region);
+      for (int a = 0; a < 3; ++a) {
+        ib[6 * c + a] = b.empty() ? 0 : b.lo[a];
+        ib[6 * c + 3 + a] = b.empty() ? 0 : b.hi[a];
+      }
+    }
+    const bool tm = scheme == "tmz";
+    if (kind == 0) {
+      if (tm)
+        K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], ib + 12, st));
+      else
+        K_OK(tez_e(F[0].p, F[1].p, F[5].p, C[0].p, C[1].p, percell ? 1.0 : cb, N[0], N[1], ib, st));
+    } else {
+      if (tm)
+        K_OK(tmz_h(F[3].p, F[4].p, F[2].p, C[3].p, C[4].p, percell ? 1.0 : db, N[0], N[1], ib + 18, st));
+      else
+        K_OK(tez_h(F[5].p, F[0].p, F[1].p, C[5].p, percell ? 1.0 : db, N[0], N[1], ib + 30, st));
+    }
+  };
+  // the D/B chain of one kind on the PML strips (+ level rotation)
+  auto upml2d_chain = [&](int kind) {
     for (int c = 3 * kind; c < 3 * kind + 3; ++c) {
       if (!present[c]) continue;
       const T* srcs[2];
@@ -1056,32 +1092,10 @@ int run(const fdtd::Settings& s) {
       }
       std::swap(p2.D[c][0], p2.D[c][1]);
     }
-    // the inner box through the plain kernels (per-component boxes clipped)
-    int ib[36];
-    for (int c = 0; c < 6; ++c) {
-      IBox ub;
-      for (int a = 0; a < 3; ++a) {
-        ub.lo[a] = boxes[6 * c + a];
-        ub.hi[a] = boxes[6 * c + 3 + a];
-      }
-      const IBox b = box_and(ub, inner2);
-      for (int a = 0; a < 3; ++a) {
-        ib[6 * c + a] = b.empty() ? 0 : b.lo[a];
-        ib[6 * c + 3 + a] = b.empty() ? 0 : b.hi[a];
-      }
-    }
-    const bool tm = scheme == "tmz";
-    if (kind == 0) {
-      if (tm)
-        K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], ib + 12, st));
-      else
-        K_OK(tez_e(F[0].p, F[1].p, F[5].p, C[0].p, C[1].p, percell ? 1.0 : cb, N[0], N[1], ib, st));
-    } else {
-      if (tm)
-        K_OK(tmz_h(F[3].p, F[4].p, F[2].p, C[3].p, C[4].p, percell ? 1.0 : db, N[0], N[1], ib + 18, st));
-      else
-        K_OK(tez_h(F[5].p, F[0].p, F[1].p, C[5].p, percell ? 1.0 : db, N[0], N[1], ib + 30, st));
-    }
+  };
+  auto pml2d_upml = [&](int kind) {
+    upml2d_chain(kind);
+    plain2d(kind, inner2);  // every sigma vanishes there
   };
   // amplitude mode state: running maxima of every component, one [x][6][y][z]
   // buffer (the layout of the blocked amplitude kernel), per-step changed
@@ -1307,6 +1321,94 @@ int run(const fdtd::Settings& s) {
         if (present[c] && !G[c].p) G[c].alloc(cells);
     }
   }
+  // 2D hybrid passes (models/blocking.py on yee2d_tb.hip): every T steps the
+  // 2D blocked kernel advances the core (cells at least T + 2 beyond the
+  // absorbing strips and the TF/SF targets) F -> G; the shell strips step in
+  // place in F with a band T - s deep into the core at step s (absorbing
+  // strips whole), are copied into G, and the buffers swap
+  int T2_h = 1;
+  std::vector<IBox> h2shell[8], h2copy;
+  IBox h2core = {{0, 0, 0}, {0, 0, 0}};
+  if (dim == 2 && (cpml || (upml && !s.doUseMetamaterials)) && !percell && !amp && !s.doUseSplitKernels &&
+      N[1] % (16 / (int)sizeof(T)) == 0) {
+    const int Th = s.hybridBlock == 0 ? 7 : s.hybridBlock;
+    if (Th > 1 && Th <= T2_max) {
+      const int pml[2] = {s.pmlSizeX + (upml ? 1 : 0), s.pmlSizeY + (upml ? 1 : 0)};
+      const int tfs[2] = {s.tfsfSizeX, s.tfsfSizeY};
+      IBox K = {{0, 0, 0}, {N[0], N[1], 1}};
+      for (int a = 0; a < 2; ++a) {
+        const int edge = std::max(pml[a], tfsf ? tfs[a] + 1 : 0);
+        K.lo[a] = edge + Th + 2;
+        K.hi[a] = N[a] - edge - Th - 2;
+      }
+      if (!K.empty() && K.volume() >= (long long)cells / 4) {
+        T2_h = Th;
+        h2core = K;
+        const IBox alloc = {{0, 0, 0}, {N[0], N[1], 1}};
+        for (int q = 0; q < T2_h; ++q) {
+          IBox Kd = K;
+          for (int a = 0; a < 2; ++a) {
+            Kd.lo[a] += T2_h - q;
+            Kd.hi[a] -= T2_h - q;
+          }
+          for (const IBox& w : box_minus(alloc, Kd))
+            if (!w.empty()) h2shell[q].push_back(w);
+        }
+        for (const IBox& b : box_minus(alloc, K))
+          if (!b.empty()) h2copy.push_back(b);
+        for (int c = 0; c < 6; ++c)
+          if (present[c] && !G[c].p) G[c].alloc(cells);
+      }
+    }
+  }
+  auto hybrid2d_pass = [&](int t) {
+    const int ord[2][3] = {{2, 3, 4}, {0, 1, 5}};  // TMz Ez Hx Hy, TEz Ex Ey Hz
+    const int m = scheme == "tmz" ? 0 : 1;
+    const int* o = ord[m];
+    const T* ei[2] = {F[o[0]].p, m ? F[o[1]].p : nullptr};
+    const T* hi[2] = {F[m ? o[2] : o[1]].p, m ? nullptr : F[o[2]].p};
+    T* eo[2] = {G[o[0]].p, m ? G[o[1]].p : nullptr};
+    T* ho[2] = {G[m ? o[2] : o[1]].p, m ? nullptr : G[o[2]].p};
+    const T* cs[3] = {C[o[0]].p, C[o[1]].p, C[o[2]].p};
+    int b2[18];
+    for (int q = 0; q < 3; ++q) std::memcpy(b2 + 6 * q, boxes + 6 * o[q], 6 * sizeof(int));
+    const int ob[6] = {h2core.lo[0], h2core.lo[1], 0, h2core.hi[0], h2core.hi[1], 1};
+    const bool in_core = sp[0] >= h2core.lo[0] && sp[0] < h2core.hi[0] && sp[1] >= h2core.lo[1] &&
+                         sp[1] < h2core.hi[1];
+    const int src[3] = {sp[0], sp[1], point_src && in_core ? (m ? 2 : 0) : -1};
+    double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int l = 0; l < T2_h; ++l) vals[l] = src_val(t + l);
+    K_OK(tb2d(m, ei, hi, eo, ho, cs, cb, db, N[0], N[1], b2, ob, T2_h, src, vals, st));
+    for (int q = 0; q < T2_h; ++q) {
+      const double sv = src_val(t + q);
+      if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
+      if (upml) {
+        upml2d_chain(0);
+        for (const IBox& w : h2shell[q]) plain2d(0, box_and(w, inner2));
+      } else {
+        for (const IBox& w : h2shell[q]) plain2d(0, w);
+        pml2d_cpml(0);
+      }
+      if (tfsf) tfsf_kind(0);
+      if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));
+      if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
+      if (upml) {
+        upml2d_chain(1);
+        for (const IBox& w : h2shell[q]) plain2d(1, box_and(w, inner2));
+      } else {
+        for (const IBox& w : h2shell[q]) plain2d(1, w);
+        pml2d_cpml(1);
+      }
+      if (tfsf) tfsf_kind(1);
+    }
+    T* src3[3] = {F[o[0]].p, F[o[1]].p, F[o[2]].p};
+    T* dst3[3] = {G[o[0]].p, G[o[1]].p, G[o[2]].p};
+    for (const IBox& b : h2copy) {
+      const int bx[6] = {b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2]};
+      K_OK(xfer(src3, dst3, 3, N[1], N[2], bx, st));
+    }
+    for (int q = 0; q < 3; ++q) std::swap(F[o[q]].p, G[o[q]].p);
+  };
   auto window_boxes = [&](const IBox& w, int c0, int* out) {
     for (int c = c0; c < c0 + 3; ++c) {
       IBox b;
@@ -1419,6 +1521,11 @@ int run(const fdtd::Settings& s) {
       hybrid_pass(t);
       t += T_h;
       n -= T_h;
+    }
+    while (T2_h > 1 && n >= T2_h) {
+      hybrid2d_pass(t);
+      t += T2_h;
+      n -= T2_h;
     }
     if (res1 && n > 0) {
       std::vector<T> hv(n);
@@ -1695,7 +1802,10 @@ int run(const fdtd::Settings& s) {
   std::printf("Value type: %s\n", Api<T>::name);
   std::printf("\n-------- Details --------\n");
   std::printf("Parallel grid: 0\n");
-  if (T_h > 1)
+  if (T2_h > 1)
+    std::printf("Backend: native HIP, hybrid passes (2D blocked core, %d steps per pass; stepped %s%s shell)\n",
+                T2_h, upml ? "UPML" : "CPML", tfsf ? " + TF/SF" : "");
+  else if (T_h > 1)
     std::printf("Backend: native HIP, hybrid passes (blocked core, %d steps per pass; stepped %s%s shell)\n", T_h,
                 upml ? "UPML" : (cpml ? "CPML" : "plain"), tfsf ? " + TF/SF" : "");
   else if (T_blk > 1 || T2_blk > 1)

@@ -117,6 +117,13 @@ CASES = {
                            "--scene", "sphere", "--sphere-center-x", "28", "--sphere-center-y", "30",
                            "--sphere-radius", "6", "--sphere-eps", "4", "--use-pml", "--pml-sizex", "5",
                            "--pml-sizey", "6"],
+    # 2D hybrid passes (yee2d_tb.hip core + stepped strips): CPML + oblique TF/SF, UPML + point source
+    "2d_tmz_cpml_tfsf_hybrid": ["--2d", "--sizex", "200", "--sizey", "192", "--time-steps", "23", "--scene",
+                                "vacuum", "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6", "--same-size-pml",
+                                "--use-tfsf", "--tfsf-sizex", "10", "--tfsf-sizey", "12", "--angle-phi", "35"],
+    "2d_tez_upml_point_hybrid": ["--2d", "--2d-mode", "tez", "--sizex", "180", "--sizey", "176", "--time-steps",
+                                 "17", "--scene", "vacuum", "--use-pml", "--pml-sizex", "8", "--pml-sizey", "7",
+                                 "--hybrid-block", "5"],
     # amplitude mode: 3D vacuum (fp32: blocked passes with the running maxima folded in), CPML (per step),
     # 2D with the CPML until the stable state (fp64: the same converged step as the Python driver)
     "3d_amp": ["--3d", "--sizex", "32", "--sizey", "28", "--sizez", "24", "--time-steps", "6", "--scene", "vacuum",
