@@ -983,6 +983,13 @@ class YeeScheme(BlockedStepping):
             self._update_chain_regions(kind, p, None if self.halo is None else self._window(kind), tfsf_here,
                                        plain_windows=windows)
             windows = []
+        fused_cpml = self.use_cpml and getattr(self.ops, "fused_cpml_ok", lambda *a: False)(self)
+        # hybrid shell without the folded CPML kernels: the psi slabs lie inside
+        # the shell, so their corrections run once per slab after all windows
+        # (one launch per slab instead of one per slab and window)
+        cpml_once = (self.use_cpml and not fused_cpml and self.hybrid is not None and len(windows) > 1
+                     and self.halo is None)
+
         def one(w):
             if chain:
                 self._update_chain_regions(kind, p, w, tfsf_here)
@@ -992,12 +999,12 @@ class YeeScheme(BlockedStepping):
                 for c in comps:
                     self._upml_region(kind, c, p, boxes[c])
                 return
-            if self.use_cpml and getattr(self.ops, "fused_cpml_ok", lambda *a: False)(self):
+            if fused_cpml:
                 # CPML folded into the update kernel (yee3d_cpml.hip)
                 self.ops.curl_update_cpml(kind, boxes, F, F, self.cb, self.cpml.kernel_table(kind, p))
             else:
                 self.ops.curl_update(kind, boxes, F, F, self.cb)
-                if self.use_cpml:
+                if self.use_cpml and not cpml_once:
                     self.cpml.apply(kind, p, boxes)
             if tfsf_here:
                 inc = self.hinc[p] if kind == "E" else self.einc[p]
@@ -1012,6 +1019,9 @@ class YeeScheme(BlockedStepping):
         else:
             for w in windows:
                 one(w)
+        if cpml_once:
+            alloc = self.domain.allocated_global()
+            self.cpml.apply(kind, p, {c: self.local_box(c, alloc) for c in comps})
         if use_tfsf and tfsf_once:
             inc = self.hinc[p] if kind == "E" else self.einc[p]
             alloc = self.domain.allocated_global()
@@ -1040,7 +1050,8 @@ class YeeScheme(BlockedStepping):
         n = int(getattr(self.cfg, "shell_streams", 0))
         if n <= 0:
             n = 3 if self.ops.name == "hip" else 1
-        if n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda":
+        if (n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda"
+                or getattr(self, "_capturing", False)):
             for f in fns:
                 f()
             return
@@ -1636,6 +1647,9 @@ class YeeScheme(BlockedStepping):
             counter = torch.zeros(1, dtype=torch.int32, device=self.device)
             graph = torch.cuda.CUDAGraph()
             self._graph_src = (tab, counter, t0)
+            # one stream inside the graph (cross-stream joins as graph nodes
+            # measured slower than the plain chain of small kernels)
+            self._capturing = True
             try:
                 with torch.cuda.graph(graph):
                     for _ in range(P):
@@ -1643,6 +1657,7 @@ class YeeScheme(BlockedStepping):
                     self.ops.counter_add(counter, G)
             finally:
                 self._graph_src = None
+                self._capturing = False
             self.t = t0  # capture records the kernels, it does not run them
             g = self._hgraph = {"key": key, "reps": reps, "graph": graph, "tab": tab, "counter": counter}
         g["tab"][:, :reps * G].copy_(vals)
