@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r4k3
+O=gpurun_out/r4k4
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1 \
   || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
