@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -1446,6 +1447,31 @@ int run(const fdtd::Settings& s) {
                    rb + 18, 0, st, v4));
       }
   };
+  // independent shell-window launches of a half step side by side on three
+  // streams (the tail of one small launch overlaps the next; models/scheme.py
+  // _par_launches), joined back into `st`
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
+  if (T_h > 1) {
+    for (int q = 0; q < 2; ++q) {
+      HIP_OK(hipStreamCreateWithFlags(&side[q], hipStreamNonBlocking));
+      HIP_OK(hipEventCreateWithFlags(&join_ev[q], hipEventDisableTiming));
+    }
+    HIP_OK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+  }
+  auto par_windows = [&](const std::vector<IBox>& wins, const std::function<void(const IBox&, hipStream_t)>& fn) {
+    if (wins.size() <= 1 || !side[0]) {
+      for (const IBox& w : wins) fn(w, st);
+      return;
+    }
+    HIP_OK(hipEventRecord(fork_ev, st));
+    for (int q = 0; q < 2; ++q) HIP_OK(hipStreamWaitEvent(side[q], fork_ev, 0));
+    for (size_t n = 0; n < wins.size(); ++n) fn(wins[n], n % 3 == 0 ? st : side[n % 3 - 1]);
+    for (int q = 0; q < 2; ++q) {
+      HIP_OK(hipEventRecord(join_ev[q], side[q]));
+      HIP_OK(hipStreamWaitEvent(st, join_ev[q], 0));
+    }
+  };
   auto hybrid_pass = [&](int t) {
     if constexpr (sizeof(T) == 4) {
       const T* ei[3] = {F[0].p, F[1].p, F[2].p};
@@ -1470,19 +1496,20 @@ int run(const fdtd::Settings& s) {
         if (upml) {
           upml_shell(0, hshell[q]);
         } else if (!cpml) {
-          for (const IBox& w : hshell[q]) {
+          par_windows(hshell[q], [&](const IBox& w, hipStream_t ss) {
             int rb[36];
             clip36(w, rb);
             K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, cb, N[0], N[1], N[2],
-                     rb, 0, st, v4));
-          }
+                     rb, 0, ss, v4));
+          });
         } else {
-          for (const IBox& w : hshell[q]) {
-            window_boxes(w, 0, wb);
+          par_windows(hshell[q], [&](const IBox& w, hipStream_t ss) {
+            int wb2[18];
+            window_boxes(w, 0, wb2);
             K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, nullptr, nullptr,
-                                             nullptr, cb, N[0], N[1], N[2], wb, 0, cpt.P[0].data(), cpt.I[0].data(),
-                                             st));
-          }
+                                             nullptr, cb, N[0], N[1], N[2], wb2, 0, cpt.P[0].data(),
+                                             cpt.I[0].data(), ss));
+          });
         }
         if (tfsf) tfsf_kind(0);
         if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));
@@ -1490,19 +1517,20 @@ int run(const fdtd::Settings& s) {
         if (upml) {
           upml_shell(1, hshell[q]);
         } else if (!cpml) {
-          for (const IBox& w : hshell[q]) {
+          par_windows(hshell[q], [&](const IBox& w, hipStream_t ss) {
             int rb[36];
             clip36(w, rb);
             K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, db, N[0], N[1], N[2],
-                     rb + 18, 0, st, v4));
-          }
+                     rb + 18, 0, ss, v4));
+          });
         } else {
-          for (const IBox& w : hshell[q]) {
-            window_boxes(w, 3, wb);
+          par_windows(hshell[q], [&](const IBox& w, hipStream_t ss) {
+            int wb2[18];
+            window_boxes(w, 3, wb2);
             K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, nullptr, nullptr,
-                                             nullptr, db, N[0], N[1], N[2], wb, 0, cpt.P[1].data(), cpt.I[1].data(),
-                                             st));
-          }
+                                             nullptr, db, N[0], N[1], N[2], wb2, 0, cpt.P[1].data(),
+                                             cpt.I[1].data(), ss));
+          });
         }
         if (tfsf) tfsf_kind(1);
       }
@@ -1848,6 +1876,11 @@ int run(const fdtd::Settings& s) {
       }
     }
   }
+  for (int q = 0; q < 2; ++q) {
+    if (side[q]) HIP_OK(hipStreamDestroy(side[q]));
+    if (join_ev[q]) HIP_OK(hipEventDestroy(join_ev[q]));
+  }
+  if (fork_ev) HIP_OK(hipEventDestroy(fork_ev));
   HIP_OK(hipStreamDestroy(st));
   return 0;
 }
