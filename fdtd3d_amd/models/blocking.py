@@ -238,72 +238,17 @@ class BlockedStepping:
         # core margin to every irregular cell: T + 1 clears the stencil reach
         # of a T-step pass (checked below; T + 2 when a staggered component's
         # irregular box sticks out one cell further)
-        mode = getattr(cfg, "hybrid_tfsf", "auto")
-        if mode not in ("auto", "core", "shell"):
-            raise ValueError("hybrid_tfsf: auto, core or shell, got %r" % (mode,))
-        if self._tfsf_core_ok() and mode == "core":
-            # TF/SF faces inside the core: the blocked kernel applies their
-            # corrections (TfsfSets), so the shell is only the absorbing
-            # layers plus margin -- 512^3 CPML + TF/SF (reference sizes PML 10,
-            # TF/SF 20): a 21-deep instead of a 32-deep stepped shell.  Opt-in:
-            # measured slower (66.9k vs 81.0k Mcells/s; the 11-cell TF/SF ring
-            # boxes run the TfsfSets kernel at 14-42 G cell-steps/s, 0.59 ms
-            # per step against the 0.17 ms the thinner shell saves;
-            # profiles/tfsf_core_r4.md)
-            for m in (T + 1, T + 2):
-                plan = self._hybrid_plan_m(T, m, in_kernel_tfsf=True)
-                if plan is not None:
-                    return self._split_tfsf_core(plan, T)
-        if mode == "core" and cfg.use_tfsf:
-            return None
         for m in (T + 1, T + 2):
             plan = self._hybrid_plan_m(T, m)
             if plan is not None:
                 return plan
         return None
 
-    def _tfsf_core_ok(self) -> bool:
-        """The core pass can apply the TF/SF corrections itself: serial 3D
-        runs with TfsfSets (incident direction along x or y; fp32 on HIP)
-        and no UPML chain box holding a target (D-form corrections)."""
-        cfg = self.cfg
-        if not cfg.use_tfsf or cfg.scheme != "3d" or self.halo is not None:
-            return False
-        if getattr(self, "tfsf_sets", None) is None or not getattr(self.ops, "tfsf_sets_ok", False):
-            return False
-        return not (self.use_upml_chain and getattr(self, "chain_regions", None) is None)
-
-    def _split_tfsf_core(self, plan, T: int):
-        """Split the core boxes into the part no TF/SF target can reach
-        within a pass (plain blocked kernel) and the ring around the faces
-        (blocked kernel with the TfsfSets corrections, ~2.5x its cost per
-        cell): ``plan["core_tf"][n]`` says which."""
-        boxes = [b for b in self.tfsf_bbox.values() if b is not None]
-        cores, flags = [], []
-        for ob in plan["core"]:
-            inner = ob
-            for b in boxes:
-                # targets lie on the surface of their bbox: its interior shrunk
-                # by the pass's reach (T + 1) plus one holds none within reach
-                sh = (tuple(b[0][d] + T + 2 for d in range(3)), tuple(b[1][d] - T - 2 for d in range(3)))
-                inner = box_intersect(inner, sh)
-            g = (tuple(inner[0][d] - T - 1 for d in range(3)), tuple(inner[1][d] + T + 1 for d in range(3)))
-            if box_empty(inner) or self._tfsf_targets_in(g):
-                cores.append(ob)
-                flags.append(True)
-                continue
-            cores.append(inner)
-            flags.append(False)
-            for r in box_subtract(ob, inner):
-                if not box_empty(r):
-                    cores.append(r)
-                    flags.append(True)
-        return dict(plan, core=cores, core_tf=flags, tfsf_in_core=True)
-
-    def _hybrid_plan_m(self, T: int, m: int, in_kernel_tfsf: bool = False):
-        """Hybrid plan with core margin ``m``; ``in_kernel_tfsf``: the core
-        pass applies the TF/SF corrections itself (TfsfSets), so the TF/SF
-        faces may lie inside the core."""
+    def _hybrid_plan_m(self, T: int, m: int):
+        """Hybrid plan with core margin ``m``: the TF/SF faces lie in the
+        stepped shell.  (Applying them in the blocked core instead -- a thinner
+        shell, the TfsfSets kernel variant on the ring around the faces or on
+        the whole core -- measured slower at 512^3: profiles/tfsf_core_r4.md.)"""
         dom = self.domain
         cfg = self.cfg
         size = cfg.size
@@ -316,7 +261,7 @@ class BlockedStepping:
             edge = 0
             if cfg.use_pml:
                 edge = max(edge, self.layout.pml_size[a])
-            if cfg.use_tfsf and not in_kernel_tfsf:
+            if cfg.use_tfsf:
                 edge = max(edge, cfg.tfsf_size[a] + 1)
             if edge > 0:
                 lo[a], hi[a] = edge + m, size[a] - edge - m
@@ -376,7 +321,7 @@ class BlockedStepping:
             g = grow(ob, T + 1)
             if any(not box_empty(box_intersect(g, b)) for b in irregular):
                 return None
-            if cfg.use_tfsf and not in_kernel_tfsf and self._tfsf_targets_in(dom.to_local(g)):
+            if cfg.use_tfsf and self._tfsf_targets_in(dom.to_local(g)):
                 return None
         if self.halo is not None:
             # decomposed: each rank's core is its owned part of the global core
@@ -477,26 +422,10 @@ class BlockedStepping:
             # the deep-halo windows from sub-step 0, whatever an earlier
             # shorter pass (periodic work, a tail) left behind
             self.sub_step = 0
-        tfs = []
-        for p in range(self.planes):
-            tf = None
-            if self.cfg.use_tfsf and self.hybrid.get("tfsf_in_core"):
-                # the pass kernel advances the incident line for the core;
-                # the stepped shell advances it again from the same state
-                line0 = (self.einc[p].clone(), self.hinc[p].clone())
-                tf = (self._tfsf_pass(p, T), line0)
-            tfs.append(tf)
-
-        tf_box = dict(zip(hp["core"], hp.get("core_tf", [True] * len(hp["core"]))))
-
         def core(boxes):
             for p in range(self.planes):
-                tf = tfs[p][0] if tfs[p] is not None else None
                 for ob in boxes:
-                    if tf is not None and tf_box.get(ob, True):
-                        self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p], tfsf=tf)
-                    else:
-                        self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
+                    self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
 
         with self.prof.phase("blocked-core"):
             core(core_now)
@@ -506,10 +435,6 @@ class BlockedStepping:
             self._mark("wait")
             with self.prof.phase("blocked-core"):
                 core(core_later)
-        for p in range(self.planes):
-            if tfs[p] is not None:
-                self.einc[p].copy_(tfs[p][1][0])
-                self.hinc[p].copy_(tfs[p][1][1])
         for s in range(T):
             self.step(hp["shells"][s])
         if self.halo is not None:

@@ -105,7 +105,6 @@ class SchemeConfig:
     cpml_alpha_max: float = 0.0
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
-    hybrid_tfsf: str = "auto"                # hybrid + TF/SF: faces in the blocked core ("core"), the shell, or auto
     shell_streams: int = 0                   # hybrid shell: streams for the independent window launches (0 auto)
     hybrid_graph: str = "auto"               # hybrid passes replayed from HIP graphs (auto / off)
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
@@ -143,7 +142,7 @@ class SchemeConfig:
             use_fused=not s.doUseSplitKernels, cpml_kappa_max=s.cpmlKappaMax, cpml_alpha_max=s.cpmlAlphaMax,
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
             amplitude_check_steps=s.amplitudeCheckSteps,
-            hybrid_block=s.hybridBlock, hybrid_tfsf=s.hybridTfsf, shell_streams=s.shellStreams, hybrid_graph=s.hybridGraph,
+            hybrid_block=s.hybridBlock, shell_streams=s.shellStreams, hybrid_graph=s.hybridGraph,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
@@ -1600,7 +1599,7 @@ class YeeScheme(BlockedStepping):
         if (hp is None or self.cfg.scheme not in ("tmz", "tez") or self.halo is not None or self.hooks
                 or self.ops.name != "hip" or self.device.type != "cuda" or self.prof.enabled
                 or not hasattr(self.ops, "inc_step_e_tab") or not hasattr(self.ops, "counter_add")
-                or getattr(self.cfg, "hybrid_graph", "auto") == "off" or hp.get("tfsf_in_core")):
+                or getattr(self.cfg, "hybrid_graph", "auto") == "off"):
             return 0
         if self.point_source is not None and self.point_source[1] is not None:
             li = self.point_source[1]

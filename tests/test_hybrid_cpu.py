@@ -130,9 +130,6 @@ RANDOM_CASES = [
     ("cpml-tfsf-box", dict(size=(64, 80, 56), pml_size=(4, 6, 5), scene="vacuum", use_pml=True, pml_type="cpml",
                            use_tfsf=True, tfsf_size=(5, 6, 5)), 4, 9),
     ("upml-point-box", dict(size=(60, 52, 76), pml_size=(5, 4, 6), scene="vacuum", use_pml=True), 3, 8),
-    # TF/SF faces inside the blocked core (TfsfSets), ring boxes around the plain inner core
-    ("cpml-tfsf-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, hybrid_tfsf="core"), 4, 11),
-    ("upml-tfsf-core-y", dict(scene="vacuum", use_pml=True, use_tfsf=True, phi=90.0, hybrid_tfsf="core"), 3, 8),
 ]
 
 
@@ -152,7 +149,6 @@ def test_hybrid_random_fields_match_stepped(name, extra, T, steps):
         s.init_grids()
         if hb > 1:
             assert s.hybrid is not None, "hybrid plan rejected"
-            assert bool(s.hybrid.get("tfsf_in_core")) == (kw.get("hybrid_tfsf") == "core")
         s.randomize_fields(seed=5)
         s.perform_steps()
         runs.append(s)
