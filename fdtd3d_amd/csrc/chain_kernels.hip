@@ -241,8 +241,16 @@ __device__ __forceinline__ void chain_finish(const ChainComp<T>& q, bool kind_e,
 
 // Thread mapping: the (y, z) cells of the launch box are flattened (z
 // fastest), so narrow boxes (a 10-cell z slab) still fill every lane and wide
-// rows stay coalesced; each thread walks CHX planes along x.
+// rows stay coalesced; each thread walks chain_chx() planes along x (default
+// CHX; FDTD3D_CHAIN_CHX overrides it, read once per library).
 constexpr int CHX = 8;
+static inline int chain_chx() {
+  static const int v = [] {
+    const char* e = getenv("FDTD3D_CHAIN_CHX");
+    return e && atoi(e) > 0 ? atoi(e) : CHX;
+  }();
+  return v;
+}
 
 // Plain Yee update of one component of one cell (mode 2 of chain_finish):
 // the cells of a dispersive box outside the material's per-row z range.
@@ -281,7 +289,7 @@ __device__ __forceinline__ int2 row_range(const RowRanges& rr, int x, int y) {
 
 template <typename T, bool DRUDE, bool CELL>
 __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q1, ChainComp<T> q2, int kind_e,
-                                                 int ny, int nz, Box3 U, RowRanges rr) {
+                                                 int ny, int nz, Box3 U, RowRanges rr, int chx) {
   const int W = U.hi[2] - U.lo[2];
   const int H = U.hi[1] - U.lo[1];
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -289,8 +297,8 @@ __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q
   int n[3];
   n[1] = U.lo[1] + (int)(idx / W);
   n[2] = U.lo[2] + (int)(idx % W);
-  const int i0 = U.lo[0] + (int)blockIdx.y * CHX;
-  const int i1 = min(i0 + CHX, U.hi[0]);
+  const int i0 = U.lo[0] + (int)blockIdx.y * chx;
+  const int i1 = min(i0 + chx, U.hi[0]);
   const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
   // dispersive launches with a row table: the next plane's range is loaded
   // one trip ahead, so the path decision never waits on its own load
@@ -520,8 +528,9 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
     }
   }
   const long long cells = (long long)(U.hi[2] - U.lo[2]) * (U.hi[1] - U.lo[1]);
-  dim3 grid(cdiv(cells, 256), cdiv(U.hi[0] - U.lo[0], CHX));
-#define CH_LAUNCH(D, C) k_chain3d<T, D, C><<<grid, 256, 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U, rr)
+  const int chx = chain_chx();
+  dim3 grid(cdiv(cells, 256), cdiv(U.hi[0] - U.lo[0], chx));
+#define CH_LAUNCH(D, C) k_chain3d<T, D, C><<<grid, 256, 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U, rr, chx)
   if (drude) {
     if (cell) CH_LAUNCH(true, true);
     else CH_LAUNCH(true, false);
