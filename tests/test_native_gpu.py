@@ -286,3 +286,56 @@ def test_native_parallel_grid_matches_python(case, tmp_path, gpu):
         tol = 1e-11 if dtype == "f64" else 2e-5
         for err, _ in errs:
             assert err <= tol * peak, (kind, err, peak)
+
+
+# checkpoints written and resumed by either driver (csrc/main.cpp ckpt_save / ckpt_load, io/checkpoint.py):
+# plain media, whose state is the field components; (argv, resume step, final step)
+CKPT = {
+    "3d_blocked_vacuum": (["--3d", "--sizex", "28", "--sizey", "20", "--sizez", "24", "--scene", "vacuum",
+                           "--time-block", "3"], 7, 19),
+    "3d_sphere": (["--3d", "--sizex", "32", "--same-size", "--scene", "sphere", "--sphere-center-x", "16",
+                   "--sphere-center-y", "16", "--sphere-center-z", "16", "--sphere-radius", "6", "--sphere-eps", "4"],
+                  6, 15),
+    "2d_tmz": (["--2d", "--sizex", "60", "--sizey", "52", "--scene", "vacuum", "--time-block", "5"], 9, 23),
+    "1d": (["--1d", "--sizex", "300", "--scene", "vacuum", "--source", "gaussian", "--gaussian-width", "8",
+            "--gaussian-delay", "30"], 13, 40),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(CKPT))
+def test_native_checkpoint_roundtrip(case, tmp_path, gpu):
+    """A native checkpoint resumed by the native driver and by the Python
+    driver, and the full run, end on the same fields (fp64)."""
+    exe = native.executable()
+    argv, k, n = CKPT[case]
+    argv = argv + ["--dtype", "f64"]
+    py = ["--backend", "torch", "--device", "cpu"]
+    d = {x: tmp_path / x for x in ("a", "nat", "py", "full")}
+
+    def nat(extra):
+        r = subprocess.run([exe] + argv + extra, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return r.stdout
+
+    nat(["--time-steps", str(k), "--checkpoint-dir", str(d["a"])])
+    assert (d["a"] / ("checkpoint[%d]_rank-0.json" % k)).exists()
+    out = nat(["--time-steps", str(n), "--load-from-file", str(d["a"]), "--checkpoint-dir", str(d["nat"])])
+    assert "Number of time steps: %d (%d timed" % (n, n - k) in out, out
+    assert py_run(argv + py + ["--time-steps", str(n), "--load-from-file", str(d["a"]), "--checkpoint-dir",
+                               str(d["py"])], out=io.StringIO()) == 0
+    assert py_run(argv + py + ["--time-steps", str(n), "--checkpoint-dir", str(d["full"])], out=io.StringIO()) == 0
+    shape, scheme = _shape(argv)
+    for kind in "EH":
+        got = {}
+        for c in COMPS[scheme]:
+            if c[0] != kind:
+                continue
+            name = "current[%d]_rank-0_%s.dat" % (n, c)
+            ref = np.fromfile(d["full"] / name, dtype=np.float64).reshape(shape)
+            got[c] = [np.abs(np.fromfile(d[x] / name, dtype=np.float64).reshape(shape) - ref).max()
+                      for x in ("nat", "py")] + [np.abs(ref).max()]
+        peak = max(v[-1] for v in got.values())
+        assert peak > 0
+        for c, v in got.items():
+            assert max(v[:2]) <= 1e-11 * peak, (c, v)
