@@ -1813,6 +1813,28 @@ int run(const fdtd::Settings& s) {
     }
   };
 
+  // --checkpoint-step P: a checkpoint after every step t with t % P == 0 (the
+  // Python driver's periodic hook), the passes ending there
+  auto run_ckpt = [&](int t, int n) {
+    const int P = s.checkpointDir.empty() ? 0 : s.checkpointStep;
+    if (P <= 0) {
+      run_steps(t, n);
+      return;
+    }
+    const int end = t + n;
+    while (t < end) {
+      const int nxt = std::min(end, (t / P + 1) * P);
+      run_steps(t, nxt - t);
+      t = nxt;
+      if (t % P == 0) {
+        HIP_OK(hipStreamSynchronize(st));
+        if (!ckpt_save<T>(s, scheme, N, present, F, t, dx, dt)) {
+          std::fprintf(stderr, "fdtd3d: cannot write the checkpoint to %s\n", s.checkpointDir.c_str());
+          std::exit(1);
+        }
+      }
+    }
+  };
   // --load-from-file: the run continues from the checkpoint's step up to --time-steps
   int t0 = 0;
   if (!s.loadFromFile.empty()) {
@@ -1822,13 +1844,13 @@ int run(const fdtd::Settings& s) {
   }
   const int steps = std::max(0, s.numTimeSteps - t0);
   const int warm = std::max(0, std::min(s.warmupSteps, steps));
-  run_steps(t0, warm);  // untimed (they advance the simulation)
+  run_ckpt(t0, warm);  // untimed (they advance the simulation)
   HIP_OK(hipStreamSynchronize(st));
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, st));
-  run_steps(t0 + warm, steps - warm);
+  run_ckpt(t0 + warm, steps - warm);
   // amplitude mode (models/scheme.py perform_amplitude_steps): check periods
   // of K steps whose changed-cell counts accumulate on the device, read once
   // per period; the run ends with the period in which a step (after the
@@ -2361,17 +2383,17 @@ int main(int argc, char** argv) {
                       (s.dimension == 3 && !s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials &&
                        !s.doUseAmplitudeMode && !s.doUseNTFF && (s.scene == "vacuum" || s.scene == "sphere") &&
                        s.topologySizeY <= 1 && s.topologySizeZ <= 1 && !s.doUseSplitKernels);
-  // checkpoints / resume: plain media (state = the field components), saved at the end of the run
+  // checkpoints / resume: plain media (state = the field components)
   const bool ckpt = !s.checkpointDir.empty() || !s.loadFromFile.empty();
   const bool ckpt_ok = !ckpt || (!s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials && !s.doUseAmplitudeMode &&
-                                 !s.doUseNTFF && !s.doUseParallelGrid && s.checkpointStep <= 0);
+                                 !s.doUseNTFF && !s.doUseParallelGrid);
   if ((s.doUsePML && !cpml_ok && !upml_ok) || (s.doUseTFSF && !tfsf_ok) || !meta_ok || !ntff_ok || !amp_ok ||
       !par_ok || !ckpt_ok || s.doUseComplexFieldValues || s.doUseDoubleMaterialPrecision) {
     std::fprintf(stderr,
                  "fdtd3d (native): CPML in 3D outside fp32 float4 rows, PML / TF/SF in 1D, TF/SF boxes reaching "
                  "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "
-                 "grids beyond 3D plain media split along x, checkpoints beyond plain media saved at the end, and "
-                 "complex fields run through the Python driver: python -m fdtd3d_amd <same options>\n");
+                 "grids beyond 3D plain media split along x, checkpoints beyond plain media, and complex "
+                 "fields run through the Python driver: python -m fdtd3d_amd <same options>\n");
     return 2;
   }
   int ndev = 0;

@@ -318,8 +318,14 @@ def test_native_checkpoint_roundtrip(case, tmp_path, gpu):
         assert r.returncode == 0, r.stdout + r.stderr
         return r.stdout
 
-    nat(["--time-steps", str(k), "--checkpoint-dir", str(d["a"])])
-    assert (d["a"] / ("checkpoint[%d]_rank-0.json" % k)).exists()
+    # periodic checkpoints every k steps (at k, 2k) and the final one; the resume takes the latest, so the
+    # later ones go before resuming
+    nat(["--time-steps", str(2 * k + 1), "--checkpoint-dir", str(d["a"]), "--checkpoint-step", str(k)])
+    for t in (k, 2 * k, 2 * k + 1):
+        side = d["a"] / ("checkpoint[%d]_rank-0.json" % t)
+        assert side.exists(), t
+        if t != k:
+            side.unlink()
     out = nat(["--time-steps", str(n), "--load-from-file", str(d["a"]), "--checkpoint-dir", str(d["nat"])])
     assert "Number of time steps: %d (%d timed" % (n, n - k) in out, out
     assert py_run(argv + py + ["--time-steps", str(n), "--load-from-file", str(d["a"]), "--checkpoint-dir",
