@@ -86,6 +86,9 @@ int fdtd_tfdev_size();
 int fdtd_tfsf_pass_f32(float* einc, float* hinc, int n, double ce, double ch, const double* src_vals, int steps,
                        int reach, int nE, int nH, const int* I0, const float* W0, const float* W1, const float* C,
                        float* gtab, void* stream);
+int fdtd_tfsf_table_f32(const float* esrc, const float* hsrc, float* einc, float* hinc, int n, double ce, double ch,
+                        const double* src_vals, int steps, int reach, int nE, int nH, const int* I0, const float* W0,
+                        const float* W1, const float* C, float* gtab, void* stream);
 int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, double* const* eout, double* const* hout,
                   const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
                   const int* boxes, const int* obox, int xchunk, int steps, const int* src, const double* src_vals,

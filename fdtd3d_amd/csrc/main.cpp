@@ -10,12 +10,15 @@
 // spheres (--use-metamaterials, scene drude-sphere) in 3D through the fused
 // chain kernel, TF/SF plane waves in 3D, the NTFF scattered power diagram
 // (--use-ntff) and DAT/BMP output of the final fields (native_physics.h).
-// 2D CPML / UPML and TF/SF (generic slab and chain kernels), and amplitude mode
+// 2D CPML / UPML and TF/SF (generic slab and chain kernels), amplitude mode
 // (running maxima folded into blocked passes for 3D vacuum fp32, a fused
-// amplitude kernel after each step otherwise).  Multi-GPU runs, complex
-// fields and resume go through the Python driver (python -m fdtd3d_amd),
-// which shares the kernels; asking this binary for them is an error, never a
-// silent fallback.
+// amplitude kernel after each step otherwise), checkpoints / resume of
+// plain-media runs in the Python driver's format (--checkpoint-dir,
+// --load-from-file) and --parallel-grid x-slab decompositions of 3D plain
+// runs over the node's GPUs from one process (run_multi).  Complex fields and
+// the decomposed physics runs go through the Python driver (python -m
+// fdtd3d_amd), which shares the kernels; asking this binary for them is an
+// error, never a silent fallback.
 #include <hip/hip_runtime.h>
 
 #include <dirent.h>
@@ -652,16 +655,20 @@ struct NativeTfsf {
   }
 };
 
-// incident-wave projection onto a component (YeeGridLayout.cpp:811-845)
+// incident-wave projection onto a component (YeeGridLayout.cpp:811-845);
+// projections zero in exact arithmetic (cos(pi/2) = 6e-17) are zero, as in
+// layout/yee.py incident_projection
 double inc_projection(int c, double t, double p, double q) {
+  double v;
   switch (c) {
-    case 0: return std::cos(q) * std::sin(p) - std::sin(q) * std::cos(t) * std::cos(p);
-    case 1: return -std::cos(q) * std::cos(p) - std::sin(q) * std::cos(t) * std::sin(p);
-    case 2: return std::sin(q) * std::sin(t);
-    case 3: return std::sin(q) * std::sin(p) + std::cos(q) * std::cos(t) * std::cos(p);
-    case 4: return -std::sin(q) * std::cos(p) + std::cos(q) * std::cos(t) * std::sin(p);
-    default: return -(std::cos(q) * std::sin(t));
+    case 0: v = std::cos(q) * std::sin(p) - std::sin(q) * std::cos(t) * std::cos(p); break;
+    case 1: v = -std::cos(q) * std::cos(p) - std::sin(q) * std::cos(t) * std::sin(p); break;
+    case 2: v = std::sin(q) * std::sin(t); break;
+    case 3: v = std::sin(q) * std::sin(p) + std::cos(q) * std::cos(t) * std::cos(p); break;
+    case 4: v = -std::sin(q) * std::cos(p) + std::cos(q) * std::cos(t) * std::sin(p); break;
+    default: v = -(std::cos(q) * std::sin(t));
   }
+  return std::fabs(v) < 1e-12 ? 0.0 : v;
 }
 
 template <typename T>
@@ -709,6 +716,7 @@ bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N,
       const int src = kCurl[c][t][0], axis = kCurl[c][t][1], sign = kCurl[c][t][2];
       if (!present[src] || axis >= dim) continue;  // the scheme's own curl terms only
       const double proj = inc_projection(src, th, ph, ps);
+      if (proj == 0.0) continue;  // no such incident component: nothing to correct
       for (int d = 0; d < 6; ++d) {
         if (dir_axis[d] != axis) continue;
         const TfsfPred* pr = nullptr;
@@ -891,6 +899,11 @@ long ckpt_load(const fdtd::Settings& s, const std::string& scheme, const fdtd::I
   else if (json_value(j, "complex") != "false") bad = "complex";
   else if (size != want) bad = "size";
   else if (shape != want) bad = "local_shape";
+  // a serial run's state: the whole grid at the origin, one rank, no
+  // deep-halo sub-step in flight (the checks of io/checkpoint.py)
+  else if (json_ints(json_value(j, "origin")) != std::vector<long>{0, 0, 0}) bad = "origin";
+  else if (json_ints(json_value(j, "topology")) != std::vector<long>{1, 1, 1}) bad = "topology";
+  else if (!json_value(j, "sub_step").empty() && json_value(j, "sub_step") != "0") bad = "sub_step";
   std::vector<std::string> names;
   for (size_t p = j.find("\"arrays\":"); p != std::string::npos;) {
     p = j.find("\"name\":", p);
@@ -1815,6 +1828,9 @@ int run(const fdtd::Settings& s) {
 
   // --checkpoint-step P: a checkpoint after every step t with t % P == 0 (the
   // Python driver's periodic hook), the passes ending there
+  // checkpoint I/O time (host wall clock, the device idle): kept out of the
+  // reported stepping rate, as the Python driver's phase timers do
+  double ckpt_ms = 0.0;
   auto run_ckpt = [&](int t, int n) {
     const int P = s.checkpointDir.empty() ? 0 : s.checkpointStep;
     if (P <= 0) {
@@ -1828,10 +1844,12 @@ int run(const fdtd::Settings& s) {
       t = nxt;
       if (t % P == 0) {
         HIP_OK(hipStreamSynchronize(st));
+        const auto c0 = std::chrono::steady_clock::now();
         if (!ckpt_save<T>(s, scheme, N, present, F, t, dx, dt)) {
           std::fprintf(stderr, "fdtd3d: cannot write the checkpoint to %s\n", s.checkpointDir.c_str());
           std::exit(1);
         }
+        ckpt_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
       }
     }
   };
@@ -1850,6 +1868,7 @@ int run(const fdtd::Settings& s) {
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, st));
+  ckpt_ms = 0.0;  // warm-up checkpoints are outside the timed region anyway
   run_ckpt(t0 + warm, steps - warm);
   // amplitude mode (models/scheme.py perform_amplitude_steps): check periods
   // of K steps whose changed-cell counts accumulate on the device, read once
@@ -2010,9 +2029,10 @@ int run(const fdtd::Settings& s) {
   HIP_OK(hipGetLastError());
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-  const double sec = ms / 1e3;
+  const double sec = std::max(0.0, (ms - ckpt_ms) / 1e3);
 
   std::printf("Total time = %f seconds\n", sec);
+  if (ckpt_ms > 0) std::printf("Checkpoint I/O = %f seconds (not in the total)\n", ckpt_ms / 1e3);
   std::printf("Dimension: %d\n", dim);
   if (dim == 3)
     std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);

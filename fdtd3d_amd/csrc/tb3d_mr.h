@@ -54,9 +54,16 @@ struct TbSrc {
 // direction along x or y the incident value a target sees depends on its
 // index along that axis only (`va`), so each pass precomputes, per level,
 // g = sign * projection * interpolated incident line at every index of a set
-// (k_tfsf_pass in yee3d_tb.hip) and the kernels add g to the target's curl
-// before the coefficient multiply -- from SCALAR loads (wave-uniform index),
-// which do not queue behind the vector prefetch.
+// (k_tfsf_pass in yee3d_tb.hip).  Inside the kernel the index along `va` is
+// the plane (va = 0) or the row (va = 1) -- both wave-uniform -- so every
+// correction is ONE scalar per (set, level, plane, row): a scalar load, a
+// lane test along z and a multiply-add on the new value (the update is
+// linear: E + c (curl + g) = (E + c curl) + c g).  A wave keeps two bit masks
+// per kind of the sets that touch its rows / lanes at all (x-face sets only
+// looked at on their plane), so a wave away from every face pays a scalar
+// compare per level.  (The round-4 form parked per-wave slot tables in VGPR
+// lanes and inlined a 6-slot loop at every level and row: 4.8x the plain
+// kernel's code, profiles/tfsf_cost_r5.md.)
 constexpr int TF_MAX_SETS = 24;
 struct TfSet {
   int n;          // component 0..5 = Ex Ey Ez Hx Hy Hz
@@ -233,15 +240,10 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   __shared__ vec sX[2][4][NW][64];
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.y);  // one wave per y (SGPR)
-  // the TF/SF table lives in LDS for the kernel's life: its fields are read in
-  // many branches (with dynamic set indices)
-  __shared__ unsigned sTFraw[TFS ? sizeof(TfDev) / 4 : 1];
-  if constexpr (TFS) {
-    for (int q = threadIdx.x + 64 * threadIdx.y; q < (int)(sizeof(TfDev) / 4); q += 64 * NW)
-      sTFraw[q] = ((const unsigned*)tf)[q];
-  }
-  if constexpr (TFS) __syncthreads();
-  const TfDev& TF = *reinterpret_cast<const TfDev*>(sTFraw);
+  // the TF/SF sets: scalar loads through the constant address space (every
+  // index the kernel uses is wave-uniform)
+  typedef const __attribute__((address_space(4))) TfDev* TfPtr;
+  const TfPtr TFc = (TfPtr)tf;
 
   // Tile of this workgroup.  A row of a tile starts at an arbitrary z (the
   // stride is the 64 - 2T owned cells), so its 64 cells straddle three
@@ -421,123 +423,37 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     }
   };
 
-  // TF/SF.  x-face sets (one plane each, all rows / lanes of the TF box) are
-  // rare per wave and go through scalar loads when a level hits their plane.
-  // y / z-face sets (one row or one lane column) touch few waves but every
-  // level of every trip of those waves, so each wave parks up to TF_SLOTS of
-  // them per kind in slots: slot metadata in VGPR lanes (read back with
-  // readlane at a compile-time lane), a per-lane bit per (slot, row) for the
-  // cells it covers, and per trip ONE vector load of the g values of every
-  // (slot, level, row) -- issued before the field prefetch, so the levels
-  // never wait behind it.
-  constexpr int TF_SLOTS = 6;                      // per kind
-  constexpr int TF_ENT = 2 * TF_SLOTS * T * R;     // g entries per trip (<= 128 for T <= 5)
-  static_assert(!TFS || TF_ENT <= 128, "TF/SF: at most 5 steps per pass");
-  unsigned tf_wx[2] = {0u, 0u};
-  unsigned tf_ov[2] = {0u, 0u};  // face sets beyond the slots: the scalar path every level
-  int tf_xe0 = -1, tf_xe1 = -1, tf_xh0 = -1, tf_xh1 = -1;  // x-face planes (E / H sets)
-  int tf_na0 = 0, tf_na1 = 0;                      // slots in use (E / H)
-  unsigned tf_lbits = 0;                           // bit slot * R + r: this lane in the slot's set, row r
-  int tf_mx = 0;                                   // lane s: x range of slot s (lo | hi << 16)
-  int tf_mn = 0;                                   // lane s: component of slot s
-  int tf_gb0 = 0, tf_gb1 = 0;                      // g index of entry lane / lane + 64 (plus X when va = 0)
-  bool tf_ok0 = false, tf_ok1 = false;
-  int tf_va = 0, tf_ld = 0;
+  // TF/SF: the sets that touch this wave's rows / lanes at all, per kind
+  // (bit = set index): x-face sets (one plane each) apart, only looked at on
+  // their plane; y / z-face sets every level (few waves have any)
+  unsigned tf_xe = 0u, tf_xh = 0u, tf_yze = 0u, tf_yzh = 0u;
+  int tf_xe0 = -1, tf_xe1 = -1, tf_xh0 = -1, tf_xh1 = -1;  // x-face planes of the E / H sets
+  int tf_ld = 0;
   if constexpr (TFS) {
-    const int ns = TF.nsets;
-    const int ld = TF.ld;
-    tf_ld = ld;
-    tf_va = TF.s[0].va;
-    int na[2] = {0, 0};
+    const int ns = TFc->nsets;
+    tf_ld = TFc->ld;
     for (int si = 0; si < ns; ++si) {
-      const TfSet& S = TF.s[si];
-      unsigned rb = 0;
+      const int lo1 = TFc->s[si].lo[1], hi1 = TFc->s[si].hi[1];
+      const int lo2 = TFc->s[si].lo[2], hi2 = TFc->s[si].hi[2];
+      bool rin = false;
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int j = jw + r;
-        rb |= (kin && j >= S.lo[1] && j < S.hi[1] && kb >= S.lo[2] && kb < S.hi[2]) ? (1u << r) : 0u;
+      for (int r = 0; r < R; ++r) rin = rin || (jw + r >= lo1 && jw + r < hi1);
+      if (!rin || !__any(kin && kb >= lo2 && kb < hi2)) continue;
+      const unsigned bit = 1u << si;
+      const bool e = TFc->s[si].n < 3;
+      if (TFc->s[si].fa == 0) {
+        tf_xe |= e ? bit : 0u;
+        tf_xh |= e ? 0u : bit;
+      } else {
+        tf_yze |= e ? bit : 0u;
+        tf_yzh |= e ? 0u : bit;
       }
-      if (!__any(rb != 0u)) continue;
-      const int k = S.n < 3 ? 0 : 1;
-      if (S.fa == 0) {
-        tf_wx[0] |= k == 0 ? (1u << si) : 0u;
-        tf_wx[1] |= k == 1 ? (1u << si) : 0u;
-        continue;
-      }
-      const int a = k == 0 ? na[0] : na[1];
-      if (a >= TF_SLOTS) {
-        tf_ov[0] |= k == 0 ? (1u << si) : 0u;
-        tf_ov[1] |= k == 1 ? (1u << si) : 0u;
-        continue;
-      }
-      const int slot = k * TF_SLOTS + a;
-      if (k == 0) ++na[0]; else ++na[1];
-      tf_lbits |= rb << (slot * R);
-      if (lane == slot) {
-        tf_mx = S.lo[0] | (S.hi[0] << 16);
-        tf_mn = S.n;
-      }
-      // entries (slot, l, r) -> entry q = (slot * T + l) * R + r
-#pragma unroll
-      for (int l = 0; l < T; ++l)
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int q = (slot * T + l) * R + r;
-          // level l: E sets on plane X - l, H sets on X - l - 1
-          const int base = l * ld + S.goff + (S.va == 0 ? -S.lo[0] - l - k : (jw + r) - S.lo[1]);
-          if (lane == q) { tf_gb0 = base; tf_ok0 = true; }
-          if (lane + 64 == q) { tf_gb1 = base; tf_ok1 = true; }
-        }
     }
-    tf_na0 = na[0];
-    tf_na1 = na[1];
-    tf_xe0 = TF.xpl[0][0];
-    tf_xe1 = TF.xpl[0][1];
-    tf_xh0 = TF.xpl[1][0];
-    tf_xh1 = TF.xpl[1][1];
+    tf_xe0 = TFc->xpl[0][0];
+    tf_xe1 = TFc->xpl[0][1];
+    tf_xh0 = TFc->xpl[1][0];
+    tf_xh1 = TFc->xpl[1][1];
   }
-  const bool tf_slots = TFS && (tf_na0 + tf_na1) > 0;
-  float tf_g0 = 0.f, tf_g1 = 0.f;  // this trip's g entries (lane q, q + 64)
-  // add the TF/SF corrections of kind k at level l, plane p, row r to the curls
-  auto tf_apply = [&](int k, int l, int p, int r, vec& c0, vec& c1, vec& c2) {
-    if constexpr (TFS) {
-      // y / z-face slots
-      if (tf_slots) {
-#pragma unroll
-        for (int a = 0; a < TF_SLOTS; ++a) {
-          if (a >= (k == 0 ? tf_na0 : tf_na1)) break;
-          const int slot = k * TF_SLOTS + a;
-          const int xr = __builtin_amdgcn_readlane(tf_mx, slot);
-          if ((unsigned)(p - (xr & 0xffff)) >= (unsigned)((xr >> 16) - (xr & 0xffff))) continue;
-          const int q = (slot * T + l) * R + r;
-          const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q < 64 ? tf_g0 : tf_g1), q & 63));
-          const float gl = ((tf_lbits >> (slot * R + r)) & 1u) ? g : 0.f;
-          const int c = __builtin_amdgcn_readlane(tf_mn, slot) - 3 * k;
-          c0 = c0 + (vec)(c == 0 ? gl : 0.f);
-          c1 = c1 + (vec)(c == 1 ? gl : 0.f);
-          c2 = c2 + (vec)(c == 2 ? gl : 0.f);
-        }
-      }
-      // x-face sets on their plane
-      const bool xp = k == 0 ? (p == tf_xe0 || p == tf_xe1) : (p == tf_xh0 || p == tf_xh1);
-      unsigned cand = (xp ? (k == 0 ? tf_wx[0] : tf_wx[1]) : 0u) | (k == 0 ? tf_ov[0] : tf_ov[1]);
-      const int j = jw + r;
-      while (cand) {
-        const int si = __builtin_ctz(cand);
-        cand &= cand - 1u;
-        const TfSet& S = TF.s[si];
-        if ((unsigned)(p - S.lo[0]) >= (unsigned)(S.hi[0] - S.lo[0]) || j < S.lo[1] || j >= S.hi[1]) continue;
-        const float g = gtab[l * TF.ld + S.goff + (S.va == 0 ? p - S.lo[0] : j - S.lo[1])];
-        // g on the set's lanes, 0 elsewhere, added to the set's component by
-        // selects (conditional adds make the compiler index a scratch array)
-        const float gl = (kb >= S.lo[2] && kb < S.hi[2]) ? g : 0.f;
-        const int c = S.n - 3 * k;
-        c0 = c0 + (vec)(c == 0 ? gl : 0.f);
-        c1 = c1 + (vec)(c == 1 ? gl : 0.f);
-        c2 = c2 + (vec)(c == 2 ? gl : 0.f);
-      }
-    }
-  };
   typedef unsigned u3 __attribute__((ext_vector_type(3)));
   auto coef_ld = [&](const float4* arr, const Box3& B, unsigned off, size_t pl, int p) -> u3 {
     const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)arr + (size_t)(p - B.lo[0]) * pl),
@@ -698,15 +614,51 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
       }
       return make_float3(sc, sc, sc);
     };
-    if (tf_slots) {
-      // this trip's g entries of the face slots (va = 0: index moves with X)
-      // (entries of planes outside a set's x range are never used; their
-      // index is clamped into the table)
-      const int dx = tf_va == 0 ? X : 0;
-      const int last = T * tf_ld - 1;
-      tf_g0 = tf_ok0 ? gtab[min(max(tf_gb0 + dx, 0), last)] : 0.f;
-      if (TF_ENT > 64) tf_g1 = tf_ok1 ? gtab[min(max(tf_gb1 + dx, 0), last)] : 0.f;
-    }
+    // TF/SF corrections of kind k (0 E, 1 H) at level l on plane p, added to
+    // the new values N of every row: N += c g, c the coefficient the update
+    // multiplied the curl with (0 outside the component's update box)
+    auto tf_fix = [&](int k, int l, int p, F3<V>* N) {
+      if constexpr (TFS) {
+        const bool xp = k == 0 ? (p == tf_xe0 || p == tf_xe1) : (p == tf_xh0 || p == tf_xh1);
+        unsigned m = (k == 0 ? tf_yze : tf_yzh) | (xp ? (k == 0 ? tf_xe : tf_xh) : 0u);
+        while (m) {
+          const int si = __builtin_ctz(m);
+          m &= m - 1u;
+          const int lo0 = TFc->s[si].lo[0], hi0 = TFc->s[si].hi[0];
+          if ((unsigned)(p - lo0) >= (unsigned)(hi0 - lo0)) continue;
+          const int n = TFc->s[si].n;
+          const int lo1 = TFc->s[si].lo[1], hi1 = TFc->s[si].hi[1];
+          const int lo2 = TFc->s[si].lo[2], hi2 = TFc->s[si].hi[2];
+          const int va = TFc->s[si].va, gb = l * tf_ld + TFc->s[si].goff;
+          const bool lin = kb >= lo2 && kb < hi2;
+          const int c = n - 3 * k;
+          // the component's update box along x (scalar selects: a reference
+          // picked among the by-value box arguments would copy them to scratch)
+          const int ulo = n == 0 ? bex.lo[0] : n == 1 ? bey.lo[0] : n == 2 ? bez.lo[0]
+                        : n == 3 ? bhx.lo[0] : n == 4 ? bhy.lo[0] : bhz.lo[0];
+          const int uhi = n == 0 ? bex.hi[0] : n == 1 ? bey.hi[0] : n == 2 ? bez.hi[0]
+                        : n == 3 ? bhx.hi[0] : n == 4 ? bhy.hi[0] : bhz.hi[0];
+          const bool uin = (unsigned)(p - ulo) < (unsigned)(uhi - ulo);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int j = jw + r;
+            if (j < lo1 || j >= hi1) continue;
+            const float g = cload(gtab, gb + (va == 0 ? p - lo0 : j - lo1));
+            const float3 kc = kcoef(k == 0, l, p, r);
+            const float sc = c == 0 ? kc.x : (c == 1 ? kc.y : kc.z);
+            vec cf;
+            if constexpr (ALLIN)
+              cf = uin ? (vec)(sc) : zero;
+            else
+              cf = cmask<V>((vec)(sc), uin ? (mbits >> ((r * 7 + n) * V)) & VM : 0u);
+            const vec add = lin ? cf * g : zero;
+            N[r].x = N[r].x + (c == 0 ? add : zero);
+            N[r].y = N[r].y + (c == 1 ? add : zero);
+            N[r].z = N[r].z + (c == 2 ? add : zero);
+          }
+        }
+      }
+    };
     // next plane(s) in flight under this plane's levels
     if (PFD == 2)
       load_plane(X + 2, Hn2, En2);
@@ -746,18 +698,33 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         vec cx = dxy - dxz;
         vec cy = dyz - dyx;
         vec cz = dzx - dzy;
-        tf_apply(0, l, pe, r, cx, cy, cz);
         En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * cx;
         En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * cy;
         En[r].z = Ec[r].z + coef(bez, pe, r, 2, ce.z) * cz;
-        if (src_plane && jw + r == src_j &&
-            (AMP ? (kb >= src_k && kb < amp.k1) : (src_k >= kb && src_k < kb + V))) {
-          const int q = AMP ? 0 : src_k - kb;
-          if (src_comp == 0) En[r].x[q] = sv.v[l];
-          if (src_comp == 1) En[r].y[q] = sv.v[l];
-          if (src_comp == 2) En[r].z[q] = sv.v[l];
+        if constexpr (!TFS) {
+          if (src_plane && jw + r == src_j &&
+              (AMP ? (kb >= src_k && kb < amp.k1) : (src_k >= kb && src_k < kb + V))) {
+            const int q = AMP ? 0 : src_k - kb;
+            if (src_comp == 0) En[r].x[q] = sv.v[l];
+            if (src_comp == 1) En[r].y[q] = sv.v[l];
+            if (src_comp == 2) En[r].z[q] = sv.v[l];
+          }
+          amp_level(0, l, pe, r, En[r]);
         }
-        amp_level(0, l, pe, r, En[r]);
+      }
+      if constexpr (TFS) {
+        // corrections first, the hard source then overrides (the stepped
+        // order: update + TF/SF tables, then sources)
+        tf_fix(0, l, pe, En);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (src_plane && jw + r == src_j && src_k >= kb && src_k < kb + V) {
+            const int q = src_k - kb;
+            if (src_comp == 0) En[r].x[q] = sv.v[l];
+            if (src_comp == 1) En[r].y[q] = sv.v[l];
+            if (src_comp == 2) En[r].z[q] = sv.v[l];
+          }
+        }
       }
       const int ph = pe - 1;
 #pragma unroll
@@ -774,7 +741,6 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         vec dx = gxz - gxy;
         vec dy = gyx - gyz;
         vec dz = gzy - gzx;
-        tf_apply(1, l, ph, r, dx, dy, dz);
         Hn.x = Hp[l][r].x + coef(bhx, ph, r, 3, ch.x) * dx;
         Hn.y = Hp[l][r].y + coef(bhy, ph, r, 4, ch.y) * dy;
         Hn.z = Hp[l][r].z + coef(bhz, ph, r, 5, ch.z) * dz;
@@ -786,6 +752,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         Hp[l][r] = Hc[r];
         Hc[r] = Hn;
       }
+      tf_fix(1, l, ph, Hc);
       // the next trip's level-0 maxima, in flight under the remaining levels
       if (AMP && l == 0) amp_prefetch(X);
     }

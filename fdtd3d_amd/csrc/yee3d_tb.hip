@@ -398,14 +398,29 @@ int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, flo
 // values from the new E line, the line's H half step -- the order of the
 // stepped scheme (models/scheme.py step).  Only the first `reach` cells of
 // the line move: beyond the wave front every value is exactly 0.
+//
+// With ``esrc`` / ``hsrc`` set, the line is first copied from them into
+// ``einc`` / ``hinc`` (scratch lines): the g tables of a pass whose real line
+// is advanced elsewhere -- the hybrid's stepped shell steps it once per step
+// while the blocked core applies the same pass's corrections in-kernel.
 __global__ __launch_bounds__(1024) void k_tfsf_pass(float* __restrict__ einc, float* __restrict__ hinc, int n,
                                                     float ce, float ch, TbSrc sv, int T, int reach, int nE, int nH,
                                                     const int* __restrict__ I0, const float* __restrict__ W0,
                                                     const float* __restrict__ W1, const float* __restrict__ C,
-                                                    float* __restrict__ gtab) {
+                                                    float* __restrict__ gtab, const float* __restrict__ esrc,
+                                                    const float* __restrict__ hsrc) {
   const int tid = threadIdx.x;
   const int ld = nE + nH;
   const int m = min(n, reach);
+  if (esrc) {
+    // every cell a level reads: the moving part plus the interpolation's
+    // upper neighbour of the farthest target (I0 + 1 < reach + 1)
+    for (int i = tid; i < min(n, reach + 1); i += blockDim.x) {
+      einc[i] = esrc[i];
+      hinc[i] = hsrc[i];
+    }
+    __syncthreads();
+  }
   for (int l = 0; l < T; ++l) {
     for (int e = tid; e < nE; e += blockDim.x)
       gtab[l * ld + e] = C[e] * (W0[e] * hinc[I0[e]] + W1[e] * hinc[I0[e] + 1]);
@@ -582,6 +597,21 @@ FDTD_API int fdtd_tfsf_pass_f32(float* einc, float* hinc, int n, double ce, doub
   TbSrc sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = l < steps ? (float)src_vals[l] : 0.f;
   k_tfsf_pass<<<1, 1024, 0, (hipStream_t)stream>>>(einc, hinc, n, (float)ce, (float)ch, sv, steps, reach, nE, nH,
-                                                   I0, W0, W1, C, gtab);
+                                                   I0, W0, W1, C, gtab, nullptr, nullptr);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
+// the g tables of a pass WITHOUT advancing the line: the line ``esrc`` /
+// ``hsrc`` is copied into the scratch lines ``einc`` / ``hinc`` (length n
+// each) and advanced there (hybrid passes, whose shell steps the real line)
+FDTD_API int fdtd_tfsf_table_f32(const float* esrc, const float* hsrc, float* einc, float* hinc, int n, double ce,
+                                 double ch, const double* src_vals, int steps, int reach, int nE, int nH,
+                                 const int* I0, const float* W0, const float* W1, const float* C, float* gtab,
+                                 void* stream) {
+  if (steps < 1 || steps > 8 || !esrc || !hsrc || esrc == einc || hsrc == hinc) return (int)hipErrorInvalidValue;
+  TbSrc sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = l < steps ? (float)src_vals[l] : 0.f;
+  k_tfsf_pass<<<1, 1024, 0, (hipStream_t)stream>>>(einc, hinc, n, (float)ce, (float)ch, sv, steps, reach, nE, nH,
+                                                   I0, W0, W1, C, gtab, esrc, hsrc);
   FDTD_RETURN_LAUNCH_STATUS();
 }

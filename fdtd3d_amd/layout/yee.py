@@ -219,7 +219,7 @@ class YeeLayout:
         t, p, s = self.theta, self.phi, self.psi
         if self.scheme in ("tmz", "tez", "1d"):
             t = math.pi / 2
-        return {
+        v = {
             "Ex": math.cos(s) * math.sin(p) - math.sin(s) * math.cos(t) * math.cos(p),
             "Ey": -math.cos(s) * math.cos(p) - math.sin(s) * math.cos(t) * math.sin(p),
             "Ez": math.sin(s) * math.sin(t),
@@ -227,6 +227,11 @@ class YeeLayout:
             "Hy": -math.sin(s) * math.cos(p) + math.cos(s) * math.cos(t) * math.sin(p),
             "Hz": -(math.cos(s) * math.sin(t)),
         }[comp]
+        # cos(pi/2) = 6e-17 in floating point: a projection that is zero in
+        # exact arithmetic (the reference default theta = 90, phi = 0, psi =
+        # 90 excites only Ez / Hy) is zero here too, so its corrections --
+        # 1e-17 of the incident wave, below fp64 round-off -- are not applied
+        return 0.0 if abs(v) < 1e-12 else v
 
 
 def component_shape(size: Sequence[int]) -> Tuple[int, int, int]:

@@ -51,8 +51,10 @@ F32_AUTO_STEPS = 5
 F32_AUTO_STEPS_MANY_RANKS = 4
 F32_AUTO_STEPS_PERCELL_BOTH = 2
 # plain runs with in-kernel TF/SF (TfsfSets): 512^3 vacuum + TF/SF T=4 127k,
-# T=5 86k Mcells/s (the TF/SF variant spills at T=5)
+# T=5 86k Mcells/s with the round-4 slot form (the TF/SF variant spilled at T=5)
 F32_AUTO_STEPS_TFSF = 4
+# longest pass of the TF/SF variant (yee3d_tb.hip launch_tb_mr_sel: T <= 5)
+TFSF_MAX_STEPS = 5
 
 
 
@@ -244,15 +246,28 @@ class BlockedStepping:
                 return plan
         return None
 
+    def _hybrid_core_tfsf(self, T: int) -> bool:
+        """True when the blocked core pass applies the TF/SF corrections
+        itself (``TfsfSets``: incidence along x or y, 3D; csrc/tb3d_mr.h
+        ``tf_fix``), so the TF/SF faces need not lie in the stepped shell."""
+        cfg = self.cfg
+        if (not cfg.use_tfsf or cfg.scheme != "3d" or getattr(self, "tfsf_sets", None) is None
+                or getattr(cfg, "hybrid_tfsf", "auto") == "shell" or T > TFSF_MAX_STEPS):
+            return False
+        return True
+
     def _hybrid_plan_m(self, T: int, m: int):
-        """Hybrid plan with core margin ``m``: the TF/SF faces lie in the
-        stepped shell.  (Applying them in the blocked core instead -- a thinner
-        shell, the TfsfSets kernel variant on the ring around the faces or on
-        the whole core -- measured slower at 512^3: profiles/tfsf_core_r4.md.)"""
+        """Hybrid plan with core margin ``m``.  With in-kernel TF/SF
+        (:meth:`_hybrid_core_tfsf`) the core reaches ``m`` cells from the
+        absorbing layers and carries the TF/SF faces; otherwise the faces lie
+        in the stepped shell.  (Round 4's TF/SF variant cost twice the plain
+        kernel per cell, so the faces stayed in the shell then:
+        profiles/tfsf_core_r4.md; profiles/tfsf_cost_r5.md for the rewrite.)"""
         dom = self.domain
         cfg = self.cfg
         size = cfg.size
         alloc = dom.allocated_global()
+        core_tf = self._hybrid_core_tfsf(T)
         lo, hi = [0, 0, 0], list(size)
         act = [self.layout.active(a) for a in range(3)]  # 2D: z is one cell, never cut
         for a in range(3):
@@ -261,7 +276,7 @@ class BlockedStepping:
             edge = 0
             if cfg.use_pml:
                 edge = max(edge, self.layout.pml_size[a])
-            if cfg.use_tfsf:
+            if cfg.use_tfsf and not core_tf:
                 edge = max(edge, cfg.tfsf_size[a] + 1)
             if edge > 0:
                 lo[a], hi[a] = edge + m, size[a] - edge - m
@@ -321,7 +336,7 @@ class BlockedStepping:
             g = grow(ob, T + 1)
             if any(not box_empty(box_intersect(g, b)) for b in irregular):
                 return None
-            if cfg.use_tfsf and self._tfsf_targets_in(dom.to_local(g)):
+            if cfg.use_tfsf and not core_tf and self._tfsf_targets_in(dom.to_local(g)):
                 return None
         if self.halo is not None:
             # decomposed: each rank's core is its owned part of the global core
@@ -374,19 +389,20 @@ class BlockedStepping:
         upd = {c: self.local_box(c, alloc) for c in self.comps}
         return {"T": T, "core": [dom.to_local(b) for b in couts], "shell": shells[0], "shells": shells,
                 "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
-                "cut_cells": box_volume(Dm) if Dm is not None else 0}
+                "cut_cells": box_volume(Dm) if Dm is not None else 0, "core_tfsf": core_tf}
 
-    def _tfsf_pass(self, p: int, T: int, level0: int = 0):
+    def _tfsf_pass(self, p: int, T: int, level0: int = 0, dry: bool = False):
         """In-kernel TF/SF of a blocked pass starting at step ``self.t`` on
-        plane ``p``: advances the plane's incident line ``T`` steps and returns
-        the ``tfsf`` argument of ``ops.tb_step`` (None without in-kernel
-        TF/SF)."""
+        plane ``p``: advances the plane's incident line ``T`` steps (``dry``:
+        on scratch copies, the line stays -- hybrid passes, whose stepped
+        shell advances it) and returns the ``tfsf`` argument of
+        ``ops.tb_step`` (None without in-kernel TF/SF)."""
         sets = getattr(self, "tfsf_sets", None)
         if not self.cfg.use_tfsf or sets is None:
             return None
         vals = [self.source_value(self.t + l, p) for l in range(T)]
         g = self.ops.tfsf_pass(self.einc[p], self.hinc[p], self.inc_ce, self.inc_ch, vals, self.t + T + 2, sets,
-                               slot=p)
+                               slot=p, dry=dry)
         return (sets, g, level0)
 
     def _pass_sources(self, t: int, T: int):
@@ -422,10 +438,18 @@ class BlockedStepping:
             # the deep-halo windows from sub-step 0, whatever an earlier
             # shorter pass (periodic work, a tail) left behind
             self.sub_step = 0
+        # in-kernel TF/SF of the core: the pass's g tables from scratch copies
+        # of the incident line (the shell steps below advance the real one)
+        tfs = ([self._tfsf_pass(p, T, dry=True) for p in range(self.planes)] if hp.get("core_tfsf")
+               else [None] * self.planes)
+
         def core(boxes):
             for p in range(self.planes):
                 for ob in boxes:
-                    self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
+                    if tfs[p] is not None:
+                        self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p], tfsf=tfs[p])
+                    else:
+                        self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])
 
         with self.prof.phase("blocked-core"):
             core(core_now)

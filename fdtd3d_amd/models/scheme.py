@@ -53,14 +53,14 @@ from ..utils.constants import ACCURACY, EPS0, MU0, PI, SPEED_OF_LIGHT
 # (profiles/amplitude_r4.md)
 AMP_TB_STEPS = 3
 from ..utils import logging as log
-from .blocking import F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64, BlockedStepping, auto_time_block
+from .blocking import (F64_AUTO_STEPS, TB2D_AUTO_STEPS, TB2D_AUTO_STEPS_F64, TFSF_MAX_STEPS, BlockedStepping,
+                       auto_time_block)
 from .tfsf import build_tfsf_sets, build_tfsf_tables, incident_line_length
 
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
 GRAPH_STEPS = 60  # steps per captured HIP graph (a multiple of 6: D/D1 level rotations return to the start)
-TFSF_MAX_STEPS = 5  # steps per pass of the blocked kernel's in-kernel TF/SF variant (yee3d_tb.hip TF_ENT)
 
 
 @dataclass
@@ -107,6 +107,7 @@ class SchemeConfig:
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
     shell_streams: int = 0                   # hybrid shell: streams for the independent window launches (0 auto)
     hybrid_graph: str = "auto"               # hybrid passes replayed from HIP graphs (auto / off)
+    hybrid_tfsf: str = "auto"                # hybrid + TF/SF: faces in the blocked core (auto / core) or the shell
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
@@ -143,6 +144,7 @@ class SchemeConfig:
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
             amplitude_check_steps=s.amplitudeCheckSteps,
             hybrid_block=s.hybridBlock, shell_streams=s.shellStreams, hybrid_graph=s.hybridGraph,
+            hybrid_tfsf=s.hybridTfsf,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
@@ -1590,11 +1592,12 @@ class YeeScheme(BlockedStepping):
         cost (not the GPU) bounds the rate.  (3D passes are GPU-bound: graphs
         measured no faster with the capture done in the warm-up and 13-30%
         slower with it in the timed run, profiles/graph2d_r4.md.)  Needs: 2D,
-        serial HIP run, no
-        periodic work, no point source inside a core box (the core pass takes
-        its values as launch arguments), and a pass count after which the
-        field buffers (2) and the UPML / Drude level lists (2 or 3 levels) are
-        back in place."""
+        serial HIP run, no per-step hooks (periodic work runs between
+        ``_advance`` calls; a replayed graph is reused only while
+        :meth:`_state_order_key` matches its capture), no point source inside
+        a core box (the core pass takes its values as launch arguments), and a
+        pass count after which the field buffers (2) and the UPML / Drude
+        level lists (2 or 3 levels) are back in place."""
         hp = self.hybrid
         if (hp is None or self.cfg.scheme not in ("tmz", "tez") or self.halo is not None or self.hooks
                 or self.ops.name != "hip" or self.device.type != "cuda" or self.prof.enabled
@@ -1614,14 +1617,32 @@ class YeeScheme(BlockedStepping):
                 return P
         return 0
 
+    def _state_order_key(self) -> tuple:
+        """Identity of every rotating state buffer in its current role: the
+        field buffer set of each plane and, with the UPML chain, the order of
+        each component's D (and Drude D1) level list, which ``_upml_rotate``
+        permutes every step.  A captured graph bakes these pointers in, so it
+        may be replayed only while the key is unchanged (two calls of
+        ``advance`` can leave the fields in the captured parity but the level
+        lists rotated: an odd number of steps in an even number of passes)."""
+        key = [self.F[p][self.comps[0]].data_ptr() for p in range(self.planes)]
+        if self.use_upml_chain:
+            for c in self.comps:
+                st = self.upml[c]
+                for name in ("D", "D1"):
+                    lv = st.get(name)
+                    if lv:
+                        key += [id(x) for p in range(self.planes) for x in lv[p]]
+        return tuple(key)
+
     def _hybrid_graph(self, n: int, P: int) -> int:
         """Replay ``P`` hybrid passes at a time from one HIP graph; the shell's
         sources (incident line, point source) read a device table through a
         step counter the graph advances (the ``_graph_src`` path of
         :meth:`step`).  The graph is captured once and kept while its buffers
-        are the current ones (same field-buffer parity, table long enough);
-        later calls refill the table and reset the counter.  Returns the
-        steps taken."""
+        are the current ones (:meth:`_state_order_key`: field-buffer parity
+        and UPML level order; table long enough); later calls refill the
+        table and reset the counter.  Returns the steps taken."""
         T = self.hybrid["T"]
         taken = 0
         if not getattr(self, "_hybrid_warm", False):
@@ -1639,7 +1660,7 @@ class YeeScheme(BlockedStepping):
         t0 = self.t
         vals = torch.tensor([[self.source_value(t0 + i, p) for i in range(reps * G)] for p in range(self.planes)],
                             dtype=torch.float64)
-        key = (P, T, tuple(self.F[p][self.comps[0]].data_ptr() for p in range(self.planes)))
+        key = (P, T, self._state_order_key())
         g = self.__dict__.get("_hgraph")
         if g is None or g["key"] != key or g["reps"] < reps:
             tab = torch.zeros((self.planes, reps * G), dtype=torch.float64, device=self.device)

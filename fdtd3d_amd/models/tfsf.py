@@ -109,6 +109,8 @@ def build_tfsf_tables(layout: YeeLayout, comps: Sequence[str], origin: Sequence[
             for dname in ("LRDUBF"):
                 if DIR_AXIS[dname] != axis or (comp, dname) not in TFSF_PREDICATES:
                     continue
+                if layout.incident_projection(s) == 0.0:
+                    continue  # the incident wave has no such component: nothing to correct
                 pred = TFSF_PREDICATES[(comp, dname)]
                 masks = []
                 for d in range(3):
@@ -258,6 +260,8 @@ def build_tfsf_sets(layout: YeeLayout, comps: Sequence[str], origin: Sequence[in
             for (s, axis, sign) in layout.curl_terms(comp):
                 for dname in "LRDUBF":
                     if DIR_AXIS[dname] != axis or (comp, dname) not in TFSF_PREDICATES:
+                        continue
+                    if layout.incident_projection(s) == 0.0:
                         continue
                     pred = TFSF_PREDICATES[(comp, dname)]
                     lo, hi = [], []

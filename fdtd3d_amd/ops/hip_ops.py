@@ -690,10 +690,12 @@ class HipOps:
     tfsf_sets_ok = True  # the fp32 blocked kernel applies TfsfSets corrections
 
     def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
-                  sets, slot: int = 0) -> torch.Tensor:
+                  sets, slot: int = 0, dry: bool = False) -> torch.Tensor:
         """Advance the incident line ``len(src_vals)`` steps and return the
         g table of the pass (levels x sets.ld, yee3d_tb.hip k_tfsf_pass);
-        ``slot`` selects the table buffer (one per field plane)."""
+        ``slot`` selects the table buffer (one per field plane).  ``dry``:
+        the line stays as it is -- the pass runs on scratch copies
+        (fdtd_tfsf_table_f32; hybrid passes, whose shell steps the line)."""
         T = len(src_vals)
         if not (1 <= T <= 8) or self.dtype != torch.float32:
             raise HipError("tfsf_pass: fp32, 1..8 steps")
@@ -707,11 +709,22 @@ class HipOps:
             g = tabs[slot] = torch.zeros(8 * max(1, sets.ld), dtype=torch.float32, device=self.device)
         for t_ in (einc, hinc):
             self._check_tensor(t_)
-        rc = self.lib.fdtd_tfsf_pass_f32(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(ce), c_double(ch),
-                                         (c_double * 8)(*(list(src_vals) + [0.0] * (8 - T))), c_int(T),
-                                         c_int(min(einc.numel(), reach)), c_int(sets.n_e), c_int(sets.n_h),
-                                         _ptr(sets.i0), _ptr(sets.w0), _ptr(sets.w1), _ptr(sets.c), _ptr(g),
-                                         _stream())
+        if einc.numel() != hinc.numel():
+            raise HipError("tfsf_pass: E / H lines of different length")
+        vals8 = (c_double * 8)(*(list(src_vals) + [0.0] * (8 - T)))
+        tail = (c_int(T), c_int(min(einc.numel(), reach)), c_int(sets.n_e), c_int(sets.n_h), _ptr(sets.i0),
+                _ptr(sets.w0), _ptr(sets.w1), _ptr(sets.c), _ptr(g), _stream())
+        if dry:
+            scr = sets.__dict__.setdefault("scratch_lines", {})
+            sl = scr.get(slot)
+            if sl is None or sl[0].numel() != einc.numel():
+                # zero beyond every reach a pass copies: cells past the wave front read 0
+                sl = scr[slot] = (torch.zeros_like(einc), torch.zeros_like(hinc))
+            rc = self.lib.fdtd_tfsf_table_f32(_ptr(einc), _ptr(hinc), _ptr(sl[0]), _ptr(sl[1]), c_int(einc.numel()),
+                                              c_double(ce), c_double(ch), vals8, *tail)
+        else:
+            rc = self.lib.fdtd_tfsf_pass_f32(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(ce), c_double(ch),
+                                             vals8, *tail)
         _check(rc, "tfsf_pass")
         self.launches += 1
         return g

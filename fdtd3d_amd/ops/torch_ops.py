@@ -186,11 +186,12 @@ class TorchOps:
         for l in range(steps):
             nxt = {c: cur[c].clone() for c in cur}
             self.curl_update("E", e, nxt, cur, cbp)
-            if sources is not None and sources[l] is not None:
-                comp, idx, val = sources[l]
-                nxt[comp][tuple(i + 1 for i in idx)] = val
             if tfsf is not None:
                 self._tfsf_level(nxt, tfsf, l, "E", shifted, cbp)
+            if sources is not None and sources[l] is not None:
+                # after the corrections, as the stepped path (and the kernel) does
+                comp, idx, val = sources[l]
+                nxt[comp][tuple(i + 1 for i in idx)] = val
             self.curl_update("H", h, nxt, nxt, cbp)
             if tfsf is not None:
                 self._tfsf_level(nxt, tfsf, l, "H", shifted, cbp)
@@ -266,10 +267,13 @@ class TorchOps:
     tfsf_sets_ok = True  # tb_step applies TfsfSets corrections (the blocked kernel's form)
 
     def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
-                  sets, slot: int = 0) -> torch.Tensor:
+                  sets, slot: int = 0, dry: bool = False) -> torch.Tensor:
         """Reference semantics of k_tfsf_pass (yee3d_tb.hip): the incident
         line advanced ``len(src_vals)`` steps, the per-level g table of the
-        pass returned (levels x sets.ld)."""
+        pass returned (levels x sets.ld).  ``dry``: the line is left as it was
+        (the g table of a hybrid pass, whose shell steps the line itself)."""
+        if dry:
+            einc, hinc = einc.clone(), hinc.clone()
         T = len(src_vals)
         n = einc.numel()
         m = min(n, reach)

@@ -94,6 +94,20 @@ def test_drude_3d(gpu):
                          pml_size=(5, 5, 5), dtype="f64"), gpu, 1e-10)
 
 
+@pytest.mark.parametrize("dtype,hybrid", [("f64", 1), ("f32", 1), ("f32", 0)])
+def test_2d_drude_upml_tfsf(gpu, dtype, hybrid):
+    """2D TMz Drude sphere (the reference's SchemeTMz.cpp:307-572 Ez PML + Drude
+    path) with UPML and a TF/SF plane wave on the HIP chain kernels -- stepped
+    (hybrid 1) and with the automatic hybrid passes (hybrid 0: 2D blocked core
+    around the dispersive box) -- vs the fp64 torch oracle.  The sphere sits
+    in the wave's path, so the dispersive update shapes the fields (the field
+    energy differs from the run without metamaterials)."""
+    cfg = SchemeConfig(scheme="tmz", size=(96, 88, 1), time_steps=120, use_pml=True, pml_size=(8, 8, 1),
+                       use_tfsf=True, tfsf_size=(14, 14, 1), scene="drude-sphere", use_metamaterials=True,
+                       sphere_center=(48.0, 44.0, 0.0), sphere_radius=14.0, dtype=dtype, hybrid_block=hybrid)
+    compare(cfg, gpu, 1e-10 if dtype == "f64" else 5e-5)
+
+
 @pytest.mark.parametrize("scheme", ["tmz", "tez"])
 def test_2d(gpu, scheme):
     compare(SchemeConfig(scheme=scheme, size=(90, 70, 1), time_steps=40, scene="vacuum", dtype="f32"), gpu)

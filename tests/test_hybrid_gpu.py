@@ -177,3 +177,29 @@ def test_hybrid_at_scale(gpu, name, extra):
         del scale
     del runs, hy, st
     torch.cuda.empty_cache()
+
+
+def test_hybrid_graph_reuse_across_advance(gpu):
+    """2D UPML hybrid passes replayed from a HIP graph over TWO ``advance``
+    calls: T = 4, 25 steps end on a tail of one 4-step and one
+    1-step pass, so the field buffers are back in the captured parity while
+    the UPML D level lists are rotated by an odd number of steps.  The second
+    call (30 steps) must recapture rather than replay a graph that reads the
+    stale level -- the result equals the stepped run."""
+    cfg = SchemeConfig(scheme="tez", size=(96, 128, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1), dtype="f32",
+                       scene="vacuum", use_pml=True, use_tfsf=True, phi=60, time_steps=55, hybrid_block=4)
+    hy = YeeScheme(cfg, make_ops("hip", None, gpu, torch.float32))
+    hy.init_scheme()
+    hy.init_grids()
+    assert hy.hybrid is not None and hy.hybrid["T"] == 4
+    hy.advance(25)
+    k1 = hy._hgraph["key"] if getattr(hy, "_hgraph", None) else None
+    hy.advance(30)
+    torch.cuda.synchronize()
+    assert k1 is not None and hy._hgraph["key"] != k1, "graph not recaptured after the level lists rotated"
+    st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, torch.float32)
+    for c in st.comps:
+        b = st.F[0][c].double().cpu()
+        scale = max(float(st.F[0][o].abs().max()) for o in st.comps if o[0] == c[0]) + 1e-30
+        err = float((hy.F[0][c].double().cpu() - b).abs().max())
+        assert err <= 2e-5 * scale, (c, err, scale)

@@ -345,3 +345,14 @@ def test_native_checkpoint_roundtrip(case, tmp_path, gpu):
         assert peak > 0
         for c, v in got.items():
             assert max(v[:2]) <= 1e-11 * peak, (c, v)
+    # the other direction: a checkpoint the PYTHON driver wrote (indent=1 sidecar with multi-line lists,
+    # __version__, origin / topology / sub_step) resumed by the native driver
+    d["pyck"], d["nat2"] = tmp_path / "pyck", tmp_path / "nat2"
+    assert py_run(argv + py + ["--time-steps", str(k), "--checkpoint-dir", str(d["pyck"])], out=io.StringIO()) == 0
+    out = nat(["--time-steps", str(n), "--load-from-file", str(d["pyck"]), "--checkpoint-dir", str(d["nat2"])])
+    assert "Number of time steps: %d (%d timed" % (n, n - k) in out, out
+    for c in COMPS[scheme]:
+        name = "current[%d]_rank-0_%s.dat" % (n, c)
+        ref = np.fromfile(d["full"] / name, dtype=np.float64).reshape(shape)
+        got = np.fromfile(d["nat2"] / name, dtype=np.float64).reshape(shape)
+        assert np.abs(got - ref).max() <= 1e-11 * (np.abs(ref).max() + 1e-300), c
