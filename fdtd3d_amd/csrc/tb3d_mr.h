@@ -55,15 +55,17 @@ struct TbSrc {
 // index along that axis only (`va`), so each pass precomputes, per level,
 // g = sign * projection * interpolated incident line at every index of a set
 // (k_tfsf_pass in yee3d_tb.hip).  Inside the kernel the index along `va` is
-// the plane (va = 0) or the row (va = 1) -- both wave-uniform -- so every
-// correction is ONE scalar per (set, level, plane, row): a scalar load, a
-// lane test along z and a multiply-add on the new value (the update is
-// linear: E + c (curl + g) = (E + c curl) + c g).  A wave keeps two bit masks
-// per kind of the sets that touch its rows / lanes at all (x-face sets only
-// looked at on their plane), so a wave away from every face pays a scalar
-// compare per level.  (The round-4 form parked per-wave slot tables in VGPR
-// lanes and inlined a 6-slot loop at every level and row: 4.8x the plain
-// kernel's code, profiles/tfsf_cost_r5.md.)
+// the plane (va = 0) or the row (va = 1) -- both wave-uniform -- so a
+// correction is ONE value per (set, level, plane or row), added to the new
+// value after the update (E + c (curl + g) = (E + c curl) + c g).  Each wave
+// numbers the sets that touch it as slots; their metadata sit in VGPR lanes
+// and the g values of a trip arrive with one vector load per kind issued
+// before the field prefetch, so the level loop reads everything with
+// readlane (no memory round trip) and a wave away from every face pays a few
+// scalar compares per level.  (Round 4 parked 6 slots per kind and unrolled
+// them at every level and row: twice the plain kernel's VALU work; the first
+// round-5 form read the set table with scalar loads inside the level loop:
+// +55% on the face tiles, which bound the pass.  profiles/tfsf_cost_r5.md.)
 constexpr int TF_MAX_SETS = 24;
 struct TfSet {
   int n;          // component 0..5 = Ex Ey Ez Hx Hy Hz
@@ -423,36 +425,97 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     }
   };
 
-  // TF/SF: the sets that touch this wave's rows / lanes at all, per kind
-  // (bit = set index): x-face sets (one plane each) apart, only looked at on
-  // their plane; y / z-face sets every level (few waves have any)
-  unsigned tf_xe = 0u, tf_xh = 0u, tf_yze = 0u, tf_yzh = 0u;
-  int tf_xe0 = -1, tf_xe1 = -1, tf_xh0 = -1, tf_xh1 = -1;  // x-face planes of the E / H sets
-  int tf_ld = 0;
+  // TF/SF slots: the sets that touch this wave's rows / lanes, per kind k
+  // (0 E, 1 H) numbered c * 4 + s (component c of the kind, its s-th set; a
+  // component has at most 4 face sets: two curl axes x two faces).  Scalar
+  // bit masks (bit c * 4 + s, E in the low half, H << 16) of the y / z-face
+  // slots (looked at every level) and of the x-face slots (looked at on the
+  // kind's x-face planes only); per-lane data in VGPR lanes, read back with
+  // readlane -- no memory round trip inside the level loop:
+  //   tf_xr    lane k * 12 + slot: x range (lo | hi << 16) of the slot's set
+  //            cut to its component's update box;
+  //   tf_lb[k] bit slot * R + r: this lane's cell of row r is a target of the
+  //            slot (set box and update box in y / z);
+  //   tf_off[k] lane e = slot * T + l (va = 0): g-table index of entry e less
+  //            the plane, added per trip;
+  //   tf_g[k][2] entries e (va = 0: slot * T + l; va = 1: (slot * T + l) * R
+  //            + r), loaded once per trip (va = 1: once per kernel, the index
+  //            does not move with the plane) before the field prefetch.
+  unsigned tf_cm = 0u, tf_xm = 0u;
+  int tf_xpl = -1, tf_xph = -1;  // x-face planes of the E / H sets: lo | hi << 16 (-1: none)
+  int tf_xr = 0;
+  // (separate scalars, not arrays: the set-up indexes them by a run-time
+  // kind, which would put an array in scratch memory for the whole kernel)
+  unsigned tf_lb0 = 0u, tf_lb1 = 0u;
+  int tf_off0 = 0, tf_off1 = 0;
+  float tf_g00 = 0.f, tf_g01 = 0.f, tf_g10 = 0.f, tf_g11 = 0.f;
+  int tf_va = 0;
+  const Rsrc tf_gr = __builtin_amdgcn_make_buffer_rsrc((void*)gtab, (short)0, TFS ? T * TFc->ld * 4 : 0, 0x00020000);
   if constexpr (TFS) {
     const int ns = TFc->nsets;
-    tf_ld = TFc->ld;
+    const int ld = TFc->ld;
+    tf_va = TFc->s[0].va;
+    unsigned cnt = 0u;  // sets taken per component, 4 bits each
     for (int si = 0; si < ns; ++si) {
       const int lo1 = TFc->s[si].lo[1], hi1 = TFc->s[si].hi[1];
       const int lo2 = TFc->s[si].lo[2], hi2 = TFc->s[si].hi[2];
-      bool rin = false;
+      const int n = TFc->s[si].n;
+      const int k = n < 3 ? 0 : 1, c = n - 3 * k;
+      // the component's update box, field by field (a Box3 picked among the
+      // by-value box arguments would copy all six to scratch memory)
+#define TF_UB(f, d) (n == 0 ? bex.f[d] : n == 1 ? bey.f[d] : n == 2 ? bez.f[d] : n == 3 ? bhx.f[d] : n == 4 ? bhy.f[d] : bhz.f[d])
+      const int ul0 = TF_UB(lo, 0), uh0 = TF_UB(hi, 0), ul1 = TF_UB(lo, 1), uh1 = TF_UB(hi, 1);
+      const int ul2 = TF_UB(lo, 2), uh2 = TF_UB(hi, 2);
+#undef TF_UB
+      unsigned rb = 0u;
 #pragma unroll
-      for (int r = 0; r < R; ++r) rin = rin || (jw + r >= lo1 && jw + r < hi1);
-      if (!rin || !__any(kin && kb >= lo2 && kb < hi2)) continue;
-      const unsigned bit = 1u << si;
-      const bool e = TFc->s[si].n < 3;
-      if (TFc->s[si].fa == 0) {
-        tf_xe |= e ? bit : 0u;
-        tf_xh |= e ? 0u : bit;
-      } else {
-        tf_yze |= e ? bit : 0u;
-        tf_yzh |= e ? 0u : bit;
+      for (int r = 0; r < R; ++r) {
+        const int j = jw + r;
+        const bool in = kin && j >= lo1 && j < hi1 && kb >= lo2 && kb < hi2 && j >= ul1 && j < uh1 && kb >= ul2 &&
+                        kb < uh2;
+        rb |= in ? (1u << r) : 0u;
+      }
+      if (!__any(rb != 0u)) continue;
+      const int s = (cnt >> (4 * n)) & 0xf;
+      cnt += 1u << (4 * n);
+      if (s >= 4) continue;  // (cannot happen: a component has 4 face sets)
+      const int slot = c * 4 + s;
+      const unsigned bit = 1u << (slot + 16 * k);
+      if (TFc->s[si].fa == 0) tf_xm |= bit; else tf_cm |= bit;
+      const int xl = max(TFc->s[si].lo[0], ul0), xh = min(TFc->s[si].hi[0], uh0);
+      if (lane == k * 12 + slot) tf_xr = xh > xl ? (xl | (xh << 16)) : 0;
+      if (k == 0) tf_lb0 |= rb << (slot * R); else tf_lb1 |= rb << (slot * R);
+      // va = 0: entry (slot, l) of plane p reads g[l * ld + goff + p - lo0]; the plane of level l at
+      // trip X is X - l (E) or X - l - 1 (H), so the index less X is fixed per entry
+#pragma unroll
+      for (int l = 0; l < T; ++l)
+        if (lane == slot * T + l) {
+          const int o = l * ld + TFc->s[si].goff - TFc->s[si].lo[0] - l - k;
+          if (k == 0) tf_off0 = o; else tf_off1 = o;
+        }
+      if (tf_va == 1) {
+        // va = 1: the index moves with the row only -- load the pass's entries now
+#pragma unroll
+        for (int l = 0; l < T; ++l)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int e = (slot * T + l) * R + r;
+            const int gi = l * ld + TFc->s[si].goff + jw + r - lo1;
+            const bool ok = jw + r >= lo1 && jw + r < hi1;
+            const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                tf_gr, (lane == (e & 63) && ok) ? (unsigned)gi * 4u : 0xF0000000u, 0, 0));
+            if (lane == (e & 63)) {
+              if (k == 0 && e < 64) tf_g00 = v;
+              if (k == 0 && e >= 64) tf_g01 = v;
+              if (k == 1 && e < 64) tf_g10 = v;
+              if (k == 1 && e >= 64) tf_g11 = v;
+            }
+          }
       }
     }
-    tf_xe0 = TFc->xpl[0][0];
-    tf_xe1 = TFc->xpl[0][1];
-    tf_xh0 = TFc->xpl[1][0];
-    tf_xh1 = TFc->xpl[1][1];
+    const int e0 = TFc->xpl[0][0], e1 = TFc->xpl[0][1], h0 = TFc->xpl[1][0], h1 = TFc->xpl[1][1];
+    tf_xpl = (e0 & 0xffff) | (e1 << 16);
+    tf_xph = (h0 & 0xffff) | (h1 << 16);
   }
   typedef unsigned u3 __attribute__((ext_vector_type(3)));
   auto coef_ld = [&](const float4* arr, const Box3& B, unsigned off, size_t pl, int p) -> u3 {
@@ -560,6 +623,9 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
       }
     }
   };
+  // per trip, bit 2 l + k: level l has TF/SF fixes of kind k (0 E, 1 H) for
+  // this wave
+  unsigned tf_lv = 0u;
   for (int X = i0 - T; X <= i1 + T - 1; ++X) {
     F3<V> Hc[R], Ec[R];
 #pragma unroll
@@ -616,49 +682,70 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     };
     // TF/SF corrections of kind k (0 E, 1 H) at level l on plane p, added to
     // the new values N of every row: N += c g, c the coefficient the update
-    // multiplied the curl with (0 outside the component's update box)
-    auto tf_fix = [&](int k, int l, int p, F3<V>* N) {
+    // multiplied the curl with (the slots' target bits already hold the
+    // update box in y / z, their x ranges the box in x).  They run at the end
+    // of the level, after the H update -- the level's barrier is a block
+    // boundary anyway, while a branch between the E and H updates costs an
+    // issue-bound level 16% even when idle (profiles/tfsf_cost_r5.md) -- so
+    // an E correction of Ey / Ez also corrects the H update that read the
+    // uncorrected value: Hadj (this level's new H on plane p - 1, same lanes
+    // and rows) gets -/+ its coefficient times the correction.
+    auto tf_fix = [&](int k, int l, int p, F3<V>* N, F3<V>* Hadj) {
       if constexpr (TFS) {
-        const bool xp = k == 0 ? (p == tf_xe0 || p == tf_xe1) : (p == tf_xh0 || p == tf_xh1);
-        unsigned m = (k == 0 ? tf_yze : tf_yzh) | (xp ? (k == 0 ? tf_xe : tf_xh) : 0u);
-        while (m) {
-          const int si = __builtin_ctz(m);
-          m &= m - 1u;
-          const int lo0 = TFc->s[si].lo[0], hi0 = TFc->s[si].hi[0];
-          if ((unsigned)(p - lo0) >= (unsigned)(hi0 - lo0)) continue;
-          const int n = TFc->s[si].n;
-          const int lo1 = TFc->s[si].lo[1], hi1 = TFc->s[si].hi[1];
-          const int lo2 = TFc->s[si].lo[2], hi2 = TFc->s[si].hi[2];
-          const int va = TFc->s[si].va, gb = l * tf_ld + TFc->s[si].goff;
-          const bool lin = kb >= lo2 && kb < hi2;
-          const int c = n - 3 * k;
-          // the component's update box along x (scalar selects: a reference
-          // picked among the by-value box arguments would copy them to scratch)
-          const int ulo = n == 0 ? bex.lo[0] : n == 1 ? bey.lo[0] : n == 2 ? bez.lo[0]
-                        : n == 3 ? bhx.lo[0] : n == 4 ? bhy.lo[0] : bhz.lo[0];
-          const int uhi = n == 0 ? bex.hi[0] : n == 1 ? bey.hi[0] : n == 2 ? bez.hi[0]
-                        : n == 3 ? bhx.hi[0] : n == 4 ? bhy.hi[0] : bhz.hi[0];
-          const bool uin = (unsigned)(p - ulo) < (unsigned)(uhi - ulo);
+        const int xpp = k == 0 ? tf_xpl : tf_xph;
+        const bool xp = p == (short)(xpp & 0xffff) || p == (xpp >> 16);
+        const unsigned m0 = ((tf_cm | (xp ? tf_xm : 0u)) >> (16 * k)) & 0xfffu;
+        if (m0 == 0u) return;
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int j = jw + r;
-            if (j < lo1 || j >= hi1) continue;
-            const float g = cload(gtab, gb + (va == 0 ? p - lo0 : j - lo1));
-            const float3 kc = kcoef(k == 0, l, p, r);
-            const float sc = c == 0 ? kc.x : (c == 1 ? kc.y : kc.z);
-            vec cf;
-            if constexpr (ALLIN)
-              cf = uin ? (vec)(sc) : zero;
-            else
-              cf = cmask<V>((vec)(sc), uin ? (mbits >> ((r * 7 + n) * V)) & VM : 0u);
-            const vec add = lin ? cf * g : zero;
-            N[r].x = N[r].x + (c == 0 ? add : zero);
-            N[r].y = N[r].y + (c == 1 ? add : zero);
-            N[r].z = N[r].z + (c == 2 ? add : zero);
+        for (int c = 0; c < 3; ++c) {
+          unsigned m = (m0 >> (4 * c)) & 0xfu;
+          while (m) {
+            const int slot = c * 4 + __builtin_ctz(m);
+            m &= m - 1u;
+            const int xr = __builtin_amdgcn_readlane(tf_xr, k * 12 + slot);
+            if ((unsigned)(p - (xr & 0xffff)) >= (unsigned)((xr >> 16) - (xr & 0xffff))) continue;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const int e = tf_va == 0 ? slot * T + l : (slot * T + l) * R + r;
+              const float gv = k == 0 ? (e < 64 ? tf_g00 : tf_g01) : (e < 64 ? tf_g10 : tf_g11);
+              const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gv), e & 63));
+              const float3 kc = kcoef(k == 0, l, p, r);
+              const float sc = c == 0 ? kc.x : (c == 1 ? kc.y : kc.z);
+              const bool t = ((k == 0 ? tf_lb0 : tf_lb1) >> (slot * R + r)) & 1u;
+              const vec d = (vec)(t ? sc * g : 0.f);
+              if (c == 0) N[r].x = N[r].x + d;
+              if (c == 1) N[r].y = N[r].y + d;
+              if (c == 2) N[r].z = N[r].z + d;
+              if (k == 0 && c == 1) Hadj[r].z = Hadj[r].z - coef(bhz, p - 1, r, 5, kcoef(false, l, p - 1, r).z) * d;
+              if (k == 0 && c == 2) Hadj[r].y = Hadj[r].y + coef(bhy, p - 1, r, 4, kcoef(false, l, p - 1, r).y) * d;
+            }
           }
         }
       }
     };
+    if constexpr (TFS) {
+      // levels of this trip with fixes, bit 2 l + k (one scalar test per
+      // level and kind); their g entries (va = 0) in one vector load per kind,
+      // issued before the field prefetch so the levels never wait behind it
+      unsigned lv = ((tf_cm & 0xfffu) ? 0x155u : 0u) | ((tf_cm >> 16) ? 0x2aau : 0u);
+      if (tf_xm & 0xfffu) {
+        const int q0 = (short)(tf_xpl & 0xffff), q1 = tf_xpl >> 16;
+        if (q0 >= 0 && (unsigned)(X - q0) < (unsigned)T) lv |= 1u << (2 * (X - q0));
+        if (q1 >= 0 && (unsigned)(X - q1) < (unsigned)T) lv |= 1u << (2 * (X - q1));
+      }
+      if (tf_xm >> 16) {
+        const int q0 = (short)(tf_xph & 0xffff), q1 = tf_xph >> 16;
+        if (q0 >= 0 && (unsigned)(X - 1 - q0) < (unsigned)T) lv |= 2u << (2 * (X - 1 - q0));
+        if (q1 >= 0 && (unsigned)(X - 1 - q1) < (unsigned)T) lv |= 2u << (2 * (X - 1 - q1));
+      }
+      tf_lv = lv & ((1u << (2 * T)) - 1u);
+      if (tf_va == 0 && tf_lv) {
+        tf_g00 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            tf_gr, lane < 12 * T ? (unsigned)(tf_off0 + X) * 4u : 0xF0000000u, 0, 0));
+        tf_g10 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            tf_gr, lane < 12 * T ? (unsigned)(tf_off1 + X) * 4u : 0xF0000000u, 0, 0));
+      }
+    }
     // next plane(s) in flight under this plane's levels
     if (PFD == 2)
       load_plane(X + 2, Hn2, En2);
@@ -701,30 +788,14 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * cx;
         En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * cy;
         En[r].z = Ec[r].z + coef(bez, pe, r, 2, ce.z) * cz;
-        if constexpr (!TFS) {
-          if (src_plane && jw + r == src_j &&
-              (AMP ? (kb >= src_k && kb < amp.k1) : (src_k >= kb && src_k < kb + V))) {
-            const int q = AMP ? 0 : src_k - kb;
-            if (src_comp == 0) En[r].x[q] = sv.v[l];
-            if (src_comp == 1) En[r].y[q] = sv.v[l];
-            if (src_comp == 2) En[r].z[q] = sv.v[l];
-          }
-          amp_level(0, l, pe, r, En[r]);
+        if (src_plane && jw + r == src_j &&
+            (AMP ? (kb >= src_k && kb < amp.k1) : (src_k >= kb && src_k < kb + V))) {
+          const int q = AMP ? 0 : src_k - kb;
+          if (src_comp == 0) En[r].x[q] = sv.v[l];
+          if (src_comp == 1) En[r].y[q] = sv.v[l];
+          if (src_comp == 2) En[r].z[q] = sv.v[l];
         }
-      }
-      if constexpr (TFS) {
-        // corrections first, the hard source then overrides (the stepped
-        // order: update + TF/SF tables, then sources)
-        tf_fix(0, l, pe, En);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (src_plane && jw + r == src_j && src_k >= kb && src_k < kb + V) {
-            const int q = src_k - kb;
-            if (src_comp == 0) En[r].x[q] = sv.v[l];
-            if (src_comp == 1) En[r].y[q] = sv.v[l];
-            if (src_comp == 2) En[r].z[q] = sv.v[l];
-          }
-        }
+        amp_level(0, l, pe, r, En[r]);
       }
       const int ph = pe - 1;
 #pragma unroll
@@ -752,7 +823,14 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         Hp[l][r] = Hc[r];
         Hc[r] = Hn;
       }
-      tf_fix(1, l, ph, Hc);
+      // TF/SF fixes of the level (after the H update, see tf_fix): E on plane
+      // pe (now Ep[l]), H on plane ph (now Hc)
+      if constexpr (TFS) {
+        if (tf_lv & (3u << (2 * l))) {
+          tf_fix(0, l, pe, Ep[l], Hc);
+          tf_fix(1, l, ph, Hc, Hc);
+        }
+      }
       // the next trip's level-0 maxima, in flight under the remaining levels
       if (AMP && l == 0) amp_prefetch(X);
     }
@@ -770,7 +848,10 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
 #pragma unroll
       for (int r = 0; r < R; ++r) Hs[r] = Hc[r];
     } else {
-      store_plane(X, En, Hc);
+      if constexpr (TFS)
+        store_plane(X, Ep[T - 1], Hc);  // (= En plus the last level's TF/SF fixes)
+      else
+        store_plane(X, En, Hc);
     }
   }
   if (DEFER) {

@@ -516,6 +516,37 @@ FDTD_API int fdtd_tb3d_v4_f32(const float* const* ein, const float* const* hin, 
   return (int)hipErrorInvalidValue;
 }
 
+// Cost experiments of the in-kernel TF/SF (FDTD3D_TF_EXP, profiles/tfsf_cost_r5.md):
+// 1 = no sets (the variant's structure alone), 2 = x-face sets only, 3 = y / z-face
+// sets only.  The physics is then wrong; timing runs only.
+static const void* tfsf_experiment(const void* tf, hipStream_t s) {
+  static int mode = -1;
+  static TfDev* scratch = nullptr;
+  static const void* last = nullptr;  // the filtered copy is made once per set table (no sync per pass)
+  if (mode < 0) {
+    const char* e = getenv("FDTD3D_TF_EXP");
+    mode = e ? atoi(e) : 0;
+  }
+  if (mode <= 0) return tf;
+  if (tf == last && scratch) return scratch;
+  last = tf;
+  TfDev h;
+  if (hipMemcpyAsync(&h, tf, sizeof(TfDev), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return tf;
+  TfDev o = h;
+  o.nsets = 0;
+  for (int i = 0; i < h.nsets; ++i) {
+    const bool xf = h.s[i].fa == 0;
+    if (mode == 1 || (mode == 2 && !xf) || (mode == 3 && xf)) continue;
+    o.s[o.nsets++] = h.s[i];
+  }
+  if (mode != 2) o.xpl[0][0] = o.xpl[0][1] = o.xpl[1][0] = o.xpl[1][1] = -1;
+  if (!scratch && hipMalloc(&scratch, sizeof(TfDev)) != hipSuccess) return tf;
+  if (hipMemcpyAsync(scratch, &o, sizeof(TfDev), hipMemcpyHostToDevice, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return tf;
+  return scratch;
+}
+
 // T fused leapfrog steps on the multi-row kernel with its extensions:
 // sparse per-cell coefficients -- ``ce4`` / ``ch4`` hold the E / H
 // coefficients of the three components as one float4 per cell of the box
@@ -538,6 +569,7 @@ FDTD_API int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin,
   TbSrc sv;
   for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
   const int fx = (ce4 && !box_empty(BE) ? 1 : 0) | (ch4 && !box_empty(BH) ? 2 : 0) | (tf && gtab ? 4 : 0);
+  if (tf && gtab) tf = tfsf_experiment(tf, (hipStream_t)stream);
   return tb_mr_dispatch(fx, ein, hin, eout, hout, (const float4*)(box_empty(BE) ? nullptr : ce4),
                         (const float4*)(box_empty(BH) ? nullptr : ch4), BE, BH, (float)cb, (float)db, nx, ny, nz, b,
                         O, xchunk, steps, src, sv, (const TfDev*)tf, gtab, AmpDev{}, (hipStream_t)stream);

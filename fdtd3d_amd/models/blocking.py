@@ -251,8 +251,16 @@ class BlockedStepping:
         itself (``TfsfSets``: incidence along x or y, 3D; csrc/tb3d_mr.h
         ``tf_fix``), so the TF/SF faces need not lie in the stepped shell."""
         cfg = self.cfg
+        mode = getattr(cfg, "hybrid_tfsf", "auto")
         if (not cfg.use_tfsf or cfg.scheme != "3d" or getattr(self, "tfsf_sets", None) is None
-                or getattr(cfg, "hybrid_tfsf", "auto") == "shell" or T > TFSF_MAX_STEPS):
+                or mode == "shell" or T > TFSF_MAX_STEPS):
+            return False
+        if mode == "auto" and self.use_cpml:
+            # measured (512^3 fp32, T = 5, profiles/tfsf_cost_r5.md): with UPML the
+            # faces in the core win (87.0k vs 81.1k Mcells/s: the D/B-form chain
+            # shell is dear per cell), with CPML the shell keeps them (93.1k vs
+            # 91.2k: the folded CPML kernels step the vacuum windows cheaply
+            # while the TF/SF face tiles still cost the core ~30%)
             return False
         return True
 

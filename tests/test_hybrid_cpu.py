@@ -113,6 +113,11 @@ def test_hybrid_checkpoint_resume(tmp_path):
 RANDOM_CASES = [
     # TF/SF along +x (the reference default) and +y
     ("cpml-tfsf-x", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 11),
+    # the TF/SF faces inside the blocked core (in-kernel TfsfSets; automatic with UPML, asked for here)
+    ("cpml-tfsf-x-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, hybrid_tfsf="core"), 5,
+     12),
+    ("cpml-tfsf-y-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90, psi=30,
+                              hybrid_tfsf="core"), 3, 10),
     ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90), 3, 10),
     ("upml-tfsf-x", dict(scene="vacuum", use_pml=True, use_tfsf=True), 5, 12),
     ("cpml-point", dict(scene="vacuum", use_pml=True, pml_type="cpml"), 5, 11),
@@ -149,6 +154,8 @@ def test_hybrid_random_fields_match_stepped(name, extra, T, steps):
         s.init_grids()
         if hb > 1:
             assert s.hybrid is not None, "hybrid plan rejected"
+            if name.endswith("-core"):
+                assert s.hybrid["core_tfsf"], "TF/SF faces not in the blocked core"
         s.randomize_fields(seed=5)
         s.perform_steps()
         runs.append(s)

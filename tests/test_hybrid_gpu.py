@@ -34,6 +34,11 @@ CASES = [
                            scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=60), 5, 17),
     # TF/SF along x / y, T = 5 passes, complex fields
     ("cpml-tfsf-x", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True), 4, 13),
+    # TF/SF faces in the blocked core (automatic with UPML; forced here), x and y incidence, T = 5
+    ("cpml-tfsf-x-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, hybrid_tfsf="core"), 5,
+     13),
+    ("cpml-tfsf-y-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0,
+                              hybrid_tfsf="core"), 4, 11),
     ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0), 3, 11),
     ("cpml-tfsf-sphere", dict(scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
                               sphere_center=(40.0, 36.0, 48.0), sphere_radius=10.0), 4, 10),
@@ -79,6 +84,8 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
     assert hy.hybrid is not None, "hybrid plan rejected"
     if name.endswith("-graph"):
         assert getattr(hy, "_hgraph", None) is not None, "no graph replay"
+    if name.endswith("-core"):
+        assert hy.hybrid["core_tfsf"], "TF/SF faces not in the blocked core"
     st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, dt)
     assert st.hybrid is None
     ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
