@@ -82,6 +82,10 @@ int fdtd_tb3d_amp_f32(const float* const* ein, const float* const* hin, float* c
                       double cb, double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
                       int steps, const int* src, const double* src_vals, float* const* amp, const int* aboxes,
                       double accuracy, unsigned* counts, void* stream);
+int fdtd_tb3d_drude_f32(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
+                        double cb, double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
+                        int steps, const int* src, const double* src_vals, const int* bbox, void* const* sin,
+                        void* const* sout, const void* lut, int nid, double cbd, void* stream);
 int fdtd_tfdev_size();
 int fdtd_tfsf_pass_f32(float* einc, float* hinc, int n, double ce, double ch, const double* src_vals, int steps,
                        int reach, int nE, int nH, const int* I0, const float* W0, const float* W1, const float* C,

@@ -104,6 +104,41 @@ struct AmpDev {
   int k1;            // the source's z line: src_k .. k1 - 1
 };
 
+// Drude box folded into the blocked passes (feature bit 16, its own launch
+// over the box grown by T: models/blocking.py _drude_blk_plan).  Reference
+// Drude form Kernels.h:103-107 / Scheme3D.cpp:266-416, stepped here by the
+// fused chain (chain_kernels.hip).  Inside the sigma = 0 region the chain
+//   Dn = D + cbd curl,  D1n = b0 Dn + b1 D + b2 Dp + m1 D1 + m2 D1p,
+//   E' = E + (cbEa D1n + ccEa D1) / (2 eps0) = E + (D1n - D1)
+// keeps E - D1 invariant (0 from rest), and the Drude ADE has
+// b1 = -(b0 + b2), so with D1 = E:
+//   E' = (b0 cbd) curl - b2 (D - Dp) + m1 E + m2 Ep,   (D - Dp)' = cbd curl,  Ep' = E
+// A cell's dispersive state is (delta = D - Dp, Ep) per E component -- six
+// floats instead of the chain's four levels of D / D1 -- and the coefficient
+// tuple (b0 cbd, b2, m1, m2) of each component comes from a per-component
+// table indexed by the cell's material id (uint8; a Drude scene holds a
+// handful of distinct tuples), parked in LDS.  The state of a cell moves
+// from level to level in registers, like the fields: level l hands its
+// output to level l + 1 of the next trip (the same plane), so a pass reads
+// and writes it once.  Memory: per cell of B, two float4 per state set:
+//   s[0] = (delta_x, delta_y, delta_z, id_x | id_y << 8 | id_z << 16 as bits)
+//   s[1] = (Ep_x, Ep_y, Ep_z, 0)
+constexpr int DR_MAX_IDS = 256;
+struct DrDev {
+  Box3 B;                  // dispersive box (local): the E components take the form above inside
+  const float4* sin0;      // state in (delta + ids, Ep), x-major over B, z fastest
+  const float4* sin1;
+  float4* sout0;           // state out (distinct buffers: tiles re-read halo cells other tiles own)
+  float4* sout1;
+  const float4* lut;       // [3][nid]: (b0 cbd, b2, m1, m2) per component and id
+  int nid;
+  float cbd;               // D update coefficient dt / dx (the chain's cbD where sigma = 0)
+};
+struct DrS {
+  float dx, dy, dz, px, py, pz;
+  unsigned id;
+};
+
 // Memory access through buffer descriptors: one descriptor per (array, x
 // plane) built in SGPRs from the wave-uniform plane index, plus ONE 32-bit
 // per-lane byte offset shared by every array (buffer_load ... offen).  Flat
@@ -224,13 +259,15 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     const float4* __restrict__ ce4, const float4* __restrict__ ch4, Box3 BE, Box3 BH, float cb,
     float db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc sv, int xcd_swz,
-    const TfDev* __restrict__ tf, const float* __restrict__ gtab, AmpDev amp) {
+    const TfDev* __restrict__ tf, const float* __restrict__ gtab, AmpDev amp, DrDev dr) {
   // feature bits: 1 per-cell E, 2 per-cell H coefficients (sparse), 4 TF/SF,
-  // 8 amplitude mode (alone; T <= 3: its LDS hand-off)
+  // 8 amplitude mode (alone; T <= 3: its LDS hand-off), 16 Drude box (alone)
   constexpr int PC = FX & 3;
   constexpr bool TFS = FX & 4;
   constexpr bool AMP = FX & 8;
+  constexpr bool DRU = FX & 16;
   static_assert(!AMP || (FX == 8 && V == 1 && T <= 3), "amplitude mode: scalar lanes, alone, T <= 3");
+  static_assert(!DRU || FX == 16, "Drude box: alone");
   static_assert(V == 1 || !FX, "sparse coefficients / TF/SF: scalar lanes");
   constexpr bool PCE = PC & 1, PCH = PC & 2;  // per-cell E / H coefficients
   static_assert(R * V <= 4, "mask bit field holds 7 boxes x R rows x V cells");
@@ -425,6 +462,36 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
     }
   };
 
+  // Drude box: per row, the lane's byte offset in one x plane of the state
+  // arrays (16 B per cell of B; past the plane outside B in y / z) and bit r
+  // of dinb when row r of this lane lies in B (y / z; x per plane)
+  unsigned doff[DRU ? R : 1];
+  unsigned dinb = 0u;
+  __shared__ float4 sL[DRU ? 3 * DR_MAX_IDS : 1];
+  const int dbz = dr.B.hi[2] - dr.B.lo[2];
+  const size_t dplane = DRU ? (size_t)(dr.B.hi[1] - dr.B.lo[1]) * dbz * 16u : 0;
+  if constexpr (DRU) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int j = jw + r;
+      const bool in = kin && j >= dr.B.lo[1] && j < dr.B.hi[1] && kb >= dr.B.lo[2] && kb < dr.B.hi[2];
+      doff[r] = in ? (unsigned)((j - dr.B.lo[1]) * dbz + (kb - dr.B.lo[2])) * 16u : 0xF0000000u;
+      dinb |= (in ? 1u : 0u) << r;
+    }
+    // the coefficient tables into LDS (read by lane id at every level)
+    for (int i = lane + 64 * w; i < 3 * DR_MAX_IDS; i += 64 * NW) {
+      const int c = i / DR_MAX_IDS, id = i - c * DR_MAX_IDS;
+      sL[i] = id < dr.nid ? dr.lut[c * dr.nid + id] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+  }
+  const bool wave_d = DRU && __any(dinb != 0u);
+  auto dr_rsrc = [&](const void* base, int p) -> Rsrc {
+    const bool in = xin(dr.B, p);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (in ? (size_t)(p - dr.B.lo[0]) * dplane : 0)),
+                                             (short)0, in ? (int)dplane : 0, 0x00020000);
+  };
+
   // TF/SF slots: the sets that touch this wave's rows / lanes, per kind k
   // (0 E, 1 H) numbered c * 4 + s (component c of the kind, its s-th set; a
   // component has at most 4 face sets: two curl axes x two faces).  Scalar
@@ -587,6 +654,40 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
   F3<V> Hs[R];  // DEFER: H_T of the previous plane, stored next trip
 #pragma unroll
   for (int r = 0; r < R; ++r) Hs[r] = F3<V>{};
+  // Drude state (see DrDev): DS[l] = the output of level l in the previous
+  // trip (plane X - 1 - l), which level l + 1 takes in this trip; Dc = the
+  // input of the level running; Dnx = the next trip's level-0 input
+  // (prefetched); DL = the last level's output, stored with the fields
+  constexpr int NDS = DRU ? (T > 1 ? T - 1 : 1) : 1;
+  constexpr int RD = DRU ? R : 1;
+  DrS DS[NDS][RD], Dnx[RD], Dc[RD], DL[RD];
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  auto dr_load = [&](int X, DrS* S) {
+    if constexpr (DRU) {
+      const Rsrc r0 = dr_rsrc(dr.sin0, X), r1 = dr_rsrc(dr.sin1, X);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u4v a = __builtin_amdgcn_raw_buffer_load_b128(r0, doff[r], 0, 0);
+        const u3 b = __builtin_amdgcn_raw_buffer_load_b96(r1, doff[r], 0, 0);
+        S[r].dx = __uint_as_float(a.x);
+        S[r].dy = __uint_as_float(a.y);
+        S[r].dz = __uint_as_float(a.z);
+        S[r].id = a.w;
+        S[r].px = __uint_as_float(b.x);
+        S[r].py = __uint_as_float(b.y);
+        S[r].pz = __uint_as_float(b.z);
+      }
+    }
+  };
+  if constexpr (DRU) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      DL[r] = Dc[r] = Dnx[r] = DrS{};
+#pragma unroll
+      for (int l = 0; l < NDS; ++l) DS[l][r] = DrS{};
+    }
+    if (wave_d) dr_load(i0 - T, Dnx);
+  }
   // stores of the results of trip X: E_T on plane X-T+1 (= Ep[T-1] until the
   // next trip's last level), H_T on plane X-T
   auto store_plane = [&](int X, const F3<V>* Es, const F3<V>* Hh) {
@@ -746,6 +847,13 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
             tf_gr, lane < 12 * T ? (unsigned)(tf_off1 + X) * 4u : 0xF0000000u, 0, 0));
       }
     }
+    // Drude: this trip's level-0 state, the next one's in flight (issued
+    // before the field prefetch: vmcnt retires in issue order)
+    if constexpr (DRU) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) Dc[r] = Dnx[r];
+      if (wave_d) dr_load(X + 1, Dnx);
+    }
     // next plane(s) in flight under this plane's levels
     if (PFD == 2)
       load_plane(X + 2, Hn2, En2);
@@ -788,6 +896,38 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         En[r].x = Ec[r].x + coef(bex, pe, r, 0, ce.x) * cx;
         En[r].y = Ec[r].y + coef(bey, pe, r, 1, ce.y) * cy;
         En[r].z = Ec[r].z + coef(bez, pe, r, 2, ce.z) * cz;
+        if constexpr (DRU) {
+          // dispersive form inside B (see DrDev); the state moves on to level l + 1
+          const DrS s = Dc[r];
+          if (wave_d && xin(dr.B, pe)) {
+            const float4 kx = sL[s.id & 0xffu];
+            const float4 ky = sL[DR_MAX_IDS + ((s.id >> 8) & 0xffu)];
+            const float4 kz = sL[2 * DR_MAX_IDS + ((s.id >> 16) & 0xffu)];
+            const bool in = (dinb >> r) & 1u;
+            const float nx_ = kx.x * cx[0] - kx.y * s.dx + kx.z * Ec[r].x[0] + kx.w * s.px;
+            const float ny_ = ky.x * cy[0] - ky.y * s.dy + ky.z * Ec[r].y[0] + ky.w * s.py;
+            const float nz_ = kz.x * cz[0] - kz.y * s.dz + kz.z * Ec[r].z[0] + kz.w * s.pz;
+            if (in) {
+              En[r].x[0] = nx_;
+              En[r].y[0] = ny_;
+              En[r].z[0] = nz_;
+            }
+          }
+          DrS o;
+          o.dx = dr.cbd * cx[0];
+          o.dy = dr.cbd * cy[0];
+          o.dz = dr.cbd * cz[0];
+          o.px = Ec[r].x[0];
+          o.py = Ec[r].y[0];
+          o.pz = Ec[r].z[0];
+          o.id = s.id;
+          if (l < T - 1) {
+            Dc[r] = DS[l < T - 1 ? l : 0][r];
+            DS[l < T - 1 ? l : 0][r] = o;
+          } else {
+            DL[r] = o;
+          }
+        }
         if (src_plane && jw + r == src_j &&
             (AMP ? (kb >= src_k && kb < amp.k1) : (src_k >= kb && src_k < kb + V))) {
           const int q = AMP ? 0 : src_k - kb;
@@ -844,6 +984,28 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_mr(
         sC[sl][2][R * w + r][lane] = __uint_as_float(RQ[r].z);
       }
     }
+    if constexpr (DRU) {
+      // the last level's state (plane X - T + 1): owned cells of B
+      const int pe = X - T + 1;
+      const Rsrc r0 = dr_rsrc(dr.sout0, pe), r1 = dr_rsrc(dr.sout1, pe);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const unsigned mo = (mbits >> ((r * 7 + 6) * V)) & VM;
+        const unsigned o = (wave_d && mo && ((dinb >> r) & 1u) && pe >= i0 && pe < i1) ? doff[r] : 0xF0000000u;
+        u4v a;
+        a.x = __float_as_uint(DL[r].dx);
+        a.y = __float_as_uint(DL[r].dy);
+        a.z = __float_as_uint(DL[r].dz);
+        a.w = DL[r].id;
+        u4v b;
+        b.x = __float_as_uint(DL[r].px);
+        b.y = __float_as_uint(DL[r].py);
+        b.z = __float_as_uint(DL[r].pz);
+        b.w = 0u;
+        __builtin_amdgcn_raw_buffer_store_b128(a, r0, o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(b, r1, o, 0, 0);
+      }
+    }
     if (DEFER) {
 #pragma unroll
       for (int r = 0; r < R; ++r) Hs[r] = Hc[r];
@@ -887,7 +1049,7 @@ template <int T, int V, int R, int FX, int NW = TBW>
 int launch_tb_mr(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,
                  const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH, float cb, float db, int nx,
                  int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src, const TbSrc& sv,
-                 const TfDev* tf, const float* gtab, const AmpDev& amp, hipStream_t s) {
+                 const TfDev* tf, const float* gtab, const AmpDev& amp, hipStream_t s, const DrDev& dr = DrDev{}) {
   constexpr int HL = (T + V - 1) / V;
   constexpr int TBZ = (64 - 2 * HL) * V;
   dim3 grid(cdiv(O.hi[2] - (O.lo[2] & ~(V - 1)), TBZ), cdiv(O.hi[1] - O.lo[1], NW * R - 2 * T),
@@ -897,7 +1059,7 @@ int launch_tb_mr(const float* const* ein, const float* const* hin, float* const*
       ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2], \
       ce4, ch4, BE, BH, cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5],                             \
       O, xchunk, src[0], src[1], src[2], src[3], sv,                                                       \
-      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, amp)
+      g_tb_mr_xcd ? (1 | (g_tb_mr_noallin << 1) | tb_patch_bits()) : (g_tb_mr_noallin << 1), tf, gtab, amp, dr)
   if constexpr (FX != 0) {
     MR_LAUNCH(1, false);  // tuning variants: uniform media only
   } else {

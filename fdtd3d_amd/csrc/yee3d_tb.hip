@@ -329,9 +329,15 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
                      float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                      float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk,
                      const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const AmpDev& amp,
-                     hipStream_t s) {
-#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, amp, s
+                     hipStream_t s, const DrDev& dr = DrDev{}) {
+#define MR_ARGS ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, amp, s, dr
   // amplitude mode: uniform media, T <= 3 (tb3d_mr.h AmpDev)
+  // Drude box (tb3d_mr.h DrDev): 8 waves x 2 rows (16-row tiles, <= 256
+  // VGPRs: the dispersive state of T - 1 levels rides in registers)
+  if (fx == 16) {
+    if constexpr (T <= 5) return launch_tb_mr<T, 1, 2, 16, 8>(MR_ARGS);
+    return (int)hipErrorInvalidValue;
+  }
   if (fx == 8) {
     if constexpr (T <= 3) {
       // 16 waves x 2 rows; the 8 x 4 shape (tuning knob 1) needs 200-256 VGPRs
@@ -366,7 +372,8 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
 // automatic x chunk of a multi-row pass over output box O
 int tb_mr_xchunk(int fx, const Box3& O, int steps) {
   const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
-  const long long gy = cdiv(O.hi[1] - O.lo[1], TBW * 2 - 2 * steps);
+  // (the Drude variant's tiles are 8 waves x 2 rows)
+  const long long gy = cdiv(O.hi[1] - O.lo[1], (fx == 16 ? 16 : TBW * 2) - 2 * steps);
   // the 8-wave shape fits two workgroups per CU
   return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) ? 2 : 1);
 }
@@ -377,9 +384,9 @@ int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, flo
                    float* const* hout, const float4* ce4, const float4* ch4, const Box3& BE, const Box3& BH,
                    float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, int steps,
                    const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const AmpDev& amp,
-                   hipStream_t s) {
+                   hipStream_t s, const DrDev& dr = DrDev{}) {
   if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
-#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, amp, s
+#define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, amp, s, dr
   switch (steps) {
     case 1: return launch_tb_mr_sel<1>(MR_ARGS);
     case 2: return launch_tb_mr_sel<2>(MR_ARGS);
@@ -615,6 +622,50 @@ FDTD_API int fdtd_tb3d_amp_f32(const float* const* ein, const float* const* hin,
   const Box3 nb = make_box(kNoBox);
   return tb_mr_dispatch(8, ein, hin, eout, hout, nullptr, nullptr, nb, nb, (float)cb, (float)db, nx, ny, nz, b, O,
                         xchunk, steps, src, sv, nullptr, nullptr, A, (hipStream_t)stream);
+}
+
+// T <= 5 fused leapfrog steps over the output box with the Drude box B
+// folded in (tb3d_mr.h DrDev; uniform media outside B, scalar coefficients):
+// ``bbox`` = B (local lo[3], hi[3]), ``sin`` / ``sout`` = the two float4
+// state arrays (delta + ids, Ep) over B before / after the pass (distinct),
+// ``lut`` = 3 x ``nid`` float4 (b0 cbd, b2, m1, m2), ``cbd`` the D update
+// coefficient.  B must lie inside the three E update boxes.  Other arguments
+// as fdtd_tb3d_v4_f32.
+FDTD_API int fdtd_tb3d_drude_f32(const float* const* ein, const float* const* hin, float* const* eout,
+                                 float* const* hout, double cb, double db, int nx, int ny, int nz, const int* boxes,
+                                 const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
+                                 const int* bbox, void* const* sin, void* const* sout, const void* lut, int nid,
+                                 double cbd, void* stream) {
+  if (nz % 4 != 0 || steps < 1 || steps > 5 || !sin || !sout || !lut || nid < 1 || nid > DR_MAX_IDS)
+    return (int)hipErrorInvalidValue;
+  Box3 b[6];
+  for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
+  const Box3 O = make_box(obox);
+  if (box_empty(O)) return 0;
+  DrDev D;
+  D.B = make_box(bbox);
+  if (box_empty(D.B)) return (int)hipErrorInvalidValue;
+  for (int d = 0; d < 3; ++d) {
+    if (D.B.lo[d] < 0 || D.B.hi[d] > (d == 0 ? nx : d == 1 ? ny : nz)) return (int)hipErrorInvalidValue;
+    for (int n = 0; n < 3; ++n)
+      if (D.B.lo[d] < b[n].lo[d] || D.B.hi[d] > b[n].hi[d]) return (int)hipErrorInvalidValue;
+  }
+  // one x plane of a state array is addressed by a 32-bit byte offset
+  if ((long long)(D.B.hi[1] - D.B.lo[1]) * (D.B.hi[2] - D.B.lo[2]) * 16 >= (1ll << 31)) return (int)hipErrorInvalidValue;
+  if (!sin[0] || !sin[1] || !sout[0] || !sout[1] || sin[0] == sout[0] || sin[1] == sout[1])
+    return (int)hipErrorInvalidValue;
+  D.sin0 = (const float4*)sin[0];
+  D.sin1 = (const float4*)sin[1];
+  D.sout0 = (float4*)sout[0];
+  D.sout1 = (float4*)sout[1];
+  D.lut = (const float4*)lut;
+  D.nid = nid;
+  D.cbd = (float)cbd;
+  TbSrc sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? (float)src_vals[l] : 0.f;
+  const Box3 nb = make_box(kNoBox);
+  return tb_mr_dispatch(16, ein, hin, eout, hout, nullptr, nullptr, nb, nb, (float)cb, (float)db, nx, ny, nz, b, O,
+                        xchunk, steps, src, sv, nullptr, nullptr, AmpDev{}, (hipStream_t)stream, D);
 }
 
 // size of the TfDev block the host fills (ABI check)

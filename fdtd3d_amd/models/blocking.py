@@ -55,6 +55,9 @@ F32_AUTO_STEPS_PERCELL_BOTH = 2
 F32_AUTO_STEPS_TFSF = 4
 # longest pass of the TF/SF variant (yee3d_tb.hip launch_tb_mr_sel: T <= 5)
 TFSF_MAX_STEPS = 5
+# steps per pass with the Drude box inside the blocked passes (its variant
+# holds T - 1 levels of dispersive state in registers: T <= 5)
+DRUDE_AUTO_STEPS = 5
 
 
 
@@ -128,6 +131,8 @@ class BlockedStepping:
     (uses its fields, ops, domain, halo, layout and per-step update methods)."""
 
     _tfsf_once = False
+    drude_blk = None   # the Drude box inside the blocked passes (_plan_drude_blk), None: off
+    _drude_plan = None
     pass_timer = None  # PassTimer of decomposed passes (bench.py / --json), None: off
     _skip_side_wait = False  # tests only: drop the main stream's wait on the exchange (negative control)
 
@@ -157,6 +162,205 @@ class BlockedStepping:
         side.wait_stream(torch.cuda.current_stream(self.device))
         return side
 
+    # ------------------------------------------------- Drude box, blocked
+    def _plan_drude_blk(self):
+        """The dispersive box inside the blocked passes (csrc/tb3d_mr.h
+        DrDev): every pass runs the plain blocked kernel over the core, then
+        the Drude variant over the box grown by T (its halo cells ran the plain
+        update in the first launch), reading and writing the box's dispersive
+        state -- (delta = D - Dp, Ep) per E component -- once per pass.  The
+        stepped chain never runs on the box (the hybrid's shell keeps the
+        absorbing layers only).  Returns the plan (T, box, tables) or None:
+        serial 3D runs of an electric Drude medium with uniform eps / gamma
+        (coefficient tuples in a table of <= 256 rows per component), the box
+        in the sigma = 0 region, no TF/SF, amplitude mode or complex fields;
+        ``--blocked-drude off`` (or one step per pass) keeps the stepped
+        dispersive box.  Reference: Scheme3D.cpp:266-416, Kernels.h:103-107."""
+        cfg = self.cfg
+        mode = getattr(cfg, "blocked_drude", "auto")
+        if (mode == "off" or not cfg.use_metamaterials or cfg.scheme != "3d" or not hasattr(self.ops, "tb_drude_step")
+                or (self.ops.name != "hip" and mode != "on")):
+            return None
+        if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
+            return None
+        if (self.halo is not None or self.planes != 1 or cfg.use_tfsf or cfg.use_amp_mode or self.graph_mode
+                or not self.use_upml_chain or getattr(self, "chain_regions", None) is None or self.use_cpml
+                or getattr(cfg, "dispersion", "drude") != "drude" or self.hooks):
+            return None
+        if any("D1" in self.upml[c] for c in self.h_comps) or not any("D1" in self.upml[c] for c in self.e_comps):
+            return None
+        if any(not self.cb[c].is_scalar for c in self.comps):
+            return None
+        T = int(cfg.hybrid_block) if int(cfg.hybrid_block) > 0 else int(cfg.time_block)
+        if T <= 0:
+            T = DRUDE_AUTO_STEPS
+        T = min(T, int(getattr(self.ops, "tb_drude_max_steps", 5)))
+        if T <= 1:
+            return None
+        dom = self.domain
+        alloc = dom.allocated_global()
+        store, B = {}, None
+        for c in self.e_comps:
+            S = self._bbox_global(self.upml[c].get("drude_active")) if "D1" in self.upml[c] else None
+            if S is not None and box_empty(S):
+                S = None
+            store[c] = S
+            if S is not None:
+                B = S if B is None else (tuple(min(B[0][d], S[0][d]) for d in range(3)),
+                                         tuple(max(B[1][d], S[1][d]) for d in range(3)))
+        if B is None:
+            return None
+        for c in self.e_comps:
+            sig0 = self._chain_sigma0.get(c)
+            ub = self._global_box(c)
+            for d in range(3):
+                if sig0 is None or B[0][d] < sig0[0][d] or B[1][d] > sig0[1][d]:
+                    return None  # the box reaches into an absorbing layer
+                if B[0][d] < ub[0][d] or B[1][d] > ub[1][d]:
+                    return None
+        Bl = dom.to_local(B)
+        bshape = tuple(Bl[1][d] - Bl[0][d] for d in range(3))
+        # D coefficient where sigma = 0 (the chain's cbD profile), the same for the three components
+        cbd = None
+        for c in self.e_comps:
+            pr = self.upml[c]["prof"]
+            aD = pr["axes"][0]
+            v = pr["cbD"][Bl[0][aD]:Bl[1][aD]].double()
+            if bool((v != v[0]).any()):
+                return None
+            if cbd is None:
+                cbd = float(v[0])
+            elif abs(float(v[0]) - cbd) > 1e-6 * abs(cbd):
+                return None
+        # per component: material index over B into (b0 cbd, b2, m1, m2) rows; cells outside the
+        # component's own dispersive box take the plain row (cb, 0, 1, 0): E' = E + cb curl
+        ids4 = torch.zeros(bshape, dtype=torch.int32, device=self.device)
+        rows = []
+        for q, c in enumerate(self.e_comps):
+            st = self.upml[c]
+            plain = [float(self.cb[c].scalar), 0.0, 1.0, 0.0]
+            S = store[c]
+            if S is None:
+                rows.append(torch.tensor([plain], dtype=torch.float64))
+                continue
+            Sl = dom.to_local(S)
+            ssl = tuple(slice(Sl[0][d], Sl[1][d]) for d in range(3))
+            lut = st.get("_drude_lut")
+            if lut is not None and lut[0] is not None:
+                ids_s = lut[0][ssl].to(torch.int32)
+                tab = lut[1].double().cpu()
+            else:
+                cells = [st[n].materialize(ssl) for n in ("b0", "b1", "b2", "ma1", "ma2")]
+                cells = torch.stack([torch.as_tensor(x, dtype=torch.float64).expand(Sl[1][0] - Sl[0][0],
+                                     Sl[1][1] - Sl[0][1], Sl[1][2] - Sl[0][2]) for x in cells], -1)
+                tab, inv = torch.unique(cells.reshape(-1, 5), dim=0, return_inverse=True)
+                tab = tab.cpu()
+                ids_s = inv.reshape(cells.shape[:3]).to(torch.int32)
+            b0, b1, b2, m1, m2 = (tab[:, k] for k in range(5))
+            if bool(((b0 + b1 + b2).abs() > 1e-5 * (b0.abs() + b1.abs() + b2.abs())).any()):
+                return None  # not the Drude ADE (b1 = -(b0 + b2))
+            nid = tab.shape[0]
+            if nid + 1 > 256:
+                return None
+            r = torch.stack([b0 * cbd, b2, m1, m2], 1)
+            rows.append(torch.cat([r, torch.tensor([plain], dtype=torch.float64)]))
+            # non-dispersive cells take the plain row too: the stepped chain runs the plain update
+            # outside each row's material z range and leaves their D / D1 levels stale
+            act = st["drude_active"][ssl].to(self.device)
+            idc = torch.full(bshape, nid, dtype=torch.int32, device=self.device)
+            idc[tuple(slice(Sl[0][d] - Bl[0][d], Sl[1][d] - Bl[0][d]) for d in range(3))] = torch.where(
+                act, ids_s.to(self.device), torch.full_like(ids_s, nid, device=self.device))
+            ids4 |= idc << (8 * q)
+        nid = max(r.shape[0] for r in rows)
+        lut = torch.zeros(3, nid, 4, dtype=torch.float64)
+        for q, r in enumerate(rows):
+            lut[q, :r.shape[0]] = r
+        return {"T": T, "box": Bl, "gbox": B, "store": store, "ids": ids4, "cbd": cbd,
+                "lut": lut.to(device=self.device, dtype=torch.float32 if self.ops.name == "hip" else self.dtype)
+                .contiguous()}
+
+    def _finish_drude_blk(self) -> None:
+        """Allocates the two state sets of the planned Drude pass (ids in
+        .w of the first array, as float bits) and arms it."""
+        dp = self._drude_plan
+        bshape = tuple(dp["box"][1][d] - dp["box"][0][d] for d in range(3)) + (4,)
+        dt = torch.float32 if self.ops.name == "hip" else self.dtype
+        state = []
+        for _ in range(2):
+            s0 = torch.zeros(bshape, dtype=dt, device=self.device)
+            s1 = torch.zeros(bshape, dtype=dt, device=self.device)
+            if dt == torch.float32:
+                s0[..., 3] = dp["ids"].view(torch.float32)
+            state.append((s0, s1))
+        self.drude_blk = dict(dp, state=state, cur=0, loc="chain")
+        self._chain_plan_cache = {}
+
+    def _drude_lv(self, t, S):
+        """The local box ``S`` of an auxiliary level (region-local or full-grid)."""
+        if hasattr(t, "view") and not isinstance(t, torch.Tensor):
+            return t.view(S)
+        return t[tuple(slice(S[0][d], S[1][d]) for d in range(3))]
+
+    def _drude_blk_import(self) -> None:
+        """Chain levels -> pass state: delta = D - Dp, Ep = D1p (E stands for D1)."""
+        db = self.drude_blk
+        if db is None or db["loc"] == "blk":
+            return
+        s0, s1 = db["state"][db["cur"]]
+        Bl = db["box"]
+        for q, c in enumerate(self.e_comps):
+            s0[..., q] = 0
+            s1[..., q] = 0
+            S = db["store"][c]
+            if S is None:
+                continue
+            Sl = self.domain.to_local(S)
+            sl = tuple(slice(Sl[0][d] - Bl[0][d], Sl[1][d] - Bl[0][d]) for d in range(3))
+            st = self.upml[c]
+            D, D1 = st["D"][0], st["D1"][0]
+            s0[sl + (q,)] = (self._drude_lv(D[0], Sl) - self._drude_lv(D[1], Sl)).to(s0.dtype)
+            s1[sl + (q,)] = self._drude_lv(D1[1], Sl).to(s1.dtype)
+        db["loc"] = "blk"
+
+    def _drude_blk_export(self) -> None:
+        """Pass state -> chain levels (checkpoints, stepped steps): the Drude
+        chain reads D only through differences (b0 + b1 + b2 = 0), so D := 0,
+        Dp := -delta; D1 := E, D1p := Ep."""
+        db = self.drude_blk
+        if db is None or db["loc"] != "blk":
+            return
+        s0, s1 = db["state"][db["cur"]]
+        Bl = db["box"]
+        for q, c in enumerate(self.e_comps):
+            S = db["store"][c]
+            if S is None:
+                continue
+            Sl = self.domain.to_local(S)
+            sl = tuple(slice(Sl[0][d] - Bl[0][d], Sl[1][d] - Bl[0][d]) for d in range(3))
+            st = self.upml[c]
+            D, D1 = st["D"][0], st["D1"][0]
+            self._drude_lv(D[0], Sl).zero_()
+            self._drude_lv(D[1], Sl).copy_(-s0[sl + (q,)])
+            self._drude_lv(D1[0], Sl).copy_(self._drude_lv(self.F[0][c], Sl))
+            self._drude_lv(D1[1], Sl).copy_(s1[sl + (q,)])
+        db["loc"] = "chain"
+
+    def _drude_pass(self, T: int, srcs) -> None:
+        """The Drude launch of a pass (after the core's plain launch, before
+        the hybrid shell steps F in place): output = the box grown by T."""
+        db = self.drude_blk
+        self._drude_blk_import()
+        Bl = db["box"]
+        shape = self.domain.shape
+        ob = (tuple(max(0, Bl[0][d] - T) for d in range(3)), tuple(min(shape[d], Bl[1][d] + T) for d in range(3)))
+        upd = {c: self.local_box(c, self.domain.allocated_global()) for c in self.comps}
+        sin, sout = db["state"][db["cur"]], db["state"][1 - db["cur"]]
+        with self.prof.phase("blocked-drude"):
+            self.ops.tb_drude_step(self.F[0], self.F_alt[0], upd, ob, self.cb, T, srcs[0],
+                                   {"box": Bl, "sin": sin, "sout": sout, "lut": db["lut"], "cbd": db["cbd"],
+                                    "ids": db["ids"]})
+        db["cur"] ^= 1
+
     # ------------------------------------------------------ hybrid blocking
     def _init_hybrid(self) -> None:
         """Blocked core + stepped shell for 3D and 2D runs with absorbing
@@ -185,6 +389,15 @@ class BlockedStepping:
             else:
                 H = HYBRID_AUTO_STEPS if self.dtype == torch.float32 else F64_AUTO_STEPS
         hmax = getattr(self.ops, "tb2d_max_steps" if two_d else "tb_max_steps", 8 if two_d else 6)
+        dp = self._drude_plan
+        if dp is not None and not self.fused and self.tb == 1 and dp["T"] <= hmax:
+            if not (cfg.use_pml or cfg.use_tfsf):
+                # no absorbing layer: plain blocked passes over the whole grid + the Drude pass
+                self.tb = dp["T"]
+                if not hasattr(self, "F_alt"):
+                    self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
+                return
+            H = dp["T"]
         if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme not in ("3d", "tmz", "tez")
                 or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode
                 or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials) or H > hmax):
@@ -204,6 +417,9 @@ class BlockedStepping:
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
                 return
         plan = self._hybrid_plan(H)
+        if plan is None and dp is not None:
+            self._drude_plan = dp = None  # the stepped dispersive box after all
+            plan = self._hybrid_plan(H)
         if plan is None:
             return
         if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.5 * self.cells():
@@ -296,7 +512,8 @@ class BlockedStepping:
             return None
         # dispersive boxes (chain boxes off the domain border) are cut out of the core
         disp = []
-        if cfg.use_metamaterials and self.use_upml_chain:
+        dblk = self._drude_plan is not None and self._drude_plan["T"] == T
+        if cfg.use_metamaterials and self.use_upml_chain and not dblk:
             for c in self.comps:
                 b = self._bbox_global(self.upml[c].get("drude_active"))
                 if not box_empty(b):
@@ -325,6 +542,8 @@ class BlockedStepping:
         if getattr(self, "chain_regions", None) is not None:
             for kind in ("E", "H"):
                 for r, _ in self.chain_regions[kind]["chain"]:
+                    if dblk and kind == "E" and all(r[c] == self._disp_chain.get(c) for c in r):
+                        continue  # the Drude box: inside the core, advanced by the Drude pass
                     irregular += [b for b in r.values() if not box_empty(b)]
         if self.use_cpml:
             for slabs in self.cpml.slabs.values():
@@ -345,6 +564,12 @@ class BlockedStepping:
             if any(not box_empty(box_intersect(g, b)) for b in irregular):
                 return None
             if cfg.use_tfsf and not core_tf and self._tfsf_targets_in(dom.to_local(g)):
+                return None
+        if dblk:
+            # the Drude pass's output (the box grown by T) must lie inside the one core box
+            gb = self._drude_plan["gbox"]
+            if len(couts) != 1 or any(gb[0][d] - T < couts[0][0][d] or gb[1][d] + T > couts[0][1][d]
+                                      for d in range(3) if act[d]):
                 return None
         if self.halo is not None:
             # decomposed: each rank's core is its owned part of the global core
@@ -397,7 +622,7 @@ class BlockedStepping:
         upd = {c: self.local_box(c, alloc) for c in self.comps}
         return {"T": T, "core": [dom.to_local(b) for b in couts], "shell": shells[0], "shells": shells,
                 "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
-                "cut_cells": box_volume(Dm) if Dm is not None else 0, "core_tfsf": core_tf}
+                "cut_cells": box_volume(Dm) if Dm is not None else 0, "core_tfsf": core_tf, "drude": dblk}
 
     def _tfsf_pass(self, p: int, T: int, level0: int = 0, dry: bool = False):
         """In-kernel TF/SF of a blocked pass starting at step ``self.t`` on
@@ -461,6 +686,8 @@ class BlockedStepping:
 
         with self.prof.phase("blocked-core"):
             core(core_now)
+        if hp.get("drude"):
+            self._drude_pass(T, srcs)  # reads F: before the shell steps below advance it in place
         if self.halo is not None:
             self._mark("interior")
             self._join_side(side)
@@ -555,6 +782,8 @@ class BlockedStepping:
                         self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p], tfsf=tfs[p])
                     else:
                         self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
+        if self.drude_blk is not None:
+            self._drude_pass(T, srcs)  # overwrites the box grown by T (run plain above)
         if self.halo is not None:
             self._mark("interior")
             if side is not None and self.prof.enabled:

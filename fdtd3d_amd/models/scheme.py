@@ -108,6 +108,7 @@ class SchemeConfig:
     shell_streams: int = 0                   # hybrid shell: streams for the independent window launches (0 auto)
     hybrid_graph: str = "auto"               # hybrid passes replayed from HIP graphs (auto / off)
     hybrid_tfsf: str = "auto"                # hybrid + TF/SF: faces in the blocked core (auto / core) or the shell
+    blocked_drude: str = "auto"              # Drude box inside the blocked passes: auto (HIP) / on / off
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
     profile_phases: bool = False             # per-phase HIP event timers (utils/profiler.py)
     use_hip_graph: bool = False              # replay captured HIP graphs of GRAPH_STEPS steps
@@ -144,7 +145,7 @@ class SchemeConfig:
             dispersion=s.dispersion, lorentz_omega0_ratio=s.lorentzOmega0Ratio, time_block=s.timeBlock,
             amplitude_check_steps=s.amplitudeCheckSteps,
             hybrid_block=s.hybridBlock, shell_streams=s.shellStreams, hybrid_graph=s.hybridGraph,
-            hybrid_tfsf=s.hybridTfsf,
+            hybrid_tfsf=s.hybridTfsf, blocked_drude=s.blockedDrude,
             profile_phases=s.doProfilePhases, use_hip_graph=s.doUseHipGraph)
 
 
@@ -384,6 +385,7 @@ class YeeScheme(BlockedStepping):
         if self.res1d:
             self.graph_mode = False
         self.hybrid = None
+        self._drude_plan = self._plan_drude_blk()
         self._init_hybrid()
         if (self.hybrid is None and cfg.scheme == "3d" and self.ops.name == "hip"
                 and getattr(self, "chain_regions", None) is not None and getattr(self, "_chain_prof", None) is not None):
@@ -396,6 +398,14 @@ class YeeScheme(BlockedStepping):
         if self.use_upml_chain:
             # after the chain boxes are final: region-local levels cover them
             self._alloc_upml_levels()
+        dp = self._drude_plan
+        if dp is not None:
+            if ((self.hybrid is not None and self.hybrid.get("drude"))
+                    or (self.hybrid is None and self.tb == dp["T"])):
+                self._finish_drude_blk()
+            else:
+                self._drude_plan = None  # neither pass form took it: the stepped dispersive box
+                self.__dict__.pop("_chain_plan_cache", None)
         # the eps-layout material grids (fp64, 8 B per cell and material) and
         # the averaged materials only feed the coefficients built above
         self.sampler.free()
@@ -810,6 +820,7 @@ class YeeScheme(BlockedStepping):
         per = {}
         sigma0 = {}  # per component: the box where every sigma vanishes (global)
         self._chain_sigma0 = sigma0
+        self._disp_chain = {}
         for c in self.comps:
             C = box_intersect(self._global_box(c), alloc)
             lo, hi = list(C[0]), list(C[1])
@@ -841,6 +852,7 @@ class YeeScheme(BlockedStepping):
             drude = [cfg.use_metamaterials and (n == 6 or not box_empty(box_intersect(chain[n], Dbox)))
                      for n in range(7)]
             per[c] = (plain, chain, drude)
+            self._disp_chain[c] = chain[6]  # the dispersive box's chain box (blocked Drude: never stepped)
         regions = {}
         for kind, comps in (("E", self.e_comps), ("H", self.h_comps)):
             plain = [{c: per[c][0][n] for c in comps} for n in range(6)]
@@ -1140,7 +1152,11 @@ class YeeScheme(BlockedStepping):
                 if not all(box_empty(b) for b in boxes.values()):
                     plain.append(boxes)
         chain = []
+        # (the hybrid shell's steps only: a whole-grid step runs the chain on the box's exported state)
+        skip_disp = pws is not None and (self.drude_blk is not None or self._drude_plan is not None)
         for r, dru in reg["chain"]:
+            if skip_disp and kind == "E" and all(r[c] == self._disp_chain.get(c) for c in comps):
+                continue  # the Drude box runs inside the blocked passes (blocking.py _drude_pass)
             boxes = {c: dom.to_local(box_intersect(r[c], w if w is not None else whole)) for c in comps}
             if all(box_empty(b) for b in boxes.values()):
                 continue
@@ -1289,7 +1305,10 @@ class YeeScheme(BlockedStepping):
             D[0], D[1] = D[1], D[0]
 
     def named_state(self) -> Dict[str, torch.Tensor]:
-        """Every array needed to resume the run, by stable name (checkpoints)."""
+        """Every array needed to resume the run, by stable name (checkpoints).
+        The blocked Drude pass's state goes back into the chain levels first
+        (the next pass re-reads them), so either path resumes the other's."""
+        self._drude_blk_export()
         out: Dict[str, torch.Tensor] = {}
         for p in range(self.planes):
             sfx = "" if p == 0 else "-im"
@@ -1379,6 +1398,8 @@ class YeeScheme(BlockedStepping):
         cfg = self.cfg
         B = self.domain.buffer_size
         halo = self.halo
+        if self.drude_blk is not None and windows is None:
+            self._drude_blk_export()  # a whole-grid step runs the chain on the Drude box
         if self.fused:
             self._fused_step(t)
             return

@@ -789,6 +789,74 @@ class HipOps:
         _check(rc, "tb3d_amp")
         self.launches += 1
 
+    tb_drude_max_steps = 5  # Drude passes: the dispersive state of T - 1 levels rides in registers
+
+    def tb_drude_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                      obox: Box, cb: Dict[str, Coef], steps: int, sources, drude: dict) -> None:
+        """``steps`` (<= 5) fused leapfrog steps over ``obox`` with the Drude
+        box folded in (tb3d_mr.h DrDev, fdtd_tb3d_drude_f32): inside
+        ``drude["box"]`` (local) the E components take the dispersive update
+        from the state ``drude["sin"]`` (two float4 arrays over the box:
+        delta + material ids, E of the previous step), written advanced to
+        ``drude["sout"]``; ``drude["lut"]`` = (3, nid, 4) float32 tuples
+        (b0 cbd, b2, m1, m2), ``drude["cbd"]`` the D coefficient.  Uniform
+        media elsewhere; ``sources`` as :meth:`tb_step`."""
+        E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
+        if self.dtype != torch.float32 or not (1 <= steps <= self.tb_drude_max_steps):
+            raise HipError("Drude passes: fp32, 1..%d steps" % self.tb_drude_max_steps)
+        shape = tuple(fin["Ex"].shape)
+        if shape[2] % 4 != 0:
+            raise HipError("fp32 tb_drude_step needs nz %% 4 == 0, got %s" % (shape,))
+        for c in E + H:
+            self._check_tensor(fin[c], shape)
+            self._check_tensor(fout[c], shape)
+            if fin[c].data_ptr() == fout[c].data_ptr():
+                raise HipError("tb_drude_step needs distinct in/out buffers")
+            if self._cell_or_none(cb[c]) is not None:
+                raise HipError("tb_drude_step: uniform media outside the Drude box only")
+        B = drude["box"]
+        for bx in list(boxes.values()) + [obox, B]:
+            for d in range(3):
+                if not _empty(bx) and (bx[0][d] < 0 or bx[1][d] > shape[d]):
+                    raise HipError("box %s outside array %s" % (bx, shape))
+        for c in E:
+            b = boxes[c]
+            if any(B[0][d] < b[0][d] or B[1][d] > b[1][d] for d in range(3)):
+                raise HipError("Drude box %s not inside the update box %s of %s" % (B, b, c))
+        bshape = tuple(B[1][d] - B[0][d] for d in range(3)) + (4,)
+        for t in list(drude["sin"]) + list(drude["sout"]):
+            self._check_tensor(t, bshape)
+        if any(a.data_ptr() == b.data_ptr() for a in drude["sin"] for b in drude["sout"]):
+            raise HipError("tb_drude_step needs distinct state in / out buffers")
+        lut = drude["lut"]
+        nid = int(lut.shape[1])
+        self._check_tensor(lut, (3, nid, 4))
+        cbv, dbv = cb["Ex"].scalar, cb["Hx"].scalar
+        if any(cb[c].scalar != cbv for c in E) or any(cb[c].scalar != dbv for c in H):
+            raise HipError("tb_drude_step: scalar coefficients must agree per kind")
+        src = [-1, -1, -1, -1]
+        vals = [0.0] * 8
+        if sources is not None and any(s is not None for s in sources):
+            first = next(s for s in sources if s is not None)
+            comp, idx = first[0], tuple(first[1])
+            if comp not in E or not all(0 <= idx[d] < shape[d] for d in range(3)):
+                raise HipError("tb_drude_step: E point source inside the array only")
+            for l, s in enumerate(sources):
+                if s is None or s[0] != comp or tuple(s[1]) != idx:
+                    raise HipError("tb_drude_step: the source must be the same point at every step")
+                vals[l] = float(s[2])
+            src = [idx[0], idx[1], idx[2], E.index(comp)]
+        arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
+        two = lambda ts: (c_vp * 2)(*[t.data_ptr() for t in ts])
+        rc = self.lib.fdtd_tb3d_drude_f32(
+            arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), c_double(cbv), c_double(dbv), c_int(shape[0]),
+            c_int(shape[1]), c_int(shape[2]), _box_arr([boxes[c] for c in E + H]), _box_arr([obox]),
+            c_int(self.tb_xchunk), c_int(steps), (c_int * 4)(*src), (c_double * 8)(*vals), _box_arr([B]),
+            two(drude["sin"]), two(drude["sout"]), c_vp(lut.data_ptr()), c_int(nid), c_double(drude["cbd"]),
+            _stream())
+        _check(rc, "tb3d_drude")
+        self.launches += 1
+
     def tb_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
                 obox: Box, cb: Dict[str, Coef], steps: int, sources=None, tfsf=None) -> None:
         """``steps`` fused leapfrog steps in one HBM pass (yee3d_tb.hip).

@@ -203,6 +203,65 @@ class TorchOps:
                 sp = tuple(slice(s.start + 1, s.stop + 1) for s in sl)
                 fout[c][sl] = cur[c][sp]
 
+    tb_drude_max_steps = 5
+
+    def tb_drude_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
+                      obox: Box, cb: Dict[str, Coef], steps: int, sources, drude: dict) -> None:
+        """Reference semantics of the Drude pass (csrc/tb3d_mr.h DrDev):
+        :meth:`tb_step`'s fused steps, with the E components inside
+        ``drude["box"]`` taking E' = (b0 cbd) curl - b2 delta + m1 E + m2 Ep
+        from the state ``drude["sin"]`` (delta + ids, Ep; float4 per cell),
+        whose advanced values go to ``drude["sout"]`` on the cells of
+        ``obox`` inside the box."""
+        B = drude["box"]
+        pad = {c: torch.nn.functional.pad(fin[c], (1, 1, 1, 1, 1, 1)) for c in fin}
+        shifted = {c: ((b[0][0] + 1, b[0][1] + 1, b[0][2] + 1), (b[1][0] + 1, b[1][1] + 1, b[1][2] + 1))
+                   for c, b in boxes.items()}
+        cbp = cb_pad(cb)
+        unit = {c: Coef(1.0) for c in cb}
+        e = {c: b for c, b in shifted.items() if c[0] == "E"}
+        h = {c: b for c, b in shifted.items() if c[0] == "H"}
+        E = ("Ex", "Ey", "Ez")
+        bsl = tuple(slice(B[0][d] + 1, B[1][d] + 1) for d in range(3))
+        s0, s1 = drude["sin"]
+        ids = drude["ids"]  # int32 over B (the kernel reads the same bits from s0[..., 3] in fp32)
+        lut = drude["lut"]
+        k = [lut[q][((ids >> (8 * q)) & 0xff).long()] for q in range(3)]  # (bx, by, bz, 4) per component
+        delta = [s0[..., q].clone() for q in range(3)]
+        ep = [s1[..., q].clone() for q in range(3)]
+        cbd = float(drude["cbd"])
+        cur = pad
+        for l in range(steps):
+            nxt = {c: cur[c].clone() for c in cur}
+            self.curl_update("E", e, nxt, cur, cbp)
+            curl = {c: torch.zeros_like(cur[c]) for c in E}
+            self.curl_update("E", e, curl, cur, unit)
+            for q, c in enumerate(E):
+                cu, ec = curl[c][bsl], cur[c][bsl]
+                nxt[c][bsl] = k[q][..., 0] * cu - k[q][..., 1] * delta[q] + k[q][..., 2] * ec + k[q][..., 3] * ep[q]
+                delta[q] = cbd * cu
+                ep[q] = ec.clone()
+            if sources is not None and sources[l] is not None:
+                comp, idx, val = sources[l]
+                nxt[comp][tuple(i + 1 for i in idx)] = val
+            self.curl_update("H", h, nxt, nxt, cbp)
+            cur = nxt
+        for c, b in boxes.items():
+            ob = box_intersect_(b, obox)
+            if not _empty(ob):
+                sl = box_slices(ob)
+                sp = tuple(slice(s.start + 1, s.stop + 1) for s in sl)
+                fout[c][sl] = cur[c][sp]
+        ob = box_intersect_(B, obox)
+        if not _empty(ob):
+            o0, o1 = drude["sout"]
+            sl = tuple(slice(ob[0][d] - B[0][d], ob[1][d] - B[0][d]) for d in range(3))
+            for q in range(3):
+                o0[sl + (q,)] = delta[q][sl]
+                o1[sl + (q,)] = ep[q][sl]
+            o0[sl + (3,)] = s0[sl + (3,)]
+            o1[sl + (3,)] = 0.0
+
     tb_amp_max_steps = 3
 
     def tb_amp_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],

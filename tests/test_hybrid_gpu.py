@@ -17,15 +17,17 @@ CASES = [
     ("upml-tfsf", dict(scene="vacuum", use_pml=True, use_tfsf=True, theta=40, phi=25, psi=15), 4, 13),
     ("cpml-tfsf", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10, psi=5), 4, 12),
     ("upml-point", dict(scene="vacuum", use_pml=True), 3, 10),
-    ("drude-upml", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, sphere_center=(40.0, 36.0, 48.0),
+    ("drude-upml", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, blocked_drude="off", sphere_center=(40.0, 36.0, 48.0),
                         sphere_radius=7.0), 4, 12),
     ("sphere-cpml", dict(scene="sphere", use_pml=True, pml_type="cpml", sphere_center=(40.0, 36.0, 48.0),
                          sphere_radius=10.0), 4, 9),
     ("upml-tfsf-f64", dict(scene="vacuum", use_pml=True, use_tfsf=True, theta=30, phi=40, psi=20, dtype="f64"), 4, 10),
+    # (the Drude cases keep the stepped dispersive box: blocked_drude="off"; the blocked Drude pass is
+    # tests/test_drude_blk_gpu.py)
     # no PML: the blocked core reaches the domain faces around the dispersive box
-    ("drude-nopml", dict(scene="drude-sphere", use_metamaterials=True, sphere_center=(40.0, 36.0, 48.0),
+    ("drude-nopml", dict(scene="drude-sphere", use_metamaterials=True, blocked_drude="off", sphere_center=(40.0, 36.0, 48.0),
                          sphere_radius=7.0), 5, 12),
-    ("drude-nopml-face", dict(scene="drude-sphere", use_metamaterials=True, sphere_center=(9.0, 30.0, 60.0),
+    ("drude-nopml-face", dict(scene="drude-sphere", use_metamaterials=True, blocked_drude="off", sphere_center=(9.0, 30.0, 60.0),
                               sphere_radius=6.0), 4, 11),
     # 2D: blocked core through yee2d_tb.hip
     ("tmz-upml-tfsf", dict(scheme="tmz", size=(120, 104, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
@@ -57,7 +59,7 @@ CASES = [
     # form stays covered
     ("cpml-tfsf-inorder", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10, psi=5,
                                shell_streams=1), 4, 12),
-    ("drude-upml-inorder", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True,
+    ("drude-upml-inorder", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, blocked_drude="off",
                                 sphere_center=(40.0, 36.0, 48.0), sphere_radius=7.0, shell_streams=1), 4, 12),
 ]
 
