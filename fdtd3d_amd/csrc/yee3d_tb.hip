@@ -321,6 +321,7 @@ int g_tb_mrows = 0;  // rows per wave of the multi-row kernel: 0 automatic, 1 = 
 
 const int kNoBox[6] = {0, 0, 0, 0, 0, 0};
 int g_tb_mr_shape = 0;  // plain multi-row kernel: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
+int g_tb_dr_shape = 0;  // Drude variant: 0 = 8 waves x 2 rows, 1 = 16 waves x 1 row (both 16-row tiles)
 
 
 
@@ -335,7 +336,10 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
   // Drude box (tb3d_mr.h DrDev): 8 waves x 2 rows (16-row tiles, <= 256
   // VGPRs: the dispersive state of T - 1 levels rides in registers)
   if (fx == 16) {
-    if constexpr (T <= 5) return launch_tb_mr<T, 1, 2, 16, 8>(MR_ARGS);
+    if constexpr (T <= 5) {
+      if (g_tb_dr_shape == 1) return launch_tb_mr<T, 1, 1, 16, 16>(MR_ARGS);
+      return launch_tb_mr<T, 1, 2, 16, 8>(MR_ARGS);
+    }
     return (int)hipErrorInvalidValue;
   }
   if (fx == 8) {
@@ -463,6 +467,8 @@ FDTD_API void fdtd_set_tb_variant(int v) {
 FDTD_API void fdtd_set_tb_patch(int pz, int py) {
   g_tb_patch = (pz > 0 && py > 0 && pz < 256 && py < 256) ? ((pz << 8) | (py << 16)) : 0;
 }
+// Drude variant tile shape (tuning): 0 = 8 waves x 2 rows, 1 = 16 waves x 1 row
+FDTD_API void fdtd_set_tb_dr_shape(int v) { g_tb_dr_shape = v == 1 ? 1 : 0; }
 // plain multi-row tile shape (tuning): 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
 FDTD_API void fdtd_set_tb_mr_shape(int v) { g_tb_mr_shape = v == 1 ? 1 : 0; }
 // largest steps-per-pass the blocked kernels accept

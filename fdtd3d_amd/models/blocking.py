@@ -56,8 +56,10 @@ F32_AUTO_STEPS_TFSF = 4
 # longest pass of the TF/SF variant (yee3d_tb.hip launch_tb_mr_sel: T <= 5)
 TFSF_MAX_STEPS = 5
 # steps per pass with the Drude box inside the blocked passes (its variant
-# holds T - 1 levels of dispersive state in registers: T <= 5)
-DRUDE_AUTO_STEPS = 5
+# holds T - 1 levels of dispersive state in registers: T <= 5).  512^3 Drude
+# sphere r = 128 (profiles/drude_blk_r5.md): T = 3 / 4 / 5 131.6k / 165-170k /
+# 155-157k Mcells/s without PML, 66.6k / 73.6-75.3k / 74.6-75.4k with UPML
+DRUDE_AUTO_STEPS = 4
 
 
 

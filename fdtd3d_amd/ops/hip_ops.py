@@ -790,6 +790,8 @@ class HipOps:
         self.launches += 1
 
     tb_drude_max_steps = 5  # Drude passes: the dispersive state of T - 1 levels rides in registers
+    # Drude variant tiles: 0 = 8 waves x 2 rows, 1 = 16 waves x 1 row (both 16 rows)
+    tb_dr_shape = int(os.environ.get("FDTD3D_TB_DR_SHAPE", "0"))
 
     def tb_drude_step(self, fin: Dict[str, torch.Tensor], fout: Dict[str, torch.Tensor], boxes: Dict[str, Box],
                       obox: Box, cb: Dict[str, Coef], steps: int, sources, drude: dict) -> None:
@@ -848,6 +850,7 @@ class HipOps:
             src = [idx[0], idx[1], idx[2], E.index(comp)]
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
         two = lambda ts: (c_vp * 2)(*[t.data_ptr() for t in ts])
+        self.lib.fdtd_set_tb_dr_shape(c_int(self.tb_dr_shape))
         rc = self.lib.fdtd_tb3d_drude_f32(
             arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), c_double(cbv), c_double(dbv), c_int(shape[0]),
             c_int(shape[1]), c_int(shape[2]), _box_arr([boxes[c] for c in E + H]), _box_arr([obox]),
