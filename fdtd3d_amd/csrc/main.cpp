@@ -1168,6 +1168,21 @@ int run(const fdtd::Settings& s) {
       }
     }
   }
+  // Drude box inside the blocked passes (models/blocking.py _plan_drude_blk,
+  // tb3d_mr.h DrDev): every hybrid pass runs the plain blocked core over the
+  // box too, then the Drude variant over the box grown by T, carrying
+  // (delta = D - Dp, Ep) per E component; the stepped chain never runs on
+  // the box.  fp32 3D electric Drude spheres without TF/SF, fresh runs (the
+  // native checkpoints cover plain media).
+  bool dr_blk = false;
+  IBox dr_box = {{0, 0, 0}, {0, 0, 0}};
+  if (sizeof(T) == 4 && v4 && upml && dim == 3 && s.doUseMetamaterials && s.blockedDrude != "off" &&
+      s.dispersion != "lorentz" && !tfsf && !amp && !percell && !chain_regs.empty() && !plain_regs.empty() &&
+      chain_disp.back() && (upt.disp[0] || upt.disp[1] || upt.disp[2]) && !upt.disp[3] && !upt.disp[4] &&
+      !upt.disp[5]) {
+    dr_blk = true;
+    dr_box = chain_regs.back();
+  }
   auto clip36 = [&](const IBox& r, int* out) {
     for (int c = 0; c < 6; ++c) {
       IBox b;
@@ -1422,7 +1437,12 @@ int run(const fdtd::Settings& s) {
   // stepped in place in F with a band T - s deep into the core at step s
   // (stale core values corrupt one band cell per step, so the shell itself
   // stays exact), copied into G, and the buffers swap.
-  const int T_h_req = s.hybridBlock == 0 ? 5 : s.hybridBlock;
+  int T_h_req = s.hybridBlock == 0 ? 5 : s.hybridBlock;
+  if (dr_blk) {
+    // (models/blocking.py DRUDE_AUTO_STEPS: the Drude variant holds T - 1 levels in registers)
+    T_h_req = s.hybridBlock > 0 ? s.hybridBlock : (s.timeBlock > 0 ? s.timeBlock : 4);
+    if (T_h_req <= 1 || T_h_req > 5) dr_blk = false;
+  }
   std::vector<IBox> hcores, hshell[8], hcopy;
   int T_h = 1;
   // (UPML runs without dispersive media too: the chain slabs run whole in
@@ -1468,7 +1488,12 @@ int run(const fdtd::Settings& s) {
     };
     IBox Dm = {{0, 0, 0}, {0, 0, 0}};
     bool ok = !K.empty();
-    if (ok && drude_h) {
+    if (ok && dr_blk) {
+      // the Drude pass's output (the box grown by T, clipped to the grid) inside the core
+      const IBox g = box_and(grow(dr_box, Th), alloc);
+      for (int a = 0; a < 3; ++a) dr_blk = dr_blk && g.lo[a] >= K.lo[a] && g.hi[a] <= K.hi[a];
+    }
+    if (ok && drude_h && !dr_blk) {
       Dm = box_and(grow(dbox_h, Th + 2), K);
       // the dispersive box runs whole in every shell step: inside every window set
       const IBox KT = shrink_inner(K, Th);
@@ -1499,6 +1524,70 @@ int run(const fdtd::Settings& s) {
       if (!Dm.empty()) hcopy.push_back(box_and(Dm, alloc));
       for (int c = 0; c < 6; ++c)
         if (present[c] && !G[c].p) G[c].alloc(cells);
+    }
+  }
+  // the Drude pass's state (two sets of two float4 arrays over the box; the
+  // material ids of Ex | Ey << 8 | Ez << 16 in .w of the first) and its
+  // (b0 cbd, b2, m1, m2) rows per component
+  if (T_h <= 1) dr_blk = false;
+  Dev<float> DRS[4], DRL;
+  int dr_nid = 0, dr_cur = 0;
+  double dr_cbd = 0.0;
+  if (dr_blk) {
+    const int bn[3] = {dr_box.hi[0] - dr_box.lo[0], dr_box.hi[1] - dr_box.lo[1], dr_box.hi[2] - dr_box.lo[2]};
+    const size_t nb = (size_t)bn[0] * bn[1] * bn[2];
+    const double two = 2 * kEps0;
+    dr_cbd = (double)(T)((two * dt / dx) / two);  // the chain's cbD where sigma = 0
+    std::vector<unsigned> ids(nb, 0u);
+    std::vector<float> rows;
+    for (int c = 0; c < 3; ++c) {
+      if (upt.disp[c]) {
+        const int nl = upt.nlut[c];
+        std::vector<T> tab(5 * (size_t)nl);
+        HIP_OK(hipMemcpy(tab.data(), upt.lut[c], tab.size() * sizeof(T), hipMemcpyDeviceToHost));
+        for (int q = 0; q < nl; ++q) {
+          const double b0 = tab[5 * q], b1 = tab[5 * q + 1], b2 = tab[5 * q + 2];
+          if (std::fabs(b0 + b1 + b2) > 1e-5 * (std::fabs(b0) + std::fabs(b1) + std::fabs(b2))) dr_blk = false;
+        }
+        dr_nid = std::max(dr_nid, nl);
+        std::vector<unsigned char> full(cells);
+        HIP_OK(hipMemcpy(full.data(), upt.ids[c], cells, hipMemcpyDeviceToHost));
+        for (int i = 0; i < bn[0]; ++i)
+          for (int j = 0; j < bn[1]; ++j)
+            for (int k = 0; k < bn[2]; ++k)
+              ids[((size_t)i * bn[1] + j) * bn[2] + k] |=
+                  (unsigned)full[((size_t)(i + dr_box.lo[0]) * N[1] + j + dr_box.lo[1]) * N[2] + k + dr_box.lo[2]]
+                  << (8 * c);
+      } else {
+        dr_nid = std::max(dr_nid, 1);  // id 0: the plain row (cb, 0, 1, 0)
+      }
+    }
+    if (dr_nid > 256) dr_blk = false;
+    if (dr_blk) {
+      rows.assign((size_t)3 * dr_nid * 4, 0.f);
+      for (int c = 0; c < 3; ++c) {
+        float* r = rows.data() + (size_t)c * dr_nid * 4;
+        if (!upt.disp[c]) {
+          r[0] = (float)cb;
+          r[2] = 1.f;
+          continue;
+        }
+        std::vector<T> tab(5 * (size_t)upt.nlut[c]);
+        HIP_OK(hipMemcpy(tab.data(), upt.lut[c], tab.size() * sizeof(T), hipMemcpyDeviceToHost));
+        for (int q = 0; q < upt.nlut[c]; ++q) {
+          r[4 * q] = (float)((double)tab[5 * q] * dr_cbd);
+          r[4 * q + 1] = (float)tab[5 * q + 2];
+          r[4 * q + 2] = (float)tab[5 * q + 3];
+          r[4 * q + 3] = (float)tab[5 * q + 4];
+        }
+      }
+      DRL.alloc(rows.size());
+      HIP_OK(hipMemcpy(DRL.p, rows.data(), rows.size() * sizeof(float), hipMemcpyHostToDevice));
+      std::vector<float> s0(4 * nb, 0.f);
+      for (size_t e = 0; e < nb; ++e) std::memcpy(&s0[4 * e + 3], &ids[e], 4);
+      for (int q = 0; q < 4; ++q) DRS[q].alloc(4 * nb);
+      HIP_OK(hipMemcpy(DRS[0].p, s0.data(), s0.size() * sizeof(float), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(DRS[2].p, s0.data(), s0.size() * sizeof(float), hipMemcpyHostToDevice));
     }
   }
   // 2D hybrid passes (models/blocking.py on yee2d_tb.hip): every T steps the
@@ -1603,29 +1692,6 @@ int run(const fdtd::Settings& s) {
       }
     }
   };
-  // UPML shell half step: the chain slabs whole (they lie inside every
-  // step's windows), the plain kernels on the windows' parts in the inner box
-  auto upml_shell = [&](int kind, const std::vector<IBox>& wins) {
-    fptrs();
-    int rb[36];
-    for (size_t q = 0; q < chain_regs.size(); ++q) {
-      clip36(chain_regs[q], rb);
-      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false, !chain_disp[q]));
-    }
-    native_phys::upml_rotate(upt, kind);
-    for (const IBox& w : wins)
-      for (const IBox& pr : plain_regs) {
-        const IBox b = box_and(w, pr);
-        if (b.empty()) continue;
-        clip36(b, rb);
-        if (kind == 0)
-          K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, cb, N[0], N[1], N[2], rb, 0,
-                   st, v4));
-        else
-          K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, db, N[0], N[1], N[2],
-                   rb + 18, 0, st, v4));
-      }
-  };
   // independent shell-window launches of a half step side by side on three
   // streams (the tail of one small launch overlaps the next; models/scheme.py
   // _par_launches), joined back into `st`
@@ -1651,7 +1717,61 @@ int run(const fdtd::Settings& s) {
       HIP_OK(hipStreamWaitEvent(st, join_ev[q], 0));
     }
   };
-  auto hybrid_pass = [&](int t) {
+  // independent launches of a half step (disjoint cells) round-robin on the
+  // three streams, joined back into `st` (models/scheme.py _par_launches)
+  auto par_fns = [&](const std::vector<std::function<void(hipStream_t)>>& fns) {
+    if (fns.size() <= 1 || !side[0]) {
+      for (const auto& fn : fns) fn(st);
+      return;
+    }
+    HIP_OK(hipEventRecord(fork_ev, st));
+    for (int q = 0; q < 2; ++q) HIP_OK(hipStreamWaitEvent(side[q], fork_ev, 0));
+    for (size_t n = 0; n < fns.size(); ++n) fns[n](n % 3 == 0 ? st : side[n % 3 - 1]);
+    for (int q = 0; q < 2; ++q) {
+      HIP_OK(hipEventRecord(join_ev[q], side[q]));
+      HIP_OK(hipStreamWaitEvent(st, join_ev[q], 0));
+    }
+  };
+  // UPML shell half step: the chain slabs whole (they lie inside every
+  // step's windows), the plain kernels on the windows' parts in the inner box
+  // (chain slabs and plain window parts are disjoint: side by side on the
+  // three streams, as the Python driver's shell -- the float4 plain kernels
+  // store only their own elements of a 4-cell group that straddles an
+  // unaligned z border with a chain box; the level rotation is a host pointer
+  // swap after the launches captured their pointers)
+  auto upml_shell = [&](int kind, const std::vector<IBox>& wins) {
+    fptrs();
+    std::vector<std::function<void(hipStream_t)>> fns, pfns;
+    for (size_t q = 0; q < chain_regs.size(); ++q) {
+      if (dr_blk && q + 1 == chain_regs.size()) continue;  // the Drude box: inside the blocked passes
+      fns.push_back([&, q, kind](hipStream_t ss) {
+        int rb[36];
+        clip36(chain_regs[q], rb);
+        K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], ss, chain_fn, false, !chain_disp[q]));
+      });
+    }
+    for (const IBox& w : wins)
+      for (const IBox& pr : plain_regs) {
+        const IBox b = box_and(w, pr);
+        if (b.empty()) continue;
+        pfns.push_back([&, b, kind](hipStream_t ss) {
+          int rb[36];
+          clip36(b, rb);
+          if (kind == 0)
+            K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, cb, N[0], N[1], N[2],
+                     rb, 0, ss, v4));
+          else
+            K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, db, N[0], N[1], N[2],
+                     rb + 18, 0, ss, v4));
+        });
+      }
+    fns.insert(fns.end(), pfns.begin(), pfns.end());
+    par_fns(fns);
+    native_phys::upml_rotate(upt, kind);
+  };
+  // one pass of k <= T_h steps (a shorter pass steps the shell windows of the
+  // pass's last k steps: band depth k - q at step q)
+  auto hybrid_pass = [&](int t, int k) {
     if constexpr (sizeof(T) == 4) {
       const T* ei[3] = {F[0].p, F[1].p, F[2].p};
       const T* hi[3] = {F[3].p, F[4].p, F[5].p};
@@ -1659,17 +1779,34 @@ int run(const fdtd::Settings& s) {
       T* ho[3] = {G[3].p, G[4].p, G[5].p};
       const T* none3[3] = {nullptr, nullptr, nullptr};
       double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int l = 0; l < T_h; ++l) vals[l] = src_val(t + l);
+      for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
       for (const IBox& hc : hcores) {
         bool in_core = true;
         for (int a = 0; a < 3; ++a) in_core = in_core && sp[a] >= hc.lo[a] && sp[a] < hc.hi[a];
         const int src[4] = {sp[0], sp[1], sp[2], point_src && in_core ? src_comp : -1};
         const int ob[6] = {hc.lo[0], hc.lo[1], hc.lo[2], hc.hi[0], hc.hi[1], hc.hi[2]};
-        K_OK(tb3d(ei, hi, eo, ho, none3, none3, cb, db, N[0], N[1], N[2], boxes, T_h, src, vals, st, nullptr, nullptr,
+        K_OK(tb3d(ei, hi, eo, ho, none3, none3, cb, db, N[0], N[1], N[2], boxes, k, src, vals, st, nullptr, nullptr,
                   ob));
       }
-      for (int q = 0; q < T_h; ++q) {
-        const double sv = src_val(t + q);
+      if (dr_blk) {
+        // the Drude pass over the box grown by k (overwrites the core pass there)
+        int ob[6], bb[6];
+        for (int a = 0; a < 3; ++a) {
+          ob[a] = std::max(0, dr_box.lo[a] - k);
+          ob[3 + a] = std::min(N[a], dr_box.hi[a] + k);
+          bb[a] = dr_box.lo[a];
+          bb[3 + a] = dr_box.hi[a];
+        }
+        const int src[4] = {sp[0], sp[1], sp[2], point_src ? src_comp : -1};
+        void* sin[2] = {DRS[2 * dr_cur].p, DRS[2 * dr_cur + 1].p};
+        void* sout[2] = {DRS[2 * (1 - dr_cur)].p, DRS[2 * (1 - dr_cur) + 1].p};
+        K_OK(fdtd_tb3d_drude_f32(ei, hi, eo, ho, cb, db, N[0], N[1], N[2], boxes, ob, 0, k, src, vals, bb, sin, sout,
+                                 DRL.p, dr_nid, dr_cbd, st));
+        dr_cur ^= 1;
+      }
+      for (int q0 = 0; q0 < k; ++q0) {
+        const int q = T_h - k + q0;  // the window set of band depth k - q0
+        const double sv = src_val(t + q0);
         int wb[18];
         if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
         if (upml) {
@@ -1724,10 +1861,13 @@ int run(const fdtd::Settings& s) {
   };
   auto advance = [&](int t0, int n) {
     int t = t0;
-    while (T_h > 1 && n >= T_h) {
-      hybrid_pass(t);
-      t += T_h;
-      n -= T_h;
+    // (with the Drude box in the passes a tail is a shorter pass too: the
+    // stepped chain never holds the box's state)
+    while (T_h > 1 && (n >= T_h || (dr_blk && n > 0))) {
+      const int k = std::min(T_h, n);
+      hybrid_pass(t, k);
+      t += k;
+      n -= k;
     }
     while (T2_h > 1 && n >= T2_h) {
       hybrid2d_pass(t);
@@ -2049,8 +2189,9 @@ int run(const fdtd::Settings& s) {
     std::printf("Backend: native HIP, hybrid passes (2D blocked core, %d steps per pass; stepped %s%s shell)\n",
                 T2_h, upml ? "UPML" : "CPML", tfsf ? " + TF/SF" : "");
   else if (T_h > 1)
-    std::printf("Backend: native HIP, hybrid passes (blocked core, %d steps per pass; stepped %s%s shell)\n", T_h,
-                upml ? "UPML" : (cpml ? "CPML" : "plain"), tfsf ? " + TF/SF" : "");
+    std::printf("Backend: native HIP, hybrid passes (blocked core, %d steps per pass; stepped %s%s shell%s)\n", T_h,
+                upml ? "UPML" : (cpml ? "CPML" : "plain"), tfsf ? " + TF/SF" : "",
+                dr_blk ? "; the Drude box inside the passes" : "");
   else if (T_blk > 1 || T2_blk > 1)
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass)\n", std::max(T_blk, T2_blk));
   else if (res1)

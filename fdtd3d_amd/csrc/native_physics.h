@@ -122,6 +122,7 @@ struct Upml {
   bool disp[6] = {};
   unsigned char* ids[6] = {};
   T* lut[6] = {};
+  int nlut[6] = {};  // rows of lut[c]
   ~Upml() {
     for (void* p : keep) (void)hipFree(p);
   }
@@ -231,6 +232,7 @@ void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt,
           for (int e = 0; e < 5; ++e) tab[5 * q2 + e] = (T)o[e];
         }
         U.lut[c] = dev_upload(tab, U.keep);
+        U.nlut[c] = (int)vals.size();
         U.ids[c] = dev_upload(id, U.keep);
         U.s[c] = 1.0;  // E from D1 (D1 already carries 1/(eps eps0))
       }

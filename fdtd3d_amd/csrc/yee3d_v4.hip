@@ -69,7 +69,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_v4(
           f4set(e, q, f4(e, q) + f4(c4, q) * ((f4(hzc, q) - f4(hz_j, q)) - (f4(hyc, q) - hym)));
         }
       }
-      st4(ex, off, e);
+      st4m(ex, off, e, mx);
     }
     if (xin_y && my) {
       float4 e = ld4(ey, off);
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_v4(
           f4set(e, q, f4(e, q) + f4(c4, q) * ((f4(hxc, q) - hxm) - (f4(hzc, q) - f4(hz_m, q))));
         }
       }
-      st4(ey, off, e);
+      st4m(ey, off, e, my);
     }
     if (xin_z && mz) {
       float4 e = ld4(ez, off);
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_v4(
           f4set(e, q, f4(e, q) + f4(c4, q) * ((f4(hyc, q) - f4(hy_m, q)) - (f4(hxc, q) - f4(hx_j, q))));
         }
       }
-      st4(ez, off, e);
+      st4m(ez, off, e, mz);
     }
     hz_m = hzc;
     hy_m = hyc;
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_h3d_v4(
           f4set(h, q, f4(h, q) + f4(c4, q) * ((eyp - f4(ey_c, q)) - (f4(ez_j, q) - f4(ez_c, q))));
         }
       }
-      st4(hx, off, h);
+      st4m(hx, off, h, mx);
     }
     if (xin_y && my) {
       float4 h = ld4(hy, off);
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_h3d_v4(
           f4set(h, q, f4(h, q) + f4(c4, q) * ((f4(ez_n, q) - f4(ez_c, q)) - (exp_ - f4(exc, q))));
         }
       }
-      st4(hy, off, h);
+      st4m(hy, off, h, my);
     }
     if (xin_z && mz) {
       float4 h = ld4(hz, off);
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(64 * TY) void k_update_h3d_v4(
           f4set(h, q, f4(h, q) + f4(c4, q) * ((f4(ex_j, q) - f4(exc, q)) - (f4(ey_n, q) - f4(ey_c, q))));
         }
       }
-      st4(hz, off, h);
+      st4m(hz, off, h, mz);
     }
     ey_c = ey_n;
     ez_c = ez_n;

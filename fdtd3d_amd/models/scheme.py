@@ -1105,7 +1105,8 @@ class YeeScheme(BlockedStepping):
             # the launch list of this (kind, window set) is static: built once
             # (the hybrid shell steps through T window sets every pass)
             plan = cache[key] = self._chain_plan(kind, w, pws)
-        fns = [(lambda boxes=boxes: self.ops.curl_update(kind, boxes, F, F, self.cb)) for boxes in plan["plain"]]
+        pfns = [(lambda boxes=boxes: self.ops.curl_update(kind, boxes, F, F, self.cb)) for boxes in plan["plain"]]
+        fns = []
         slow_all = []
         for launches, slow in plan["chain"]:
             for sel, form, plain_form, fold, rows in launches:
@@ -1121,10 +1122,12 @@ class YeeScheme(BlockedStepping):
             slow_all += slow
         if plain_windows is not None and self.hybrid is not None and not slow_all:
             # hybrid shell: plain slabs and chain boxes are disjoint -- their
-            # launches run side by side on several streams
-            self._par_launches(fns)
+            # launches run side by side on several streams (the float4 plain
+            # kernels store only their own elements of a 4-cell group that
+            # straddles an unaligned z border with a chain box: st4m)
+            self._par_launches(pfns + fns)
         else:
-            for f in fns:
+            for f in pfns + fns:
                 f()
         for c, b in slow_all:
             self._upml_region(kind, c, p, b)
