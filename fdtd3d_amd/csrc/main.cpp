@@ -25,6 +25,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <array>
 #include <cctype>
 #include <cerrno>
 #include <chrono>
@@ -1168,6 +1169,12 @@ int run(const fdtd::Settings& s) {
       }
     }
   }
+  if (upml && dim == 3) {
+    // region-local D / D1 levels over the chain regions (models/regions.py)
+    std::vector<std::array<int, 6>> rb;
+    for (const IBox& r : chain_regs) rb.push_back({r.lo[0], r.lo[1], r.lo[2], r.hi[0], r.hi[1], r.hi[2]});
+    native_phys::alloc_levels(upt, rb, chain_disp);
+  }
   // Drude box inside the blocked passes (models/blocking.py _plan_drude_blk,
   // tb3d_mr.h DrDev): every hybrid pass runs the plain blocked core over the
   // box too, then the Drude variant over the box grown by T, carrying
@@ -1322,7 +1329,8 @@ int run(const fdtd::Settings& s) {
     int rb[36];
     for (size_t q = 0; q < chain_regs.size(); ++q) {
       clip36(chain_regs[q], rb);
-      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false, !chain_disp[q]));
+      K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], st, chain_fn, false, !chain_disp[q], nullptr,
+                                     1.0, (int)q));
     }
     native_phys::upml_rotate(upt, kind);
     for (const IBox& r : plain_regs) {
@@ -1739,21 +1747,46 @@ int run(const fdtd::Settings& s) {
   // store only their own elements of a 4-cell group that straddles an
   // unaligned z border with a chain box; the level rotation is a host pointer
   // swap after the launches captured their pointers)
+  // A thin plain part on the z side of a non-dispersive chain slab with a
+  // footprint inside the slab's rides in that slab's chain launch (its rows
+  // are read once, whole; models/scheme.py _chain_plan "fold").
   auto upml_shell = [&](int kind, const std::vector<IBox>& wins) {
     fptrs();
     std::vector<std::function<void(hipStream_t)>> fns, pfns;
-    for (size_t q = 0; q < chain_regs.size(); ++q) {
-      if (dr_blk && q + 1 == chain_regs.size()) continue;  // the Drude box: inside the blocked passes
-      fns.push_back([&, q, kind](hipStream_t ss) {
-        int rb[36];
-        clip36(chain_regs[q], rb);
-        K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], ss, chain_fn, false, !chain_disp[q]));
-      });
-    }
+    std::vector<IBox> parts;
     for (const IBox& w : wins)
       for (const IBox& pr : plain_regs) {
         const IBox b = box_and(w, pr);
-        if (b.empty()) continue;
+        if (!b.empty()) parts.push_back(b);
+      }
+    std::vector<int> fold(chain_regs.size(), -1);
+    std::vector<bool> folded(parts.size(), false);
+    for (size_t n = 0; n < parts.size(); ++n) {
+      const IBox& b = parts[n];
+      if (b.hi[2] - b.lo[2] > 64) continue;
+      for (size_t q = 0; q < chain_regs.size(); ++q) {
+        const IBox& cr = chain_regs[q];
+        if (fold[q] >= 0 || chain_disp[q] || (dr_blk && q + 1 == chain_regs.size())) continue;
+        if (b.lo[0] < cr.lo[0] || b.hi[0] > cr.hi[0] || b.lo[1] < cr.lo[1] || b.hi[1] > cr.hi[1]) continue;
+        if (b.lo[2] != cr.hi[2] && b.hi[2] != cr.lo[2]) continue;
+        fold[q] = (int)n;
+        folded[n] = true;
+        break;
+      }
+    }
+    for (size_t q = 0; q < chain_regs.size(); ++q) {
+      if (dr_blk && q + 1 == chain_regs.size()) continue;  // the Drude box: inside the blocked passes
+      fns.push_back([&, q, kind](hipStream_t ss) {
+        int rb[36], pb[36];
+        clip36(chain_regs[q], rb);
+        if (fold[q] >= 0) clip36(parts[fold[q]], pb);
+        K_OK(native_phys::upml_kind<T>(upt, Fp, rb, kind, N[1], N[2], ss, chain_fn, false, !chain_disp[q],
+                                       fold[q] >= 0 ? pb : nullptr, kind == 0 ? cb : db, (int)q));
+      });
+    }
+    for (size_t n = 0; n < parts.size(); ++n) {
+        if (folded[n]) continue;
+        const IBox b = parts[n];
         pfns.push_back([&, b, kind](hipStream_t ss) {
           int rb[36];
           clip36(b, rb);
@@ -1764,7 +1797,7 @@ int run(const fdtd::Settings& s) {
             K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, db, N[0], N[1], N[2],
                      rb + 18, 0, ss, v4));
         });
-      }
+    }
     fns.insert(fns.end(), pfns.begin(), pfns.end());
     par_fns(fns);
     native_phys::upml_rotate(upt, kind);
@@ -2107,8 +2140,11 @@ int run(const fdtd::Settings& s) {
       for (int c = 0; c < 6; ++c) {
         for (int l = 0; l < 2; ++l)
           if (p2.D[c][l]) v.push_back({p2.D[c][l], cells * sizeof(T)});
-        for (T* d : upt.D[c]) v.push_back({d, cells * sizeof(T)});
-        for (T* d : upt.D1[c]) v.push_back({d, cells * sizeof(T)});
+        for (const auto& lv : upt.D[c])
+          for (size_t q = 0; q < lv.size(); ++q) v.push_back({lv[q], upt.rvol[q] * sizeof(T)});
+        for (const auto& lv : upt.D1[c])
+          for (size_t q = 0; q < lv.size(); ++q)
+            if (lv[q]) v.push_back({lv[q], upt.rvol[q] * sizeof(T)});
       }
       return v;
     };

@@ -10,6 +10,8 @@
 // 4093-4509.
 #pragma once
 
+#include <array>
+
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -118,7 +120,12 @@ struct Upml {
   const T* prof[6][6] = {};
   T* cell[6] = {};
   double s[6] = {};
-  std::vector<T*> D[6], D1[6];
+  // D / D1 levels region-local (models/regions.py): D[c][l][q] = level l of
+  // component c over chain region q (lo[3] hi[3] in rbox[q], x-major, z
+  // fastest); only chain cells ever read their levels
+  std::vector<std::vector<T*>> D[6], D1[6];
+  std::vector<std::array<int, 6>> rbox;
+  std::vector<size_t> rvol;
   bool disp[6] = {};
   unsigned char* ids[6] = {};
   T* lut[6] = {};
@@ -251,10 +258,27 @@ void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt,
       U.cell[c] = dev_upload(cl, U.keep);
       U.s[c] = 1.0;
     }
+  }
+}
+
+// the level storage over the chain regions (after the plan knows them):
+// ``disp_reg[q]`` -- region q runs the dispersive form (D1 levels there)
+template <typename T>
+void alloc_levels(Upml<T>& U, const std::vector<std::array<int, 6>>& regs, const std::vector<bool>& disp_reg) {
+  U.rbox = regs;
+  U.rvol.clear();
+  for (const auto& b : regs)
+    U.rvol.push_back((size_t)std::max(0, b[3] - b[0]) * std::max(0, b[4] - b[1]) * std::max(0, b[5] - b[2]));
+  for (int c = 0; c < 6; ++c) {
     const int nlev = U.disp[c] ? 3 : 2;
-    for (int l = 0; l < nlev; ++l) U.D[c].push_back(dev_zeros<T>(cells, U.keep));
+    U.D[c].assign(nlev, std::vector<T*>(regs.size(), nullptr));
+    U.D1[c].assign(U.disp[c] ? 3 : 0, std::vector<T*>(regs.size(), nullptr));
+    for (int l = 0; l < nlev; ++l)
+      for (size_t q = 0; q < regs.size(); ++q) U.D[c][l][q] = dev_zeros<T>(std::max<size_t>(1, U.rvol[q]), U.keep);
     if (U.disp[c])
-      for (int l = 0; l < 3; ++l) U.D1[c].push_back(dev_zeros<T>(cells, U.keep));
+      for (int l = 0; l < 3; ++l)
+        for (size_t q = 0; q < regs.size(); ++q)
+          if (disp_reg[q]) U.D1[c][l][q] = dev_zeros<T>(std::max<size_t>(1, U.rvol[q]), U.keep);
   }
 }
 
@@ -265,17 +289,13 @@ template <typename T>
 void upml_rotate(Upml<T>& U, int kind) {
   for (int cc = 0; cc < 3; ++cc) {
     const int c = 3 * kind + cc;
-    std::vector<T*>& D = U.D[c];
+    auto& D = U.D[c];
     if (D.size() == 3) {
-      T* n = D[2];
-      D[2] = D[1];
-      D[1] = D[0];
-      D[0] = n;
-      std::vector<T*>& E1 = U.D1[c];
-      T* n1 = E1[2];
-      E1[2] = E1[1];
-      E1[1] = E1[0];
-      E1[0] = n1;
+      std::swap(D[2], D[1]);
+      std::swap(D[1], D[0]);  // (new, cur, prev) -> (old prev, new, cur)
+      auto& E1 = U.D1[c];
+      std::swap(E1[2], E1[1]);
+      std::swap(E1[1], E1[0]);
     } else if (D.size() == 2) {
       std::swap(D[0], D[1]);
     }
@@ -285,7 +305,10 @@ void upml_rotate(Upml<T>& U, int kind) {
 template <typename T>
 int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int nz, void* stream,
               int (*chain)(const void* const*, const double*, const int*, int, int, int, int, void*),
-              bool rotate = true, bool plain_form = false) {
+              bool rotate = true, bool plain_form = false, const int* pboxes = nullptr, double pcb = 1.0,
+              int region = 0) {
+  // pboxes (36 ints, per component lo[3] hi[3]): plain Yee cells folded into
+  // the launch, F += pcb curl (a thin shell window on the z side of a z slab)
   // plain_form: dispersive components take the non-dispersive chain (E from D
   // through 1/eps0) -- the launches over boxes without dispersive cells (the
   // PML slabs around an interior sphere)
@@ -299,15 +322,17 @@ int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int n
     const void** p = P + 24 * cc;
     const bool d = U.disp[c] && !plain_form;
     drude = drude || d;
-    std::vector<T*>& D = U.D[c];
+    const auto& D = U.D[c];
+    const int q = region;
     p[0] = F[c];
-    p[1] = D.back();
-    p[2] = D[0];
-    p[3] = d ? D[1] : nullptr;
+    p[1] = D.back()[q];
+    p[2] = D[0][q];
+    p[3] = d ? D[1][q] : nullptr;
     if (d) {
-      p[4] = U.D1[c][2];
-      p[5] = U.D1[c][0];
-      p[6] = U.D1[c][1];
+      p[4] = U.D1[c][2][q];
+      p[5] = U.D1[c][0][q];
+      p[6] = U.D1[c][1][q];
+      if (!p[4] || !p[5] || !p[6]) return (int)hipErrorInvalidValue;
     }
     p[7] = F[kCurlT[c][0][0]];
     p[8] = F[kCurlT[c][1][0]];
@@ -316,7 +341,7 @@ int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int n
     p[21] = U.ids[c];
     p[22] = U.lut[c];
     S[2 * cc] = (U.disp[c] && !d) ? 1.0 / (c < 3 ? kEps0 : kMu0) : U.s[c];
-    S[2 * cc + 1] = 1.0;
+    S[2 * cc + 1] = pcb;
     int* in = I + 25 * cc;
     in[0] = kCurlT[c][0][1];
     in[1] = kCurlT[c][1][1];
@@ -326,6 +351,9 @@ int upml_kind(Upml<T>& U, T* const* F, const int* boxes, int kind, int ny, int n
     in[5] = kUpmlAxes[c][1];
     in[6] = kUpmlAxes[c][2];
     for (int q = 0; q < 6; ++q) in[7 + q] = boxes[6 * c + q];
+    if (pboxes)
+      for (int e = 0; e < 6; ++e) in[13 + e] = pboxes[6 * c + e];
+    for (int e = 0; e < 6; ++e) in[19 + e] = U.rbox[q][e];  // the storage box of the levels
   }
   // a kind launches in one form: every component dispersive, or none
   for (int cc = 0; cc < 3; ++cc)
