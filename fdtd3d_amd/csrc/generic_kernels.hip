@@ -373,7 +373,100 @@ __global__ __launch_bounds__(256) void k_cpml(T* __restrict__ target, const T* _
   const T corr = kc[n] * d + ps;
   target[off] += coef_at(cb, i, j, k, off) * (sign > 0 ? corr : -corr);
 }
+
+// Up to 8 CPML slab corrections of one half step in ONE launch (the 2D hybrid
+// shell replays ~30 small launches a step from a HIP graph, so a step costs
+// its launch count; profiles/graph2d_r4.md): blocks numbered slab by slab,
+// each slab the k_cpml grid (plane blocks x x planes) of its box.
+constexpr int CPML_MANY = 8;
+template <typename T>
+struct CpmlOne {
+  T* target;
+  const T* src;
+  T* psi;
+  const T* bc;
+  const T* cc;
+  const T* kc;
+  Coef3<T> cb;
+  Box3 b, pb;
+  int axis, sign, gpl;  // gpl: plane blocks of b
+};
+template <typename T>
+struct CpmlMany {
+  CpmlOne<T> e[CPML_MANY];
+  int start[CPML_MANY + 1];
+  int n, kind_e, ny, nz;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_cpml_many(CpmlMany<T> M) {
+  const int id = (int)blockIdx.x;
+  int q = 0;
+#pragma unroll
+  for (int r = 1; r < CPML_MANY; ++r) q += (r < M.n && id >= M.start[r]) ? 1 : 0;
+  const CpmlOne<T>& E = M.e[q];
+  const int loc = id - M.start[q];
+  const int bxi = loc % E.gpl, pl = loc / E.gpl;
+  const unsigned kspan = (unsigned)(E.b.hi[2] - E.b.lo[2]);
+  const unsigned t = (unsigned)bxi * 256u + threadIdx.y * 64u + threadIdx.x;
+  const unsigned jj = t / kspan;
+  const int j = E.b.lo[1] + (int)jj, k = E.b.lo[2] + (int)(t - jj * kspan);
+  if (j >= E.b.hi[1]) return;
+  const int i = E.b.lo[0] + pl;
+  const int ny = M.ny, nz = M.nz;
+  const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
+  const size_t off = ((size_t)i * ny + j) * nz + k;
+  const long long s = stride[E.axis];
+  const T d = M.kind_e ? (E.src[off] - E.src[off - s]) : (E.src[off + s] - E.src[off]);
+  const int pny = E.pb.hi[1] - E.pb.lo[1], pnz = E.pb.hi[2] - E.pb.lo[2];
+  const size_t poff = ((size_t)(i - E.pb.lo[0]) * pny + (j - E.pb.lo[1])) * pnz + (k - E.pb.lo[2]);
+  const int n = E.axis == 0 ? i : (E.axis == 1 ? j : k);
+  const T ps = E.bc[n] * E.psi[poff] + E.cc[n] * d;
+  E.psi[poff] = ps;
+  const T corr = E.kc[n] * d + ps;
+  E.target[off] += coef_at(E.cb, i, j, k, off) * (E.sign > 0 ? corr : -corr);
+}
 }  // namespace
+
+// n <= 8 slabs of one kind: per slab P[7 q ..] = target src psi bc cc kc (+ 4 coef pointers at
+// CP[4 q ..]), S[q] = coefficient scalar, I[14 q ..] = axis sign box[6] psi_box[6]
+#define FDTD_CPML_MANY_API(SUF, T)                                                                            \
+  FDTD_API int fdtd_cpml_apply_many_##SUF(void* const* P, const void* const* CP, const double* S,            \
+                                          const int* I, int n, int kind_e, int ny, int nz, void* s) {         \
+    if (n < 0 || n > CPML_MANY) return (int)hipErrorInvalidValue;                                            \
+    CpmlMany<T> M;                                                                                            \
+    M.n = 0;                                                                                                  \
+    M.start[0] = 0;                                                                                           \
+    M.kind_e = kind_e;                                                                                        \
+    M.ny = ny;                                                                                                \
+    M.nz = nz;                                                                                                \
+    for (int q = 0; q < n; ++q) {                                                                             \
+      const Box3 b = make_box(I + 14 * q + 2);                                                                \
+      if (box_empty(b)) continue;                                                                             \
+      CpmlOne<T>& E = M.e[M.n];                                                                               \
+      E.target = (T*)P[6 * q];                                                                                \
+      E.src = (const T*)P[6 * q + 1];                                                                         \
+      E.psi = (T*)P[6 * q + 2];                                                                               \
+      E.bc = (const T*)P[6 * q + 3];                                                                          \
+      E.cc = (const T*)P[6 * q + 4];                                                                          \
+      E.kc = (const T*)P[6 * q + 5];                                                                          \
+      E.cb = coef_from<T>(S + q, CP + 4 * q);                                                                 \
+      E.b = b;                                                                                                \
+      E.pb = make_box(I + 14 * q + 8);                                                                        \
+      E.axis = I[14 * q];                                                                                     \
+      E.sign = I[14 * q + 1];                                                                                 \
+      const dim3 g = cell_grid(b);                                                                            \
+      E.gpl = (int)g.x;                                                                                       \
+      M.start[M.n + 1] = M.start[M.n] + (int)(g.x * g.z);                                                     \
+      ++M.n;                                                                                                  \
+    }                                                                                                         \
+    for (int q = M.n; q < CPML_MANY; ++q) M.start[q + 1] = M.start[M.n];                                      \
+    if (M.start[M.n] == 0) return 0;                                                                          \
+    k_cpml_many<T><<<(unsigned)M.start[M.n], dim3(64, 4), 0, (hipStream_t)s>>>(M);                            \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }
+FDTD_CPML_MANY_API(f32, float)
+FDTD_CPML_MANY_API(f64, double)
 
 #define FDTD_CPML_API(SUF, T)                                                                                 \
   FDTD_API int fdtd_cpml_apply_##SUF(T* target, const T* src, T* psi, int axis, int sign, int kind_e,         \

@@ -144,6 +144,7 @@ class CPML:
     def apply(self, kind: str, p: int, boxes) -> None:
         s = self.s
         F = s.F[p]
+        items = []
         for c, box in boxes.items():
             if box_empty(box):
                 continue
@@ -151,8 +152,26 @@ class CPML:
                 b = box_intersect(box, sl.lbox)
                 if box_empty(b):
                     continue
-                s.ops.cpml_apply(kind, F[c], F[sl.src], sl.axis, sl.sign, sl.psi[p], sl.lbox, b, sl.b, sl.c,
-                                 sl.kinv_m1, s.cb[c])
+                items.append((F[c], F[sl.src], sl.axis, sl.sign, sl.psi[p], sl.lbox, b, sl.b, sl.c, sl.kinv_m1,
+                              s.cb[c]))
+        if len(items) > 1 and hasattr(s.ops, "cpml_apply_many"):
+            # one launch per group of slabs that update disjoint cells (2D hybrid
+            # shell graphs: a step costs its launches): the slabs of one
+            # component overlap in the corners, where two axes' psi both add
+            # to a cell -- those go to different groups (launches in order)
+            groups = []
+            for it in items:
+                for g in groups:
+                    if all(it[0].data_ptr() != o[0].data_ptr() or box_empty(box_intersect(it[6], o[6])) for o in g):
+                        g.append(it)
+                        break
+                else:
+                    groups.append([it])
+            for g in groups:
+                s.ops.cpml_apply_many(kind, g)
+            return
+        for it in items:
+            s.ops.cpml_apply(kind, *it)
 
     def state_tensors(self, p: int) -> List[torch.Tensor]:
         return [sl.psi[p] for c in self.slabs for sl in self.slabs[c]]

@@ -1025,7 +1025,15 @@ class YeeScheme(BlockedStepping):
                     for tab in self.tfsf[c]:
                         self.ops.tfsf_apply(F[c], tab, inc, boxes[c])
 
-        if len(windows) > 1 and not tfsf_here and self.hybrid is not None:
+        multi = (len(windows) > 1 and not tfsf_here and self.hybrid is not None and not chain
+                 and not self.use_upml_chain and not fused_cpml and (not self.use_cpml or cpml_once)
+                 and self.cfg.scheme in ("tmz", "tez") and getattr(self.ops, "multi2d", False))
+        if multi:
+            # 2D hybrid shell: every window of the half step in one launch (its
+            # passes replay from a HIP graph, where a step costs its launch count)
+            self.ops.curl_update_multi(kind, [{c: self.local_box(c, w) for c in comps} for w in windows], F, F,
+                                       self.cb)
+        elif len(windows) > 1 and not tfsf_here and self.hybrid is not None:
             # the hybrid shell's windows are disjoint: their launches of a half
             # step are independent and run side by side on several streams
             self._par_launches([(lambda w=w: one(w)) for w in windows])

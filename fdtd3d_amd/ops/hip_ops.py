@@ -152,6 +152,53 @@ class HipOps:
         return c.cell
 
     # ------------------------------------------------------------------ curl
+    multi2d = True  # 2D windows of a half step in one launch (curl_update_multi)
+
+    def curl_update_multi(self, kind: str, windows: Sequence[Dict[str, Box]], dst: Dict[str, torch.Tensor],
+                          src: Dict[str, torch.Tensor], cb: Dict[str, Coef]) -> None:
+        """2D (TMz / TEz): :meth:`curl_update` of several disjoint windows
+        (per window the component boxes) in one launch per 8 windows
+        (yee_lowdim.hip ``Win2``: the hybrid shell's strips replay from a HIP
+        graph, where a step costs its launch count)."""
+        scheme = self.layout.scheme
+        if scheme not in ("tmz", "tez"):
+            for w in windows:
+                self.curl_update(kind, w, dst, src, cb)
+            return
+        names = {("tmz", "E"): ("Ez",), ("tmz", "H"): ("Hx", "Hy"), ("tez", "E"): ("Ex", "Ey"),
+                 ("tez", "H"): ("Hz",)}[(scheme, kind)]
+        shape = tuple(dst[names[0]].shape)
+        for c in names:
+            self._check_tensor(dst[c], shape)
+        wins = [w for w in windows if not all(_empty(w[c]) for c in names)]
+        for w in wins:
+            for c in names:
+                if not _empty(w[c]):
+                    self._check_stencil_box(kind, c, w[c], shape)
+        st = _stream()
+        for q in range(0, len(wins), 8):
+            part = wins[q:q + 8]
+            bx = _box_arr([w[c] for w in part for c in names])
+            n = c_int(len(part))
+            if scheme == "tmz" and kind == "E":
+                rc = self.fn("tmz_e_multi")(_ptr(dst["Ez"]), _ptr(src["Hx"]), _ptr(src["Hy"]), self._cellp(cb["Ez"]),
+                                            c_double(self._scal(cb["Ez"])), c_int(shape[0]), c_int(shape[1]), bx, n,
+                                            st)
+            elif scheme == "tmz":
+                rc = self.fn("tmz_h_multi")(_ptr(dst["Hx"]), _ptr(dst["Hy"]), _ptr(src["Ez"]), self._cellp(cb["Hx"]),
+                                            self._cellp(cb["Hy"]), c_double(self._scal(cb["Hx"])), c_int(shape[0]),
+                                            c_int(shape[1]), bx, n, st)
+            elif kind == "E":
+                rc = self.fn("tez_e_multi")(_ptr(dst["Ex"]), _ptr(dst["Ey"]), _ptr(src["Hz"]), self._cellp(cb["Ex"]),
+                                            self._cellp(cb["Ey"]), c_double(self._scal(cb["Ex"])), c_int(shape[0]),
+                                            c_int(shape[1]), bx, n, st)
+            else:
+                rc = self.fn("tez_h_multi")(_ptr(dst["Hz"]), _ptr(src["Ex"]), _ptr(src["Ey"]), self._cellp(cb["Hz"]),
+                                            c_double(self._scal(cb["Hz"])), c_int(shape[0]), c_int(shape[1]), bx, n,
+                                            st)
+            _check(rc, "%s_%s_multi" % (scheme, kind.lower()))
+            self.launches += 1
+
     def curl_update(self, kind: str, boxes: Dict[str, Box], dst: Dict[str, torch.Tensor],
                     src: Dict[str, torch.Tensor], cb: Dict[str, Coef]) -> None:
         lay = self.layout
@@ -453,6 +500,45 @@ class HipOps:
                                    c_int(shape[1]), c_int(shape[2]), _box_arr([box]), _box_arr([psi_box]), _stream())
         _check(rc, "cpml_apply")
         self.launches += 1
+
+    def cpml_apply_many(self, kind: str, items) -> None:
+        """Several :meth:`cpml_apply` corrections of one kind in one launch
+        per 8 (generic_kernels.hip ``k_cpml_many``); ``items`` are the
+        argument tuples of :meth:`cpml_apply` without ``kind`` (their boxes
+        must be disjoint in the targets they update)."""
+        items = [it for it in items if not _empty(it[6])]
+        for q in range(0, len(items), 8):
+            part = items[q:q + 8]
+            P, CP, S, I = [], [], [], []
+            ny = nz = None
+            for target, src, axis, sign, psi, psi_box, box, b, c, kinv_m1, cb in part:
+                shape = tuple(target.shape)
+                self._check_tensor(target, shape)
+                self._check_tensor(src, shape)
+                for d in range(3):
+                    if not (psi_box[0][d] <= box[0][d] and box[1][d] <= psi_box[1][d]):
+                        raise HipError("CPML box %s outside psi box %s" % (box, psi_box))
+                    if box[0][d] < 0 or box[1][d] > shape[d]:
+                        raise HipError("CPML box %s outside array %s" % (box, shape))
+                if kind == "E" and box[0][axis] < 1 or kind == "H" and box[1][axis] > shape[axis] - 1:
+                    raise HipError("CPML box %s would read outside the array" % (box,))
+                if tuple(psi.shape) != tuple(psi_box[1][d] - psi_box[0][d] for d in range(3)):
+                    raise HipError("psi shape mismatch")
+                if ny is None:
+                    ny, nz = shape[1], shape[2]
+                elif (ny, nz) != (shape[1], shape[2]):
+                    raise HipError("cpml_apply_many: one array shape per launch")
+                cbs, cbp = self._coef_args(cb)
+                P += [target.data_ptr(), src.data_ptr(), psi.data_ptr(), b.data_ptr(), c.data_ptr(),
+                      kinv_m1.data_ptr()]
+                CP += list(cbp)
+                S.append(float(cbs.value))
+                I += [axis, sign] + list(box[0]) + list(box[1]) + list(psi_box[0]) + list(psi_box[1])
+            rc = self.fn("cpml_apply_many")((c_vp * len(P))(*P), (c_vp * len(CP))(*CP), (c_double * len(S))(*S),
+                                            (c_int * len(I))(*I), c_int(len(part)), c_int(1 if kind == "E" else 0),
+                                            c_int(ny), c_int(nz), _stream())
+            _check(rc, "cpml_apply_many")
+            self.launches += 1
 
     # --------------------------------------------------------------- sources
     def set_value(self, t: torch.Tensor, idx: Sequence[int], value: float) -> None:
