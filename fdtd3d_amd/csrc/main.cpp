@@ -44,928 +44,12 @@
 #include "native_physics.h"
 #include "settings_native.h"
 
+#include "native_api.h"
+#include "native_setup.h"
+#include "native_ckpt.h"
+
 namespace {
 
-constexpr double kC = 2.99792458e8;
-constexpr double kEps0 = 8.8541878176203892e-12;
-constexpr double kMu0 = 1.2566370614359173e-6;
-constexpr double kPi = 3.14159265358979323846;
-
-#define HIP_OK(x)                                                                       \
-  do {                                                                                  \
-    hipError_t e_ = (x);                                                                \
-    if (e_ != hipSuccess) {                                                             \
-      std::fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
-      std::exit(1);                                                                     \
-    }                                                                                   \
-  } while (0)
-
-#define K_OK(x)                                                              \
-  do {                                                                       \
-    int r_ = (x);                                                            \
-    if (r_ != 0) {                                                           \
-      std::fprintf(stderr, "kernel launch failed (%d) at %s:%d\n", r_, __FILE__, __LINE__); \
-      std::exit(1);                                                          \
-    }                                                                        \
-  } while (0)
-
-double sphere_eps(double x, double y, double z, const double c[3], double r, double eps) {
-  // linear sub-cell smoothing (reference Approximation.cpp:286-314)
-  const double d = std::sqrt((x - c[0]) * (x - c[0]) + (y - c[1]) * (y - c[1]) + (z - c[2]) * (z - c[2]));
-  const double diff = d - r;
-  if (diff < -0.5) return eps;
-  if (diff > 0.5) return 1.0;
-  const double p = 0.5 - diff;
-  return p * eps + (1 - p) * 1.0;
-}
-
-template <typename T>
-struct Dev {
-  T* p = nullptr;
-  size_t n = 0;
-  void alloc(size_t count) {
-    n = count;
-    HIP_OK(hipMalloc(&p, n * sizeof(T)));
-    HIP_OK(hipMemset(p, 0, n * sizeof(T)));
-  }
-  void reset() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
-  ~Dev() { reset(); }
-};
-
-template <typename T>
-struct Api;
-template <>
-struct Api<float> {
-  static constexpr const char* name = "float";
-};
-template <>
-struct Api<double> {
-  static constexpr const char* name = "double";
-};
-
-int e3d(float* a, float* b, float* c, const float* d, const float* e, const float* f, const float* g,
-        const float* h, const float* i, double cb, int nx, int ny, int nz, const int* bx, int xc, void* s, bool v4) {
-  return v4 ? fdtd_update_e3d_v4_f32(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s)
-            : fdtd_update_e3d_f32(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s);
-}
-int e3d(double* a, double* b, double* c, const double* d, const double* e, const double* f, const double* g,
-        const double* h, const double* i, double cb, int nx, int ny, int nz, const int* bx, int xc, void* s, bool) {
-  return fdtd_update_e3d_f64(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s);
-}
-int h3d(float* a, float* b, float* c, const float* d, const float* e, const float* f, const float* g,
-        const float* h, const float* i, double cb, int nx, int ny, int nz, const int* bx, int xc, void* s, bool v4) {
-  return v4 ? fdtd_update_h3d_v4_f32(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s)
-            : fdtd_update_h3d_f32(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s);
-}
-int h3d(double* a, double* b, double* c, const double* d, const double* e, const double* f, const double* g,
-        const double* h, const double* i, double cb, int nx, int ny, int nz, const int* bx, int xc, void* s, bool) {
-  return fdtd_update_h3d_f64(a, b, c, d, e, f, g, h, i, cb, nx, ny, nz, bx, xc, s);
-}
-int fused(const float* const* ei, const float* const* hi, float* const* eo, float* const* ho,
-          const float* const* cbs, const float* const* dbs, double cb, double db, int nx, int ny, int nz,
-          const int* bx, long long so, int sc, double sv, void* s, bool v4) {
-  return v4 ? fdtd_fused3d_v4_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s)
-            : fdtd_fused3d_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s);
-}
-int fused(const double* const* ei, const double* const* hi, double* const* eo, double* const* ho,
-          const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
-          const int* bx, long long so, int sc, double sv, void* s, bool) {
-  return fdtd_fused3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, 0, so, sc, sv, s);
-}
-// temporally blocked pass (fp32: yee3d_tb.hip, fp64: yee3d_tb64.hip)
-// fp32: a sparse float4 box of the E coefficients (ce4 over ebox, scalar cb
-// elsewhere, scalar db) takes the multi-row kernel; otherwise per-kind arrays
-int tb3d(const float* const* ei, const float* const* hi, float* const* eo, float* const* ho, const float* const* cbs,
-         const float* const* dbs, double cb, double db, int nx, int ny, int nz, const int* bx, int T,
-         const int* src, const double* vals, void* s, const void* ce4 = nullptr, const int* ebox = nullptr,
-         const int* obox = nullptr) {
-  const int whole[6] = {0, 0, 0, nx, ny, nz};
-  const int* ob = obox ? obox : whole;
-  if (ce4) {
-    const int none[6] = {0, 0, 0, 0, 0, 0};
-    return fdtd_tb3d_ext_f32(ei, hi, eo, ho, ce4, ebox, nullptr, none, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals,
-                             nullptr, nullptr, s);
-  }
-  return fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
-}
-int tb3d(const double* const* ei, const double* const* hi, double* const* eo, double* const* ho,
-         const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
-         const int* bx, int T, const int* src, const double* vals, void* s, const void* = nullptr,
-         const int* = nullptr) {
-  const int ob[6] = {0, 0, 0, nx, ny, nz};
-  return fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
-}
-int tb2d(int mode, const float* const* ei, const float* const* hi, float* const* eo, float* const* ho,
-         const float* const* cs, double cb, double db, int nx, int ny, const int* bx, const int* ob, int T,
-         const int* src, const double* vals, void* s) {
-  return fdtd_tb2d_f32(mode, ei, hi, eo, ho, cs, cb, db, nx, ny, bx, ob, 0, T, src, vals, s);
-}
-int tb2d(int mode, const double* const* ei, const double* const* hi, double* const* eo, double* const* ho,
-         const double* const* cs, double cb, double db, int nx, int ny, const int* bx, const int* ob, int T,
-         const int* src, const double* vals, void* s) {
-  return fdtd_tb2d_f64(mode, ei, hi, eo, ho, cs, cb, db, nx, ny, bx, ob, 0, T, src, vals, s);
-}
-int res1d(float* ez, float* hy, const float* ce, const float* ch, double cb, double db, int n, const int* bx, int steps,
-          int si, const float* vals, void* s) {
-  return fdtd_res1d_f32(ez, hy, ce, ch, cb, db, n, bx, steps, si, vals, s);
-}
-int res1d(double* ez, double* hy, const double* ce, const double* ch, double cb, double db, int n, const int* bx,
-          int steps, int si, const double* vals, void* s) {
-  return fdtd_res1d_f64(ez, hy, ce, ch, cb, db, n, bx, steps, si, vals, s);
-}
-int setv(float* f, long long off, double v, void* s) { return fdtd_set_value_f32(f, off, v, s); }
-int setv(double* f, long long off, double v, void* s) { return fdtd_set_value_f64(f, off, v, s); }
-int tmz_e(float* a, const float* b, const float* c, const float* d, double cb, int nx, int ny, const int* bx, void* s) {
-  return fdtd_tmz_e_f32(a, b, c, d, cb, nx, ny, bx, 0, s);
-}
-int tmz_e(double* a, const double* b, const double* c, const double* d, double cb, int nx, int ny, const int* bx,
-          void* s) {
-  return fdtd_tmz_e_f64(a, b, c, d, cb, nx, ny, bx, 0, s);
-}
-int tmz_h(float* a, float* b, const float* c, const float* d, const float* e, double db, int nx, int ny,
-          const int* bx, void* s) {
-  return fdtd_tmz_h_f32(a, b, c, d, e, db, nx, ny, bx, 0, s);
-}
-int tmz_h(double* a, double* b, const double* c, const double* d, const double* e, double db, int nx, int ny,
-          const int* bx, void* s) {
-  return fdtd_tmz_h_f64(a, b, c, d, e, db, nx, ny, bx, 0, s);
-}
-int tez_e(float* a, float* b, const float* c, const float* d, const float* e, double cb, int nx, int ny,
-          const int* bx, void* s) {
-  return fdtd_tez_e_f32(a, b, c, d, e, cb, nx, ny, bx, 0, s);
-}
-int tez_e(double* a, double* b, const double* c, const double* d, const double* e, double cb, int nx, int ny,
-          const int* bx, void* s) {
-  return fdtd_tez_e_f64(a, b, c, d, e, cb, nx, ny, bx, 0, s);
-}
-int tez_h(float* a, const float* b, const float* c, const float* d, double db, int nx, int ny, const int* bx, void* s) {
-  return fdtd_tez_h_f32(a, b, c, d, db, nx, ny, bx, 0, s);
-}
-int tez_h(double* a, const double* b, const double* c, const double* d, double db, int nx, int ny, const int* bx,
-          void* s) {
-  return fdtd_tez_h_f64(a, b, c, d, db, nx, ny, bx, 0, s);
-}
-int e1d(float* a, const float* b, const float* c, double cb, int lo, int hi, void* s) {
-  return fdtd_1d_e_f32(a, b, c, cb, lo, hi, s);
-}
-int e1d(double* a, const double* b, const double* c, double cb, int lo, int hi, void* s) {
-  return fdtd_1d_e_f64(a, b, c, cb, lo, hi, s);
-}
-int h1d(float* a, const float* b, const float* c, double db, int lo, int hi, void* s) {
-  return fdtd_1d_h_f32(a, b, c, db, lo, hi, s);
-}
-int h1d(double* a, const double* b, const double* c, double db, int lo, int hi, void* s) {
-  return fdtd_1d_h_f64(a, b, c, db, lo, hi, s);
-}
-int xfer(float* const* a, float* const* b, int n, int ny, int nz, const int* bx, void* s) {
-  return fdtd_box_xfer_f32(a, b, n, ny, nz, bx, s);
-}
-int xfer(double* const* a, double* const* b, int n, int ny, int nz, const int* bx, void* s) {
-  return fdtd_box_xfer_f64(a, b, n, ny, nz, bx, s);
-}
-int setvs(float* f, const long long* o, int n, double v, void* s) { return fdtd_set_values_f32(f, o, n, v, s); }
-int setvs(double* f, const long long* o, int n, double v, void* s) { return fdtd_set_values_f64(f, o, n, v, s); }
-int curl_gen(float* out, const float* inp, const float* const* srcs, const int* axes, const int* signs, int nt,
-             int ke, const void* const* ca, const void* const* cbp, int ny, int nz, const int* box, void* s) {
-  return fdtd_curl_general_f32(out, inp, srcs, axes, signs, nt, ke, 1.0, ca, 1.0, cbp, ny, nz, box, s);
-}
-int curl_gen(double* out, const double* inp, const double* const* srcs, const int* axes, const int* signs, int nt,
-             int ke, const void* const* ca, const void* const* cbp, int ny, int nz, const int* box, void* s) {
-  return fdtd_curl_general_f64(out, inp, srcs, axes, signs, nt, ke, 1.0, ca, 1.0, cbp, ny, nz, box, s);
-}
-int lincomb(float* out, int nt, const double* sc, const void* const* p, const float* const* xs, int ny, int nz,
-            const int* box, void* s) {
-  return fdtd_lincomb_f32(out, nt, sc, p, xs, ny, nz, box, s);
-}
-int lincomb(double* out, int nt, const double* sc, const void* const* p, const double* const* xs, int ny, int nz,
-            const int* box, void* s) {
-  return fdtd_lincomb_f64(out, nt, sc, p, xs, ny, nz, box, s);
-}
-int cpml_apply(float* t, const float* src, float* psi, int axis, int sign, int ke, const float* b, const float* c,
-               const float* k, double cbs, const void* const* cbp, int ny, int nz, const int* box, const int* pb,
-               void* s) {
-  return fdtd_cpml_apply_f32(t, src, psi, axis, sign, ke, b, c, k, cbs, cbp, ny, nz, box, pb, s);
-}
-int cpml_apply(double* t, const double* src, double* psi, int axis, int sign, int ke, const double* b,
-               const double* c, const double* k, double cbs, const void* const* cbp, int ny, int nz, const int* box,
-               const int* pb, void* s) {
-  return fdtd_cpml_apply_f64(t, src, psi, axis, sign, ke, b, c, k, cbs, cbp, ny, nz, box, pb, s);
-}
-int amp_many(const float* const* f, float* const* a, int n, int ny, int nz, const int* bx, long long xs, double acc,
-             unsigned* cnt, void* s) {
-  return fdtd_amplitude_many_f32((const void* const*)f, (void* const*)a, n, ny, nz, bx, xs, acc, cnt, s);
-}
-int amp_many(const double* const* f, double* const* a, int n, int ny, int nz, const int* bx, long long xs,
-             double acc, unsigned* cnt, void* s) {
-  return fdtd_amplitude_many_f64((const void* const*)f, (void* const*)a, n, ny, nz, bx, xs, acc, cnt, s);
-}
-
-// CPML (3D, fp32 float4 kernels): profiles, psi slabs and the per-kind term
-// tables of yee3d_cpml.hip -- the same slabs and profiles as
-// fdtd3d_amd/models/cpml.py (polynomial grading m = 4, R = 1e-8, kappa and
-// alpha from --cpml-kappa-max / --cpml-alpha-max, each component's own
-// staggered position).
-// ---- boxes (lo[3], hi[3]) for the hybrid passes
-struct IBox {
-  int lo[3], hi[3];
-  bool empty() const { return hi[0] <= lo[0] || hi[1] <= lo[1] || hi[2] <= lo[2]; }
-  long long volume() const { return empty() ? 0 : (long long)(hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]); }
-};
-
-IBox box_and(const IBox& a, const IBox& b) {
-  IBox r;
-  for (int d = 0; d < 3; ++d) {
-    r.lo[d] = std::max(a.lo[d], b.lo[d]);
-    r.hi[d] = std::min(a.hi[d], b.hi[d]);
-  }
-  return r;
-}
-
-// a minus b as up to six disjoint slabs (x first, then y, then z)
-std::vector<IBox> box_minus(const IBox& a, const IBox& b) {
-  std::vector<IBox> out;
-  const IBox c = box_and(a, b);
-  if (c.empty()) {
-    out.push_back(a);
-    return out;
-  }
-  IBox rest = a;
-  for (int d = 0; d < 3; ++d) {
-    if (rest.lo[d] < c.lo[d]) {
-      IBox s = rest;
-      s.hi[d] = c.lo[d];
-      out.push_back(s);
-    }
-    if (c.hi[d] < rest.hi[d]) {
-      IBox s = rest;
-      s.lo[d] = c.hi[d];
-      out.push_back(s);
-    }
-    rest.lo[d] = c.lo[d];
-    rest.hi[d] = c.hi[d];
-  }
-  return out;
-}
-
-struct NativeCpml {
-  std::vector<Dev<float>*> keep;       // psi slabs and profile arrays
-  std::vector<const void*> P[2];       // per kind (E, H): 9 x 5 pointers
-  std::vector<int> I[2];               // per kind: 9 x 4 ints
-  ~NativeCpml() {
-    for (auto* d : keep) delete d;
-  }
-  float* upload(const std::vector<float>& h) {
-    auto* d = new Dev<float>();
-    d->alloc(h.size());
-    HIP_OK(hipMemcpy(d->p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
-    keep.push_back(d);
-    return d->p;
-  }
-  float* zeros(size_t n) {
-    auto* d = new Dev<float>();
-    d->alloc(n);
-    keep.push_back(d);
-    return d->p;
-  }
-};
-
-void setup_cpml(NativeCpml& cp, const fdtd::Settings& s, const fdtd::Int3& N, const std::vector<int>& active,
-                double dt, double dx) {
-  // staggered offset of each component inside its cell (layout/yee.py MIN_COORD_FP)
-  static const double mco[6][3] = {{1.0, 0.5, 0.5}, {0.5, 1.0, 0.5}, {0.5, 0.5, 1.0},
-                                   {0.5, 1.0, 1.0}, {1.0, 0.5, 1.0}, {1.0, 1.0, 0.5}};
-  const int Ps[3] = {s.pmlSizeX, s.pmlSizeY, s.pmlSizeZ};
-  const double eta = std::sqrt(kMu0 / kEps0);
-  const double kmax = s.cpmlKappaMax, amax = s.cpmlAlphaMax;
-  for (int kind = 0; kind < 2; ++kind) {
-    cp.P[kind].assign(45, nullptr);
-    cp.I[kind].assign(36, 0);
-    for (int cc = 0; cc < 3; ++cc) {
-      const int c = 3 * kind + cc;
-      fdtd::Int3 glo, ghi;
-      fdtd::global_range(c, N, active, glo, ghi);
-      for (int a = 0; a < 3; ++a) {
-        // a component's two curl terms differentiate along the other two axes
-        const int P = Ps[a];
-        if (a == cc || P <= 0 || std::find(active.begin(), active.end(), a) == active.end()) continue;
-        const int n = N[a];
-        const double m = mco[c][a];
-        const double sig_max = -(4 + 1) * std::log(1e-8) / (2 * eta * P * dx);
-        std::vector<float> b(n, 1.f), cv(n, 0.f), kk(n, 0.f);
-        const void* psi[2] = {nullptr, nullptr};
-        int rng[2][2] = {{0, 0}, {0, 0}};
-        for (int side = 0; side < 2; ++side) {
-          int lo = glo[a], hi = ghi[a];
-          if (side == 0)
-            hi = std::min(hi, (int)std::ceil(P - m));
-          else
-            lo = std::max(lo, (int)std::floor(N[a] - P - m) + 1);
-          bool empty = hi <= lo;
-          for (int d = 0; d < 3; ++d) empty = empty || ghi[d] <= glo[d];
-          if (empty) continue;
-          if (a == 2 && N[2] % 4 == 0) {  // z slabs padded to whole float4 groups (c = 0 there)
-            lo &= ~3;
-            hi = std::min(N[2], (hi + 3) & ~3);
-          }
-          for (int v = lo; v < hi; ++v) {
-            const double idx = v + m;
-            double depth = side == 0 ? (P - idx) / P : (idx - (N[a] - P)) / P;
-            depth = std::min(1.0, std::max(0.0, depth));
-            const double d4 = depth * depth * depth * depth;
-            const double sig = sig_max * d4, kap = 1.0 + (kmax - 1.0) * d4, alp = amax * (1.0 - depth);
-            const double bc = std::exp(-(sig / kap + alp) * dt / kEps0);
-            const double den = sig * kap + kap * kap * alp;
-            b[v] = (float)bc;
-            cv[v] = (float)(den > 0 ? sig / den * (bc - 1.0) : 0.0);
-            kk[v] = (float)(1.0 / kap - 1.0);
-          }
-          // psi storage: the slab's range along a x the full extents of the other two
-          size_t vol = (size_t)(hi - lo);
-          for (int d = 0; d < 3; ++d)
-            if (d != a) vol *= (size_t)N[d];
-          psi[side] = cp.zeros(vol);
-          rng[side][0] = lo;
-          rng[side][1] = hi;
-        }
-        const int t = 3 * cc + a;
-        cp.P[kind][5 * t] = psi[0];
-        cp.P[kind][5 * t + 1] = psi[1];
-        cp.P[kind][5 * t + 2] = cp.upload(b);
-        cp.P[kind][5 * t + 3] = cp.upload(cv);
-        cp.P[kind][5 * t + 4] = cp.upload(kk);
-        cp.I[kind][4 * t] = rng[0][0];
-        cp.I[kind][4 * t + 1] = rng[0][1];
-        cp.I[kind][4 * t + 2] = rng[1][0];
-        cp.I[kind][4 * t + 3] = rng[1][1];
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------ TF/SF
-// Plane-wave injection through a total-field / scattered-field box, 3D: the
-// 1D incident line (k_inc_e / k_inc_h) and per-component correction tables
-// applied after each half step (k_tfsf_apply) -- the tables of
-// fdtd3d_amd/models/tfsf.py build_tfsf_tables, built here on the host.
-
-// numerical phase velocity of a plane wave on the Yee grid (Taflove;
-// reference Approximation.cpp:212-269, layout/approximation.py)
-double phase_velocity_3d(double delta, double wl, double courant, double nl, double theta, double phi) {
-  const double half = kPi / 2;
-  if (theta == half && (phi == 0.0 || phi == half || phi == kPi || phi == 3 * half))
-    return kC * kPi / (nl * std::asin(std::sin(kPi * courant / nl) / courant));
-  if (theta == half && (phi == kPi / 4 || phi == 3 * kPi / 4 || phi == 5 * kPi / 4 || phi == 7 * kPi / 4)) {
-    const double s2 = std::sqrt(2.0);
-    return kC * kPi / (nl * s2 * std::asin(std::sin(kPi * courant / nl) / (courant * s2)));
-  }
-  const double acc = 1e-7;  // Approximation.cpp:7
-  double k = 2 * kPi, kp = k + acc;
-  const double nd = delta / wl;
-  const double A = nd * std::sin(theta) * std::cos(phi) / 2, B = nd * std::sin(theta) * std::sin(phi) / 2;
-  const double C = nd * std::cos(theta) / 2;
-  const double D = std::pow(std::sin(kPi * courant / nl), 2) / (courant * courant);
-  for (int it = 0; (kp - k) * (kp - k) >= acc && it < 1000; ++it) {
-    kp = k;
-    const double f = std::pow(std::sin(A * k), 2) + std::pow(std::sin(B * k), 2) + std::pow(std::sin(C * k), 2) - D;
-    const double df = A * std::sin(2 * A * k) + B * std::sin(2 * B * k) + C * std::sin(2 * C * k);
-    k -= f / df;
-  }
-  return kC * 2 * kPi / k;
-}
-
-// (component, direction) -> per-axis open interval (ref lo, offset, ref hi,
-// offset), ref 0 = the box's left border L, 1 = its right border R; directions
-// L R D U B F (x low / high, y low / high, z low / high) -- models/tfsf.py
-struct TfsfPred {
-  int comp, dir;
-  struct {
-    int ra;
-    double oa;
-    int rb;
-    double ob;
-  } iv[3];
-};
-const TfsfPred kTfsfPred[24] = {
-    {0, 2, {{0, -0.5, 1, 0.5}, {0, -1.0, 0, 0.0}, {0, 0.0, 1, 0.0}}},
-    {0, 3, {{0, -0.5, 1, 0.5}, {1, 0.0, 1, 1.0}, {0, 0.0, 1, 0.0}}},
-    {0, 4, {{0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {0, -1.0, 0, 0.0}}},
-    {0, 5, {{0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {1, 0.0, 1, 1.0}}},
-    {1, 0, {{0, -1.0, 0, 0.0}, {0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
-    {1, 1, {{1, 0.0, 1, 1.0}, {0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
-    {1, 4, {{0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}, {0, -1.0, 0, 0.0}}},
-    {1, 5, {{0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}, {1, 0.0, 1, 1.0}}},
-    {2, 0, {{0, -1.0, 0, 0.0}, {0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}}},
-    {2, 1, {{1, 0.0, 1, 1.0}, {0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}}},
-    {2, 2, {{0, 0.0, 1, 0.0}, {0, -1.0, 0, 0.0}, {0, -0.5, 1, 0.5}}},
-    {2, 3, {{0, 0.0, 1, 0.0}, {1, 0.0, 1, 1.0}, {0, -0.5, 1, 0.5}}},
-    {3, 2, {{0, 0.0, 1, 0.0}, {0, -0.5, 0, 0.5}, {0, -0.5, 1, 0.5}}},
-    {3, 3, {{0, 0.0, 1, 0.0}, {1, -0.5, 1, 0.5}, {0, -0.5, 1, 0.5}}},
-    {3, 4, {{0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}, {0, -0.5, 0, 0.5}}},
-    {3, 5, {{0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}, {1, -0.5, 1, 0.5}}},
-    {4, 0, {{0, -0.5, 0, 0.5}, {0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}}},
-    {4, 1, {{1, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {0, -0.5, 1, 0.5}}},
-    {4, 4, {{0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {0, -0.5, 0, 0.5}}},
-    {4, 5, {{0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}, {1, -0.5, 1, 0.5}}},
-    {5, 0, {{0, -0.5, 0, 0.5}, {0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
-    {5, 1, {{1, -0.5, 1, 0.5}, {0, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
-    {5, 2, {{0, -0.5, 1, 0.5}, {0, -0.5, 0, 0.5}, {0, 0.0, 1, 0.0}}},
-    {5, 3, {{0, -0.5, 1, 0.5}, {1, -0.5, 1, 0.5}, {0, 0.0, 1, 0.0}}},
-};
-// curl terms (source component, derivative axis, sign) of each component (layout/yee.py CURL_TERMS)
-const int kCurl[6][2][3] = {{{5, 1, +1}, {4, 2, -1}}, {{3, 2, +1}, {5, 0, -1}}, {{4, 0, +1}, {3, 1, -1}},
-                            {{1, 2, +1}, {2, 1, -1}}, {{2, 0, +1}, {0, 2, -1}}, {{0, 1, +1}, {1, 0, -1}}};
-// staggered offset of each component inside its cell (layout/yee.py MIN_COORD_FP)
-const double kMinFP[6][3] = {{1.0, 0.5, 0.5}, {0.5, 1.0, 0.5}, {0.5, 0.5, 1.0},
-                             {0.5, 1.0, 1.0}, {1.0, 0.5, 1.0}, {1.0, 1.0, 0.5}};
-
-// ------------------------------------------------------------- 2D PML
-// Absorbing layers of the 2D schemes (TMz / TEz, fp32 / fp64) on the generic
-// one-thread-per-cell kernels of generic_kernels.hip, whose flattened (y, z)
-// plane keeps every lane busy at nz = 1:
-//  * CPML: the plain 2D update runs on every cell, then each (component, curl
-//    term, side) slab updates its psi and adds its term (models/cpml.py);
-//  * UPML (the reference's 2D PML, SchemeTMz.cpp:1896-1945): every component
-//    runs the D/B chain on its update box -- D_new = caD D + cbD curl
-//    (curl_general), E = caE E + s cell ica (cbEa D_new + ccEa D) (lincomb),
-//    the factored profiles of models/scheme.py _init_upml; where every sigma
-//    vanishes this is the plain update to round-off.
-template <typename T>
-struct Slab2d {
-  int comp, src, axis, sign;
-  int box[6], pbox[6];
-  T *psi, *b, *c, *k;
-};
-
-template <typename T>
-struct Pml2d {
-  std::vector<void*> keep;
-  std::vector<Slab2d<T>> slabs;
-  // UPML: D levels [cur, new] and the coefficient pointer sets per component
-  T* D[6][2] = {};
-  const void* ca[6][4] = {};
-  const void* cbp[6][4] = {};
-  const void* lin[6][12] = {};
-  double s[6] = {};
-  ~Pml2d() {
-    for (void* p : keep) (void)hipFree(p);
-  }
-};
-
-template <typename T>
-void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, const std::vector<int>& active,
-                  const bool* present, double dt, double dx) {
-  const int Ps[3] = {s.pmlSizeX, s.pmlSizeY, 0};
-  const double eta = std::sqrt(kMu0 / kEps0);
-  const double kmax = s.cpmlKappaMax, amax = s.cpmlAlphaMax;
-  for (int c = 0; c < 6; ++c) {
-    if (!present[c]) continue;
-    fdtd::Int3 glo, ghi;
-    fdtd::global_range(c, N, active, glo, ghi);
-    for (int t = 0; t < 2; ++t) {
-      const int src = kCurl[c][t][0], axis = kCurl[c][t][1], sign = kCurl[c][t][2];
-      if (!present[src] || axis >= 2 || Ps[axis] <= 0) continue;
-      const int Pa = Ps[axis], n = N[axis];
-      const double m = kMinFP[c][axis];
-      const double sig_max = -(4 + 1) * std::log(1e-8) / (2 * eta * Pa * dx);
-      for (int side = 0; side < 2; ++side) {
-        int lo = glo[axis], hi = ghi[axis];
-        if (side == 0)
-          hi = std::min(hi, (int)std::ceil(Pa - m));
-        else
-          lo = std::max(lo, (int)std::floor(n - Pa - m) + 1);
-        bool empty = hi <= lo;
-        for (int d = 0; d < 3; ++d) empty = empty || ghi[d] <= glo[d];
-        if (empty) continue;
-        // profiles over the whole axis with this side's clamped depth (models/cpml.py)
-        std::vector<T> b(n), cv(n), kk(n);
-        for (int v = 0; v < n; ++v) {
-          const double idx = v + m;
-          double depth = side == 0 ? (Pa - idx) / Pa : (idx - (n - Pa)) / Pa;
-          depth = std::min(1.0, std::max(0.0, depth));
-          const double d4 = depth * depth * depth * depth;
-          const double sig = sig_max * d4, kap = 1.0 + (kmax - 1.0) * d4, alp = amax * (1.0 - depth);
-          const double bc = std::exp(-(sig / kap + alp) * dt / kEps0);
-          const double den = sig * kap + kap * kap * alp;
-          b[v] = (T)bc;
-          cv[v] = (T)(den > 0 ? sig / den * (bc - 1.0) : 0.0);
-          kk[v] = (T)(1.0 / kap - 1.0);
-        }
-        Slab2d<T> sl;
-        sl.comp = c;
-        sl.src = src;
-        sl.axis = axis;
-        sl.sign = sign;
-        size_t vol = 1;
-        for (int d = 0; d < 3; ++d) {
-          sl.box[d] = d == axis ? lo : glo[d];
-          sl.box[3 + d] = d == axis ? hi : ghi[d];
-          sl.pbox[d] = d == axis ? lo : 0;
-          sl.pbox[3 + d] = d == axis ? hi : N[d];
-          vol *= (size_t)(sl.pbox[3 + d] - sl.pbox[d]);
-        }
-        sl.psi = native_phys::dev_zeros<T>(vol, P.keep);
-        sl.b = native_phys::dev_upload(b, P.keep);
-        sl.c = native_phys::dev_upload(cv, P.keep);
-        sl.k = native_phys::dev_upload(kk, P.keep);
-        P.slabs.push_back(sl);
-      }
-    }
-  }
-}
-
-// 2D UPML coefficients; ``cell_inv`` (optional, per present E component):
-// 1 / (eps eps0) per cell of a dielectric scene
-template <typename T>
-void setup_upml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, const bool* present, double dt,
-                  double dx, std::vector<T>* cell_inv) {
-  const size_t cells = (size_t)N[0] * N[1] * N[2];
-  std::vector<double> sig[3];
-  const int pml[3] = {s.pmlSizeX, s.pmlSizeY, 0};
-  for (int a = 0; a < 3; ++a) sig[a] = native_phys::sigma_profile(N[a] + 1, pml[a], dx);
-  for (int c = 0; c < 6; ++c) {
-    if (!present[c]) continue;
-    const int aD = native_phys::kUpmlAxes[c][0], aA = native_phys::kUpmlAxes[c][1], aB = native_phys::kUpmlAxes[c][2];
-    auto avg = [&](int a) {
-      std::vector<double> out(N[a]);
-      double v[4];
-      for (int n = 0; n < N[a]; ++n) {
-        for (int p = 0; p < native_phys::kStencilN[c]; ++p) v[p] = sig[a][n + native_phys::kStencil[c][p][a]];
-        out[n] = native_phys::approx_mean(v, native_phys::kStencilN[c]);
-      }
-      return out;
-    };
-    const std::vector<double> sD = avg(aD), sA = avg(aA), sB = avg(aB);
-    const double two = 2 * kEps0;
-    std::vector<T> caD(N[aD]), cbD(N[aD]), caE(N[aA]), ica(N[aA]), cbEa(N[aB]), ccEa(N[aB]);
-    for (int n = 0; n < N[aD]; ++n) {
-      caD[n] = (T)((two - sD[n] * dt) / (two + sD[n] * dt));
-      cbD[n] = (T)((two * dt / dx) / (two + sD[n] * dt));
-    }
-    for (int n = 0; n < N[aA]; ++n) {
-      caE[n] = (T)((two - sA[n] * dt) / (two + sA[n] * dt));
-      ica[n] = (T)(1.0 / (two + sA[n] * dt));
-    }
-    for (int n = 0; n < N[aB]; ++n) {
-      cbEa[n] = (T)(two + sB[n] * dt);
-      ccEa[n] = (T)(-(two - sB[n] * dt));
-    }
-    const T* cell = nullptr;
-    P.s[c] = 1.0 / (c < 3 ? kEps0 : kMu0);
-    if (cell_inv && c < 3 && !cell_inv[c].empty()) {
-      cell = native_phys::dev_upload(cell_inv[c], P.keep);
-      P.s[c] = 1.0;
-    }
-    P.ca[c][aD] = native_phys::dev_upload(caD, P.keep);
-    P.cbp[c][aD] = native_phys::dev_upload(cbD, P.keep);
-    const T* caEd = native_phys::dev_upload(caE, P.keep);
-    const T* icad = native_phys::dev_upload(ica, P.keep);
-    const T* cbEd = native_phys::dev_upload(cbEa, P.keep);
-    const T* ccEd = native_phys::dev_upload(ccEa, P.keep);
-    // lincomb terms: (caE, E), (s ica cbEa cell, D_new), (s ica ccEa cell, D)
-    P.lin[c][aA] = caEd;
-    P.lin[c][4 + aA] = icad;
-    P.lin[c][4 + aB] = cbEd;
-    P.lin[c][4 + 3] = cell;
-    P.lin[c][8 + aA] = icad;
-    P.lin[c][8 + aB] = ccEd;
-    P.lin[c][8 + 3] = cell;
-    for (int l = 0; l < 2; ++l) P.D[c][l] = native_phys::dev_zeros<T>(cells, P.keep);
-  }
-}
-
-template <typename T>
-struct TfsfLayer {
-  Dev<long long> off, i0;
-  Dev<T> w0, w1, coef;
-  int n = 0;
-};
-
-template <typename T>
-struct NativeTfsf {
-  std::vector<TfsfLayer<T>*> tab[6];
-  Dev<T> einc, hinc;
-  int nline = 0;
-  double ce = 0, ch = 0;
-  ~NativeTfsf() {
-    for (auto& v : tab)
-      for (auto* l : v) delete l;
-  }
-};
-
-// incident-wave projection onto a component (YeeGridLayout.cpp:811-845);
-// projections zero in exact arithmetic (cos(pi/2) = 6e-17) are zero, as in
-// layout/yee.py incident_projection
-double inc_projection(int c, double t, double p, double q) {
-  double v;
-  switch (c) {
-    case 0: v = std::cos(q) * std::sin(p) - std::sin(q) * std::cos(t) * std::cos(p); break;
-    case 1: v = -std::cos(q) * std::cos(p) - std::sin(q) * std::cos(t) * std::sin(p); break;
-    case 2: v = std::sin(q) * std::sin(t); break;
-    case 3: v = std::sin(q) * std::sin(p) + std::cos(q) * std::cos(t) * std::cos(p); break;
-    case 4: v = -std::sin(q) * std::cos(p) + std::cos(q) * std::cos(t) * std::sin(p); break;
-    default: v = -(std::cos(q) * std::sin(t));
-  }
-  return std::fabs(v) < 1e-12 ? 0.0 : v;
-}
-
-template <typename T>
-bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N, const int* boxes,
-                const Dev<T>* Cc, double cb, double db, double dt, double dx, double freq, int dim,
-                const bool* present) {
-  // 2D (TMz / TEz): propagation in the xy plane, theta = pi / 2, the line
-  // 100 (Nx + Ny) long (SchemeTMz.h:186), z never bounds the TF box
-  const bool d2 = dim == 2;
-  const double th = d2 ? kPi / 2 : s.incidentWaveAngle1 * (kPi / 180.0), ph = s.incidentWaveAngle2 * (kPi / 180.0);
-  const double ps = s.incidentWaveAngle3 * (kPi / 180.0);
-  if (!(th >= 0 && th <= kPi / 2 + 1e-12 && ph >= 0 && ph <= kPi / 2 + 1e-12)) {
-    std::fprintf(stderr, "fdtd3d (native): TF/SF incident angles must lie in [0, 90] degrees\n");
-    return false;
-  }
-  const double wl = kC / freq, nl = wl / dx, courant = s.courantNum;
-  const double rel = phase_velocity_3d(dx, wl, courant, nl, kPi / 2, 0.0) /
-                     phase_velocity_3d(dx, wl, courant, nl, th, ph);
-  tf.ce = dt / (rel * kEps0 * dx);
-  tf.ch = dt / (rel * kMu0 * dx);
-  tf.nline = 100 * (N[0] + N[1] + (d2 ? 0 : N[2]));
-  tf.einc.alloc(tf.nline);
-  tf.hinc.alloc(tf.nline);
-  const double L[3] = {(double)s.tfsfSizeX, (double)s.tfsfSizeY, (double)s.tfsfSizeZ};
-  const double R[3] = {N[0] - L[0], N[1] - L[1], N[2] - L[2]};
-  const double dir[3] = {std::sin(th) * std::cos(ph), std::sin(th) * std::sin(ph), d2 ? 0.0 : std::cos(th)};
-  const double zero[3] = {L[0] - 2.5 * std::sin(th) * std::cos(ph), L[1] - 2.5 * std::sin(th) * std::sin(ph),
-                          d2 ? 0.0 : L[2] - 2.5 * std::cos(th)};
-  const int dir_axis[6] = {0, 0, 1, 1, 2, 2};
-  const bool dir_low[6] = {true, false, true, false, true, false};
-  std::vector<T> hc((size_t)N[0] * N[1] * N[2]);
-  for (int c = 0; c < 6; ++c) {
-    const int* bx = boxes + 6 * c;
-    if (bx[3] <= bx[0] || bx[4] <= bx[1] || bx[5] <= bx[2]) continue;
-    const bool kind_e = c < 3;
-    const bool pc = Cc[c].p != nullptr;
-    if (pc) HIP_OK(hipMemcpy(hc.data(), Cc[c].p, hc.size() * sizeof(T), hipMemcpyDeviceToHost));
-    struct Ent {
-      long long flat, i0;
-      double w0, w1, cv;
-      size_t seq;
-    };
-    std::vector<Ent> ents;
-    for (int t = 0; t < 2; ++t) {
-      const int src = kCurl[c][t][0], axis = kCurl[c][t][1], sign = kCurl[c][t][2];
-      if (!present[src] || axis >= dim) continue;  // the scheme's own curl terms only
-      const double proj = inc_projection(src, th, ph, ps);
-      if (proj == 0.0) continue;  // no such incident component: nothing to correct
-      for (int d = 0; d < 6; ++d) {
-        if (dir_axis[d] != axis) continue;
-        const TfsfPred* pr = nullptr;
-        for (const auto& q : kTfsfPred)
-          if (q.comp == c && q.dir == d) pr = &q;
-        if (!pr) continue;
-        std::vector<int> sel[3];
-        for (int a = 0; a < 3; ++a) {
-          const double lo = (pr->iv[a].ra ? R[a] : L[a]) + pr->iv[a].oa;
-          const double hi = (pr->iv[a].rb ? R[a] : L[a]) + pr->iv[a].ob;
-          for (int v = bx[a]; v < bx[3 + a]; ++v) {
-            const double g = v + kMinFP[c][a];
-            if (a >= dim || (g > lo && g < hi)) sel[a].push_back(v);
-          }
-        }
-        const int nb = kind_e ? (dir_low[d] ? 0 : -1) : (dir_low[d] ? 0 : 1);
-        const int tsign = dir_low[d] ? -sign : sign;
-        for (int i : sel[0])
-          for (int j : sel[1])
-            for (int k : sel[2]) {
-              int ni[3] = {i, j, k};
-              ni[axis] += nb;
-              double dd = 0.0;
-              for (int a = 0; a < 3; ++a) dd += (ni[a] + kMinFP[src][a] - zero[a]) * dir[a];
-              dd -= kind_e ? 0.5 : 0.0;
-              const long long i0 = (long long)std::floor(dd);
-              if (i0 < 0 || i0 + 1 >= tf.nline) {
-                std::fprintf(stderr, "fdtd3d (native): TF/SF box does not fit the incident line\n");
-                return false;
-              }
-              const long long flat = ((long long)i * N[1] + j) * N[2] + k;
-              const double cf = pc ? (double)hc[flat] : (kind_e ? cb : db);
-              const double w1 = dd - (double)i0;
-              ents.push_back({flat, i0, 1.0 - w1, w1, cf * tsign * proj, ents.size()});
-            }
-      }
-    }
-    if (ents.empty()) continue;
-    // layers of unique targets (k_tfsf_apply has no atomics): stable order, the
-    // r-th entry of a target goes to layer r
-    std::stable_sort(ents.begin(), ents.end(), [](const Ent& a, const Ent& b) { return a.flat < b.flat; });
-    std::vector<int> rank(ents.size(), 0);
-    int maxr = 0;
-    for (size_t q = 1; q < ents.size(); ++q)
-      if (ents[q].flat == ents[q - 1].flat) maxr = std::max(maxr, rank[q] = rank[q - 1] + 1);
-    for (int r = 0; r <= maxr; ++r) {
-      std::vector<long long> off, i0;
-      std::vector<T> w0, w1, cv;
-      for (size_t q = 0; q < ents.size(); ++q)
-        if (rank[q] == r) {
-          off.push_back(ents[q].flat);
-          i0.push_back(ents[q].i0);
-          w0.push_back((T)ents[q].w0);
-          w1.push_back((T)ents[q].w1);
-          cv.push_back((T)ents[q].cv);
-        }
-      auto* l = new TfsfLayer<T>();
-      l->n = (int)off.size();
-      l->off.alloc(off.size());
-      l->i0.alloc(i0.size());
-      l->w0.alloc(w0.size());
-      l->w1.alloc(w1.size());
-      l->coef.alloc(cv.size());
-      HIP_OK(hipMemcpy(l->off.p, off.data(), off.size() * sizeof(long long), hipMemcpyHostToDevice));
-      HIP_OK(hipMemcpy(l->i0.p, i0.data(), i0.size() * sizeof(long long), hipMemcpyHostToDevice));
-      HIP_OK(hipMemcpy(l->w0.p, w0.data(), w0.size() * sizeof(T), hipMemcpyHostToDevice));
-      HIP_OK(hipMemcpy(l->w1.p, w1.data(), w1.size() * sizeof(T), hipMemcpyHostToDevice));
-      HIP_OK(hipMemcpy(l->coef.p, cv.data(), cv.size() * sizeof(T), hipMemcpyHostToDevice));
-      tf.tab[c].push_back(l);
-    }
-  }
-  return true;
-}
-
-int inc_e(float* e, const float* h, int n, double c, double v, void* s) { return fdtd_inc_e_f32(e, h, n, c, v, s); }
-int inc_e(double* e, const double* h, int n, double c, double v, void* s) { return fdtd_inc_e_f64(e, h, n, c, v, s); }
-int inc_h(const float* e, float* h, int n, double c, void* s) { return fdtd_inc_h_f32(e, h, n, c, s); }
-int inc_h(const double* e, double* h, int n, double c, void* s) { return fdtd_inc_h_f64(e, h, n, c, s); }
-int tfsf_apply(float* t, const TfsfLayer<float>& l, const float* inc, const int* box, void* s) {
-  return fdtd_tfsf_apply_f32(t, l.off.p, l.i0.p, l.w0.p, l.w1.p, l.coef.p, nullptr, l.n, inc, box, s);
-}
-int tfsf_apply(double* t, const TfsfLayer<double>& l, const double* inc, const int* box, void* s) {
-  return fdtd_tfsf_apply_f64(t, l.off.p, l.i0.p, l.w0.p, l.w1.p, l.coef.p, nullptr, l.n, inc, box, s);
-}
-
-// ------------------------------------------------------------ checkpoints
-// The Python driver's format (io/checkpoint.py): per state array a DAT file
-// current[<step>]_rank-<r>_<name>.dat (raw values, z fastest) plus a JSON
-// sidecar checkpoint[<step>]_rank-<r>.json.  The native driver writes and
-// resumes the plain-media runs, whose state is the field components alone, so
-// checkpoints move between the two drivers in both directions.
-std::string ckpt_sidecar(const std::string& dir, long step) {
-  return dir + "/checkpoint[" + std::to_string(step) + "]_rank-0.json";
-}
-
-// raw text of a top-level JSON value: a string's contents, a [...] list, or a scalar
-std::string json_value(const std::string& j, const std::string& key, size_t from = 0) {
-  const std::string k = "\"" + key + "\":";
-  size_t p = j.find(k, from);
-  if (p == std::string::npos) return "";
-  p += k.size();
-  while (p < j.size() && std::isspace((unsigned char)j[p])) ++p;
-  if (p >= j.size()) return "";
-  if (j[p] == '"') {
-    const size_t e = j.find('"', p + 1);
-    return e == std::string::npos ? "" : j.substr(p + 1, e - p - 1);
-  }
-  if (j[p] == '[') {
-    const size_t e = j.find(']', p);
-    return e == std::string::npos ? "" : j.substr(p, e - p + 1);
-  }
-  const size_t e = j.find_first_of(",}\n", p);
-  std::string v = j.substr(p, e == std::string::npos ? std::string::npos : e - p);
-  while (!v.empty() && std::isspace((unsigned char)v.back())) v.pop_back();
-  return v;
-}
-
-std::vector<long> json_ints(const std::string& list) {
-  std::vector<long> out;
-  const char* c = list.c_str();
-  while (*c) {
-    if (*c == '-' || std::isdigit((unsigned char)*c)) {
-      char* e = nullptr;
-      out.push_back(std::strtol(c, &e, 10));
-      c = e;
-    } else {
-      ++c;
-    }
-  }
-  return out;
-}
-
-long ckpt_latest(const std::string& dir) {
-  long best = -1;
-  DIR* d = opendir(dir.c_str());
-  if (!d) return -1;
-  const std::string pre = "checkpoint[", suf = "]_rank-0.json";
-  while (dirent* e = readdir(d)) {
-    const std::string f = e->d_name;
-    if (f.size() > pre.size() + suf.size() && f.compare(0, pre.size(), pre) == 0 &&
-        f.compare(f.size() - suf.size(), suf.size(), suf) == 0)
-      best = std::max(best, std::strtol(f.c_str() + pre.size(), nullptr, 10));
-  }
-  closedir(d);
-  return best;
-}
-
-bool make_dirs(const std::string& dir) {
-  for (size_t p = 1; p <= dir.size(); ++p)
-    if (p == dir.size() || dir[p] == '/') {
-      const std::string part = dir.substr(0, p);
-      if (mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return false;
-    }
-  return true;
-}
-
-const char* const kCompNames[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
-
-// Restores the present field components of a plain-media run; returns the
-// checkpoint's step, or -1 (with a message) when the directory holds no
-// matching checkpoint
-template <typename T>
-long ckpt_load(const fdtd::Settings& s, const std::string& scheme, const fdtd::Int3& N, const bool* present,
-               Dev<T>* F) {
-  const std::string& dir = s.loadFromFile;
-  const long step = ckpt_latest(dir);
-  if (step < 0) {
-    std::fprintf(stderr, "fdtd3d: no checkpoint for rank 0 in %s\n", dir.c_str());
-    return -1;
-  }
-  std::ifstream f(ckpt_sidecar(dir, step));
-  std::stringstream buf;
-  buf << f.rdbuf();
-  const std::string j = buf.str();
-  const std::vector<long> size = json_ints(json_value(j, "size")), shape = json_ints(json_value(j, "local_shape"));
-  const std::vector<long> want = {N[0], N[1], N[2]};
-  const char* bad = nullptr;
-  if (json_value(j, "scheme") != scheme) bad = "scheme";
-  else if (json_value(j, "dtype") != s.valueType) bad = "dtype";
-  else if (json_value(j, "complex") != "false") bad = "complex";
-  else if (size != want) bad = "size";
-  else if (shape != want) bad = "local_shape";
-  // a serial run's state: the whole grid at the origin, one rank, no
-  // deep-halo sub-step in flight (the checks of io/checkpoint.py)
-  else if (json_ints(json_value(j, "origin")) != std::vector<long>{0, 0, 0}) bad = "origin";
-  else if (json_ints(json_value(j, "topology")) != std::vector<long>{1, 1, 1}) bad = "topology";
-  else if (!json_value(j, "sub_step").empty() && json_value(j, "sub_step") != "0") bad = "sub_step";
-  std::vector<std::string> names;
-  for (size_t p = j.find("\"arrays\":"); p != std::string::npos;) {
-    p = j.find("\"name\":", p);
-    if (p == std::string::npos) break;
-    names.push_back(json_value(j, "name", p));
-    p += 7;
-  }
-  std::vector<std::string> fields;
-  for (int c = 0; c < 6; ++c)
-    if (present[c]) fields.push_back(kCompNames[c]);
-  if (!bad && names != fields) bad = "arrays (a plain-media checkpoint holds the field components only)";
-  if (bad) {
-    std::fprintf(stderr, "fdtd3d: checkpoint %s mismatch in %s\n", bad, ckpt_sidecar(dir, step).c_str());
-    return -1;
-  }
-  const size_t cells = (size_t)N[0] * N[1] * N[2];
-  std::vector<T> host(cells);
-  for (int c = 0; c < 6; ++c) {
-    if (!present[c]) continue;
-    const std::string path = fdtd::grid_file_name(step, 0, kCompNames[c], dir) + ".dat";
-    std::ifstream in(path, std::ios::binary | std::ios::ate);
-    if (!in || (size_t)in.tellg() != cells * sizeof(T)) {
-      std::fprintf(stderr, "fdtd3d: %s missing or not %zu values\n", path.c_str(), cells);
-      return -1;
-    }
-    in.seekg(0);
-    in.read((char*)host.data(), (std::streamsize)(cells * sizeof(T)));
-    HIP_OK(hipMemcpy(F[c].p, host.data(), cells * sizeof(T), hipMemcpyHostToDevice));
-  }
-  return step;
-}
-
-template <typename T>
-bool ckpt_save(const fdtd::Settings& s, const std::string& scheme, const fdtd::Int3& N, const bool* present,
-               const Dev<T>* F, long step, double dx, double dt) {
-  const std::string& dir = s.checkpointDir;
-  if (!make_dirs(dir)) return false;
-  const size_t cells = (size_t)N[0] * N[1] * N[2];
-  std::vector<T> host(cells);
-  char shape[96];
-  std::snprintf(shape, sizeof(shape), "[%d, %d, %d]", N[0], N[1], N[2]);
-  std::string arrays;
-  for (int c = 0; c < 6; ++c) {
-    if (!present[c]) continue;
-    HIP_OK(hipMemcpy(host.data(), F[c].p, cells * sizeof(T), hipMemcpyDeviceToHost));
-    if (!fdtd::write_dat(fdtd::grid_file_name(step, 0, kCompNames[c], dir) + ".dat", host.data(), cells * sizeof(T)))
-      return false;
-    arrays += std::string(arrays.empty() ? "" : ", ") + "{\"name\": \"" + kCompNames[c] + "\", \"shape\": " + shape + "}";
-  }
-  std::ofstream f(ckpt_sidecar(dir, step));
-  char num[64];
-  f << "{\"format\": \"fdtd3d-amd-checkpoint-1\", \"version\": \"native\", \"step\": " << step
-    << ", \"sub_step\": 0, \"scheme\": \"" << scheme << "\", \"size\": " << shape << ", \"dtype\": \""
-    << s.valueType << "\", \"complex\": false, \"rank\": 0, \"topology\": [1, 1, 1], \"buffer_size\": 1"
-    << ", \"lo\": [0, 0, 0], \"hi\": " << shape << ", \"origin\": [0, 0, 0], \"local_shape\": " << shape;
-  std::snprintf(num, sizeof(num), "%.17g", dx);
-  f << ", \"dx\": " << num;
-  std::snprintf(num, sizeof(num), "%.17g", dt);
-  f << ", \"dt\": " << num << ", \"arrays\": [" << arrays << "]}\n";
-  return (bool)f;
-}
 
 template <typename T>
 int run(const fdtd::Settings& s) {
@@ -2281,265 +1365,9 @@ int run(const fdtd::Settings& s) {
   return 0;
 }
 
-// ------------------------------------------------------------ multi-GPU
-// --parallel-grid: the 3D grid split into x slabs over P ranks, all driven
-// by this one process (rank r on device r % devices; --topology-sizex P, or
-// one rank per visible GPU).  x is the slowest axis, so a rank's T ghost
-// planes on each side are contiguous: no pack / unpack kernels, one
-// device-to-device (xGMI peer) copy per field and side.  Every T steps each
-// rank runs the temporally blocked kernel over its owned planes (reading the
-// T-deep ghosts, the pass's dependency cone), then pulls its neighbours'
-// fresh boundary planes on its own stream; events order the passes and the
-// pulls across streams (a rank's next pass waits for its neighbours' pulls
-// from the buffer it is about to overwrite).  Point-to-point and nearest-
-// neighbour only, the shape of the node's xGMI links.  Plain Yee media
-// (vacuum / dielectric sphere) with the point source; the reference's MPI
-// grid: Source/Grid/ParallelGrid.cpp:1600-1823 (exchange), :2161-2194.
-template <typename T>
-struct XRank {
-  int dev = 0;
-  hipStream_t st = nullptr;
-  hipEvent_t done = nullptr, copied = nullptr;
-  int lo = 0, hi = 0, gl = 0, gh = 0, x0 = 0, nx = 0;
-  Dev<T> F[6], G[6], C[6];
-  int boxes[36];
-};
-
-template <typename T>
-int run_multi(const fdtd::Settings& s) {
-  fdtd::Int3 N = {s.sizeX, s.sizeY, s.sizeZ};
-  const std::vector<int> active = {0, 1, 2};
-  const double dx = s.gridStep, courant = s.courantNum;
-  const double dt = dx * courant / kC;
-  const double freq = kC / s.sourceWaveLength;
-  const double cb = dt / (kEps0 * dx), db = dt / (kMu0 * dx);
-  const bool percell = s.scene != "vacuum";
-  int ndev = 0;
-  HIP_OK(hipGetDeviceCount(&ndev));
-  const int P = s.topologySizeX > 1 ? s.topologySizeX : ndev;
-  const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
-  const int TB = std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
-  if (sizeof(T) == 4 && N[2] % 4 != 0) {
-    std::fprintf(stderr, "fdtd3d (native): fp32 parallel grids need sizez %% 4 == 0 (float4 rows)\n");
-    return 2;
-  }
-  if (N[0] / P < TB) {
-    std::fprintf(stderr, "fdtd3d (native): %d x planes over %d ranks leave fewer than %d planes per rank\n", N[0], P,
-                 TB);
-    return 2;
-  }
-  const size_t plane = (size_t)N[1] * N[2];
-  std::vector<XRank<T>> R(P);
-  for (int r = 0, x = 0; r < P; ++r) {
-    XRank<T>& q = R[r];
-    q.dev = r % ndev;
-    q.lo = x;
-    q.hi = x + N[0] / P + (r < N[0] % P ? 1 : 0);
-    x = q.hi;
-    q.gl = r > 0 ? TB : 0;
-    q.gh = r < P - 1 ? TB : 0;
-    q.x0 = q.lo - q.gl;
-    q.nx = q.hi - q.lo + q.gl + q.gh;
-    HIP_OK(hipSetDevice(q.dev));
-    HIP_OK(hipStreamCreate(&q.st));
-    HIP_OK(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&q.copied, hipEventDisableTiming));
-    const size_t n = (size_t)q.nx * plane;
-    for (int c = 0; c < 6; ++c) {
-      q.F[c].alloc(n);
-      q.G[c].alloc(n);
-    }
-    // update boxes in local indices: the global range of each component
-    // clipped to the rank's planes (ghosts included)
-    for (int c = 0; c < 6; ++c) {
-      fdtd::Int3 glo, ghi;
-      fdtd::global_range(c, N, active, glo, ghi);
-      q.boxes[6 * c] = std::max(glo[0], q.x0) - q.x0;
-      q.boxes[6 * c + 3] = std::min(ghi[0], q.x0 + q.nx) - q.x0;
-      for (int a = 1; a < 3; ++a) {
-        q.boxes[6 * c + a] = glo[a];
-        q.boxes[6 * c + 3 + a] = ghi[a];
-      }
-    }
-    if (percell) {
-      // per-cell E coefficients of the dielectric sphere (2-point eps
-      // averages, as the single-rank path), H on the scalar db
-      const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
-      std::vector<T> host(n);
-      for (int c = 0; c < 3; ++c) {
-        const int di = c == 0, dj = c == 1, dk = c == 2;
-        for (int li = 0; li < q.nx; ++li)
-          for (int j = 0; j < N[1]; ++j)
-            for (int k = 0; k < N[2]; ++k) {
-              const int i = q.x0 + li;
-              const double a = sphere_eps(i + 0.5, j + 0.5, k + 0.5, ctr, s.sphereRadius, s.sphereEps);
-              const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, k + dk + 0.5, ctr, s.sphereRadius, s.sphereEps);
-              host[((size_t)li * N[1] + j) * N[2] + k] = (T)(cb * 2.0 / (a + b));
-            }
-        q.C[c].alloc(n);
-        HIP_OK(hipMemcpy(q.C[c].p, host.data(), n * sizeof(T), hipMemcpyHostToDevice));
-      }
-    }
-  }
-  // peer access between neighbouring devices (xGMI)
-  for (int r = 0; r + 1 < P; ++r)
-    if (R[r].dev != R[r + 1].dev) {
-      for (int d = 0; d < 2; ++d) {
-        const int a = R[r + d].dev, b = R[r + 1 - d].dev;
-        int ok = 0;
-        HIP_OK(hipDeviceCanAccessPeer(&ok, a, b));
-        if (ok) {
-          HIP_OK(hipSetDevice(a));
-          const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
-        }
-      }
-    }
-  (void)hipGetLastError();
-  const fdtd::Int3 sp = {N[0] / 2, N[1] / 2, N[2] / 2};
-  auto src_val = [&](int t) {
-    if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
-    return std::sin(dt * t * 2 * kPi * freq);
-  };
-  bool first = true;
-  // k steps on every rank, then the ghost pulls
-  auto pass = [&](int t, int k) {
-    for (int r = 0; r < P; ++r) {
-      XRank<T>& q = R[r];
-      HIP_OK(hipSetDevice(q.dev));
-      if (!first) {
-        // the neighbours' pulls from this rank's (old) F are done before the
-        // pass overwrites it as its output buffer
-        if (r > 0) HIP_OK(hipStreamWaitEvent(q.st, R[r - 1].copied, 0));
-        if (r < P - 1) HIP_OK(hipStreamWaitEvent(q.st, R[r + 1].copied, 0));
-      }
-      const T* ei[3] = {q.F[0].p, q.F[1].p, q.F[2].p};
-      const T* hi[3] = {q.F[3].p, q.F[4].p, q.F[5].p};
-      T* eo[3] = {q.G[0].p, q.G[1].p, q.G[2].p};
-      T* ho[3] = {q.G[3].p, q.G[4].p, q.G[5].p};
-      const T* cbs[3] = {q.C[0].p, q.C[1].p, q.C[2].p};
-      const T* dbs[3] = {nullptr, nullptr, nullptr};
-      // every rank whose planes (ghosts included) hold the source plane sets
-      // the hard source: a neighbour's redundant ghost-plane levels need it
-      const bool has = sp[0] >= q.x0 && sp[0] < q.x0 + q.nx;
-      const int src[4] = {sp[0] - q.x0, sp[1], sp[2], has ? 2 : -1};
-      double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
-      const int ob[6] = {q.lo - q.x0, 0, 0, q.hi - q.x0, N[1], N[2]};
-      if constexpr (sizeof(T) == 4)
-        K_OK(fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.nx, N[1], N[2], q.boxes, ob, 0, k,
-                              src, vals, q.st));
-      else
-        K_OK(fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.nx, N[1], N[2], q.boxes, ob, 0, k, src,
-                           vals, q.st));
-      for (int c = 0; c < 6; ++c) std::swap(q.F[c].p, q.G[c].p);
-      HIP_OK(hipEventRecord(q.done, q.st));
-    }
-    for (int r = 0; r < P; ++r) {
-      XRank<T>& q = R[r];
-      HIP_OK(hipSetDevice(q.dev));
-      for (int side = 0; side < 2; ++side) {
-        const int nb = side == 0 ? r - 1 : r + 1;
-        if (nb < 0 || nb >= P) continue;
-        const XRank<T>& o = R[nb];
-        HIP_OK(hipStreamWaitEvent(q.st, o.done, 0));
-        // low ghosts <- the lower neighbour's top T owned planes; high ghosts
-        // <- the upper neighbour's bottom T owned planes
-        const int src_x = side == 0 ? o.hi - TB : o.lo;
-        const int dst_x = side == 0 ? q.lo - TB : q.hi;
-        const size_t bytes = (size_t)TB * plane * sizeof(T);
-        for (int c = 0; c < 6; ++c) {
-          T* dst = q.F[c].p + (size_t)(dst_x - q.x0) * plane;
-          const T* srcp = o.F[c].p + (size_t)(src_x - o.x0) * plane;
-          if (o.dev == q.dev)
-            HIP_OK(hipMemcpyAsync(dst, srcp, bytes, hipMemcpyDeviceToDevice, q.st));
-          else
-            HIP_OK(hipMemcpyPeerAsync(dst, q.dev, srcp, o.dev, bytes, q.st));
-        }
-      }
-      HIP_OK(hipEventRecord(q.copied, q.st));
-    }
-    first = false;
-  };
-  auto advance = [&](int t0, int n) {
-    int t = t0;
-    while (n > 0) {
-      const int k = std::min(TB, n);
-      pass(t, k);
-      t += k;
-      n -= k;
-    }
-  };
-  auto sync_all = [&]() {
-    for (int r = 0; r < P; ++r) {
-      HIP_OK(hipSetDevice(R[r].dev));
-      HIP_OK(hipStreamSynchronize(R[r].st));
-    }
-  };
-  const int steps = s.numTimeSteps;
-  const int warm = std::max(0, std::min(s.warmupSteps, steps));
-  advance(0, warm);
-  sync_all();
-  const auto c0 = std::chrono::steady_clock::now();
-  advance(warm, steps - warm);
-  sync_all();
-  HIP_OK(hipGetLastError());
-  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
-  const double cells = (double)N[0] * N[1] * N[2];
-  const int timed = steps - warm;
-  std::printf("Total time = %f seconds\n", sec);
-  std::printf("Dimension: 3\n");
-  std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);
-  std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", steps, timed, warm);
-  std::printf("Value type: %s\n", Api<T>::name);
-  std::printf("\n-------- Details --------\n");
-  std::printf("Parallel grid: 1\n");
-  std::printf("Number of processes: %d (ranks of one process on %d device%s)\n", P, std::min(P, ndev),
-              std::min(P, ndev) > 1 ? "s" : "");
-  std::printf("Parallel grid scheme: X (topology %dx1x1)\n", P);
-  std::printf("Buffer size: %d\n", TB);
-  std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), x-slab ghost planes by peer copies\n",
-              TB);
-  std::printf("Throughput: %.1f Mcells/s\n", cells * timed / sec / 1e6);
-  if (s.doPrintJson)
-    std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f, \"ranks\": %d}\n", sec, timed,
-                cells * timed / sec / 1e6, P);
-  if (s.doSaveRes) {
-    const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
-    std::vector<T> host((size_t)N[0] * plane);
-    for (int c = 0; c < 6; ++c) {
-      for (int r = 0; r < P; ++r) {
-        const XRank<T>& q = R[r];
-        HIP_OK(hipSetDevice(q.dev));
-        HIP_OK(hipMemcpy(host.data() + (size_t)q.lo * plane, q.F[c].p + (size_t)q.gl * plane,
-                         (size_t)(q.hi - q.lo) * plane * sizeof(T), hipMemcpyDeviceToHost));
-      }
-      const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
-      if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), host.size() * sizeof(T));
-      if (s.saveAsBMP || !s.saveAsDAT) {
-        const int kz = N[2] / 2;
-        std::vector<double> v((size_t)N[0] * N[1]);
-        for (int i = 0; i < N[0]; ++i)
-          for (int j = 0; j < N[1]; ++j) v[(size_t)i * N[1] + j] = host[((size_t)i * N[1] + j) * N[2] + kz];
-        fdtd::write_bmp(base + std::to_string(kz) + "-Re.bmp", v, N[0], N[1], s.dumperPalette);
-      }
-    }
-  }
-  for (auto& q : R) {
-    HIP_OK(hipSetDevice(q.dev));
-    for (int c = 0; c < 6; ++c) {  // freed with the rank's device current
-      q.F[c].reset();
-      q.G[c].reset();
-      q.C[c].reset();
-    }
-    HIP_OK(hipEventDestroy(q.done));
-    HIP_OK(hipEventDestroy(q.copied));
-    HIP_OK(hipStreamDestroy(q.st));
-  }
-  return 0;
-}
-
 }  // namespace
+
+#include "native_multi.h"
 
 
 int main(int argc, char** argv) {
