@@ -1063,15 +1063,16 @@ class YeeScheme(BlockedStepping):
             for c in comps:
                 self._upml_rotate(c, p)
 
-    def _par_launches(self, fns) -> None:
+    def _par_launches(self, fns, decomposed_ok: bool = False) -> None:
         """Run independent launch callables round-robin on ``--shell-streams``
         HIP streams (the current one first), joined back into the current
         stream: the tail of one small window launch overlaps the next instead
-        of idling CUs.  Serial runs on the HIP path only."""
+        of idling CUs.  HIP path only; decomposed runs only where the caller
+        says the launches touch no exchange buffer (``decomposed_ok``)."""
         n = int(getattr(self.cfg, "shell_streams", 0))
         if n <= 0:
             n = 3 if self.ops.name == "hip" else 1
-        if (n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda"
+        if (n <= 1 or len(fns) <= 1 or (self.halo is not None and not decomposed_ok) or self.device.type != "cuda"
                 or getattr(self, "_capturing", False)):
             for f in fns:
                 f()
@@ -1081,17 +1082,17 @@ class YeeScheme(BlockedStepping):
         if pool is None or len(pool) < n - 1:
             pool = self._shell_pool = [torch.cuda.Stream(device=self.device) for _ in range(n - 1)]
         pool = pool[:n - 1]
-        used = set()
+        used = range(1, min(n, len(fns)))
+        for k in used:
+            # fork before the first launch: a wait recorded after it would
+            # hold the side streams until the main stream's launch has ended
+            pool[k - 1].wait_stream(main)
         for q, f in enumerate(fns):
             k = q % n
             if k == 0:
                 f()
                 continue
-            s = pool[k - 1]
-            if k not in used:
-                s.wait_stream(main)
-                used.add(k)
-            with torch.cuda.stream(s):
+            with torch.cuda.stream(pool[k - 1]):
                 f()
         for k in used:
             main.wait_stream(pool[k - 1])

@@ -100,6 +100,10 @@ def main():
     ap.add_argument("--topology", type=int, nargs=3, default=None, help="force a rank grid (e.g. 4 2 1)")
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--thin", type=int, default=1, help="thin y shells on the single-row kernel (T <= 4)")
+    ap.add_argument("--shell-streams", type=int, default=0,
+                    help="streams the T-thick shell slabs run on (0 = automatic: 3, 1 = in order)")
+    ap.add_argument("--skip-exchange", action="store_true",
+                    help="no exchange at all (ghosts stale): the interior pass alone, no side-stream work")
     ap.add_argument("--transport", default="null", choices=("null", "loopback"))
     ap.add_argument("--link-gbs", type=float, default=0.0,
                     help="loopback: emulate the wire time of the largest message at this xGMI link rate (GB/s)")
@@ -126,11 +130,13 @@ def main():
             return sum((x >= 0) for pair in d.neighbors for x in pair)
         rank = max(range(core.used_procs), key=nn)
     dom = core.domain(rank, T, align_z=4)
-    cfg = SchemeConfig(scheme="3d", size=size, scene="vacuum", dtype="f32", use_fused=True, time_block=T)
+    cfg = SchemeConfig(scheme="3d", size=size, scene="vacuum", dtype="f32", use_fused=True, time_block=T,
+                       shell_streams=a.shell_streams)
     if a.physics != "vacuum":
         cfg = SchemeConfig(scheme="3d", size=size, scene="vacuum", dtype="f32", use_pml=True,
                            pml_type="upml" if a.physics.startswith("upml") else "cpml",
-                           use_tfsf=a.physics.endswith("tfsf"), hybrid_block=T)
+                           use_tfsf=a.physics.endswith("tfsf"), hybrid_block=T,
+                           shell_streams=a.shell_streams)
 
     breakdown = {}
 
@@ -168,6 +174,8 @@ def main():
 
     comm = (LoopbackComm(rank, a.world, a.link_gbs) if a.transport == "loopback" else NullComm(rank, a.world))
     halo = HaloExchanger(dom, comm=comm)
+    if a.skip_exchange:
+        halo.exchange_all = lambda scheme, stream=None: None
     t_dec = timed(dom, halo)
     if breakdown:
         wait_frac = breakdown["exchange_wait_ms"] / max(1e-9, breakdown["interior_ms"])
