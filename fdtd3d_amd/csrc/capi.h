@@ -76,6 +76,10 @@ int fdtd_tb3d_ext_f32(const float* const* ein, const float* const* hin, float* c
                       const void* ce4, const int* ebox, const void* ch4, const int* hbox, double cb, double db,
                       int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk, int steps,
                       const int* src, const double* src_vals, const void* tf, const float* gtab, void* stream);
+int fdtd_box_pack_f32(float* const* fields, float* buf, int ncomp, int ny, int nz, const int* box, void* s);
+int fdtd_box_pack_f64(double* const* fields, double* buf, int ncomp, int ny, int nz, const int* box, void* s);
+int fdtd_box_unpack_f32(float* const* fields, const float* buf, int ncomp, int ny, int nz, const int* box, void* s);
+int fdtd_box_unpack_f64(double* const* fields, const double* buf, int ncomp, int ny, int nz, const int* box, void* s);
 int fdtd_box_xfer_f32(float* const* src, float* const* dst, int ncomp, int ny, int nz, const int* box, void* s);
 int fdtd_box_xfer_f64(double* const* src, double* const* dst, int ncomp, int ny, int nz, const int* box, void* s);
 int fdtd_tb3d_amp_f32(const float* const* ein, const float* const* hin, float* const* eout, float* const* hout,

@@ -14,8 +14,8 @@
 // (running maxima folded into blocked passes for 3D vacuum fp32, a fused
 // amplitude kernel after each step otherwise), checkpoints / resume of
 // plain-media runs in the Python driver's format (--checkpoint-dir,
-// --load-from-file) and --parallel-grid x-slab decompositions of 3D plain
-// runs over the node's GPUs from one process (run_multi).  Complex fields and
+// --load-from-file) and --parallel-grid decompositions (any x / y / z rank
+// grid) of 3D plain runs over the node's GPUs from one process (run_multi).  Complex fields and
 // the decomposed physics runs go through the Python driver (python -m
 // fdtd3d_amd), which shares the kernels; asking this binary for them is an
 // error, never a silent fallback.
@@ -1403,11 +1403,11 @@ int main(int argc, char** argv) {
   const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
   // amplitude mode: any scheme, not with the NTFF diagram
   const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
-  // parallel grids: 3D plain media (vacuum / dielectric sphere) with the point source, x slabs
+  // parallel grids: 3D plain media (vacuum / dielectric sphere) with the point source, any rank grid
   const bool par_ok = !s.doUseParallelGrid ||
                       (s.dimension == 3 && !s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials &&
                        !s.doUseAmplitudeMode && !s.doUseNTFF && (s.scene == "vacuum" || s.scene == "sphere") &&
-                       s.topologySizeY <= 1 && s.topologySizeZ <= 1 && !s.doUseSplitKernels);
+                       !s.doUseSplitKernels);
   // checkpoints / resume: plain media (state = the field components)
   const bool ckpt = !s.checkpointDir.empty() || !s.loadFromFile.empty();
   const bool ckpt_ok = !ckpt || (!s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials && !s.doUseAmplitudeMode &&
@@ -1417,7 +1417,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr,
                  "fdtd3d (native): CPML in 3D outside fp32 float4 rows, PML / TF/SF in 1D, TF/SF boxes reaching "
                  "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "
-                 "grids beyond 3D plain media split along x, checkpoints beyond plain media, and complex "
+                 "grids beyond 3D plain media, checkpoints beyond plain media, and complex "
                  "fields run through the Python driver: python -m fdtd3d_amd <same options>\n");
     return 2;
   }

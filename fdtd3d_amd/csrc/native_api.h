@@ -148,6 +148,18 @@ int res1d(double* ez, double* hy, const double* ce, const double* ch, double cb,
           int steps, int si, const double* vals, void* s) {
   return fdtd_res1d_f64(ez, hy, ce, ch, cb, db, n, bx, steps, si, vals, s);
 }
+int box_pack(float* const* f, float* buf, int n, int ny, int nz, const int* box, void* s) {
+  return fdtd_box_pack_f32(f, buf, n, ny, nz, box, s);
+}
+int box_pack(double* const* f, double* buf, int n, int ny, int nz, const int* box, void* s) {
+  return fdtd_box_pack_f64(f, buf, n, ny, nz, box, s);
+}
+int box_unpack(float* const* f, const float* buf, int n, int ny, int nz, const int* box, void* s) {
+  return fdtd_box_unpack_f32(f, buf, n, ny, nz, box, s);
+}
+int box_unpack(double* const* f, const double* buf, int n, int ny, int nz, const int* box, void* s) {
+  return fdtd_box_unpack_f64(f, buf, n, ny, nz, box, s);
+}
 int setv(float* f, long long off, double v, void* s) { return fdtd_set_value_f32(f, off, v, s); }
 int setv(double* f, long long off, double v, void* s) { return fdtd_set_value_f64(f, off, v, s); }
 int tmz_e(float* a, const float* b, const float* c, const float* d, double cb, int nx, int ny, const int* bx, void* s) {

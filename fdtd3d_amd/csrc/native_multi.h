@@ -1,4 +1,4 @@
-// native_multi.h -- --parallel-grid x-slab decompositions driven from one process.
+// native_multi.h -- --parallel-grid decompositions (x / y / z rank grids) driven from one process.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -21,27 +21,36 @@
 namespace {
 
 // ------------------------------------------------------------ multi-GPU
-// --parallel-grid: the 3D grid split into x slabs over P ranks, all driven
-// by this one process (rank r on device r % devices; --topology-sizex P, or
-// one rank per visible GPU).  x is the slowest axis, so a rank's T ghost
-// planes on each side are contiguous: no pack / unpack kernels, one
-// device-to-device (xGMI peer) copy per field and side.  Every T steps each
-// rank runs the temporally blocked kernel over its owned planes (reading the
-// T-deep ghosts, the pass's dependency cone), then pulls its neighbours'
-// fresh boundary planes on its own stream; events order the passes and the
-// pulls across streams (a rank's next pass waits for its neighbours' pulls
-// from the buffer it is about to overwrite).  Point-to-point and nearest-
-// neighbour only, the shape of the node's xGMI links.  Plain Yee media
-// (vacuum / dielectric sphere) with the point source; the reference's MPI
-// grid: Source/Grid/ParallelGrid.cpp:1600-1823 (exchange), :2161-2194.
+// --parallel-grid: the 3D grid split over a Px x Py x Pz rank grid
+// (--topology-sizex/y/z; none given: one x slab per visible GPU), every rank
+// driven by this one process (rank r on device r % devices).  Every T steps
+// each rank runs the temporally blocked kernel over its owned cells, reading
+// T-deep ghosts (the pass's dependency cone); then it packs, for each of its
+// up to 26 face / edge / corner neighbours, the owned T-deep box that
+// neighbour holds as ghosts (one kernel, six components), and each rank pulls
+// its neighbours' packed boxes (xGMI peer copies between devices) and unpacks
+// them into its ghosts -- the direct 26-neighbour exchange of
+// parallel/halo.py, point-to-point only, the shape of the node's xGMI links.
+// Events order the streams: a neighbour's pull waits for the pack, a rank's
+// next pack waits for its neighbours' pulls of the previous one.  Plain Yee
+// media (vacuum / dielectric sphere) with the point source; the reference's
+// MPI grid: Source/Grid/ParallelGrid.cpp:1600-1823 (exchange), :2161-2194.
 template <typename T>
 struct XRank {
   int dev = 0;
   hipStream_t st = nullptr;
   hipEvent_t done = nullptr, copied = nullptr;
-  int lo = 0, hi = 0, gl = 0, gh = 0, x0 = 0, nx = 0;
+  int crd[3] = {0, 0, 0};
+  int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // owned global range
+  int g0[3] = {0, 0, 0}, n[3] = {0, 0, 0};   // allocated box (ghosts included): global origin, extent
   Dev<T> F[6], G[6], C[6];
   int boxes[36];
+  // per direction d (0..26, 13 = self): the owned box sent to the neighbour
+  // at d and the ghost box received from it (local indices), its buffers
+  int nb[27];
+  int sbox[27][6], rbox[27][6];
+  Dev<T> sbuf[27], rbuf[27];
+  size_t cells() const { return (size_t)n[0] * n[1] * n[2]; }
 };
 
 template <typename T>
@@ -55,50 +64,93 @@ int run_multi(const fdtd::Settings& s) {
   const bool percell = s.scene != "vacuum";
   int ndev = 0;
   HIP_OK(hipGetDeviceCount(&ndev));
-  const int P = s.topologySizeX > 1 ? s.topologySizeX : ndev;
+  int Pd[3] = {std::max(1, s.topologySizeX), std::max(1, s.topologySizeY), std::max(1, s.topologySizeZ)};
+  if (Pd[0] * Pd[1] * Pd[2] == 1) Pd[0] = ndev;
+  const int P = Pd[0] * Pd[1] * Pd[2];
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
   const int TB = std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
-  if (sizeof(T) == 4 && N[2] % 4 != 0) {
-    std::fprintf(stderr, "fdtd3d (native): fp32 parallel grids need sizez %% 4 == 0 (float4 rows)\n");
-    return 2;
-  }
-  if (N[0] / P < TB) {
-    std::fprintf(stderr, "fdtd3d (native): %d x planes over %d ranks leave fewer than %d planes per rank\n", N[0], P,
-                 TB);
-    return 2;
-  }
-  const size_t plane = (size_t)N[1] * N[2];
+  for (int a = 0; a < 3; ++a)
+    if (N[a] / Pd[a] < TB) {
+      std::fprintf(stderr, "fdtd3d (native): %d cells along axis %d over %d ranks leave fewer than %d per rank\n",
+                   N[a], a, Pd[a], TB);
+      return 2;
+    }
   std::vector<XRank<T>> R(P);
-  for (int r = 0, x = 0; r < P; ++r) {
+  auto rank_of = [&](const int* c) { return (c[0] * Pd[1] + c[1]) * Pd[2] + c[2]; };
+  for (int r = 0; r < P; ++r) {
+    XRank<T>& q = R[r];
+    q.crd[0] = r / (Pd[1] * Pd[2]);
+    q.crd[1] = (r / Pd[2]) % Pd[1];
+    q.crd[2] = r % Pd[2];
+    for (int a = 0; a < 3; ++a) {
+      // near-equal split, the remainder on the first ranks
+      const int base = N[a] / Pd[a], rem = N[a] % Pd[a], c = q.crd[a];
+      q.lo[a] = c * base + std::min(c, rem);
+      q.hi[a] = q.lo[a] + base + (c < rem ? 1 : 0);
+      const int gl = c > 0 ? TB : 0, gh = c < Pd[a] - 1 ? TB : 0;
+      q.g0[a] = q.lo[a] - gl;
+      q.n[a] = q.hi[a] - q.lo[a] + gl + gh;
+    }
+    if (sizeof(T) == 4 && q.n[2] % 4 != 0) {
+      std::fprintf(stderr, "fdtd3d (native): fp32 parallel grids need every rank's z extent (ghosts included) "
+                           "%% 4 == 0 (float4 rows): rank %d has %d\n", r, q.n[2]);
+      return 2;
+    }
+  }
+  for (int r = 0; r < P; ++r) {
     XRank<T>& q = R[r];
     q.dev = r % ndev;
-    q.lo = x;
-    q.hi = x + N[0] / P + (r < N[0] % P ? 1 : 0);
-    x = q.hi;
-    q.gl = r > 0 ? TB : 0;
-    q.gh = r < P - 1 ? TB : 0;
-    q.x0 = q.lo - q.gl;
-    q.nx = q.hi - q.lo + q.gl + q.gh;
     HIP_OK(hipSetDevice(q.dev));
     HIP_OK(hipStreamCreate(&q.st));
     HIP_OK(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&q.copied, hipEventDisableTiming));
-    const size_t n = (size_t)q.nx * plane;
+    const size_t n = q.cells();
     for (int c = 0; c < 6; ++c) {
       q.F[c].alloc(n);
       q.G[c].alloc(n);
     }
     // update boxes in local indices: the global range of each component
-    // clipped to the rank's planes (ghosts included)
+    // clipped to the rank's allocated box
     for (int c = 0; c < 6; ++c) {
       fdtd::Int3 glo, ghi;
       fdtd::global_range(c, N, active, glo, ghi);
-      q.boxes[6 * c] = std::max(glo[0], q.x0) - q.x0;
-      q.boxes[6 * c + 3] = std::min(ghi[0], q.x0 + q.nx) - q.x0;
-      for (int a = 1; a < 3; ++a) {
-        q.boxes[6 * c + a] = glo[a];
-        q.boxes[6 * c + 3 + a] = ghi[a];
+      for (int a = 0; a < 3; ++a) {
+        q.boxes[6 * c + a] = std::max(glo[a], q.g0[a]) - q.g0[a];
+        q.boxes[6 * c + 3 + a] = std::min(ghi[a], q.g0[a] + q.n[a]) - q.g0[a];
       }
+    }
+    // messages: direction d = (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)
+    for (int d = 0; d < 27; ++d) {
+      const int off[3] = {d / 9 - 1, (d / 3) % 3 - 1, d % 3 - 1};
+      int c[3];
+      bool ok = d != 13;
+      for (int a = 0; a < 3; ++a) {
+        c[a] = q.crd[a] + off[a];
+        ok = ok && c[a] >= 0 && c[a] < Pd[a];
+      }
+      q.nb[d] = ok ? rank_of(c) : -1;
+      if (!ok) continue;
+      size_t vol = 6;
+      for (int a = 0; a < 3; ++a) {
+        // send: the owned layers next to the neighbour; receive: the ghosts there
+        int slo = q.lo[a], shi = q.hi[a], rlo = q.lo[a], rhi = q.hi[a];
+        if (off[a] < 0) {
+          shi = q.lo[a] + TB;
+          rlo = q.lo[a] - TB;
+          rhi = q.lo[a];
+        } else if (off[a] > 0) {
+          slo = q.hi[a] - TB;
+          rlo = q.hi[a];
+          rhi = q.hi[a] + TB;
+        }
+        q.sbox[d][a] = slo - q.g0[a];
+        q.sbox[d][3 + a] = shi - q.g0[a];
+        q.rbox[d][a] = rlo - q.g0[a];
+        q.rbox[d][3 + a] = rhi - q.g0[a];
+        vol *= (size_t)(shi - slo);
+      }
+      q.sbuf[d].alloc(vol);
+      q.rbuf[d].alloc(vol);
     }
     if (percell) {
       // per-cell E coefficients of the dielectric sphere (2-point eps
@@ -107,31 +159,30 @@ int run_multi(const fdtd::Settings& s) {
       std::vector<T> host(n);
       for (int c = 0; c < 3; ++c) {
         const int di = c == 0, dj = c == 1, dk = c == 2;
-        for (int li = 0; li < q.nx; ++li)
-          for (int j = 0; j < N[1]; ++j)
-            for (int k = 0; k < N[2]; ++k) {
-              const int i = q.x0 + li;
+        for (int li = 0; li < q.n[0]; ++li)
+          for (int lj = 0; lj < q.n[1]; ++lj)
+            for (int lk = 0; lk < q.n[2]; ++lk) {
+              const int i = q.g0[0] + li, j = q.g0[1] + lj, k = q.g0[2] + lk;
               const double a = sphere_eps(i + 0.5, j + 0.5, k + 0.5, ctr, s.sphereRadius, s.sphereEps);
               const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, k + dk + 0.5, ctr, s.sphereRadius, s.sphereEps);
-              host[((size_t)li * N[1] + j) * N[2] + k] = (T)(cb * 2.0 / (a + b));
+              host[((size_t)li * q.n[1] + lj) * q.n[2] + lk] = (T)(cb * 2.0 / (a + b));
             }
         q.C[c].alloc(n);
         HIP_OK(hipMemcpy(q.C[c].p, host.data(), n * sizeof(T), hipMemcpyHostToDevice));
       }
     }
   }
-  // peer access between neighbouring devices (xGMI)
-  for (int r = 0; r + 1 < P; ++r)
-    if (R[r].dev != R[r + 1].dev) {
-      for (int d = 0; d < 2; ++d) {
-        const int a = R[r + d].dev, b = R[r + 1 - d].dev;
-        int ok = 0;
-        HIP_OK(hipDeviceCanAccessPeer(&ok, a, b));
-        if (ok) {
-          HIP_OK(hipSetDevice(a));
-          const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
-        }
+  // peer access between the devices of neighbouring ranks (xGMI)
+  for (int r = 0; r < P; ++r)
+    for (int d = 0; d < 27; ++d) {
+      const int o = R[r].nb[d];
+      if (o < 0 || R[o].dev == R[r].dev) continue;
+      int ok = 0;
+      HIP_OK(hipDeviceCanAccessPeer(&ok, R[r].dev, R[o].dev));
+      if (ok) {
+        HIP_OK(hipSetDevice(R[r].dev));
+        const hipError_t e = hipDeviceEnablePeerAccess(R[o].dev, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
       }
     }
   (void)hipGetLastError();
@@ -141,60 +192,60 @@ int run_multi(const fdtd::Settings& s) {
     return std::sin(dt * t * 2 * kPi * freq);
   };
   bool first = true;
-  // k steps on every rank, then the ghost pulls
+  // k steps on every rank, the packs, then the ghost pulls
   auto pass = [&](int t, int k) {
     for (int r = 0; r < P; ++r) {
       XRank<T>& q = R[r];
       HIP_OK(hipSetDevice(q.dev));
-      if (!first) {
-        // the neighbours' pulls from this rank's (old) F are done before the
-        // pass overwrites it as its output buffer
-        if (r > 0) HIP_OK(hipStreamWaitEvent(q.st, R[r - 1].copied, 0));
-        if (r < P - 1) HIP_OK(hipStreamWaitEvent(q.st, R[r + 1].copied, 0));
-      }
       const T* ei[3] = {q.F[0].p, q.F[1].p, q.F[2].p};
       const T* hi[3] = {q.F[3].p, q.F[4].p, q.F[5].p};
       T* eo[3] = {q.G[0].p, q.G[1].p, q.G[2].p};
       T* ho[3] = {q.G[3].p, q.G[4].p, q.G[5].p};
       const T* cbs[3] = {q.C[0].p, q.C[1].p, q.C[2].p};
       const T* dbs[3] = {nullptr, nullptr, nullptr};
-      // every rank whose planes (ghosts included) hold the source plane sets
-      // the hard source: a neighbour's redundant ghost-plane levels need it
-      const bool has = sp[0] >= q.x0 && sp[0] < q.x0 + q.nx;
-      const int src[4] = {sp[0] - q.x0, sp[1], sp[2], has ? 2 : -1};
+      // every rank whose allocated box (ghosts included) holds the source
+      // sets the hard source: a neighbour's redundant ghost levels need it
+      bool has = true;
+      for (int a = 0; a < 3; ++a) has = has && sp[a] >= q.g0[a] && sp[a] < q.g0[a] + q.n[a];
+      const int src[4] = {sp[0] - q.g0[0], sp[1] - q.g0[1], sp[2] - q.g0[2], has ? 2 : -1};
       double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
-      const int ob[6] = {q.lo - q.x0, 0, 0, q.hi - q.x0, N[1], N[2]};
+      int ob[6];
+      for (int a = 0; a < 3; ++a) {
+        ob[a] = q.lo[a] - q.g0[a];
+        ob[3 + a] = q.hi[a] - q.g0[a];
+      }
       if constexpr (sizeof(T) == 4)
-        K_OK(fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.nx, N[1], N[2], q.boxes, ob, 0, k,
-                              src, vals, q.st));
+        K_OK(fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes, ob,
+                              0, k, src, vals, q.st));
       else
-        K_OK(fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.nx, N[1], N[2], q.boxes, ob, 0, k, src,
-                           vals, q.st));
+        K_OK(fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes, ob, 0,
+                           k, src, vals, q.st));
       for (int c = 0; c < 6; ++c) std::swap(q.F[c].p, q.G[c].p);
+      // the neighbours have pulled the previous packs before these overwrite them
+      if (!first)
+        for (int d = 0; d < 27; ++d)
+          if (q.nb[d] >= 0) HIP_OK(hipStreamWaitEvent(q.st, R[q.nb[d]].copied, 0));
+      T* f[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
+      for (int d = 0; d < 27; ++d)
+        if (q.nb[d] >= 0) K_OK(box_pack(f, q.sbuf[d].p, 6, q.n[1], q.n[2], q.sbox[d], q.st));
       HIP_OK(hipEventRecord(q.done, q.st));
     }
     for (int r = 0; r < P; ++r) {
       XRank<T>& q = R[r];
       HIP_OK(hipSetDevice(q.dev));
-      for (int side = 0; side < 2; ++side) {
-        const int nb = side == 0 ? r - 1 : r + 1;
-        if (nb < 0 || nb >= P) continue;
-        const XRank<T>& o = R[nb];
+      T* f[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
+      for (int d = 0; d < 27; ++d) {
+        if (q.nb[d] < 0) continue;
+        const XRank<T>& o = R[q.nb[d]];
         HIP_OK(hipStreamWaitEvent(q.st, o.done, 0));
-        // low ghosts <- the lower neighbour's top T owned planes; high ghosts
-        // <- the upper neighbour's bottom T owned planes
-        const int src_x = side == 0 ? o.hi - TB : o.lo;
-        const int dst_x = side == 0 ? q.lo - TB : q.hi;
-        const size_t bytes = (size_t)TB * plane * sizeof(T);
-        for (int c = 0; c < 6; ++c) {
-          T* dst = q.F[c].p + (size_t)(dst_x - q.x0) * plane;
-          const T* srcp = o.F[c].p + (size_t)(src_x - o.x0) * plane;
-          if (o.dev == q.dev)
-            HIP_OK(hipMemcpyAsync(dst, srcp, bytes, hipMemcpyDeviceToDevice, q.st));
-          else
-            HIP_OK(hipMemcpyPeerAsync(dst, q.dev, srcp, o.dev, bytes, q.st));
-        }
+        // the neighbour at d packed its box for direction 26 - d (towards us)
+        const size_t bytes = q.rbuf[d].n * sizeof(T);
+        if (o.dev == q.dev)
+          HIP_OK(hipMemcpyAsync(q.rbuf[d].p, o.sbuf[26 - d].p, bytes, hipMemcpyDeviceToDevice, q.st));
+        else
+          HIP_OK(hipMemcpyPeerAsync(q.rbuf[d].p, q.dev, o.sbuf[26 - d].p, o.dev, bytes, q.st));
+        K_OK(box_unpack(f, q.rbuf[d].p, 6, q.n[1], q.n[2], q.rbox[d], q.st));
       }
       HIP_OK(hipEventRecord(q.copied, q.st));
     }
@@ -235,23 +286,33 @@ int run_multi(const fdtd::Settings& s) {
   std::printf("Parallel grid: 1\n");
   std::printf("Number of processes: %d (ranks of one process on %d device%s)\n", P, std::min(P, ndev),
               std::min(P, ndev) > 1 ? "s" : "");
-  std::printf("Parallel grid scheme: X (topology %dx1x1)\n", P);
+  std::string scheme;
+  for (int a = 0; a < 3; ++a)
+    if (Pd[a] > 1) scheme += "XYZ"[a];
+  std::printf("Parallel grid scheme: %s (topology %dx%dx%d)\n", scheme.empty() ? "X" : scheme.c_str(), Pd[0], Pd[1],
+              Pd[2]);
   std::printf("Buffer size: %d\n", TB);
-  std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), x-slab ghost planes by peer copies\n",
-              TB);
+  std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), 26-neighbour ghost boxes by packed "
+              "peer copies\n", TB);
   std::printf("Throughput: %.1f Mcells/s\n", cells * timed / sec / 1e6);
   if (s.doPrintJson)
     std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f, \"ranks\": %d}\n", sec, timed,
                 cells * timed / sec / 1e6, P);
   if (s.doSaveRes) {
     const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
-    std::vector<T> host((size_t)N[0] * plane);
+    const size_t plane = (size_t)N[1] * N[2];
+    std::vector<T> host((size_t)N[0] * plane), loc;
     for (int c = 0; c < 6; ++c) {
       for (int r = 0; r < P; ++r) {
         const XRank<T>& q = R[r];
         HIP_OK(hipSetDevice(q.dev));
-        HIP_OK(hipMemcpy(host.data() + (size_t)q.lo * plane, q.F[c].p + (size_t)q.gl * plane,
-                         (size_t)(q.hi - q.lo) * plane * sizeof(T), hipMemcpyDeviceToHost));
+        loc.resize(q.cells());
+        HIP_OK(hipMemcpy(loc.data(), q.F[c].p, loc.size() * sizeof(T), hipMemcpyDeviceToHost));
+        for (int i = q.lo[0]; i < q.hi[0]; ++i)
+          for (int j = q.lo[1]; j < q.hi[1]; ++j)
+            std::memcpy(host.data() + ((size_t)i * N[1] + j) * N[2] + q.lo[2],
+                        loc.data() + ((size_t)(i - q.g0[0]) * q.n[1] + (j - q.g0[1])) * q.n[2] + (q.lo[2] - q.g0[2]),
+                        (size_t)(q.hi[2] - q.lo[2]) * sizeof(T));
       }
       const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
       if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), host.size() * sizeof(T));
@@ -270,6 +331,10 @@ int run_multi(const fdtd::Settings& s) {
       q.F[c].reset();
       q.G[c].reset();
       q.C[c].reset();
+    }
+    for (int d = 0; d < 27; ++d) {
+      q.sbuf[d].reset();
+      q.rbuf[d].reset();
     }
     HIP_OK(hipEventDestroy(q.done));
     HIP_OK(hipEventDestroy(q.copied));

@@ -90,9 +90,7 @@ class PassTimer:
     while the exchange runs on the side stream), ``exchange_wait`` (main
     stream blocked on the side stream after the interior: the part of the
     exchange the interior did not hide) and ``shell`` (the parts that read
-    the fresh ghosts; 0 when they run on the side stream next to the interior,
-    as plain blocked passes do: ``exchange_wait`` then covers exchange plus
-    shells beyond the interior).  HIP events on the GPU, wall clock on the CPU (where
+    the fresh ghosts).  HIP events on the GPU, wall clock on the CPU (where
     the gloo exchange is synchronous and lands in ``exchange_wait``)."""
 
     def __init__(self, device):
@@ -771,8 +769,8 @@ class BlockedStepping:
 
     def _tb_step(self, T: int) -> None:
         """``T`` steps in one blocked pass.  Decomposed runs overlap the
-        T-deep ghost exchange (side stream) and, after it on the same stream,
-        the shell slabs with the interior pass."""
+        T-deep ghost exchange (side stream) with the interior pass and run the
+        shell slabs after it."""
         upd, outs = self._tb_regions(T)
         srcs = self._pass_sources(self.t, T)
         tfs = [self._tfsf_pass(p, T) for p in range(self.planes)] if self.cfg.use_tfsf else [None] * self.planes
@@ -798,14 +796,6 @@ class BlockedStepping:
                     self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p], tfsf=tfs[p])
                 else:
                     self.ops.tb_step(self.F[p], self.F_alt[p], upd, ob, self.cb, T, srcs[p])
-            shells = [(lambda ob=ob, p=p: shell(ob, p)) for ob in outs[1:] for p in range(self.planes)]
-            # The shells follow the unpack on the (high-priority) exchange
-            # stream, side by side with the interior pass: they write other
-            # cells of F_alt and read F only, so nothing orders them after the
-            # interior, and they fill the CUs its last round leaves idle.  The
-            # main stream joins at the pass end (the next pass reads them).
-            # A Drude pass overwrites cells that may lie in a shell: after it.
-            conc = side is not None and self.drude_blk is None
             if side is not None and self.prof.enabled:
                 with torch.cuda.stream(side):
                     with self.prof.phase("halo-overlapped"):
@@ -813,16 +803,17 @@ class BlockedStepping:
             else:
                 with self.prof.phase("halo-overlapped"):
                     self.halo.exchange_all(self, stream=side)
-            if conc:
-                with torch.cuda.stream(side):
-                    with self.prof.phase("blocked-shells"):
-                        for f in shells:
-                            f()
             self._join_side(side)
             self._mark("wait")
-            if not conc:
-                with self.prof.phase("blocked-shells"):
-                    self._par_launches(shells, decomposed_ok=True)
+            # in order on the main stream: side by side with the interior
+            # (on the exchange stream after the unpack) the shells' small
+            # workgroups fragment the CUs the interior's one-per-CU workgroups
+            # need (4x2x1 0.646 vs 0.632 ms a step), and on three streams of
+            # their own they gain nothing (profiles/decomp_r5.md)
+            with self.prof.phase("blocked-shells"):
+                for ob in outs[1:]:
+                    for p in range(self.planes):
+                        shell(ob, p)
             self._mark("end")
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]

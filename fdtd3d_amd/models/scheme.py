@@ -1063,16 +1063,15 @@ class YeeScheme(BlockedStepping):
             for c in comps:
                 self._upml_rotate(c, p)
 
-    def _par_launches(self, fns, decomposed_ok: bool = False) -> None:
+    def _par_launches(self, fns) -> None:
         """Run independent launch callables round-robin on ``--shell-streams``
         HIP streams (the current one first), joined back into the current
         stream: the tail of one small window launch overlaps the next instead
-        of idling CUs.  HIP path only; decomposed runs only where the caller
-        says the launches touch no exchange buffer (``decomposed_ok``)."""
+        of idling CUs.  Serial runs on the HIP path only."""
         n = int(getattr(self.cfg, "shell_streams", 0))
         if n <= 0:
             n = 3 if self.ops.name == "hip" else 1
-        if (n <= 1 or len(fns) <= 1 or (self.halo is not None and not decomposed_ok) or self.device.type != "cuda"
+        if (n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda"
                 or getattr(self, "_capturing", False)):
             for f in fns:
                 f()

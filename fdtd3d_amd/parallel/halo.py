@@ -282,6 +282,20 @@ class HaloExchanger:
             sbox, rbox = d.to_local(sg), d.to_local(rg)
             key = (off[0] + 1) * 9 + (off[1] + 1) * 3 + (off[2] + 1)
             back = (-off[0] + 1) * 9 + (-off[1] + 1) * 3 + (-off[2] + 1)
+            if off[1] == 0 and off[2] == 0 and not boxed and self.direct_x_faces:
+                # x faces: x is the slowest axis, so B whole allocated planes
+                # of an array are one contiguous slice -- sent from and received
+                # into the arrays themselves, no pack / unpack kernels.  The
+                # planes carry the sender's y / z ghost rows too; the edge and
+                # corner messages, unpacked after every transfer has landed,
+                # overwrite those parts of the receiver's ghost planes (peers of
+                # one rank column share the allocated y / z extents).
+                for i, t in enumerate(tensors):
+                    ops_list.append(P2P(True, t[sbox[0][0]:sbox[1][0]], peer, 1000 + 32 * i + key))
+                    ops_list.append(P2P(False, t[rbox[0][0]:rbox[1][0]], peer, 1000 + 32 * i + back))
+                    self.bytes_sent += t[sbox[0][0]:sbox[1][0]].numel() * t.element_size()
+                    self.messages += 1
+                continue
             sb = self._buf(("xs", key), _msg_len(tensors, boxed, sg), tensors[0])
             _pack_state(ops, tensors, boxed, sbox, sg, d, sb)
             rb = self._buf(("xr", key), _msg_len(tensors, boxed, rg), tensors[0])
@@ -301,6 +315,7 @@ class HaloExchanger:
             _unpack_state(ops, tensors, boxed, rbox, rg, d, rb)
 
     debug_delay_cycles = 0
+    direct_x_faces = True  # x-face messages straight from / into the arrays (no pack / unpack)
 
     def _exchange_sweep(self, scheme) -> None:
         d = self.domain

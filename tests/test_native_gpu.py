@@ -238,9 +238,10 @@ def test_native_ntff_matches_python(dtype, gpu):
         assert abs(x - y) <= tol * peak, (h, x, y, peak)
 
 
-# x-slab parallel grids of the native driver (csrc/main.cpp run_multi): 3 / 4 ranks of one process on one
-# GPU (ghost planes by device copies; peer xGMI copies on a multi-GPU node), 23 steps = passes + a tail;
-# the 4-rank case puts the source on a rank's first plane (its lower neighbour's ghosts hold it too)
+# parallel grids of the native driver (csrc/native_multi.h run_multi): 3 / 4 / 8 ranks of one process on one
+# GPU (ghost boxes packed, copied and unpacked on the device; peer xGMI copies on a multi-GPU node), 23 steps =
+# passes + a tail; x slabs, x-y and x-z grids (edge messages) and a 2x2x2 grid (corner messages); the 4-rank x
+# case puts the source on a rank's first plane (its lower neighbour's ghosts hold it too)
 MULTI = {
     "f32_vacuum_3ranks": ["--3d", "--sizex", "40", "--sizey", "24", "--sizez", "32", "--time-steps", "23",
                           "--scene", "vacuum", "--parallel-grid", "--topology-sizex", "3", "--dtype", "f32"],
@@ -248,6 +249,16 @@ MULTI = {
                           "--scene", "sphere", "--sphere-center-x", "17", "--sphere-center-y", "10",
                           "--sphere-center-z", "12", "--sphere-radius", "5", "--sphere-eps", "3", "--parallel-grid",
                           "--topology-sizex", "4", "--time-block", "3", "--dtype", "f64"],
+    "f32_vacuum_2x2x1": ["--3d", "--sizex", "40", "--sizey", "36", "--sizez", "32", "--time-steps", "23",
+                         "--scene", "vacuum", "--parallel-grid", "--topology-sizex", "2", "--topology-sizey", "2",
+                         "--dtype", "f32"],
+    "f32_sphere_2x1x2": ["--3d", "--sizex", "36", "--sizey", "24", "--sizez", "40", "--time-steps", "23",
+                         "--scene", "sphere", "--sphere-center-x", "18", "--sphere-center-y", "11",
+                         "--sphere-center-z", "19", "--sphere-radius", "6", "--sphere-eps", "3", "--parallel-grid",
+                         "--topology-sizex", "2", "--topology-sizez", "2", "--time-block", "4", "--dtype", "f32"],
+    "f64_vacuum_2x2x2": ["--3d", "--sizex", "28", "--sizey", "24", "--sizez", "32", "--time-steps", "23",
+                         "--scene", "vacuum", "--parallel-grid", "--topology-sizex", "2", "--topology-sizey", "2",
+                         "--topology-sizez", "2", "--time-block", "3", "--dtype", "f64"],
 }
 
 
@@ -261,12 +272,15 @@ def test_native_parallel_grid_matches_python(case, tmp_path, gpu):
     pd.mkdir()
     r = subprocess.run([exe] + argv + ["--output-dir", str(nd)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "Parallel grid: 1" in r.stdout and "x-slab ghost planes" in r.stdout, r.stdout
-    ranks = int(argv[argv.index("--topology-sizex") + 1])
-    assert "Number of processes: %d" % ranks in r.stdout
+    assert "Parallel grid: 1" in r.stdout and "26-neighbour ghost boxes" in r.stdout, r.stdout
+    ranks = 1
     serial = [a for a in argv if a not in ("--parallel-grid",)]
-    i = serial.index("--topology-sizex")
-    serial = serial[:i] + serial[i + 2:]
+    for flag in ("--topology-sizex", "--topology-sizey", "--topology-sizez"):
+        if flag in serial:
+            i = serial.index(flag)
+            ranks *= int(serial[i + 1])
+            serial = serial[:i] + serial[i + 2:]
+    assert "Number of processes: %d" % ranks in r.stdout
     i = serial.index("--dtype")
     dtype = serial[i + 1]
     serial = serial[:i] + serial[i + 2:]
