@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -27,19 +28,21 @@ namespace {
 // each rank runs the temporally blocked kernel over its owned cells, reading
 // T-deep ghosts (the pass's dependency cone); then it packs, for each of its
 // up to 26 face / edge / corner neighbours, the owned T-deep box that
-// neighbour holds as ghosts (one kernel, six components), and each rank pulls
-// its neighbours' packed boxes (xGMI peer copies between devices) and unpacks
-// them into its ghosts -- the direct 26-neighbour exchange of
-// parallel/halo.py, point-to-point only, the shape of the node's xGMI links.
-// Events order the streams: a neighbour's pull waits for the pack, a rank's
-// next pack waits for its neighbours' pulls of the previous one.  Plain Yee
+// neighbour holds as ghosts (one kernel, six components); at the next pass
+// each rank pulls its neighbours' packed boxes (xGMI peer copies between
+// devices) and unpacks them into its ghosts on a side stream while its main
+// stream runs the interior (cells that need no fresh ghost), then the
+// T-thick shells -- the direct 26-neighbour exchange of parallel/halo.py
+// overlapped as models/blocking.py _tb_step does, point-to-point only, the
+// shape of the node's xGMI links.  Plain Yee
 // media (vacuum / dielectric sphere) with the point source; the reference's
 // MPI grid: Source/Grid/ParallelGrid.cpp:1600-1823 (exchange), :2161-2194.
 template <typename T>
 struct XRank {
   int dev = 0;
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr, side = nullptr;  // passes / ghost pulls
   hipEvent_t done = nullptr, copied = nullptr;
+  std::vector<std::array<int, 6>> outs;      // output boxes of a pass: interior, then the shells
   int crd[3] = {0, 0, 0};
   int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // owned global range
   int g0[3] = {0, 0, 0}, n[3] = {0, 0, 0};   // allocated box (ghosts included): global origin, extent
@@ -102,6 +105,7 @@ int run_multi(const fdtd::Settings& s) {
     q.dev = r % ndev;
     HIP_OK(hipSetDevice(q.dev));
     HIP_OK(hipStreamCreate(&q.st));
+    HIP_OK(hipStreamCreate(&q.side));
     HIP_OK(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&q.copied, hipEventDisableTiming));
     const size_t n = q.cells();
@@ -191,9 +195,62 @@ int run_multi(const fdtd::Settings& s) {
     if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
     return std::sin(dt * t * 2 * kPi * freq);
   };
+  // output boxes of a pass (local indices): the interior (owned cells at
+  // least TB from every neighbour: needs no fresh ghost) first, then the
+  // TB-thick shell slabs peeled off axis by axis (models/blocking.py _tb_regions)
+  for (XRank<T>& q : R) {
+    int lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = q.lo[a] - q.g0[a];
+      hi[a] = q.hi[a] - q.g0[a];
+    }
+    std::vector<std::array<int, 6>> sh;
+    for (int a = 0; a < 3; ++a)
+      for (int side = 0; side < 2; ++side) {
+        if ((side == 0 ? q.crd[a] == 0 : q.crd[a] == Pd[a] - 1)) continue;
+        std::array<int, 6> b = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
+        if (side == 0) {
+          b[3 + a] = lo[a] + TB;
+          lo[a] += TB;
+        } else {
+          b[a] = hi[a] - TB;
+          hi[a] -= TB;
+        }
+        sh.push_back(b);
+      }
+    q.outs.push_back({lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
+    for (const auto& b : sh) q.outs.push_back(b);
+  }
   bool first = true;
-  // k steps on every rank, the packs, then the ghost pulls
+  // One pass of k steps.  Phase 1, every rank on its side stream: pull the
+  // neighbours' packs of the previous pass (after their `done` and its own,
+  // which orders the ghost writes after the passes that read them) and
+  // unpack them into the ghosts.  Phase 2, on the main stream: the interior
+  // -- concurrent with phase 1, it reads no ghost -- then, after the pulls,
+  // the shells, and the packs for the next pass once the neighbours have
+  // pulled this pass's (their `copied`).  The phases are issued rank after
+  // rank on the host, so every event waited on is already recorded.
   auto pass = [&](int t, int k) {
+    if (!first)
+      for (int r = 0; r < P; ++r) {
+        XRank<T>& q = R[r];
+        HIP_OK(hipSetDevice(q.dev));
+        HIP_OK(hipStreamWaitEvent(q.side, q.done, 0));
+        T* f[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
+        for (int d = 0; d < 27; ++d) {
+          if (q.nb[d] < 0) continue;
+          const XRank<T>& o = R[q.nb[d]];
+          HIP_OK(hipStreamWaitEvent(q.side, o.done, 0));
+          // the neighbour at d packed its box for direction 26 - d (towards us)
+          const size_t bytes = q.rbuf[d].n * sizeof(T);
+          if (o.dev == q.dev)
+            HIP_OK(hipMemcpyAsync(q.rbuf[d].p, o.sbuf[26 - d].p, bytes, hipMemcpyDeviceToDevice, q.side));
+          else
+            HIP_OK(hipMemcpyPeerAsync(q.rbuf[d].p, q.dev, o.sbuf[26 - d].p, o.dev, bytes, q.side));
+          K_OK(box_unpack(f, q.rbuf[d].p, 6, q.n[1], q.n[2], q.rbox[d], q.side));
+        }
+        HIP_OK(hipEventRecord(q.copied, q.side));
+      }
     for (int r = 0; r < P; ++r) {
       XRank<T>& q = R[r];
       HIP_OK(hipSetDevice(q.dev));
@@ -210,17 +267,18 @@ int run_multi(const fdtd::Settings& s) {
       const int src[4] = {sp[0] - q.g0[0], sp[1] - q.g0[1], sp[2] - q.g0[2], has ? 2 : -1};
       double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
-      int ob[6];
-      for (int a = 0; a < 3; ++a) {
-        ob[a] = q.lo[a] - q.g0[a];
-        ob[3 + a] = q.hi[a] - q.g0[a];
+      for (size_t b = 0; b < q.outs.size(); ++b) {
+        const int* ob = q.outs[b].data();
+        if (b == 1 && !first) HIP_OK(hipStreamWaitEvent(q.st, q.copied, 0));  // the shells read the fresh ghosts
+        if (ob[3] <= ob[0] || ob[4] <= ob[1] || ob[5] <= ob[2]) continue;
+        if constexpr (sizeof(T) == 4)
+          K_OK(fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes,
+                                ob, 0, k, src, vals, q.st));
+        else
+          K_OK(fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes, ob,
+                             0, k, src, vals, q.st));
       }
-      if constexpr (sizeof(T) == 4)
-        K_OK(fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes, ob,
-                              0, k, src, vals, q.st));
-      else
-        K_OK(fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes, ob, 0,
-                           k, src, vals, q.st));
+      if (!first && q.outs.size() == 1) HIP_OK(hipStreamWaitEvent(q.st, q.copied, 0));  // a lone rank
       for (int c = 0; c < 6; ++c) std::swap(q.F[c].p, q.G[c].p);
       // the neighbours have pulled the previous packs before these overwrite them
       if (!first)
@@ -230,24 +288,6 @@ int run_multi(const fdtd::Settings& s) {
       for (int d = 0; d < 27; ++d)
         if (q.nb[d] >= 0) K_OK(box_pack(f, q.sbuf[d].p, 6, q.n[1], q.n[2], q.sbox[d], q.st));
       HIP_OK(hipEventRecord(q.done, q.st));
-    }
-    for (int r = 0; r < P; ++r) {
-      XRank<T>& q = R[r];
-      HIP_OK(hipSetDevice(q.dev));
-      T* f[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
-      for (int d = 0; d < 27; ++d) {
-        if (q.nb[d] < 0) continue;
-        const XRank<T>& o = R[q.nb[d]];
-        HIP_OK(hipStreamWaitEvent(q.st, o.done, 0));
-        // the neighbour at d packed its box for direction 26 - d (towards us)
-        const size_t bytes = q.rbuf[d].n * sizeof(T);
-        if (o.dev == q.dev)
-          HIP_OK(hipMemcpyAsync(q.rbuf[d].p, o.sbuf[26 - d].p, bytes, hipMemcpyDeviceToDevice, q.st));
-        else
-          HIP_OK(hipMemcpyPeerAsync(q.rbuf[d].p, q.dev, o.sbuf[26 - d].p, o.dev, bytes, q.st));
-        K_OK(box_unpack(f, q.rbuf[d].p, 6, q.n[1], q.n[2], q.rbox[d], q.st));
-      }
-      HIP_OK(hipEventRecord(q.copied, q.st));
     }
     first = false;
   };
@@ -339,6 +379,7 @@ int run_multi(const fdtd::Settings& s) {
     HIP_OK(hipEventDestroy(q.done));
     HIP_OK(hipEventDestroy(q.copied));
     HIP_OK(hipStreamDestroy(q.st));
+    HIP_OK(hipStreamDestroy(q.side));
   }
   return 0;
 }

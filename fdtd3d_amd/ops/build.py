@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import glob
+import re
 import os
 import shutil
 import subprocess
@@ -40,6 +41,28 @@ HOST_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 
 def _headers() -> List[str]:
     return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc"))
+
+
+_INCLUDE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _deps(src: str, seen=None) -> List[str]:
+    """``src`` plus the in-tree headers it includes, transitively (a change
+    to the native driver's headers then rebuilds main.cpp only)."""
+    seen = set() if seen is None else seen
+    if src in seen:
+        return []
+    seen.add(src)
+    out = [src]
+    try:
+        text = open(src).read()
+    except OSError:
+        return out
+    for name in _INCLUDE.findall(text):
+        h = os.path.join(CSRC, name)
+        if os.path.exists(h):
+            out += _deps(h, seen)
+    return out
 
 
 def _stale(target: str, deps: List[str]) -> bool:
@@ -70,11 +93,10 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, exe: bool =
           hip: bool = True) -> None:
     """Incremental build; ``hip=False`` builds only the host library."""
     os.makedirs(BUILD_DIR, exist_ok=True)
-    hdrs = _headers()
 
     def obj(src: str, hip: bool) -> str:
         o = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
-        if force or _stale(o, [src] + hdrs):
+        if force or _stale(o, _deps(src)):
             cc = HIPCC if hip else "g++"
             flags = HIP_FLAGS if hip else HOST_FLAGS
             cmd = [cc] + flags + ["-I", CSRC, "-c", src, "-o", o]
