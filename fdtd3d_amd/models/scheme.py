@@ -1003,6 +1003,10 @@ class YeeScheme(BlockedStepping):
         cpml_once = (self.use_cpml and not fused_cpml and self.hybrid is not None and len(windows) > 1
                      and self.halo is None)
 
+        # built (first call: device tensors) on the current stream BEFORE the
+        # window launches fork onto the shell streams, which would not wait for it
+        ktab = self.cpml.kernel_table(kind, p) if fused_cpml else None
+
         def one(w):
             if chain:
                 self._update_chain_regions(kind, p, w, tfsf_here)
@@ -1014,7 +1018,7 @@ class YeeScheme(BlockedStepping):
                 return
             if fused_cpml:
                 # CPML folded into the update kernel (yee3d_cpml.hip)
-                self.ops.curl_update_cpml(kind, boxes, F, F, self.cb, self.cpml.kernel_table(kind, p))
+                self.ops.curl_update_cpml(kind, boxes, F, F, self.cb, ktab)
             else:
                 self.ops.curl_update(kind, boxes, F, F, self.cb)
                 if self.use_cpml and not cpml_once:
@@ -1067,7 +1071,9 @@ class YeeScheme(BlockedStepping):
         """Run independent launch callables round-robin on ``--shell-streams``
         HIP streams (the current one first), joined back into the current
         stream: the tail of one small window launch overlaps the next instead
-        of idling CUs.  Serial runs on the HIP path only."""
+        of idling CUs.  Serial runs on the HIP path only.  The side streams
+        fork before the first launch, so a callable must not create device
+        data others read (lazy tables): build those before the call."""
         n = int(getattr(self.cfg, "shell_streams", 0))
         if n <= 0:
             n = 3 if self.ops.name == "hip" else 1
