@@ -47,6 +47,8 @@
 #include "native_api.h"
 #include "native_setup.h"
 #include "native_ckpt.h"
+#include "native_amp.h"
+#include "native_lowdim.h"
 
 namespace {
 
@@ -300,113 +302,14 @@ int run(const fdtd::Settings& s) {
       for (auto* l : tft.tab[c]) K_OK(tfsf_apply(F[c].p, *l, kind == 0 ? tft.hinc.p : tft.einc.p, whole, st));
   };
 
-  // 2D absorbing layers of one kind (0 = E) after / instead of the plain update
-  auto pml2d_cpml = [&](int kind) {
-    for (const Slab2d<T>& sl : p2.slabs) {
-      if ((sl.comp < 3) != (kind == 0)) continue;
-      const void* cp[4] = {nullptr, nullptr, nullptr, percell ? (const void*)C[sl.comp].p : nullptr};
-      K_OK(cpml_apply(F[sl.comp].p, F[sl.src].p, sl.psi, sl.axis, sl.sign, kind == 0 ? 1 : 0, sl.b, sl.c, sl.k,
-                      percell ? 1.0 : (kind == 0 ? cb : db), cp, N[1], N[2], sl.box, sl.pbox, st));
-    }
-  };
-  // 2D UPML half step: the D/B chain on the four PML strips (one cell of
-  // staggering slack inside), the plain 2D kernel on the inner box, where
-  // every sigma vanishes and the chain is the plain update to round-off (the
-  // strips' D levels are the only ones ever read)
-  const int ppx = s.pmlSizeX + 1, ppy = s.pmlSizeY + 1;
-  const IBox inner2 = {{ppx, ppy, 0}, {N[0] - ppx, N[1] - ppy, N[2]}};
-  const IBox strips2[4] = {{{0, 0, 0}, {std::min(ppx, N[0]), N[1], N[2]}},
-                           {{std::max(0, N[0] - ppx), 0, 0}, {N[0], N[1], N[2]}},
-                           {{ppx, 0, 0}, {N[0] - ppx, std::min(ppy, N[1]), N[2]}},
-                           {{ppx, std::max(0, N[1] - ppy), 0}, {N[0] - ppx, N[1], N[2]}}};
-  // the plain 2D kernels of one kind over the per-component update boxes
-  // clipped to `region`
-  auto plain2d = [&](int kind, const IBox& region) {
-    int ib[36];
-    for (int c = 0; c < 6; ++c) {
-      IBox ub;
-      for (int a = 0; a < 3; ++a) {
-        ub.lo[a] = boxes[6 * c + a];
-        ub.hi[a] = boxes[6 * c + 3 + a];
-      }
-      const IBox b = box_and(ub, region);
-      for (int a = 0; a < 3; ++a) {
-        ib[6 * c + a] = b.empty() ? 0 : b.lo[a];
-        ib[6 * c + 3 + a] = b.empty() ? 0 : b.hi[a];
-      }
-    }
-    const bool tm = scheme == "tmz";
-    if (kind == 0) {
-      if (tm)
-        K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], ib + 12, st));
-      else
-        K_OK(tez_e(F[0].p, F[1].p, F[5].p, C[0].p, C[1].p, percell ? 1.0 : cb, N[0], N[1], ib, st));
-    } else {
-      if (tm)
-        K_OK(tmz_h(F[3].p, F[4].p, F[2].p, C[3].p, C[4].p, percell ? 1.0 : db, N[0], N[1], ib + 18, st));
-      else
-        K_OK(tez_h(F[5].p, F[0].p, F[1].p, C[5].p, percell ? 1.0 : db, N[0], N[1], ib + 30, st));
-    }
-  };
-  // the D/B chain of one kind on the PML strips (+ level rotation)
-  auto upml2d_chain = [&](int kind) {
-    for (int c = 3 * kind; c < 3 * kind + 3; ++c) {
-      if (!present[c]) continue;
-      const T* srcs[2];
-      int axes[2], signs[2], nt = 0;
-      for (int q = 0; q < 2; ++q) {
-        const int sc = kCurl[c][q][0], ax = kCurl[c][q][1];
-        if (!present[sc] || ax >= 2) continue;
-        srcs[nt] = F[sc].p;
-        axes[nt] = ax;
-        signs[nt++] = kCurl[c][q][2];
-      }
-      IBox ub;
-      for (int a = 0; a < 3; ++a) {
-        ub.lo[a] = boxes[6 * c + a];
-        ub.hi[a] = boxes[6 * c + 3 + a];
-      }
-      const double sc3[3] = {1.0, p2.s[c], p2.s[c]};
-      const T* xs[3] = {F[c].p, p2.D[c][1], p2.D[c][0]};
-      for (const IBox& sb : strips2) {
-        const IBox b = box_and(sb, ub);
-        if (b.empty()) continue;
-        const int bx[6] = {b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2]};
-        K_OK(curl_gen(p2.D[c][1], p2.D[c][0], srcs, axes, signs, nt, kind == 0 ? 1 : 0, p2.ca[c], p2.cbp[c], N[1],
-                      N[2], bx, st));
-        K_OK(lincomb(F[c].p, 3, sc3, p2.lin[c], xs, N[1], N[2], bx, st));
-      }
-      std::swap(p2.D[c][0], p2.D[c][1]);
-    }
-  };
-  auto pml2d_upml = [&](int kind) {
-    upml2d_chain(kind);
-    plain2d(kind, inner2);  // every sigma vanishes there
-  };
-  // amplitude mode state: running maxima of every component, one [x][6][y][z]
-  // buffer (the layout of the blocked amplitude kernel), per-step changed
-  // counts, the Ez z-line source at (Nx/8, Ny/2, k outside the z PML) of 3D
-  // runs (Scheme3D.cpp:2995-3013)
-  bool amp_phase = false;
-  Dev<T> AMP;
-  Dev<unsigned> CNT;
-  Dev<long long> LINE;
-  int line_n = 0, line_k0 = 0;
+  // 2D PML half steps and the plain 2D kernels on boxes (native_lowdim.h)
+  Lowdim2d<T> ld(s, F, C, boxes, N, present, p2, scheme == "tmz", percell, cb, db, st);
+  const IBox& inner2 = ld.inner;
+
+  // amplitude mode state (native_amp.h): running maxima, changed counts, the 3D z-line source
+  AmpMode<T> ampm;
   const size_t plane = (size_t)N[1] * N[2];
-  if (amp) {
-    AMP.alloc((size_t)N[0] * 6 * plane);
-    CNT.alloc(std::max(1, s.amplitudeCheckSteps));
-    if (dim == 3 && point_src) {
-      line_k0 = s.doUsePML ? s.pmlSizeZ : 0;
-      std::vector<long long> offs;
-      for (int k = line_k0; k < N[2] - line_k0; ++k) offs.push_back(((long long)(N[0] / 8) * N[1] + N[1] / 2) * N[2] + k);
-      line_n = (int)offs.size();
-      if (line_n > 0) {
-        LINE.alloc(offs.size());
-        HIP_OK(hipMemcpy(LINE.p, offs.data(), offs.size() * sizeof(long long), hipMemcpyHostToDevice));
-      }
-    }
-  }
+  if (amp) ampm.init(s, N, dim == 3 && point_src);
 
   auto upml_regions = [&](int kind) {
     fptrs();
@@ -459,8 +362,8 @@ int run(const fdtd::Settings& s) {
         }
         if (tfsf) tfsf_kind(0);
         if (point_src) {
-          if (amp_phase && line_n > 0)  // the amplitude mode's Ez z-line replaces the point source
-            K_OK(setvs(F[2].p, LINE.p, line_n, sv, st));
+          if (ampm.active && ampm.line_n > 0)  // the amplitude mode's Ez z-line replaces the point source
+            K_OK(setvs(F[2].p, ampm.LINE.p, ampm.line_n, sv, st));
           else
             K_OK(setv(F[src_comp].p, src_off, sv, st));
         }
@@ -484,17 +387,17 @@ int run(const fdtd::Settings& s) {
       const bool tm = scheme == "tmz";
       if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
       if (upml)
-        pml2d_upml(0);
+        ld.upml(0);
       else if (tm)
         K_OK(tmz_e(F[2].p, F[3].p, F[4].p, C[2].p, percell ? 1.0 : cb, N[0], N[1], boxes + 12, st));
       else
         K_OK(tez_e(F[0].p, F[1].p, F[5].p, C[0].p, C[1].p, percell ? 1.0 : cb, N[0], N[1], boxes, st));
-      if (cpml) pml2d_cpml(0);
+      if (cpml) ld.cpml(0);
       if (tfsf) tfsf_kind(0);
       if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));  // hard source between the E and H updates
       if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
       if (upml) {
-        pml2d_upml(1);
+        ld.upml(1);
       } else if (tm) {
         int hb[12];
         std::memcpy(hb, boxes + 18, 12 * sizeof(int));
@@ -502,7 +405,7 @@ int run(const fdtd::Settings& s) {
       } else {
         K_OK(tez_h(F[5].p, F[0].p, F[1].p, C[5].p, percell ? 1.0 : db, N[0], N[1], boxes + 30, st));
       }
-      if (cpml) pml2d_cpml(1);
+      if (cpml) ld.cpml(1);
       if (tfsf) tfsf_kind(1);
     } else {
       K_OK(e1d(F[2].p, F[4].p, C[2].p, percell ? 1.0 : cb, boxes[12], boxes[15], st));
@@ -744,21 +647,21 @@ int run(const fdtd::Settings& s) {
       const double sv = src_val(t + q);
       if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
       if (upml) {
-        upml2d_chain(0);
-        for (const IBox& w : h2shell[q]) plain2d(0, box_and(w, inner2));
+        ld.upml_chain(0);
+        for (const IBox& w : h2shell[q]) ld.plain(0, box_and(w, inner2));
       } else {
-        for (const IBox& w : h2shell[q]) plain2d(0, w);
-        pml2d_cpml(0);
+        for (const IBox& w : h2shell[q]) ld.plain(0, w);
+        ld.cpml(0);
       }
       if (tfsf) tfsf_kind(0);
       if (point_src) K_OK(setv(F[src_comp].p, src_off, sv, st));
       if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
       if (upml) {
-        upml2d_chain(1);
-        for (const IBox& w : h2shell[q]) plain2d(1, box_and(w, inner2));
+        ld.upml_chain(1);
+        for (const IBox& w : h2shell[q]) ld.plain(1, box_and(w, inner2));
       } else {
-        for (const IBox& w : h2shell[q]) plain2d(1, w);
-        pml2d_cpml(1);
+        for (const IBox& w : h2shell[q]) ld.plain(1, w);
+        ld.cpml(1);
       }
       if (tfsf) tfsf_kind(1);
     }
@@ -1127,92 +1030,19 @@ int run(const fdtd::Settings& s) {
   HIP_OK(hipEventRecord(e0, st));
   ckpt_ms = 0.0;  // warm-up checkpoints are outside the timed region anyway
   run_ckpt(t0 + warm, steps - warm);
-  // amplitude mode (models/scheme.py perform_amplitude_steps): check periods
-  // of K steps whose changed-cell counts accumulate on the device, read once
-  // per period; the run ends with the period in which a step (after the
-  // first) changed no running maximum, or after --amplitude-time-steps steps
-  int t_end = t0 + steps, amp_taken = 0, amp_stable = -1;
+  // amplitude mode (native_amp.h): after the regular steps, check periods
+  // until a step changes no running maximum
+  int t_end = t0 + steps;
   if (amp) {
-    amp_phase = true;
-    const int K = std::max(1, s.amplitudeCheckSteps);
-    // amplitude box per component: its update box minus the PML cells
-    // (Scheme3D.cpp:3016-3030); only present components
-    int ab[36] = {}, na = 0;
-    const T* af[6];
-    T* aa[6];
-    for (int c = 0; c < 6; ++c) {
-      int* b = ab + 6 * c;
-      for (int q = 0; q < 6; ++q) b[q] = boxes[6 * c + q];
-      const int left[3] = {s.doUsePML ? s.pmlSizeX : 0, s.doUsePML ? s.pmlSizeY : 0, s.doUsePML ? s.pmlSizeZ : 0};
-      for (int a : active) {
-        const int right = N[a] - left[a];
-        if (left[a] == right) continue;
-        b[a] = std::max(b[a], (int)std::ceil(left[a] - kMinFP[c][a]));
-        b[3 + a] = std::min(b[3 + a], (int)std::ceil(right - kMinFP[c][a]));
-      }
-    }
-    int abp[36];
-    for (int c = 0; c < 6; ++c)
-      if (present[c]) {
-        af[na] = F[c].p;
-        aa[na] = AMP.p + c * plane;
-        std::memcpy(abp + 6 * na, ab + 6 * c, 6 * sizeof(int));
-        ++na;
-      }
-    // blocked passes with the amplitude update folded in (tb3d_mr.h AmpDev):
-    // 3D vacuum fp32 float4 rows, no absorbing layer / TF/SF / NTFF
-    const int Ta = (scheme == "3d" && sizeof(T) == 4 && v4 && !percell && !cpml && !upml && !tfsf && !ntff &&
-                    line_n > 0 && !s.doUseSplitKernels)
-                       ? 3
-                       : 1;
-    if (Ta > 1)
-      for (int c = 0; c < 6; ++c)
-        if (!G[c].p) G[c].alloc(cells);
-    std::vector<unsigned> got(K);
-    int t = t0 + steps;
-    // one check period of n steps: blocked amplitude passes where they apply,
-    // per-step stepping + the fused amplitude kernel otherwise; returns the
-    // per-step changed counts
-    auto period = [&](int n) {
-      HIP_OK(hipMemsetAsync(CNT.p, 0, K * sizeof(unsigned), st));
-      int q = 0;
-      while (q < n) {
-        if (Ta > 1 && n - q >= 2) {
-          if constexpr (sizeof(T) == 4) {
-            const int k = std::min(Ta, n - q);
-            const T* ei[3] = {F[0].p, F[1].p, F[2].p};
-            const T* hi[3] = {F[3].p, F[4].p, F[5].p};
-            T* eo[3] = {G[0].p, G[1].p, G[2].p};
-            T* ho[3] = {G[3].p, G[4].p, G[5].p};
-            const int ob[6] = {0, 0, 0, N[0], N[1], N[2]};
-            const int src5[5] = {N[0] / 8, N[1] / 2, line_k0, 2, line_k0 + line_n};
-            double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
-            K_OK(fdtd_tb3d_amp_f32(ei, hi, eo, ho, cb, db, N[0], N[1], N[2], boxes, ob, 0, k, src5, vals, aa, ab,
-                                   0.001, CNT.p + q, st));
-            for (int c = 0; c < 6; ++c) std::swap(F[c].p, G[c].p);
-            for (int c = 0; c < 6; ++c) af[c] = F[c].p;
-            q += k;
-            t += k;
-            continue;
-          }
-        }
-        step(t);
-        K_OK(amp_many(af, aa, na, N[1], N[2], abp, (long long)(6 * plane), 0.001, CNT.p + q, st));
-        ++q;
-        ++t;
-      }
-      HIP_OK(hipMemcpyAsync(got.data(), CNT.p, n * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-    };
-    // every array that carries state between steps, in logical order (the
-    // current F / D level lists, whatever the pointer swaps did): the
-    // near-convergence snapshot (models/scheme.py perform_amplitude_steps)
+    // blocked amplitude passes: 3D vacuum fp32 float4 rows, no absorbing layer / TF/SF / NTFF
+    const bool blocked = scheme == "3d" && sizeof(T) == 4 && v4 && !percell && !cpml && !upml && !tfsf && !ntff &&
+                         ampm.line_n > 0 && !s.doUseSplitKernels;
+    // every other array that carries state between steps, in logical order
+    // (the current F / D level lists, whatever the pointer swaps did)
     auto state = [&]() {
       std::vector<std::pair<void*, size_t>> v;
       for (int c = 0; c < 6; ++c)
         if (present[c]) v.push_back({F[c].p, cells * sizeof(T)});
-      v.push_back({AMP.p, (size_t)N[0] * 6 * plane * sizeof(T)});
       if (tfsf) {
         v.push_back({tft.einc.p, (size_t)tft.nline * sizeof(T)});
         v.push_back({tft.hinc.p, (size_t)tft.nline * sizeof(T)});
@@ -1232,57 +1062,7 @@ int run(const fdtd::Settings& s) {
       }
       return v;
     };
-    long long acells = 0;
-    for (int c = 0; c < na; ++c) {
-      const int* b = abp + 6 * c;
-      acells += (long long)std::max(0, b[3] - b[0]) * std::max(0, b[4] - b[1]) * std::max(0, b[5] - b[2]);
-    }
-    const long long near = std::max(1LL, (long long)(0.02 * (double)acells));
-    Dev<char> SNAP;
-    long long last = -1;
-    bool done = false;
-    while (!done && amp_taken < s.numAmplitudeTimeSteps) {
-      int n = std::min(K, s.numAmplitudeTimeSteps - amp_taken);
-      int t_snap = -1;
-      if (n > 1 && last >= 0 && last <= near) {
-        const auto v = state();
-        size_t total = 0;
-        for (const auto& e : v) total += e.second;
-        if (!SNAP.p) SNAP.alloc(total);
-        size_t o = 0;
-        for (const auto& e : v) {
-          HIP_OK(hipMemcpyAsync(SNAP.p + o, e.first, e.second, hipMemcpyDeviceToDevice, st));
-          o += e.second;
-        }
-        t_snap = t;
-      }
-      period(n);
-      int first = -1;
-      for (int r = 0; r < n && first < 0; ++r)
-        if (got[r] == 0 && amp_taken + r + 1 > 1) first = r;
-      if (first < 0) {
-        last = got[n - 1];
-        amp_taken += n;
-        continue;
-      }
-      amp_stable = amp_taken + first + 1;
-      if (first + 1 < n && t_snap >= 0) {
-        // back to the period's start, then exactly the steps up to the stable one
-        const auto v = state();
-        size_t o = 0;
-        for (const auto& e : v) {
-          HIP_OK(hipMemcpyAsync(e.first, SNAP.p + o, e.second, hipMemcpyDeviceToDevice, st));
-          o += e.second;
-        }
-        t = t_snap;
-        n = first + 1;
-        period(n);
-      }
-      amp_taken += n;
-      done = true;
-    }
-    amp_phase = false;
-    t_end = t;
+    t_end = ampm.run(s, N, active, present, boxes, F, G, blocked, cb, db, st, t0 + steps, src_val, step, state);
   }
   HIP_OK(hipEventRecord(e1, st));
   HIP_OK(hipEventSynchronize(e1));
@@ -1300,7 +1080,7 @@ int run(const fdtd::Settings& s) {
     std::printf("Grid size: %dx%d\n", N[0], N[1]);
   else
     std::printf("Grid size: %d\n", N[0]);
-  const int timed = steps - warm + amp_taken;
+  const int timed = steps - warm + ampm.taken;
   std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", t_end, timed, warm);
   std::printf("Value type: %s\n", Api<T>::name);
   std::printf("\n-------- Details --------\n");
@@ -1323,10 +1103,10 @@ int run(const fdtd::Settings& s) {
     std::printf("Backend: native HIP, %s kernels%s\n", use_fused ? "fused E+H" : "split", v4 ? " (float4)" : "");
   std::printf("Throughput: %.1f Mcells/s\n", cells * (double)timed / sec / 1e6);
   if (amp) {
-    if (amp_stable > 0)
-      std::printf("Amplitude mode: stable after %d steps (%d amplitude steps taken)\n", amp_stable, amp_taken);
+    if (ampm.stable > 0)
+      std::printf("Amplitude mode: stable after %d steps (%d amplitude steps taken)\n", ampm.stable, ampm.taken);
     else
-      std::printf("Amplitude mode: stable state not reached after %d steps\n", amp_taken);
+      std::printf("Amplitude mode: stable state not reached after %d steps\n", ampm.taken);
   }
   if (s.doPrintJson)
     std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f}\n", sec, timed,
@@ -1385,35 +1165,7 @@ int main(int argc, char** argv) {
     std::fprintf(stdout, "ERROR: %s\n", s.message.c_str());
     return 1;
   }
-  // CPML absorbing layers: 3D fp32 with whole float4 z rows (the folded
-  // float4 kernels), 2D in either precision (generic slab kernels)
-  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && !s.doUseMetamaterials &&
-                       ((s.dimension == 3 && s.valueType == "f32" && s.sizeZ % 4 == 0) || s.dimension == 2);
-  // UPML (D/B chain) and Drude / Lorentz spheres: 3D, any precision; the 2D UPML without dispersive media
-  const bool upml_ok = s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials) &&
-                       (s.dimension == 3 || (s.dimension == 2 && !s.doUseMetamaterials));
-  const bool meta_ok = !s.doUseMetamaterials || (s.dimension == 3 && s.scene == "drude-sphere");
-  // TF/SF plane waves: 3D and 2D (any precision), with the CPML or the UPML;
-  // with the UPML the corrections take the E form, exact where every sigma
-  // vanishes: the TF/SF box must lie inside the absorbing layers' interior
-  bool tfsf_ok = s.doUseTFSF && s.dimension >= 2;
-  if (tfsf_ok && s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials))
-    tfsf_ok = s.tfsfSizeX > s.pmlSizeX + 1 && s.tfsfSizeY > s.pmlSizeY + 1 &&
-              (s.dimension == 2 || s.tfsfSizeZ > s.pmlSizeZ + 1);
-  const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
-  // amplitude mode: any scheme, not with the NTFF diagram
-  const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
-  // parallel grids: 3D plain media (vacuum / dielectric sphere) with the point source, any rank grid
-  const bool par_ok = !s.doUseParallelGrid ||
-                      (s.dimension == 3 && !s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials &&
-                       !s.doUseAmplitudeMode && !s.doUseNTFF && (s.scene == "vacuum" || s.scene == "sphere") &&
-                       !s.doUseSplitKernels);
-  // checkpoints / resume: plain media (state = the field components)
-  const bool ckpt = !s.checkpointDir.empty() || !s.loadFromFile.empty();
-  const bool ckpt_ok = !ckpt || (!s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials && !s.doUseAmplitudeMode &&
-                                 !s.doUseNTFF && !s.doUseParallelGrid);
-  if ((s.doUsePML && !cpml_ok && !upml_ok) || (s.doUseTFSF && !tfsf_ok) || !meta_ok || !ntff_ok || !amp_ok ||
-      !par_ok || !ckpt_ok || s.doUseComplexFieldValues || s.doUseDoubleMaterialPrecision) {
+  if (!native_supported(s)) {
     std::fprintf(stderr,
                  "fdtd3d (native): CPML in 3D outside fp32 float4 rows, PML / TF/SF in 1D, TF/SF boxes reaching "
                  "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "

@@ -560,4 +560,38 @@ int tfsf_apply(double* t, const TfsfLayer<double>& l, const double* inc, const i
   return fdtd_tfsf_apply_f64(t, l.off.p, l.i0.p, l.w0.p, l.w1.p, l.coef.p, nullptr, l.n, inc, box, s);
 }
 
+// The options this binary runs (everything else goes through the Python
+// driver, never a silent fallback).
+bool native_supported(const fdtd::Settings& s) {
+  // CPML absorbing layers: 3D fp32 with whole float4 z rows (the folded
+  // float4 kernels), 2D in either precision (generic slab kernels)
+  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && !s.doUseMetamaterials &&
+                       ((s.dimension == 3 && s.valueType == "f32" && s.sizeZ % 4 == 0) || s.dimension == 2);
+  // UPML (D/B chain) and Drude / Lorentz spheres: 3D, any precision; the 2D UPML without dispersive media
+  const bool upml_ok = s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials) &&
+                       (s.dimension == 3 || (s.dimension == 2 && !s.doUseMetamaterials));
+  const bool meta_ok = !s.doUseMetamaterials || (s.dimension == 3 && s.scene == "drude-sphere");
+  // TF/SF plane waves: 3D and 2D (any precision), with the CPML or the UPML;
+  // with the UPML the corrections take the E form, exact where every sigma
+  // vanishes: the TF/SF box must lie inside the absorbing layers' interior
+  bool tfsf_ok = s.doUseTFSF && s.dimension >= 2;
+  if (tfsf_ok && s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials))
+    tfsf_ok = s.tfsfSizeX > s.pmlSizeX + 1 && s.tfsfSizeY > s.pmlSizeY + 1 &&
+              (s.dimension == 2 || s.tfsfSizeZ > s.pmlSizeZ + 1);
+  const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
+  // amplitude mode: any scheme, not with the NTFF diagram
+  const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
+  // parallel grids: 3D plain media (vacuum / dielectric sphere) with the point source, any rank grid
+  const bool par_ok = !s.doUseParallelGrid ||
+                      (s.dimension == 3 && !s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials &&
+                       !s.doUseAmplitudeMode && !s.doUseNTFF && (s.scene == "vacuum" || s.scene == "sphere") &&
+                       !s.doUseSplitKernels);
+  // checkpoints / resume: plain media (state = the field components)
+  const bool ckpt = !s.checkpointDir.empty() || !s.loadFromFile.empty();
+  const bool ckpt_ok = !ckpt || (!s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials && !s.doUseAmplitudeMode &&
+                                 !s.doUseNTFF && !s.doUseParallelGrid);
+  return !((s.doUsePML && !cpml_ok && !upml_ok) || (s.doUseTFSF && !tfsf_ok) || !meta_ok || !ntff_ok || !amp_ok ||
+           !par_ok || !ckpt_ok || s.doUseComplexFieldValues || s.doUseDoubleMaterialPrecision);
+}
+
 }  // namespace
