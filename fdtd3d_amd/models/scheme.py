@@ -1077,6 +1077,9 @@ class YeeScheme(BlockedStepping):
         n = int(getattr(self.cfg, "shell_streams", 0))
         if n <= 0:
             n = 3 if self.ops.name == "hip" else 1
+        # decomposed runs in order: their deep-halo shell windows on three
+        # streams measured slower (2x2x1 of 512^3 CPML + TF/SF: 30.6k vs
+        # 35.3k Mcells/s per GPU, tools/gpu_r5_zi.sh)
         if (n <= 1 or len(fns) <= 1 or self.halo is not None or self.device.type != "cuda"
                 or getattr(self, "_capturing", False)):
             for f in fns:
