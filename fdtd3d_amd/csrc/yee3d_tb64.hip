@@ -309,16 +309,18 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
   store_out(i1 + T - 1);
 }
 
-// patch order of the XCD tile run: pz | (py << 8), 0 = z fastest;
-// FDTD3D_TB64_PATCH="PZxPY" at first use, fdtd_set_tb64_patch
+// patch order of the XCD tile run: pz | (py << 8), 0 = z fastest.  Default
+// 2 x 8 (z x y tiles): 1024^3 fp64 123.3k vs 118.3k Mcells/s z fastest, means
+// of 3 / 4 alternating runs (profiles/fp64_patch_r5.md); FDTD3D_TB64_PATCH=
+// "PZxPY" at first use ("0x0": z fastest), fdtd_set_tb64_patch
 int g_tb64_patch = -1;
 int tb64_patch() {
   if (g_tb64_patch < 0) {
-    g_tb64_patch = 0;
+    g_tb64_patch = 2 | (8 << 8);
     const char* e = getenv("FDTD3D_TB64_PATCH");
     int pz = 0, py = 0;
-    if (e && sscanf(e, "%dx%d", &pz, &py) == 2 && pz > 0 && py > 0 && pz < 256 && py < 256)
-      g_tb64_patch = pz | (py << 8);
+    if (e && sscanf(e, "%dx%d", &pz, &py) == 2 && pz >= 0 && py >= 0 && pz < 256 && py < 256)
+      g_tb64_patch = (pz > 0 && py > 0) ? (pz | (py << 8)) : 0;
   }
   return g_tb64_patch;
 }

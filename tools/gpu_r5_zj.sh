@@ -11,6 +11,13 @@ run() {
   env "$@" timeout -k 10 300 python bench.py $B $EXTRA > $O/$lab.log 2>&1 || { echo "$lab failed"; tail -3 $O/$lab.log; return 0; }
   echo "$lab $(tail -1 $O/$lab.log | grep -o '"value": [0-9.]*')"
 }
+if [ "${SWEEP:-1}" = 2 ]; then
+  for r in 1 2; do
+    run base_$r A=1
+    for p in 2x8 1x8 2x4 2x16 4x8 3x8 1x16; do run p${p}_$r FDTD3D_TB64_PATCH=$p; done
+  done
+  exit 0
+fi
 run base A=1
 run p4x4 FDTD3D_TB64_PATCH=4x4
 run p8x2 FDTD3D_TB64_PATCH=8x2
