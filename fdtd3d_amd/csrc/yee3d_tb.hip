@@ -320,7 +320,7 @@ constexpr int MR_AUTO_ROWS = 2;
 int g_tb_mrows = 0;  // rows per wave of the multi-row kernel: 0 automatic, 1 = single-row kernel, 2 / 4
 
 const int kNoBox[6] = {0, 0, 0, 0, 0, 0};
-int g_tb_mr_shape = 0;  // plain multi-row kernel: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
+int g_tb_mr_shape = 0;  // plain multi-row kernel: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows, 2 = 8 x 2
 int g_tb_dr_shape = 0;  // Drude variant: 0 = 8 waves x 2 rows, 1 = 16 waves x 1 row (both 16-row tiles)
 
 
@@ -369,6 +369,10 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
   // rows (2 waves / SIMD, <= 256 VGPRs: more rows of ILP per wave, half the
   // LDS row exchanges); both a 32-row tile
   if (g_tb_mr_shape == 1) return launch_tb_mr<T, 1, 4, 0, 8>(MR_ARGS);
+  // 8 waves x 2 rows (16-row tiles, two workgroups per CU): thin y boxes, the
+  // y shells of decomposed passes
+  if constexpr (T <= 5)
+    if (g_tb_mr_shape == 2) return launch_tb_mr<T, 1, 2, 0, 8>(MR_ARGS);
   return launch_tb_mr<T, 1, 2, 0>(MR_ARGS);
 #undef MR_ARGS
 }
@@ -377,9 +381,10 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
 int tb_mr_xchunk(int fx, const Box3& O, int steps) {
   const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
   // (the Drude variant's tiles are 8 waves x 2 rows)
-  const long long gy = cdiv(O.hi[1] - O.lo[1], (fx == 16 ? 16 : TBW * 2) - 2 * steps);
-  // the 8-wave shape fits two workgroups per CU
-  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape == 1) ? 2 : 1);
+  const bool rows16 = fx == 16 || (fx == 0 && g_tb_mr_shape == 2 && steps <= 5);
+  const long long gy = cdiv(O.hi[1] - O.lo[1], (rows16 ? 16 : TBW * 2) - 2 * steps);
+  // the 8-wave shapes fit two workgroups per CU
+  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape >= 1) ? 2 : 1);
 }
 
 // multi-row pass (scalar lanes, 2 rows per wave): uniform media, sparse
@@ -470,7 +475,7 @@ FDTD_API void fdtd_set_tb_patch(int pz, int py) {
 // Drude variant tile shape (tuning): 0 = 8 waves x 2 rows, 1 = 16 waves x 1 row
 FDTD_API void fdtd_set_tb_dr_shape(int v) { g_tb_dr_shape = v == 1 ? 1 : 0; }
 // plain multi-row tile shape (tuning): 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows
-FDTD_API void fdtd_set_tb_mr_shape(int v) { g_tb_mr_shape = v == 1 ? 1 : 0; }
+FDTD_API void fdtd_set_tb_mr_shape(int v) { g_tb_mr_shape = (v == 1 || v == 2) ? v : 0; }
 // largest steps-per-pass the blocked kernels accept
 FDTD_API int fdtd_tb_max_steps() { return 6; }
 

@@ -1036,13 +1036,18 @@ class HipOps:
             self.lib.fdtd_set_tb_rows(c_int(self.tb_rows))
             self.lib.fdtd_set_tb_xcd(c_int(self.tb_xcd))
             mr = self.tb_mrows
+            shape = self.tb_mr_shape
             if mr == 0 and self.tb_thin_single_row and steps <= 4 and obox[1][1] - obox[0][1] <= 8:
-                # thin y shells of a decomposed pass: the single-row kernel's
-                # 16-row tiles waste half as many rows as the 32-row multi-row tiles
-                mr = 1
+                # thin y shells of a decomposed pass: 16-row tiles waste half
+                # as many rows as the 32-row multi-row tiles -- the single-row
+                # kernel's, or the multi-row kernel's 8-wave form (tb_thin_mr16)
+                if self.tb_thin_mr16:
+                    shape = 2
+                else:
+                    mr = 1
             self.lib.fdtd_set_tb_mrows(c_int(mr))
             self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
-            self.lib.fdtd_set_tb_mr_shape(c_int(self.tb_mr_shape))
+            self.lib.fdtd_set_tb_mr_shape(c_int(shape))
         else:
             self.lib.fdtd_set_tb64_shape(c_int(self.tb64_half))
         # fp32: yee3d_tb.hip (multi-row / single-row tiles); fp64: yee3d_tb64.hip
@@ -1131,7 +1136,8 @@ class HipOps:
     tb_xcd = 0  # XCD-aware tile order (off: measured no gain)
     tb_variant = 4  # multi-row kernel: bit 0 deferred stores, bit 1 two planes prefetched, bit 2 XCD tile order
     tb_mrows = 0  # adjacent y rows per wave (multi-row kernel): 0 auto, 1 single-row kernel, 2
-    tb_thin_single_row = True  # auto mode: output boxes <= 8 rows in y use the single-row kernel
+    tb_thin_single_row = True  # auto mode: output boxes <= 8 rows in y use 16-row tiles
+    tb_thin_mr16 = os.environ.get("FDTD3D_TB_THIN_MR16", "0") == "1"  # ... of the multi-row kernel (else single-row)
     tb_sparse = True  # per-cell fp32 coefficients: sparse float4 boxes on the multi-row kernel
     # plain multi-row tile shape: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows (two workgroups per CU)
     tb_mr_shape = int(os.environ.get("FDTD3D_TB_MR_SHAPE", "0"))

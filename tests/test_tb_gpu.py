@@ -204,14 +204,17 @@ def test_tb_f64_scheme_matches_fused(gpu, T):
 
 
 @pytest.mark.parametrize("size,T,scene,obox,src", [c for c in CASES_MR if c[2] == "vacuum"])
-@pytest.mark.parametrize("variant", [0, 4])
-def test_tb_mr_shape8(gpu, size, T, scene, obox, src, variant):
-    """8-wave x 4-row tiles of the plain multi-row kernel (two workgroups per
-    CU) vs the fp64 torch oracle."""
+@pytest.mark.parametrize("variant,shape", [(0, 1), (4, 1), (0, 2)])
+def test_tb_mr_shape8(gpu, size, T, scene, obox, src, variant, shape):
+    """8-wave tiles of the plain multi-row kernel (two workgroups per CU):
+    x 4 rows (shape 1) and x 2 rows (shape 2, the 16-row tiles of thin y
+    boxes) vs the fp64 torch oracle."""
+    if shape == 2 and T > 5:
+        pytest.skip("16-row tiles: T <= 5")
     cfg = SchemeConfig(scheme="3d", size=size, scene=scene, dtype="f32", use_fused=True)
     a = _scheme(cfg, "hip", gpu, torch.float32)
     a.ops.tb_mrows = 2
-    a.ops.tb_mr_shape = 1
+    a.ops.tb_mr_shape = shape
     a.ops.tb_variant = variant
     b = _scheme(dataclasses.replace(cfg, dtype="f64"), "torch", "cpu", torch.float64)
     _randomize(a)
