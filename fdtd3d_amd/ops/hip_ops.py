@@ -1036,18 +1036,18 @@ class HipOps:
             self.lib.fdtd_set_tb_rows(c_int(self.tb_rows))
             self.lib.fdtd_set_tb_xcd(c_int(self.tb_xcd))
             mr = self.tb_mrows
-            shape = self.tb_mr_shape
+            mr_shape = self.tb_mr_shape
             if mr == 0 and self.tb_thin_single_row and steps <= 4 and obox[1][1] - obox[0][1] <= 8:
                 # thin y shells of a decomposed pass: 16-row tiles waste half
                 # as many rows as the 32-row multi-row tiles -- the single-row
                 # kernel's, or the multi-row kernel's 8-wave form (tb_thin_mr16)
                 if self.tb_thin_mr16:
-                    shape = 2
+                    mr_shape = 2
                 else:
                     mr = 1
             self.lib.fdtd_set_tb_mrows(c_int(mr))
             self.lib.fdtd_set_tb_variant(c_int(self.tb_variant))
-            self.lib.fdtd_set_tb_mr_shape(c_int(shape))
+            self.lib.fdtd_set_tb_mr_shape(c_int(mr_shape))
         else:
             self.lib.fdtd_set_tb64_shape(c_int(self.tb64_half))
         # fp32: yee3d_tb.hip (multi-row / single-row tiles); fp64: yee3d_tb64.hip
