@@ -282,7 +282,8 @@ class HaloExchanger:
             sbox, rbox = d.to_local(sg), d.to_local(rg)
             key = (off[0] + 1) * 9 + (off[1] + 1) * 3 + (off[2] + 1)
             back = (-off[0] + 1) * 9 + (-off[1] + 1) * 3 + (-off[2] + 1)
-            if off[1] == 0 and off[2] == 0 and not boxed and self.direct_x_faces:
+            if (off[1] == 0 and off[2] == 0 and not boxed and self.direct_x_faces
+                    and all(t.is_contiguous() for t in tensors)):
                 # x faces: x is the slowest axis, so B whole allocated planes
                 # of an array are one contiguous slice -- sent from and received
                 # into the arrays themselves, no pack / unpack kernels.  The
