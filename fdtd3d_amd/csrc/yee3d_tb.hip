@@ -276,12 +276,18 @@ int pick_xchunk(long long tiles_yz, int nxo, int T, int wg_per_cu = 1) {
   };
   long long rounds = 1;
   const int best = search(nxo, &rounds);
-  // A pass of several rounds balances better over the CUs with chunks of at
-  // most 256 planes than the uniform-workgroup model predicts (measured T=5:
-  // 1024^3 297k vs 288k Mcells/s at 256 vs 512 planes, 2048x1024x1024 293k vs
-  // 263k at 256 vs 1024); a one-round pass keeps its long chunks (512^3:
-  // 247k at 512 planes vs 236k at 256).
-  if (rounds >= 2 && best > 256) return search(256, &rounds);
+  // A pass of several rounds balances better over the CUs with shorter
+  // chunks than the uniform-workgroup model predicts (measured T=5: 1024^3
+  // 297k vs 288k Mcells/s at 256 vs 512 planes, 2048x1024x1024 293k vs 263k
+  // at 256 vs 1024; round 5: 1024^3 305.9k / 305.3k at 171 planes vs 302.4k /
+  // 302.4k at 256, profiles/validation_r5.md); a one-round pass keeps its long
+  // chunks (512^3: 247k at 512 planes vs 236k at 256).  FDTD3D_TB_XCAP: cap.
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("FDTD3D_TB_XCAP");
+    cap = (e && atoi(e) > 0) ? atoi(e) : 192;
+  }
+  if (rounds >= 2 && best > cap) return search(cap, &rounds);
   return best;
 }
 
