@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r5v6
+O=gpurun_out/r5v7
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread \
   --deselect "tests/test_native_gpu.py::test_native_checkpoint_roundtrip" > $O/tests.log 2>&1 \
