@@ -238,7 +238,7 @@ def test_tb_mr_shape8(gpu, size, T, scene, obox, src, variant, shape):
 
 def test_tb_bench_scale(gpu):
     """The bench configuration itself: 1024^3 fp32 with the automatic x chunks
-    (256-plane chunks at T=5), 10 steps as two blocked passes == 10 fused
+    (171-plane chunks at T=5), 10 steps as two blocked passes == 10 fused
     single steps, from random fields."""
     cfg = SchemeConfig(scheme="3d", size=(1024, 1024, 1024), scene="vacuum", dtype="f32", use_fused=True,
                        time_steps=10)
