@@ -275,6 +275,20 @@ int run(const fdtd::Settings& s) {
       !upt.disp[5]) {
     dr_blk = true;
     dr_box = chain_regs.back();
+    // the ADE rows must be the Drude form (b1 = -(b0 + b2)) and fit the
+    // 8-bit ids: checked HERE, before the hybrid plan keeps the box inside
+    // the core -- turning the pass off after planning would leave the box on
+    // the plain update (no shell window, no copy box covers it)
+    for (int c = 0; c < 3 && dr_blk; ++c) {
+      if (!upt.disp[c]) continue;
+      if (upt.nlut[c] > 256) dr_blk = false;
+      std::vector<T> tab(5 * (size_t)upt.nlut[c]);
+      HIP_OK(hipMemcpy(tab.data(), upt.lut[c], tab.size() * sizeof(T), hipMemcpyDeviceToHost));
+      for (int q = 0; q < upt.nlut[c]; ++q) {
+        const double b0 = tab[5 * q], b1 = tab[5 * q + 1], b2 = tab[5 * q + 2];
+        if (std::fabs(b0 + b1 + b2) > 1e-5 * (std::fabs(b0) + std::fabs(b1) + std::fabs(b2))) dr_blk = false;
+      }
+    }
   }
   auto clip36 = [&](const IBox& r, int* out) {
     for (int c = 0; c < 6; ++c) {
@@ -435,8 +449,11 @@ int run(const fdtd::Settings& s) {
   int T_h_req = s.hybridBlock == 0 ? 5 : s.hybridBlock;
   if (dr_blk) {
     // (models/blocking.py DRUDE_AUTO_STEPS: the Drude variant holds T - 1 levels in registers)
-    T_h_req = s.hybridBlock > 0 ? s.hybridBlock : (s.timeBlock > 0 ? s.timeBlock : 4);
-    if (T_h_req <= 1 || T_h_req > 5) dr_blk = false;
+    const int T_dr = s.hybridBlock > 0 ? s.hybridBlock : (s.timeBlock > 0 ? s.timeBlock : 4);
+    if (T_dr <= 1 || T_dr > 5)
+      dr_blk = false;  // the stepped dispersive box with the usual hybrid T
+    else
+      T_h_req = T_dr;
   }
   std::vector<IBox> hcores, hshell[8], hcopy;
   int T_h = 1;
@@ -537,14 +554,7 @@ int run(const fdtd::Settings& s) {
     std::vector<float> rows;
     for (int c = 0; c < 3; ++c) {
       if (upt.disp[c]) {
-        const int nl = upt.nlut[c];
-        std::vector<T> tab(5 * (size_t)nl);
-        HIP_OK(hipMemcpy(tab.data(), upt.lut[c], tab.size() * sizeof(T), hipMemcpyDeviceToHost));
-        for (int q = 0; q < nl; ++q) {
-          const double b0 = tab[5 * q], b1 = tab[5 * q + 1], b2 = tab[5 * q + 2];
-          if (std::fabs(b0 + b1 + b2) > 1e-5 * (std::fabs(b0) + std::fabs(b1) + std::fabs(b2))) dr_blk = false;
-        }
-        dr_nid = std::max(dr_nid, nl);
+        dr_nid = std::max(dr_nid, upt.nlut[c]);
         std::vector<unsigned char> full(cells);
         HIP_OK(hipMemcpy(full.data(), upt.ids[c], cells, hipMemcpyDeviceToHost));
         for (int i = 0; i < bn[0]; ++i)
@@ -557,8 +567,11 @@ int run(const fdtd::Settings& s) {
         dr_nid = std::max(dr_nid, 1);  // id 0: the plain row (cb, 0, 1, 0)
       }
     }
-    if (dr_nid > 256) dr_blk = false;
-    if (dr_blk) {
+    if (dr_nid > 256) {  // excluded before the hybrid plan (above)
+      std::fprintf(stderr, "internal error: Drude LUT of %d rows after planning\n", dr_nid);
+      std::exit(3);
+    }
+    {
       rows.assign((size_t)3 * dr_nid * 4, 0.f);
       for (int c = 0; c < 3; ++c) {
         float* r = rows.data() + (size_t)c * dr_nid * 4;

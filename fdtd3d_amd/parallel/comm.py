@@ -116,17 +116,22 @@ class DistComm:
 
 
 class LocalHub:
-    """Mailboxes shared by ``world`` in-process ranks."""
+    """Mailboxes shared by ``world`` in-process ranks.  ``tagless``: one FIFO
+    per (sender, receiver) pair whatever the tag -- RCCL's matching rule (the
+    k-th send to a peer lands in that peer's k-th receive from the sender), so
+    an op list whose per-peer order differs between the two sides shows up as
+    wrong ghosts on the CPU, where gloo's tag matching would hide it."""
 
-    def __init__(self, world: int):
+    def __init__(self, world: int, tagless: bool = False):
         self.world = world
-        self._boxes: Dict[Tuple[int, int, int], "queue.Queue"] = {}
+        self.tagless = tagless
+        self._boxes: Dict[Tuple[int, ...], "queue.Queue"] = {}
         self._lock = threading.Lock()
         self._barrier = threading.Barrier(world)
         self._red: List[float] = [0.0] * world
 
     def box(self, src: int, dst: int, tag: int) -> "queue.Queue":
-        key = (src, dst, tag)
+        key = (src, dst) if self.tagless else (src, dst, tag)
         with self._lock:
             q = self._boxes.get(key)
             if q is None:
@@ -144,6 +149,9 @@ class _LocalRecv:
 
     def wait(self):
         src, ev = self.q.get(timeout=120)
+        if src.shape != self.dst.shape:
+            raise RuntimeError("message size mismatch: sent %s, receive %s (send / receive order differs "
+                               "between the peers)" % (tuple(src.shape), tuple(self.dst.shape)))
         if ev is not None:
             # stream-ordered like RCCL's work.wait(): the receiver's CURRENT
             # stream waits for the sender's snapshot, the host does not -- a

@@ -115,6 +115,11 @@ CASES = [
     ("hybrid-cpml-tfsf-xy4", SchemeConfig(scheme="3d", size=(96, 96, 96), time_steps=10, scene="vacuum", dtype="f32",
                                           use_pml=True, pml_type="cpml", use_tfsf=True, pml_size=(5, 5, 5),
                                           tfsf_size=(10, 10, 10), use_fused=True, hybrid_block=4), 4, "xy", 4),
+    # UPML + TF/SF: automatic mode puts the TF/SF faces inside the blocked core
+    # (models/blocking.py _hybrid_core_tfsf), split over an x / y rank grid
+    ("hybrid-upml-tfsf-xy4", SchemeConfig(scheme="3d", size=(96, 88, 96), time_steps=10, scene="vacuum", dtype="f32",
+                                          use_pml=True, pml_type="upml", use_tfsf=True, pml_size=(5, 5, 5),
+                                          tfsf_size=(8, 8, 8), use_fused=True, hybrid_block=4), 4, "xy", 4),
     ("hybrid-upml-drude-z2", SchemeConfig(scheme="3d", size=(80, 80, 96), time_steps=9, dtype="f32", use_pml=True,
                                           use_metamaterials=True, scene="drude-sphere", sphere_radius=6,
                                           sphere_center=(40.0, 40.0, 48.0), pml_size=(5, 5, 5), use_fused=True,
