@@ -33,6 +33,15 @@ int fdtd_update_h3d_cpml_v4_f32(float* hx, float* hy, float* hz, const float* ex
                                 const float* dbx, const float* dby, const float* dbz, double db, int nx, int ny,
                                 int nz, const int* boxes, int xchunk, const void* const* cp, const int* ci,
                                 void* stream);
+// the same on 4-cell double groups
+int fdtd_update_e3d_cpml_v4_f64(double* ex, double* ey, double* ez, const double* hx, const double* hy,
+                                const double* hz, const double* cbx, const double* cby, const double* cbz, double cb,
+                                int nx, int ny, int nz, const int* boxes, int xchunk, const void* const* cp,
+                                const int* ci, void* stream);
+int fdtd_update_h3d_cpml_v4_f64(double* hx, double* hy, double* hz, const double* ex, const double* ey,
+                                const double* ez, const double* dbx, const double* dby, const double* dbz, double db,
+                                int nx, int ny, int nz, const int* boxes, int xchunk, const void* const* cp,
+                                const int* ci, void* stream);
 // fused UPML / Drude chain of the three components of a kind (chain_kernels.hip):
 // P = 24 pointers, S = 2 scalars, I = 25 ints per component (layout there)
 int fdtd_chain_ints_per_comp();

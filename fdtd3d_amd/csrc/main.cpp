@@ -4,8 +4,8 @@
 //
 // Covers the plain Yee solvers (1D, 2D TMz/TEz, 3D) on one GPU with the
 // vacuum / dielectric-sphere scenes and the hard point source, fp32 or fp64,
-// fused or split 3D kernels, CPML absorbing layers in 3D fp32 (--use-pml
-// --pml-type cpml; with hybrid passes -- blocked core, stepped shell -- like
+// fused or split 3D kernels, CPML absorbing layers in 3D fp32 or fp64 (--use-pml
+// --pml-type cpml; fp32 with hybrid passes -- blocked core, stepped shell -- like
 // the Python driver's automatic plan), the UPML in the reference's D/B form and Drude / Lorentz
 // spheres (--use-metamaterials, scene drude-sphere) in 3D through the fused
 // chain kernel, TF/SF plane waves in 3D, the NTFF scattered power diagram
@@ -169,7 +169,7 @@ int run(const fdtd::Settings& s) {
     if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
     return std::sin(dt * t * 2 * kPi * freq);
   };
-  NativeCpml cpt;
+  NativeCpml<T> cpt;
   if (cpml && dim == 3) setup_cpml(cpt, s, N, active, dt, dx);
   native_phys::Upml<T> upt;
   Pml2d<T> p2;
@@ -366,8 +366,13 @@ int run(const fdtd::Settings& s) {
         if (upml) {
           upml_regions(0);
         } else if (cpml) {
+          // (4-cell z lanes: float4 / double4)
           if constexpr (sizeof(T) == 4)
             K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p,
+                                             percell ? 1.0 : cb, N[0], N[1], N[2], boxes, 0, cpt.P[0].data(),
+                                             cpt.I[0].data(), st));
+          else
+            K_OK(fdtd_update_e3d_cpml_v4_f64(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p,
                                              percell ? 1.0 : cb, N[0], N[1], N[2], boxes, 0, cpt.P[0].data(),
                                              cpt.I[0].data(), st));
         } else {
@@ -387,6 +392,10 @@ int run(const fdtd::Settings& s) {
         } else if (cpml) {
           if constexpr (sizeof(T) == 4)
             K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p,
+                                             percell ? 1.0 : db, N[0], N[1], N[2], boxes + 18, 0, cpt.P[1].data(),
+                                             cpt.I[1].data(), st));
+          else
+            K_OK(fdtd_update_h3d_cpml_v4_f64(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p,
                                              percell ? 1.0 : db, N[0], N[1], N[2], boxes + 18, 0, cpt.P[1].data(),
                                              cpt.I[1].data(), st));
         } else {
@@ -1180,7 +1189,7 @@ int main(int argc, char** argv) {
   }
   if (!native_supported(s)) {
     std::fprintf(stderr,
-                 "fdtd3d (native): CPML in 3D outside fp32 float4 rows, PML / TF/SF in 1D, TF/SF boxes reaching "
+                 "fdtd3d (native): CPML in 3D outside whole 4-cell z rows, PML / TF/SF in 1D, TF/SF boxes reaching "
                  "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "
                  "grids beyond 3D plain media, checkpoints beyond plain media, and complex "
                  "fields run through the Python driver: python -m fdtd3d_amd <same options>\n");

@@ -21,7 +21,7 @@
 // hence the unnamed namespace.
 namespace {
 
-// CPML (3D, fp32 float4 kernels): profiles, psi slabs and the per-kind term
+// CPML (3D, 4-cell z lanes: fp32 float4 / fp64 double4): profiles, psi slabs and the per-kind term
 // tables of yee3d_cpml.hip -- the same slabs and profiles as
 // fdtd3d_amd/models/cpml.py (polynomial grading m = 4, R = 1e-8, kappa and
 // alpha from --cpml-kappa-max / --cpml-alpha-max, each component's own
@@ -68,29 +68,31 @@ std::vector<IBox> box_minus(const IBox& a, const IBox& b) {
   return out;
 }
 
+template <typename T>
 struct NativeCpml {
-  std::vector<Dev<float>*> keep;       // psi slabs and profile arrays
+  std::vector<Dev<T>*> keep;           // psi slabs and profile arrays
   std::vector<const void*> P[2];       // per kind (E, H): 9 x 5 pointers
   std::vector<int> I[2];               // per kind: 9 x 4 ints
   ~NativeCpml() {
     for (auto* d : keep) delete d;
   }
-  float* upload(const std::vector<float>& h) {
-    auto* d = new Dev<float>();
+  T* upload(const std::vector<T>& h) {
+    auto* d = new Dev<T>();
     d->alloc(h.size());
-    HIP_OK(hipMemcpy(d->p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d->p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
     keep.push_back(d);
     return d->p;
   }
-  float* zeros(size_t n) {
-    auto* d = new Dev<float>();
+  T* zeros(size_t n) {
+    auto* d = new Dev<T>();
     d->alloc(n);
     keep.push_back(d);
     return d->p;
   }
 };
 
-void setup_cpml(NativeCpml& cp, const fdtd::Settings& s, const fdtd::Int3& N, const std::vector<int>& active,
+template <typename T>
+void setup_cpml(NativeCpml<T>& cp, const fdtd::Settings& s, const fdtd::Int3& N, const std::vector<int>& active,
                 double dt, double dx) {
   // staggered offset of each component inside its cell (layout/yee.py MIN_COORD_FP)
   static const double mco[6][3] = {{1.0, 0.5, 0.5}, {0.5, 1.0, 0.5}, {0.5, 0.5, 1.0},
@@ -112,7 +114,7 @@ void setup_cpml(NativeCpml& cp, const fdtd::Settings& s, const fdtd::Int3& N, co
         const int n = N[a];
         const double m = mco[c][a];
         const double sig_max = -(4 + 1) * std::log(1e-8) / (2 * eta * P * dx);
-        std::vector<float> b(n, 1.f), cv(n, 0.f), kk(n, 0.f);
+        std::vector<T> b(n, T(1)), cv(n, T(0)), kk(n, T(0));
         const void* psi[2] = {nullptr, nullptr};
         int rng[2][2] = {{0, 0}, {0, 0}};
         for (int side = 0; side < 2; ++side) {
@@ -136,9 +138,9 @@ void setup_cpml(NativeCpml& cp, const fdtd::Settings& s, const fdtd::Int3& N, co
             const double sig = sig_max * d4, kap = 1.0 + (kmax - 1.0) * d4, alp = amax * (1.0 - depth);
             const double bc = std::exp(-(sig / kap + alp) * dt / kEps0);
             const double den = sig * kap + kap * kap * alp;
-            b[v] = (float)bc;
-            cv[v] = (float)(den > 0 ? sig / den * (bc - 1.0) : 0.0);
-            kk[v] = (float)(1.0 / kap - 1.0);
+            b[v] = (T)bc;
+            cv[v] = (T)(den > 0 ? sig / den * (bc - 1.0) : 0.0);
+            kk[v] = (T)(1.0 / kap - 1.0);
           }
           // psi storage: the slab's range along a x the full extents of the other two
           size_t vol = (size_t)(hi - lo);
@@ -563,10 +565,10 @@ int tfsf_apply(double* t, const TfsfLayer<double>& l, const double* inc, const i
 // The options this binary runs (everything else goes through the Python
 // driver, never a silent fallback).
 bool native_supported(const fdtd::Settings& s) {
-  // CPML absorbing layers: 3D fp32 with whole float4 z rows (the folded
-  // float4 kernels), 2D in either precision (generic slab kernels)
+  // CPML absorbing layers: 3D with whole 4-cell z rows (the folded float4 /
+  // double4 kernels), 2D in either precision (generic slab kernels)
   const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && !s.doUseMetamaterials &&
-                       ((s.dimension == 3 && s.valueType == "f32" && s.sizeZ % 4 == 0) || s.dimension == 2);
+                       ((s.dimension == 3 && s.sizeZ % 4 == 0) || s.dimension == 2);
   // UPML (D/B chain) and Drude / Lorentz spheres: 3D, any precision; the 2D UPML without dispersive media
   const bool upml_ok = s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials) &&
                        (s.dimension == 3 || (s.dimension == 2 && !s.doUseMetamaterials));

@@ -1286,7 +1286,8 @@ class HipOps:
 
     # ------------------------------------------------------------ fused CPML
     def fused_cpml_ok(self, scheme) -> bool:
-        return (self.vec4 and self.dtype == torch.float32 and scheme.cfg.scheme == "3d"
+        # fp32 float4 / fp64 double4 lanes of 4 z cells (yee3d_cpml.hip)
+        return (self.vec4 and self.dtype in (torch.float32, torch.float64) and scheme.cfg.scheme == "3d"
                 and scheme.domain.shape[2] % 4 == 0)
 
     def curl_update_cpml(self, kind: str, boxes: Dict[str, Box], dst: Dict[str, torch.Tensor],
@@ -1302,8 +1303,8 @@ class HipOps:
                 self._check_stencil_box(kind, c, boxes[c], shape)
         for c in other:
             self._check_tensor(src[c], shape)
-        if shape[2] % 4 != 0 or self.dtype != torch.float32:
-            raise HipError("fused CPML kernel needs fp32 and nz % 4 == 0")
+        if shape[2] % 4 != 0 or self.dtype not in (torch.float32, torch.float64):
+            raise HipError("fused CPML kernel needs fp32 / fp64 and nz % 4 == 0")
         per = [self._cell_or_none(cb[c]) for c in names]
         if per[0] is not None:
             per_p = [_ptr(self._scaled_cell(cb[c])) for c in names]

@@ -63,13 +63,15 @@ def test_cpml_3d(gpu):
                          pml_size=(6, 6, 6), scene="vacuum", dtype="f32"), gpu, 5e-5)
 
 
-def test_cpml_fused_f32_sphere_tfsf(gpu):
-    """fp32 CPML folded into the float4 update kernels (yee3d_cpml.hip):
-    per-cell coefficients, z slabs straddling float4 lanes, kappa / alpha."""
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_cpml_fused_sphere_tfsf(gpu, dtype):
+    """CPML folded into the 4-cell-lane update kernels (yee3d_cpml.hip, fp32
+    float4 / fp64 double4): per-cell coefficients, z slabs straddling lanes,
+    kappa / alpha."""
     compare(SchemeConfig(scheme="3d", size=(36, 40, 52), time_steps=30, use_pml=True, pml_type="cpml",
                          use_tfsf=True, pml_size=(7, 6, 7), tfsf_size=(12, 12, 14), scene="sphere",
-                         sphere_radius=5, sphere_center=(18.5, 20.5, 26.5), dtype="f32", cpml_kappa_max=3.0,
-                         cpml_alpha_max=0.05), gpu, 5e-5)
+                         sphere_radius=5, sphere_center=(18.5, 20.5, 26.5), dtype=dtype, cpml_kappa_max=3.0,
+                         cpml_alpha_max=0.05), gpu, 5e-5 if dtype == "f32" else 1e-10)
 
 
 def test_cpml_tfsf_3d(gpu):

@@ -22,6 +22,9 @@ CASES = [
     ("sphere-cpml", dict(scene="sphere", use_pml=True, pml_type="cpml", sphere_center=(40.0, 36.0, 48.0),
                          sphere_radius=10.0), 4, 9),
     ("upml-tfsf-f64", dict(scene="vacuum", use_pml=True, use_tfsf=True, theta=30, phi=40, psi=20, dtype="f64"), 4, 10),
+    # fp64 CPML shell on the double4 fused CPML kernels (yee3d_cpml.hip)
+    ("cpml-tfsf-f64", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10, psi=5,
+                           dtype="f64"), 4, 10),
     # (the Drude cases keep the stepped dispersive box: blocked_drude="off"; the blocked Drude pass is
     # tests/test_drude_blk_gpu.py)
     # no PML: the blocked core reaches the domain faces around the dispersive box

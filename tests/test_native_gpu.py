@@ -134,9 +134,9 @@ CASES = {
     "2d_tmz_amp_cpml": ["--2d", "--sizex", "60", "--sizey", "52", "--time-steps", "10", "--scene", "vacuum",
                         "--use-amp-mode", "--amplitude-time-steps", "300", "--use-pml", "--pml-type", "cpml"],
 }
-FP32_ONLY = {"3d_cpml", "3d_cpml_sphere_kappa", "3d_cpml_tfsf", "3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid",
-             "3d_amp_cpml", "3d_upml_tfsf_hybrid", "3d_upml_point_hybrid", "3d_drude_upml_hybrid", "3d_drude_hybrid",
-             "3d_tfsf_hybrid"}
+# (native hybrid passes are fp32; the stepped 3D CPML runs in both precisions)
+FP32_ONLY = {"3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid", "3d_upml_tfsf_hybrid", "3d_upml_point_hybrid",
+             "3d_drude_upml_hybrid", "3d_drude_hybrid", "3d_tfsf_hybrid"}
 # the converged step depends on running-maximum comparisons at round-off level: fp64 only
 FP64_ONLY = {"2d_tmz_amp_cpml"}
 
@@ -163,7 +163,7 @@ def test_native_driver_matches_python(case, dtype, tmp_path, gpu):
     exe = native.executable()
     assert os.path.exists(exe), "native fdtd3d executable missing (run python -m fdtd3d_amd.ops.build)"
     if case in FP32_ONLY and dtype != "f32":
-        pytest.skip("native CPML: fp32 float4 kernels")
+        pytest.skip("native hybrid passes: fp32")
     if case in FP64_ONLY and dtype != "f64":
         pytest.skip("converged amplitude step compared in fp64")
     argv = CASES[case] + ["--dtype", dtype, "--save-res", "--save-as-dat"]
