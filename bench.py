@@ -41,6 +41,8 @@ T_START = time.perf_counter()
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 HEADLINE_SIZE = (1024, 1024, 1024)
+# rank grids of the headline grid measured fastest per GPU (profiles/decomp_r6.md)
+MEASURED_GRIDS = {2: (2, 1, 1), 4: (2, 2, 1), 8: (4, 2, 1)}
 
 
 def metric_name(size) -> str:
@@ -63,9 +65,13 @@ def parse_topology(spec: str, size, world: int, blocked: bool):
             raise SystemExit("--topology %s does not match %d ranks" % (spec, world))
         return ParallelGridCore.create(size, world, "xyz", requested=t, optimal=False)
     if spec == "auto":
-        # blocked passes: split x and y only.  The blocked kernel tiles z in
-        # 54-cell rows, so a T-thick z shell costs a whole tile row
-        # (tools/decomp_cost.py, profiles/decomp_r2.md)
+        # blocked passes: the measured best rank grid at 1024^3 (per-GPU cost
+        # with a loopback transport, tools/decomp_cost.py, profiles/decomp_r6.md:
+        # 8 ranks T = 4 -- 4x2x1 240.5k, 2x4x1 237.4k, 8x1x1 226.6k, 2x2x2
+        # 219.0k Mcells/s per GPU; a T-thick z shell costs a whole 56-lane tile
+        # row), else x and y split by the reference's halo-surface optimiser
+        if blocked and world in MEASURED_GRIDS and tuple(size) == HEADLINE_SIZE:
+            return ParallelGridCore.create(size, world, "xyz", requested=MEASURED_GRIDS[world], optimal=False)
         spec = "xy" if blocked else "xyz"
     return ParallelGridCore.create(size, world, spec)
 

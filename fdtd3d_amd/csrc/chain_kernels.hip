@@ -338,6 +338,43 @@ __global__ __launch_bounds__(256) void k_chain3d(ChainComp<T> q0, ChainComp<T> q
   }
 }
 
+// Non-dispersive chain, one component per thread: blockIdx.z picks the
+// component, whose struct is read through a uniform index into the kernel
+// argument block (scalar loads of ONE component's pointers and boxes).  The
+// three-components-per-thread kernel above keeps ~75 SGPRs of arguments per
+// component live and spills 170-290 SGPRs into VGPR lanes (read back every
+// plane); here a thread holds one component's operands, loads them all
+// before its single store, and the arguments fit the SGPR file.
+template <typename T>
+struct ChainSet {
+  ChainComp<T> q[3];
+};
+
+template <typename T, bool CELL>
+__global__ __launch_bounds__(256) void k_chain3d_c(ChainSet<T> S, int kind_e, int ny, int nz, Box3 U, int chx) {
+  const ChainComp<T>& q = S.q[blockIdx.z];
+  const Box3 B = box_union(q.box, q.pbox);
+  // the component's own boxes inside the launch's union box U
+  const int W = U.hi[2] - U.lo[2];
+  const int H = U.hi[1] - U.lo[1];
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)W * H) return;
+  int n[3];
+  n[1] = U.lo[1] + (int)(idx / W);
+  n[2] = U.lo[2] + (int)(idx % W);
+  if (n[1] < B.lo[1] || n[1] >= B.hi[1] || n[2] < B.lo[2] || n[2] >= B.hi[2]) return;
+  const int i0 = max(U.lo[0] + (int)blockIdx.y * chx, B.lo[0]);
+  const int i1 = min(min(U.lo[0] + ((int)blockIdx.y + 1) * chx, U.hi[0]), B.hi[0]);
+  const long long stride[3] = {(long long)ny * nz, (long long)nz, 1};
+#pragma unroll 1
+  for (int i = i0; i < i1; ++i) {
+    n[0] = i;
+    const size_t off = ((size_t)i * ny + n[1]) * nz + n[2];
+    const ChainIn<T> v = chain_load<T, false, CELL>(q, kind_e != 0, stride, n, off);
+    chain_finish<T, false>(q, kind_e != 0, v, off);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // float4 form of the non-dispersive chain (fp32, z rows of 4-cell groups):
 // each thread owns 4 consecutive z cells of one (y, x-run), 16-byte loads and
@@ -432,6 +469,17 @@ __global__ __launch_bounds__(256) void k_chain3d_v4(ChainComp<float> q0, ChainCo
 // off by default: measured slower than one cell per thread (512^3 UPML + TF/SF
 // 58.1k vs 71.3k, Drude + UPML 46.2k vs 55.4k Mcells/s): A-B knob (fdtd_set_chain_v4)
 static bool g_chain_v4 = false;
+
+// non-dispersive chain launches: one component per thread (k_chain3d_c) or
+// all three (k_chain3d); FDTD3D_CHAIN_SPLIT=0 / 1 overrides
+static int g_chain_split = -1;
+static bool chain_split() {
+  if (g_chain_split < 0) {
+    const char* e = getenv("FDTD3D_CHAIN_SPLIT");
+    g_chain_split = (e && *e) ? (atoi(e) != 0) : 1;
+  }
+  return g_chain_split != 0;
+}
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
@@ -530,6 +578,16 @@ int launch_chain(const void* const* P, const double* S, const int* I, int drude,
   const long long cells = (long long)(U.hi[2] - U.lo[2]) * (U.hi[1] - U.lo[1]);
   const int chx = chain_chx();
   dim3 grid(cdiv(cells, 256), cdiv(U.hi[0] - U.lo[0], chx));
+  if (!drude && chain_split()) {
+    ChainSet<T> S;
+    for (int c = 0; c < 3; ++c) S.q[c] = q[c];
+    dim3 g3(grid.x, grid.y, 3);
+    if (cell)
+      k_chain3d_c<T, true><<<g3, 256, 0, s>>>(S, kind_e, ny, nz, U, chx);
+    else
+      k_chain3d_c<T, false><<<g3, 256, 0, s>>>(S, kind_e, ny, nz, U, chx);
+    FDTD_RETURN_LAUNCH_STATUS();
+  }
 #define CH_LAUNCH(D, C) k_chain3d<T, D, C><<<grid, 256, 0, s>>>(q[0], q[1], q[2], kind_e, ny, nz, U, rr, chx)
   if (drude) {
     if (cell) CH_LAUNCH(true, true);

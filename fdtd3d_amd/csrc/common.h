@@ -22,11 +22,11 @@ __device__ __forceinline__ bool in_box(const Box3& b, int i, int j, int k) {
   return i >= b.lo[0] && i < b.hi[0] && j >= b.lo[1] && j < b.hi[1] && k >= b.lo[2] && k < b.hi[2];
 }
 
-static inline bool box_empty(const Box3& b) {
+__host__ __device__ static inline bool box_empty(const Box3& b) {
   return b.hi[0] <= b.lo[0] || b.hi[1] <= b.lo[1] || b.hi[2] <= b.lo[2];
 }
 
-static inline Box3 box_union(const Box3& a, const Box3& b) {
+__host__ __device__ static inline Box3 box_union(const Box3& a, const Box3& b) {
   if (box_empty(a)) return b;
   if (box_empty(b)) return a;
   Box3 r;

@@ -175,7 +175,8 @@ class BlockedStepping:
         absorbing layers only).  Returns the plan (T, box, tables) or None:
         serial 3D runs of an electric Drude medium with uniform eps / gamma
         (coefficient tuples in a table of <= 256 rows per component), the box
-        in the sigma = 0 region, no TF/SF, amplitude mode or complex fields;
+        in the sigma = 0 region, TF/SF targets (if any) clear of the Drude
+        launch's cone, no amplitude mode or complex fields;
         ``--blocked-drude off`` (or one step per pass) keeps the stepped
         dispersive box.  Reference: Scheme3D.cpp:266-416, Kernels.h:103-107."""
         cfg = self.cfg
@@ -185,7 +186,7 @@ class BlockedStepping:
             return None
         if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
             return None
-        if (self.halo is not None or self.planes != 1 or cfg.use_tfsf or cfg.use_amp_mode or self.graph_mode
+        if (self.halo is not None or self.planes != 1 or cfg.use_amp_mode or self.graph_mode
                 or not self.use_upml_chain or getattr(self, "chain_regions", None) is None or self.use_cpml
                 or getattr(cfg, "dispersion", "drude") != "drude" or self.hooks):
             return None
@@ -221,6 +222,16 @@ class BlockedStepping:
                 if B[0][d] < ub[0][d] or B[1][d] > ub[1][d]:
                     return None
         Bl = dom.to_local(B)
+        if cfg.use_tfsf:
+            # a scattering scene (reference Scheme3D.cpp:3452-3492 with :138-208): the Drude launch
+            # recomputes the box grown by T from the pass-start fields, its halo cells on the plain
+            # update without TF/SF fixes, so every TF/SF target must lie outside the launch's cone
+            # (the box grown by 2T, one more cell for the staggering); the core pass / stepped shell
+            # correct the faces as without the Drude box
+            reach = 2 * T + 2
+            cone = (tuple(Bl[0][d] - reach for d in range(3)), tuple(Bl[1][d] + reach for d in range(3)))
+            if getattr(self, "tfsf", None) is None or self._tfsf_targets_in(cone):
+                return None
         bshape = tuple(Bl[1][d] - Bl[0][d] for d in range(3))
         # D coefficient where sigma = 0 (the chain's cbD profile), the same for the three components
         cbd = None

@@ -31,12 +31,22 @@ def _close(a, b, tol=1e-12):
 
 
 @pytest.mark.parametrize("extra,T,steps", [({}, 4, 13), ({"use_pml": True, "pml_size": (5, 5, 5)}, 4, 14),
-                                           ({}, 5, 12)], ids=["nopml", "upml", "nopml-T5"])
+                                           ({}, 5, 12),
+                                           # the reference's scattering scene: Drude sphere + UPML + TF/SF
+                                           # (the faces lie in the stepped shell here: a grid big enough for
+                                           # a core of a quarter of the cells; the sphere near the corner the
+                                           # wave enters by, its cone clear of the faces)
+                                           ({"use_pml": True, "pml_size": (5, 5, 5), "use_tfsf": True,
+                                             "tfsf_size": (9, 9, 9), "theta": 60.0, "phi": 20.0, "psi": 30.0,
+                                             "size": (80, 80, 84), "sphere_center": (27.0, 27.0, 27.0)}, 4, 56),
+                                           ({"use_tfsf": True, "tfsf_size": (10, 10, 10),
+                                             "sphere_center": (26.0, 30.0, 34.0)}, 3, 36)],
+                         ids=["nopml", "upml", "nopml-T5", "upml-tfsf", "tfsf-nopml"])
 def test_drude_blocked_vs_chain(extra, T, steps):
-    cfg = SchemeConfig(time_steps=steps, **BASE, **extra)
+    cfg = SchemeConfig(time_steps=steps, **dict(BASE, **extra))
     blk = _scheme(dataclasses.replace(cfg, blocked_drude="on", hybrid_block=T, time_block=T))
     assert blk.drude_blk is not None
-    if cfg.use_pml:
+    if cfg.use_pml or cfg.use_tfsf:
         assert blk.hybrid is not None and blk.hybrid["drude"]
     else:
         assert blk.hybrid is None and blk.tb == T
