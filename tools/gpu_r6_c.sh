@@ -20,3 +20,12 @@ for rep in 1 2; do
   done
 done
 FDTD3D_CHAIN_SPLIT=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/t_du -o run -- python3 -m fdtd3d_amd $DU > $O/ktdu.log 2>&1 && cp /tmp/t_du/run_kernel_stats.csv $O/kt_du_split.csv || { echo "ktdu failed"; exit 1; }
+# config 3 with the TF/SF faces in the core at T = 4 (the TF/SF variant spills VGPRs at T = 5) vs the shell form
+C3="--3d --sizex 512 --same-size --dtype f32 --warmup-steps 10 --time-steps 40 --json --scene vacuum --use-pml --pml-type cpml --use-tfsf"
+for rep in 1 2; do
+  for v in "core 4" "core 5" "shell 5" "shell 4"; do
+    set -- $v
+    timeout -k 10 200 python3 -m fdtd3d_amd $C3 --hybrid-tfsf $1 --hybrid-block $2 > $O/c3_$1_$2.log 2>&1 || { echo "c3 $v failed"; exit 1; }
+    echo "rep $rep config 3 faces in $1, T=$2: $(grep -o '"mcells_per_s": [0-9.]*' $O/c3_$1_$2.log | cut -d' ' -f2)"
+  done
+done
