@@ -57,29 +57,70 @@ struct XRank {
 };
 
 template <typename T>
-int run_multi(const fdtd::Settings& s) {
-  fdtd::Int3 N = {s.sizeX, s.sizeY, s.sizeZ};
+class MultiRun {
+ public:
+  explicit MultiRun(const fdtd::Settings& s_) : s(s_) {}
+  ~MultiRun() { release(); }
+  int main();
+
+ private:
+  const fdtd::Settings& s;
+  fdtd::Int3 N;
   const std::vector<int> active = {0, 1, 2};
-  const double dx = s.gridStep, courant = s.courantNum;
-  const double dt = dx * courant / kC;
-  const double freq = kC / s.sourceWaveLength;
-  const double cb = dt / (kEps0 * dx), db = dt / (kMu0 * dx);
-  const bool percell = s.scene != "vacuum";
-  int ndev = 0;
+  double dt = 0, freq = 0, cb = 0, db = 0;
+  bool percell = false;
+  int ndev = 0, P = 1, TB = 1;
+  int Pd[3] = {1, 1, 1};
+  fdtd::Int3 sp;
+  std::vector<XRank<T>> R;
+  bool first = true;
+
+  double src_val(int t) const {
+    if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
+    return std::sin(dt * t * 2 * kPi * freq);
+  }
+  int rank_of(const int* c) const { return (c[0] * Pd[1] + c[1]) * Pd[2] + c[2]; }
+  int plan_ranks();
+  void setup_rank(int r);
+  void enable_peers();
+  void plan_outputs();
+  void pull_ghosts();
+  void rank_pass(XRank<T>& q, int t, int k);
+  void pass(int t, int k);
+  void advance(int t0, int n);
+  void sync_all();
+  void report(double sec, int steps, int warm) const;
+  void save_results(int steps);
+  void release();
+};
+
+// the rank grid (--topology-sizex/y/z, else one x slab per GPU), the steps
+// per pass and every rank's owned / allocated box; 2 when the grid does not
+// split that way
+template <typename T>
+int MultiRun<T>::plan_ranks() {
+  N = {s.sizeX, s.sizeY, s.sizeZ};
+  const double dx = s.gridStep;
+  dt = dx * s.courantNum / kC;
+  freq = kC / s.sourceWaveLength;
+  cb = dt / (kEps0 * dx);
+  db = dt / (kMu0 * dx);
+  percell = s.scene != "vacuum";
   HIP_OK(hipGetDeviceCount(&ndev));
-  int Pd[3] = {std::max(1, s.topologySizeX), std::max(1, s.topologySizeY), std::max(1, s.topologySizeZ)};
+  Pd[0] = std::max(1, s.topologySizeX);
+  Pd[1] = std::max(1, s.topologySizeY);
+  Pd[2] = std::max(1, s.topologySizeZ);
   if (Pd[0] * Pd[1] * Pd[2] == 1) Pd[0] = ndev;
-  const int P = Pd[0] * Pd[1] * Pd[2];
+  P = Pd[0] * Pd[1] * Pd[2];
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
-  const int TB = std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
+  TB = std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
   for (int a = 0; a < 3; ++a)
     if (N[a] / Pd[a] < TB) {
       std::fprintf(stderr, "fdtd3d (native): %d cells along axis %d over %d ranks leave fewer than %d per rank\n",
                    N[a], a, Pd[a], TB);
       return 2;
     }
-  std::vector<XRank<T>> R(P);
-  auto rank_of = [&](const int* c) { return (c[0] * Pd[1] + c[1]) * Pd[2] + c[2]; };
+  R.resize(P);
   for (int r = 0; r < P; ++r) {
     XRank<T>& q = R[r];
     q.crd[0] = r / (Pd[1] * Pd[2]);
@@ -100,83 +141,93 @@ int run_multi(const fdtd::Settings& s) {
       return 2;
     }
   }
-  for (int r = 0; r < P; ++r) {
-    XRank<T>& q = R[r];
-    q.dev = r % ndev;
-    HIP_OK(hipSetDevice(q.dev));
-    HIP_OK(hipStreamCreate(&q.st));
-    HIP_OK(hipStreamCreate(&q.side));
-    HIP_OK(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&q.copied, hipEventDisableTiming));
-    const size_t n = q.cells();
-    for (int c = 0; c < 6; ++c) {
-      q.F[c].alloc(n);
-      q.G[c].alloc(n);
-    }
-    // update boxes in local indices: the global range of each component
-    // clipped to the rank's allocated box
-    for (int c = 0; c < 6; ++c) {
-      fdtd::Int3 glo, ghi;
-      fdtd::global_range(c, N, active, glo, ghi);
-      for (int a = 0; a < 3; ++a) {
-        q.boxes[6 * c + a] = std::max(glo[a], q.g0[a]) - q.g0[a];
-        q.boxes[6 * c + 3 + a] = std::min(ghi[a], q.g0[a] + q.n[a]) - q.g0[a];
-      }
-    }
-    // messages: direction d = (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)
-    for (int d = 0; d < 27; ++d) {
-      const int off[3] = {d / 9 - 1, (d / 3) % 3 - 1, d % 3 - 1};
-      int c[3];
-      bool ok = d != 13;
-      for (int a = 0; a < 3; ++a) {
-        c[a] = q.crd[a] + off[a];
-        ok = ok && c[a] >= 0 && c[a] < Pd[a];
-      }
-      q.nb[d] = ok ? rank_of(c) : -1;
-      if (!ok) continue;
-      size_t vol = 6;
-      for (int a = 0; a < 3; ++a) {
-        // send: the owned layers next to the neighbour; receive: the ghosts there
-        int slo = q.lo[a], shi = q.hi[a], rlo = q.lo[a], rhi = q.hi[a];
-        if (off[a] < 0) {
-          shi = q.lo[a] + TB;
-          rlo = q.lo[a] - TB;
-          rhi = q.lo[a];
-        } else if (off[a] > 0) {
-          slo = q.hi[a] - TB;
-          rlo = q.hi[a];
-          rhi = q.hi[a] + TB;
-        }
-        q.sbox[d][a] = slo - q.g0[a];
-        q.sbox[d][3 + a] = shi - q.g0[a];
-        q.rbox[d][a] = rlo - q.g0[a];
-        q.rbox[d][3 + a] = rhi - q.g0[a];
-        vol *= (size_t)(shi - slo);
-      }
-      q.sbuf[d].alloc(vol);
-      q.rbuf[d].alloc(vol);
-    }
-    if (percell) {
-      // per-cell E coefficients of the dielectric sphere (2-point eps
-      // averages, as the single-rank path), H on the scalar db
-      const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
-      std::vector<T> host(n);
-      for (int c = 0; c < 3; ++c) {
-        const int di = c == 0, dj = c == 1, dk = c == 2;
-        for (int li = 0; li < q.n[0]; ++li)
-          for (int lj = 0; lj < q.n[1]; ++lj)
-            for (int lk = 0; lk < q.n[2]; ++lk) {
-              const int i = q.g0[0] + li, j = q.g0[1] + lj, k = q.g0[2] + lk;
-              const double a = sphere_eps(i + 0.5, j + 0.5, k + 0.5, ctr, s.sphereRadius, s.sphereEps);
-              const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, k + dk + 0.5, ctr, s.sphereRadius, s.sphereEps);
-              host[((size_t)li * q.n[1] + lj) * q.n[2] + lk] = (T)(cb * 2.0 / (a + b));
-            }
-        q.C[c].alloc(n);
-        HIP_OK(hipMemcpy(q.C[c].p, host.data(), n * sizeof(T), hipMemcpyHostToDevice));
-      }
+  sp = {N[0] / 2, N[1] / 2, N[2] / 2};
+  return 0;
+}
+
+// one rank on device r % devices: streams, fields, update boxes, the 26
+// message boxes and buffers, per-cell coefficients
+template <typename T>
+void MultiRun<T>::setup_rank(int r) {
+  XRank<T>& q = R[r];
+  q.dev = r % ndev;
+  HIP_OK(hipSetDevice(q.dev));
+  HIP_OK(hipStreamCreate(&q.st));
+  HIP_OK(hipStreamCreate(&q.side));
+  HIP_OK(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&q.copied, hipEventDisableTiming));
+  const size_t n = q.cells();
+  for (int c = 0; c < 6; ++c) {
+    q.F[c].alloc(n);
+    q.G[c].alloc(n);
+  }
+  // update boxes in local indices: the global range of each component
+  // clipped to the rank's allocated box
+  for (int c = 0; c < 6; ++c) {
+    fdtd::Int3 glo, ghi;
+    fdtd::global_range(c, N, active, glo, ghi);
+    for (int a = 0; a < 3; ++a) {
+      q.boxes[6 * c + a] = std::max(glo[a], q.g0[a]) - q.g0[a];
+      q.boxes[6 * c + 3 + a] = std::min(ghi[a], q.g0[a] + q.n[a]) - q.g0[a];
     }
   }
-  // peer access between the devices of neighbouring ranks (xGMI)
+  // messages: direction d = (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)
+  for (int d = 0; d < 27; ++d) {
+    const int off[3] = {d / 9 - 1, (d / 3) % 3 - 1, d % 3 - 1};
+    int c[3];
+    bool ok = d != 13;
+    for (int a = 0; a < 3; ++a) {
+      c[a] = q.crd[a] + off[a];
+      ok = ok && c[a] >= 0 && c[a] < Pd[a];
+    }
+    q.nb[d] = ok ? rank_of(c) : -1;
+    if (!ok) continue;
+    size_t vol = 6;
+    for (int a = 0; a < 3; ++a) {
+      // send: the owned layers next to the neighbour; receive: the ghosts there
+      int slo = q.lo[a], shi = q.hi[a], rlo = q.lo[a], rhi = q.hi[a];
+      if (off[a] < 0) {
+        shi = q.lo[a] + TB;
+        rlo = q.lo[a] - TB;
+        rhi = q.lo[a];
+      } else if (off[a] > 0) {
+        slo = q.hi[a] - TB;
+        rlo = q.hi[a];
+        rhi = q.hi[a] + TB;
+      }
+      q.sbox[d][a] = slo - q.g0[a];
+      q.sbox[d][3 + a] = shi - q.g0[a];
+      q.rbox[d][a] = rlo - q.g0[a];
+      q.rbox[d][3 + a] = rhi - q.g0[a];
+      vol *= (size_t)(shi - slo);
+    }
+    q.sbuf[d].alloc(vol);
+    q.rbuf[d].alloc(vol);
+  }
+  if (percell) {
+    // per-cell E coefficients of the dielectric sphere (2-point eps
+    // averages, as the single-rank path), H on the scalar db
+    const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
+    std::vector<T> host(n);
+    for (int c = 0; c < 3; ++c) {
+      const int di = c == 0, dj = c == 1, dk = c == 2;
+      for (int li = 0; li < q.n[0]; ++li)
+        for (int lj = 0; lj < q.n[1]; ++lj)
+          for (int lk = 0; lk < q.n[2]; ++lk) {
+            const int i = q.g0[0] + li, j = q.g0[1] + lj, k = q.g0[2] + lk;
+            const double a = sphere_eps(i + 0.5, j + 0.5, k + 0.5, ctr, s.sphereRadius, s.sphereEps);
+            const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, k + dk + 0.5, ctr, s.sphereRadius, s.sphereEps);
+            host[((size_t)li * q.n[1] + lj) * q.n[2] + lk] = (T)(cb * 2.0 / (a + b));
+          }
+      q.C[c].alloc(n);
+      HIP_OK(hipMemcpy(q.C[c].p, host.data(), n * sizeof(T), hipMemcpyHostToDevice));
+    }
+  }
+}
+
+// peer access between the devices of neighbouring ranks (xGMI)
+template <typename T>
+void MultiRun<T>::enable_peers() {
   for (int r = 0; r < P; ++r)
     for (int d = 0; d < 27; ++d) {
       const int o = R[r].nb[d];
@@ -190,14 +241,13 @@ int run_multi(const fdtd::Settings& s) {
       }
     }
   (void)hipGetLastError();
-  const fdtd::Int3 sp = {N[0] / 2, N[1] / 2, N[2] / 2};
-  auto src_val = [&](int t) {
-    if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
-    return std::sin(dt * t * 2 * kPi * freq);
-  };
-  // output boxes of a pass (local indices): the interior (owned cells at
-  // least TB from every neighbour: needs no fresh ghost) first, then the
-  // TB-thick shell slabs peeled off axis by axis (models/blocking.py _tb_regions)
+}
+
+// output boxes of a pass (local indices): the interior (owned cells at
+// least TB from every neighbour: needs no fresh ghost) first, then the
+// TB-thick shell slabs peeled off axis by axis (models/blocking.py _tb_regions)
+template <typename T>
+void MultiRun<T>::plan_outputs() {
   for (XRank<T>& q : R) {
     int lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
@@ -221,100 +271,108 @@ int run_multi(const fdtd::Settings& s) {
     q.outs.push_back({lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
     for (const auto& b : sh) q.outs.push_back(b);
   }
-  bool first = true;
-  // One pass of k steps.  Phase 1, every rank on its side stream: pull the
-  // neighbours' packs of the previous pass (after their `done` and its own,
-  // which orders the ghost writes after the passes that read them) and
-  // unpack them into the ghosts.  Phase 2, on the main stream: the interior
-  // -- concurrent with phase 1, it reads no ghost -- then, after the pulls,
-  // the shells, and the packs for the next pass once the neighbours have
-  // pulled this pass's (their `copied`).  The phases are issued rank after
-  // rank on the host, so every event waited on is already recorded.
-  auto pass = [&](int t, int k) {
-    if (!first)
-      for (int r = 0; r < P; ++r) {
-        XRank<T>& q = R[r];
-        HIP_OK(hipSetDevice(q.dev));
-        HIP_OK(hipStreamWaitEvent(q.side, q.done, 0));
-        T* f[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
-        for (int d = 0; d < 27; ++d) {
-          if (q.nb[d] < 0) continue;
-          const XRank<T>& o = R[q.nb[d]];
-          HIP_OK(hipStreamWaitEvent(q.side, o.done, 0));
-          // the neighbour at d packed its box for direction 26 - d (towards us)
-          const size_t bytes = q.rbuf[d].n * sizeof(T);
-          if (o.dev == q.dev)
-            HIP_OK(hipMemcpyAsync(q.rbuf[d].p, o.sbuf[26 - d].p, bytes, hipMemcpyDeviceToDevice, q.side));
-          else
-            HIP_OK(hipMemcpyPeerAsync(q.rbuf[d].p, q.dev, o.sbuf[26 - d].p, o.dev, bytes, q.side));
-          K_OK(box_unpack(f, q.rbuf[d].p, 6, q.n[1], q.n[2], q.rbox[d], q.side));
-        }
-        HIP_OK(hipEventRecord(q.copied, q.side));
-      }
-    for (int r = 0; r < P; ++r) {
-      XRank<T>& q = R[r];
-      HIP_OK(hipSetDevice(q.dev));
-      const T* ei[3] = {q.F[0].p, q.F[1].p, q.F[2].p};
-      const T* hi[3] = {q.F[3].p, q.F[4].p, q.F[5].p};
-      T* eo[3] = {q.G[0].p, q.G[1].p, q.G[2].p};
-      T* ho[3] = {q.G[3].p, q.G[4].p, q.G[5].p};
-      const T* cbs[3] = {q.C[0].p, q.C[1].p, q.C[2].p};
-      const T* dbs[3] = {nullptr, nullptr, nullptr};
-      // every rank whose allocated box (ghosts included) holds the source
-      // sets the hard source: a neighbour's redundant ghost levels need it
-      bool has = true;
-      for (int a = 0; a < 3; ++a) has = has && sp[a] >= q.g0[a] && sp[a] < q.g0[a] + q.n[a];
-      const int src[4] = {sp[0] - q.g0[0], sp[1] - q.g0[1], sp[2] - q.g0[2], has ? 2 : -1};
-      double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
-      for (size_t b = 0; b < q.outs.size(); ++b) {
-        const int* ob = q.outs[b].data();
-        if (b == 1 && !first) HIP_OK(hipStreamWaitEvent(q.st, q.copied, 0));  // the shells read the fresh ghosts
-        if (ob[3] <= ob[0] || ob[4] <= ob[1] || ob[5] <= ob[2]) continue;
-        if constexpr (sizeof(T) == 4)
-          K_OK(fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes,
-                                ob, 0, k, src, vals, q.st));
-        else
-          K_OK(fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes, ob,
-                             0, k, src, vals, q.st));
-      }
-      if (!first && q.outs.size() == 1) HIP_OK(hipStreamWaitEvent(q.st, q.copied, 0));  // a lone rank
-      for (int c = 0; c < 6; ++c) std::swap(q.F[c].p, q.G[c].p);
-      // the neighbours have pulled the previous packs before these overwrite them
-      if (!first)
-        for (int d = 0; d < 27; ++d)
-          if (q.nb[d] >= 0) HIP_OK(hipStreamWaitEvent(q.st, R[q.nb[d]].copied, 0));
-      T* f[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
-      for (int d = 0; d < 27; ++d)
-        if (q.nb[d] >= 0) K_OK(box_pack(f, q.sbuf[d].p, 6, q.n[1], q.n[2], q.sbox[d], q.st));
-      HIP_OK(hipEventRecord(q.done, q.st));
+}
+
+// Phase 1 of a pass, every rank on its side stream: pull the neighbours'
+// packs of the previous pass (after their `done` and its own, which orders
+// the ghost writes after the passes that read them) and unpack them into the
+// ghosts
+template <typename T>
+void MultiRun<T>::pull_ghosts() {
+  for (int r = 0; r < P; ++r) {
+    XRank<T>& q = R[r];
+    HIP_OK(hipSetDevice(q.dev));
+    HIP_OK(hipStreamWaitEvent(q.side, q.done, 0));
+    T* f[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
+    for (int d = 0; d < 27; ++d) {
+      if (q.nb[d] < 0) continue;
+      const XRank<T>& o = R[q.nb[d]];
+      HIP_OK(hipStreamWaitEvent(q.side, o.done, 0));
+      // the neighbour at d packed its box for direction 26 - d (towards us)
+      const size_t bytes = q.rbuf[d].n * sizeof(T);
+      if (o.dev == q.dev)
+        HIP_OK(hipMemcpyAsync(q.rbuf[d].p, o.sbuf[26 - d].p, bytes, hipMemcpyDeviceToDevice, q.side));
+      else
+        HIP_OK(hipMemcpyPeerAsync(q.rbuf[d].p, q.dev, o.sbuf[26 - d].p, o.dev, bytes, q.side));
+      K_OK(box_unpack(f, q.rbuf[d].p, 6, q.n[1], q.n[2], q.rbox[d], q.side));
     }
-    first = false;
-  };
-  auto advance = [&](int t0, int n) {
-    int t = t0;
-    while (n > 0) {
-      const int k = std::min(TB, n);
-      pass(t, k);
-      t += k;
-      n -= k;
-    }
-  };
-  auto sync_all = [&]() {
-    for (int r = 0; r < P; ++r) {
-      HIP_OK(hipSetDevice(R[r].dev));
-      HIP_OK(hipStreamSynchronize(R[r].st));
-    }
-  };
-  const int steps = s.numTimeSteps;
-  const int warm = std::max(0, std::min(s.warmupSteps, steps));
-  advance(0, warm);
-  sync_all();
-  const auto c0 = std::chrono::steady_clock::now();
-  advance(warm, steps - warm);
-  sync_all();
-  HIP_OK(hipGetLastError());
-  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+    HIP_OK(hipEventRecord(q.copied, q.side));
+  }
+}
+
+// Phase 2 for one rank, on its main stream: the interior -- concurrent with
+// phase 1, it reads no ghost -- then, after the pulls, the shells, and the
+// packs for the next pass once the neighbours have pulled this pass's (their
+// `copied`)
+template <typename T>
+void MultiRun<T>::rank_pass(XRank<T>& q, int t, int k) {
+  HIP_OK(hipSetDevice(q.dev));
+  const T* ei[3] = {q.F[0].p, q.F[1].p, q.F[2].p};
+  const T* hi[3] = {q.F[3].p, q.F[4].p, q.F[5].p};
+  T* eo[3] = {q.G[0].p, q.G[1].p, q.G[2].p};
+  T* ho[3] = {q.G[3].p, q.G[4].p, q.G[5].p};
+  const T* cbs[3] = {q.C[0].p, q.C[1].p, q.C[2].p};
+  const T* dbs[3] = {nullptr, nullptr, nullptr};
+  // every rank whose allocated box (ghosts included) holds the source
+  // sets the hard source: a neighbour's redundant ghost levels need it
+  bool has = true;
+  for (int a = 0; a < 3; ++a) has = has && sp[a] >= q.g0[a] && sp[a] < q.g0[a] + q.n[a];
+  const int src[4] = {sp[0] - q.g0[0], sp[1] - q.g0[1], sp[2] - q.g0[2], has ? 2 : -1};
+  double vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int l = 0; l < k; ++l) vals[l] = src_val(t + l);
+  for (size_t b = 0; b < q.outs.size(); ++b) {
+    const int* ob = q.outs[b].data();
+    if (b == 1 && !first) HIP_OK(hipStreamWaitEvent(q.st, q.copied, 0));  // the shells read the fresh ghosts
+    if (ob[3] <= ob[0] || ob[4] <= ob[1] || ob[5] <= ob[2]) continue;
+    if constexpr (sizeof(T) == 4)
+      K_OK(fdtd_tb3d_v4_f32(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes, ob, 0,
+                            k, src, vals, q.st));
+    else
+      K_OK(fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, percell ? 1.0 : cb, db, q.n[0], q.n[1], q.n[2], q.boxes, ob, 0, k,
+                         src, vals, q.st));
+  }
+  if (!first && q.outs.size() == 1) HIP_OK(hipStreamWaitEvent(q.st, q.copied, 0));  // a lone rank
+  for (int c = 0; c < 6; ++c) std::swap(q.F[c].p, q.G[c].p);
+  // the neighbours have pulled the previous packs before these overwrite them
+  if (!first)
+    for (int d = 0; d < 27; ++d)
+      if (q.nb[d] >= 0) HIP_OK(hipStreamWaitEvent(q.st, R[q.nb[d]].copied, 0));
+  T* f[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
+  for (int d = 0; d < 27; ++d)
+    if (q.nb[d] >= 0) K_OK(box_pack(f, q.sbuf[d].p, 6, q.n[1], q.n[2], q.sbox[d], q.st));
+  HIP_OK(hipEventRecord(q.done, q.st));
+}
+
+// One pass of k steps: the phases are issued rank after rank on the host, so
+// every event waited on is already recorded.
+template <typename T>
+void MultiRun<T>::pass(int t, int k) {
+  if (!first) pull_ghosts();
+  for (int r = 0; r < P; ++r) rank_pass(R[r], t, k);
+  first = false;
+}
+
+template <typename T>
+void MultiRun<T>::advance(int t0, int n) {
+  int t = t0;
+  while (n > 0) {
+    const int k = std::min(TB, n);
+    pass(t, k);
+    t += k;
+    n -= k;
+  }
+}
+
+template <typename T>
+void MultiRun<T>::sync_all() {
+  for (int r = 0; r < P; ++r) {
+    HIP_OK(hipSetDevice(R[r].dev));
+    HIP_OK(hipStreamSynchronize(R[r].st));
+  }
+}
+
+template <typename T>
+void MultiRun<T>::report(double sec, int steps, int warm) const {
   const double cells = (double)N[0] * N[1] * N[2];
   const int timed = steps - warm;
   std::printf("Total time = %f seconds\n", sec);
@@ -338,34 +396,43 @@ int run_multi(const fdtd::Settings& s) {
   if (s.doPrintJson)
     std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f, \"ranks\": %d}\n", sec, timed,
                 cells * timed / sec / 1e6, P);
-  if (s.doSaveRes) {
-    const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
-    const size_t plane = (size_t)N[1] * N[2];
-    std::vector<T> host((size_t)N[0] * plane), loc;
-    for (int c = 0; c < 6; ++c) {
-      for (int r = 0; r < P; ++r) {
-        const XRank<T>& q = R[r];
-        HIP_OK(hipSetDevice(q.dev));
-        loc.resize(q.cells());
-        HIP_OK(hipMemcpy(loc.data(), q.F[c].p, loc.size() * sizeof(T), hipMemcpyDeviceToHost));
-        for (int i = q.lo[0]; i < q.hi[0]; ++i)
-          for (int j = q.lo[1]; j < q.hi[1]; ++j)
-            std::memcpy(host.data() + ((size_t)i * N[1] + j) * N[2] + q.lo[2],
-                        loc.data() + ((size_t)(i - q.g0[0]) * q.n[1] + (j - q.g0[1])) * q.n[2] + (q.lo[2] - q.g0[2]),
-                        (size_t)(q.hi[2] - q.lo[2]) * sizeof(T));
-      }
-      const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
-      if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), host.size() * sizeof(T));
-      if (s.saveAsBMP || !s.saveAsDAT) {
-        const int kz = N[2] / 2;
-        std::vector<double> v((size_t)N[0] * N[1]);
-        for (int i = 0; i < N[0]; ++i)
-          for (int j = 0; j < N[1]; ++j) v[(size_t)i * N[1] + j] = host[((size_t)i * N[1] + j) * N[2] + kz];
-        fdtd::write_bmp(base + std::to_string(kz) + "-Re.bmp", v, N[0], N[1], s.dumperPalette);
-      }
+}
+
+// --save-res: the owned blocks of every rank assembled into global DAT / BMP files
+template <typename T>
+void MultiRun<T>::save_results(int steps) {
+  if (!s.doSaveRes) return;
+  const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
+  const size_t plane = (size_t)N[1] * N[2];
+  std::vector<T> host((size_t)N[0] * plane), loc;
+  for (int c = 0; c < 6; ++c) {
+    for (int r = 0; r < P; ++r) {
+      const XRank<T>& q = R[r];
+      HIP_OK(hipSetDevice(q.dev));
+      loc.resize(q.cells());
+      HIP_OK(hipMemcpy(loc.data(), q.F[c].p, loc.size() * sizeof(T), hipMemcpyDeviceToHost));
+      for (int i = q.lo[0]; i < q.hi[0]; ++i)
+        for (int j = q.lo[1]; j < q.hi[1]; ++j)
+          std::memcpy(host.data() + ((size_t)i * N[1] + j) * N[2] + q.lo[2],
+                      loc.data() + ((size_t)(i - q.g0[0]) * q.n[1] + (j - q.g0[1])) * q.n[2] + (q.lo[2] - q.g0[2]),
+                      (size_t)(q.hi[2] - q.lo[2]) * sizeof(T));
+    }
+    const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
+    if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), host.size() * sizeof(T));
+    if (s.saveAsBMP || !s.saveAsDAT) {
+      const int kz = N[2] / 2;
+      std::vector<double> v((size_t)N[0] * N[1]);
+      for (int i = 0; i < N[0]; ++i)
+        for (int j = 0; j < N[1]; ++j) v[(size_t)i * N[1] + j] = host[((size_t)i * N[1] + j) * N[2] + kz];
+      fdtd::write_bmp(base + std::to_string(kz) + "-Re.bmp", v, N[0], N[1], s.dumperPalette);
     }
   }
+}
+
+template <typename T>
+void MultiRun<T>::release() {
   for (auto& q : R) {
+    if (!q.st) continue;
     HIP_OK(hipSetDevice(q.dev));
     for (int c = 0; c < 6; ++c) {  // freed with the rank's device current
       q.F[c].reset();
@@ -380,8 +447,34 @@ int run_multi(const fdtd::Settings& s) {
     HIP_OK(hipEventDestroy(q.copied));
     HIP_OK(hipStreamDestroy(q.st));
     HIP_OK(hipStreamDestroy(q.side));
+    q.st = nullptr;
   }
+}
+
+template <typename T>
+int MultiRun<T>::main() {
+  if (const int rc = plan_ranks()) return rc;
+  for (int r = 0; r < P; ++r) setup_rank(r);
+  enable_peers();
+  plan_outputs();
+  const int steps = s.numTimeSteps;
+  const int warm = std::max(0, std::min(s.warmupSteps, steps));
+  advance(0, warm);
+  sync_all();
+  const auto c0 = std::chrono::steady_clock::now();
+  advance(warm, steps - warm);
+  sync_all();
+  HIP_OK(hipGetLastError());
+  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+  report(sec, steps, warm);
+  save_results(steps);
   return 0;
+}
+
+template <typename T>
+int run_multi(const fdtd::Settings& s) {
+  MultiRun<T> m(s);
+  return m.main();
 }
 
 }  // namespace

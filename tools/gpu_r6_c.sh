@@ -1,13 +1,12 @@
 #!/bin/bash
-# Round 6 (c): non-dispersive UPML chain with one component per thread (k_chain3d_c, no SGPR spills) against
+# Round 6 (c): the whole GPU suite; non-dispersive UPML chain with one component per thread (k_chain3d_c, no SGPR spills) against
 # the three-component kernel (FDTD3D_CHAIN_SPLIT=0), alternating on one box; the UPML / Drude GPU tests
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r6c
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_hip_gpu.py tests/test_hybrid_gpu.py tests/test_drude_blk_gpu.py \
-  -k "upml or drude or chain" -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; tail -40 $O/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; grep -E "FAILED|Error" $O/tests.log | head -30; tail -5 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 DU="--3d --sizex 512 --same-size --dtype f32 --warmup-steps 12 --time-steps 40 --json --scene drude-sphere --use-metamaterials --use-pml --sphere-center-x 256 --sphere-center-y 256 --sphere-center-z 256 --sphere-radius 128"
 UT="--3d --sizex 512 --same-size --warmup-steps 10 --time-steps 30 --json --scene vacuum --use-pml --use-tfsf"
