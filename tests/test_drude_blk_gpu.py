@@ -21,10 +21,14 @@ CASES = [
     ("upml-T3", dict(use_pml=True, pml_size=(6, 6, 6)), 3, 17),
     # the box on the x = 0 face (grown by T it is clipped to the grid), off-centre in y / z
     ("face", dict(sphere_center=(8.5, 29.0, 61.0), sphere_radius=6.0), 5, 21),
-    # the reference's scattering scene: Drude sphere + UPML + TF/SF plane wave (faces in the blocked core),
-    # the sphere near the corner the wave enters by, its Drude launch's cone clear of the TF/SF faces
-    ("upml-tfsf", dict(use_pml=True, pml_size=(5, 5, 5), use_tfsf=True, tfsf_size=(9, 9, 9), theta=60.0, phi=20.0,
-                       psi=30.0, size=(96, 96, 100), sphere_center=(30.0, 30.0, 30.0), sphere_radius=6.0), 4, 60),
+    # the reference's scattering scene: Drude sphere + UPML + TF/SF plane wave; the sphere near the face the
+    # wave enters by, its Drude launch's cone clear of the TF/SF faces.  Incidence along x: the faces in the
+    # blocked core (in-kernel TF/SF); oblique: in the stepped shell
+    ("upml-tfsf", dict(use_pml=True, pml_size=(5, 5, 5), use_tfsf=True, tfsf_size=(9, 9, 9), size=(96, 96, 100),
+                       sphere_center=(30.0, 48.0, 50.0), sphere_radius=6.0), 4, 48),
+    ("upml-tfsf-oblique", dict(use_pml=True, pml_size=(5, 5, 5), use_tfsf=True, tfsf_size=(9, 9, 9), theta=60.0,
+                               phi=20.0, psi=30.0, size=(96, 96, 100), sphere_center=(30.0, 30.0, 30.0),
+                               sphere_radius=6.0), 4, 60),
     ("tfsf-nopml", dict(use_tfsf=True, tfsf_size=(10, 10, 10), sphere_center=(28.0, 36.0, 48.0), sphere_radius=6.0),
      4, 37),
 ]
@@ -50,7 +54,8 @@ def test_drude_blocked_gpu(gpu, name, extra, T, steps):
     assert blk.drude_blk is not None, "blocked Drude plan rejected"
     assert blk.ops.launches > 0
     if cfg.use_tfsf:
-        assert blk.hybrid is not None and blk.hybrid["drude"] and blk.hybrid["core_tfsf"]
+        assert blk.hybrid is not None and blk.hybrid["drude"]
+        assert blk.hybrid["core_tfsf"] == (not name.endswith("oblique")), blk.hybrid["core_tfsf"]
     st = _run(dataclasses.replace(cfg, blocked_drude="off", hybrid_block=1, time_block=1), "hip", gpu, torch.float32)
     assert st.drude_blk is None
     ref = _run(dataclasses.replace(cfg, blocked_drude="off", hybrid_block=1, time_block=1, dtype="f64"), "torch",
