@@ -97,8 +97,15 @@ def _empty(b: Box) -> bool:
     return any(b[1][d] <= b[0][d] for d in range(3))
 
 
+# a CPML term table with no slab (9 terms x 5 null pointers, 9 x 4 zero ranges): the
+# folded-CPML kernels then run the plain update
+_EMPTY_CPML = ((c_vp * 45)(), (c_int * 36)())
+
+
 class HipOps:
     name = "hip"
+    # fp64 3D split updates on the double4 lanes of yee3d_cpml.hip (FDTD3D_F64_V4=0: the scalar kernels)
+    f64_v4 = os.environ.get("FDTD3D_F64_V4", "1") != "0"
 
     def __init__(self, layout: Optional[YeeLayout], device, dtype, xchunk: int = 0, vec4: bool = True):
         self.vec4 = vec4
@@ -224,9 +231,6 @@ class HipOps:
                 raise HipError("scalar coefficients must agree across components")
             bx = _box_arr([boxes[c] for c in names])
             base = "update_e3d" if kind == "E" else "update_h3d"
-            if self.vec4 and self.dtype == torch.float32 and shape[2] % 4 == 0:
-                base += "_v4"
-            fn = self.fn(base)
             per_p = [_ptr(p) if p is not None else None for p in per]
             if per[0] is not None:
                 scal_use = 1.0
@@ -234,8 +238,19 @@ class HipOps:
                 per_p = [_ptr(self._scaled_cell(cb[c])) for c in names]
             else:
                 scal_use = scal
-            rc = fn(*[_ptr(dst[c]) for c in names], *[_ptr(src[c]) for c in other], *per_p, c_double(scal_use),
-                    c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), bx, c_int(self.xchunk), st)
+            args = [*[_ptr(dst[c]) for c in names], *[_ptr(src[c]) for c in other], *per_p, c_double(scal_use),
+                    c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), bx, c_int(self.xchunk)]
+            if self.vec4 and self.dtype == torch.float64 and shape[2] % 4 == 0 and self.f64_v4:
+                # fp64: the 4-cell double4 lanes of yee3d_cpml.hip with an empty CPML
+                # table -- the plain update, with the thin-box lane layouts (a z-thin
+                # shell window runs 8- or 16-lane rows instead of idle 64-lane ones)
+                rc = self.fn(base + "_cpml_v4")(*args, _EMPTY_CPML[0], _EMPTY_CPML[1], st)
+                _check(rc, "update_%s3d" % kind.lower())
+                self.launches += 1
+                return
+            if self.vec4 and self.dtype == torch.float32 and shape[2] % 4 == 0:
+                base += "_v4"
+            rc = self.fn(base)(*args, st)
             _check(rc, "update_%s3d" % kind.lower())
             self.launches += 1
             return
