@@ -157,7 +157,113 @@ bool write_bmp(const std::string& path, const std::vector<double>& v, int w, int
   return (bool)f;
 }
 
+// ---- hybrid pass geometry ----
+namespace {
+bool empty6(const Box6& b) { return b[3] <= b[0] || b[4] <= b[1] || b[5] <= b[2]; }
+Box6 and6(const Box6& a, const Box6& b) {
+  Box6 r;
+  for (int d = 0; d < 3; ++d) {
+    r[d] = std::max(a[d], b[d]);
+    r[3 + d] = std::min(a[3 + d], b[3 + d]);
+  }
+  return r;
+}
+}  // namespace
+
+std::vector<Box6> box_minus6(const Box6& a, const Box6& b) {
+  std::vector<Box6> out;
+  const Box6 c = and6(a, b);
+  if (empty6(c)) {
+    if (!empty6(a)) out.push_back(a);
+    return out;
+  }
+  Box6 rest = a;
+  for (int d = 0; d < 3; ++d) {
+    if (rest[d] < c[d]) {
+      Box6 sl = rest;
+      sl[3 + d] = c[d];
+      out.push_back(sl);
+    }
+    if (c[3 + d] < rest[3 + d]) {
+      Box6 sl = rest;
+      sl[d] = c[3 + d];
+      out.push_back(sl);
+    }
+    rest[d] = c[d];
+    rest[3 + d] = c[3 + d];
+  }
+  return out;
+}
+
+bool hybrid_windows(const Box6& alloc, const Box6& K, const Box6& Dm, int T, const bool* act, const Int3& size,
+                    std::vector<std::vector<Box6>>& shells, std::vector<Box6>& copy) {
+  shells.assign(T, {});
+  copy.clear();
+  const bool cut = !empty6(Dm);
+  for (int s = 0; s < T; ++s) {
+    const int n = T - s;
+    // the core shrunk by n on the sides inside the domain (a side on the
+    // domain border has no shell beyond it)
+    Box6 Kd = K;
+    for (int d = 0; d < 3; ++d) {
+      if (!act[d]) continue;
+      if (Kd[d] > 0) Kd[d] += n;
+      if (Kd[3 + d] < size[d]) Kd[3 + d] -= n;
+    }
+    if (empty6(Kd)) return false;
+    shells[s] = box_minus6(alloc, Kd);
+    if (cut) {
+      Box6 g = Dm;
+      for (int d = 0; d < 3; ++d)
+        if (act[d]) {
+          g[d] -= n;
+          g[3 + d] += n;
+        }
+      const Box6 w = and6(g, Kd);
+      if (!empty6(w)) shells[s].push_back(w);
+    }
+  }
+  copy = box_minus6(alloc, K);
+  if (cut) {
+    const Box6 w = and6(Dm, alloc);
+    if (!empty6(w)) copy.push_back(w);
+  }
+  return true;
+}
+
 }  // namespace fdtd
+
+// C ABI used by the Python driver (models/blocking.py _hybrid_plan_m): the
+// hybrid pass geometry of fdtd::hybrid_windows, flattened as
+// [n_0, boxes of step 0 ..., ..., n_{T-1}, ..., n_copy, copy boxes ...] (six
+// ints lo[3] hi[3] per box).  Returns the ints written, -1 when a step's core
+// vanishes (no hybrid plan), -2 when `cap` is too small.
+extern "C" __attribute__((visibility("default"))) int fdtd_hybrid_windows(const int* alloc, const int* K,
+                                                                         const int* Dm, const int* size,
+                                                                         const int* act, int T, int* out, int cap) {
+  fdtd::Box6 a, k, dm;
+  for (int q = 0; q < 6; ++q) {
+    a[q] = alloc[q];
+    k[q] = K[q];
+    dm[q] = Dm[q];
+  }
+  const bool ac[3] = {act[0] != 0, act[1] != 0, act[2] != 0};
+  std::vector<std::vector<fdtd::Box6>> shells;
+  std::vector<fdtd::Box6> copy;
+  if (T < 1 || !fdtd::hybrid_windows(a, k, dm, T, ac, {size[0], size[1], size[2]}, shells, copy)) return -1;
+  int n = 0;
+  auto put = [&](const std::vector<fdtd::Box6>& v) {
+    if (n + 1 + 6 * (int)v.size() > cap) return false;
+    out[n++] = (int)v.size();
+    for (const auto& b : v)
+      for (int q = 0; q < 6; ++q) out[n++] = b[q];
+    return true;
+  };
+  for (const auto& v : shells)
+    if (!put(v)) return -2;
+  if (!put(copy)) return -2;
+  return n;
+}
 
 // C ABI used by the Python parity tests
 extern "C" __attribute__((visibility("default"))) void fdtd_optimal_topology(const int* size, int nprocs,

@@ -499,24 +499,22 @@ void NativeRun<T>::plan_hybrid3d(int T_h_req) {
   long long vol = 0;
   for (const IBox& b : cores) vol += b.volume();
   if (!(ok && vol >= (long long)cells / 4)) return;
+  // the shell windows of every step and the copy boxes: the one geometry the
+  // Python driver plans too (host_native.cpp fdtd::hybrid_windows)
+  auto b6 = [](const IBox& b) { return fdtd::Box6{b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2]}; };
+  auto ib = [](const fdtd::Box6& b) { return IBox{{b[0], b[1], b[2]}, {b[3], b[4], b[5]}}; };
+  const bool act[3] = {true, true, true};
+  std::vector<std::vector<fdtd::Box6>> shells;
+  std::vector<fdtd::Box6> copy;
+  if (!fdtd::hybrid_windows(b6(alloc), b6(K), b6(Dm), Th, act, N, shells, copy)) return;
   T_h = Th;
   hcores = cores;
   for (int q = 0; q < T_h; ++q) {
-    const IBox Kd = shrink_inner(K, T_h - q);
-    hshell[q] = box_minus(alloc, Kd);
-    if (!Dm.empty()) {
-      const IBox w = box_and(grow(Dm, T_h - q), Kd);
-      if (!w.empty()) hshell[q].push_back(w);
-    }
-    std::vector<IBox> keep;
-    for (const IBox& w : hshell[q])
-      if (!w.empty()) keep.push_back(w);
-    hshell[q] = keep;
+    hshell[q].clear();
+    for (const auto& w : shells[q]) hshell[q].push_back(ib(w));
   }
   hcopy.clear();
-  for (const IBox& b : box_minus(alloc, K))
-    if (!b.empty()) hcopy.push_back(b);
-  if (!Dm.empty()) hcopy.push_back(box_and(Dm, alloc));
+  for (const auto& w : copy) hcopy.push_back(ib(w));
   for (int c = 0; c < 6; ++c)
     if (present[c] && !G[c].p) G[c].alloc(cells);
 }

@@ -326,6 +326,14 @@ constexpr int MR_AUTO_ROWS = 2;
 int g_tb_mrows = 0;  // rows per wave of the multi-row kernel: 0 automatic, 1 = single-row kernel, 2 / 4
 
 const int kNoBox[6] = {0, 0, 0, 0, 0, 0};
+// amplitude-mode tile shape (tuning): 0 = 16 waves x 2 rows, 2 = 8 waves x 2 rows
+static int tb_amp_shape() {
+  static const int v = [] {
+    const char* e = getenv("FDTD3D_TB_AMP_SHAPE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 int g_tb_mr_shape = 0;  // plain multi-row kernel: 0 = 16 waves x 2 rows, 1 = 8 waves x 4 rows, 2 = 8 x 2
 int g_tb_dr_shape = 0;  // Drude variant: 0 = 8 waves x 2 rows, 1 = 16 waves x 1 row (both 16-row tiles)
 
@@ -350,8 +358,11 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
   }
   if (fx == 8) {
     if constexpr (T <= 3) {
-      // 16 waves x 2 rows; the 8 x 4 shape (tuning knob 1) needs 200-256 VGPRs
+      // 16 waves x 2 rows; the 8 x 4 shape (tuning knob 1) needs 200-256 VGPRs;
+      // 8 waves x 2 rows (FDTD3D_TB_AMP_SHAPE=2: 16-row tiles, up to 256
+      // VGPRs -- the 16 x 2 form caps at 128 and spills)
       if (g_tb_mr_shape == 1) return launch_tb_mr<T, 1, 4, 8, 8>(MR_ARGS);
+      if (tb_amp_shape() == 2) return launch_tb_mr<T, 1, 2, 8, 8>(MR_ARGS);
       return launch_tb_mr<T, 1, 2, 8>(MR_ARGS);
     }
     return (int)hipErrorInvalidValue;
@@ -387,10 +398,11 @@ int launch_tb_mr_sel(int fx, const float* const* ein, const float* const* hin, f
 int tb_mr_xchunk(int fx, const Box3& O, int steps) {
   const long long gz = cdiv(O.hi[2] - O.lo[2], 64 - 2 * steps);
   // (the Drude variant's tiles are 8 waves x 2 rows)
-  const bool rows16 = fx == 16 || (fx == 0 && g_tb_mr_shape == 2 && steps <= 5);
+  const bool amp16 = fx == 8 && g_tb_mr_shape != 1 && tb_amp_shape() == 2;
+  const bool rows16 = fx == 16 || amp16 || (fx == 0 && g_tb_mr_shape == 2 && steps <= 5);
   const long long gy = cdiv(O.hi[1] - O.lo[1], (rows16 ? 16 : TBW * 2) - 2 * steps);
   // the 8-wave shapes fit two workgroups per CU
-  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, (fx == 0 && g_tb_mr_shape >= 1) ? 2 : 1);
+  return pick_xchunk(gz * gy, O.hi[0] - O.lo[0], steps, ((fx == 0 && g_tb_mr_shape >= 1) || amp16) ? 2 : 1);
 }
 
 // multi-row pass (scalar lanes, 2 rows per wave): uniform media, sparse

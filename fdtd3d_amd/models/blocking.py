@@ -588,38 +588,17 @@ class BlockedStepping:
             # decomposed: each rank's core is its owned part of the global core
             couts = [box_intersect(b, dom.owned_global()) for b in couts]
             couts = [b for b in couts if not box_empty(b)]
-        def shrink_inner(b, n):
-            # shrink by n only the sides that lie inside the domain (a side
-            # on the domain border has no shell beyond it)
-            return (tuple(b[0][d] + (n if act[d] and b[0][d] > 0 else 0) for d in range(3)),
-                    tuple(b[1][d] - (n if act[d] and b[1][d] < size[d] else 0) for d in range(3)))
-
-        def shell_windows(d):
-            # everything but the core cells deeper than d inside it
-            Kd = shrink_inner(K, d)
-            if box_empty(Kd):
-                return None
-            ws = [b for b in box_subtract(alloc, Kd) if not box_empty(b)]
-            if Dm is not None and not box_empty(Dm):
-                inner = box_intersect(grow(Dm, d), Kd)
-                if not box_empty(inner):
-                    ws.append(inner)
-            return ws
-
         # step s of the pass (0-based) advances the shell plus a band T - s
         # deep into the core: the stale core beyond the band corrupts one
         # more band cell per step, so after step s the band is exact to depth
-        # T - 1 - s, and after the last step the shell itself (depth 0)
-        shells = [shell_windows(T - s) for s in range(T)]
-        if shells[0] is None:
+        # T - 1 - s, and after the last step the shell itself (depth 0).  The
+        # windows and the copy boxes come from the one geometry both drivers
+        # use (csrc/host_native.cpp fdtd::hybrid_windows)
+        from ..native import hybrid_windows
+        got = hybrid_windows(alloc, K, Dm if Dm is not None and not box_empty(Dm) else None, size, act, T)
+        if got is None:
             return None
-        copy_boxes = [b for b in box_subtract(alloc, K) if not box_empty(b)]
-        if Dm is not None and not box_empty(Dm):
-            # (a decomposed run's dispersive box can reach past this rank's
-            # allocation: clip before turning it into local slices)
-            dma = box_intersect(Dm, alloc)
-            if not box_empty(dma):
-                copy_boxes.append(dma)
+        shells, copy_boxes = got
         # TF/SF corrections once per half step, unless a component's TF/SF
         # targets reach into a UPML chain box (D-form corrections there)
         self._tfsf_once = bool(cfg.use_tfsf)

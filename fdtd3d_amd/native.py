@@ -32,6 +32,9 @@ def load_host_library(build_if_missing: bool = True) -> ctypes.CDLL:
                                           ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_int)]
     lib.fdtd_optimal_topology.restype = None
+    ip = ctypes.POINTER(ctypes.c_int)
+    lib.fdtd_hybrid_windows.argtypes = [ip, ip, ip, ip, ip, ctypes.c_int, ip, ctypes.c_int]
+    lib.fdtd_hybrid_windows.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -55,6 +58,41 @@ def optimal_topology(size: Sequence[int], nprocs: int, axes: Sequence[int] = (0,
     out = (ctypes.c_int * 3)()
     lib.fdtd_optimal_topology(s, nprocs, ax, len(axes), out)
     return tuple(out)
+
+
+def hybrid_windows(alloc, core, cut, size: Sequence[int], active: Sequence[bool], T: int):
+    """Geometry of a hybrid pass (``csrc/host_native.cpp`` ``fdtd::hybrid_windows``,
+    the plan the native driver uses too): per step s of the pass the stepped
+    shell's windows, and the boxes copied into the core pass's output
+    afterwards.  Boxes are ((lo), (hi)); ``cut`` is a box cut out of the core
+    and stepped with the shell (None: none).  None when a step's core
+    vanishes."""
+    lib = load_host_library()
+
+    def flat(b):
+        return (ctypes.c_int * 6)(*(list(b[0]) + list(b[1])))
+
+    none = ((0, 0, 0), (0, 0, 0))
+    cap = 6 * 16 * (T + 1) + T + 1
+    out = (ctypes.c_int * cap)()
+    n = lib.fdtd_hybrid_windows(flat(alloc), flat(core), flat(cut if cut is not None else none),
+                                (ctypes.c_int * 3)(*size), (ctypes.c_int * 3)(*[1 if a else 0 for a in active]),
+                                int(T), out, cap)
+    if n == -1:
+        return None
+    if n < 0:
+        raise RuntimeError("fdtd_hybrid_windows: output table too small")
+    vals, q, lists = list(out[:n]), 0, []
+    for _ in range(T + 1):
+        cnt = vals[q]
+        q += 1
+        boxes = []
+        for _ in range(cnt):
+            b = vals[q:q + 6]
+            q += 6
+            boxes.append((tuple(b[:3]), tuple(b[3:])))
+        lists.append(boxes)
+    return lists[:T], lists[T]
 
 
 def executable() -> str:
