@@ -14,7 +14,7 @@ and is decomposed over the GPUs (``--topology``: ``auto``, an axis set such as
 Every timed step is the full leapfrog: E and H updates of all cells, the hard
 source and (N>1) the RCCL halo exchange.  Several leapfrog steps run per HBM
 pass through the temporally blocked kernel (``csrc/yee3d_tb.hip``;
-automatic: 5 steps per pass on one and two GPUs, 4 on more); decomposed runs
+automatic: 5 steps per pass on one GPU, 4 on more); decomposed runs
 exchange T-deep ghosts with all face, edge and corner neighbours once per
 pass, overlapped with the interior pass.  A step count that is not a multiple
 of T ends with one shorter pass, so exactly K steps are timed.
@@ -93,9 +93,9 @@ def run_one(a, dtype_name: str, world: int, rank: int, device: str, backend: str
     T = a.time_block
     if T <= 0:
         # automatic (models/blocking.py auto_time_block; the torch backend
-        # rehearses the HIP rule): 5 steps per pass on one and two GPUs, 4 on
-        # more -- there the 5-deep ghosts and shells cost more than the saved
-        # HBM traffic
+        # rehearses the HIP rule): 5 steps per pass on one GPU, 4 on more --
+        # there the 5-deep ghosts and shells cost more than the saved HBM
+        # traffic (profiles/decomp_r6.md)
         T = auto_time_block("3d", dtype_name, "hip", False, world)
     cfg = SchemeConfig(scheme="3d", size=size, time_steps=a.steps, scene="vacuum", dtype=dtype_name,
                        use_pml=False, use_tfsf=False, use_fused=not a.split, time_block=T)

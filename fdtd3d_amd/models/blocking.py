@@ -40,9 +40,10 @@ TB2D_AUTO_STEPS_F64 = 7
 
 
 # automatic steps per pass of the fp32 3D blocked kernel: uniform media
-# (1024^3: T=5 281-289k vs T=4 260-263k Mcells/s on one GPU; decomposed over
-# more than two ranks T=4, whose ghosts and shells are thinner:
-# tools/decomp_cost.py 8 ranks T=4 229k vs T=5 221k per GPU).  Per-cell
+# (1024^3: T=5 281-289k vs T=4 260-263k Mcells/s on one GPU; decomposed
+# T=4, whose ghosts and shells are thinner: tools/decomp_cost.py at 1024^3,
+# profiles/decomp_r6.md -- 2 ranks 266-298k vs 261-263k, 4 ranks 232-249k vs
+# 225-238k, 8 ranks 240-246k vs 202-207k per GPU).  Per-cell
 # coefficients of one kind (dielectric or magnetic scenes) run the sparse
 # multi-row kernel with an LDS ring of coefficient planes (512^3 eps sphere:
 # T=3 160k, 4 188k, 5 203k Mcells/s); per-cell E AND H keep the planes in
@@ -81,7 +82,7 @@ def auto_time_block(scheme: str, dtype_name: str, backend: str, percell, world: 
         return F32_AUTO_STEPS_PERCELL_BOTH
     if tfsf:
         return F32_AUTO_STEPS_TFSF
-    return F32_AUTO_STEPS if world <= 2 else F32_AUTO_STEPS_MANY_RANKS
+    return F32_AUTO_STEPS if world <= 1 else F32_AUTO_STEPS_MANY_RANKS
 
 
 class PassTimer:

@@ -106,7 +106,7 @@ class SchemeConfig:
     time_block: int = 1                      # steps per HBM pass (temporal blocking, 3D vacuum/dielectric); 0 = auto
     hybrid_block: int = 0                    # PML / TF-SF / dispersive 3D runs: blocked core + stepped shell
     shell_streams: int = 0                   # hybrid shell: streams for the independent window launches (0 auto)
-    hybrid_graph: str = "auto"               # hybrid passes replayed from HIP graphs (auto / off)
+    hybrid_graph: str = "auto"               # 2D hybrid passes: auto (launch records) / graph (HIP graphs) / off
     hybrid_tfsf: str = "auto"                # hybrid + TF/SF: faces in the blocked core (auto / core) or the shell
     blocked_drude: str = "auto"              # Drude box inside the blocked passes: auto (HIP) / on / off
                                              # (0 = auto: 4 on the HIP fp32 path, 1 = off)
@@ -1702,6 +1702,8 @@ class YeeScheme(BlockedStepping):
         vals = torch.tensor([[self.source_value(t0 + i, p) for i in range(reps * G)] for p in range(self.planes)],
                             dtype=torch.float64)
         key = (P, T, self._state_order_key())
+        if getattr(self.cfg, "hybrid_graph", "auto") != "graph" and hasattr(self.ops, "record"):
+            return taken + self._hybrid_replay(reps, P, T, t0, vals, key)
         g = self.__dict__.get("_hgraph")
         if g is None or g["key"] != key or g["reps"] < reps:
             tab = torch.zeros((self.planes, reps * G), dtype=torch.float64, device=self.device)
@@ -1727,6 +1729,47 @@ class YeeScheme(BlockedStepping):
             g["graph"].replay()
         self.t = t0 + reps * G
         return taken + reps * G
+
+    def _hybrid_replay(self, reps: int, P: int, T: int, t0: int, vals: torch.Tensor, key: tuple) -> int:
+        """``reps`` times ``P`` hybrid passes from a launch record: the first
+        ``P`` passes run with the ops recording their library calls (one
+        stream, sources read from the device table through the counter, as a
+        graph would), the other repetitions re-issue the recorded calls from
+        a list (``HipOps.replay``) -- the kernels of a pass without the Python
+        planning around them.  Direct launches on the stream pipeline better
+        than a replayed HIP graph of the same ~80 small kernels a pass (2D
+        8192^2 CPML + TF/SF: the graph's GPU idled ~40% between its nodes,
+        profiles/graph2d_r6.md).  The record is kept while its buffers are
+        the current ones (:meth:`_state_order_key`) and its table is long
+        enough.  Returns the steps taken."""
+        G = P * T
+        r = self.__dict__.get("_hrec")
+        done = 0
+        if r is None or r["key"] != key or r["reps"] < reps:
+            tab = torch.zeros((self.planes, reps * G), dtype=torch.float64, device=self.device)
+            counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+            tab.copy_(vals)
+            rec = []
+            self._graph_src = (tab, counter, t0)
+            self._capturing = True  # one stream: no shell-stream forks (torch stream waits are not recorded)
+            self.ops.record(rec)
+            try:
+                for _ in range(P):
+                    self._hybrid_step(T)
+                self.ops.counter_add(counter, G)
+            finally:
+                self.ops.record(None)
+                self._graph_src = None
+                self._capturing = False
+            r = self._hrec = {"key": key, "reps": reps, "rec": rec, "tab": tab, "counter": counter}
+            done = 1
+        else:
+            r["tab"][:, :reps * G].copy_(vals)
+            r["counter"].zero_()
+        for _ in range(reps - done):
+            self.ops.replay(r["rec"])
+        self.t = t0 + reps * G
+        return reps * G
 
     def _resident_1d(self, n: int) -> None:
         """``n`` 1D steps in one launch per plane (ops.resident_1d): per-step

@@ -97,6 +97,39 @@ def _empty(b: Box) -> bool:
     return any(b[1][d] <= b[0][d] for d in range(3))
 
 
+class _RecFn:
+    """A ``libfdtd3d_hip`` entry point that, while its ops object records
+    (:meth:`HipOps.record`), also appends (function, arguments, returns a
+    status) to the record: every argument is already a ctypes value, so the
+    call replays as is."""
+    __slots__ = ("f", "ops", "status")
+
+    def __init__(self, f, ops, status):
+        self.f, self.ops, self.status = f, ops, status
+
+    def __call__(self, *args):
+        rec = self.ops._rec
+        if rec is not None:
+            rec.append((self.f, args, self.status))
+        return self.f(*args)
+
+
+class _LibProxy:
+    """``libfdtd3d_hip`` seen through :class:`_RecFn` wrappers."""
+
+    def __init__(self, lib, ops):
+        self._lib, self._ops, self._w = lib, ops, {}
+
+    def __getattr__(self, name):
+        w = self._w.get(name)
+        if w is None:
+            f = getattr(self._lib, name)
+            # the knob setters (fdtd_set_tb_*, ...) return void; everything else an hipError status
+            status = not (name.startswith("fdtd_set_") and not name.startswith("fdtd_set_value"))
+            w = self._w[name] = _RecFn(f, self._ops, status) if name.startswith("fdtd_") else f
+        return w
+
+
 # a CPML term table with no slab (9 terms x 5 null pointers, 9 x 4 zero ranges): the
 # folded-CPML kernels then run the plain update
 _EMPTY_CPML = ((c_vp * 45)(), (c_int * 36)())
@@ -104,8 +137,9 @@ _EMPTY_CPML = ((c_vp * 45)(), (c_int * 36)())
 
 class HipOps:
     name = "hip"
-    # fp64 3D split updates on the double4 lanes of yee3d_cpml.hip (FDTD3D_F64_V4=0: the scalar kernels)
-    f64_v4 = os.environ.get("FDTD3D_F64_V4", "1") != "0"
+    # fp64 3D split updates on the double4 lanes of yee3d_cpml.hip (FDTD3D_F64_V4=1): 512^3 stepped vacuum
+    # +6%, but the UPML shell windows -3% (profiles/fp64_physics_r6.md): off by default
+    f64_v4 = os.environ.get("FDTD3D_F64_V4", "0") == "1"
 
     def __init__(self, layout: Optional[YeeLayout], device, dtype, xchunk: int = 0, vec4: bool = True):
         self.vec4 = vec4
@@ -115,7 +149,8 @@ class HipOps:
             raise HipError("the HIP backend needs a GPU device, got %s" % self.device)
         self.dtype = dtype
         self.suf = {torch.float32: "f32", torch.float64: "f64"}[dtype]
-        self.lib = load_library()
+        self._rec = None
+        self.lib = _LibProxy(load_library(), self)
         self.xchunk = xchunk
         self._fn: Dict[str, object] = {}
         self.launches = 0
@@ -124,9 +159,27 @@ class HipOps:
         f = self._fn.get(name)
         if f is None:
             f = getattr(self.lib, "fdtd_%s_%s" % (name, self.suf))
-            f.restype = c_int
+            f.f.restype = c_int
             self._fn[name] = f
         return f
+
+    # ------------------------------------------------------------ launch records
+    def record(self, rec: Optional[list]) -> None:
+        """Start (a list) / stop (None) recording every library call: the
+        calls still run; :meth:`replay` re-issues the recorded ones.  Only
+        kernel launches through this object are recorded -- the recorded
+        section must not depend on torch operations."""
+        self._rec = rec
+
+    @staticmethod
+    def replay(rec: list) -> None:
+        """Re-issue recorded library calls in order, as recorded (pointers,
+        boxes and the stream are baked into the arguments): a pass's launches
+        straight from a list, without the Python planning around them."""
+        for f, args, status in rec:
+            rc = f(*args)
+            if status and rc:
+                raise HipError("replayed launch failed: hipError %d" % rc)
 
     # ------------------------------------------------------------ validation
     def _check_tensor(self, t: torch.Tensor, shape=None) -> None:

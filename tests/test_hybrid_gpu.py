@@ -58,6 +58,10 @@ CASES = [
                                  scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=30), 5, 37),
     ("tez-upml-tfsf-graph", dict(scheme="tez", size=(96, 128, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
                                  scene="vacuum", use_pml=True, use_tfsf=True, phi=60), 4, 30),
+    # the same passes replayed from HIP graphs (--hybrid-graph graph) instead of launch records
+    ("tmz-cpml-tfsf-hipgraph", dict(scheme="tmz", size=(120, 104, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1),
+                                    scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=30,
+                                    hybrid_graph="graph"), 5, 37),
     # the shell's window launches run on several streams (--shell-streams auto = 3); the in-order single-stream
     # form stays covered
     ("cpml-tfsf-inorder", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10, psi=5,
@@ -88,6 +92,8 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
     hy = _run(dataclasses.replace(cfg, hybrid_block=T), "hip", gpu, dt)
     assert hy.hybrid is not None, "hybrid plan rejected"
     if name.endswith("-graph"):
+        assert getattr(hy, "_hrec", None) is not None, "no launch-record replay"
+    if name.endswith("-hipgraph"):
         assert getattr(hy, "_hgraph", None) is not None, "no graph replay"
     if name.endswith("-core"):
         assert hy.hybrid["core_tfsf"], "TF/SF faces not in the blocked core"
@@ -191,24 +197,27 @@ def test_hybrid_at_scale(gpu, name, extra):
     torch.cuda.empty_cache()
 
 
-def test_hybrid_graph_reuse_across_advance(gpu):
-    """2D UPML hybrid passes replayed from a HIP graph over TWO ``advance``
-    calls: T = 4, 25 steps end on a tail of one 4-step and one
-    1-step pass, so the field buffers are back in the captured parity while
-    the UPML D level lists are rotated by an odd number of steps.  The second
-    call (30 steps) must recapture rather than replay a graph that reads the
-    stale level -- the result equals the stepped run."""
+@pytest.mark.parametrize("mode,attr", [("auto", "_hrec"), ("graph", "_hgraph")])
+def test_hybrid_graph_reuse_across_advance(gpu, mode, attr):
+    """2D UPML hybrid passes replayed from a launch record (auto) / a HIP
+    graph over TWO ``advance`` calls: T = 4, 25 steps end on a
+    tail of one 4-step and one 1-step pass, so the field buffers are back in
+    the recorded parity while the UPML D level lists are rotated by an odd
+    number of steps.  The second call (30 steps) must re-record rather than
+    replay launches that read the stale level -- the result equals the
+    stepped run."""
     cfg = SchemeConfig(scheme="tez", size=(96, 128, 1), pml_size=(6, 6, 1), tfsf_size=(10, 10, 1), dtype="f32",
-                       scene="vacuum", use_pml=True, use_tfsf=True, phi=60, time_steps=55, hybrid_block=4)
+                       scene="vacuum", use_pml=True, use_tfsf=True, phi=60, time_steps=55, hybrid_block=4,
+                       hybrid_graph=mode)
     hy = YeeScheme(cfg, make_ops("hip", None, gpu, torch.float32))
     hy.init_scheme()
     hy.init_grids()
     assert hy.hybrid is not None and hy.hybrid["T"] == 4
     hy.advance(25)
-    k1 = hy._hgraph["key"] if getattr(hy, "_hgraph", None) else None
+    k1 = getattr(hy, attr)["key"] if getattr(hy, attr, None) else None
     hy.advance(30)
     torch.cuda.synchronize()
-    assert k1 is not None and hy._hgraph["key"] != k1, "graph not recaptured after the level lists rotated"
+    assert k1 is not None and getattr(hy, attr)["key"] != k1, "not re-recorded after the level lists rotated"
     st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, torch.float32)
     for c in st.comps:
         b = st.F[0][c].double().cpu()

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 6 (g): 2D hybrid passes re-issued from launch records (default) vs HIP graphs vs planned every pass;
+# the hybrid GPU tests
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r6g
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_hybrid_gpu.py -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; grep -E "FAILED|Error" $O/tests.log | head -20; tail -5 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for cfg in "tmz_cpml:--2d --sizex 8192 --sizey 8192 --use-pml --pml-type cpml --use-tfsf" "tmz_upml:--2d --sizex 8192 --sizey 8192 --use-pml --use-tfsf" "tez_cpml:--2d --2d-mode tez --sizex 8192 --sizey 8192 --use-pml --pml-type cpml --use-tfsf"; do
+  lab=${cfg%%:*}; args=${cfg#*:}
+  for rep in 1 2; do
+    for m in auto graph off; do
+      timeout -k 10 200 python3 -m fdtd3d_amd $args --time-steps 224 --warmup-steps 14 --scene vacuum --dtype f32 --json --hybrid-graph $m > $O/${lab}_$m.log 2>&1 || { echo "$lab $m failed"; tail -3 $O/${lab}_$m.log; exit 1; }
+    done
+    timeout -k 10 200 ./fdtd3d_amd/fdtd3d $args --time-steps 224 --warmup-steps 14 --scene vacuum --dtype f32 --json > $O/${lab}_native.log 2>&1 || { echo "$lab native failed"; exit 1; }
+    echo "$lab rep $rep: record $(grep -o '"mcells_per_s": [0-9.]*' $O/${lab}_auto.log | cut -d' ' -f2)  graph $(grep -o '"mcells_per_s": [0-9.]*' $O/${lab}_graph.log | cut -d' ' -f2)  off $(grep -o '"mcells_per_s": [0-9.]*' $O/${lab}_off.log | cut -d' ' -f2)  native $(grep -o '"mcells_per_s": [0-9.]*' $O/${lab}_native.log | cut -d' ' -f2)"
+  done
+done
