@@ -138,7 +138,7 @@ _EMPTY_CPML = ((c_vp * 45)(), (c_int * 36)())
 class HipOps:
     name = "hip"
     # fp64 3D split updates on the double4 lanes of yee3d_cpml.hip (FDTD3D_F64_V4=1): 512^3 stepped vacuum
-    # +6%, but the UPML shell windows -3% (profiles/fp64_physics_r6.md): off by default
+    # +6%, but the UPML shell windows -3% (profiles/physics_r6.md): off by default
     f64_v4 = os.environ.get("FDTD3D_F64_V4", "0") == "1"
 
     def __init__(self, layout: Optional[YeeLayout], device, dtype, xchunk: int = 0, vec4: bool = True):
