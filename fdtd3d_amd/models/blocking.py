@@ -136,6 +136,7 @@ class BlockedStepping:
     _tfsf_once = False
     drude_blk = None   # the Drude box inside the blocked passes (_plan_drude_blk), None: off
     _drude_plan = None
+    _drude_glob = None  # (T, global Drude box) of the pass form every rank takes (None: off)
     pass_timer = None  # PassTimer of decomposed passes (bench.py / --json), None: off
     _skip_side_wait = False  # tests only: drop the main stream's wait on the exchange (negative control)
 
@@ -174,12 +175,17 @@ class BlockedStepping:
         state -- (delta = D - Dp, Ep) per E component -- once per pass.  The
         stepped chain never runs on the box (the hybrid's shell keeps the
         absorbing layers only).  Returns the plan (T, box, tables) or None:
-        serial 3D runs of an electric Drude medium with uniform eps / gamma
+        3D runs of an electric Drude medium with uniform eps / gamma
         (coefficient tuples in a table of <= 256 rows per component), the box
         in the sigma = 0 region, TF/SF targets (if any) clear of the Drude
         launch's cone, no amplitude mode or complex fields;
         ``--blocked-drude off`` (or one step per pass) keeps the stepped
-        dispersive box.  Reference: Scheme3D.cpp:266-416, Kernels.h:103-107."""
+        dispersive box.  Decomposed runs: T is the ghost depth, every rank
+        plans the global box clipped to its allocation (its state joins the
+        deep exchange), and the ranks vote -- one rank's refusal keeps the
+        stepped box everywhere.  Reference: Scheme3D.cpp:266-416,
+        Kernels.h:103-107; the MPI counterpart shares D1 / B1 on
+        nextTimeStep, Scheme3D.h:161-222."""
         cfg = self.cfg
         mode = getattr(cfg, "blocked_drude", "auto")
         if (mode == "off" or not cfg.use_metamaterials or cfg.scheme != "3d" or not hasattr(self.ops, "tb_drude_step")
@@ -187,7 +193,7 @@ class BlockedStepping:
             return None
         if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
             return None
-        if (self.halo is not None or self.planes != 1 or cfg.use_amp_mode or self.graph_mode
+        if (self.planes != 1 or cfg.use_amp_mode or self.graph_mode
                 or not self.use_upml_chain or getattr(self, "chain_regions", None) is None or self.use_cpml
                 or getattr(cfg, "dispersion", "drude") != "drude" or self.hooks):
             return None
@@ -198,30 +204,61 @@ class BlockedStepping:
         T = int(cfg.hybrid_block) if int(cfg.hybrid_block) > 0 else int(cfg.time_block)
         if T <= 0:
             T = DRUDE_AUTO_STEPS
+        if self.halo is not None:
+            T = self.domain.buffer_size  # one T-deep exchange per pass
         T = min(T, int(getattr(self.ops, "tb_drude_max_steps", 5)))
-        if T <= 1:
+        if T <= 1 or (self.halo is not None and T != self.domain.buffer_size):
             return None
+        G = self._drude_gbox()
+        if G is None:
+            return None
+        plan = self._plan_drude_local(T, G)
+        if self.halo is not None:
+            # every rank takes the pass or none does (False: this rank refused); a rank whose
+            # allocation misses the box (None) runs the same pass plan without a Drude launch
+            if self.halo.allreduce_max(1.0 if plan is False else 0.0) > 0:
+                return None
+        elif not plan:
+            return None
+        self._drude_glob = (T, G)
+        return plan if plan else None
+
+    def _drude_gbox(self):
+        """Bounding box of the E components' global dispersive boxes (the
+        same on every rank), None without one."""
+        G = None
+        for c in self.e_comps:
+            if "D1" in self.upml[c] and not box_empty(self._disp_box(c)):
+                g = self._disp_box(c)
+                G = g if G is None else (tuple(min(G[0][d], g[0][d]) for d in range(3)),
+                                         tuple(max(G[1][d], g[1][d]) for d in range(3)))
+        return G
+
+    def _plan_drude_local(self, T: int, G):
+        """This rank's part of :meth:`_plan_drude_blk` for the global box
+        ``G``: the plan, None (``G`` misses this rank's allocation) or False
+        (refused).  The rank's box is ``G`` clipped to its allocation, so the
+        boxed state messages of two neighbours cover the same cells."""
+        cfg = self.cfg
         dom = self.domain
         alloc = dom.allocated_global()
-        store, B = {}, None
+        B = box_intersect(G, alloc)
+        if box_empty(B):
+            return None
+        store = {}
         for c in self.e_comps:
-            S = self._bbox_global(self.upml[c].get("drude_active")) if "D1" in self.upml[c] else None
+            S = box_intersect(self._disp_box(c), alloc) if "D1" in self.upml[c] else None
             if S is not None and box_empty(S):
                 S = None
             store[c] = S
-            if S is not None:
-                B = S if B is None else (tuple(min(B[0][d], S[0][d]) for d in range(3)),
-                                         tuple(max(B[1][d], S[1][d]) for d in range(3)))
-        if B is None:
-            return None
         for c in self.e_comps:
             sig0 = self._chain_sigma0.get(c)
             ub = self._global_box(c)
             for d in range(3):
                 if sig0 is None or B[0][d] < sig0[0][d] or B[1][d] > sig0[1][d]:
-                    return None  # the box reaches into an absorbing layer
+                    return False  # the box reaches into an absorbing layer
                 if B[0][d] < ub[0][d] or B[1][d] > ub[1][d]:
-                    return None
+                    return False
         Bl = dom.to_local(B)
         if cfg.use_tfsf:
             # a scattering scene (reference Scheme3D.cpp:3452-3492 with :138-208): the Drude launch
@@ -232,7 +269,7 @@ class BlockedStepping:
             reach = 2 * T + 2
             cone = (tuple(Bl[0][d] - reach for d in range(3)), tuple(Bl[1][d] + reach for d in range(3)))
             if getattr(self, "tfsf", None) is None or self._tfsf_targets_in(cone):
-                return None
+                return False
         bshape = tuple(Bl[1][d] - Bl[0][d] for d in range(3))
         # D coefficient where sigma = 0 (the chain's cbD profile), the same for the three components
         cbd = None
@@ -241,11 +278,11 @@ class BlockedStepping:
             aD = pr["axes"][0]
             v = pr["cbD"][Bl[0][aD]:Bl[1][aD]].double()
             if bool((v != v[0]).any()):
-                return None
+                return False
             if cbd is None:
                 cbd = float(v[0])
             elif abs(float(v[0]) - cbd) > 1e-6 * abs(cbd):
-                return None
+                return False
         # per component: material index over B into (b0 cbd, b2, m1, m2) rows; cells outside the
         # component's own dispersive box take the plain row (cb, 0, 1, 0): E' = E + cb curl
         ids4 = torch.zeros(bshape, dtype=torch.int32, device=self.device)
@@ -272,10 +309,10 @@ class BlockedStepping:
                 ids_s = inv.reshape(cells.shape[:3]).to(torch.int32)
             b0, b1, b2, m1, m2 = (tab[:, k] for k in range(5))
             if bool(((b0 + b1 + b2).abs() > 1e-5 * (b0.abs() + b1.abs() + b2.abs())).any()):
-                return None  # not the Drude ADE (b1 = -(b0 + b2))
+                return False  # not the Drude ADE (b1 = -(b0 + b2))
             nid = tab.shape[0]
             if nid + 1 > 256:
-                return None
+                return False
             r = torch.stack([b0 * cbd, b2, m1, m2], 1)
             rows.append(torch.cat([r, torch.tensor([plain], dtype=torch.float64)]))
             # non-dispersive cells take the plain row too: the stepped chain runs the plain update
@@ -289,6 +326,7 @@ class BlockedStepping:
         lut = torch.zeros(3, nid, 4, dtype=torch.float64)
         for q, r in enumerate(rows):
             lut[q, :r.shape[0]] = r
+        # gbox: this rank's box (the global box clipped to its allocation)
         return {"T": T, "box": Bl, "gbox": B, "store": store, "ids": ids4, "cbd": cbd,
                 "lut": lut.to(device=self.device, dtype=torch.float32 if self.ops.name == "hip" else self.dtype)
                 .contiguous()}
@@ -363,12 +401,24 @@ class BlockedStepping:
         """The Drude launch of a pass (after the core's plain launch, before
         the hybrid shell steps F in place): output = the box grown by T."""
         db = self.drude_blk
+        if db is None:
+            return  # decomposed: the box misses this rank
         self._drude_blk_import()
         Bl = db["box"]
         shape = self.domain.shape
         ob = (tuple(max(0, Bl[0][d] - T) for d in range(3)), tuple(min(shape[d], Bl[1][d] + T) for d in range(3)))
         upd = {c: self.local_box(c, self.domain.allocated_global()) for c in self.comps}
         sin, sout = db["state"][db["cur"]], db["state"][1 - db["cur"]]
+        if self.halo is not None:
+            # decomposed (after the exchange and every plain launch of the pass): this rank's owned
+            # cells only; the ghost state came from the neighbours with THEIR material ids in .w
+            # (fp32 state): this rank's ids back in
+            ob = box_intersect(ob, self.domain.to_local(self.domain.owned_global()))
+            if sin[0].dtype == torch.float32:
+                sin[0][..., 3] = db["ids"].view(torch.float32)
+            if box_empty(ob):
+                db["cur"] ^= 1
+                return
         with self.prof.phase("blocked-drude"):
             self.ops.tb_drude_step(self.F[0], self.F_alt[0], upd, ob, self.cb, T, srcs[0],
                                    {"box": Bl, "sin": sin, "sout": sout, "lut": db["lut"], "cbd": db["cbd"],
@@ -402,16 +452,18 @@ class BlockedStepping:
                 H = TB2D_AUTO_STEPS if self.dtype == torch.float32 else TB2D_AUTO_STEPS_F64
             else:
                 H = HYBRID_AUTO_STEPS if self.dtype == torch.float32 else F64_AUTO_STEPS
+                if self.halo is not None:
+                    H = self.domain.buffer_size  # decomposed: one pass per ghost exchange, every rank alike
         hmax = getattr(self.ops, "tb2d_max_steps" if two_d else "tb_max_steps", 8 if two_d else 6)
-        dp = self._drude_plan
-        if dp is not None and not self.fused and self.tb == 1 and dp["T"] <= hmax:
+        dg = self._drude_glob
+        if dg is not None and not self.fused and self.tb == 1 and dg[0] <= hmax:
             if not (cfg.use_pml or cfg.use_tfsf):
                 # no absorbing layer: plain blocked passes over the whole grid + the Drude pass
-                self.tb = dp["T"]
+                self.tb = dg[0]
                 if not hasattr(self, "F_alt"):
                     self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
                 return
-            H = dp["T"]
+            H = dg[0]
         if (H <= 1 or self.fused or self.tb > 1 or cfg.scheme not in ("3d", "tmz", "tez")
                 or not hasattr(self.ops, "tb_step") or cfg.use_amp_mode or self.graph_mode
                 or not (cfg.use_pml or cfg.use_tfsf or cfg.use_metamaterials) or H > hmax):
@@ -430,10 +482,10 @@ class BlockedStepping:
                 return
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
                 return
-        plan = self._hybrid_plan(H)
-        if plan is None and dp is not None:
-            self._drude_plan = dp = None  # the stepped dispersive box after all
-            plan = self._hybrid_plan(H)
+        plan = self._voted(self._hybrid_plan(H))
+        if plan is None and dg is not None:
+            self._drude_plan = self._drude_glob = dg = None  # the stepped dispersive box after all
+            plan = self._voted(self._hybrid_plan(H))
         if plan is None:
             return
         if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.5 * self.cells():
@@ -446,6 +498,14 @@ class BlockedStepping:
         if not hasattr(self, "F_alt"):
             self.F_alt = [{c: self._zeros() for c in self.comps} for _ in range(self.planes)]
         self.hybrid = plan
+
+    def _voted(self, plan):
+        """Decomposed: a hybrid plan only when every rank found one (the
+        checks near the TF/SF targets are local), so all ranks run the same
+        pass structure and exchanges."""
+        if self.halo is not None and self.halo.allreduce_max(1.0 if plan is None else 0.0) > 0:
+            return None
+        return plan
 
     def _tfsf_targets_in(self, lbox: Box, outside: bool = False) -> bool:
         """True when some TF/SF target lies inside the local box (``outside``:
@@ -526,7 +586,7 @@ class BlockedStepping:
             return None
         # dispersive boxes (chain boxes off the domain border) are cut out of the core
         disp = []
-        dblk = self._drude_plan is not None and self._drude_plan["T"] == T
+        dblk = self._drude_glob is not None and self._drude_glob[0] == T
         if cfg.use_metamaterials and self.use_upml_chain and not dblk:
             for c in self.comps:
                 b = self._bbox_global(self.upml[c].get("drude_active"))
@@ -581,7 +641,7 @@ class BlockedStepping:
                 return None
         if dblk:
             # the Drude pass's output (the box grown by T) must lie inside the one core box
-            gb = self._drude_plan["gbox"]
+            gb = self._drude_glob[1]
             if len(couts) != 1 or any(gb[0][d] - T < couts[0][0][d] or gb[1][d] + T > couts[0][1][d]
                                       for d in range(3) if act[d]):
                 return None
@@ -679,7 +739,7 @@ class BlockedStepping:
 
         with self.prof.phase("blocked-core"):
             core(core_now)
-        if hp.get("drude"):
+        if hp.get("drude") and self.halo is None:
             self._drude_pass(T, srcs)  # reads F: before the shell steps below advance it in place
         if self.halo is not None:
             self._mark("interior")
@@ -687,6 +747,8 @@ class BlockedStepping:
             self._mark("wait")
             with self.prof.phase("blocked-core"):
                 core(core_later)
+            if hp.get("drude"):
+                self._drude_pass(T, srcs)  # after the exchange (its cone reads ghosts), before the shell steps
         for s in range(T):
             self.step(hp["shells"][s])
         if self.halo is not None:
@@ -776,7 +838,7 @@ class BlockedStepping:
                         self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p], tfsf=tfs[p])
                     else:
                         self.ops.tb_step(self.F[p], self.F_alt[p], upd, outs[0], self.cb, T, srcs[p])
-        if self.drude_blk is not None:
+        if self.drude_blk is not None and self.halo is None:
             self._drude_pass(T, srcs)  # overwrites the box grown by T (run plain above)
         if self.halo is not None:
             self._mark("interior")
@@ -805,6 +867,8 @@ class BlockedStepping:
                 for ob in outs[1:]:
                     for p in range(self.planes):
                         shell(ob, p)
+            if self.drude_blk is not None:
+                self._drude_pass(T, srcs)  # its cone reads the fresh ghosts: after the exchange
             self._mark("end")
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]

@@ -398,13 +398,14 @@ class YeeScheme(BlockedStepping):
         if self.use_upml_chain:
             # after the chain boxes are final: region-local levels cover them
             self._alloc_upml_levels()
-        dp = self._drude_plan
-        if dp is not None:
+        dg = self._drude_glob  # every rank alike (decomposed: ranks the box misses have no local plan)
+        if dg is not None:
             if ((self.hybrid is not None and self.hybrid.get("drude"))
-                    or (self.hybrid is None and self.tb == dp["T"])):
-                self._finish_drude_blk()
+                    or (self.hybrid is None and self.tb == dg[0])):
+                if self._drude_plan is not None:
+                    self._finish_drude_blk()
             else:
-                self._drude_plan = None  # neither pass form took it: the stepped dispersive box
+                self._drude_plan = self._drude_glob = None  # neither pass form took it: the stepped dispersive box
                 self.__dict__.pop("_chain_plan_cache", None)
         # the eps-layout material grids (fp64, 8 B per cell and material) and
         # the averaged materials only feed the coefficients built above
@@ -801,6 +802,33 @@ class YeeScheme(BlockedStepping):
             hi.append(int(nzv.max()) + 1)
         return self.domain.to_global((tuple(lo), tuple(hi)))
 
+    def _disp_box(self, c: str) -> Box:
+        """Global bounding box of component ``c``'s dispersive cells over ALL
+        ranks (serial: the local box).  A rank's region-local arrays over it
+        (the dispersive chain box, the blocked Drude state) cover the box
+        clipped to the rank's allocation, so two neighbours agree on the cells
+        of every ghost message (a sphere's cap seen by one rank has a smaller
+        local bounding box than the sphere clipped to that rank).  Collective
+        on the first call per component (all ranks call it in init_grids),
+        cached after."""
+        cache = self.__dict__.setdefault("_disp_box_cache", {})
+        if c in cache:
+            return cache[c]
+        b = self._bbox_global(self.upml[c].get("drude_active")) if c in getattr(self, "upml", {}) else None
+        if b is None:
+            o = self.domain.origin
+            b = (o, o)
+        if self.halo is not None:
+            big = float(1 << 30)
+            e = box_empty(b)
+            vals = [-big if e else -float(b[0][d]) for d in range(3)] + [-big if e else float(b[1][d]) for d in range(3)]
+            r = [self.halo.allreduce_max(v) for v in vals]
+            lo, hi = tuple(int(-r[d]) for d in range(3)), tuple(int(r[3 + d]) for d in range(3))
+            o = self.domain.origin
+            b = (lo, hi) if all(hi[d] > lo[d] for d in range(3)) else (o, o)
+        cache[c] = b
+        return b
+
     def _init_chain_regions(self, prof, z_align: int = 1) -> None:
         """Region-local UPML/Drude chain (3D and 2D).  Where all sigma values
         of a component vanish and its Drude parameters are zero the chain is
@@ -844,7 +872,7 @@ class YeeScheme(BlockedStepping):
             if box_empty(I):
                 I = (C[0], C[0])
             sigma0[c] = I
-            Dbox = self._bbox_global(self.upml[c].get("drude_active"))
+            Dbox = box_intersect(self._disp_box(c), alloc)
             plain_core = I
             plain = box_subtract(plain_core, Dbox) if not box_empty(plain_core) else [(C[0], C[0])] * 6
             chain = box_subtract(C, plain_core) + [box_intersect(plain_core, Dbox)]
@@ -1371,6 +1399,12 @@ class YeeScheme(BlockedStepping):
                             out += list(t.data) if isinstance(t, RegionLevel) else [t]
             if self.use_cpml:
                 out += self.cpml.state_tensors(p)
+        db = self.drude_blk
+        if db is not None:
+            # the blocked Drude pass's current state set (float4 per box cell, seen
+            # as z x 4 floats; models/blocking.py _drude_pass)
+            s0, s1 = db["state"][db["cur"]]
+            out += [s0.view(s0.shape[0], s0.shape[1], -1), s1.view(s1.shape[0], s1.shape[1], -1)]
         return out
 
     def state_boxes(self) -> List[Optional[Tuple[Box, Tuple[int, int, int]]]]:
@@ -1391,6 +1425,10 @@ class YeeScheme(BlockedStepping):
                                 out.append(None)
             if self.use_cpml:
                 out += self.cpml.state_boxes(p)
+        db = self.drude_blk
+        if db is not None:
+            cover = self.domain.to_global(db["box"])
+            out += [(cover, db["box"][0], 4)] * 2  # (global box, local first index, z cells x 4 floats)
         return out
 
     def _apply_sources(self, t: int, p: int) -> None:

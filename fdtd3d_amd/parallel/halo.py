@@ -282,7 +282,9 @@ class HaloExchanger:
             sbox, rbox = d.to_local(sg), d.to_local(rg)
             key = (off[0] + 1) * 9 + (off[1] + 1) * 3 + (off[2] + 1)
             back = (-off[0] + 1) * 9 + (-off[1] + 1) * 3 + (-off[2] + 1)
-            if (off[1] == 0 and off[2] == 0 and not boxed and self.direct_x_faces
+            if (off[1] == 0 and off[2] == 0 and self.direct_x_faces
+                    and not any(_boxed_part(g, cover, first, d) is not None
+                                for g in (sg, rg) for _, cover, first, _ in boxed)
                     and all(t.is_contiguous() for t in tensors)):
                 # x faces: x is the slowest axis, so B whole allocated planes
                 # of an array are one contiguous slice -- sent from and received
@@ -290,7 +292,10 @@ class HaloExchanger:
                 # planes carry the sender's y / z ghost rows too; the edge and
                 # corner messages, unpacked after every transfer has landed,
                 # overwrite those parts of the receiver's ghost planes (peers of
-                # one rank column share the allocated y / z extents).
+                # one rank column share the allocated y / z extents).  Only when
+                # no boxed array reaches either face (the same test on both
+                # peers: a boxed array covers one global box clipped to each
+                # rank's allocation).
                 for i, t in enumerate(tensors):
                     ops_list.append(P2P(True, t[sbox[0][0]:sbox[1][0]], peer, 1000 + 32 * i + key))
                     ops_list.append(P2P(False, t[rbox[0][0]:rbox[1][0]], peer, 1000 + 32 * i + back))
@@ -393,38 +398,43 @@ def _pack_many(ops, tensors, box, buf):
 
 def _split_state(scheme):
     """(arrays of the local field shape, [(array, global box it covers, local
-    index of its first element)]) of the scheme's state."""
+    index of its first element, values per cell along z)]) of the scheme's
+    state."""
     ts = scheme.state_tensors()
     bx = scheme.state_boxes() if hasattr(scheme, "state_boxes") else [None] * len(ts)
     full = [t for t, b in zip(ts, bx) if b is None]
-    boxed = [(t, b[0], b[1]) for t, b in zip(ts, bx) if b is not None]
+    boxed = [(t, b[0], b[1], b[2] if len(b) > 2 else 1) for t, b in zip(ts, bx) if b is not None]
     return full, boxed
 
 
-def _boxed_part(g: Box, cover: Box, first, d):
+def _boxed_part(g: Box, cover: Box, first, d, zmul: int = 1):
     """Local box inside a boxed array (first element at local ``first``) of
-    the global message box ``g`` clipped to the array's global ``cover``."""
+    the global message box ``g`` clipped to the array's global ``cover``
+    (``zmul`` values per cell along z: a vector array seen as scalars)."""
     from .domain import box_intersect
     c = box_intersect(g, cover)
     if any(c[1][a] <= c[0][a] for a in range(3)):
         return None
     lc = d.to_local(c)
-    return (tuple(lc[0][a] - first[a] for a in range(3)), tuple(lc[1][a] - first[a] for a in range(3)))
+    lo = [lc[0][a] - first[a] for a in range(3)]
+    hi = [lc[1][a] - first[a] for a in range(3)]
+    lo[2], hi[2] = lo[2] * zmul, hi[2] * zmul
+    return tuple(lo), tuple(hi)
 
 
 def _msg_len(full, boxed, g) -> int:
     n = _vol(g) * len(full)
-    for t, cover, first in boxed:
+    for t, cover, first, zmul in boxed:
         from .domain import box_intersect
-        n += _vol(box_intersect(g, cover))
+        n += _vol(box_intersect(g, cover)) * zmul
     return n
 
 
 def _pack_state(ops, full, boxed, lbox, g, d, buf):
     n = _vol(lbox) * len(full)
     _pack_many(ops, full, lbox, buf[:n])
-    for t, cover, first in boxed:
-        b = _boxed_part(g, cover, first, d)
+    for t, cover, first, zmul in boxed:
+        b = _boxed_part(g, cover, first, d, zmul)
         if b is None:
             continue
         m = _vol(b)
@@ -435,8 +445,8 @@ def _pack_state(ops, full, boxed, lbox, g, d, buf):
 def _unpack_state(ops, full, boxed, lbox, g, d, buf):
     n = _vol(lbox) * len(full)
     _unpack_many(ops, full, lbox, buf[:n])
-    for t, cover, first in boxed:
-        b = _boxed_part(g, cover, first, d)
+    for t, cover, first, zmul in boxed:
+        b = _boxed_part(g, cover, first, d, zmul)
         if b is None:
             continue
         m = _vol(b)

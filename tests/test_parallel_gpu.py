@@ -24,13 +24,14 @@ pytestmark = pytest.mark.gpu
 
 
 def run_threads(cfg, world, axes, buf, device, delay_cycles=0, skip_side_wait=False, split=None,
-                random_init=False):
+                random_init=False, check=None):
     """Decomposed run with one thread per rank, each on its OWN main stream
     (like one process per GPU): the in-process transport orders streams with
     events only, so every cross-stream dependency must be explicit.
     ``delay_cycles`` holds every ghost unpack back on the exchange stream;
     ``skip_side_wait`` drops the main stream's wait on it (negative control);
-    ``split`` = (steps, ...) runs perform_steps in pieces (passes cut short)."""
+    ``split`` = (steps, ...) runs perform_steps in pieces (passes cut short);
+    ``check(scheme)`` runs on every rank before the steps."""
     core = ParallelGridCore.create(cfg.size, world, axes, active_axes=(0, 1, 2) if cfg.scheme == "3d" else (0, 1))
     hub = LocalHub(world)
     dt = torch.float32 if cfg.dtype == "f32" else torch.float64
@@ -57,6 +58,8 @@ def run_threads(cfg, world, axes, buf, device, delay_cycles=0, skip_side_wait=Fa
                     assert s.tb == (buf if cfg.time_block == 0 else max(1, cfg.time_block))
                 if random_init:
                     s.randomize_fields()
+                if check is not None:
+                    check(s)
                 if split:
                     for n in split:
                         s.perform_steps(n)
@@ -197,3 +200,38 @@ def test_gpu_hybrid_split_passes(gpu):
     s = _serial(cfg, gpu, random_init=True)
     par = run_threads(cfg, world, axes, buf, gpu, split=(2, 4, 3, 1), random_init=True)
     assert _max_rel_err(par, s) <= 1e-5
+
+
+DRUDE = dict(scheme="3d", dtype="f32", scene="drude-sphere", use_metamaterials=True, use_fused=True,
+             blocked_drude="on")
+DRUDE_CASES = [
+    # plain blocked passes + the Drude pass, the sphere across the x / y rank borders
+    ("drude-tb4-xy4", SchemeConfig(size=(80, 72, 96), time_steps=23, sphere_center=(40.0, 36.0, 48.0),
+                                   sphere_radius=9.0, time_block=4, **DRUDE), 4, "xy", 4),
+    # the reference's scattering scene (Drude sphere + UPML + TF/SF, incidence along x: the faces in the
+    # blocked core) on hybrid passes; the sphere across the y border, inside the x = 0..48 ranks
+    ("drude-upml-tfsf-xy4", SchemeConfig(size=(96, 96, 100), time_steps=48, sphere_center=(30.0, 48.0, 50.0),
+                                         sphere_radius=6.0, use_pml=True, pml_size=(5, 5, 5), use_tfsf=True,
+                                         tfsf_size=(9, 9, 9), hybrid_block=4, time_block=4, **DRUDE), 4, "xy", 4),
+]
+
+
+@pytest.mark.parametrize("name,cfg,world,axes,buf", DRUDE_CASES, ids=[c[0] for c in DRUDE_CASES])
+def test_gpu_decomposed_drude_blocked(gpu, name, cfg, world, axes, buf):
+    """The Drude box inside decomposed blocked / hybrid passes (its state in
+    the deep exchange, the pass after the exchange join) on the HIP kernels:
+    equals the serial blocked run and the serial stepped chain."""
+    seen = []
+
+    def check(s):
+        seen.append((s.drude_blk is not None, s._drude_glob is not None))
+
+    par = run_threads(cfg, world, axes, buf, gpu, check=check)
+    assert all(g for _, g in seen) and any(d for d, _ in seen), seen
+    import dataclasses
+    blk = _serial(cfg, gpu)
+    assert blk.drude_blk is not None
+    st = _serial(dataclasses.replace(cfg, blocked_drude="off", hybrid_block=1, time_block=1, use_fused=False), gpu)
+    assert st.drude_blk is None
+    assert _max_rel_err(par, blk) <= 5e-6, name
+    assert _max_rel_err(par, st) <= 2e-5, name

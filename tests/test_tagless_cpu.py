@@ -10,7 +10,9 @@ equal sizes): the decomposed run must still equal the serial one, over face
 mode, the direct 26-neighbour deep exchange (x faces straight from the
 arrays), the sweep exchange and hybrid passes with region-local auxiliary
 arrays.  Also: the direct exchange with and without the unpacked x faces is
-bit-for-bit the same.
+bit-for-bit the same, and the Drude box inside decomposed blocked
+/ hybrid passes (its float4-per-cell state in the deep exchange, ranks the box
+misses, a box across rank borders) equals the serial stepped chain.
 """
 
 import threading
@@ -25,7 +27,8 @@ from fdtd3d_amd.parallel.halo import HaloExchanger
 from fdtd3d_amd.parallel.topology import ParallelGridCore
 
 
-def run_threads(cfg, world, axes, buf, mode="direct", direct_x=True, tagless=True):
+def run_threads(cfg, world, axes, buf, mode="direct", direct_x=True, tagless=True, randomize=True,
+                check=None):
     core = ParallelGridCore.create(cfg.size, world, axes)
     hub = LocalHub(world, tagless=tagless)
     out, errors = [None] * world, []
@@ -38,7 +41,10 @@ def run_threads(cfg, world, axes, buf, mode="direct", direct_x=True, tagless=Tru
             s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64), dom, halo)
             s.init_scheme()
             s.init_grids()
-            s.randomize_fields()
+            if randomize:
+                s.randomize_fields()
+            if check is not None:
+                check(s)
             s.perform_steps()
             halo.drain(s)
             out[rank] = s
@@ -63,11 +69,12 @@ def run_threads(cfg, world, axes, buf, mode="direct", direct_x=True, tagless=Tru
     return full
 
 
-def serial(cfg):
+def serial(cfg, randomize=True):
     s = YeeScheme(cfg, make_ops("torch", None, "cpu", torch.float64))
     s.init_scheme()
     s.init_grids()
-    s.randomize_fields()
+    if randomize:
+        s.randomize_fields()
     s.perform_steps()
     return {c: s.F[0][c] for c in s.comps}
 
@@ -104,3 +111,45 @@ def test_direct_x_faces_bitwise():
     b = run_threads(cfg, world, axes, buf, direct_x=False)
     for c in a:
         assert torch.equal(a[c], b[c]), c
+
+
+DRUDE = dict(scheme="3d", dtype="f64", scene="drude-sphere", use_metamaterials=True, blocked_drude="on")
+DRUDE_CASES = [
+    # plain blocked passes + the Drude pass; the box across the x / y rank borders
+    ("nopml-xy4-b3", SchemeConfig(size=(32, 30, 36), time_steps=10, sphere_center=(16.0, 15.0, 18.0),
+                                  sphere_radius=6.0, time_block=3, **DRUDE), 4, "xy", 3),
+    # x slabs 8 cells thick: the box misses the last rank's allocation
+    ("nopml-x4-b3-miss", SchemeConfig(size=(32, 30, 36), time_steps=10, sphere_center=(12.0, 15.0, 18.0),
+                                      sphere_radius=4.0, time_block=3, **DRUDE), 4, "x", 3),
+    # hybrid passes with UPML: the Drude pass after the exchange join, before the shell steps
+    ("upml-xy4-b3", SchemeConfig(size=(48, 48, 40), time_steps=10, sphere_center=(24.0, 24.0, 20.0),
+                                 sphere_radius=5.0, use_pml=True, pml_size=(4, 4, 4), hybrid_block=3,
+                                 time_block=3, **DRUDE), 4, "xy", 3),
+]
+
+
+@pytest.mark.parametrize("name,cfg,world,axes,buf", DRUDE_CASES, ids=[c[0] for c in DRUDE_CASES])
+def test_tagless_drude_blocked_equals_serial(name, cfg, world, axes, buf):
+    seen = []
+
+    def check(s):
+        seen.append((s.drude_blk is not None, s.hybrid is not None and bool(s.hybrid.get("drude")), s.tb,
+                     s._drude_glob is not None))
+
+    par = run_threads(cfg, world, axes, buf, randomize=False, check=check)
+    # every rank runs the pass form (the ranks the box misses without a Drude launch)
+    assert all(g for _, _, _, g in seen), seen
+    if cfg.use_pml:
+        assert all(h for _, h, _, _ in seen), seen
+    else:
+        assert all(tb == buf for _, _, tb, _ in seen), seen
+    if name.endswith("-miss"):
+        assert not all(d for d, _, _, _ in seen) and any(d for d, _, _, _ in seen), seen
+    else:
+        assert all(d for d, _, _, _ in seen), seen
+    import dataclasses
+    ser = serial(dataclasses.replace(cfg, blocked_drude="off", time_block=1, hybrid_block=1), randomize=False)
+    for c, b in ser.items():
+        scale = max(float(v.abs().max()) for o, v in ser.items() if o[0] == c[0]) + 1e-300
+        err = float((par[c] - b).abs().max())
+        assert err <= 1e-12 * scale, (name, c, err, scale)
