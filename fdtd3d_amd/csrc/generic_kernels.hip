@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void k_cpml_many(CpmlMany<T> M) {
 }
 }  // namespace
 
-// n <= 8 slabs of one kind: per slab P[7 q ..] = target src psi bc cc kc (+ 4 coef pointers at
+// n <= 8 slabs of one kind: per slab P[6 q ..] = target src psi bc cc kc (+ 4 coef pointers at
 // CP[4 q ..]), S[q] = coefficient scalar, I[14 q ..] = axis sign box[6] psi_box[6]
 #define FDTD_CPML_MANY_API(SUF, T)                                                                            \
   FDTD_API int fdtd_cpml_apply_many_##SUF(void* const* P, const void* const* CP, const double* S,            \

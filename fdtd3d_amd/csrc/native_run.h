@@ -414,18 +414,19 @@ void NativeRun<T>::plan_blocking() {
                : 1;
   // 1D: the whole run in one launch of the register-resident kernel
   res1 = dim == 1 && use_fused && N[0] <= fdtd_res1d_max_cells((int)sizeof(T));
-  int T_h_req = s.hybridBlock == 0 ? 5 : s.hybridBlock;
+  const int T_h_def = s.hybridBlock == 0 ? 5 : s.hybridBlock;
   if (dr_blk) {
     // (models/blocking.py DRUDE_AUTO_STEPS: the Drude variant holds T - 1 levels in registers)
     const int T_dr = s.hybridBlock > 0 ? s.hybridBlock : (s.timeBlock > 0 ? s.timeBlock : 4);
-    if (T_dr <= 1 || T_dr > 5)
-      dr_blk = false;  // the stepped dispersive box with the usual hybrid T
-    else
-      T_h_req = T_dr;
+    if (T_dr > 1 && T_dr <= 5) plan_hybrid3d(T_dr);
+    // the Drude pass runs inside hybrid passes only; when it does not fit, the
+    // stepped dispersive box cut out of the core at the usual hybrid T
+    if (T_dr <= 1 || T_dr > 5 || !dr_blk || T_h <= 1) {
+      dr_blk = false;
+      T_h = 1;
+    }
   }
-  plan_hybrid3d(T_h_req);
-  // the Drude pass runs inside hybrid passes only
-  if (T_h <= 1) dr_blk = false;
+  if (!dr_blk) plan_hybrid3d(T_h_def);
   if (dr_blk) setup_drude_state();
   plan_hybrid2d();
 }

@@ -39,7 +39,8 @@ import torch.distributed as dist
 
 from .comm import P2P, DistComm
 from .domain import Domain, box_empty, box_intersect
-from .topology import coords_rank
+from ..utils.assertions import fdtd_assert
+from .topology import chunk_bounds, coords_rank
 
 Box = Tuple[Tuple[int, int, int], Tuple[int, int, int]]
 
@@ -269,6 +270,13 @@ class HaloExchanger:
                 elif off[a] > 0:
                     slo[a] = d.hi[a] - B
                     rlo[a], rhi[a] = d.hi[a], d.hi[a] + B
+            if off[1] == 0 and off[2] == 0:
+                # direct x faces send whole allocated planes: the peer's y / z extents (owned,
+                # ghosts, padding) must be this rank's -- true of a Cartesian rank grid, whose
+                # per-axis bounds depend on that axis' coordinate only
+                for a in (1, 2):
+                    fdtd_assert(chunk_bounds(d.global_size[a], d.topology[a], c[a]) == (d.lo[a], d.hi[a]),
+                                "x-face peer with other y / z extents")
             out.append((off, coords_rank(c, d.topology), (tuple(slo), tuple(shi)), (tuple(rlo), tuple(rhi))))
         self._deep_msgs = out
         return out

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 6 (h): the whole GPU suite (decomposed blocked Drude cases included), smoke(), the 1-GPU bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r6h
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_parallel_gpu.py -k drude -v --timeout 240 --timeout-method thread > $O/drude_par.log 2>&1 || { echo drude par failed; grep -E "FAILED|Error|assert" $O/drude_par.log | head -30; tail -5 $O/drude_par.log; exit 1; }
+tail -1 $O/drude_par.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1 || { echo tests failed; grep -E "FAILED|Error" $O/tests.log | head -30; tail -5 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; tail -5 $O/smoke.log; exit 1; }
+echo smoke ok
+timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { echo bench failed; tail -5 $O/bench.log; exit 1; }
+tail -1 $O/bench.log
