@@ -412,6 +412,14 @@ int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, flo
                    float cb, float db, int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, int steps,
                    const int* src, const TbSrc& sv, const TfDev* tf, const float* gtab, const AmpDev& amp,
                    hipStream_t s, const DrDev& dr = DrDev{}) {
+  if (xchunk <= 0 && (fx & 4)) {
+    // tuning: x chunk of the TF/SF variant's passes (FDTD3D_TF_XCHUNK, 0 automatic)
+    static const int tfx = [] {
+      const char* e = getenv("FDTD3D_TF_XCHUNK");
+      return e ? atoi(e) : 0;
+    }();
+    if (tfx > 0) xchunk = tfx;
+  }
   if (xchunk <= 0) xchunk = tb_mr_xchunk(fx, O, steps);
 #define MR_ARGS fx, ein, hin, eout, hout, ce4, ch4, BE, BH, cb, db, nx, ny, nz, b, O, xchunk, src, sv, tf, gtab, amp, s, dr
   switch (steps) {
