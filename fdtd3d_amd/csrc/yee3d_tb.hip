@@ -445,12 +445,18 @@ int tb_mr_dispatch(int fx, const float* const* ein, const float* const* hin, flo
 // ``einc`` / ``hinc`` (scratch lines): the g tables of a pass whose real line
 // is advanced elsewhere -- the hybrid's stepped shell steps it once per step
 // while the blocked core applies the same pass's corrections in-kernel.
-__global__ __launch_bounds__(1024) void k_tfsf_pass(float* __restrict__ einc, float* __restrict__ hinc, int n,
-                                                    float ce, float ch, TbSrc sv, int T, int reach, int nE, int nH,
-                                                    const int* __restrict__ I0, const float* __restrict__ W0,
-                                                    const float* __restrict__ W1, const float* __restrict__ C,
-                                                    float* __restrict__ gtab, const float* __restrict__ esrc,
-                                                    const float* __restrict__ hsrc) {
+// (one template for the fp32 and fp64 blocked kernels' tables)
+template <typename R>
+struct LineSrc {
+  R v[8];
+};
+template <typename R>
+__global__ __launch_bounds__(1024) void k_tfsf_pass(R* __restrict__ einc, R* __restrict__ hinc, int n, R ce, R ch,
+                                                    LineSrc<R> sv, int T, int reach, int nE, int nH,
+                                                    const int* __restrict__ I0, const R* __restrict__ W0,
+                                                    const R* __restrict__ W1, const R* __restrict__ C,
+                                                    R* __restrict__ gtab, const R* __restrict__ esrc,
+                                                    const R* __restrict__ hsrc) {
   const int tid = threadIdx.x;
   const int ld = nE + nH;
   const int m = min(n, reach);
@@ -710,15 +716,32 @@ FDTD_API int fdtd_tfdev_size() { return (int)sizeof(TfDev); }
 
 // incident line advanced ``steps`` steps from step t (source value per step
 // in ``src_vals``) and the per-level g tables of the pass (k_tfsf_pass)
+namespace {
+template <typename R>
+int tfsf_pass(const R* esrc, const R* hsrc, R* einc, R* hinc, int n, double ce, double ch, const double* src_vals,
+              int steps, int reach, int nE, int nH, const int* I0, const R* W0, const R* W1, const R* C, R* gtab,
+              void* stream) {
+  if (steps < 1 || steps > 8) return (int)hipErrorInvalidValue;
+  if ((esrc || hsrc) && (!esrc || !hsrc || esrc == einc || hsrc == hinc)) return (int)hipErrorInvalidValue;
+  LineSrc<R> sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = l < steps ? (R)src_vals[l] : (R)0;
+  k_tfsf_pass<R><<<1, 1024, 0, (hipStream_t)stream>>>(einc, hinc, n, (R)ce, (R)ch, sv, steps, reach, nE, nH, I0, W0,
+                                                      W1, C, gtab, esrc, hsrc);
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+}  // namespace
+
 FDTD_API int fdtd_tfsf_pass_f32(float* einc, float* hinc, int n, double ce, double ch, const double* src_vals,
                                 int steps, int reach, int nE, int nH, const int* I0, const float* W0,
                                 const float* W1, const float* C, float* gtab, void* stream) {
-  if (steps < 1 || steps > 8) return (int)hipErrorInvalidValue;
-  TbSrc sv;
-  for (int l = 0; l < 8; ++l) sv.v[l] = l < steps ? (float)src_vals[l] : 0.f;
-  k_tfsf_pass<<<1, 1024, 0, (hipStream_t)stream>>>(einc, hinc, n, (float)ce, (float)ch, sv, steps, reach, nE, nH,
-                                                   I0, W0, W1, C, gtab, nullptr, nullptr);
-  FDTD_RETURN_LAUNCH_STATUS();
+  return tfsf_pass<float>(nullptr, nullptr, einc, hinc, n, ce, ch, src_vals, steps, reach, nE, nH, I0, W0, W1, C,
+                          gtab, stream);
+}
+FDTD_API int fdtd_tfsf_pass_f64(double* einc, double* hinc, int n, double ce, double ch, const double* src_vals,
+                                int steps, int reach, int nE, int nH, const int* I0, const double* W0,
+                                const double* W1, const double* C, double* gtab, void* stream) {
+  return tfsf_pass<double>(nullptr, nullptr, einc, hinc, n, ce, ch, src_vals, steps, reach, nE, nH, I0, W0, W1, C,
+                           gtab, stream);
 }
 
 // the g tables of a pass WITHOUT advancing the line: the line ``esrc`` /
@@ -728,10 +751,15 @@ FDTD_API int fdtd_tfsf_table_f32(const float* esrc, const float* hsrc, float* ei
                                  double ch, const double* src_vals, int steps, int reach, int nE, int nH,
                                  const int* I0, const float* W0, const float* W1, const float* C, float* gtab,
                                  void* stream) {
-  if (steps < 1 || steps > 8 || !esrc || !hsrc || esrc == einc || hsrc == hinc) return (int)hipErrorInvalidValue;
-  TbSrc sv;
-  for (int l = 0; l < 8; ++l) sv.v[l] = l < steps ? (float)src_vals[l] : 0.f;
-  k_tfsf_pass<<<1, 1024, 0, (hipStream_t)stream>>>(einc, hinc, n, (float)ce, (float)ch, sv, steps, reach, nE, nH,
-                                                   I0, W0, W1, C, gtab, esrc, hsrc);
-  FDTD_RETURN_LAUNCH_STATUS();
+  if (!esrc || !hsrc) return (int)hipErrorInvalidValue;
+  return tfsf_pass<float>(esrc, hsrc, einc, hinc, n, ce, ch, src_vals, steps, reach, nE, nH, I0, W0, W1, C, gtab,
+                          stream);
+}
+FDTD_API int fdtd_tfsf_table_f64(const double* esrc, const double* hsrc, double* einc, double* hinc, int n,
+                                 double ce, double ch, const double* src_vals, int steps, int reach, int nE, int nH,
+                                 const int* I0, const double* W0, const double* W1, const double* C, double* gtab,
+                                 void* stream) {
+  if (!esrc || !hsrc) return (int)hipErrorInvalidValue;
+  return tfsf_pass<double>(esrc, hsrc, einc, hinc, n, ce, ch, src_vals, steps, reach, nE, nH, I0, W0, W1, C, gtab,
+                           stream);
 }

@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "tfsf_dev.h"
 
 namespace {
 
@@ -100,12 +101,20 @@ int pick_xchunk64(long long tiles_yz, int nxo, int T) {
   return best;
 }
 
+// TFS: TF/SF corrections of the sets in ``tf`` (tfsf_dev.h; the fp64 g table
+// ``gtab`` of the pass's levels, k_tfsf_pass<double>), added to a target's
+// new value right after its kind's update -- E + c (curl + g) -- so the H
+// update of the same level reads the corrected E, as the stepped scheme does.
+// The kernel streams HBM at ~43 B per cell-step, so the corrections run from
+// the set table directly: per wave, bit masks of the sets touching its lanes
+// (y / z faces every level, x faces on their planes only), per lane the sets
+// whose target it is; the set's fields and g come through scalar loads.
 // HALF: each wave holds two y rows of 32 z lanes (lanes 0-31 row 2w, 32-63
 // row 2w+1): 32 x 32 tiles instead of 16 x 64, so a larger share of the
 // tile is owned (T = 4: 24 x 24 of 32 x 32 = 56% against 8 x 56 of 16 x 64 =
 // 44%) for the same registers.  The z shift crosses the half boundary only
 // into halo lanes; y neighbours are one flat LDS row (32 lanes) apart.
-template <int T, int R, bool PERCELL, bool HALF, int NW>
+template <int T, int R, bool PERCELL, bool HALF, int NW, bool TFS>
 __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
     const double* __restrict__ exi, const double* __restrict__ eyi, const double* __restrict__ ezi,
     const double* __restrict__ hxi, const double* __restrict__ hyi, const double* __restrict__ hzi,
@@ -114,7 +123,8 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
     const double* __restrict__ cbx, const double* __restrict__ cby, const double* __restrict__ cbz,
     const double* __restrict__ dbx, const double* __restrict__ dby, const double* __restrict__ dbz, double cb,
     double db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
-    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc64 sv, int patch) {
+    int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc64 sv, int patch,
+    const tb3d::TfDev* __restrict__ tf, const double* __restrict__ gtab) {
   constexpr int LW = HALF ? 32 : 64;  // z lanes per row
   constexpr int TBZ = LW - 2 * T;       // owned z cells per tile
   constexpr int ROWS = NW * R * (HALF ? 2 : 1);
@@ -182,6 +192,66 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
     const bool in = xin(b, p) && ((mbits >> (r * 7 + n)) & 1u);
     if (PERCELL && arr) return in ? bld64(plane_rsrc64(arr, p, nx, plane), roff[r]) : 0.0;
     return in ? sc : 0.0;
+  };
+  // TF/SF (TFS): wave masks of the E / H sets touching this wave's lanes
+  // (y / z-face sets: tf_c*, x-face sets: tf_x*), bit si per set index;
+  // tf_lm: this lane's cell is a target of set si (set box and its
+  // component's update box, y / z)
+  typedef const __attribute__((address_space(4))) tb3d::TfDev* TfPtr;
+  const TfPtr TFc = (TfPtr)tf;
+  unsigned tf_ce = 0u, tf_ch = 0u, tf_xe = 0u, tf_xh = 0u, tf_lm = 0u;
+  int tf_pe = -1, tf_ph = -1;  // x-face planes of the E / H sets: lo | hi << 16
+  if constexpr (TFS) {
+    const int ns = TFc->nsets;
+    for (int si = 0; si < ns; ++si) {
+      const int n = TFc->s[si].n;
+#define TF_UB(f, d) (n == 0 ? bex.f[d] : n == 1 ? bey.f[d] : n == 2 ? bez.f[d] : n == 3 ? bhx.f[d] : n == 4 ? bhy.f[d] : bhz.f[d])
+      const int ul1 = TF_UB(lo, 1), uh1 = TF_UB(hi, 1), ul2 = TF_UB(lo, 2), uh2 = TF_UB(hi, 2);
+#undef TF_UB
+      const bool in = kin && jw >= TFc->s[si].lo[1] && jw < TFc->s[si].hi[1] && k >= TFc->s[si].lo[2] &&
+                      k < TFc->s[si].hi[2] && jw >= ul1 && jw < uh1 && k >= ul2 && k < uh2;
+      const unsigned bit = 1u << si;
+      tf_lm |= in ? bit : 0u;
+      if (__any(in)) {
+        if (TFc->s[si].fa == 0)
+          (n < 3 ? tf_xe : tf_xh) |= bit;
+        else
+          (n < 3 ? tf_ce : tf_ch) |= bit;
+      }
+    }
+    tf_ce = __builtin_amdgcn_readfirstlane(tf_ce);
+    tf_ch = __builtin_amdgcn_readfirstlane(tf_ch);
+    tf_xe = __builtin_amdgcn_readfirstlane(tf_xe);
+    tf_xh = __builtin_amdgcn_readfirstlane(tf_xh);
+    tf_pe = (TFc->xpl[0][0] & 0xffff) | (TFc->xpl[0][1] << 16);
+    tf_ph = (TFc->xpl[1][0] & 0xffff) | (TFc->xpl[1][1] << 16);
+  }
+  // the corrections of kind k (0 E, 1 H) at level l on plane p to the new
+  // values f of row 0 (R == 1)
+  auto tf_fix = [&](int kk, int l, int p, F3d& f) {
+    const int xp = kk == 0 ? tf_pe : tf_ph;
+    const bool xplane = p == (xp & 0xffff) || p == (xp >> 16);
+    unsigned m = (kk == 0 ? tf_ce : tf_ch) | (xplane ? (kk == 0 ? tf_xe : tf_xh) : 0u);
+    while (m) {
+      const int si = __builtin_ctz(m);
+      m &= m - 1u;
+      const int lo0 = TFc->s[si].lo[0];
+      if (p < lo0 || p >= TFc->s[si].hi[0]) continue;
+      const int idx = TFc->s[si].va == 0 ? p - lo0 : jw - TFc->s[si].lo[1];
+      const int gi = l * TFc->ld + TFc->s[si].goff + idx;
+      if (!((tf_lm >> si) & 1u)) continue;
+      const double g = gtab[gi];
+      const int c = TFc->s[si].n - 3 * kk;
+      if (kk == 0) {
+        if (c == 0) f.x += coef(cbx, bex, p, 0, 0, cb) * g;
+        else if (c == 1) f.y += coef(cby, bey, p, 0, 1, cb) * g;
+        else f.z += coef(cbz, bez, p, 0, 2, cb) * g;
+      } else {
+        if (c == 0) f.x += coef(dbx, bhx, p, 0, 3, db) * g;
+        else if (c == 1) f.y += coef(dby, bhy, p, 0, 4, db) * g;
+        else f.z += coef(dbz, bhz, p, 0, 5, db) * g;
+      }
+    }
   };
   F3d Hp[T][R], Ep[T][R];
 #pragma unroll
@@ -277,6 +347,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
         En[r].x = Ec[r].x + coef(cbx, bex, pe, r, 0, cb) * ((Hc[r].z - hz_j) - (Hc[r].y - hy_k));
         En[r].y = Ec[r].y + coef(cby, bey, pe, r, 1, cb) * ((Hc[r].x - hx_k) - (Hc[r].z - Hp[l][r].z));
         En[r].z = Ec[r].z + coef(cbz, bez, pe, r, 2, cb) * ((Hc[r].y - Hp[l][r].y) - (Hc[r].x - hx_j));
+        if constexpr (TFS) tf_fix(0, l, pe, En[r]);
         if (src_plane && jw + r == src_j && src_k == k) {
           if (src_comp == 0) En[r].x = sv.v[l];
           if (src_comp == 1) En[r].y = sv.v[l];
@@ -294,6 +365,7 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
         Hn.x = Hp[l][r].x + coef(dbx, bhx, ph, r, 3, db) * ((ey_k - Ep[l][r].y) - (ez_jn - Ep[l][r].z));
         Hn.y = Hp[l][r].y + coef(dby, bhy, ph, r, 4, db) * ((En[r].z - Ep[l][r].z) - (ex_k - Ep[l][r].x));
         Hn.z = Hp[l][r].z + coef(dbz, bhz, ph, r, 5, db) * ((ex_jn - Ep[l][r].x) - (En[r].y - Ep[l][r].y));
+        if constexpr (TFS) tf_fix(1, l, ph, Hn);
         Ec[r] = Ep[l][r];
         Ep[l][r] = En[r];
         Hp[l][r] = Hc[r];
@@ -329,7 +401,7 @@ template <int T, int R, bool HALF, int NW = TBW>
 int launch_tb64(bool pc, const double* const* ein, const double* const* hin, double* const* eout,
                 double* const* hout, const double* const* cbs, const double* const* dbs, double cb, double db,
                 int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src,
-                const TbSrc64& sv, hipStream_t s) {
+                const TbSrc64& sv, hipStream_t s, const tb3d::TfDev* tf = nullptr, const double* gtab = nullptr) {
   constexpr int TBZ = (HALF ? 32 : 64) - 2 * T;
   const long long gz = cdiv(O.hi[2] - O.lo[2], TBZ);
   const long long gy = cdiv(O.hi[1] - O.lo[1], NW * R * (HALF ? 2 : 1) - 2 * T);
@@ -338,11 +410,17 @@ int launch_tb64(bool pc, const double* const* ein, const double* const* hin, dou
 #define TB64_ARGS                                                                                              \
   ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2],      \
       cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
-      O, xchunk, src[0], src[1], src[2], src[3], sv, tb64_patch()
-  if (pc)
-    k_tb3d_f64<T, R, true, HALF, NW><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
-  else
-    k_tb3d_f64<T, R, false, HALF, NW><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+      O, xchunk, src[0], src[1], src[2], src[3], sv, tb64_patch(), tf, gtab
+  if (tf && gtab) {
+    if (pc)
+      k_tb3d_f64<T, R, true, HALF, NW, true><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+    else
+      k_tb3d_f64<T, R, false, HALF, NW, true><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+  } else if (pc) {
+    k_tb3d_f64<T, R, true, HALF, NW, false><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+  } else {
+    k_tb3d_f64<T, R, false, HALF, NW, false><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+  }
 #undef TB64_ARGS
   FDTD_RETURN_LAUNCH_STATUS();
 }
@@ -360,12 +438,11 @@ FDTD_API void fdtd_set_tb64_patch(int pz, int py) {
   g_tb64_patch = (pz > 0 && py > 0 && pz < 256 && py < 256) ? (pz | (py << 8)) : 0;
 }
 
-// fp64 counterpart of fdtd_tb3d_v4_f32 (same arguments, double arrays), 1..4
-// steps per pass, any nz.
-FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, double* const* eout,
-                           double* const* hout, const double* const* cbs, const double* const* dbs, double cb,
-                           double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
-                           int steps, const int* src, const double* src_vals, void* stream) {
+namespace {
+int tb64_run(const double* const* ein, const double* const* hin, double* const* eout, double* const* hout,
+             const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
+             const int* boxes, const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
+             const tb3d::TfDev* tf, const double* gtab, void* stream) {
   if (steps < 1 || steps > 5) return (int)hipErrorInvalidValue;
   Box3 b[6];
   for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
@@ -377,7 +454,7 @@ FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, d
   hipStream_t s = (hipStream_t)stream;
   // one row per wave: two rows of fp64 state spill from T = 2 on
 #define TB64(TT, HF) \
-  launch_tb64<TT, 1, HF>(pc, ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s)
+  launch_tb64<TT, 1, HF>(pc, ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s, tf, gtab)
   if (g_tb64_half) {
     switch (steps) {
       case 1: return TB64(1, true);
@@ -397,4 +474,28 @@ FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, d
   }
 #undef TB64
   return (int)hipErrorInvalidValue;
+}
+}  // namespace
+
+// fp64 counterpart of fdtd_tb3d_v4_f32 (same arguments, double arrays), 1..5
+// steps per pass, any nz.
+FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, double* const* eout,
+                           double* const* hout, const double* const* cbs, const double* const* dbs, double cb,
+                           double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
+                           int steps, const int* src, const double* src_vals, void* stream) {
+  return tb64_run(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, boxes, obox, xchunk, steps, src, src_vals,
+                  nullptr, nullptr, stream);
+}
+
+// ... with the TF/SF corrections of the device set table ``tf`` (tfsf_dev.h
+// TfDev, filled by models/tfsf.py TfsfSets) and the fp64 g table ``gtab`` of
+// the pass's first level (fdtd_tfsf_pass_f64 / fdtd_tfsf_table_f64)
+FDTD_API int fdtd_tb3d_tf_f64(const double* const* ein, const double* const* hin, double* const* eout,
+                              double* const* hout, const double* const* cbs, const double* const* dbs, double cb,
+                              double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
+                              int steps, const int* src, const double* src_vals, const void* tf, const double* gtab,
+                              void* stream) {
+  if (!tf || !gtab) return (int)hipErrorInvalidValue;
+  return tb64_run(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, boxes, obox, xchunk, steps, src, src_vals,
+                  (const tb3d::TfDev*)tf, gtab, stream);
 }

@@ -545,12 +545,14 @@ class BlockedStepping:
         if (not cfg.use_tfsf or cfg.scheme != "3d" or getattr(self, "tfsf_sets", None) is None
                 or mode == "shell" or T > TFSF_MAX_STEPS):
             return False
-        if mode == "auto" and self.use_cpml:
+        if mode == "auto" and self.use_cpml and self.dtype == torch.float32:
             # measured (512^3 fp32, T = 5, profiles/tfsf_cost_r5.md): with UPML the
             # faces in the core win (87.0k vs 81.1k Mcells/s: the D/B-form chain
             # shell is dear per cell), with CPML the shell keeps them (93.1k vs
             # 91.2k: the folded CPML kernels step the vacuum windows cheaply
-            # while the TF/SF face tiles still cost the core ~30%)
+            # while the TF/SF face tiles still cost the core ~30%).  fp64: the
+            # blocked kernel is HBM-bound, the corrections ride along
+            # (profiles/physics_r6.md)
             return False
         return True
 

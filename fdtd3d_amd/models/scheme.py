@@ -915,11 +915,10 @@ class YeeScheme(BlockedStepping):
         if self.use_upml_chain:
             self.tfsf_D = build_tfsf_tables(self.layout, self.comps, self.domain.origin, self.domain.shape, boxes,
                                             {c: self.upml[c]["cbD"] for c in self.comps}, self.device, self.dtype, n)
-        # in-kernel form for the blocked passes (fp32 HIP, incident direction
-        # along x or y; models/tfsf.py TfsfSets)
+        # in-kernel form for the blocked passes (incident direction along x or
+        # y; models/tfsf.py TfsfSets; fp32 and, from round 6, fp64 HIP kernels)
         self.tfsf_sets = None
-        if (self.cfg.scheme == "3d" and getattr(self.ops, "tfsf_sets_ok", False)
-                and (self.ops.name != "hip" or self.dtype == torch.float32)):
+        if self.cfg.scheme == "3d" and getattr(self.ops, "tfsf_sets_ok", False):
             self.tfsf_sets = build_tfsf_sets(self.layout, self.comps, self.domain.origin, self.domain.shape, boxes,
                                              self.device, self.dtype, n)
             if self.tfsf_sets is not None:

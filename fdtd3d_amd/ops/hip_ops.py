@@ -841,7 +841,7 @@ class HipOps:
         return out
 
     # ------------------------------------------------------ temporal blocking
-    tfsf_sets_ok = True  # the fp32 blocked kernel applies TfsfSets corrections
+    tfsf_sets_ok = True  # the blocked kernels (fp32 and fp64) apply TfsfSets corrections
 
     def tfsf_pass(self, einc: torch.Tensor, hinc: torch.Tensor, ce: float, ch: float, src_vals, reach: int,
                   sets, slot: int = 0, dry: bool = False) -> torch.Tensor:
@@ -851,8 +851,9 @@ class HipOps:
         the line stays as it is -- the pass runs on scratch copies
         (fdtd_tfsf_table_f32; hybrid passes, whose shell steps the line)."""
         T = len(src_vals)
-        if not (1 <= T <= 8) or self.dtype != torch.float32:
-            raise HipError("tfsf_pass: fp32, 1..8 steps")
+        if not (1 <= T <= 8):
+            raise HipError("tfsf_pass: 1..8 steps")
+        sfx = "f32" if self.dtype == torch.float32 else "f64"
         if int(self.lib.fdtd_tfdev_size()) != 4 * sets.dev.numel():
             raise HipError("TfDev layout mismatch (%d vs %d bytes)" % (self.lib.fdtd_tfdev_size(),
                                                                        4 * sets.dev.numel()))
@@ -860,7 +861,7 @@ class HipOps:
         tabs = sets.__dict__.setdefault("gtab", {})
         g = tabs.get(slot)
         if g is None or g.numel() < need:
-            g = tabs[slot] = torch.zeros(8 * max(1, sets.ld), dtype=torch.float32, device=self.device)
+            g = tabs[slot] = torch.zeros(8 * max(1, sets.ld), dtype=self.dtype, device=self.device)
         for t_ in (einc, hinc):
             self._check_tensor(t_)
         if einc.numel() != hinc.numel():
@@ -874,11 +875,12 @@ class HipOps:
             if sl is None or sl[0].numel() != einc.numel():
                 # zero beyond every reach a pass copies: cells past the wave front read 0
                 sl = scr[slot] = (torch.zeros_like(einc), torch.zeros_like(hinc))
-            rc = self.lib.fdtd_tfsf_table_f32(_ptr(einc), _ptr(hinc), _ptr(sl[0]), _ptr(sl[1]), c_int(einc.numel()),
-                                              c_double(ce), c_double(ch), vals8, *tail)
+            rc = getattr(self.lib, "fdtd_tfsf_table_" + sfx)(_ptr(einc), _ptr(hinc), _ptr(sl[0]), _ptr(sl[1]),
+                                                             c_int(einc.numel()), c_double(ce), c_double(ch), vals8,
+                                                             *tail)
         else:
-            rc = self.lib.fdtd_tfsf_pass_f32(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(ce), c_double(ch),
-                                             vals8, *tail)
+            rc = getattr(self.lib, "fdtd_tfsf_pass_" + sfx)(_ptr(einc), _ptr(hinc), c_int(einc.numel()), c_double(ce),
+                                                            c_double(ch), vals8, *tail)
         _check(rc, "tfsf_pass")
         self.launches += 1
         return g
@@ -1075,7 +1077,19 @@ class HipOps:
             src = [idx[0], idx[1], idx[2], E.index(comp)]
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
         if tfsf is not None and self.dtype != torch.float32:
-            raise HipError("in-kernel TF/SF: fp32 only")
+            # fp64 kernel with the TF/SF corrections (yee3d_tb64.hip TFS)
+            sets, gtab, level0 = tfsf
+            if int(self.lib.fdtd_tfdev_size()) != 4 * sets.dev.numel():
+                raise HipError("TfDev layout mismatch")
+            self.lib.fdtd_set_tb64_shape(c_int(self.tb64_half))
+            rc = self.lib.fdtd_tb3d_tf_f64(
+                arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), cbs, dbs, c_double(cbv), c_double(dbv),
+                c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), _box_arr([boxes[c] for c in E + H]), _box_arr([obox]),
+                c_int(self.tb_xchunk), c_int(steps), (c_int * 4)(*src), (c_double * 8)(*vals), _ptr(sets.dev),
+                c_vp(gtab.data_ptr() + gtab.element_size() * level0 * sets.ld), _stream())
+            _check(rc, "tb3d_tf_f64")
+            self.launches += 1
+            return
         if (percell and self.dtype == torch.float32 and self.tb_sparse) or tfsf is not None:
             # multi-row kernel with sparse per-cell coefficients / TF/SF sets
             if percell and steps > 5:

@@ -45,6 +45,13 @@ CASES = [
     ("cpml-tfsf-y-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0,
                               hybrid_tfsf="core"), 4, 11),
     ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0), 3, 11),
+    # fp64: the TF/SF faces in the fp64 blocked core (yee3d_tb64.hip tf_fix; automatic in fp64), x and y
+    # incidence, CPML and UPML shells
+    ("cpml-tfsf-x-f64-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, dtype="f64"), 4,
+     13),
+    ("cpml-tfsf-y-f64-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0,
+                                  dtype="f64"), 3, 11),
+    ("upml-tfsf-x-f64-core", dict(scene="vacuum", use_pml=True, use_tfsf=True, dtype="f64"), 4, 12),
     ("cpml-tfsf-sphere", dict(scene="sphere", use_pml=True, pml_type="cpml", use_tfsf=True,
                               sphere_center=(40.0, 36.0, 48.0), sphere_radius=10.0), 4, 10),
     ("cpml-point-T5", dict(scene="vacuum", use_pml=True, pml_type="cpml"), 5, 12),
