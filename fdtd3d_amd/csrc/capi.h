@@ -110,6 +110,10 @@ int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, double* co
                   const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
                   const int* boxes, const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
                   void* stream);
+int fdtd_tb3d_drude_f64(const double* const* ein, const double* const* hin, double* const* eout, double* const* hout,
+                        double cb, double db, int nx, int ny, int nz, const int* boxes, const int* obox, int xchunk,
+                        int steps, const int* src, const double* src_vals, const int* bbox, void* const* sin,
+                        void* const* sout, const double* lut, int nid, double cbd, void* stream);
 int fdtd_tfsf_pass_f64(double* einc, double* hinc, int n, double ce, double ch, const double* src_vals, int steps,
                        int reach, int nE, int nH, const int* I0, const double* W0, const double* W1, const double* C,
                        double* gtab, void* stream);

@@ -71,6 +71,31 @@ struct F3d {
   double x, y, z;
 };
 
+// Drude box of an fp64 pass (DRU; the fp32 form is tb3d_mr.h DrDev, whose
+// comment derives the update): inside B the E components take
+//   E' = (b0 cbd) curl - b2 delta + m1 E + m2 Ep,  delta' = cbd curl,  Ep' = E
+// with (delta, Ep) carried level to level in registers and read / written
+// once per pass: per cell of B two 32-byte records,
+//   s0 = (delta_x, delta_y, delta_z, ids: id_x | id_y << 8 | id_z << 16 in the
+//   low word of the fourth double), s1 = (Ep_x, Ep_y, Ep_z, 0);
+// the (b0 cbd, b2, m1, m2) rows of each component's material ids in LDS.
+constexpr int DR64_MAX_IDS = 256;
+struct DrDev64 {
+  Box3 B;
+  const double* sin0;  // x-major over B, z fastest, 4 doubles per cell
+  const double* sin1;
+  double* sout0;       // distinct from sin: tiles re-read halo cells other tiles own
+  double* sout1;
+  const double* lut;   // [3][nid][4]
+  int nid;
+  double cbd;
+};
+struct DrS64 {
+  double dx, dy, dz, px, py, pz;
+  unsigned id;
+};
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
 int g_num_cus64 = 0;
 bool g_tb64_half = true;
 
@@ -114,7 +139,7 @@ int pick_xchunk64(long long tiles_yz, int nxo, int T) {
 // tile is owned (T = 4: 24 x 24 of 32 x 32 = 56% against 8 x 56 of 16 x 64 =
 // 44%) for the same registers.  The z shift crosses the half boundary only
 // into halo lanes; y neighbours are one flat LDS row (32 lanes) apart.
-template <int T, int R, bool PERCELL, bool HALF, int NW, bool TFS>
+template <int T, int R, bool PERCELL, bool HALF, int NW, bool TFS, bool DRU>
 __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
     const double* __restrict__ exi, const double* __restrict__ eyi, const double* __restrict__ ezi,
     const double* __restrict__ hxi, const double* __restrict__ hyi, const double* __restrict__ hzi,
@@ -124,7 +149,8 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
     const double* __restrict__ dbx, const double* __restrict__ dby, const double* __restrict__ dbz, double cb,
     double db, int nx, int ny, int nz, Box3 bex, Box3 bey, Box3 bez, Box3 bhx, Box3 bhy, Box3 bhz, Box3 O,
     int xchunk, int src_i, int src_j, int src_k, int src_comp, TbSrc64 sv, int patch,
-    const tb3d::TfDev* __restrict__ tf, const double* __restrict__ gtab) {
+    const tb3d::TfDev* __restrict__ tf, const double* __restrict__ gtab, DrDev64 dr) {
+  static_assert(!DRU || (!PERCELL && !TFS && R == 1), "Drude box: uniform media, alone");
   constexpr int LW = HALF ? 32 : 64;  // z lanes per row
   constexpr int TBZ = LW - 2 * T;       // owned z cells per tile
   constexpr int ROWS = NW * R * (HALF ? 2 : 1);
@@ -253,6 +279,53 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
       }
     }
   };
+  // Drude box (DRU): the lane's byte offset in one x plane of the state
+  // records (past the plane outside B in y / z), the coefficient rows in LDS
+  __shared__ double sL[DRU ? 3 * DR64_MAX_IDS * 4 : 1];
+  const int drz = dr.B.hi[2] - dr.B.lo[2];
+  const size_t dplane = DRU ? (size_t)(dr.B.hi[1] - dr.B.lo[1]) * drz * 32u : 0;
+  unsigned doff = 0xF0000000u;
+  bool din = false;
+  if constexpr (DRU) {
+    din = kin && jw >= dr.B.lo[1] && jw < dr.B.hi[1] && k >= dr.B.lo[2] && k < dr.B.hi[2];
+    if (din) doff = (unsigned)((jw - dr.B.lo[1]) * drz + (k - dr.B.lo[2])) * 32u;
+    for (int i = lane + 64 * w; i < 3 * DR64_MAX_IDS; i += 64 * NW) {
+      const int c = i / DR64_MAX_IDS, id = i - c * DR64_MAX_IDS;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sL[4 * i + q] = id < dr.nid ? dr.lut[(c * dr.nid + id) * 4 + q] : 0.0;
+    }
+    __syncthreads();
+  }
+  const bool wave_d = DRU && __any(din);
+  auto dr_rsrc = [&](const double* base, int p) -> Rsrc {
+    const bool in = xin(dr.B, p);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (in ? (size_t)(p - dr.B.lo[0]) * dplane : 0)),
+                                             (short)0, in ? (int)dplane : 0, 0x00020000);
+  };
+  auto dr_load = [&](int p, DrS64& S) {
+    const Rsrc r0 = dr_rsrc(dr.sin0, p), r1 = dr_rsrc(dr.sin1, p);
+    const u4 a = __builtin_amdgcn_raw_buffer_load_b128(r0, doff, 0, 0);
+    const u4 b = __builtin_amdgcn_raw_buffer_load_b128(r0, doff, 16, 0);
+    const u4 c = __builtin_amdgcn_raw_buffer_load_b128(r1, doff, 0, 0);
+    const u2 d = __builtin_amdgcn_raw_buffer_load_b64(r1, doff, 16, 0);
+    S.dx = __builtin_bit_cast(double, u2{a.x, a.y});
+    S.dy = __builtin_bit_cast(double, u2{a.z, a.w});
+    S.dz = __builtin_bit_cast(double, u2{b.x, b.y});
+    S.id = b.z;
+    S.px = __builtin_bit_cast(double, u2{c.x, c.y});
+    S.py = __builtin_bit_cast(double, u2{c.z, c.w});
+    S.pz = __builtin_bit_cast(double, d);
+  };
+  // DS[l]: the output of level l in the previous trip (plane X - 1 - l), the
+  // input of level l + 1 in this one; Dc: the input of the level running;
+  // Dnx: the next trip's level-0 input; DL: the last level's output
+  constexpr int NDS = DRU ? (T > 1 ? T - 1 : 1) : 1;
+  DrS64 DS[NDS], Dnx{}, Dc{}, DL{};
+  if constexpr (DRU) {
+#pragma unroll
+    for (int l = 0; l < NDS; ++l) DS[l] = DrS64{};
+    if (wave_d) dr_load(i0 - T, Dnx);
+  }
   F3d Hp[T][R], Ep[T][R];
 #pragma unroll
   for (int l = 0; l < T; ++l)
@@ -309,6 +382,11 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
       Hc[r] = Hnx[r];
       Ec[r] = Enx[r];
     }
+    if constexpr (DRU) {
+      // this trip's level-0 state; the next trip's in flight before the field prefetch
+      Dc = Dnx;
+      if (wave_d) dr_load(X + 1, Dnx);
+    }
     load_plane(X + 1, Hnx, Enx);
     store_out(X - 1);  // the first plane's are out of [i0, i1): dropped
     F3d En[R];
@@ -344,9 +422,42 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
         const double hx_j = r == 0 ? hx_dn : Hc[r > 0 ? r - 1 : 0].x;
         const double hy_k = lane_up64(Hc[r].y);
         const double hx_k = lane_up64(Hc[r].x);
-        En[r].x = Ec[r].x + coef(cbx, bex, pe, r, 0, cb) * ((Hc[r].z - hz_j) - (Hc[r].y - hy_k));
-        En[r].y = Ec[r].y + coef(cby, bey, pe, r, 1, cb) * ((Hc[r].x - hx_k) - (Hc[r].z - Hp[l][r].z));
-        En[r].z = Ec[r].z + coef(cbz, bez, pe, r, 2, cb) * ((Hc[r].y - Hp[l][r].y) - (Hc[r].x - hx_j));
+        const double cx = (Hc[r].z - hz_j) - (Hc[r].y - hy_k);
+        const double cy = (Hc[r].x - hx_k) - (Hc[r].z - Hp[l][r].z);
+        const double cz = (Hc[r].y - Hp[l][r].y) - (Hc[r].x - hx_j);
+        En[r].x = Ec[r].x + coef(cbx, bex, pe, r, 0, cb) * cx;
+        En[r].y = Ec[r].y + coef(cby, bey, pe, r, 1, cb) * cy;
+        En[r].z = Ec[r].z + coef(cbz, bez, pe, r, 2, cb) * cz;
+        if constexpr (DRU) {
+          const DrS64 st = Dc;
+          if (wave_d && xin(dr.B, pe)) {
+            const double* kx = &sL[4 * (st.id & 0xffu)];
+            const double* ky = &sL[4 * (DR64_MAX_IDS + ((st.id >> 8) & 0xffu))];
+            const double* kz = &sL[4 * (2 * DR64_MAX_IDS + ((st.id >> 16) & 0xffu))];
+            const double nx_ = kx[0] * cx - kx[1] * st.dx + kx[2] * Ec[r].x + kx[3] * st.px;
+            const double ny_ = ky[0] * cy - ky[1] * st.dy + ky[2] * Ec[r].y + ky[3] * st.py;
+            const double nz_ = kz[0] * cz - kz[1] * st.dz + kz[2] * Ec[r].z + kz[3] * st.pz;
+            if (din) {
+              En[r].x = nx_;
+              En[r].y = ny_;
+              En[r].z = nz_;
+            }
+          }
+          DrS64 o;
+          o.dx = dr.cbd * cx;
+          o.dy = dr.cbd * cy;
+          o.dz = dr.cbd * cz;
+          o.px = Ec[r].x;
+          o.py = Ec[r].y;
+          o.pz = Ec[r].z;
+          o.id = st.id;
+          if (l < T - 1) {
+            Dc = DS[l < T - 1 ? l : 0];
+            DS[l < T - 1 ? l : 0] = o;
+          } else {
+            DL = o;
+          }
+        }
         if constexpr (TFS) tf_fix(0, l, pe, En[r]);
         if (src_plane && jw + r == src_j && src_k == k) {
           if (src_comp == 0) En[r].x = sv.v[l];
@@ -377,6 +488,19 @@ __global__ __launch_bounds__(64 * NW) void k_tb3d_f64(
       Ed[r] = En[r];
       Hd[r] = Hc[r];
     }
+    if constexpr (DRU) {
+      // the last level's state (plane X - T + 1): owned cells of B
+      const int pe = X - T + 1;
+      const Rsrc r0 = dr_rsrc(dr.sout0, pe), r1 = dr_rsrc(dr.sout1, pe);
+      const bool own = (mbits >> 6) & 1u;
+      const unsigned o = (wave_d && own && din && pe >= i0 && pe < i1) ? doff : 0xF0000000u;
+      const u2 vx = __builtin_bit_cast(u2, DL.dx), vy = __builtin_bit_cast(u2, DL.dy), vz = __builtin_bit_cast(u2, DL.dz);
+      const u2 px = __builtin_bit_cast(u2, DL.px), py = __builtin_bit_cast(u2, DL.py), pz = __builtin_bit_cast(u2, DL.pz);
+      __builtin_amdgcn_raw_buffer_store_b128(u4{vx.x, vx.y, vy.x, vy.y}, r0, o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u4{vz.x, vz.y, DL.id, 0u}, r0, o, 16, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u4{px.x, px.y, py.x, py.y}, r1, o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u4{pz.x, pz.y, 0u, 0u}, r1, o, 16, 0);
+    }
   }
   store_out(i1 + T - 1);
 }
@@ -401,7 +525,8 @@ template <int T, int R, bool HALF, int NW = TBW>
 int launch_tb64(bool pc, const double* const* ein, const double* const* hin, double* const* eout,
                 double* const* hout, const double* const* cbs, const double* const* dbs, double cb, double db,
                 int nx, int ny, int nz, const Box3* b, const Box3& O, int xchunk, const int* src,
-                const TbSrc64& sv, hipStream_t s, const tb3d::TfDev* tf = nullptr, const double* gtab = nullptr) {
+                const TbSrc64& sv, hipStream_t s, const tb3d::TfDev* tf = nullptr, const double* gtab = nullptr,
+                const DrDev64* dr = nullptr) {
   constexpr int TBZ = (HALF ? 32 : 64) - 2 * T;
   const long long gz = cdiv(O.hi[2] - O.lo[2], TBZ);
   const long long gy = cdiv(O.hi[1] - O.lo[1], NW * R * (HALF ? 2 : 1) - 2 * T);
@@ -410,16 +535,23 @@ int launch_tb64(bool pc, const double* const* ein, const double* const* hin, dou
 #define TB64_ARGS                                                                                              \
   ein[0], ein[1], ein[2], hin[0], hin[1], hin[2], eout[0], eout[1], eout[2], hout[0], hout[1], hout[2],      \
       cbs[0], cbs[1], cbs[2], dbs[0], dbs[1], dbs[2], cb, db, nx, ny, nz, b[0], b[1], b[2], b[3], b[4], b[5], \
-      O, xchunk, src[0], src[1], src[2], src[3], sv, tb64_patch(), tf, gtab
-  if (tf && gtab) {
+      O, xchunk, src[0], src[1], src[2], src[3], sv, tb64_patch(), tf, gtab, dr ? *dr : DrDev64{}
+  if (dr) {
+    if constexpr (NW == 8) {
+      if (pc || tf) return (int)hipErrorInvalidValue;
+      k_tb3d_f64<T, R, false, HALF, NW, false, true><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
+  } else if (tf && gtab) {
     if (pc)
-      k_tb3d_f64<T, R, true, HALF, NW, true><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+      k_tb3d_f64<T, R, true, HALF, NW, true, false><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
     else
-      k_tb3d_f64<T, R, false, HALF, NW, true><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+      k_tb3d_f64<T, R, false, HALF, NW, true, false><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
   } else if (pc) {
-    k_tb3d_f64<T, R, true, HALF, NW, false><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+    k_tb3d_f64<T, R, true, HALF, NW, false, false><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
   } else {
-    k_tb3d_f64<T, R, false, HALF, NW, false><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
+    k_tb3d_f64<T, R, false, HALF, NW, false, false><<<grid, dim3(64, NW), 0, s>>>(TB64_ARGS);
   }
 #undef TB64_ARGS
   FDTD_RETURN_LAUNCH_STATUS();
@@ -485,6 +617,59 @@ FDTD_API int fdtd_tb3d_f64(const double* const* ein, const double* const* hin, d
                            int steps, const int* src, const double* src_vals, void* stream) {
   return tb64_run(ein, hin, eout, hout, cbs, dbs, cb, db, nx, ny, nz, boxes, obox, xchunk, steps, src, src_vals,
                   nullptr, nullptr, stream);
+}
+
+// ... with the Drude box folded in (DrDev64; the fp64 counterpart of
+// fdtd_tb3d_drude_f32): ``bbox`` = the box B (local, inside the E update
+// boxes), ``sin`` / ``sout`` = the two 32-byte state records per cell of B in
+// / out (distinct), ``lut`` = [3][nid][4] doubles (b0 cbd, b2, m1, m2),
+// ``cbd`` the D coefficient; uniform media elsewhere.  Tiles of 8 waves x two
+// 32-lane rows (the state of T - 1 levels rides in registers: <= 256 VGPRs).
+FDTD_API int fdtd_tb3d_drude_f64(const double* const* ein, const double* const* hin, double* const* eout,
+                                 double* const* hout, double cb, double db, int nx, int ny, int nz, const int* boxes,
+                                 const int* obox, int xchunk, int steps, const int* src, const double* src_vals,
+                                 const int* bbox, void* const* sin, void* const* sout, const double* lut, int nid,
+                                 double cbd, void* stream) {
+  if (steps < 1 || steps > 5 || !sin || !sout || !lut || nid < 1 || nid > DR64_MAX_IDS) return (int)hipErrorInvalidValue;
+  Box3 b[6];
+  for (int n = 0; n < 6; ++n) b[n] = make_box(boxes + 6 * n);
+  const Box3 O = make_box(obox);
+  if (box_empty(O)) return 0;
+  DrDev64 D;
+  D.B = make_box(bbox);
+  if (box_empty(D.B)) return (int)hipErrorInvalidValue;
+  for (int d = 0; d < 3; ++d) {
+    if (D.B.lo[d] < 0 || D.B.hi[d] > (d == 0 ? nx : d == 1 ? ny : nz)) return (int)hipErrorInvalidValue;
+    for (int n = 0; n < 3; ++n)
+      if (D.B.lo[d] < b[n].lo[d] || D.B.hi[d] > b[n].hi[d]) return (int)hipErrorInvalidValue;
+  }
+  // one x plane of a state array is addressed by a 32-bit byte offset
+  if ((long long)(D.B.hi[1] - D.B.lo[1]) * (D.B.hi[2] - D.B.lo[2]) * 32 >= (1ll << 31)) return (int)hipErrorInvalidValue;
+  if (!sin[0] || !sin[1] || !sout[0] || !sout[1] || sin[0] == sout[0] || sin[1] == sout[1])
+    return (int)hipErrorInvalidValue;
+  D.sin0 = (const double*)sin[0];
+  D.sin1 = (const double*)sin[1];
+  D.sout0 = (double*)sout[0];
+  D.sout1 = (double*)sout[1];
+  D.lut = lut;
+  D.nid = nid;
+  D.cbd = cbd;
+  TbSrc64 sv;
+  for (int l = 0; l < 8; ++l) sv.v[l] = (src[3] >= 0 && l < steps) ? src_vals[l] : 0.0;
+  const double* none[3] = {nullptr, nullptr, nullptr};
+  hipStream_t s = (hipStream_t)stream;
+#define TB64D(TT) \
+  launch_tb64<TT, 1, true, 8>(false, ein, hin, eout, hout, none, none, cb, db, nx, ny, nz, b, O, xchunk, src, sv, s, \
+                              nullptr, nullptr, &D)
+  switch (steps) {
+    case 1: return TB64D(1);
+    case 2: return TB64D(2);
+    case 3: return TB64D(3);
+    case 4: return TB64D(4);
+    case 5: return TB64D(5);
+  }
+#undef TB64D
+  return (int)hipErrorInvalidValue;
 }
 
 // ... with the TF/SF corrections of the device set table ``tf`` (tfsf_dev.h

@@ -191,7 +191,7 @@ class BlockedStepping:
         if (mode == "off" or not cfg.use_metamaterials or cfg.scheme != "3d" or not hasattr(self.ops, "tb_drude_step")
                 or (self.ops.name != "hip" and mode != "on")):
             return None
-        if self.ops.name == "hip" and (self.dtype != torch.float32 or self.domain.shape[2] % 4 != 0):
+        if self.ops.name == "hip" and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
             return None
         if (self.planes != 1 or cfg.use_amp_mode or self.graph_mode
                 or not self.use_upml_chain or getattr(self, "chain_regions", None) is None or self.use_cpml
@@ -328,24 +328,32 @@ class BlockedStepping:
             lut[q, :r.shape[0]] = r
         # gbox: this rank's box (the global box clipped to its allocation)
         return {"T": T, "box": Bl, "gbox": B, "store": store, "ids": ids4, "cbd": cbd,
-                "lut": lut.to(device=self.device, dtype=torch.float32 if self.ops.name == "hip" else self.dtype)
-                .contiguous()}
+                "lut": lut.to(device=self.device, dtype=self.dtype).contiguous()}
 
     def _finish_drude_blk(self) -> None:
         """Allocates the two state sets of the planned Drude pass (ids in
         .w of the first array, as float bits) and arms it."""
         dp = self._drude_plan
         bshape = tuple(dp["box"][1][d] - dp["box"][0][d] for d in range(3)) + (4,)
-        dt = torch.float32 if self.ops.name == "hip" else self.dtype
         state = []
         for _ in range(2):
-            s0 = torch.zeros(bshape, dtype=dt, device=self.device)
-            s1 = torch.zeros(bshape, dtype=dt, device=self.device)
-            if dt == torch.float32:
-                s0[..., 3] = dp["ids"].view(torch.float32)
+            s0 = torch.zeros(bshape, dtype=self.dtype, device=self.device)
+            s1 = torch.zeros(bshape, dtype=self.dtype, device=self.device)
+            self._drude_ids_in(s0, dp["ids"])
             state.append((s0, s1))
         self.drude_blk = dict(dp, state=state, cur=0, loc="chain")
         self._chain_plan_cache = {}
+
+    def _drude_ids_in(self, s0, ids) -> None:
+        """The HIP kernels' material ids into .w of the first state array (as
+        float bits; fp64: the low word of the double); the torch oracle reads
+        them from the plan."""
+        if self.ops.name != "hip":
+            return
+        if s0.dtype == torch.float32:
+            s0[..., 3] = ids.view(torch.float32)
+        else:
+            s0[..., 3] = (ids.to(torch.int64) & 0xFFFFFFFF).view(torch.float64)
 
     def _drude_lv(self, t, S):
         """The local box ``S`` of an auxiliary level (region-local or full-grid)."""
@@ -414,8 +422,7 @@ class BlockedStepping:
             # cells only; the ghost state came from the neighbours with THEIR material ids in .w
             # (fp32 state): this rank's ids back in
             ob = box_intersect(ob, self.domain.to_local(self.domain.owned_global()))
-            if sin[0].dtype == torch.float32:
-                sin[0][..., 3] = db["ids"].view(torch.float32)
+            self._drude_ids_in(sin[0], db["ids"])
             if box_empty(ob):
                 db["cur"] ^= 1
                 return

@@ -960,10 +960,11 @@ class HipOps:
         (b0 cbd, b2, m1, m2), ``drude["cbd"]`` the D coefficient.  Uniform
         media elsewhere; ``sources`` as :meth:`tb_step`."""
         E, H = ("Ex", "Ey", "Ez"), ("Hx", "Hy", "Hz")
-        if self.dtype != torch.float32 or not (1 <= steps <= self.tb_drude_max_steps):
-            raise HipError("Drude passes: fp32, 1..%d steps" % self.tb_drude_max_steps)
+        if not (1 <= steps <= self.tb_drude_max_steps):
+            raise HipError("Drude passes: 1..%d steps" % self.tb_drude_max_steps)
         shape = tuple(fin["Ex"].shape)
-        if shape[2] % 4 != 0:
+        f32 = self.dtype == torch.float32
+        if f32 and shape[2] % 4 != 0:
             raise HipError("fp32 tb_drude_step needs nz %% 4 == 0, got %s" % (shape,))
         for c in E + H:
             self._check_tensor(fin[c], shape)
@@ -1006,8 +1007,9 @@ class HipOps:
             src = [idx[0], idx[1], idx[2], E.index(comp)]
         arr = lambda names, f: (c_vp * 3)(*[f[c].data_ptr() for c in names])
         two = lambda ts: (c_vp * 2)(*[t.data_ptr() for t in ts])
-        self.lib.fdtd_set_tb_dr_shape(c_int(self.tb_dr_shape))
-        rc = self.lib.fdtd_tb3d_drude_f32(
+        if f32:
+            self.lib.fdtd_set_tb_dr_shape(c_int(self.tb_dr_shape))
+        rc = (self.lib.fdtd_tb3d_drude_f32 if f32 else self.lib.fdtd_tb3d_drude_f64)(
             arr(E, fin), arr(H, fin), arr(E, fout), arr(H, fout), c_double(cbv), c_double(dbv), c_int(shape[0]),
             c_int(shape[1]), c_int(shape[2]), _box_arr([boxes[c] for c in E + H]), _box_arr([obox]),
             c_int(self.tb_xchunk), c_int(steps), (c_int * 4)(*src), (c_double * 8)(*vals), _box_arr([B]),

@@ -1,6 +1,7 @@
 """The Drude box inside the blocked passes on the GPU (csrc/tb3d_mr.h DrDev,
-fdtd_tb3d_drude_f32): blocked vs the stepped HIP chain vs the fp64 torch
-oracle, without and with UPML, a sphere on the domain face, tails."""
+fdtd_tb3d_drude_f32; fp64: csrc/yee3d_tb64.hip DrDev64, fdtd_tb3d_drude_f64):
+blocked vs the stepped HIP chain vs the fp64 torch oracle, without and with
+UPML, a sphere on the domain face, TF/SF, tails."""
 import dataclasses
 
 import pytest
@@ -47,26 +48,34 @@ def _run(cfg, backend, device, dtype, steps=None):
     return s
 
 
+# fp64 (the reference's default value type): the fp64 blocked kernel's Drude variant
+F64 = ("nopml-T4-tail", "upml-T3", "face", "upml-tfsf", "upml-tfsf-oblique")
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
 @pytest.mark.parametrize("name,extra,T,steps", CASES, ids=[c[0] for c in CASES])
-def test_drude_blocked_gpu(gpu, name, extra, T, steps):
-    cfg = SchemeConfig(time_steps=steps, **dict(BASE, **extra))
-    blk = _run(dataclasses.replace(cfg, hybrid_block=T, time_block=T), "hip", gpu, torch.float32)
+def test_drude_blocked_gpu(gpu, name, extra, T, steps, dtype):
+    if dtype == "f64" and name not in F64:
+        pytest.skip("fp64: a subset of the cases")
+    cfg = SchemeConfig(time_steps=steps, **dict(BASE, dtype=dtype, **extra))
+    dt = torch.float32 if dtype == "f32" else torch.float64
+    blk = _run(dataclasses.replace(cfg, hybrid_block=T, time_block=T), "hip", gpu, dt)
     assert blk.drude_blk is not None, "blocked Drude plan rejected"
     assert blk.ops.launches > 0
     if cfg.use_tfsf:
         assert blk.hybrid is not None and blk.hybrid["drude"]
         assert blk.hybrid["core_tfsf"] == (not name.endswith("oblique")), blk.hybrid["core_tfsf"]
-    st = _run(dataclasses.replace(cfg, blocked_drude="off", hybrid_block=1, time_block=1), "hip", gpu, torch.float32)
+    st = _run(dataclasses.replace(cfg, blocked_drude="off", hybrid_block=1, time_block=1), "hip", gpu, dt)
     assert st.drude_blk is None
     ref = _run(dataclasses.replace(cfg, blocked_drude="off", hybrid_block=1, time_block=1, dtype="f64"), "torch",
                "cpu", torch.float64)
-    tol = 2e-5
+    tol = 2e-5 if dtype == "f32" else 1e-11
     for c in ref.comps:
         scale = max(float(ref.F[0][o].abs().max()) for o in ref.comps if o[0] == c[0]) + 1e-30
         e_st = float((blk.F[0][c].double().cpu() - st.F[0][c].double().cpu()).abs().max())
         e_ref = float((blk.F[0][c].double().cpu() - ref.F[0][c]).abs().max())
-        assert e_st <= tol * scale, (name, c, "blocked vs stepped", e_st, scale)
-        assert e_ref <= 10 * tol * scale, (name, c, "blocked vs fp64 oracle", e_ref, scale)
+        assert e_st <= tol * scale, (name, dtype, c, "blocked vs stepped", e_st, scale)
+        assert e_ref <= 10 * tol * scale, (name, dtype, c, "blocked vs fp64 oracle", e_ref, scale)
 
 
 def test_drude_blocked_state_round_trip_gpu(gpu):
