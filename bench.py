@@ -236,6 +236,11 @@ PHYSICS_CONFIGS = (
       "--use-pml", "--sphere-center-x", "256", "--sphere-center-y", "256", "--sphere-center-z", "256",
       "--sphere-radius", "128"]),
 )
+# the same configs in fp64, the reference's default value type (CMakeLists.txt VALUE_TYPE "d")
+PHYSICS_CONFIGS += tuple(
+    (name + "_f64", desc.replace("fp32", "fp64 (the reference's default value type)"),
+     [("f64" if v == "f32" else v) for v in args])
+    for name, desc, args in PHYSICS_CONFIGS)
 
 
 def physics_args(args, n: int):
