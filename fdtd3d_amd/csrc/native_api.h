@@ -126,9 +126,43 @@ int tb3d(const float* const* ei, const float* const* hi, float* const* eo, float
 int tb3d(const double* const* ei, const double* const* hi, double* const* eo, double* const* ho,
          const double* const* cbs, const double* const* dbs, double cb, double db, int nx, int ny, int nz,
          const int* bx, int T, const int* src, const double* vals, void* s, const void* = nullptr,
-         const int* = nullptr) {
-  const int ob[6] = {0, 0, 0, nx, ny, nz};
-  return fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, s);
+         const int* = nullptr, const int* obox = nullptr) {
+  const int whole[6] = {0, 0, 0, nx, ny, nz};
+  return fdtd_tb3d_f64(ei, hi, eo, ho, cbs, dbs, cb, db, nx, ny, nz, bx, obox ? obox : whole, 0, T, src, vals, s);
+}
+// the Drude pass of a hybrid pass (fp32: tb3d_mr.h DrDev, fp64: yee3d_tb64.hip DrDev64)
+int drude3d(const float* const* ei, const float* const* hi, float* const* eo, float* const* ho, double cb, double db,
+            int nx, int ny, int nz, const int* bx, const int* ob, int T, const int* src, const double* vals,
+            const int* bb, void* const* sin, void* const* sout, const float* lut, int nid, double cbd, void* s) {
+  return fdtd_tb3d_drude_f32(ei, hi, eo, ho, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, bb, sin, sout, lut, nid,
+                             cbd, s);
+}
+int drude3d(const double* const* ei, const double* const* hi, double* const* eo, double* const* ho, double cb,
+            double db, int nx, int ny, int nz, const int* bx, const int* ob, int T, const int* src, const double* vals,
+            const int* bb, void* const* sin, void* const* sout, const double* lut, int nid, double cbd, void* s) {
+  return fdtd_tb3d_drude_f64(ei, hi, eo, ho, cb, db, nx, ny, nz, bx, ob, 0, T, src, vals, bb, sin, sout, lut, nid,
+                             cbd, s);
+}
+// CPML half steps with the psi terms folded in (yee3d_cpml.hip, 4-cell z lanes)
+int cpml_e3d(float* const* F, const float* const* C, double cb, int nx, int ny, int nz, const int* bx,
+             const void* const* P, const int* I, void* s) {
+  return fdtd_update_e3d_cpml_v4_f32(F[0], F[1], F[2], F[3], F[4], F[5], C[0], C[1], C[2], cb, nx, ny, nz, bx, 0, P,
+                                     I, s);
+}
+int cpml_e3d(double* const* F, const double* const* C, double cb, int nx, int ny, int nz, const int* bx,
+             const void* const* P, const int* I, void* s) {
+  return fdtd_update_e3d_cpml_v4_f64(F[0], F[1], F[2], F[3], F[4], F[5], C[0], C[1], C[2], cb, nx, ny, nz, bx, 0, P,
+                                     I, s);
+}
+int cpml_h3d(float* const* F, const float* const* C, double db, int nx, int ny, int nz, const int* bx,
+             const void* const* P, const int* I, void* s) {
+  return fdtd_update_h3d_cpml_v4_f32(F[3], F[4], F[5], F[0], F[1], F[2], C[3], C[4], C[5], db, nx, ny, nz, bx, 0, P,
+                                     I, s);
+}
+int cpml_h3d(double* const* F, const double* const* C, double db, int nx, int ny, int nz, const int* bx,
+             const void* const* P, const int* I, void* s) {
+  return fdtd_update_h3d_cpml_v4_f64(F[3], F[4], F[5], F[0], F[1], F[2], C[3], C[4], C[5], db, nx, ny, nz, bx, 0, P,
+                                     I, s);
 }
 int tb2d(int mode, const float* const* ei, const float* const* hi, float* const* eo, float* const* ho,
          const float* const* cs, double cb, double db, int nx, int ny, const int* bx, const int* ob, int T,

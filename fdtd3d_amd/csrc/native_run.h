@@ -70,7 +70,7 @@ class NativeRun {
   bool res1 = false;
   int T_h = 1;
   std::vector<IBox> hcores, hshell[8], hcopy;
-  Dev<float> DRS[4], DRL;
+  Dev<T> DRS[4], DRL;
   int dr_nid = 0, dr_cur = 0;
   double dr_cbd = 0.0;
   int T2_h = 1;
@@ -356,14 +356,14 @@ void NativeRun<T>::setup_chain_regions() {
 }
 
 // Drude box inside the blocked passes (models/blocking.py _plan_drude_blk,
-// tb3d_mr.h DrDev): every hybrid pass runs the plain blocked core over the
-// box too, then the Drude variant over the box grown by T, carrying
-// (delta = D - Dp, Ep) per E component; the stepped chain never runs on
-// the box.  fp32 3D electric Drude spheres without TF/SF, fresh runs (the
-// native checkpoints cover plain media).
+// tb3d_mr.h DrDev, fp64: yee3d_tb64.hip DrDev64): every hybrid pass runs the
+// plain blocked core over the box too, then the Drude variant over the box
+// grown by T, carrying (delta = D - Dp, Ep) per E component; the stepped
+// chain never runs on the box.  3D electric Drude spheres without TF/SF,
+// fresh runs (the native checkpoints cover plain media).
 template <typename T>
 void NativeRun<T>::plan_drude() {
-  if (!(sizeof(T) == 4 && v4 && upml && dim == 3 && s.doUseMetamaterials && s.blockedDrude != "off" &&
+  if (!((v4 || sizeof(T) == 8) && upml && dim == 3 && s.doUseMetamaterials && s.blockedDrude != "off" &&
         s.dispersion != "lorentz" && !tfsf && !amp && !percell && !chain_regs.empty() && !plain_regs.empty() &&
         chain_disp.back() && (upt.disp[0] || upt.disp[1] || upt.disp[2]) && !upt.disp[3] && !upt.disp[4] &&
         !upt.disp[5]))
@@ -414,7 +414,8 @@ void NativeRun<T>::plan_blocking() {
                : 1;
   // 1D: the whole run in one launch of the register-resident kernel
   res1 = dim == 1 && use_fused && N[0] <= fdtd_res1d_max_cells((int)sizeof(T));
-  const int T_h_def = s.hybridBlock == 0 ? 5 : s.hybridBlock;
+  // (fp64: 4 steps per pass, models/blocking.py F64_AUTO_STEPS)
+  const int T_h_def = s.hybridBlock == 0 ? (sizeof(T) == 4 ? 5 : 4) : s.hybridBlock;
   if (dr_blk) {
     // (models/blocking.py DRUDE_AUTO_STEPS: the Drude variant holds T - 1 levels in registers)
     const int T_dr = s.hybridBlock > 0 ? s.hybridBlock : (s.timeBlock > 0 ? s.timeBlock : 4);
@@ -450,8 +451,11 @@ void NativeRun<T>::plan_hybrid3d(int T_h_req) {
   const bool drude_h = !dbox_h.empty();
   // TF/SF without absorbing layers: the shell is the TF/SF band on the plain kernels
   const bool tfsf_h = tfsf && !s.doUsePML && !upml;
-  if (!(scheme == "3d" && sizeof(T) == 4 && v4 && (cpml || upml_h || drude_h || tfsf_h) && !percell && !amp &&
-        T_h_req > 1 && T_h_req <= fdtd_tb_max_steps()))
+  // (fp32 rows of float4 lanes; fp64: the CPML windows' 4-cell double groups)
+  const bool rows_ok = sizeof(T) == 4 ? v4 : N[2] % 4 == 0;
+  const int tb_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
+  if (!(scheme == "3d" && rows_ok && (cpml || upml_h || drude_h || tfsf_h) && !percell && !amp && T_h_req > 1 &&
+        T_h_req <= tb_max))
     return;
   const int Th = T_h_req;
   const int pml[3] = {s.doUsePML ? s.pmlSizeX + (upml ? 1 : 0) : 0, s.doUsePML ? s.pmlSizeY + (upml ? 1 : 0) : 0,
@@ -549,30 +553,31 @@ void NativeRun<T>::setup_drude_state() {
     std::fprintf(stderr, "internal error: Drude LUT of %d rows after planning\n", dr_nid);
     std::exit(3);
   }
-  std::vector<float> rows((size_t)3 * dr_nid * 4, 0.f);
+  std::vector<T> rows((size_t)3 * dr_nid * 4, T(0));
   for (int c = 0; c < 3; ++c) {
-    float* r = rows.data() + (size_t)c * dr_nid * 4;
+    T* r = rows.data() + (size_t)c * dr_nid * 4;
     if (!upt.disp[c]) {
-      r[0] = (float)cb;
-      r[2] = 1.f;
+      r[0] = (T)cb;
+      r[2] = T(1);
       continue;
     }
     std::vector<T> tab(5 * (size_t)upt.nlut[c]);
     HIP_OK(hipMemcpy(tab.data(), upt.lut[c], tab.size() * sizeof(T), hipMemcpyDeviceToHost));
     for (int q = 0; q < upt.nlut[c]; ++q) {
-      r[4 * q] = (float)((double)tab[5 * q] * dr_cbd);
-      r[4 * q + 1] = (float)tab[5 * q + 2];
-      r[4 * q + 2] = (float)tab[5 * q + 3];
-      r[4 * q + 3] = (float)tab[5 * q + 4];
+      r[4 * q] = (T)((double)tab[5 * q] * dr_cbd);
+      r[4 * q + 1] = tab[5 * q + 2];
+      r[4 * q + 2] = tab[5 * q + 3];
+      r[4 * q + 3] = tab[5 * q + 4];
     }
   }
   DRL.alloc(rows.size());
-  HIP_OK(hipMemcpy(DRL.p, rows.data(), rows.size() * sizeof(float), hipMemcpyHostToDevice));
-  std::vector<float> s0(4 * nb, 0.f);
+  HIP_OK(hipMemcpy(DRL.p, rows.data(), rows.size() * sizeof(T), hipMemcpyHostToDevice));
+  // the ids' bits in the first 4 bytes of the fourth element (fp64: its low word)
+  std::vector<T> s0(4 * nb, T(0));
   for (size_t e = 0; e < nb; ++e) std::memcpy(&s0[4 * e + 3], &ids[e], 4);
   for (int q = 0; q < 4; ++q) DRS[q].alloc(4 * nb);
-  HIP_OK(hipMemcpy(DRS[0].p, s0.data(), s0.size() * sizeof(float), hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(DRS[2].p, s0.data(), s0.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(DRS[0].p, s0.data(), s0.size() * sizeof(T), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(DRS[2].p, s0.data(), s0.size() * sizeof(T), hipMemcpyHostToDevice));
 }
 
 // 2D hybrid passes (models/blocking.py on yee2d_tb.hip): every T steps the
@@ -894,7 +899,7 @@ void NativeRun<T>::upml_shell(int kind, const std::vector<IBox>& wins) {
 // pass's last k steps: band depth k - q at step q)
 template <typename T>
 void NativeRun<T>::hybrid_pass(int t, int k) {
-  if constexpr (sizeof(T) == 4) {
+  {
     const T* ei[3] = {F[0].p, F[1].p, F[2].p};
     const T* hi[3] = {F[3].p, F[4].p, F[5].p};
     T* eo[3] = {G[0].p, G[1].p, G[2].p};
@@ -922,16 +927,16 @@ void NativeRun<T>::hybrid_pass(int t, int k) {
       const int src[4] = {sp[0], sp[1], sp[2], point_src ? src_comp : -1};
       void* sin[2] = {DRS[2 * dr_cur].p, DRS[2 * dr_cur + 1].p};
       void* sout[2] = {DRS[2 * (1 - dr_cur)].p, DRS[2 * (1 - dr_cur) + 1].p};
-      K_OK(fdtd_tb3d_drude_f32(ei, hi, eo, ho, cb, db, N[0], N[1], N[2], boxes, ob, 0, k, src, vals, bb, sin, sout,
-                               DRL.p, dr_nid, dr_cbd, st));
+      K_OK(drude3d(ei, hi, eo, ho, cb, db, N[0], N[1], N[2], boxes, ob, k, src, vals, bb, sin, sout, DRL.p, dr_nid,
+                   dr_cbd, st));
       dr_cur ^= 1;
     }
     for (int q0 = 0; q0 < k; ++q0) hybrid_shell_step(T_h - k + q0, src_val(t + q0));  // band depth k - q0
-    float* src6[6] = {F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p};
-    float* dst6[6] = {G[0].p, G[1].p, G[2].p, G[3].p, G[4].p, G[5].p};
+    T* src6[6] = {F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p};
+    T* dst6[6] = {G[0].p, G[1].p, G[2].p, G[3].p, G[4].p, G[5].p};
     for (const IBox& b : hcopy) {
       const int bx[6] = {b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2]};
-      K_OK(fdtd_box_xfer_f32(src6, dst6, 6, N[1], N[2], bx, st));
+      K_OK(xfer(src6, dst6, 6, N[1], N[2], bx, st));
     }
     for (int c = 0; c < 6; ++c) std::swap(F[c].p, G[c].p);
   }
@@ -940,7 +945,9 @@ void NativeRun<T>::hybrid_pass(int t, int k) {
 // one stepped step of the hybrid shell on window set q, in place in F
 template <typename T>
 void NativeRun<T>::hybrid_shell_step(int q, double sv) {
-  if constexpr (sizeof(T) == 4) {
+  {
+    T* const F6[6] = {F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p};
+    const T* const none6[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
     if (upml) {
       upml_shell(0, hshell[q]);
@@ -955,8 +962,7 @@ void NativeRun<T>::hybrid_shell_step(int q, double sv) {
       par_windows(hshell[q], [&](const IBox& w, hipStream_t ss) {
         int wb2[18];
         window_boxes(w, 0, wb2);
-        K_OK(fdtd_update_e3d_cpml_v4_f32(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, nullptr, nullptr, nullptr,
-                                         cb, N[0], N[1], N[2], wb2, 0, cpt.P[0].data(), cpt.I[0].data(), ss));
+        K_OK(cpml_e3d(F6, none6, cb, N[0], N[1], N[2], wb2, cpt.P[0].data(), cpt.I[0].data(), ss));
       });
     }
     if (tfsf) tfsf_kind(0);
@@ -975,8 +981,7 @@ void NativeRun<T>::hybrid_shell_step(int q, double sv) {
       par_windows(hshell[q], [&](const IBox& w, hipStream_t ss) {
         int wb2[18];
         window_boxes(w, 3, wb2);
-        K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, nullptr, nullptr, nullptr,
-                                         db, N[0], N[1], N[2], wb2, 0, cpt.P[1].data(), cpt.I[1].data(), ss));
+        K_OK(cpml_h3d(F6, none6, db, N[0], N[1], N[2], wb2, cpt.P[1].data(), cpt.I[1].data(), ss));
       });
     }
     if (tfsf) tfsf_kind(1);

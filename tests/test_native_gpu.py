@@ -134,9 +134,8 @@ CASES = {
     "2d_tmz_amp_cpml": ["--2d", "--sizex", "60", "--sizey", "52", "--time-steps", "10", "--scene", "vacuum",
                         "--use-amp-mode", "--amplitude-time-steps", "300", "--use-pml", "--pml-type", "cpml"],
 }
-# (native hybrid passes are fp32; the stepped 3D CPML runs in both precisions)
-FP32_ONLY = {"3d_cpml_tfsf_hybrid", "3d_cpml_point_hybrid", "3d_upml_tfsf_hybrid", "3d_upml_point_hybrid",
-             "3d_drude_upml_hybrid", "3d_drude_hybrid", "3d_tfsf_hybrid"}
+# (round 6: the native hybrid passes run in both precisions -- fp64 blocked core, Drude pass and CPML windows)
+FP32_ONLY = set()
 # the converged step depends on running-maximum comparisons at round-off level: fp64 only
 FP64_ONLY = {"2d_tmz_amp_cpml"}
 
