@@ -191,15 +191,11 @@ class BlockedStepping:
         if (mode == "off" or not cfg.use_metamaterials or cfg.scheme != "3d" or not hasattr(self.ops, "tb_drude_step")
                 or (self.ops.name != "hip" and mode != "on")):
             return None
-        if self.ops.name == "hip" and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
-            return None
         if (self.planes != 1 or cfg.use_amp_mode or self.graph_mode
                 or not self.use_upml_chain or getattr(self, "chain_regions", None) is None or self.use_cpml
                 or getattr(cfg, "dispersion", "drude") != "drude" or self.hooks):
             return None
         if any("D1" in self.upml[c] for c in self.h_comps) or not any("D1" in self.upml[c] for c in self.e_comps):
-            return None
-        if any(not self.cb[c].is_scalar for c in self.comps):
             return None
         T = int(cfg.hybrid_block) if int(cfg.hybrid_block) > 0 else int(cfg.time_block)
         if T <= 0:
@@ -212,7 +208,10 @@ class BlockedStepping:
         G = self._drude_gbox()
         if G is None:
             return None
-        plan = self._plan_drude_local(T, G)
+        # (checks on this rank's arrays refuse through the vote below: every rank reaches it)
+        local_ok = (not (self.ops.name == "hip" and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0)
+                    and all(self.cb[c].is_scalar for c in self.comps))
+        plan = self._plan_drude_local(T, G) if local_ok else False
         if self.halo is not None:
             # every rank takes the pass or none does (False: this rank refused); a rank whose
             # allocation misses the box (None) runs the same pass plan without a Drude launch
@@ -484,15 +483,16 @@ class BlockedStepping:
         # 8192^2 TMz + TF/SF -- until the 2D passes replayed from HIP graphs:
         # 158k, profiles/graph2d_r4.md)
         # fp32 3D rows are float4 along z, 2D rows 16-byte lanes along y
+        shape_ok = True  # (this rank's arrays: refused through the vote, which every rank reaches)
         if self.ops.name == "hip":
             if two_d and self.domain.shape[1] % (16 // self.dtype.itemsize) != 0:
-                return
+                shape_ok = False
             if not two_d and self.dtype == torch.float32 and self.domain.shape[2] % 4 != 0:
-                return
-        plan = self._voted(self._hybrid_plan(H))
+                shape_ok = False
+        plan = self._voted(self._hybrid_plan(H) if shape_ok else None)
         if plan is None and dg is not None:
             self._drude_plan = self._drude_glob = dg = None  # the stepped dispersive box after all
-            plan = self._voted(self._hybrid_plan(H))
+            plan = self._voted(self._hybrid_plan(H) if shape_ok else None)
         if plan is None:
             return
         if int(cfg.hybrid_block) <= 0 and plan["cut_cells"] > 0.5 * self.cells():
