@@ -119,6 +119,30 @@ __device__ __forceinline__ V cpml_term(const CpmlT<T>& t, const V& d, int i, int
 }
 
 // F += c * (sa*da + sb*db + sa*corr_a + sb*corr_b) on the masked elements
+// Several disjoint windows of one half step in ONE launch (the hybrid shell:
+// its windows are independent; one launch per row layout instead of one per
+// window): per window its three component boxes, their union, x chunk and
+// block grid; blocks numbered window by window (start[w]).
+constexpr int MAXW3 = 8;
+struct Win3 {
+  Box3 bx[MAXW3], by[MAXW3], bz[MAXW3], bu[MAXW3];
+  int xc[MAXW3], gx[MAXW3], gy[MAXW3], start[MAXW3 + 1];
+  int n;
+};
+
+// window of this block (wave-uniform) and its block coordinates in it
+__device__ __forceinline__ int win3_of(const Win3& W, int& gbx, int& gby, int& gbz) {
+  const int id = (int)blockIdx.x;
+  int w = 0;
+#pragma unroll
+  for (int q = 1; q < MAXW3; ++q) w += (q < W.n && id >= W.start[q]) ? 1 : 0;
+  const int loc = id - W.start[w];
+  gbx = loc % W.gx[w];
+  gby = (loc / W.gx[w]) % W.gy[w];
+  gbz = loc / (W.gx[w] * W.gy[w]);
+  return w;
+}
+
 template <typename V>
 __device__ __forceinline__ void apply4(V& f, const V& c, const V& v, unsigned m) {
 #pragma unroll
@@ -138,17 +162,17 @@ __device__ __forceinline__ V comb(const V& da, const V& ca, const V& db, const V
 }
 
 template <typename T, bool PERCELL, int LZ>
-__global__ __launch_bounds__(64 * TY) void k_update_e3d_cpml_v4(
+__device__ __forceinline__ void e3d_cpml_body(
     T* __restrict__ ex, T* __restrict__ ey, T* __restrict__ ez, const T* __restrict__ hx,
     const T* __restrict__ hy, const T* __restrict__ hz, const T* __restrict__ cbx,
-    const T* __restrict__ cby, const T* __restrict__ cbz, T cb, int nx, int ny, int nz, Box3 bx,
-    Box3 by, Box3 bz, Box3 bu, int xchunk, CpmlK<T> P) {
+    const T* __restrict__ cby, const T* __restrict__ cbz, T cb, int nx, int ny, int nz, const Box3& bx, const Box3& by,
+    const Box3& bz, const Box3& bu, int xchunk, int gbx, int gby, int gbz, const CpmlK<T>& P) {
   // LZ lanes per z row, 64 / LZ rows per wave (LZ < 64 for z-thin boxes)
   const int zl = threadIdx.x % LZ;
-  const int kb = (bu.lo[2] & ~3) + 4 * (blockIdx.x * LZ + zl);
-  const int j = bu.lo[1] + (blockIdx.y * TY + threadIdx.y) * (64 / LZ) + threadIdx.x / LZ;
+  const int kb = (bu.lo[2] & ~3) + 4 * (gbx * LZ + zl);
+  const int j = bu.lo[1] + (gby * TY + threadIdx.y) * (64 / LZ) + threadIdx.x / LZ;
   const bool act = (kb < bu.hi[2]) && (j < bu.hi[1]);
-  const int i0 = bu.lo[0] + blockIdx.z * xchunk;
+  const int i0 = bu.lo[0] + gbz * xchunk;
   const int i1 = min(i0 + xchunk, bu.hi[0]);
   const size_t plane = (size_t)ny * nz;
   const size_t row = act ? (size_t)j * nz + kb : 0;
@@ -214,18 +238,40 @@ __global__ __launch_bounds__(64 * TY) void k_update_e3d_cpml_v4(
 }
 
 template <typename T, bool PERCELL, int LZ>
-__global__ __launch_bounds__(64 * TY) void k_update_h3d_cpml_v4(
+__global__ __launch_bounds__(64 * TY) void k_update_e3d_cpml_v4(
+    T* __restrict__ ex, T* __restrict__ ey, T* __restrict__ ez, const T* __restrict__ hx,
+    const T* __restrict__ hy, const T* __restrict__ hz, const T* __restrict__ cbx,
+    const T* __restrict__ cby, const T* __restrict__ cbz, T cb, int nx, int ny, int nz, Box3 bx,
+    Box3 by, Box3 bz, Box3 bu, int xchunk, CpmlK<T> P) {
+  e3d_cpml_body<T, PERCELL, LZ>(ex, ey, ez, hx, hy, hz, cbx, cby, cbz, cb, nx, ny, nz, bx, by, bz, bu, xchunk,
+                                blockIdx.x, blockIdx.y, blockIdx.z, P);
+}
+
+template <typename T, bool PERCELL, int LZ>
+__global__ __launch_bounds__(64 * TY) void k_update_e3d_cpml_multi(
+    T* __restrict__ ex, T* __restrict__ ey, T* __restrict__ ez, const T* __restrict__ hx,
+    const T* __restrict__ hy, const T* __restrict__ hz, const T* __restrict__ cbx,
+    const T* __restrict__ cby, const T* __restrict__ cbz, T cb, int nx, int ny, int nz, Win3 W,
+    CpmlK<T> P) {
+  int gbx, gby, gbz;
+  const int w = win3_of(W, gbx, gby, gbz);
+  e3d_cpml_body<T, PERCELL, LZ>(ex, ey, ez, hx, hy, hz, cbx, cby, cbz, cb, nx, ny, nz, W.bx[w], W.by[w], W.bz[w],
+                                W.bu[w], W.xc[w], gbx, gby, gbz, P);
+}
+
+template <typename T, bool PERCELL, int LZ>
+__device__ __forceinline__ void h3d_cpml_body(
     T* __restrict__ hx, T* __restrict__ hy, T* __restrict__ hz, const T* __restrict__ ex,
     const T* __restrict__ ey, const T* __restrict__ ez, const T* __restrict__ dbx,
-    const T* __restrict__ dby, const T* __restrict__ dbz, T db, int nx, int ny, int nz, Box3 bx,
-    Box3 by, Box3 bz, Box3 bu, int xchunk, CpmlK<T> P) {
+    const T* __restrict__ dby, const T* __restrict__ dbz, T db, int nx, int ny, int nz, const Box3& bx, const Box3& by,
+    const Box3& bz, const Box3& bu, int xchunk, int gbx, int gby, int gbz, const CpmlK<T>& P) {
   // LZ lanes per z row, 64 / LZ rows per wave (LZ < 64 for z-thin boxes)
   const int zl = threadIdx.x % LZ;
-  const int kb = (bu.lo[2] & ~3) + 4 * (blockIdx.x * LZ + zl);
-  const int j = bu.lo[1] + (blockIdx.y * TY + threadIdx.y) * (64 / LZ) + threadIdx.x / LZ;
+  const int kb = (bu.lo[2] & ~3) + 4 * (gbx * LZ + zl);
+  const int j = bu.lo[1] + (gby * TY + threadIdx.y) * (64 / LZ) + threadIdx.x / LZ;
   const bool act = (kb < bu.hi[2]) && (j < bu.hi[1]);
   const bool ld_ok = (kb < nz) && (j < ny);
-  const int i0 = bu.lo[0] + blockIdx.z * xchunk;
+  const int i0 = bu.lo[0] + gbz * xchunk;
   const int i1 = min(i0 + xchunk, bu.hi[0]);
   const size_t plane = (size_t)ny * nz;
   const size_t row = ld_ok ? (size_t)j * nz + kb : 0;
@@ -290,6 +336,28 @@ __global__ __launch_bounds__(64 * TY) void k_update_h3d_cpml_v4(
     ey_c = ey_n;
     ez_c = ez_n;
   }
+}
+
+template <typename T, bool PERCELL, int LZ>
+__global__ __launch_bounds__(64 * TY) void k_update_h3d_cpml_v4(
+    T* __restrict__ hx, T* __restrict__ hy, T* __restrict__ hz, const T* __restrict__ ex,
+    const T* __restrict__ ey, const T* __restrict__ ez, const T* __restrict__ dbx,
+    const T* __restrict__ dby, const T* __restrict__ dbz, T db, int nx, int ny, int nz, Box3 bx,
+    Box3 by, Box3 bz, Box3 bu, int xchunk, CpmlK<T> P) {
+  h3d_cpml_body<T, PERCELL, LZ>(hx, hy, hz, ex, ey, ez, dbx, dby, dbz, db, nx, ny, nz, bx, by, bz, bu, xchunk,
+                                blockIdx.x, blockIdx.y, blockIdx.z, P);
+}
+
+template <typename T, bool PERCELL, int LZ>
+__global__ __launch_bounds__(64 * TY) void k_update_h3d_cpml_multi(
+    T* __restrict__ hx, T* __restrict__ hy, T* __restrict__ hz, const T* __restrict__ ex,
+    const T* __restrict__ ey, const T* __restrict__ ez, const T* __restrict__ dbx,
+    const T* __restrict__ dby, const T* __restrict__ dbz, T db, int nx, int ny, int nz, Win3 W,
+    CpmlK<T> P) {
+  int gbx, gby, gbz;
+  const int w = win3_of(W, gbx, gby, gbz);
+  h3d_cpml_body<T, PERCELL, LZ>(hx, hy, hz, ex, ey, ez, dbx, dby, dbz, db, nx, ny, nz, W.bx[w], W.by[w], W.bz[w],
+                                W.bu[w], W.xc[w], gbx, gby, gbz, P);
 }
 
 template <typename T>
@@ -385,6 +453,73 @@ int launch_cpml_h(T* hx, T* hy, T* hz, const T* ex, const T* ey, const T* ez, co
   FDTD_RETURN_LAUNCH_STATUS();
 }
 
+// the windows of one half step (boxes: 18 ints per window, the component
+// boxes) grouped by row layout, up to MAXW3 per launch
+template <typename T, bool KE>
+int launch_cpml_multi(T* f0, T* f1, T* f2, const T* g0, const T* g1, const T* g2, const T* c0, const T* c1,
+                      const T* c2, double cf, int nx, int ny, int nz, const int* boxes, int nwin,
+                      const void* const* cp, const int* ci, void* s) {
+  if (nz % 4 != 0 || nwin < 0) return (int)hipErrorInvalidValue;
+  const CpmlK<T> K = make_cpml<T>(cp, ci);
+  const bool pc = c0 != nullptr;
+  const hipStream_t st = (hipStream_t)s;
+  for (int lz : {64, 16, 8}) {
+    Win3 W;
+    W.n = 0;
+    int total = 0;
+    auto flush = [&]() {
+      if (W.n == 0) return;
+      W.start[W.n] = total;
+      for (int q = W.n + 1; q <= MAXW3; ++q) W.start[q] = total;
+      const dim3 g((unsigned)total), b(64, TY);
+#define CPML_MULTI(LZ)                                                                                          \
+  if (KE) {                                                                                                     \
+    if (pc)                                                                                                     \
+      k_update_e3d_cpml_multi<T, true, LZ><<<g, b, 0, st>>>(f0, f1, f2, g0, g1, g2, c0, c1, c2, (T)cf, nx, ny, nz, W, K); \
+    else                                                                                                        \
+      k_update_e3d_cpml_multi<T, false, LZ><<<g, b, 0, st>>>(f0, f1, f2, g0, g1, g2, c0, c1, c2, (T)cf, nx, ny, nz, W, K); \
+  } else {                                                                                                      \
+    if (pc)                                                                                                     \
+      k_update_h3d_cpml_multi<T, true, LZ><<<g, b, 0, st>>>(f0, f1, f2, g0, g1, g2, c0, c1, c2, (T)cf, nx, ny, nz, W, K); \
+    else                                                                                                        \
+      k_update_h3d_cpml_multi<T, false, LZ><<<g, b, 0, st>>>(f0, f1, f2, g0, g1, g2, c0, c1, c2, (T)cf, nx, ny, nz, W, K); \
+  }
+      if (lz == 64) {
+        CPML_MULTI(64)
+      } else if (lz == 16) {
+        CPML_MULTI(16)
+      } else {
+        CPML_MULTI(8)
+      }
+#undef CPML_MULTI
+      W.n = 0;
+      total = 0;
+    };
+    for (int q = 0; q < nwin; ++q) {
+      const Box3 bx = make_box(boxes + 18 * q), by = make_box(boxes + 18 * q + 6), bz = make_box(boxes + 18 * q + 12);
+      const Box3 bu = box_union(box_union(bx, by), bz);
+      if (box_empty(bu) || lanes_z(bu) != lz) continue;
+      const dim3 g1 = grid_c(bu, 1, lz);
+      const int xc = split_xchunk(bu.hi[0] - bu.lo[0], (long long)g1.x * g1.y, 0);
+      const dim3 g = grid_c(bu, xc, lz);
+      const int n = W.n;
+      W.bx[n] = bx;
+      W.by[n] = by;
+      W.bz[n] = bz;
+      W.bu[n] = bu;
+      W.xc[n] = xc;
+      W.gx[n] = (int)g.x;
+      W.gy[n] = (int)g.y;
+      W.start[n] = total;
+      total += (int)(g.x * g.y * g.z);
+      W.n = n + 1;
+      if (W.n == MAXW3) flush();
+    }
+    flush();
+  }
+  FDTD_RETURN_LAUNCH_STATUS();
+}
+
 }  // namespace
 
 // Same arguments as fdtd_update_{e,h}3d_v4_f32 plus the CPML term table
@@ -405,3 +540,25 @@ int launch_cpml_h(T* hx, T* hy, T* hz, const T* ex, const T* ey, const T* ez, co
   }
 FDTD_CPML_V4_API(f32, float)
 FDTD_CPML_V4_API(f64, double)
+
+// The split CPML updates of several disjoint windows in one launch per row
+// layout (the hybrid shell's windows of a half step): ``boxes`` = 18 ints per
+// window (the three component boxes), ``nwin`` windows; other arguments as
+// fdtd_update_{e,h}3d_cpml_v4_*.
+#define FDTD_CPML_MULTI_API(SUF, T)                                                                          \
+  FDTD_API int fdtd_update_e3d_cpml_multi_##SUF(T* ex, T* ey, T* ez, const T* hx, const T* hy, const T* hz,  \
+                                                const T* cbx, const T* cby, const T* cbz, double cb, int nx, \
+                                                int ny, int nz, const int* boxes, int nwin,                  \
+                                                const void* const* cp, const int* ci, void* s) {             \
+    return launch_cpml_multi<T, true>(ex, ey, ez, hx, hy, hz, cbx, cby, cbz, cb, nx, ny, nz, boxes, nwin, cp,  \
+                                      ci, s);                                                                \
+  }                                                                                                          \
+  FDTD_API int fdtd_update_h3d_cpml_multi_##SUF(T* hx, T* hy, T* hz, const T* ex, const T* ey, const T* ez,  \
+                                                const T* dbx, const T* dby, const T* dbz, double db, int nx, \
+                                                int ny, int nz, const int* boxes, int nwin,                  \
+                                                const void* const* cp, const int* ci, void* s) {             \
+    return launch_cpml_multi<T, false>(hx, hy, hz, ex, ey, ez, dbx, dby, dbz, db, nx, ny, nz, boxes, nwin, cp, \
+                                       ci, s);                                                               \
+  }
+FDTD_CPML_MULTI_API(f32, float)
+FDTD_CPML_MULTI_API(f64, double)

@@ -29,6 +29,7 @@ with the complex source ``sin + i cos`` split between them.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -170,6 +171,12 @@ def _torch_dtype(name: str):
 
 class YeeScheme(BlockedStepping):
     """A Yee FDTD solver on one (possibly decomposed) domain."""
+
+    # decomposed 3D hybrid shells with the folded CPML: the windows of a half step in one launch per row
+    # layout (a rank's in-order window launches; 512^3 config 3 on 2x2x1: 37.5k vs 33.3k Mcells/s per GPU,
+    # while one GPU keeps its per-window launches on the shell streams: 92.9k-94.9k vs 95.0k-95.6k,
+    # profiles/decomp_r6.md).  FDTD3D_MULTI_CPML=0: per-window launches (A/B)
+    multi_cpml = os.environ.get("FDTD3D_MULTI_CPML", "1") != "0"
 
     def __init__(self, cfg: SchemeConfig, ops, domain: Optional[Domain] = None, halo=None):
         self.cfg = cfg
@@ -1059,11 +1066,19 @@ class YeeScheme(BlockedStepping):
         multi = (len(windows) > 1 and not tfsf_here and self.hybrid is not None and not chain
                  and not self.use_upml_chain and not fused_cpml and (not self.use_cpml or cpml_once)
                  and self.cfg.scheme in ("tmz", "tez") and getattr(self.ops, "multi2d", False))
+        multi_cpml = (len(windows) > 1 and not tfsf_here and self.hybrid is not None and not chain and fused_cpml
+                      and self.cfg.scheme == "3d" and self.multi_cpml and self.halo is not None
+                      and hasattr(self.ops, "curl_update_cpml_multi"))
         if multi:
             # 2D hybrid shell: every window of the half step in one launch (its
             # passes replay from a HIP graph, where a step costs its launch count)
             self.ops.curl_update_multi(kind, [{c: self.local_box(c, w) for c in comps} for w in windows], F, F,
                                        self.cb)
+        elif multi_cpml:
+            # decomposed 3D hybrid shell with the folded CPML: the windows of the half step in one launch
+            # per row layout (a rank's small windows were launch-bound, profiles/decomp_r6.md)
+            self.ops.curl_update_cpml_multi(kind, [{c: self.local_box(c, w) for c in comps} for w in windows], F, F,
+                                            self.cb, ktab)
         elif len(windows) > 1 and not tfsf_here and self.hybrid is not None:
             # the hybrid shell's windows are disjoint: their launches of a half
             # step are independent and run side by side on several streams

@@ -1406,6 +1406,45 @@ class HipOps:
         _check(rc, "update_%s3d_cpml" % kind.lower())
         self.launches += 1
 
+    def curl_update_cpml_multi(self, kind: str, windows: Sequence[Dict[str, Box]], dst: Dict[str, torch.Tensor],
+                               src: Dict[str, torch.Tensor], cb: Dict[str, Coef], table) -> None:
+        """:meth:`curl_update_cpml` of several disjoint windows (per window the
+        component boxes) in one launch per row layout (yee3d_cpml.hip
+        ``Win3``, <= 8 windows a launch): the hybrid shell's windows of a half
+        step."""
+        names = ("Ex", "Ey", "Ez") if kind == "E" else ("Hx", "Hy", "Hz")
+        other = ("Hx", "Hy", "Hz") if kind == "E" else ("Ex", "Ey", "Ez")
+        shape = tuple(dst[names[0]].shape)
+        for c in names:
+            self._check_tensor(dst[c], shape)
+        for c in other:
+            self._check_tensor(src[c], shape)
+        if shape[2] % 4 != 0 or self.dtype not in (torch.float32, torch.float64):
+            raise HipError("fused CPML kernel needs fp32 / fp64 and nz % 4 == 0")
+        wins = [w for w in windows if not all(_empty(w[c]) for c in names)]
+        for w in wins:
+            for c in names:
+                if not _empty(w[c]):
+                    self._check_stencil_box(kind, c, w[c], shape)
+        if not wins:
+            return
+        per = [self._cell_or_none(cb[c]) for c in names]
+        if per[0] is not None:
+            per_p = [_ptr(self._scaled_cell(cb[c])) for c in names]
+            scal = 1.0
+        else:
+            per_p = [None, None, None]
+            scal = cb[names[0]].scalar
+            if any(cb[c].scalar != scal for c in names):
+                raise HipError("scalar coefficients must agree across components")
+        ptrs, ints, _keep = table
+        fn = self.fn("update_e3d_cpml_multi" if kind == "E" else "update_h3d_cpml_multi")
+        rc = fn(*[_ptr(dst[c]) for c in names], *[_ptr(src[c]) for c in other], *per_p, c_double(scal),
+                c_int(shape[0]), c_int(shape[1]), c_int(shape[2]), _box_arr([w[c] for w in wins for c in names]),
+                c_int(len(wins)), (c_vp * len(ptrs))(*ptrs), (c_int * len(ints))(*ints), _stream())
+        _check(rc, "update_%s3d_cpml_multi" % kind.lower())
+        self.launches += 1
+
     # ------------------------------------------------------------ HIP graphs
     def set_value_tab(self, t: torch.Tensor, idx: Sequence[int], tab: torch.Tensor, counter: torch.Tensor,
                       lag: int) -> None:
