@@ -365,6 +365,45 @@ inline unsigned reduce_grid(long long n) {
   return (unsigned)g;
 }
 
+// Many boxes of many arrays to / from contiguous buffers in ONE launch (the
+// halo exchange of a decomposed run: every message's fields and region-local
+// auxiliary arrays, packed before the sends / unpacked after the receives).
+// One table entry per (array, box, buffer part); the blocks of entry e are
+// blk0[e] .. blk0[e + 1] - 1, 256 elements each, box cells z fastest.
+struct BoxEnt {
+  long long arr;  // array base (its dims: ny x nz per x plane)
+  long long buf;  // this entry's first buffer element
+  int ny, nz;
+  int lo[3], hi[3];
+  int blk0, pad[3];
+};
+static_assert(sizeof(BoxEnt) == 64, "BoxEnt layout (parallel/halo.py _BoxList)");
+
+template <typename T, bool PACK>
+__global__ __launch_bounds__(256) void k_box_list(const BoxEnt* __restrict__ tab, int n) {
+  // the block's entry: binary search over blk0 (wave-uniform scalar loads)
+  typedef const __attribute__((address_space(4))) BoxEnt* EntPtr;
+  const EntPtr E = (EntPtr)tab;
+  const int b = (int)blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (E[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const int bx = E[lo].hi[0] - E[lo].lo[0], by = E[lo].hi[1] - E[lo].lo[1], bz = E[lo].hi[2] - E[lo].lo[2];
+  const int idx = (b - E[lo].blk0) * 256 + (int)threadIdx.x;
+  if (idx >= bx * by * bz) return;
+  const int k = idx % bz, jj = idx / bz;
+  const int j = jj % by, i = jj / by;
+  T* a = (T*)E[lo].arr;
+  T* f = (T*)E[lo].buf;
+  const size_t off = ((size_t)(E[lo].lo[0] + i) * E[lo].ny + (E[lo].lo[1] + j)) * E[lo].nz + (E[lo].lo[2] + k);
+  if (PACK)
+    f[idx] = a[off];
+  else
+    a[off] = f[idx];
+}
+
 }  // namespace
 
 #define FDTD_AUX_API(SUF, T)                                                                                  \
@@ -418,6 +457,21 @@ inline unsigned reduce_grid(long long n) {
 
 FDTD_AUX_API(f32, float)
 FDTD_AUX_API(f64, double)
+
+// k_box_list over a device table of n BoxEnt entries (nblocks = the last
+// entry's blk0 + its blocks): pack (arrays -> buffers) or unpack
+#define FDTD_BOX_LIST_API(SUF, T)                                                                            \
+  FDTD_API int fdtd_box_list_##SUF(const void* tab, int n, int nblocks, int pack, void* s) {                  \
+    if (n <= 0 || nblocks <= 0) return 0;                                                                     \
+    if (pack)                                                                                                 \
+      k_box_list<T, true><<<nblocks, 256, 0, (hipStream_t)s>>>((const BoxEnt*)tab, n);                       \
+    else                                                                                                      \
+      k_box_list<T, false><<<nblocks, 256, 0, (hipStream_t)s>>>((const BoxEnt*)tab, n);                      \
+    FDTD_RETURN_LAUNCH_STATUS();                                                                              \
+  }
+FDTD_BOX_LIST_API(f32, float)
+FDTD_BOX_LIST_API(f64, double)
+FDTD_API int fdtd_box_ent_size() { return (int)sizeof(BoxEnt); }
 
 template <typename T>
 int amplitude_many(const void* const* f, void* const* amp, int ncomp, int ny, int nz, const int* boxes,

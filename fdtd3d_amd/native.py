@@ -10,18 +10,38 @@ from __future__ import annotations
 import ctypes
 import json
 import os
+import threading
 from typing import Dict, Sequence, Tuple
 
 from .ops.build import EXE, LIB_HOST
 
 _lib = None
+_lock = threading.Lock()
+
+
+def _host_stale() -> bool:
+    """The host library is missing or older than a host source (the object
+    files do not travel to the GPU boxes, so their timestamps say nothing)."""
+    if not os.path.exists(LIB_HOST):
+        return True
+    from .ops import build as _b
+    t = os.path.getmtime(LIB_HOST)
+    return any(os.path.getmtime(d) > t for src in _b.host_sources() for d in _b._deps(src))
 
 
 def load_host_library(build_if_missing: bool = True) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if build_if_missing:
+    with _lock:  # decomposed thread ranks reach here together on their first hybrid plan
+        if _lib is not None:
+            return _lib
+        return _load_host_library(build_if_missing)
+
+
+def _load_host_library(build_if_missing: bool) -> ctypes.CDLL:
+    global _lib
+    if build_if_missing and _host_stale():
         from .ops import build as _b
         _b.build(exe=False, hip=False)  # incremental: rebuilds only when csrc changed
     lib = ctypes.CDLL(LIB_HOST)

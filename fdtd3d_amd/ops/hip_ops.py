@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -51,7 +52,17 @@ def lib_path() -> str:
     return _LIB_PATH
 
 
+_LIB_LOCK = threading.Lock()
+
+
 def load_library(build_if_missing: bool = True):
+    if _LIB is not None:
+        return _LIB
+    with _LIB_LOCK:  # thread ranks construct their ops together
+        return _load_library(build_if_missing)
+
+
+def _load_library(build_if_missing: bool):
     global _LIB
     if _LIB is not None:
         return _LIB
@@ -647,6 +658,20 @@ class HipOps:
         _check(rc, "box_pack")
         self.launches += 1
         return out
+
+    def box_list(self, table: torch.Tensor, n: int, nblocks: int, pack: bool) -> None:
+        """Many (array, box) <-> contiguous buffer copies in one launch
+        (aux_kernels.hip k_box_list); ``table`` = n device entries of
+        ``box_ent_size()`` bytes (parallel/halo.py ``_BoxList`` builds them and
+        checked every box against its array)."""
+        if table.device.type != "cuda" or not table.is_contiguous():
+            raise HipError("box_list: a contiguous device table")
+        rc = self.fn("box_list")(_ptr(table), c_int(n), c_int(nblocks), c_int(1 if pack else 0), _stream())
+        _check(rc, "box_list")
+        self.launches += 1
+
+    def box_ent_size(self) -> int:
+        return int(self.lib.fdtd_box_ent_size())
 
     def unpack(self, tensors: Sequence[torch.Tensor], box: Box, buf: torch.Tensor) -> None:
         shape = tuple(tensors[0].shape)

@@ -32,6 +32,7 @@ MI355X, ``gloo`` on CPU):
 from __future__ import annotations
 
 import itertools
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -284,6 +285,9 @@ class HaloExchanger:
     def _exchange_direct(self, scheme) -> None:
         ops = scheme.ops
         tensors, boxed = _split_state(scheme)
+        if self.listed and hasattr(ops, "box_list") and tensors[0].is_cuda:
+            self._exchange_direct_listed(ops, tensors, boxed)
+            return
         d = self.domain
         ops_list, recvs = [], []
         for off, peer, sg, rg in self.deep_messages():
@@ -328,8 +332,84 @@ class HaloExchanger:
         for rbox, rg, rb in recvs:
             _unpack_state(ops, tensors, boxed, rbox, rg, d, rb)
 
+    def _direct_plan(self, ops, tensors, boxed):
+        """The direct exchange of this state set as a fixed plan: the P2P
+        ops (x faces straight from the arrays, the other messages through
+        plan-owned buffers) and ONE table of every pack and one of every
+        unpack (``ops.box_list``), cached per set of state arrays (the field
+        buffers alternate between passes, the UPML levels rotate).  The same
+        message layout as :func:`_pack_state`: per array its box, fields first."""
+        key = (tuple(t.data_ptr() for t in tensors),
+               tuple((t.data_ptr(), cover, first, zmul) for t, cover, first, zmul in boxed))
+        plans = self.__dict__.setdefault("_plans", {})
+        plan = plans.get(key)
+        if plan is not None:
+            return plan
+        d = self.domain
+        ops_list, nbytes, nmsg = [], 0, 0
+        pack, unpack = _BoxList(), _BoxList()
+        bufs = []
+        for off, peer, sg, rg in self.deep_messages():
+            sbox, rbox = d.to_local(sg), d.to_local(rg)
+            key_m = (off[0] + 1) * 9 + (off[1] + 1) * 3 + (off[2] + 1)
+            back = (-off[0] + 1) * 9 + (-off[1] + 1) * 3 + (-off[2] + 1)
+            if (off[1] == 0 and off[2] == 0 and self.direct_x_faces
+                    and not any(_boxed_part(g, cover, first, d) is not None
+                                for g in (sg, rg) for _, cover, first, _ in boxed)
+                    and all(t.is_contiguous() for t in tensors)):
+                # (see _exchange_direct: whole allocated planes, y / z ghosts overwritten by the edges)
+                for i, t in enumerate(tensors):
+                    ops_list.append(P2P(True, t[sbox[0][0]:sbox[1][0]], peer, 1000 + 32 * i + key_m))
+                    ops_list.append(P2P(False, t[rbox[0][0]:rbox[1][0]], peer, 1000 + 32 * i + back))
+                    nbytes += t[sbox[0][0]:sbox[1][0]].numel() * t.element_size()
+                    nmsg += 1
+                continue
+            sb = torch.empty(_msg_len(tensors, boxed, sg), dtype=tensors[0].dtype, device=tensors[0].device)
+            rb = torch.empty(_msg_len(tensors, boxed, rg), dtype=tensors[0].dtype, device=tensors[0].device)
+            bufs += [sb, rb]
+            for lst, lbox, g, buf in ((pack, sbox, sg, sb), (unpack, rbox, rg, rb)):
+                n = 0
+                for t in tensors:
+                    lst.add(t, lbox, buf, n)
+                    n += _vol(lbox)
+                for t, cover, first, zmul in boxed:
+                    b = _boxed_part(g, cover, first, d, zmul)
+                    if b is not None:
+                        lst.add(t, b, buf, n)
+                        n += _vol(b)
+            ops_list.append(P2P(True, sb, peer, 300 + key_m))
+            ops_list.append(P2P(False, rb, peer, 300 + back))
+            nbytes += sb.numel() * sb.element_size()
+            nmsg += 1
+        plan = {"ops": ops_list, "pack": pack.build(ops), "unpack": unpack.build(ops), "bytes": nbytes,
+                "messages": nmsg, "bufs": bufs}
+        if len(plans) >= 16:
+            plans.pop(next(iter(plans)))
+        plans[key] = plan
+        return plan
+
+    def _exchange_direct_listed(self, ops, tensors, boxed) -> None:
+        """The direct exchange from a cached plan: one pack launch, the
+        batched P2P ops, one unpack launch (a decomposed physics pass issued
+        ~40 pack / unpack launches and their Python planning per exchange,
+        profiles/decomp_r6.md)."""
+        plan = self._direct_plan(ops, tensors, boxed)
+        if plan["pack"] is not None:
+            ops.box_list(*plan["pack"], True)
+        for w in self._post(plan["ops"]):
+            w.wait()
+        if self.debug_delay_cycles and tensors[0].is_cuda:
+            torch.cuda._sleep(int(self.debug_delay_cycles))
+        if plan["unpack"] is not None:
+            ops.box_list(*plan["unpack"], False)
+        self.bytes_sent += plan["bytes"]
+        self.messages += plan["messages"]
+
     debug_delay_cycles = 0
     direct_x_faces = True  # x-face messages straight from / into the arrays (no pack / unpack)
+    # HIP: the direct exchange from a cached plan with one pack / unpack launch (FDTD3D_HALO_LISTED=0: per
+    # message and array, A/B)
+    listed = os.environ.get("FDTD3D_HALO_LISTED", "1") != "0"
 
     def _exchange_sweep(self, scheme) -> None:
         d = self.domain
@@ -402,6 +482,47 @@ def _pack_many(ops, tensors, box, buf):
     for i in range(0, len(tensors), 8):
         chunk = tensors[i:i + 8]
         ops.pack(chunk, box, buf[i * n:(i + len(chunk)) * n])
+
+
+class _BoxList:
+    """(array, local box, buffer, first buffer element) entries of one
+    ``ops.box_list`` launch, as the device table of aux_kernels.hip
+    ``BoxEnt`` (64 bytes: two pointers, ny, nz, box, first block)."""
+
+    def __init__(self):
+        self.rows = []
+
+    def add(self, t: torch.Tensor, box: Box, buf: torch.Tensor, off: int) -> None:
+        if t.dim() != 3 or not t.is_contiguous():
+            raise ValueError("box list: contiguous 3D arrays")
+        for a in range(3):
+            if box[0][a] < 0 or box[1][a] > t.shape[a] or box[1][a] <= box[0][a]:
+                raise ValueError("box list: box %s outside array %s" % (box, tuple(t.shape)))
+        if off + _vol(box) > buf.numel() or buf.dtype != t.dtype:
+            raise ValueError("box list: buffer part out of range")
+        self.rows.append((t, box, buf, off))
+
+    def build(self, ops):
+        """(device table, entries, blocks) or None when empty."""
+        import numpy as np
+        if not self.rows:
+            return None
+        n = len(self.rows)
+        if ops.box_ent_size() != 64:
+            raise RuntimeError("BoxEnt layout mismatch")
+        e64 = np.zeros((n, 8), dtype=np.int64)
+        e32 = e64.view(np.int32)
+        blk = 0
+        for r, (t, box, buf, off) in enumerate(self.rows):
+            e64[r, 0] = t.data_ptr()
+            e64[r, 1] = buf.data_ptr() + off * buf.element_size()
+            e32[r, 4], e32[r, 5] = t.shape[1], t.shape[2]
+            e32[r, 6:9] = box[0]
+            e32[r, 9:12] = box[1]
+            e32[r, 12] = blk
+            blk += -(-_vol(box) // 256)
+        tab = torch.from_numpy(e64).to(self.rows[0][0].device)
+        return (tab, n, blk)
 
 
 def _split_state(scheme):
