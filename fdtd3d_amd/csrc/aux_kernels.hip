@@ -375,9 +375,37 @@ struct BoxEnt {
   long long buf;  // this entry's first buffer element
   int ny, nz;
   int lo[3], hi[3];
-  int blk0, pad[3];
+  int blk0;       // first block of the entry
+  int vec;        // elements per thread: 16-byte vectors (4 fp32 / 2 fp64) when every row run is aligned, else 1
+  int pad[2];
 };
 static_assert(sizeof(BoxEnt) == 64, "BoxEnt layout (parallel/halo.py _BoxList)");
+
+template <typename T, bool PACK, int V>
+__device__ __forceinline__ void box_list_copy(const BoxEnt& e, int blk) {
+  typedef T VT __attribute__((ext_vector_type(V)));
+  const int by = e.hi[1] - e.lo[1], bzv = (e.hi[2] - e.lo[2]) / V;
+  const int n = (e.hi[0] - e.lo[0]) * by * bzv;
+  const int idx = blk * 256 + (int)threadIdx.x;  // in V-element groups
+  if (idx >= n) return;
+  const int kv = idx % bzv, jj = idx / bzv;
+  const int j = jj % by, i = jj / by;
+  T* a = (T*)e.arr;
+  T* f = (T*)e.buf;
+  const size_t off = ((size_t)(e.lo[0] + i) * e.ny + (e.lo[1] + j)) * e.nz + (e.lo[2] + kv * V);
+  const size_t boff = (size_t)idx * V;
+  if (V == 1) {
+    if (PACK)
+      f[boff] = a[off];
+    else
+      a[off] = f[boff];
+  } else {
+    if (PACK)
+      *reinterpret_cast<VT*>(f + boff) = *reinterpret_cast<const VT*>(a + off);
+    else
+      *reinterpret_cast<VT*>(a + off) = *reinterpret_cast<const VT*>(f + boff);
+  }
+}
 
 template <typename T, bool PACK>
 __global__ __launch_bounds__(256) void k_box_list(const BoxEnt* __restrict__ tab, int n) {
@@ -390,18 +418,23 @@ __global__ __launch_bounds__(256) void k_box_list(const BoxEnt* __restrict__ tab
     const int mid = (lo + hi + 1) >> 1;
     if (E[mid].blk0 <= b) lo = mid; else hi = mid - 1;
   }
-  const int bx = E[lo].hi[0] - E[lo].lo[0], by = E[lo].hi[1] - E[lo].lo[1], bz = E[lo].hi[2] - E[lo].lo[2];
-  const int idx = (b - E[lo].blk0) * 256 + (int)threadIdx.x;
-  if (idx >= bx * by * bz) return;
-  const int k = idx % bz, jj = idx / bz;
-  const int j = jj % by, i = jj / by;
-  T* a = (T*)E[lo].arr;
-  T* f = (T*)E[lo].buf;
-  const size_t off = ((size_t)(E[lo].lo[0] + i) * E[lo].ny + (E[lo].lo[1] + j)) * E[lo].nz + (E[lo].lo[2] + k);
-  if (PACK)
-    f[idx] = a[off];
+  BoxEnt e;  // (field by field: the constant-address-space entry has no implicit copy)
+  e.arr = E[lo].arr;
+  e.buf = E[lo].buf;
+  e.ny = E[lo].ny;
+  e.nz = E[lo].nz;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    e.lo[d] = E[lo].lo[d];
+    e.hi[d] = E[lo].hi[d];
+  }
+  e.blk0 = E[lo].blk0;
+  e.vec = E[lo].vec;
+  constexpr int VW = 16 / sizeof(T);
+  if (e.vec == VW)
+    box_list_copy<T, PACK, VW>(e, b - e.blk0);
   else
-    a[off] = f[idx];
+    box_list_copy<T, PACK, 1>(e, b - e.blk0);
 }
 
 }  // namespace

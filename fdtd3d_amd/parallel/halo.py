@@ -487,7 +487,8 @@ def _pack_many(ops, tensors, box, buf):
 class _BoxList:
     """(array, local box, buffer, first buffer element) entries of one
     ``ops.box_list`` launch, as the device table of aux_kernels.hip
-    ``BoxEnt`` (64 bytes: two pointers, ny, nz, box, first block)."""
+    ``BoxEnt`` (64 bytes: two pointers, ny, nz, box, first block, vector
+    width)."""
 
     def __init__(self):
         self.rows = []
@@ -520,7 +521,12 @@ class _BoxList:
             e32[r, 6:9] = box[0]
             e32[r, 9:12] = box[1]
             e32[r, 12] = blk
-            blk += -(-_vol(box) // 256)
+            # 16-byte vectors when the array rows, the box's z range and the buffer part are aligned
+            v = 16 // t.element_size()
+            al = (t.shape[2] % v == 0 and box[0][2] % v == 0 and box[1][2] % v == 0 and off % v == 0
+                  and t.data_ptr() % 16 == 0 and buf.data_ptr() % 16 == 0)
+            e32[r, 13] = v if al else 1
+            blk += -(-(_vol(box) // (v if al else 1)) // 256)
         tab = torch.from_numpy(e64).to(self.rows[0][0].device)
         return (tab, n, blk)
 
