@@ -16,6 +16,8 @@ per component and step (``Source/Cuda/CudaInterface.cu:583-812``).
 
 from __future__ import annotations
 
+import os
+
 from typing import Tuple
 
 import torch
@@ -136,7 +138,10 @@ class BlockedStepping:
     _tfsf_once = False
     drude_blk = None   # the Drude box inside the blocked passes (_plan_drude_blk), None: off
     _drude_plan = None
-    _drude_glob = None  # (T, global Drude box) of the pass form every rank takes (None: off)
+    _drude_glob = None
+    # the Drude pass of a serial hybrid pass on a stream of its own, next to the shell steps (when its
+    # cone is clear of the shell); FDTD3D_DRUDE_SIDE=0: in order (A/B)
+    drude_side = os.environ.get("FDTD3D_DRUDE_SIDE", "1") != "0"  # (T, global Drude box) of the pass form every rank takes (None: off)
     pass_timer = None  # PassTimer of decomposed passes (bench.py / --json), None: off
     _skip_side_wait = False  # tests only: drop the main stream's wait on the exchange (negative control)
 
@@ -682,9 +687,16 @@ class BlockedStepping:
                         if tb is not None and not box_empty(b) and not box_empty(box_intersect(dom.to_local(b), tb)):
                             self._tfsf_once = False
         upd = {c: self.local_box(c, alloc) for c in self.comps}
+        # the Drude pass may run next to the shell steps when its cone (the box grown by 2T, one more
+        # cell for the staggering) meets no shell window (stepped in place in F) and no copy box
+        dside = False
+        if dblk:
+            cone = grow(self._drude_glob[1], 2 * T + 1)
+            dside = not any(not box_empty(box_intersect(cone, w)) for ws in shells for w in ws + copy_boxes)
         return {"T": T, "core": [dom.to_local(b) for b in couts], "shell": shells[0], "shells": shells,
                 "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
-                "cut_cells": box_volume(Dm) if Dm is not None else 0, "core_tfsf": core_tf, "drude": dblk}
+                "cut_cells": box_volume(Dm) if Dm is not None else 0, "core_tfsf": core_tf, "drude": dblk,
+                "drude_side": dside}
 
     def _tfsf_pass(self, p: int, T: int, level0: int = 0, dry: bool = False):
         """In-kernel TF/SF of a blocked pass starting at step ``self.t`` on
@@ -748,8 +760,19 @@ class BlockedStepping:
 
         with self.prof.phase("blocked-core"):
             core(core_now)
+        dside = None
         if hp.get("drude") and self.halo is None:
-            self._drude_pass(T, srcs)  # reads F: before the shell steps below advance it in place
+            if hp.get("drude_side") and self.device.type == "cuda" and self.drude_side:
+                # its cone is clear of every shell window and copy box (_hybrid_plan_m): it runs next to
+                # the shell steps on a stream of its own, after the core pass it overwrites
+                dside = self.__dict__.get("_drude_stream")
+                if dside is None:
+                    dside = self._drude_stream = torch.cuda.Stream(device=self.device)
+                dside.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(dside):
+                    self._drude_pass(T, srcs)
+            else:
+                self._drude_pass(T, srcs)  # reads F: before the shell steps below advance it in place
         if self.halo is not None:
             self._mark("interior")
             self._join_side(side)
@@ -769,6 +792,8 @@ class BlockedStepping:
                 dst = [self.F_alt[p][c] for c in self.comps]
                 fns += [(lambda b=b, src=src, dst=dst: self.ops.copy_box(src, dst, b)) for b in hp["copy"]]
             self._par_launches(fns)  # disjoint boxes: side by side on the shell streams
+        if dside is not None:
+            torch.cuda.current_stream(self.device).wait_stream(dside)
         for p in range(self.planes):
             self.F[p], self.F_alt[p] = self.F_alt[p], self.F[p]
 
