@@ -235,3 +235,17 @@ def test_gpu_decomposed_drude_blocked(gpu, name, cfg, world, axes, buf):
     assert st.drude_blk is None
     assert _max_rel_err(par, blk) <= 5e-6, name
     assert _max_rel_err(par, st) <= 2e-5, name
+
+
+@pytest.mark.parametrize("name", ["hybrid-cpml-tfsf-xy4", "tb4-xy4"])
+def test_gpu_listed_exchange_bitwise(gpu, name, monkeypatch):
+    """The direct exchange from a cached plan (one box-list pack and unpack
+    launch, parallel/halo.py _exchange_direct_listed) moves exactly the
+    bytes of the per-message, per-array form: the decomposed runs agree bit
+    for bit."""
+    _, cfg, world, axes, buf = [c for c in CASES if c[0] == name][0]
+    a = run_threads(cfg, world, axes, buf, gpu, random_init=True)
+    monkeypatch.setattr(HaloExchanger, "listed", False)
+    b = run_threads(cfg, world, axes, buf, gpu, random_init=True)
+    for c in a:
+        assert torch.equal(a[c], b[c]), (name, c)
