@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -37,6 +38,18 @@ namespace {
 // shape of the node's xGMI links.  Plain Yee
 // media (vacuum / dielectric sphere) with the point source; the reference's
 // MPI grid: Source/Grid/ParallelGrid.cpp:1600-1823 (exchange), :2161-2194.
+//
+// Physics (CPML absorbing layers, TF/SF plane waves, point source, vacuum or
+// the dielectric sphere): every rank steps its owned cells with the split
+// half-step kernels of the single-GPU stepped path (the folded 4-cell-lane
+// CPML kernels, the TF/SF correction tables, the incident line), and the
+// updated kind's three components go to the face neighbours after every half
+// step -- one-cell ghosts in x / y, 4-cell ghosts in z (whole lanes), the
+// reference's buffer-size-1 exchange (ParallelGrid.cpp:1600-1823 after each
+// of performExSteps / performHxSteps, Scheme3D.cpp:1900-2942).  The CPML
+// profiles, psi slabs and TF/SF targets are built per rank from the global
+// positions (native_setup.h setup_cpml / setup_tfsf with the rank's origin),
+// so no psi ever needs a ghost: ghosts are read, never updated.
 template <typename T>
 struct XRank {
   int dev = 0;
@@ -53,6 +66,13 @@ struct XRank {
   int nb[27];
   int sbox[27][6], rbox[27][6];
   Dev<T> sbuf[27], rbuf[27];
+  // physics: the owned part of every component's update range (local
+  // indices), the rank's CPML tables, TF/SF tables and incident line, the
+  // point source's local offset (-1: not owned)
+  int own36[36];
+  std::unique_ptr<NativeCpml<T>> cp;
+  std::unique_ptr<NativeTfsf<T>> tf;
+  long long src_off = -1;
   size_t cells() const { return (size_t)n[0] * n[1] * n[2]; }
 };
 
@@ -69,8 +89,10 @@ class MultiRun {
   const std::vector<int> active = {0, 1, 2};
   double dt = 0, freq = 0, cb = 0, db = 0;
   bool percell = false;
+  bool phys = false, cpml = false, tfsf = false, point_src = true;
   int ndev = 0, P = 1, TB = 1;
   int Pd[3] = {1, 1, 1};
+  int gd[3] = {1, 1, 1};  // ghost depth per axis
   fdtd::Int3 sp;
   std::vector<XRank<T>> R;
   bool first = true;
@@ -87,6 +109,10 @@ class MultiRun {
   void pull_ghosts();
   void rank_pass(XRank<T>& q, int t, int k);
   void pass(int t, int k);
+  bool setup_physics(int r);
+  void phys_half(XRank<T>& q, int kind, double sv);
+  void exchange(int kind);
+  void phys_step(int t);
   void advance(int t0, int n);
   void sync_all();
   void report(double sec, int steps, int warm) const;
@@ -112,12 +138,18 @@ int MultiRun<T>::plan_ranks() {
   Pd[2] = std::max(1, s.topologySizeZ);
   if (Pd[0] * Pd[1] * Pd[2] == 1) Pd[0] = ndev;
   P = Pd[0] * Pd[1] * Pd[2];
+  cpml = s.doUsePML;  // (the UPML / metamaterials are refused by native_supported)
+  tfsf = s.doUseTFSF;
+  phys = cpml || tfsf;
+  point_src = !tfsf || s.doUsePointSource;
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
-  TB = std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
+  TB = phys ? 1 : std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
+  for (int a = 0; a < 3; ++a) gd[a] = TB;
+  if (phys) gd[2] = Pd[2] > 1 ? 4 : 1;  // z ghosts of whole 4-cell lanes
   for (int a = 0; a < 3; ++a)
-    if (N[a] / Pd[a] < TB) {
+    if (N[a] / Pd[a] < gd[a]) {
       std::fprintf(stderr, "fdtd3d (native): %d cells along axis %d over %d ranks leave fewer than %d per rank\n",
-                   N[a], a, Pd[a], TB);
+                   N[a], a, Pd[a], gd[a]);
       return 2;
     }
   R.resize(P);
@@ -131,13 +163,13 @@ int MultiRun<T>::plan_ranks() {
       const int base = N[a] / Pd[a], rem = N[a] % Pd[a], c = q.crd[a];
       q.lo[a] = c * base + std::min(c, rem);
       q.hi[a] = q.lo[a] + base + (c < rem ? 1 : 0);
-      const int gl = c > 0 ? TB : 0, gh = c < Pd[a] - 1 ? TB : 0;
+      const int gl = c > 0 ? gd[a] : 0, gh = c < Pd[a] - 1 ? gd[a] : 0;
       q.g0[a] = q.lo[a] - gl;
       q.n[a] = q.hi[a] - q.lo[a] + gl + gh;
     }
-    if (sizeof(T) == 4 && q.n[2] % 4 != 0) {
-      std::fprintf(stderr, "fdtd3d (native): fp32 parallel grids need every rank's z extent (ghosts included) "
-                           "%% 4 == 0 (float4 rows): rank %d has %d\n", r, q.n[2]);
+    if ((sizeof(T) == 4 || cpml) && q.n[2] % 4 != 0) {
+      std::fprintf(stderr, "fdtd3d (native): fp32 / CPML parallel grids need every rank's z extent (ghosts "
+                           "included) %% 4 == 0 (4-cell rows): rank %d has %d\n", r, q.n[2]);
       return 2;
     }
   }
@@ -180,20 +212,23 @@ void MultiRun<T>::setup_rank(int r) {
       c[a] = q.crd[a] + off[a];
       ok = ok && c[a] >= 0 && c[a] < Pd[a];
     }
+    // (physics: the face neighbours only -- the split half steps read no
+    // diagonal ghost)
+    if (phys) ok = ok && std::abs(off[0]) + std::abs(off[1]) + std::abs(off[2]) == 1;
     q.nb[d] = ok ? rank_of(c) : -1;
     if (!ok) continue;
-    size_t vol = 6;
+    size_t vol = phys ? 3 : 6;
     for (int a = 0; a < 3; ++a) {
       // send: the owned layers next to the neighbour; receive: the ghosts there
       int slo = q.lo[a], shi = q.hi[a], rlo = q.lo[a], rhi = q.hi[a];
       if (off[a] < 0) {
-        shi = q.lo[a] + TB;
-        rlo = q.lo[a] - TB;
+        shi = q.lo[a] + gd[a];
+        rlo = q.lo[a] - gd[a];
         rhi = q.lo[a];
       } else if (off[a] > 0) {
-        slo = q.hi[a] - TB;
+        slo = q.hi[a] - gd[a];
         rlo = q.hi[a];
-        rhi = q.hi[a] + TB;
+        rhi = q.hi[a] + gd[a];
       }
       q.sbox[d][a] = slo - q.g0[a];
       q.sbox[d][3 + a] = shi - q.g0[a];
@@ -352,8 +387,142 @@ void MultiRun<T>::pass(int t, int k) {
   first = false;
 }
 
+// physics set-up of rank r (its device current): owned update boxes, CPML
+// tables, TF/SF tables and incident line, the point source; false when the
+// TF/SF box does not fit the incident line
+template <typename T>
+bool MultiRun<T>::setup_physics(int r) {
+  XRank<T>& q = R[r];
+  int own[6], gb36[36];
+  for (int a = 0; a < 3; ++a) {
+    own[a] = q.lo[a];
+    own[3 + a] = q.hi[a];
+  }
+  for (int c = 0; c < 6; ++c) {
+    fdtd::Int3 glo, ghi;
+    fdtd::global_range(c, N, active, glo, ghi);
+    bool empty = false;
+    for (int a = 0; a < 3; ++a) {
+      const int lo = std::max(glo[a], q.lo[a]), hi = std::min(ghi[a], q.hi[a]);
+      empty = empty || hi <= lo;
+      gb36[6 * c + a] = lo;
+      gb36[6 * c + 3 + a] = hi;
+    }
+    for (int a = 0; a < 3; ++a) {
+      if (empty) gb36[6 * c + a] = gb36[6 * c + 3 + a] = 0;
+      q.own36[6 * c + a] = empty ? 0 : gb36[6 * c + a] - q.g0[a];
+      q.own36[6 * c + 3 + a] = empty ? 0 : gb36[6 * c + 3 + a] - q.g0[a];
+    }
+  }
+  if (cpml) {
+    q.cp.reset(new NativeCpml<T>());
+    setup_cpml(*q.cp, s, N, active, dt, s.gridStep, own, q.g0, q.n);
+  }
+  if (tfsf) {
+    q.tf.reset(new NativeTfsf<T>());
+    const bool present[6] = {true, true, true, true, true, true};
+    // (E: per-cell arrays of the sphere or the scalar; H: always the scalar db, mu = 1)
+    if (!setup_tfsf(*q.tf, s, N, gb36, q.C, percell ? 1.0 : cb, db, dt, s.gridStep, freq, 3, present, q.g0, q.n))
+      return false;
+  }
+  bool has = point_src;
+  for (int a = 0; a < 3; ++a) has = has && sp[a] >= q.lo[a] && sp[a] < q.hi[a];
+  q.src_off = has ? ((long long)(sp[0] - q.g0[0]) * q.n[1] + (sp[1] - q.g0[1])) * q.n[2] + (sp[2] - q.g0[2]) : -1;
+  return true;
+}
+
+// one half step of one rank on its main stream, the order of the single-GPU
+// stepped path (native_run.h step3d_split): [incident line] update (+ CPML
+// psi) [TF/SF corrections] [point source, E]
+template <typename T>
+void MultiRun<T>::phys_half(XRank<T>& q, int kind, double sv) {
+  HIP_OK(hipSetDevice(q.dev));
+  T* F[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
+  const T* C[6] = {q.C[0].p, q.C[1].p, q.C[2].p, nullptr, nullptr, nullptr};
+  const bool v4 = sizeof(T) == 4 && q.n[2] % 4 == 0;
+  if (tfsf) {
+    NativeTfsf<T>& tf = *q.tf;
+    if (kind == 0)
+      K_OK(inc_e(tf.einc.p, tf.hinc.p, tf.nline, tf.ce, sv, q.st));
+    else
+      K_OK(inc_h(tf.einc.p, tf.hinc.p, tf.nline, tf.ch, q.st));
+  }
+  const int* bx = q.own36 + 18 * kind;
+  if (kind == 0) {
+    if (cpml)
+      K_OK(cpml_e3d(F, C, percell ? 1.0 : cb, q.n[0], q.n[1], q.n[2], q.own36, q.cp->P[0].data(), q.cp->I[0].data(),
+                    q.st));
+    else
+      K_OK(e3d(F[0], F[1], F[2], F[3], F[4], F[5], C[0], C[1], C[2], percell ? 1.0 : cb, q.n[0], q.n[1], q.n[2], bx,
+               0, q.st, v4));
+  } else {
+    if (cpml)
+      K_OK(cpml_h3d(F, C, db, q.n[0], q.n[1], q.n[2], bx, q.cp->P[1].data(), q.cp->I[1].data(), q.st));
+    else
+      K_OK(h3d(F[3], F[4], F[5], F[0], F[1], F[2], nullptr, nullptr, nullptr, db, q.n[0], q.n[1], q.n[2], bx, 0, q.st,
+               v4));
+  }
+  if (tfsf) {
+    const int whole[6] = {0, 0, 0, q.n[0], q.n[1], q.n[2]};
+    for (int c = 3 * kind; c < 3 * kind + 3; ++c)
+      for (auto* l : q.tf->tab[c])
+        K_OK(tfsf_apply(F[c], *l, kind == 0 ? q.tf->hinc.p : q.tf->einc.p, whole, q.st));
+  }
+  if (kind == 0 && q.src_off >= 0) K_OK(setv(F[2], q.src_off, sv, q.st));
+}
+
+// the updated kind's three components to the face neighbours' ghosts: every
+// rank packs its boxes (after the neighbours pulled the previous ones), then
+// every rank pulls (peer copies across devices) and unpacks on its main
+// stream, so its next half step reads the fresh ghosts
+template <typename T>
+void MultiRun<T>::exchange(int kind) {
+  for (int r = 0; r < P; ++r) {
+    XRank<T>& q = R[r];
+    HIP_OK(hipSetDevice(q.dev));
+    T* f[3] = {q.F[3 * kind].p, q.F[3 * kind + 1].p, q.F[3 * kind + 2].p};
+    for (int d = 0; d < 27; ++d) {
+      if (q.nb[d] < 0) continue;
+      if (!first) HIP_OK(hipStreamWaitEvent(q.st, R[q.nb[d]].copied, 0));
+      K_OK(box_pack(f, q.sbuf[d].p, 3, q.n[1], q.n[2], q.sbox[d], q.st));
+    }
+    HIP_OK(hipEventRecord(q.done, q.st));
+  }
+  for (int r = 0; r < P; ++r) {
+    XRank<T>& q = R[r];
+    HIP_OK(hipSetDevice(q.dev));
+    T* f[3] = {q.F[3 * kind].p, q.F[3 * kind + 1].p, q.F[3 * kind + 2].p};
+    for (int d = 0; d < 27; ++d) {
+      if (q.nb[d] < 0) continue;
+      const XRank<T>& o = R[q.nb[d]];
+      HIP_OK(hipStreamWaitEvent(q.st, o.done, 0));
+      const size_t bytes = q.rbuf[d].n * sizeof(T);
+      if (o.dev == q.dev)
+        HIP_OK(hipMemcpyAsync(q.rbuf[d].p, o.sbuf[26 - d].p, bytes, hipMemcpyDeviceToDevice, q.st));
+      else
+        HIP_OK(hipMemcpyPeerAsync(q.rbuf[d].p, q.dev, o.sbuf[26 - d].p, o.dev, bytes, q.st));
+      K_OK(box_unpack(f, q.rbuf[d].p, 3, q.n[1], q.n[2], q.rbox[d], q.st));
+    }
+    HIP_OK(hipEventRecord(q.copied, q.st));
+  }
+  first = false;
+}
+
+template <typename T>
+void MultiRun<T>::phys_step(int t) {
+  const double sv = src_val(t);
+  for (int kind = 0; kind < 2; ++kind) {
+    for (int r = 0; r < P; ++r) phys_half(R[r], kind, sv);
+    if (P > 1) exchange(kind);
+  }
+}
+
 template <typename T>
 void MultiRun<T>::advance(int t0, int n) {
+  if (phys) {
+    for (int q = 0; q < n; ++q) phys_step(t0 + q);
+    return;
+  }
   int t = t0;
   while (n > 0) {
     const int k = std::min(TB, n);
@@ -390,8 +559,13 @@ void MultiRun<T>::report(double sec, int steps, int warm) const {
   std::printf("Parallel grid scheme: %s (topology %dx%dx%d)\n", scheme.empty() ? "X" : scheme.c_str(), Pd[0], Pd[1],
               Pd[2]);
   std::printf("Buffer size: %d\n", TB);
-  std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), 26-neighbour ghost boxes by packed "
-              "peer copies\n", TB);
+  if (phys)
+    std::printf("Backend: native HIP, split half-step kernels (%s%s%s), face ghosts (%d x / %d y / %d z cells) by "
+                "packed peer copies after every half step\n", cpml ? "CPML" : "", cpml && tfsf ? " + " : "",
+                tfsf ? "TF/SF" : "", gd[0], gd[1], gd[2]);
+  else
+    std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), 26-neighbour ghost boxes by "
+                "packed peer copies\n", TB);
   std::printf("Throughput: %.1f Mcells/s\n", cells * timed / sec / 1e6);
   if (s.doPrintJson)
     std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f, \"ranks\": %d}\n", sec, timed,
@@ -443,6 +617,8 @@ void MultiRun<T>::release() {
       q.sbuf[d].reset();
       q.rbuf[d].reset();
     }
+    q.cp.reset();
+    q.tf.reset();
     HIP_OK(hipEventDestroy(q.done));
     HIP_OK(hipEventDestroy(q.copied));
     HIP_OK(hipStreamDestroy(q.st));
@@ -454,7 +630,10 @@ void MultiRun<T>::release() {
 template <typename T>
 int MultiRun<T>::main() {
   if (const int rc = plan_ranks()) return rc;
-  for (int r = 0; r < P; ++r) setup_rank(r);
+  for (int r = 0; r < P; ++r) {
+    setup_rank(r);
+    if (phys && !setup_physics(r)) return 2;
+  }
   enable_peers();
   plan_outputs();
   const int steps = s.numTimeSteps;

@@ -91,9 +91,17 @@ struct NativeCpml {
   }
 };
 
+// (decomposed runs: `own` = the rank's owned cells [lo, hi) in global
+// indices, `org` / `nl` = its allocated box's global origin and extents; the
+// profiles follow the global position, psi and ranges are in the rank's own
+// array indices)
 template <typename T>
 void setup_cpml(NativeCpml<T>& cp, const fdtd::Settings& s, const fdtd::Int3& N, const std::vector<int>& active,
-                double dt, double dx) {
+                double dt, double dx, const int* own = nullptr, const int* org = nullptr, const int* nl = nullptr) {
+  const int o0[3] = {0, 0, 0};
+  const int n0[3] = {N[0], N[1], N[2]};
+  if (!org) org = o0;
+  if (!nl) nl = n0;
   // staggered offset of each component inside its cell (layout/yee.py MIN_COORD_FP)
   static const double mco[6][3] = {{1.0, 0.5, 0.5}, {0.5, 1.0, 0.5}, {0.5, 0.5, 1.0},
                                    {0.5, 1.0, 1.0}, {1.0, 0.5, 1.0}, {1.0, 1.0, 0.5}};
@@ -107,11 +115,16 @@ void setup_cpml(NativeCpml<T>& cp, const fdtd::Settings& s, const fdtd::Int3& N,
       const int c = 3 * kind + cc;
       fdtd::Int3 glo, ghi;
       fdtd::global_range(c, N, active, glo, ghi);
+      if (own)
+        for (int a = 0; a < 3; ++a) {
+          glo[a] = std::max(glo[a], own[a]);
+          ghi[a] = std::min(ghi[a], own[3 + a]);
+        }
       for (int a = 0; a < 3; ++a) {
         // a component's two curl terms differentiate along the other two axes
         const int P = Ps[a];
         if (a == cc || P <= 0 || std::find(active.begin(), active.end(), a) == active.end()) continue;
-        const int n = N[a];
+        const int n = nl[a];
         const double m = mco[c][a];
         const double sig_max = -(4 + 1) * std::log(1e-8) / (2 * eta * P * dx);
         std::vector<T> b(n, T(1)), cv(n, T(0)), kk(n, T(0));
@@ -126,12 +139,14 @@ void setup_cpml(NativeCpml<T>& cp, const fdtd::Settings& s, const fdtd::Int3& N,
           bool empty = hi <= lo;
           for (int d = 0; d < 3; ++d) empty = empty || ghi[d] <= glo[d];
           if (empty) continue;
-          if (a == 2 && N[2] % 4 == 0) {  // z slabs padded to whole float4 groups (c = 0 there)
+          lo -= org[a];  // the rank's array indices
+          hi -= org[a];
+          if (a == 2 && nl[2] % 4 == 0) {  // z slabs padded to whole float4 groups (c = 0 there)
             lo &= ~3;
-            hi = std::min(N[2], (hi + 3) & ~3);
+            hi = std::min(nl[2], (hi + 3) & ~3);
           }
           for (int v = lo; v < hi; ++v) {
-            const double idx = v + m;
+            const double idx = v + org[a] + m;
             double depth = side == 0 ? (P - idx) / P : (idx - (N[a] - P)) / P;
             depth = std::min(1.0, std::max(0.0, depth));
             const double d4 = depth * depth * depth * depth;
@@ -145,7 +160,7 @@ void setup_cpml(NativeCpml<T>& cp, const fdtd::Settings& s, const fdtd::Int3& N,
           // psi storage: the slab's range along a x the full extents of the other two
           size_t vol = (size_t)(hi - lo);
           for (int d = 0; d < 3; ++d)
-            if (d != a) vol *= (size_t)N[d];
+            if (d != a) vol *= (size_t)nl[d];
           psi[side] = cp.zeros(vol);
           rng[side][0] = lo;
           rng[side][1] = hi;
@@ -434,7 +449,14 @@ double inc_projection(int c, double t, double p, double q) {
 template <typename T>
 bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N, const int* boxes,
                 const Dev<T>* Cc, double cb, double db, double dt, double dx, double freq, int dim,
-                const bool* present) {
+                const bool* present, const int* org = nullptr, const int* ext = nullptr) {
+  // (decomposed runs: `boxes` = the rank's owned part of every component's
+  // range in global indices, targets at the rank's array offsets -- allocated
+  // box at global origin `org`, extents `ext`; the incident line is global)
+  const int o0[3] = {0, 0, 0};
+  const int n0[3] = {N[0], N[1], N[2]};
+  if (!org) org = o0;
+  if (!ext) ext = n0;
   // 2D (TMz / TEz): propagation in the xy plane, theta = pi / 2, the line
   // 100 (Nx + Ny) long (SchemeTMz.h:186), z never bounds the TF box
   const bool d2 = dim == 2;
@@ -459,7 +481,7 @@ bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N,
                           d2 ? 0.0 : L[2] - 2.5 * std::cos(th)};
   const int dir_axis[6] = {0, 0, 1, 1, 2, 2};
   const bool dir_low[6] = {true, false, true, false, true, false};
-  std::vector<T> hc((size_t)N[0] * N[1] * N[2]);
+  std::vector<T> hc((size_t)ext[0] * ext[1] * ext[2]);
   for (int c = 0; c < 6; ++c) {
     const int* bx = boxes + 6 * c;
     if (bx[3] <= bx[0] || bx[4] <= bx[1] || bx[5] <= bx[2]) continue;
@@ -507,7 +529,7 @@ bool setup_tfsf(NativeTfsf<T>& tf, const fdtd::Settings& s, const fdtd::Int3& N,
                 std::fprintf(stderr, "fdtd3d (native): TF/SF box does not fit the incident line\n");
                 return false;
               }
-              const long long flat = ((long long)i * N[1] + j) * N[2] + k;
+              const long long flat = ((long long)(i - org[0]) * ext[1] + (j - org[1])) * ext[2] + (k - org[2]);
               const double cf = pc ? (double)hc[flat] : (kind_e ? cb : db);
               const double w1 = dd - (double)i0;
               ents.push_back({flat, i0, 1.0 - w1, w1, cf * tsign * proj, ents.size()});
@@ -583,11 +605,13 @@ bool native_supported(const fdtd::Settings& s) {
   const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
   // amplitude mode: any scheme, not with the NTFF diagram
   const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
-  // parallel grids: 3D plain media (vacuum / dielectric sphere) with the point source, any rank grid
+  // parallel grids: 3D vacuum / dielectric sphere, any rank grid -- plain media on blocked passes, CPML and
+  // TF/SF (point source optional) on the split half steps (native_multi.h)
+  const bool par_phys = s.doUsePML || s.doUseTFSF;
   const bool par_ok = !s.doUseParallelGrid ||
-                      (s.dimension == 3 && !s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials &&
+                      (s.dimension == 3 && !s.doUseMetamaterials && (!s.doUsePML || s.pmlType == "cpml") &&
                        !s.doUseAmplitudeMode && !s.doUseNTFF && (s.scene == "vacuum" || s.scene == "sphere") &&
-                       !s.doUseSplitKernels);
+                       (par_phys || !s.doUseSplitKernels));
   // checkpoints / resume: plain media (state = the field components)
   const bool ckpt = !s.checkpointDir.empty() || !s.loadFromFile.empty();
   const bool ckpt_ok = !ckpt || (!s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials && !s.doUseAmplitudeMode &&

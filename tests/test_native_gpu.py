@@ -258,6 +258,30 @@ MULTI = {
     "f64_vacuum_2x2x2": ["--3d", "--sizex", "28", "--sizey", "24", "--sizez", "32", "--time-steps", "23",
                          "--scene", "vacuum", "--parallel-grid", "--topology-sizex", "2", "--topology-sizey", "2",
                          "--topology-sizez", "2", "--time-block", "3", "--dtype", "f64"],
+    # physics over ranks (split half steps, face ghosts after every half step): rank borders across the CPML
+    # slabs, the TF/SF faces (oblique incidence) and a dielectric sphere
+    "f32_cpml_tfsf_2x2x1": ["--3d", "--sizex", "40", "--sizey", "36", "--sizez", "32", "--time-steps", "23",
+                            "--scene", "vacuum", "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6",
+                            "--pml-sizey", "5", "--pml-sizez", "4", "--use-tfsf", "--tfsf-sizex", "10",
+                            "--tfsf-sizey", "9", "--tfsf-sizez", "8", "--angle-teta", "60", "--angle-phi", "20",
+                            "--angle-psi", "30", "--parallel-grid", "--topology-sizex", "2", "--topology-sizey", "2",
+                            "--dtype", "f32"],
+    "f64_cpml_tfsf_sphere_2x1x2": ["--3d", "--sizex", "36", "--sizey", "32", "--sizez", "40", "--time-steps", "23",
+                                   "--scene", "sphere", "--sphere-center-x", "17", "--sphere-center-y", "15",
+                                   "--sphere-center-z", "21", "--sphere-radius", "5", "--sphere-eps", "3",
+                                   "--use-pml", "--pml-type", "cpml", "--pml-sizex", "5", "--same-size-pml",
+                                   "--cpml-kappa-max", "2", "--cpml-alpha-max", "0.05", "--use-tfsf",
+                                   "--tfsf-sizex", "9", "--same-size-tfsf", "--angle-teta", "50", "--angle-phi", "30",
+                                   "--angle-psi", "20", "--parallel-grid", "--topology-sizex", "2",
+                                   "--topology-sizez", "2", "--dtype", "f64"],
+    "f32_cpml_point_3x1x1": ["--3d", "--sizex", "42", "--sizey", "30", "--sizez", "32", "--time-steps", "23",
+                             "--scene", "vacuum", "--use-pml", "--pml-type", "cpml", "--pml-sizex", "6",
+                             "--pml-sizey", "5", "--pml-sizez", "4", "--parallel-grid", "--topology-sizex", "3",
+                             "--dtype", "f32"],
+    "f64_tfsf_1x2x2": ["--3d", "--sizex", "32", "--sizey", "40", "--sizez", "48", "--time-steps", "23",
+                       "--scene", "vacuum", "--use-tfsf", "--tfsf-sizex", "8", "--tfsf-sizey", "9", "--tfsf-sizez",
+                       "10", "--angle-teta", "40", "--angle-phi", "25", "--angle-psi", "15", "--parallel-grid",
+                       "--topology-sizey", "2", "--topology-sizez", "2", "--dtype", "f64"],
 }
 
 
@@ -271,7 +295,11 @@ def test_native_parallel_grid_matches_python(case, tmp_path, gpu):
     pd.mkdir()
     r = subprocess.run([exe] + argv + ["--output-dir", str(nd)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "Parallel grid: 1" in r.stdout and "26-neighbour ghost boxes" in r.stdout, r.stdout
+    assert "Parallel grid: 1" in r.stdout, r.stdout
+    if "--use-pml" in argv or "--use-tfsf" in argv:
+        assert "split half-step kernels" in r.stdout and "face ghosts" in r.stdout, r.stdout
+    else:
+        assert "26-neighbour ghost boxes" in r.stdout, r.stdout
     ranks = 1
     serial = [a for a in argv if a not in ("--parallel-grid",)]
     for flag in ("--topology-sizex", "--topology-sizey", "--topology-sizez"):
