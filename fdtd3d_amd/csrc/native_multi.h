@@ -72,6 +72,11 @@ struct XRank {
   int own36[36];
   std::unique_ptr<NativeCpml<T>> cp;
   std::unique_ptr<NativeTfsf<T>> tf;
+  // UPML / Drude: the rank's chain tables and region-local D levels, its part
+  // of the global chain and plain regions (local indices)
+  std::unique_ptr<native_phys::Upml<T>> up;
+  std::vector<IBox> chain_regs, plain_regs;
+  std::vector<bool> chain_disp;
   long long src_off = -1;
   size_t cells() const { return (size_t)n[0] * n[1] * n[2]; }
 };
@@ -89,7 +94,7 @@ class MultiRun {
   const std::vector<int> active = {0, 1, 2};
   double dt = 0, freq = 0, cb = 0, db = 0;
   bool percell = false;
-  bool phys = false, cpml = false, tfsf = false, point_src = true;
+  bool phys = false, cpml = false, upml = false, tfsf = false, point_src = true;
   int ndev = 0, P = 1, TB = 1;
   int Pd[3] = {1, 1, 1};
   int gd[3] = {1, 1, 1};  // ghost depth per axis
@@ -110,6 +115,8 @@ class MultiRun {
   void rank_pass(XRank<T>& q, int t, int k);
   void pass(int t, int k);
   bool setup_physics(int r);
+  void setup_chain(XRank<T>& q);
+  static void clip36(const int* b36, const IBox& r, int* out);
   void phys_half(XRank<T>& q, int kind, double sv);
   void exchange(int kind);
   void phys_step(int t);
@@ -131,16 +138,17 @@ int MultiRun<T>::plan_ranks() {
   freq = kC / s.sourceWaveLength;
   cb = dt / (kEps0 * dx);
   db = dt / (kMu0 * dx);
-  percell = s.scene != "vacuum";
+  percell = s.scene != "vacuum" && s.scene != "drude-sphere";  // (a Drude sphere's eps_inf is 1)
   HIP_OK(hipGetDeviceCount(&ndev));
   Pd[0] = std::max(1, s.topologySizeX);
   Pd[1] = std::max(1, s.topologySizeY);
   Pd[2] = std::max(1, s.topologySizeZ);
   if (Pd[0] * Pd[1] * Pd[2] == 1) Pd[0] = ndev;
   P = Pd[0] * Pd[1] * Pd[2];
-  cpml = s.doUsePML;  // (the UPML / metamaterials are refused by native_supported)
+  upml = (s.doUsePML && s.pmlType == "upml") || s.doUseMetamaterials;  // the D/B chain
+  cpml = s.doUsePML && !upml;
   tfsf = s.doUseTFSF;
-  phys = cpml || tfsf;
+  phys = cpml || upml || tfsf;
   point_src = !tfsf || s.doUsePointSource;
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
   TB = phys ? 1 : std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
@@ -387,6 +395,101 @@ void MultiRun<T>::pass(int t, int k) {
   first = false;
 }
 
+// UPML / Drude tables of a rank at the global positions, and its part of the
+// global chain regions (the PML slabs with one cell of staggering slack, the
+// dispersive sphere's box; native_run.h setup_chain_regions) with their
+// region-local D / D1 levels
+template <typename T>
+void MultiRun<T>::setup_chain(XRank<T>& q) {
+  native_phys::UpmlScene sc;
+  sc.pml[0] = s.pmlSizeX;
+  sc.pml[1] = s.pmlSizeY;
+  sc.pml[2] = s.pmlSizeZ;
+  sc.use_pml = s.doUsePML;
+  sc.metamaterials = s.doUseMetamaterials;
+  sc.lorentz = s.dispersion == "lorentz";
+  sc.lorentz_ratio = s.lorentzOmega0Ratio;
+  sc.freq = freq;
+  sc.sphere_eps = s.scene == "sphere";
+  sc.drude_sphere = s.scene == "drude-sphere";
+  sc.ctr[0] = s.sphereCenterX;
+  sc.ctr[1] = s.sphereCenterY;
+  sc.ctr[2] = s.sphereCenterZ;
+  sc.radius = s.sphereRadius;
+  sc.eps_in = s.sphereEps;
+  q.up.reset(new native_phys::Upml<T>());
+  native_phys::setup_upml<T>(*q.up, N, sc, dt, s.gridStep, q.g0, q.n, true);
+  // the global regions
+  const IBox whole_box = {{0, 0, 0}, {N[0], N[1], N[2]}};
+  const int pp[3] = {s.doUsePML ? s.pmlSizeX + 1 : 0, s.doUsePML ? s.pmlSizeY + 1 : 0,
+                     s.doUsePML ? s.pmlSizeZ + 1 : 0};
+  const IBox inner = {{pp[0], pp[1], pp[2]}, {N[0] - pp[0], N[1] - pp[1], N[2] - pp[2]}};
+  IBox dbox = {{0, 0, 0}, {0, 0, 0}};
+  if (s.doUseMetamaterials)
+    for (int a = 0; a < 3; ++a) {
+      dbox.lo[a] = std::max(0, (int)std::floor(sc.ctr[a] - s.sphereRadius) - 2);
+      dbox.hi[a] = std::min(N[a], (int)std::ceil(sc.ctr[a] + s.sphereRadius) + 3);
+    }
+  bool inside = !inner.empty();
+  for (int a = 0; a < 3 && !dbox.empty(); ++a) inside = inside && dbox.lo[a] >= inner.lo[a] && dbox.hi[a] <= inner.hi[a];
+  std::vector<IBox> creg, preg;
+  std::vector<bool> cdisp;
+  if (!inside) {
+    creg.push_back(whole_box);
+    cdisp.push_back(true);
+  } else {
+    if (s.doUsePML) creg = box_minus(whole_box, inner);
+    cdisp.assign(creg.size(), false);
+    if (!dbox.empty()) {
+      creg.push_back(dbox);
+      cdisp.push_back(true);
+      preg = box_minus(inner, dbox);
+    } else {
+      preg.push_back(inner);
+    }
+  }
+  // the rank's parts, local indices
+  const IBox own = {{q.lo[0], q.lo[1], q.lo[2]}, {q.hi[0], q.hi[1], q.hi[2]}};
+  auto local = [&](const IBox& b) {
+    IBox r = box_and(b, own);
+    for (int a = 0; a < 3; ++a) {
+      r.lo[a] -= q.g0[a];
+      r.hi[a] -= q.g0[a];
+    }
+    return r;
+  };
+  std::vector<std::array<int, 6>> rb;
+  for (size_t r = 0; r < creg.size(); ++r) {
+    const IBox b = local(creg[r]);
+    if (b.empty()) continue;
+    q.chain_regs.push_back(b);
+    q.chain_disp.push_back(cdisp[r]);
+    rb.push_back({b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2]});
+  }
+  for (const IBox& p : preg) {
+    const IBox b = local(p);
+    if (!b.empty()) q.plain_regs.push_back(b);
+  }
+  native_phys::alloc_levels(*q.up, rb, q.chain_disp);
+}
+
+// the component boxes (36 ints) clipped to a region
+template <typename T>
+void MultiRun<T>::clip36(const int* b36, const IBox& r, int* out) {
+  for (int c = 0; c < 6; ++c) {
+    IBox b;
+    for (int a = 0; a < 3; ++a) {
+      b.lo[a] = b36[6 * c + a];
+      b.hi[a] = b36[6 * c + 3 + a];
+    }
+    b = box_and(b, r);
+    for (int a = 0; a < 3; ++a) {
+      out[6 * c + a] = b.empty() ? 0 : b.lo[a];
+      out[6 * c + 3 + a] = b.empty() ? 0 : b.hi[a];
+    }
+  }
+}
+
 // physics set-up of rank r (its device current): owned update boxes, CPML
 // tables, TF/SF tables and incident line, the point source; false when the
 // TF/SF box does not fit the incident line
@@ -418,6 +521,7 @@ bool MultiRun<T>::setup_physics(int r) {
     q.cp.reset(new NativeCpml<T>());
     setup_cpml(*q.cp, s, N, active, dt, s.gridStep, own, q.g0, q.n);
   }
+  if (upml) setup_chain(q);
   if (tfsf) {
     q.tf.reset(new NativeTfsf<T>());
     const bool present[6] = {true, true, true, true, true, true};
@@ -448,7 +552,28 @@ void MultiRun<T>::phys_half(XRank<T>& q, int kind, double sv) {
       K_OK(inc_h(tf.einc.p, tf.hinc.p, tf.nline, tf.ch, q.st));
   }
   const int* bx = q.own36 + 18 * kind;
-  if (kind == 0) {
+  if (upml) {
+    // the chain on the rank's part of the PML slabs and the dispersive box,
+    // the plain update on the rest (native_run.h upml_regions)
+    using ChainFn = int (*)(const void* const*, const double*, const int*, int, int, int, int, void*);
+    const ChainFn chain = sizeof(T) == 4 ? (ChainFn)fdtd_chain3d_f32 : (ChainFn)fdtd_chain3d_f64;
+    int rb[36];
+    for (size_t r = 0; r < q.chain_regs.size(); ++r) {
+      clip36(q.own36, q.chain_regs[r], rb);
+      K_OK(native_phys::upml_kind<T>(*q.up, F, rb, kind, q.n[1], q.n[2], q.st, chain, false, !q.chain_disp[r], nullptr,
+                                     1.0, (int)r));
+    }
+    native_phys::upml_rotate(*q.up, kind);
+    for (const IBox& pr : q.plain_regs) {
+      clip36(q.own36, pr, rb);
+      if (kind == 0)
+        K_OK(e3d(F[0], F[1], F[2], F[3], F[4], F[5], C[0], C[1], C[2], percell ? 1.0 : cb, q.n[0], q.n[1], q.n[2], rb,
+                 0, q.st, v4));
+      else
+        K_OK(h3d(F[3], F[4], F[5], F[0], F[1], F[2], nullptr, nullptr, nullptr, db, q.n[0], q.n[1], q.n[2], rb + 18,
+                 0, q.st, v4));
+    }
+  } else if (kind == 0) {
     if (cpml)
       K_OK(cpml_e3d(F, C, percell ? 1.0 : cb, q.n[0], q.n[1], q.n[2], q.own36, q.cp->P[0].data(), q.cp->I[0].data(),
                     q.st));
@@ -561,8 +686,10 @@ void MultiRun<T>::report(double sec, int steps, int warm) const {
   std::printf("Buffer size: %d\n", TB);
   if (phys)
     std::printf("Backend: native HIP, split half-step kernels (%s%s%s), face ghosts (%d x / %d y / %d z cells) by "
-                "packed peer copies after every half step\n", cpml ? "CPML" : "", cpml && tfsf ? " + " : "",
-                tfsf ? "TF/SF" : "", gd[0], gd[1], gd[2]);
+                "packed peer copies after every half step\n",
+                cpml ? "CPML" : (upml ? (s.doUseMetamaterials ? "UPML D/B chain + dispersive sphere" : "UPML D/B chain")
+                                      : ""),
+                (cpml || upml) && tfsf ? " + " : "", tfsf ? "TF/SF" : "", gd[0], gd[1], gd[2]);
   else
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), 26-neighbour ghost boxes by "
                 "packed peer copies\n", TB);
@@ -619,6 +746,7 @@ void MultiRun<T>::release() {
     }
     q.cp.reset();
     q.tf.reset();
+    q.up.reset();
     HIP_OK(hipEventDestroy(q.done));
     HIP_OK(hipEventDestroy(q.copied));
     HIP_OK(hipStreamDestroy(q.st));

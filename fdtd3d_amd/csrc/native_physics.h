@@ -159,9 +159,19 @@ inline double sphere_eps_at(double x, double y, double z, const UpmlScene& sc) {
   return p * sc.eps_in + (1 - p) * 1.0;
 }
 
+// (decomposed runs: the rank's arrays -- allocated box at global origin `org`,
+// extents `ext` -- with the profiles, materials and ids at the global
+// positions; `all_disp`: every E component takes the dispersive form wherever
+// the global sphere makes it dispersive, so every rank's chain launches agree
+// on the form -- a rank the sphere misses gets the omega = 0 row)
 template <typename T>
-void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt, double dx) {
-  const size_t cells = (size_t)N[0] * N[1] * N[2];
+void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt, double dx,
+                const int* org = nullptr, const int* ext = nullptr, bool all_disp = false) {
+  const int o0[3] = {0, 0, 0};
+  const int n0[3] = {N[0], N[1], N[2]};
+  if (!org) org = o0;
+  if (!ext) ext = n0;
+  const size_t cells = (size_t)ext[0] * ext[1] * ext[2];
   std::vector<double> sig[3];
   for (int a = 0; a < 3; ++a) sig[a] = sigma_profile(N[a] + 1, sc.use_pml ? sc.pml[a] : 0, dx);
   // omega_p of the dispersive sphere on the eps layout (float32 sqrt(2), as the reference)
@@ -177,26 +187,26 @@ void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt,
     const int aD = kUpmlAxes[c][0], aA = kUpmlAxes[c][1], aB = kUpmlAxes[c][2];
     const double base = c < 3 ? kEps0 : kMu0;
     auto avg_prof = [&](int a) {
-      std::vector<double> out(N[a]);
+      std::vector<double> out(ext[a]);
       double v[4];
-      for (int n = 0; n < N[a]; ++n) {
-        for (int p = 0; p < kStencilN[c]; ++p) v[p] = sig[a][n + kStencil[c][p][a]];
+      for (int n = 0; n < ext[a]; ++n) {
+        for (int p = 0; p < kStencilN[c]; ++p) v[p] = sig[a][org[a] + n + kStencil[c][p][a]];
         out[n] = approx_mean(v, kStencilN[c]);
       }
       return out;
     };
     const std::vector<double> sD = avg_prof(aD), sA = avg_prof(aA), sB = avg_prof(aB);
     const double two = 2 * kEps0;  // H-side sigma normalised by eps0 too (Scheme3D.cpp:1198-1201)
-    std::vector<T> caD(N[aD]), cbD(N[aD]), caE(N[aA]), ica(N[aA]), cbEa(N[aB]), ccEa(N[aB]);
-    for (int n = 0; n < N[aD]; ++n) {
+    std::vector<T> caD(ext[aD]), cbD(ext[aD]), caE(ext[aA]), ica(ext[aA]), cbEa(ext[aB]), ccEa(ext[aB]);
+    for (int n = 0; n < ext[aD]; ++n) {
       caD[n] = (T)((two - sD[n] * dt) / (two + sD[n] * dt));
       cbD[n] = (T)((two * dt / dx) / (two + sD[n] * dt));
     }
-    for (int n = 0; n < N[aA]; ++n) {
+    for (int n = 0; n < ext[aA]; ++n) {
       caE[n] = (T)((two - sA[n] * dt) / (two + sA[n] * dt));
       ica[n] = (T)(1.0 / (two + sA[n] * dt));
     }
-    for (int n = 0; n < N[aB]; ++n) {
+    for (int n = 0; n < ext[aB]; ++n) {
       cbEa[n] = (T)(two + sB[n] * dt);
       ccEa[n] = (T)(-(two - sB[n] * dt));
     }
@@ -209,9 +219,10 @@ void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt,
     if (sc.metamaterials && sc.drude_sphere && c < 3) {
       std::vector<double> vals;
       std::vector<unsigned char> id(cells);
-      for (int i = 0; i < N[0]; ++i)
-        for (int j = 0; j < N[1]; ++j)
-          for (int k = 0; k < N[2]; ++k) {
+      for (int li = 0; li < ext[0]; ++li)
+        for (int lj = 0; lj < ext[1]; ++lj)
+          for (int lk = 0; lk < ext[2]; ++lk) {
+            const int i = org[0] + li, j = org[1] + lj, k = org[2] + lk;
             double sq = 0.0;
             for (int p = 0; p < kStencilN[c]; ++p) {
               const double w = in_sphere(i + kStencil[c][p][0], j + kStencil[c][p][1], k + kStencil[c][p][2]) ? wp
@@ -222,13 +233,13 @@ void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt,
             size_t q2 = 0;
             while (q2 < vals.size() && vals[q2] != w) ++q2;
             if (q2 == vals.size()) vals.push_back(w);
-            id[((size_t)i * N[1] + j) * N[2] + k] = (unsigned char)q2;
+            id[((size_t)li * ext[1] + lj) * ext[2] + lk] = (unsigned char)q2;
           }
       if (vals.size() > 256) {
         std::fprintf(stderr, "fdtd3d (native): more than 256 distinct Drude tuples\n");
         std::exit(1);
       }
-      bool any = false;
+      bool any = all_disp && sc.radius > 0;
       for (double w : vals) any = any || w != 0.0;
       if (any) {
         U.disp[c] = true;
@@ -246,14 +257,15 @@ void setup_upml(Upml<T>& U, const fdtd::Int3& N, const UpmlScene& sc, double dt,
     } else if (sc.sphere_eps && c < 3) {
       // per-cell 1/(eps eps0) with eps averaged at the component (E only; mu = 1)
       std::vector<T> cl(cells);
-      for (int i = 0; i < N[0]; ++i)
-        for (int j = 0; j < N[1]; ++j)
-          for (int k = 0; k < N[2]; ++k) {
+      for (int li = 0; li < ext[0]; ++li)
+        for (int lj = 0; lj < ext[1]; ++lj)
+          for (int lk = 0; lk < ext[2]; ++lk) {
+            const int i = org[0] + li, j = org[1] + lj, k = org[2] + lk;
             double v[2];
             for (int p = 0; p < 2; ++p)
               v[p] = sphere_eps_at(i + kStencil[c][p][0] + 0.5, j + kStencil[c][p][1] + 0.5,
                                    k + kStencil[c][p][2] + 0.5, sc);
-            cl[((size_t)i * N[1] + j) * N[2] + k] = (T)(1.0 / (approx_mean(v, 2) * base));
+            cl[((size_t)li * ext[1] + lj) * ext[2] + lk] = (T)(1.0 / (approx_mean(v, 2) * base));
           }
       U.cell[c] = dev_upload(cl, U.keep);
       U.s[c] = 1.0;

@@ -605,13 +605,13 @@ bool native_supported(const fdtd::Settings& s) {
   const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
   // amplitude mode: any scheme, not with the NTFF diagram
   const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
-  // parallel grids: 3D vacuum / dielectric sphere, any rank grid -- plain media on blocked passes, CPML and
-  // TF/SF (point source optional) on the split half steps (native_multi.h)
-  const bool par_phys = s.doUsePML || s.doUseTFSF;
+  // parallel grids: 3D, any rank grid -- plain media on blocked passes; CPML, the UPML, Drude / Lorentz spheres
+  // and TF/SF (point source optional) on the split half steps (native_multi.h)
+  const bool par_phys = s.doUsePML || s.doUseTFSF || s.doUseMetamaterials;
   const bool par_ok = !s.doUseParallelGrid ||
-                      (s.dimension == 3 && !s.doUseMetamaterials && (!s.doUsePML || s.pmlType == "cpml") &&
-                       !s.doUseAmplitudeMode && !s.doUseNTFF && (s.scene == "vacuum" || s.scene == "sphere") &&
-                       (par_phys || !s.doUseSplitKernels));
+                      (s.dimension == 3 && !s.doUseAmplitudeMode && !s.doUseNTFF &&
+                       (s.scene == "vacuum" || s.scene == "sphere" || s.scene == "drude-sphere") &&
+                       (par_phys || s.doUseMetamaterials || !s.doUseSplitKernels));
   // checkpoints / resume: plain media (state = the field components)
   const bool ckpt = !s.checkpointDir.empty() || !s.loadFromFile.empty();
   const bool ckpt_ok = !ckpt || (!s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials && !s.doUseAmplitudeMode &&

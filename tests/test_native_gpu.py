@@ -282,6 +282,25 @@ MULTI = {
                        "--scene", "vacuum", "--use-tfsf", "--tfsf-sizex", "8", "--tfsf-sizey", "9", "--tfsf-sizez",
                        "10", "--angle-teta", "40", "--angle-phi", "25", "--angle-psi", "15", "--parallel-grid",
                        "--topology-sizey", "2", "--topology-sizez", "2", "--dtype", "f64"],
+    # the UPML D/B chain and dispersive spheres over ranks: the chain on each rank's part of the PML slabs and
+    # the sphere's box (region-local levels), a sphere across two rank borders, a Lorentz sphere with TF/SF
+    "f64_upml_tfsf_2x2x1": ["--3d", "--sizex", "36", "--sizey", "32", "--sizez", "40", "--time-steps", "23",
+                            "--scene", "vacuum", "--use-pml", "--pml-sizex", "5", "--pml-sizey", "4", "--pml-sizez",
+                            "6", "--use-tfsf", "--tfsf-sizex", "9", "--tfsf-sizey", "8", "--tfsf-sizez", "10",
+                            "--angle-teta", "60", "--angle-phi", "20", "--angle-psi", "30", "--parallel-grid",
+                            "--topology-sizex", "2", "--topology-sizey", "2", "--dtype", "f64"],
+    "f32_drude_upml_2x1x2": ["--3d", "--sizex", "40", "--sizey", "36", "--sizez", "32", "--time-steps", "23",
+                             "--scene", "drude-sphere", "--use-metamaterials", "--use-pml", "--pml-sizex", "5",
+                             "--same-size-pml", "--sphere-center-x", "20", "--sphere-center-y", "18",
+                             "--sphere-center-z", "16", "--sphere-radius", "7", "--parallel-grid",
+                             "--topology-sizex", "2", "--topology-sizez", "2", "--dtype", "f32"],
+    "f64_lorentz_upml_tfsf_1x2x2": ["--3d", "--sizex", "40", "--same-size", "--time-steps", "23", "--scene",
+                                    "drude-sphere", "--use-metamaterials", "--dispersion", "lorentz",
+                                    "--lorentz-omega0", "0.7", "--use-pml", "--pml-sizex", "5", "--same-size-pml",
+                                    "--sphere-center-x", "20", "--sphere-center-y", "21", "--sphere-center-z", "19",
+                                    "--sphere-radius", "6", "--use-tfsf", "--tfsf-sizex", "9", "--same-size-tfsf",
+                                    "--parallel-grid", "--topology-sizey", "2", "--topology-sizez", "2",
+                                    "--dtype", "f64"],
 }
 
 
@@ -296,7 +315,7 @@ def test_native_parallel_grid_matches_python(case, tmp_path, gpu):
     r = subprocess.run([exe] + argv + ["--output-dir", str(nd)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Parallel grid: 1" in r.stdout, r.stdout
-    if "--use-pml" in argv or "--use-tfsf" in argv:
+    if "--use-pml" in argv or "--use-tfsf" in argv or "--use-metamaterials" in argv:
         assert "split half-step kernels" in r.stdout and "face ghosts" in r.stdout, r.stdout
     else:
         assert "26-neighbour ghost boxes" in r.stdout, r.stdout

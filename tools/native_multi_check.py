@@ -20,7 +20,18 @@ KAP = ["--cpml-kappa-max", "2", "--cpml-alpha-max", "0.05"]
 TFSF = ["--use-tfsf", "--tfsf-sizex", "9", "--same-size-tfsf", "--angle-teta", "50", "--angle-phi", "30",
         "--angle-psi", "20"]
 VAC = ["--scene", "vacuum"]
+UPML = ["--use-pml", "--pml-sizex", "5", "--same-size-pml"]
+DRU = ["--scene", "drude-sphere", "--use-metamaterials", "--sphere-center-x", "17", "--sphere-center-y", "15",
+       "--sphere-center-z", "21", "--sphere-radius", "5"]
 VARIANTS = [
+    ("f64 vac upml 2x1x2", VAC + UPML + ["--dtype", "f64"], (2, 1, 2)),
+    ("f64 vac upml tfsf 1x2x1", VAC + UPML + TFSF + ["--dtype", "f64"], (1, 2, 1)),
+    ("f64 sph upml 2x1x1", SPH + UPML + ["--dtype", "f64"], (2, 1, 1)),
+    ("f64 drude upml 2x1x2", DRU + UPML + ["--dtype", "f64"], (2, 1, 2)),
+    ("f64 drude 1x1x2", DRU + ["--dtype", "f64"], (1, 1, 2)),
+    ("f32 drude upml 2x2x1", DRU + UPML + ["--dtype", "f32"], (2, 2, 1)),
+]
+VARIANTS_CPML = [
     ("f64 sph cpml kap tfsf 2x1x2", SPH + CPML + KAP + TFSF + ["--dtype", "f64"], (2, 1, 2)),
     ("f64 sph cpml kap tfsf 2x1x1", SPH + CPML + KAP + TFSF + ["--dtype", "f64"], (2, 1, 1)),
     ("f64 sph cpml kap tfsf 1x1x2", SPH + CPML + KAP + TFSF + ["--dtype", "f64"], (1, 1, 2)),
