@@ -94,7 +94,8 @@ class MultiRun {
   const std::vector<int> active = {0, 1, 2};
   double dt = 0, freq = 0, cb = 0, db = 0;
   bool percell = false;
-  bool phys = false, cpml = false, upml = false, tfsf = false, point_src = true;
+  bool phys = false, cpml = false, upml = false, tfsf = false, point_src = true, ntff = false;
+  Dev<T> NG[6];  // NTFF: the whole grid assembled on the first rank's device
   int ndev = 0, P = 1, TB = 1;
   int Pd[3] = {1, 1, 1};
   int gd[3] = {1, 1, 1};  // ghost depth per axis
@@ -121,6 +122,9 @@ class MultiRun {
   void exchange(int kind);
   void phys_step(int t);
   void advance(int t0, int n);
+  void run_steps(int t0, int n);
+  void gather(int c, std::vector<T>& host);
+  void ntff_report(int t);
   void sync_all();
   void report(double sec, int steps, int warm) const;
   void save_results(int steps);
@@ -149,6 +153,7 @@ int MultiRun<T>::plan_ranks() {
   cpml = s.doUsePML && !upml;
   tfsf = s.doUseTFSF;
   phys = cpml || upml || tfsf;
+  ntff = s.doUseNTFF;
   point_src = !tfsf || s.doUsePointSource;
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
   TB = phys ? 1 : std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
@@ -699,25 +704,75 @@ void MultiRun<T>::report(double sec, int steps, int warm) const {
                 cells * timed / sec / 1e6, P);
 }
 
+// component c of the whole grid on the host: every rank's owned block
+template <typename T>
+void MultiRun<T>::gather(int c, std::vector<T>& host) {
+  host.resize((size_t)N[0] * N[1] * N[2]);
+  std::vector<T> loc;
+  for (int r = 0; r < P; ++r) {
+    const XRank<T>& q = R[r];
+    HIP_OK(hipSetDevice(q.dev));
+    loc.resize(q.cells());
+    HIP_OK(hipMemcpy(loc.data(), q.F[c].p, loc.size() * sizeof(T), hipMemcpyDeviceToHost));
+    for (int i = q.lo[0]; i < q.hi[0]; ++i)
+      for (int j = q.lo[1]; j < q.hi[1]; ++j)
+        std::memcpy(host.data() + ((size_t)i * N[1] + j) * N[2] + q.lo[2],
+                    loc.data() + ((size_t)(i - q.g0[0]) * q.n[1] + (j - q.g0[1])) * q.n[2] + (q.lo[2] - q.g0[2]),
+                    (size_t)(q.hi[2] - q.lo[2]) * sizeof(T));
+  }
+}
+
+// the NTFF scattered power diagram of step t (native_run.h ntff_report): the
+// ranks' owned blocks assembled into whole-grid arrays on the first rank's
+// device, then the one-GPU surface reduction
+template <typename T>
+void MultiRun<T>::ntff_report(int t) {
+  sync_all();
+  std::vector<T> host;
+  T* Fp[6];
+  for (int c = 0; c < 6; ++c) {
+    gather(c, host);
+    HIP_OK(hipSetDevice(R[0].dev));
+    if (!NG[c].p) NG[c].alloc(host.size());
+    HIP_OK(hipMemcpy(NG[c].p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+    Fp[c] = NG[c].p;
+  }
+  const int nbox[3] = {s.ntffSizeX, s.ntffSizeY, s.ntffSizeZ};
+  const std::vector<double> phis = native_phys::reference_angles();
+  const std::vector<double> p = native_phys::ntff_power<T>(Fp, N, nbox, s.gridStep, s.sourceWaveLength,
+                                                           s.incidentWaveAngle1 * (kPi / 180.0), phis);
+  for (size_t q = 0; q < phis.size(); ++q)
+    std::printf("=== t=%u, inc angle=%f; angle %f === %.17g \n", (unsigned)t, s.incidentWaveAngle2 * (kPi / 180.0),
+                phis[q], p[q]);
+}
+
+// the steps, with the NTFF diagram after every step t with (t - 1) % ntffStep
+// == 0 (native_run.h run_steps)
+template <typename T>
+void MultiRun<T>::run_steps(int t0, int n) {
+  if (!ntff) {
+    advance(t0, n);
+    return;
+  }
+  const int nstep = std::max(1, s.ntffStep);
+  int t = t0;
+  const int end = t0 + n;
+  while (t < end) {
+    const int nxt = std::min(end, t + 1 + ((1 - (t + 1)) % nstep + nstep) % nstep);
+    advance(t, nxt - t);
+    t = nxt;
+    if ((t - 1) % nstep == 0) ntff_report(t - 1);
+  }
+}
+
 // --save-res: the owned blocks of every rank assembled into global DAT / BMP files
 template <typename T>
 void MultiRun<T>::save_results(int steps) {
   if (!s.doSaveRes) return;
   const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
-  const size_t plane = (size_t)N[1] * N[2];
-  std::vector<T> host((size_t)N[0] * plane), loc;
+  std::vector<T> host;
   for (int c = 0; c < 6; ++c) {
-    for (int r = 0; r < P; ++r) {
-      const XRank<T>& q = R[r];
-      HIP_OK(hipSetDevice(q.dev));
-      loc.resize(q.cells());
-      HIP_OK(hipMemcpy(loc.data(), q.F[c].p, loc.size() * sizeof(T), hipMemcpyDeviceToHost));
-      for (int i = q.lo[0]; i < q.hi[0]; ++i)
-        for (int j = q.lo[1]; j < q.hi[1]; ++j)
-          std::memcpy(host.data() + ((size_t)i * N[1] + j) * N[2] + q.lo[2],
-                      loc.data() + ((size_t)(i - q.g0[0]) * q.n[1] + (j - q.g0[1])) * q.n[2] + (q.lo[2] - q.g0[2]),
-                      (size_t)(q.hi[2] - q.lo[2]) * sizeof(T));
-    }
+    gather(c, host);
     const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
     if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), host.size() * sizeof(T));
     if (s.saveAsBMP || !s.saveAsDAT) {
@@ -753,6 +808,10 @@ void MultiRun<T>::release() {
     HIP_OK(hipStreamDestroy(q.side));
     q.st = nullptr;
   }
+  if (!R.empty()) {
+    HIP_OK(hipSetDevice(R[0].dev));
+    for (int c = 0; c < 6; ++c) NG[c].reset();
+  }
 }
 
 template <typename T>
@@ -766,10 +825,10 @@ int MultiRun<T>::main() {
   plan_outputs();
   const int steps = s.numTimeSteps;
   const int warm = std::max(0, std::min(s.warmupSteps, steps));
-  advance(0, warm);
+  run_steps(0, warm);
   sync_all();
   const auto c0 = std::chrono::steady_clock::now();
-  advance(warm, steps - warm);
+  run_steps(warm, steps - warm);
   sync_all();
   HIP_OK(hipGetLastError());
   const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();

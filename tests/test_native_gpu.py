@@ -237,6 +237,27 @@ def test_native_ntff_matches_python(dtype, gpu):
         assert abs(x - y) <= tol * peak, (h, x, y, peak)
 
 
+@pytest.mark.gpu
+def test_native_ntff_parallel_grid():
+    """The NTFF diagram of a decomposed native run (2x2x1 ranks: UPML chain + TF/SF + sphere on the split half
+    steps, the grid gathered for each report) equals the single-rank native run's to fp64 round-off."""
+    exe = native.executable()
+    argv = NTFF_ARGV + ["--dtype", "f64"]
+    one = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=300)
+    assert one.returncode == 0, one.stdout + one.stderr
+    par = subprocess.run([exe] + argv + ["--parallel-grid", "--topology-sizex", "2", "--topology-sizey", "2"],
+                         capture_output=True, text=True, timeout=300)
+    assert par.returncode == 0, par.stdout + par.stderr
+    assert "Number of processes: 4" in par.stdout
+    a, b = _ntff_lines(par.stdout), _ntff_lines(one.stdout)
+    assert len(a) == len(b) == 4 * 181, (len(a), len(b))
+    assert [h for h, _ in a] == [h for h, _ in b]
+    peak = max(abs(v) for _, v in b)
+    assert peak > 0
+    for (h, x), (_, y) in zip(a, b):
+        assert abs(x - y) <= 1e-11 * peak, (h, x, y, peak)
+
+
 # parallel grids of the native driver (csrc/native_multi.h run_multi): 3 / 4 / 8 ranks of one process on one
 # GPU (ghost boxes packed, copied and unpacked on the device; peer xGMI copies on a multi-GPU node), 23 steps =
 # passes + a tail; x slabs, x-y and x-z grids (edge messages) and a 2x2x2 grid (corner messages); the 4-rank x
