@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -94,9 +96,11 @@ const char* const kCompNames[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
 // Restores the present field components of a plain-media run; returns the
 // checkpoint's step, or -1 (with a message) when the directory holds no
 // matching checkpoint
+// (`put(c, host)` places component c of the whole grid: the device array of a
+// one-GPU run, every rank's allocated box of a --parallel-grid run)
 template <typename T>
 long ckpt_load(const fdtd::Settings& s, const std::string& scheme, const fdtd::Int3& N, const bool* present,
-               Dev<T>* F) {
+               const std::function<void(int, const std::vector<T>&)>& put) {
   const std::string& dir = s.loadFromFile;
   const long step = ckpt_latest(dir);
   if (step < 0) {
@@ -147,14 +151,25 @@ long ckpt_load(const fdtd::Settings& s, const std::string& scheme, const fdtd::I
     }
     in.seekg(0);
     in.read((char*)host.data(), (std::streamsize)(cells * sizeof(T)));
-    HIP_OK(hipMemcpy(F[c].p, host.data(), cells * sizeof(T), hipMemcpyHostToDevice));
+    put(c, host);
   }
   return step;
 }
 
 template <typename T>
+long ckpt_load(const fdtd::Settings& s, const std::string& scheme, const fdtd::Int3& N, const bool* present,
+               Dev<T>* F) {
+  return ckpt_load<T>(s, scheme, N, present, [&](int c, const std::vector<T>& host) {
+    HIP_OK(hipMemcpy(F[c].p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+  });
+}
+
+// (`fetch(c, host)` fills component c of the whole grid; a --parallel-grid
+// run gathers its ranks' owned blocks: the checkpoint is the serial form,
+// which either driver resumes, decomposed or not)
+template <typename T>
 bool ckpt_save(const fdtd::Settings& s, const std::string& scheme, const fdtd::Int3& N, const bool* present,
-               const Dev<T>* F, long step, double dx, double dt) {
+               const std::function<void(int, std::vector<T>&)>& fetch, long step, double dx, double dt) {
   const std::string& dir = s.checkpointDir;
   if (!make_dirs(dir)) return false;
   const size_t cells = (size_t)N[0] * N[1] * N[2];
@@ -164,7 +179,7 @@ bool ckpt_save(const fdtd::Settings& s, const std::string& scheme, const fdtd::I
   std::string arrays;
   for (int c = 0; c < 6; ++c) {
     if (!present[c]) continue;
-    HIP_OK(hipMemcpy(host.data(), F[c].p, cells * sizeof(T), hipMemcpyDeviceToHost));
+    fetch(c, host);
     if (!fdtd::write_dat(fdtd::grid_file_name(step, 0, kCompNames[c], dir) + ".dat", host.data(), cells * sizeof(T)))
       return false;
     arrays += std::string(arrays.empty() ? "" : ", ") + "{\"name\": \"" + kCompNames[c] + "\", \"shape\": " + shape + "}";
@@ -180,6 +195,14 @@ bool ckpt_save(const fdtd::Settings& s, const std::string& scheme, const fdtd::I
   std::snprintf(num, sizeof(num), "%.17g", dt);
   f << ", \"dt\": " << num << ", \"arrays\": [" << arrays << "]}\n";
   return (bool)f;
+}
+
+template <typename T>
+bool ckpt_save(const fdtd::Settings& s, const std::string& scheme, const fdtd::Int3& N, const bool* present,
+               const Dev<T>* F, long step, double dx, double dt) {
+  return ckpt_save<T>(s, scheme, N, present, [&](int c, std::vector<T>& host) {
+    HIP_OK(hipMemcpy(host.data(), F[c].p, host.size() * sizeof(T), hipMemcpyDeviceToHost));
+  }, step, dx, dt);
 }
 
 }  // namespace

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <cmath>
 #include <cstdio>
@@ -17,6 +18,7 @@
 #include "settings_native.h"
 #include "native_api.h"
 #include "native_setup.h"
+#include "native_ckpt.h"
 
 // Part of the native driver: included by main.cpp only (one translation unit),
 // hence the unnamed namespace.
@@ -96,6 +98,7 @@ class MultiRun {
   bool percell = false;
   bool phys = false, cpml = false, upml = false, tfsf = false, point_src = true, ntff = false;
   Dev<T> NG[6];  // NTFF: the whole grid assembled on the first rank's device
+  double ckpt_ms = 0.0;
   int ndev = 0, P = 1, TB = 1;
   int Pd[3] = {1, 1, 1};
   int gd[3] = {1, 1, 1};  // ghost depth per axis
@@ -123,11 +126,13 @@ class MultiRun {
   void phys_step(int t);
   void advance(int t0, int n);
   void run_steps(int t0, int n);
+  void run_ckpt(int t, int n);
   void gather(int c, std::vector<T>& host);
+  void scatter(int c, const std::vector<T>& host);
   void ntff_report(int t);
   void sync_all();
-  void report(double sec, int steps, int warm) const;
-  void save_results(int steps);
+  void report(double sec, int t_end, int steps, int warm) const;
+  bool save_results(int steps);
   void release();
 };
 
@@ -671,13 +676,13 @@ void MultiRun<T>::sync_all() {
 }
 
 template <typename T>
-void MultiRun<T>::report(double sec, int steps, int warm) const {
+void MultiRun<T>::report(double sec, int t_end, int steps, int warm) const {
   const double cells = (double)N[0] * N[1] * N[2];
   const int timed = steps - warm;
   std::printf("Total time = %f seconds\n", sec);
   std::printf("Dimension: 3\n");
   std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);
-  std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", steps, timed, warm);
+  std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", t_end, timed, warm);
   std::printf("Value type: %s\n", Api<T>::name);
   std::printf("\n-------- Details --------\n");
   std::printf("Parallel grid: 1\n");
@@ -765,10 +770,66 @@ void MultiRun<T>::run_steps(int t0, int n) {
   }
 }
 
-// --save-res: the owned blocks of every rank assembled into global DAT / BMP files
+// component c of the whole grid into every rank's allocated box (owned cells
+// and ghosts: a resumed run's first pass reads the ghosts as they are)
 template <typename T>
-void MultiRun<T>::save_results(int steps) {
-  if (!s.doSaveRes) return;
+void MultiRun<T>::scatter(int c, const std::vector<T>& host) {
+  std::vector<T> loc;
+  for (int r = 0; r < P; ++r) {
+    XRank<T>& q = R[r];
+    loc.resize(q.cells());
+    for (int li = 0; li < q.n[0]; ++li)
+      for (int lj = 0; lj < q.n[1]; ++lj)
+        std::memcpy(loc.data() + ((size_t)li * q.n[1] + lj) * q.n[2],
+                    host.data() + ((size_t)(q.g0[0] + li) * N[1] + (q.g0[1] + lj)) * N[2] + q.g0[2],
+                    (size_t)q.n[2] * sizeof(T));
+    HIP_OK(hipSetDevice(q.dev));
+    HIP_OK(hipMemcpy(q.F[c].p, loc.data(), loc.size() * sizeof(T), hipMemcpyHostToDevice));
+  }
+}
+
+// --checkpoint-step P: a checkpoint after every step t with t % P == 0 (the
+// gathered grid in the serial form, native_ckpt.h; its I/O time is kept out
+// of the reported rate as in native_run.h run_ckpt)
+template <typename T>
+void MultiRun<T>::run_ckpt(int t, int n) {
+  const int Pc = s.checkpointDir.empty() ? 0 : s.checkpointStep;
+  if (Pc <= 0) {
+    run_steps(t, n);
+    return;
+  }
+  const int end = t + n;
+  while (t < end) {
+    const int nxt = std::min(end, (t / Pc + 1) * Pc);
+    run_steps(t, nxt - t);
+    t = nxt;
+    if (t % Pc == 0) {
+      sync_all();
+      const auto c0 = std::chrono::steady_clock::now();
+      const bool present[6] = {true, true, true, true, true, true};
+      if (!ckpt_save<T>(s, "3d", N, present, [this](int c, std::vector<T>& host) { gather(c, host); }, t,
+                        s.gridStep, dt)) {
+        std::fprintf(stderr, "fdtd3d: cannot write the checkpoint to %s\n", s.checkpointDir.c_str());
+        std::exit(1);
+      }
+      ckpt_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
+    }
+  }
+}
+
+// --save-res: the owned blocks of every rank assembled into global DAT / BMP
+// files; --checkpoint-dir: the final checkpoint (gathered, serial form)
+template <typename T>
+bool MultiRun<T>::save_results(int steps) {
+  if (!s.checkpointDir.empty()) {
+    const bool present[6] = {true, true, true, true, true, true};
+    if (!ckpt_save<T>(s, "3d", N, present, [this](int c, std::vector<T>& host) { gather(c, host); }, steps,
+                      s.gridStep, dt)) {
+      std::fprintf(stderr, "fdtd3d: cannot write the checkpoint to %s\n", s.checkpointDir.c_str());
+      return false;
+    }
+  }
+  if (!s.doSaveRes) return true;
   const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
   std::vector<T> host;
   for (int c = 0; c < 6; ++c) {
@@ -783,6 +844,7 @@ void MultiRun<T>::save_results(int steps) {
       fdtd::write_bmp(base + std::to_string(kz) + "-Re.bmp", v, N[0], N[1], s.dumperPalette);
     }
   }
+  return true;
 }
 
 template <typename T>
@@ -823,18 +885,28 @@ int MultiRun<T>::main() {
   }
   enable_peers();
   plan_outputs();
-  const int steps = s.numTimeSteps;
+  // --load-from-file: a serial-form checkpoint (either driver's, or a
+  // decomposed native run's gathered one) scattered over the ranks
+  int t0 = 0;
+  if (!s.loadFromFile.empty()) {
+    const bool present[6] = {true, true, true, true, true, true};
+    const long got = ckpt_load<T>(s, "3d", N, present, [this](int c, const std::vector<T>& host) { scatter(c, host); });
+    if (got < 0) return 1;
+    t0 = (int)got;
+  }
+  const int steps = std::max(0, s.numTimeSteps - t0);
   const int warm = std::max(0, std::min(s.warmupSteps, steps));
-  run_steps(0, warm);
+  run_ckpt(t0, warm);
   sync_all();
   const auto c0 = std::chrono::steady_clock::now();
-  run_steps(warm, steps - warm);
+  ckpt_ms = 0.0;
+  run_ckpt(t0 + warm, steps - warm);
   sync_all();
   HIP_OK(hipGetLastError());
-  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
-  report(sec, steps, warm);
-  save_results(steps);
-  return 0;
+  const double sec =
+      std::max(0.0, std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count() - ckpt_ms / 1e3);
+  report(sec, t0 + steps, steps, warm);
+  return save_results(t0 + steps) ? 0 : 1;
 }
 
 template <typename T>

@@ -615,8 +615,9 @@ bool native_supported(const fdtd::Settings& s) {
                        (par_phys || s.doUseMetamaterials || !s.doUseSplitKernels));
   // checkpoints / resume: plain media (state = the field components)
   const bool ckpt = !s.checkpointDir.empty() || !s.loadFromFile.empty();
+  // (parallel grids: the gathered grid in the serial form, scattered over the ranks on resume)
   const bool ckpt_ok = !ckpt || (!s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials && !s.doUseAmplitudeMode &&
-                                 !s.doUseNTFF && !s.doUseParallelGrid);
+                                 !s.doUseNTFF && (!s.doUseParallelGrid || s.dimension == 3));
   return !((s.doUsePML && !cpml_ok && !upml_ok) || (s.doUseTFSF && !tfsf_ok) || !meta_ok || !ntff_ok || !amp_ok ||
            !par_ok || !ckpt_ok || s.doUseComplexFieldValues || s.doUseDoubleMaterialPrecision);
 }

@@ -97,7 +97,7 @@ def test_native_executable_cli(host):
                  ["--2d", "--parallel-grid"],
                  ["--3d", "--use-pml", "--use-tfsf", "--pml-sizex", "10", "--tfsf-sizex", "8"],
                  ["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f32", "--checkpoint-dir", "/tmp/ck"],
-                 ["--3d", "--parallel-grid", "--checkpoint-dir", "/tmp/ck", "--checkpoint-step", "5"],
+                 ["--3d", "--parallel-grid", "--use-pml", "--pml-type", "cpml", "--checkpoint-dir", "/tmp/ck"],
                  ["--2d", "--use-tfsf", "--load-from-file", "/tmp/ck"]):
         r = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=60)
         assert r.returncode == 2 and "python -m fdtd3d_amd" in r.stderr, argv

@@ -238,6 +238,50 @@ def test_native_ntff_matches_python(dtype, gpu):
 
 
 @pytest.mark.gpu
+def test_native_parallel_grid_checkpoint(tmp_path):
+    """Checkpoints of a decomposed native run (2x2x1 ranks, the gathered grid in the serial form): resumed by
+    the decomposed native run, by the single-rank native run and by the Python driver, every one ends on the
+    fields of the Python driver's full run (fp64)."""
+    exe = native.executable()
+    argv = ["--3d", "--sizex", "28", "--sizey", "20", "--sizez", "24", "--scene", "vacuum", "--time-block", "3",
+            "--dtype", "f64"]
+    par = ["--parallel-grid", "--topology-sizex", "2", "--topology-sizey", "2"]
+    py = ["--backend", "torch", "--device", "cpu"]
+    k, n = 7, 19
+    d = {x: tmp_path / x for x in ("a", "par", "one", "py", "full")}
+
+    def nat(extra):
+        r = subprocess.run([exe] + argv + extra, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return r.stdout
+
+    out = nat(par + ["--time-steps", str(2 * k + 1), "--checkpoint-dir", str(d["a"]), "--checkpoint-step", str(k)])
+    assert "Number of processes: 4" in out
+    for t in (k, 2 * k, 2 * k + 1):
+        side = d["a"] / ("checkpoint[%d]_rank-0.json" % t)
+        assert side.exists(), t
+        if t != k:
+            side.unlink()
+    out = nat(par + ["--time-steps", str(n), "--load-from-file", str(d["a"]), "--checkpoint-dir", str(d["par"])])
+    assert "Number of time steps: %d (%d timed" % (n, n - k) in out, out
+    nat(["--time-steps", str(n), "--load-from-file", str(d["a"]), "--checkpoint-dir", str(d["one"])])
+    assert py_run(argv + py + ["--time-steps", str(n), "--load-from-file", str(d["a"]), "--checkpoint-dir",
+                               str(d["py"])], out=io.StringIO()) == 0
+    assert py_run(argv + py + ["--time-steps", str(n), "--checkpoint-dir", str(d["full"])], out=io.StringIO()) == 0
+    shape = (28, 20, 24)
+    for kind in "EH":
+        errs, peak = [], 0.0
+        for c in "xyz":
+            name = "current[%d]_rank-0_%s%s.dat" % (n, kind, c)
+            ref = np.fromfile(d["full"] / name, dtype=np.float64).reshape(shape)
+            peak = max(peak, np.abs(ref).max())
+            errs += [np.abs(np.fromfile(d[x] / name, dtype=np.float64).reshape(shape) - ref).max()
+                     for x in ("par", "one", "py")]
+        assert peak > 0
+        assert max(errs) <= 1e-11 * peak, (kind, errs, peak)
+
+
+@pytest.mark.gpu
 def test_native_ntff_parallel_grid():
     """The NTFF diagram of a decomposed native run (2x2x1 ranks: UPML chain + TF/SF + sphere on the split half
     steps, the grid gathered for each report) equals the single-rank native run's to fp64 round-off."""
