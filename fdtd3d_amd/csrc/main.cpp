@@ -16,11 +16,11 @@
 // plain-media runs in the Python driver's format (--checkpoint-dir,
 // --load-from-file) and --parallel-grid decompositions (any x / y / z rank
 // grid) over the node's GPUs from one process (run_multi): plain media on
-// blocked passes; CPML, the UPML, Drude / Lorentz spheres and TF/SF on the
-// split half steps.  Complex fields and the decomposed amplitude / NTFF /
-// checkpoint runs go through the Python driver (python -m fdtd3d_amd), which
-// shares the kernels; asking this binary for them is an error, never a silent
-// fallback.
+// blocked passes; CPML, the UPML, Drude / Lorentz spheres, TF/SF and
+// amplitude mode on the split half steps; the NTFF diagram and plain-media
+// checkpoints from the gathered grid.  Complex fields go through the Python
+// driver (python -m fdtd3d_amd), which shares the kernels; asking this binary
+// for them is an error, never a silent fallback.
 #include <hip/hip_runtime.h>
 
 #include <dirent.h>
@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr,
                  "fdtd3d (native): CPML in 3D outside whole 4-cell z rows, PML / TF/SF in 1D, TF/SF boxes reaching "
                  "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "
-                 "grids with amplitude mode or NTFF, checkpoints beyond plain media, and complex "
+                 "grids beyond 3D, checkpoints beyond plain media, and complex "
                  "fields run through the Python driver: python -m fdtd3d_amd <same options>\n");
     return 2;
   }

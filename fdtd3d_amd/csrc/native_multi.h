@@ -80,6 +80,15 @@ struct XRank {
   std::vector<IBox> chain_regs, plain_regs;
   std::vector<bool> chain_disp;
   long long src_off = -1;
+  // amplitude mode: running maxima ([x][6][y][z]), changed counts of a
+  // check period, the amplitude boxes (local), the z-line cells it owns,
+  // the near-convergence snapshot
+  Dev<T> AMP;
+  Dev<unsigned> CNT;
+  Dev<long long> LINE;
+  int line_n = 0;
+  int ab[36];
+  Dev<char> SNAP;
   size_t cells() const { return (size_t)n[0] * n[1] * n[2]; }
 };
 
@@ -97,6 +106,8 @@ class MultiRun {
   double dt = 0, freq = 0, cb = 0, db = 0;
   bool percell = false;
   bool phys = false, cpml = false, upml = false, tfsf = false, point_src = true, ntff = false;
+  bool amp = false, amp_on = false, amp_line = false;  // amplitude mode; its phase; the global z line exists
+  int amp_taken = 0, amp_stable = -1;
   Dev<T> NG[6];  // NTFF: the whole grid assembled on the first rank's device
   double ckpt_ms = 0.0;
   int ndev = 0, P = 1, TB = 1;
@@ -124,6 +135,9 @@ class MultiRun {
   void phys_half(XRank<T>& q, int kind, double sv);
   void exchange(int kind);
   void phys_step(int t);
+  void setup_amp(XRank<T>& q);
+  std::vector<std::pair<void*, size_t>> rank_state(XRank<T>& q);
+  int amp_run(int t);
   void advance(int t0, int n);
   void run_steps(int t0, int n);
   void run_ckpt(int t, int n);
@@ -157,7 +171,8 @@ int MultiRun<T>::plan_ranks() {
   upml = (s.doUsePML && s.pmlType == "upml") || s.doUseMetamaterials;  // the D/B chain
   cpml = s.doUsePML && !upml;
   tfsf = s.doUseTFSF;
-  phys = cpml || upml || tfsf;
+  amp = s.doUseAmplitudeMode;
+  phys = cpml || upml || tfsf || amp;
   ntff = s.doUseNTFF;
   point_src = !tfsf || s.doUsePointSource;
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
@@ -500,6 +515,170 @@ void MultiRun<T>::clip36(const int* b36, const IBox& r, int* out) {
   }
 }
 
+// amplitude mode of a rank (native_amp.h AmpMode on the rank's cells): the
+// maxima and counts, each component's amplitude box (its update range minus
+// the PML cells, Scheme3D.cpp:3016-3030) clipped to the owned cells, the owned
+// cells of the Ez z line at (Nx / 8, Ny / 2) outside the z PML (Scheme3D.cpp:2995-3013)
+template <typename T>
+void MultiRun<T>::setup_amp(XRank<T>& q) {
+  const size_t plane = (size_t)q.n[1] * q.n[2];
+  q.AMP.alloc((size_t)q.n[0] * 6 * plane);
+  q.CNT.alloc(std::max(1, s.amplitudeCheckSteps));
+  const int left[3] = {s.doUsePML ? s.pmlSizeX : 0, s.doUsePML ? s.pmlSizeY : 0, s.doUsePML ? s.pmlSizeZ : 0};
+  for (int c = 0; c < 6; ++c) {
+    fdtd::Int3 glo, ghi;
+    fdtd::global_range(c, N, active, glo, ghi);
+    int* b = q.ab + 6 * c;
+    bool empty = false;
+    for (int a = 0; a < 3; ++a) {
+      int lo = glo[a], hi = ghi[a];
+      const int right = N[a] - left[a];
+      if (left[a] != right) {
+        lo = std::max(lo, (int)std::ceil(left[a] - kMinFP[c][a]));
+        hi = std::min(hi, (int)std::ceil(right - kMinFP[c][a]));
+      }
+      lo = std::max(lo, q.lo[a]);
+      hi = std::min(hi, q.hi[a]);
+      empty = empty || hi <= lo;
+      b[a] = lo - q.g0[a];
+      b[3 + a] = hi - q.g0[a];
+    }
+    if (empty)
+      for (int e = 0; e < 6; ++e) b[e] = 0;
+  }
+  amp_line = point_src;
+  if (!amp_line) return;
+  const int k0 = s.doUsePML ? s.pmlSizeZ : 0;
+  amp_line = N[2] - 2 * k0 > 0;
+  const int li = N[0] / 8, lj = N[1] / 2;
+  std::vector<long long> offs;
+  if (li >= q.lo[0] && li < q.hi[0] && lj >= q.lo[1] && lj < q.hi[1])
+    for (int k = std::max(k0, q.lo[2]); k < std::min(N[2] - k0, q.hi[2]); ++k)
+      offs.push_back(((long long)(li - q.g0[0]) * q.n[1] + (lj - q.g0[1])) * q.n[2] + (k - q.g0[2]));
+  q.line_n = (int)offs.size();
+  if (q.line_n > 0) {
+    q.LINE.alloc(offs.size());
+    HIP_OK(hipMemcpy(q.LINE.p, offs.data(), offs.size() * sizeof(long long), hipMemcpyHostToDevice));
+  }
+}
+
+// every array of a rank that carries state between steps (the amplitude
+// phase's near-convergence snapshot; native_run.h amp_state)
+template <typename T>
+std::vector<std::pair<void*, size_t>> MultiRun<T>::rank_state(XRank<T>& q) {
+  std::vector<std::pair<void*, size_t>> v;
+  for (int c = 0; c < 6; ++c) v.push_back({q.F[c].p, q.cells() * sizeof(T)});
+  v.push_back({q.AMP.p, q.AMP.n * sizeof(T)});
+  if (q.tf) {
+    v.push_back({q.tf->einc.p, (size_t)q.tf->nline * sizeof(T)});
+    v.push_back({q.tf->hinc.p, (size_t)q.tf->nline * sizeof(T)});
+  }
+  if (q.cp)
+    for (auto* d : q.cp->keep) v.push_back({d->p, d->n * sizeof(T)});
+  if (q.up)
+    for (int c = 0; c < 6; ++c) {
+      for (const auto& lv : q.up->D[c])
+        for (size_t r = 0; r < lv.size(); ++r) v.push_back({lv[r], q.up->rvol[r] * sizeof(T)});
+      for (const auto& lv : q.up->D1[c])
+        for (size_t r = 0; r < lv.size(); ++r)
+          if (lv[r]) v.push_back({lv[r], q.up->rvol[r] * sizeof(T)});
+    }
+  return v;
+}
+
+// The amplitude phase from step t over the ranks (native_amp.h AmpMode::run):
+// check periods of K steps, each step's changed-maximum counts summed over
+// the ranks once per period; the run ends with the period in which a step
+// (after the first) changed no maximum -- redone from a snapshot up to that
+// step near convergence -- or after --amplitude-time-steps steps.  Returns
+// the last step.
+template <typename T>
+int MultiRun<T>::amp_run(int t) {
+  amp_on = true;
+  const int K = std::max(1, s.amplitudeCheckSteps);
+  std::vector<unsigned> got(K), part(K);
+  auto period = [&](int n) {
+    for (XRank<T>& q : R) {
+      HIP_OK(hipSetDevice(q.dev));
+      HIP_OK(hipMemsetAsync(q.CNT.p, 0, K * sizeof(unsigned), q.st));
+    }
+    for (int i = 0; i < n; ++i) {
+      phys_step(t);
+      for (XRank<T>& q : R) {
+        HIP_OK(hipSetDevice(q.dev));
+        const T* af[6] = {q.F[0].p, q.F[1].p, q.F[2].p, q.F[3].p, q.F[4].p, q.F[5].p};
+        const size_t plane = (size_t)q.n[1] * q.n[2];
+        T* aa[6];
+        for (int c = 0; c < 6; ++c) aa[c] = q.AMP.p + c * plane;
+        K_OK(amp_many(af, aa, 6, q.n[1], q.n[2], q.ab, (long long)(6 * plane), 0.001, q.CNT.p + i, q.st));
+      }
+      ++t;
+    }
+    std::fill(got.begin(), got.end(), 0u);
+    for (XRank<T>& q : R) {
+      HIP_OK(hipSetDevice(q.dev));
+      HIP_OK(hipMemcpyAsync(part.data(), q.CNT.p, n * sizeof(unsigned), hipMemcpyDeviceToHost, q.st));
+      HIP_OK(hipStreamSynchronize(q.st));
+      for (int i = 0; i < n; ++i) got[i] += part[i];
+    }
+  };
+  long long acells = 0;
+  for (XRank<T>& q : R)
+    for (int c = 0; c < 6; ++c) {
+      const int* b = q.ab + 6 * c;
+      acells += (long long)std::max(0, b[3] - b[0]) * std::max(0, b[4] - b[1]) * std::max(0, b[5] - b[2]);
+    }
+  const long long near = std::max(1LL, (long long)(0.02 * (double)acells));
+  long long last = -1;
+  bool done = false;
+  while (!done && amp_taken < s.numAmplitudeTimeSteps) {
+    int n = std::min(K, s.numAmplitudeTimeSteps - amp_taken);
+    int t_snap = -1;
+    if (n > 1 && last >= 0 && last <= near) {
+      for (XRank<T>& q : R) {
+        HIP_OK(hipSetDevice(q.dev));
+        const auto v = rank_state(q);
+        size_t total = 0, o = 0;
+        for (const auto& e : v) total += e.second;
+        if (!q.SNAP.p) q.SNAP.alloc(total);
+        for (const auto& e : v) {
+          HIP_OK(hipMemcpyAsync(q.SNAP.p + o, e.first, e.second, hipMemcpyDeviceToDevice, q.st));
+          o += e.second;
+        }
+      }
+      t_snap = t;
+    }
+    period(n);
+    int first = -1;
+    for (int r = 0; r < n && first < 0; ++r)
+      if (got[r] == 0 && amp_taken + r + 1 > 1) first = r;
+    if (first < 0) {
+      last = got[n - 1];
+      amp_taken += n;
+      continue;
+    }
+    amp_stable = amp_taken + first + 1;
+    if (first + 1 < n && t_snap >= 0) {
+      for (XRank<T>& q : R) {
+        HIP_OK(hipSetDevice(q.dev));
+        const auto v = rank_state(q);
+        size_t o = 0;
+        for (const auto& e : v) {
+          HIP_OK(hipMemcpyAsync(e.first, q.SNAP.p + o, e.second, hipMemcpyDeviceToDevice, q.st));
+          o += e.second;
+        }
+      }
+      t = t_snap;
+      n = first + 1;
+      period(n);
+    }
+    amp_taken += n;
+    done = true;
+  }
+  amp_on = false;
+  return t;
+}
+
 // physics set-up of rank r (its device current): owned update boxes, CPML
 // tables, TF/SF tables and incident line, the point source; false when the
 // TF/SF box does not fit the incident line
@@ -539,6 +718,7 @@ bool MultiRun<T>::setup_physics(int r) {
     if (!setup_tfsf(*q.tf, s, N, gb36, q.C, percell ? 1.0 : cb, db, dt, s.gridStep, freq, 3, present, q.g0, q.n))
       return false;
   }
+  if (amp) setup_amp(q);
   bool has = point_src;
   for (int a = 0; a < 3; ++a) has = has && sp[a] >= q.lo[a] && sp[a] < q.hi[a];
   q.src_off = has ? ((long long)(sp[0] - q.g0[0]) * q.n[1] + (sp[1] - q.g0[1])) * q.n[2] + (sp[2] - q.g0[2]) : -1;
@@ -603,7 +783,13 @@ void MultiRun<T>::phys_half(XRank<T>& q, int kind, double sv) {
       for (auto* l : q.tf->tab[c])
         K_OK(tfsf_apply(F[c], *l, kind == 0 ? q.tf->hinc.p : q.tf->einc.p, whole, q.st));
   }
-  if (kind == 0 && q.src_off >= 0) K_OK(setv(F[2], q.src_off, sv, q.st));
+  if (kind == 0) {
+    if (amp_on && amp_line) {  // the amplitude phase's Ez z line replaces the point source
+      if (q.line_n > 0) K_OK(setvs(F[2], q.LINE.p, q.line_n, sv, q.st));
+    } else if (q.src_off >= 0) {
+      K_OK(setv(F[2], q.src_off, sv, q.st));
+    }
+  }
 }
 
 // the updated kind's three components to the face neighbours' ghosts: every
@@ -678,7 +864,7 @@ void MultiRun<T>::sync_all() {
 template <typename T>
 void MultiRun<T>::report(double sec, int t_end, int steps, int warm) const {
   const double cells = (double)N[0] * N[1] * N[2];
-  const int timed = steps - warm;
+  const int timed = steps - warm + amp_taken;
   std::printf("Total time = %f seconds\n", sec);
   std::printf("Dimension: 3\n");
   std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);
@@ -704,6 +890,12 @@ void MultiRun<T>::report(double sec, int t_end, int steps, int warm) const {
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), 26-neighbour ghost boxes by "
                 "packed peer copies\n", TB);
   std::printf("Throughput: %.1f Mcells/s\n", cells * timed / sec / 1e6);
+  if (amp) {
+    if (amp_stable > 0)
+      std::printf("Amplitude mode: stable after %d steps (%d amplitude steps taken)\n", amp_stable, amp_taken);
+    else
+      std::printf("Amplitude mode: stable state not reached after %d steps\n", amp_taken);
+  }
   if (s.doPrintJson)
     std::printf("{\"seconds\": %.6f, \"steps\": %d, \"mcells_per_s\": %.3f, \"ranks\": %d}\n", sec, timed,
                 cells * timed / sec / 1e6, P);
@@ -864,6 +1056,10 @@ void MultiRun<T>::release() {
     q.cp.reset();
     q.tf.reset();
     q.up.reset();
+    q.AMP.reset();
+    q.CNT.reset();
+    q.LINE.reset();
+    q.SNAP.reset();
     HIP_OK(hipEventDestroy(q.done));
     HIP_OK(hipEventDestroy(q.copied));
     HIP_OK(hipStreamDestroy(q.st));
@@ -901,12 +1097,15 @@ int MultiRun<T>::main() {
   const auto c0 = std::chrono::steady_clock::now();
   ckpt_ms = 0.0;
   run_ckpt(t0 + warm, steps - warm);
+  // amplitude mode: after the regular steps, check periods until a step
+  // changes no running maximum (native_amp.h)
+  const int t_end = amp ? amp_run(t0 + steps) : t0 + steps;
   sync_all();
   HIP_OK(hipGetLastError());
   const double sec =
       std::max(0.0, std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count() - ckpt_ms / 1e3);
-  report(sec, t0 + steps, steps, warm);
-  return save_results(t0 + steps) ? 0 : 1;
+  report(sec, t_end, steps, warm);
+  return save_results(t_end) ? 0 : 1;
 }
 
 template <typename T>

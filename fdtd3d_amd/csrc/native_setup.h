@@ -607,10 +607,10 @@ bool native_supported(const fdtd::Settings& s) {
   const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
   // parallel grids: 3D, any rank grid -- plain media on blocked passes; CPML, the UPML, Drude / Lorentz spheres
   // and TF/SF (point source optional) on the split half steps, the NTFF diagram from the gathered grid
-  // (native_multi.h); not amplitude mode
+  // (native_multi.h), amplitude mode on the split half steps
   const bool par_phys = s.doUsePML || s.doUseTFSF || s.doUseMetamaterials;
   const bool par_ok = !s.doUseParallelGrid ||
-                      (s.dimension == 3 && !s.doUseAmplitudeMode &&
+                      (s.dimension == 3 &&
                        (s.scene == "vacuum" || s.scene == "sphere" || s.scene == "drude-sphere") &&
                        (par_phys || s.doUseMetamaterials || !s.doUseSplitKernels));
   // checkpoints / resume: plain media (state = the field components)

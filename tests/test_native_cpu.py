@@ -88,12 +88,12 @@ def test_native_executable_cli(host):
     # CPML runs natively in 3D (whole 4-cell z rows, fp32 / fp64) and in 2D, the UPML in 3D and 2D, the Drude
     # chain and NTFF in 3D, parallel grids for 3D plain media, CPML, UPML, Drude spheres and TF/SF; 3D CPML on z
     # rows of a size not divisible by 4, 2D metamaterials, metamaterials outside the drude-sphere scene, amplitude
-    # mode with NTFF and parallel grids with amplitude mode go to the Python driver
+    # mode with NTFF go to the Python driver
     for argv in (["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f64", "--sizez", "42"],
                  ["--2d", "--use-ntff"],
                  ["--2d", "--use-pml", "--use-metamaterials"],
                  ["--3d", "--use-metamaterials", "--use-pml", "--scene", "reference"],
-                 ["--3d", "--use-amp-mode", "--use-ntff"], ["--3d", "--parallel-grid", "--use-amp-mode"],
+                 ["--3d", "--use-amp-mode", "--use-ntff"], ["--3d", "--parallel-grid", "--use-amp-mode", "--use-ntff"],
                  ["--2d", "--parallel-grid"],
                  ["--3d", "--use-pml", "--use-tfsf", "--pml-sizex", "10", "--tfsf-sizex", "8"],
                  ["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f32", "--checkpoint-dir", "/tmp/ck"],

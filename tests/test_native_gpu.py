@@ -281,6 +281,53 @@ def test_native_parallel_grid_checkpoint(tmp_path):
         assert max(errs) <= 1e-11 * peak, (kind, errs, peak)
 
 
+AMP_MULTI = {
+    "amp_2x2x1": (CASES["3d_amp"], ["--topology-sizex", "2", "--topology-sizey", "2"]),
+    "amp_cpml_2x1x2": (CASES["3d_amp_cpml"], ["--topology-sizex", "2", "--topology-sizez", "2"]),
+    # until the stable state (the near-convergence snapshot and the redone period over the ranks)
+    # (the single-rank run: stable after 1015 steps)
+    "amp_cpml_stable_2x2x1": (["--3d", "--sizex", "20", "--same-size", "--time-steps", "5", "--scene", "vacuum",
+                               "--use-amp-mode", "--amplitude-time-steps", "1200", "--use-pml", "--pml-type", "cpml",
+                               "--pml-sizex", "5", "--same-size-pml"],
+                              ["--topology-sizex", "2", "--topology-sizey", "2"]),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(AMP_MULTI))
+def test_native_parallel_grid_amplitude(case, tmp_path):
+    """Amplitude mode of a decomposed native run (running maxima per rank, changed counts summed over the ranks
+    per check period): the same amplitude steps and final fields as the single-rank native run (fp64)."""
+    exe = native.executable()
+    base, topo = AMP_MULTI[case]
+    argv = base + ["--dtype", "f64", "--save-res", "--save-as-dat"]
+    outs = {}
+    for lab, extra in (("one", []), ("par", ["--parallel-grid"] + topo)):
+        d = tmp_path / lab
+        d.mkdir()
+        r = subprocess.run([exe] + argv + extra + ["--output-dir", str(d)], capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs[lab] = [l for l in r.stdout.splitlines() if l.startswith("Amplitude mode:")]
+    assert outs["one"] and outs["one"] == outs["par"], outs
+    line = outs["one"][0]
+    steps = int(base[base.index("--time-steps") + 1])
+    steps += int(line.split("after ")[1].split()[0]) if "not reached" in line else int(line.split("(")[1].split()[0])
+    if case.endswith("stable_2x2x1"):
+        assert "stable after" in line, line
+    shape, _ = _shape(argv)
+    for kind in "EH":
+        errs, peak = [], 0.0
+        for c in "xyz":
+            name = "current[%d]_rank-0_%s%s.dat" % (steps, kind, c)
+            a = np.fromfile(tmp_path / "par" / name, dtype=np.float64).reshape(shape)
+            b = np.fromfile(tmp_path / "one" / name, dtype=np.float64).reshape(shape)
+            errs.append(np.abs(a - b).max())
+            peak = max(peak, np.abs(b).max())
+        assert peak > 0
+        assert max(errs) <= 1e-12 * peak, (kind, errs, peak)
+
+
 @pytest.mark.gpu
 def test_native_ntff_parallel_grid():
     """The NTFF diagram of a decomposed native run (2x2x1 ranks: UPML chain + TF/SF + sphere on the split half
