@@ -31,16 +31,27 @@ struct Lowdim2d {
   // to round-off) and the four PML strips (one cell of staggering slack inside)
   IBox inner, strips[4];
 
+  // (decomposed runs: N_ = the rank's array extents, `G` = the global grid,
+  // `org` = the rank's global origin: the strips are the global ones in the
+  // rank's indices; `boxes` hold its owned update boxes)
   Lowdim2d(const fdtd::Settings& s, Dev<T>* F_, Dev<T>* C_, const int* boxes_, const fdtd::Int3& N_,
-           const bool* present_, Pml2d<T>& p2_, bool tm_, bool percell_, double cb_, double db_, hipStream_t st_)
+           const bool* present_, Pml2d<T>& p2_, bool tm_, bool percell_, double cb_, double db_, hipStream_t st_,
+           const fdtd::Int3* G = nullptr, const int* org = nullptr)
       : F(F_), C(C_), boxes(boxes_), N(N_), present(present_), p2(p2_), tm(tm_), percell(percell_), cb(cb_), db(db_),
         st(st_) {
+    const fdtd::Int3 M = G ? *G : N;
+    const int o[3] = {org ? org[0] : 0, org ? org[1] : 0, org ? org[2] : 0};
     const int ppx = s.pmlSizeX + 1, ppy = s.pmlSizeY + 1;
-    inner = {{ppx, ppy, 0}, {N[0] - ppx, N[1] - ppy, N[2]}};
-    strips[0] = {{0, 0, 0}, {std::min(ppx, N[0]), N[1], N[2]}};
-    strips[1] = {{std::max(0, N[0] - ppx), 0, 0}, {N[0], N[1], N[2]}};
-    strips[2] = {{ppx, 0, 0}, {N[0] - ppx, std::min(ppy, N[1]), N[2]}};
-    strips[3] = {{ppx, std::max(0, N[1] - ppy), 0}, {N[0] - ppx, N[1], N[2]}};
+    inner = {{ppx, ppy, 0}, {M[0] - ppx, M[1] - ppy, M[2]}};
+    strips[0] = {{0, 0, 0}, {std::min(ppx, M[0]), M[1], M[2]}};
+    strips[1] = {{std::max(0, M[0] - ppx), 0, 0}, {M[0], M[1], M[2]}};
+    strips[2] = {{ppx, 0, 0}, {M[0] - ppx, std::min(ppy, M[1]), M[2]}};
+    strips[3] = {{ppx, std::max(0, M[1] - ppy), 0}, {M[0] - ppx, M[1], M[2]}};
+    for (IBox* b : {&inner, &strips[0], &strips[1], &strips[2], &strips[3]})
+      for (int a = 0; a < 3; ++a) {
+        b->lo[a] -= o[a];
+        b->hi[a] -= o[a];
+      }
   }
 
   // 2D CPML corrections of one kind (0 = E) after the plain update

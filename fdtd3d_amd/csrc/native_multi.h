@@ -77,6 +77,9 @@ struct XRank {
   // UPML / Drude: the rank's chain tables and region-local D levels, its part
   // of the global chain and plain regions (local indices)
   std::unique_ptr<native_phys::Upml<T>> up;
+  // 2D: the CPML slabs / UPML strips tables and the half-step helper
+  std::unique_ptr<Pml2d<T>> p2;
+  std::unique_ptr<Lowdim2d<T>> ld;
   std::vector<IBox> chain_regs, plain_regs;
   std::vector<bool> chain_disp;
   long long src_off = -1;
@@ -102,7 +105,11 @@ class MultiRun {
  private:
   const fdtd::Settings& s;
   fdtd::Int3 N;
-  const std::vector<int> active = {0, 1, 2};
+  int dim = 3;
+  std::string scheme = "3d";
+  std::vector<int> active = {0, 1, 2};
+  bool present[6] = {true, true, true, true, true, true};
+  int src_comp = 2;
   double dt = 0, freq = 0, cb = 0, db = 0;
   bool percell = false;
   bool phys = false, cpml = false, upml = false, tfsf = false, point_src = true, ntff = false;
@@ -155,7 +162,17 @@ class MultiRun {
 // split that way
 template <typename T>
 int MultiRun<T>::plan_ranks() {
-  N = {s.sizeX, s.sizeY, s.sizeZ};
+  dim = s.dimension;
+  scheme = dim == 3 ? "3d" : s.mode2D;
+  N = {s.sizeX, s.sizeY, dim == 3 ? s.sizeZ : 1};
+  if (dim == 2) {
+    // TMz (Ez Hx Hy) / TEz (Ex Ey Hz) on an x / y rank grid
+    active = {0, 1};
+    for (int c = 0; c < 6; ++c) present[c] = false;
+    if (scheme == "tmz") present[2] = present[3] = present[4] = true;
+    else present[0] = present[1] = present[5] = true;
+    src_comp = scheme == "tmz" ? 2 : 5;
+  }
   const double dx = s.gridStep;
   dt = dx * s.courantNum / kC;
   freq = kC / s.sourceWaveLength;
@@ -165,15 +182,15 @@ int MultiRun<T>::plan_ranks() {
   HIP_OK(hipGetDeviceCount(&ndev));
   Pd[0] = std::max(1, s.topologySizeX);
   Pd[1] = std::max(1, s.topologySizeY);
-  Pd[2] = std::max(1, s.topologySizeZ);
+  Pd[2] = dim == 3 ? std::max(1, s.topologySizeZ) : 1;
   if (Pd[0] * Pd[1] * Pd[2] == 1) Pd[0] = ndev;
   P = Pd[0] * Pd[1] * Pd[2];
   upml = (s.doUsePML && s.pmlType == "upml") || s.doUseMetamaterials;  // the D/B chain
   cpml = s.doUsePML && !upml;
   tfsf = s.doUseTFSF;
   amp = s.doUseAmplitudeMode;
-  phys = cpml || upml || tfsf || amp;
-  ntff = s.doUseNTFF;
+  phys = cpml || upml || tfsf || amp || dim == 2;  // (2D: the split half steps always)
+  ntff = s.doUseNTFF && dim == 3;
   point_src = !tfsf || s.doUsePointSource;
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
   TB = phys ? 1 : std::max(1, std::min(T_max, s.timeBlock <= 0 ? (sizeof(T) == 4 ? 5 : 4) : s.timeBlock));
@@ -200,13 +217,14 @@ int MultiRun<T>::plan_ranks() {
       q.g0[a] = q.lo[a] - gl;
       q.n[a] = q.hi[a] - q.lo[a] + gl + gh;
     }
-    if ((sizeof(T) == 4 || cpml) && q.n[2] % 4 != 0) {
+    if (dim == 3 && (sizeof(T) == 4 || cpml) && q.n[2] % 4 != 0) {
       std::fprintf(stderr, "fdtd3d (native): fp32 / CPML parallel grids need every rank's z extent (ghosts "
                            "included) %% 4 == 0 (4-cell rows): rank %d has %d\n", r, q.n[2]);
       return 2;
     }
   }
   sp = {N[0] / 2, N[1] / 2, N[2] / 2};
+  if (scheme == "tmz") sp = {N[0] > 140 ? 70 : N[0] / 2, N[1] / 2, 0};  // (SchemeTMz.cpp:1345)
   return 0;
 }
 
@@ -274,21 +292,31 @@ void MultiRun<T>::setup_rank(int r) {
   }
   if (percell) {
     // per-cell E coefficients of the dielectric sphere (2-point eps
-    // averages, as the single-rank path), H on the scalar db
+    // averages, as the single-rank path; 2D: the cylinder's section at the
+    // centre's z), H on the scalar db (2D: db arrays, the 2D kernels take one
+    // coefficient form per launch)
     const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
     std::vector<T> host(n);
     for (int c = 0; c < 3; ++c) {
-      const int di = c == 0, dj = c == 1, dk = c == 2;
+      const int di = c == 0, dj = c == 1, dk = c == 2 && dim == 3;
       for (int li = 0; li < q.n[0]; ++li)
         for (int lj = 0; lj < q.n[1]; ++lj)
           for (int lk = 0; lk < q.n[2]; ++lk) {
             const int i = q.g0[0] + li, j = q.g0[1] + lj, k = q.g0[2] + lk;
-            const double a = sphere_eps(i + 0.5, j + 0.5, k + 0.5, ctr, s.sphereRadius, s.sphereEps);
-            const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, k + dk + 0.5, ctr, s.sphereRadius, s.sphereEps);
+            const double z0 = dim == 3 ? k + 0.5 : ctr[2], z1 = dim == 3 ? k + dk + 0.5 : ctr[2];
+            const double a = sphere_eps(i + 0.5, j + 0.5, z0, ctr, s.sphereRadius, s.sphereEps);
+            const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, z1, ctr, s.sphereRadius, s.sphereEps);
             host[((size_t)li * q.n[1] + lj) * q.n[2] + lk] = (T)(cb * 2.0 / (a + b));
           }
       q.C[c].alloc(n);
       HIP_OK(hipMemcpy(q.C[c].p, host.data(), n * sizeof(T), hipMemcpyHostToDevice));
+    }
+    if (dim == 2) {
+      std::fill(host.begin(), host.end(), (T)db);
+      for (int c = 3; c < 6; ++c) {
+        q.C[c].alloc(n);
+        HIP_OK(hipMemcpy(q.C[c].p, host.data(), n * sizeof(T), hipMemcpyHostToDevice));
+      }
     }
   }
 }
@@ -533,7 +561,8 @@ void MultiRun<T>::setup_amp(XRank<T>& q) {
     for (int a = 0; a < 3; ++a) {
       int lo = glo[a], hi = ghi[a];
       const int right = N[a] - left[a];
-      if (left[a] != right) {
+      const bool act = std::find(active.begin(), active.end(), a) != active.end();
+      if (act && left[a] != right) {
         lo = std::max(lo, (int)std::ceil(left[a] - kMinFP[c][a]));
         hi = std::min(hi, (int)std::ceil(right - kMinFP[c][a]));
       }
@@ -543,10 +572,10 @@ void MultiRun<T>::setup_amp(XRank<T>& q) {
       b[a] = lo - q.g0[a];
       b[3 + a] = hi - q.g0[a];
     }
-    if (empty)
+    if (empty || !present[c])
       for (int e = 0; e < 6; ++e) b[e] = 0;
   }
-  amp_line = point_src;
+  amp_line = point_src && dim == 3;  // (2D: the point source stays)
   if (!amp_line) return;
   const int k0 = s.doUsePML ? s.pmlSizeZ : 0;
   amp_line = N[2] - 2 * k0 > 0;
@@ -575,6 +604,14 @@ std::vector<std::pair<void*, size_t>> MultiRun<T>::rank_state(XRank<T>& q) {
   }
   if (q.cp)
     for (auto* d : q.cp->keep) v.push_back({d->p, d->n * sizeof(T)});
+  if (q.p2) {
+    for (const Slab2d<T>& sl : q.p2->slabs)
+      v.push_back({sl.psi, (size_t)(sl.pbox[3] - sl.pbox[0]) * (sl.pbox[4] - sl.pbox[1]) * (sl.pbox[5] - sl.pbox[2]) *
+                               sizeof(T)});
+    for (int c = 0; c < 6; ++c)
+      for (int l = 0; l < 2; ++l)
+        if (q.p2->D[c][l]) v.push_back({q.p2->D[c][l], q.cells() * sizeof(T)});
+  }
   if (q.up)
     for (int c = 0; c < 6; ++c) {
       for (const auto& lv : q.up->D[c])
@@ -706,22 +743,51 @@ bool MultiRun<T>::setup_physics(int r) {
       q.own36[6 * c + 3 + a] = empty ? 0 : gb36[6 * c + 3 + a] - q.g0[a];
     }
   }
-  if (cpml) {
-    q.cp.reset(new NativeCpml<T>());
-    setup_cpml(*q.cp, s, N, active, dt, s.gridStep, own, q.g0, q.n);
+  if (dim == 2) {
+    q.p2.reset(new Pml2d<T>());
+    if (cpml) setup_cpml2d(*q.p2, s, N, active, present, dt, s.gridStep, own, q.g0, q.n);
+    if (upml) {
+      // per-cell 1 / (eps eps0) of a dielectric scene (E components), as native_run.h setup_absorbers
+      std::vector<T> inv[3];
+      if (percell) {
+        const double ctr[3] = {s.sphereCenterX, s.sphereCenterY, s.sphereCenterZ};
+        for (int c = 0; c < 3; ++c) {
+          if (!present[c]) continue;
+          inv[c].resize(q.cells());
+          const int di = c == 0, dj = c == 1;
+          for (int li = 0; li < q.n[0]; ++li)
+            for (int lj = 0; lj < q.n[1]; ++lj) {
+              const int i = q.g0[0] + li, j = q.g0[1] + lj;
+              const double a = sphere_eps(i + 0.5, j + 0.5, ctr[2], ctr, s.sphereRadius, s.sphereEps);
+              const double b = sphere_eps(i + di + 0.5, j + dj + 0.5, ctr[2], ctr, s.sphereRadius, s.sphereEps);
+              inv[c][(size_t)li * q.n[1] + lj] = (T)(1.0 / ((a + b) / 2.0 * kEps0));
+            }
+        }
+      }
+      setup_upml2d(*q.p2, s, N, present, dt, s.gridStep, inv, q.g0, q.n);
+    }
+    const fdtd::Int3 ext = {q.n[0], q.n[1], q.n[2]};
+    q.ld.reset(new Lowdim2d<T>(s, q.F, q.C, q.own36, ext, present, *q.p2, scheme == "tmz", percell, cb, db, q.st, &N,
+                               q.g0));
+  } else {
+    if (cpml) {
+      q.cp.reset(new NativeCpml<T>());
+      setup_cpml(*q.cp, s, N, active, dt, s.gridStep, own, q.g0, q.n);
+    }
+    if (upml) setup_chain(q);
   }
-  if (upml) setup_chain(q);
   if (tfsf) {
     q.tf.reset(new NativeTfsf<T>());
-    const bool present[6] = {true, true, true, true, true, true};
-    // (E: per-cell arrays of the sphere or the scalar; H: always the scalar db, mu = 1)
-    if (!setup_tfsf(*q.tf, s, N, gb36, q.C, percell ? 1.0 : cb, db, dt, s.gridStep, freq, 3, present, q.g0, q.n))
+    // (E: per-cell arrays of the sphere or the scalar; H: the scalar db, mu = 1 -- 2D: db arrays)
+    if (!setup_tfsf(*q.tf, s, N, gb36, q.C, percell ? 1.0 : cb, dim == 2 && percell ? 1.0 : db, dt, s.gridStep, freq,
+                    dim, present, q.g0, q.n))
       return false;
   }
   if (amp) setup_amp(q);
   bool has = point_src;
   for (int a = 0; a < 3; ++a) has = has && sp[a] >= q.lo[a] && sp[a] < q.hi[a];
   q.src_off = has ? ((long long)(sp[0] - q.g0[0]) * q.n[1] + (sp[1] - q.g0[1])) * q.n[2] + (sp[2] - q.g0[2]) : -1;
+  if (dim == 2 && !present[2] && src_comp == 2) q.src_off = -1;
   return true;
 }
 
@@ -742,7 +808,16 @@ void MultiRun<T>::phys_half(XRank<T>& q, int kind, double sv) {
       K_OK(inc_h(tf.einc.p, tf.hinc.p, tf.nline, tf.ch, q.st));
   }
   const int* bx = q.own36 + 18 * kind;
-  if (upml) {
+  if (dim == 2) {
+    // native_run.h step2d: the plain 2D kernels (or the UPML chain on the
+    // strips + the plain kernels inside), then the CPML corrections
+    const IBox all = {{0, 0, 0}, {q.n[0], q.n[1], q.n[2]}};
+    if (upml)
+      q.ld->upml(kind);
+    else
+      q.ld->plain(kind, all);
+    if (cpml) q.ld->cpml(kind);
+  } else if (upml) {
     // the chain on the rank's part of the PML slabs and the dispersive box,
     // the plain update on the rest (native_run.h upml_regions)
     using ChainFn = int (*)(const void* const*, const double*, const int*, int, int, int, int, void*);
@@ -787,7 +862,7 @@ void MultiRun<T>::phys_half(XRank<T>& q, int kind, double sv) {
     if (amp_on && amp_line) {  // the amplitude phase's Ez z line replaces the point source
       if (q.line_n > 0) K_OK(setvs(F[2], q.LINE.p, q.line_n, sv, q.st));
     } else if (q.src_off >= 0) {
-      K_OK(setv(F[2], q.src_off, sv, q.st));
+      K_OK(setv(F[src_comp], q.src_off, sv, q.st));
     }
   }
 }
@@ -866,8 +941,11 @@ void MultiRun<T>::report(double sec, int t_end, int steps, int warm) const {
   const double cells = (double)N[0] * N[1] * N[2];
   const int timed = steps - warm + amp_taken;
   std::printf("Total time = %f seconds\n", sec);
-  std::printf("Dimension: 3\n");
-  std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);
+  std::printf("Dimension: %d\n", dim);
+  if (dim == 3)
+    std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);
+  else
+    std::printf("Grid size: %dx%d\n", N[0], N[1]);
   std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", t_end, timed, warm);
   std::printf("Value type: %s\n", Api<T>::name);
   std::printf("\n-------- Details --------\n");
@@ -884,7 +962,7 @@ void MultiRun<T>::report(double sec, int t_end, int steps, int warm) const {
     std::printf("Backend: native HIP, split half-step kernels (%s%s%s), face ghosts (%d x / %d y / %d z cells) by "
                 "packed peer copies after every half step\n",
                 cpml ? "CPML" : (upml ? (s.doUseMetamaterials ? "UPML D/B chain + dispersive sphere" : "UPML D/B chain")
-                                      : ""),
+                                      : (tfsf ? "" : (dim == 2 ? "2D" : "plain"))),
                 (cpml || upml) && tfsf ? " + " : "", tfsf ? "TF/SF" : "", gd[0], gd[1], gd[2]);
   else
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), 26-neighbour ghost boxes by "
@@ -998,8 +1076,7 @@ void MultiRun<T>::run_ckpt(int t, int n) {
     if (t % Pc == 0) {
       sync_all();
       const auto c0 = std::chrono::steady_clock::now();
-      const bool present[6] = {true, true, true, true, true, true};
-      if (!ckpt_save<T>(s, "3d", N, present, [this](int c, std::vector<T>& host) { gather(c, host); }, t,
+      if (!ckpt_save<T>(s, scheme, N, present, [this](int c, std::vector<T>& host) { gather(c, host); }, t,
                         s.gridStep, dt)) {
         std::fprintf(stderr, "fdtd3d: cannot write the checkpoint to %s\n", s.checkpointDir.c_str());
         std::exit(1);
@@ -1014,8 +1091,7 @@ void MultiRun<T>::run_ckpt(int t, int n) {
 template <typename T>
 bool MultiRun<T>::save_results(int steps) {
   if (!s.checkpointDir.empty()) {
-    const bool present[6] = {true, true, true, true, true, true};
-    if (!ckpt_save<T>(s, "3d", N, present, [this](int c, std::vector<T>& host) { gather(c, host); }, steps,
+    if (!ckpt_save<T>(s, scheme, N, present, [this](int c, std::vector<T>& host) { gather(c, host); }, steps,
                       s.gridStep, dt)) {
       std::fprintf(stderr, "fdtd3d: cannot write the checkpoint to %s\n", s.checkpointDir.c_str());
       return false;
@@ -1025,15 +1101,17 @@ bool MultiRun<T>::save_results(int steps) {
   const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
   std::vector<T> host;
   for (int c = 0; c < 6; ++c) {
+    if (!present[c]) continue;
     gather(c, host);
     const std::string base = fdtd::grid_file_name(steps, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
     if (s.saveAsDAT) fdtd::write_dat(base + ".dat", host.data(), host.size() * sizeof(T));
     if (s.saveAsBMP || !s.saveAsDAT) {
-      const int kz = N[2] / 2;
+      const int kz = dim == 3 ? N[2] / 2 : 0;
       std::vector<double> v((size_t)N[0] * N[1]);
       for (int i = 0; i < N[0]; ++i)
         for (int j = 0; j < N[1]; ++j) v[(size_t)i * N[1] + j] = host[((size_t)i * N[1] + j) * N[2] + kz];
-      fdtd::write_bmp(base + std::to_string(kz) + "-Re.bmp", v, N[0], N[1], s.dumperPalette);
+      fdtd::write_bmp(dim == 3 ? base + std::to_string(kz) + "-Re.bmp" : base + "-Re.bmp", v, N[0], N[1],
+                      s.dumperPalette);
     }
   }
   return true;
@@ -1056,6 +1134,8 @@ void MultiRun<T>::release() {
     q.cp.reset();
     q.tf.reset();
     q.up.reset();
+    q.ld.reset();
+    q.p2.reset();
     q.AMP.reset();
     q.CNT.reset();
     q.LINE.reset();
@@ -1085,8 +1165,8 @@ int MultiRun<T>::main() {
   // decomposed native run's gathered one) scattered over the ranks
   int t0 = 0;
   if (!s.loadFromFile.empty()) {
-    const bool present[6] = {true, true, true, true, true, true};
-    const long got = ckpt_load<T>(s, "3d", N, present, [this](int c, const std::vector<T>& host) { scatter(c, host); });
+    const long got =
+        ckpt_load<T>(s, scheme, N, present, [this](int c, const std::vector<T>& host) { scatter(c, host); });
     if (got < 0) return 1;
     t0 = (int)got;
   }

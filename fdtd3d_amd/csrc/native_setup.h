@@ -289,9 +289,17 @@ struct Pml2d {
   }
 };
 
+// (decomposed runs: `own` = the rank's owned cells in global indices, `org` /
+// `ext` = its allocated box's origin and extents; slabs and psi in the rank's
+// array indices, profiles at the global positions)
 template <typename T>
 void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, const std::vector<int>& active,
-                  const bool* present, double dt, double dx) {
+                  const bool* present, double dt, double dx, const int* own = nullptr, const int* org = nullptr,
+                  const int* ext = nullptr) {
+  const int o0[3] = {0, 0, 0};
+  const int n0[3] = {N[0], N[1], N[2]};
+  if (!org) org = o0;
+  if (!ext) ext = n0;
   const int Ps[3] = {s.pmlSizeX, s.pmlSizeY, 0};
   const double eta = std::sqrt(kMu0 / kEps0);
   const double kmax = s.cpmlKappaMax, amax = s.cpmlAlphaMax;
@@ -299,6 +307,11 @@ void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, con
     if (!present[c]) continue;
     fdtd::Int3 glo, ghi;
     fdtd::global_range(c, N, active, glo, ghi);
+    if (own)
+      for (int a = 0; a < 3; ++a) {
+        glo[a] = std::max(glo[a], own[a]);
+        ghi[a] = std::min(ghi[a], own[3 + a]);
+      }
     for (int t = 0; t < 2; ++t) {
       const int src = kCurl[c][t][0], axis = kCurl[c][t][1], sign = kCurl[c][t][2];
       if (!present[src] || axis >= 2 || Ps[axis] <= 0) continue;
@@ -315,9 +328,10 @@ void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, con
         for (int d = 0; d < 3; ++d) empty = empty || ghi[d] <= glo[d];
         if (empty) continue;
         // profiles over the whole axis with this side's clamped depth (models/cpml.py)
-        std::vector<T> b(n), cv(n), kk(n);
-        for (int v = 0; v < n; ++v) {
-          const double idx = v + m;
+        const int ne = ext[axis];
+        std::vector<T> b(ne), cv(ne), kk(ne);
+        for (int v = 0; v < ne; ++v) {
+          const double idx = v + org[axis] + m;
           double depth = side == 0 ? (Pa - idx) / Pa : (idx - (n - Pa)) / Pa;
           depth = std::min(1.0, std::max(0.0, depth));
           const double d4 = depth * depth * depth * depth;
@@ -335,10 +349,10 @@ void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, con
         sl.sign = sign;
         size_t vol = 1;
         for (int d = 0; d < 3; ++d) {
-          sl.box[d] = d == axis ? lo : glo[d];
-          sl.box[3 + d] = d == axis ? hi : ghi[d];
-          sl.pbox[d] = d == axis ? lo : 0;
-          sl.pbox[3 + d] = d == axis ? hi : N[d];
+          sl.box[d] = (d == axis ? lo : glo[d]) - org[d];
+          sl.box[3 + d] = (d == axis ? hi : ghi[d]) - org[d];
+          sl.pbox[d] = d == axis ? lo - org[d] : 0;
+          sl.pbox[3 + d] = d == axis ? hi - org[d] : ext[d];
           vol *= (size_t)(sl.pbox[3 + d] - sl.pbox[d]);
         }
         sl.psi = native_phys::dev_zeros<T>(vol, P.keep);
@@ -353,10 +367,16 @@ void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, con
 
 // 2D UPML coefficients; ``cell_inv`` (optional, per present E component):
 // 1 / (eps eps0) per cell of a dielectric scene
+// (decomposed runs: the rank's arrays at global origin `org`, extents `ext`,
+// the profiles at the global positions; `cell_inv` over the rank's cells)
 template <typename T>
 void setup_upml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, const bool* present, double dt,
-                  double dx, std::vector<T>* cell_inv) {
-  const size_t cells = (size_t)N[0] * N[1] * N[2];
+                  double dx, std::vector<T>* cell_inv, const int* org = nullptr, const int* ext = nullptr) {
+  const int o0[3] = {0, 0, 0};
+  const int n0[3] = {N[0], N[1], N[2]};
+  if (!org) org = o0;
+  if (!ext) ext = n0;
+  const size_t cells = (size_t)ext[0] * ext[1] * ext[2];
   std::vector<double> sig[3];
   const int pml[3] = {s.pmlSizeX, s.pmlSizeY, 0};
   for (int a = 0; a < 3; ++a) sig[a] = native_phys::sigma_profile(N[a] + 1, pml[a], dx);
@@ -364,26 +384,27 @@ void setup_upml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, con
     if (!present[c]) continue;
     const int aD = native_phys::kUpmlAxes[c][0], aA = native_phys::kUpmlAxes[c][1], aB = native_phys::kUpmlAxes[c][2];
     auto avg = [&](int a) {
-      std::vector<double> out(N[a]);
+      std::vector<double> out(ext[a]);
       double v[4];
-      for (int n = 0; n < N[a]; ++n) {
-        for (int p = 0; p < native_phys::kStencilN[c]; ++p) v[p] = sig[a][n + native_phys::kStencil[c][p][a]];
+      for (int n = 0; n < ext[a]; ++n) {
+        for (int p = 0; p < native_phys::kStencilN[c]; ++p)
+          v[p] = sig[a][org[a] + n + native_phys::kStencil[c][p][a]];
         out[n] = native_phys::approx_mean(v, native_phys::kStencilN[c]);
       }
       return out;
     };
     const std::vector<double> sD = avg(aD), sA = avg(aA), sB = avg(aB);
     const double two = 2 * kEps0;
-    std::vector<T> caD(N[aD]), cbD(N[aD]), caE(N[aA]), ica(N[aA]), cbEa(N[aB]), ccEa(N[aB]);
-    for (int n = 0; n < N[aD]; ++n) {
+    std::vector<T> caD(ext[aD]), cbD(ext[aD]), caE(ext[aA]), ica(ext[aA]), cbEa(ext[aB]), ccEa(ext[aB]);
+    for (int n = 0; n < ext[aD]; ++n) {
       caD[n] = (T)((two - sD[n] * dt) / (two + sD[n] * dt));
       cbD[n] = (T)((two * dt / dx) / (two + sD[n] * dt));
     }
-    for (int n = 0; n < N[aA]; ++n) {
+    for (int n = 0; n < ext[aA]; ++n) {
       caE[n] = (T)((two - sA[n] * dt) / (two + sA[n] * dt));
       ica[n] = (T)(1.0 / (two + sA[n] * dt));
     }
-    for (int n = 0; n < N[aB]; ++n) {
+    for (int n = 0; n < ext[aB]; ++n) {
       cbEa[n] = (T)(two + sB[n] * dt);
       ccEa[n] = (T)(-(two - sB[n] * dt));
     }
@@ -605,12 +626,12 @@ bool native_supported(const fdtd::Settings& s) {
   const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
   // amplitude mode: any scheme, not with the NTFF diagram
   const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
-  // parallel grids: 3D, any rank grid -- plain media on blocked passes; CPML, the UPML, Drude / Lorentz spheres
+  // parallel grids: 3D (any rank grid) / 2D (x / y) -- 3D plain media on blocked passes; CPML, the UPML, Drude / Lorentz spheres
   // and TF/SF (point source optional) on the split half steps, the NTFF diagram from the gathered grid
   // (native_multi.h), amplitude mode on the split half steps
   const bool par_phys = s.doUsePML || s.doUseTFSF || s.doUseMetamaterials;
   const bool par_ok = !s.doUseParallelGrid ||
-                      (s.dimension == 3 &&
+                      (s.dimension >= 2 &&
                        (s.scene == "vacuum" || s.scene == "sphere" || s.scene == "drude-sphere") &&
                        (par_phys || s.doUseMetamaterials || !s.doUseSplitKernels));
   // checkpoints / resume: plain media (state = the field components)

@@ -285,6 +285,7 @@ AMP_MULTI = {
     "amp_2x2x1": (CASES["3d_amp"], ["--topology-sizex", "2", "--topology-sizey", "2"]),
     "amp_cpml_2x1x2": (CASES["3d_amp_cpml"], ["--topology-sizex", "2", "--topology-sizez", "2"]),
     # until the stable state (the near-convergence snapshot and the redone period over the ranks)
+    "amp_2d_tmz_cpml_2x2": (CASES["2d_tmz_amp_cpml"], ["--topology-sizex", "2", "--topology-sizey", "2"]),
     # (the single-rank run: stable after 1015 steps)
     "amp_cpml_stable_2x2x1": (["--3d", "--sizex", "20", "--same-size", "--time-steps", "5", "--scene", "vacuum",
                                "--use-amp-mode", "--amplitude-time-steps", "1200", "--use-pml", "--pml-type", "cpml",
@@ -315,10 +316,10 @@ def test_native_parallel_grid_amplitude(case, tmp_path):
     steps += int(line.split("after ")[1].split()[0]) if "not reached" in line else int(line.split("(")[1].split()[0])
     if case.endswith("stable_2x2x1"):
         assert "stable after" in line, line
-    shape, _ = _shape(argv)
+    shape, scheme = _shape(argv)
     for kind in "EH":
         errs, peak = [], 0.0
-        for c in "xyz":
+        for c in [c[1] for c in COMPS[scheme] if c[0] == kind]:
             name = "current[%d]_rank-0_%s%s.dat" % (steps, kind, c)
             a = np.fromfile(tmp_path / "par" / name, dtype=np.float64).reshape(shape)
             b = np.fromfile(tmp_path / "one" / name, dtype=np.float64).reshape(shape)
@@ -413,6 +414,20 @@ MULTI = {
                                     "--sphere-radius", "6", "--use-tfsf", "--tfsf-sizex", "9", "--same-size-tfsf",
                                     "--parallel-grid", "--topology-sizey", "2", "--topology-sizez", "2",
                                     "--dtype", "f64"],
+    # 2D schemes over x / y rank grids (the 2D kernels, CPML slabs / UPML strips per rank)
+    "f64_tmz_upml_tfsf_2x2": ["--2d", "--sizex", "60", "--sizey", "52", "--time-steps", "23", "--scene", "vacuum",
+                              "--use-pml", "--pml-sizex", "6", "--pml-sizey", "5", "--use-tfsf", "--tfsf-sizex",
+                              "10", "--tfsf-sizey", "9", "--angle-phi", "30", "--parallel-grid", "--topology-sizex",
+                              "2", "--topology-sizey", "2", "--dtype", "f64"],
+    "f32_tez_cpml_sphere_2x1": ["--2d", "--2d-mode", "tez", "--sizex", "56", "--sizey", "60", "--time-steps", "23",
+                                "--scene", "sphere", "--sphere-center-x", "28", "--sphere-center-y", "30",
+                                "--sphere-radius", "6", "--sphere-eps", "4", "--use-pml", "--pml-type", "cpml",
+                                "--pml-sizex", "5", "--pml-sizey", "6", "--cpml-kappa-max", "2", "--cpml-alpha-max",
+                                "0.05", "--parallel-grid", "--topology-sizex", "2", "--dtype", "f32"],
+    "f64_tmz_upml_sphere_1x3": ["--2d", "--sizex", "64", "--sizey", "66", "--time-steps", "23", "--scene", "sphere",
+                                "--sphere-center-x", "30", "--sphere-center-y", "33", "--sphere-radius", "7",
+                                "--sphere-eps", "3", "--use-pml", "--pml-sizex", "5", "--pml-sizey", "6",
+                                "--parallel-grid", "--topology-sizey", "3", "--dtype", "f64"],
 }
 
 
@@ -444,11 +459,11 @@ def test_native_parallel_grid_matches_python(case, tmp_path, gpu):
     serial = serial[:i] + serial[i + 2:]
     assert py_run(serial + ["--dtype", "f64", "--backend", "torch", "--device", "cpu", "--output-dir", str(pd)],
                   out=io.StringIO()) == 0
-    shape, _ = _shape(argv)
+    shape, scheme = _shape(argv)
     ndt = np.float32 if dtype == "f32" else np.float64
     for kind in "EH":
         errs = []
-        for c in ("x", "y", "z"):
+        for c in [c[1] for c in COMPS[scheme] if c[0] == kind]:
             name = "current[23]_rank-0_%s%s.dat" % (kind, c)
             a = np.fromfile(nd / name, dtype=ndt).astype(np.float64).reshape(shape)
             b = np.fromfile(pd / name, dtype=np.float64).reshape(shape)
