@@ -15,7 +15,7 @@
 // amplitude kernel after each step otherwise), checkpoints / resume of
 // plain-media runs in the Python driver's format (--checkpoint-dir,
 // --load-from-file) and --parallel-grid decompositions (any x / y / z rank
-// grid) over the node's GPUs from one process (run_multi): plain media on
+// grid; 2D x / y, 1D x) over the node's GPUs from one process (run_multi): 3D plain media on
 // blocked passes; CPML, the UPML, Drude / Lorentz spheres, TF/SF and
 // amplitude mode on the split half steps; the NTFF diagram and plain-media
 // checkpoints from the gathered grid.  Complex fields go through the Python
@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr,
                  "fdtd3d (native): CPML in 3D outside whole 4-cell z rows, PML / TF/SF in 1D, TF/SF boxes reaching "
                  "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "
-                 "grids beyond 3D, checkpoints beyond plain media, and complex "
+                 "grids with NTFF in 2D, checkpoints beyond plain media, and complex "
                  "fields run through the Python driver: python -m fdtd3d_amd <same options>\n");
     return 2;
   }

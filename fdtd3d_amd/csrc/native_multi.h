@@ -163,8 +163,13 @@ class MultiRun {
 template <typename T>
 int MultiRun<T>::plan_ranks() {
   dim = s.dimension;
-  scheme = dim == 3 ? "3d" : s.mode2D;
-  N = {s.sizeX, s.sizeY, dim == 3 ? s.sizeZ : 1};
+  scheme = dim == 3 ? "3d" : (dim == 2 ? s.mode2D : "1d");
+  N = {s.sizeX, dim >= 2 ? s.sizeY : 1, dim == 3 ? s.sizeZ : 1};
+  if (dim == 1) {
+    // Ez / Hy on x slabs
+    active = {0};
+    for (int c = 0; c < 6; ++c) present[c] = c == 2 || c == 4;
+  }
   if (dim == 2) {
     // TMz (Ez Hx Hy) / TEz (Ex Ey Hz) on an x / y rank grid
     active = {0, 1};
@@ -182,6 +187,7 @@ int MultiRun<T>::plan_ranks() {
   HIP_OK(hipGetDeviceCount(&ndev));
   Pd[0] = std::max(1, s.topologySizeX);
   Pd[1] = std::max(1, s.topologySizeY);
+  Pd[1] = dim >= 2 ? Pd[1] : 1;
   Pd[2] = dim == 3 ? std::max(1, s.topologySizeZ) : 1;
   if (Pd[0] * Pd[1] * Pd[2] == 1) Pd[0] = ndev;
   P = Pd[0] * Pd[1] * Pd[2];
@@ -189,7 +195,7 @@ int MultiRun<T>::plan_ranks() {
   cpml = s.doUsePML && !upml;
   tfsf = s.doUseTFSF;
   amp = s.doUseAmplitudeMode;
-  phys = cpml || upml || tfsf || amp || dim == 2;  // (2D: the split half steps always)
+  phys = cpml || upml || tfsf || amp || dim < 3;  // (1D / 2D: the split half steps always)
   ntff = s.doUseNTFF && dim == 3;
   point_src = !tfsf || s.doUsePointSource;
   const int T_max = sizeof(T) == 4 ? fdtd_tb_max_steps() : fdtd_tb64_max_steps();
@@ -225,6 +231,7 @@ int MultiRun<T>::plan_ranks() {
   }
   sp = {N[0] / 2, N[1] / 2, N[2] / 2};
   if (scheme == "tmz") sp = {N[0] > 140 ? 70 : N[0] / 2, N[1] / 2, 0};  // (SchemeTMz.cpp:1345)
+  if (dim == 1) sp = {N[0] / 2, 0, 0};
   return 0;
 }
 
@@ -311,7 +318,7 @@ void MultiRun<T>::setup_rank(int r) {
       q.C[c].alloc(n);
       HIP_OK(hipMemcpy(q.C[c].p, host.data(), n * sizeof(T), hipMemcpyHostToDevice));
     }
-    if (dim == 2) {
+    if (dim < 3) {
       std::fill(host.begin(), host.end(), (T)db);
       for (int c = 3; c < 6; ++c) {
         q.C[c].alloc(n);
@@ -808,7 +815,13 @@ void MultiRun<T>::phys_half(XRank<T>& q, int kind, double sv) {
       K_OK(inc_h(tf.einc.p, tf.hinc.p, tf.nline, tf.ch, q.st));
   }
   const int* bx = q.own36 + 18 * kind;
-  if (dim == 2) {
+  if (dim == 1) {
+    // native_run.h step: the 1D Ez / Hy kernels over the owned x range
+    if (kind == 0)
+      K_OK(e1d(F[2], F[4], C[2], percell ? 1.0 : cb, q.own36[12], q.own36[15], q.st));
+    else
+      K_OK(h1d(F[4], F[2], q.C[4].p, percell ? 1.0 : db, q.own36[24], q.own36[27], q.st));
+  } else if (dim == 2) {
     // native_run.h step2d: the plain 2D kernels (or the UPML chain on the
     // strips + the plain kernels inside), then the CPML corrections
     const IBox all = {{0, 0, 0}, {q.n[0], q.n[1], q.n[2]}};
@@ -944,8 +957,10 @@ void MultiRun<T>::report(double sec, int t_end, int steps, int warm) const {
   std::printf("Dimension: %d\n", dim);
   if (dim == 3)
     std::printf("Grid size: %dx%dx%d\n", N[0], N[1], N[2]);
-  else
+  else if (dim == 2)
     std::printf("Grid size: %dx%d\n", N[0], N[1]);
+  else
+    std::printf("Grid size: %d\n", N[0]);
   std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", t_end, timed, warm);
   std::printf("Value type: %s\n", Api<T>::name);
   std::printf("\n-------- Details --------\n");
@@ -962,7 +977,7 @@ void MultiRun<T>::report(double sec, int t_end, int steps, int warm) const {
     std::printf("Backend: native HIP, split half-step kernels (%s%s%s), face ghosts (%d x / %d y / %d z cells) by "
                 "packed peer copies after every half step\n",
                 cpml ? "CPML" : (upml ? (s.doUseMetamaterials ? "UPML D/B chain + dispersive sphere" : "UPML D/B chain")
-                                      : (tfsf ? "" : (dim == 2 ? "2D" : "plain"))),
+                                      : (tfsf ? "" : (dim == 3 ? "plain" : (dim == 2 ? "2D" : "1D")))),
                 (cpml || upml) && tfsf ? " + " : "", tfsf ? "TF/SF" : "", gd[0], gd[1], gd[2]);
   else
     std::printf("Backend: native HIP, temporally blocked kernel (%d steps per pass), 26-neighbour ghost boxes by "

@@ -626,12 +626,12 @@ bool native_supported(const fdtd::Settings& s) {
   const bool ntff_ok = !s.doUseNTFF || s.dimension == 3;
   // amplitude mode: any scheme, not with the NTFF diagram
   const bool amp_ok = !s.doUseAmplitudeMode || !s.doUseNTFF;
-  // parallel grids: 3D (any rank grid) / 2D (x / y) -- 3D plain media on blocked passes; CPML, the UPML, Drude / Lorentz spheres
+  // parallel grids: 3D (any rank grid) / 2D (x / y) / 1D (x) -- 3D plain media on blocked passes; CPML, the UPML, Drude / Lorentz spheres
   // and TF/SF (point source optional) on the split half steps, the NTFF diagram from the gathered grid
   // (native_multi.h), amplitude mode on the split half steps
   const bool par_phys = s.doUsePML || s.doUseTFSF || s.doUseMetamaterials;
   const bool par_ok = !s.doUseParallelGrid ||
-                      (s.dimension >= 2 &&
+                      (s.dimension >= 1 &&
                        (s.scene == "vacuum" || s.scene == "sphere" || s.scene == "drude-sphere") &&
                        (par_phys || s.doUseMetamaterials || !s.doUseSplitKernels));
   // checkpoints / resume: plain media (state = the field components)

@@ -428,6 +428,13 @@ MULTI = {
                                 "--sphere-center-x", "30", "--sphere-center-y", "33", "--sphere-radius", "7",
                                 "--sphere-eps", "3", "--use-pml", "--pml-sizex", "5", "--pml-sizey", "6",
                                 "--parallel-grid", "--topology-sizey", "3", "--dtype", "f64"],
+    # 1D: x slabs (the Ez / Hy kernels per rank)
+    "f64_1d_x3": ["--1d", "--sizex", "300", "--time-steps", "40", "--scene", "vacuum", "--source", "gaussian",
+                  "--gaussian-width", "8", "--gaussian-delay", "30", "--parallel-grid", "--topology-sizex", "3",
+                  "--dtype", "f64"],
+    "f32_1d_sphere_x4": ["--1d", "--sizex", "320", "--time-steps", "40", "--scene", "sphere", "--sphere-center-x",
+                         "150", "--sphere-radius", "30", "--sphere-eps", "4", "--parallel-grid", "--topology-sizex",
+                         "4", "--dtype", "f32"],
 }
 
 
@@ -442,7 +449,7 @@ def test_native_parallel_grid_matches_python(case, tmp_path, gpu):
     r = subprocess.run([exe] + argv + ["--output-dir", str(nd)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Parallel grid: 1" in r.stdout, r.stdout
-    if "--use-pml" in argv or "--use-tfsf" in argv or "--use-metamaterials" in argv:
+    if any(f in argv for f in ("--use-pml", "--use-tfsf", "--use-metamaterials", "--1d", "--2d")):
         assert "split half-step kernels" in r.stdout and "face ghosts" in r.stdout, r.stdout
     else:
         assert "26-neighbour ghost boxes" in r.stdout, r.stdout
@@ -460,11 +467,12 @@ def test_native_parallel_grid_matches_python(case, tmp_path, gpu):
     assert py_run(serial + ["--dtype", "f64", "--backend", "torch", "--device", "cpu", "--output-dir", str(pd)],
                   out=io.StringIO()) == 0
     shape, scheme = _shape(argv)
+    steps = int(argv[argv.index("--time-steps") + 1])
     ndt = np.float32 if dtype == "f32" else np.float64
     for kind in "EH":
         errs = []
         for c in [c[1] for c in COMPS[scheme] if c[0] == kind]:
-            name = "current[23]_rank-0_%s%s.dat" % (kind, c)
+            name = "current[%d]_rank-0_%s%s.dat" % (steps, kind, c)
             a = np.fromfile(nd / name, dtype=ndt).astype(np.float64).reshape(shape)
             b = np.fromfile(pd / name, dtype=np.float64).reshape(shape)
             errs.append((np.abs(a - b).max(), np.abs(b).max()))
