@@ -580,6 +580,12 @@ class BlockedStepping:
         size = cfg.size
         alloc = dom.allocated_global()
         core_tf = self._hybrid_core_tfsf(T)
+        # split: the x faces (every x-streaming tile of the core meets them) in
+        # the stepped shell, the y / z faces in the core, whose tiles clear of
+        # them run the plain kernel -- the TF/SF variant only on the core's
+        # y / z border slabs (serial runs)
+        split = (core_tf and getattr(cfg, "hybrid_tfsf", "auto") == "split" and self.halo is None
+                 and cfg.scheme == "3d")
         lo, hi = [0, 0, 0], list(size)
         act = [self.layout.active(a) for a in range(3)]  # 2D: z is one cell, never cut
         for a in range(3):
@@ -588,7 +594,7 @@ class BlockedStepping:
             edge = 0
             if cfg.use_pml:
                 edge = max(edge, self.layout.pml_size[a])
-            if cfg.use_tfsf and not core_tf:
+            if cfg.use_tfsf and (not core_tf or (split and a == 0)):
                 edge = max(edge, cfg.tfsf_size[a] + 1)
             if edge > 0:
                 lo[a], hi[a] = edge + m, size[a] - edge - m
@@ -687,6 +693,29 @@ class BlockedStepping:
                         if tb is not None and not box_empty(b) and not box_empty(box_intersect(dom.to_local(b), tb)):
                             self._tfsf_once = False
         upd = {c: self.local_box(c, alloc) for c in self.comps}
+        core_tfs = None
+        if split and D is None:
+            # inner boxes: no TF/SF target within T + 1 of their output (the
+            # plain kernel); the rest of the core (the y / z border slabs) takes
+            # the TF/SF variant
+            boxes, flags = [], []
+            for ob in couts:
+                ilo, ihi = list(ob[0]), list(ob[1])
+                for a in (1, 2):
+                    ilo[a] = max(ilo[a], cfg.tfsf_size[a] + T + 2)
+                    ihi[a] = min(ihi[a], size[a] - cfg.tfsf_size[a] - T - 2)
+                inner = (tuple(ilo), tuple(ihi))
+                if box_empty(inner) or self._tfsf_targets_in(dom.to_local(grow(inner, T + 1))):
+                    boxes, flags = None, None
+                    break
+                boxes.append(inner)
+                flags.append(False)
+                for b in box_subtract(ob, inner):
+                    if not box_empty(b):
+                        boxes.append(b)
+                        flags.append(True)
+            if boxes is not None:
+                couts, core_tfs = boxes, flags
         # the Drude pass may run next to the shell steps when its cone (the box grown by 2T, one more
         # cell for the staggering) meets no shell window (stepped in place in F) and no copy box
         dside = False
@@ -695,7 +724,8 @@ class BlockedStepping:
             dside = not any(not box_empty(box_intersect(cone, w)) for ws in shells for w in ws + copy_boxes)
         return {"T": T, "core": [dom.to_local(b) for b in couts], "shell": shells[0], "shells": shells,
                 "copy": [dom.to_local(b) for b in copy_boxes], "upd": upd, "core_cells": core_cells,
-                "cut_cells": box_volume(Dm) if Dm is not None else 0, "core_tfsf": core_tf, "drude": dblk,
+                "cut_cells": box_volume(Dm) if Dm is not None else 0, "core_tfsf": core_tf, "core_tfs": core_tfs,
+                "drude": dblk,
                 "drude_side": dside}
 
     def _tfsf_pass(self, p: int, T: int, level0: int = 0, dry: bool = False):
@@ -750,10 +780,12 @@ class BlockedStepping:
         tfs = ([self._tfsf_pass(p, T, dry=True) for p in range(self.planes)] if hp.get("core_tfsf")
                else [None] * self.planes)
 
+        flags = hp.get("core_tfs") if self.halo is None else None  # split: the TF/SF variant per core box
+
         def core(boxes):
             for p in range(self.planes):
-                for ob in boxes:
-                    if tfs[p] is not None:
+                for i, ob in enumerate(boxes):
+                    if tfs[p] is not None and (flags is None or flags[i]):
                         self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p], tfsf=tfs[p])
                     else:
                         self.ops.tb_step(self.F[p], self.F_alt[p], hp["upd"], ob, self.cb, T, srcs[p])

@@ -45,6 +45,12 @@ CASES = [
     ("cpml-tfsf-y-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0,
                               hybrid_tfsf="core"), 4, 11),
     ("cpml-tfsf-y", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0), 3, 11),
+    # split: the x faces in the shell, the y / z faces in the core (the TF/SF variant on its border slabs only)
+    ("cpml-tfsf-x-split", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, hybrid_tfsf="split"), 5,
+     13),
+    ("cpml-tfsf-y-split", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, phi=90.0, psi=30.0,
+                               hybrid_tfsf="split"), 4, 11),
+    ("upml-tfsf-x-split", dict(scene="vacuum", use_pml=True, use_tfsf=True, hybrid_tfsf="split"), 4, 12),
     # fp64: the TF/SF faces in the fp64 blocked core (yee3d_tb64.hip tf_fix; automatic in fp64), x and y
     # incidence, CPML and UPML shells
     ("cpml-tfsf-x-f64-core", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, dtype="f64"), 4,
@@ -104,6 +110,9 @@ def test_hybrid_gpu(gpu, name, extra, T, steps):
         assert getattr(hy, "_hgraph", None) is not None, "no graph replay"
     if name.endswith("-core"):
         assert hy.hybrid["core_tfsf"], "TF/SF faces not in the blocked core"
+    if name.endswith("-split"):
+        assert hy.hybrid["core_tfsf"] and hy.hybrid["core_tfs"], "no split core"
+        assert False in hy.hybrid["core_tfs"] and True in hy.hybrid["core_tfs"], hy.hybrid["core_tfs"]
     st = _run(dataclasses.replace(cfg, hybrid_block=1), "hip", gpu, dt)
     assert st.hybrid is None
     ref = _run(dataclasses.replace(cfg, hybrid_block=1, dtype="f64"), "torch", "cpu", torch.float64)
