@@ -18,9 +18,11 @@
 // grid; 2D x / y, 1D x) over the node's GPUs from one process (run_multi): 3D plain media on
 // blocked passes; CPML, the UPML, Drude / Lorentz spheres, TF/SF and
 // amplitude mode on the split half steps; the NTFF diagram and plain-media
-// checkpoints from the gathered grid.  Complex fields go through the Python
-// driver (python -m fdtd3d_amd), which shares the kernels; asking this binary
-// for them is an error, never a silent fallback.
+// checkpoints from the gathered grid.  Complex fields (one GPU) as two real
+// planes.  What this binary does not run (complex fields with amplitude mode,
+// NTFF, checkpoints or parallel grids) goes through the Python driver (python
+// -m fdtd3d_amd), which shares the kernels; asking this binary for it is an
+// error, never a silent fallback.
 #include <hip/hip_runtime.h>
 
 #include <dirent.h>
@@ -59,6 +61,17 @@ namespace {
 // one GPU: the stages of native_run.h (set-up, pass plans, the run loop, the report)
 template <typename T>
 int run(const fdtd::Settings& s) {
+  if (s.doUseComplexFieldValues) {
+    // complex fields (the reference's COMPLEX_FIELD_VALUES): the real and the
+    // imaginary plane step as two real runs with the sin / cos source
+    // (models/scheme.py planes); the rate counts both planes' time
+    NativeRun<T> re(s, 0), im(s, 1);
+    if (!re.prepare() || !im.prepare()) return 1;
+    re.run_timed();
+    im.run_timed();
+    re.report_run(im.seconds());
+    return re.save_complex(im) ? 0 : 1;
+  }
   NativeRun<T> r(s);
   return r.main();
 }
@@ -87,8 +100,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr,
                  "fdtd3d (native): CPML in 3D outside whole 4-cell z rows, PML / TF/SF in 1D, TF/SF boxes reaching "
                  "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "
-                 "grids with NTFF in 2D, checkpoints beyond plain media, and complex "
-                 "fields run through the Python driver: python -m fdtd3d_amd <same options>\n");
+                 "grids with NTFF in 2D, checkpoints beyond plain media, and complex fields with amplitude mode, "
+                 "NTFF, checkpoints or parallel grids run through the Python driver: python -m fdtd3d_amd <same options>\n");
     return 2;
   }
   int ndev = 0;

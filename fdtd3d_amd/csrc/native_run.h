@@ -19,16 +19,29 @@ namespace {
 template <typename T>
 class NativeRun {
  public:
-  explicit NativeRun(const fdtd::Settings& s_);
+  // plane: 0 = the real run, 1 = the imaginary part of a complex run (the
+  // cos / zero source; the update is real-linear, so the two parts step
+  // independently -- models/scheme.py planes)
+  explicit NativeRun(const fdtd::Settings& s_, int plane_ = 0);
   ~NativeRun();
   // set-up, warm-up, timed steps, report, outputs: the process exit status
   int main();
+  // the stages of main (a complex run drives two planes through them)
+  bool prepare();
+  void run_timed();
+  void report_run(double extra_sec = 0.0) const { report(sec_ + extra_sec, t_end_, steps_, warm_); }
+  double seconds() const { return sec_; }
+  int t_end() const { return t_end_; }
+  bool save_complex(const NativeRun<T>& im) const;
 
  private:
   using ChainFn = int (*)(const void* const*, const double*, const int*, int, int, int, int, void*);
 
   // ------------------------------------------------------------ configuration
   const fdtd::Settings& s;
+  int plane = 0;
+  int t0_ = 0, steps_ = 0, warm_ = 0, t_end_ = 0;
+  double sec_ = 0.0;
   int dim;
   std::string scheme;
   fdtd::Int3 N;
@@ -126,7 +139,7 @@ class NativeRun {
 // ============================================================== configuration
 
 template <typename T>
-NativeRun<T>::NativeRun(const fdtd::Settings& s_) : s(s_) {
+NativeRun<T>::NativeRun(const fdtd::Settings& s_, int plane_) : s(s_), plane(plane_) {
   dim = s.dimension;
   scheme = dim == 3 ? "3d" : (dim == 2 ? s.mode2D : "1d");
   N = {s.sizeX, dim >= 2 ? s.sizeY : 1, dim == 3 ? s.sizeZ : 1};
@@ -170,8 +183,10 @@ NativeRun<T>::~NativeRun() {
 
 template <typename T>
 double NativeRun<T>::src_val(int t) const {
-  if (s.sourceType == "gaussian") return std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2));
-  return std::sin(dt * t * 2 * kPi * freq);
+  // (complex runs: the imaginary plane takes the cos / zero source, models/scheme.py source_value)
+  if (s.sourceType == "gaussian")
+    return plane == 0 ? std::exp(-std::pow((t - s.gaussianDelay) / s.gaussianWidth, 2)) : 0.0;
+  return plane == 0 ? std::sin(dt * t * 2 * kPi * freq) : std::cos(dt * t * 2 * kPi * freq);
 }
 
 template <typename T>
@@ -1231,6 +1246,7 @@ void NativeRun<T>::report(double sec, int t_end, int steps, int warm) const {
   const int timed = steps - warm + ampm.taken;
   std::printf("Number of time steps: %d (%d timed after %d warm-up)\n\n", t_end, timed, warm);
   std::printf("Value type: %s\n", Api<T>::name);
+  if (s.doUseComplexFieldValues) std::printf("Complex field values: 1 (real and imaginary planes)\n");
   std::printf("\n-------- Details --------\n");
   std::printf("Parallel grid: 0\n");
   if (T2_h > 1)
@@ -1292,23 +1308,29 @@ bool NativeRun<T>::save_results(int t_end) {
 }
 
 template <typename T>
-int NativeRun<T>::main() {
+bool NativeRun<T>::prepare() {
   setup_fields();
   setup_absorbers();
   setup_chain_regions();
   plan_drude();
-  if (!setup_sources_and_modes()) return 1;
+  if (!setup_sources_and_modes()) return false;
   plan_blocking();
   setup_streams();
   // --load-from-file: the run continues from the checkpoint's step up to --time-steps
-  int t0 = 0;
+  t0_ = 0;
   if (!s.loadFromFile.empty()) {
     const long got = ckpt_load<T>(s, scheme, N, present, F);
-    if (got < 0) return 1;
-    t0 = (int)got;
+    if (got < 0) return false;
+    t0_ = (int)got;
   }
-  const int steps = std::max(0, s.numTimeSteps - t0);
-  const int warm = std::max(0, std::min(s.warmupSteps, steps));
+  steps_ = std::max(0, s.numTimeSteps - t0_);
+  warm_ = std::max(0, std::min(s.warmupSteps, steps_));
+  return true;
+}
+
+template <typename T>
+void NativeRun<T>::run_timed() {
+  const int t0 = t0_, steps = steps_, warm = warm_;
   run_ckpt(t0, warm);  // untimed (they advance the simulation)
   HIP_OK(hipStreamSynchronize(st));
   hipEvent_t e0, e1;
@@ -1335,9 +1357,54 @@ int NativeRun<T>::main() {
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));
   HIP_OK(hipEventDestroy(e0));
   HIP_OK(hipEventDestroy(e1));
-  const double sec = std::max(0.0, (ms - ckpt_ms) / 1e3);
-  report(sec, t_end, steps, warm);
-  return save_results(t_end) ? 0 : 1;
+  sec_ = std::max(0.0, (ms - ckpt_ms) / 1e3);
+  t_end_ = t_end;
+}
+
+template <typename T>
+int NativeRun<T>::main() {
+  if (!prepare()) return 1;
+  run_timed();
+  report_run();
+  return save_results(t_end_) ? 0 : 1;
+}
+
+// a complex run's outputs (this = the real plane): DAT files of interleaved
+// (real, imaginary) values -- the reference's std::complex<T> layout, as
+// io/dat.py writes them -- and -Re / -Im / -Mod images of the middle slice
+template <typename T>
+bool NativeRun<T>::save_complex(const NativeRun<T>& im) const {
+  if (!s.doSaveRes) return true;
+  const char* names[6] = {"Ex", "Ey", "Ez", "Hx", "Hy", "Hz"};
+  std::vector<T> re(cells), ip(cells), both(2 * cells);
+  for (int c = 0; c < 6; ++c) {
+    if (!present[c]) continue;
+    HIP_OK(hipMemcpy(re.data(), F[c].p, cells * sizeof(T), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(ip.data(), im.F[c].p, cells * sizeof(T), hipMemcpyDeviceToHost));
+    for (size_t q = 0; q < cells; ++q) {
+      both[2 * q] = re[q];
+      both[2 * q + 1] = ip[q];
+    }
+    const std::string base = fdtd::grid_file_name(t_end_, 0, names[c], s.outputDir == "." ? "" : s.outputDir);
+    if (s.saveAsDAT && !fdtd::write_dat(base + ".dat", both.data(), both.size() * sizeof(T))) return false;
+    if (s.saveAsBMP || !s.saveAsDAT) {
+      const int w = N[0], h = N[1];
+      const int kz = dim == 3 ? N[2] / 2 : 0;
+      std::vector<double> vr((size_t)w * h), vi((size_t)w * h), vm((size_t)w * h);
+      for (int i = 0; i < w; ++i)
+        for (int j = 0; j < h; ++j) {
+          const size_t o = ((size_t)i * N[1] + j) * N[2] + kz, q = (size_t)i * h + j;
+          vr[q] = re[o];
+          vi[q] = ip[o];
+          vm[q] = std::sqrt(vr[q] * vr[q] + vi[q] * vi[q]);
+        }
+      const std::string stem = dim == 3 ? base + std::to_string(kz) : base;
+      fdtd::write_bmp(stem + "-Re.bmp", vr, w, h, s.dumperPalette);
+      fdtd::write_bmp(stem + "-Im.bmp", vi, w, h, s.dumperPalette);
+      fdtd::write_bmp(stem + "-Mod.bmp", vm, w, h, s.dumperPalette);
+    }
+  }
+  return true;
 }
 
 }  // namespace

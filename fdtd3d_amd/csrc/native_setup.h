@@ -640,7 +640,9 @@ bool native_supported(const fdtd::Settings& s) {
   const bool ckpt_ok = !ckpt || (!s.doUsePML && !s.doUseTFSF && !s.doUseMetamaterials && !s.doUseAmplitudeMode &&
                                  !s.doUseNTFF && (!s.doUseParallelGrid || s.dimension == 3));
   return !((s.doUsePML && !cpml_ok && !upml_ok) || (s.doUseTFSF && !tfsf_ok) || !meta_ok || !ntff_ok || !amp_ok ||
-           !par_ok || !ckpt_ok || s.doUseComplexFieldValues || s.doUseDoubleMaterialPrecision);
+           !par_ok || !ckpt_ok || s.doUseDoubleMaterialPrecision ||
+           // complex fields: two real planes of one-GPU runs (main.cpp run)
+           (s.doUseComplexFieldValues && (s.doUseAmplitudeMode || s.doUseNTFF || s.doUseParallelGrid || ckpt)));
 }
 
 }  // namespace

@@ -94,7 +94,8 @@ def test_native_executable_cli(host):
                  ["--2d", "--use-pml", "--use-metamaterials"],
                  ["--3d", "--use-metamaterials", "--use-pml", "--scene", "reference"],
                  ["--3d", "--use-amp-mode", "--use-ntff"], ["--3d", "--parallel-grid", "--use-amp-mode", "--use-ntff"],
-                 ["--1d", "--parallel-grid", "--use-tfsf"],
+                 ["--1d", "--parallel-grid", "--use-tfsf"], ["--3d", "--complex-field-values", "--use-amp-mode"],
+                 ["--3d", "--complex-field-values", "--parallel-grid"],
                  ["--3d", "--use-pml", "--use-tfsf", "--pml-sizex", "10", "--tfsf-sizex", "8"],
                  ["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f32", "--checkpoint-dir", "/tmp/ck"],
                  ["--3d", "--parallel-grid", "--use-pml", "--pml-type", "cpml", "--checkpoint-dir", "/tmp/ck"],

@@ -281,6 +281,50 @@ def test_native_parallel_grid_checkpoint(tmp_path):
         assert max(errs) <= 1e-11 * peak, (kind, errs, peak)
 
 
+COMPLEX = {
+    "3d_cpml_tfsf": CASES["3d_cpml_tfsf"],
+    "3d_vacuum_blocked": ["--3d", "--sizex", "32", "--sizey", "28", "--sizez", "24", "--time-steps", "13", "--scene",
+                          "vacuum"],
+    "3d_drude_upml": CASES["3d_drude_upml"],
+    "2d_tmz_upml_tfsf": CASES["2d_tmz_upml_tfsf"],
+    "1d_gauss": ["--1d", "--sizex", "300", "--time-steps", "40", "--scene", "vacuum", "--source", "gaussian",
+                 "--gaussian-width", "8", "--gaussian-delay", "30"],
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("case", list(COMPLEX))
+def test_native_complex_matches_python(case, dtype, tmp_path):
+    """Complex fields natively (the real and imaginary planes as two real runs, sin / cos source) against the
+    Python driver's complex run (torch CPU, fp64): the interleaved complex DAT outputs agree."""
+    exe = native.executable()
+    argv = COMPLEX[case] + ["--complex-field-values", "--save-res", "--save-as-dat"]
+    nd, pd = tmp_path / "native", tmp_path / "py"
+    nd.mkdir()
+    pd.mkdir()
+    r = subprocess.run([exe] + argv + ["--dtype", dtype, "--output-dir", str(nd)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Complex field values: 1" in r.stdout, r.stdout
+    assert py_run(argv + ["--dtype", "f64", "--backend", "torch", "--device", "cpu", "--output-dir", str(pd)],
+                  out=io.StringIO()) == 0
+    shape, scheme = _shape(argv)
+    steps = int(argv[argv.index("--time-steps") + 1])
+    ndt = np.complex64 if dtype == "f32" else np.complex128
+    tol = 1e-11 if dtype == "f64" else 2e-5
+    for kind in "EH":
+        errs, peak = [], 0.0
+        for c in [c for c in COMPS[scheme] if c[0] == kind]:
+            name = "current[%d]_rank-0_%s.dat" % (steps, c)
+            a = np.fromfile(nd / name, dtype=ndt).astype(np.complex128).reshape(shape)
+            b = np.fromfile(pd / name, dtype=np.complex128).reshape(shape)
+            errs.append(np.abs(a - b).max())
+            peak = max(peak, np.abs(b).max())
+        assert peak > 0
+        assert max(errs) <= tol * peak, (kind, errs, peak)
+
+
 AMP_MULTI = {
     "amp_2x2x1": (CASES["3d_amp"], ["--topology-sizex", "2", "--topology-sizey", "2"]),
     "amp_cpml_2x1x2": (CASES["3d_amp_cpml"], ["--topology-sizex", "2", "--topology-sizez", "2"]),
