@@ -785,8 +785,8 @@ bool MultiRun<T>::setup_physics(int r) {
   }
   if (tfsf) {
     q.tf.reset(new NativeTfsf<T>());
-    // (E: per-cell arrays of the sphere or the scalar; H: the scalar db, mu = 1 -- 2D: db arrays)
-    if (!setup_tfsf(*q.tf, s, N, gb36, q.C, percell ? 1.0 : cb, dim == 2 && percell ? 1.0 : db, dt, s.gridStep, freq,
+    // (E: per-cell arrays of the sphere or the scalar; H: the scalar db, mu = 1 -- 1D / 2D: db arrays)
+    if (!setup_tfsf(*q.tf, s, N, gb36, q.C, percell ? 1.0 : cb, dim < 3 && percell ? 1.0 : db, dt, s.gridStep, freq,
                     dim, present, q.g0, q.n))
       return false;
   }
@@ -794,7 +794,6 @@ bool MultiRun<T>::setup_physics(int r) {
   bool has = point_src;
   for (int a = 0; a < 3; ++a) has = has && sp[a] >= q.lo[a] && sp[a] < q.hi[a];
   q.src_off = has ? ((long long)(sp[0] - q.g0[0]) * q.n[1] + (sp[1] - q.g0[1])) * q.n[2] + (sp[2] - q.g0[2]) : -1;
-  if (dim == 2 && !present[2] && src_comp == 2) q.src_off = -1;
   return true;
 }
 
