@@ -5,8 +5,9 @@
 // Covers the plain Yee solvers (1D, 2D TMz/TEz, 3D) on one GPU with the
 // vacuum / dielectric-sphere scenes and the hard point source, fp32 or fp64,
 // fused or split 3D kernels, CPML absorbing layers in 3D fp32 or fp64 (--use-pml
-// --pml-type cpml; fp32 with hybrid passes -- blocked core, stepped shell -- like
-// the Python driver's automatic plan), the UPML in the reference's D/B form and Drude / Lorentz
+// --pml-type cpml; with hybrid passes -- blocked core, stepped shell -- like
+// the Python driver's automatic plan; z sizes not divisible by 4 on the scalar
+// kernels + generic slab corrections), the UPML in the reference's D/B form and Drude / Lorentz
 // spheres (--use-metamaterials, scene drude-sphere) in 3D through the fused
 // chain kernel, TF/SF plane waves in 3D, the NTFF scattered power diagram
 // (--use-ntff) and DAT/BMP output of the final fields (native_physics.h).
@@ -98,7 +99,7 @@ int main(int argc, char** argv) {
   }
   if (!native_supported(s)) {
     std::fprintf(stderr,
-                 "fdtd3d (native): CPML in 3D outside whole 4-cell z rows, PML / TF/SF in 1D, TF/SF boxes reaching "
+                 "fdtd3d (native): decomposed 3D CPML outside whole 4-cell z rows, PML / TF/SF in 1D, TF/SF boxes reaching "
                  "the UPML, metamaterials outside the 3D drude-sphere scene, amplitude mode with NTFF, parallel "
                  "grids with NTFF in 2D, checkpoints beyond plain media, and complex fields with amplitude mode, "
                  "NTFF, checkpoints or parallel grids run through the Python driver: python -m fdtd3d_amd <same options>\n");

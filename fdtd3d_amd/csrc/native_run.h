@@ -49,6 +49,7 @@ class NativeRun {
   size_t cells;
   double dx, dt, freq;
   bool vacuum, v4, upml, cpml, tfsf, ntff, amp, use_fused, percell;
+  bool cpml_generic = false;
   hipStream_t st = nullptr;
 
   // ------------------------------------------------- fields and coefficients
@@ -118,6 +119,7 @@ class NativeRun {
   void upml_regions(int kind);
   void step(int t);
   void step3d_split(double sv);
+  void cpml_slabs(int kind);
   void step2d(double sv);
   void upml_shell(int kind, const std::vector<IBox>& wins);
   void hybrid_pass(int t, int k);
@@ -284,7 +286,11 @@ void NativeRun<T>::setup_fields() {
 // CPML (3D / 2D) and UPML (2D strips, 3D D/B chain with the Drude / Lorentz sphere) tables
 template <typename T>
 void NativeRun<T>::setup_absorbers() {
-  if (cpml && dim == 3) setup_cpml(cpt, s, N, active, dt, dx);
+  // 3D CPML on rows of a z size not divisible by 4: the scalar split kernels +
+  // the generic slab corrections (the 2D form, models/cpml.py)
+  cpml_generic = cpml && dim == 3 && N[2] % 4 != 0;
+  if (cpml && dim == 3 && !cpml_generic) setup_cpml(cpt, s, N, active, dt, dx);
+  if (cpml_generic) setup_cpml2d(p2, s, N, active, present, dt, dx);
   if (dim == 2 && cpml) setup_cpml2d(p2, s, N, active, present, dt, dx);
   if (dim == 2 && upml) {
     // per-cell 1 / (eps eps0) of a dielectric scene (E components; the
@@ -777,6 +783,10 @@ void NativeRun<T>::step3d_split(double sv) {
   if (tfsf) K_OK(inc_e(tft.einc.p, tft.hinc.p, tft.nline, tft.ce, sv, st));
   if (upml) {
     upml_regions(0);
+  } else if (cpml_generic) {
+    K_OK(e3d(F[0].p, F[1].p, F[2].p, F[3].p, F[4].p, F[5].p, C[0].p, C[1].p, C[2].p, percell ? 1.0 : cb, N[0], N[1],
+             N[2], boxes, 0, st, false));
+    cpml_slabs(0);
   } else if (cpml) {
     // (4-cell z lanes: float4 / double4)
     if constexpr (sizeof(T) == 4)
@@ -801,6 +811,10 @@ void NativeRun<T>::step3d_split(double sv) {
   if (tfsf) K_OK(inc_h(tft.einc.p, tft.hinc.p, tft.nline, tft.ch, st));
   if (upml) {
     upml_regions(1);
+  } else if (cpml_generic) {
+    K_OK(h3d(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p, percell ? 1.0 : db, N[0], N[1],
+             N[2], boxes + 18, 0, st, false));
+    cpml_slabs(1);
   } else if (cpml) {
     if constexpr (sizeof(T) == 4)
       K_OK(fdtd_update_h3d_cpml_v4_f32(F[3].p, F[4].p, F[5].p, F[0].p, F[1].p, F[2].p, C[3].p, C[4].p, C[5].p,
@@ -815,6 +829,18 @@ void NativeRun<T>::step3d_split(double sv) {
              N[2], boxes + 18, 0, st, v4));
   }
   if (tfsf) tfsf_kind(1);
+}
+
+// the generic CPML slab corrections of one kind (0 = E) after the plain
+// update (3D rows of a z size not divisible by 4; native_lowdim.h cpml)
+template <typename T>
+void NativeRun<T>::cpml_slabs(int kind) {
+  for (const Slab2d<T>& sl : p2.slabs) {
+    if ((sl.comp < 3) != (kind == 0)) continue;
+    const void* cp[4] = {nullptr, nullptr, nullptr, percell ? (const void*)C[sl.comp].p : nullptr};
+    K_OK(cpml_apply(F[sl.comp].p, F[sl.src].p, sl.psi, sl.axis, sl.sign, kind == 0 ? 1 : 0, sl.b, sl.c, sl.k,
+                    percell ? 1.0 : (kind == 0 ? cb : db), cp, N[1], N[2], sl.box, sl.pbox, st));
+  }
 }
 
 // [incident line E] E update (+ CPML slabs | UPML chain) [TF/SF on E]

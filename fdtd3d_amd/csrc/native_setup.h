@@ -300,7 +300,10 @@ void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, con
   const int n0[3] = {N[0], N[1], N[2]};
   if (!org) org = o0;
   if (!ext) ext = n0;
-  const int Ps[3] = {s.pmlSizeX, s.pmlSizeY, 0};
+  // (3D -- three active axes -- the generic slabs of 3D CPML runs whose z rows
+  // are not whole 4-cell lanes)
+  const int Ps[3] = {s.pmlSizeX, s.pmlSizeY, active.size() == 3 ? s.pmlSizeZ : 0};
+  const int nact = (int)active.size();
   const double eta = std::sqrt(kMu0 / kEps0);
   const double kmax = s.cpmlKappaMax, amax = s.cpmlAlphaMax;
   for (int c = 0; c < 6; ++c) {
@@ -314,7 +317,7 @@ void setup_cpml2d(Pml2d<T>& P, const fdtd::Settings& s, const fdtd::Int3& N, con
       }
     for (int t = 0; t < 2; ++t) {
       const int src = kCurl[c][t][0], axis = kCurl[c][t][1], sign = kCurl[c][t][2];
-      if (!present[src] || axis >= 2 || Ps[axis] <= 0) continue;
+      if (!present[src] || axis >= std::max(2, nact) || Ps[axis] <= 0) continue;
       const int Pa = Ps[axis], n = N[axis];
       const double m = kMinFP[c][axis];
       const double sig_max = -(4 + 1) * std::log(1e-8) / (2 * eta * Pa * dx);
@@ -608,10 +611,11 @@ int tfsf_apply(double* t, const TfsfLayer<double>& l, const double* inc, const i
 // The options this binary runs (everything else goes through the Python
 // driver, never a silent fallback).
 bool native_supported(const fdtd::Settings& s) {
-  // CPML absorbing layers: 3D with whole 4-cell z rows (the folded float4 /
-  // double4 kernels), 2D in either precision (generic slab kernels)
-  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && !s.doUseMetamaterials &&
-                       ((s.dimension == 3 && s.sizeZ % 4 == 0) || s.dimension == 2);
+  // CPML absorbing layers: 3D (the folded float4 / double4 kernels on whole
+  // 4-cell z rows, else the plain kernels + generic slab kernels), 2D in
+  // either precision (generic slab kernels)
+  const bool cpml_ok = s.doUsePML && s.pmlType == "cpml" && !s.doUseMetamaterials && s.dimension >= 2 &&
+                       (s.dimension == 2 || s.sizeZ % 4 == 0 || !s.doUseParallelGrid);
   // UPML (D/B chain) and Drude / Lorentz spheres: 3D, any precision; the 2D UPML without dispersive media
   const bool upml_ok = s.doUsePML && (s.pmlType == "upml" || s.doUseMetamaterials) &&
                        (s.dimension == 3 || (s.dimension == 2 && !s.doUseMetamaterials));

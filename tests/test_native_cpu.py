@@ -86,10 +86,10 @@ def test_native_executable_cli(host):
     r = subprocess.run([exe, "--1d", "--use-tfsf"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "python -m fdtd3d_amd" in r.stderr
     # CPML runs natively in 3D (whole 4-cell z rows, fp32 / fp64) and in 2D, the UPML in 3D and 2D, the Drude
-    # chain and NTFF in 3D, parallel grids for 3D plain media, CPML, UPML, Drude spheres and TF/SF; 3D CPML on z
-    # rows of a size not divisible by 4, 2D metamaterials, metamaterials outside the drude-sphere scene, amplitude
+    # chain and NTFF in 3D, parallel grids for 3D plain media, CPML, UPML, Drude spheres and TF/SF; decomposed 3D
+    # CPML on z rows of a size not divisible by 4, 2D metamaterials, metamaterials outside the drude-sphere scene, amplitude
     # mode with NTFF go to the Python driver
-    for argv in (["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f64", "--sizez", "42"],
+    for argv in (["--3d", "--use-pml", "--pml-type", "cpml", "--dtype", "f64", "--sizez", "42", "--parallel-grid"],
                  ["--2d", "--use-ntff"],
                  ["--2d", "--use-pml", "--use-metamaterials"],
                  ["--3d", "--use-metamaterials", "--use-pml", "--scene", "reference"],

@@ -42,6 +42,13 @@ CASES = {
                              "--sphere-radius", "5", "--sphere-eps", "3", "--use-pml", "--pml-type", "cpml",
                              "--pml-sizex", "6", "--same-size-pml", "--cpml-kappa-max", "3",
                              "--cpml-alpha-max", "0.05"],
+    # 3D CPML on z rows of a size not divisible by 4: the scalar split kernels + the generic slab corrections
+    "3d_cpml_tfsf_z42": ["--3d", "--sizex", "30", "--sizey", "28", "--sizez", "42", "--time-steps", "24", "--scene",
+                         "sphere", "--sphere-center-x", "15", "--sphere-center-y", "14", "--sphere-center-z", "21",
+                         "--sphere-radius", "4", "--sphere-eps", "3", "--use-pml", "--pml-type", "cpml",
+                         "--pml-sizex", "5", "--same-size-pml", "--cpml-kappa-max", "2", "--cpml-alpha-max", "0.05",
+                         "--use-tfsf", "--tfsf-sizex", "9", "--same-size-tfsf", "--angle-teta", "50", "--angle-phi",
+                         "30", "--angle-psi", "20"],
     # TF/SF plane wave (oblique incidence; fp32 and fp64), and CPML + TF/SF (BASELINE config 3, fp32)
     "3d_tfsf": ["--3d", "--sizex", "36", "--sizey", "32", "--sizez", "40", "--time-steps", "30", "--scene", "sphere",
                 "--sphere-center-x", "18", "--sphere-center-y", "16", "--sphere-center-z", "20", "--sphere-radius",
