@@ -1118,7 +1118,10 @@ class YeeScheme(BlockedStepping):
         data others read (lazy tables): build those before the call."""
         n = int(getattr(self.cfg, "shell_streams", 0))
         if n <= 0:
-            n = 3 if self.ops.name == "hip" else 1
+            # two streams: 512^3 alternating runs (profiles/physics_r6.md, tools/gpu_r6_as.sh) -- CPML + TF/SF
+            # 96.0k vs 94.2k with three, UPML + TF/SF 92.3k vs 91.5k, fp64 CPML + TF/SF 49.1k vs 48.6k, Drude
+            # + UPML 83.7k vs 84.0k
+            n = 2 if self.ops.name == "hip" else 1
         # decomposed runs in order: their deep-halo shell windows on three
         # streams measured slower (2x2x1 of 512^3 CPML + TF/SF: 30.6k vs
         # 35.3k Mcells/s per GPU, tools/gpu_r5_zi.sh)

@@ -79,6 +79,10 @@ CASES = [
     # form stays covered
     ("cpml-tfsf-inorder", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10, psi=5,
                                shell_streams=1), 4, 12),
+    ("cpml-tfsf-3streams", dict(scene="vacuum", use_pml=True, pml_type="cpml", use_tfsf=True, theta=60, phi=10,
+                                psi=5, shell_streams=3), 4, 12),
+    ("drude-upml-3streams", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, sphere_center=(40.0, 36.0,
+                                 48.0), sphere_radius=7.0, shell_streams=3), 4, 12),
     ("drude-upml-inorder", dict(scene="drude-sphere", use_pml=True, use_metamaterials=True, blocked_drude="off",
                                 sphere_center=(40.0, 36.0, 48.0), sphere_radius=7.0, shell_streams=1), 4, 12),
 ]
