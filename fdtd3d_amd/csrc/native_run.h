@@ -91,6 +91,7 @@ class NativeRun {
   std::vector<IBox> h2shell[8], h2copy;
   IBox h2core = {{0, 0, 0}, {0, 0, 0}};
   hipStream_t side[2] = {nullptr, nullptr};
+  int nstreams = 3;  // shell streams (--shell-streams; 0 = automatic)
   hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
   double ckpt_ms = 0.0;
 
@@ -646,6 +647,7 @@ void NativeRun<T>::plan_hybrid2d() {
 template <typename T>
 void NativeRun<T>::setup_streams() {
   if (T_h <= 1) return;
+  nstreams = s.shellStreams > 0 ? std::min(3, s.shellStreams) : 3;
   for (int q = 0; q < 2; ++q) {
     HIP_OK(hipStreamCreateWithFlags(&side[q], hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&join_ev[q], hipEventDisableTiming));
@@ -700,10 +702,11 @@ void NativeRun<T>::par_windows(const std::vector<IBox>& wins,
     for (const IBox& w : wins) fn(w, st);
     return;
   }
+  const int ns = nstreams;
   HIP_OK(hipEventRecord(fork_ev, st));
-  for (int q = 0; q < 2; ++q) HIP_OK(hipStreamWaitEvent(side[q], fork_ev, 0));
-  for (size_t n = 0; n < wins.size(); ++n) fn(wins[n], n % 3 == 0 ? st : side[n % 3 - 1]);
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < ns - 1; ++q) HIP_OK(hipStreamWaitEvent(side[q], fork_ev, 0));
+  for (size_t n = 0; n < wins.size(); ++n) fn(wins[n], n % ns == 0 ? st : side[n % ns - 1]);
+  for (int q = 0; q < ns - 1; ++q) {
     HIP_OK(hipEventRecord(join_ev[q], side[q]));
     HIP_OK(hipStreamWaitEvent(st, join_ev[q], 0));
   }
@@ -717,10 +720,11 @@ void NativeRun<T>::par_fns(const std::vector<std::function<void(hipStream_t)>>& 
     for (const auto& fn : fns) fn(st);
     return;
   }
+  const int ns = nstreams;
   HIP_OK(hipEventRecord(fork_ev, st));
-  for (int q = 0; q < 2; ++q) HIP_OK(hipStreamWaitEvent(side[q], fork_ev, 0));
-  for (size_t n = 0; n < fns.size(); ++n) fns[n](n % 3 == 0 ? st : side[n % 3 - 1]);
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < ns - 1; ++q) HIP_OK(hipStreamWaitEvent(side[q], fork_ev, 0));
+  for (size_t n = 0; n < fns.size(); ++n) fns[n](n % ns == 0 ? st : side[n % ns - 1]);
+  for (int q = 0; q < ns - 1; ++q) {
     HIP_OK(hipEventRecord(join_ev[q], side[q]));
     HIP_OK(hipStreamWaitEvent(st, join_ev[q], 0));
   }
